@@ -1,0 +1,118 @@
+"""Loader for the in-tree native libraries (ctypes, no Python-C++ ABI coupling).
+
+``kernels()`` returns the gfx950 HIP kernel library.  It MUST be loaded after
+``import torch``: torch ships ``libamdhip64.so`` with SONAME ``libamdhip64.so.7``
+and our library NEEDs that SONAME, so the dynamic loader binds our kernels to
+the very HIP runtime (and device context / allocator) torch already uses.
+
+When a GPU is present and the library cannot be built or loaded, every GPU op
+raises — there is no silent eager fallback on a GPU box.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import threading
+from pathlib import Path
+
+import torch  # noqa: F401  (must precede the CDLL load, see module docstring)
+
+HERE = Path(__file__).resolve().parent
+_lock = threading.Lock()
+_kernels = None
+_host = None
+
+c_int = ctypes.c_int
+c_ll = ctypes.c_longlong
+c_vp = ctypes.c_void_p
+c_dbl = ctypes.c_double
+c_float = ctypes.c_float
+
+
+class NativeError(RuntimeError):
+    pass
+
+
+# name -> (restype, [argtypes])
+_KERNEL_SIGS = {
+    "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int]),
+    "cml_kmeans_assign_threads": (c_int, []),
+    "cml_kmeans_accum_threads": (c_int, []),
+    "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp,
+                                       c_int, c_int, c_vp, c_int, c_vp]),
+    "cml_kmeans_accum_bf16": (c_int, [c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
+    "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
+                                  c_vp]),
+}
+
+_HOST_SIGS = {}
+
+
+def register_kernel_sigs(sigs: dict) -> None:
+    _KERNEL_SIGS.update(sigs)
+
+
+def register_host_sigs(sigs: dict) -> None:
+    _HOST_SIGS.update(sigs)
+
+
+def _declare(lib, sigs):
+    for name, (res, args) in sigs.items():
+        fn = getattr(lib, name, None)
+        if fn is None:
+            raise NativeError(f"symbol {name} missing from {lib._name}; rebuild with _native.build --force")
+        fn.restype = res
+        fn.argtypes = args
+
+
+def kernels():
+    """The gfx950 kernel library (built in-tree on first use if missing)."""
+    global _kernels
+    if _kernels is not None:
+        return _kernels
+    with _lock:
+        if _kernels is None:
+            from . import build as _build
+            path = HERE / "libcml_kernels.so"
+            if os.environ.get("CML_NO_AUTOBUILD") != "1":
+                _build.build_kernels()
+            if not path.exists():
+                raise NativeError(f"{path} missing and could not be built")
+            lib = ctypes.CDLL(str(path), mode=ctypes.RTLD_GLOBAL)
+            _declare(lib, _KERNEL_SIGS)
+            _kernels = lib
+    return _kernels
+
+
+def host():
+    """Host-side C++ runtime library (CSV parser, RNG helpers)."""
+    global _host
+    if _host is not None:
+        return _host
+    with _lock:
+        if _host is None:
+            from . import build as _build
+            path = HERE / "libcml_host.so"
+            if os.environ.get("CML_NO_AUTOBUILD") != "1":
+                _build.build_host()
+            if not path.exists():
+                raise NativeError(f"{path} missing and could not be built")
+            lib = ctypes.CDLL(str(path))
+            _declare(lib, _HOST_SIGS)
+            _host = lib
+    return _host
+
+
+def check(status: int, what: str) -> None:
+    if status != 0:
+        raise NativeError(f"{what} failed with hipError {status}")
+
+
+def stream_ptr(stream=None) -> int:
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return s.cuda_stream
+
+
+def ptr(t) -> int:
+    return t.data_ptr() if t is not None else 0

@@ -1,0 +1,121 @@
+"""In-tree build of the native libraries.
+
+* ``libcml_kernels.so`` — every ``csrc/*.hip`` file, compiled by ``hipcc`` for
+  gfx950 only (CDNA4 / MI355X).  No CUDA, no hipify, no multi-arch fat binary.
+* ``libcml_host.so``   — the host-side C++ runtime pieces (``host/*.cpp``):
+  multithreaded CSV tokenizer/parser, counter-based RNG helpers, etc.
+
+Both land next to this file so that ``gpurun`` snapshots carry them to the GPU
+box and the round-end check sees them loaded from the tree.  A build is skipped
+when the library is newer than every source and header (content hash stamp).
+
+Usage::
+
+    python -m clustermachinelearningforhospitalnetworks_apache_spark_amd._native.build [--force]
+"""
+from __future__ import annotations
+
+import concurrent.futures as cf
+import hashlib
+import os
+import shutil
+import subprocess
+import sys
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+CSRC = HERE / "csrc"
+HOST = HERE / "host"
+OBJ = HERE / "build"
+KERNEL_LIB = HERE / "libcml_kernels.so"
+HOST_LIB = HERE / "libcml_host.so"
+ARCH = os.environ.get("CML_OFFLOAD_ARCH", "gfx950")
+
+
+def _hipcc() -> str:
+    cand = shutil.which("hipcc") or "/opt/rocm/bin/hipcc"
+    if not Path(cand).exists():
+        raise RuntimeError("hipcc not found: the ROCm toolchain is required to build the gfx950 kernels")
+    return cand
+
+
+def _digest(paths, extra: str) -> str:
+    h = hashlib.sha256(extra.encode())
+    for p in sorted(paths):
+        h.update(p.name.encode())
+        h.update(p.read_bytes())
+    return h.hexdigest()
+
+
+def _stamp_ok(lib: Path, digest: str) -> bool:
+    st = lib.with_suffix(lib.suffix + ".stamp")
+    return lib.exists() and st.exists() and st.read_text().strip() == digest
+
+
+def _write_stamp(lib: Path, digest: str) -> None:
+    lib.with_suffix(lib.suffix + ".stamp").write_text(digest + "\n")
+
+
+def _run(cmd):
+    r = subprocess.run(cmd, capture_output=True, text=True)
+    if r.returncode != 0:
+        raise RuntimeError(f"build command failed ({r.returncode}): {' '.join(cmd)}\n{r.stdout}\n{r.stderr}")
+    return r
+
+
+def build_kernels(force: bool = False, verbose: bool = False) -> Path:
+    srcs = sorted(CSRC.glob("*.hip"))
+    hdrs = sorted(CSRC.glob("*.h"))
+    flags = ["-O3", "-std=c++17", "-fPIC", f"--offload-arch={ARCH}", "-munsafe-fp-atomics",
+             "-Wno-unused-result", "-fvisibility=hidden"]
+    digest = _digest(srcs + hdrs, " ".join(flags))
+    if not force and _stamp_ok(KERNEL_LIB, digest):
+        return KERNEL_LIB
+    OBJ.mkdir(exist_ok=True)
+    hipcc = _hipcc()
+
+    def compile_one(src: Path) -> Path:
+        out = OBJ / (src.stem + ".o")
+        _run([hipcc, *flags, "-I", str(CSRC), "-c", str(src), "-o", str(out)])
+        if verbose:
+            print(f"[cml build] {src.name} -> {out.name}")
+        return out
+
+    jobs = max(1, min(len(srcs), int(os.environ.get("MAX_JOBS", "8")), 8))
+    with cf.ThreadPoolExecutor(jobs) as ex:
+        objs = list(ex.map(compile_one, srcs))
+    tmp = KERNEL_LIB.with_suffix(".so.tmp")
+    _run([hipcc, "-shared", "-fPIC", f"--offload-arch={ARCH}", *map(str, objs), "-o", str(tmp)])
+    os.replace(tmp, KERNEL_LIB)
+    _write_stamp(KERNEL_LIB, digest)
+    return KERNEL_LIB
+
+
+def build_host(force: bool = False, verbose: bool = False) -> Path:
+    srcs = sorted(HOST.glob("*.cpp"))
+    hdrs = sorted(HOST.glob("*.h"))
+    if not srcs:
+        return HOST_LIB
+    cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden"]
+    digest = _digest(srcs + hdrs, " ".join(flags))
+    if not force and _stamp_ok(HOST_LIB, digest):
+        return HOST_LIB
+    tmp = HOST_LIB.with_suffix(".so.tmp")
+    _run([cxx, *flags, *map(str, srcs), "-o", str(tmp)])
+    os.replace(tmp, HOST_LIB)
+    _write_stamp(HOST_LIB, digest)
+    if verbose:
+        print(f"[cml build] host -> {HOST_LIB.name}")
+    return HOST_LIB
+
+
+def build_all(force: bool = False, verbose: bool = False):
+    return build_kernels(force, verbose), build_host(force, verbose)
+
+
+if __name__ == "__main__":
+    force = "--force" in sys.argv
+    k, h = build_all(force=force, verbose=True)
+    print(k)
+    print(h)

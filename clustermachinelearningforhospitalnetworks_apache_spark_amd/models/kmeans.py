@@ -1,0 +1,323 @@
+"""Distributed Lloyd engine for KMeans (the north-star workload, BASELINE.json).
+
+The reference contains no KMeans; semantics follow Spark MLlib's
+KMeans defaults: k-means|| initialisation with initSteps=2,
+maxIter=20, tol=1e-4 (converged when every centre moved ≤ tol), empty clusters
+keep their previous centre, trainingCost = cost of the last iteration's
+assignment.
+
+Per iteration on each rank (E5 in SURVEY.md §3):
+
+    for chunk c of the local HBM-resident shard:
+        K9  assign  (MFMA distance GEMM + argmin, centres LDS-resident)
+        K10 accumulate (LDS-privatised per-cluster sums) -> K10b reduce -> msg[c]
+        RCCL all-reduce(msg[c]) enqueued asynchronously — it runs on the
+        process group's stream while chunk c+1's distance GEMM runs
+    K11 update from Σ_c msg[c]  (the only exposed collective is the last chunk's)
+
+CPU tensors run the same algorithm with torch float64 ops (``local[n]`` mode and
+the numerical oracle).
+"""
+from __future__ import annotations
+
+import math
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import kmeans_ops as K
+from ..parallel.comm import Communicator, local_comm
+from ..utils import rng
+from ..utils.device import padded_dim, round_up
+
+
+def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
+    """bf16 [n, dp] zero-padded copy of a GPU feature matrix (dp = padded_dim(d))."""
+    d = x.shape[1] if d is None else d
+    dp = padded_dim(d)
+    if x.dtype == torch.bfloat16 and x.shape[1] == dp and x.is_contiguous():
+        return x
+    out = torch.zeros((x.shape[0], dp), dtype=torch.bfloat16, device=x.device)
+    step = 1 << 22
+    for s in range(0, x.shape[0], step):
+        out[s:s + step, :d] = x[s:s + step, :d].to(torch.bfloat16)
+    return out
+
+
+class LloydEngine:
+    """Rank-local shard + distributed Lloyd iterations."""
+
+    def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
+                 row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None):
+        self.comm = comm or local_comm()
+        self.k = int(k)
+        self.d = int(d)
+        self.gpu = x.is_cuda
+        self.n = int(x.shape[0])
+        self.device = x.device
+        if self.gpu:
+            self.x = to_device_matrix(x, d)
+            self.dp = self.x.shape[1]
+        else:
+            self.x = x[:, :d].to(torch.float64)
+            self.dp = d
+        self._row_ids = row_ids
+        if row_chunks is None:
+            row_chunks = 2 if (self.comm.is_distributed and self.n >= (1 << 20)) else 1
+        self.row_chunks = max(1, min(int(row_chunks), max(1, self.n)))
+        self.centers = torch.zeros((self.k, self.d), dtype=torch.float64, device=self.device)
+        self.iterations = 0
+        self.last_cost = None
+        self._shift2 = None
+        if self.gpu:
+            self._alloc_gpu()
+
+    # ------------------------------------------------------------------ setup
+    def _alloc_gpu(self):
+        dev = self.device
+        k, d, dp, n = self.k, self.d, self.dp, self.n
+        self.kp = round_up(k, 32)
+        bounds = [round(i * n / self.row_chunks) for i in range(self.row_chunks + 1)]
+        # keep chunk boundaries on 32-row tiles
+        bounds = [min(n, round_up(b, 32)) if 0 < i < self.row_chunks else b for i, b in enumerate(bounds)]
+        self.bounds = bounds
+        maxn = max(bounds[i + 1] - bounds[i] for i in range(self.row_chunks)) if n else 0
+        self.aplan = K.plan_assign(max(maxn, 1), dp, k, dev.index or 0)
+        self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0)
+        self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        self.best = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
+        self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dsl, dtype=torch.float32,
+                                device=dev)
+        self.cslab = torch.empty(self.cplan.gx * k, dtype=torch.int32, device=dev)
+        self.msg_len = k * d + k + 1
+        self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
+        self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
+        self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
+        self.shift2 = torch.zeros(k, dtype=torch.float64, device=dev)
+
+    @property
+    def global_n(self) -> int:
+        return int(self.comm.sum_scalar(float(self.n)))
+
+    def row_ids(self) -> torch.Tensor:
+        if self._row_ids is None:
+            counts = self.comm.allgather_object(self.n)
+            off = sum(counts[: self.comm.rank])
+            self._row_ids = torch.arange(off, off + self.n, dtype=torch.int64, device=self.device)
+        return self._row_ids
+
+    def set_centers(self, centers) -> None:
+        c = torch.as_tensor(np.asarray(centers, dtype=np.float64), device=self.device)
+        if c.shape != (self.k, self.d):
+            raise ValueError(f"centers shape {tuple(c.shape)} != {(self.k, self.d)}")
+        self.centers = c.contiguous().clone()
+        if self.gpu:
+            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+
+    # ------------------------------------------------------------------ iteration
+    def step(self) -> None:
+        """One Lloyd iteration over the global dataset (all ranks participate)."""
+        if self.gpu:
+            self._step_gpu()
+        else:
+            self._step_cpu()
+        self.iterations += 1
+
+    def _step_gpu(self):
+        handles = []
+        for c in range(self.row_chunks):
+            r0, r1 = self.bounds[c], self.bounds[c + 1]
+            nrow = r1 - r0
+            msg = self.msgs[c]
+            if nrow > 0:
+                xc = self.x[r0:r1]
+                lab = self.labels[r0:r1]
+                K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
+                              self.cost_part)
+                K.accumulate_bf16(xc, nrow, lab, self.k, self.cplan, self.slab, self.cslab)
+                K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, self.k, self.d, self.cplan,
+                               msg)
+            else:
+                msg.zero_()
+            handles.append(self.comm.allreduce_async(msg))
+        for h in handles:
+            h.wait()
+        self.last_cost = self.msgs[:, -1].sum()
+        K.update_centers(self.msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
+                         self.shift2)
+        self._shift2 = self.shift2
+
+    def _step_cpu(self):
+        labels, best = K.assign_reference(self.x, self.centers)
+        sums, counts = K.sums_reference(self.x, labels, self.k)
+        msg = torch.cat([sums.reshape(-1), counts, best.sum().reshape(1)])
+        self.comm.allreduce_(msg)
+        kd = self.k * self.d
+        sums = msg[:kd].reshape(self.k, self.d)
+        counts = msg[kd:kd + self.k]
+        new = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], self.centers)
+        self._shift2 = ((new - self.centers) ** 2).sum(1)
+        self.centers = new
+        self.last_cost = msg[-1]
+        self.labels = labels
+
+    def converged(self, tol: float) -> bool:
+        """Spark's rule: converged iff every centre moved at most tol (euclidean)."""
+        if self._shift2 is None:
+            return False
+        return bool((self._shift2 <= tol * tol).all().item())
+
+    def fit(self, max_iter: int, tol: float) -> int:
+        it = 0
+        while it < max_iter:
+            self.step()
+            it += 1
+            if tol > 0 and self.converged(tol):
+                break
+        return it
+
+    # ------------------------------------------------------------------ prediction / cost
+    def assign(self, centers: Optional[torch.Tensor] = None):
+        """(labels, squared distance) of every local row against `centers` (default: current)."""
+        if centers is not None:
+            centers = torch.as_tensor(centers, dtype=torch.float64, device=self.device)
+        if not self.gpu:
+            return K.assign_reference(self.x, self.centers if centers is None else centers)
+        return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers)
+
+    def training_cost(self) -> float:
+        return float(self.last_cost.item()) if self.last_cost is not None else float("nan")
+
+    # ------------------------------------------------------------------ initialisation
+    def init_random(self, seed: int) -> np.ndarray:
+        """Spark initMode="random": k distinct rows sampled uniformly without replacement."""
+        ids = self.row_ids()
+        u = rng.uniform(ids, seed, stream=11)
+        take = min(self.k, self.n)
+        loc_u, loc_i = torch.topk(-u, take) if take > 0 else (u[:0], ids[:0].long())
+        cand_u = -loc_u
+        rows = self._rows_f64(loc_i)
+        all_u = self.comm.allgather_cat(cand_u.to(torch.float64))
+        all_rows = self.comm.allgather_cat(rows)
+        order = torch.argsort(all_u)[: self.k]
+        return all_rows[order].cpu().numpy()
+
+    def _rows_f64(self, idx: torch.Tensor) -> torch.Tensor:
+        if self.gpu:
+            return self.x[idx.long(), : self.d].to(torch.float64)
+        return self.x[idx.long()]
+
+    def _min_dist(self, cands: torch.Tensor) -> torch.Tensor:
+        if not self.gpu:
+            return K.assign_reference(self.x, cands)[1]
+        return assign_gpu(self.x, self.dp, self.d, cands)[1].to(torch.float64)
+
+    def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
+        """k-means|| (Bahmani et al.), Spark's default initMode, then weighted local k-means++."""
+        k = self.k
+        ids = self.row_ids()
+        gn = self.global_n
+        if gn == 0:
+            raise ValueError("KMeans on an empty dataset")
+        # first centre: one uniformly drawn global row (same draw on every rank)
+        u = rng.uniform(ids, seed, stream=1)
+        lu, li = (torch.min(u, 0) if self.n else (torch.tensor(2.0, device=self.device), torch.tensor(0)))
+        first_u = self.comm.allgather_cat(lu.reshape(1).to(torch.float64))
+        owner = int(torch.argmin(first_u).item())
+        row = self._rows_f64(li.reshape(1)) if self.n else torch.zeros((1, self.d), dtype=torch.float64,
+                                                                      device=self.device)
+        row = self.comm.allgather(row)[owner] if self.comm.is_distributed else row
+        centers = [row.reshape(1, self.d)]
+        costs = self._min_dist(centers[0]) if self.n else torch.zeros(0, dtype=torch.float64, device=self.device)
+        for step in range(steps):
+            sum_cost = self.comm.sum_scalar(float(costs.sum().item()) if self.n else 0.0)
+            if sum_cost <= 0:
+                break
+            us = rng.uniform(ids, seed, stream=100 + step)
+            prob = 2.0 * k * costs / sum_cost
+            chosen = torch.nonzero(us < prob).flatten()
+            new = self._rows_f64(chosen) if chosen.numel() else torch.zeros((0, self.d), dtype=torch.float64,
+                                                                            device=self.device)
+            new = self.comm.allgather_cat(new)
+            if new.shape[0] == 0:
+                continue
+            centers.append(new)
+            if self.n:
+                costs = torch.minimum(costs, self._min_dist(new))
+        cand = torch.cat(centers, 0)
+        cand_np = np.unique(cand.cpu().numpy(), axis=0)
+        if cand_np.shape[0] <= k:
+            out = cand_np
+        else:
+            cand_t = torch.as_tensor(cand_np, device=self.device)
+            if self.n:
+                lab = (K.assign_reference(self.x, cand_t)[0] if not self.gpu
+                       else assign_gpu(self.x, self.dp, self.d, cand_t)[0].long())
+                w = torch.bincount(lab, minlength=cand_np.shape[0]).to(torch.float64)
+            else:
+                w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
+            self.comm.allreduce_(w)
+            out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30)
+        if out.shape[0] < k:
+            # Spark may return fewer centres when there are < k distinct points; pad by repetition so the
+            # device buffers keep their shape, and record the real count.
+            self.k_effective = out.shape[0]
+            out = np.concatenate([out, np.repeat(out[-1:], k - out.shape[0], 0)], 0)
+        else:
+            self.k_effective = k
+        return out
+
+
+def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor):
+    """K9 against an arbitrary centre set (used for transform, cost and k-means||)."""
+    k = centers.shape[0]
+    kp = round_up(max(k, 1), 32)
+    dev = x.device
+    n = x.shape[0]
+    cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
+    cn = torch.zeros(kp, dtype=torch.float32, device=dev)
+    cent = centers.to(device=dev, dtype=torch.float64).contiguous().clone()
+    K.update_centers(None, k, d, cent, cb, dp, kp, cn, None)
+    labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+    if n:
+        plan = K.plan_assign(n, dp, k, dev.index or 0)
+        K.assign_bf16(x, n, dp, cb, cn, plan, labels, best, None)
+    return labels[:n], best[:n]
+
+
+def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, max_iter: int = 30) -> np.ndarray:
+    """Weighted k-means++ seeding + weighted Lloyd on the candidate set (host, float64)."""
+    rs = np.random.RandomState(seed & 0x7FFFFFFF)
+    n = points.shape[0]
+    w = np.maximum(weights.astype(np.float64), 0)
+    if w.sum() <= 0:
+        w = np.ones(n)
+    centers = np.empty((k, points.shape[1]))
+    centers[0] = points[rs.choice(n, p=w / w.sum())]
+    d2 = ((points - centers[0]) ** 2).sum(1)
+    for i in range(1, k):
+        p = w * d2
+        s = p.sum()
+        idx = rs.choice(n, p=p / s) if s > 0 else rs.randint(n)
+        centers[i] = points[idx]
+        d2 = np.minimum(d2, ((points - centers[i]) ** 2).sum(1))
+    pn = (points * points).sum(1)
+    for _ in range(max_iter):
+        dist = pn[:, None] - 2.0 * points @ centers.T + (centers * centers).sum(1)[None, :]
+        lab = dist.argmin(1)
+        moved = False
+        for j in range(k):
+            m = lab == j
+            if m.any():
+                c = (points[m] * w[m, None]).sum(0) / max(w[m].sum(), 1e-300)
+            else:
+                c = points[rs.randint(n)]
+            if not np.allclose(c, centers[j]):
+                moved = True
+            centers[j] = c
+        if not moved:
+            break
+    return centers

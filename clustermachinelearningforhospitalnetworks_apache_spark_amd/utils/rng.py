@@ -1,0 +1,60 @@
+"""Counter-based random numbers keyed by (seed, stream, global row id).
+
+Spark draws per-partition XORShift sequences, so a row's random value depends on
+how the data is partitioned (``ref.py:139``).  Here every random
+decision about a row is a pure hash of (seed, stream, row id): results are
+identical on 1, 2, 4 or 8 GPUs and on the CPU (the same int64 torch ops run on
+both devices, wrap-around multiplication included).
+"""
+from __future__ import annotations
+
+import torch
+
+_M31 = (1 << 31) - 1
+_M53 = (1 << 53) - 1
+
+
+def _s64(c: int) -> int:
+    c &= (1 << 64) - 1
+    return c - (1 << 64) if c >= (1 << 63) else c
+
+
+_C1 = _s64(0xBF58476D1CE4E5B9)
+_C2 = _s64(0x94D049BB133111EB)
+_GOLD = _s64(0x9E3779B97F4A7C15)
+
+
+def _lsr(x: torch.Tensor, s: int) -> torch.Tensor:
+    """Logical shift right of int64 (torch's >> is arithmetic)."""
+    return (x >> s) & ((1 << (64 - s)) - 1)
+
+
+def splitmix64(x: torch.Tensor) -> torch.Tensor:
+    x = x + _GOLD
+    x = (x ^ _lsr(x, 30)) * _C1
+    x = (x ^ _lsr(x, 27)) * _C2
+    return x ^ _lsr(x, 31)
+
+
+def key(seed: int, stream: int = 0) -> int:
+    t = torch.tensor([_s64(seed * 0x100000001B3 + stream * 0xC2B2AE3D27D4EB4F)], dtype=torch.int64)
+    return int(splitmix64(t)[0])
+
+
+def uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
+    """u in [0, 1) (float64) for every row id."""
+    h = splitmix64(row_ids.to(torch.int64) ^ key(seed, stream))
+    return _lsr(h, 11).to(torch.float64) * (1.0 / (1 << 53))
+
+
+def poisson1(row_ids: torch.Tensor, seed: int, stream: int = 0, max_k: int = 16) -> torch.Tensor:
+    """Poisson(λ=1) counts per row by CDF inversion of one counter-based uniform."""
+    u = uniform(row_ids, seed, stream)
+    out = torch.zeros_like(u, dtype=torch.int32)
+    p = torch.exp(torch.tensor(-1.0, dtype=torch.float64)).item()
+    cdf = p
+    for kk in range(1, max_k + 1):
+        out += (u >= cdf).to(torch.int32)
+        p = p / kk
+        cdf += p
+    return out

@@ -1,0 +1,82 @@
+"""Numerics of the KMeans HIP kernels (K9/K10/K11) against float64 torch references."""
+import numpy as np
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import (LloydEngine, assign_gpu,
+                                                                                       to_device_matrix)
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+
+pytestmark = pytest.mark.gpu
+
+
+def _ref_assign(xb, cb):
+    x = xb.double().cpu()
+    c = cb.double().cpu()
+    sc = (c * c).sum(1)[None, :] - 2 * x @ c.T
+    srt, idx = torch.sort(sc, 1)
+    d = (x * x).sum(1) + srt[:, 0]
+    gap = srt[:, 1] - srt[:, 0] if c.shape[0] > 1 else torch.full_like(d, 1e9)
+    return idx[:, 0], d.clamp(min=0), gap
+
+
+@pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (4097, 100, 70), (20000, 256, 256), (3000, 512, 200),
+                                   (777, 16, 33), (5000, 128, 64)])
+def test_assign_matches_reference(n, d, k):
+    torch.manual_seed(0)
+    dev = torch.device("cuda")
+    x = torch.randn(n, d, device=dev) * 2
+    c = torch.randn(k, d, device=dev) * 2
+    xm = to_device_matrix(x, d)
+    lab, best = assign_gpu(xm, xm.shape[1], d, c.double())
+    torch.cuda.synchronize()
+    cb = c.to(torch.bfloat16)
+    ref_lab, ref_d, gap = _ref_assign(x.to(torch.bfloat16), cb)
+    lab = lab.cpu().long()
+    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
+    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
+    np.testing.assert_allclose(best.cpu().double().numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
+
+
+@pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (50000, 256, 256), (9999, 100, 70), (2000, 16, 3)])
+def test_lloyd_step_matches_reference(n, d, k):
+    torch.manual_seed(1)
+    dev = torch.device("cuda")
+    x = (torch.randn(n, d, device=dev) * 3).to(torch.bfloat16)
+    init = x[:k].double().cpu().numpy()
+    eng = LloydEngine(x, d, k)
+    eng.set_centers(init)
+    labels_before = None
+    eng.step()
+    torch.cuda.synchronize()
+    lab = eng.labels[:n].cpu().long()
+    # reference sums with the GPU's labels (tests K10/K11 independently of near-tie flips)
+    xs = x.double().cpu()
+    sums, counts = K.sums_reference(xs, lab, k)
+    old = torch.as_tensor(init)
+    want = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], old)
+    np.testing.assert_allclose(eng.centers.cpu().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
+    msg = eng.msgs[0].cpu()
+    np.testing.assert_array_equal(msg[k * d:k * d + k].numpy(), counts.numpy())
+    # label agreement with the exact reference (allowing bf16 near-ties)
+    ref_lab, ref_d, gap = _ref_assign(x, torch.as_tensor(init).to(torch.bfloat16))
+    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
+    assert ok.all()
+    assert abs(eng.training_cost() - ref_d.sum().item()) <= 1e-3 * ref_d.sum().item() + 1e-3
+
+
+def test_fit_converges_on_blobs():
+    torch.manual_seed(2)
+    dev = torch.device("cuda")
+    k, d, n = 8, 32, 100000
+    centers = torch.randn(k, d, device=dev) * 10
+    lab = torch.randint(0, k, (n,), device=dev)
+    x = (centers[lab] + torch.randn(n, d, device=dev)).to(torch.bfloat16)
+    eng = LloydEngine(x, d, k)
+    eng.set_centers(eng.init_kmeans_parallel(seed=7))
+    it = eng.fit(max_iter=20, tol=1e-4)
+    assert it <= 20
+    got = torch.as_tensor(eng.centers.cpu())
+    # every true centre is matched by a fitted centre
+    dist = torch.cdist(centers.double().cpu(), got)
+    assert dist.min(1).values.max().item() < 0.5
