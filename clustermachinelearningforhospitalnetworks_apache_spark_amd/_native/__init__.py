@@ -33,28 +33,22 @@ class NativeError(RuntimeError):
     pass
 
 
-# name -> (restype, [argtypes])
-_KERNEL_SIGS = {
-    "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int]),
-    "cml_kmeans_assign_threads": (c_int, []),
-    "cml_kmeans_accum_threads": (c_int, []),
-    "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp,
-                                       c_int, c_int, c_vp, c_int, c_vp]),
-    "cml_kmeans_accum_bf16": (c_int, [c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_vp, c_vp, c_int, c_int, c_vp]),
-    "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
-    "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
-                                  c_vp]),
-}
+# name -> (restype, [argtypes]); each ops module registers the symbols it binds.
+_KERNEL_SIGS = {}
 
 _HOST_SIGS = {}
 
 
 def register_kernel_sigs(sigs: dict) -> None:
     _KERNEL_SIGS.update(sigs)
+    if _kernels is not None:
+        _declare(_kernels, sigs)
 
 
 def register_host_sigs(sigs: dict) -> None:
     _HOST_SIGS.update(sigs)
+    if _host is not None:
+        _declare(_host, sigs)
 
 
 def _declare(lib, sigs):

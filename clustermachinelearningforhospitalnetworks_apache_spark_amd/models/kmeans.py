@@ -49,8 +49,10 @@ class LloydEngine:
     """Rank-local shard + distributed Lloyd iterations."""
 
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
-                 row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None):
+                 row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
+                 accum_mode: Optional[str] = None):
         self.comm = comm or local_comm()
+        self._accum_mode = accum_mode
         self.k = int(k)
         self.d = int(d)
         self.gpu = x.is_cuda
@@ -84,13 +86,20 @@ class LloydEngine:
         self.bounds = bounds
         maxn = max(bounds[i + 1] - bounds[i] for i in range(self.row_chunks)) if n else 0
         self.aplan = K.plan_assign(max(maxn, 1), dp, k, dev.index or 0)
-        self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0)
+        self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode)
         self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         self.best = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
-        self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dsl, dtype=torch.float32,
-                                device=dev)
-        self.cslab = torch.empty(self.cplan.gx * k, dtype=torch.int32, device=dev)
+        if self.cplan.mode == "priv":
+            self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
+                                    device=dev)
+            self.cslab = torch.empty(self.cplan.gx * k, dtype=torch.int32, device=dev)
+        else:
+            self.hist = torch.zeros(self.aplan.grid * self.aplan.kp, dtype=torch.int32, device=dev)
+            self.rank = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+            self.off = torch.zeros(max(k * self.aplan.grid, 1), dtype=torch.int32, device=dev)
+            self.seg = torch.zeros(K.seg_buffer_ints(k), dtype=torch.int32, device=dev)
+            self.perm = torch.zeros(max(maxn, 1), dtype=torch.int32, device=dev)
         self.msg_len = k * d + k + 1
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
@@ -134,11 +143,18 @@ class LloydEngine:
             if nrow > 0:
                 xc = self.x[r0:r1]
                 lab = self.labels[r0:r1]
-                K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
-                              self.cost_part)
-                K.accumulate_bf16(xc, nrow, lab, self.k, self.cplan, self.slab, self.cslab)
-                K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, self.k, self.d, self.cplan,
-                               msg)
+                if self.cplan.mode == "priv":
+                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
+                                  self.cost_part)
+                    K.accumulate_priv(xc, nrow, lab, self.k, self.cplan, self.slab, self.cslab)
+                    K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, self.k, self.d,
+                                   self.cplan, msg)
+                else:
+                    rank = self.rank[r0:r1]
+                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
+                                  self.cost_part, self.hist, rank)
+                    K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
+                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, msg)
             else:
                 msg.zero_()
             handles.append(self.comm.allreduce_async(msg))

@@ -7,13 +7,30 @@ numerical oracle of the tests).
 """
 from __future__ import annotations
 
-import ctypes
 from dataclasses import dataclass
 
 import torch
 
 from .. import _native
-from ..utils.device import LDS_BUDGET, next_pow2, num_cus, round_up
+from .._native import c_int, c_ll, c_vp
+from ..utils.device import LDS_BUDGET, num_cus, round_up
+
+_native.register_kernel_sigs({
+    "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int, c_int]),
+    "cml_kmeans_assign_threads": (c_int, []),
+    "cml_kmeans_seg_threads": (c_int, []),
+    "cml_kmeans_seg_ints": (c_ll, [c_int]),
+    "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
+                                       c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
+    "cml_kmeans_accum_priv": (c_int, [c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int,
+                                      c_vp]),
+    "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
+    "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
+                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+    "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
+                                  c_vp]),
+})
 
 
 @dataclass
@@ -23,75 +40,105 @@ class AssignPlan:
     kp: int
     kc: int            # centres per launch (multiple of 32)
     grid: int
+    nwaves: int
 
 
 @dataclass
 class AccumPlan:
-    lpr: int
-    dsl: int
-    nsl: int
-    gx: int
+    """Race-free accumulation regime (kmeans.hip K10).
+
+    ``priv``: per-(wave,row-group) private LDS copies (small k·dw) — slabs + reduce.
+    ``sort``: counting sort by label + segmented f64 accumulation (large k·D, skew-proof).
+    """
+    mode: str
+    dw: int = 0
+    cpl: int = 2
+    rpw: int = 0
+    nsl: int = 1
+    gx: int = 1
+    seg_grid: int = 1
+
+    @property
+    def dsl(self) -> int:
+        return self.dw
 
 
 def plan_assign(n: int, dp: int, k: int, device_index: int = 0) -> AssignPlan:
     lib = _native.kernels()
     kp = round_up(max(k, 1), 32)
     kc = kp
-    while kc > 32 and lib.cml_kmeans_assign_lds_bytes(kc, dp) > LDS_BUDGET:
+    while kc > 32 and lib.cml_kmeans_assign_lds_bytes(kc, kp, dp) > LDS_BUDGET:
         kc -= 32
-    lds = lib.cml_kmeans_assign_lds_bytes(kc, dp)
+    lds = lib.cml_kmeans_assign_lds_bytes(kc, kp, dp)
     if lds > LDS_BUDGET:
-        raise ValueError(f"feature width {dp} too large for the LDS-resident centroid tile")
+        raise ValueError(f"feature width {dp} / k={k} too large for the LDS-resident centroid tile")
     waves = lib.cml_kmeans_assign_threads() // 64
     per_cu = max(1, min(4, (160 * 1024) // max(lds, 1)))
     ntiles = (n + 31) // 32
     grid = max(1, min((ntiles + waves - 1) // waves, num_cus(device_index) * per_cu))
-    return AssignPlan(n=n, dp=dp, kp=kp, kc=kc, grid=grid)
+    return AssignPlan(n=n, dp=dp, kp=kp, kc=kc, grid=grid, nwaves=waves)
 
 
-def plan_accum(n: int, dp: int, k: int, device_index: int = 0) -> AccumPlan:
-    lpr = min(64, max(1, dp // 2))
-    while lpr > 1 and k * 2 * lpr * 4 + 4 * k > 128 * 1024:
-        lpr //= 2
-    lpr = min(lpr, next_pow2(lpr))
-    dsl = 2 * lpr
-    nsl = (dp + dsl - 1) // dsl
-    lds = k * dsl * 4 + 4 * k
-    per_cu = max(1, min(2, (160 * 1024) // max(lds, 1)))
-    rows_per_wg = 16 * (64 // lpr) * 4  # waves * rows/wave-iter * unroll
-    want = max(1, (n + rows_per_wg - 1) // rows_per_wg)
-    gx = max(1, min(want, (num_cus(device_index) * per_cu + nsl - 1) // nsl))
-    return AccumPlan(lpr=lpr, dsl=dsl, nsl=nsl, gx=gx)
+def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None = None) -> AccumPlan:
+    lib = _native.kernels()
+    ncu = num_cus(device_index)
+    dw = min(dp, 256)
+    cpl = 4 if dw > 128 else 2
+    if force != "sort":
+        r = max(1, min(16, (cpl * 64) // dw))
+        while r >= 1:
+            lds = lib.cml_kmeans_priv_lds_bytes(k, dw, r)
+            if lds <= LDS_BUDGET:
+                nsl = (dp + dw - 1) // dw
+                per_cu = max(1, min(2, (160 * 1024) // max(lds, 1)))
+                want = max(1, (n + 8191) // 8192)
+                gx = max(1, min(want, (ncu * per_cu + nsl - 1) // nsl))
+                return AccumPlan(mode="priv", dw=dw, cpl=cpl, rpw=r, nsl=nsl, gx=gx)
+            r //= 2
+    if force == "priv":
+        raise ValueError("private-copy accumulation does not fit LDS")
+    if dp > 512:
+        raise ValueError("sort-regime accumulation supports Dp <= 512")
+    scpl = 2 if dp <= 128 else (4 if dp <= 256 else 8)
+    seg_grid = max(1, min((n + 255) // 256, ncu * 4))
+    return AccumPlan(mode="sort", cpl=scpl, seg_grid=seg_grid, dw=dp)
 
 
 def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor, plan: AssignPlan,
                 labels: torch.Tensor, best: torch.Tensor, cost_part: torch.Tensor | None,
-                stream=None) -> None:
-    """K9: labels/best[i] = argmin/min_j ||x_i - c_j||² over all kp (padded) centres."""
+                hist: torch.Tensor | None = None, rank: torch.Tensor | None = None, stream=None) -> None:
+    """K9: labels/best[i] = argmin/min_j ||x_i - c_j||² over all kp (padded) centres.
+
+    With ``hist``/``rank`` also emits the per-workgroup label histogram and per-row rank
+    (first pass of the counting sort used by the sort accumulation regime).
+    """
     lib = _native.kernels()
     st = _native.stream_ptr(stream)
     nch = (plan.kp + plan.kc - 1) // plan.kc
     for ci in range(nch):
         c0 = ci * plan.kc
         kc = min(plan.kc, plan.kp - c0)
+        last = ci == nch - 1
         status = lib.cml_kmeans_assign_bf16(
             x.data_ptr(), n, x.stride(0), dp,
-            cb.data_ptr() + c0 * cb.stride(0) * 2, cb.stride(0), kc, c0,
+            cb.data_ptr() + c0 * cb.stride(0) * 2, cb.stride(0), kc, plan.kp, c0,
             cnorm.data_ptr() + c0 * 4, labels.data_ptr(), best.data_ptr(),
-            int(ci == 0), int(ci == nch - 1),
-            cost_part.data_ptr() if (cost_part is not None and ci == nch - 1) else 0,
+            int(ci == 0), int(last),
+            cost_part.data_ptr() if (cost_part is not None and last) else 0,
+            hist.data_ptr() if (hist is not None and last) else 0,
+            rank.data_ptr() if (rank is not None and last) else 0,
             plan.grid, st)
         _native.check(status, "kmeans_assign_bf16")
 
 
-def accumulate_bf16(x: torch.Tensor, n: int, labels: torch.Tensor, k: int, plan: AccumPlan,
+def accumulate_priv(x: torch.Tensor, n: int, labels: torch.Tensor, k: int, plan: AccumPlan,
                     slab: torch.Tensor, cslab: torch.Tensor, stream=None) -> None:
-    """K10: slab[sl][g][c][d] = Σ_{rows of WG g, label c} x[row, sl*dsl + d]."""
+    """K10 regime A: slab[sl][g][c][d] = Σ_{rows of WG g, label c} x[row, sl*dw + d]."""
     lib = _native.kernels()
-    status = lib.cml_kmeans_accum_bf16(x.data_ptr(), n, x.stride(0), labels.data_ptr(), k, plan.lpr,
-                                       slab.data_ptr(), cslab.data_ptr(), plan.gx, plan.nsl,
+    status = lib.cml_kmeans_accum_priv(x.data_ptr(), n, x.stride(0), labels.data_ptr(), k, plan.dw, plan.cpl,
+                                       plan.rpw, slab.data_ptr(), cslab.data_ptr(), plan.gx, plan.nsl,
                                        _native.stream_ptr(stream))
-    _native.check(status, "kmeans_accum_bf16")
+    _native.check(status, "kmeans_accum_priv")
 
 
 def reduce_slabs(slab, cslab, cost_part, ncost: int, k: int, d: int, plan: AccumPlan, out: torch.Tensor,
@@ -101,6 +148,23 @@ def reduce_slabs(slab, cslab, cost_part, ncost: int, k: int, d: int, plan: Accum
     status = lib.cml_kmeans_reduce(slab.data_ptr(), cslab.data_ptr(), cost_part.data_ptr(), plan.gx, ncost, k,
                                    d, plan.dsl, out.data_ptr(), _native.stream_ptr(stream))
     _native.check(status, "kmeans_reduce")
+
+
+def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tensor, rank: torch.Tensor,
+                    hist: torch.Tensor, aplan: AssignPlan, k: int, cost_part: torch.Tensor, off: torch.Tensor,
+                    seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor, stream=None) -> None:
+    """K10 regime B: counting sort by label, then segmented f64 sums -> msg."""
+    lib = _native.kernels()
+    status = lib.cml_kmeans_sort_accum(x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(),
+                                       hist.data_ptr(), aplan.grid, aplan.nwaves, k, aplan.kp,
+                                       cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
+                                       perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
+                                       _native.stream_ptr(stream))
+    _native.check(status, "kmeans_sort_accum")
+
+
+def seg_buffer_ints(k: int) -> int:
+    return int(_native.kernels().cml_kmeans_seg_ints(k))
 
 
 def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int,
@@ -126,8 +190,8 @@ def assign_reference(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 1
     x = x.to(torch.float64)
     c = centers.to(torch.float64)
     cn = (c * c).sum(1)
-    labels = torch.empty(x.shape[0], dtype=torch.int64)
-    best = torch.empty(x.shape[0], dtype=torch.float64)
+    labels = torch.empty(x.shape[0], dtype=torch.int64, device=x.device)
+    best = torch.empty(x.shape[0], dtype=torch.float64, device=x.device)
     for s in range(0, x.shape[0], chunk):
         xb = x[s:s + chunk]
         sc = cn[None, :] - 2.0 * xb @ c.T
@@ -139,7 +203,7 @@ def assign_reference(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 1
 
 def sums_reference(x: torch.Tensor, labels: torch.Tensor, k: int):
     x = x.to(torch.float64)
-    sums = torch.zeros(k, x.shape[1], dtype=torch.float64)
+    sums = torch.zeros(k, x.shape[1], dtype=torch.float64, device=x.device)
     sums.index_add_(0, labels, x)
     counts = torch.bincount(labels, minlength=k).to(torch.float64)
     return sums, counts

@@ -38,15 +38,16 @@ def test_assign_matches_reference(n, d, k):
     np.testing.assert_allclose(best.cpu().double().numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
 
 
-@pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (50000, 256, 256), (9999, 100, 70), (2000, 16, 3)])
-def test_lloyd_step_matches_reference(n, d, k):
+@pytest.mark.parametrize("mode", [None, "sort"])
+@pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (50000, 256, 256), (9999, 100, 70), (2000, 16, 3),
+                                   (3000, 512, 40), (40000, 128, 64)])
+def test_lloyd_step_matches_reference(n, d, k, mode):
     torch.manual_seed(1)
     dev = torch.device("cuda")
     x = (torch.randn(n, d, device=dev) * 3).to(torch.bfloat16)
     init = x[:k].double().cpu().numpy()
-    eng = LloydEngine(x, d, k)
+    eng = LloydEngine(x, d, k, accum_mode=mode)
     eng.set_centers(init)
-    labels_before = None
     eng.step()
     torch.cuda.synchronize()
     lab = eng.labels[:n].cpu().long()
@@ -80,3 +81,20 @@ def test_fit_converges_on_blobs():
     # every true centre is matched by a fitted centre
     dist = torch.cdist(centers.double().cpu(), got)
     assert dist.min(1).values.max().item() < 0.5
+
+
+def test_sort_regime_handles_skew():
+    """All rows in one cluster: the segmented sum must still be exact (and not serialise)."""
+    dev = torch.device("cuda")
+    n, d, k = 30000, 256, 256
+    x = (torch.randn(n, d, device=dev) * 0.01).to(torch.bfloat16)
+    init = np.zeros((k, d))
+    init[1:] = 100.0 + np.arange(1, k)[:, None]  # every row is closest to centre 0
+    eng = LloydEngine(x, d, k, accum_mode="sort")
+    eng.set_centers(init)
+    eng.step()
+    torch.cuda.synchronize()
+    assert (eng.labels[:n] == 0).all()
+    want = x.double().mean(0).cpu().numpy()
+    np.testing.assert_allclose(eng.centers[0].cpu().numpy(), want, rtol=1e-6, atol=1e-9)
+    np.testing.assert_allclose(eng.centers[1:].cpu().numpy(), init[1:])
