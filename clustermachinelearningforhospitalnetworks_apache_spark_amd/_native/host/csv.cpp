@@ -1,0 +1,277 @@
+// Host-side CSV tokenizer / typed parser (K1 in SURVEY.md §2.5).
+//
+// Replaces Spark's per-row CSV parsing on executors for the streaming file source and
+// spark.read.csv (ref.py:75-78).  Two passes over an in-memory file image:
+//   1. cml_csv_index   — find record starts (RFC-4180 quoting: separators and newlines inside
+//                        "..." do not split, "" is an escaped quote), optional header skip;
+//   2. cml_csv_parse   — split each record into fields and convert them straight into typed,
+//                        column-major output buffers (int32/int64/float64/float32/bool/
+//                        timestamp-µs/date-days) plus a validity byte per cell; string cells
+//                        are returned as (offset, length, needs-unquote) triples into the
+//                        image.  Records are distributed over std::threads in contiguous
+//                        blocks, so the output is identical for any thread count.
+// PERMISSIVE semantics like Spark: empty or unparseable cells become null, short records pad
+// with nulls, extra fields are ignored.
+#include <algorithm>
+#include <cerrno>
+#include <cmath>
+#include <cstdint>
+#include <cstdlib>
+#include <cstring>
+#include <thread>
+#include <vector>
+
+#define CML_HOST_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+enum ColType : int { kString = 0, kInt32 = 1, kInt64 = 2, kFloat64 = 3, kTimestamp = 4, kBool = 5, kFloat32 = 6, kDate = 7 };
+
+inline long long days_from_civil(long long y, unsigned m, unsigned d) {
+  y -= m <= 2;
+  const long long era = (y >= 0 ? y : y - 399) / 400;
+  const unsigned yoe = static_cast<unsigned>(y - era * 400);
+  const unsigned doy = (153 * (m + (m > 2 ? -3 : 9)) + 2) / 5 + d - 1;
+  const unsigned doe = yoe * 365 + yoe / 4 - yoe / 100 + doy;
+  return era * 146097 + static_cast<long long>(doe) - 719468;
+}
+
+inline bool parse_uint(const char*& p, const char* e, int ndig_min, int ndig_max, long long& out) {
+  long long v = 0;
+  int n = 0;
+  while (p < e && n < ndig_max && *p >= '0' && *p <= '9') {
+    v = v * 10 + (*p - '0');
+    ++p;
+    ++n;
+  }
+  out = v;
+  return n >= ndig_min;
+}
+
+// "YYYY-MM-DD[( |T)HH:MM[:SS[.ffffff]]][Z]" -> microseconds since epoch (UTC)
+bool parse_timestamp(const char* p, const char* e, long long& us, bool date_only) {
+  long long y, mo, d, hh = 0, mm = 0, ss = 0, frac = 0;
+  if (!parse_uint(p, e, 4, 4, y) || p >= e || *p++ != '-') return false;
+  if (!parse_uint(p, e, 1, 2, mo) || p >= e || *p++ != '-') return false;
+  if (!parse_uint(p, e, 1, 2, d)) return false;
+  if (p < e && (*p == ' ' || *p == 'T')) {
+    ++p;
+    if (!parse_uint(p, e, 1, 2, hh) || p >= e || *p++ != ':') return false;
+    if (!parse_uint(p, e, 1, 2, mm)) return false;
+    if (p < e && *p == ':') {
+      ++p;
+      if (!parse_uint(p, e, 1, 2, ss)) return false;
+      if (p < e && *p == '.') {
+        ++p;
+        int n = 0;
+        while (p < e && *p >= '0' && *p <= '9') {
+          if (n < 6) { frac = frac * 10 + (*p - '0'); ++n; }
+          ++p;
+        }
+        while (n < 6) { frac *= 10; ++n; }
+      }
+    }
+  }
+  if (p < e && *p == 'Z') ++p;
+  while (p < e && (*p == ' ' || *p == '\r')) ++p;
+  if (p != e) return false;
+  if (mo < 1 || mo > 12 || d < 1 || d > 31 || hh > 23 || mm > 59 || ss > 60) return false;
+  const long long days = days_from_civil(y, (unsigned)mo, (unsigned)d);
+  us = date_only ? days : ((days * 86400 + hh * 3600 + mm * 60 + ss) * 1000000LL + frac);
+  return true;
+}
+
+inline void trim(const char*& b, const char*& e) {
+  while (b < e && (*b == ' ' || *b == '\t')) ++b;
+  while (e > b && (e[-1] == ' ' || e[-1] == '\t' || e[-1] == '\r')) --e;
+}
+
+struct Outputs {
+  int ncols;
+  const int* types;
+  void** data;               // per column: typed array [nrows] (strings: int64 triples [nrows*3])
+  unsigned char** valid;     // per column: [nrows]
+};
+
+void store_cell(const Outputs& o, int c, long long r, const char* b, const char* e, bool quoted, bool has_esc) {
+  unsigned char* v = o.valid[c];
+  if (o.types[c] != kString) trim(b, e);
+  if (b == e && !quoted) {
+    v[r] = 0;
+    if (o.types[c] == kString) {
+      long long* t = static_cast<long long*>(o.data[c]) + 3 * r;
+      t[0] = 0; t[1] = 0; t[2] = 0;
+    }
+    return;
+  }
+  char buf[96];
+  switch (o.types[c]) {
+    case kString: {
+      long long* t = static_cast<long long*>(o.data[c]) + 3 * r;
+      t[0] = (long long)(intptr_t)b;  // absolute pointer; converted to an offset by the caller
+      t[1] = (long long)(e - b);
+      t[2] = has_esc ? 1 : 0;
+      v[r] = 1;
+      return;
+    }
+    case kInt32:
+    case kInt64: {
+      const size_t n = std::min<size_t>(e - b, sizeof(buf) - 1);
+      memcpy(buf, b, n);
+      buf[n] = 0;
+      char* end = nullptr;
+      errno = 0;
+      long long x = strtoll(buf, &end, 10);
+      bool ok = end == buf + n && errno == 0;
+      if (!ok) {  // accept "3.0"-style integers like Spark's permissive cast? no: Spark nulls them
+        v[r] = 0;
+        return;
+      }
+      if (o.types[c] == kInt32) {
+        if (x < INT32_MIN || x > INT32_MAX) { v[r] = 0; return; }
+        static_cast<int32_t*>(o.data[c])[r] = (int32_t)x;
+      } else {
+        static_cast<int64_t*>(o.data[c])[r] = x;
+      }
+      v[r] = 1;
+      return;
+    }
+    case kFloat64:
+    case kFloat32: {
+      const size_t n = std::min<size_t>(e - b, sizeof(buf) - 1);
+      memcpy(buf, b, n);
+      buf[n] = 0;
+      char* end = nullptr;
+      double x = strtod(buf, &end);
+      if (end != buf + n) { v[r] = 0; return; }
+      if (o.types[c] == kFloat64) static_cast<double*>(o.data[c])[r] = x;
+      else static_cast<float*>(o.data[c])[r] = (float)x;
+      v[r] = 1;
+      return;
+    }
+    case kBool: {
+      const size_t n = e - b;
+      bool val;
+      if (n == 4 && strncasecmp(b, "true", 4) == 0) val = true;
+      else if (n == 5 && strncasecmp(b, "false", 5) == 0) val = false;
+      else { v[r] = 0; return; }
+      static_cast<unsigned char*>(o.data[c])[r] = val;
+      v[r] = 1;
+      return;
+    }
+    case kTimestamp:
+    case kDate: {
+      long long us = 0;
+      const bool date_only = o.types[c] == kDate;
+      if (!parse_timestamp(b, e, us, date_only)) { v[r] = 0; return; }
+      if (date_only) static_cast<int32_t*>(o.data[c])[r] = (int32_t)us;
+      else static_cast<int64_t*>(o.data[c])[r] = us;
+      v[r] = 1;
+      return;
+    }
+    default:
+      v[r] = 0;
+  }
+}
+
+void parse_record(const char* p, const char* end, char sep, char quote, const Outputs& o, long long r) {
+  int c = 0;
+  while (c < o.ncols) {
+    const char* fb;
+    const char* fe;
+    bool quoted = false, esc = false;
+    if (p < end && *p == quote) {
+      quoted = true;
+      ++p;
+      fb = p;
+      while (p < end) {
+        if (*p == quote) {
+          if (p + 1 < end && p[1] == quote) { esc = true; p += 2; continue; }
+          break;
+        }
+        ++p;
+      }
+      fe = p;
+      if (p < end) ++p;  // closing quote
+      while (p < end && *p != sep && *p != '\n') ++p;
+    } else {
+      fb = p;
+      while (p < end && *p != sep && *p != '\n') ++p;
+      fe = p;
+    }
+    store_cell(o, c, r, fb, fe, quoted, esc);
+    ++c;
+    if (p < end && *p == sep) {
+      ++p;
+      continue;
+    }
+    break;  // end of record
+  }
+  for (; c < o.ncols; ++c) store_cell(o, c, r, p, p, false, false);  // short record: nulls
+}
+
+}  // namespace
+
+// Record starts of `buf`: returns the number of records (after skipping `skip_header` records),
+// writes at most `cap` starts (pass cap = 0 to only count). Blank lines are skipped.
+CML_HOST_API long long cml_csv_index(const char* buf, long long len, char quote, int skip_header, long long* starts,
+                                     long long cap) {
+  long long n = 0;
+  long long i = 0;
+  int skipped = 0;
+  while (i < len) {
+    const long long s = i;
+    bool inq = false;
+    while (i < len) {
+      const char ch = buf[i];
+      if (ch == quote) inq = !inq;
+      else if (ch == '\n' && !inq) break;
+      ++i;
+    }
+    long long e = i;
+    if (i < len) ++i;  // consume '\n'
+    while (e > s && (buf[e - 1] == '\r' || buf[e - 1] == ' ')) --e;
+    if (e == s) continue;  // blank line
+    if (skipped < skip_header) { ++skipped; continue; }
+    if (n < cap && starts) starts[n] = s;
+    ++n;
+  }
+  return n;
+}
+
+// Parse `nrows` records starting at byte offsets `starts` into column buffers. String cells are
+// written as (byte offset into buf, byte length, needs-unquote) triples. Returns 0 on success.
+CML_HOST_API int cml_csv_parse(const char* buf, long long len, const long long* starts, long long nrows, int ncols,
+                               char sep, char quote, const int* types, void** data, unsigned char** valid,
+                               int nthreads) {
+  Outputs o{ncols, types, data, valid};
+  if (nthreads < 1) nthreads = 1;
+  const long long per = (nrows + nthreads - 1) / nthreads;
+  auto work = [&](long long r0, long long r1) {
+    for (long long r = r0; r < r1; ++r) {
+      const char* p = buf + starts[r];
+      const char* e = r + 1 < nrows ? buf + starts[r + 1] : buf + len;
+      // the record ends at the first unquoted newline; parse_record stops there itself
+      parse_record(p, e, sep, quote, o, r);
+    }
+  };
+  std::vector<std::thread> th;
+  for (int t = 0; t < nthreads; ++t) {
+    const long long r0 = t * per, r1 = std::min(nrows, r0 + per);
+    if (r0 >= r1) break;
+    if (t == nthreads - 1 || r1 == nrows) { work(r0, r1); break; }
+    th.emplace_back(work, r0, r1);
+  }
+  for (auto& x : th) x.join();
+  // convert string pointers to offsets
+  for (int c = 0; c < ncols; ++c) {
+    if (types[c] != kString) continue;
+    long long* t = static_cast<long long*>(data[c]);
+    for (long long r = 0; r < nrows; ++r)
+      if (valid[c][r]) t[3 * r] -= (long long)(intptr_t)buf;
+  }
+  return 0;
+}
+
+// Days-from-civil exposed for the Python side (tests / scalar conversions).
+CML_HOST_API long long cml_days_from_civil(long long y, int m, int d) { return days_from_civil(y, (unsigned)m, (unsigned)d); }

@@ -1,0 +1,188 @@
+"""CSV source (spark.read.csv / readStream.csv, ref.py:75-78) on the native host parser.
+
+Files are split over ranks (whole files round-robin when there are at least as many
+files as ranks, otherwise record ranges of each file); every row gets the global
+id ``(file_index << 40) | record_index`` so results do not depend on the rank count.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+from typing import Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _native
+from .._native import c_int, c_ll, c_vp
+from ..sql import types as T
+from ..sql.builder import column_from_values, shard_range
+from ..sql.column import ColumnData
+
+_native.register_host_sigs({
+    "cml_csv_index": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll]),
+    "cml_csv_parse": (c_int, [ctypes.c_char_p, c_ll, c_vp, c_ll, c_int, ctypes.c_char, ctypes.c_char, c_vp, c_vp,
+                              c_vp, c_int]),
+})
+
+_TYPE_CODE = {T.StringType: 0, T.IntegerType: 1, T.LongType: 2, T.DoubleType: 3, T.TimestampType: 4,
+              T.BooleanType: 5, T.FloatType: 6, T.DateType: 7, T.ShortType: 1, T.ByteType: 1}
+
+
+def _code(dt: T.DataType) -> int:
+    return _TYPE_CODE.get(type(dt), 0)
+
+
+def _np_dtype(code: int):
+    return {0: np.int64, 1: np.int32, 2: np.int64, 3: np.float64, 4: np.int64, 5: np.uint8, 6: np.float32,
+            7: np.int32}[code]
+
+
+def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = ",", quote: str = '"',
+                    rows: Optional[slice] = None, nthreads: Optional[int] = None):
+    """Parse a CSV image into host arrays: {name: (values np.ndarray, valid np.ndarray)}, nrecords."""
+    lib = _native.host()
+    n_all = lib.cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, None, 0)
+    starts = np.zeros(max(n_all, 1), dtype=np.int64)
+    lib.cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, starts.ctypes.data, n_all)
+    starts = starts[:n_all]
+    if rows is not None:
+        starts = starts[rows]
+    n = int(starts.shape[0])
+    ncols = len(schema.fields)
+    codes = np.array([_code(f.dataType) for f in schema.fields], dtype=np.int32)
+    datas = [np.zeros(n * 3 if c == 0 else n, dtype=_np_dtype(c)) for c in codes]
+    valids = [np.zeros(max(n, 1), dtype=np.uint8) for _ in codes]
+    dptr = (ctypes.c_void_p * ncols)(*[d.ctypes.data for d in datas])
+    vptr = (ctypes.c_void_p * ncols)(*[v.ctypes.data for v in valids])
+    if n:
+        nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+        st = lib.cml_csv_parse(buf, len(buf), starts.ctypes.data, n, ncols, sep.encode(), quote.encode(),
+                               codes.ctypes.data, dptr, vptr, nthreads)
+        if st != 0:
+            raise RuntimeError("CSV parse failed")
+    out = {}
+    for f, c, d, v in zip(schema.fields, codes, datas, valids):
+        valid = v[:n].astype(bool)
+        if c == 0:
+            trip = d.reshape(n, 3) if n else d.reshape(0, 3)
+            vals = np.empty(n, dtype=object)
+            for i in range(n):
+                if valid[i]:
+                    s = buf[trip[i, 0]: trip[i, 0] + trip[i, 1]].decode("utf-8", "replace")
+                    if trip[i, 2]:
+                        s = s.replace(quote * 2, quote)
+                    vals[i] = s
+            out[f.name] = (vals, valid)
+        elif c == 5:
+            out[f.name] = (d[:n].astype(bool), valid)
+        else:
+            out[f.name] = (d[:n], valid)
+    return out, n
+
+
+def header_names(buf: bytes, sep: str = ",", quote: str = '"') -> List[str]:
+    line = buf.split(b"\n", 1)[0].decode("utf-8", "replace").rstrip("\r")
+    import csv as _csv
+    return [c.strip() for c in next(_csv.reader([line], delimiter=sep, quotechar=quote))]
+
+
+def infer_schema(buf: bytes, header: bool, sep: str, quote: str, infer: bool, sample: int = 1000) -> T.StructType:
+    names = header_names(buf, sep, quote)
+    if not header:
+        names = [f"_c{i}" for i in range(len(names))]
+    st = T.StructType([T.StructField(n, T.StringType()) for n in names])
+    if not infer:
+        return st
+    parsed, n = parse_csv_bytes(buf, st, header, sep, quote, rows=slice(0, sample))
+    fields = []
+    for name in names:
+        vals, valid = parsed[name]
+        fields.append(T.StructField(name, _infer_from_strings([v for v, ok in zip(vals, valid) if ok])))
+    return T.StructType(fields)
+
+
+def _infer_from_strings(vals: List[str]) -> T.DataType:
+    from ..sql.column import ts_to_micros
+    if not vals:
+        return T.StringType()
+
+    def all_ok(fn):
+        try:
+            for v in vals:
+                fn(v)
+            return True
+        except (ValueError, TypeError):
+            return False
+
+    if all_ok(lambda v: int(v) if -2**31 <= int(v) < 2**31 else (_ for _ in ()).throw(ValueError())):
+        return T.IntegerType()
+    if all_ok(int):
+        return T.LongType()
+    if all_ok(float):
+        return T.DoubleType()
+    if all(v.lower() in ("true", "false") for v in vals):
+        return T.BooleanType()
+    if all_ok(ts_to_micros):
+        return T.TimestampType()
+    return T.StringType()
+
+
+def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType], header: bool, sep: str = ",",
+                   quote: str = '"', infer: bool = False, file_index_base: int = 0,
+                   file_ids: Optional[Sequence[int]] = None):
+    """Read CSV files into this rank's shard. Returns a DataFrame."""
+    from ..sql.builder import frame_from_pycolumns
+    comm = session._comm
+    W, rank = comm.world_size, comm.rank
+    paths = list(paths)
+    if schema is None:
+        if not paths:
+            raise ValueError("cannot infer a schema without input files; pass .schema(...)")
+        with open(paths[0], "rb") as fh:
+            schema = infer_schema(fh.read(1 << 20), header, sep, quote, infer)
+    fids = list(file_ids) if file_ids is not None else [file_index_base + i for i in range(len(paths))]
+    whole_files = len(paths) >= W
+    cols: Dict[str, List] = {f.name: [] for f in schema.fields}
+    valids: Dict[str, List] = {f.name: [] for f in schema.fields}
+    ids: List[np.ndarray] = []
+    for i, (p, fid) in enumerate(zip(paths, fids)):
+        if whole_files and i % W != rank:
+            continue
+        with open(p, "rb") as fh:
+            buf = fh.read()
+        if whole_files:
+            sl = None
+        else:
+            n_all = _native.host().cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, None, 0)
+            a, b = shard_range(n_all, rank, W)
+            sl = slice(a, b)
+        parsed, n = parse_csv_bytes(buf, schema, header, sep, quote, rows=sl)
+        start = 0 if sl is None else sl.start
+        ids.append((np.int64(fid) << np.int64(40)) + np.arange(start, start + n, dtype=np.int64))
+        for f in schema.fields:
+            v, ok = parsed[f.name]
+            cols[f.name].append(v)
+            valids[f.name].append(ok)
+    dev = session._device
+    from ..sql.dataframe import DataFrame
+    out_cols = {}
+    n_total = int(sum(a.shape[0] for a in ids)) if ids else 0
+    for f in schema.fields:
+        if cols[f.name]:
+            vals = np.concatenate(cols[f.name])
+            ok = np.concatenate(valids[f.name])
+        else:
+            vals = np.zeros(0, dtype=object if isinstance(f.dataType, T.StringType) else np.float64)
+            ok = np.zeros(0, dtype=bool)
+        out_cols[f.name] = _to_column(vals, ok, f.dataType, dev)
+    rid = torch.as_tensor(np.concatenate(ids) if ids else np.zeros(0, dtype=np.int64), device=dev)
+    return DataFrame(session, schema, out_cols, n_total, rid, dev)
+
+
+def _to_column(vals: np.ndarray, ok: np.ndarray, dt: T.DataType, dev) -> ColumnData:
+    if isinstance(dt, (T.StringType, T.BinaryType)) or dt.torch_dtype is None:
+        return ColumnData(vals.astype(object), None if ok.all() else ok, dt)
+    t = torch.as_tensor(np.ascontiguousarray(vals)).to(device=dev, dtype=dt.torch_dtype)
+    valid = None if ok.all() else torch.as_tensor(ok, device=dev)
+    return ColumnData(t, valid, dt)

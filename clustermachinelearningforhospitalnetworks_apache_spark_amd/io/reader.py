@@ -1,0 +1,147 @@
+"""spark.read — DataFrameReader (csv / parquet / json / table / delta-style table paths)."""
+from __future__ import annotations
+
+import glob
+import os
+from typing import Dict, List, Optional, Union
+
+from ..sql import types as T
+
+
+def expand_paths(path: Union[str, List[str]], exts=None) -> List[str]:
+    paths = [path] if isinstance(path, str) else list(path)
+    out: List[str] = []
+    for p in paths:
+        p = strip_scheme(p)
+        if os.path.isdir(p):
+            for root, dirs, files in os.walk(p):
+                dirs[:] = sorted(d for d in dirs if not d.startswith(("_", ".")))
+                for f in sorted(files):
+                    if f.startswith(("_", ".")):
+                        continue
+                    if exts and not any(f.endswith(e) for e in exts):
+                        continue
+                    out.append(os.path.join(root, f))
+        elif any(ch in p for ch in "*?["):
+            out += sorted(glob.glob(p))
+        else:
+            out.append(p)
+    return out
+
+
+def strip_scheme(p: str) -> str:
+    """file:// paths are local; hdfs://host:port/x maps onto the local warehouse root (no HDFS here)."""
+    if p.startswith("file://"):
+        return p[len("file://"):]
+    if p.startswith("hdfs://"):
+        rest = p[len("hdfs://"):]
+        rest = rest.split("/", 1)[1] if "/" in rest else ""
+        base = os.environ.get("CML_HDFS_ROOT", os.path.join(os.getcwd(), "hdfs"))
+        return os.path.join(base, rest)
+    return p
+
+
+class DataFrameReader:
+    def __init__(self, session):
+        self._session = session
+        self._format = "parquet"
+        self._schema: Optional[T.StructType] = None
+        self._options: Dict[str, str] = {}
+
+    def format(self, source: str) -> "DataFrameReader":
+        self._format = source.lower()
+        return self
+
+    def schema(self, schema) -> "DataFrameReader":
+        self._schema = T.parse_ddl_schema(schema) if isinstance(schema, str) else schema
+        return self
+
+    def option(self, key: str, value) -> "DataFrameReader":
+        self._options[key.lower()] = value
+        return self
+
+    def options(self, **opts) -> "DataFrameReader":
+        for k, v in opts.items():
+            self.option(k, v)
+        return self
+
+    def _bool(self, key, default=False) -> bool:
+        v = self._options.get(key, default)
+        return v if isinstance(v, bool) else str(v).lower() == "true"
+
+    def load(self, path=None, format=None, schema=None, **options):
+        if format:
+            self.format(format)
+        if schema is not None:
+            self.schema(schema)
+        for k, v in options.items():
+            self.option(k, v)
+        f = self._format
+        if f == "csv":
+            return self.csv(path)
+        if f == "parquet":
+            return self.parquet(path)
+        if f == "json":
+            return self.json(path)
+        if f in ("delta", "table"):
+            from . import table
+            return table.read_table(self._session, strip_scheme(path), self._options.get("versionasof"))
+        raise ValueError(f"unsupported format {f}")
+
+    def csv(self, path, schema=None, sep=None, header=None, inferSchema=None, **kw):
+        from .csv import read_csv_files
+        if schema is not None:
+            self.schema(schema)
+        if header is not None:
+            self.option("header", header)
+        if sep is not None:
+            self.option("sep", sep)
+        if inferSchema is not None:
+            self.option("inferschema", inferSchema)
+        files = expand_paths(path)
+        return read_csv_files(self._session, files, self._schema, self._bool("header"),
+                              sep=str(self._options.get("sep", self._options.get("delimiter", ","))),
+                              quote=str(self._options.get("quote", '"')), infer=self._bool("inferschema"))
+
+    def parquet(self, *paths):
+        from .arrow import read_parquet_files
+        from . import table
+        files: List[str] = []
+        for p in paths:
+            sp = strip_scheme(p)
+            if os.path.isdir(sp) and table.exists(sp):
+                return table.read_table(self._session, sp)
+            files += expand_paths(p, exts=[".parquet"])
+        return read_parquet_files(self._session, files, self._schema)
+
+    def json(self, path, schema=None):
+        import pandas as pd
+        import pyarrow as pa
+        from .arrow import frame_from_arrow
+        from ..sql.builder import shard_range
+        if schema is not None:
+            self.schema(schema)
+        files = expand_paths(path)
+        frames = [pd.read_json(f, lines=True) for f in files]
+        pdf = pd.concat(frames, ignore_index=True) if frames else pd.DataFrame()
+        comm = self._session._comm
+        a, b = shard_range(len(pdf), comm.rank, comm.world_size)
+        table = pa.Table.from_pandas(pdf.iloc[a:b], preserve_index=False)
+        df = frame_from_arrow(self._session, table, list(range(a, b)))
+        if self._schema is not None:
+            df = df.select(*[df[f.name].cast(f.dataType).alias(f.name) for f in self._schema.fields])
+        return df
+
+    def table(self, name: str):
+        return self._session.table(name)
+
+    def text(self, path):
+        from ..sql.builder import frame_from_pycolumns, shard_range
+        lines: List[str] = []
+        for f in expand_paths(path):
+            with open(f) as fh:
+                lines += fh.read().splitlines()
+        comm = self._session._comm
+        a, b = shard_range(len(lines), comm.rank, comm.world_size)
+        schema = T.StructType([T.StructField("value", T.StringType())])
+        return frame_from_pycolumns(self._session, schema, {"value": lines[a:b]}, list(range(a, b)))

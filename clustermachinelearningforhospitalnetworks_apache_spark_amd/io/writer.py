@@ -1,0 +1,144 @@
+"""df.write — DataFrameWriter (parquet / csv / json / table / saveAsTable)."""
+from __future__ import annotations
+
+import os
+import shutil
+from typing import Dict, Optional
+
+from .reader import strip_scheme
+
+
+class DataFrameWriter:
+    def __init__(self, df):
+        self._df = df
+        self._format = "parquet"
+        self._mode = "errorifexists"
+        self._options: Dict[str, str] = {}
+        self._partition_by = None
+
+    def format(self, source: str) -> "DataFrameWriter":
+        self._format = source.lower()
+        return self
+
+    def mode(self, saveMode: str) -> "DataFrameWriter":
+        m = (saveMode or "errorifexists").lower()
+        if m not in ("append", "overwrite", "error", "errorifexists", "ignore"):
+            raise ValueError(f"unknown save mode {saveMode}")
+        self._mode = m
+        return self
+
+    def option(self, key, value) -> "DataFrameWriter":
+        self._options[key.lower()] = value
+        return self
+
+    def options(self, **opts) -> "DataFrameWriter":
+        for k, v in opts.items():
+            self.option(k, v)
+        return self
+
+    def partitionBy(self, *cols) -> "DataFrameWriter":
+        self._partition_by = cols
+        return self
+
+    def _prepare_dir(self, path: str) -> bool:
+        """Apply the save mode to a plain directory output. Returns False when the write is skipped."""
+        comm = self._df._comm
+        exists = os.path.exists(path) and bool(os.listdir(path)) if os.path.isdir(path) else os.path.exists(path)
+        if exists:
+            if self._mode in ("error", "errorifexists"):
+                raise FileExistsError(f"path {path} already exists")
+            if self._mode == "ignore":
+                return False
+            if self._mode == "overwrite":
+                comm.barrier()
+                if comm.is_root:
+                    shutil.rmtree(path) if os.path.isdir(path) else os.remove(path)
+                comm.barrier()
+        os.makedirs(path, exist_ok=True)
+        comm.barrier()
+        return True
+
+    def save(self, path: Optional[str] = None, format: Optional[str] = None, mode: Optional[str] = None, **opts):
+        if format:
+            self.format(format)
+        if mode:
+            self.mode(mode)
+        path = strip_scheme(path)
+        f = self._format
+        if f in ("delta", "table"):
+            from . import table
+            table.write_frame(self._df, path, self._mode)
+            return
+        if f == "parquet":
+            return self.parquet(path)
+        if f == "csv":
+            return self.csv(path)
+        if f == "json":
+            return self.json(path)
+        raise ValueError(f"unsupported format {f}")
+
+    def _part(self, path: str, ext: str) -> str:
+        comm = self._df._comm
+        import uuid
+        return os.path.join(path, f"part-{comm.rank:05d}-{uuid.uuid4().hex[:8]}.{ext}")
+
+    def _success(self, path: str):
+        comm = self._df._comm
+        comm.barrier()
+        if comm.is_root:
+            open(os.path.join(path, "_SUCCESS"), "w").close()
+        comm.barrier()
+
+    def parquet(self, path: str, mode: Optional[str] = None):
+        import pyarrow.parquet as pq
+        from .arrow import frame_to_arrow
+        if mode:
+            self.mode(mode)
+        path = strip_scheme(path)
+        if not self._prepare_dir(path):
+            return
+        pq.write_table(frame_to_arrow(self._df), self._part(path, "parquet"))
+        self._success(path)
+
+    def csv(self, path: str, mode: Optional[str] = None, header=None, sep=None):
+        if mode:
+            self.mode(mode)
+        if header is not None:
+            self.option("header", header)
+        if sep is not None:
+            self.option("sep", sep)
+        path = strip_scheme(path)
+        if not self._prepare_dir(path):
+            return
+        pdf = self._local_pandas()
+        hdr = str(self._options.get("header", "false")).lower() == "true"
+        pdf.to_csv(self._part(path, "csv"), index=False, header=hdr, sep=self._options.get("sep", ","))
+        self._success(path)
+
+    def json(self, path: str, mode: Optional[str] = None):
+        if mode:
+            self.mode(mode)
+        path = strip_scheme(path)
+        if not self._prepare_dir(path):
+            return
+        self._local_pandas().to_json(self._part(path, "json"), orient="records", lines=True, date_format="iso")
+        self._success(path)
+
+    def _local_pandas(self):
+        import pandas as pd
+        from ..sql.dataframe import column_to_python
+        df = self._df
+        data = {}
+        for f in df.schema.fields:
+            vals = column_to_python(df._cols[f.name])
+            data[f.name] = [v.toArray().tolist() if hasattr(v, "toArray") else v for v in vals]
+        return pd.DataFrame(data, columns=df.columns)
+
+    def saveAsTable(self, name: str, format: Optional[str] = None, mode: Optional[str] = None):
+        if mode:
+            self.mode(mode)
+        self._df._session.catalog._save_table(name, self._df, self._mode)
+
+    def insertInto(self, tableName: str, overwrite: bool = False):
+        self.mode("overwrite" if overwrite else "append")
+        self._df._session.catalog._save_table(tableName, self._df, self._mode)

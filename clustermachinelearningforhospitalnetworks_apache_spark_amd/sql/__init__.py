@@ -1,0 +1,10 @@
+"""pyspark.sql-compatible front end on a sharded, device-resident columnar frame."""
+from . import functions, types
+from .column import Column
+from .dataframe import DataFrame, DataFrameNaFunctions
+from .group import GroupedData
+from .session import SparkSession, Session
+from .types import Row
+
+__all__ = ["SparkSession", "Session", "DataFrame", "DataFrameNaFunctions", "Column", "Row", "GroupedData",
+           "functions", "types"]

@@ -1,0 +1,376 @@
+"""Global (cross-shard) relational operators: aggregation, grouping, sort, distinct,
+describe, join, rebalance.
+
+Aggregation computes partial statistics per group on each rank (count, Σ,
+mean/M2 for Chan's parallel variance merge, min, max), all-gathers the small
+partials and merges them; results are placed on ranks round-robin so
+``count()``/``collect()`` see every group exactly once.  Sort / distinct / join
+gather to the host — they serve reference-scale analytics, not the hot path.
+"""
+from __future__ import annotations
+
+import math
+from typing import Any, Dict, List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from . import types as T
+from .builder import rows_contiguous, rows_round_robin
+from .column import AggExpr, Alias, ColRef, Column, ColumnData, Expr, SortOrder, _to_host
+from .dataframe import DataFrame, _as_expr, column_to_python
+
+
+def _agg_name(e: Expr) -> str:
+    return e.name()
+
+
+def _result_type(fn: str, in_type: Optional[T.DataType]) -> T.DataType:
+    if fn == "count":
+        return T.LongType()
+    if fn in ("avg", "stddev", "stddev_pop", "variance", "var_pop"):
+        return T.DoubleType()
+    if fn == "sum":
+        return T.LongType() if in_type is not None and T.is_integral(in_type) else T.DoubleType()
+    return in_type or T.DoubleType()
+
+
+def _unwrap(e: Expr):
+    alias = None
+    if isinstance(e, Alias):
+        alias, e = e.alias, e.child
+    return alias, e
+
+
+def _partial(values: List[Any], fn: str, distinct: bool):
+    vals = [v for v in values if v is not None and not (isinstance(v, float) and math.isnan(v) and fn != "count")]
+    if fn == "count":
+        return ("set", set(vals)) if distinct else ("n", len(vals))
+    if fn == "first":
+        return ("first", vals[0] if vals else None)
+    if fn in ("min", "max"):
+        if not vals:
+            return (fn, None)
+        return (fn, min(vals) if fn == "min" else max(vals))
+    nums = [float(v) for v in vals]
+    if fn == "sum" and vals and all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in vals):
+        return ("isum", len(nums), int(np.sum(np.asarray(vals, dtype=np.int64))))
+    if not nums:
+        return ("mom", 0, 0.0, 0.0, 0.0)
+    a = np.asarray(nums, dtype=np.float64)
+    mu = float(a.mean())
+    return ("mom", len(nums), float(a.sum()), mu, float(((a - mu) ** 2).sum()))
+
+
+def _merge(parts, fn: str):
+    kind = parts[0][0]
+    if kind == "n":
+        return sum(p[1] for p in parts)
+    if kind == "set":
+        s = set()
+        for p in parts:
+            s |= p[1]
+        return len(s)
+    if kind == "first":
+        for p in parts:
+            if p[1] is not None:
+                return p[1]
+        return None
+    if kind in ("min", "max"):
+        vals = [p[1] for p in parts if p[1] is not None]
+        if not vals:
+            return None
+        return min(vals) if kind == "min" else max(vals)
+    if kind == "isum" or all(p[0] == "isum" for p in parts):
+        n = sum(p[1] for p in parts if p[0] == "isum")
+        s = sum(p[2] for p in parts if p[0] == "isum") + sum(p[2] for p in parts if p[0] == "mom")
+        return s if n else None
+    # Chan et al. parallel merge of (count, mean, M2)
+    n, mean, m2, s = 0, 0.0, 0.0, 0.0
+    for p in parts:
+        if p[0] != "mom" or p[1] == 0:
+            continue
+        nb, sb, mb, m2b = p[1], p[2], p[3], p[4]
+        delta = mb - mean
+        tot = n + nb
+        mean = mean + delta * nb / tot
+        m2 = m2 + m2b + delta * delta * n * nb / tot
+        n = tot
+        s += sb
+    if n == 0:
+        return None
+    if fn == "sum":
+        return s
+    if fn == "avg":
+        return s / n
+    var_pop = max(m2 / n, 0.0)
+    if fn in ("var_pop", "stddev_pop"):
+        return var_pop if fn == "var_pop" else math.sqrt(var_pop)
+    if n < 2:
+        return None
+    var = var_pop * n / (n - 1)
+    return var if fn == "variance" else math.sqrt(var)
+
+
+def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
+    comm = df._comm
+    key_names = [k.name() for k in keys]
+    key_vals = [column_to_python(k.eval(df)) for k in keys]
+    key_types = [k.eval(df).dtype for k in keys] if keys else []
+    specs = []
+    for e in exprs:
+        alias, inner = _unwrap(e)
+        if not isinstance(inner, AggExpr):
+            if isinstance(inner, ColRef) and inner.col in key_names:
+                specs.append(("key", alias or inner.col, key_names.index(inner.col), None))
+                continue
+            raise ValueError(f"expression {e} is neither an aggregate nor a grouping column")
+        if inner.child is None:
+            vals = [1] * df._nrows
+            itype = T.LongType()
+        else:
+            cd = inner.child.eval(df)
+            vals = column_to_python(cd)
+            itype = cd.dtype
+        specs.append(("agg", alias or _agg_name(inner), inner, vals, itype))
+    # local partials per group
+    groups: Dict[tuple, List[Any]] = {}
+    order: List[tuple] = []
+    for i in range(df._nrows):
+        key = tuple(kv[i] for kv in key_vals)
+        if key not in groups:
+            groups[key] = []
+            order.append(key)
+        groups[key].append(i)
+    if not keys and not groups:
+        groups[()] = []
+        order.append(())
+    local = {}
+    for key in order:
+        idx = groups[key]
+        parts = []
+        for sp in specs:
+            if sp[0] == "key":
+                parts.append(None)
+            else:
+                _, _, agg, vals, _ = sp
+                parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct))
+        local[key] = parts
+    gathered = comm.allgather_object(local)
+    merged: Dict[tuple, List[List[Any]]] = {}
+    morder: List[tuple] = []
+    for part in gathered:
+        for key, parts in part.items():
+            if key not in merged:
+                merged[key] = [[] for _ in specs]
+                morder.append(key)
+            for j, p in enumerate(parts):
+                if p is not None:
+                    merged[key][j].append(p)
+    rows = []
+    for key in morder:
+        row = []
+        for j, sp in enumerate(specs):
+            if sp[0] == "key":
+                row.append(key[sp[2]])
+            else:
+                row.append(_merge(merged[key][j], sp[2].fn))
+        rows.append(row)
+    fields = []
+    for sp in specs:
+        if sp[0] == "key":
+            fields.append(T.StructField(sp[1], key_types[sp[2]], True))
+        else:
+            fields.append(T.StructField(sp[1], _result_type(sp[2].fn, sp[4]), True))
+    schema = T.StructType(fields)
+    for j, f in enumerate(fields):
+        if isinstance(f.dataType, T.LongType):
+            for r in rows:
+                if r[j] is not None:
+                    r[j] = int(r[j])
+    return rows_round_robin(df._session, schema, rows)
+
+
+class GroupedData:
+    def __init__(self, df: DataFrame, keys: List[Expr]):
+        self.df = df
+        self.keys = keys
+
+    def agg(self, *exprs) -> DataFrame:
+        if len(exprs) == 1 and isinstance(exprs[0], dict):
+            from . import functions as F
+            exprs = tuple(getattr(F, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})")
+                          for c, fn in exprs[0].items())
+        es = [ColRef(k.name()) for k in self.keys] + [_as_expr(e) for e in exprs]
+        return aggregate(self.df, self.keys, es)
+
+    def _simple(self, fn: str, cols) -> DataFrame:
+        from . import functions as F
+        if not cols:
+            cols = [f.name for f in self.df.schema.fields
+                    if T.is_numeric(f.dataType) and f.name not in [k.name() for k in self.keys]]
+        return self.agg(*[getattr(F, fn)(c).alias(f"{fn}({c})") for c in cols])
+
+    def count(self) -> DataFrame:
+        from . import functions as F
+        return self.agg(F.count("*").alias("count"))
+
+    def sum(self, *cols): return self._simple("sum", cols)
+    def avg(self, *cols): return self._simple("avg", cols)
+    mean = avg
+    def min(self, *cols): return self._simple("min", cols)
+    def max(self, *cols): return self._simple("max", cols)
+
+
+def _sort_key(v, ascending: bool, nulls_first: bool):
+    if v is None:
+        return (0 if nulls_first else 2, 0)
+    return (1, v if ascending else _Neg(v))
+
+
+class _Neg:
+    __slots__ = ("v",)
+
+    def __init__(self, v):
+        self.v = v
+
+    def __lt__(self, o):
+        return self.v > o.v
+
+    def __gt__(self, o):
+        return self.v < o.v
+
+    def __eq__(self, o):
+        return self.v == o.v
+
+
+def sort_frame(df: DataFrame, orders: List[SortOrder]) -> DataFrame:
+    names, rows, ids = df._gather_host()
+    keyvals = []
+    for o in orders:
+        kcol = column_to_python(o.expr.eval(df))
+        keyvals.append(df._comm.allgather_object(kcol))
+    flat_keys = [[v for part in kv for v in part] for kv in keyvals]
+    perm = sorted(range(len(rows)), key=lambda i: tuple(
+        _sort_key(flat_keys[j][i], o.ascending, o.nulls_first) for j, o in enumerate(orders)))
+    rows = [rows[i] for i in perm]
+    ids = [ids[i] for i in perm]
+    return rows_contiguous(df._session, df.schema, rows, ids)
+
+
+def drop_duplicates(df: DataFrame, subset: Optional[Sequence[str]]) -> DataFrame:
+    names, rows, ids = df._gather_host()
+    cols = list(range(len(names))) if subset is None else [names.index(c) for c in subset]
+    seen = set()
+    keep_rows, keep_ids = [], []
+    for r, i in zip(rows, ids):
+        key = tuple(_hashable(r[c]) for c in cols)
+        if key in seen:
+            continue
+        seen.add(key)
+        keep_rows.append(r)
+        keep_ids.append(i)
+    return rows_contiguous(df._session, df.schema, keep_rows, keep_ids)
+
+
+def _hashable(v):
+    if hasattr(v, "toArray"):
+        return tuple(v.toArray().tolist())
+    return v
+
+
+def describe(df: DataFrame, cols: List[str]) -> DataFrame:
+    from . import functions as F
+    if not cols:
+        cols = [f.name for f in df.schema.fields if T.is_numeric(f.dataType) or isinstance(f.dataType, T.StringType)]
+    stats = ["count", "mean", "stddev", "min", "max"]
+    out_rows = [[s] for s in stats]
+    for c in cols:
+        is_num = T.is_numeric(df.schema[c].dataType)
+        exprs = [F.count(c)]
+        if is_num:
+            exprs += [F.avg(c), F.stddev(c)]
+        exprs += [F.min(c), F.max(c)]
+        vals = df.agg(*exprs).collect()[0]
+        if is_num:
+            cnt, mean, sd, mn, mx = vals
+        else:
+            cnt, mn, mx = vals
+            mean = sd = None
+        for r, v in zip(out_rows, [cnt, mean, sd, mn, mx]):
+            r.append(None if v is None else str(v))
+    schema = T.StructType([T.StructField("summary", T.StringType())] + [T.StructField(c, T.StringType()) for c in cols])
+    return rows_round_robin(df._session, schema, out_rows)
+
+
+def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
+    """Broadcast hash join: the right side is gathered to every rank (reference-scale tables)."""
+    how = how.lower().replace("_", "")
+    how = {"leftouter": "left", "rightouter": "right", "fullouter": "full", "outer": "full"}.get(how, how)
+    rnames, rrows, _ = right._gather_host()
+    lnames = left.columns
+    lcols = left._local_rows_host()
+    if on is None:
+        keys = []
+    elif isinstance(on, str):
+        keys = [on]
+    elif isinstance(on, (list, tuple)) and all(isinstance(k, str) for k in on):
+        keys = list(on)
+    else:
+        raise NotImplementedError("join supports column-name keys")
+    index: Dict[tuple, List[int]] = {}
+    for j, r in enumerate(rrows):
+        index.setdefault(tuple(r[rnames.index(k)] for k in keys), []).append(j)
+    r_extra = [n for n in rnames if n not in keys]
+    out_names = lnames + [n for n in r_extra if n not in lnames] + [n + "_r" for n in r_extra if n in lnames]
+    r_out_idx = [rnames.index(n) for n in r_extra]
+    out_rows = []
+    matched_right = set()
+    for i in range(left._nrows):
+        lrow = [lcols[n][i] for n in lnames]
+        key = tuple(lcols[k][i] for k in keys)
+        hits = list(range(len(rrows))) if how == "cross" else index.get(key, [])
+        if how == "leftanti":
+            if not hits:
+                out_rows.append(lrow)
+            continue
+        if how == "leftsemi":
+            if hits:
+                out_rows.append(lrow)
+            continue
+        if hits:
+            for j in hits:
+                matched_right.add(j)
+                out_rows.append(lrow + [rrows[j][t] for t in r_out_idx])
+        elif how in ("left", "full"):
+            out_rows.append(lrow + [None] * len(r_out_idx))
+    if how in ("leftanti", "leftsemi"):
+        out_names = lnames
+    if how in ("right", "full"):
+        allm = left._comm.allgather_object(sorted(matched_right))
+        m = set()
+        for a in allm:
+            m |= set(a)
+        if left._comm.rank == 0:
+            for j, r in enumerate(rrows):
+                if j not in m:
+                    lrow = [r[rnames.index(n)] if n in keys else None for n in lnames]
+                    out_rows.append(lrow + [r[t] for t in r_out_idx])
+        if how == "right":
+            out_rows = [r for r in out_rows if any(v is not None for v in r[len(lnames):]) or True]
+    fields = [T.StructField(n, left.schema[n].dataType) for n in lnames]
+    if how not in ("leftanti", "leftsemi"):
+        fields += [T.StructField(n if n in out_names else n + "_r", right.schema[n].dataType) for n in r_extra]
+        fields = [T.StructField(nm, f.dataType) for nm, f in zip(out_names, fields)]
+    schema = T.StructType(fields)
+    # gather-free placement: keep this rank's output rows local
+    from .builder import frame_from_pycolumns
+    pycols = {f.name: [r[j] for r in out_rows] for j, f in enumerate(schema.fields)}
+    counts = left._comm.allgather_object(len(out_rows))
+    off = sum(counts[: left._comm.rank])
+    return frame_from_pycolumns(left._session, schema, pycols, list(range(off, off + len(out_rows))))
+
+
+def rebalance(df: DataFrame) -> DataFrame:
+    names, rows, ids = df._gather_host()
+    return rows_contiguous(df._session, df.schema, rows, ids)

@@ -1,0 +1,560 @@
+"""Structured-streaming micro-batch engine (N5) — the reference's ingest path
+(ref.py:75-118): file source over a directory of CSV uploads, event-time watermark,
+per-batch ``current_timestamp()`` ingest time, ``foreachBatch`` per-batch hook and
+an append-only table sink with a checkpoint directory.
+
+Exactly-once: each micro-batch is planned by writing ``offsets/<id>`` (the files it
+covers, the batch timestamp and watermark) before it runs and ``commits/<id>`` after
+its sink finished.  On restart an offsets entry without a commit is re-run with the
+*same* files and timestamp; the table sink skips batches whose (queryId, batchId)
+transaction is already in the table log, so a crash between the sink commit and the
+checkpoint commit cannot duplicate rows.
+
+Defects of the reference are not reproduced: ``foreachBatch``
+calls ``fn(df, batch_id)``; ``.table(name)`` is accepted as an alias of
+``toTable``; when both a foreachBatch function and a table target are given, each
+batch is appended to the table first and then handed to the function.
+
+Multi-rank (SPMD) runs: rank 0 lists the directory and plans the batch, the plan
+is broadcast, every rank reads its share of the batch's files.  Micro-batches run
+in the caller's thread there (``processAllAvailable`` / ``availableNow`` /
+``awaitTermination``) so collectives never race with the main program; a
+single-process query with a processing-time trigger runs on a background thread.
+"""
+from __future__ import annotations
+
+import json
+import logging
+import os
+import re
+import threading
+import time
+import uuid
+from typing import Any, Callable, Dict, List, Optional
+
+from . import types as T
+
+log = logging.getLogger("cml.streaming")
+
+
+def parse_interval_ms(s) -> int:
+    if isinstance(s, (int, float)):
+        return int(s)
+    m = re.fullmatch(r"\s*(\d+(?:\.\d+)?)\s*(ms|millisecond|milliseconds|s|sec|second|seconds|min|minute|minutes|"
+                     r"h|hour|hours|d|day|days)?\s*", str(s).lower())
+    if not m:
+        raise ValueError(f"bad interval {s!r}")
+    v = float(m.group(1))
+    unit = m.group(2) or "ms"
+    mult = {"ms": 1, "millisecond": 1, "milliseconds": 1, "s": 1000, "sec": 1000, "second": 1000,
+            "seconds": 1000, "min": 60000, "minute": 60000, "minutes": 60000, "h": 3600000, "hour": 3600000,
+            "hours": 3600000, "d": 86400000, "day": 86400000, "days": 86400000}[unit]
+    return int(v * mult)
+
+
+class StreamPlan:
+    """Source description + recorded per-batch transformations."""
+
+    def __init__(self, fmt: str, path: str, schema: T.StructType, options: Dict[str, Any], ops=None):
+        self.fmt, self.path, self.schema, self.options = fmt, path, schema, options
+        self.ops = list(ops or [])
+        self.watermark = None
+
+    def extend(self, method, args, kwargs) -> "StreamPlan":
+        p = StreamPlan(self.fmt, self.path, self.schema, self.options, self.ops + [(method, args, kwargs)])
+        p.watermark = self.watermark
+        return p
+
+
+class DataStreamReader:
+    def __init__(self, session):
+        self._session = session
+        self._format = "parquet"
+        self._schema: Optional[T.StructType] = None
+        self._options: Dict[str, Any] = {}
+
+    def format(self, source: str) -> "DataStreamReader":
+        self._format = source.lower()
+        return self
+
+    def schema(self, schema) -> "DataStreamReader":
+        self._schema = T.parse_ddl_schema(schema) if isinstance(schema, str) else schema
+        return self
+
+    def option(self, key, value) -> "DataStreamReader":
+        self._options[key.lower()] = value
+        return self
+
+    def options(self, **opts) -> "DataStreamReader":
+        for k, v in opts.items():
+            self.option(k, v)
+        return self
+
+    def load(self, path: Optional[str] = None, format: Optional[str] = None, schema=None, **options):
+        if format:
+            self.format(format)
+        if schema is not None:
+            self.schema(schema)
+        for k, v in options.items():
+            self.option(k, v)
+        return self._frame(path)
+
+    def csv(self, path: str, schema=None, **kw):
+        self.format("csv")
+        return self.load(path, schema=schema, **kw)
+
+    def parquet(self, path: str):
+        self.format("parquet")
+        return self.load(path)
+
+    def json(self, path: str, schema=None):
+        self.format("json")
+        return self.load(path, schema=schema)
+
+    def _frame(self, path: str):
+        from ..io.reader import strip_scheme
+        from .dataframe import DataFrame
+        if self._schema is None:
+            raise ValueError("Schema must be specified when creating a streaming source DataFrame")
+        plan = StreamPlan(self._format, strip_scheme(path), self._schema, dict(self._options))
+        return DataFrame(self._session, self._schema, {}, 0, None, self._session._device, plan)
+
+
+class DataStreamWriter:
+    def __init__(self, df):
+        self._df = df
+        self._format = None
+        self._mode = "append"
+        self._options: Dict[str, Any] = {}
+        self._foreach_batch: Optional[Callable] = None
+        self._trigger: Dict[str, Any] = {"processingTime": 0}
+        self._name: Optional[str] = None
+
+    def format(self, source: str) -> "DataStreamWriter":
+        self._format = source.lower()
+        return self
+
+    def outputMode(self, mode: str) -> "DataStreamWriter":
+        m = mode.lower()
+        if m not in ("append", "update", "complete"):
+            raise ValueError(f"unknown output mode {mode}")
+        if m != "append":
+            raise NotImplementedError("only outputMode('append') is supported (the reference's mode, ref.py:113)")
+        self._mode = m
+        return self
+
+    def option(self, key, value) -> "DataStreamWriter":
+        self._options[key.lower()] = value
+        return self
+
+    def options(self, **opts) -> "DataStreamWriter":
+        for k, v in opts.items():
+            self.option(k, v)
+        return self
+
+    def queryName(self, name: str) -> "DataStreamWriter":
+        self._name = name
+        return self
+
+    def foreachBatch(self, func: Callable) -> "DataStreamWriter":
+        self._foreach_batch = func
+        return self
+
+    def trigger(self, processingTime=None, once=None, availableNow=None, continuous=None) -> "DataStreamWriter":
+        if once:
+            self._trigger = {"once": True}
+        elif availableNow:
+            self._trigger = {"availableNow": True}
+        elif processingTime is not None:
+            self._trigger = {"processingTime": parse_interval_ms(processingTime)}
+        elif continuous is not None:
+            raise NotImplementedError("continuous processing is not supported; use micro-batches")
+        return self
+
+    def partitionBy(self, *cols) -> "DataStreamWriter":
+        return self
+
+    def toTable(self, tableName: str, format=None, outputMode=None, partitionBy=None, queryName=None, **options):
+        if outputMode:
+            self.outputMode(outputMode)
+        if queryName:
+            self.queryName(queryName)
+        for k, v in options.items():
+            self.option(k, v)
+        return self._start(table=tableName)
+
+    # the reference calls DataStreamWriter.table(...) (ref.py:115); accept it as toTable
+    table = toTable
+
+    def start(self, path: Optional[str] = None, format=None, outputMode=None, queryName=None, **options):
+        if format:
+            self.format(format)
+        if outputMode:
+            self.outputMode(outputMode)
+        if queryName:
+            self.queryName(queryName)
+        for k, v in options.items():
+            self.option(k, v)
+        return self._start(path=path or self._options.get("path"))
+
+    def _start(self, table: Optional[str] = None, path: Optional[str] = None):
+        session = self._df._session
+        q = StreamingQuery(session, self._df._stream, self, table=table, path=path)
+        session.streams._register(q)
+        q._launch()
+        return q
+
+
+class StreamingQuery:
+    def __init__(self, session, plan: StreamPlan, writer: DataStreamWriter, table=None, path=None):
+        from ..io.reader import strip_scheme
+        self._session = session
+        self._plan = plan
+        self._writer = writer
+        self._table = table
+        self._path = strip_scheme(path) if path else None
+        self.name = writer._name
+        ckpt = writer._options.get("checkpointlocation")
+        if ckpt is None:
+            ckpt = os.path.join(session.catalog.warehouse, "_checkpoints", table or self.name or uuid.uuid4().hex)
+        self._ckpt = strip_scheme(ckpt)
+        self.runId = uuid.uuid4().hex
+        self.id = self._load_or_create_id()
+        self._stop = threading.Event()
+        self._thread: Optional[threading.Thread] = None
+        self._error: Optional[BaseException] = None
+        self.recentProgress: List[dict] = []
+        self._watermark_ms = 0
+        self._lock = threading.Lock()
+        self._next_batch = None
+
+    # ------------------------------------------------------------------ checkpoint files
+    def _load_or_create_id(self) -> str:
+        comm = self._session._comm
+        qid = None
+        if comm.is_root:
+            os.makedirs(os.path.join(self._ckpt, "offsets"), exist_ok=True)
+            os.makedirs(os.path.join(self._ckpt, "commits"), exist_ok=True)
+            os.makedirs(os.path.join(self._ckpt, "sources", "0"), exist_ok=True)
+            meta = os.path.join(self._ckpt, "metadata")
+            if os.path.exists(meta):
+                with open(meta) as fh:
+                    qid = json.load(fh)["id"]
+            else:
+                qid = uuid.uuid4().hex
+                with open(meta, "w") as fh:
+                    json.dump({"id": qid}, fh)
+        return comm.broadcast_object(qid)
+
+    def _ids(self, sub: str) -> List[int]:
+        d = os.path.join(self._ckpt, sub)
+        return sorted(int(f) for f in os.listdir(d) if f.isdigit()) if os.path.isdir(d) else []
+
+    def _read_json(self, sub: str, bid: int):
+        with open(os.path.join(self._ckpt, sub, str(bid))) as fh:
+            return json.load(fh)
+
+    def _write_json(self, sub: str, bid: int, obj) -> None:
+        p = os.path.join(self._ckpt, sub, str(bid))
+        tmp = p + ".tmp"
+        with open(tmp, "w") as fh:
+            json.dump(obj, fh)
+        os.replace(tmp, p)
+
+    def _seen_files(self) -> List[str]:
+        seen: List[str] = []
+        for bid in self._ids(os.path.join("sources", "0")):
+            seen += self._read_json(os.path.join("sources", "0"), bid)["files"]
+        return seen
+
+    # ------------------------------------------------------------------ planning (rank 0)
+    def _list_new(self, seen: set) -> List[str]:
+        d = self._plan.path
+        if not os.path.isdir(d):
+            return []
+        ext = {"csv": (".csv", ".txt", ".csv.gz"), "json": (".json", ".jsonl"), "parquet": (".parquet",)}.get(
+            self._plan.fmt)
+        files = []
+        for root, dirs, fs in os.walk(d):
+            dirs[:] = sorted(x for x in dirs if not x.startswith(("_", ".")))
+            for f in fs:
+                if f.startswith(("_", ".")) or f.endswith((".tmp", ".crc")):
+                    continue
+                if ext and not f.endswith(ext):
+                    continue
+                p = os.path.join(root, f)
+                if p not in seen:
+                    files.append(p)
+        files.sort(key=lambda p: (os.path.getmtime(p), p))
+        mf = self._plan.options.get("maxfilespertrigger")
+        if mf:
+            files = files[: int(mf)]
+        return files
+
+    def _plan_next(self):
+        """Decide the next batch on rank 0: (batch_id, files, ts_ms, watermark_ms, is_replay) or None."""
+        comm = self._session._comm
+        plan = None
+        if comm.is_root:
+            offs, commits = self._ids("offsets"), self._ids("commits")
+            last_commit = commits[-1] if commits else -1
+            if offs and offs[-1] > last_commit:
+                bid = offs[-1]
+                o = self._read_json("offsets", bid)
+                plan = (bid, o["files"], o["batchTimestampMs"], o["batchWatermarkMs"], True)
+            else:
+                seen = set(self._seen_files())
+                new = self._list_new(seen)
+                if new:
+                    bid = last_commit + 1
+                    ts = int(time.time() * 1000)
+                    plan = (bid, new, ts, self._watermark_ms, False)
+                    self._write_json(os.path.join("sources", "0"), bid, {"files": new})
+                    self._write_json("offsets", bid, {"batchId": bid, "files": new, "batchTimestampMs": ts,
+                                                      "batchWatermarkMs": self._watermark_ms,
+                                                      "queryId": self.id})
+        return comm.broadcast_object(plan)
+
+    # ------------------------------------------------------------------ execution
+    def _file_ids(self, files: List[str]) -> List[int]:
+        order = {}
+        for i, f in enumerate(self._seen_files_cached()):
+            order.setdefault(f, i)
+        return [order.get(f, hash(f) & 0xFFFFF) for f in files]
+
+    def _seen_files_cached(self):
+        comm = self._session._comm
+        return comm.broadcast_object(self._seen_files() if comm.is_root else None)
+
+    def _read_batch(self, files: List[str], ts_ms: int):
+        from ..io.arrow import read_parquet_files
+        from ..io.csv import read_csv_files
+        s = self._session
+        opts = self._plan.options
+        fids = self._file_ids(files)
+        if self._plan.fmt == "csv":
+            hdr = opts.get("header", False)
+            hdr = hdr if isinstance(hdr, bool) else str(hdr).lower() == "true"
+            df = read_csv_files(s, files, self._plan.schema, hdr, sep=str(opts.get("sep", ",")),
+                                quote=str(opts.get("quote", '"')), file_ids=fids)
+        elif self._plan.fmt == "parquet":
+            df = read_parquet_files(s, files, self._plan.schema, file_ids=fids)
+        elif self._plan.fmt == "json":
+            df = s.read.schema(self._plan.schema).json(files)
+        else:
+            raise ValueError(f"unsupported streaming source format {self._plan.fmt}")
+        df._batch_time_us = int(ts_ms) * 1000
+        for method, args, kwargs in self._plan.ops:
+            if method == "withWatermark":
+                continue
+            df = getattr(df, method)(*args, **kwargs)
+            df._batch_time_us = int(ts_ms) * 1000
+        return df
+
+    def _advance_watermark(self, df) -> None:
+        wm = self._plan.watermark
+        if not wm:
+            return
+        col, delay = wm
+        try:
+            cd = df._cols[col]
+        except KeyError:
+            return
+        if cd.is_host or len(cd) == 0:
+            local = -2**62
+        else:
+            v = cd.values[cd.valid_mask()] if cd.valid is not None else cd.values
+            local = int(v.max().item()) if v.numel() else -2**62
+        gmax = int(self._session._comm.max_scalar(float(local)))
+        if gmax > -2**61:
+            self._watermark_ms = max(self._watermark_ms, gmax // 1000 - parse_interval_ms(delay))
+
+    def _run_batch(self, plan) -> dict:
+        bid, files, ts_ms, wm_ms, replay = plan
+        t0 = time.time()
+        self._watermark_ms = max(self._watermark_ms, wm_ms)
+        df = self._read_batch(files, ts_ms)
+        nrows = df.count()
+        w = self._writer
+        if self._table is not None:
+            from ..io import table as tbl
+            root = self._session.catalog._table_path(self._table)
+            if tbl.committed_txn(root, self.id) < bid:
+                tbl.write_frame(df, root, "append", operation="STREAMING UPDATE",
+                                txn={"appId": self.id, "version": bid})
+        elif self._path is not None or (w._format not in (None, "console", "memory", "delta", "noop")):
+            if self._path is None:
+                raise ValueError("file sink needs a path")
+            fmt = w._format or "parquet"
+            if fmt == "delta":
+                from ..io import table as tbl
+                if tbl.committed_txn(self._path, self.id) < bid:
+                    tbl.write_frame(df, self._path, "append", "STREAMING UPDATE", {"appId": self.id, "version": bid})
+            else:
+                df.write.mode("append").format(fmt).save(os.path.join(self._path, f"batch={bid}"))
+        elif w._format == "console" and self._foreach_batch_absent():
+            if self._session._comm.is_root:
+                print(f"-------------------------------------------\nBatch: {bid}\n"
+                      f"-------------------------------------------")
+            df.show()
+        elif w._format == "memory":
+            name = self.name or "memory_sink"
+            prev = self._session.catalog._views.get(name)
+            self._session.catalog._register_view(name, df if prev is None else prev.union(df), True)
+        if w._foreach_batch is not None:
+            w._foreach_batch(df, bid)
+        self._advance_watermark(df)
+        comm = self._session._comm
+        comm.barrier()
+        if comm.is_root:
+            self._write_json("commits", bid, {"nextBatchWatermarkMs": self._watermark_ms})
+        prog = {"id": self.id, "runId": self.runId, "name": self.name, "batchId": bid, "numInputRows": nrows,
+                "numInputFiles": len(files), "timestamp": ts_ms, "replayed": replay,
+                "durationMs": {"triggerExecution": int((time.time() - t0) * 1000)},
+                "eventTime": {"watermark": self._watermark_ms}, "sink": self._table or self._path}
+        with self._lock:
+            self.recentProgress.append(prog)
+            self.recentProgress = self.recentProgress[-100:]
+        return prog
+
+    def _foreach_batch_absent(self) -> bool:
+        return self._writer._foreach_batch is None
+
+    def _drain(self) -> int:
+        """Run micro-batches until no new data. Returns batches run."""
+        n = 0
+        while not self._stop.is_set():
+            plan = self._plan_next()
+            if plan is None:
+                break
+            self._run_batch(plan)
+            n += 1
+        return n
+
+    def _launch(self) -> None:
+        trig = self._writer._trigger
+        comm = self._session._comm
+        if trig.get("once"):
+            plan = self._plan_next()
+            if plan is not None:
+                self._run_batch(plan)
+            self._stop.set()
+        elif trig.get("availableNow"):
+            self._drain()
+            self._stop.set()
+        elif comm.is_distributed:
+            # SPMD: batches execute in the caller's thread (processAllAvailable / awaitTermination)
+            self._drain()
+        else:
+            interval = trig.get("processingTime", 0) / 1000.0
+            dev = self._session._device
+
+            def loop():
+                try:
+                    if dev.type == "cuda":
+                        import torch
+                        torch.cuda.set_device(dev)
+                    while not self._stop.is_set():
+                        t0 = time.time()
+                        self._drain()
+                        wait = max(interval - (time.time() - t0), 0.05)
+                        self._stop.wait(wait)
+                except BaseException as e:  # surfaced by awaitTermination
+                    self._error = e
+                    log.exception("streaming query failed")
+            self._thread = threading.Thread(target=loop, name=f"stream-{self.id[:8]}", daemon=True)
+            self._thread.start()
+
+    # ------------------------------------------------------------------ public API
+    @property
+    def isActive(self) -> bool:
+        if self._thread is not None:
+            return self._thread.is_alive() and not self._stop.is_set()
+        return not self._stop.is_set()
+
+    @property
+    def lastProgress(self) -> Optional[dict]:
+        with self._lock:
+            return self.recentProgress[-1] if self.recentProgress else None
+
+    @property
+    def status(self) -> dict:
+        return {"message": "Waiting for data to arrive" if self.isActive else "Stopped",
+                "isDataAvailable": False, "isTriggerActive": self.isActive}
+
+    def exception(self):
+        return self._error
+
+    def processAllAvailable(self) -> None:
+        if self._thread is not None:
+            # let the background loop see every file currently present
+            while True:
+                if self._error:
+                    raise self._error
+                with self._lock:
+                    pass
+                if self._session._comm.is_root and not self._pending():
+                    time.sleep(0.1)
+                    if not self._pending():
+                        return
+                time.sleep(0.05)
+        else:
+            self._drain()
+
+    def _pending(self) -> bool:
+        offs, commits = self._ids("offsets"), self._ids("commits")
+        if offs and (not commits or offs[-1] > commits[-1]):
+            return True
+        return bool(self._list_new(set(self._seen_files())))
+
+    def awaitTermination(self, timeout: Optional[float] = None) -> Optional[bool]:
+        if self._thread is None:
+            if not self._stop.is_set():
+                deadline = None if timeout is None else time.time() + timeout
+                while not self._stop.is_set() and (deadline is None or time.time() < deadline):
+                    self._drain()
+                    if self._stop.wait(0.1):
+                        break
+            return self._stop.is_set() if timeout is not None else None
+        self._thread.join(timeout)
+        if self._error:
+            raise self._error
+        return not self._thread.is_alive() if timeout is not None else None
+
+    def stop(self) -> None:
+        self._stop.set()
+        if self._thread is not None:
+            self._thread.join(timeout=30)
+        self._session.streams._unregister(self)
+
+    def explain(self, extended=False):
+        print(f"StreamingQuery {self.name or self.id}: {self._plan.fmt} source {self._plan.path} -> "
+              f"{self._table or self._path or self._writer._format}")
+
+
+class StreamingQueryManager:
+    def __init__(self, session):
+        self._session = session
+        self._queries: Dict[str, StreamingQuery] = {}
+
+    def _register(self, q: StreamingQuery) -> None:
+        self._queries[q.id] = q
+
+    def _unregister(self, q: StreamingQuery) -> None:
+        self._queries.pop(q.id, None)
+
+    @property
+    def active(self) -> List[StreamingQuery]:
+        return [q for q in self._queries.values() if q.isActive]
+
+    def get(self, qid: str) -> Optional[StreamingQuery]:
+        return self._queries.get(qid)
+
+    def awaitAnyTermination(self, timeout: Optional[float] = None):
+        qs = list(self._queries.values())
+        if not qs:
+            return True
+        return qs[0].awaitTermination(timeout)
+
+    def resetTerminated(self) -> None:
+        return None
