@@ -1,0 +1,80 @@
+"""Estimator / Transformer / Model / Evaluator (pyspark.ml-compatible).
+
+``Estimator.fit(df) -> Model`` and ``Model.transform(df) -> df`` are the only
+contracts the reference relies on (ref.py:147-190).  Streaming DataFrames are
+accepted by ``transform`` too: the transformation is recorded and replayed on
+every micro-batch.
+"""
+from __future__ import annotations
+
+from typing import Any, Dict, List, Optional, Union
+
+import torch
+
+from .param import Params
+from .util import MLReadable, MLWritable
+
+
+class Transformer(Params, MLWritable, MLReadable):
+    def transform(self, dataset, params: Optional[Dict] = None):
+        inst = self.copy(params) if params else self
+        if dataset.isStreaming:
+            return dataset._lazy("_apply_transformer", inst)
+        return inst._transform(dataset)
+
+    def _transform(self, dataset):
+        raise NotImplementedError
+
+
+class Estimator(Params, MLWritable, MLReadable):
+    def fit(self, dataset, params: Optional[Union[Dict, List[Dict]]] = None):
+        if isinstance(params, (list, tuple)):
+            return [self.fit(dataset, p) for p in params]
+        if dataset.isStreaming:
+            raise RuntimeError("fit() on a streaming DataFrame: use writeStream.foreachBatch to train per batch")
+        inst = self.copy(params) if params else self
+        model = inst._fit(dataset)
+        if model is not None and getattr(model, "parent", None) is None:
+            model.parent = inst
+            model.uid = inst.uid  # Spark models carry their estimator's uid
+        return model
+
+    def fitMultiple(self, dataset, paramMaps):
+        for i, pm in enumerate(paramMaps):
+            yield i, self.fit(dataset, pm)
+
+    def _fit(self, dataset):
+        raise NotImplementedError
+
+
+class Model(Transformer):
+    parent = None
+
+    def hasSummary(self) -> bool:
+        return getattr(self, "_summary", None) is not None
+
+    @property
+    def summary(self):
+        if getattr(self, "_summary", None) is None:
+            raise RuntimeError("No training summary available for this model")
+        return self._summary
+
+
+class Evaluator(Params, MLWritable, MLReadable):
+    def evaluate(self, dataset, params: Optional[Dict] = None) -> float:
+        inst = self.copy(params) if params else self
+        return inst._evaluate(dataset)
+
+    def _evaluate(self, dataset) -> float:
+        raise NotImplementedError
+
+    def isLargerBetter(self) -> bool:
+        return True
+
+
+def session_of(df):
+    return df._session
+
+
+def feature_matrix(df, col: str) -> torch.Tensor:
+    return df._feature_matrix(col)

@@ -1,0 +1,163 @@
+"""KMeans estimator/model (the [NS] headline workload; no KMeans in the reference,
+SURVEY.md §0.3) on the distributed Lloyd engine of ``models/kmeans.py``.
+
+Spark defaults: k=2, maxIter=20, tol=1e-4, initMode="k-means||", initSteps=2,
+distanceMeasure="euclidean", seed = Java hashCode of the class name.
+On GPU ranks the assignment runs on the bf16 MFMA kernel (K9) — centres are kept
+in float64, sums are exact-f64 (K10), so only near-ties between two centres can
+differ from a float64 evaluation.
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..models.kmeans import LloydEngine
+from ..sql import types as T
+from ..sql.column import ColumnData
+from . import util as U
+from .base import Estimator, Model
+from .feature import _replace_col
+from .linalg import DenseVector, as_array
+
+
+def java_hash(s: str) -> int:
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
+
+
+_KMEANS_PARAMS = {
+    "featuresCol": ("features", "features column name", str),
+    "predictionCol": ("prediction", "prediction column name", str),
+    "k": (2, "number of clusters to create (> 1)", int),
+    "maxIter": (20, "max number of iterations (>= 0)", int),
+    "tol": (1e-4, "convergence tolerance for iterative algorithms (>= 0)", float),
+    "initMode": ("k-means||", "initialization algorithm: 'random' or 'k-means||'", str),
+    "initSteps": (2, "number of steps for k-means|| (> 0)", int),
+    "seed": (java_hash("org.apache.spark.ml.clustering.KMeans"), "random seed", int),
+    "distanceMeasure": ("euclidean", "'euclidean' or 'cosine'", str),
+    "weightCol": (None, "weight column name", None),
+    "solver": ("auto", "'auto', 'row' or 'block'", str),
+    "maxBlockSizeInMB": (0.0, "maximum memory in MB for stacking input data into blocks", float),
+}
+
+
+class KMeans(Estimator):
+    _params = _KMEANS_PARAMS
+
+    def __init__(self, featuresCol=None, predictionCol=None, k=None, initMode=None, initSteps=None, tol=None,
+                 maxIter=None, seed=None, distanceMeasure=None, weightCol=None, solver=None, maxBlockSizeInMB=None):
+        super().__init__(featuresCol=featuresCol, predictionCol=predictionCol, k=k, initMode=initMode,
+                         initSteps=initSteps, tol=tol, maxIter=maxIter, seed=seed, distanceMeasure=distanceMeasure,
+                         weightCol=weightCol, solver=solver, maxBlockSizeInMB=maxBlockSizeInMB)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _fit(self, df):
+        if self.getOrDefault("distanceMeasure") != "euclidean":
+            raise NotImplementedError("only distanceMeasure='euclidean' runs on the MFMA kernels")
+        if self.isSet("weightCol"):
+            raise NotImplementedError("weighted KMeans is not supported yet")
+        x = df._feature_matrix(self.getFeaturesCol())
+        d = x.shape[1]
+        k = self.getK()
+        comm = df._comm
+        seed = int(self.getSeed())
+        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids)
+        if self.getInitMode() == "random":
+            init = eng.init_random(seed)
+        else:
+            init = eng.init_kmeans_parallel(seed, self.getInitSteps())
+            k_eff = getattr(eng, "k_effective", k)
+            if k_eff < k:
+                init = init[:k_eff]
+                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids)
+        eng.set_centers(init)
+        iters = eng.fit(self.getMaxIter(), self.getTol())
+        centers = eng.centers.cpu().numpy()
+        labels, dist = eng.assign()
+        sizes = torch.bincount(labels.long(), minlength=eng.k).to(torch.float64) if eng.n else torch.zeros(
+            eng.k, dtype=torch.float64, device=x.device)
+        comm.allreduce_(sizes)
+        model = KMeansModel(centers)
+        self._copyValues(model)
+        model._summary = KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
+                                       [int(s) for s in sizes.cpu().tolist()])
+        return model
+
+
+class KMeansModel(Model):
+    _params = _KMEANS_PARAMS
+
+    def __init__(self, centers=None):
+        super().__init__()
+        self._centers = np.asarray(centers if centers is not None else np.zeros((0, 0)), dtype=np.float64)
+        self._summary = None
+
+    def clusterCenters(self) -> List[np.ndarray]:
+        return [c.copy() for c in self._centers]
+
+    @property
+    def numFeatures(self) -> int:
+        return int(self._centers.shape[1])
+
+    def predict(self, value) -> int:
+        v = as_array(value)
+        return int(((self._centers - v) ** 2).sum(1).argmin())
+
+    def _assign(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        c = torch.as_tensor(self._centers, device=x.device)
+        if x.is_cuda:
+            from ..models.kmeans import assign_gpu, to_device_matrix
+            xm = to_device_matrix(x, x.shape[1])
+            lab, dist = assign_gpu(xm, xm.shape[1], x.shape[1], c)
+            return lab.long(), dist.to(torch.float64)
+        from ..ops.kmeans_ops import assign_reference
+        return assign_reference(x, c)
+
+    def _transform(self, df):
+        lab, _ = self._assign(df)
+        return _replace_col(df, self.getPredictionCol(), ColumnData(lab.to(torch.int32), None, T.IntegerType()))
+
+    def computeCost(self, df) -> float:
+        _, dist = self._assign(df)
+        return df._comm.sum_scalar(float(dist.sum().item()) if dist.numel() else 0.0)
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        rows = [{"clusterIdx": i, "clusterCenter": U.vector_struct(c)} for i, c in enumerate(self._centers)]
+        U.write_parquet(path, "data", pa.Table.from_pylist(
+            rows, schema=pa.schema([pa.field("clusterIdx", pa.int32(), nullable=False),
+                                    ("clusterCenter", U.vector_arrow_type())])))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        rows = sorted(U.read_parquet(path, "data").to_pylist(), key=lambda r: r["clusterIdx"])
+        m = cls(np.stack([U.vector_from_struct(r["clusterCenter"]) for r in rows]) if rows else None)
+        U.apply_params(m, md)
+        return m
+
+
+class KMeansSummary:
+    def __init__(self, model, df, k, num_iter, cost, sizes):
+        self._model = model
+        self._df = df
+        self.k = k
+        self.numIter = num_iter
+        self.trainingCost = cost
+        self.clusterSizes = sizes
+        self.featuresCol = model.getFeaturesCol()
+        self.predictionCol = model.getPredictionCol()
+
+    @property
+    def predictions(self):
+        return self._model.transform(self._df)
+
+    @property
+    def cluster(self):
+        return self.predictions.select(self.predictionCol)

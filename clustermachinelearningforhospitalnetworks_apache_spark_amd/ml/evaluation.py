@@ -1,0 +1,270 @@
+"""Evaluators (ref.py:31, ref.py:33, ref.py:162-169, ref.py:192-198).
+
+Every metric is a handful of sums computed on the rank's shard (K23: fused
+device reductions) and combined with ONE all-reduce (C8) — no collect to a driver.
+"""
+from __future__ import annotations
+
+import math
+
+import numpy as np
+import torch
+
+from .base import Evaluator
+from .param import NO_DEFAULT
+
+
+def _col(df, name, dtype=torch.float64):
+    cd = df._column_data(name)
+    if cd.is_host:
+        raise TypeError(f"column {name!r} must be numeric")
+    v = cd.values
+    return v.to(dtype) if v.dim() == 1 else v
+
+
+class RegressionEvaluator(Evaluator):
+    """metricName: rmse (default) | mse | r2 | mae | var."""
+    _params = {
+        "predictionCol": ("prediction", "prediction column name", str),
+        "labelCol": ("label", "label column name", str),
+        "weightCol": (None, "weight column name", None),
+        "metricName": ("rmse", "metric name in evaluation (mse|rmse|r2|mae|var)", str),
+        "throughOrigin": (False, "whether the regression is through the origin", bool),
+    }
+
+    def __init__(self, predictionCol=None, labelCol=None, metricName=None, weightCol=None, throughOrigin=None):
+        super().__init__(predictionCol=predictionCol, labelCol=labelCol, metricName=metricName, weightCol=weightCol,
+                         throughOrigin=throughOrigin)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _evaluate(self, df) -> float:
+        y = _col(df, self.getLabelCol())
+        p = _col(df, self.getPredictionCol())
+        w = _col(df, self.getOrDefault("weightCol")) if self.isSet("weightCol") else torch.ones_like(y)
+        e = y - p
+        stats = torch.stack([w.sum(), (w * e * e).sum(), (w * e.abs()).sum(), (w * y).sum(), (w * y * y).sum(),
+                             (w * p).sum(), (w * p * p).sum()]) if y.numel() else torch.zeros(
+            7, dtype=torch.float64, device=y.device)
+        df._comm.allreduce_(stats)
+        n, sse, sae, sy, syy, sp, spp = stats.tolist()
+        if n == 0:
+            return float("nan")
+        m = self.getMetricName()
+        mse = sse / n
+        if m == "rmse":
+            return math.sqrt(mse)
+        if m == "mse":
+            return mse
+        if m == "mae":
+            return sae / n
+        if m == "r2":
+            if self.getThroughOrigin():
+                sst = syy
+            else:
+                sst = syy - sy * sy / n
+            return 1.0 - sse / sst if sst > 0 else float("nan")
+        if m == "var":
+            return spp / n - (sp / n) ** 2
+        raise ValueError(f"unknown metric {m}")
+
+    def isLargerBetter(self) -> bool:
+        return self.getMetricName() in ("r2", "var")
+
+
+class MulticlassClassificationEvaluator(Evaluator):
+    """metricName: f1 (default) | accuracy | weightedPrecision | weightedRecall | weightedTruePositiveRate |
+    weightedFalsePositiveRate | weightedFMeasure | truePositiveRateByLabel | falsePositiveRateByLabel |
+    precisionByLabel | recallByLabel | fMeasureByLabel | logLoss | hammingLoss."""
+    _params = {
+        "predictionCol": ("prediction", "prediction column name", str),
+        "labelCol": ("label", "label column name", str),
+        "weightCol": (None, "weight column name", None),
+        "probabilityCol": ("probability", "probability column name", str),
+        "metricName": ("f1", "metric name in evaluation", str),
+        "metricLabel": (0.0, "the class whose metric will be computed in *ByLabel", float),
+        "beta": (1.0, "the beta value used in fMeasureByLabel/weightedFMeasure", float),
+        "eps": (1e-15, "log-loss clipping epsilon", float),
+    }
+
+    def __init__(self, predictionCol=None, labelCol=None, metricName=None, weightCol=None, metricLabel=None,
+                 beta=None, probabilityCol=None, eps=None):
+        super().__init__(predictionCol=predictionCol, labelCol=labelCol, metricName=metricName, weightCol=weightCol,
+                         metricLabel=metricLabel, beta=beta, probabilityCol=probabilityCol, eps=eps)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _confusion(self, df):
+        y = _col(df, self.getLabelCol()).to(torch.int64)
+        p = _col(df, self.getPredictionCol()).to(torch.int64)
+        w = _col(df, self.getOrDefault("weightCol")) if self.isSet("weightCol") else torch.ones(
+            y.shape[0], dtype=torch.float64, device=y.device)
+        local_max = int(max(y.max().item() if y.numel() else 0, p.max().item() if p.numel() else 0))
+        C = int(df._comm.max_scalar(float(local_max))) + 1
+        cm = torch.zeros(C * C, dtype=torch.float64, device=y.device)
+        if y.numel():
+            cm.index_add_(0, y * C + p, w)
+        df._comm.allreduce_(cm)
+        return cm.reshape(C, C).cpu().numpy()  # rows = label, cols = prediction
+
+    def _evaluate(self, df) -> float:
+        m = self.getMetricName()
+        if m == "logLoss":
+            return self._logloss(df)
+        cm = self._confusion(df)
+        total = cm.sum()
+        if total == 0:
+            return float("nan")
+        tp = np.diag(cm)
+        lab = cm.sum(1)
+        pred = cm.sum(0)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            prec = np.where(pred > 0, tp / np.where(pred > 0, pred, 1), 0.0)
+            rec = np.where(lab > 0, tp / np.where(lab > 0, lab, 1), 0.0)
+            fpr = np.where(total - lab > 0, (pred - tp) / np.where(total - lab > 0, total - lab, 1), 0.0)
+        beta = self.getBeta()
+        b2 = beta * beta
+        with np.errstate(divide="ignore", invalid="ignore"):
+            fm = np.where(prec + rec > 0, (1 + b2) * prec * rec / np.where(b2 * prec + rec > 0, b2 * prec + rec, 1),
+                          0.0)
+        wts = lab / total
+        if m == "accuracy":
+            return float(tp.sum() / total)
+        if m in ("f1", "weightedFMeasure"):
+            return float((wts * fm).sum())
+        if m == "weightedPrecision":
+            return float((wts * prec).sum())
+        if m in ("weightedRecall", "weightedTruePositiveRate"):
+            return float((wts * rec).sum())
+        if m == "weightedFalsePositiveRate":
+            return float((wts * fpr).sum())
+        if m == "hammingLoss":
+            return float(1.0 - tp.sum() / total)
+        li = int(self.getMetricLabel())
+        if li >= len(tp):
+            return 0.0
+        if m == "truePositiveRateByLabel" or m == "recallByLabel":
+            return float(rec[li])
+        if m == "falsePositiveRateByLabel":
+            return float(fpr[li])
+        if m == "precisionByLabel":
+            return float(prec[li])
+        if m == "fMeasureByLabel":
+            return float(fm[li])
+        raise ValueError(f"unknown metric {m}")
+
+    def _logloss(self, df) -> float:
+        y = _col(df, self.getLabelCol()).to(torch.int64)
+        prob = df._feature_matrix(self.getProbabilityCol()).to(torch.float64)
+        eps = self.getEps()
+        if y.numel():
+            p = prob.gather(1, y.reshape(-1, 1)).reshape(-1).clamp(eps, 1 - eps)
+            s = torch.stack([-torch.log(p).sum(), torch.tensor(float(y.numel()), device=y.device,
+                                                               dtype=torch.float64)])
+        else:
+            s = torch.zeros(2, dtype=torch.float64, device=y.device)
+        df._comm.allreduce_(s)
+        return float(s[0] / s[1]) if s[1] > 0 else float("nan")
+
+    def isLargerBetter(self) -> bool:
+        return self.getMetricName() not in ("weightedFalsePositiveRate", "falsePositiveRateByLabel", "logLoss",
+                                            "hammingLoss")
+
+
+class BinaryClassificationEvaluator(Evaluator):
+    """areaUnderROC (default) | areaUnderPR, from rawPrediction/probability scores."""
+    _params = {
+        "rawPredictionCol": ("rawPrediction", "raw prediction (score) column", str),
+        "labelCol": ("label", "label column name", str),
+        "weightCol": (None, "weight column name", None),
+        "metricName": ("areaUnderROC", "areaUnderROC|areaUnderPR", str),
+        "numBins": (1000, "number of bins to down-sample the curves (0 = exact)", int),
+    }
+
+    def __init__(self, rawPredictionCol=None, labelCol=None, metricName=None, weightCol=None, numBins=None):
+        super().__init__(rawPredictionCol=rawPredictionCol, labelCol=labelCol, metricName=metricName,
+                         weightCol=weightCol, numBins=numBins)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _evaluate(self, df) -> float:
+        cd = df._column_data(self.getRawPredictionCol())
+        s = cd.values.to(torch.float64)
+        score = s[:, -1] if s.dim() == 2 else s
+        y = _col(df, self.getLabelCol())
+        w = _col(df, self.getOrDefault("weightCol")) if self.isSet("weightCol") else torch.ones_like(y)
+        # exact curves from the gathered (score, label, weight) triples — sorted once on the host
+        parts = df._comm.allgather_object((score.cpu().numpy(), y.cpu().numpy(), w.cpu().numpy()))
+        sc = np.concatenate([p[0] for p in parts])
+        yy = np.concatenate([p[1] for p in parts])
+        ww = np.concatenate([p[2] for p in parts])
+        order = np.argsort(-sc, kind="stable")
+        sc, yy, ww = sc[order], yy[order], ww[order]
+        pos = (yy > 0.5) * ww
+        neg = (yy <= 0.5) * ww
+        # group ties
+        uniq = np.r_[True, sc[1:] != sc[:-1]]
+        idx = np.cumsum(uniq) - 1
+        tp = np.bincount(idx, pos)
+        fp = np.bincount(idx, neg)
+        ctp, cfp = np.cumsum(tp), np.cumsum(fp)
+        P, N = ctp[-1] if len(ctp) else 0.0, cfp[-1] if len(cfp) else 0.0
+        if self.getMetricName() == "areaUnderROC":
+            if P == 0 or N == 0:
+                return float("nan")
+            tpr = np.r_[0.0, ctp / P]
+            fpr = np.r_[0.0, cfp / N]
+            return float(np.trapz(tpr, fpr))
+        if P == 0:
+            return float("nan")
+        rec = np.r_[0.0, ctp / P]
+        prec = np.r_[1.0, ctp / np.maximum(ctp + cfp, 1e-300)]
+        return float(np.trapz(prec, rec))
+
+
+class ClusteringEvaluator(Evaluator):
+    """Silhouette with squared euclidean distance (Spark's default), computed from per-cluster sums."""
+    _params = {
+        "predictionCol": ("prediction", "prediction column name", str),
+        "featuresCol": ("features", "features column name", str),
+        "metricName": ("silhouette", "metric name", str),
+        "distanceMeasure": ("squaredEuclidean", "squaredEuclidean|cosine", str),
+        "weightCol": (None, "weight column name", None),
+    }
+
+    def __init__(self, predictionCol=None, featuresCol=None, metricName=None, distanceMeasure=None, weightCol=None):
+        super().__init__(predictionCol=predictionCol, featuresCol=featuresCol, metricName=metricName,
+                         distanceMeasure=distanceMeasure, weightCol=weightCol)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _evaluate(self, df) -> float:
+        x = df._feature_matrix(self.getFeaturesCol()).to(torch.float64)
+        lab = _col(df, self.getPredictionCol()).to(torch.int64)
+        K = int(df._comm.max_scalar(float(lab.max().item()) if lab.numel() else 0.0)) + 1
+        d = x.shape[1]
+        sums = torch.zeros(K, d, dtype=torch.float64, device=x.device)
+        cnt = torch.zeros(K, dtype=torch.float64, device=x.device)
+        sq = torch.zeros(K, dtype=torch.float64, device=x.device)
+        if lab.numel():
+            sums.index_add_(0, lab, x)
+            cnt.index_add_(0, lab, torch.ones_like(lab, dtype=torch.float64))
+            sq.index_add_(0, lab, (x * x).sum(1))
+        msg = torch.cat([sums.reshape(-1), cnt, sq])
+        df._comm.allreduce_(msg)
+        sums = msg[: K * d].reshape(K, d)
+        cnt = msg[K * d: K * d + K]
+        sq = msg[K * d + K:]
+        if lab.numel() == 0:
+            part = torch.zeros(2, dtype=torch.float64, device=x.device)
+        else:
+            xx = (x * x).sum(1, keepdim=True)
+            # mean squared distance from each point to every cluster: (N_c|x|² − 2x·S_c + Q_c)/N_c
+            dist = (cnt[None, :] * xx - 2 * x @ sums.T + sq[None, :]) / cnt.clamp(min=1)[None, :]
+            own = dist.gather(1, lab.reshape(-1, 1)).reshape(-1)
+            nc = cnt[lab]
+            a = torch.where(nc > 1, own * nc / (nc - 1).clamp(min=1), torch.zeros_like(own))
+            other = dist.clone()
+            other[torch.arange(len(lab), device=x.device), lab] = float("inf")
+            other[:, cnt == 0] = float("inf")
+            b = other.min(1).values
+            s = torch.where(nc > 1, (b - a) / torch.maximum(a, b).clamp(min=1e-300), torch.zeros_like(a))
+            part = torch.stack([s.sum(), torch.tensor(float(len(lab)), dtype=torch.float64, device=x.device)])
+        df._comm.allreduce_(part)
+        return float(part[0] / part[1]) if part[1] > 0 else float("nan")

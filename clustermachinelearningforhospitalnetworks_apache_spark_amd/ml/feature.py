@@ -1,0 +1,392 @@
+"""Feature transformers: VectorAssembler (ref.py:134-136, ref.py:179), StringIndexer
+(imported by the reference, ref.py:29), StandardScaler ([NS]), Binarizer (the
+reference's ``when(LOS > 5.0, 1).otherwise(0)`` label, ref.py:176-177, as a
+transformer), MinMaxScaler.
+
+A vector column is one dense [n, d] tensor on the rank's device.  The assembler
+packs columns with a single device concat (K2); the scaler computes per-feature
+moments with the K7 kernel + one all-reduce and applies K8.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, List, Optional
+
+import numpy as np
+import torch
+
+from ..ops import glm_ops
+from ..sql import types as T
+from ..sql.column import ColumnData
+from .base import Estimator, Model, Transformer
+from .linalg import DenseVector
+from .param import NO_DEFAULT
+from . import util as U
+
+
+def features_dtype(session) -> torch.dtype:
+    name = session.conf.get("cml.ml.features.dtype", "float64")
+    return {"float64": torch.float64, "double": torch.float64, "float32": torch.float32, "float": torch.float32,
+            "bfloat16": torch.bfloat16, "bf16": torch.bfloat16}[str(name).lower()]
+
+
+def _replace_col(df, name: str, data: ColumnData):
+    fields = list(df.schema.fields)
+    cols = dict(df._cols)
+    if name in cols:
+        fields[df.schema.names.index(name)] = T.StructField(name, data.dtype, True)
+    else:
+        fields.append(T.StructField(name, data.dtype, True))
+    cols[name] = data
+    return df._new(T.StructType(fields), cols, df._nrows, df._row_ids)
+
+
+class VectorAssembler(Transformer):
+    _params = {
+        "inputCols": (NO_DEFAULT, "input column names", "liststr"),
+        "outputCol": ("__auto__", "output column name", str),
+        "handleInvalid": ("error", "how to handle invalid data (NULL/NaN): 'error', 'skip' or 'keep'", str),
+    }
+
+    def __init__(self, inputCols=None, outputCol=None, handleInvalid=None):
+        super().__init__(inputCols=inputCols, outputCol=outputCol, handleInvalid=handleInvalid)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _transform(self, df):
+        cols = self.getInputCols()
+        dtype = features_dtype(df._session)
+        parts, bad = [], None
+        for c in cols:
+            cd = df._column_data(c)
+            if cd.is_host:
+                raise TypeError(f"VectorAssembler: column {c!r} of type {cd.dtype.simpleString()} is not numeric")
+            v = cd.values
+            if v.dim() == 1:
+                v = v.reshape(-1, 1)
+            v = v.to(torch.float64)
+            invalid = ~cd.valid_mask().reshape(-1) if cd.valid is not None else None
+            nan = torch.isnan(v).any(1)
+            inv = nan if invalid is None else (nan | invalid)
+            bad = inv if bad is None else (bad | inv)
+            if invalid is not None:
+                v = torch.where(invalid.reshape(-1, 1), torch.full_like(v, float("nan")), v)
+            parts.append(v)
+        x = torch.cat(parts, 1) if parts else torch.zeros((df._nrows, 0), dtype=torch.float64, device=df._device)
+        hi = self.getHandleInvalid()
+        if bad is not None and df._nrows:
+            if hi == "error":
+                if bool(bad.any().item()):
+                    raise ValueError("VectorAssembler: encountered NULL or NaN values with handleInvalid='error'; "
+                                     "drop them first (df.na.drop()) or set handleInvalid='skip'/'keep'")
+            elif hi == "skip":
+                keep = ~bad
+                df = df._mask_rows(keep)
+                x = x[keep]
+        return _replace_col(df, self.getOutputCol(), ColumnData(x.to(dtype).contiguous(), None, T.VectorUDT()))
+
+    def _save_impl(self, path):
+        U.write_metadata(self, path)
+
+
+class StandardScaler(Estimator):
+    """Spark defaults: withMean=False, withStd=True, unbiased (n-1) standard deviation."""
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "withMean": (False, "whether to center data with mean", bool),
+        "withStd": (True, "whether to scale the data to unit standard deviation", bool),
+        "outputDtype": ("auto", "cml extension: dtype of the scaled vectors (auto/float64/float32/bfloat16)", str),
+    }
+
+    def __init__(self, withMean=None, withStd=None, inputCol=None, outputCol=None, outputDtype=None):
+        super().__init__(withMean=withMean, withStd=withStd, inputCol=inputCol, outputCol=outputCol,
+                         outputDtype=outputDtype)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _fit(self, df):
+        x = df._feature_matrix(self.getInputCol())
+        d = x.shape[1]
+        n, s1, s2, shift = glm_ops.moments(x, d)
+        comm = df._comm
+        # merge shifted moments across ranks exactly: use a common shift (rank 0's first row)
+        common = comm.broadcast_object(shift.cpu().numpy() if n else None, 0)
+        if common is None:
+            common = np.zeros(d)
+        common_t = torch.as_tensor(common, dtype=torch.float64, device=x.device)
+        delta = shift - common_t
+        # Σ(x-c) = Σ(x-s) + n(s-c); Σ(x-c)² = Σ(x-s)² + 2(s-c)Σ(x-s) + n(s-c)²
+        t1 = s1 + n * delta
+        t2 = s2 + 2 * delta * s1 + n * delta * delta
+        msg = torch.cat([torch.tensor([float(n)], dtype=torch.float64, device=x.device), t1, t2])
+        comm.allreduce_(msg)
+        N = msg[0].item()
+        T1, T2 = msg[1:1 + d], msg[1 + d:]
+        mean = common_t + T1 / max(N, 1)
+        m2 = torch.clamp(T2 - T1 * T1 / max(N, 1), min=0.0)
+        var = m2 / (N - 1) if N > 1 else torch.zeros_like(m2)
+        std = torch.sqrt(var)
+        model = StandardScalerModel(mean.cpu().numpy(), std.cpu().numpy())
+        self._copyValues(model)
+        return model
+
+
+class StandardScalerModel(Model):
+    _params = StandardScaler._params
+
+    def __init__(self, mean=None, std=None):
+        super().__init__()
+        self._mean = np.asarray(mean if mean is not None else [], dtype=np.float64)
+        self._std = np.asarray(std if std is not None else [], dtype=np.float64)
+
+    @property
+    def mean(self) -> DenseVector:
+        return DenseVector(self._mean)
+
+    @property
+    def std(self) -> DenseVector:
+        return DenseVector(self._std)
+
+    def _transform(self, df):
+        x = df._feature_matrix(self.getInputCol())
+        d = x.shape[1]
+        with_std = self.getWithStd()
+        inv = np.where(self._std > 0, 1.0 / np.where(self._std > 0, self._std, 1.0), 0.0) if with_std \
+            else np.ones(d)
+        dev = x.device
+        od = self.getOutputDtype()
+        out_dtype = x.dtype if od == "auto" else {"float64": torch.float64, "float32": torch.float32,
+                                                 "bfloat16": torch.bfloat16}[od]
+        y = glm_ops.scale_apply(x, d, torch.as_tensor(self._mean, device=dev), torch.as_tensor(inv, device=dev),
+                                self.getWithMean(), out_dtype=out_dtype)
+        return _replace_col(df, self.getOutputCol(), ColumnData(y, None, T.VectorUDT()))
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        table = pa.Table.from_pylist([{"std": U.vector_struct(self._std), "mean": U.vector_struct(self._mean)}],
+                                     schema=pa.schema([("std", U.vector_arrow_type()), ("mean", U.vector_arrow_type())]))
+        U.write_parquet(path, "data", table)
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(U.vector_from_struct(row["mean"]), U.vector_from_struct(row["std"]))
+        U.apply_params(m, md)
+        return m
+
+
+class MinMaxScaler(Estimator):
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "min": (0.0, "lower bound of the output feature range", float),
+        "max": (1.0, "upper bound of the output feature range", float),
+    }
+
+    def __init__(self, min=None, max=None, inputCol=None, outputCol=None):  # noqa: A002
+        super().__init__(min=min, max=max, inputCol=inputCol, outputCol=outputCol)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _fit(self, df):
+        x = df._feature_matrix(self.getInputCol()).to(torch.float64)
+        d = x.shape[1]
+        comm = df._comm
+        lo = x.min(0).values if x.shape[0] else torch.full((d,), float("inf"), device=x.device, dtype=torch.float64)
+        hi = x.max(0).values if x.shape[0] else torch.full((d,), float("-inf"), device=x.device, dtype=torch.float64)
+        lo, hi = lo.clone(), hi.clone()
+        comm.allreduce_(lo, "min")
+        comm.allreduce_(hi, "max")
+        m = MinMaxScalerModel(lo.cpu().numpy(), hi.cpu().numpy())
+        self._copyValues(m)
+        return m
+
+
+class MinMaxScalerModel(Model):
+    _params = MinMaxScaler._params
+
+    def __init__(self, originalMin=None, originalMax=None):
+        super().__init__()
+        self._omin = np.asarray(originalMin if originalMin is not None else [], dtype=np.float64)
+        self._omax = np.asarray(originalMax if originalMax is not None else [], dtype=np.float64)
+
+    @property
+    def originalMin(self):
+        return DenseVector(self._omin)
+
+    @property
+    def originalMax(self):
+        return DenseVector(self._omax)
+
+    def _transform(self, df):
+        x = df._feature_matrix(self.getInputCol())
+        dev = x.device
+        rng = self._omax - self._omin
+        lo, hi = self.getMin(), self.getMax()
+        scale = np.where(rng != 0, (hi - lo) / np.where(rng != 0, rng, 1.0), 0.0)
+        # y = (x - omin) * scale + lo   (constant features map to (lo+hi)/2 as in Spark)
+        y = glm_ops.scale_apply(x, x.shape[1], torch.as_tensor(self._omin, device=dev),
+                                torch.as_tensor(scale, device=dev), True, out_dtype=x.dtype).to(torch.float64)
+        const = torch.as_tensor(rng == 0, device=dev)
+        y = torch.where(const, torch.full_like(y, 0.5 * (lo + hi)), y + lo).to(x.dtype)
+        return _replace_col(df, self.getOutputCol(), ColumnData(y, None, T.VectorUDT()))
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        table = pa.Table.from_pylist([{"originalMin": U.vector_struct(self._omin),
+                                       "originalMax": U.vector_struct(self._omax)}],
+                                     schema=pa.schema([("originalMin", U.vector_arrow_type()),
+                                                       ("originalMax", U.vector_arrow_type())]))
+        U.write_parquet(path, "data", table)
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(U.vector_from_struct(row["originalMin"]), U.vector_from_struct(row["originalMax"]))
+        U.apply_params(m, md)
+        return m
+
+
+class Binarizer(Transformer):
+    """x > threshold -> 1.0 else 0.0 (the reference's LOS_binary label, ref.py:176-177)."""
+    _params = {
+        "threshold": (0.0, "threshold used to binarize continuous features", float),
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+    }
+
+    def __init__(self, threshold=None, inputCol=None, outputCol=None):
+        super().__init__(threshold=threshold, inputCol=inputCol, outputCol=outputCol)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _transform(self, df):
+        cd = df._column_data(self.getInputCol())
+        v = cd.values
+        out = (v.to(torch.float64) > self.getThreshold()).to(torch.float64)
+        dt = T.VectorUDT() if isinstance(cd.dtype, T.VectorUDT) else T.DoubleType()
+        return _replace_col(df, self.getOutputCol(), ColumnData(out, cd.valid, dt))
+
+
+class StringIndexer(Estimator):
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "handleInvalid": ("error", "how to handle unseen labels: 'error', 'skip' or 'keep'", str),
+        "stringOrderType": ("frequencyDesc", "frequencyDesc|frequencyAsc|alphabetDesc|alphabetAsc", str),
+    }
+
+    def __init__(self, inputCol=None, outputCol=None, handleInvalid=None, stringOrderType=None):
+        super().__init__(inputCol=inputCol, outputCol=outputCol, handleInvalid=handleInvalid,
+                         stringOrderType=stringOrderType)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _fit(self, df):
+        from ..sql.dataframe import column_to_python
+        vals = column_to_python(df._column_data(self.getInputCol()))
+        counts: Dict[str, int] = {}
+        for v in vals:
+            if v is None:
+                continue
+            k = _fmt_label(v)
+            counts[k] = counts.get(k, 0) + 1
+        merged: Dict[str, int] = {}
+        for part in df._comm.allgather_object(counts):
+            for k, c in part.items():
+                merged[k] = merged.get(k, 0) + c
+        order = self.getStringOrderType()
+        items = list(merged.items())
+        if order == "frequencyDesc":
+            items.sort(key=lambda kv: (-kv[1], kv[0]))
+        elif order == "frequencyAsc":
+            items.sort(key=lambda kv: (kv[1], kv[0]))
+        elif order == "alphabetDesc":
+            items.sort(key=lambda kv: kv[0], reverse=True)
+        else:
+            items.sort(key=lambda kv: kv[0])
+        m = StringIndexerModel([k for k, _ in items])
+        self._copyValues(m)
+        return m
+
+
+def _fmt_label(v) -> str:
+    if isinstance(v, float) and v.is_integer():
+        return repr(v)
+    return str(v)
+
+
+class StringIndexerModel(Model):
+    _params = StringIndexer._params
+
+    def __init__(self, labels: Optional[List[str]] = None):
+        super().__init__()
+        self._labels = list(labels or [])
+
+    @property
+    def labels(self) -> List[str]:
+        return list(self._labels)
+
+    @property
+    def labelsArray(self) -> List[List[str]]:
+        return [list(self._labels)]
+
+    def _transform(self, df):
+        from ..sql.dataframe import column_to_python
+        vals = column_to_python(df._column_data(self.getInputCol()))
+        idx = {l: i for i, l in enumerate(self._labels)}
+        hi = self.getHandleInvalid()
+        out = np.zeros(len(vals), dtype=np.float64)
+        keep = np.ones(len(vals), dtype=bool)
+        for i, v in enumerate(vals):
+            k = None if v is None else idx.get(_fmt_label(v))
+            if k is None:
+                if hi == "error":
+                    raise ValueError(f"StringIndexer: unseen label {v!r}; set handleInvalid='skip' or 'keep'")
+                if hi == "skip":
+                    keep[i] = False
+                else:
+                    out[i] = len(self._labels)
+            else:
+                out[i] = k
+        res = _replace_col(df, self.getOutputCol(),
+                           ColumnData(torch.as_tensor(out, device=df._device), None, T.DoubleType()))
+        if not keep.all():
+            res = res._mask_rows(torch.as_tensor(keep, device=df._device))
+        return res
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        U.write_parquet(path, "data", pa.table({"labelsArray": pa.array([[self._labels]],
+                                                                        type=pa.list_(pa.list_(pa.string())))}))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(row["labelsArray"][0])
+        U.apply_params(m, md)
+        return m
+
+
+class IndexToString(Transformer):
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "labels": (NO_DEFAULT, "ordered list of labels", "liststr"),
+    }
+
+    def __init__(self, inputCol=None, outputCol=None, labels=None):
+        super().__init__(inputCol=inputCol, outputCol=outputCol, labels=labels)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _transform(self, df):
+        cd = df._column_data(self.getInputCol())
+        labels = self.getLabels()
+        vals = cd.values.cpu().numpy()
+        out = np.array([labels[int(v)] if 0 <= int(v) < len(labels) else None for v in vals], dtype=object)
+        return _replace_col(df, self.getOutputCol(), ColumnData(out, None, T.StringType()))

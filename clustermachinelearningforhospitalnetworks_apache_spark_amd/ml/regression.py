@@ -1,0 +1,381 @@
+"""Regressors of the reference (ref.py:30, ref.py:145-158): LinearRegression,
+DecisionTreeRegressor, RandomForestRegressor.
+
+LinearRegression (Spark defaults maxIter=100, regParam=0, elasticNetParam=0,
+tol=1e-6, fitIntercept=True, standardization=True, solver="auto"): the normal
+equations are built on the device in ONE pass (K15 Gram [X 1 y]ᵀ[X 1 y] in f64),
+all-reduced (C4), and solved on the host in float64 — Cholesky, with ridge in the
+standardized space like Spark's WeightedLeastSquares; L1/elastic-net by coordinate
+descent on the same Gram (same optimum as Spark's OWL-QN); a singular system falls
+back to the minimum-norm least-squares solution.
+"""
+from __future__ import annotations
+
+import math
+from typing import Optional
+
+import numpy as np
+import torch
+
+from ..ops import glm_ops
+from ..sql import types as T
+from ..sql.column import ColumnData
+from . import util as U
+from .base import Estimator, Model
+from .evaluation import RegressionEvaluator
+from .feature import _replace_col
+from .linalg import DenseVector, as_array
+from .tree_models import (FOREST_PARAMS, TREE_PARAMS, TreeEstimatorMixin, TreeModelMixin, _default_seed)
+
+_LR_PARAMS = {
+    "featuresCol": ("features", "features column name", str),
+    "labelCol": ("label", "label column name", str),
+    "predictionCol": ("prediction", "prediction column name", str),
+    "maxIter": (100, "max number of iterations (>= 0)", int),
+    "regParam": (0.0, "regularization parameter (>= 0)", float),
+    "elasticNetParam": (0.0, "ElasticNet mixing parameter in [0, 1]: 0 = L2, 1 = L1", float),
+    "tol": (1e-6, "convergence tolerance for iterative algorithms (>= 0)", float),
+    "fitIntercept": (True, "whether to fit an intercept term", bool),
+    "standardization": (True, "whether to standardize the training features before fitting", bool),
+    "solver": ("auto", "the solver algorithm for optimization: auto, normal, l-bfgs", str),
+    "weightCol": (None, "weight column name", None),
+    "aggregationDepth": (2, "suggested depth for treeAggregate (>= 2)", int),
+    "loss": ("squaredError", "the loss function to be optimized: squaredError, huber", str),
+    "epsilon": (1.35, "the shape parameter to control the amount of robustness (huber)", float),
+    "maxBlockSizeInMB": (0.0, "maximum memory in MB for stacking input data into blocks", float),
+}
+
+
+def solve_wls(G: np.ndarray, d: int, reg: float, alpha: float, fit_intercept: bool, standardization: bool,
+              max_iter: int = 1000, tol: float = 1e-10):
+    """Solve weighted least squares from the Gram matrix of [X 1 y] (weights folded in).
+
+    Returns (coefficients [d], intercept, diag info dict).
+    """
+    n = G[d, d]
+    sx = G[:d, d]
+    sy = G[d, d + 1]
+    XtX = G[:d, :d]
+    Xty = G[:d, d + 1]
+    yty = G[d + 1, d + 1]
+    mx = sx / n
+    my = sy / n
+    if fit_intercept:
+        Cxx = XtX / n - np.outer(mx, mx)
+        cxy = Xty / n - mx * my
+        vy = yty / n - my * my
+    else:
+        Cxx = XtX / n
+        cxy = Xty / n
+        vy = yty / n
+    var_x = np.maximum(np.diag(XtX) / n - mx * mx, 0.0)
+    unbiased = n / (n - 1) if n > 1 else 1.0
+    sigx = np.sqrt(var_x * unbiased)
+    sigy = math.sqrt(max(yty / n - my * my, 0.0) * unbiased)
+    info = {"n": n, "mean_x": mx, "mean_y": my, "std_x": sigx, "std_y": sigy}
+    if sigy == 0.0 and fit_intercept:
+        # constant label: Spark returns zero coefficients and intercept = label mean
+        return np.zeros(d), my, info
+    active = sigx > 0
+    if reg == 0.0:
+        A = Cxx[np.ix_(active, active)]
+        b = cxy[active]
+        w = np.zeros(d)
+        try:
+            L = np.linalg.cholesky(A)
+            w[active] = np.linalg.solve(L.T, np.linalg.solve(L, b))
+        except np.linalg.LinAlgError:
+            w[active] = np.linalg.lstsq(A, b, rcond=None)[0]
+    else:
+        sy_ = sigy if sigy > 0 else 1.0
+        s = np.where(active, sigx, 1.0)
+        Z = Cxx / np.outer(s, s)                    # covariance of standardized features
+        zt = cxy / s / sy_                          # covariance with standardized label
+        l2 = reg * (1.0 - alpha)
+        l1 = reg * alpha
+        # standardization=False penalises the original-scale coefficients: rescale per feature
+        pen2 = np.full(d, l2) if standardization else l2 / (s * s)
+        pen1 = np.full(d, l1) if standardization else l1 / s
+        beta = np.zeros(d)
+        if l1 == 0.0:
+            A = Z + np.diag(pen2)
+            A = A[np.ix_(active, active)]
+            beta[active] = np.linalg.solve(A, zt[active])
+        else:
+            for _ in range(max_iter):
+                maxd = 0.0
+                for j in np.nonzero(active)[0]:
+                    rj = zt[j] - Z[j] @ beta + Z[j, j] * beta[j]
+                    new = np.sign(rj) * max(abs(rj) - pen1[j], 0.0) / (Z[j, j] + pen2[j])
+                    maxd = max(maxd, abs(new - beta[j]))
+                    beta[j] = new
+                if maxd < tol:
+                    break
+        w = np.where(active, beta * sy_ / s, 0.0)
+    intercept = (my - mx @ w) if fit_intercept else 0.0
+    return w, float(intercept), info
+
+
+class LinearRegression(Estimator):
+    _params = _LR_PARAMS
+
+    def __init__(self, featuresCol=None, labelCol=None, predictionCol=None, maxIter=None, regParam=None,
+                 elasticNetParam=None, tol=None, fitIntercept=None, standardization=None, solver=None,
+                 weightCol=None, aggregationDepth=None, loss=None, epsilon=None, maxBlockSizeInMB=None):
+        super().__init__(featuresCol=featuresCol, labelCol=labelCol, predictionCol=predictionCol, maxIter=maxIter,
+                         regParam=regParam, elasticNetParam=elasticNetParam, tol=tol, fitIntercept=fitIntercept,
+                         standardization=standardization, solver=solver, weightCol=weightCol,
+                         aggregationDepth=aggregationDepth, loss=loss, epsilon=epsilon,
+                         maxBlockSizeInMB=maxBlockSizeInMB)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _fit(self, df):
+        if self.getLoss() != "squaredError":
+            raise NotImplementedError("only loss='squaredError' is supported")
+        x = df._feature_matrix(self.getFeaturesCol())
+        d = x.shape[1]
+        y = df._column_data(self.getLabelCol()).values.to(torch.float64)
+        w = df._column_data(self.getOrDefault("weightCol")).values.to(torch.float64) \
+            if self.isSet("weightCol") else None
+        G = glm_ops.gram(x, d, y, w)
+        df._comm.allreduce_(G)
+        Gn = G.cpu().numpy()
+        if Gn[d, d] == 0:
+            raise ValueError("LinearRegression: empty training set")
+        coef, intercept, info = solve_wls(Gn, d, self.getRegParam(), self.getElasticNetParam(),
+                                          self.getFitIntercept(), self.getStandardization(),
+                                          max_iter=max(self.getMaxIter(), 1) * 10, tol=self.getTol())
+        model = LinearRegressionModel(coef, intercept)
+        self._copyValues(model)
+        model._summary = LinearRegressionTrainingSummary(model, df, Gn, d, self.getRegParam() == 0.0)
+        return model
+
+
+class LinearRegressionModel(Model):
+    _params = _LR_PARAMS
+
+    def __init__(self, coefficients=None, intercept: float = 0.0, scale: float = 1.0):
+        super().__init__()
+        self._coef = np.asarray(coefficients if coefficients is not None else [], dtype=np.float64)
+        self._intercept = float(intercept)
+        self._scale = float(scale)
+        self._summary = None
+
+    @property
+    def coefficients(self) -> DenseVector:
+        return DenseVector(self._coef)
+
+    @property
+    def intercept(self) -> float:
+        return self._intercept
+
+    @property
+    def scale(self) -> float:
+        return self._scale
+
+    @property
+    def numFeatures(self) -> int:
+        return int(self._coef.shape[0])
+
+    def predict(self, value) -> float:
+        return float(as_array(value) @ self._coef + self._intercept)
+
+    def _transform(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        coef = torch.as_tensor(np.r_[self._coef, self._intercept], device=x.device)
+        pred = glm_ops.linear_predict(x, x.shape[1], coef, "identity")
+        return _replace_col(df, self.getPredictionCol(), ColumnData(pred, None, T.DoubleType()))
+
+    def evaluate(self, df) -> "LinearRegressionSummary":
+        return LinearRegressionSummary(self, df)
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        table = pa.Table.from_pylist(
+            [{"intercept": self._intercept, "coefficients": U.vector_struct(self._coef), "scale": self._scale}],
+            schema=pa.schema([pa.field("intercept", pa.float64(), nullable=False),
+                              ("coefficients", U.vector_arrow_type()),
+                              pa.field("scale", pa.float64(), nullable=False)]))
+        U.write_parquet(path, "data", table)
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(U.vector_from_struct(row["coefficients"]), row["intercept"], row.get("scale", 1.0))
+        U.apply_params(m, md)
+        return m
+
+
+class LinearRegressionSummary:
+    def __init__(self, model: LinearRegressionModel, df):
+        self._model = model
+        self._df = df
+        self.labelCol = model.getLabelCol()
+        self.predictionCol = model.getPredictionCol()
+        self.featuresCol = model.getFeaturesCol()
+        self._pred = None
+
+    @property
+    def predictions(self):
+        if self._pred is None:
+            self._pred = self._model.transform(self._df)
+        return self._pred
+
+    def _metric(self, name):
+        return RegressionEvaluator(labelCol=self.labelCol, predictionCol=self.predictionCol,
+                                   metricName=name).evaluate(self.predictions)
+
+    @property
+    def rootMeanSquaredError(self) -> float:
+        return self._metric("rmse")
+
+    @property
+    def meanSquaredError(self) -> float:
+        return self._metric("mse")
+
+    @property
+    def meanAbsoluteError(self) -> float:
+        return self._metric("mae")
+
+    @property
+    def r2(self) -> float:
+        return self._metric("r2")
+
+    @property
+    def explainedVariance(self) -> float:
+        return self._metric("var")
+
+    @property
+    def numInstances(self) -> int:
+        return self._df.count()
+
+    @property
+    def degreesOfFreedom(self) -> int:
+        return self.numInstances - self._model.numFeatures - (1 if self._model.getFitIntercept() else 0)
+
+    @property
+    def r2adj(self) -> float:
+        n = self.numInstances
+        p = self._model.numFeatures
+        k = 1 if self._model.getFitIntercept() else 0
+        return 1.0 - (1.0 - self.r2) * (n - k) / max(n - p - k, 1)
+
+    @property
+    def residuals(self):
+        from ..sql import functions as F
+        p = self.predictions
+        return p.select((F.col(self.labelCol) - F.col(self.predictionCol)).alias("residuals"))
+
+
+class LinearRegressionTrainingSummary(LinearRegressionSummary):
+    def __init__(self, model, df, G: np.ndarray, d: int, exact: bool):
+        super().__init__(model, df)
+        self._G = G
+        self._d = d
+        self._exact = exact
+        self.objectiveHistory = [0.0]
+        self.totalIterations = 1
+
+    def _cov(self):
+        if not self._exact:
+            raise RuntimeError("coefficient statistics need regParam=0 (normal equation solver)")
+        G, d = self._G, self._d
+        fi = self._model.getFitIntercept()
+        idx = list(range(d)) + ([d] if fi else [])
+        A = G[np.ix_(idx, idx)]
+        n = G[d, d]
+        dof = n - len(idx)
+        coef = np.r_[self._model._coef, [self._model._intercept] if fi else []]
+        # SSE from the Gram: yᵀy − 2 βᵀAᵀy + βᵀAβ
+        Aty = G[idx, d + 1]
+        sse = G[d + 1, d + 1] - 2 * coef @ Aty + coef @ A @ coef
+        sigma2 = max(sse, 0.0) / max(dof, 1)
+        cov = sigma2 * np.linalg.pinv(A)
+        return coef, cov, dof
+
+    @property
+    def coefficientStandardErrors(self):
+        _, cov, _ = self._cov()
+        return list(np.sqrt(np.maximum(np.diag(cov), 0.0)))
+
+    @property
+    def tValues(self):
+        coef, cov, _ = self._cov()
+        se = np.sqrt(np.maximum(np.diag(cov), 1e-300))
+        return list(coef / se)
+
+    @property
+    def pValues(self):
+        from scipy import stats
+        coef, cov, dof = self._cov()
+        se = np.sqrt(np.maximum(np.diag(cov), 1e-300))
+        t = np.abs(coef / se)
+        return list(2 * stats.t.sf(t, max(dof, 1)))
+
+
+# ------------------------------------------------------------------------------------------------ trees
+
+class DecisionTreeRegressor(TreeEstimatorMixin, Estimator):
+    _task = "regression"
+    _params = dict(TREE_PARAMS, impurity=("variance", "criterion used for information gain (variance)", str),
+                   seed=(_default_seed("org.apache.spark.ml.regression.DecisionTreeRegressor"), "random seed", int),
+                   varianceCol=(None, "column name for the biased sample variance of prediction", None))
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self._defaultParamMap.pop("weightCol", None)
+        self._defaultParamMap.pop("varianceCol", None)
+
+    def _fit(self, df):
+        trees, d, _ = self._tree_fit(df)
+        m = DecisionTreeRegressionModel()
+        self._copyValues(m)
+        m._init_trees(trees, d)
+        return m
+
+
+class DecisionTreeRegressionModel(TreeModelMixin, Model):
+    _task = "regression"
+    _params = DecisionTreeRegressor._params
+
+    def __init__(self):
+        super().__init__()
+        self._init_trees([], 0)
+
+    @staticmethod
+    def _single_tree_class():
+        return DecisionTreeRegressionModel
+
+
+class RandomForestRegressor(TreeEstimatorMixin, Estimator):
+    _task = "regression"
+    _forest = True
+    _params = dict(TREE_PARAMS, **FOREST_PARAMS,
+                   impurity=("variance", "criterion used for information gain (variance)", str),
+                   seed=(_default_seed("org.apache.spark.ml.regression.RandomForestRegressor"), "random seed", int))
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _fit(self, df):
+        trees, d, _ = self._tree_fit(df)
+        m = RandomForestRegressionModel()
+        self._copyValues(m)
+        m._init_trees(trees, d)
+        return m
+
+
+class RandomForestRegressionModel(TreeModelMixin, Model):
+    _task = "regression"
+    _forest = True
+    _params = RandomForestRegressor._params
+
+    def __init__(self):
+        super().__init__()
+        self._init_trees([], 0)
+
+    @staticmethod
+    def _single_tree_class():
+        return DecisionTreeRegressionModel

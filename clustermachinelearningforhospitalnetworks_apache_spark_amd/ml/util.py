@@ -1,0 +1,281 @@
+"""Model persistence in Spark's on-disk ML format (ref.py:241-243).
+
+``path/metadata/part-00000``: one JSON line ``{"class", "timestamp", "sparkVersion",
+"uid", "paramMap", "defaultParamMap"}`` (+ ``_SUCCESS``); ``path/data/part-*.parquet``
+holds the model data with Spark's schemas (VectorUDT / MatrixUDT structs).  The
+layouts come from Spark 3.x knowledge and could not be verified offline (no JVM
+here) — they are kept in this one module.
+
+``model.save(p)`` refuses an existing path (Spark semantics, the reference's dead
+per-batch save ref.py:103); ``model.write().overwrite().save(p)`` replaces it
+(ref.py:241-243).  Only rank 0 writes; all ranks meet at a barrier.
+"""
+from __future__ import annotations
+
+import importlib
+import json
+import os
+import shutil
+import time
+import uuid
+from typing import Any, Dict, List, Optional
+
+import numpy as np
+
+SPARK_VERSION = "3.5.1"
+
+# python class  <->  Spark JVM class names
+_JVM = {
+    "LinearRegression": "org.apache.spark.ml.regression.LinearRegression",
+    "LinearRegressionModel": "org.apache.spark.ml.regression.LinearRegressionModel",
+    "DecisionTreeRegressor": "org.apache.spark.ml.regression.DecisionTreeRegressor",
+    "DecisionTreeRegressionModel": "org.apache.spark.ml.regression.DecisionTreeRegressionModel",
+    "RandomForestRegressor": "org.apache.spark.ml.regression.RandomForestRegressor",
+    "RandomForestRegressionModel": "org.apache.spark.ml.regression.RandomForestRegressionModel",
+    "DecisionTreeClassifier": "org.apache.spark.ml.classification.DecisionTreeClassifier",
+    "DecisionTreeClassificationModel": "org.apache.spark.ml.classification.DecisionTreeClassificationModel",
+    "RandomForestClassifier": "org.apache.spark.ml.classification.RandomForestClassifier",
+    "RandomForestClassificationModel": "org.apache.spark.ml.classification.RandomForestClassificationModel",
+    "LogisticRegression": "org.apache.spark.ml.classification.LogisticRegression",
+    "LogisticRegressionModel": "org.apache.spark.ml.classification.LogisticRegressionModel",
+    "KMeans": "org.apache.spark.ml.clustering.KMeans",
+    "KMeansModel": "org.apache.spark.ml.clustering.KMeansModel",
+    "StandardScaler": "org.apache.spark.ml.feature.StandardScaler",
+    "StandardScalerModel": "org.apache.spark.ml.feature.StandardScalerModel",
+    "VectorAssembler": "org.apache.spark.ml.feature.VectorAssembler",
+    "StringIndexer": "org.apache.spark.ml.feature.StringIndexer",
+    "StringIndexerModel": "org.apache.spark.ml.feature.StringIndexerModel",
+    "Binarizer": "org.apache.spark.ml.feature.Binarizer",
+    "MinMaxScaler": "org.apache.spark.ml.feature.MinMaxScaler",
+    "MinMaxScalerModel": "org.apache.spark.ml.feature.MinMaxScalerModel",
+    "Pipeline": "org.apache.spark.ml.Pipeline",
+    "PipelineModel": "org.apache.spark.ml.PipelineModel",
+    "RegressionEvaluator": "org.apache.spark.ml.evaluation.RegressionEvaluator",
+    "MulticlassClassificationEvaluator": "org.apache.spark.ml.evaluation.MulticlassClassificationEvaluator",
+    "BinaryClassificationEvaluator": "org.apache.spark.ml.evaluation.BinaryClassificationEvaluator",
+    "ClusteringEvaluator": "org.apache.spark.ml.evaluation.ClusteringEvaluator",
+}
+_PY = {
+    "LinearRegression": "regression", "LinearRegressionModel": "regression",
+    "DecisionTreeRegressor": "regression", "DecisionTreeRegressionModel": "regression",
+    "RandomForestRegressor": "regression", "RandomForestRegressionModel": "regression",
+    "DecisionTreeClassifier": "classification", "DecisionTreeClassificationModel": "classification",
+    "RandomForestClassifier": "classification", "RandomForestClassificationModel": "classification",
+    "LogisticRegression": "classification", "LogisticRegressionModel": "classification",
+    "KMeans": "clustering", "KMeansModel": "clustering",
+    "StandardScaler": "feature", "StandardScalerModel": "feature", "VectorAssembler": "feature",
+    "StringIndexer": "feature", "StringIndexerModel": "feature", "Binarizer": "feature",
+    "MinMaxScaler": "feature", "MinMaxScalerModel": "feature",
+    "Pipeline": "pipeline", "PipelineModel": "pipeline",
+    "RegressionEvaluator": "evaluation", "MulticlassClassificationEvaluator": "evaluation",
+    "BinaryClassificationEvaluator": "evaluation", "ClusteringEvaluator": "evaluation",
+}
+
+
+def jvm_class(obj) -> str:
+    name = type(obj).__name__
+    return _JVM.get(name, f"cml.{type(obj).__module__}.{name}")
+
+
+def py_class_from_jvm(jvm: str):
+    short = jvm.rsplit(".", 1)[-1]
+    mod = _PY.get(short)
+    if mod is None:
+        raise ValueError(f"unknown model class {jvm}")
+    m = importlib.import_module(f"clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.{mod}")
+    return getattr(m, short)
+
+
+def _json_value(v):
+    if isinstance(v, (np.integer,)):
+        return int(v)
+    if isinstance(v, (np.floating,)):
+        return float(v)
+    if isinstance(v, np.ndarray):
+        return v.tolist()
+    return v
+
+
+def _comm():
+    from ..sql.session import SparkSession
+    s = SparkSession.getActiveSession()
+    if s is None:
+        from ..parallel.comm import local_comm
+        return local_comm()
+    return s._comm
+
+
+def write_metadata(instance, path: str, extra: Optional[Dict[str, Any]] = None, param_map=None) -> None:
+    md = {"class": jvm_class(instance), "timestamp": int(time.time() * 1000), "sparkVersion": SPARK_VERSION,
+          "uid": instance.uid,
+          "paramMap": {k: _json_value(v) for k, v in (param_map if param_map is not None
+                                                      else instance._paramMap).items()},
+          "defaultParamMap": {k: _json_value(v) for k, v in instance._defaultParamMap.items()}}
+    if extra:
+        md.update(extra)
+    d = os.path.join(path, "metadata")
+    os.makedirs(d, exist_ok=True)
+    with open(os.path.join(d, "part-00000"), "w") as fh:
+        fh.write(json.dumps(md, separators=(",", ":")) + "\n")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def read_metadata(path: str) -> Dict[str, Any]:
+    with open(os.path.join(path, "metadata", "part-00000")) as fh:
+        return json.loads(fh.readline())
+
+
+def apply_params(instance, md: Dict[str, Any]) -> None:
+    instance.uid = md.get("uid", instance.uid)
+    for k, v in md.get("defaultParamMap", {}).items():
+        if instance.hasParam(k):
+            instance._defaultParamMap[k] = v
+    for k, v in md.get("paramMap", {}).items():
+        if instance.hasParam(k):
+            instance._paramMap[k] = v
+
+
+def write_parquet(path: str, sub: str, table) -> None:
+    import pyarrow.parquet as pq
+    d = os.path.join(path, sub)
+    os.makedirs(d, exist_ok=True)
+    pq.write_table(table, os.path.join(d, f"part-00000-{uuid.uuid4()}-c000.snappy.parquet"), compression="snappy")
+    open(os.path.join(d, "_SUCCESS"), "w").close()
+
+
+def read_parquet(path: str, sub: str):
+    import pyarrow as pa
+    import pyarrow.parquet as pq
+    d = os.path.join(path, sub)
+    files = sorted(f for f in os.listdir(d) if f.endswith(".parquet"))
+    return pa.concat_tables([pq.read_table(os.path.join(d, f)) for f in files])
+
+
+# ---------------------------------------------------------------------------------------------- UDT encoders
+
+def vector_struct(v) -> Dict[str, Any]:
+    """VectorUDT row value (dense)."""
+    arr = np.asarray(v.toArray() if hasattr(v, "toArray") else v, dtype=np.float64)
+    return {"type": 1, "size": None, "indices": None, "values": arr.tolist()}
+
+
+def vector_from_struct(s) -> np.ndarray:
+    if s is None:
+        return None
+    if s["type"] == 0:
+        a = np.zeros(s["size"])
+        a[np.asarray(s["indices"], dtype=np.int64)] = s["values"]
+        return a
+    return np.asarray(s["values"], dtype=np.float64)
+
+
+def matrix_struct(m: np.ndarray) -> Dict[str, Any]:
+    """MatrixUDT row value (dense, column-major, isTransposed=false)."""
+    m = np.asarray(m, dtype=np.float64)
+    return {"type": 1, "numRows": int(m.shape[0]), "numCols": int(m.shape[1]), "colPtrs": None,
+            "rowIndices": None, "values": m.T.reshape(-1).tolist(), "isTransposed": False}
+
+
+def matrix_from_struct(s) -> np.ndarray:
+    vals = np.asarray(s["values"], dtype=np.float64)
+    if s.get("isTransposed"):
+        return vals.reshape(s["numRows"], s["numCols"])
+    return vals.reshape(s["numCols"], s["numRows"]).T
+
+
+def vector_arrow_type():
+    from ..io.arrow import vector_udt_arrow
+    return vector_udt_arrow()
+
+
+def matrix_arrow_type():
+    import pyarrow as pa
+    return pa.struct([pa.field("type", pa.int8(), nullable=False), pa.field("numRows", pa.int32(), nullable=False),
+                      pa.field("numCols", pa.int32(), nullable=False),
+                      pa.field("colPtrs", pa.list_(pa.field("element", pa.int32(), nullable=False))),
+                      pa.field("rowIndices", pa.list_(pa.field("element", pa.int32(), nullable=False))),
+                      pa.field("values", pa.list_(pa.field("element", pa.float64(), nullable=False))),
+                      pa.field("isTransposed", pa.bool_(), nullable=False)])
+
+
+# ---------------------------------------------------------------------------------------------- writer/reader
+
+class MLWriter:
+    def __init__(self, instance):
+        self.instance = instance
+        self._overwrite = False
+
+    def overwrite(self) -> "MLWriter":
+        self._overwrite = True
+        return self
+
+    def option(self, key, value) -> "MLWriter":
+        return self
+
+    def session(self, spark) -> "MLWriter":
+        return self
+
+    def save(self, path: str) -> None:
+        from ..io.reader import strip_scheme
+        path = strip_scheme(path)
+        comm = _comm()
+        if os.path.exists(path) and not self._overwrite:
+            raise FileExistsError(f"Path {path} already exists. To overwrite it, use write().overwrite().save(path)")
+        comm.barrier()
+        if comm.is_root:
+            if os.path.exists(path):
+                shutil.rmtree(path)
+            os.makedirs(path, exist_ok=True)
+            self.instance._save_impl(path)
+        comm.barrier()
+
+
+class MLWritable:
+    def write(self) -> MLWriter:
+        return MLWriter(self)
+
+    def save(self, path: str) -> None:
+        self.write().save(path)
+
+    def _save_impl(self, path: str) -> None:
+        write_metadata(self, path)
+
+
+class MLReader:
+    def __init__(self, cls):
+        self.cls = cls
+
+    def load(self, path: str):
+        from ..io.reader import strip_scheme
+        path = strip_scheme(path)
+        md = read_metadata(path)
+        cls = py_class_from_jvm(md["class"]) if self.cls is None else self.cls
+        return cls._load_impl(path, md)
+
+    def session(self, spark) -> "MLReader":
+        return self
+
+
+class MLReadable:
+    @classmethod
+    def read(cls) -> MLReader:
+        return MLReader(cls)
+
+    @classmethod
+    def load(cls, path: str):
+        return cls.read().load(path)
+
+    @classmethod
+    def _load_impl(cls, path: str, md: Dict[str, Any]):
+        inst = cls()
+        apply_params(inst, md)
+        return inst
+
+
+DefaultParamsWritable = MLWritable
+DefaultParamsReadable = MLReadable
+
+
+def load(path: str):
+    """Load any saved estimator/model/pipeline by its metadata class."""
+    return MLReader(None).load(path)

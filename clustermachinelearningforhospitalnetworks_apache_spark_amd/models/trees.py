@@ -1,0 +1,503 @@
+"""Level-wise decision-tree / random-forest engine (Spark MLlib semantics).
+
+Used by DecisionTreeRegressor / RandomForestRegressor (ref.py:150-158) and
+DecisionTreeClassifier / RandomForestClassifier (ref.py:182-190).  Spark defaults
+the reference relies on: maxDepth=5, maxBins=32,
+minInstancesPerNode=1, minInfoGain=0, impurity variance (regression) / gini
+(classification), RF numTrees=20 with Poisson(1) bootstrap weights and per-node
+feature subsets ("auto" -> onethird for regression, sqrt for classification).
+
+Pipeline per fit (each rank holds a row shard, all trees are grown together):
+  1. split candidates: a counter-based row sample (GPU-count invariant) of
+     max(maxBins², 10000) rows is all-gathered, thresholds per feature follow
+     Spark's findSplitsForContinuousFeature rule (midpoints between distinct
+     values, or count-stride quantiles when there are more than maxBins-1);
+  2. K17 binize: uint8 bin codes [n, d] resident on the device;
+  3. per level: K18 histogram of (tree, node, feature, bin) stats for every tree at
+     once, ONE all-reduce of the histogram buffer, best split per node on the host
+     (identical on every rank), K20 routes rows to children;
+  4. leaves keep the (weighted) impurity statistics Spark stores in NodeData.
+"""
+from __future__ import annotations
+
+import math
+from dataclasses import dataclass, field
+from typing import List, Optional, Sequence
+
+import numpy as np
+import torch
+
+from .. import _native
+from .._native import c_int, c_ll, c_vp
+from ..parallel.comm import Communicator, local_comm
+from ..utils import rng
+
+_native.register_kernel_sigs({
+    "cml_tree_binize": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "cml_tree_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int,
+                              c_vp]),
+    "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+})
+
+
+@dataclass
+class Node:
+    id: int = -1                       # preorder id (assigned at the end, Spark's NodeData id)
+    prediction: float = 0.0
+    impurity: float = 0.0
+    stats: np.ndarray = None           # impurity calculator stats
+    count: float = 0.0                 # weighted instance count
+    gain: float = -1.0
+    feature: int = -1                  # split feature (-1: leaf)
+    threshold: float = 0.0
+    split_bin: int = -1
+    left: Optional["Node"] = None
+    right: Optional["Node"] = None
+
+    @property
+    def is_leaf(self) -> bool:
+        return self.feature < 0
+
+
+@dataclass
+class TreeParams:
+    task: str = "regression"           # or "classification"
+    num_classes: int = 2
+    impurity: str = "variance"
+    max_depth: int = 5
+    max_bins: int = 32
+    min_instances: int = 1
+    min_weight_fraction: float = 0.0
+    min_info_gain: float = 0.0
+    num_trees: int = 1
+    subsampling_rate: float = 1.0
+    bootstrap: bool = True
+    feature_subset: str = "auto"
+    seed: int = 0
+
+
+# ---------------------------------------------------------------------------------------------- impurity
+
+def impurity_of(stats: np.ndarray, kind: str) -> float:
+    if kind == "variance":
+        w = stats[0]
+        if w <= 0:
+            return 0.0
+        m = stats[1] / w
+        return max(stats[2] / w - m * m, 0.0)
+    tot = stats.sum()
+    if tot <= 0:
+        return 0.0
+    p = stats / tot
+    if kind == "gini":
+        return float(1.0 - (p * p).sum())
+    nz = p[p > 0]
+    return float(-(nz * np.log2(nz)).sum())
+
+
+def count_of(stats: np.ndarray, kind: str) -> float:
+    return float(stats[0]) if kind == "variance" else float(stats.sum())
+
+
+def predict_of(stats: np.ndarray, kind: str) -> float:
+    if kind == "variance":
+        return float(stats[1] / stats[0]) if stats[0] > 0 else 0.0
+    return float(np.argmax(stats))
+
+
+# ---------------------------------------------------------------------------------------------- split candidates
+
+def continuous_splits(values: np.ndarray, num_splits: int) -> np.ndarray:
+    """Spark findSplitsForContinuousFeature: midpoints of distinct values, or count-stride cut points."""
+    if values.size == 0:
+        return np.zeros(0)
+    uniq, counts = np.unique(values, return_counts=True)
+    if uniq.size - 1 <= num_splits:
+        return (uniq[:-1] + uniq[1:]) / 2.0
+    stride = counts.sum() / (num_splits + 1)
+    out = []
+    current = counts[0]
+    target = stride
+    for i in range(1, uniq.size):
+        prev = current
+        current += counts[i]
+        if abs(prev - target) < abs(current - target):
+            out.append((uniq[i - 1] + uniq[i]) / 2.0)
+            target += stride
+    return np.asarray(out, dtype=np.float64)
+
+
+def subset_size(strategy: str, d: int, task: str, num_trees: int) -> int:
+    s = strategy.lower()
+    if s == "auto":
+        s = "all" if num_trees == 1 else ("sqrt" if task == "classification" else "onethird")
+    if s == "all":
+        return d
+    if s == "sqrt":
+        return max(1, int(math.ceil(math.sqrt(d))))
+    if s == "log2":
+        return max(1, int(math.ceil(math.log2(d))))
+    if s == "onethird":
+        return max(1, int(math.ceil(d / 3.0)))
+    try:
+        v = float(s)
+    except ValueError:
+        raise ValueError(f"unknown featureSubsetStrategy {strategy!r}")
+    if v.is_integer() and v >= 1:
+        return min(d, int(v))
+    return max(1, int(math.ceil(v * d)))
+
+
+# ---------------------------------------------------------------------------------------------- engine
+
+class ForestEngine:
+    def __init__(self, x: torch.Tensor, y: torch.Tensor, params: TreeParams, comm: Optional[Communicator] = None,
+                 row_ids: Optional[torch.Tensor] = None, weights: Optional[torch.Tensor] = None):
+        self.comm = comm or local_comm()
+        self.p = params
+        self.x = x.to(torch.float64).contiguous()
+        self.n, self.d = int(x.shape[0]), int(x.shape[1])
+        self.dev = x.device
+        self.gpu = x.is_cuda
+        self.y = y.to(torch.float64).contiguous()
+        self.row_ids = row_ids if row_ids is not None else torch.arange(self.n, device=self.dev)
+        self.sample_weight = weights
+        self.kind = params.impurity
+        self.S = 3 if self.kind == "variance" else params.num_classes
+
+    # -------------------------------------------------------------- splits
+    def find_splits(self) -> List[np.ndarray]:
+        p = self.p
+        gn = self.comm.sum_scalar(float(self.n))
+        required = max(p.max_bins * p.max_bins, 10000)
+        frac = min(required / max(gn, 1.0), 1.0)
+        if self.n:
+            u = rng.uniform(self.row_ids, p.seed, stream=21)
+            sample = self.x[u < frac] if frac < 1.0 else self.x
+        else:
+            sample = self.x
+        allv = self.comm.allgather_cat(sample.to(torch.float64)).cpu().numpy()
+        return [continuous_splits(allv[:, j], p.max_bins - 1) for j in range(self.d)]
+
+    def binize(self, splits: List[np.ndarray]) -> torch.Tensor:
+        ms = max(1, max((len(s) for s in splits), default=1))
+        thr = np.full((self.d, ms), np.inf)
+        ns = np.zeros(self.d, dtype=np.int32)
+        for j, s in enumerate(splits):
+            thr[j, : len(s)] = s
+            ns[j] = len(s)
+        self.nbins = ms + 1
+        if not self.gpu or self.n == 0:
+            t = torch.as_tensor(thr, device=self.dev)
+            bins = torch.empty((self.n, self.d), dtype=torch.uint8, device=self.dev)
+            for j in range(self.d):
+                bins[:, j] = torch.searchsorted(t[j, : max(ns[j], 0)].contiguous(), self.x[:, j].contiguous(),
+                                                right=False).to(torch.uint8) if ns[j] else 0
+            return bins
+        thr_t = torch.as_tensor(thr, device=self.dev)
+        ns_t = torch.as_tensor(ns, device=self.dev)
+        bins = torch.empty((self.n, self.d), dtype=torch.uint8, device=self.dev)
+        st = _native.kernels().cml_tree_binize(self.x.data_ptr(), self.n, self.x.stride(0), self.d, thr_t.data_ptr(),
+                                               ms, ns_t.data_ptr(), bins.data_ptr(), _native.stream_ptr())
+        _native.check(st, "tree_binize")
+        return bins
+
+    # -------------------------------------------------------------- histogram / routing
+    def histogram(self, bins, node_of, wt, nodes: int) -> torch.Tensor:
+        T, S, d, nb = self.p.num_trees, self.S, self.d, self.nbins
+        out = torch.zeros((T, nodes, d, nb, S), dtype=torch.float64, device=self.dev)
+        if self.n == 0 or nodes == 0:
+            return out
+        if self.gpu:
+            cls = self.y.to(torch.int32).contiguous() if self.kind != "variance" else None
+            rb = max(1, min((self.n + 255) // 256, 1024 // max(T, 1) + 1))
+            st = _native.kernels().cml_tree_hist(bins.data_ptr(), self.n, d, nb, node_of.data_ptr(), T,
+                                                 wt.data_ptr() if wt is not None else 0, self.y.data_ptr(),
+                                                 cls.data_ptr() if cls is not None else 0, S, nodes, out.data_ptr(),
+                                                 rb, _native.stream_ptr())
+            _native.check(st, "tree_hist")
+            return out
+        flat = out.view(-1)
+        for t in range(T):
+            nd = node_of[t]
+            active = nd >= 0
+            if wt is not None:
+                active = active & (wt[t] > 0)
+            idx_rows = torch.nonzero(active).flatten()
+            if idx_rows.numel() == 0:
+                continue
+            w = wt[t][idx_rows].to(torch.float64) if wt is not None else torch.ones(idx_rows.numel(),
+                                                                                   dtype=torch.float64)
+            nsel = nd[idx_rows].long()
+            b = bins[idx_rows].long()
+            yy = self.y[idx_rows]
+            feat = torch.arange(d, device=self.dev)
+            base = (((t * nodes + nsel)[:, None] * d + feat[None, :]) * nb + b) * S
+            if self.kind == "variance":
+                for s, v in enumerate((w, w * yy, w * yy * yy)):
+                    flat.index_add_(0, (base + s).reshape(-1), v[:, None].expand(-1, d).reshape(-1))
+            else:
+                c = yy.long()
+                flat.index_add_(0, (base + c[:, None]).reshape(-1), w[:, None].expand(-1, d).reshape(-1))
+        return out
+
+    def route(self, bins, node_of, split_feat, split_bin, left_id, right_id, nodes: int) -> None:
+        T = self.p.num_trees
+        if self.n == 0:
+            return
+        sf = torch.as_tensor(split_feat, dtype=torch.int32, device=self.dev).contiguous()
+        sb = torch.as_tensor(split_bin, dtype=torch.int32, device=self.dev).contiguous()
+        li = torch.as_tensor(left_id, dtype=torch.int32, device=self.dev).contiguous()
+        ri = torch.as_tensor(right_id, dtype=torch.int32, device=self.dev).contiguous()
+        if self.gpu:
+            st = _native.kernels().cml_tree_route(bins.data_ptr(), self.n, self.d, T, nodes, node_of.data_ptr(),
+                                                  sf.data_ptr(), sb.data_ptr(), li.data_ptr(), ri.data_ptr(),
+                                                  _native.stream_ptr())
+            _native.check(st, "tree_route")
+            return
+        for t in range(T):
+            nd = node_of[t]
+            act = nd >= 0
+            k = (t * nodes + nd.clamp(min=0)).long()
+            f = sf[k]
+            leaf = f < 0
+            fb = bins.gather(1, f.clamp(min=0).long().reshape(-1, 1)).reshape(-1).to(torch.int32)
+            go_left = fb <= sb[k]
+            new = torch.where(go_left, li[k], ri[k])
+            new = torch.where(leaf, torch.full_like(new, -1), new)
+            node_of[t] = torch.where(act, new, nd)
+
+    # -------------------------------------------------------------- fit
+    def fit(self) -> List[Node]:
+        p = self.p
+        T = p.num_trees
+        splits = self.find_splits()
+        self.splits = splits
+        bins = self.binize(splits)
+        # bagging weights (Spark BaggedPoint: Poisson(rate) with replacement, Bernoulli without)
+        if T > 1 and p.bootstrap:
+            wt = torch.stack([rng.poisson1(self.row_ids, p.seed, 1000 + t).to(torch.float32)
+                              for t in range(T)]) if p.subsampling_rate == 1.0 else torch.stack(
+                [_poisson(self.row_ids, p.seed, 1000 + t, p.subsampling_rate) for t in range(T)])
+        elif p.subsampling_rate < 1.0:
+            wt = torch.stack([(rng.uniform(self.row_ids, p.seed, 1000 + t) < p.subsampling_rate).to(torch.float32)
+                              for t in range(T)])
+        else:
+            wt = None
+        if self.sample_weight is not None:
+            sw = self.sample_weight.to(torch.float32)
+            wt = sw[None, :].repeat(T, 1) if wt is None else wt * sw[None, :]
+        if wt is not None:
+            wt = wt.to(self.dev).contiguous()
+        node_of = torch.zeros((T, self.n), dtype=torch.int32, device=self.dev)
+        k_sub = subset_size(p.feature_subset, self.d, p.task, T)
+        roots = [Node() for _ in range(T)]
+        level_nodes: List[List[Node]] = [[r] for r in roots]
+        rs = np.random.RandomState(p.seed & 0x7FFFFFFF)
+        for depth in range(p.max_depth + 1):
+            nodes = max(len(l) for l in level_nodes)
+            if nodes == 0 or depth == p.max_depth:
+                break  # nodes at maxDepth are leaves; their stats came with the parent's split
+            hist = self.histogram(bins, node_of, wt, nodes)
+            self.comm.allreduce_(hist)
+            h = hist.cpu().numpy()
+            split_feat = np.full((T, nodes), -1, dtype=np.int32)
+            split_bin = np.zeros((T, nodes), dtype=np.int32)
+            left_id = np.full((T, nodes), -1, dtype=np.int32)
+            right_id = np.full((T, nodes), -1, dtype=np.int32)
+            next_level: List[List[Node]] = [[] for _ in range(T)]
+            for t in range(T):
+                for j, node in enumerate(level_nodes[t]):
+                    hh = h[t, j]  # [d, nbins, S]
+                    tot = hh[0].sum(0) if self.d else np.zeros(self.S)
+                    if node.stats is None:
+                        node.stats = tot
+                    node.count = count_of(node.stats, self.kind)
+                    node.impurity = impurity_of(node.stats, self.kind)
+                    node.prediction = predict_of(node.stats, self.kind)
+                    if depth == p.max_depth or node.count <= 0:
+                        continue
+                    feats = np.arange(self.d)
+                    if k_sub < self.d:
+                        feats = np.sort(rs.choice(self.d, k_sub, replace=False))
+                    best = self._best_split(hh, node, feats)
+                    if best is None:
+                        continue
+                    gain, f, b, lstats, rstats = best
+                    node.gain, node.feature, node.split_bin = gain, int(f), int(b)
+                    node.threshold = float(splits[f][b])
+                    node.left = Node(stats=lstats)
+                    node.right = Node(stats=rstats)
+                    for child in (node.left, node.right):
+                        child.count = count_of(child.stats, self.kind)
+                        child.impurity = impurity_of(child.stats, self.kind)
+                        child.prediction = predict_of(child.stats, self.kind)
+                    split_feat[t, j] = f
+                    split_bin[t, j] = b
+                    left_id[t, j] = len(next_level[t])
+                    next_level[t].append(node.left)
+                    right_id[t, j] = len(next_level[t])
+                    next_level[t].append(node.right)
+            if depth < p.max_depth and any(next_level):
+                self.route(bins, node_of, split_feat.reshape(-1), split_bin.reshape(-1), left_id.reshape(-1),
+                           right_id.reshape(-1), nodes)
+            level_nodes = next_level
+            if not any(level_nodes):
+                break
+        for r in roots:
+            _assign_ids(r)
+        return roots
+
+    def _best_split(self, hh: np.ndarray, node: Node, feats: Sequence[int]):
+        p = self.p
+        total = node.stats
+        wtot = count_of(total, self.kind)
+        imp = impurity_of(total, self.kind)
+        best = None
+        min_w = max(p.min_instances, p.min_weight_fraction * wtot)
+        for f in feats:
+            nsp = len(self.splits[f])
+            if nsp == 0:
+                continue
+            cum = np.cumsum(hh[f], axis=0)  # [nbins, S]: bins <= b go left
+            for b in range(nsp):
+                ls = cum[b]
+                rs_ = total - ls
+                wl, wr = count_of(ls, self.kind), count_of(rs_, self.kind)
+                if wl < min_w or wr < min_w or wl <= 0 or wr <= 0:
+                    continue
+                gain = imp - (wl / wtot) * impurity_of(ls, self.kind) - (wr / wtot) * impurity_of(rs_, self.kind)
+                if gain < p.min_info_gain:
+                    continue
+                if best is None or gain > best[0] + 1e-15:
+                    best = (gain, f, b, ls.copy(), rs_.copy())
+        if best is None or best[0] <= 0:
+            return None
+        return best
+
+
+def _poisson(row_ids, seed, stream, lam):
+    u = rng.uniform(row_ids, seed, stream)
+    out = torch.zeros_like(u, dtype=torch.float32)
+    p = math.exp(-lam)
+    cdf = p
+    for k in range(1, 17):
+        out += (u >= cdf).to(torch.float32)
+        p = p * lam / k
+        cdf += p
+    return out
+
+
+def _assign_ids(root: Node) -> None:
+    """Spark NodeData ids: preorder numbering (root 0, then the left subtree, then the right)."""
+    nid = 0
+    stack = [root]
+    while stack:
+        n = stack.pop()
+        n.id = nid
+        nid += 1
+        if not n.is_leaf:
+            stack.append(n.right)
+            stack.append(n.left)
+
+
+def preorder(root: Node) -> List[Node]:
+    out = []
+    stack = [root]
+    while stack:
+        n = stack.pop()
+        out.append(n)
+        if not n.is_leaf:
+            stack.append(n.right)
+            stack.append(n.left)
+    return out
+
+
+def tree_depth(root: Node) -> int:
+    if root.is_leaf:
+        return 0
+    return 1 + max(tree_depth(root.left), tree_depth(root.right))
+
+
+def num_nodes(root: Node) -> int:
+    return len(preorder(root))
+
+
+def feature_importances(trees: List[Node], d: int) -> np.ndarray:
+    """Spark: per tree Σ gain·count over split nodes, normalised; forest = mean, renormalised."""
+    total = np.zeros(d)
+    for t in trees:
+        imp = np.zeros(d)
+        for n in preorder(t):
+            if not n.is_leaf:
+                imp[n.feature] += n.gain * n.count
+        s = imp.sum()
+        if s > 0:
+            imp /= s
+        total += imp
+    if len(trees) > 1:
+        total /= len(trees)
+    s = total.sum()
+    return total / s if s > 0 else total
+
+
+def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: int, average: bool,
+                   normalize_leaves: bool) -> torch.Tensor:
+    """[n, S] per-row accumulated leaf values: regression -> prediction (mean if `average`),
+    classification -> summed class distributions (normalised per tree when `normalize_leaves`)."""
+    S = 1 if kind == "variance" else num_classes
+    feats, thrs, lefts, rights, leaves, roots = [], [], [], [], [], []
+    for t in trees:
+        nodes = preorder(t)
+        base = len(feats)
+        roots.append(base)
+        index = {id(nd): base + i for i, nd in enumerate(nodes)}
+        for nd in nodes:
+            feats.append(nd.feature if not nd.is_leaf else -1)
+            thrs.append(nd.threshold)
+            lefts.append(index[id(nd.left)] if not nd.is_leaf else -1)
+            rights.append(index[id(nd.right)] if not nd.is_leaf else -1)
+            if kind == "variance":
+                leaves.append([nd.prediction])
+            else:
+                st = np.asarray(nd.stats, dtype=np.float64)
+                if normalize_leaves:
+                    s = st.sum()
+                    st = st / s if s > 0 else st
+                leaves.append(list(st))
+    dev = x.device
+    n = x.shape[0]
+    xx = x.to(torch.float64).contiguous()
+    out = torch.zeros((n, S), dtype=torch.float64, device=dev)
+    if n == 0:
+        return out
+    if x.is_cuda and S <= 16:
+        to = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt, device=dev).contiguous()  # noqa: E731
+        r, f, th, l, rr, lv = (to(roots, torch.int32), to(feats, torch.int32), to(thrs, torch.float64),
+                               to(lefts, torch.int32), to(rights, torch.int32),
+                               to(np.asarray(leaves, dtype=np.float64).reshape(-1), torch.float64))
+        st = _native.kernels().cml_tree_predict(xx.data_ptr(), n, xx.stride(0), len(trees), r.data_ptr(),
+                                                f.data_ptr(), th.data_ptr(), l.data_ptr(), rr.data_ptr(),
+                                                lv.data_ptr(), S, out.data_ptr(), _native.stream_ptr())
+        _native.check(st, "tree_predict")
+    else:
+        f = torch.as_tensor(feats, dtype=torch.long, device=dev)
+        th = torch.as_tensor(thrs, dtype=torch.float64, device=dev)
+        l = torch.as_tensor(lefts, dtype=torch.long, device=dev)
+        rr = torch.as_tensor(rights, dtype=torch.long, device=dev)
+        lv = torch.as_tensor(np.asarray(leaves, dtype=np.float64), device=dev)
+        for root in roots:
+            k = torch.full((n,), root, dtype=torch.long, device=dev)
+            for _ in range(64):
+                ff = f[k]
+                inner = ff >= 0
+                if not bool(inner.any()):
+                    break
+                v = xx.gather(1, ff.clamp(min=0).reshape(-1, 1)).reshape(-1)
+                nxt = torch.where(v <= th[k], l[k], rr[k])
+                k = torch.where(inner, nxt, k)
+            out += lv[k]
+    if average and len(trees) > 1:
+        out /= len(trees)
+    return out

@@ -1,0 +1,170 @@
+"""Bindings of the GLM / feature-statistics kernels (K7, K8, K13, K15, K24 in glm.hip).
+
+GPU tensors run the gfx950 kernels (no fallback); CPU tensors run torch float64
+reference code with identical semantics.  All functions work on a rank-local
+shard and return *partial* statistics; callers all-reduce them.
+"""
+from __future__ import annotations
+
+from typing import Optional, Tuple
+
+import torch
+
+from .. import _native
+from .._native import c_int, c_ll, c_vp
+from ..utils.device import num_cus
+
+_native.register_kernel_sigs({
+    "cml_glm_grid": (c_int, [c_ll, c_int, c_int, c_int]),
+    "cml_col_moments": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
+    "cml_scale_apply": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_vp]),
+    "cml_logreg_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_linear_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
+    "cml_gram": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+})
+
+_CODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
+
+
+def _prep(x: torch.Tensor) -> torch.Tensor:
+    """Row-major with a 16-byte multiple row pitch (vector loads), supported dtype."""
+    if x.dtype not in _CODE:
+        x = x.to(torch.float64)
+    if x.dim() == 1:
+        x = x[:, None]
+    if x.stride(1) != 1 or (x.stride(0) * x.element_size()) % 16 != 0 or x.data_ptr() % 16 != 0:
+        per = 16 // x.element_size()
+        ld = (x.shape[1] + per - 1) // per * per
+        buf = torch.zeros((x.shape[0], ld), dtype=x.dtype, device=x.device)
+        buf[:, : x.shape[1]] = x
+        x = buf
+    return x
+
+
+def _grid(n: int, d: int, code: int, dev) -> int:
+    g = _native.kernels().cml_glm_grid(n, d, code, num_cus(dev.index or 0) * 4)
+    if g < 0:
+        raise ValueError(f"feature width {d} too large for the GLM kernels")
+    return g
+
+
+def moments(x: torch.Tensor, d: Optional[int] = None) -> Tuple[int, torch.Tensor, torch.Tensor]:
+    """Local (count, shifted Σ, shifted Σ², shift) with shift = first row — merge with all-reduce."""
+    d = x.shape[1] if d is None else d
+    n = x.shape[0]
+    if n == 0:
+        z = torch.zeros(d, dtype=torch.float64, device=x.device)
+        return 0, z, z.clone(), z.clone()
+    shift = x[0, :d].to(torch.float64).contiguous()
+    if not x.is_cuda:
+        xs = x[:, :d].to(torch.float64) - shift
+        return n, xs.sum(0), (xs * xs).sum(0), shift
+    xx = _prep(x)
+    code = _CODE[xx.dtype]
+    g = _grid(n, d, code, xx.device)
+    out = torch.empty((g, 2, d), dtype=torch.float64, device=xx.device)
+    st = _native.kernels().cml_col_moments(xx.data_ptr(), n, xx.stride(0), d, code, shift.data_ptr(), out.data_ptr(),
+                                           g, _native.stream_ptr())
+    _native.check(st, "col_moments")
+    s = out.sum(0)
+    return n, s[0], s[1], shift
+
+
+def scale_apply(x: torch.Tensor, d: int, mean: torch.Tensor, inv_std: torch.Tensor, with_mean: bool,
+                out_dtype=torch.float64, out_width: Optional[int] = None) -> torch.Tensor:
+    n = x.shape[0]
+    width = d if out_width is None else out_width
+    if not x.is_cuda:
+        y = x[:, :d].to(torch.float64)
+        if with_mean:
+            y = y - mean
+        y = y * inv_std
+        if width > d:
+            y = torch.nn.functional.pad(y, (0, width - d))
+        return y.to(out_dtype)
+    xx = x if x.dtype in _CODE else x.to(torch.float64)
+    if xx.stride(1) != 1:
+        xx = xx.contiguous()
+    out = torch.empty((n, width), dtype=out_dtype, device=x.device)
+    if n == 0:
+        return out
+    st = _native.kernels().cml_scale_apply(xx.data_ptr(), n, xx.stride(0), d, _CODE[xx.dtype],
+                                           mean.to(torch.float64).contiguous().data_ptr(),
+                                           inv_std.to(torch.float64).contiguous().data_ptr(), int(with_mean),
+                                           out.data_ptr(), out.stride(0), width, _CODE[out_dtype],
+                                           _native.stream_ptr())
+    _native.check(st, "scale_apply")
+    return out
+
+
+def logreg_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
+                weight: Optional[torch.Tensor] = None):
+    """Binomial logistic loss + gradient over the local shard.
+
+    coef = [w (d) | b] in the ORIGINAL feature space.  Returns a float64 tensor
+    [grad_w (d) | grad_b | loss | weight_sum] (sums, not means).
+    """
+    n = x.shape[0]
+    coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    if not x.is_cuda or n == 0:
+        xf = x[:, :d].to(torch.float64)
+        m = xf @ coef[:d] + coef[d]
+        yy = y.to(torch.float64)
+        ww = torch.ones_like(yy) if weight is None else weight.to(torch.float64)
+        p = torch.sigmoid(m)
+        r = ww * (p - yy)
+        loss = (ww * (torch.nn.functional.softplus(m) - yy * m)).sum()
+        return torch.cat([xf.T @ r, r.sum().reshape(1), loss.reshape(1), ww.sum().reshape(1)])
+    xx = _prep(x)
+    code = _CODE[xx.dtype]
+    g = _grid(n, d, code, xx.device)
+    out = torch.empty((g, d + 3), dtype=torch.float64, device=xx.device)
+    yy = y.to(torch.float64).contiguous()
+    ww = weight.to(torch.float64).contiguous() if weight is not None else None
+    st = _native.kernels().cml_logreg_grad(xx.data_ptr(), n, xx.stride(0), d, code, yy.data_ptr(),
+                                           ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
+                                           g, _native.stream_ptr())
+    _native.check(st, "logreg_grad")
+    return out.sum(0)
+
+
+def linear_predict(x: torch.Tensor, d: int, coef: torch.Tensor, link: str = "identity") -> torch.Tensor:
+    n = x.shape[0]
+    coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    if not x.is_cuda or n == 0:
+        m = x[:, :d].to(torch.float64) @ coef[:d] + coef[d]
+        return torch.sigmoid(m) if link == "logistic" else m
+    xx = _prep(x)
+    code = _CODE[xx.dtype]
+    g = _grid(n, d, code, xx.device)
+    out = torch.empty(n, dtype=torch.float64, device=xx.device)
+    st = _native.kernels().cml_linear_predict(xx.data_ptr(), n, xx.stride(0), d, code, coef.data_ptr(),
+                                              1 if link == "logistic" else 0, out.data_ptr(), g,
+                                              _native.stream_ptr())
+    _native.check(st, "linear_predict")
+    return out
+
+
+def gram(x: torch.Tensor, d: int, y: torch.Tensor, weight: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[X 1 y]ᵀ W [X 1 y] (float64, (d+2)×(d+2), symmetric) of the local shard."""
+    n = x.shape[0]
+    m = d + 2
+    if (not x.is_cuda) or d > 30 or n == 0:
+        a = torch.cat([x[:, :d].to(torch.float64), torch.ones((n, 1), dtype=torch.float64, device=x.device),
+                       y.to(torch.float64).reshape(-1, 1)], 1)
+        if weight is not None:
+            a = a * weight.to(torch.float64).sqrt().reshape(-1, 1)
+        return a.T @ a
+    xx = x if x.dtype in _CODE else x.to(torch.float64)
+    if xx.stride(1) != 1:
+        xx = xx.contiguous()
+    grid = max(1, min((n + 4095) // 4096, num_cus(xx.device.index or 0) * 2))
+    out = torch.zeros((grid, m * m), dtype=torch.float64, device=xx.device)
+    yy = y.to(torch.float64).contiguous()
+    ww = weight.to(torch.float64).contiguous() if weight is not None else None
+    st = _native.kernels().cml_gram(xx.data_ptr(), n, xx.stride(0), d, _CODE[xx.dtype], yy.data_ptr(),
+                                    ww.data_ptr() if ww is not None else 0, out.data_ptr(), grid,
+                                    _native.stream_ptr())
+    _native.check(st, "gram")
+    g = out.sum(0).reshape(m, m)
+    return torch.triu(g) + torch.triu(g, 1).T

@@ -578,6 +578,13 @@ class DataFrame:
         print(f"== Physical Plan ==\n{kind}Scan [{', '.join(self.columns)}] on {self._device} "
               f"(rank {self._comm.rank}/{self._comm.world_size})")
 
+    def _apply_transformer(self, model) -> "DataFrame":
+        """Used to replay ``model.transform`` on each micro-batch of a streaming frame."""
+        return model.transform(self)
+
+    def transform(self, func, *args, **kwargs) -> "DataFrame":
+        return func(self, *args, **kwargs)
+
     # ------------------------------------------------------------------------------------------ device helpers
     def _feature_matrix(self, col: str) -> torch.Tensor:
         """The [n, d] tensor of a vector column (row-major, device-resident)."""
