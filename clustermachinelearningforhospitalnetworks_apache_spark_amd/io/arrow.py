@@ -141,7 +141,7 @@ def arrow_column_to_data(arr, dt: T.DataType, device) -> ColumnData:
         np_arr = arr.fill_null(False).to_numpy(zero_copy_only=False).astype(bool)
     else:
         np_arr = arr.fill_null(0).to_numpy(zero_copy_only=False)
-    t = torch.as_tensor(np.ascontiguousarray(np_arr)).to(device=device, dtype=dt.torch_dtype)
+    t = torch.as_tensor(np.array(np_arr, copy=True)).to(device=device, dtype=dt.torch_dtype)
     return ColumnData(t, None if valid_np is None else torch.as_tensor(valid_np, device=device), dt)
 
 

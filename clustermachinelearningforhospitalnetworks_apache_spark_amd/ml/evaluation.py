@@ -211,12 +211,12 @@ class BinaryClassificationEvaluator(Evaluator):
                 return float("nan")
             tpr = np.r_[0.0, ctp / P]
             fpr = np.r_[0.0, cfp / N]
-            return float(np.trapz(tpr, fpr))
+            return float(np.trapezoid(tpr, fpr))
         if P == 0:
             return float("nan")
         rec = np.r_[0.0, ctp / P]
         prec = np.r_[1.0, ctp / np.maximum(ctp + cfp, 1e-300)]
-        return float(np.trapz(prec, rec))
+        return float(np.trapezoid(prec, rec))
 
 
 class ClusteringEvaluator(Evaluator):

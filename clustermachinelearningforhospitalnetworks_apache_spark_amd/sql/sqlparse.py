@@ -439,18 +439,24 @@ def _run(session, sel: Select):
             exprs += [ColRef(n) for n in df.columns]
         else:
             exprs.append(Alias(e, alias) if alias else e)
+    ordered = False
     if sel.group_by or any(x.is_aggregate() for x in exprs):
         from .group import aggregate
-        having_aggs = []
         out = aggregate(df, sel.group_by, exprs)
         if sel.having is not None:
             out = out.filter(Column(_rewrite_aggs(sel.having, exprs)))
         df = out
     else:
+        out_names = {x.name() for x in exprs}
+        if sel.order_by and not sel.distinct and any(
+                r not in out_names for o in sel.order_by for r in o.expr.refs()):
+            # ORDER BY a source column that is not projected: sort first, then project
+            df = df.orderBy(*sel.order_by)
+            ordered = True
         df = df.select(*[Column(x) for x in exprs])
     if sel.distinct:
         df = df.distinct()
-    if sel.order_by:
+    if sel.order_by and not ordered:
         df = df.orderBy(*[SortOrder(_rewrite_aggs(o.expr, exprs), o.ascending, o.nulls_first)
                           for o in sel.order_by])
     if sel.limit is not None:
