@@ -1,0 +1,110 @@
+"""Distributed correctness without GPUs: the same SPMD code on W gloo ranks must match
+W=1 (row ids, counter-based randomness and fixed-order reductions make it GPU-count
+invariant). Mirrors the RCCL path: only the backend differs."""
+import json
+import os
+import socket
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch.multiprocessing as mp
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    p = s.getsockname()[1]
+    s.close()
+    return p
+
+
+def _workload(out_path, rank):
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegression
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.evaluation import RegressionEvaluator
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import StandardScaler, VectorAssembler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import (DecisionTreeRegressor,
+                                                                                            LinearRegression,
+                                                                                            RandomForestRegressor)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    rs = np.random.RandomState(0)
+    n = 3001
+    X = rs.randn(n, 4) * [1, 2, 3, 4] + [0, 1, 2, 3]
+    y = X @ [0.5, -1, 0.25, 2] + 1 + rs.randn(n) * 0.3
+    pdf = pd.DataFrame(X, columns=list("abcd"))
+    pdf["y"] = y
+    pdf["g"] = [f"k{i % 5}" for i in range(n)]
+    df = spark.createDataFrame(pdf)
+    f = VectorAssembler(inputCols=list("abcd"), outputCol="features").transform(df)
+    tr, te = f.randomSplit([0.7, 0.3], seed=42)
+    res = {"world": spark.world_size, "count": f.count(), "train": tr.count(),
+           "train_ids": sorted(int(r.a * 1e9) for r in tr.select("a").collect())[:50]}
+    lr = LinearRegression(featuresCol="features", labelCol="y").fit(tr)
+    res["lr"] = lr.coefficients.toArray().tolist() + [lr.intercept]
+    res["rmse"] = RegressionEvaluator(labelCol="y").evaluate(lr.transform(te))
+    sc = StandardScaler(inputCol="features", outputCol="s", withMean=True).fit(f)
+    res["std"] = sc.std.toArray().tolist()
+    dt = DecisionTreeRegressor(featuresCol="features", labelCol="y").fit(tr)
+    res["dt_imp"] = dt.featureImportances.toArray().tolist()
+    res["dt_nodes"] = dt.numNodes
+    rf = RandomForestRegressor(featuresCol="features", labelCol="y", numTrees=4).fit(tr)
+    res["rf_imp"] = rf.featureImportances.toArray().tolist()
+    km = KMeans(k=3, seed=5, maxIter=10).fit(f)
+    res["km"] = np.stack(km.clusterCenters()).tolist()
+    res["km_cost"] = km.summary.trainingCost
+    lab = f.withColumn("label", F.when(F.col("y") > 1.0, 1).otherwise(0))
+    lg = LogisticRegression(maxIter=50).fit(lab)
+    res["logreg"] = lg.coefficients.toArray().tolist() + [lg.intercept]
+    g = spark.createDataFrame(pdf).groupBy("g").agg(F.sum("y").alias("s")).orderBy("g").collect()
+    res["groupby"] = [(r.g, r.s) for r in g]
+    res["sql"] = spark.createDataFrame(pdf).filter("a > 0 AND b < 2").count()
+    if rank == 0:
+        with open(out_path, "w") as fh:
+            json.dump(res, fh)
+    spark.stop()
+
+
+def _rank_main(rank, world, port, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "CML_FORCE_CPU": "1"})
+    import torch
+    torch.set_num_threads(1)
+    _workload(out_path, rank)
+
+
+def _run(world, tmp_path):
+    out = str(tmp_path / f"res_w{world}.json")
+    if world == 1:
+        for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
+            os.environ.pop(k, None)
+        _workload(out, 0)
+    else:
+        mp.start_processes(_rank_main, args=(world, _free_port(), out), nprocs=world, join=True,
+                           start_method="spawn")
+    with open(out) as fh:
+        return json.load(fh)
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spmd_results_invariant_to_world_size(tmp_path, world):
+    r1 = _run(1, tmp_path)
+    rw = _run(world, tmp_path)
+    assert rw["world"] == world and r1["world"] == 1
+    assert rw["count"] == r1["count"] and rw["train"] == r1["train"]
+    assert rw["train_ids"] == r1["train_ids"]
+    np.testing.assert_allclose(rw["lr"], r1["lr"], rtol=1e-9, atol=1e-11)
+    assert abs(rw["rmse"] - r1["rmse"]) < 1e-9
+    np.testing.assert_allclose(rw["std"], r1["std"], rtol=1e-10)
+    np.testing.assert_allclose(rw["dt_imp"], r1["dt_imp"], rtol=1e-9, atol=1e-12)
+    assert rw["dt_nodes"] == r1["dt_nodes"]
+    np.testing.assert_allclose(rw["rf_imp"], r1["rf_imp"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rw["km"], r1["km"], rtol=1e-9, atol=1e-9)
+    assert abs(rw["km_cost"] - r1["km_cost"]) < 1e-6 * r1["km_cost"]
+    np.testing.assert_allclose(rw["logreg"], r1["logreg"], rtol=1e-6, atol=1e-8)
+    assert [g for g, _ in rw["groupby"]] == [g for g, _ in r1["groupby"]]
+    np.testing.assert_allclose([s for _, s in rw["groupby"]], [s for _, s in r1["groupby"]], rtol=1e-12)
+    assert rw["sql"] == r1["sql"]

@@ -1,0 +1,91 @@
+"""GPU numerics of the GLM (K7/K8/K13/K15/K24) and tree (K17/K18/K20/K21) kernels vs the
+float64 torch references of the same ops (the CPU code paths)."""
+import numpy as np
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.models import trees as TR
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import glm_ops
+
+pytestmark = pytest.mark.gpu
+DT = [torch.float64, torch.float32, torch.bfloat16]
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,d", [(1000, 4), (5000, 37), (20000, 256), (3000, 600), (7, 1)])
+def test_moments_and_scale(dtype, n, d):
+    torch.manual_seed(0)
+    x = (torch.randn(n, d, dtype=torch.float64) * 3 + 5).to(dtype)
+    xc, xg = x, x.cuda()
+    nc, s1c, s2c, shc = glm_ops.moments(xc, d)
+    ng, s1g, s2g, shg = glm_ops.moments(xg, d)
+    assert nc == ng
+    tol = 1e-9 if dtype == torch.float64 else 1e-6
+    np.testing.assert_allclose(s1g.cpu().numpy(), s1c.numpy(), rtol=tol, atol=tol * n * 10)
+    np.testing.assert_allclose(s2g.cpu().numpy(), s2c.numpy(), rtol=tol, atol=tol * n * 10)
+    mean = torch.randn(d, dtype=torch.float64)
+    inv = torch.rand(d, dtype=torch.float64) + 0.5
+    for od in DT:
+        yc = glm_ops.scale_apply(xc, d, mean, inv, True, od)
+        yg = glm_ops.scale_apply(xg, d, mean.cuda(), inv.cuda(), True, od)
+        np.testing.assert_allclose(yg.cpu().double().numpy(), yc.double().numpy(),
+                                   rtol=1e-2 if od == torch.bfloat16 else 1e-6, atol=1e-2)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,d", [(1000, 4), (4097, 31), (20000, 256), (3000, 513)])
+def test_logreg_grad_and_predict(dtype, n, d):
+    torch.manual_seed(1)
+    x = torch.randn(n, d, dtype=torch.float64).to(dtype)
+    y = (torch.rand(n) > 0.5).double()
+    w = torch.rand(n, dtype=torch.float64) + 0.5
+    coef = torch.randn(d + 1, dtype=torch.float64) * 0.1
+    for wt in (None, w):
+        oc = glm_ops.logreg_grad(x, d, y, coef, wt)
+        og = glm_ops.logreg_grad(x.cuda(), d, y.cuda(), coef.cuda(), None if wt is None else wt.cuda())
+        np.testing.assert_allclose(og.cpu().numpy(), oc.numpy(), rtol=1e-8, atol=1e-8 * n)
+    for link in ("identity", "logistic"):
+        pc = glm_ops.linear_predict(x, d, coef, link)
+        pg = glm_ops.linear_predict(x.cuda(), d, coef.cuda(), link)
+        np.testing.assert_allclose(pg.cpu().numpy(), pc.numpy(), rtol=1e-9, atol=1e-9)
+
+
+@pytest.mark.parametrize("dtype", DT)
+@pytest.mark.parametrize("n,d", [(1000, 4), (50000, 12), (3000, 30)])
+def test_gram(dtype, n, d):
+    torch.manual_seed(2)
+    x = torch.randn(n, d, dtype=torch.float64).to(dtype)
+    y = torch.randn(n, dtype=torch.float64)
+    w = torch.rand(n, dtype=torch.float64)
+    for wt in (None, w):
+        gc = glm_ops.gram(x, d, y, wt)
+        gg = glm_ops.gram(x.cuda(), d, y.cuda(), None if wt is None else wt.cuda())
+        np.testing.assert_allclose(gg.cpu().numpy(), gc.numpy(), rtol=1e-10, atol=1e-8)
+
+
+@pytest.mark.parametrize("task", ["regression", "classification"])
+@pytest.mark.parametrize("trees", [1, 7])
+def test_forest_gpu_matches_cpu(task, trees):
+    torch.manual_seed(3)
+    n, d = 6000, 6
+    x = torch.randn(n, d, dtype=torch.float64)
+    if task == "regression":
+        y = x[:, 0] * 2 + (x[:, 1] > 0).double() + torch.randn(n, dtype=torch.float64) * 0.1
+        imp = "variance"
+    else:
+        y = ((x[:, 0] + x[:, 2] * 0.5) > 0).double() + (x[:, 3] > 1).double()
+        imp = "gini"
+    p = TR.TreeParams(task=task, num_classes=3, impurity=imp, num_trees=trees, seed=11,
+                      feature_subset="auto")
+    cpu = TR.ForestEngine(x, y, p).fit()
+    gpu = TR.ForestEngine(x.cuda(), y.cuda(), p).fit()
+    for a, b in zip(cpu, gpu):
+        na, nb = TR.preorder(a), TR.preorder(b)
+        assert len(na) == len(nb)
+        for u, v in zip(na, nb):
+            assert u.feature == v.feature and u.split_bin == v.split_bin
+            np.testing.assert_allclose(u.stats, v.stats, rtol=1e-5, atol=1e-3)
+    kind = imp
+    pc = TR.predict_forest(cpu, x, kind, 3, average=True, normalize_leaves=trees > 1)
+    pg = TR.predict_forest(gpu, x.cuda(), kind, 3, average=True, normalize_leaves=trees > 1)
+    np.testing.assert_allclose(pg.cpu().numpy(), pc.numpy(), rtol=1e-4, atol=1e-4)
