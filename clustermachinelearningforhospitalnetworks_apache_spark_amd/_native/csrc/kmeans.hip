@@ -37,123 +37,272 @@
 //   that is all-reduced over RCCL.
 // K11 kmeans_update: new centres (empty clusters keep their old centre, as Spark
 //     MLlib does), bf16 copy, norms of the bf16 centres, per-centre squared shift.
+#include <algorithm>
+
 #include "common.h"
 
 namespace {
 
-constexpr int kAssignThreads = 512;  // 8 waves: 2 per SIMD
 constexpr int kAccumThreads = 1024;  // 16 waves
 constexpr int kSegThreads = 256;     // 4 waves
 
-template <int DS>
-__device__ __forceinline__ int c_phys(int row, int c16) {
-  constexpr int NCH = 2 * DS;
-  constexpr int MASK = NCH >= 16 ? 15 : NCH - 1;
-  return (c16 & ~MASK) | ((c16 & MASK) ^ (row & MASK));
+// ---------------------------------------------------------------------------------------------
+// K9 on v_mfma_f32_16x16x32_bf16. Operand layout (wave64): lane l holds A row (l&15) /
+// B column (l&15), k = 8(l>>4) + j; the 16x16 f32 result puts column (l&15) on the lane and
+// rows 4(l>>4)+i, i<4, in its 4 registers. X is the B operand (row of X on the lane), the
+// -2-scaled centres the A operand. Why 16x16x32 and not 32x32x16: the B operand of a 32-wide
+// MFMA forces every global load to touch 32 rows x 32 B (measured 3.5 TB/s ceiling on MI355X),
+// the 16-wide one 16 rows x 64 B (6.0 TB/s) — the assign pass is HBM-bound, so the load shape
+// decides. It also runs ~1.1x the FLOP/s of the 32-wide form.
+// ---------------------------------------------------------------------------------------------
+template <int DP>
+struct AssignShape {
+  static constexpr int NCH = DP / 8;                 // 16-byte chunks per row
+  static constexpr int KS = DP >= 32 ? DP / 32 : 1;  // MFMA k-steps per 16x16 block
+};
+
+// X fragments of one 16-row sub-tile: lane (row l&15, group g=l>>4) reads chunk 4s+g of its row,
+// so each load instruction covers 16 rows x 64 contiguous bytes.
+template <int DP>
+__device__ __forceinline__ void load_x16(const u16* __restrict__ X, long long n, long long ldx, long long row0,
+                                         int r, int g, bf16x8 (&xf)[AssignShape<DP>::KS]) {
+  constexpr int NCH = AssignShape<DP>::NCH;
+  const long long row = row0 + r;
+  const bool valid = row < n;
+  const u16* xp = X + (valid ? row : 0) * ldx;
+#pragma unroll
+  for (int s = 0; s < AssignShape<DP>::KS; ++s) {
+    const int q = 4 * s + g;
+    u32x4 v = {0u, 0u, 0u, 0u};
+    if (q < NCH && valid) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xp + 8 * q));
+    xf[s] = __builtin_bit_cast(bf16x8, v);
+  }
 }
 
-template <int DS>
-__global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_bf16(
-    const u16* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
-    int kc, int kp, int c_base, const float* __restrict__ cnorm, int* __restrict__ labels,
-    float* __restrict__ best_io, int first, int last, double* __restrict__ cost_part,
-    int* __restrict__ hist_out, int* __restrict__ rank_out) {
-  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  constexpr int NCH = 2 * DS;
-  uint4* cl = reinterpret_cast<uint4*>(smem);
-  float* cn = reinterpret_cast<float*>(smem + (size_t)kc * NCH * 16);
-  int* hist = reinterpret_cast<int*>(cn + kc);
-  double* red = reinterpret_cast<double*>(hist + ((kp + 3) & ~3));
+template <int DP, int RT>
+struct XTile {
+  bf16x8 f[RT][AssignShape<DP>::KS];
+};
 
-  const int tid = threadIdx.x;
-  for (int id = tid; id < kc * NCH; id += blockDim.x) {
-    const int row = id / NCH, c16 = id - row * NCH;
-    const uint4 v = *reinterpret_cast<const uint4*>(C + (long long)row * ldc + c16 * 8);
-    cl[row * NCH + c_phys<DS>(row, c16)] = v;
+template <int DP, int RT>
+__device__ __forceinline__ void load_xtile(const u16* __restrict__ X, long long n, long long ldx, long long tile,
+                                           int r, int g, XTile<DP, RT>& xt) {
+#pragma unroll
+  for (int t = 0; t < RT; ++t) load_x16<DP>(X, n, ldx, tile * (16 * RT) + 16 * t, r, g, xt.f[t]);
+}
+
+// Centres live in LDS in FRAGMENT order: fragment (ct, s) is 64 lanes x 16 B contiguous, lane l
+// holding -2·c[16ct + (l&15)][k = 32s + 8(l>>4) .. +8) (zero past Dp). A lane's read address is
+// therefore lane·16 + (ct·KS + s)·1 KiB: conflict-free for ds_read_b128 (16 distinct 16-B bank
+// slots per lane group), the s part folds into the instruction's immediate offset and the ct
+// part is one add per centre tile — no per-read address arithmetic.
+struct AssignCtx {
+  const unsigned char* frag;  // this lane's byte address of fragment (0, 0)
+  const float* cn;            // ||c||² of the chunk's centres
+  int nct;                    // 16-centre tiles
+  int cmask;                  // low key bits holding the tile index
+};
+
+template <int DP>
+__device__ __forceinline__ uint4 frag_at(const AssignCtx& cx, int ct, int s) {
+  ct = ct < cx.nct ? ct : cx.nct - 1;  // ring run-ahead past the last tile: harmless re-read
+  return *reinterpret_cast<const uint4*>(cx.frag + ((ct * AssignShape<DP>::KS + s) << 10));
+}
+
+// Running minimum per (sub-tile, accumulator slot) as ONE signed int key: the f32 distance bits
+// with the low `cmask` bits replaced by the centre-tile index. Distances are >= 0 up to rounding;
+// a rounding-negative one keys below every positive distance (it IS the near-zero minimum), and
+// non-negative f32 order equals int order, so v_and_or + v_min_i32 (2 VALU) replace a compare
+// and two selects. The tile index in the low bits makes ties resolve to the earliest tile; the
+// truncation costs 2^-(23-bits) relative precision (bits = log2 #tiles, 4 for k = 256).
+template <int RT>
+__device__ __forceinline__ void slot_update(const f32x4 (&acc)[RT], int t, int i, int ct, int cmask,
+                                            int (&key)[RT][4]) {
+  const int k = (__float_as_int(acc[t][i]) & ~cmask) | ct;
+  key[t][i] = k < key[t][i] ? k : key[t][i];
+}
+
+// MFMA chain of centre tile `ct` for all RT sub-tiles into `acc` (each A fragment feeds RT
+// MFMAs; the accumulators start at ||c||² + ||x||², so they end as squared distances), with the
+// slot updates of the previous tile's accumulators interleaved.
+template <int DP, int RT, int RING, bool PREV>
+__device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& xt, const float (&xn)[RT], int ct,
+                                      int g, f32x4 (&acc)[RT], const f32x4 (&prev)[RT], uint4 (&ring)[RING],
+                                      int (&key)[RT][4]) {
+  constexpr int KS = AssignShape<DP>::KS;
+  constexpr int NSLOT = RT * 4;
+  const float4 c4 = *reinterpret_cast<const float4*>(cx.cn + ct * 16 + 4 * g);
+#pragma unroll
+  for (int t = 0; t < RT; ++t) acc[t] = f32x4{c4.x + xn[t], c4.y + xn[t], c4.z + xn[t], c4.w + xn[t]};
+#pragma unroll
+  for (int s = 0; s < KS; ++s) {
+    const uint4 a = ring[s % RING];
+    ring[s % RING] = frag_at<DP>(cx, ct + (s + RING) / KS, (s + RING) % KS);
+#pragma unroll
+    for (int t = 0; t < RT; ++t)
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), xt.f[t][s], acc[t], 0, 0, 0);
+    if constexpr (PREV) {
+#pragma unroll
+      for (int q = (s * NSLOT) / KS; q < ((s + 1) * NSLOT) / KS; ++q)
+        slot_update<RT>(prev, q >> 2, q & 3, ct - 1, cx.cmask, key);
+    }
   }
-  for (int i = tid; i < kc; i += blockDim.x) cn[i] = cnorm[i];
-  const bool ranking = last && rank_out != nullptr;
-  if (ranking)
-    for (int i = tid; i < kp; i += blockDim.x) hist[i] = 0;
-  __syncthreads();
+}
 
-  const int lane = tid & 63, wave = tid >> 6, nwaves = blockDim.x >> 6;
-  const int r = lane & 31, h = lane >> 5;
-  const long long ntiles = (n + 31) >> 5;
-  const long long tw = (long long)gridDim.x * nwaves;
-  double cost = 0.0;
-
-  int aoff[DS];
+template <int DP, int RT, int RINGMAX>
+__device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP, RT>& xt, long long tile,
+                                            long long n, int r, int g, int c_base, const float* __restrict__ xnorm,
+                                            int* __restrict__ labels, float* __restrict__ best_io, int first,
+                                            int last, bool ranking, int* hist, int* __restrict__ rank_out,
+                                            double& cost) {
+  constexpr int KS = AssignShape<DP>::KS;
+  constexpr int RING = KS < RINGMAX ? KS : RINGMAX;
+  float xn[RT];
 #pragma unroll
-  for (int s = 0; s < DS; ++s) aoff[s] = r * NCH + c_phys<DS>(r, 2 * s + h);
-
-  for (long long tile = (long long)blockIdx.x * nwaves + wave; tile < ntiles; tile += tw) {
-    const long long row = tile * 32 + r;
-    const bool valid = row < n;
-    const u16* xp = X + (valid ? row : 0) * ldx + 8 * h;
-    bf16x8 xf[DS];
+  for (int t = 0; t < RT; ++t) {
+    const long long row = tile * (16 * RT) + 16 * t + r;
+    xn[t] = row < n ? xnorm[row] : 0.f;
+  }
+  int key[RT][4];
 #pragma unroll
-    for (int s = 0; s < DS; ++s) {
-      uint4 v = *reinterpret_cast<const uint4*>(xp + 16 * s);
-      if (!valid) v = make_uint4(0, 0, 0, 0);
-      xf[s] = __builtin_bit_cast(bf16x8, v);
+  for (int t = 0; t < RT; ++t)
+#pragma unroll
+    for (int i = 0; i < 4; ++i) key[t][i] = 0x7fffffff;
+  uint4 ring[RING];
+#pragma unroll
+  for (int q = 0; q < RING; ++q) ring[q] = frag_at<DP>(cx, q / KS, q % KS);
+  f32x4 acc0[RT], acc1[RT];
+  const int nct = cx.nct;
+  chain<DP, RT, RING, false>(cx, xt, xn, 0, g, acc0, acc1, ring, key);
+  int ct = 1;
+  for (; ct + 1 < nct; ct += 2) {
+    chain<DP, RT, RING, true>(cx, xt, xn, ct, g, acc1, acc0, ring, key);
+    chain<DP, RT, RING, true>(cx, xt, xn, ct + 1, g, acc0, acc1, ring, key);
+  }
+  if (ct < nct) {
+    chain<DP, RT, RING, true>(cx, xt, xn, ct, g, acc1, acc0, ring, key);
+#pragma unroll
+    for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc1, q >> 2, q & 3, ct, cx.cmask, key);
+  } else {
+#pragma unroll
+    for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc0, q >> 2, q & 3, ct - 1, cx.cmask, key);
+  }
+#pragma unroll
+  for (int t = 0; t < RT; ++t) {
+    // slot (t,i) holding tile c is centre 16c + 4g + i
+    float best = __int_as_float(key[t][0] & ~cx.cmask);
+    int bidx = (key[t][0] & cx.cmask) * 16 + 4 * g;
+#pragma unroll
+    for (int i = 1; i < 4; ++i) {
+      const float v = __int_as_float(key[t][i] & ~cx.cmask);
+      const int idx = (key[t][i] & cx.cmask) * 16 + 4 * g + i;
+      if (v < best || (v == best && idx < bidx)) { best = v; bidx = idx; }
     }
-    float best = __builtin_huge_valf();
-    int bidx = 0;
-    for (int ct = 0; ct < (kc >> 5); ++ct) {
-      f32x16 acc = {};
-      const uint4* cb = cl + ct * 32 * NCH;
 #pragma unroll
-      for (int s = 0; s < DS; ++s) {
-        const uint4 av = cb[aoff[s]];
-        acc = __builtin_amdgcn_mfma_f32_32x32x16_bf16(__builtin_bit_cast(bf16x8, av), xf[s], acc, 0, 0, 0);
-      }
-#pragma unroll
-      for (int g = 0; g < 4; ++g) {
-        const int i0 = ct * 32 + 8 * g + 4 * h;
-        const float4 c4 = *reinterpret_cast<const float4*>(cn + i0);
-        const float s0 = fmaf(-2.f, acc[4 * g + 0], c4.x);
-        const float s1 = fmaf(-2.f, acc[4 * g + 1], c4.y);
-        const float s2 = fmaf(-2.f, acc[4 * g + 2], c4.z);
-        const float s3 = fmaf(-2.f, acc[4 * g + 3], c4.w);
-        if (s0 < best) { best = s0; bidx = i0 + 0; }
-        if (s1 < best) { best = s1; bidx = i0 + 1; }
-        if (s2 < best) { best = s2; bidx = i0 + 2; }
-        if (s3 < best) { best = s3; bidx = i0 + 3; }
-      }
-    }
-    {
-      const float ob = __shfl_xor(best, 32, 64);
-      const int oi = __shfl_xor(bidx, 32, 64);
+    for (int o = 16; o <= 32; o <<= 1) {
+      const float ob = __shfl_xor(best, o, 64);
+      const int oi = __shfl_xor(bidx, o, 64);
       if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
     }
     bidx += c_base;
-    if (!first && valid) {
+    const long long row = tile * (16 * RT) + 16 * t + r;
+    const bool mine = g == 0 && row < n;
+    if (!first && mine) {
       const float pb = best_io[row];
       const int pi = labels[row];
       if (pb <= best) { best = pb; bidx = pi; }  // earlier chunks hold smaller indices
     }
-    if (last) {
-      float xn = 0.f;
-#pragma unroll
-      for (int s = 0; s < DS; ++s) {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) {
-          const float f = (float)xf[s][j];
-          xn = fmaf(f, f, xn);
-        }
-      }
-      xn += __shfl_xor(xn, 32, 64);
-      const float d = fmaxf(xn + best, 0.f);
-      if (h == 0 && valid) {
-        labels[row] = bidx;
-        best_io[row] = d;
+    if (mine) {
+      labels[row] = bidx;
+      if (last) {
+        const float d = fmaxf(best, 0.f);
+        if (best_io != nullptr) best_io[row] = d;
         cost += (double)d;
         if (ranking) rank_out[row] = atomicAdd(hist + bidx, 1);
+      } else {
+        best_io[row] = best;
       }
-    } else if (h == 0 && valid) {
-      labels[row] = bidx;
-      best_io[row] = best;
+    }
+  }
+}
+
+// NT threads; each wave owns super-tiles of RT x 16 rows. PF: the next super-tile's rows are in
+// flight while this one computes (double-buffered X registers).
+template <int DP, int RT, int NT, bool PF, int RINGMAX>
+__global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
+    const u16* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
+    int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
+    int* __restrict__ labels, float* __restrict__ best_io, int first, int last, double* __restrict__ cost_part,
+    int* __restrict__ hist_out, int* __restrict__ rank_out) {
+  extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
+  constexpr int NCH = AssignShape<DP>::NCH;
+  constexpr int KS = AssignShape<DP>::KS;
+  const int nct = kc >> 4;
+  uint4* fr = reinterpret_cast<uint4*>(smem);
+  float* cn = reinterpret_cast<float*>(smem + (size_t)nct * KS * 1024);
+  int* hist = reinterpret_cast<int*>(cn + kc);
+  double* red = reinterpret_cast<double*>(hist + ((kp + 3) & ~3));
+
+  const int tid = threadIdx.x;
+  for (int id = tid; id < nct * KS * 64; id += NT) {
+    const int l = id & 63, f = id >> 6;  // fragment f = ct*KS + s
+    const int ct = f / KS, st = f - ct * KS;
+    const int c = ct * 16 + (l & 15), q = 4 * st + (l >> 4);
+    unsigned o[4] = {0u, 0u, 0u, 0u};
+    if (q < NCH) {
+      const uint4 v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + q * 8);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // x -2, exact: bf16 -> f32 -> bf16 round trip of a power-of-two scale
+        const float lo = -2.f * bf16_to_f32((u16)(w[e] & 0xffffu));
+        const float hi = -2.f * bf16_to_f32((u16)(w[e] >> 16));
+        o[e] = (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+      }
+    }
+    fr[id] = make_uint4(o[0], o[1], o[2], o[3]);
+  }
+  for (int i = tid; i < kc; i += NT) cn[i] = cnorm[i];
+  const bool ranking = last && rank_out != nullptr;
+  if (ranking)
+    for (int i = tid; i < kp; i += NT) hist[i] = 0;
+  __syncthreads();
+
+  constexpr int nwaves = NT / 64;
+  const int lane = tid & 63, wave = tid >> 6;
+  const int r = lane & 15, g = lane >> 4;
+  constexpr int ROWS = 16 * RT;
+  const long long ntiles = (n + ROWS - 1) / ROWS;
+  const long long tw = (long long)gridDim.x * nwaves;
+  double cost = 0.0;
+
+  AssignCtx cx;
+  cx.frag = smem + lane * 16;
+  cx.cn = cn;
+  cx.nct = nct;
+  int bits = 1;
+  while ((1 << bits) < nct) ++bits;
+  cx.cmask = (1 << bits) - 1;
+
+  long long tile = (long long)blockIdx.x * nwaves + wave;
+  if constexpr (PF) {
+    XTile<DP, RT> xa, xb;
+    if (tile < ntiles) load_xtile<DP, RT>(X, n, ldx, tile, r, g, xa);
+    for (; tile < ntiles; tile += 2 * tw) {
+      const long long t1 = tile + tw;
+      if (t1 < ntiles) load_xtile<DP, RT>(X, n, ldx, t1, r, g, xb);
+      assign_tile<DP, RT, RINGMAX>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+                          rank_out, cost);
+      if (t1 >= ntiles) break;
+      if (t1 + tw < ntiles) load_xtile<DP, RT>(X, n, ldx, t1 + tw, r, g, xa);
+      assign_tile<DP, RT, RINGMAX>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+                          rank_out, cost);
+    }
+  } else {
+    for (; tile < ntiles; tile += tw) {
+      XTile<DP, RT> xt;
+      load_xtile<DP, RT>(X, n, ldx, tile, r, g, xt);
+      assign_tile<DP, RT, RINGMAX>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+                          rank_out, cost);
     }
   }
   if (last && (cost_part != nullptr || ranking)) {
@@ -166,7 +315,36 @@ __global__ __launch_bounds__(kAssignThreads, 2) void kmeans_assign_bf16(
       cost_part[blockIdx.x] = t;
     }
     if (ranking)
-      for (int i = tid; i < kp; i += blockDim.x) hist_out[(long long)blockIdx.x * kp + i] = hist[i];
+      for (int i = tid; i < kp; i += NT) hist_out[(long long)blockIdx.x * kp + i] = hist[i];
+  }
+}
+
+// ||x_i||² of the bf16 rows (f32), once per fit: the assign epilogue then reads 4 B/row
+// instead of re-deriving the norm from the tile (128 converts + FMAs per lane per tile).
+template <int NCH>
+__global__ __launch_bounds__(256) void row_sqnorm_bf16(const u16* __restrict__ X, long long n, long long ldx,
+                                                       float* __restrict__ out) {
+  constexpr int RPW = 64 / NCH;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / NCH, c = lane - sub * NCH;
+  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW) {
+    const long long row = r0 + sub;
+    float s = 0.f;
+    if (row < n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(X + row * ldx + 8 * c);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float lo = bf16_to_f32((u16)(w[q] & 0xffffu)), hi = bf16_to_f32((u16)(w[q] >> 16));
+        s = fmaf(lo, lo, s);
+        s = fmaf(hi, hi, s);
+      }
+    }
+#pragma unroll
+    for (int o = NCH / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (c == 0 && row < n) out[row] = s;
   }
 }
 
@@ -353,11 +531,11 @@ __global__ __launch_bounds__(256) void kmeans_seg_offsets(const int* __restrict_
 
 // Sort regime, pass 3: perm[off[label][block(row)] + rank[row]] = row.
 __global__ void kmeans_scatter(const int* __restrict__ labels, const int* __restrict__ rank, long long n, int nblk,
-                               int nwaves, const int* __restrict__ off, int* __restrict__ perm) {
+                               int nwaves, int tile_rows, const int* __restrict__ off, int* __restrict__ perm) {
   const long long tw = (long long)nblk * nwaves;
   for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < n;
        row += (long long)gridDim.x * blockDim.x) {
-    const long long tile = row >> 5;
+    const long long tile = row / tile_rows;
     const int blk = (int)((tile % tw) / nwaves);
     const int lab = labels[row];
     perm[off[(long long)lab * nblk + blk] + rank[row]] = (int)row;
@@ -507,17 +685,66 @@ __global__ void kmeans_update_kernel(const double* __restrict__ bufs, int nbuf, 
 }
 
 long long assign_lds_bytes(int kc, int kp, int Dp) {
-  return (long long)kc * Dp * 2 + (long long)kc * 4 + (long long)((kp + 3) & ~3) * 4 + 16 * 8;
+  const long long ks = Dp >= 32 ? Dp / 32 : 1;
+  return (long long)(kc / 16) * ks * 1024 + (long long)kc * 4 + (long long)((kp + 3) & ~3) * 4 + 16 * 8;
 }
 
-template <int DS>
+// Assign launch shape (measured on MI355X, see profiles/): RT 16-row sub-tiles per wave share
+// each centre fragment; 512 threads = two waves per SIMD. Large rows (Dp >= 256) are MFMA-heavy
+// per byte: RT 4 halves the LDS fragment traffic and amortises the per-tile epilogue (no X
+// double buffer fits next to it; the partner wave hides the loads). Small rows are bytes-heavy:
+// RT 1 with the next tile's X in flight and more waves per CU.
+// Variant (tuning/experiments): 0 auto, 1 = RT 2 + X double buffer, 2 = RT 1, 3 = RT 4.
+int g_assign_variant = 0;
+inline int assign_threads(int /*DS*/) { return 512; }
+
+template <int DP>
+const void* assign_kernel_ptr() {
+  constexpr bool PF = AssignShape<DP>::KS <= 8;
+  constexpr int RT_BIG = DP >= 512 ? 2 : 4;
+  switch (g_assign_variant) {
+    case 1: return (const void*)kmeans_assign_bf16<DP, 2, 512, PF, 4>;
+    case 2: return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4>;
+    case 3: return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, 2>;
+    default:
+      if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2>;
+      else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4>;
+  }
+}
+
+// Rows per wave tile of the launch assign_kernel_ptr<DP> selects (the sort regime's scatter
+// recovers a row's workgroup from it).
+inline int assign_tile_rows(int Dp) {
+  switch (g_assign_variant) {
+    case 1: return 32;
+    case 2: return 16;
+    case 3: return Dp >= 512 ? 32 : 64;
+    default: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
+  }
+}
+
+template <int DP>
+int assign_occupancy(int kc, int kp) {
+  const size_t lds = (size_t)assign_lds_bytes(kc, kp, DP);
+  const void* fn = assign_kernel_ptr<DP>();
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  int nb = 0;
+  hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, assign_threads(0), lds);
+  return nb;
+}
+
+template <int DP>
 int launch_assign(const u16* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp,
-                  int c_base, const float* cnorm, int* labels, float* best, int first, int last,
+                  int c_base, const float* cnorm, const float* xnorm, int* labels, float* best, int first, int last,
                   double* cost_part, int* hist, int* rank, int grid, hipStream_t st) {
-  const size_t lds = (size_t)assign_lds_bytes(kc, kp, 16 * DS);
-  hipFuncSetAttribute((const void*)kmeans_assign_bf16<DS>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(kmeans_assign_bf16<DS>, dim3(grid), dim3(kAssignThreads), lds, st, X, n, ldx, C, ldc, kc, kp,
-                     c_base, cnorm, labels, best, first, last, cost_part, hist, rank);
+  const size_t lds = (size_t)assign_lds_bytes(kc, kp, DP);
+  const void* fn = assign_kernel_ptr<DP>();
+  hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  void* args[] = {(void*)&X, (void*)&n, (void*)&ldx, (void*)&C, (void*)&ldc, (void*)&kc, (void*)&kp,
+                  (void*)&c_base, (void*)&cnorm, (void*)&xnorm, (void*)&labels, (void*)&best, (void*)&first,
+                  (void*)&last, (void*)&cost_part, (void*)&hist, (void*)&rank};
+  const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(assign_threads(0)), args, lds, st);
+  if (e != hipSuccess) return (int)e;
   return cml_status();
 }
 
@@ -539,29 +766,72 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
 }  // namespace
 
 CML_API long long cml_kmeans_assign_lds_bytes(int kc, int kp, int Dp) { return assign_lds_bytes(kc, kp, Dp); }
-CML_API int cml_kmeans_assign_threads() { return kAssignThreads; }
+CML_API int cml_kmeans_assign_threads(int Dp) { return assign_threads(Dp / 16); }
+// Resident workgroups per CU of the assign kernel for this shape (persistent-grid sizing).
+CML_API int cml_kmeans_assign_occupancy(int Dp, int kc, int kp) {
+  switch (Dp / 16) {
+    case 1: return assign_occupancy<16>(kc, kp);
+    case 2: return assign_occupancy<32>(kc, kp);
+    case 4: return assign_occupancy<64>(kc, kp);
+    case 8: return assign_occupancy<128>(kc, kp);
+    case 16: return assign_occupancy<256>(kc, kp);
+    case 32: return assign_occupancy<512>(kc, kp);
+    default: return 0;
+  }
+}
+CML_API int cml_kmeans_set_assign_variant(int v) {
+  if (v < 0 || v > 3) return (int)hipErrorInvalidValue;
+  g_assign_variant = v;
+  return 0;
+}
 CML_API int cml_kmeans_accum_threads() { return kAccumThreads; }
 CML_API int cml_kmeans_seg_threads() { return kSegThreads; }
 CML_API long long cml_kmeans_seg_ints(int k) { return (long long)(k + 1) + ((k + 1) & 1) + 2LL * k + 2; }
 
 // X: bf16 [n, ldx] (Dp = 16*DS used columns, zero padded). C: bf16 [kc, ldc] (kc % 32 == 0).
 // hist/rank may be null; when given (last chunk only) hist is [grid][kp] and rank is [n].
+// xnorm (f32 [n], cml_row_sqnorm_bf16) is required: it seeds the MFMA accumulators.
+// best may be null on a single-chunk (first && last) launch: only labels/cost are produced.
 CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, int Dp, const void* C, long long ldc,
-                                   int kc, int kp, int c_base, const float* cnorm, int* labels, float* best,
-                                   int first, int last, double* cost_part, int* hist, int* rank, int grid,
-                                   void* stream) {
-  if (kc % 32 != 0 || Dp % 16 != 0 || ldx % 8 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+                                   int kc, int kp, int c_base, const float* cnorm, const float* xnorm, int* labels,
+                                   float* best, int first, int last, double* cost_part, int* hist, int* rank,
+                                   int grid, void* stream) {
+  if (kc % 16 != 0 || Dp % 16 != 0 || ldx % 8 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
   if ((hist == nullptr) != (rank == nullptr)) return (int)hipErrorInvalidValue;
+  if (best == nullptr && !(first && last)) return (int)hipErrorInvalidValue;
+  if (xnorm == nullptr) return (int)hipErrorInvalidValue;  // ||x||² seeds the accumulators
   hipStream_t st = (hipStream_t)stream;
   const u16* x = (const u16*)X;
   const u16* c = (const u16*)C;
-#define CML_ASSIGN(DS) \
-  case DS: return launch_assign<DS>(x, n, ldx, c, ldc, kc, kp, c_base, cnorm, labels, best, first, last, cost_part, hist, rank, grid, st)
+#define CML_ASSIGN(DS, DP)                                                                                       \
+  case DS:                                                                                                       \
+    return launch_assign<DP>(x, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last,        \
+                                 cost_part, hist, rank, grid, st)
   switch (Dp / 16) {
-    CML_ASSIGN(1); CML_ASSIGN(2); CML_ASSIGN(4); CML_ASSIGN(8); CML_ASSIGN(16); CML_ASSIGN(32);
+    CML_ASSIGN(1, 16); CML_ASSIGN(2, 32); CML_ASSIGN(4, 64); CML_ASSIGN(8, 128); CML_ASSIGN(16, 256);
+    CML_ASSIGN(32, 512);
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_ASSIGN
+}
+
+CML_API int cml_row_sqnorm_bf16(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
+  if (Dp % 16 != 0 || Dp > 512 || ldx % 8 != 0) return (int)hipErrorInvalidValue;
+  const u16* x = (const u16*)X;
+  hipStream_t st = (hipStream_t)stream;
+  const long long rows_per_block = 4LL * (64 / (Dp / 8));
+  const long long blocks = std::min<long long>((n + rows_per_block - 1) / rows_per_block, 256LL * 16);
+  const dim3 g((unsigned)std::max<long long>(blocks, 1));
+  switch (Dp / 8) {
+    case 2: hipLaunchKernelGGL(row_sqnorm_bf16<2>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 4: hipLaunchKernelGGL(row_sqnorm_bf16<4>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 8: hipLaunchKernelGGL(row_sqnorm_bf16<8>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 16: hipLaunchKernelGGL(row_sqnorm_bf16<16>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 32: hipLaunchKernelGGL(row_sqnorm_bf16<32>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 64: hipLaunchKernelGGL(row_sqnorm_bf16<64>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return cml_status();
 }
 
 // Regime A. rpw rows per wave-instruction, private copies; dw <= cpl*64/rpw.
@@ -607,7 +877,8 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
   if (e) return e;
   if (n == 0) return 0;
   const long long sblocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
-  hipLaunchKernelGGL(kmeans_scatter, dim3((unsigned)sblocks), dim3(256), 0, st, labels, rank, n, nblk, nwaves, off,
+  hipLaunchKernelGGL(kmeans_scatter, dim3((unsigned)sblocks), dim3(256), 0, st, labels, rank, n, nblk, nwaves,
+                     assign_tile_rows(Dp), off,
                      perm);
   e = cml_status();
   if (e) return e;

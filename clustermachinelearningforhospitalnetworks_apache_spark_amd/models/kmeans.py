@@ -88,7 +88,10 @@ class LloydEngine:
         self.aplan = K.plan_assign(max(maxn, 1), dp, k, dev.index or 0)
         self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode)
         self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
-        self.best = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        # distance scratch only when the centres need several LDS chunks (running min through HBM)
+        self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev) if self.aplan.kc < self.aplan.kp
+                     else None)
+        self.xnorm = K.row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
             self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
@@ -134,6 +137,9 @@ class LloydEngine:
             self._step_cpu()
         self.iterations += 1
 
+    def _best(self, r0: int, r1: int):
+        return None if self.best is None else self.best[r0:r1]
+
     def _step_gpu(self):
         handles = []
         for c in range(self.row_chunks):
@@ -144,15 +150,15 @@ class LloydEngine:
                 xc = self.x[r0:r1]
                 lab = self.labels[r0:r1]
                 if self.cplan.mode == "priv":
-                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
-                                  self.cost_part)
+                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
+                                  self.cost_part, xnorm=self.xnorm[r0:r1])
                     K.accumulate_priv(xc, nrow, lab, self.k, self.cplan, self.slab, self.cslab)
                     K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, self.k, self.d,
                                    self.cplan, msg)
                 else:
                     rank = self.rank[r0:r1]
-                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self.best[r0:r1],
-                                  self.cost_part, self.hist, rank)
+                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
+                                  self.cost_part, self.hist, rank, xnorm=self.xnorm[r0:r1])
                     K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
                                       self.cost_part, self.off, self.seg, self.perm, self.cplan, msg)
             else:
@@ -286,7 +292,7 @@ class LloydEngine:
         return out
 
 
-def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor):
+def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: Optional[torch.Tensor] = None):
     """K9 against an arbitrary centre set (used for transform, cost and k-means||)."""
     k = centers.shape[0]
     kp = round_up(max(k, 1), 32)
@@ -299,8 +305,10 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor):
     labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     if n:
+        if xnorm is None:
+            xnorm = K.row_sqnorm(x, n, dp)
         plan = K.plan_assign(n, dp, k, dev.index or 0)
-        K.assign_bf16(x, n, dp, cb, cn, plan, labels, best, None)
+        K.assign_bf16(x, n, dp, cb, cn, plan, labels, best, None, xnorm=xnorm)
     return labels[:n], best[:n]
 
 

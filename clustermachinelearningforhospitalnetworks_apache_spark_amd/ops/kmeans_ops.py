@@ -17,11 +17,14 @@ from ..utils.device import LDS_BUDGET, num_cus, round_up
 
 _native.register_kernel_sigs({
     "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int, c_int]),
-    "cml_kmeans_assign_threads": (c_int, []),
+    "cml_kmeans_assign_threads": (c_int, [c_int]),
+    "cml_kmeans_set_assign_variant": (c_int, [c_int]),
+    "cml_kmeans_assign_occupancy": (c_int, [c_int, c_int, c_int]),
     "cml_kmeans_seg_threads": (c_int, []),
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
     "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                       c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
     "cml_kmeans_accum_priv": (c_int, [c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int,
                                       c_vp]),
@@ -72,11 +75,20 @@ def plan_assign(n: int, dp: int, k: int, device_index: int = 0) -> AssignPlan:
     lds = lib.cml_kmeans_assign_lds_bytes(kc, kp, dp)
     if lds > LDS_BUDGET:
         raise ValueError(f"feature width {dp} / k={k} too large for the LDS-resident centroid tile")
-    waves = lib.cml_kmeans_assign_threads() // 64
+    waves = lib.cml_kmeans_assign_threads(dp) // 64
     per_cu = max(1, min(4, (160 * 1024) // max(lds, 1)))
+    if torch.cuda.is_available():
+        occ = lib.cml_kmeans_assign_occupancy(dp, kc, kp)
+        if occ > 0:  # persistent grid: never more workgroups than can be resident at once
+            per_cu = max(1, min(per_cu, occ))
     ntiles = (n + 31) // 32
     grid = max(1, min((ntiles + waves - 1) // waves, num_cus(device_index) * per_cu))
     return AssignPlan(n=n, dp=dp, kp=kp, kc=kc, grid=grid, nwaves=waves)
+
+
+def set_assign_variant(v: int) -> None:
+    """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD)."""
+    _native.check(_native.kernels().cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
 
 
 def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None = None) -> AccumPlan:
@@ -105,16 +117,24 @@ def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None
 
 
 def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor, plan: AssignPlan,
-                labels: torch.Tensor, best: torch.Tensor, cost_part: torch.Tensor | None,
-                hist: torch.Tensor | None = None, rank: torch.Tensor | None = None, stream=None) -> None:
+                labels: torch.Tensor, best: torch.Tensor | None, cost_part: torch.Tensor | None,
+                hist: torch.Tensor | None = None, rank: torch.Tensor | None = None, stream=None,
+                xnorm: torch.Tensor | None = None) -> None:
     """K9: labels/best[i] = argmin/min_j ||x_i - c_j||² over all kp (padded) centres.
 
     With ``hist``/``rank`` also emits the per-workgroup label histogram and per-row rank
-    (first pass of the counting sort used by the sort accumulation regime).
+    (first pass of the counting sort used by the sort accumulation regime). ``xnorm`` are the
+    cached ||x_i||² (row_sqnorm; Spark's KMeans caches point norms the same way,
+    mllib/clustering/KMeans.scala ``VectorWithNorm``); ``best`` may be None when the centres fit
+    one LDS chunk and the distances themselves are not wanted.
     """
     lib = _native.kernels()
     st = _native.stream_ptr(stream)
     nch = (plan.kp + plan.kc - 1) // plan.kc
+    if xnorm is None:
+        xnorm = row_sqnorm(x, n, dp, stream=stream)
+    if best is None and nch > 1:
+        raise ValueError("multi-chunk assignment needs the `best` scratch buffer")
     for ci in range(nch):
         c0 = ci * plan.kc
         kc = min(plan.kc, plan.kp - c0)
@@ -122,13 +142,24 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
         status = lib.cml_kmeans_assign_bf16(
             x.data_ptr(), n, x.stride(0), dp,
             cb.data_ptr() + c0 * cb.stride(0) * 2, cb.stride(0), kc, plan.kp, c0,
-            cnorm.data_ptr() + c0 * 4, labels.data_ptr(), best.data_ptr(),
+            cnorm.data_ptr() + c0 * 4, xnorm.data_ptr(),
+            labels.data_ptr(), best.data_ptr() if best is not None else 0,
             int(ci == 0), int(last),
             cost_part.data_ptr() if (cost_part is not None and last) else 0,
             hist.data_ptr() if (hist is not None and last) else 0,
             rank.data_ptr() if (rank is not None and last) else 0,
             plan.grid, st)
         _native.check(status, "kmeans_assign_bf16")
+
+
+def row_sqnorm(x: torch.Tensor, n: int, dp: int, out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """||x_i||² (f32) of the padded bf16 device matrix, computed once per fit."""
+    if out is None:
+        out = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
+    if n > 0:
+        _native.check(_native.kernels().cml_row_sqnorm_bf16(x.data_ptr(), n, x.stride(0), dp, out.data_ptr(),
+                                                             _native.stream_ptr(stream)), "row_sqnorm_bf16")
+    return out
 
 
 def accumulate_priv(x: torch.Tensor, n: int, labels: torch.Tensor, k: int, plan: AccumPlan,

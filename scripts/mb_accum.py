@@ -14,20 +14,27 @@ def timeit(fn, reps=3):
     return best
 
 
-for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16, 5)]:
+for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16, 5), (4_000_000, 512, 128)]:
     g = torch.Generator(device="cuda"); g.manual_seed(0)
     cen = torch.randn(k, d, device="cuda", generator=g) * 4
     x = (cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn(n, d, device="cuda", generator=g)).to(torch.bfloat16)
     del cen
+    gb = n * d * 2 / 1e9
     for mode in (None, "sort"):
+        K.set_assign_variant(0)
         eng = LloydEngine(x, d, k, accum_mode=mode)
         eng.set_centers(x[:k].double().cpu().numpy())
-        ap = eng.aplan
-        t_as = timeit(lambda: K.assign_bf16(x, n, d, eng.cb, eng.cnorm, ap, eng.labels, eng.best, eng.cost_part))
+        if mode is None:
+            for v in (0,):
+                K.set_assign_variant(v)
+                ap = K.plan_assign(n, eng.dp, k)
+                t_as = timeit(lambda: K.assign_bf16(x, n, eng.dp, eng.cb, eng.cnorm, ap, eng.labels, eng.best,
+                                                    eng.cost_part, xnorm=eng.xnorm))
+                print(f"n={n} d={d} k={k} variant {v} grid {ap.grid}x{ap.nwaves}w: assign {t_as:.3f} ms "
+                      f"({gb/t_as:.2f} TB/s, {2*n*d*k/t_as/1e9:.0f} TF/s)", flush=True)
+            K.set_assign_variant(0)
         t_st = timeit(lambda: eng.step())
-        gb = n * d * 2 / 1e9
-        print(f"n={n} d={d} k={k} {eng.cplan}: assign {t_as:.3f} ms ({gb/t_as:.2f} TB/s, {2*n*d*k/t_as/1e9:.0f} TF/s)"
-              f" step {t_st:.3f} ms -> {n/t_st/1e6:.2f} Gsamples/s", flush=True)
+        print(f"n={n} d={d} k={k} {eng.cplan}: step {t_st:.3f} ms -> {n/t_st/1e6:.2f} Gsamples/s", flush=True)
         del eng
         torch.cuda.empty_cache()
     del x

@@ -22,13 +22,19 @@ def _ref_assign(xb, cb):
 
 @pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (4097, 100, 70), (20000, 256, 256), (3000, 512, 200),
                                    (777, 16, 33), (5000, 128, 64)])
-def test_assign_matches_reference(n, d, k):
+@pytest.mark.parametrize("cached_norm", [False, True])
+def test_assign_matches_reference(n, d, k, cached_norm):
+    """Every row's label is the bf16-exact argmin up to near-ties; rows equal to a centre keep
+    distance ~0 (the rounding-negative case of the packed-key minimum)."""
     torch.manual_seed(0)
     dev = torch.device("cuda")
     x = torch.randn(n, d, device=dev) * 2
     c = torch.randn(k, d, device=dev) * 2
     xm = to_device_matrix(x, d)
-    lab, best = assign_gpu(xm, xm.shape[1], d, c.double())
+    xn = K.row_sqnorm(xm, n, xm.shape[1]) if cached_norm else None
+    if xn is not None:
+        np.testing.assert_allclose(xn.cpu().double().numpy(), (xm.double() ** 2).sum(1).cpu().numpy(), rtol=1e-5)
+    lab, best = assign_gpu(xm, xm.shape[1], d, c.double(), xnorm=xn)
     torch.cuda.synchronize()
     cb = c.to(torch.bfloat16)
     ref_lab, ref_d, gap = _ref_assign(x.to(torch.bfloat16), cb)
@@ -38,10 +44,18 @@ def test_assign_matches_reference(n, d, k):
     np.testing.assert_allclose(best.cpu().double().numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
 
 
+@pytest.fixture
+def assign_variant(request):
+    K.set_assign_variant(request.param)
+    yield request.param
+    K.set_assign_variant(0)
+
+
+@pytest.mark.parametrize("assign_variant", [0, 1, 2, 3], indirect=True)
 @pytest.mark.parametrize("mode", [None, "sort"])
 @pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (50000, 256, 256), (9999, 100, 70), (2000, 16, 3),
                                    (3000, 512, 40), (40000, 128, 64)])
-def test_lloyd_step_matches_reference(n, d, k, mode):
+def test_lloyd_step_matches_reference(n, d, k, mode, assign_variant):
     torch.manual_seed(1)
     dev = torch.device("cuda")
     x = (torch.randn(n, d, device=dev) * 3).to(torch.bfloat16)
