@@ -207,7 +207,7 @@ class LloydEngine:
             centers = torch.as_tensor(centers, dtype=torch.float64, device=self.device)
         if not self.gpu:
             return K.assign_reference(self.x, self.centers if centers is None else centers)
-        return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers)
+        return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers, self.xnorm)
 
     def training_cost(self) -> float:
         return float(self.last_cost.item()) if self.last_cost is not None else float("nan")
@@ -234,7 +234,7 @@ class LloydEngine:
     def _min_dist(self, cands: torch.Tensor) -> torch.Tensor:
         if not self.gpu:
             return K.assign_reference(self.x, cands)[1]
-        return assign_gpu(self.x, self.dp, self.d, cands)[1].to(torch.float64)
+        return assign_gpu(self.x, self.dp, self.d, cands, self.xnorm)[1].to(torch.float64)
 
     def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
         """k-means|| (Bahmani et al.), Spark's default initMode, then weighted local k-means++."""
@@ -276,7 +276,7 @@ class LloydEngine:
             cand_t = torch.as_tensor(cand_np, device=self.device)
             if self.n:
                 lab = (K.assign_reference(self.x, cand_t)[0] if not self.gpu
-                       else assign_gpu(self.x, self.dp, self.d, cand_t)[0].long())
+                       else assign_gpu(self.x, self.dp, self.d, cand_t, self.xnorm)[0].long())
                 w = torch.bincount(lab, minlength=cand_np.shape[0]).to(torch.float64)
             else:
                 w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
