@@ -1,0 +1,438 @@
+// Columnar-frame kernels for gfx950: the memory-bound glue between the
+// reference's DataFrame steps and the estimators. Every kernel streams its inputs once.
+//
+// K2  assemble_pack   typed columns (+ validity bytes, + vector columns) -> row-major [n, ld]
+//                     f64/f32/bf16 feature matrix and a per-row "invalid" byte (null or NaN) —
+//                     VectorAssembler (ref.py:134-136) with handleInvalid error/skip/keep.
+// K3  compact         bool mask -> ascending int64 indices of the set rows (count, block scan,
+//                     scatter) — filter / na.drop / BETWEEN (ref.py:123-128) and the splits.
+// K5  split_buckets   counter hash (splitmix64) of (seed, stream, global row id) -> split index
+//                     by cumulative weights; GPU-count invariant (ref.py:139, ref.py:180).
+// K22 poisson1        Poisson(1) bagging counts by CDF inversion of the same counter uniform
+//                     (RandomForest bootstrap, ref.py:155-158, ref.py:187-190).
+// K6  binarize        y = x > thr ? 1 : 0 (ref.py:176-177 `when(col > 5.0, 1).otherwise(0)`).
+// K23 reg_metrics     fused weighted SSE / SAE / Σy / Σy² / Σŷ / Σŷ² / Σw partials (RMSE, MSE, MAE,
+//                     R², explained variance: ref.py:160-169); cls_confusion: weighted confusion
+//                     matrix (accuracy, F1, precision, recall: ref.py:192-198).
+// K4  col_absmax / quant_fp8   per-feature amax and x·scale -> OCP e4m3fn bytes.
+//
+// The uniform/Poisson kernels reproduce utils/rng.py bit for bit (same uint64 arithmetic, the
+// CDF thresholds are computed on the host once), so CPU and GPU runs make identical decisions.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kCompactItems = 16;                       // per thread
+constexpr int kCompactTile = kThreads * kCompactItems;  // rows per compaction block
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+__device__ __forceinline__ double counter_uniform(long long row, unsigned long long key) {
+  const unsigned long long h = splitmix64((unsigned long long)row ^ key);
+  return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// ------------------------------------------------------------------------------------- K5 / K22
+struct Cum {
+  double c[17];  // c[0] = 0 ... c[nb] (>= 1)
+  int nb;
+};
+
+__global__ __launch_bounds__(kThreads) void split_buckets_kernel(const long long* __restrict__ rows, long long n,
+                                                                 unsigned long long key, Cum cum,
+                                                                 signed char* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const double u = counter_uniform(rows[i], key);
+    int b = -1;
+    for (int j = 0; j < cum.nb; ++j)
+      if (b < 0 && u >= cum.c[j] && u < cum.c[j + 1]) b = j;
+    out[i] = (signed char)b;
+  }
+}
+
+struct PoissonCdf {
+  double t[17];  // t[k-1] = P(X <= k-1); count = #{k : u >= t[k-1]}
+  int kmax;
+};
+
+__global__ __launch_bounds__(kThreads) void poisson1_kernel(const long long* __restrict__ rows, long long n,
+                                                            unsigned long long key, PoissonCdf cdf,
+                                                            int* __restrict__ out_i32, float* __restrict__ out_f32) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const double u = counter_uniform(rows[i], key);
+    int c = 0;
+    for (int k = 0; k < cdf.kmax; ++k) c += u >= cdf.t[k] ? 1 : 0;
+    if (out_i32 != nullptr) out_i32[i] = c;
+    if (out_f32 != nullptr) out_f32[i] = (float)c;
+  }
+}
+
+__global__ __launch_bounds__(kThreads) void uniform_kernel(const long long* __restrict__ rows, long long n,
+                                                           unsigned long long key, double* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads)
+    out[i] = counter_uniform(rows[i], key);
+}
+
+// --------------------------------------------------------------------------------------------- K3
+__device__ __forceinline__ int block_exclusive_scan(int v, int* sh, int& total) {
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  int incl = v;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int t = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += t;
+  }
+  if (lane == 63) sh[w] = incl;
+  __syncthreads();
+  int wbase = 0, tot = 0;
+#pragma unroll
+  for (int j = 0; j < kThreads / 64; ++j) {
+    const int s = sh[j];
+    if (j < w) wbase += s;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return wbase + incl - v;
+}
+
+__global__ __launch_bounds__(kThreads) void compact_count_kernel(const unsigned char* __restrict__ mask, long long n,
+                                                                 long long* __restrict__ bcount) {
+  __shared__ int sh[kThreads / 64];
+  const long long base = (long long)blockIdx.x * kCompactTile + (long long)threadIdx.x * kCompactItems;
+  int c = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) c += (base + j < n && mask[base + j]) ? 1 : 0;
+  int total;
+  block_exclusive_scan(c, sh, total);
+  if (threadIdx.x == 0) bcount[blockIdx.x] = total;
+}
+
+// one block: in-place exclusive scan of the block counts, total -> count_out
+__global__ __launch_bounds__(kThreads) void compact_scan_kernel(long long* __restrict__ bcount, long long nb,
+                                                                long long* __restrict__ count_out) {
+  __shared__ int sh[kThreads / 64];
+  long long carry = 0;
+  for (long long b0 = 0; b0 < nb; b0 += kThreads) {
+    const long long i = b0 + threadIdx.x;
+    const int v = i < nb ? (int)bcount[i] : 0;  // per-block counts <= kCompactTile
+    int total;
+    const int ex = block_exclusive_scan(v, sh, total);
+    if (i < nb) bcount[i] = carry + ex;
+    carry += total;
+  }
+  if (threadIdx.x == 0) *count_out = carry;
+}
+
+__global__ __launch_bounds__(kThreads) void compact_scatter_kernel(const unsigned char* __restrict__ mask, long long n,
+                                                                   const long long* __restrict__ boff,
+                                                                   long long* __restrict__ idx) {
+  __shared__ int sh[kThreads / 64];
+  const long long base = (long long)blockIdx.x * kCompactTile + (long long)threadIdx.x * kCompactItems;
+  unsigned bits = 0;
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j) bits |= (base + j < n && mask[base + j]) ? (1u << j) : 0u;
+  int total;
+  long long pos = boff[blockIdx.x] + block_exclusive_scan(__popc(bits), sh, total);
+#pragma unroll
+  for (int j = 0; j < kCompactItems; ++j)
+    if (bits & (1u << j)) idx[pos++] = base + j;
+}
+
+// --------------------------------------------------------------------------------------------- K2
+// Source column types.
+enum SrcType : int { kF64 = 0, kF32 = 1, kI32 = 2, kI64 = 3, kU8 = 4, kI16 = 5, kBF16 = 6, kI8 = 7 };
+
+struct AsmCol {
+  const void* ptr;
+  const unsigned char* valid;  // null = all valid
+  long long ld;                // elements between rows (vector columns), 1 for scalars
+  int type;
+  int width;                   // 1 for scalars
+  int out_off;
+  int pad;
+};
+
+__device__ __forceinline__ double load_as_f64(const void* p, int type, long long i) {
+  switch (type) {
+    case kF64: return reinterpret_cast<const double*>(p)[i];
+    case kF32: return (double)reinterpret_cast<const float*>(p)[i];
+    case kI32: return (double)reinterpret_cast<const int*>(p)[i];
+    case kI64: return (double)reinterpret_cast<const long long*>(p)[i];
+    case kU8: return (double)reinterpret_cast<const unsigned char*>(p)[i];
+    case kI16: return (double)reinterpret_cast<const short*>(p)[i];
+    case kBF16: return (double)bf16_to_f32(reinterpret_cast<const u16*>(p)[i]);
+    default: return (double)reinterpret_cast<const signed char*>(p)[i];
+  }
+}
+
+// f64 -> bf16 with ONE rounding (as torch's .to(bfloat16)): round-to-odd into f32 (truncate and set
+// the sticky bit when inexact), then round-to-nearest-even into bf16 — 13 spare bits make the
+// double rounding exact.
+__device__ __forceinline__ u16 f64_to_bf16(double v) {
+  if (v != v) return f32_to_bf16((float)v);
+  float f = __double2float_rz(v);
+  if ((double)f != v && !__builtin_isinf(f)) f = __uint_as_float(__float_as_uint(f) | 1u);
+  return f32_to_bf16(f);
+}
+
+template <int OUT>  // 0 f64, 1 f32, 2 bf16
+__global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmCol* __restrict__ cols, int ncols, long long n,
+                                                            void* __restrict__ out, long long ldo, int dout,
+                                                            unsigned char* __restrict__ invalid, int nan_keep) {
+  for (long long r = (long long)blockIdx.x * kThreads + threadIdx.x; r < n; r += (long long)gridDim.x * kThreads) {
+    bool bad = false;
+    for (int c = 0; c < ncols; ++c) {
+      const AsmCol col = cols[c];
+      const bool ok = col.valid == nullptr || col.valid[r] != 0;
+      for (int j = 0; j < col.width; ++j) {
+        double v = ok ? load_as_f64(col.ptr, col.type, r * col.ld + j) : __builtin_nan("");
+        bad |= !ok || v != v;
+        if (!nan_keep && v != v) v = 0.0;
+        const long long o = r * ldo + col.out_off + j;
+        if constexpr (OUT == 0) reinterpret_cast<double*>(out)[o] = v;
+        else if constexpr (OUT == 1) reinterpret_cast<float*>(out)[o] = (float)v;
+        else reinterpret_cast<u16*>(out)[o] = f64_to_bf16(v);
+      }
+    }
+    for (long long o = r * ldo + dout; o < r * ldo + ldo; ++o) {  // zero the padding columns
+      if constexpr (OUT == 0) reinterpret_cast<double*>(out)[o] = 0.0;
+      else if constexpr (OUT == 1) reinterpret_cast<float*>(out)[o] = 0.f;
+      else reinterpret_cast<u16*>(out)[o] = 0;
+    }
+    if (invalid != nullptr) invalid[r] = bad ? 1 : 0;
+  }
+}
+
+// --------------------------------------------------------------------------------------------- K6
+__global__ __launch_bounds__(kThreads) void binarize_kernel(const void* __restrict__ x, int type, long long n,
+                                                            double thr, double* __restrict__ out) {
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads)
+    out[i] = load_as_f64(x, type, i) > thr ? 1.0 : 0.0;
+}
+
+// -------------------------------------------------------------------------------------------- K23
+// partial[b][0..6] = Σw, Σw e², Σw |e|, Σw y, Σw y², Σw p, Σw p²   (e = y - p)
+__global__ __launch_bounds__(kThreads) void reg_metrics_kernel(const double* __restrict__ y, const double* __restrict__ p,
+                                                               const double* __restrict__ w, long long n,
+                                                               double* __restrict__ partial) {
+  __shared__ double sh[7][kThreads / 64];
+  double s[7] = {0, 0, 0, 0, 0, 0, 0};
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const double wi = w != nullptr ? w[i] : 1.0;
+    const double yi = y[i], pi = p[i], e = yi - pi;
+    s[0] += wi;
+    s[1] += wi * e * e;
+    s[2] += wi * fabs(e);
+    s[3] += wi * yi;
+    s[4] += wi * yi * yi;
+    s[5] += wi * pi;
+    s[6] += wi * pi * pi;
+  }
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < 7; ++q) {
+    const double t = wave_sum_f64(s[q]);
+    if (lane == 0) sh[q][wv] = t;
+  }
+  __syncthreads();
+  if (threadIdx.x < 7) {
+    double t = 0.0;
+    for (int j = 0; j < kThreads / 64; ++j) t += sh[threadIdx.x][j];
+    partial[(long long)blockIdx.x * 7 + threadIdx.x] = t;
+  }
+}
+
+// partial[b][C*C]: weighted confusion counts cm[label][pred], labels/preds in [0, C).
+// Per-thread register-free: each block accumulates into LDS f64 with ds_add_f64 (C <= 32).
+__global__ __launch_bounds__(kThreads) void cls_confusion_kernel(const long long* __restrict__ y,
+                                                                 const long long* __restrict__ p,
+                                                                 const double* __restrict__ w, long long n, int C,
+                                                                 double* __restrict__ partial) {
+  extern __shared__ double cm[];
+  for (int i = threadIdx.x; i < C * C; i += kThreads) cm[i] = 0.0;
+  __syncthreads();
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const long long a = y[i], b = p[i];
+    if (a >= 0 && a < C && b >= 0 && b < C) atomicAdd(&cm[a * C + b], w != nullptr ? w[i] : 1.0);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < C * C; i += kThreads) partial[(long long)blockIdx.x * C * C + i] = cm[i];
+}
+
+// --------------------------------------------------------------------------------------------- K4
+// per-block partial column amax: partial[b][j] = max |x[r, j]| over the block's rows.
+template <typename T>
+__device__ __forceinline__ float ld_f32(const T* p, long long i);
+template <>
+__device__ __forceinline__ float ld_f32<float>(const float* p, long long i) { return p[i]; }
+template <>
+__device__ __forceinline__ float ld_f32<u16>(const u16* p, long long i) { return bf16_to_f32(p[i]); }
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void col_absmax_kernel(const T* __restrict__ x, long long n, int d, long long ldx,
+                                                              int rows_per_block, float* __restrict__ partial) {
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  for (int j = threadIdx.x; j < d; j += kThreads) {
+    float m = 0.f;
+    for (long long r = r0; r < r1; ++r) m = fmaxf(m, fabsf(ld_f32<T>(x, r * ldx + j)));
+    partial[(long long)blockIdx.x * d + j] = m;
+  }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kThreads) void quant_fp8_kernel(const T* __restrict__ x, long long n, int d, long long ldx,
+                                                             const float* __restrict__ scale,
+                                                             unsigned char* __restrict__ out, long long ldo) {
+  // two values per thread -> one packed v_cvt_pk_fp8_f32 (OCP e4m3fn on gfx950, saturating)
+  const long long pairs_per_row = (ldo + 1) / 2;
+  const long long total = n * pairs_per_row;
+  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+    const long long r = t / pairs_per_row;
+    const int j = (int)(t - r * pairs_per_row) * 2;
+    const float a = j < d ? ld_f32<T>(x, r * ldx + j) * scale[j] : 0.f;
+    const float b = j + 1 < d ? ld_f32<T>(x, r * ldx + j + 1) * scale[j + 1] : 0.f;
+    const int packed = __builtin_amdgcn_cvt_pk_fp8_f32(a, b, 0, false);
+    out[r * ldo + j] = (unsigned char)(packed & 0xff);
+    if (j + 1 < ldo) out[r * ldo + j + 1] = (unsigned char)((packed >> 8) & 0xff);
+  }
+}
+
+inline unsigned grid_for(long long n, long long per = kThreads) {
+  long long g = (n + per - 1) / per;
+  if (g < 1) g = 1;
+  if (g > 256LL * 32) g = 256LL * 32;
+  return (unsigned)g;
+}
+
+}  // namespace
+
+// ---------------------------------------------------------------------------------------- exports
+
+CML_API int cml_split_buckets(const long long* rows, long long n, unsigned long long key, const double* cum, int nb,
+                              signed char* out, void* stream) {
+  if (nb < 1 || nb > 16) return (int)hipErrorInvalidValue;
+  Cum c{};
+  for (int i = 0; i <= nb; ++i) c.c[i] = cum[i];
+  c.nb = nb;
+  if (n > 0)
+    hipLaunchKernelGGL(split_buckets_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, rows, n, key,
+                       c, out);
+  return cml_status();
+}
+
+CML_API int cml_poisson1(const long long* rows, long long n, unsigned long long key, const double* thresholds,
+                         int kmax, int* out_i32, float* out_f32, void* stream) {
+  if (kmax < 1 || kmax > 17) return (int)hipErrorInvalidValue;
+  PoissonCdf c{};
+  for (int i = 0; i < kmax; ++i) c.t[i] = thresholds[i];
+  c.kmax = kmax;
+  if (n > 0)
+    hipLaunchKernelGGL(poisson1_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, rows, n, key, c,
+                       out_i32, out_f32);
+  return cml_status();
+}
+
+CML_API int cml_counter_uniform(const long long* rows, long long n, unsigned long long key, double* out,
+                                void* stream) {
+  if (n > 0)
+    hipLaunchKernelGGL(uniform_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, rows, n, key, out);
+  return cml_status();
+}
+
+CML_API long long cml_compact_blocks(long long n) { return (n + kCompactTile - 1) / kCompactTile; }
+
+// idx must hold n entries (worst case); bscratch cml_compact_blocks(n) int64; count_out one int64 (device).
+CML_API int cml_compact(const unsigned char* mask, long long n, long long* idx, long long* bscratch,
+                        long long* count_out, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const long long nb = (n + kCompactTile - 1) / kCompactTile;
+  if (nb > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  if (n <= 0) {
+    hipMemsetAsync(count_out, 0, sizeof(long long), st);
+    return cml_status();
+  }
+  hipLaunchKernelGGL(compact_count_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, mask, n, bscratch);
+  hipLaunchKernelGGL(compact_scan_kernel, dim3(1), dim3(kThreads), 0, st, bscratch, nb, count_out);
+  hipLaunchKernelGGL(compact_scatter_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, mask, n, bscratch, idx);
+  return cml_status();
+}
+
+// cols: device array of AsmCol (see struct layout: ptr, valid, ld, type, width, out_off, pad).
+CML_API int cml_assemble(const void* cols, int ncols, long long n, void* out, int out_dtype, long long ldo, int dout,
+                         unsigned char* invalid, int nan_keep, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const AsmCol* c = (const AsmCol*)cols;
+  if (n <= 0) return 0;
+  switch (out_dtype) {
+    case 0: hipLaunchKernelGGL(assemble_kernel<0>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
+    case 1: hipLaunchKernelGGL(assemble_kernel<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
+    case 2: hipLaunchKernelGGL(assemble_kernel<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return cml_status();
+}
+
+CML_API int cml_assemble_col_bytes() { return (int)sizeof(AsmCol); }
+
+CML_API int cml_binarize(const void* x, int type, long long n, double thr, double* out, void* stream) {
+  if (n > 0)
+    hipLaunchKernelGGL(binarize_kernel, dim3(grid_for(n)), dim3(kThreads), 0, (hipStream_t)stream, x, type, n, thr,
+                       out);
+  return cml_status();
+}
+
+CML_API int cml_metric_grid(long long n) { return (int)grid_for(n, 4LL * kThreads); }
+
+CML_API int cml_reg_metrics(const double* y, const double* p, const double* w, long long n, double* partial, int grid,
+                            void* stream) {
+  hipLaunchKernelGGL(reg_metrics_kernel, dim3(grid), dim3(kThreads), 0, (hipStream_t)stream, y, p, w, n, partial);
+  return cml_status();
+}
+
+CML_API int cml_cls_confusion(const long long* y, const long long* p, const double* w, long long n, int C,
+                              double* partial, int grid, void* stream) {
+  if (C < 1 || C > 64) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(cls_confusion_kernel, dim3(grid), dim3(kThreads), (size_t)C * C * sizeof(double),
+                     (hipStream_t)stream, y, p, w, n, C, partial);
+  return cml_status();
+}
+
+CML_API int cml_col_absmax(const void* x, int dtype, long long n, int d, long long ldx, int rows_per_block,
+                           float* partial, void* stream) {
+  const long long nb = (n + rows_per_block - 1) / rows_per_block;
+  if (nb <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  if (dtype == 1)
+    hipLaunchKernelGGL(col_absmax_kernel<float>, dim3((unsigned)nb), dim3(kThreads), 0, st, (const float*)x, n, d,
+                       ldx, rows_per_block, partial);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(col_absmax_kernel<u16>, dim3((unsigned)nb), dim3(kThreads), 0, st, (const u16*)x, n, d, ldx,
+                       rows_per_block, partial);
+  else
+    return (int)hipErrorInvalidValue;
+  return cml_status();
+}
+
+CML_API int cml_quant_fp8(const void* x, int dtype, long long n, int d, long long ldx, const float* scale,
+                          unsigned char* out, long long ldo, void* stream) {
+  if (n <= 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = n * ((ldo + 1) / 2);
+  if (dtype == 1)
+    hipLaunchKernelGGL(quant_fp8_kernel<float>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const float*)x, n, d,
+                       ldx, scale, out, ldo);
+  else if (dtype == 0)
+    hipLaunchKernelGGL(quant_fp8_kernel<u16>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const u16*)x, n, d, ldx,
+                       scale, out, ldo);
+  else
+    return (int)hipErrorInvalidValue;
+  return cml_status();
+}

@@ -14,6 +14,17 @@ from .base import Evaluator
 from .param import NO_DEFAULT
 
 
+def reg_sums_torch(y, p, w=None):
+    """[Σw, Σw e², Σw |e|, Σw y, Σw y², Σw p, Σw p²] — CPU path and K23 oracle."""
+    if w is None:
+        w = torch.ones_like(y)
+    e = y - p
+    if not y.numel():
+        return torch.zeros(7, dtype=torch.float64, device=y.device)
+    return torch.stack([w.sum(), (w * e * e).sum(), (w * e.abs()).sum(), (w * y).sum(), (w * y * y).sum(),
+                        (w * p).sum(), (w * p * p).sum()])
+
+
 def _col(df, name, dtype=torch.float64):
     cd = df._column_data(name)
     if cd.is_host:
@@ -40,11 +51,12 @@ class RegressionEvaluator(Evaluator):
     def _evaluate(self, df) -> float:
         y = _col(df, self.getLabelCol())
         p = _col(df, self.getPredictionCol())
-        w = _col(df, self.getOrDefault("weightCol")) if self.isSet("weightCol") else torch.ones_like(y)
-        e = y - p
-        stats = torch.stack([w.sum(), (w * e * e).sum(), (w * e.abs()).sum(), (w * y).sum(), (w * y * y).sum(),
-                             (w * p).sum(), (w * p * p).sum()]) if y.numel() else torch.zeros(
-            7, dtype=torch.float64, device=y.device)
+        w = _col(df, self.getOrDefault("weightCol")) if self.isSet("weightCol") else None
+        if y.is_cuda and y.numel():
+            from ..ops import frame_ops  # K23: one fused pass for all seven sums
+            stats = frame_ops.reg_metric_sums(y, p, w)
+        else:
+            stats = reg_sums_torch(y, p, w)
         df._comm.allreduce_(stats)
         n, sse, sae, sy, syy, sp, spp = stats.tolist()
         if n == 0:
@@ -99,9 +111,13 @@ class MulticlassClassificationEvaluator(Evaluator):
             y.shape[0], dtype=torch.float64, device=y.device)
         local_max = int(max(y.max().item() if y.numel() else 0, p.max().item() if p.numel() else 0))
         C = int(df._comm.max_scalar(float(local_max))) + 1
-        cm = torch.zeros(C * C, dtype=torch.float64, device=y.device)
-        if y.numel():
-            cm.index_add_(0, y * C + p, w)
+        if y.is_cuda and y.numel() and C <= 64:
+            from ..ops import frame_ops  # K23: weighted confusion counts in one pass
+            cm = frame_ops.confusion(y, p, C, None if not self.isSet("weightCol") else w).reshape(-1)
+        else:
+            cm = torch.zeros(C * C, dtype=torch.float64, device=y.device)
+            if y.numel():
+                cm.index_add_(0, y * C + p, w)
         df._comm.allreduce_(cm)
         return cm.reshape(C, C).cpu().numpy()  # rows = label, cols = prediction
 

@@ -56,34 +56,49 @@ class VectorAssembler(Transformer):
     def _transform(self, df):
         cols = self.getInputCols()
         dtype = features_dtype(df._session)
-        parts, bad = [], None
+        cds = []
         for c in cols:
             cd = df._column_data(c)
             if cd.is_host:
                 raise TypeError(f"VectorAssembler: column {c!r} of type {cd.dtype.simpleString()} is not numeric")
-            v = cd.values
-            if v.dim() == 1:
-                v = v.reshape(-1, 1)
-            v = v.to(torch.float64)
-            invalid = ~cd.valid_mask().reshape(-1) if cd.valid is not None else None
-            nan = torch.isnan(v).any(1)
-            inv = nan if invalid is None else (nan | invalid)
-            bad = inv if bad is None else (bad | inv)
-            if invalid is not None:
-                v = torch.where(invalid.reshape(-1, 1), torch.full_like(v, float("nan")), v)
-            parts.append(v)
-        x = torch.cat(parts, 1) if parts else torch.zeros((df._nrows, 0), dtype=torch.float64, device=df._device)
+            cds.append(cd)
         hi = self.getHandleInvalid()
-        if bad is not None and df._nrows:
+        if df._device.type == "cuda" and cds and df._nrows:
+            # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags
+            from ..ops import frame_ops
+            x, bad = frame_ops.assemble([(cd.values, cd.valid) for cd in cds], out_dtype=dtype)
+        else:
+            x, bad = self._assemble_torch(df, cds)
+            x = x.to(dtype)
+        if df._nrows and cds:
             if hi == "error":
                 if bool(bad.any().item()):
                     raise ValueError("VectorAssembler: encountered NULL or NaN values with handleInvalid='error'; "
                                      "drop them first (df.na.drop()) or set handleInvalid='skip'/'keep'")
             elif hi == "skip":
                 keep = ~bad
-                df = df._mask_rows(keep)
-                x = x[keep]
-        return _replace_col(df, self.getOutputCol(), ColumnData(x.to(dtype).contiguous(), None, T.VectorUDT()))
+                idx = df._mask_index(keep)
+                df = df._take_rows(idx)
+                x = x[idx]
+        return _replace_col(df, self.getOutputCol(), ColumnData(x.contiguous(), None, T.VectorUDT()))
+
+    @staticmethod
+    def _assemble_torch(df, cds):
+        """CPU path (and the oracle of the K2 kernel test)."""
+        parts, bad = [], torch.zeros(df._nrows, dtype=torch.bool, device=df._device)
+        for cd in cds:
+            v = cd.values
+            if v.dim() == 1:
+                v = v.reshape(-1, 1)
+            v = v.to(torch.float64)
+            invalid = ~cd.valid_mask().reshape(-1) if cd.valid is not None else None
+            nan = torch.isnan(v).any(1)
+            bad = bad | (nan if invalid is None else (nan | invalid))
+            if invalid is not None:
+                v = torch.where(invalid.reshape(-1, 1), torch.full_like(v, float("nan")), v)
+            parts.append(v)
+        x = torch.cat(parts, 1) if parts else torch.zeros((df._nrows, 0), dtype=torch.float64, device=df._device)
+        return x, bad
 
     def _save_impl(self, path):
         U.write_metadata(self, path)
@@ -266,7 +281,11 @@ class Binarizer(Transformer):
     def _transform(self, df):
         cd = df._column_data(self.getInputCol())
         v = cd.values
-        out = (v.to(torch.float64) > self.getThreshold()).to(torch.float64)
+        if v.is_cuda and v.numel():
+            from ..ops import frame_ops  # K6
+            out = frame_ops.binarize(v, self.getThreshold())
+        else:
+            out = (v.to(torch.float64) > self.getThreshold()).to(torch.float64)
         dt = T.VectorUDT() if isinstance(cd.dtype, T.VectorUDT) else T.DoubleType()
         return _replace_col(df, self.getOutputCol(), ColumnData(out, cd.valid, dt))
 

@@ -206,9 +206,16 @@ class DataFrame:
         cols = {k: v.take(idx) for k, v in self._cols.items()}
         return self._new(self._schema, cols, int(idx.numel()), self._row_ids[idx])
 
+    def _mask_index(self, mask: torch.Tensor) -> torch.Tensor:
+        """Ascending row indices of a bool mask (GPU: the K3 compaction kernel)."""
+        mask = mask.to(self._device)
+        if mask.is_cuda:
+            from ..ops import frame_ops
+            return frame_ops.compact(mask)
+        return torch.nonzero(mask, as_tuple=False).flatten()
+
     def _mask_rows(self, mask: torch.Tensor) -> "DataFrame":
-        idx = torch.nonzero(mask.to(self._device), as_tuple=False).flatten()
-        return self._take_rows(idx)
+        return self._take_rows(self._mask_index(mask))
 
     def filter(self, condition) -> "DataFrame":
         if self._stream is not None:
@@ -259,7 +266,13 @@ class DataFrame:
         cum = np.concatenate([[0.0], np.cumsum(w / w.sum())])
         cum[-1] = 1.0 + 1e-12
         seed = np.random.randint(0, 2**31 - 1) if seed is None else int(seed)
-        u = rng.uniform(self._row_ids, seed, stream=2).to(self._device) if self._nrows else torch.zeros(
+        rows = self._row_ids.to(self._device)
+        if rows.is_cuda and self._nrows and len(w) <= 16:
+            # K5: one fused hash + bucket pass, then one compaction per split
+            from ..ops import frame_ops
+            b = frame_ops.split_buckets(rows, rng.key(seed, 2), cum)
+            return [self._mask_rows(b == i) for i in range(len(w))]
+        u = rng.uniform(rows, seed, stream=2) if self._nrows else torch.zeros(
             0, dtype=torch.float64, device=self._device)
         out = []
         for i in range(len(w)):

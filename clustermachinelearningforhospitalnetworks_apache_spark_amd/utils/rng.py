@@ -42,19 +42,36 @@ def key(seed: int, stream: int = 0) -> int:
 
 
 def uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:
-    """u in [0, 1) (float64) for every row id."""
+    """u in [0, 1) (float64) for every row id (device tensors: one fused HIP kernel, K5)."""
+    if row_ids.is_cuda:
+        from ..ops import frame_ops
+        return frame_ops.counter_uniform(row_ids, key(seed, stream))
     h = splitmix64(row_ids.to(torch.int64) ^ key(seed, stream))
     return _lsr(h, 11).to(torch.float64) * (1.0 / (1 << 53))
 
 
-def poisson1(row_ids: torch.Tensor, seed: int, stream: int = 0, max_k: int = 16) -> torch.Tensor:
-    """Poisson(λ=1) counts per row by CDF inversion of one counter-based uniform."""
-    u = uniform(row_ids, seed, stream)
-    out = torch.zeros_like(u, dtype=torch.int32)
+def poisson_thresholds(max_k: int = 16) -> list:
+    """CDF of Poisson(1) at 0..max_k-1, accumulated in float64 in a fixed order (shared by the
+    CPU path and the K22 kernel, so both invert the same thresholds)."""
     p = torch.exp(torch.tensor(-1.0, dtype=torch.float64)).item()
     cdf = p
+    out = []
     for kk in range(1, max_k + 1):
-        out += (u >= cdf).to(torch.int32)
+        out.append(cdf)
         p = p / kk
         cdf += p
     return out
+
+
+def poisson1(row_ids: torch.Tensor, seed: int, stream: int = 0, max_k: int = 16,
+             dtype: torch.dtype = torch.int32) -> torch.Tensor:
+    """Poisson(λ=1) counts per row by CDF inversion of one counter-based uniform."""
+    th = poisson_thresholds(max_k)
+    if row_ids.is_cuda:
+        from ..ops import frame_ops
+        return frame_ops.poisson1(row_ids, key(seed, stream), th, out_dtype=dtype)
+    u = uniform(row_ids, seed, stream)
+    out = torch.zeros_like(u, dtype=torch.int32)
+    for t in th:
+        out += (u >= t).to(torch.int32)
+    return out.to(dtype)
