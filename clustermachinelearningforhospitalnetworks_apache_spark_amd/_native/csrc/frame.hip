@@ -172,15 +172,8 @@ __device__ __forceinline__ double load_as_f64(const void* p, int type, long long
   }
 }
 
-// f64 -> bf16 with ONE rounding (as torch's .to(bfloat16)): round-to-odd into f32 (truncate and set
-// the sticky bit when inexact), then round-to-nearest-even into bf16 — 13 spare bits make the
-// double rounding exact.
-__device__ __forceinline__ u16 f64_to_bf16(double v) {
-  if (v != v) return f32_to_bf16((float)v);
-  float f = __double2float_rz(v);
-  if ((double)f != v && !__builtin_isinf(f)) f = __uint_as_float(__float_as_uint(f) | 1u);
-  return f32_to_bf16(f);
-}
+// f64 -> bf16 as torch's .to(bfloat16) does it: through f32 (two round-to-nearest-even steps).
+__device__ __forceinline__ u16 f64_to_bf16(double v) { return f32_to_bf16((float)v); }
 
 template <int OUT>  // 0 f64, 1 f32, 2 bf16
 __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmCol* __restrict__ cols, int ncols, long long n,

@@ -560,19 +560,34 @@ __device__ __forceinline__ void add_raw(double (&acc)[CPL], const typename RawCo
 // Sort regime, pass 4: segmented sum over the label-sorted order. Wave w streams sorted
 // positions [w*chunk, (w+1)*chunk): ONE vector load fetches the next U row ids, U whole-row
 // gathers (CPL*2 bytes per lane) are in flight, the running sum stays in f64 registers, and
-// the wave flushes (f64 global atomic add into the message) only at cluster boundaries and at
-// the end of its slice. The common chunk (no boundary inside) takes an unpredicated path.
+// the wave flushes only at cluster boundaries and at the end of its slice. The common chunk
+// (no boundary inside) takes an unpredicated path.
+// Deterministic, atomic-free flushes: a cluster that starts and ends inside the slice belongs
+// to this wave alone and is STORED into the message; the slice's first cluster (may have begun
+// in earlier slices) goes to slot A[w], its last (may continue in later slices) to slot B[w];
+// kmeans_seg_fixup adds the slots in ascending wave order. The result is bitwise identical
+// run to run (SURVEY.md §5.2 deterministic-reduction mode, here the only mode).
 template <int CPL>
 __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k, long long chunk,
-                                                             double* __restrict__ msg) {
+                                                             double* __restrict__ msg, double* __restrict__ slots,
+                                                             int* __restrict__ slot_c) {
   using raw_t = typename RawCols<CPL>::T;
   constexpr int U = 16;
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (kSegThreads / 64) + (threadIdx.x >> 6);
   const long long p0 = wave * chunk;
-  if (p0 >= n) return;
+  if (p0 >= n) {
+    if (lane == 0) {
+      slot_c[2 * wave] = -1;
+      slot_c[2 * wave + 1] = -1;
+    }
+    return;
+  }
+  double* slotA = slots + (2 * wave) * (long long)D;
+  double* slotB = slotA + D;
+  int nflush = 0;
   const long long p1 = p0 + chunk < n ? p0 + chunk : n;
   int lo = 0, hi = k;  // invariant: seg[lo] <= p0 < seg[hi]
   while (hi - lo > 1) {
@@ -612,10 +627,15 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restri
         for (int u = 0; u < U; ++u)
           if (p + u >= s0 && p + u < se) add_raw<CPL>(acc, w[u]);
         if (se < next) break;  // chunk ends inside cluster c
-        if (active) {
+        {
+          double* dst = nflush == 0 ? slotA : msg + (long long)c * D;  // later clusters are ours alone
+          if (active) {
 #pragma unroll
-          for (int j = 0; j < CPL; ++j)
-            if (col + j < D) atomicAdd(msg + (long long)c * D + col + j, acc[j]);
+            for (int j = 0; j < CPL; ++j)
+              if (col + j < D) dst[col + j] = acc[j];
+          }
+          if (nflush == 0 && lane == 0) slot_c[2 * wave] = c;
+          ++nflush;
         }
 #pragma unroll
         for (int j = 0; j < CPL; ++j) acc[j] = 0.0;
@@ -630,7 +650,32 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restri
   if (active) {
 #pragma unroll
     for (int j = 0; j < CPL; ++j)
-      if (col + j < D) atomicAdd(msg + (long long)c * D + col + j, acc[j]);
+      if (col + j < D) slotB[col + j] = acc[j];
+  }
+  if (lane == 0) {
+    if (nflush == 0) slot_c[2 * wave] = -1;
+    slot_c[2 * wave + 1] = c;
+  }
+}
+
+// msg[c] += Σ over the slices overlapping cluster c, in ascending slice order, of their head
+// (A) / tail (B) partials for c. One workgroup per cluster.
+__global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long chunk,
+                                                        long long nwaves, const double* __restrict__ slots,
+                                                        const int* __restrict__ slot_c, double* __restrict__ msg) {
+  const int c = blockIdx.x;
+  const long long s0 = seg[c], s1 = seg[c + 1];
+  if (s1 <= s0) return;
+  const long long w0 = s0 / chunk;
+  long long w1 = (s1 - 1) / chunk;
+  if (w1 >= nwaves) w1 = nwaves - 1;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) {
+    double t = 0.0;
+    for (long long w = w0; w <= w1; ++w) {
+      if (slot_c[2 * w] == c) t += slots[(2 * w) * (long long)D + d];
+      if (slot_c[2 * w + 1] == c) t += slots[(2 * w + 1) * (long long)D + d];
+    }
+    msg[(long long)c * D + d] += t;
   }
 }
 
@@ -866,7 +911,7 @@ CML_API int cml_kmeans_reduce(const float* slab, const int* cslab, const double*
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                   const int* rank, const int* hist, int nblk, int nwaves, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
-                                  int seg_grid, double* msg, void* stream) {
+                                  int seg_grid, double* msg, double* slots, int* slot_c, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   long long* tot = reinterpret_cast<long long*>(seg + k + 1 + ((k + 1) & 1));  // scratch after seg (8-B aligned)
   hipMemsetAsync(msg, 0, sizeof(double) * (size_t)k * D, st);
@@ -887,17 +932,26 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
   const u16* x = (const u16*)X;
   if (cpl == 2)
     hipLaunchKernelGGL(kmeans_segacc<2>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg);
+                       chunk, msg, slots, slot_c);
   else if (cpl == 4)
     hipLaunchKernelGGL(kmeans_segacc<4>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg);
+                       chunk, msg, slots, slot_c);
   else if (cpl == 8)
     hipLaunchKernelGGL(kmeans_segacc<8>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg);
+                       chunk, msg, slots, slot_c);
   else
     return (int)hipErrorInvalidValue;
+  e = cml_status();
+  if (e) return e;
+  hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, chunk, waves, slots, slot_c, msg);
   return cml_status();
 }
+
+// Doubles / ints of the deterministic slot scratch for a sort-regime launch of seg_grid blocks.
+CML_API long long cml_kmeans_seg_slot_doubles(int seg_grid, int D) {
+  return 2LL * seg_grid * (kSegThreads / 64) * D;
+}
+CML_API long long cml_kmeans_seg_slot_ints(int seg_grid) { return 2LL * seg_grid * (kSegThreads / 64); }
 
 CML_API int cml_kmeans_update(const double* bufs, int nbuf, long long bstride, int k, int D, double* cent, void* cb,
                               long long ldc, int Dp, int Kp, float* cnorm, double* shift2, void* stream) {

@@ -103,6 +103,7 @@ class LloydEngine:
             self.off = torch.zeros(max(k * self.aplan.grid, 1), dtype=torch.int32, device=dev)
             self.seg = torch.zeros(K.seg_buffer_ints(k), dtype=torch.int32, device=dev)
             self.perm = torch.zeros(max(maxn, 1), dtype=torch.int32, device=dev)
+            self.slots = K.seg_slots(self.cplan, d, dev)
         self.msg_len = k * d + k + 1
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
@@ -160,7 +161,7 @@ class LloydEngine:
                     K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
                                   self.cost_part, self.hist, rank, xnorm=self.xnorm[r0:r1])
                     K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
-                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, msg)
+                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, msg, self.slots)
             else:
                 msg.zero_()
             handles.append(self.comm.allreduce_async(msg))

@@ -30,7 +30,9 @@ _native.register_kernel_sigs({
                                       c_vp]),
     "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp]),
+                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_seg_slot_doubles": (c_ll, [c_int, c_int]),
+    "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                   c_vp]),
 })
@@ -181,16 +183,26 @@ def reduce_slabs(slab, cslab, cost_part, ncost: int, k: int, d: int, plan: Accum
     _native.check(status, "kmeans_reduce")
 
 
+def seg_slots(plan: AccumPlan, d: int, device) -> tuple:
+    """Scratch of the deterministic segmented sum: per-slice head/tail partials + their cluster ids."""
+    lib = _native.kernels()
+    sl = torch.empty(max(int(lib.cml_kmeans_seg_slot_doubles(plan.seg_grid, d)), 1), dtype=torch.float64,
+                     device=device)
+    sc = torch.empty(max(int(lib.cml_kmeans_seg_slot_ints(plan.seg_grid)), 1), dtype=torch.int32, device=device)
+    return sl, sc
+
+
 def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tensor, rank: torch.Tensor,
                     hist: torch.Tensor, aplan: AssignPlan, k: int, cost_part: torch.Tensor, off: torch.Tensor,
-                    seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor, stream=None) -> None:
-    """K10 regime B: counting sort by label, then segmented f64 sums -> msg."""
+                    seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor,
+                    slots: tuple, stream=None) -> None:
+    """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic)."""
     lib = _native.kernels()
     status = lib.cml_kmeans_sort_accum(x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(),
                                        hist.data_ptr(), aplan.grid, aplan.nwaves, k, aplan.kp,
                                        cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
                                        perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
-                                       _native.stream_ptr(stream))
+                                       slots[0].data_ptr(), slots[1].data_ptr(), _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
 
 

@@ -80,7 +80,17 @@ def test_assemble_matches_torch(out_dtype):
     assert torch.equal(gbad.cpu(), wbad)
     np.testing.assert_array_equal(np.isnan(got.double().cpu().numpy()), np.isnan(want.numpy()))
     ok = ~torch.isnan(want)
-    np.testing.assert_array_equal(got.double().cpu()[ok].numpy(), want.to(out_dtype).double()[ok].numpy())
+    g_ok, w_ok = got.double().cpu()[ok], want.to(out_dtype).double()[ok]
+    if out_dtype == torch.bfloat16:
+        # torch rounds f64 -> f32 -> bf16 (twice); the GPU conversion rounds once, so values within
+        # 2^-24 of a bf16 midpoint may land one ulp apart (always on the correctly rounded side).
+        diff = (g_ok - w_ok).abs()
+        ulp = w_ok.abs().clamp(min=1e-30) * 2.0 ** -7
+        assert (diff <= ulp * 1.01).all() and (diff > 0).float().mean() < 1e-3
+        exact = (want[ok] - g_ok).abs() <= (want[ok] - w_ok).abs()
+        assert exact.all()
+    else:
+        assert torch.equal(g_ok, w_ok)
 
 
 def test_binarize_and_metric_sums():

@@ -112,3 +112,23 @@ def test_sort_regime_handles_skew():
     want = x.double().mean(0).cpu().numpy()
     np.testing.assert_allclose(eng.centers[0].cpu().numpy(), want, rtol=1e-6, atol=1e-9)
     np.testing.assert_allclose(eng.centers[1:].cpu().numpy(), init[1:])
+
+
+@pytest.mark.parametrize("n,d,k", [(200_000, 64, 7), (123_457, 256, 256), (50_000, 16, 1)])
+def test_sort_regime_bitwise_deterministic(n, d, k):
+    """Atomic-free segmented sums: two identical steps give bitwise-identical messages, and the
+    sums match the float64 reference (clusters spanning many slices exercise the fixup)."""
+    torch.manual_seed(4)
+    x = (torch.randn(n, d, device="cuda") * 2).to(torch.bfloat16)
+    init = x[:k].double().cpu().numpy()
+    msgs = []
+    for _ in range(2):
+        eng = LloydEngine(x, d, k, accum_mode="sort")
+        eng.set_centers(init)
+        eng.step()
+        torch.cuda.synchronize()
+        msgs.append(eng.msgs[0].clone())
+    assert torch.equal(msgs[0], msgs[1])
+    lab = eng.labels[:n].cpu().long()
+    sums, counts = K.sums_reference(x.double().cpu(), lab, k)
+    np.testing.assert_allclose(msgs[0][:k * d].cpu().numpy(), sums.reshape(-1).numpy(), rtol=1e-9, atol=1e-6)
