@@ -12,6 +12,7 @@ from typing import Any, Dict, List, Optional, Union
 import torch
 
 from .param import Params
+from ..utils.trace import trace
 from .util import MLReadable, MLWritable
 
 
@@ -20,7 +21,8 @@ class Transformer(Params, MLWritable, MLReadable):
         inst = self.copy(params) if params else self
         if dataset.isStreaming:
             return dataset._lazy("_apply_transformer", inst)
-        return inst._transform(dataset)
+        with trace(f"{type(self).__name__}.transform"):
+            return inst._transform(dataset)
 
     def _transform(self, dataset):
         raise NotImplementedError
@@ -33,7 +35,8 @@ class Estimator(Params, MLWritable, MLReadable):
         if dataset.isStreaming:
             raise RuntimeError("fit() on a streaming DataFrame: use writeStream.foreachBatch to train per batch")
         inst = self.copy(params) if params else self
-        model = inst._fit(dataset)
+        with trace(f"{type(self).__name__}.fit"):
+            model = inst._fit(dataset)
         if model is not None and getattr(model, "parent", None) is None:
             model.parent = inst
             model.uid = inst.uid  # Spark models carry their estimator's uid
@@ -63,7 +66,8 @@ class Model(Transformer):
 class Evaluator(Params, MLWritable, MLReadable):
     def evaluate(self, dataset, params: Optional[Dict] = None) -> float:
         inst = self.copy(params) if params else self
-        return inst._evaluate(dataset)
+        with trace(f"{type(self).__name__}.evaluate"):
+            return inst._evaluate(dataset)
 
     def _evaluate(self, dataset) -> float:
         raise NotImplementedError

@@ -15,6 +15,7 @@ import numpy as np
 import torch
 
 from ..models.kmeans import LloydEngine
+from ..utils import checkpoint as ckpt
 from ..sql import types as T
 from ..sql.column import ColumnData
 from . import util as U
@@ -67,7 +68,20 @@ class KMeans(Estimator):
         comm = df._comm
         seed = int(self.getSeed())
         eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids)
-        if self.getInitMode() == "random":
+        conf = df._session.conf
+        ckdir = conf.get("cml.ml.checkpointDir", None)
+        every = int(conf.get("cml.ml.checkpointInterval", 10))
+        n_global = int(comm.sum_scalar(float(eng.n)))
+        ckkey = (f"kmeans|n={n_global}|d={d}|k={k}|seed={seed}|init={self.getInitMode()}|"
+                 f"steps={self.getInitSteps()}|tol={self.getTol()}")
+        resumed = ckpt.load(ckdir, f"kmeans-{self.uid}", ckkey) if ckdir else None
+        start = 0
+        if resumed is not None:
+            start, arrs = resumed
+            init = arrs["centers"]
+            if init.shape[0] < k:
+                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids)
+        elif self.getInitMode() == "random":
             init = eng.init_random(seed)
         else:
             init = eng.init_kmeans_parallel(seed, self.getInitSteps())
@@ -76,7 +90,15 @@ class KMeans(Estimator):
                 init = init[:k_eff]
                 eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids)
         eng.set_centers(init)
-        iters = eng.fit(self.getMaxIter(), self.getTol())
+
+        def on_iter(it):
+            if ckdir and (it % max(every, 1) == 0):
+                ckpt.save(ckdir, f"kmeans-{self.uid}", ckkey, it, {"centers": eng.centers.cpu().numpy()}, comm)
+
+        iters = eng.fit(self.getMaxIter(), self.getTol(), start_iter=start, on_iter=on_iter)
+        if ckdir:
+            comm.barrier()
+            ckpt.clear(ckdir, f"kmeans-{self.uid}", comm)
         centers = eng.centers.cpu().numpy()
         labels, dist = eng.assign()
         sizes = torch.bincount(labels.long(), minlength=eng.k).to(torch.float64) if eng.n else torch.zeros(

@@ -118,6 +118,8 @@ def write_metadata(instance, path: str, extra: Optional[Dict[str, Any]] = None, 
     with open(os.path.join(d, "part-00000"), "w") as fh:
         fh.write(json.dumps(md, separators=(",", ":")) + "\n")
     open(os.path.join(d, "_SUCCESS"), "w").close()
+    from ..utils.fault import maybe_fail
+    maybe_fail("ml.save")  # crash point: metadata written, data not yet
 
 
 def read_metadata(path: str) -> Dict[str, Any]:
@@ -216,18 +218,38 @@ class MLWriter:
         return self
 
     def save(self, path: str) -> None:
+        """Crash-consistent save: the model is written into a sibling temp directory and renamed
+        into place, so a failure mid-save never leaves a half-written model and,
+        with overwrite, the previous model survives until the new one is complete."""
         from ..io.reader import strip_scheme
-        path = strip_scheme(path)
+        path = strip_scheme(path).rstrip("/")
         comm = _comm()
         if os.path.exists(path) and not self._overwrite:
             raise FileExistsError(f"Path {path} already exists. To overwrite it, use write().overwrite().save(path)")
         comm.barrier()
+        err = None
         if comm.is_root:
-            if os.path.exists(path):
-                shutil.rmtree(path)
-            os.makedirs(path, exist_ok=True)
-            self.instance._save_impl(path)
+            parent = os.path.dirname(os.path.abspath(path))
+            os.makedirs(parent, exist_ok=True)
+            tmp = os.path.join(parent, f".{os.path.basename(path)}.tmp-{os.getpid()}")
+            if os.path.exists(tmp):
+                shutil.rmtree(tmp)
+            os.makedirs(tmp)
+            try:
+                self.instance._save_impl(tmp)
+                if os.path.exists(path):
+                    old = os.path.join(parent, f".{os.path.basename(path)}.old-{os.getpid()}")
+                    os.replace(path, old)
+                    os.replace(tmp, path)
+                    shutil.rmtree(old, ignore_errors=True)
+                else:
+                    os.replace(tmp, path)
+            except BaseException as e:  # keep the previous model; drop the partial one
+                shutil.rmtree(tmp, ignore_errors=True)
+                err = e
         comm.barrier()
+        if err is not None:
+            raise err
 
 
 class MLWritable:

@@ -30,6 +30,8 @@ from ..ops import kmeans_ops as K
 from ..parallel.comm import Communicator, local_comm
 from ..utils import rng
 from ..utils.device import padded_dim, round_up
+from ..utils.fault import maybe_fail
+from ..utils.trace import trace
 
 
 def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
@@ -192,11 +194,17 @@ class LloydEngine:
             return False
         return bool((self._shift2 <= tol * tol).all().item())
 
-    def fit(self, max_iter: int, tol: float) -> int:
-        it = 0
+    def fit(self, max_iter: int, tol: float, start_iter: int = 0, on_iter=None) -> int:
+        """Lloyd iterations until every centre moves <= tol or max_iter. ``start_iter`` resumes a
+        checkpointed fit; ``on_iter(it)`` runs after each iteration (checkpoint hook)."""
+        it = start_iter
         while it < max_iter:
-            self.step()
+            maybe_fail("kmeans.iteration", it)  # crash point (SURVEY.md §5.3 "mid-iteration k")
+            with trace("kmeans.step"):
+                self.step()
             it += 1
+            if on_iter is not None:
+                on_iter(it)
             if tol > 0 and self.converged(tol):
                 break
         return it

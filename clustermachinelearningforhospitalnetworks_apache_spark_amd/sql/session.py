@@ -113,7 +113,11 @@ class SparkSession:
         self._kind = kind
         if kind == "local" and n:
             torch.set_num_threads(max(1, n))
-        self._comm = Communicator.from_env(want_gpu=(kind == "gpu"))
+        # collective watchdog: a rank that stops participating fails the job after the timeout
+        # instead of hanging it; RCCL errors surface asynchronously as exceptions
+        os.environ.setdefault("TORCH_NCCL_ASYNC_ERROR_HANDLING", "1")
+        self._comm = Communicator.from_env(want_gpu=(kind == "gpu"),
+                                           timeout_s=float(opts.get("cml.comm.timeoutSeconds", 600)))
         if kind == "gpu" and not self._comm.device.type == "cuda":
             log.warning("master=%s requested GPUs but none is visible; running on CPU", opts.get("spark.master"))
         self._device = self._comm.device

@@ -25,6 +25,9 @@ from __future__ import annotations
 
 import json
 import logging
+
+from ..utils.fault import maybe_fail
+from ..utils.trace import trace
 import os
 import re
 import threading
@@ -370,7 +373,12 @@ class StreamingQuery:
             self._watermark_ms = max(self._watermark_ms, gmax // 1000 - parse_interval_ms(delay))
 
     def _run_batch(self, plan) -> dict:
+        with trace("stream.batch"):
+            return self._run_batch_impl(plan)
+
+    def _run_batch_impl(self, plan) -> dict:
         bid, files, ts_ms, wm_ms, replay = plan
+        maybe_fail("stream.after_offsets", bid)  # crash point: batch planned (offsets logged), nothing written
         t0 = time.time()
         self._watermark_ms = max(self._watermark_ms, wm_ms)
         df = self._read_batch(files, ts_ms)
@@ -390,8 +398,8 @@ class StreamingQuery:
                 from ..io import table as tbl
                 if tbl.committed_txn(self._path, self.id) < bid:
                     tbl.write_frame(df, self._path, "append", "STREAMING UPDATE", {"appId": self.id, "version": bid})
-            else:
-                df.write.mode("append").format(fmt).save(os.path.join(self._path, f"batch={bid}"))
+            else:  # one directory per batch, overwritten on replay: idempotent
+                df.write.mode("overwrite").format(fmt).save(os.path.join(self._path, f"batch={bid}"))
         elif w._format == "console" and self._foreach_batch_absent():
             if self._session._comm.is_root:
                 print(f"-------------------------------------------\nBatch: {bid}\n"
@@ -406,6 +414,7 @@ class StreamingQuery:
         self._advance_watermark(df)
         comm = self._session._comm
         comm.barrier()
+        maybe_fail("stream.before_commit", bid)  # crash point: sink done, commit not yet logged
         if comm.is_root:
             self._write_json("commits", bid, {"nextBatchWatermarkMs": self._watermark_ms})
         prog = {"id": self.id, "runId": self.runId, "name": self.name, "batchId": bid, "numInputRows": nrows,
