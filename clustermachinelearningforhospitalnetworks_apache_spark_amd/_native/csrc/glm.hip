@@ -155,91 +155,206 @@ __global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __res
   }
 }
 
-// ---------------------------------------------------------------------------- K8 scale
-template <typename TI, typename TO>
-__global__ void scale_apply_kernel(const TI* __restrict__ X, long long n, long long ldx, int d,
-                                   const double* __restrict__ mean, const double* __restrict__ inv_std, int with_mean,
-                                   TO* __restrict__ Y, long long ldy, int dpad) {
-  const long long total = n * (long long)dpad;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
-       i += (long long)gridDim.x * blockDim.x) {
-    const long long r = i / dpad;
-    const int c = (int)(i - r * dpad);
-    double v = 0.0;
-    if (c < d) {
-      double x;
-      if constexpr (sizeof(TI) == 2) x = (double)bf16_to_f32(((const u16*)X)[r * ldx + c]);
-      else x = (double)X[r * ldx + c];
-      v = (with_mean ? x - mean[c] : x) * inv_std[c];
+// ---------------------------------------------------------------------------- row streaming
+// Streaming kernels below use one layout: a row is split into 16-byte chunks; LPR lanes (power of
+// two) share a row and each owns NCH chunks, chunk k of lane li being row chunk k·LPR + li. One
+// load instruction therefore covers LPR·16 contiguous bytes of each of 64/LPR rows (>= 128 B per
+// row once LPR >= 8: the full-rate shape on MI355X, profiles/README.md). Compute type CT is f32
+// for bf16/f32 data (packed FMAs, v_exp_f32) and f64 for f64 data; every accumulation that
+// spans rows is f64.
+template <typename T> struct CompT { using type = float; };
+template <> struct CompT<double> { using type = double; };
+
+template <typename T, typename CT>
+__device__ inline void load_chunk_ct(const T* X, long long row, long long ld, int c0, int d, CT* v) {
+  constexpr int CPT = Elt<T>::CPT;
+  if (c0 + CPT <= d) {
+    if constexpr (sizeof(T) == 2) {
+      const uint4 w = *reinterpret_cast<const uint4*>(X + row * ld + c0);
+      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[2 * q] = __uint_as_float(ws[q] << 16);
+        v[2 * q + 1] = __uint_as_float(ws[q] & 0xffff0000u);
+      }
+    } else if constexpr (sizeof(T) == 4) {
+      const float4 w = *reinterpret_cast<const float4*>(X + row * ld + c0);
+      v[0] = w.x; v[1] = w.y; v[2] = w.z; v[3] = w.w;
+    } else {
+      const double2 w = *reinterpret_cast<const double2*>(X + row * ld + c0);
+      v[0] = w.x; v[1] = w.y;
     }
-    if constexpr (sizeof(TO) == 2) ((u16*)Y)[r * ldy + c] = f32_to_bf16((float)v);
-    else Y[r * ldy + c] = (TO)v;
+  } else {
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      CT t = 0;
+      if (c0 + j < d) {
+        if constexpr (sizeof(T) == 2) t = bf16_to_f32(((const u16*)X)[row * ld + c0 + j]);
+        else t = (CT)X[row * ld + c0 + j];
+      }
+      v[j] = t;
+    }
   }
 }
 
-// ---------------------------------------------------------------------------- K13 logistic gradient
-template <typename T, int NCH>
-__global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
-    const T* __restrict__ X, long long n, long long ld, int d, int lpr, const double* __restrict__ y,
-    const double* __restrict__ wt, const double* __restrict__ coef /*[d+1], last = intercept*/,
-    double* __restrict__ out /*[grid][d + 3]: grad (d), grad_b, loss, weight sum*/) {
-  constexpr int CPT = Elt<T>::CPT;
+template <typename CT>
+__device__ inline CT group_sum_ct(CT v, int lpr) {
+  for (int o = lpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+  return v;
+}
+
+__device__ inline float sigmoid_ct(float m) { return 1.f / (1.f + __expf(-m)); }
+__device__ inline double sigmoid_ct(double m) {
+  const double e = exp(-fabs(m));
+  return m >= 0 ? 1.0 / (1.0 + e) : e / (1.0 + e);
+}
+__device__ inline float softplus_ct(float m) { return fmaxf(m, 0.f) + __logf(1.f + __expf(-fabsf(m))); }
+__device__ inline double softplus_ct(double m) { return fmax(m, 0.0) + log1p(exp(-fabs(m))); }
+
+// ---------------------------------------------------------------------------- K8 scale
+template <typename TI, typename TO, int NCH>
+__global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __restrict__ X, long long n, long long ldx,
+                                                                  int d, int lpr, const double* __restrict__ mean,
+                                                                  const double* __restrict__ inv_std, int with_mean,
+                                                                  TO* __restrict__ Y, long long ldy, int dpad) {
+  using CT = typename CompT<TO>::type;
+  constexpr int CPT = Elt<TI>::CPT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
-  double w[NCH][CPT], g[NCH][CPT];
+  CT mu[NCH][CPT], is[NCH][CPT];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < CPT; ++j) {
       const int col = (c * lpr + li) * CPT + j;
-      w[c][j] = col < d ? coef[col] : 0.0;
-      g[c][j] = 0.0;
+      mu[c][j] = (col < d && with_mean) ? (CT)mean[col] : (CT)0;
+      is[c][j] = col < d ? (CT)inv_std[col] : (CT)0;
     }
-  const double b = coef[d];
+  const long long step = (long long)gridDim.x * nw * rpw;
+  const bool vec_ok = ((ldy * (long long)sizeof(TO)) % 16 == 0) && ((reinterpret_cast<size_t>(Y) & 15) == 0);
+  for (long long row = ((long long)blockIdx.x * nw + wave) * rpw + sub; row < n; row += step) {
+#pragma unroll
+    for (int c = 0; c < NCH; ++c) {
+      const int c0 = (c * lpr + li) * CPT;
+      if (c0 >= dpad) continue;
+      CT v[CPT];
+      if constexpr (sizeof(TI) == 8 && sizeof(TO) < 8) {
+        double t[CPT];
+        load_chunk_ct<TI, double>(X, row, ldx, c0, d, t);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) v[j] = (CT)((t[j] - (double)mu[c][j]) * (double)is[c][j]);
+      } else {
+        load_chunk_ct<TI, CT>(X, row, ldx, c0, d, v);
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) v[j] = (v[j] - mu[c][j]) * is[c][j];
+      }
+      TO* yp = Y + row * ldy + c0;
+      if (vec_ok && c0 + CPT <= dpad) {
+        if constexpr (sizeof(TO) == 2) {
+          unsigned w[CPT / 2];
+#pragma unroll
+          for (int q = 0; q < CPT / 2; ++q)
+            w[q] = (unsigned)f32_to_bf16((float)v[2 * q]) | ((unsigned)f32_to_bf16((float)v[2 * q + 1]) << 16);
+          if constexpr (CPT == 8) *reinterpret_cast<uint4*>(yp) = make_uint4(w[0], w[1], w[2], w[3]);
+          else if constexpr (CPT == 4) *reinterpret_cast<uint2*>(yp) = make_uint2(w[0], w[1]);
+          else *reinterpret_cast<unsigned*>(yp) = w[0];
+        } else {
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) yp[j] = (TO)v[j];
+        }
+      } else {
+        for (int j = 0; c0 + j < dpad && j < CPT; ++j) {
+          if constexpr (sizeof(TO) == 2) ((u16*)yp)[j] = f32_to_bf16((float)v[j]);
+          else yp[j] = (TO)v[j];
+        }
+      }
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- K13 logistic gradient
+// Per row group: margin m = x·w + b (CT), p = σ(m), r = wt·(p − y); the lane's chunk of r·x goes
+// into CT accumulators that are folded into f64 every FLUSH rows; loss and weights in f64.
+template <typename T, int NCH>
+__global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
+    const T* __restrict__ X, long long n, long long ld, int d, int lpr, const double* __restrict__ y,
+    const double* __restrict__ wt, const double* __restrict__ coef /*[d+1], last = intercept*/,
+    double* __restrict__ out /*[grid][d + 3]: grad (d), grad_b, loss, weight sum*/) {
+  using CT = typename CompT<T>::type;
+  constexpr int CPT = Elt<T>::CPT;
+  constexpr int FLUSH = 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
+  CT w[NCH][CPT], g[NCH][CPT];
+  double g64[NCH][CPT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int col = (c * lpr + li) * CPT + j;
+      w[c][j] = col < d ? (CT)coef[col] : (CT)0;
+      g[c][j] = 0;
+      g64[c][j] = 0.0;
+    }
+  const CT b = (CT)coef[d];
   double gb = 0.0, loss = 0.0, wsum = 0.0;
   const long long step = (long long)gridDim.x * nw * rpw;
+  int since = 0;
   for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += step) {
     const long long row = row0 + sub;
     const bool ok = row < n;
-    double v[NCH][CPT];
-    double m = 0.0;
+    CT v[NCH][CPT];
+    CT m = 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int c0 = (c * lpr + li) * CPT;
       if (ok && c0 < d) {
-        load_chunk<T>(X, row, ld, c0, d, v[c]);
+        load_chunk_ct<T, CT>(X, row, ld, c0, d, v[c]);
       } else {
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) v[c][j] = 0.0;
+        for (int j = 0; j < CPT; ++j) v[c][j] = 0;
       }
 #pragma unroll
       for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
     }
-    m = group_sum(m, lpr) + b;
+    m = group_sum_ct<CT>(m, lpr) + b;
     const double yi = ok ? y[row] : 0.0;
     const double wi = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
-    // p = sigmoid(m) and softplus(m), numerically stable
-    const double e = exp(-fabs(m));
-    const double p = m >= 0 ? 1.0 / (1.0 + e) : e / (1.0 + e);
-    const double sp = fmax(m, 0.0) + log1p(e);
-    const double r = wi * (p - yi);
+    const CT p = sigmoid_ct(m);
+    const CT r = (CT)wi * (p - (CT)yi);
 #pragma unroll
     for (int c = 0; c < NCH; ++c)
 #pragma unroll
       for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
     if (li == 0) {
-      gb += r;
-      loss += wi * (sp - yi * m);
+      gb += (double)r;
+      loss += wi * ((double)softplus_ct(m) - yi * (double)m);
       wsum += wi;
     }
+    if constexpr (sizeof(CT) == 4) {
+      if (++since == FLUSH) {
+        since = 0;
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) {
+            g64[c][j] += (double)g[c][j];
+            g[c][j] = 0;
+          }
+      }
+    }
   }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) g64[c][j] += (double)g[c][j];
   // reduce across row sub-groups, then across waves
   __shared__ double red[kGlmThreads / 64][64 * 8 + 3];
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < CPT; ++j)
-      for (int o = lpr; o < 64; o <<= 1) g[c][j] += __shfl_xor(g[c][j], o, 64);
+      for (int o = lpr; o < 64; o <<= 1) g64[c][j] += __shfl_xor(g64[c][j], o, 64);
   for (int o = 1; o < 64; o <<= 1) {
     gb += __shfl_xor(gb, o, 64);
     loss += __shfl_xor(loss, o, 64);
@@ -251,7 +366,7 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     __syncthreads();
     if (sub == 0)
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) red[wave][li * CPT + j] = g[c][j];
+      for (int j = 0; j < CPT; ++j) red[wave][li * CPT + j] = g64[c][j];
     if (lane == 0 && c == 0) {
       red[wave][64 * 8] = gb;
       red[wave][64 * 8 + 1] = loss;
@@ -279,26 +394,36 @@ __global__ __launch_bounds__(kGlmThreads) void linear_predict_kernel(const T* __
                                                                      long long ld, int d, int lpr,
                                                                      const double* __restrict__ coef, int link,
                                                                      double* __restrict__ out) {
+  using CT = typename CompT<T>::type;
   constexpr int CPT = Elt<T>::CPT;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
   const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
+  CT w[NCH][CPT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      const int col = (c * lpr + li) * CPT + j;
+      w[c][j] = col < d ? (CT)coef[col] : (CT)0;
+    }
+  const double b = coef[d];
   const long long step = (long long)gridDim.x * nw * rpw;
   for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += step) {
     const long long row = row0 + sub;
     const bool ok = row < n;
-    double m = 0.0;
+    CT m = 0;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int c0 = (c * lpr + li) * CPT;
       if (ok && c0 < d) {
-        double v[CPT];
-        load_chunk<T>(X, row, ld, c0, d, v);
+        CT v[CPT];
+        load_chunk_ct<T, CT>(X, row, ld, c0, d, v);
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) m = fma(v[j], c0 + j < d ? coef[c0 + j] : 0.0, m);
+        for (int j = 0; j < CPT; ++j) m = fma(v[j], w[c][j], m);
       }
     }
-    m = group_sum(m, lpr) + coef[d];
-    if (ok && li == 0) out[row] = link == 1 ? 1.0 / (1.0 + exp(-m)) : m;
+    const double mm = (double)group_sum_ct<CT>(m, lpr) + b;
+    if (ok && li == 0) out[row] = link == 1 ? sigmoid_ct(mm) : mm;
   }
 }
 
@@ -356,6 +481,89 @@ __global__ __launch_bounds__(256) void gram_kernel(const T* __restrict__ X, long
   }
 }
 
+// Small Gram (m = d + 2 <= 8, e.g. the reference's 4 features): one row per lane, the upper
+// triangle of a·aᵀ (a = √w·[x 1 y]) in m(m+1)/2 f64 registers, rows streamed straight from HBM;
+// lanes then waves reduced once per block.
+template <typename T, int M>
+__global__ __launch_bounds__(256) void gram_small_kernel(const T* __restrict__ X, long long n, long long ld, int d,
+                                                         const double* __restrict__ y,
+                                                         const double* __restrict__ wt,
+                                                         double* __restrict__ out /*[grid][M*M]*/) {
+  constexpr int NP = M * (M + 1) / 2;
+  double acc[NP];
+#pragma unroll
+  for (int q = 0; q < NP; ++q) acc[q] = 0.0;
+  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < n;
+       row += (long long)gridDim.x * blockDim.x) {
+    double a[M];
+    const double sw = wt != nullptr ? sqrt(wt[row]) : 1.0;
+#pragma unroll
+    for (int j = 0; j < M - 2; ++j) {
+      double v;
+      if constexpr (sizeof(T) == 2) v = (double)bf16_to_f32(((const u16*)X)[row * ld + j]);
+      else v = (double)X[row * ld + j];
+      a[j] = v * sw;
+    }
+    a[M - 2] = sw;
+    a[M - 1] = y[row] * sw;
+    int q = 0;
+#pragma unroll
+    for (int i = 0; i < M; ++i)
+#pragma unroll
+      for (int j = i; j < M; ++j) acc[q++] = fma(a[i], a[j], acc[q]);
+  }
+  __shared__ double red[256 / 64][NP];
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+#pragma unroll
+  for (int q = 0; q < NP; ++q) {
+    const double t = wave_sum_f64(acc[q]);
+    if (lane == 0) red[wave][q] = t;
+  }
+  __syncthreads();
+  for (int q = threadIdx.x; q < NP; q += blockDim.x) {
+    double t = 0.0;
+    for (int w = 0; w < (int)(blockDim.x >> 6); ++w) t += red[w][q];
+    int i = 0, rem = q;
+    while (rem >= M - i) { rem -= M - i; ++i; }
+    out[(long long)blockIdx.x * M * M + i * M + (i + rem)] = t;
+  }
+}
+
+template <typename T>
+int launch_gram_small(const void* X, long long n, long long ld, int d, const double* y, const double* wt,
+                      double* out, int grid, hipStream_t st) {
+  const T* x = (const T*)X;
+  switch (d + 2) {
+    case 2: hipLaunchKernelGGL((gram_small_kernel<T, 2>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 3: hipLaunchKernelGGL((gram_small_kernel<T, 3>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 4: hipLaunchKernelGGL((gram_small_kernel<T, 4>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 5: hipLaunchKernelGGL((gram_small_kernel<T, 5>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 6: hipLaunchKernelGGL((gram_small_kernel<T, 6>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 7: hipLaunchKernelGGL((gram_small_kernel<T, 7>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    case 8: hipLaunchKernelGGL((gram_small_kernel<T, 8>), dim3(grid), dim3(256), 0, st, x, n, ld, d, y, wt, out); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return cml_status();
+}
+
+// Streaming layout choice: ~16 columns per lane, power-of-two lanes per row.
+inline int pow2ceil(int v) {
+  int p = 1;
+  while (p < v) p <<= 1;
+  return p;
+}
+inline bool stream_layout(int d, int cpt, int& lpr, int& nch) {
+  const int ch = (d + cpt - 1) / cpt;
+  const int want = 16 / cpt > 0 ? 16 / cpt : 1;
+  nch = ch < want ? pow2ceil(ch) : want;
+  lpr = pow2ceil((ch + nch - 1) / nch);
+  if (lpr > 64) {
+    lpr = 64;
+    nch = pow2ceil((ch + 63) / 64);
+  }
+  return nch <= 8;
+}
+
 int pick_lpr(int d, int cpt, int nch) {
   int need = (d + cpt * nch - 1) / (cpt * nch);
   int l = 1;
@@ -401,9 +609,9 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
 
 CML_API int cml_glm_grid(long long n, int d, int dtype, int cap) {
   const int cpt = dtype == 0 ? 8 : dtype == 1 ? 4 : 2;
-  const int nch = pick_nch(d, cpt);
-  if (nch < 0) return -1;
-  const int lpr = pick_lpr(d, cpt, nch);
+  if (pick_nch(d, cpt) < 0) return -1;  // moments layout limit
+  int lpr, nch;
+  if (!stream_layout(d, cpt, lpr, nch)) return -1;
   const int rows = (kGlmThreads / 64) * (64 / lpr) * 16;
   return grid_for(n, rows, cap);
 }
@@ -427,18 +635,25 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
                             const double* inv_std, int with_mean, void* Y, long long ldy, int dpad, int out_dtype,
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
-  const long long total = n * (long long)dpad;
-  const int blocks = (int)((total + 255) / 256 < 8192 ? (total + 255) / 256 : 8192);
-  if (blocks == 0) return 0;
-#define CML_SCALE_OUT(TI)                                                                                          \
-  switch (out_dtype) {                                                                                             \
-    case 0: hipLaunchKernelGGL((scale_apply_kernel<TI, u16>), dim3(blocks), dim3(256), 0, st, (const TI*)X, n, ldx, \
-                               d, mean, inv_std, with_mean, (u16*)Y, ldy, dpad); break;                           \
-    case 1: hipLaunchKernelGGL((scale_apply_kernel<TI, float>), dim3(blocks), dim3(256), 0, st, (const TI*)X, n,    \
-                               ldx, d, mean, inv_std, with_mean, (float*)Y, ldy, dpad); break;                    \
-    case 2: hipLaunchKernelGGL((scale_apply_kernel<TI, double>), dim3(blocks), dim3(256), 0, st, (const TI*)X, n,   \
-                               ldx, d, mean, inv_std, with_mean, (double*)Y, ldy, dpad); break;                   \
-    default: return (int)hipErrorInvalidValue;                                                                     \
+  if (n <= 0) return 0;
+  const int cap = 256 * 8;
+#define CML_SCALE_LAUNCH(TI, TO)                                                                                  \
+  {                                                                                                               \
+    int lpr = 0;                                                                                                  \
+    int nch = 0;                                                                                                  \
+    if (!stream_layout(dpad, Elt<TI>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;                           \
+    const int grid = grid_for(n, (kGlmThreads / 64) * (64 / lpr) * 4, cap);                                       \
+    CML_NCH_SWITCH(nch, {                                                                                         \
+      hipLaunchKernelGGL((scale_apply_kernel<TI, TO, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const TI*)X, n, \
+                         ldx, d, lpr, mean, inv_std, with_mean, (TO*)Y, ldy, dpad);                              \
+    });                                                                                                           \
+  }
+#define CML_SCALE_OUT(TI)                                        \
+  switch (out_dtype) {                                           \
+    case 0: CML_SCALE_LAUNCH(TI, u16); break;                    \
+    case 1: CML_SCALE_LAUNCH(TI, float); break;                  \
+    case 2: CML_SCALE_LAUNCH(TI, double); break;                 \
+    default: return (int)hipErrorInvalidValue;                   \
   }
   switch (in_dtype) {
     case 0: CML_SCALE_OUT(u16); break;
@@ -447,6 +662,7 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_SCALE_OUT
+#undef CML_SCALE_LAUNCH
   return cml_status();
 }
 
@@ -454,9 +670,9 @@ CML_API int cml_logreg_grad(const void* X, long long n, long long ld, int d, int
                             const double* wt, const double* coef, double* out, int grid, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   CML_T_SWITCH(dtype, {
-    constexpr int CPT = Elt<T>::CPT;
-    const int nch = pick_nch(d, CPT);
-    const int lpr = pick_lpr(d, CPT, nch < 0 ? 8 : nch);
+    int lpr = 0;
+    int nch = 0;
+    if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
       hipLaunchKernelGGL((logreg_grad_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const T*)X, n, ld, d,
                          lpr, y, wt, coef, out);
@@ -469,9 +685,9 @@ CML_API int cml_linear_predict(const void* X, long long n, long long ld, int d, 
                                int link, double* out, int grid, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   CML_T_SWITCH(dtype, {
-    constexpr int CPT = Elt<T>::CPT;
-    const int nch = pick_nch(d, CPT);
-    const int lpr = pick_lpr(d, CPT, nch < 0 ? 8 : nch);
+    int lpr = 0;
+    int nch = 0;
+    if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
       hipLaunchKernelGGL((linear_predict_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const T*)X, n, ld,
                          d, lpr, coef, link, out);
@@ -484,6 +700,15 @@ CML_API int cml_gram(const void* X, long long n, long long ld, int d, int dtype,
                      double* out, int grid, void* stream) {
   if (d > 30) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  const int m = d + 2;
+  if (m <= 8) {
+    switch (dtype) {
+      case 0: return launch_gram_small<u16>(X, n, ld, d, y, wt, out, grid, st);
+      case 1: return launch_gram_small<float>(X, n, ld, d, y, wt, out, grid, st);
+      case 2: return launch_gram_small<double>(X, n, ld, d, y, wt, out, grid, st);
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
   CML_T_SWITCH(dtype, {
     hipLaunchKernelGGL((gram_kernel<T>), dim3(grid), dim3(256), 0, st, (const T*)X, n, ld, d, y, wt, out);
   });

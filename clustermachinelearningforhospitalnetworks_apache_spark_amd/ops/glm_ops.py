@@ -82,9 +82,7 @@ def scale_apply(x: torch.Tensor, d: int, mean: torch.Tensor, inv_std: torch.Tens
         if width > d:
             y = torch.nn.functional.pad(y, (0, width - d))
         return y.to(out_dtype)
-    xx = x if x.dtype in _CODE else x.to(torch.float64)
-    if xx.stride(1) != 1:
-        xx = xx.contiguous()
+    xx = _prep(x)
     out = torch.empty((n, width), dtype=out_dtype, device=x.device)
     if n == 0:
         return out
@@ -158,7 +156,7 @@ def gram(x: torch.Tensor, d: int, y: torch.Tensor, weight: Optional[torch.Tensor
     xx = x if x.dtype in _CODE else x.to(torch.float64)
     if xx.stride(1) != 1:
         xx = xx.contiguous()
-    grid = max(1, min((n + 4095) // 4096, num_cus(xx.device.index or 0) * 2))
+    grid = max(1, min((n + 2047) // 2048, num_cus(xx.device.index or 0) * 4))
     out = torch.zeros((grid, m * m), dtype=torch.float64, device=xx.device)
     yy = y.to(torch.float64).contiguous()
     ww = weight.to(torch.float64).contiguous() if weight is not None else None
