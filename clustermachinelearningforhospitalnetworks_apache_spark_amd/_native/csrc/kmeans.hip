@@ -63,20 +63,54 @@ struct AssignShape {
 
 // X fragments of one 16-row sub-tile: lane (row l&15, group g=l>>4) reads chunk 4s+g of its row,
 // so each load instruction covers 16 rows x 64 contiguous bytes.
-template <int DP>
-__device__ __forceinline__ void load_x16(const u16* __restrict__ X, long long n, long long ldx, long long row0,
+// F8 (OCP e4m3fn storage, half the bytes): one 16-byte load per lane covers TWO k-steps — step
+// 2t+h of lane (r,g) holds k = 64t + 16g + 8h + j — still 16 rows x 64 B per instruction; the
+// fp8 -> bf16 conversion is exact (e4m3 values are a subset of bf16) and runs once per X tile,
+// which is then reused against every centre tile. The centre fragments use the same k order.
+template <bool HI>
+__device__ __forceinline__ unsigned f8x2_to_bf16x2(unsigned w) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const f2 v = __builtin_amdgcn_cvt_pk_f32_fp8((int)w, HI);
+  return (__float_as_uint(v.x) >> 16) | (__float_as_uint(v.y) & 0xffff0000u);
+}
+
+template <int DP, bool F8>
+__device__ __forceinline__ void load_x16(const void* __restrict__ Xv, long long n, long long ldx, long long row0,
                                          int r, int g, bf16x8 (&xf)[AssignShape<DP>::KS]) {
-  constexpr int NCH = AssignShape<DP>::NCH;
+  constexpr int KS = AssignShape<DP>::KS;
   const long long row = row0 + r;
   const bool valid = row < n;
-  const u16* xp = X + (valid ? row : 0) * ldx;
+  if constexpr (F8) {
+    static_assert(DP >= 64, "fp8 rows are padded to >= 64 features");
+    const unsigned char* xp = reinterpret_cast<const unsigned char*>(Xv) + (valid ? row : 0) * ldx;
 #pragma unroll
-  for (int s = 0; s < AssignShape<DP>::KS; ++s) {
-    const int q = 4 * s + g;
-    u32x4 v = {0u, 0u, 0u, 0u};
-    if (q < NCH && valid) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xp + 8 * q));
-    xf[s] = __builtin_bit_cast(bf16x8, v);
+    for (int t = 0; t < KS / 2; ++t) {
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (valid) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xp + 64 * t + 16 * g));
+      const u32x4 lo = {f8x2_to_bf16x2<false>(v.x), f8x2_to_bf16x2<true>(v.x), f8x2_to_bf16x2<false>(v.y),
+                        f8x2_to_bf16x2<true>(v.y)};
+      const u32x4 hi = {f8x2_to_bf16x2<false>(v.z), f8x2_to_bf16x2<true>(v.z), f8x2_to_bf16x2<false>(v.w),
+                        f8x2_to_bf16x2<true>(v.w)};
+      xf[2 * t] = __builtin_bit_cast(bf16x8, lo);
+      xf[2 * t + 1] = __builtin_bit_cast(bf16x8, hi);
+    }
+  } else {
+    constexpr int NCH = AssignShape<DP>::NCH;
+    const u16* xp = reinterpret_cast<const u16*>(Xv) + (valid ? row : 0) * ldx;
+#pragma unroll
+    for (int s = 0; s < KS; ++s) {
+      const int q = 4 * s + g;
+      u32x4 v = {0u, 0u, 0u, 0u};
+      if (q < NCH && valid) v = __builtin_nontemporal_load(reinterpret_cast<const u32x4*>(xp + 8 * q));
+      xf[s] = __builtin_bit_cast(bf16x8, v);
+    }
   }
+}
+
+// first k of the 8 a lane of group g holds at MFMA step s (X and centre fragments agree)
+template <bool F8>
+__device__ __forceinline__ int frag_k0(int s, int g) {
+  return F8 ? 64 * (s >> 1) + 16 * g + 8 * (s & 1) : 32 * s + 8 * g;
 }
 
 template <int DP, int RT>
@@ -84,11 +118,11 @@ struct XTile {
   bf16x8 f[RT][AssignShape<DP>::KS];
 };
 
-template <int DP, int RT>
-__device__ __forceinline__ void load_xtile(const u16* __restrict__ X, long long n, long long ldx, long long tile,
+template <int DP, int RT, bool F8>
+__device__ __forceinline__ void load_xtile(const void* __restrict__ X, long long n, long long ldx, long long tile,
                                            int r, int g, XTile<DP, RT>& xt) {
 #pragma unroll
-  for (int t = 0; t < RT; ++t) load_x16<DP>(X, n, ldx, tile * (16 * RT) + 16 * t, r, g, xt.f[t]);
+  for (int t = 0; t < RT; ++t) load_x16<DP, F8>(X, n, ldx, tile * (16 * RT) + 16 * t, r, g, xt.f[t]);
 }
 
 // Centres live in LDS in FRAGMENT order: fragment (ct, s) is 64 lanes x 16 B contiguous, lane l
@@ -228,9 +262,9 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
 
 // NT threads; each wave owns super-tiles of RT x 16 rows. PF: the next super-tile's rows are in
 // flight while this one computes (double-buffered X registers).
-template <int DP, int RT, int NT, bool PF, int RINGMAX>
+template <int DP, int RT, int NT, bool PF, int RINGMAX, bool F8>
 __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
-    const u16* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
+    const void* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
     int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
     int* __restrict__ labels, float* __restrict__ best_io, int first, int last, double* __restrict__ cost_part,
     int* __restrict__ hist_out, int* __restrict__ rank_out) {
@@ -247,10 +281,10 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   for (int id = tid; id < nct * KS * 64; id += NT) {
     const int l = id & 63, f = id >> 6;  // fragment f = ct*KS + s
     const int ct = f / KS, st = f - ct * KS;
-    const int c = ct * 16 + (l & 15), q = 4 * st + (l >> 4);
+    const int c = ct * 16 + (l & 15), k0 = frag_k0<F8>(st, l >> 4);
     unsigned o[4] = {0u, 0u, 0u, 0u};
-    if (q < NCH) {
-      const uint4 v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + q * 8);
+    if (k0 < 8 * NCH) {
+      const uint4 v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + k0);
       const unsigned w[4] = {v.x, v.y, v.z, v.w};
 #pragma unroll
       for (int e = 0; e < 4; ++e) {  // x -2, exact: bf16 -> f32 -> bf16 round trip of a power-of-two scale
@@ -286,21 +320,21 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   long long tile = (long long)blockIdx.x * nwaves + wave;
   if constexpr (PF) {
     XTile<DP, RT> xa, xb;
-    if (tile < ntiles) load_xtile<DP, RT>(X, n, ldx, tile, r, g, xa);
+    if (tile < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xa);
     for (; tile < ntiles; tile += 2 * tw) {
       const long long t1 = tile + tw;
-      if (t1 < ntiles) load_xtile<DP, RT>(X, n, ldx, t1, r, g, xb);
+      if (t1 < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1, r, g, xb);
       assign_tile<DP, RT, RINGMAX>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, cost);
       if (t1 >= ntiles) break;
-      if (t1 + tw < ntiles) load_xtile<DP, RT>(X, n, ldx, t1 + tw, r, g, xa);
+      if (t1 + tw < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1 + tw, r, g, xa);
       assign_tile<DP, RT, RINGMAX>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, cost);
     }
   } else {
     for (; tile < ntiles; tile += tw) {
       XTile<DP, RT> xt;
-      load_xtile<DP, RT>(X, n, ldx, tile, r, g, xt);
+      load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xt);
       assign_tile<DP, RT, RINGMAX>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, cost);
     }
@@ -340,6 +374,38 @@ __global__ __launch_bounds__(256) void row_sqnorm_bf16(const u16* __restrict__ X
         const float lo = bf16_to_f32((u16)(w[q] & 0xffffu)), hi = bf16_to_f32((u16)(w[q] >> 16));
         s = fmaf(lo, lo, s);
         s = fmaf(hi, hi, s);
+      }
+    }
+#pragma unroll
+    for (int o = NCH / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+    if (c == 0 && row < n) out[row] = s;
+  }
+}
+
+// ||x_i||² of OCP e4m3fn rows (f32): NCH 16-byte chunks per row.
+template <int NCH>
+__global__ __launch_bounds__(256) void row_sqnorm_fp8(const unsigned char* __restrict__ X, long long n, long long ldx,
+                                                      float* __restrict__ out) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int RPW = 64 / NCH;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / NCH, c = lane - sub * NCH;
+  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW) {
+    const long long row = r0 + sub;
+    float s = 0.f;
+    if (row < n) {
+      const uint4 v = *reinterpret_cast<const uint4*>(X + row * ldx + 16 * c);
+      const unsigned w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], false);
+        const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], true);
+        s = fmaf(a.x, a.x, s);
+        s = fmaf(a.y, a.y, s);
+        s = fmaf(b.x, b.x, s);
+        s = fmaf(b.y, b.y, s);
       }
     }
 #pragma unroll
@@ -557,6 +623,30 @@ __device__ __forceinline__ void add_raw(double (&acc)[CPL], const typename RawCo
   }
 }
 
+// OCP e4m3fn rows: CPL bytes per lane.
+template <int CPL> struct RawCols8;
+template <> struct RawCols8<4> { using T = unsigned; };
+template <> struct RawCols8<8> { using T = uint2; };
+template <> struct RawCols8<16> { using T = uint4; };
+
+template <int CPL>
+__device__ __forceinline__ void add_raw8(double (&acc)[CPL], const typename RawCols8<CPL>::T& w) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const unsigned* ws = reinterpret_cast<const unsigned*>(&w);
+#pragma unroll
+  for (int q = 0; q < CPL / 4; ++q) {
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], false);
+    const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], true);
+    acc[4 * q] += (double)a.x;
+    acc[4 * q + 1] += (double)a.y;
+    acc[4 * q + 2] += (double)b.x;
+    acc[4 * q + 3] += (double)b.y;
+  }
+}
+
+template <int CPL, bool F8> struct SegRaw { using T = typename RawCols<CPL>::T; };
+template <int CPL> struct SegRaw<CPL, true> { using T = typename RawCols8<CPL>::T; };
+
 // Sort regime, pass 4: segmented sum over the label-sorted order. Wave w streams sorted
 // positions [w*chunk, (w+1)*chunk): ONE vector load fetches the next U row ids, U whole-row
 // gathers (CPL*2 bytes per lane) are in flight, the running sum stays in f64 registers, and
@@ -567,14 +657,16 @@ __device__ __forceinline__ void add_raw(double (&acc)[CPL], const typename RawCo
 // in earlier slices) goes to slot A[w], its last (may continue in later slices) to slot B[w];
 // kmeans_seg_fixup adds the slots in ascending wave order. The result is bitwise identical
 // run to run (SURVEY.md §5.2 deterministic-reduction mode, here the only mode).
-template <int CPL>
-__global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restrict__ X, long long n, long long ldx,
+template <int CPL, bool F8>
+__global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k, long long chunk,
                                                              double* __restrict__ msg, double* __restrict__ slots,
                                                              int* __restrict__ slot_c) {
-  using raw_t = typename RawCols<CPL>::T;
+  using raw_t = typename SegRaw<CPL, F8>::T;
   constexpr int U = 16;
+  const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
+  constexpr int ESZ = F8 ? 1 : 2;  // bytes per element
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (kSegThreads / 64) + (threadIdx.x >> 6);
   const long long p0 = wave * chunk;
@@ -610,7 +702,7 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restri
     for (int u = 0; u < U; ++u) {
       const long long row = __builtin_amdgcn_readlane(pr, u);
       if (u < cnt && active) {
-        w[u] = *reinterpret_cast<const raw_t*>(X + row * ldx + col);
+        w[u] = *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ);
       } else {
         w[u] = raw_t{};
       }
@@ -618,14 +710,20 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const u16* __restri
     const long long pe = p + cnt;
     if (next >= pe) {
 #pragma unroll
-      for (int u = 0; u < U; ++u) add_raw<CPL>(acc, w[u]);
+      for (int u = 0; u < U; ++u) {
+        if constexpr (F8) add_raw8<CPL>(acc, w[u]);
+        else add_raw<CPL>(acc, w[u]);
+      }
     } else {
       long long s0 = p;
       while (true) {
         const long long se = next < pe ? next : pe;
 #pragma unroll
         for (int u = 0; u < U; ++u)
-          if (p + u >= s0 && p + u < se) add_raw<CPL>(acc, w[u]);
+          if (p + u >= s0 && p + u < se) {
+            if constexpr (F8) add_raw8<CPL>(acc, w[u]);
+            else add_raw<CPL>(acc, w[u]);
+          }
         if (se < next) break;  // chunk ends inside cluster c
         {
           double* dst = nflush == 0 ? slotA : msg + (long long)c * D;  // later clusters are ours alone
@@ -743,17 +841,17 @@ long long assign_lds_bytes(int kc, int kp, int Dp) {
 int g_assign_variant = 0;
 inline int assign_threads(int /*DS*/) { return 512; }
 
-template <int DP>
+template <int DP, bool F8>
 const void* assign_kernel_ptr() {
   constexpr bool PF = AssignShape<DP>::KS <= 8;
   constexpr int RT_BIG = DP >= 512 ? 2 : 4;
   switch (g_assign_variant) {
-    case 1: return (const void*)kmeans_assign_bf16<DP, 2, 512, PF, 4>;
-    case 2: return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4>;
-    case 3: return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, 2>;
+    case 1: return (const void*)kmeans_assign_bf16<DP, 2, 512, PF, 4, F8>;
+    case 2: return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
+    case 3: return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, 2, F8>;
     default:
-      if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2>;
-      else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4>;
+      if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8>;
+      else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
   }
 }
 
@@ -768,22 +866,22 @@ inline int assign_tile_rows(int Dp) {
   }
 }
 
-template <int DP>
+template <int DP, bool F8>
 int assign_occupancy(int kc, int kp) {
   const size_t lds = (size_t)assign_lds_bytes(kc, kp, DP);
-  const void* fn = assign_kernel_ptr<DP>();
+  const void* fn = assign_kernel_ptr<DP, F8>();
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   int nb = 0;
   hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, fn, assign_threads(0), lds);
   return nb;
 }
 
-template <int DP>
-int launch_assign(const u16* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp,
+template <int DP, bool F8>
+int launch_assign(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp,
                   int c_base, const float* cnorm, const float* xnorm, int* labels, float* best, int first, int last,
                   double* cost_part, int* hist, int* rank, int grid, hipStream_t st) {
   const size_t lds = (size_t)assign_lds_bytes(kc, kp, DP);
-  const void* fn = assign_kernel_ptr<DP>();
+  const void* fn = assign_kernel_ptr<DP, F8>();
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   void* args[] = {(void*)&X, (void*)&n, (void*)&ldx, (void*)&C, (void*)&ldc, (void*)&kc, (void*)&kp,
                   (void*)&c_base, (void*)&cnorm, (void*)&xnorm, (void*)&labels, (void*)&best, (void*)&first,
@@ -813,14 +911,23 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
 CML_API long long cml_kmeans_assign_lds_bytes(int kc, int kp, int Dp) { return assign_lds_bytes(kc, kp, Dp); }
 CML_API int cml_kmeans_assign_threads(int Dp) { return assign_threads(Dp / 16); }
 // Resident workgroups per CU of the assign kernel for this shape (persistent-grid sizing).
-CML_API int cml_kmeans_assign_occupancy(int Dp, int kc, int kp) {
+CML_API int cml_kmeans_assign_occupancy(int Dp, int kc, int kp, int xfp8) {
+  if (xfp8) {
+    switch (Dp) {
+      case 64: return assign_occupancy<64, true>(kc, kp);
+      case 128: return assign_occupancy<128, true>(kc, kp);
+      case 256: return assign_occupancy<256, true>(kc, kp);
+      case 512: return assign_occupancy<512, true>(kc, kp);
+      default: return 0;
+    }
+  }
   switch (Dp / 16) {
-    case 1: return assign_occupancy<16>(kc, kp);
-    case 2: return assign_occupancy<32>(kc, kp);
-    case 4: return assign_occupancy<64>(kc, kp);
-    case 8: return assign_occupancy<128>(kc, kp);
-    case 16: return assign_occupancy<256>(kc, kp);
-    case 32: return assign_occupancy<512>(kc, kp);
+    case 1: return assign_occupancy<16, false>(kc, kp);
+    case 2: return assign_occupancy<32, false>(kc, kp);
+    case 4: return assign_occupancy<64, false>(kc, kp);
+    case 8: return assign_occupancy<128, false>(kc, kp);
+    case 16: return assign_occupancy<256, false>(kc, kp);
+    case 32: return assign_occupancy<512, false>(kc, kp);
     default: return 0;
   }
 }
@@ -833,31 +940,61 @@ CML_API int cml_kmeans_accum_threads() { return kAccumThreads; }
 CML_API int cml_kmeans_seg_threads() { return kSegThreads; }
 CML_API long long cml_kmeans_seg_ints(int k) { return (long long)(k + 1) + ((k + 1) & 1) + 2LL * k + 2; }
 
-// X: bf16 [n, ldx] (Dp = 16*DS used columns, zero padded). C: bf16 [kc, ldc] (kc % 32 == 0).
+// X: bf16 [n, ldx] (Dp = 16*DS used columns, zero padded), or with xfp8 OCP e4m3fn bytes [n, ldx]
+// (Dp in {64,...,512}, ldx bytes, 16-B aligned rows). C: bf16 [kc, ldc] (kc % 16 == 0).
 // hist/rank may be null; when given (last chunk only) hist is [grid][kp] and rank is [n].
-// xnorm (f32 [n], cml_row_sqnorm_bf16) is required: it seeds the MFMA accumulators.
+// xnorm (f32 [n], cml_row_sqnorm_*) is required: it seeds the MFMA accumulators.
 // best may be null on a single-chunk (first && last) launch: only labels/cost are produced.
 CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, int Dp, const void* C, long long ldc,
                                    int kc, int kp, int c_base, const float* cnorm, const float* xnorm, int* labels,
                                    float* best, int first, int last, double* cost_part, int* hist, int* rank,
-                                   int grid, void* stream) {
-  if (kc % 16 != 0 || Dp % 16 != 0 || ldx % 8 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+                                   int grid, int xfp8, void* stream) {
+  if (kc % 16 != 0 || Dp % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if ((hist == nullptr) != (rank == nullptr)) return (int)hipErrorInvalidValue;
   if (best == nullptr && !(first && last)) return (int)hipErrorInvalidValue;
   if (xnorm == nullptr) return (int)hipErrorInvalidValue;  // ||x||² seeds the accumulators
   hipStream_t st = (hipStream_t)stream;
-  const u16* x = (const u16*)X;
   const u16* c = (const u16*)C;
+  if (xfp8) {
+    switch (Dp) {
+#define CML_ASSIGN8(DP)                                                                                          \
+  case DP:                                                                                                       \
+    return launch_assign<DP, true>(X, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last,  \
+                                   cost_part, hist, rank, grid, st)
+      CML_ASSIGN8(64); CML_ASSIGN8(128); CML_ASSIGN8(256); CML_ASSIGN8(512);
+#undef CML_ASSIGN8
+      default: return (int)hipErrorInvalidValue;
+    }
+  }
 #define CML_ASSIGN(DS, DP)                                                                                       \
   case DS:                                                                                                       \
-    return launch_assign<DP>(x, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last,        \
-                                 cost_part, hist, rank, grid, st)
+    return launch_assign<DP, false>(X, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last, \
+                                    cost_part, hist, rank, grid, st)
   switch (Dp / 16) {
     CML_ASSIGN(1, 16); CML_ASSIGN(2, 32); CML_ASSIGN(4, 64); CML_ASSIGN(8, 128); CML_ASSIGN(16, 256);
     CML_ASSIGN(32, 512);
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_ASSIGN
+}
+
+CML_API int cml_row_sqnorm_fp8(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
+  if (Dp % 64 != 0 || Dp > 1024 || ldx % 16 != 0) return (int)hipErrorInvalidValue;
+  const unsigned char* x = (const unsigned char*)X;
+  hipStream_t st = (hipStream_t)stream;
+  const long long rows_per_block = 4LL * (64 / (Dp / 16));
+  const long long blocks = std::min<long long>((n + rows_per_block - 1) / rows_per_block, 256LL * 16);
+  const dim3 g((unsigned)std::max<long long>(blocks, 1));
+  switch (Dp / 16) {
+    case 4: hipLaunchKernelGGL(row_sqnorm_fp8<4>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 8: hipLaunchKernelGGL(row_sqnorm_fp8<8>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 16: hipLaunchKernelGGL(row_sqnorm_fp8<16>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 32: hipLaunchKernelGGL(row_sqnorm_fp8<32>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    case 64: hipLaunchKernelGGL(row_sqnorm_fp8<64>, g, dim3(256), 0, st, x, n, ldx, out); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+  return cml_status();
 }
 
 CML_API int cml_row_sqnorm_bf16(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
@@ -911,7 +1048,7 @@ CML_API int cml_kmeans_reduce(const float* slab, const int* cslab, const double*
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                   const int* rank, const int* hist, int nblk, int nwaves, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
-                                  int seg_grid, double* msg, double* slots, int* slot_c, void* stream) {
+                                  int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   long long* tot = reinterpret_cast<long long*>(seg + k + 1 + ((k + 1) & 1));  // scratch after seg (8-B aligned)
   hipMemsetAsync(msg, 0, sizeof(double) * (size_t)k * D, st);
@@ -929,16 +1066,27 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
   if (e) return e;
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
   const long long chunk = (n + waves - 1) / waves;
-  const u16* x = (const u16*)X;
-  if (cpl == 2)
-    hipLaunchKernelGGL(kmeans_segacc<2>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg, slots, slot_c);
+  if (xfp8) {
+    if (cpl == 4)
+      hipLaunchKernelGGL((kmeans_segacc<4, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                         seg, k, chunk, msg, slots, slot_c);
+    else if (cpl == 8)
+      hipLaunchKernelGGL((kmeans_segacc<8, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                         seg, k, chunk, msg, slots, slot_c);
+    else if (cpl == 16)
+      hipLaunchKernelGGL((kmeans_segacc<16, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                         seg, k, chunk, msg, slots, slot_c);
+    else
+      return (int)hipErrorInvalidValue;
+  } else if (cpl == 2)
+    hipLaunchKernelGGL((kmeans_segacc<2, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                       seg, k, chunk, msg, slots, slot_c);
   else if (cpl == 4)
-    hipLaunchKernelGGL(kmeans_segacc<4>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg, slots, slot_c);
+    hipLaunchKernelGGL((kmeans_segacc<4, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                       seg, k, chunk, msg, slots, slot_c);
   else if (cpl == 8)
-    hipLaunchKernelGGL(kmeans_segacc<8>, dim3(seg_grid), dim3(kSegThreads), 0, st, x, n, ldx, Dp, D, perm, seg, k,
-                       chunk, msg, slots, slot_c);
+    hipLaunchKernelGGL((kmeans_segacc<8, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
+                       seg, k, chunk, msg, slots, slot_c);
   else
     return (int)hipErrorInvalidValue;
   e = cml_status();

@@ -34,9 +34,22 @@ from ..utils.fault import maybe_fail
 from ..utils.trace import trace
 
 
+def padded_dim_fp8(d: int) -> int:
+    """fp8 rows: >= 256 bytes, power of two (16-B loads covering two MFMA k-steps, sort-regime lanes)."""
+    return max(256, 1 << max(0, (d - 1).bit_length()))
+
+
 def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
-    """bf16 [n, dp] zero-padded copy of a GPU feature matrix (dp = padded_dim(d))."""
+    """Zero-padded GPU copy of a feature matrix in the kernels' layout: bf16 [n, padded_dim(d)], or
+    OCP e4m3fn [n, padded_dim_fp8(d)] when the features already are fp8 (SURVEY config 5)."""
     d = x.shape[1] if d is None else d
+    if x.dtype == torch.float8_e4m3fn:
+        dp = padded_dim_fp8(d)
+        if x.shape[1] == dp and x.is_contiguous():
+            return x
+        out = torch.zeros((x.shape[0], dp), dtype=torch.uint8, device=x.device)
+        out[:, :d] = x[:, :d].view(torch.uint8)
+        return out.view(torch.float8_e4m3fn)
     dp = padded_dim(d)
     if x.dtype == torch.bfloat16 and x.shape[1] == dp and x.is_contiguous():
         return x
@@ -87,8 +100,9 @@ class LloydEngine:
         bounds = [min(n, round_up(b, 32)) if 0 < i < self.row_chunks else b for i, b in enumerate(bounds)]
         self.bounds = bounds
         maxn = max(bounds[i + 1] - bounds[i] for i in range(self.row_chunks)) if n else 0
-        self.aplan = K.plan_assign(max(maxn, 1), dp, k, dev.index or 0)
-        self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode)
+        fp8 = K.is_fp8(self.x)
+        self.aplan = K.plan_assign(max(maxn, 1), dp, k, dev.index or 0, fp8=fp8)
+        self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode, fp8=fp8)
         self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         # distance scratch only when the centres need several LDS chunks (running min through HBM)
         self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev) if self.aplan.kc < self.aplan.kp
@@ -316,7 +330,7 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: O
     if n:
         if xnorm is None:
             xnorm = K.row_sqnorm(x, n, dp)
-        plan = K.plan_assign(n, dp, k, dev.index or 0)
+        plan = K.plan_assign(n, dp, k, dev.index or 0, fp8=K.is_fp8(x))
         K.assign_bf16(x, n, dp, cb, cn, plan, labels, best, None, xnorm=xnorm)
     return labels[:n], best[:n]
 

@@ -19,18 +19,19 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int, c_int]),
     "cml_kmeans_assign_threads": (c_int, [c_int]),
     "cml_kmeans_set_assign_variant": (c_int, [c_int]),
-    "cml_kmeans_assign_occupancy": (c_int, [c_int, c_int, c_int]),
+    "cml_kmeans_assign_occupancy": (c_int, [c_int, c_int, c_int, c_int]),
     "cml_kmeans_seg_threads": (c_int, []),
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
     "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
+    "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
     "cml_kmeans_accum_priv": (c_int, [c_vp, c_ll, c_ll, c_vp, c_int, c_int, c_int, c_int, c_vp, c_vp, c_int, c_int,
                                       c_vp]),
     "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_seg_slot_doubles": (c_ll, [c_int, c_int]),
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
@@ -68,7 +69,14 @@ class AccumPlan:
         return self.dw
 
 
-def plan_assign(n: int, dp: int, k: int, device_index: int = 0) -> AssignPlan:
+FP8 = torch.float8_e4m3fn
+
+
+def is_fp8(x: torch.Tensor) -> bool:
+    return x.dtype == FP8
+
+
+def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = False) -> AssignPlan:
     lib = _native.kernels()
     kp = round_up(max(k, 1), 32)
     kc = kp
@@ -80,7 +88,7 @@ def plan_assign(n: int, dp: int, k: int, device_index: int = 0) -> AssignPlan:
     waves = lib.cml_kmeans_assign_threads(dp) // 64
     per_cu = max(1, min(4, (160 * 1024) // max(lds, 1)))
     if torch.cuda.is_available():
-        occ = lib.cml_kmeans_assign_occupancy(dp, kc, kp)
+        occ = lib.cml_kmeans_assign_occupancy(dp, kc, kp, int(fp8))
         if occ > 0:  # persistent grid: never more workgroups than can be resident at once
             per_cu = max(1, min(per_cu, occ))
     ntiles = (n + 31) // 32
@@ -93,9 +101,14 @@ def set_assign_variant(v: int) -> None:
     _native.check(_native.kernels().cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
 
 
-def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None = None) -> AccumPlan:
+def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None = None,
+               fp8: bool = False) -> AccumPlan:
     lib = _native.kernels()
     ncu = num_cus(device_index)
+    if fp8:  # e4m3 rows: sort regime, CPL bytes per lane (dp >= 256)
+        if force == "priv" or dp < 256 or dp > 1024:
+            raise ValueError("fp8 features accumulate in the sort regime with 256 <= Dp <= 1024")
+        return AccumPlan(mode="sort", cpl=dp // 64, seg_grid=max(1, min((n + 255) // 256, ncu * 4)), dw=dp)
     dw = min(dp, 256)
     cpl = 4 if dw > 128 else 2
     if force != "sort":
@@ -150,7 +163,7 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
             cost_part.data_ptr() if (cost_part is not None and last) else 0,
             hist.data_ptr() if (hist is not None and last) else 0,
             rank.data_ptr() if (rank is not None and last) else 0,
-            plan.grid, st)
+            plan.grid, int(is_fp8(x)), st)
         _native.check(status, "kmeans_assign_bf16")
 
 
@@ -159,8 +172,8 @@ def row_sqnorm(x: torch.Tensor, n: int, dp: int, out: torch.Tensor | None = None
     if out is None:
         out = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
     if n > 0:
-        _native.check(_native.kernels().cml_row_sqnorm_bf16(x.data_ptr(), n, x.stride(0), dp, out.data_ptr(),
-                                                             _native.stream_ptr(stream)), "row_sqnorm_bf16")
+        fn = _native.kernels().cml_row_sqnorm_fp8 if is_fp8(x) else _native.kernels().cml_row_sqnorm_bf16
+        _native.check(fn(x.data_ptr(), n, x.stride(0), dp, out.data_ptr(), _native.stream_ptr(stream)), "row_sqnorm")
     return out
 
 
@@ -202,7 +215,8 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
                                        hist.data_ptr(), aplan.grid, aplan.nwaves, k, aplan.kp,
                                        cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
                                        perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
-                                       slots[0].data_ptr(), slots[1].data_ptr(), _native.stream_ptr(stream))
+                                       slots[0].data_ptr(), slots[1].data_ptr(), int(is_fp8(x)),
+                                       _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
 
 

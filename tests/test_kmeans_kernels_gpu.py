@@ -132,3 +132,29 @@ def test_sort_regime_bitwise_deterministic(n, d, k):
     lab = eng.labels[:n].cpu().long()
     sums, counts = K.sums_reference(x.double().cpu(), lab, k)
     np.testing.assert_allclose(msgs[0][:k * d].cpu().numpy(), sums.reshape(-1).numpy(), rtol=1e-9, atol=1e-6)
+
+
+@pytest.mark.parametrize("n,d,k", [(30_000, 37, 5), (50_000, 256, 256), (20_000, 512, 64), (9_999, 200, 33)])
+@pytest.mark.parametrize("mode", [None, "sort"])
+def test_fp8_features_lloyd_step(n, d, k, mode):
+    """OCP e4m3fn feature storage (SURVEY config 5): the kernels dequantise exactly to bf16, so the
+    step must equal the bf16 computation on the dequantised values."""
+    torch.manual_seed(5)
+    xf = torch.randn(n, d, device="cuda") * 1.5
+    x8 = xf.to(torch.float8_e4m3fn)
+    xd = x8.to(torch.float32)  # exact dequantisation
+    init = xd[:k].double().cpu().numpy()
+    eng = LloydEngine(x8, d, k, accum_mode=mode)
+    assert eng.x.dtype == torch.float8_e4m3fn and eng.x.shape[1] >= 256
+    np.testing.assert_allclose(eng.xnorm[:n].cpu().numpy(), (xd.double() ** 2).sum(1).cpu().numpy(), rtol=1e-5)
+    eng.set_centers(init)
+    eng.step()
+    torch.cuda.synchronize()
+    lab = eng.labels[:n].cpu().long()
+    sums, counts = K.sums_reference(xd.double().cpu(), lab, k)
+    msg = eng.msgs[0].cpu()
+    np.testing.assert_array_equal(msg[k * d:k * d + k].numpy(), counts.numpy())
+    np.testing.assert_allclose(msg[:k * d].numpy(), sums.reshape(-1).numpy(), rtol=1e-9, atol=1e-6)
+    ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), torch.as_tensor(init).to(torch.bfloat16))
+    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
+    assert ok.all()
