@@ -20,7 +20,32 @@ namespace {
 
 constexpr int kGlmThreads = 256;
 
+// OCP e4m3fn storage (SURVEY config 5): decoded with v_cvt_pk_f32_fp8, computed in f32.
+typedef unsigned char f8_t;
+typedef float f32x2_t __attribute__((ext_vector_type(2)));
+__device__ inline float f8_decode(f8_t b) {
+  const f32x2_t a = __builtin_amdgcn_cvt_pk_f32_fp8((int)b, false);
+  return a.x;
+}
+template <typename CT>
+__device__ inline void f8_decode16(const uint4 w, CT* v) {
+  const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    const f32x2_t a = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], false);
+    const f32x2_t b = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], true);
+    v[4 * q] = (CT)a.x;
+    v[4 * q + 1] = (CT)a.y;
+    v[4 * q + 2] = (CT)b.x;
+    v[4 * q + 3] = (CT)b.y;
+  }
+}
+
 template <typename T> struct Elt;
+template <> struct Elt<f8_t> {
+  static constexpr int CPT = 16;
+  __device__ static inline void load(const f8_t* p, double* v) { f8_decode16<double>(*reinterpret_cast<const uint4*>(p), v); }
+};
 template <> struct Elt<u16> {
   static constexpr int CPT = 8;
   __device__ static inline void load(const u16* p, double* v) {
@@ -70,6 +95,7 @@ __device__ inline void load_chunk(const T* X, long long row, long long ld, int c
     for (int j = 0; j < CPT; ++j) v[j] = 0.0;
     for (int j = 0; c0 + j < d && j < CPT; ++j) {
       if constexpr (sizeof(T) == 2) v[j] = (double)bf16_to_f32(((const u16*)X)[row * ld + c0 + j]);
+      else if constexpr (sizeof(T) == 1) v[j] = (double)f8_decode(((const f8_t*)X)[row * ld + c0 + j]);
       else v[j] = (double)X[row * ld + c0 + j];
     }
   }
@@ -162,14 +188,16 @@ __global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __res
 // row once LPR >= 8: the full-rate shape on MI355X, profiles/README.md). Compute type CT is f32
 // for bf16/f32 data (packed FMAs, v_exp_f32) and f64 for f64 data; every accumulation that
 // spans rows is f64.
-template <typename T> struct CompT { using type = float; };
+template <typename T> struct CompT { using type = float; };  // bf16, f32, fp8
 template <> struct CompT<double> { using type = double; };
 
 template <typename T, typename CT>
 __device__ inline void load_chunk_ct(const T* X, long long row, long long ld, int c0, int d, CT* v) {
   constexpr int CPT = Elt<T>::CPT;
   if (c0 + CPT <= d) {
-    if constexpr (sizeof(T) == 2) {
+    if constexpr (sizeof(T) == 1) {
+      f8_decode16<CT>(*reinterpret_cast<const uint4*>(X + row * ld + c0), v);
+    } else if constexpr (sizeof(T) == 2) {
       const uint4 w = *reinterpret_cast<const uint4*>(X + row * ld + c0);
       const unsigned ws[4] = {w.x, w.y, w.z, w.w};
 #pragma unroll
@@ -190,6 +218,7 @@ __device__ inline void load_chunk_ct(const T* X, long long row, long long ld, in
       CT t = 0;
       if (c0 + j < d) {
         if constexpr (sizeof(T) == 2) t = bf16_to_f32(((const u16*)X)[row * ld + c0 + j]);
+        else if constexpr (sizeof(T) == 1) t = (CT)f8_decode(((const f8_t*)X)[row * ld + c0 + j]);
         else t = (CT)X[row * ld + c0 + j];
       }
       v[j] = t;
@@ -255,9 +284,16 @@ __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __re
 #pragma unroll
           for (int q = 0; q < CPT / 2; ++q)
             w[q] = (unsigned)f32_to_bf16((float)v[2 * q]) | ((unsigned)f32_to_bf16((float)v[2 * q + 1]) << 16);
-          if constexpr (CPT == 8) *reinterpret_cast<uint4*>(yp) = make_uint4(w[0], w[1], w[2], w[3]);
-          else if constexpr (CPT == 4) *reinterpret_cast<uint2*>(yp) = make_uint2(w[0], w[1]);
-          else *reinterpret_cast<unsigned*>(yp) = w[0];
+          if constexpr (CPT == 16) {
+            *reinterpret_cast<uint4*>(yp) = make_uint4(w[0], w[1], w[2], w[3]);
+            *reinterpret_cast<uint4*>(yp + 8) = make_uint4(w[4], w[5], w[6], w[7]);
+          } else if constexpr (CPT == 8) {
+            *reinterpret_cast<uint4*>(yp) = make_uint4(w[0], w[1], w[2], w[3]);
+          } else if constexpr (CPT == 4) {
+            *reinterpret_cast<uint2*>(yp) = make_uint2(w[0], w[1]);
+          } else {
+            *reinterpret_cast<unsigned*>(yp) = w[0];
+          }
         } else {
 #pragma unroll
           for (int j = 0; j < CPT; ++j) yp[j] = (TO)v[j];
@@ -349,7 +385,7 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
 #pragma unroll
     for (int j = 0; j < CPT; ++j) g64[c][j] += (double)g[c][j];
   // reduce across row sub-groups, then across waves
-  __shared__ double red[kGlmThreads / 64][64 * 8 + 3];
+  __shared__ double red[kGlmThreads / 64][64 * 16 + 3];  // lpr*CPT <= 64*16 (fp8)
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -368,9 +404,9 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
 #pragma unroll
       for (int j = 0; j < CPT; ++j) red[wave][li * CPT + j] = g64[c][j];
     if (lane == 0 && c == 0) {
-      red[wave][64 * 8] = gb;
-      red[wave][64 * 8 + 1] = loss;
-      red[wave][64 * 8 + 2] = wsum;
+      red[wave][64 * 16] = gb;
+      red[wave][64 * 16 + 1] = loss;
+      red[wave][64 * 16 + 2] = wsum;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < lpr * CPT; t += blockDim.x) {
@@ -382,7 +418,7 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     }
     if (c == 0 && threadIdx.x < 3) {
       double a = 0.0;
-      for (int ww = 0; ww < nw; ++ww) a += red[ww][64 * 8 + threadIdx.x];
+      for (int ww = 0; ww < nw; ++ww) a += red[ww][64 * 16 + threadIdx.x];
       o_[d + threadIdx.x] = a;
     }
   }
@@ -452,6 +488,7 @@ __global__ __launch_bounds__(256) void gram_kernel(const T* __restrict__ X, long
         const double sw = wt != nullptr ? sqrt(wt[row]) : 1.0;
         if (cc < d) {
           if constexpr (sizeof(T) == 2) v = (double)bf16_to_f32(((const u16*)X)[row * ld + cc]);
+          else if constexpr (sizeof(T) == 1) v = (double)f8_decode(((const f8_t*)X)[row * ld + cc]);
           else v = (double)X[row * ld + cc];
         } else if (cc == d) {
           v = 1.0;
@@ -501,6 +538,7 @@ __global__ __launch_bounds__(256) void gram_small_kernel(const T* __restrict__ X
     for (int j = 0; j < M - 2; ++j) {
       double v;
       if constexpr (sizeof(T) == 2) v = (double)bf16_to_f32(((const u16*)X)[row * ld + j]);
+      else if constexpr (sizeof(T) == 1) v = (double)f8_decode(((const f8_t*)X)[row * ld + j]);
       else v = (double)X[row * ld + j];
       a[j] = v * sw;
     }
@@ -595,6 +633,7 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
     case 0: { using T = u16; BODY; } break;   \
     case 1: { using T = float; BODY; } break; \
     case 2: { using T = double; BODY; } break;\
+    case 3: { using T = f8_t; BODY; } break;  \
     default: return (int)hipErrorInvalidValue;\
   }
 
@@ -608,7 +647,7 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
   }
 
 CML_API int cml_glm_grid(long long n, int d, int dtype, int cap) {
-  const int cpt = dtype == 0 ? 8 : dtype == 1 ? 4 : 2;
+  const int cpt = dtype == 0 ? 8 : dtype == 1 ? 4 : dtype == 2 ? 2 : 16;
   if (pick_nch(d, cpt) < 0) return -1;  // moments layout limit
   int lpr, nch;
   if (!stream_layout(d, cpt, lpr, nch)) return -1;
@@ -619,6 +658,7 @@ CML_API int cml_glm_grid(long long n, int d, int dtype, int cap) {
 CML_API int cml_col_moments(const void* X, long long n, long long ld, int d, int dtype, const double* shift,
                             double* out, int grid, void* stream) {
   hipStream_t st = (hipStream_t)stream;
+  if (dtype == 3) return (int)hipErrorInvalidValue;  // fp8: the caller streams exact bf16 chunks
   CML_T_SWITCH(dtype, {
     constexpr int CPT = Elt<T>::CPT;
     const int nch = pick_nch(d, CPT);
@@ -659,6 +699,7 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
     case 0: CML_SCALE_OUT(u16); break;
     case 1: CML_SCALE_OUT(float); break;
     case 2: CML_SCALE_OUT(double); break;
+    case 3: CML_SCALE_OUT(f8_t); break;
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_SCALE_OUT
@@ -706,6 +747,7 @@ CML_API int cml_gram(const void* X, long long n, long long ld, int d, int dtype,
       case 0: return launch_gram_small<u16>(X, n, ld, d, y, wt, out, grid, st);
       case 1: return launch_gram_small<float>(X, n, ld, d, y, wt, out, grid, st);
       case 2: return launch_gram_small<double>(X, n, ld, d, y, wt, out, grid, st);
+      case 3: return launch_gram_small<f8_t>(X, n, ld, d, y, wt, out, grid, st);
       default: return (int)hipErrorInvalidValue;
     }
   }

@@ -23,7 +23,7 @@ _native.register_kernel_sigs({
     "cml_gram": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
 })
 
-_CODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2}
+_CODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2, torch.float8_e4m3fn: 3}
 
 
 def _prep(x: torch.Tensor) -> torch.Tensor:
@@ -59,6 +59,20 @@ def moments(x: torch.Tensor, d: Optional[int] = None) -> Tuple[int, torch.Tensor
     if not x.is_cuda:
         xs = x[:, :d].to(torch.float64) - shift
         return n, xs.sum(0), (xs * xs).sum(0), shift
+    if x.dtype == torch.float8_e4m3fn:  # exact bf16 copies of row chunks (e4m3 is a subset of bf16)
+        s1 = torch.zeros(d, dtype=torch.float64, device=x.device)
+        s2 = torch.zeros_like(s1)
+        for r0 in range(0, n, 1 << 22):
+            _, a, b, _ = _moments_kernel(x[r0:r0 + (1 << 22), :d].to(torch.bfloat16), d, shift)
+            s1 += a
+            s2 += b
+        return n, s1, s2, shift
+    _, s1, s2, _ = _moments_kernel(x, d, shift)
+    return n, s1, s2, shift
+
+
+def _moments_kernel(x: torch.Tensor, d: int, shift: torch.Tensor):
+    n = x.shape[0]
     xx = _prep(x)
     code = _CODE[xx.dtype]
     g = _grid(n, d, code, xx.device)
