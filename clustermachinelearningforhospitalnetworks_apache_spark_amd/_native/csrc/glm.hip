@@ -278,6 +278,19 @@ __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __re
         for (int j = 0; j < CPT; ++j) v[j] = (v[j] - mu[c][j]) * is[c][j];
       }
       TO* yp = Y + row * ldy + c0;
+      if constexpr (sizeof(TO) == 1) {  // OCP e4m3fn output, saturated to +-448
+        unsigned char b[CPT];
+#pragma unroll
+        for (int j = 0; j < CPT; j += 2) {
+          const float a0 = fminf(fmaxf((float)v[j], -448.f), 448.f);
+          const float a1 = j + 1 < CPT ? fminf(fmaxf((float)v[j + 1], -448.f), 448.f) : 0.f;
+          const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
+          b[j] = (unsigned char)(pk & 0xff);
+          if (j + 1 < CPT) b[j + 1] = (unsigned char)((pk >> 8) & 0xff);
+        }
+        for (int j = 0; c0 + j < dpad && j < CPT; ++j) ((unsigned char*)yp)[j] = b[j];
+        continue;
+      }
       if (vec_ok && c0 + CPT <= dpad) {
         if constexpr (sizeof(TO) == 2) {
           unsigned w[CPT / 2];
@@ -693,6 +706,7 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
     case 0: CML_SCALE_LAUNCH(TI, u16); break;                    \
     case 1: CML_SCALE_LAUNCH(TI, float); break;                  \
     case 2: CML_SCALE_LAUNCH(TI, double); break;                 \
+    case 3: CML_SCALE_LAUNCH(TI, f8_t); break;                   \
     default: return (int)hipErrorInvalidValue;                   \
   }
   switch (in_dtype) {

@@ -111,7 +111,8 @@ class StandardScaler(Estimator):
         "outputCol": ("__auto__", "output column name", str),
         "withMean": (False, "whether to center data with mean", bool),
         "withStd": (True, "whether to scale the data to unit standard deviation", bool),
-        "outputDtype": ("auto", "cml extension: dtype of the scaled vectors (auto/float64/float32/bfloat16)", str),
+        "outputDtype": ("auto", "cml extension: dtype of the scaled vectors (auto/float64/float32/bfloat16/fp8); "
+                                "fp8 = OCP e4m3fn, saturated at +-448 (standardized values fit it)", str),
     }
 
     def __init__(self, withMean=None, withStd=None, inputCol=None, outputCol=None, outputDtype=None):
@@ -172,7 +173,8 @@ class StandardScalerModel(Model):
         dev = x.device
         od = self.getOutputDtype()
         out_dtype = x.dtype if od == "auto" else {"float64": torch.float64, "float32": torch.float32,
-                                                 "bfloat16": torch.bfloat16}[od]
+                                                 "bfloat16": torch.bfloat16, "fp8": torch.float8_e4m3fn,
+                                                 "float8_e4m3fn": torch.float8_e4m3fn}[od]
         y = glm_ops.scale_apply(x, d, torch.as_tensor(self._mean, device=dev), torch.as_tensor(inv, device=dev),
                                 self.getWithMean(), out_dtype=out_dtype)
         return _replace_col(df, self.getOutputCol(), ColumnData(y, None, T.VectorUDT()))

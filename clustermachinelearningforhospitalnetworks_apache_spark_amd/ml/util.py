@@ -105,12 +105,26 @@ def _comm():
     return s._comm
 
 
+def _is_extension_param(instance, name: str) -> bool:
+    """Params that Spark's class does not have (docs start with "cml") — kept out of Spark's
+    paramMap/defaultParamMap, whose readers reject unknown names, and stored under cml keys."""
+    spec = getattr(type(instance), "_all_params", {}).get(name)
+    return bool(spec) and str(spec[1]).startswith("cml")
+
+
 def write_metadata(instance, path: str, extra: Optional[Dict[str, Any]] = None, param_map=None) -> None:
+    pm = param_map if param_map is not None else instance._paramMap
+    dm = instance._defaultParamMap
     md = {"class": jvm_class(instance), "timestamp": int(time.time() * 1000), "sparkVersion": SPARK_VERSION,
           "uid": instance.uid,
-          "paramMap": {k: _json_value(v) for k, v in (param_map if param_map is not None
-                                                      else instance._paramMap).items()},
-          "defaultParamMap": {k: _json_value(v) for k, v in instance._defaultParamMap.items()}}
+          "paramMap": {k: _json_value(v) for k, v in pm.items() if not _is_extension_param(instance, k)},
+          "defaultParamMap": {k: _json_value(v) for k, v in dm.items() if not _is_extension_param(instance, k)}}
+    ext = {k: _json_value(v) for k, v in pm.items() if _is_extension_param(instance, k)}
+    ext_d = {k: _json_value(v) for k, v in dm.items() if _is_extension_param(instance, k)}
+    if ext:
+        md["cmlParamMap"] = ext
+    if ext_d:
+        md["cmlDefaultParamMap"] = ext_d
     if extra:
         md.update(extra)
     d = os.path.join(path, "metadata")
@@ -129,12 +143,14 @@ def read_metadata(path: str) -> Dict[str, Any]:
 
 def apply_params(instance, md: Dict[str, Any]) -> None:
     instance.uid = md.get("uid", instance.uid)
-    for k, v in md.get("defaultParamMap", {}).items():
-        if instance.hasParam(k):
-            instance._defaultParamMap[k] = v
-    for k, v in md.get("paramMap", {}).items():
-        if instance.hasParam(k):
-            instance._paramMap[k] = v
+    for key in ("defaultParamMap", "cmlDefaultParamMap"):
+        for k, v in md.get(key, {}).items():
+            if instance.hasParam(k):
+                instance._defaultParamMap[k] = v
+    for key in ("paramMap", "cmlParamMap"):
+        for k, v in md.get(key, {}).items():
+            if instance.hasParam(k):
+                instance._paramMap[k] = v
 
 
 def write_parquet(path: str, sub: str, table) -> None:

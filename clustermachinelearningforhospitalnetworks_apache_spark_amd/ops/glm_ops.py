@@ -95,6 +95,8 @@ def scale_apply(x: torch.Tensor, d: int, mean: torch.Tensor, inv_std: torch.Tens
         y = y * inv_std
         if width > d:
             y = torch.nn.functional.pad(y, (0, width - d))
+        if out_dtype == torch.float8_e4m3fn:
+            y = y.clamp(-448.0, 448.0)
         return y.to(out_dtype)
     xx = _prep(x)
     out = torch.empty((n, width), dtype=out_dtype, device=x.device)

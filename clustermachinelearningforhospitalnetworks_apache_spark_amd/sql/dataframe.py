@@ -676,7 +676,7 @@ def column_to_python(cd: ColumnData) -> List[Any]:
         vm = cd.valid_mask()
         return [v if vm[i] else None for i, v in enumerate(cd.values)]
     vals = cd.values.detach()
-    if vals.dtype == torch.bfloat16:
+    if vals.dtype in (torch.bfloat16, torch.float8_e4m3fn):
         vals = vals.float()
     arr = vals.cpu().numpy()
     vm = cd.valid_mask().cpu().numpy() if n else np.ones(0, dtype=bool)
