@@ -54,12 +54,17 @@ def main():
     ap.add_argument("--k", type=int, default=256)
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
-    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg"],
+    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
-                         "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update")
+                         "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update; "
+                         "pipeline = BASELINE config 5 (VectorAssembler -> StandardScaler(fp8) -> KMeans -> "
+                         "LogisticRegression, 125M x 512 per GPU = 1B x 512 at 8 GPUs), one step = one Pipeline.fit")
+    ap.add_argument("--rows-per-gpu", type=int, default=125_000_000, help="pipeline workload (weak scaling)")
     args = ap.parse_args()
     if args.workload == "logreg":
         return bench_logreg(args)
+    if args.workload == "pipeline":
+        return bench_pipeline(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world != 1:
@@ -226,6 +231,87 @@ def bench_logreg(args):
             "extra": {"datagen_s": round(gen_s, 3), "scaler_s": round(scaler_s, 3), "final_loss": hist[-1] if hist
                       else None}}), flush=True)
     comm.shutdown()
+
+
+def bench_pipeline(args):
+    """BASELINE.json config 5 through the public API: a sharded frame of HBM-resident bf16 raw
+    features -> Pipeline(VectorAssembler, StandardScaler(withMean, outputDtype=fp8),
+    KMeans(k=128, 10 Lloyd iterations after k-means||), LogisticRegression(10 L-BFGS iterations)).
+    Timed: whole Pipeline.fit calls (every stage's fit and the intermediate transforms)."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegression
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import StandardScaler, VectorAssembler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.pipeline import Pipeline
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    gpu = torch.cuda.is_available()
+    n, d = args.rows_per_gpu, (args.dim if args.dim != 256 else 512)
+    if not gpu:
+        n, d = min(n, 100_000), min(d, 64)
+    spark = (SparkSession.builder.appName("bench-pipeline").master("mi355x" if gpu else "local[4]")
+             .config("cml.ml.features.dtype", "bf16" if gpu else "float64").getOrCreate())
+    comm = spark._comm
+    rank, W = comm.rank, comm.world_size
+    dev = spark._device
+    t0 = time.perf_counter()
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    centers = torch.randn((32, d), generator=g, device=dev) * 3
+    spread = torch.rand(d, generator=g, device=dev) * 4 + 0.25
+    offset = torch.randn(d, generator=g, device=dev) * 10
+    w_true = torch.randn(d, generator=g, device=dev) / d ** 0.5
+    g.manual_seed(5000 + rank)
+    raw = torch.empty((n, d), dtype=torch.bfloat16 if gpu else torch.float64, device=dev)
+    y = torch.empty(n, dtype=torch.float64, device=dev)
+    for s0 in range(0, n, 1 << 22):
+        m = min(1 << 22, n - s0)
+        z = centers[torch.randint(0, 32, (m,), generator=g, device=dev)] + torch.randn((m, d), generator=g,
+                                                                                         device=dev)
+        raw[s0:s0 + m] = (z * spread + offset).to(raw.dtype)
+        y[s0:s0 + m] = ((z @ w_true) > 0).to(torch.float64)
+        del z
+    df = spark.createDataFrameFromTensors({"raw": raw, "label": y})
+    del raw, y
+    if gpu:
+        torch.cuda.synchronize()
+    gen_s = time.perf_counter() - t0
+    pipe = Pipeline(stages=[
+        VectorAssembler(inputCols=["raw"], outputCol="assembled"),
+        StandardScaler(inputCol="assembled", outputCol="features", withMean=True,
+                       outputDtype="fp8" if gpu else "float64"),
+        KMeans(k=128, maxIter=10, tol=0.0, seed=11, predictionCol="cluster"),
+        LogisticRegression(maxIter=10, tol=0.0),
+    ])
+    for _ in range(args.warmup):
+        pipe.fit(df)
+    comm.barrier()
+    if gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(args.steps):
+        model = pipe.fit(df)
+    if gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    elapsed = comm.max_scalar(time.perf_counter() - t0)
+    total = n * W
+    if rank == 0:
+        km, lr = model.stages[2], model.stages[3]
+        print(json.dumps({
+            "metric": f"Pipeline fit rows/sec (whole node), VectorAssembler->StandardScaler(fp8)->KMeans->LogReg, "
+                      f"{total / 1e9:g}B x {d}",
+            "value": total * args.steps / elapsed, "unit": "rows/s", "n_gpus": W if gpu else 0, "steps": args.steps,
+            "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
+            "scaling": "weak", "vs_baseline": None, "dtype": "fp8 features (e4m3fn), bf16 MFMA" if gpu else "fp64",
+            "data": "synthetic (Gaussian blobs, logistic labels), generated on device",
+            "config": {"model": "Pipeline[VectorAssembler, StandardScaler, KMeans k=128 x10, LogReg x10]",
+                       "global_batch": total, "seq_len": None, "parallelism": f"dp{W}", "rows_per_gpu": n, "dim": d},
+            "extra": {"datagen_s": round(gen_s, 3), "kmeans_iters": km.summary.numIter,
+                      "kmeans_cost": km.summary.trainingCost, "logreg_iters": lr.summary.totalIterations}}),
+              flush=True)
+        if os.environ.get("CML_TRACE") == "1":
+            from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
+            print(TRACER.report(), file=sys.stderr, flush=True)
+    spark.stop()
 
 
 if __name__ == "__main__":

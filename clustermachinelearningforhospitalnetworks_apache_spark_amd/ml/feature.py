@@ -63,6 +63,16 @@ class VectorAssembler(Transformer):
                 raise TypeError(f"VectorAssembler: column {c!r} of type {cd.dtype.simpleString()} is not numeric")
             cds.append(cd)
         hi = self.getHandleInvalid()
+        if (len(cds) == 1 and isinstance(cds[0].dtype, T.VectorUDT) and cds[0].valid is None
+                and cds[0].values.dtype == dtype and cds[0].values.is_contiguous() and hi != "skip"):
+            # one dense vector input already in the target dtype: the assembled matrix IS the input
+            # (no 2x HBM footprint for 100+ GB shards); only the invalid-value check reads it
+            x = cds[0].values
+            if hi == "error" and df._nrows and x.is_floating_point():
+                for r0 in range(0, df._nrows, 1 << 22):
+                    if bool(torch.isnan(x[r0:r0 + (1 << 22)].float()).any().item()):
+                        raise ValueError("VectorAssembler: encountered NaN values with handleInvalid='error'")
+            return _replace_col(df, self.getOutputCol(), ColumnData(x, None, T.VectorUDT()))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags
             from ..ops import frame_ops

@@ -175,6 +175,36 @@ class SparkSession:
             self._streams = StreamingQueryManager(self)
         return self._streams
 
+    def createDataFrameFromTensors(self, columns: Dict[str, torch.Tensor]):
+        """cml extension: a frame over THIS rank's shard of device-resident tensors, without a host
+        round trip ([n, d] tensors become vector columns, [n] tensors numeric columns). Rows are
+        numbered globally in rank order (rank r's rows follow ranks < r), which keeps every
+        counter-based random decision independent of the GPU count."""
+        from .column import ColumnData
+        from .dataframe import DataFrame
+        if not columns:
+            raise ValueError("createDataFrameFromTensors needs at least one column")
+        n = int(next(iter(columns.values())).shape[0])
+        fields, cols = [], {}
+        kinds = {torch.float64: T.DoubleType(), torch.float32: T.FloatType(), torch.int32: T.IntegerType(),
+                 torch.int64: T.LongType(), torch.bool: T.BooleanType(), torch.int16: T.ShortType()}
+        for name, t in columns.items():
+            if int(t.shape[0]) != n:
+                raise ValueError("all columns need the same number of rows")
+            t = t.to(self._device)
+            if t.dim() == 2:
+                dt = T.VectorUDT()
+            elif t.dtype in kinds:
+                dt = kinds[t.dtype]
+            else:
+                raise TypeError(f"column {name!r}: unsupported scalar dtype {t.dtype}")
+            fields.append(T.StructField(name, dt, True))
+            cols[name] = ColumnData(t, None, dt)
+        counts = self._comm.allgather_object(n)
+        off = sum(counts[: self._comm.rank])
+        rows = torch.arange(off, off + n, dtype=torch.int64, device=self._device)
+        return DataFrame(self, T.StructType(fields), cols, n, rows, self._device)
+
     def createDataFrame(self, data, schema=None, samplingRatio=None, verifySchema=True):
         """Rows / tuples / dicts / pandas / numpy -> sharded frame.
 
