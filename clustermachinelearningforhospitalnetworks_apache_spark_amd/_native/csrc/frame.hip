@@ -298,6 +298,43 @@ __global__ __launch_bounds__(kThreads) void quant_fp8_kernel(const T* __restrict
   }
 }
 
+// ----------------------------------------------------------------------------- invalid check
+// Any NaN among the first d columns of a row-major bf16 / f32 / f64 matrix: 16-byte loads, NaN
+// test on the raw bits, one flag per block (VectorAssembler handleInvalid="error" on a vector
+// input that is used in place).
+template <int ESZ>
+__global__ __launch_bounds__(kThreads) void has_nan_kernel(const unsigned char* __restrict__ x, long long n, int d,
+                                                           long long ld_bytes, int* __restrict__ flag) {
+  const int per = 16 / ESZ;
+  const int chunks = (d + per - 1) / per;
+  const long long total = n * chunks;
+  int found = 0;
+  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+    const long long r = t / chunks;
+    const int c = (int)(t - r * chunks);
+    const uint4 v = *reinterpret_cast<const uint4*>(x + r * ld_bytes + 16LL * c);
+    const unsigned w[4] = {v.x, v.y, v.z, v.w};
+    const int valid = d - c * per < per ? d - c * per : per;
+    if constexpr (ESZ == 2) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) {
+        const unsigned h = (w[e >> 1] >> (16 * (e & 1))) & 0xffffu;
+        found |= (e < valid) & ((h & 0x7fffu) > 0x7f80u);
+      }
+    } else if constexpr (ESZ == 4) {
+#pragma unroll
+      for (int e = 0; e < 4; ++e) found |= (e < valid) & ((w[e] & 0x7fffffffu) > 0x7f800000u);
+    } else {
+#pragma unroll
+      for (int e = 0; e < 2; ++e) {
+        const unsigned long long b = ((unsigned long long)w[2 * e + 1] << 32) | w[2 * e];
+        found |= (e < valid) & ((b & 0x7fffffffffffffffull) > 0x7ff0000000000000ull);
+      }
+    }
+  }
+  if (__any(found) && (threadIdx.x & 63) == 0) atomicOr(flag, 1);
+}
+
 inline unsigned grid_for(long long n, long long per = kThreads) {
   long long g = (n + per - 1) / per;
   if (g < 1) g = 1;
@@ -427,5 +464,21 @@ CML_API int cml_quant_fp8(const void* x, int dtype, long long n, int d, long lon
                        scale, out, ldo);
   else
     return (int)hipErrorInvalidValue;
+  return cml_status();
+}
+
+// flag (device int, zeroed by the caller) |= any NaN in x[:, :d]; esize 2 (bf16), 4 (f32), 8 (f64).
+CML_API int cml_has_nan(const void* x, long long n, int d, long long ld_bytes, int esize, int* flag, void* stream) {
+  if (n <= 0 || d <= 0) return 0;
+  if (ld_bytes % 16 != 0 || (reinterpret_cast<size_t>(x) & 15) != 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  const long long total = n * ((d * esize + 15) / 16);
+  const unsigned char* p = (const unsigned char*)x;
+  switch (esize) {
+    case 2: hipLaunchKernelGGL(has_nan_kernel<2>, dim3(grid_for(total)), dim3(kThreads), 0, st, p, n, d, ld_bytes, flag); break;
+    case 4: hipLaunchKernelGGL(has_nan_kernel<4>, dim3(grid_for(total)), dim3(kThreads), 0, st, p, n, d, ld_bytes, flag); break;
+    case 8: hipLaunchKernelGGL(has_nan_kernel<8>, dim3(grid_for(total)), dim3(kThreads), 0, st, p, n, d, ld_bytes, flag); break;
+    default: return (int)hipErrorInvalidValue;
+  }
   return cml_status();
 }

@@ -69,9 +69,13 @@ class VectorAssembler(Transformer):
             # (no 2x HBM footprint for 100+ GB shards); only the invalid-value check reads it
             x = cds[0].values
             if hi == "error" and df._nrows and x.is_floating_point():
-                for r0 in range(0, df._nrows, 1 << 22):
-                    if bool(torch.isnan(x[r0:r0 + (1 << 22)].float()).any().item()):
-                        raise ValueError("VectorAssembler: encountered NaN values with handleInvalid='error'")
+                if x.is_cuda:
+                    from ..ops import frame_ops
+                    bad_any = frame_ops.has_nan(x)
+                else:
+                    bad_any = bool(torch.isnan(x).any().item())
+                if bad_any:
+                    raise ValueError("VectorAssembler: encountered NaN values with handleInvalid='error'")
             return _replace_col(df, self.getOutputCol(), ColumnData(x, None, T.VectorUDT()))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags

@@ -32,7 +32,21 @@ _native.register_kernel_sigs({
     "cml_cls_confusion": (c_int, [c_vp, c_vp, c_vp, c_ll, c_int, c_vp, c_int, c_vp]),
     "cml_col_absmax": (c_int, [c_vp, c_int, c_ll, c_int, c_ll, c_int, c_vp, c_vp]),
     "cml_quant_fp8": (c_int, [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_ll, c_vp]),
+    "cml_has_nan": (c_int, [c_vp, c_ll, c_int, c_ll, c_int, c_vp, c_vp]),
 })
+
+
+def has_nan(x: torch.Tensor, d: Optional[int] = None, stream=None) -> bool:
+    """Any NaN in x[:, :d] (one streaming pass; bf16/f32/f64 with 16-B aligned rows)."""
+    _dev(x, "has_nan")
+    d = x.shape[1] if d is None else d
+    if x.dtype not in (torch.bfloat16, torch.float32, torch.float64) or x.stride(1) != 1 \
+            or (x.stride(0) * x.element_size()) % 16 or x.data_ptr() % 16:
+        return bool(torch.isnan(x[:, :d]).any().item()) if x.is_floating_point() else False
+    flag = torch.zeros(1, dtype=torch.int32, device=x.device)
+    _native.check(_native.kernels().cml_has_nan(x.data_ptr(), x.shape[0], d, x.stride(0) * x.element_size(),
+                                                x.element_size(), flag.data_ptr(), _st(stream)), "has_nan")
+    return bool(flag.item())
 
 _SRC_TYPES = {torch.float64: 0, torch.float32: 1, torch.int32: 2, torch.int64: 3, torch.uint8: 4,
               torch.bool: 4, torch.int16: 5, torch.bfloat16: 6, torch.int8: 7}

@@ -59,7 +59,7 @@ def moments(x: torch.Tensor, d: Optional[int] = None) -> Tuple[int, torch.Tensor
     if not x.is_cuda:
         xs = x[:, :d].to(torch.float64) - shift
         return n, xs.sum(0), (xs * xs).sum(0), shift
-    if x.dtype == torch.float8_e4m3fn:  # exact bf16 copies of row chunks (e4m3 is a subset of bf16)
+    if x.dtype == torch.float8_e4m3fn and d > 512:  # exact bf16 copies of row chunks (e4m3 ⊂ bf16)
         s1 = torch.zeros(d, dtype=torch.float64, device=x.device)
         s2 = torch.zeros_like(s1)
         for r0 in range(0, n, 1 << 22):

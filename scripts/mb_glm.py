@@ -13,9 +13,9 @@ def timeit(fn, reps=5):
     return best
 
 
-for n, d, dt in [(20_000_000, 256, torch.bfloat16), (10_000_000, 256, torch.float32), (20_000_000, 4, torch.float64),
+for n, d, dt in [(20_000_000, 512, torch.float8_e4m3fn), (20_000_000, 256, torch.bfloat16), (10_000_000, 256, torch.float32), (20_000_000, 4, torch.float64),
                  (20_000_000, 512, torch.bfloat16)]:
-    x = torch.randn(n, d, device="cuda").to(dt)
+    x = torch.randn(n, d, device="cuda").to(dt) if dt != torch.float8_e4m3fn else torch.randn(n, d, device="cuda").to(torch.bfloat16).to(dt)
     y = (torch.rand(n, device="cuda") > 0.5).double()
     coef = torch.randn(d + 1, device="cuda", dtype=torch.float64) * 0.05
     gb = x.numel() * x.element_size() / 1e9

@@ -122,3 +122,16 @@ def test_fp8_quantisation(src):
     want = (x.float() * scale).clamp(-448, 448).to(torch.float8_e4m3fn)
     assert torch.equal(q[:, :d].view(torch.uint8), want.view(torch.uint8))
     assert (q[:, d:].view(torch.uint8) == 0).all()
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32, torch.float64])
+def test_has_nan(dtype):
+    x = torch.randn(10_001, 40, dtype=torch.float64).to(dtype)
+    xp = torch.zeros((10_001, 64), dtype=dtype)
+    xp[:, :40] = x
+    assert not F.has_nan(xp.cuda(), 40)
+    xp[7777, 39] = float("nan")
+    assert F.has_nan(xp.cuda(), 40)
+    xp[7777, 39] = 0
+    xp[5, 50] = float("nan")  # beyond d: ignored
+    assert not F.has_nan(xp.cuda(), 40)
