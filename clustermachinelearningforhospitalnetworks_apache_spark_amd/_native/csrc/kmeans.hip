@@ -839,7 +839,9 @@ long long assign_lds_bytes(int kc, int kp, int Dp) {
 // RT 1 with the next tile's X in flight and more waves per CU.
 // Variant (tuning/experiments): 0 auto, 1 = RT 2 + X double buffer, 2 = RT 1, 3 = RT 4.
 int g_assign_variant = 0;
-inline int assign_threads(int /*DS*/) { return 512; }
+inline int assign_threads(int /*DS*/) {
+  return g_assign_variant == 4 ? 768 : (g_assign_variant == 5 ? 1024 : 512);
+}
 
 template <int DP, bool F8>
 const void* assign_kernel_ptr() {
@@ -849,6 +851,8 @@ const void* assign_kernel_ptr() {
     case 1: return (const void*)kmeans_assign_bf16<DP, 2, 512, PF, 4, F8>;
     case 2: return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
     case 3: return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, 2, F8>;
+    case 4: return (const void*)kmeans_assign_bf16<DP, 2, 768, false, 4, F8>;
+    case 5: return (const void*)kmeans_assign_bf16<DP, 1, 1024, PF, 4, F8>;
     default:
       if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8>;
       else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
@@ -862,6 +866,8 @@ inline int assign_tile_rows(int Dp) {
     case 1: return 32;
     case 2: return 16;
     case 3: return Dp >= 512 ? 32 : 64;
+    case 4: return 32;
+    case 5: return 16;
     default: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
   }
 }
@@ -932,7 +938,7 @@ CML_API int cml_kmeans_assign_occupancy(int Dp, int kc, int kp, int xfp8) {
   }
 }
 CML_API int cml_kmeans_set_assign_variant(int v) {
-  if (v < 0 || v > 3) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 5) return (int)hipErrorInvalidValue;
   g_assign_variant = v;
   return 0;
 }

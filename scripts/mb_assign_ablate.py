@@ -18,7 +18,7 @@ def timeit(fn, reps=5):
 
 lib = _native.kernels()
 shapes = [(20_000_000, 256, 256), (20_000_000, 16, 5), (10_000_000, 128, 64)]
-variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 3]
+variants = [int(v) for v in sys.argv[1:]] or [0, 1, 2, 3, 4, 5]
 for (n, d, k) in shapes:
     x = torch.randn(n, d, device="cuda", dtype=torch.bfloat16)
     dp = x.shape[1]
@@ -38,7 +38,7 @@ for (n, d, k) in shapes:
                 def run():
                     st = lib.cml_kmeans_assign_bf16(x.data_ptr(), n, ldx, dp, cb.data_ptr(), dp, ap.kc, ap.kp, 0,
                                                     cn.data_ptr(), xn.data_ptr(), lab.data_ptr(), 0, 1, 1,
-                                                    cost.data_ptr(), 0, 0, ap.grid, 0)
+                                                    cost.data_ptr(), 0, 0, ap.grid, 0, 0)
                     _native.check(st, "assign")
                 t = timeit(run)
                 print(f"n={n} d={d} k={kk} v{v} grid={ap.grid}x{ap.nwaves}w {tag:5s}: {t:.3f} ms "
