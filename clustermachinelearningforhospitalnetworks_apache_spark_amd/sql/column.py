@@ -433,6 +433,12 @@ class Cast(Expr):
             h = _to_host(c)
             return ColumnData(np.array([None if v is None else _fmt(v) for v in h.values], dtype=object),
                               h.valid, to)
+        if isinstance(to, T.DateType) and (c.is_host or isinstance(c.dtype, T.TimestampType)):
+            ts = _parse_ts_column(c, frame) if c.is_host else c
+            days = torch.div(ts.values, 86_400_000_000, rounding_mode="floor").to(torch.int32)
+            return ColumnData(days, ts.valid, to)
+        if isinstance(to, T.TimestampType) and not c.is_host and isinstance(c.dtype, T.DateType):
+            return ColumnData(c.values.to(torch.int64) * 86_400_000_000, c.valid, to)
         if c.is_host:
             if isinstance(to, T.TimestampType):
                 return _parse_ts_column(c, frame)

@@ -5,6 +5,7 @@ them at ref.py:82 and ref.py:176-177; the rest are the commonly used siblings.
 """
 from __future__ import annotations
 
+import builtins
 import time
 from typing import Iterable, Union
 
@@ -249,3 +250,224 @@ def var_pop(c: ColumnOrName) -> Column:
 
 def first(c: ColumnOrName) -> Column:
     return Column(AggExpr("first", _c(c)))
+
+
+# ------------------------------------------------------------------------------------------------ UDFs
+
+def _return_type(rt) -> T.DataType:
+    if rt is None:
+        return T.StringType()
+    if isinstance(rt, T.DataType):
+        return rt
+    return T.parse_type(str(rt))
+
+
+class UserDefinedFunction:
+    """pyspark ``udf``: a Python function applied row by row on the host (rank-local shard).
+
+    Nulls are passed as ``None``; the result is converted to ``returnType`` and moved back to
+    the frame's device when that type is device-resident. Use ``pandas_udf`` for vectorised
+    functions — both are host fallbacks, the GPU never runs Python.
+    """
+
+    def __init__(self, func, returnType=None, vectorized: bool = False, name: str = None):
+        self.func = func
+        self.returnType = _return_type(returnType)
+        self.vectorized = vectorized
+        self.__name__ = name or getattr(func, "__name__", "udf")
+        self.evalType = 200 if vectorized else 100
+
+    def __call__(self, *cols) -> Column:
+        from .builder import column_from_values
+        from .dataframe import column_to_python
+        fn, rt, vec = self.func, self.returnType, self.vectorized
+
+        def impl(frame, args):
+            pys = [column_to_python(a) for a in args]
+            if vec:
+                import pandas as pd
+                res = fn(*[pd.Series(p) for p in pys])
+                vals = list(res.tolist() if hasattr(res, "tolist") else res)
+                vals = [None if (v is not None and isinstance(v, float) and v != v and not isinstance(
+                    rt, (T.DoubleType, T.FloatType))) else v for v in vals]
+            else:
+                vals = [fn(*row) for row in zip(*pys)] if pys else [fn() for _ in range(frame._nrows)]
+            if len(vals) != frame._nrows:
+                raise ValueError(f"UDF {self.__name__} returned {len(vals)} values for {frame._nrows} rows")
+            return column_from_values(vals, rt, frame._device)
+        return Column(Func(self.__name__, [_c(c) for c in cols], impl))
+
+    def asNondeterministic(self):
+        return self
+
+
+def udf(f=None, returnType=None):
+    """``udf(f, returnType)`` or ``@udf(returnType=...)`` / ``@udf``."""
+    if f is None or isinstance(f, (str, T.DataType)):
+        rt = f if returnType is None else returnType
+        return lambda fn: UserDefinedFunction(fn, rt)
+    return UserDefinedFunction(f, returnType)
+
+
+def pandas_udf(f=None, returnType=None, functionType=None):
+    """Vectorised UDF: the function receives one pandas Series per argument (the rank's shard)."""
+    if f is None or isinstance(f, (str, T.DataType)):
+        rt = f if returnType is None else returnType
+        return lambda fn: UserDefinedFunction(fn, rt, vectorized=True)
+    return UserDefinedFunction(f, returnType, vectorized=True)
+
+
+# ------------------------------------------------------------------------------------------------ strings / dates
+
+def _host_map(name, cols, fn, rt):
+    """Row-wise host function over one or more columns (null in -> null out unless fn handles it)."""
+    def wrapped(*vals):
+        return None if any(v is None for v in vals) else fn(*vals)
+    return UserDefinedFunction(wrapped, rt, name=name)(*cols)
+
+
+def substring(c: ColumnOrName, pos: int, length: int) -> Column:
+    """1-based position like Spark; pos <= 0 counts from the end."""
+    def f(s):
+        s = str(s)
+        start = builtins.max(pos - 1 if pos > 0 else (len(s) + pos if pos < 0 else 0), 0)
+        return s[start:start + length]
+    return _host_map(f"substring({pos},{length})", [c], f, T.StringType())
+
+
+def concat_ws(sep: str, *cols: ColumnOrName) -> Column:
+    def f(*vals):
+        return sep.join(str(v) for v in vals if v is not None)
+    return UserDefinedFunction(f, T.StringType(), name="concat_ws")(*cols)
+
+
+def regexp_replace(c: ColumnOrName, pattern: str, replacement: str) -> Column:
+    import re
+    rx = re.compile(pattern)
+    repl = re.sub(r"\$(\d+)", r"\\\1", replacement)  # Java $1 -> Python \1
+    return _host_map("regexp_replace", [c], lambda s: rx.sub(repl, str(s)), T.StringType())
+
+
+def regexp_extract(c: ColumnOrName, pattern: str, idx: int) -> Column:
+    import re
+    rx = re.compile(pattern)
+
+    def f(s):
+        m = rx.search(str(s))
+        return (m.group(idx) or "") if m else ""
+    return _host_map("regexp_extract", [c], f, T.StringType())
+
+
+def split(c: ColumnOrName, pattern: str) -> Column:
+    import re
+    rx = re.compile(pattern)
+    return _host_map("split", [c], lambda s: rx.split(str(s)), T.ArrayType(T.StringType()))
+
+
+def lpad(c: ColumnOrName, width: int, pad: str) -> Column:
+    return _host_map("lpad", [c], lambda s: (pad * width + str(s))[-width:] if len(str(s)) < width
+                     else str(s)[:width], T.StringType())
+
+
+def rpad(c: ColumnOrName, width: int, pad: str) -> Column:
+    return _host_map("rpad", [c], lambda s: (str(s) + pad * width)[:width], T.StringType())
+
+
+def _spark_to_strftime(fmt: str) -> str:
+    out = fmt
+    for a, b in (("yyyy", "%Y"), ("MM", "%m"), ("dd", "%d"), ("HH", "%H"), ("mm", "%M"), ("ss", "%S"),
+                 ("yy", "%y"), ("EEE", "%a"), ("MMM", "%b")):
+        out = out.replace(a, b)
+    return out
+
+
+def date_format(c: ColumnOrName, fmt: str) -> Column:
+    py = _spark_to_strftime(fmt)
+    return _host_map("date_format", [c], lambda t: t.strftime(py), T.StringType())
+
+
+def _days(cd: ColumnData) -> torch.Tensor:
+    if isinstance(cd.dtype, T.DateType):
+        return cd.values.to(torch.int64)
+    if isinstance(cd.dtype, T.TimestampType):
+        return torch.div(cd.values, 86_400_000_000, rounding_mode="floor")
+    raise TypeError("date function needs a date or timestamp column")
+
+
+def to_date(c: ColumnOrName, fmt: str = None) -> Column:
+    def impl(frame, args):
+        a = args[0]
+        if a.is_host or isinstance(a.dtype, T.StringType):
+            return _cast_host_date(frame, a)
+        return ColumnData(_days(a).to(torch.int32), a.valid, T.DateType())
+    return Column(Func("to_date", [_c(c)], impl))
+
+
+def _cast_host_date(frame, a):
+    from .column import Cast as _Cast
+    tmp = ColumnData(a.values, a.valid, a.dtype)
+
+    class _Const(Expr):
+        def eval(self, fr):
+            return tmp
+
+        def refs(self):
+            return []
+    return _Cast(_Const(), T.DateType()).eval(frame)
+
+
+def datediff(end: ColumnOrName, start: ColumnOrName) -> Column:
+    def impl(frame, args):
+        e, s = args
+        valid = None
+        if e.valid is not None or s.valid is not None:
+            valid = e.valid_mask() & s.valid_mask()
+        return ColumnData((_days(e) - _days(s)).to(torch.int32), valid, T.IntegerType())
+    return Column(Func("datediff", [_c(end), _c(start)], impl))
+
+
+def date_add(c: ColumnOrName, days: int) -> Column:
+    def impl(frame, args):
+        a = args[0]
+        return ColumnData((_days(a) + int(days)).to(torch.int32), a.valid, T.DateType())
+    return Column(Func(f"date_add({days})", [_c(c)], impl))
+
+
+def date_sub(c: ColumnOrName, days: int) -> Column:
+    return date_add(c, -int(days))
+
+
+def unix_timestamp(c: ColumnOrName = None, fmt: str = None) -> Column:
+    if c is None:
+        return Column(Func("unix_timestamp", [], lambda frame, args: ColumnData(
+            torch.full((frame._nrows,), int(time.time()), dtype=torch.int64, device=frame._device), None,
+            T.LongType())))
+
+    def impl(frame, args):
+        a = args[0]
+        if isinstance(a.dtype, T.DateType):
+            return ColumnData(a.values.to(torch.int64) * 86400, a.valid, T.LongType())
+        if isinstance(a.dtype, T.TimestampType):
+            return ColumnData(torch.div(a.values, 1_000_000, rounding_mode="floor"), a.valid, T.LongType())
+        ts = _cast_host_ts(frame, a)
+        return ColumnData(torch.div(ts.values, 1_000_000, rounding_mode="floor"), ts.valid, T.LongType())
+    return Column(Func("unix_timestamp", [_c(c)], impl))
+
+
+def _cast_host_ts(frame, a):
+    from .column import Cast as _Cast
+
+    class _Const(Expr):
+        def eval(self, fr):
+            return a
+
+        def refs(self):
+            return []
+    return _Cast(_Const(), T.TimestampType()).eval(frame)
+
+
+def from_unixtime(c: ColumnOrName, fmt: str = "yyyy-MM-dd HH:mm:ss") -> Column:
+    import datetime as _dt
+    py = _spark_to_strftime(fmt)
+    return _host_map("from_unixtime", [c], lambda s: _dt.datetime.utcfromtimestamp(int(s)).strftime(py),
+                     T.StringType())
