@@ -243,14 +243,38 @@ def _coerce_pair(a: ColumnData, b: ColumnData, frame):
 
 
 def _parse_ts_column(cd: ColumnData, frame) -> ColumnData:
-    vals = np.zeros(len(cd), dtype=np.int64)
+    """Host strings -> timestamp micros. Each distinct string is parsed once (a broadcast literal
+    such as the reference's BETWEEN bounds, ref.py:126-127, is one parse, not one per row)."""
+    dev = frame._device
+    n = len(cd)
     valid = cd.valid_mask().copy()
+    if n and valid.all() and all(v is cd.values[0] for v in (cd.values[0], cd.values[n // 2], cd.values[-1])) \
+            and isinstance(cd.values[0], str):
+        first = cd.values[0]
+        if all(v is first for v in cd.values):  # identity check only: a literal column
+            try:
+                us = ts_to_micros(first)
+            except (TypeError, ValueError):
+                return ColumnData(torch.zeros(n, dtype=torch.int64, device=dev),
+                                  torch.zeros(n, dtype=torch.bool, device=dev), T.TimestampType())
+            return ColumnData(torch.full((n,), us, dtype=torch.int64, device=dev), None, T.TimestampType())
+    vals = np.zeros(n, dtype=np.int64)
+    cache = {}
     for i, v in enumerate(cd.values):
         if valid[i] and v is not None:
-            vals[i] = ts_to_micros(v)
+            r = cache.get(v)
+            if r is None:
+                try:
+                    r = ts_to_micros(v)
+                except (TypeError, ValueError):
+                    r = False
+                cache[v] = r
+            if r is False:
+                valid[i] = False
+            else:
+                vals[i] = r
         else:
             valid[i] = False
-    dev = frame._device
     return ColumnData(torch.as_tensor(vals, device=dev), torch.as_tensor(valid, device=dev), T.TimestampType())
 
 

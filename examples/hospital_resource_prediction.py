@@ -79,7 +79,13 @@ def main(argv=None):
     ap.add_argument("--master", default=CONFIG["hdfsMaster"])
     ap.add_argument("--out", default=os.environ.get("CML_HDFS_ROOT", os.path.join(os.getcwd(), "hdfs")))
     ap.add_argument("--plots", default=None, help="directory for the two regression plots (headless savefig)")
+    ap.add_argument("--synth-files", type=int, default=4, help="synthetic uploads when the input dir is empty")
+    ap.add_argument("--synth-rows", type=int, default=2500, help="rows per synthetic upload file")
+    ap.add_argument("--trace", action="store_true", help="print per-phase timings (utils.trace)")
     args = ap.parse_args(argv)
+    if args.trace:
+        from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
+        TRACER.enable(sync=True)
     os.environ["CML_HDFS_ROOT"] = args.out
 
     spark = (SparkSession.builder.appName(CONFIG["appName"]).master(args.master)
@@ -88,7 +94,7 @@ def main(argv=None):
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.io.reader import strip_scheme
     incoming = strip_scheme(CONFIG["hdfsInputPath"])
     if root and not (os.path.isdir(incoming) and os.listdir(incoming)):
-        synth_uploads(incoming)
+        synth_uploads(incoming, n_files=args.synth_files, rows=args.synth_rows)
     spark._comm.barrier()
 
     schema = StructType([
@@ -181,6 +187,9 @@ def main(argv=None):
             print(f"{feature}: {importance}")
         from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.report import operational_insights
         print(operational_insights(lr_rmse, dt_rmse, rf_rmse, dt_accuracy, rf_accuracy))
+        if args.trace:
+            from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
+            print(TRACER.report())
     spark.stop()
     return {"lr_rmse": lr_rmse, "dt_rmse": dt_rmse, "rf_rmse": rf_rmse, "dt_accuracy": dt_accuracy,
             "rf_accuracy": rf_accuracy, "batches": per_batch_rmse, "n_pred": len(predictions_pd)}

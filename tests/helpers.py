@@ -9,8 +9,13 @@ PKG = "clustermachinelearningforhospitalnetworks_apache_spark_amd"
 
 
 def session():
+    """The shared local session, with the temp views of earlier tests dropped (a view shadows a
+    table of the same name, as in Spark, so leftovers would leak between test modules)."""
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
-    return SparkSession.builder.appName("tests").master("local[2]").getOrCreate()
+    s = SparkSession.builder.appName("tests").master("local[2]").getOrCreate()
+    for v in list(s.catalog._views):
+        s.catalog.dropTempView(v)
+    return s
 
 
 def hospital_schema():
