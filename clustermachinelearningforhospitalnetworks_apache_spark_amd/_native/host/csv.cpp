@@ -275,3 +275,29 @@ CML_HOST_API int cml_csv_parse(const char* buf, long long len, const long long* 
 
 // Days-from-civil exposed for the Python side (tests / scalar conversions).
 CML_HOST_API long long cml_days_from_civil(long long y, int m, int d) { return days_from_civil(y, (unsigned)m, (unsigned)d); }
+
+// Arrow-layout materialisation of a parsed string column: trip = n x (offset, len, needs_unquote)
+// from cml_csv_parse, valid = n bytes. First call with data == nullptr returns the byte total
+// (after "" -> " unescaping); second call fills offsets[n+1] (int64) and data.
+CML_HOST_API long long cml_csv_gather_strings(const char* buf, const long long* trip, const unsigned char* valid,
+                                              long long n, char quote, long long* offsets, char* data) {
+  long long pos = 0;
+  for (long long r = 0; r < n; ++r) {
+    if (offsets != nullptr) offsets[r] = pos;
+    if (!valid[r]) continue;
+    const char* s = buf + trip[3 * r];
+    const long long len = trip[3 * r + 1];
+    if (!trip[3 * r + 2]) {
+      if (data != nullptr) std::memcpy(data + pos, s, (size_t)len);
+      pos += len;
+    } else {
+      for (long long i = 0; i < len; ++i) {
+        if (s[i] == quote && i + 1 < len && s[i + 1] == quote) ++i;  // "" -> "
+        if (data != nullptr) data[pos] = s[i];
+        ++pos;
+      }
+    }
+  }
+  if (offsets != nullptr) offsets[n] = pos;
+  return pos;
+}

@@ -129,9 +129,14 @@ def arrow_column_to_data(arr, dt: T.DataType, device) -> ColumnData:
         return ColumnData(torch.as_tensor(mat, device=device), None if valid_np is None else torch.as_tensor(
             valid_np, device=device), dt)
     if dt.torch_dtype is None or dt.host_only:
-        vals = np.array(arr.to_pylist(), dtype=object)
-        if isinstance(dt, T.StringType):
-            vals = np.array([None if v is None else str(v) for v in vals], dtype=object)
+        if isinstance(dt, T.StringType) and (pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type)):
+            vals = arr.to_numpy(zero_copy_only=False)  # Arrow builds the str objects in C++
+            if vals.dtype != object:
+                vals = vals.astype(object)
+        else:
+            vals = np.array(arr.to_pylist(), dtype=object)
+            if isinstance(dt, T.StringType):
+                vals = np.array([None if v is None else str(v) for v in vals], dtype=object)
         return ColumnData(vals, valid_np, dt)
     if isinstance(dt, T.TimestampType):
         np_arr = arr.cast(pa.timestamp("us")).cast(pa.int64()).fill_null(0).to_numpy()

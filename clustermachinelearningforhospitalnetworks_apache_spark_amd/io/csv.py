@@ -21,6 +21,7 @@ from ..sql.column import ColumnData
 
 _native.register_host_sigs({
     "cml_csv_index": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll]),
+    "cml_csv_gather_strings": (c_ll, [ctypes.c_char_p, c_vp, c_vp, c_ll, ctypes.c_char, c_vp, c_vp]),
     "cml_csv_parse": (c_int, [ctypes.c_char_p, c_ll, c_vp, c_ll, c_int, ctypes.c_char, ctypes.c_char, c_vp, c_vp,
                               c_vp, c_int]),
 })
@@ -65,20 +66,28 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
     for f, c, d, v in zip(schema.fields, codes, datas, valids):
         valid = v[:n].astype(bool)
         if c == 0:
-            trip = d.reshape(n, 3) if n else d.reshape(0, 3)
-            vals = np.empty(n, dtype=object)
-            for i in range(n):
-                if valid[i]:
-                    s = buf[trip[i, 0]: trip[i, 0] + trip[i, 1]].decode("utf-8", "replace")
-                    if trip[i, 2]:
-                        s = s.replace(quote * 2, quote)
-                    vals[i] = s
-            out[f.name] = (vals, valid)
+            out[f.name] = (_strings(lib, buf, d, v, n, quote), valid)
         elif c == 5:
             out[f.name] = (d[:n].astype(bool), valid)
         else:
             out[f.name] = (d[:n], valid)
     return out, n
+
+
+def _strings(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int, quote: str) -> np.ndarray:
+    """Object array of str (None for nulls): the native gather writes one Arrow string buffer,
+    Arrow's C++ builds the Python strings — no per-row Python work."""
+    import pyarrow as pa
+    if n == 0:
+        return np.empty(0, dtype=object)
+    total = lib.cml_csv_gather_strings(buf, trip.ctypes.data, valid_u8.ctypes.data, n, quote.encode(), None, None)
+    offsets = np.zeros(n + 1, dtype=np.int64)
+    data = np.zeros(max(total, 1), dtype=np.uint8)
+    lib.cml_csv_gather_strings(buf, trip.ctypes.data, valid_u8.ctypes.data, n, quote.encode(), offsets.ctypes.data,
+                               data.ctypes.data)
+    mask = pa.array(valid_u8[:n].astype(bool)).buffers()[1]
+    arr = pa.LargeStringArray.from_buffers(n, pa.py_buffer(offsets), pa.py_buffer(data), mask)
+    return arr.to_numpy(zero_copy_only=False)
 
 
 def header_names(buf: bytes, sep: str = ",", quote: str = '"') -> List[str]:

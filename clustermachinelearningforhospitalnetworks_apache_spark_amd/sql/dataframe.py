@@ -642,9 +642,9 @@ class DataFrameNaFunctions:
 
 def _non_null_mask(cd: ColumnData) -> torch.Tensor:
     if cd.is_host:
-        m = cd.valid_mask() & np.array([v is not None and not (isinstance(v, float) and math.isnan(v))
-                                        for v in cd.values], dtype=bool)
-        return torch.as_tensor(m)
+        import pandas as pd
+        m = cd.valid_mask() & ~pd.isna(cd.values)  # None / NaN test in C, not a Python loop
+        return torch.as_tensor(np.asarray(m, dtype=bool))
     m = cd.valid_mask()
     if cd.values.is_floating_point():
         if cd.values.dim() == 1:

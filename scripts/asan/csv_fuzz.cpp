@@ -14,6 +14,8 @@
 extern "C" long long cml_csv_index(const char*, long long, char, int, long long*, long long);
 extern "C" int cml_csv_parse(const char*, long long, const long long*, long long, int, char, char, const int*, void**,
                              unsigned char**, int);
+extern "C" long long cml_csv_gather_strings(const char*, const long long*, const unsigned char*, long long, char,
+                                            long long*, char*);
 
 static std::string field(std::mt19937& g) {
   static const char* pieces[] = {"", "1", "-42", "3.25", "1e308", "nan", "true", "false", "2025-03-31 22:00:00",
@@ -61,6 +63,15 @@ int main(int argc, char** argv) {
     const int rc = cml_csv_parse(buf.data(), (long long)buf.size(), starts.data(), n, ncols, ',', '"', types.data(),
                                  data.data(), vptr.data(), 1 + (int)(g() % 4));
     if (rc != 0) continue;
+    for (int c = 0; c < ncols; ++c) {
+      if (types[c] != 0) continue;
+      const long long* trip = reinterpret_cast<const long long*>(store[c].data());
+      const long long bytes = cml_csv_gather_strings(buf.data(), trip, vptr[c], n, '"', nullptr, nullptr);
+      std::vector<long long> offs(n + 1);
+      std::vector<char> chars((size_t)bytes + 1);
+      cml_csv_gather_strings(buf.data(), trip, vptr[c], n, '"', offs.data(), chars.data());
+      if (offs[n] != bytes) return 2;
+    }
     total_rows += n;
   }
   std::printf("csv_fuzz ok: %d inputs, %lld rows parsed\n", iters, total_rows);
