@@ -65,9 +65,14 @@ class LloydEngine:
 
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
-                 accum_mode: Optional[str] = None):
+                 accum_mode: Optional[str] = None, use_graph: Optional[bool] = None):
         self.comm = comm or local_comm()
         self._accum_mode = accum_mode
+        # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
+        # removes the per-launch host cost that dominates small shards. Default: single rank (a
+        # multi-rank step contains RCCL collectives, which stay eagerly launched).
+        self.use_graph = (self.comm.world_size == 1) if use_graph is None else bool(use_graph)
+        self._graph = None
         self.k = int(k)
         self.d = int(d)
         self.gpu = x.is_cuda
@@ -141,18 +146,39 @@ class LloydEngine:
         c = torch.as_tensor(np.asarray(centers, dtype=np.float64), device=self.device)
         if c.shape != (self.k, self.d):
             raise ValueError(f"centers shape {tuple(c.shape)} != {(self.k, self.d)}")
-        self.centers = c.contiguous().clone()
+        if self.centers.shape == c.shape and self.centers.dtype == c.dtype:
+            self.centers.copy_(c)  # in place: a captured step graph keeps reading this buffer
+        else:
+            self.centers = c.contiguous().clone()
         if self.gpu:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
 
     # ------------------------------------------------------------------ iteration
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
-        if self.gpu:
+        if self.gpu and self.use_graph:
+            self._step_graph()
+        elif self.gpu:
             self._step_gpu()
         else:
             self._step_cpu()
         self.iterations += 1
+
+    def _step_graph(self):
+        """Replay the captured step (captured on the first call after one eager warm-up step,
+        which also settles every lazily allocated buffer). All step state lives in buffers the
+        graph reads in place: new centres from set_centers/update are picked up by the replay."""
+        if self._graph is None:
+            if not getattr(self, "_graph_warm", False):
+                self._graph_warm = True
+                self._step_gpu()
+                return
+            torch.cuda.synchronize(self.device)
+            g = torch.cuda.CUDAGraph()
+            with torch.cuda.graph(g):
+                self._step_gpu()
+            self._graph = g
+        self._graph.replay()
 
     def _best(self, r0: int, r1: int):
         return None if self.best is None else self.best[r0:r1]

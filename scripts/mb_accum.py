@@ -14,7 +14,8 @@ def timeit(fn, reps=3):
     return best
 
 
-for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16, 5), (4_000_000, 512, 128)]:
+for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16, 5), (4_000_000, 512, 128),
+                  (1_250_000, 128, 64), (100_000, 16, 5)]:
     g = torch.Generator(device="cuda"); g.manual_seed(0)
     cen = torch.randn(k, d, device="cuda", generator=g) * 4
     x = (cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn(n, d, device="cuda", generator=g)).to(torch.bfloat16)
@@ -33,8 +34,11 @@ for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16
                 print(f"n={n} d={d} k={k} variant {v} grid {ap.grid}x{ap.nwaves}w: assign {t_as:.3f} ms "
                       f"({gb/t_as:.2f} TB/s, {2*n*d*k/t_as/1e9:.0f} TF/s)", flush=True)
             K.set_assign_variant(0)
-        t_st = timeit(lambda: eng.step())
-        print(f"n={n} d={d} k={k} {eng.cplan}: step {t_st:.3f} ms -> {n/t_st/1e6:.2f} Gsamples/s", flush=True)
+        for g in (False, True):
+            eng.use_graph = g
+            t_st = timeit(lambda: eng.step())
+            print(f"n={n} d={d} k={k} {eng.cplan} graph={g}: step {t_st:.3f} ms -> {n/t_st/1e6:.2f} Gsamples/s",
+                  flush=True)
         del eng
         torch.cuda.empty_cache()
     del x

@@ -158,3 +158,27 @@ def test_fp8_features_lloyd_step(n, d, k, mode):
     ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), torch.as_tensor(init).to(torch.bfloat16))
     ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
     assert ok.all()
+
+
+@pytest.mark.parametrize("n,d,k,mode", [(200_000, 64, 16, None), (100_000, 256, 256, "sort"), (50_000, 16, 5, None)])
+def test_graph_replay_matches_eager(n, d, k, mode):
+    """The captured (hipGraph) Lloyd step reproduces eager steps bit for bit, including after
+    set_centers() between fits."""
+    torch.manual_seed(6)
+    x = (torch.randn(n, d, device="cuda") * 2).to(torch.bfloat16)
+    init = x[:k].double().cpu().numpy()
+    out = {}
+    for use_graph in (False, True):
+        eng = LloydEngine(x, d, k, accum_mode=mode, use_graph=use_graph)
+        eng.set_centers(init)
+        for _ in range(4):
+            eng.step()
+        c1 = eng.centers.clone()
+        eng.set_centers(init)
+        for _ in range(2):
+            eng.step()
+        torch.cuda.synchronize()
+        out[use_graph] = (c1, eng.centers.clone(), eng.training_cost())
+        assert (eng._graph is not None) == use_graph
+    assert torch.equal(out[False][0], out[True][0]) and torch.equal(out[False][1], out[True][1])
+    assert out[False][2] == out[True][2]
