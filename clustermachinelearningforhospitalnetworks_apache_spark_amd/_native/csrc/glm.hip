@@ -6,6 +6,8 @@
 // K13 logreg_grad     fused binomial logistic pass: margin = x·w + b, p = σ(margin),
 //                     ∇w += (p − y)·x, ∇b += p − y, loss += softplus(margin) − y·margin,
 //                     X read ONCE per pass (L-BFGS full batch or an SGD mini-batch)
+// K13b partial_colsum  fixed-order sum of the per-block partials (device-side, capturable)
+// K14 sgd_update      momentum SGD step on the device (mini-batch LogisticRegression)
 // K15 gram            [X 1 y]ᵀ[X 1 y] upper triangle in f64 (LinearRegression normal equations)
 // K24 linear_predict  ŷ = x·w + b (identity) or σ(x·w + b) (logistic)
 //
@@ -324,12 +326,20 @@ __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __re
 // ---------------------------------------------------------------------------- K13 logistic gradient
 // Per row group: margin m = x·w + b (CT), p = σ(m), r = wt·(p − y); the lane's chunk of r·x goes
 // into CT accumulators that are folded into f64 every FLUSH rows; loss and weights in f64.
-template <typename T, int NCH>
+template <typename T, int NCH, int U>
 __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     const T* __restrict__ X, long long n, long long ld, int d, int lpr, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[d+1], last = intercept*/,
-    double* __restrict__ out /*[grid][d + 3]: grad (d), grad_b, loss, weight sum*/) {
+    double* __restrict__ out /*[grid][d + 3]: grad (d), grad_b, loss, weight sum*/,
+    const long long* __restrict__ row_base /*optional device row offset: a graph-captured SGD step
+                                              reads its mini-batch position at run time*/) {
   using CT = typename CompT<T>::type;
+  if (row_base != nullptr) {
+    const long long b0 = *row_base;
+    X += b0 * ld;
+    y += b0;
+    if (wt != nullptr) wt += b0;
+  }
   constexpr int CPT = Elt<T>::CPT;
   constexpr int FLUSH = 32;
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
@@ -348,40 +358,54 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   const CT b = (CT)coef[d];
   double gb = 0.0, loss = 0.0, wsum = 0.0;
   const long long step = (long long)gridDim.x * nw * rpw;
+  // U row groups per trip: all groups' loads (X chunks, y, wt) are issued before any margin is
+  // reduced, so each wave keeps U times the bytes in flight, at the price of U·NCH·CPT more VGPRs
+  // (which can cost a resident block per CU; cml_glm_grid sizes the grid from the real occupancy).
   int since = 0;
-  for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += step) {
-    const long long row = row0 + sub;
-    const bool ok = row < n;
-    CT v[NCH][CPT];
-    CT m = 0;
+  for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += U * step) {
+    CT v[U][NCH][CPT];
+    double yi[U], wi[U];
+    bool ok[U];
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int c0 = (c * lpr + li) * CPT;
-      if (ok && c0 < d) {
-        load_chunk_ct<T, CT>(X, row, ld, c0, d, v[c]);
-      } else {
+    for (int u = 0; u < U; ++u) {
+      const long long row = row0 + u * step + sub;
+      ok[u] = row < n;
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) v[c][j] = 0;
+      for (int c = 0; c < NCH; ++c) {
+        const int c0 = (c * lpr + li) * CPT;
+        if (ok[u] && c0 < d) {
+          load_chunk_ct<T, CT>(X, row, ld, c0, d, v[u][c]);
+        } else {
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) v[u][c][j] = 0;
+        }
       }
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
+      yi[u] = ok[u] ? y[row] : 0.0;
+      wi[u] = ok[u] ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
     }
-    m = group_sum_ct<CT>(m, lpr) + b;
-    const double yi = ok ? y[row] : 0.0;
-    const double wi = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
-    const CT p = sigmoid_ct(m);
-    const CT r = (CT)wi * (p - (CT)yi);
 #pragma unroll
-    for (int c = 0; c < NCH; ++c)
+    for (int u = 0; u < U; ++u) {
+      CT m = 0;
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
-    if (li == 0) {
-      gb += (double)r;
-      loss += wi * ((double)softplus_ct(m) - yi * (double)m);
-      wsum += wi;
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) m = fma(v[u][c][j], w[c][j], m);
+      m = group_sum_ct<CT>(m, lpr) + b;
+      const CT p = sigmoid_ct(m);
+      const CT r = (CT)wi[u] * (p - (CT)yi[u]);
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[u][c][j], g[c][j]);
+      if (li == 0) {
+        gb += (double)r;
+        loss += wi[u] * ((double)softplus_ct(m) - yi[u] * (double)m);
+        wsum += wi[u];
+      }
     }
     if constexpr (sizeof(CT) == 4) {
-      if (++since == FLUSH) {
+      since += U;
+      if (since >= FLUSH) {
         since = 0;
 #pragma unroll
         for (int c = 0; c < NCH; ++c)
@@ -398,7 +422,10 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
 #pragma unroll
     for (int j = 0; j < CPT; ++j) g64[c][j] += (double)g[c][j];
   // reduce across row sub-groups, then across waves
-  __shared__ double red[kGlmThreads / 64][64 * 16 + 3];  // lpr*CPT <= 64*16 (fp8)
+  // per-wave rows of lpr·CPT column sums + 3 scalars, sized at launch (logreg_lds_bytes): a fixed
+  // fp8-sized buffer (33 KB) would cap residency at 4 blocks per CU for every dtype
+  extern __shared__ double red_dyn[];
+  const int rs = lpr * CPT + 3;
 #pragma unroll
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -415,25 +442,86 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     __syncthreads();
     if (sub == 0)
 #pragma unroll
-      for (int j = 0; j < CPT; ++j) red[wave][li * CPT + j] = g64[c][j];
+      for (int j = 0; j < CPT; ++j) red_dyn[wave * rs + li * CPT + j] = g64[c][j];
     if (lane == 0 && c == 0) {
-      red[wave][64 * 16] = gb;
-      red[wave][64 * 16 + 1] = loss;
-      red[wave][64 * 16 + 2] = wsum;
+      red_dyn[wave * rs + rs - 3] = gb;
+      red_dyn[wave * rs + rs - 2] = loss;
+      red_dyn[wave * rs + rs - 1] = wsum;
     }
     __syncthreads();
     for (int t = threadIdx.x; t < lpr * CPT; t += blockDim.x) {
       const int col = c * lpr * CPT + t;
       if (col >= d) continue;
       double a = 0.0;
-      for (int ww = 0; ww < nw; ++ww) a += red[ww][t];
+      for (int ww = 0; ww < nw; ++ww) a += red_dyn[ww * rs + t];
       o_[col] = a;
     }
     if (c == 0 && threadIdx.x < 3) {
       double a = 0.0;
-      for (int ww = 0; ww < nw; ++ww) a += red[ww][64 * 16 + threadIdx.x];
+      for (int ww = 0; ww < nw; ++ww) a += red_dyn[ww * rs + rs - 3 + threadIdx.x];
       o_[d + threadIdx.x] = a;
     }
+  }
+}
+
+// ---------------------------------------------------------------------------- K13b / K14 SGD step
+// K13b partial_colsum: msg[j] = Σ_b part[b][j] over the grid's per-block partials in a fixed order:
+// a block owns 16 columns (128-byte row segments) and 64 row slices; slice sums are combined in
+// slice order in LDS. Deterministic, no atomics; ~17 blocks for d = 256 — one short latency chain
+// per thread (a device-scope fence + arrival-counter two-level version measured 3x slower: the
+// release fence writes back L2).
+// K14 sgd_update: the mini-batch optimizer step on the device — g = msg/Σw ⊙ gscale (+ L2 on w),
+// vel = μ·vel − lr·g, coef += vel, eff = coef ⊙ kscale (the coefficients the next K13 reads),
+// loss_acc += loss/Σw, base = (base + batch) mod wrap. With K13 and K13b (plus the RCCL all-reduce
+// of msg when there are several ranks) one SGD step is 3 kernels, none of which the host waits on.
+constexpr int kColsumCols = 16, kColsumSlices = 64;
+
+__global__ __launch_bounds__(kColsumCols* kColsumSlices) void partial_colsum_kernel(const double* __restrict__ part,
+                                                                                   int nb, int m,
+                                                                                   double* __restrict__ msg) {
+  __shared__ double red[kColsumSlices][kColsumCols + 1];
+  const int c = threadIdx.x % kColsumCols, sl = threadIdx.x / kColsumCols;
+  const int col = blockIdx.x * kColsumCols + c;
+  double a = 0.0;
+  if (col < m) {
+#pragma unroll 4
+    for (int b = sl; b < nb; b += kColsumSlices) a += part[(long long)b * m + col];
+  }
+  red[sl][c] = a;
+  __syncthreads();
+  if (sl == 0 && col < m) {
+    double t = 0.0;
+    for (int q = 0; q < kColsumSlices; ++q) t += red[q][c];
+    msg[col] = t;
+  }
+}
+
+__global__ __launch_bounds__(256) void sgd_update_kernel(const double* __restrict__ msg, int d, double* __restrict__ coef,
+                                                         double* __restrict__ vel, double* __restrict__ eff,
+                                                         const double* __restrict__ lr, double mom, double l2,
+                                                         int fit_intercept, const double* __restrict__ gscale,
+                                                         const double* __restrict__ kscale,
+                                                         double* __restrict__ loss_acc, long long* __restrict__ base,
+                                                         long long batch, long long wrap) {
+  const double wsum = fmax(msg[d + 2], 1e-300);
+  const double rate = *lr;
+  for (int j = threadIdx.x; j <= d; j += blockDim.x) {
+    double g = msg[j] / wsum;
+    if (gscale != nullptr) g = g * gscale[j];
+    if (j < d) {
+      if (l2 > 0.0) g = g + l2 * coef[j];
+    } else if (!fit_intercept) {
+      g = 0.0;
+    }
+    const double v = vel[j] * mom - g * rate;
+    vel[j] = v;
+    const double c = coef[j] + v;
+    coef[j] = c;
+    eff[j] = kscale != nullptr ? c * kscale[j] : c;
+  }
+  if (threadIdx.x == 0) {
+    *loss_acc += msg[d + 1] / wsum;
+    *base = (*base + batch) % wrap;
   }
 }
 
@@ -659,13 +747,57 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
     default: return (int)hipErrorInvalidValue;        \
   }
 
-CML_API int cml_glm_grid(long long n, int d, int dtype, int cap) {
+int g_logreg_unroll = 0;  // 0 = auto, else forced U (ablation: cml_glm_set_logreg_unroll)
+
+int logreg_unroll(int nch) {
+  if (g_logreg_unroll == 1 || g_logreg_unroll == 2) return g_logreg_unroll;
+  return 1;  // U = 2 measured slower at every batch size once the grid follows occupancy (mb_logreg.py)
+}
+
+#define CML_U_SWITCH(u, BODY)                                          \
+  if ((u) == 2) { constexpr int U = 2; BODY; } else { constexpr int U = 1; BODY; }
+
+size_t logreg_lds_bytes(int lpr, int cpt) { return (size_t)(kGlmThreads / 64) * (lpr * cpt + 3) * sizeof(double); }
+
+template <typename K>
+int resident_blocks(K kernel, size_t lds = 0) {
+  int nb = 0;
+  if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&nb, kernel, kGlmThreads, lds) != hipSuccess || nb < 1) {
+    (void)hipGetLastError();
+    nb = 1;
+  }
+  return nb;
+}
+
+CML_API int cml_glm_set_logreg_unroll(int u) {
+  g_logreg_unroll = u;
+  return 0;
+}
+
+// Grid of the grid-stride GLM kernels: one block per block-iteration of rows, capped at what the
+// chip holds at once (blocks/CU from the kernel's real VGPR/LDS occupancy × CUs) — a larger
+// persistent grid leaves a tail wave of blocks that runs after everything else.
+// kind: 0 = K7 moments, 1 = K13 logreg_grad, 2 = K24 linear_predict.
+CML_API int cml_glm_grid(long long n, int d, int dtype, int ncu, int kind) {
   const int cpt = dtype == 0 ? 8 : dtype == 1 ? 4 : dtype == 2 ? 2 : 16;
   if (pick_nch(d, cpt) < 0) return -1;  // moments layout limit
   int lpr, nch;
   if (!stream_layout(d, cpt, lpr, nch)) return -1;
-  const int rows = (kGlmThreads / 64) * (64 / lpr) * 16;
-  return grid_for(n, rows, cap);
+  int per_cu = 1;
+  CML_T_SWITCH(dtype, {
+    if (kind == 0) {
+      const int mn = pick_nch(d, Elt<T>::CPT);
+      CML_NCH_SWITCH(mn, { per_cu = resident_blocks(col_moments_kernel<T, NCH>); });
+    } else if (kind == 1) {
+      CML_NCH_SWITCH(nch, {
+        CML_U_SWITCH(logreg_unroll(nch), { per_cu = resident_blocks(logreg_grad_kernel<T, NCH, U>, logreg_lds_bytes(lpr, Elt<T>::CPT)); });
+      });
+    } else {
+      CML_NCH_SWITCH(nch, { per_cu = resident_blocks(linear_predict_kernel<T, NCH>); });
+    }
+  });
+  const int rows = (kGlmThreads / 64) * (64 / lpr);
+  return grid_for(n, rows, per_cu * ncu);
 }
 
 CML_API int cml_col_moments(const void* X, long long n, long long ld, int d, int dtype, const double* shift,
@@ -722,17 +854,37 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
 }
 
 CML_API int cml_logreg_grad(const void* X, long long n, long long ld, int d, int dtype, const double* y,
-                            const double* wt, const double* coef, double* out, int grid, void* stream) {
+                            const double* wt, const double* coef, double* out, int grid, const long long* row_base,
+                            void* stream) {
   hipStream_t st = (hipStream_t)stream;
   CML_T_SWITCH(dtype, {
     int lpr = 0;
     int nch = 0;
     if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
-      hipLaunchKernelGGL((logreg_grad_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const T*)X, n, ld, d,
-                         lpr, y, wt, coef, out);
+      CML_U_SWITCH(logreg_unroll(nch), {
+        hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, U>), dim3(grid), dim3(kGlmThreads),
+                           logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld,
+                           d, lpr, y, wt, coef, out, row_base);
+      });
     });
   });
+  return cml_status();
+}
+
+CML_API int cml_partial_colsum(const double* part, int nb, int m, double* msg, void* stream) {
+  if (nb < 1 || m < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(partial_colsum_kernel, dim3((m + kColsumCols - 1) / kColsumCols), dim3(kColsumCols * kColsumSlices),
+                     0, (hipStream_t)stream, part, nb, m, msg);
+  return cml_status();
+}
+
+CML_API int cml_sgd_update(const double* msg, int d, double* coef, double* vel, double* eff, const double* lr,
+                           double mom, double l2, int fit_intercept, const double* gscale, const double* kscale,
+                           double* loss_acc, long long* base, long long batch, long long wrap, void* stream) {
+  if (d < 1 || batch < 1 || wrap < batch) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_update_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, msg, d, coef, vel, eff, lr, mom,
+                     l2, fit_intercept, gscale, kscale, loss_acc, base, batch, wrap);
   return cml_status();
 }
 

@@ -149,40 +149,21 @@ class LogisticRegression(Estimator):
         return coef, float(p[d]) if fi else 0.0, hist, iters
 
     def _fit_sgd(self, x, y, w, d, std, comm):
-        """Mini-batch SGD with momentum; coefficients and velocity stay on the device."""
-        dev = x.device
+        """Data-parallel mini-batch SGD with momentum (models/sgd.py): coefficients and velocity stay
+        on the device; on one GPU each step is a replayed HIP graph."""
+        from ..models.sgd import LogisticSGD
         l2, _ = self._reg()
         n = x.shape[0]
-        bs = max(1, self.getBatchSize())
-        counts = comm.allgather_object(n)
-        steps_per_epoch = max(1, max((c + bs - 1) // bs for c in counts))
-        coef = torch.zeros(d + 1, dtype=torch.float64, device=dev)
-        vel = torch.zeros_like(coef)
-        lr0, mom = self.getStepSize(), self.getMomentum()
-        fi = self.getFitIntercept()
+        bs = max(1, min(self.getBatchSize(), max(n, 1)))
+        steps_per_epoch = max(1, max(c // max(1, min(bs, c)) if c else 0 for c in comm.allgather_object(n)))
+        opt = LogisticSGD(x, d, y, w, comm, bs, self.getStepSize(), self.getMomentum(), l2, self.getFitIntercept())
         hist = []
-        it = 0
         for epoch in range(self.getMaxIter()):
-            loss_acc = torch.zeros((), dtype=torch.float64, device=dev)
-            for s in range(steps_per_epoch):
-                a = (s * bs) % max(n, 1)
-                b = min(a + bs, n)
-                xb = x[a:b]
-                out = glm_ops.logreg_grad(xb, d, y[a:b], coef, None if w is None else w[a:b])
-                comm.allreduce_(out)
-                wsum = out[d + 2].clamp(min=1e-300)
-                g = torch.cat([out[:d] / wsum + l2 * coef[:d], (out[d] / wsum).reshape(1) if fi
-                               else torch.zeros(1, dtype=torch.float64, device=dev)])
-                lr = lr0 / math.sqrt(1.0 + epoch)
-                vel.mul_(mom).add_(g, alpha=-lr)
-                coef.add_(vel)
-                loss_acc += out[d + 1] / wsum
-                it += 1
-            hist.append(float(loss_acc.item()) / steps_per_epoch)
+            hist.append(opt.epoch(epoch, self.getStepSize(), steps_per_epoch))
             if len(hist) > 1 and abs(hist[-2] - hist[-1]) < self.getTol() * max(abs(hist[-1]), 1.0):
                 break
-        c = coef.cpu().numpy()
-        return c[:d], float(c[d]), hist, it
+        c = opt.coef.cpu().numpy()
+        return c[:d], float(c[d]), hist, opt.steps
 
     def _fit_multinomial(self, x, y, w, d, C, std, comm):
         l2, l1 = self._reg()

@@ -6,21 +6,26 @@ shard and return *partial* statistics; callers all-reduce them.
 """
 from __future__ import annotations
 
+import functools
 from typing import Optional, Tuple
 
 import torch
 
 from .. import _native
-from .._native import c_int, c_ll, c_vp
+from .._native import c_dbl, c_int, c_ll, c_vp
 from ..utils.device import num_cus
 
 _native.register_kernel_sigs({
-    "cml_glm_grid": (c_int, [c_ll, c_int, c_int, c_int]),
+    "cml_glm_grid": (c_int, [c_ll, c_int, c_int, c_int, c_int]),
+    "cml_glm_set_logreg_unroll": (c_int, [c_int]),
     "cml_col_moments": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_scale_apply": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_vp]),
-    "cml_logreg_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_logreg_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_linear_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "cml_gram": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_partial_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
+                               c_vp, c_ll, c_ll, c_vp]),
 })
 
 _CODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2, torch.float8_e4m3fn: 3}
@@ -41,8 +46,19 @@ def _prep(x: torch.Tensor) -> torch.Tensor:
     return x
 
 
-def _grid(n: int, d: int, code: int, dev) -> int:
-    g = _native.kernels().cml_glm_grid(n, d, code, num_cus(dev.index or 0) * 4)
+_KIND = {"moments": 0, "logreg": 1, "predict": 2}
+
+
+_UNROLL = [0]
+
+
+def _grid(n: int, d: int, code: int, dev, kind: str) -> int:
+    return _grid_cached(n, d, code, dev.index or 0, kind, _UNROLL[0])
+
+
+@functools.lru_cache(maxsize=256)
+def _grid_cached(n: int, d: int, code: int, dev_index: int, kind: str, unroll: int) -> int:
+    g = _native.kernels().cml_glm_grid(n, d, code, num_cus(dev_index), _KIND[kind])
     if g < 0:
         raise ValueError(f"feature width {d} too large for the GLM kernels")
     return g
@@ -75,7 +91,7 @@ def _moments_kernel(x: torch.Tensor, d: int, shift: torch.Tensor):
     n = x.shape[0]
     xx = _prep(x)
     code = _CODE[xx.dtype]
-    g = _grid(n, d, code, xx.device)
+    g = _grid(n, d, code, xx.device, "moments")
     out = torch.empty((g, 2, d), dtype=torch.float64, device=xx.device)
     st = _native.kernels().cml_col_moments(xx.data_ptr(), n, xx.stride(0), d, code, shift.data_ptr(), out.data_ptr(),
                                            g, _native.stream_ptr())
@@ -112,12 +128,21 @@ def scale_apply(x: torch.Tensor, d: int, mean: torch.Tensor, inv_std: torch.Tens
 
 
 def logreg_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
-                weight: Optional[torch.Tensor] = None):
+                weight: Optional[torch.Tensor] = None, batch: Optional[int] = None,
+                row_base: Optional[torch.Tensor] = None):
     """Binomial logistic loss + gradient over the local shard.
 
     coef = [w (d) | b] in the ORIGINAL feature space.  Returns a float64 tensor
     [grad_w (d) | grad_b | loss | weight_sum] (sums, not means).
+    With ``row_base`` (int64 device scalar) and ``batch``, the pass covers rows
+    [row_base, row_base + batch) read at kernel run time — the form a captured SGD graph replays.
     """
+    if row_base is not None:
+        if not x.is_cuda:
+            b0 = int(row_base.item())
+            return logreg_grad(x[b0:b0 + batch], d, y[b0:b0 + batch], coef,
+                               None if weight is None else weight[b0:b0 + batch])
+        return _logreg_grad_dev(x, d, y, coef, weight, batch, row_base)
     n = x.shape[0]
     coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
     if not x.is_cuda or n == 0:
@@ -131,15 +156,76 @@ def logreg_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
         return torch.cat([xf.T @ r, r.sum().reshape(1), loss.reshape(1), ww.sum().reshape(1)])
     xx = _prep(x)
     code = _CODE[xx.dtype]
-    g = _grid(n, d, code, xx.device)
+    g = _grid(n, d, code, xx.device, "logreg")
     out = torch.empty((g, d + 3), dtype=torch.float64, device=xx.device)
     yy = y.to(torch.float64).contiguous()
     ww = weight.to(torch.float64).contiguous() if weight is not None else None
     st = _native.kernels().cml_logreg_grad(xx.data_ptr(), n, xx.stride(0), d, code, yy.data_ptr(),
                                            ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
-                                           g, _native.stream_ptr())
+                                           g, 0, _native.stream_ptr())
     _native.check(st, "logreg_grad")
-    return out.sum(0)
+    return partial_colsum(out)
+
+
+def _logreg_grad_dev(x, d, y, coef, weight, batch, row_base):
+    """Device-offset variant: no host read of the batch position (capturable)."""
+    xx = _prep(x)
+    code = _CODE[xx.dtype]
+    coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    g = _grid(batch, d, code, xx.device, "logreg")
+    out = torch.empty((g, d + 3), dtype=torch.float64, device=xx.device)
+    if y.dtype != torch.float64 or not y.is_contiguous():
+        raise ValueError("device-offset logreg_grad needs float64 contiguous labels")
+    st = _native.kernels().cml_logreg_grad(xx.data_ptr(), batch, xx.stride(0), d, code, y.data_ptr(),
+                                           weight.data_ptr() if weight is not None else 0, coef.data_ptr(),
+                                           out.data_ptr(), g, row_base.data_ptr(), _native.stream_ptr())
+    _native.check(st, "logreg_grad")
+    return partial_colsum(out)
+
+
+def partial_colsum(part: torch.Tensor) -> torch.Tensor:
+    """K13b: column sums of the [grid, m] float64 per-block partials, fixed order (deterministic)."""
+    if not part.is_cuda:
+        return part.sum(0)
+    part = part.contiguous()
+    nb, m = part.shape
+    msg = torch.empty(m, dtype=torch.float64, device=part.device)
+    st = _native.kernels().cml_partial_colsum(part.data_ptr(), nb, m, msg.data_ptr(), _native.stream_ptr())
+    _native.check(st, "partial_colsum")
+    return msg
+
+
+def sgd_update(msg: torch.Tensor, d: int, coef: torch.Tensor, vel: torch.Tensor, eff: torch.Tensor,
+               lr: torch.Tensor, momentum: float, l2: float, fit_intercept: bool,
+               gscale: Optional[torch.Tensor], kscale: Optional[torch.Tensor], loss_acc: torch.Tensor,
+               base: torch.Tensor, batch: int, wrap: int) -> None:
+    """K14: one momentum-SGD step from the all-reduced [grad_w | grad_b | loss | Σw] message, in place:
+    vel = μ·vel − lr·(msg/Σw ⊙ gscale + l2·w), coef += vel, eff = coef ⊙ kscale,
+    loss_acc += loss/Σw, base = (base + batch) mod wrap.  All device scalars; nothing syncs."""
+    if not coef.is_cuda:
+        wsum = msg[d + 2].clamp(min=1e-300)
+        g = msg[: d + 1] / wsum
+        if gscale is not None:
+            g = g * gscale
+        if l2 > 0:
+            g = g + torch.cat([l2 * coef[:d], coef.new_zeros(1)])
+        if not fit_intercept:
+            g = torch.cat([g[:d], g.new_zeros(1)])
+        vel.mul_(momentum).sub_(g * lr)
+        coef.add_(vel)
+        eff.copy_(coef if kscale is None else coef * kscale)
+        loss_acc.add_(msg[d + 1] / wsum)
+        base.add_(batch).remainder_(wrap)
+        return
+    for t in (msg, coef, vel, eff):
+        if t.dtype != torch.float64 or not t.is_contiguous():
+            raise ValueError("sgd_update needs contiguous float64 state")
+    ptr = lambda t: 0 if t is None else t.data_ptr()  # noqa: E731
+    st = _native.kernels().cml_sgd_update(msg.data_ptr(), d, coef.data_ptr(), vel.data_ptr(), eff.data_ptr(),
+                                          lr.data_ptr(), float(momentum), float(l2), int(bool(fit_intercept)),
+                                          ptr(gscale), ptr(kscale), loss_acc.data_ptr(), base.data_ptr(), int(batch),
+                                          int(wrap), _native.stream_ptr())
+    _native.check(st, "sgd_update")
 
 
 def linear_predict(x: torch.Tensor, d: int, coef: torch.Tensor, link: str = "identity") -> torch.Tensor:
@@ -150,7 +236,7 @@ def linear_predict(x: torch.Tensor, d: int, coef: torch.Tensor, link: str = "ide
         return torch.sigmoid(m) if link == "logistic" else m
     xx = _prep(x)
     code = _CODE[xx.dtype]
-    g = _grid(n, d, code, xx.device)
+    g = _grid(n, d, code, xx.device, "predict")
     out = torch.empty(n, dtype=torch.float64, device=xx.device)
     st = _native.kernels().cml_linear_predict(xx.data_ptr(), n, xx.stride(0), d, code, coef.data_ptr(),
                                               1 if link == "logistic" else 0, out.data_ptr(), g,
@@ -182,3 +268,9 @@ def gram(x: torch.Tensor, d: int, y: torch.Tensor, weight: Optional[torch.Tensor
     _native.check(st, "gram")
     g = out.sum(0).reshape(m, m)
     return torch.triu(g) + torch.triu(g, 1).T
+
+
+def set_logreg_unroll(u: int) -> None:
+    """Force K13's rows-in-flight per wave (1 or 2; 0 = automatic) — for ablations."""
+    _native.kernels().cml_glm_set_logreg_unroll(int(u))
+    _UNROLL[0] = int(u)
