@@ -85,103 +85,6 @@ template <> struct Elt<double> {
   }
 };
 
-// Load CPT values of row `row` starting at column c0 (zero beyond d; the row stride keeps the
-// vector load in bounds because ld is padded to a multiple of CPT).
-template <typename T>
-__device__ inline void load_chunk(const T* X, long long row, long long ld, int c0, int d, double* v) {
-  constexpr int CPT = Elt<T>::CPT;
-  if (c0 + CPT <= d) {
-    Elt<T>::load(X + row * ld + c0, v);
-  } else {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) v[j] = 0.0;
-    for (int j = 0; c0 + j < d && j < CPT; ++j) {
-      if constexpr (sizeof(T) == 2) v[j] = (double)bf16_to_f32(((const u16*)X)[row * ld + c0 + j]);
-      else if constexpr (sizeof(T) == 1) v[j] = (double)f8_decode(((const f8_t*)X)[row * ld + c0 + j]);
-      else v[j] = (double)X[row * ld + c0 + j];
-    }
-  }
-}
-
-__device__ inline double group_sum(double v, int lpr) {
-  for (int o = lpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
-}
-
-// ---------------------------------------------------------------------------- K7 moments
-template <typename T, int NCH>
-__global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __restrict__ X, long long n, long long ld,
-                                                                  int d, int lpr, const double* __restrict__ shift,
-                                                                  double* __restrict__ out /*[grid][2][d]*/) {
-  constexpr int CPT = Elt<T>::CPT;
-  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
-  const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
-  double s1[NCH][CPT], s2[NCH][CPT], sh[NCH][CPT];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c)
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      s1[c][j] = 0.0;
-      s2[c][j] = 0.0;
-      const int col = (c * lpr + li) * CPT + j;
-      sh[c][j] = col < d ? shift[col] : 0.0;
-    }
-  const long long step = (long long)gridDim.x * nw * rpw;
-  for (long long row = ((long long)blockIdx.x * nw + wave) * rpw + sub; row < n; row += step) {
-#pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int c0 = (c * lpr + li) * CPT;
-      if (c0 >= d) continue;
-      double v[CPT];
-      load_chunk<T>(X, row, ld, c0, d, v);
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        const double t = v[j] - sh[c][j];
-        s1[c][j] += t;
-        s2[c][j] = fma(t, t, s2[c][j]);
-      }
-    }
-  }
-  // reduce the rpw row groups of the wave and the waves of the block through LDS
-  __shared__ double red[kGlmThreads / 64][64 * 8 * 2];
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-#pragma unroll
-    for (int j = 0; j < CPT; ++j) {
-      double a = s1[c][j], b = s2[c][j];
-      for (int o = lpr; o < 64; o <<= 1) {  // sum over sub-groups (lanes li, li+lpr, ...)
-        a += __shfl_xor(a, o, 64);
-        b += __shfl_xor(b, o, 64);
-      }
-      s1[c][j] = a;
-      s2[c][j] = b;
-    }
-  }
-  // lanes 0..lpr-1 of each wave hold the wave totals for their columns
-#pragma unroll
-  for (int c = 0; c < NCH; ++c) {
-    __syncthreads();
-    if (sub == 0) {
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) {
-        red[wave][(li * CPT + j) * 2] = s1[c][j];
-        red[wave][(li * CPT + j) * 2 + 1] = s2[c][j];
-      }
-    }
-    __syncthreads();
-    for (int t = threadIdx.x; t < lpr * CPT; t += blockDim.x) {
-      const int col = c * lpr * CPT + t;
-      if (col >= d) continue;
-      double a = 0.0, b = 0.0;
-      for (int w = 0; w < nw; ++w) {
-        a += red[w][t * 2];
-        b += red[w][t * 2 + 1];
-      }
-      out[((long long)blockIdx.x * 2) * d + col] = a;
-      out[((long long)blockIdx.x * 2 + 1) * d + col] = b;
-    }
-  }
-}
 
 // ---------------------------------------------------------------------------- row streaming
 // Streaming kernels below use one layout: a row is split into 16-byte chunks; LPR lanes (power of
@@ -228,6 +131,130 @@ __device__ inline void load_chunk_ct(const T* X, long long row, long long ld, in
   }
 }
 
+// Raw 16-byte chunks of one row group (zeros for rows past the end; a lane whose chunk starts at
+// or beyond d loads nothing). A chunk straddling d is loaded whole — the row pitch is a multiple
+// of 16 bytes (ops/glm_ops._prep) so the load stays inside the row — and decode_group zeroes the
+// columns >= d, so padding contents (even NaN) never reach a margin.
+template <typename T, int NCH>
+__device__ inline void load_raw_group(const T* X, long long row, long long ld, int lpr, int li, int d, bool ok,
+                                      uint4 (&raw)[NCH]) {
+  constexpr int CPT = Elt<T>::CPT;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int c0 = (c * lpr + li) * CPT;
+    raw[c] = (ok && c0 < d) ? *reinterpret_cast<const uint4*>(X + row * ld + c0) : make_uint4(0u, 0u, 0u, 0u);
+  }
+}
+
+template <typename T, typename CT, int NCH>
+__device__ inline void decode_group(const uint4 (&raw)[NCH], int lpr, int li, int d, CT (&v)[NCH][Elt<T>::CPT]) {
+  constexpr int CPT = Elt<T>::CPT;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const uint4 w = raw[c];
+    const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+    if constexpr (sizeof(T) == 1) {
+      f8_decode16<CT>(w, v[c]);
+    } else if constexpr (sizeof(T) == 2) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        v[c][2 * q] = __uint_as_float(ws[q] << 16);
+        v[c][2 * q + 1] = __uint_as_float(ws[q] & 0xffff0000u);
+      }
+    } else if constexpr (sizeof(T) == 4) {
+#pragma unroll
+      for (int q = 0; q < 4; ++q) v[c][q] = __uint_as_float(ws[q]);
+    } else {
+      v[c][0] = __hiloint2double((int)ws[1], (int)ws[0]);
+      v[c][1] = __hiloint2double((int)ws[3], (int)ws[2]);
+    }
+    const int c0 = (c * lpr + li) * CPT;
+    if (c0 + CPT > d) {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j)
+        if (c0 + j >= d) v[c][j] = 0;
+    }
+  }
+}
+
+// ---------------------------------------------------------------------------- K7 moments
+// Row-streaming layout with the next row group's raw chunks prefetched (as K13). t = x − shift is
+// formed in CT (exact for bf16/f32/fp8 data: the shift is a data row, so it is representable),
+// Σt and Σt² accumulate in f64. Per-wave column sums go through LDS sized at launch.
+template <typename T, int NCH>
+__global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __restrict__ X, long long n, long long ld,
+                                                                  int d, int lpr, const double* __restrict__ shift,
+                                                                  double* __restrict__ out /*[grid][2][d]*/) {
+  using CT = typename CompT<T>::type;
+  constexpr int CPT = Elt<T>::CPT;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
+  double s1[NCH][CPT], s2[NCH][CPT];
+  CT sh[NCH][CPT];
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j) {
+      s1[c][j] = 0.0;
+      s2[c][j] = 0.0;
+      const int col = (c * lpr + li) * CPT + j;
+      sh[c][j] = col < d ? (CT)shift[col] : (CT)0;
+    }
+  const long long step = (long long)gridDim.x * nw * rpw;
+  long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
+  uint4 raw[NCH];
+  if (row0 < n) load_raw_group<T, NCH>(X, row0 + sub, ld, lpr, li, d, row0 + sub < n, raw);
+  for (; row0 < n; row0 += step) {
+    const bool ok = row0 + sub < n;
+    CT v[NCH][CPT];
+    decode_group<T, CT, NCH>(raw, lpr, li, d, v);
+    load_raw_group<T, NCH>(X, row0 + step + sub, ld, lpr, li, d, row0 + step + sub < n, raw);
+    if (ok) {
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          const double t = (double)(v[c][j] - sh[c][j]);
+          s1[c][j] += t;
+          s2[c][j] = fma(t, t, s2[c][j]);
+        }
+    }
+  }
+#pragma unroll
+  for (int c = 0; c < NCH; ++c)
+#pragma unroll
+    for (int j = 0; j < CPT; ++j)
+      for (int o = lpr; o < 64; o <<= 1) {  // sum over the wave's row sub-groups
+        s1[c][j] += __shfl_xor(s1[c][j], o, 64);
+        s2[c][j] += __shfl_xor(s2[c][j], o, 64);
+      }
+  extern __shared__ double red_dyn[];
+  const int rs = 2 * lpr * CPT;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    __syncthreads();
+    if (sub == 0) {
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        red_dyn[wave * rs + (li * CPT + j) * 2] = s1[c][j];
+        red_dyn[wave * rs + (li * CPT + j) * 2 + 1] = s2[c][j];
+      }
+    }
+    __syncthreads();
+    for (int t = threadIdx.x; t < lpr * CPT; t += blockDim.x) {
+      const int col = c * lpr * CPT + t;
+      if (col >= d) continue;
+      double a = 0.0, b = 0.0;
+      for (int w = 0; w < nw; ++w) {
+        a += red_dyn[w * rs + t * 2];
+        b += red_dyn[w * rs + t * 2 + 1];
+      }
+      out[((long long)blockIdx.x * 2) * d + col] = a;
+      out[((long long)blockIdx.x * 2 + 1) * d + col] = b;
+    }
+  }
+}
+
 template <typename CT>
 __device__ inline CT group_sum_ct(CT v, int lpr) {
   for (int o = lpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
@@ -263,39 +290,49 @@ __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __re
     }
   const long long step = (long long)gridDim.x * nw * rpw;
   const bool vec_ok = ((ldy * (long long)sizeof(TO)) % 16 == 0) && ((reinterpret_cast<size_t>(Y) & 15) == 0);
-  for (long long row = ((long long)blockIdx.x * nw + wave) * rpw + sub; row < n; row += step) {
+  // f64 input into a narrower output is scaled in f64, then rounded once
+  using CD = typename std::conditional<sizeof(TI) == 8, double, CT>::type;
+  long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
+  uint4 raw[NCH];
+  if (row0 < n) load_raw_group<TI, NCH>(X, row0 + sub, ldx, lpr, li, d, row0 + sub < n, raw);
+  for (; row0 < n; row0 += step) {
+    const long long row = row0 + sub;
+    CD t[NCH][CPT];
+    decode_group<TI, CD, NCH>(raw, lpr, li, d, t);
+    load_raw_group<TI, NCH>(X, row + step, ldx, lpr, li, d, row + step < n, raw);  // prefetch
+    if (row >= n) continue;
 #pragma unroll
     for (int c = 0; c < NCH; ++c) {
       const int c0 = (c * lpr + li) * CPT;
       if (c0 >= dpad) continue;
       CT v[CPT];
-      if constexpr (sizeof(TI) == 8 && sizeof(TO) < 8) {
-        double t[CPT];
-        load_chunk_ct<TI, double>(X, row, ldx, c0, d, t);
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) v[j] = (CT)((t[j] - (double)mu[c][j]) * (double)is[c][j]);
-      } else {
-        load_chunk_ct<TI, CT>(X, row, ldx, c0, d, v);
-#pragma unroll
-        for (int j = 0; j < CPT; ++j) v[j] = (v[j] - mu[c][j]) * is[c][j];
-      }
+      for (int j = 0; j < CPT; ++j) v[j] = (CT)((t[c][j] - (CD)mu[c][j]) * (CD)is[c][j]);
       TO* yp = Y + row * ldy + c0;
-      if constexpr (sizeof(TO) == 1) {  // OCP e4m3fn output, saturated to +-448
-        unsigned char b[CPT];
+      const bool full = vec_ok && c0 + CPT <= dpad;
+      if constexpr (sizeof(TO) == 1) {  // OCP e4m3fn output, saturated to +-448, packed 4 per word
+        constexpr int NW = (CPT + 3) / 4;
+        unsigned w[NW];
+#pragma unroll
+        for (int q = 0; q < NW; ++q) w[q] = 0u;
 #pragma unroll
         for (int j = 0; j < CPT; j += 2) {
           const float a0 = fminf(fmaxf((float)v[j], -448.f), 448.f);
           const float a1 = j + 1 < CPT ? fminf(fmaxf((float)v[j + 1], -448.f), 448.f) : 0.f;
-          const int pk = __builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false);
-          b[j] = (unsigned char)(pk & 0xff);
-          if (j + 1 < CPT) b[j + 1] = (unsigned char)((pk >> 8) & 0xff);
+          const unsigned pk = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(a0, a1, 0, false) & 0xffffu;
+          w[j / 4] |= pk << (8 * (j % 4));
         }
-        for (int j = 0; c0 + j < dpad && j < CPT; ++j) ((unsigned char*)yp)[j] = b[j];
-        continue;
-      }
-      if (vec_ok && c0 + CPT <= dpad) {
+        if (full) {
+          if constexpr (CPT == 16) *reinterpret_cast<uint4*>(yp) = make_uint4(w[0], w[1], w[2], w[3]);
+          else if constexpr (CPT == 8) *reinterpret_cast<uint2*>(yp) = make_uint2(w[0], w[1]);
+          else if constexpr (CPT == 4) *reinterpret_cast<unsigned*>(yp) = w[0];
+          else *reinterpret_cast<u16*>(yp) = (u16)w[0];
+        } else {
+          for (int j = 0; c0 + j < dpad && j < CPT; ++j) ((unsigned char*)yp)[j] = (unsigned char)(w[j / 4] >> (8 * (j % 4)));
+        }
+      } else if (full) {
         if constexpr (sizeof(TO) == 2) {
-          unsigned w[CPT / 2];
+          unsigned w[(CPT + 1) / 2];
 #pragma unroll
           for (int q = 0; q < CPT / 2; ++q)
             w[q] = (unsigned)f32_to_bf16((float)v[2 * q]) | ((unsigned)f32_to_bf16((float)v[2 * q + 1]) << 16);
@@ -358,30 +395,41 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   const CT b = (CT)coef[d];
   double gb = 0.0, loss = 0.0, wsum = 0.0;
   const long long step = (long long)gridDim.x * nw * rpw;
-  // U row groups per trip: all groups' loads (X chunks, y, wt) are issued before any margin is
-  // reduced, so each wave keeps U times the bytes in flight, at the price of U·NCH·CPT more VGPRs
-  // (which can cost a resident block per CU; cml_glm_grid sizes the grid from the real occupancy).
+  // Software pipeline: the raw 16-byte chunks (and y, wt) of the wave's NEXT row group are loaded
+  // before the current group is decoded and reduced, so two groups are in flight per wave for only
+  // NCH·4 extra VGPRs (raw words, decoded after the wait) — a second decoded group (U = 2, kept for
+  // ablation) costs NCH·CPT·U VGPRs and a resident block per CU.
   int since = 0;
-  for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += U * step) {
+  long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
+  uint4 raw[NCH];
+  double yn = 0.0, wn = 0.0;
+  if (row0 < n) {
+    const long long row = row0 + sub;
+    load_raw_group<T, NCH>(X, row, ld, lpr, li, d, row < n, raw);
+    yn = row < n ? y[row] : 0.0;
+    wn = row < n ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+  }
+  for (; row0 < n; row0 += U * step) {
     CT v[U][NCH][CPT];
     double yi[U], wi[U];
-    bool ok[U];
+    decode_group<T, CT, NCH>(raw, lpr, li, d, v[0]);
+    yi[0] = yn;
+    wi[0] = wn;
 #pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int u = 1; u < U; ++u) {
       const long long row = row0 + u * step + sub;
-      ok[u] = row < n;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c) {
-        const int c0 = (c * lpr + li) * CPT;
-        if (ok[u] && c0 < d) {
-          load_chunk_ct<T, CT>(X, row, ld, c0, d, v[u][c]);
-        } else {
-#pragma unroll
-          for (int j = 0; j < CPT; ++j) v[u][c][j] = 0;
-        }
-      }
-      yi[u] = ok[u] ? y[row] : 0.0;
-      wi[u] = ok[u] ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+      uint4 r2[NCH];
+      load_raw_group<T, NCH>(X, row, ld, lpr, li, d, row < n, r2);
+      yi[u] = row < n ? y[row] : 0.0;
+      wi[u] = row < n ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+      decode_group<T, CT, NCH>(r2, lpr, li, d, v[u]);
+    }
+    {
+      const long long row = row0 + U * step + sub;
+      const bool ok = row < n;
+      load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw);
+      yn = ok ? y[row] : 0.0;
+      wn = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
     }
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -545,20 +593,20 @@ __global__ __launch_bounds__(kGlmThreads) void linear_predict_kernel(const T* __
     }
   const double b = coef[d];
   const long long step = (long long)gridDim.x * nw * rpw;
-  for (long long row0 = ((long long)blockIdx.x * nw + wave) * rpw; row0 < n; row0 += step) {
+  long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
+  uint4 raw[NCH];
+  if (row0 < n) load_raw_group<T, NCH>(X, row0 + sub, ld, lpr, li, d, row0 + sub < n, raw);
+  for (; row0 < n; row0 += step) {
     const long long row = row0 + sub;
     const bool ok = row < n;
+    CT v[NCH][CPT];
+    decode_group<T, CT, NCH>(raw, lpr, li, d, v);
+    load_raw_group<T, NCH>(X, row + step, ld, lpr, li, d, row + step < n, raw);  // prefetch
     CT m = 0;
 #pragma unroll
-    for (int c = 0; c < NCH; ++c) {
-      const int c0 = (c * lpr + li) * CPT;
-      if (ok && c0 < d) {
-        CT v[CPT];
-        load_chunk_ct<T, CT>(X, row, ld, c0, d, v);
+    for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) m = fma(v[j], w[c][j], m);
-      }
-    }
+      for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
     const double mm = (double)group_sum_ct<CT>(m, lpr) + b;
     if (ok && li == 0) out[row] = link == 1 ? sigmoid_ct(mm) : mm;
   }
@@ -757,6 +805,7 @@ int logreg_unroll(int nch) {
 #define CML_U_SWITCH(u, BODY)                                          \
   if ((u) == 2) { constexpr int U = 2; BODY; } else { constexpr int U = 1; BODY; }
 
+size_t moments_lds_bytes(int lpr, int cpt) { return (size_t)(kGlmThreads / 64) * 2 * lpr * cpt * sizeof(double); }
 size_t logreg_lds_bytes(int lpr, int cpt) { return (size_t)(kGlmThreads / 64) * (lpr * cpt + 3) * sizeof(double); }
 
 template <typename K>
@@ -786,8 +835,7 @@ CML_API int cml_glm_grid(long long n, int d, int dtype, int ncu, int kind) {
   int per_cu = 1;
   CML_T_SWITCH(dtype, {
     if (kind == 0) {
-      const int mn = pick_nch(d, Elt<T>::CPT);
-      CML_NCH_SWITCH(mn, { per_cu = resident_blocks(col_moments_kernel<T, NCH>); });
+      CML_NCH_SWITCH(nch, { per_cu = resident_blocks(col_moments_kernel<T, NCH>, moments_lds_bytes(lpr, Elt<T>::CPT)); });
     } else if (kind == 1) {
       CML_NCH_SWITCH(nch, {
         CML_U_SWITCH(logreg_unroll(nch), { per_cu = resident_blocks(logreg_grad_kernel<T, NCH, U>, logreg_lds_bytes(lpr, Elt<T>::CPT)); });
@@ -805,12 +853,12 @@ CML_API int cml_col_moments(const void* X, long long n, long long ld, int d, int
   hipStream_t st = (hipStream_t)stream;
   if (dtype == 3 && d > 512) return (int)hipErrorInvalidValue;  // fp8 wider rows: caller streams bf16 chunks
   CML_T_SWITCH(dtype, {
-    constexpr int CPT = Elt<T>::CPT;
-    const int nch = pick_nch(d, CPT);
-    const int lpr = pick_lpr(d, CPT, nch < 0 ? 8 : nch);
+    int lpr = 0;
+    int nch = 0;
+    if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
-      hipLaunchKernelGGL((col_moments_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const T*)X, n, ld, d,
-                         lpr, shift, out);
+      hipLaunchKernelGGL((col_moments_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads),
+                         moments_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, shift, out);
     });
   });
   return cml_status();
@@ -821,14 +869,16 @@ CML_API int cml_scale_apply(const void* X, long long n, long long ldx, int d, in
                             void* stream) {
   hipStream_t st = (hipStream_t)stream;
   if (n <= 0) return 0;
-  const int cap = 256 * 8;
+  int dev = 0, ncu = 256;
+  if (hipGetDevice(&dev) == hipSuccess) (void)hipDeviceGetAttribute(&ncu, hipDeviceAttributeMultiprocessorCount, dev);
 #define CML_SCALE_LAUNCH(TI, TO)                                                                                  \
   {                                                                                                               \
     int lpr = 0;                                                                                                  \
     int nch = 0;                                                                                                  \
     if (!stream_layout(dpad, Elt<TI>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;                           \
-    const int grid = grid_for(n, (kGlmThreads / 64) * (64 / lpr) * 4, cap);                                       \
     CML_NCH_SWITCH(nch, {                                                                                         \
+      const int grid = grid_for(n, (kGlmThreads / 64) * (64 / lpr),                                              \
+                                resident_blocks(scale_apply_kernel<TI, TO, NCH>) * ncu);                           \
       hipLaunchKernelGGL((scale_apply_kernel<TI, TO, NCH>), dim3(grid), dim3(kGlmThreads), 0, st, (const TI*)X, n, \
                          ldx, d, lpr, mean, inv_std, with_mean, (TO*)Y, ldy, dpad);                              \
     });                                                                                                           \

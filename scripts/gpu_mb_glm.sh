@@ -1,4 +1,8 @@
 set -o pipefail
 cd $GRAFT_REPO_ROOT
-python -c "import __graft_entry__ as g; g.build()" > /dev/null 2>&1 || exit 1
-PYTHONPATH=$GRAFT_REPO_ROOT timeout -k 10 300 python scripts/mb_glm.py 2>&1 | grep -v amdgpu.ids
+mkdir -p gpurun_out/mb
+python -c "import __graft_entry__ as g; g.build()" > gpurun_out/build.log 2>&1 || exit 1
+PYTHONPATH=$GRAFT_REPO_ROOT timeout -k 10 400 python scripts/mb_glm.py > gpurun_out/mb/glm.log 2>&1
+rc=$?
+tail -30 gpurun_out/mb/glm.log
+exit $rc
