@@ -328,8 +328,12 @@ def bench_pipeline(args):
     comm.barrier()
     if gpu:
         torch.cuda.synchronize()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
+    TRACER.reset()  # the CML_TRACE report covers the timed fits only
     t0 = time.perf_counter()
+    model = None
     for _ in range(args.steps):
+        model = None  # release the previous fit's transformed columns (its summaries hold them) first
         model = pipe.fit(df)
     if gpu:
         torch.cuda.synchronize()
@@ -351,7 +355,6 @@ def bench_pipeline(args):
                       "kmeans_cost": km.summary.trainingCost, "logreg_iters": lr.summary.totalIterations}}),
               flush=True)
         if os.environ.get("CML_TRACE") == "1":
-            from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
             print(TRACER.report(), file=sys.stderr, flush=True)
     spark.stop()
 

@@ -7,6 +7,7 @@ every micro-batch.
 """
 from __future__ import annotations
 
+import copy
 from typing import Any, Dict, List, Optional, Union
 
 import torch
@@ -58,9 +59,22 @@ class Model(Transformer):
 
     @property
     def summary(self):
-        if getattr(self, "_summary", None) is None:
+        s = getattr(self, "_summary", None)
+        if s is None:
             raise RuntimeError("No training summary available for this model")
-        return self._summary
+        if hasattr(s, "_model") and s._model is None:
+            # stored detached (no model <-> summary reference cycle, which would keep the training
+            # DataFrame's HBM alive until Python's cycle collector happened to run); hand out a
+            # shallow copy bound to this model
+            b = copy.copy(s)
+            b._model = self
+            return b
+        return s
+
+    def _attach_summary(self, s) -> None:
+        if hasattr(s, "_model"):
+            s._model = None
+        self._summary = s
 
 
 class Evaluator(Params, MLWritable, MLReadable):

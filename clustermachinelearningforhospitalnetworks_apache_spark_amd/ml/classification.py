@@ -99,7 +99,7 @@ class LogisticRegression(Estimator):
             coef, icpt = coef[None, :], np.array([icpt])
         model = LogisticRegressionModel(coef, icpt, num_classes, multinomial)
         self._copyValues(model)
-        model._summary = LogisticRegressionTrainingSummary(model, df, hist, iters)
+        model._attach_summary(LogisticRegressionTrainingSummary(model, df, hist, iters))
         return model
 
     def _reg(self):

@@ -16,6 +16,7 @@ import torch
 
 from ..models.kmeans import LloydEngine
 from ..utils import checkpoint as ckpt
+from ..utils.trace import trace
 from ..sql import types as T
 from ..sql.column import ColumnData
 from . import util as U
@@ -82,9 +83,11 @@ class KMeans(Estimator):
             if init.shape[0] < k:
                 eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids)
         elif self.getInitMode() == "random":
-            init = eng.init_random(seed)
+            with trace("kmeans.init"):
+                init = eng.init_random(seed)
         else:
-            init = eng.init_kmeans_parallel(seed, self.getInitSteps())
+            with trace("kmeans.init"):
+                init = eng.init_kmeans_parallel(seed, self.getInitSteps())
             k_eff = getattr(eng, "k_effective", k)
             if k_eff < k:
                 init = init[:k_eff]
@@ -106,8 +109,8 @@ class KMeans(Estimator):
         comm.allreduce_(sizes)
         model = KMeansModel(centers)
         self._copyValues(model)
-        model._summary = KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
-                                       [int(s) for s in sizes.cpu().tolist()])
+        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
+                                            [int(s) for s in sizes.cpu().tolist()]))
         return model
 
 

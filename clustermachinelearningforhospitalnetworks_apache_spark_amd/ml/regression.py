@@ -147,7 +147,7 @@ class LinearRegression(Estimator):
                                           max_iter=max(self.getMaxIter(), 1) * 10, tol=self.getTol())
         model = LinearRegressionModel(coef, intercept)
         self._copyValues(model)
-        model._summary = LinearRegressionTrainingSummary(model, df, Gn, d, self.getRegParam() == 0.0)
+        model._attach_summary(LinearRegressionTrainingSummary(model, df, Gn, d, self.getRegParam() == 0.0))
         return model
 
 

@@ -330,7 +330,10 @@ class LloydEngine:
             else:
                 w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)
-            out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30)
+            if self.gpu:  # the host BLAS is the slow part of init on a busy CPU; same draws on the device
+                out = local_kmeans_pp_device(torch.as_tensor(cand_np, device=self.device), w, k, seed, max_iter=30)
+            else:
+                out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30)
         if out.shape[0] < k:
             # Spark may return fewer centres when there are < k distinct points; pad by repetition so the
             # device buffers keep their shape, and record the real count.
@@ -378,19 +381,60 @@ def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, 
         centers[i] = points[idx]
         d2 = np.minimum(d2, ((points - centers[i]) ** 2).sum(1))
     pn = (points * points).sum(1)
+    wp = points * w[:, None]
     for _ in range(max_iter):
         dist = pn[:, None] - 2.0 * points @ centers.T + (centers * centers).sum(1)[None, :]
         lab = dist.argmin(1)
-        moved = False
-        for j in range(k):
-            m = lab == j
-            if m.any():
-                c = (points[m] * w[m, None]).sum(0) / max(w[m].sum(), 1e-300)
-            else:
-                c = points[rs.randint(n)]
-            if not np.allclose(c, centers[j]):
-                moved = True
-            centers[j] = c
+        # weighted means of every cluster at once (one scatter-add, no per-cluster Python loop)
+        sums = np.zeros_like(centers)
+        np.add.at(sums, lab, wp)
+        wsum = np.bincount(lab, weights=w, minlength=k)
+        cnt = np.bincount(lab, minlength=k)
+        new = sums / np.maximum(wsum, 1e-300)[:, None]
+        for j in np.flatnonzero(cnt == 0):  # empty clusters re-seed in index order (same draws as before)
+            new[j] = points[rs.randint(n)]
+        moved = not np.isclose(new, centers).all()
+        centers = new
         if not moved:
             break
     return centers
+
+
+def local_kmeans_pp_device(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
+                           max_iter: int = 30) -> np.ndarray:
+    """local_kmeans_pp with the float64 arithmetic on ``points.device``: the RandomState draws are
+    the same calls in the same order (each D²-weighted pick copies only its n probabilities to the
+    host for ``RandomState.choice``), so it picks what the host version picks up to last-bit
+    differences of the distance sums."""
+    rs = np.random.RandomState(seed & 0x7FFFFFFF)
+    pts = points.to(torch.float64)
+    n = pts.shape[0]
+    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0)
+    if float(w.sum()) <= 0:
+        w = torch.ones(n, dtype=torch.float64, device=pts.device)
+    w_np = w.cpu().numpy()
+    centers = torch.empty((k, pts.shape[1]), dtype=torch.float64, device=pts.device)
+    centers[0] = pts[int(rs.choice(n, p=w_np / w_np.sum()))]
+    d2 = ((pts - centers[0]) ** 2).sum(1)
+    for i in range(1, k):
+        pr = (w * d2).cpu().numpy()
+        s = pr.sum()
+        idx = rs.choice(n, p=pr / s) if s > 0 else rs.randint(n)
+        centers[i] = pts[int(idx)]
+        d2 = torch.minimum(d2, ((pts - centers[i]) ** 2).sum(1))
+    pn = (pts * pts).sum(1)
+    wp = pts * w[:, None]
+    for _ in range(max_iter):
+        dist = pn[:, None] - 2.0 * pts @ centers.T + (centers * centers).sum(1)[None, :]
+        lab = dist.argmin(1)
+        sums = torch.zeros_like(centers).index_add_(0, lab, wp)
+        wsum = torch.zeros(k, dtype=torch.float64, device=pts.device).index_add_(0, lab, w)
+        cnt = torch.bincount(lab, minlength=k)
+        new = sums / wsum.clamp(min=1e-300)[:, None]
+        for j in np.flatnonzero(cnt.cpu().numpy() == 0):
+            new[j] = pts[int(rs.randint(n))]
+        moved = not bool(torch.isclose(new, centers).all())
+        centers = new
+        if not moved:
+            break
+    return centers.cpu().numpy()

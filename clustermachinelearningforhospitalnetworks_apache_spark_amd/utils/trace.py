@@ -81,9 +81,10 @@ class Tracer:
 
     def report(self) -> str:
         rows = sorted(self.summary().items(), key=lambda kv: -kv[1]["total_s"])
-        out = [f"{'range':40s} {'count':>7s} {'total ms':>10s} {'avg ms':>9s}"]
+        out = [f"{'range':40s} {'count':>7s} {'total ms':>10s} {'avg ms':>9s} {'max ms':>9s}"]
         for k, v in rows:
-            out.append(f"{k:40s} {v['count']:7d} {v['total_s'] * 1e3:10.2f} {v['total_s'] * 1e3 / v['count']:9.3f}")
+            out.append(f"{k:40s} {v['count']:7d} {v['total_s'] * 1e3:10.2f} {v['total_s'] * 1e3 / v['count']:9.3f} "
+                       f"{v['max_s'] * 1e3:9.3f}")
         return "\n".join(out)
 
 

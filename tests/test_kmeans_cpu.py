@@ -58,3 +58,14 @@ def test_rng_is_deterministic_and_uniform():
     assert u1.min() >= 0 and u1.max() < 1
     p = rng.poisson1(ids, 7).double()
     assert abs(p.mean().item() - 1.0) < 0.01 and abs(p.var().item() - 1.0) < 0.02
+
+
+def test_local_kmeans_pp_device_variant_matches_host():
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import local_kmeans_pp_device
+    rs = np.random.RandomState(4)
+    pts = rs.randn(400, 6) + rs.randint(0, 6, (400, 1)) * 4.0
+    w = rs.rand(400) * 5
+    a = local_kmeans_pp(pts, w, 9, seed=11)
+    b = local_kmeans_pp_device(torch.as_tensor(pts), torch.as_tensor(w), 9, seed=11)
+    np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)
