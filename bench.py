@@ -3,9 +3,13 @@
 "KMeans k=256 on 100M×256, DP across MI355X with RCCL all-reduce of centroid sums".
 
 One step = one full distributed Lloyd iteration on the whole 100M-row dataset:
-K9 MFMA distance GEMM + argmin, K10 per-cluster sums, RCCL all-reduce of the
-f64 [k·D sums | k counts | cost] message, K11 centre update.  Nothing is skipped
-inside the timed region.  The dataset is fixed (100M rows total) and sharded
+K9 MFMA distance GEMM + argmin of EVERY row against EVERY centre, K10 per-cluster
+sums, RCCL all-reduce of the f64 [k·D sums | k counts | cost] message, K11 centre
+update.  K10 is the engine's default incremental form (sums of the current labels
+kept across steps, only rows whose label changed re-read; exact in f64, equal to
+the full re-accumulation — tests/test_kmeans_incremental_gpu.py); the JSON line
+also reports the same steps forced to re-accumulate every row
+(extra.full_accumulate_ms_per_step, or run with --full-accumulate).  The dataset is fixed (100M rows total) and sharded
 over the N ranks, so scaling is *strong*.  Data: synthetic Gaussian blobs
 generated on the GPU, bf16 features, random-init k-means|| centres (no network).
 
@@ -54,6 +58,8 @@ def main():
     ap.add_argument("--k", type=int, default=256)
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
+    ap.add_argument("--full-accumulate", action="store_true",
+                    help="re-accumulate every row each step instead of the exact incremental sums")
     ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
                          "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update; "
@@ -89,7 +95,7 @@ def main():
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
 
-    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks)
+    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks, incremental=not args.full_accumulate)
     t0 = time.perf_counter()
     init = eng.init_kmeans_parallel(seed=42) if args.init == "k-means||" else eng.init_random(seed=42)
     eng.set_centers(init)
@@ -111,6 +117,20 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_scalar(elapsed)
     cost = eng.training_cost()
+    acc = {"accumulate": "incremental (exact)" if eng.delta is not None else "full"}
+    if eng.delta is not None and gpu:
+        # transparency: the same steps with every step forced to re-accumulate all rows
+        acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
+        acc["last_step_full_rank0"] = eng.delta.was_full()
+        comm.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            eng.delta.invalidate()
+            eng.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        acc["full_accumulate_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - t1) / args.steps
 
     total_rows = args.rows
     value = total_rows * args.steps / elapsed
@@ -140,7 +160,7 @@ def main():
                 "row_chunks_per_rank": eng.row_chunks,
             },
             "extra": {"datagen_s": round(gen_s, 3), "init_s": round(init_s, 3),
-                      "training_cost": cost, "device": torch.cuda.get_device_name(dev) if gpu else "cpu"},
+                      "training_cost": cost, "device": torch.cuda.get_device_name(dev) if gpu else "cpu", **acc},
         }
         print(json.dumps(out), flush=True)
     comm.shutdown()

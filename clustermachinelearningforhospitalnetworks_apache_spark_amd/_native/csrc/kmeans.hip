@@ -183,12 +183,22 @@ __device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& 
   }
 }
 
+// Incremental sums (Lloyd step on label changes only): the single-launch assign appends every row
+// whose label differs from the one it held before this step to (rows, old), in wave-aggregated
+// batches; `count` may exceed `cap` (the step then falls back to the full accumulate).
+struct DeltaOut {
+  int* rows;
+  int* old;
+  unsigned* count;
+  int cap;
+};
+
 template <int DP, int RT, int RINGMAX>
 __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP, RT>& xt, long long tile,
                                             long long n, int r, int g, int c_base, const float* __restrict__ xnorm,
                                             int* __restrict__ labels, float* __restrict__ best_io, int first,
                                             int last, bool ranking, int* hist, int* __restrict__ rank_out,
-                                            double& cost) {
+                                            const DeltaOut& dout, double& cost) {
   constexpr int KS = AssignShape<DP>::KS;
   constexpr int RING = KS < RINGMAX ? KS : RINGMAX;
   float xn[RT];
@@ -246,6 +256,23 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
       const int pi = labels[row];
       if (pb <= best) { best = pb; bidx = pi; }  // earlier chunks hold smaller indices
     }
+    if (dout.rows != nullptr) {  // incremental sums: log rows whose label changed (single-launch assign)
+      const int prev = mine ? labels[row] : bidx;
+      const bool ch = mine && prev != bidx;
+      const unsigned long long bal = __ballot(ch);
+      if (bal != 0ull) {
+        const int lane = r + 16 * g;
+        const int leader = __builtin_ctzll(bal);
+        unsigned base = 0u;
+        if (lane == leader) base = atomicAdd(dout.count, (unsigned)__popcll(bal));
+        base = __shfl(base, leader, 64);
+        const unsigned at = base + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
+        if (ch && at < (unsigned)dout.cap) {
+          dout.rows[at] = (int)row;
+          dout.old[at] = prev;
+        }
+      }
+    }
     if (mine) {
       labels[row] = bidx;
       if (last) {
@@ -267,7 +294,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     const void* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
     int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
     int* __restrict__ labels, float* __restrict__ best_io, int first, int last, double* __restrict__ cost_part,
-    int* __restrict__ hist_out, int* __restrict__ rank_out) {
+    int* __restrict__ hist_out, int* __restrict__ rank_out, DeltaOut dout) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NCH = AssignShape<DP>::NCH;
   constexpr int KS = AssignShape<DP>::KS;
@@ -325,18 +352,18 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
       const long long t1 = tile + tw;
       if (t1 < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1, r, g, xb);
       assign_tile<DP, RT, RINGMAX>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
-                          rank_out, cost);
+                          rank_out, dout, cost);
       if (t1 >= ntiles) break;
       if (t1 + tw < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1 + tw, r, g, xa);
       assign_tile<DP, RT, RINGMAX>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
-                          rank_out, cost);
+                          rank_out, dout, cost);
     }
   } else {
     for (; tile < ntiles; tile += tw) {
       XTile<DP, RT> xt;
       load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xt);
       assign_tile<DP, RT, RINGMAX>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
-                          rank_out, cost);
+                          rank_out, dout, cost);
     }
   }
   if (last && (cost_part != nullptr || ranking)) {
@@ -532,7 +559,9 @@ __global__ void kmeans_reduce_kernel(const float* __restrict__ slab, const int* 
 
 // Sort regime, pass 2a: tot[c] = Σ_b hist[b][c]   (one block per cluster).
 __global__ __launch_bounds__(256) void kmeans_seg_totals(const int* __restrict__ hist, int nblk, int kp,
-                                                         long long* __restrict__ tot) {
+                                                         long long* __restrict__ tot, const int* __restrict__ gate,
+                                                         int want) {
+  if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
   __shared__ long long ws[4];
   const int c = blockIdx.x, tid = threadIdx.x;
   long long s = 0;
@@ -550,7 +579,9 @@ __global__ __launch_bounds__(256) void kmeans_seg_offsets(const int* __restrict_
                                                           const long long* __restrict__ tot,
                                                           const double* __restrict__ cost_part, int ncost, int D,
                                                           int* __restrict__ off, int* __restrict__ seg,
-                                                          double* __restrict__ msg) {
+                                                          double* __restrict__ msg, const int* __restrict__ gate,
+                                                          int want) {
+  if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
   __shared__ long long ws[4];
   __shared__ long long carry;
   const int c = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
@@ -596,15 +627,40 @@ __global__ __launch_bounds__(256) void kmeans_seg_offsets(const int* __restrict_
 }
 
 // Sort regime, pass 3: perm[off[label][block(row)] + rank[row]] = row.
-__global__ void kmeans_scatter(const int* __restrict__ labels, const int* __restrict__ rank, long long n, int nblk,
-                               int nwaves, int tile_rows, const int* __restrict__ off, int* __restrict__ perm) {
-  const long long tw = (long long)nblk * nwaves;
-  for (long long row = (long long)blockIdx.x * blockDim.x + threadIdx.x; row < n;
-       row += (long long)gridDim.x * blockDim.x) {
-    const long long tile = row / tile_rows;
-    const int blk = (int)((tile % tw) / nwaves);
-    const int lab = labels[row];
-    perm[off[(long long)lab * nblk + blk] + rank[row]] = (int)row;
+// One workgroup per assign workgroup b: it walks exactly the rows b ranked (groups of
+// nwaves*tile_rows consecutive rows every nblk*nwaves tiles), so the block index needs no
+// per-row 64-bit division, and b's k offsets sit in LDS instead of being gathered per row.
+// Every thread keeps kScatterU of b's rounds' loads in flight (one dependent load pair per thread
+// left the pass latency-bound). All of b's rows stay on ONE workgroup: its (b, label) output runs
+// are then written from one CU / L2 only — splitting a run over workgroups on several XCDs made
+// the partial-line writes 1.4x slower.
+constexpr int kScatterThreads = 512;
+constexpr int kScatterU = 4;
+__global__ __launch_bounds__(kScatterThreads) void kmeans_scatter(const int* __restrict__ labels,
+                                                                  const int* __restrict__ rank, long long n, int nblk,
+                                                                  int nwaves, int tile_rows, int k,
+                                                                  const int* __restrict__ off, int* __restrict__ perm,
+                                                                  const int* __restrict__ gate, int want) {
+  extern __shared__ int soff[];
+  if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
+  const int b = blockIdx.x;
+  for (int c = threadIdx.x; c < k; c += blockDim.x) soff[c] = off[(long long)c * nblk + b];
+  __syncthreads();
+  const long long grp = (long long)nwaves * tile_rows;  // rows b owns per round
+  const long long stride = grp * nblk;                  // rows between two of b's rounds
+  for (long long r0 = (long long)b * grp; r0 < n; r0 += stride * kScatterU) {
+    for (long long o = threadIdx.x; o < grp; o += blockDim.x) {
+      int lab[kScatterU], rk[kScatterU];
+#pragma unroll
+      for (int u = 0; u < kScatterU; ++u) {
+        const long long row = r0 + u * stride + o;
+        lab[u] = row < n ? labels[row] : -1;
+        rk[u] = row < n ? rank[row] : 0;
+      }
+#pragma unroll
+      for (int u = 0; u < kScatterU; ++u)
+        if (lab[u] >= 0) perm[soff[lab[u]] + rk[u]] = (int)(r0 + u * stride + o);
+    }
   }
 }
 
@@ -662,14 +718,17 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k, long long chunk,
                                                              double* __restrict__ msg, double* __restrict__ slots,
-                                                             int* __restrict__ slot_c) {
+                                                             int* __restrict__ slot_c, const int* __restrict__ gate,
+                                                             int want) {
   using raw_t = typename SegRaw<CPL, F8>::T;
   constexpr int U = 16;
+  if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
   const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
   constexpr int ESZ = F8 ? 1 : 2;  // bytes per element
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (kSegThreads / 64) + (threadIdx.x >> 6);
   const long long p0 = wave * chunk;
+  n = n < (long long)seg[k] ? n : (long long)seg[k];  // sorted positions actually filled (delta lists: <= bound)
   if (p0 >= n) {
     if (lane == 0) {
       slot_c[2 * wave] = -1;
@@ -760,7 +819,9 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
 // (A) / tail (B) partials for c. One workgroup per cluster.
 __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long chunk,
                                                         long long nwaves, const double* __restrict__ slots,
-                                                        const int* __restrict__ slot_c, double* __restrict__ msg) {
+                                                        const int* __restrict__ slot_c, double* __restrict__ msg,
+                                                        const int* __restrict__ gate, int want) {
+  if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
   const int c = blockIdx.x;
   const long long s0 = seg[c], s1 = seg[c + 1];
   if (s1 <= s0) return;
@@ -827,6 +888,159 @@ __global__ void kmeans_update_kernel(const double* __restrict__ bufs, int nbuf, 
   }
 }
 
+__global__ void zero_f64_gated(double* __restrict__ p, long long n, const int* __restrict__ gate, int want) {
+  if (gate != nullptr && gate[0] != want) return;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x)
+    p[i] = 0.0;
+}
+
+// ---------------------------------------------------------------------------------------------
+// Incremental sums. Lloyd's new per-cluster sums equal the previous ones plus the rows that moved
+// in minus the rows that moved out, so once labels settle (measured on the bench data: 0.03-0.4 %
+// of rows change per iteration) the accumulate only has to touch the changed rows instead of
+// re-reading all of X. The state `acc` = [k·D sums | k counts | cost] of the CURRENT labels lives
+// across steps; the message that is all-reduced is a copy of it.
+//   gate kernel : mode[0] = 1 (full accumulate into acc) if forced or more than cap rows changed,
+//                 else 0; mode[1] = #changed rows; resets the change counter and the delta histogram.
+//   delta path  : counting sort of the 2m entries (+row under its new label, -row under its old
+//                 label, key = label or k + label) -> the same segmented f64 sums as the full path
+//                 over 2k segments -> acc[c] += S[c] - S[k + c], counts likewise.
+// Every value is a bf16/fp8 row summed in f64: those sums are exact while they stay inside f64's
+// 53-bit window, so the incremental result equals the full recompute (and, like the full path, does
+// not depend on the order rows are added in) — tests/test_kmeans_kernels_gpu.py checks it bitwise.
+// ---------------------------------------------------------------------------------------------
+constexpr int kDeltaThreads = 256;
+constexpr int kDeltaBlocks = 512;
+
+__global__ __launch_bounds__(256) void kmeans_delta_gate(unsigned* __restrict__ count, int cap,
+                                                         int* __restrict__ force, int* __restrict__ mode, int k,
+                                                         int* __restrict__ dh) {
+  __shared__ int full;
+  if (threadIdx.x == 0) {
+    const unsigned m = *count;
+    full = (*force != 0 || m > (unsigned)cap) ? 1 : 0;
+    mode[0] = full;
+    mode[1] = full ? 0 : (int)m;
+    *count = 0u;
+    *force = 0;
+  }
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) dh[i] = 0;
+}
+
+// Range of the change list one delta block owns (m from the gate, known only on the device).
+__device__ __forceinline__ void delta_range(const int* mode, int& i0, int& i1) {
+  const long long m = mode[1];
+  i0 = (int)(m * blockIdx.x / gridDim.x);
+  i1 = (int)(m * (blockIdx.x + 1) / gridDim.x);
+}
+
+// Histogram of the 2m delta entries by key, block-aggregated in LDS.
+__global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_hist(const int* __restrict__ rows,
+                                                                   const int* __restrict__ old,
+                                                                   const int* __restrict__ labels,
+                                                                   const int* __restrict__ mode, int k,
+                                                                   int* __restrict__ dh) {
+  if (mode[0] != 0) return;
+  extern __shared__ int lh[];
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  int i0, i1;
+  delta_range(mode, i0, i1);
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    atomicAdd(lh + labels[rows[i]], 1);
+    atomicAdd(lh + k + old[i], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x)
+    if (lh[i]) atomicAdd(dh + i, lh[i]);
+}
+
+// seg[j] = first sorted position of key j (seg[2k] = 2m); cursor[j] = seg[j]. One workgroup.
+__global__ __launch_bounds__(256) void kmeans_delta_scan(const int* __restrict__ dh, const int* __restrict__ mode,
+                                                         int k, int* __restrict__ seg, int* __restrict__ cursor) {
+  if (mode[0] != 0) return;
+  __shared__ int part[256];
+  const int nk = 2 * k, per = (nk + 255) / 256, t = threadIdx.x;
+  int s = 0;
+  for (int j = t * per; j < (t + 1) * per && j < nk; ++j) s += dh[j];
+  part[t] = s;
+  __syncthreads();
+  if (t == 0) {
+    int acc = 0;
+    for (int i = 0; i < 256; ++i) {
+      const int v = part[i];
+      part[i] = acc;
+      acc += v;
+    }
+    seg[nk] = acc;
+  }
+  __syncthreads();
+  int acc = part[t];
+  for (int j = t * per; j < (t + 1) * per && j < nk; ++j) {
+    seg[j] = acc;
+    cursor[j] = acc;
+    acc += dh[j];
+  }
+}
+
+// perm[cursor[key]++] = row for both entries of every changed row (block reserves per-key ranges).
+__global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_scatter(const int* __restrict__ rows,
+                                                                      const int* __restrict__ old,
+                                                                      const int* __restrict__ labels,
+                                                                      const int* __restrict__ mode, int k,
+                                                                      int* __restrict__ cursor,
+                                                                      int* __restrict__ perm) {
+  if (mode[0] != 0) return;
+  extern __shared__ int lh[];  // [2k] counts, then bases
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
+  __syncthreads();
+  int i0, i1;
+  delta_range(mode, i0, i1);
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    atomicAdd(lh + labels[rows[i]], 1);
+    atomicAdd(lh + k + old[i], 1);
+  }
+  __syncthreads();
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = lh[i] ? atomicAdd(cursor + i, lh[i]) : 0;
+  __syncthreads();
+  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+    const int row = rows[i];
+    perm[atomicAdd(lh + labels[row], 1)] = row;
+    perm[atomicAdd(lh + k + old[i], 1)] = row;
+  }
+}
+
+// acc[c] += S[c] - S[k+c] (sums), counts from the segment sizes, cost from the assign partials;
+// on full steps only the cost. Then msg = acc (the buffer that is all-reduced).
+__global__ void kmeans_delta_apply(double* __restrict__ acc, const double* __restrict__ dsum,
+                                   const int* __restrict__ seg, const int* __restrict__ mode, int k, int D,
+                                   const double* __restrict__ cost_part, int ncost, double* __restrict__ msg) {
+  const long long kd = (long long)k * D;
+  const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const bool delta = mode[0] == 0;
+  if (idx < kd) {
+    double v = acc[idx];
+    if (delta) {
+      v += dsum[idx] - dsum[kd + idx];
+      acc[idx] = v;
+    }
+    msg[idx] = v;
+  } else if (idx < kd + k) {
+    const int c = (int)(idx - kd);
+    double v = acc[idx];
+    if (delta) {
+      v += (double)((seg[c + 1] - seg[c]) - (seg[k + c + 1] - seg[k + c]));
+      acc[idx] = v;
+    }
+    msg[idx] = v;
+  } else if (idx == kd + k) {
+    double cs = 0.0;
+    for (int i = 0; i < ncost; ++i) cs += cost_part[i];
+    acc[idx] = cs;
+    msg[idx] = cs;
+  }
+}
+
 long long assign_lds_bytes(int kc, int kp, int Dp) {
   const long long ks = Dp >= 32 ? Dp / 32 : 1;
   return (long long)(kc / 16) * ks * 1024 + (long long)kc * 4 + (long long)((kp + 3) & ~3) * 4 + 16 * 8;
@@ -885,13 +1099,13 @@ int assign_occupancy(int kc, int kp) {
 template <int DP, bool F8>
 int launch_assign(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp,
                   int c_base, const float* cnorm, const float* xnorm, int* labels, float* best, int first, int last,
-                  double* cost_part, int* hist, int* rank, int grid, hipStream_t st) {
+                  double* cost_part, int* hist, int* rank, DeltaOut dout, int grid, hipStream_t st) {
   const size_t lds = (size_t)assign_lds_bytes(kc, kp, DP);
   const void* fn = assign_kernel_ptr<DP, F8>();
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   void* args[] = {(void*)&X, (void*)&n, (void*)&ldx, (void*)&C, (void*)&ldc, (void*)&kc, (void*)&kp,
                   (void*)&c_base, (void*)&cnorm, (void*)&xnorm, (void*)&labels, (void*)&best, (void*)&first,
-                  (void*)&last, (void*)&cost_part, (void*)&hist, (void*)&rank};
+                  (void*)&last, (void*)&cost_part, (void*)&hist, (void*)&rank, (void*)&dout};
   const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(assign_threads(0)), args, lds, st);
   if (e != hipSuccess) return (int)e;
   return cml_status();
@@ -909,6 +1123,33 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
   hipFuncSetAttribute((const void*)kmeans_accum_priv<CPL, RPW>, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL((kmeans_accum_priv<CPL, RPW>), dim3(gx, nsl), dim3(kAccumThreads), lds, st, X, n, ldx, labels, k,
                      dw, slab, cslab);
+  return cml_status();
+}
+
+// Segmented f64 sums over a sorted position list (kmeans_segacc + kmeans_seg_fixup); n is an upper
+// bound of the filled positions (the kernels clamp to seg[k]).
+int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, const int* perm, const int* seg, int k,
+                  int cpl, int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate, int want,
+                  hipStream_t st) {
+  const long long waves = (long long)seg_grid * (kSegThreads / 64);
+  const long long chunk = (n + waves - 1) / waves;
+#define CML_SEG(C, F)                                                                                              \
+  hipLaunchKernelGGL((kmeans_segacc<C, F>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm, seg, \
+                     k, chunk, msg, slots, slot_c, gate, want)
+  if (xfp8) {
+    if (cpl == 4) CML_SEG(4, true);
+    else if (cpl == 8) CML_SEG(8, true);
+    else if (cpl == 16) CML_SEG(16, true);
+    else return (int)hipErrorInvalidValue;
+  } else if (cpl == 2) CML_SEG(2, false);
+  else if (cpl == 4) CML_SEG(4, false);
+  else if (cpl == 8) CML_SEG(8, false);
+  else return (int)hipErrorInvalidValue;
+#undef CML_SEG
+  const int e = cml_status();
+  if (e) return e;
+  hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, chunk, waves, slots, slot_c, msg, gate,
+                     want);
   return cml_status();
 }
 
@@ -954,8 +1195,12 @@ CML_API long long cml_kmeans_seg_ints(int k) { return (long long)(k + 1) + ((k +
 CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, int Dp, const void* C, long long ldc,
                                    int kc, int kp, int c_base, const float* cnorm, const float* xnorm, int* labels,
                                    float* best, int first, int last, double* cost_part, int* hist, int* rank,
-                                   int grid, int xfp8, void* stream) {
+                                   int grid, int xfp8, int* chg_rows, int* chg_old, unsigned* chg_count, int chg_cap,
+                                   void* stream) {
   if (kc % 16 != 0 || Dp % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  if (chg_rows != nullptr && (!(first && last) || chg_old == nullptr || chg_count == nullptr || chg_cap < 0))
+    return (int)hipErrorInvalidValue;  // label changes are only defined for a single-launch assign
+  const DeltaOut dout{chg_rows, chg_old, chg_count, chg_cap};
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if ((hist == nullptr) != (rank == nullptr)) return (int)hipErrorInvalidValue;
   if (best == nullptr && !(first && last)) return (int)hipErrorInvalidValue;
@@ -967,7 +1212,7 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
 #define CML_ASSIGN8(DP)                                                                                          \
   case DP:                                                                                                       \
     return launch_assign<DP, true>(X, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last,  \
-                                   cost_part, hist, rank, grid, st)
+                                   cost_part, hist, rank, dout, grid, st)
       CML_ASSIGN8(64); CML_ASSIGN8(128); CML_ASSIGN8(256); CML_ASSIGN8(512);
 #undef CML_ASSIGN8
       default: return (int)hipErrorInvalidValue;
@@ -976,7 +1221,7 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
 #define CML_ASSIGN(DS, DP)                                                                                       \
   case DS:                                                                                                       \
     return launch_assign<DP, false>(X, n, ldx, c, ldc, kc, kp, c_base, cnorm, xnorm, labels, best, first, last, \
-                                    cost_part, hist, rank, grid, st)
+                                    cost_part, hist, rank, dout, grid, st)
   switch (Dp / 16) {
     CML_ASSIGN(1, 16); CML_ASSIGN(2, 32); CML_ASSIGN(4, 64); CML_ASSIGN(8, 128); CML_ASSIGN(16, 256);
     CML_ASSIGN(32, 512);
@@ -1054,50 +1299,65 @@ CML_API int cml_kmeans_reduce(const float* slab, const int* cslab, const double*
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                   const int* rank, const int* hist, int nblk, int nwaves, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
-                                  int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, void* stream) {
+                                  int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
+                                  void* stream) {
   hipStream_t st = (hipStream_t)stream;
   long long* tot = reinterpret_cast<long long*>(seg + k + 1 + ((k + 1) & 1));  // scratch after seg (8-B aligned)
-  hipMemsetAsync(msg, 0, sizeof(double) * (size_t)k * D, st);
-  hipLaunchKernelGGL(kmeans_seg_totals, dim3(k), dim3(256), 0, st, hist, nblk, kp, tot);
+  const int want = 1;  // gated launches run on full-accumulate steps only
+  if (gate == nullptr) {
+    hipMemsetAsync(msg, 0, sizeof(double) * (size_t)k * D, st);
+  } else {
+    hipLaunchKernelGGL(zero_f64_gated, dim3(256), dim3(256), 0, st, msg, (long long)k * D, gate, want);
+  }
+  hipLaunchKernelGGL(kmeans_seg_totals, dim3(k), dim3(256), 0, st, hist, nblk, kp, tot, gate, want);
   hipLaunchKernelGGL(kmeans_seg_offsets, dim3(k), dim3(256), 0, st, hist, nblk, k, kp, tot, cost_part, ncost, D, off,
-                     seg, msg);
+                     seg, msg, gate, want);
   int e = cml_status();
   if (e) return e;
   if (n == 0) return 0;
-  const long long sblocks = (n + 255) / 256 < 4096 ? (n + 255) / 256 : 4096;
-  hipLaunchKernelGGL(kmeans_scatter, dim3((unsigned)sblocks), dim3(256), 0, st, labels, rank, n, nblk, nwaves,
-                     assign_tile_rows(Dp), off,
-                     perm);
+  hipLaunchKernelGGL(kmeans_scatter, dim3(nblk), dim3(kScatterThreads), sizeof(int) * (size_t)k, st,
+                     labels, rank, n,
+                     nblk, nwaves, assign_tile_rows(Dp), k, off, perm, gate, want);
   e = cml_status();
   if (e) return e;
-  const long long waves = (long long)seg_grid * (kSegThreads / 64);
-  const long long chunk = (n + waves - 1) / waves;
-  if (xfp8) {
-    if (cpl == 4)
-      hipLaunchKernelGGL((kmeans_segacc<4, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                         seg, k, chunk, msg, slots, slot_c);
-    else if (cpl == 8)
-      hipLaunchKernelGGL((kmeans_segacc<8, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                         seg, k, chunk, msg, slots, slot_c);
-    else if (cpl == 16)
-      hipLaunchKernelGGL((kmeans_segacc<16, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                         seg, k, chunk, msg, slots, slot_c);
-    else
-      return (int)hipErrorInvalidValue;
-  } else if (cpl == 2)
-    hipLaunchKernelGGL((kmeans_segacc<2, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                       seg, k, chunk, msg, slots, slot_c);
-  else if (cpl == 4)
-    hipLaunchKernelGGL((kmeans_segacc<4, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                       seg, k, chunk, msg, slots, slot_c);
-  else if (cpl == 8)
-    hipLaunchKernelGGL((kmeans_segacc<8, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm,
-                       seg, k, chunk, msg, slots, slot_c);
-  else
-    return (int)hipErrorInvalidValue;
-  e = cml_status();
+  return launch_segsum(X, n, ldx, Dp, D, perm, seg, k, cpl, seg_grid, msg, slots, slot_c, xfp8, gate, want, st);
+}
+
+// ---- incremental sums (see kmeans_delta_gate). Per step, after the single-launch assign that
+// logged label changes: cml_kmeans_delta_gate, then cml_kmeans_sort_accum(gate = mode, msg = acc),
+// then cml_kmeans_delta_accum (which also publishes msg = acc).
+CML_API int cml_kmeans_delta_gate(unsigned* chg_count, int cap, int* force, int* mode, int k, int* dh,
+                                  void* stream) {
+  hipLaunchKernelGGL(kmeans_delta_gate, dim3(1), dim3(256), 0, (hipStream_t)stream, chg_count, cap, force, mode, k,
+                     dh);
+  return cml_status();
+}
+
+// dseg: 2k+1 ints, cursor: 2k ints, dperm: 2*cap ints, dsum: 2k*D doubles; slots/slot_c sized for
+// seg_grid (cml_kmeans_seg_slot_*); acc/msg: k*D + k + 1 doubles.
+CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, const int* labels, const int* chg_rows,
+                                   const int* chg_old, int cap, const int* mode, int k, int* dh, int* dseg,
+                                   int* cursor, int* dperm, int cpl, int seg_grid, double* dsum, double* slots,
+                                   int* slot_c, double* acc, const double* cost_part, int ncost, double* msg, int xfp8,
+                                   void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  const size_t lh = sizeof(int) * 2 * (size_t)k;
+  hipLaunchKernelGGL(kmeans_delta_hist, dim3(kDeltaBlocks), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
+                     mode, k, dh);
+  hipLaunchKernelGGL(kmeans_delta_scan, dim3(1), dim3(256), 0, st, dh, mode, k, dseg, cursor);
+  hipLaunchKernelGGL(kmeans_delta_scatter, dim3(kDeltaBlocks), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
+                     mode, k, cursor, dperm);
+  hipLaunchKernelGGL(zero_f64_gated, dim3(256), dim3(256), 0, st, dsum, 2LL * k * D, mode, 0);
+  int e = cml_status();
   if (e) return e;
-  hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, chunk, waves, slots, slot_c, msg);
+  if (cap > 0) {
+    e = launch_segsum(X, 2LL * cap, ldx, Dp, D, dperm, dseg, 2 * k, cpl, seg_grid, dsum, slots, slot_c, xfp8, mode, 0,
+                      st);
+    if (e) return e;
+  }
+  const long long total = (long long)k * D + k + 1;
+  hipLaunchKernelGGL(kmeans_delta_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, acc, dsum, dseg,
+                     mode, k, D, cost_part, ncost, msg);
   return cml_status();
 }
 

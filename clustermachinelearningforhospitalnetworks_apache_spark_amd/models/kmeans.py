@@ -15,6 +15,11 @@ Per iteration on each rank (E5 in SURVEY.md §3):
         process group's stream while chunk c+1's distance GEMM runs
     K11 update from Σ_c msg[c]  (the only exposed collective is the last chunk's)
 
+Incremental sums (default on the sort regime): the per-cluster sums of the current labels are kept
+across steps; a step re-reads only the rows whose label changed (new sums = old + moved in − moved
+out, exact in f64 for bf16/fp8 rows), falling back to the full accumulate on the first step and
+whenever more than 1/16 of the rows changed. Every step still assigns every row against every centre.
+
 CPU tensors run the same algorithm with torch float64 ops (``local[n]`` mode and
 the numerical oracle).
 """
@@ -65,9 +70,11 @@ class LloydEngine:
 
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
-                 accum_mode: Optional[str] = None, use_graph: Optional[bool] = None):
+                 accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
+                 incremental: Optional[bool] = None):
         self.comm = comm or local_comm()
         self._accum_mode = accum_mode
+        self._incremental = True if incremental is None else bool(incremental)
         # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
         # removes the per-launch host cost that dominates small shards. Default: single rank (a
         # multi-rank step contains RCCL collectives, which stay eagerly launched).
@@ -92,6 +99,7 @@ class LloydEngine:
         self.iterations = 0
         self.last_cost = None
         self._shift2 = None
+        self.delta = None  # incremental-sums state (GPU sort regime), see _alloc_gpu
         if self.gpu:
             self._alloc_gpu()
 
@@ -126,6 +134,9 @@ class LloydEngine:
             self.perm = torch.zeros(max(maxn, 1), dtype=torch.int32, device=dev)
             self.slots = K.seg_slots(self.cplan, d, dev)
         self.msg_len = k * d + k + 1
+        # incremental sums: sort regime with the centres in one LDS chunk (labels are final after one launch)
+        self.delta = (K.DeltaState(max(maxn, 1), k, d, dp, self.row_chunks, self.msg_len, dev, fp8=fp8)
+                      if self._incremental and self.cplan.mode == "sort" and self.aplan.kc == self.aplan.kp else None)
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
@@ -198,6 +209,17 @@ class LloydEngine:
                     K.accumulate_priv(xc, nrow, lab, self.k, self.cplan, self.slab, self.cslab)
                     K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, self.k, self.d,
                                    self.cplan, msg)
+                elif self.delta is not None:
+                    # label changes logged by the assign; the gate picks the full or the delta accumulate
+                    # on the device (no host sync, graph-capturable), both update delta.acc[c] -> msg
+                    rank, dl = self.rank[r0:r1], self.delta
+                    K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
+                                  self.cost_part, self.hist, rank, xnorm=self.xnorm[r0:r1], delta=dl)
+                    dl.gate(c)
+                    K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
+                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, dl.acc[c],
+                                      self.slots, gate=dl.mode[c])
+                    dl.accumulate(xc, self.dp, lab, c, self.cost_part, self.aplan.grid, msg)
                 else:
                     rank = self.rank[r0:r1]
                     K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),

@@ -23,7 +23,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_seg_threads": (c_int, []),
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
     "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
+                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                       c_vp]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
@@ -31,7 +32,12 @@ _native.register_kernel_sigs({
                                       c_vp]),
     "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
-                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
+                                      c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
+                                      c_vp]),
+    "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp,
+                                       c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
+                                       c_vp]),
     "cml_kmeans_seg_slot_doubles": (c_ll, [c_int, c_int]),
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
@@ -134,14 +140,15 @@ def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None
 def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor, plan: AssignPlan,
                 labels: torch.Tensor, best: torch.Tensor | None, cost_part: torch.Tensor | None,
                 hist: torch.Tensor | None = None, rank: torch.Tensor | None = None, stream=None,
-                xnorm: torch.Tensor | None = None) -> None:
+                xnorm: torch.Tensor | None = None, delta: "DeltaState | None" = None) -> None:
     """K9: labels/best[i] = argmin/min_j ||x_i - c_j||² over all kp (padded) centres.
 
     With ``hist``/``rank`` also emits the per-workgroup label histogram and per-row rank
     (first pass of the counting sort used by the sort accumulation regime). ``xnorm`` are the
     cached ||x_i||² (row_sqnorm; Spark's KMeans caches point norms the same way,
     mllib/clustering/KMeans.scala ``VectorWithNorm``); ``best`` may be None when the centres fit
-    one LDS chunk and the distances themselves are not wanted.
+    one LDS chunk and the distances themselves are not wanted. With ``delta`` (single-launch plans
+    only) rows whose label changes are logged for the incremental sums.
     """
     lib = _native.kernels()
     st = _native.stream_ptr(stream)
@@ -150,6 +157,8 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
         xnorm = row_sqnorm(x, n, dp, stream=stream)
     if best is None and nch > 1:
         raise ValueError("multi-chunk assignment needs the `best` scratch buffer")
+    if delta is not None and nch > 1:
+        raise ValueError("label-change logging needs a single-launch assign")
     for ci in range(nch):
         c0 = ci * plan.kc
         kc = min(plan.kc, plan.kp - c0)
@@ -163,7 +172,9 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
             cost_part.data_ptr() if (cost_part is not None and last) else 0,
             hist.data_ptr() if (hist is not None and last) else 0,
             rank.data_ptr() if (rank is not None and last) else 0,
-            plan.grid, int(is_fp8(x)), st)
+            plan.grid, int(is_fp8(x)),
+            delta.rows.data_ptr() if delta is not None else 0, delta.old.data_ptr() if delta is not None else 0,
+            delta.count.data_ptr() if delta is not None else 0, delta.cap if delta is not None else 0, st)
         _native.check(status, "kmeans_assign_bf16")
 
 
@@ -208,16 +219,71 @@ def seg_slots(plan: AccumPlan, d: int, device) -> tuple:
 def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tensor, rank: torch.Tensor,
                     hist: torch.Tensor, aplan: AssignPlan, k: int, cost_part: torch.Tensor, off: torch.Tensor,
                     seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor,
-                    slots: tuple, stream=None) -> None:
-    """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic)."""
+                    slots: tuple, stream=None, gate: torch.Tensor | None = None) -> None:
+    """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic).
+    With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full."""
     lib = _native.kernels()
     status = lib.cml_kmeans_sort_accum(x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(),
                                        hist.data_ptr(), aplan.grid, aplan.nwaves, k, aplan.kp,
                                        cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
                                        perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
                                        slots[0].data_ptr(), slots[1].data_ptr(), int(is_fp8(x)),
-                                       _native.stream_ptr(stream))
+                                       gate.data_ptr() if gate is not None else 0, _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
+
+
+class DeltaState:
+    """Device state of the incremental-sums Lloyd step (kmeans.hip ``kmeans_delta_gate``).
+
+    ``acc`` rows hold, per row chunk, [k·D sums | k counts | cost] of the chunk's CURRENT labels;
+    a step whose label changes exceed ``cap`` rows (or that is forced: the first one) re-accumulates
+    ``acc`` in full, every other step applies only the changed rows. ``force`` is set on creation and
+    by ``invalidate()``."""
+
+    def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, fp8: bool = False,
+                 cap_fraction: float = 1.0 / 16):
+        self.k, self.d = k, d
+        self.cap = max(1024, int(n * cap_fraction))
+        self.rows = torch.zeros(self.cap, dtype=torch.int32, device=device)
+        self.old = torch.zeros(self.cap, dtype=torch.int32, device=device)
+        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        self.mode = torch.zeros((chunks, 2), dtype=torch.int32, device=device)
+        self.force = torch.ones(chunks, dtype=torch.int32, device=device)
+        self.dh = torch.zeros(2 * k, dtype=torch.int32, device=device)
+        self.dseg = torch.zeros(2 * k + 2, dtype=torch.int32, device=device)
+        self.cursor = torch.zeros(2 * k, dtype=torch.int32, device=device)
+        self.dperm = torch.zeros(2 * self.cap, dtype=torch.int32, device=device)
+        self.dsum = torch.zeros(2 * k * d, dtype=torch.float64, device=device)
+        self.acc = torch.zeros((chunks, msg_len), dtype=torch.float64, device=device)
+        ncu = num_cus(device.index or 0)
+        self.plan = AccumPlan(mode="sort", cpl=(dp // 64 if fp8 else (2 if dp <= 128 else (4 if dp <= 256 else 8))),
+                              seg_grid=max(1, min((2 * self.cap + 255) // 256, ncu * 4)), dw=dp)
+        self.slots = seg_slots(self.plan, d, device)
+
+    def invalidate(self) -> None:
+        """Next step re-accumulates in full (labels or acc no longer describe each other)."""
+        self.force.fill_(1)
+
+    def gate(self, chunk: int, stream=None) -> None:
+        _native.check(_native.kernels().cml_kmeans_delta_gate(
+            self.count.data_ptr(), self.cap, self.force[chunk:].data_ptr(), self.mode[chunk].data_ptr(), self.k,
+            self.dh.data_ptr(), _native.stream_ptr(stream)), "kmeans_delta_gate")
+
+    def accumulate(self, x: torch.Tensor, dp: int, labels: torch.Tensor, chunk: int, cost_part: torch.Tensor,
+                   ncost: int, msg: torch.Tensor, stream=None) -> None:
+        _native.check(_native.kernels().cml_kmeans_delta_accum(
+            x.data_ptr(), x.stride(0), dp, self.d, labels.data_ptr(), self.rows.data_ptr(), self.old.data_ptr(),
+            self.cap, self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(), self.dseg.data_ptr(),
+            self.cursor.data_ptr(), self.dperm.data_ptr(), self.plan.cpl, self.plan.seg_grid, self.dsum.data_ptr(),
+            self.slots[0].data_ptr(), self.slots[1].data_ptr(), self.acc[chunk].data_ptr(), cost_part.data_ptr(),
+            ncost, msg.data_ptr(), int(is_fp8(x)), _native.stream_ptr(stream)), "kmeans_delta_accum")
+
+    def changed_rows(self, chunk: int = 0) -> int:
+        """Label changes of the last step (0 on a full step). Synchronises."""
+        return int(self.mode[chunk, 1].item())
+
+    def was_full(self, chunk: int = 0) -> bool:
+        return bool(self.mode[chunk, 0].item())
 
 
 def seg_buffer_ints(k: int) -> int:

@@ -1,0 +1,108 @@
+"""Incremental-sums Lloyd step (kmeans.hip kmeans_delta_*) against the full re-accumulation.
+
+The engine keeps the per-cluster sums of the current labels and, on steps where few labels change,
+applies only the changed rows. On data whose f64 sums are exact (values on a 1/8 grid) the two
+must agree bit for bit; on general data to f64 rounding.
+"""
+import numpy as np
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+
+pytestmark = pytest.mark.gpu
+
+
+def _blobs(n, d, k, seed, grid=True, dtype=torch.bfloat16):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(seed)
+    cen = torch.randn(k, d, device="cuda", generator=g) * 3
+    x = cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn(n, d, device="cuda", generator=g)
+    if grid:
+        x = torch.round(x * 8) / 8  # exact in bf16, f64 sums exact
+    return x.to(dtype)
+
+
+def _run(x, d, k, init, steps, **kw):
+    eng = LloydEngine(x, d, k, **kw)
+    eng.set_centers(init)
+    hist = []
+    for _ in range(steps):
+        eng.step()
+        torch.cuda.synchronize()
+        full = eng.delta.was_full() if eng.delta is not None else True
+        ch = eng.delta.changed_rows() if eng.delta is not None else -1
+        hist.append((eng.centers.clone(), eng.msgs.clone(), full, ch))
+    return eng, hist
+
+
+@pytest.mark.parametrize("n,d,k", [(200_000, 256, 256), (150_001, 128, 64), (60_000, 512, 40)])
+def test_incremental_equals_full_bitwise(n, d, k):
+    x = _blobs(n, d, k, seed=1)
+    init = x[torch.randperm(n, generator=torch.Generator().manual_seed(0))[:k]].double().cpu().numpy()
+    eng, inc = _run(x, d, k, init, 8, accum_mode="sort", use_graph=False)
+    assert eng.delta is not None
+    _, ful = _run(x, d, k, init, 8, accum_mode="sort", use_graph=False, incremental=False)
+    assert inc[0][2], "first step must re-accumulate in full"
+    assert any(not h[2] and h[3] > 0 for h in inc), "no step took the incremental path"
+    for (ci, mi, _, _), (cf, mf, _, _) in zip(inc, ful):
+        assert torch.equal(mi, mf)
+        assert torch.equal(ci, cf)
+
+
+def test_incremental_general_data_and_graph():
+    """Unrounded Gaussian data (f64 rounding only) and the captured-graph step."""
+    n, d, k = 120_000, 256, 128
+    x = _blobs(n, d, k, seed=2, grid=False)
+    init = x[:k].double().cpu().numpy()
+    _, ful = _run(x, d, k, init, 6, accum_mode="sort", use_graph=False, incremental=False)
+    for use_graph in (False, True):
+        eng, inc = _run(x, d, k, init, 6, accum_mode="sort", use_graph=use_graph)
+        assert any(not h[2] for h in inc)
+        for (ci, mi, _, _), (cf, mf, _, _) in zip(inc, ful):
+            np.testing.assert_allclose(mi.cpu().numpy(), mf.cpu().numpy(), rtol=1e-12, atol=1e-9)
+            np.testing.assert_allclose(ci.cpu().numpy(), cf.cpu().numpy(), rtol=1e-12, atol=1e-12)
+
+
+def test_incremental_falls_back_when_many_labels_change():
+    """More changed rows than the change log holds: the step re-accumulates in full."""
+    n, d, k = 100_000, 128, 64
+    x = _blobs(n, d, k, seed=3)
+    init = (x[:k].double() + 5.0).cpu().numpy()  # far-off start: many labels move for a few steps
+    eng = LloydEngine(x, d, k, accum_mode="sort", use_graph=False)
+    eng.delta.cap = 1500
+    eng.set_centers(init)
+    _, ful = _run(x, d, k, init, 6, accum_mode="sort", use_graph=False, incremental=False)
+    modes = []
+    for s in range(6):
+        eng.step()
+        torch.cuda.synchronize()
+        modes.append(eng.delta.was_full())
+        assert torch.equal(eng.msgs, ful[s][1])
+    assert modes[0] and sum(modes) >= 2  # forced first step + at least one overflow fallback
+
+
+def test_incremental_fp8_and_row_chunks():
+    n, d, k = 90_000, 256, 96
+    xb = _blobs(n, d, k, seed=4, grid=False, dtype=torch.float32)
+    for x, chunks in ((xb.to(torch.float8_e4m3fn), 1), (xb.to(torch.bfloat16), 3)):
+        init = x[:k].to(torch.float32).double().cpu().numpy()
+        eng, inc = _run(x, d, k, init, 5, accum_mode="sort", use_graph=False, row_chunks=chunks)
+        _, ful = _run(x, d, k, init, 5, accum_mode="sort", use_graph=False, row_chunks=chunks, incremental=False)
+        assert eng.delta is not None and eng.row_chunks == chunks
+        for (ci, mi, _, _), (cf, mf, _, _) in zip(inc, ful):
+            np.testing.assert_allclose(mi.cpu().numpy(), mf.cpu().numpy(), rtol=1e-12, atol=1e-9)
+
+
+def test_invalidate_forces_full_step():
+    n, d, k = 50_000, 64, 16
+    x = _blobs(n, d, k, seed=5)
+    eng = LloydEngine(x, d, k, accum_mode="sort", use_graph=False)
+    eng.set_centers(x[:k].double().cpu().numpy())
+    for _ in range(3):
+        eng.step()
+    torch.cuda.synchronize()
+    eng.delta.invalidate()
+    eng.step()
+    torch.cuda.synchronize()
+    assert eng.delta.was_full()
