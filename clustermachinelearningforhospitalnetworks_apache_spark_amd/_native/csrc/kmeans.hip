@@ -294,7 +294,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     const void* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
     int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
     int* __restrict__ labels, float* __restrict__ best_io, int first, int last, double* __restrict__ cost_part,
-    int* __restrict__ hist_out, int* __restrict__ rank_out, DeltaOut dout) {
+    int* __restrict__ hist_out, int* __restrict__ rank_out, DeltaOut dout, int sched) {
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   constexpr int NCH = AssignShape<DP>::NCH;
   constexpr int KS = AssignShape<DP>::KS;
@@ -345,6 +345,14 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   cx.cmask = (1 << bits) - 1;
 
   long long tile = (long long)blockIdx.x * nwaves + wave;
+  // SIMD partners (waves w and w + 4) run the same program: desynchronise them so one streams its
+  // next X tile while the other computes (sched bit 0: static priority for the second half, bit 1:
+  // the second half starts ~sched>>2 x 512 cycles late).
+  if (wave >= nwaves / 2) {
+    if (sched & 1) __builtin_amdgcn_s_setprio(1);
+    if (sched & 2)
+      for (int i = 0; i < (sched >> 2); ++i) __builtin_amdgcn_s_sleep(8);
+  }
   if constexpr (PF) {
     XTile<DP, RT> xa, xb;
     if (tile < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xa);
@@ -1053,6 +1061,7 @@ long long assign_lds_bytes(int kc, int kp, int Dp) {
 // RT 1 with the next tile's X in flight and more waves per CU.
 // Variant (tuning/experiments): 0 auto, 1 = RT 2 + X double buffer, 2 = RT 1, 3 = RT 4.
 int g_assign_variant = 0;
+int g_assign_sched = 0;  // kmeans_assign_bf16 `sched` (partner-wave desynchronisation), tuning knob
 inline int assign_threads(int /*DS*/) {
   return g_assign_variant == 4 ? 768 : (g_assign_variant == 5 ? 1024 : 512);
 }
@@ -1105,7 +1114,8 @@ int launch_assign(const void* X, long long n, long long ldx, const u16* C, long 
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   void* args[] = {(void*)&X, (void*)&n, (void*)&ldx, (void*)&C, (void*)&ldc, (void*)&kc, (void*)&kp,
                   (void*)&c_base, (void*)&cnorm, (void*)&xnorm, (void*)&labels, (void*)&best, (void*)&first,
-                  (void*)&last, (void*)&cost_part, (void*)&hist, (void*)&rank, (void*)&dout};
+                  (void*)&last, (void*)&cost_part, (void*)&hist, (void*)&rank, (void*)&dout,
+                  (void*)&g_assign_sched};
   const hipError_t e = hipLaunchKernel(fn, dim3(grid), dim3(assign_threads(0)), args, lds, st);
   if (e != hipSuccess) return (int)e;
   return cml_status();
@@ -1177,6 +1187,11 @@ CML_API int cml_kmeans_assign_occupancy(int Dp, int kc, int kp, int xfp8) {
     case 32: return assign_occupancy<512, false>(kc, kp);
     default: return 0;
   }
+}
+CML_API int cml_kmeans_set_assign_sched(int v) {
+  if (v < 0) return (int)hipErrorInvalidValue;
+  g_assign_sched = v;
+  return 0;
 }
 CML_API int cml_kmeans_set_assign_variant(int v) {
   if (v < 0 || v > 5) return (int)hipErrorInvalidValue;

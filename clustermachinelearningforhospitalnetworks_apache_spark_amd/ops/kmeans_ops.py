@@ -19,6 +19,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_lds_bytes": (c_ll, [c_int, c_int, c_int]),
     "cml_kmeans_assign_threads": (c_int, [c_int]),
     "cml_kmeans_set_assign_variant": (c_int, [c_int]),
+    "cml_kmeans_set_assign_sched": (c_int, [c_int]),
     "cml_kmeans_assign_occupancy": (c_int, [c_int, c_int, c_int, c_int]),
     "cml_kmeans_seg_threads": (c_int, []),
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
@@ -105,6 +106,11 @@ def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = Fals
 def set_assign_variant(v: int) -> None:
     """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD)."""
     _native.check(_native.kernels().cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
+
+
+def set_assign_sched(v: int) -> None:
+    """Tuning knob: partner-wave desynchronisation of K9 (bit 0 priority, bit 1 + v>>2 stagger)."""
+    _native.check(_native.kernels().cml_kmeans_set_assign_sched(int(v)), "set_assign_sched")
 
 
 def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None = None,
