@@ -9,7 +9,8 @@
 // K17 tree_binize  value -> bin: #thresholds < value (binary search, thresholds in LDS)
 // K18 tree_hist    hist[t][node][f][bin][s] += w_t(row)·stat_s(row) for rows whose node
 //                  at this level is `node`; LDS-privatised per workgroup (one tree ×
-//                  feature chunk per workgroup), flushed once with f64 global adds.
+//                  feature chunk per workgroup), 64-bit fixed point (order-independent,
+//                  exact), flushed once with integer global adds.
 // K20 tree_route   node_of[t][row] <- left/right child after the level's splits
 // K21 tree_predict per-row traversal of every tree (arrays in LDS), forest mean
 //                  (regression) or summed normalised class distributions (classification)
@@ -39,51 +40,57 @@ __global__ void tree_binize_kernel(const double* __restrict__ X, long long n, lo
   }
 }
 
-// grid: (row blocks, trees, feature chunks). LDS: nodes * fc * nbins * S floats.
+// grid: (row blocks, trees, feature chunks). LDS: nodes * fc * nbins * S int64.
+// Statistics accumulate as 64-bit FIXED POINT (value * 2^e_s, e_s chosen on the host from the
+// global n, max weight and max |y| so no sum can overflow): integer adds are associative, so the
+// histogram — and every split chosen from it — is bit-identical whatever the row order, the number
+// of workgroups or the number of GPUs, with f64-class precision (Spark aggregates these in f64;
+// f32 partials lost ~1e-7 of Σy² and made splits world-size dependent).
 __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __restrict__ bins, long long n, int d,
                                                         int nbins, const int* __restrict__ node_of,
                                                         const float* __restrict__ wt, const double* __restrict__ y,
                                                         const int* __restrict__ cls, int S, int nodes, int fc,
-                                                        double* __restrict__ out) {
-  extern __shared__ float h[];
+                                                        double sc0, double sc1, double sc2,
+                                                        unsigned long long* __restrict__ out) {
+  extern __shared__ unsigned long long h[];
   const int t = blockIdx.y;
   const int f0 = blockIdx.z * fc;
   const int fcount = min(fc, d - f0);
   const int hsize = nodes * fc * nbins * S;
-  for (int i = threadIdx.x; i < hsize; i += blockDim.x) h[i] = 0.f;
+  for (int i = threadIdx.x; i < hsize; i += blockDim.x) h[i] = 0ull;
   __syncthreads();
   const int* nd = node_of + (long long)t * n;
   const float* w = wt != nullptr ? wt + (long long)t * n : nullptr;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
     const int node = nd[r];
     if (node < 0) continue;
-    const float wr = w != nullptr ? w[r] : 1.f;
-    if (wr == 0.f) continue;
-    float s0 = wr, s1 = 0.f, s2 = 0.f;
+    const double wr = w != nullptr ? (double)w[r] : 1.0;
+    if (wr == 0.0) continue;
+    unsigned long long q0 = (unsigned long long)llrint(wr * sc0), q1 = 0ull, q2 = 0ull;
     int c = -1;
     if (cls == nullptr) {
-      const float yv = (float)y[r];
-      s1 = wr * yv;
-      s2 = wr * yv * yv;
+      const double yv = y[r];
+      q1 = (unsigned long long)llrint(wr * yv * sc1);
+      q2 = (unsigned long long)llrint(wr * yv * yv * sc2);
     } else {
       c = cls[r];
     }
     const unsigned char* br = bins + r * d + f0;
     for (int f = 0; f < fcount; ++f) {
-      float* cell = h + ((node * fc + f) * nbins + br[f]) * S;
+      unsigned long long* cell = h + ((node * fc + f) * nbins + br[f]) * S;
       if (cls == nullptr) {
-        atomicAdd(cell + 0, s0);
-        atomicAdd(cell + 1, s1);
-        atomicAdd(cell + 2, s2);
+        atomicAdd(cell + 0, q0);
+        atomicAdd(cell + 1, q1);
+        atomicAdd(cell + 2, q2);
       } else {
-        atomicAdd(cell + c, wr);
+        atomicAdd(cell + c, q0);
       }
     }
   }
   __syncthreads();
   for (int i = threadIdx.x; i < hsize; i += blockDim.x) {
-    const float v = h[i];
-    if (v == 0.f) continue;
+    const unsigned long long v = h[i];
+    if (v == 0ull) continue;
     const int s = i % S;
     const int rest = i / S;
     const int b = rest % nbins;
@@ -91,7 +98,7 @@ __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __r
     const int f = rest2 % fc;
     const int node = rest2 / fc;
     if (f >= fcount) continue;
-    atomicAdd(out + ((((long long)t * nodes + node) * d + f0 + f) * nbins + b) * S + s, (double)v);
+    atomicAdd(out + ((((long long)t * nodes + node) * d + f0 + f) * nbins + b) * S + s, v);
   }
 }
 
@@ -155,9 +162,9 @@ CML_API int cml_tree_binize(const double* X, long long n, long long ld, int d, c
 
 // Returns the feature chunk used (features per workgroup) so the host can size nothing; out must be zeroed.
 CML_API int cml_tree_hist(const unsigned char* bins, long long n, int d, int nbins, const int* node_of, int T,
-                          const float* wt, const double* y, const int* cls, int S, int nodes, double* out,
-                          int row_blocks, void* stream) {
-  const long long per_feat = (long long)nodes * nbins * S * 4;
+                          const float* wt, const double* y, const int* cls, int S, int nodes, const double* scales,
+                          unsigned long long* out, int row_blocks, void* stream) {
+  const long long per_feat = (long long)nodes * nbins * S * 8;
   int fc = (int)((96 * 1024) / (per_feat > 0 ? per_feat : 1));
   if (fc < 1) return (int)hipErrorInvalidValue;
   if (fc > d) fc = d;
@@ -165,7 +172,7 @@ CML_API int cml_tree_hist(const unsigned char* bins, long long n, int d, int nbi
   const size_t lds = (size_t)per_feat * fc;
   hipFuncSetAttribute((const void*)tree_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(tree_hist_kernel, dim3(row_blocks, T, fchunks), dim3(256), lds, (hipStream_t)stream, bins, n, d,
-                     nbins, node_of, wt, y, cls, S, nodes, fc, out);
+                     nbins, node_of, wt, y, cls, S, nodes, fc, scales[0], scales[1], scales[2], out);
   return cml_status();
 }
 

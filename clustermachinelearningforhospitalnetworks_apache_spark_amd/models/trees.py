@@ -34,8 +34,8 @@ from ..utils import rng
 
 _native.register_kernel_sigs({
     "cml_tree_binize": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
-    "cml_tree_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_int,
-                              c_vp]),
+    "cml_tree_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
+                              c_int, c_vp]),
     "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
 })
@@ -204,19 +204,40 @@ class ForestEngine:
         return bins
 
     # -------------------------------------------------------------- histogram / routing
+    def fixed_point_scales(self, wt) -> np.ndarray:
+        """Per-statistic scales 2^e of the GPU histogram's 64-bit fixed point: the largest e for
+        which n_global · max w · max|y|^p still fits 2^61 (global maxima, so every rank and every
+        world size uses the same scales and the integer histograms add up exactly)."""
+        ymax = float(self.y.abs().max().item()) if (self.n and self.kind == "variance") else 1.0
+        wmax = float(wt.max().item()) if (wt is not None and self.n) else 1.0
+        ymax = self.comm.max_scalar(max(ymax, 1e-300))
+        wmax = self.comm.max_scalar(max(wmax, 1e-300))
+        gn = max(self.comm.sum_scalar(float(self.n)), 1.0)
+        out = np.ones(3)
+        for s in range(3):
+            bound = gn * wmax * (ymax ** s if self.kind == "variance" else 1.0)
+            out[s] = 2.0 ** max(-1000, min(1000, 61 - math.ceil(math.log2(max(bound, 1e-300)))))
+        return out
+
     def histogram(self, bins, node_of, wt, nodes: int) -> torch.Tensor:
+        """(T, nodes, d, nbins, S) statistics of this rank's rows. GPU: int64 fixed point (scale
+        ``self.scales``), converted by ``to_stats`` after the all-reduce; CPU: float64."""
         T, S, d, nb = self.p.num_trees, self.S, self.d, self.nbins
-        out = torch.zeros((T, nodes, d, nb, S), dtype=torch.float64, device=self.dev)
-        if self.n == 0 or nodes == 0:
-            return out
         if self.gpu:
+            out = torch.zeros((T, nodes, d, nb, S), dtype=torch.int64, device=self.dev)
+            if self.n == 0 or nodes == 0:
+                return out
             cls = self.y.to(torch.int32).contiguous() if self.kind != "variance" else None
             rb = max(1, min((self.n + 255) // 256, 1024 // max(T, 1) + 1))
             st = _native.kernels().cml_tree_hist(bins.data_ptr(), self.n, d, nb, node_of.data_ptr(), T,
                                                  wt.data_ptr() if wt is not None else 0, self.y.data_ptr(),
-                                                 cls.data_ptr() if cls is not None else 0, S, nodes, out.data_ptr(),
-                                                 rb, _native.stream_ptr())
+                                                 cls.data_ptr() if cls is not None else 0, S, nodes,
+                                                 self._scales_host.data_ptr(), out.data_ptr(), rb,
+                                                 _native.stream_ptr())
             _native.check(st, "tree_hist")
+            return out
+        out = torch.zeros((T, nodes, d, nb, S), dtype=torch.float64, device=self.dev)
+        if self.n == 0 or nodes == 0:
             return out
         flat = out.view(-1)
         for t in range(T):
@@ -291,6 +312,9 @@ class ForestEngine:
         if wt is not None:
             wt = wt.to(self.dev).contiguous()
         node_of = torch.zeros((T, self.n), dtype=torch.int32, device=self.dev)
+        if self.gpu:
+            self.scales = self.fixed_point_scales(wt)
+            self._scales_host = torch.as_tensor(self.scales, dtype=torch.float64).contiguous()
         k_sub = subset_size(p.feature_subset, self.d, p.task, T)
         roots = [Node() for _ in range(T)]
         level_nodes: List[List[Node]] = [[r] for r in roots]
@@ -302,6 +326,9 @@ class ForestEngine:
             hist = self.histogram(bins, node_of, wt, nodes)
             self.comm.allreduce_(hist)
             h = hist.cpu().numpy()
+            if self.gpu:  # exact integer sums -> float64 statistics
+                sc = self.scales[:3] if self.kind == "variance" else np.full(self.S, self.scales[0])
+                h = h.astype(np.float64) / sc
             split_feat = np.full((T, nodes), -1, dtype=np.int32)
             split_bin = np.zeros((T, nodes), dtype=np.int32)
             left_id = np.full((T, nodes), -1, dtype=np.int32)

@@ -123,6 +123,11 @@ def plan_accum(n: int, dp: int, k: int, device_index: int = 0, force: str | None
         return AccumPlan(mode="sort", cpl=dp // 64, seg_grid=max(1, min((n + 255) // 256, ncu * 4)), dw=dp)
     dw = min(dp, 256)
     cpl = 4 if dw > 128 else 2
+    # Default: the sort regime whenever it applies. Its f64 segmented sums of bf16 rows are exact, so
+    # results do not depend on how rows are split over workgroups or GPUs, and it carries the
+    # incremental-sums step. The private-copy regime (f32 LDS partials) stays for Dp > 512 and on request.
+    if force is None and dp <= 512:
+        force = "sort"
     if force != "sort":
         r = max(1, min(16, (cpl * 64) // dw))
         while r >= 1:

@@ -70,13 +70,15 @@ class Communicator:
             device = torch.device("cpu")
         if world == 1:
             return cls(0, 1, device, None)
-        backend = "nccl" if use_gpu else "gloo"
+        # CML_COMM_BACKEND=gloo keeps GPU-resident shards but runs the collectives over gloo: several
+        # ranks can then share one device (tests on a 1-GPU box; RCCL needs a device per rank)
+        backend = os.environ.get("CML_COMM_BACKEND") or ("nccl" if use_gpu else "gloo")
         owns = False
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
             kwargs = dict(backend=backend, rank=rank, world_size=world,
                           timeout=datetime.timedelta(seconds=timeout_s))
-            if use_gpu:
+            if use_gpu and backend == "nccl":
                 kwargs["device_id"] = device
             dist.init_process_group(**kwargs)
             owns = True

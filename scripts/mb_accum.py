@@ -21,9 +21,13 @@ for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16
     x = (cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn(n, d, device="cuda", generator=g)).to(torch.bfloat16)
     del cen
     gb = n * d * 2 / 1e9
-    for mode in (None, "sort"):
+    for mode in (None, "priv"):
         K.set_assign_variant(0)
-        eng = LloydEngine(x, d, k, accum_mode=mode)
+        try:
+            eng = LloydEngine(x, d, k, accum_mode=mode)
+        except ValueError as e:
+            print(f"n={n} d={d} k={k} mode={mode}: {e}")
+            continue
         eng.set_centers(x[:k].double().cpu().numpy())
         if mode is None:
             for v in (0,):
@@ -36,7 +40,7 @@ for (n, d, k) in [(20_000_000, 256, 256), (10_000_000, 128, 64), (20_000_000, 16
             K.set_assign_variant(0)
         for g in (False, True):
             eng.use_graph = g
-            t_st = timeit(lambda: eng.step())
+            t_st = timeit(lambda: eng.step(), reps=5)
             print(f"n={n} d={d} k={k} {eng.cplan} graph={g}: step {t_st:.3f} ms -> {n/t_st/1e6:.2f} Gsamples/s",
                   flush=True)
         del eng

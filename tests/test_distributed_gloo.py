@@ -19,7 +19,7 @@ def _free_port():
     return p
 
 
-def _workload(out_path, rank):
+def _workload(out_path, rank, master="local[1]"):
     import torch
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegression
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
@@ -30,7 +30,7 @@ def _workload(out_path, rank):
                                                                                             RandomForestRegressor)
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
-    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    spark = SparkSession.builder.master(master).getOrCreate()
     rs = np.random.RandomState(0)
     n = 3001
     X = rs.randn(n, 4) * [1, 2, 3, 4] + [0, 1, 2, 3]
@@ -68,31 +68,32 @@ def _workload(out_path, rank):
     spark.stop()
 
 
-def _rank_main(rank, world, port, out_path):
+def _rank_main(rank, world, port, out_path, gpu=False):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
-                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "CML_FORCE_CPU": "1"})
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    if gpu:  # every rank on the one visible GPU, collectives over gloo (RCCL needs a GPU per rank)
+        os.environ["CML_COMM_BACKEND"] = "gloo"
+    else:
+        os.environ["CML_FORCE_CPU"] = "1"
     import torch
     torch.set_num_threads(1)
-    _workload(out_path, rank)
+    _workload(out_path, rank, "mi355x" if gpu else "local[1]")
 
 
-def _run(world, tmp_path):
-    out = str(tmp_path / f"res_w{world}.json")
+def _run(world, tmp_path, gpu=False):
+    out = str(tmp_path / f"res_w{world}{'_gpu' if gpu else ''}.json")
     if world == 1:
         for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK"):
             os.environ.pop(k, None)
-        _workload(out, 0)
+        _workload(out, 0, "mi355x" if gpu else "local[1]")
     else:
-        mp.start_processes(_rank_main, args=(world, _free_port(), out), nprocs=world, join=True,
+        mp.start_processes(_rank_main, args=(world, _free_port(), out, gpu), nprocs=world, join=True,
                            start_method="spawn")
     with open(out) as fh:
         return json.load(fh)
 
 
-@pytest.mark.parametrize("world", [2, 3])
-def test_spmd_results_invariant_to_world_size(tmp_path, world):
-    r1 = _run(1, tmp_path)
-    rw = _run(world, tmp_path)
+def _check_invariant(r1, rw, world):
     assert rw["world"] == world and r1["world"] == 1
     assert rw["count"] == r1["count"] and rw["train"] == r1["train"]
     assert rw["train_ids"] == r1["train_ids"]
@@ -108,3 +109,15 @@ def test_spmd_results_invariant_to_world_size(tmp_path, world):
     assert [g for g, _ in rw["groupby"]] == [g for g, _ in r1["groupby"]]
     np.testing.assert_allclose([s for _, s in rw["groupby"]], [s for _, s in r1["groupby"]], rtol=1e-12)
     assert rw["sql"] == r1["sql"]
+
+
+@pytest.mark.parametrize("world", [2, 3])
+def test_spmd_results_invariant_to_world_size(tmp_path, world):
+    _check_invariant(_run(1, tmp_path), _run(world, tmp_path), world)
+
+
+@pytest.mark.gpu
+def test_spmd_gpu_ranks_invariant_to_world_size(tmp_path):
+    """The same workload with GPU-resident shards and the HIP kernels: 2 ranks sharing the one
+    visible MI355X (gloo collectives) against 1 rank."""
+    _check_invariant(_run(1, tmp_path, gpu=True), _run(2, tmp_path, gpu=True), 2)
