@@ -395,73 +395,63 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   const CT b = (CT)coef[d];
   double gb = 0.0, loss = 0.0, wsum = 0.0;
   const long long step = (long long)gridDim.x * nw * rpw;
-  // Software pipeline: the raw 16-byte chunks (and y, wt) of the wave's NEXT row group are loaded
-  // before the current group is decoded and reduced, so two groups are in flight per wave for only
-  // NCH·4 extra VGPRs (raw words, decoded after the wait) — a second decoded group (U = 2, kept for
-  // ablation) costs NCH·CPT·U VGPRs and a resident block per CU.
+  // Software pipeline: the raw 16-byte chunks (and y, wt) of the wave's next U row groups are in
+  // flight while the current one is decoded and reduced — a ring of U undecoded groups costs only
+  // NCH·4 + 4 VGPRs per slot (U = 1: one group ahead, the measured optimum; see logreg_unroll).
   int since = 0;
   long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
-  uint4 raw[NCH];
-  double yn = 0.0, wn = 0.0;
-  if (row0 < n) {
-    const long long row = row0 + sub;
-    load_raw_group<T, NCH>(X, row, ld, lpr, li, d, row < n, raw);
-    yn = row < n ? y[row] : 0.0;
-    wn = row < n ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+  uint4 raw[U][NCH];
+  double yn[U], wn[U];
+#pragma unroll
+  for (int q = 0; q < U; ++q) {
+    const long long row = row0 + q * step + sub;
+    const bool ok = row < n;
+    load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw[q]);
+    yn[q] = ok ? y[row] : 0.0;
+    wn[q] = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
   }
   for (; row0 < n; row0 += U * step) {
-    CT v[U][NCH][CPT];
-    double yi[U], wi[U];
-    decode_group<T, CT, NCH>(raw, lpr, li, d, v[0]);
-    yi[0] = yn;
-    wi[0] = wn;
 #pragma unroll
-    for (int u = 1; u < U; ++u) {
-      const long long row = row0 + u * step + sub;
-      uint4 r2[NCH];
-      load_raw_group<T, NCH>(X, row, ld, lpr, li, d, row < n, r2);
-      yi[u] = row < n ? y[row] : 0.0;
-      wi[u] = row < n ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
-      decode_group<T, CT, NCH>(r2, lpr, li, d, v[u]);
-    }
-    {
-      const long long row = row0 + U * step + sub;
-      const bool ok = row < n;
-      load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw);
-      yn = ok ? y[row] : 0.0;
-      wn = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
-    }
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
+    for (int q = 0; q < U; ++q) {
+      if (row0 + q * step >= n) break;  // wave-uniform
+      CT v[NCH][CPT];
+      decode_group<T, CT, NCH>(raw[q], lpr, li, d, v);
+      const double yi = yn[q], wi = wn[q];
+      {
+        const long long row = row0 + (q + U) * step + sub;
+        const bool ok = row < n;
+        load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw[q]);
+        yn[q] = ok ? y[row] : 0.0;
+        wn[q] = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+      }
       CT m = 0;
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) m = fma(v[u][c][j], w[c][j], m);
+        for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
       m = group_sum_ct<CT>(m, lpr) + b;
       const CT p = sigmoid_ct(m);
-      const CT r = (CT)wi[u] * (p - (CT)yi[u]);
+      const CT r = (CT)wi * (p - (CT)yi);
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[u][c][j], g[c][j]);
+        for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
       if (li == 0) {
         gb += (double)r;
-        loss += wi[u] * ((double)softplus_ct(m) - yi[u] * (double)m);
-        wsum += wi[u];
+        loss += wi * ((double)softplus_ct(m) - yi * (double)m);
+        wsum += wi;
       }
-    }
-    if constexpr (sizeof(CT) == 4) {
-      since += U;
-      if (since >= FLUSH) {
-        since = 0;
+      if constexpr (sizeof(CT) == 4) {
+        if (++since >= FLUSH) {
+          since = 0;
 #pragma unroll
-        for (int c = 0; c < NCH; ++c)
+          for (int c = 0; c < NCH; ++c)
 #pragma unroll
-          for (int j = 0; j < CPT; ++j) {
-            g64[c][j] += (double)g[c][j];
-            g[c][j] = 0;
-          }
+            for (int j = 0; j < CPT; ++j) {
+              g64[c][j] += (double)g[c][j];
+              g[c][j] = 0;
+            }
+        }
       }
     }
   }
@@ -795,15 +785,18 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
     default: return (int)hipErrorInvalidValue;        \
   }
 
-int g_logreg_unroll = 0;  // 0 = auto, else forced U (ablation: cml_glm_set_logreg_unroll)
+int g_logreg_unroll = 0;  // 0 = auto, else forced prefetch depth U (ablation: cml_glm_set_logreg_unroll)
 
 int logreg_unroll(int nch) {
-  if (g_logreg_unroll == 1 || g_logreg_unroll == 2) return g_logreg_unroll;
-  return 1;  // U = 2 measured slower at every batch size once the grid follows occupancy (mb_logreg.py)
+  if (g_logreg_unroll == 1 || g_logreg_unroll == 2 || g_logreg_unroll == 4) return g_logreg_unroll;
+  // one group ahead: deeper rings measured SLOWER at every size (profiles/logreg_prefetch_depth.log:
+  // 50M x 256 bf16 5.65 / 4.20 / 2.85 TB/s at U = 1 / 2 / 4, fp8 x 512 3.96 / 2.68 / 1.90)
+  return 1;
 }
 
 #define CML_U_SWITCH(u, BODY)                                          \
-  if ((u) == 2) { constexpr int U = 2; BODY; } else { constexpr int U = 1; BODY; }
+  if ((u) == 4) { constexpr int U = 4; BODY; }                         \
+  else if ((u) == 2) { constexpr int U = 2; BODY; } else { constexpr int U = 1; BODY; }
 
 size_t moments_lds_bytes(int lpr, int cpt) { return (size_t)(kGlmThreads / 64) * 2 * lpr * cpt * sizeof(double); }
 size_t logreg_lds_bytes(int lpr, int cpt) { return (size_t)(kGlmThreads / 64) * (lpr * cpt + 3) * sizeof(double); }

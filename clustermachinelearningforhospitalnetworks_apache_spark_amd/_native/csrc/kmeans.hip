@@ -184,13 +184,17 @@ __device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& 
 }
 
 // Incremental sums (Lloyd step on label changes only): the single-launch assign appends every row
-// whose label differs from the one it held before this step to (rows, old), in wave-aggregated
-// batches; `count` may exceed `cap` (the step then falls back to the full accumulate).
+// whose label differs from the one it held before this step to its WORKGROUP's list
+// (rows/old[b * pcap ...], one LDS counter per workgroup, one LDS atomic per wave batch; a single
+// global counter serialised ~8M atomics per pass when many labels moved). wg_count[b] receives the
+// list length; a list longer than pcap sets *overflow (the step then re-accumulates in full).
 struct DeltaOut {
   int* rows;
   int* old;
-  unsigned* count;
-  int cap;
+  int* wg_count;
+  int* overflow;
+  int pcap;
+  int* lds_count;  // set in the kernel
 };
 
 template <int DP, int RT, int RINGMAX>
@@ -263,13 +267,14 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
       if (bal != 0ull) {
         const int lane = r + 16 * g;
         const int leader = __builtin_ctzll(bal);
-        unsigned base = 0u;
-        if (lane == leader) base = atomicAdd(dout.count, (unsigned)__popcll(bal));
+        int base = 0;
+        if (lane == leader) base = atomicAdd(dout.lds_count, (int)__popcll(bal));
         base = __shfl(base, leader, 64);
-        const unsigned at = base + (unsigned)__popcll(bal & ((1ull << lane) - 1ull));
-        if (ch && at < (unsigned)dout.cap) {
-          dout.rows[at] = (int)row;
-          dout.old[at] = prev;
+        const int at = base + (int)__popcll(bal & ((1ull << lane) - 1ull));
+        if (ch && at < dout.pcap) {
+          const long long o = (long long)blockIdx.x * dout.pcap + at;
+          dout.rows[o] = (int)row;
+          dout.old[o] = prev;
         }
       }
     }
@@ -303,6 +308,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   float* cn = reinterpret_cast<float*>(smem + (size_t)nct * KS * 1024);
   int* hist = reinterpret_cast<int*>(cn + kc);
   double* red = reinterpret_cast<double*>(hist + ((kp + 3) & ~3));
+  dout.lds_count = reinterpret_cast<int*>(red + 16);
 
   const int tid = threadIdx.x;
   for (int id = tid; id < nct * KS * 64; id += NT) {
@@ -326,6 +332,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   const bool ranking = last && rank_out != nullptr;
   if (ranking)
     for (int i = tid; i < kp; i += NT) hist[i] = 0;
+  if (tid == 0) *dout.lds_count = 0;
   __syncthreads();
 
   constexpr int nwaves = NT / 64;
@@ -385,6 +392,11 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     }
     if (ranking)
       for (int i = tid; i < kp; i += NT) hist_out[(long long)blockIdx.x * kp + i] = hist[i];
+    if (dout.rows != nullptr && tid == 0) {
+      const int c = *dout.lds_count;
+      dout.wg_count[blockIdx.x] = c < dout.pcap ? c : dout.pcap;
+      if (c > dout.pcap) *dout.overflow = 1;
+    }
   }
 }
 
@@ -918,43 +930,42 @@ __global__ void zero_f64_gated(double* __restrict__ p, long long n, const int* _
 // not depend on the order rows are added in) — tests/test_kmeans_kernels_gpu.py checks it bitwise.
 // ---------------------------------------------------------------------------------------------
 constexpr int kDeltaThreads = 256;
-constexpr int kDeltaBlocks = 512;
 
-__global__ __launch_bounds__(256) void kmeans_delta_gate(unsigned* __restrict__ count, int cap,
-                                                         int* __restrict__ force, int* __restrict__ mode, int k,
-                                                         int* __restrict__ dh) {
-  __shared__ int full;
+__global__ __launch_bounds__(256) void kmeans_delta_gate(const int* __restrict__ wg_count, int nblk, int cap,
+                                                         int* __restrict__ overflow, int* __restrict__ force,
+                                                         int* __restrict__ mode, int k, int* __restrict__ dh) {
+  __shared__ long long part[4];
+  long long m = 0;
+  for (int b = threadIdx.x; b < nblk; b += blockDim.x) m += wg_count[b];
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) m += __shfl_xor(m, o, 64);
+  if ((threadIdx.x & 63) == 0) part[threadIdx.x >> 6] = m;
+  __syncthreads();
   if (threadIdx.x == 0) {
-    const unsigned m = *count;
-    full = (*force != 0 || m > (unsigned)cap) ? 1 : 0;
+    m = part[0] + part[1] + part[2] + part[3];
+    const int full = (*force != 0 || *overflow != 0 || m > (long long)cap) ? 1 : 0;
     mode[0] = full;
     mode[1] = full ? 0 : (int)m;
-    *count = 0u;
+    *overflow = 0;
     *force = 0;
   }
   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) dh[i] = 0;
 }
 
-// Range of the change list one delta block owns (m from the gate, known only on the device).
-__device__ __forceinline__ void delta_range(const int* mode, int& i0, int& i1) {
-  const long long m = mode[1];
-  i0 = (int)(m * blockIdx.x / gridDim.x);
-  i1 = (int)(m * (blockIdx.x + 1) / gridDim.x);
-}
-
+// One delta workgroup per assign workgroup b: its change list is rows/old[b*pcap, + wg_count[b]).
 // Histogram of the 2m delta entries by key, block-aggregated in LDS.
 __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_hist(const int* __restrict__ rows,
                                                                    const int* __restrict__ old,
                                                                    const int* __restrict__ labels,
+                                                                   const int* __restrict__ wg_count, int pcap,
                                                                    const int* __restrict__ mode, int k,
                                                                    int* __restrict__ dh) {
   if (mode[0] != 0) return;
   extern __shared__ int lh[];
   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
   __syncthreads();
-  int i0, i1;
-  delta_range(mode, i0, i1);
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+  const long long i0 = (long long)blockIdx.x * pcap, i1 = i0 + wg_count[blockIdx.x];
+  for (long long i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     atomicAdd(lh + labels[rows[i]], 1);
     atomicAdd(lh + k + old[i], 1);
   }
@@ -995,6 +1006,7 @@ __global__ __launch_bounds__(256) void kmeans_delta_scan(const int* __restrict__
 __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_scatter(const int* __restrict__ rows,
                                                                       const int* __restrict__ old,
                                                                       const int* __restrict__ labels,
+                                                                      const int* __restrict__ wg_count, int pcap,
                                                                       const int* __restrict__ mode, int k,
                                                                       int* __restrict__ cursor,
                                                                       int* __restrict__ perm) {
@@ -1002,16 +1014,15 @@ __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_scatter(const int*
   extern __shared__ int lh[];  // [2k] counts, then bases
   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
   __syncthreads();
-  int i0, i1;
-  delta_range(mode, i0, i1);
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+  const long long i0 = (long long)blockIdx.x * pcap, i1 = i0 + wg_count[blockIdx.x];
+  for (long long i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     atomicAdd(lh + labels[rows[i]], 1);
     atomicAdd(lh + k + old[i], 1);
   }
   __syncthreads();
   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = lh[i] ? atomicAdd(cursor + i, lh[i]) : 0;
   __syncthreads();
-  for (int i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
+  for (long long i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int row = rows[i];
     perm[atomicAdd(lh + labels[row], 1)] = row;
     perm[atomicAdd(lh + k + old[i], 1)] = row;
@@ -1051,7 +1062,7 @@ __global__ void kmeans_delta_apply(double* __restrict__ acc, const double* __res
 
 long long assign_lds_bytes(int kc, int kp, int Dp) {
   const long long ks = Dp >= 32 ? Dp / 32 : 1;
-  return (long long)(kc / 16) * ks * 1024 + (long long)kc * 4 + (long long)((kp + 3) & ~3) * 4 + 16 * 8;
+  return (long long)(kc / 16) * ks * 1024 + (long long)kc * 4 + (long long)((kp + 3) & ~3) * 4 + 16 * 8 + 16;
 }
 
 // Assign launch shape (measured on MI355X, see profiles/): RT 16-row sub-tiles per wave share
@@ -1210,12 +1221,14 @@ CML_API long long cml_kmeans_seg_ints(int k) { return (long long)(k + 1) + ((k +
 CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, int Dp, const void* C, long long ldc,
                                    int kc, int kp, int c_base, const float* cnorm, const float* xnorm, int* labels,
                                    float* best, int first, int last, double* cost_part, int* hist, int* rank,
-                                   int grid, int xfp8, int* chg_rows, int* chg_old, unsigned* chg_count, int chg_cap,
+                                   int grid, int xfp8, int* chg_rows, int* chg_old, int* chg_wg_count,
+                                   int* chg_overflow, int chg_pcap,
                                    void* stream) {
   if (kc % 16 != 0 || Dp % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
-  if (chg_rows != nullptr && (!(first && last) || chg_old == nullptr || chg_count == nullptr || chg_cap < 0))
-    return (int)hipErrorInvalidValue;  // label changes are only defined for a single-launch assign
-  const DeltaOut dout{chg_rows, chg_old, chg_count, chg_cap};
+  if (chg_rows != nullptr && (!(first && last) || chg_old == nullptr || chg_wg_count == nullptr ||
+                              chg_overflow == nullptr || chg_pcap < 0 || hist == nullptr || cost_part == nullptr))
+    return (int)hipErrorInvalidValue;  // label changes: single-launch assign with the ranking epilogue
+  const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if ((hist == nullptr) != (rank == nullptr)) return (int)hipErrorInvalidValue;
   if (best == nullptr && !(first && last)) return (int)hipErrorInvalidValue;
@@ -1341,27 +1354,28 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
 // ---- incremental sums (see kmeans_delta_gate). Per step, after the single-launch assign that
 // logged label changes: cml_kmeans_delta_gate, then cml_kmeans_sort_accum(gate = mode, msg = acc),
 // then cml_kmeans_delta_accum (which also publishes msg = acc).
-CML_API int cml_kmeans_delta_gate(unsigned* chg_count, int cap, int* force, int* mode, int k, int* dh,
-                                  void* stream) {
-  hipLaunchKernelGGL(kmeans_delta_gate, dim3(1), dim3(256), 0, (hipStream_t)stream, chg_count, cap, force, mode, k,
-                     dh);
+CML_API int cml_kmeans_delta_gate(const int* chg_wg_count, int nblk, int cap, int* chg_overflow, int* force, int* mode,
+                                  int k, int* dh, void* stream) {
+  hipLaunchKernelGGL(kmeans_delta_gate, dim3(1), dim3(256), 0, (hipStream_t)stream, chg_wg_count, nblk, cap,
+                     chg_overflow, force, mode, k, dh);
   return cml_status();
 }
 
 // dseg: 2k+1 ints, cursor: 2k ints, dperm: 2*cap ints, dsum: 2k*D doubles; slots/slot_c sized for
 // seg_grid (cml_kmeans_seg_slot_*); acc/msg: k*D + k + 1 doubles.
 CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, const int* labels, const int* chg_rows,
-                                   const int* chg_old, int cap, const int* mode, int k, int* dh, int* dseg,
+                                   const int* chg_old, const int* chg_wg_count, int nblk, int pcap, int cap,
+                                   const int* mode, int k, int* dh, int* dseg,
                                    int* cursor, int* dperm, int cpl, int seg_grid, double* dsum, double* slots,
                                    int* slot_c, double* acc, const double* cost_part, int ncost, double* msg, int xfp8,
                                    void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t lh = sizeof(int) * 2 * (size_t)k;
-  hipLaunchKernelGGL(kmeans_delta_hist, dim3(kDeltaBlocks), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
-                     mode, k, dh);
+  hipLaunchKernelGGL(kmeans_delta_hist, dim3(nblk), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
+                     chg_wg_count, pcap, mode, k, dh);
   hipLaunchKernelGGL(kmeans_delta_scan, dim3(1), dim3(256), 0, st, dh, mode, k, dseg, cursor);
-  hipLaunchKernelGGL(kmeans_delta_scatter, dim3(kDeltaBlocks), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
-                     mode, k, cursor, dperm);
+  hipLaunchKernelGGL(kmeans_delta_scatter, dim3(nblk), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
+                     chg_wg_count, pcap, mode, k, cursor, dperm);
   hipLaunchKernelGGL(zero_f64_gated, dim3(256), dim3(256), 0, st, dsum, 2LL * k * D, mode, 0);
   int e = cml_status();
   if (e) return e;

@@ -135,7 +135,8 @@ class LloydEngine:
             self.slots = K.seg_slots(self.cplan, d, dev)
         self.msg_len = k * d + k + 1
         # incremental sums: sort regime with the centres in one LDS chunk (labels are final after one launch)
-        self.delta = (K.DeltaState(max(maxn, 1), k, d, dp, self.row_chunks, self.msg_len, dev, fp8=fp8)
+        self.delta = (K.DeltaState(max(maxn, 1), k, d, dp, self.row_chunks, self.msg_len, dev, self.aplan.grid,
+                                   fp8=fp8)
                       if self._incremental and self.cplan.mode == "sort" and self.aplan.kc == self.aplan.kp else None)
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
@@ -302,10 +303,13 @@ class LloydEngine:
             return self.x[idx.long(), : self.d].to(torch.float64)
         return self.x[idx.long()]
 
-    def _min_dist(self, cands: torch.Tensor) -> torch.Tensor:
+    def _min_dist_idx(self, cands: torch.Tensor):
+        """(squared distance to the nearest of `cands` as f64, its index) of every local row."""
         if not self.gpu:
-            return K.assign_reference(self.x, cands)[1]
-        return assign_gpu(self.x, self.dp, self.d, cands, self.xnorm)[1].to(torch.float64)
+            lab, best = K.assign_reference(self.x, cands)
+            return best, lab
+        lab, best = assign_gpu(self.x, self.dp, self.d, cands, self.xnorm)
+        return best.to(torch.float64), lab.long()
 
     def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
         """k-means|| (Bahmani et al.), Spark's default initMode, then weighted local k-means++."""
@@ -323,7 +327,15 @@ class LloydEngine:
                                                                       device=self.device)
         row = self.comm.allgather(row)[owner] if self.comm.is_distributed else row
         centers = [row.reshape(1, self.d)]
-        costs = self._min_dist(centers[0]) if self.n else torch.zeros(0, dtype=torch.float64, device=self.device)
+        # nearest-candidate index is tracked across rounds (strict improvement keeps the earlier
+        # candidate, i.e. argmin's first-index rule over the concatenated candidate list), so the
+        # candidate weights need no extra assignment pass over the data at the end
+        if self.n:
+            costs, nearest = self._min_dist_idx(centers[0])
+        else:
+            costs = torch.zeros(0, dtype=torch.float64, device=self.device)
+            nearest = torch.zeros(0, dtype=torch.int64, device=self.device)
+        ncand = 1
         for step in range(steps):
             sum_cost = self.comm.sum_scalar(float(costs.sum().item()) if self.n else 0.0)
             if sum_cost <= 0:
@@ -338,17 +350,19 @@ class LloydEngine:
                 continue
             centers.append(new)
             if self.n:
-                costs = torch.minimum(costs, self._min_dist(new))
+                d_new, i_new = self._min_dist_idx(new)
+                better = d_new < costs
+                costs = torch.where(better, d_new, costs)
+                nearest = torch.where(better, i_new + ncand, nearest)
+            ncand += new.shape[0]
         cand = torch.cat(centers, 0)
-        cand_np = np.unique(cand.cpu().numpy(), axis=0)
+        cand_np, inverse = np.unique(cand.cpu().numpy(), axis=0, return_inverse=True)
         if cand_np.shape[0] <= k:
             out = cand_np
         else:
-            cand_t = torch.as_tensor(cand_np, device=self.device)
             if self.n:
-                lab = (K.assign_reference(self.x, cand_t)[0] if not self.gpu
-                       else assign_gpu(self.x, self.dp, self.d, cand_t, self.xnorm)[0].long())
-                w = torch.bincount(lab, minlength=cand_np.shape[0]).to(torch.float64)
+                inv = torch.as_tensor(inverse.reshape(-1), dtype=torch.int64, device=self.device)
+                w = torch.bincount(inv[nearest], minlength=cand_np.shape[0]).to(torch.float64)
             else:
                 w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)

@@ -24,8 +24,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_seg_threads": (c_int, []),
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
     "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
-                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
-                                       c_vp]),
+                                       c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
+                                       c_int, c_vp]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
@@ -35,10 +35,10 @@ _native.register_kernel_sigs({
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
                                       c_vp]),
-    "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_vp, c_vp, c_int, c_vp, c_vp]),
-    "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp, c_vp,
-                                       c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_int,
-                                       c_vp]),
+    "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
+                                       c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                       c_int, c_vp, c_int, c_vp]),
     "cml_kmeans_seg_slot_doubles": (c_ll, [c_int, c_int]),
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
@@ -185,7 +185,8 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
             rank.data_ptr() if (rank is not None and last) else 0,
             plan.grid, int(is_fp8(x)),
             delta.rows.data_ptr() if delta is not None else 0, delta.old.data_ptr() if delta is not None else 0,
-            delta.count.data_ptr() if delta is not None else 0, delta.cap if delta is not None else 0, st)
+            delta.wg_count.data_ptr() if delta is not None else 0,
+            delta.overflow.data_ptr() if delta is not None else 0, delta.pcap if delta is not None else 0, st)
         _native.check(status, "kmeans_assign_bf16")
 
 
@@ -251,13 +252,16 @@ class DeltaState:
     ``acc`` in full, every other step applies only the changed rows. ``force`` is set on creation and
     by ``invalidate()``."""
 
-    def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, fp8: bool = False,
-                 cap_fraction: float = 1.0 / 16):
-        self.k, self.d = k, d
+    def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, nblk: int,
+                 fp8: bool = False, cap_fraction: float = 1.0 / 16):
+        self.k, self.d, self.nblk = k, d, int(nblk)
         self.cap = max(1024, int(n * cap_fraction))
-        self.rows = torch.zeros(self.cap, dtype=torch.int32, device=device)
-        self.old = torch.zeros(self.cap, dtype=torch.int32, device=device)
-        self.count = torch.zeros(1, dtype=torch.int32, device=device)
+        # change lists are per assign workgroup: nblk lists of pcap entries (slack for uneven churn)
+        self.pcap = max(64, -(-2 * self.cap // self.nblk))
+        self.rows = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
+        self.old = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
+        self.wg_count = torch.zeros(self.nblk, dtype=torch.int32, device=device)
+        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
         self.mode = torch.zeros((chunks, 2), dtype=torch.int32, device=device)
         self.force = torch.ones(chunks, dtype=torch.int32, device=device)
         self.dh = torch.zeros(2 * k, dtype=torch.int32, device=device)
@@ -277,14 +281,15 @@ class DeltaState:
 
     def gate(self, chunk: int, stream=None) -> None:
         _native.check(_native.kernels().cml_kmeans_delta_gate(
-            self.count.data_ptr(), self.cap, self.force[chunk:].data_ptr(), self.mode[chunk].data_ptr(), self.k,
-            self.dh.data_ptr(), _native.stream_ptr(stream)), "kmeans_delta_gate")
+            self.wg_count.data_ptr(), self.nblk, self.cap, self.overflow.data_ptr(), self.force[chunk:].data_ptr(),
+            self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(), _native.stream_ptr(stream)), "kmeans_delta_gate")
 
     def accumulate(self, x: torch.Tensor, dp: int, labels: torch.Tensor, chunk: int, cost_part: torch.Tensor,
                    ncost: int, msg: torch.Tensor, stream=None) -> None:
         _native.check(_native.kernels().cml_kmeans_delta_accum(
             x.data_ptr(), x.stride(0), dp, self.d, labels.data_ptr(), self.rows.data_ptr(), self.old.data_ptr(),
-            self.cap, self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(), self.dseg.data_ptr(),
+            self.wg_count.data_ptr(), self.nblk, self.pcap, self.cap, self.mode[chunk].data_ptr(), self.k,
+            self.dh.data_ptr(), self.dseg.data_ptr(),
             self.cursor.data_ptr(), self.dperm.data_ptr(), self.plan.cpl, self.plan.seg_grid, self.dsum.data_ptr(),
             self.slots[0].data_ptr(), self.slots[1].data_ptr(), self.acc[chunk].data_ptr(), cost_part.data_ptr(),
             ncost, msg.data_ptr(), int(is_fp8(x)), _native.stream_ptr(stream)), "kmeans_delta_accum")
