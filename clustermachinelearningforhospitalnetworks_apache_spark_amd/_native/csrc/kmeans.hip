@@ -720,6 +720,21 @@ __device__ __forceinline__ void add_raw8(double (&acc)[CPL], const typename RawC
   }
 }
 
+template <int CPL>
+__device__ __forceinline__ void add_raw8_f32(float (&acc)[CPL], const typename RawCols8<CPL>::T& w) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  const unsigned* ws = reinterpret_cast<const unsigned*>(&w);
+#pragma unroll
+  for (int q = 0; q < CPL / 4; ++q) {
+    const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], false);
+    const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], true);
+    acc[4 * q] += a.x;
+    acc[4 * q + 1] += a.y;
+    acc[4 * q + 2] += b.x;
+    acc[4 * q + 3] += b.y;
+  }
+}
+
 template <int CPL, bool F8> struct SegRaw { using T = typename RawCols<CPL>::T; };
 template <int CPL> struct SegRaw<CPL, true> { using T = typename RawCols8<CPL>::T; };
 
@@ -788,23 +803,28 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
     }
     const long long pe = p + cnt;
     if (next >= pe) {
+      if constexpr (F8) {
+        // e4m3 values are multiples of 2^-9 below 2^9: 16 of them sum EXACTLY in f32, so the rows
+        // are added in f32 and folded into f64 once per batch (half the f64 adds and conversions)
+        float part[CPL];
 #pragma unroll
-      for (int u = 0; u < U; ++u) {
-        if constexpr (F8) add_raw8<CPL>(acc, w[u]);
-        else add_raw<CPL>(acc, w[u]);
+        for (int j = 0; j < CPL; ++j) part[j] = 0.f;
+#pragma unroll
+        for (int u = 0; u < U; ++u) add_raw8_f32<CPL>(part, w[u]);
+#pragma unroll
+        for (int j = 0; j < CPL; ++j) acc[j] += (double)part[j];
+      } else {
+#pragma unroll
+        for (int u = 0; u < U; ++u) add_raw<CPL>(acc, w[u]);
       }
     } else {
-      long long s0 = p;
-      while (true) {
-        const long long se = next < pe ? next : pe;
-#pragma unroll
-        for (int u = 0; u < U; ++u)
-          if (p + u >= s0 && p + u < se) {
-            if constexpr (F8) add_raw8<CPL>(acc, w[u]);
-            else add_raw<CPL>(acc, w[u]);
-          }
-        if (se < next) break;  // chunk ends inside cluster c
-        {
+      // a cluster boundary inside this batch (~k + #waves batches per pass): walk its rows one at a
+      // time, re-reading each (cache hits) instead of keeping the batch's registers live — the
+      // unrolled predicated form doubled the kernel's VGPRs and halved its occupancy
+#pragma unroll 1
+      for (int u = 0; u < cnt; ++u) {
+        const long long pos = p + u;
+        while (pos >= next) {  // cluster c ended before pos
           double* dst = nflush == 0 ? slotA : msg + (long long)c * D;  // later clusters are ours alone
           if (active) {
 #pragma unroll
@@ -813,14 +833,17 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
           }
           if (nflush == 0 && lane == 0) slot_c[2 * wave] = c;
           ++nflush;
-        }
 #pragma unroll
-        for (int j = 0; j < CPL; ++j) acc[j] = 0.0;
-        ++c;
-        next = seg[c + 1];
-        while (next <= se && c < k - 1) { ++c; next = seg[c + 1]; }
-        s0 = se;
-        if (s0 >= pe) break;
+          for (int j = 0; j < CPL; ++j) acc[j] = 0.0;
+          ++c;
+          next = seg[c + 1];
+          while (next <= pos && c < k - 1) { ++c; next = seg[c + 1]; }
+        }
+        const long long row = __builtin_amdgcn_readlane(pr, u);
+        raw_t v = raw_t{};
+        if (active) v = *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ);
+        if constexpr (F8) add_raw8<CPL>(acc, v);
+        else add_raw<CPL>(acc, v);
       }
     }
   }
