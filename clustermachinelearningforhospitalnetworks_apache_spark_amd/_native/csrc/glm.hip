@@ -255,10 +255,30 @@ __global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __res
   }
 }
 
+// Sum over the lpr lanes of a row group, result in every lane. f32: the within-16-lane steps are
+// DPP lane permutes on the VALU (quad swaps, half-row and row mirrors: each pairs a lane with one
+// of the other half, which is all a sum needs), only the 16/32 steps cross rows through the LDS
+// crossbar — a chain of five ds_bpermute round trips per row group was the latency floor of the
+// margin reduction. f64 keeps the shuffle form.
+template <int CTRL>
+__device__ __forceinline__ float dpp_f32(float v) {
+  return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), CTRL, 0xf, 0xf, false));
+}
+
 template <typename CT>
 __device__ inline CT group_sum_ct(CT v, int lpr) {
-  for (int o = lpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
-  return v;
+  if constexpr (sizeof(CT) == 4) {
+    if (lpr >= 2) v += dpp_f32<0xB1>(v);   // quad_perm(1,0,3,2)
+    if (lpr >= 4) v += dpp_f32<0x4E>(v);   // quad_perm(2,3,0,1)
+    if (lpr >= 8) v += dpp_f32<0x141>(v);  // row_half_mirror
+    if (lpr >= 16) v += dpp_f32<0x140>(v); // row_mirror
+    if (lpr >= 32) v += __shfl_xor(v, 16, 64);
+    if (lpr >= 64) v += __shfl_xor(v, 32, 64);
+    return v;
+  } else {
+    for (int o = lpr >> 1; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+  }
 }
 
 __device__ inline float sigmoid_ct(float m) { return 1.f / (1.f + __expf(-m)); }
