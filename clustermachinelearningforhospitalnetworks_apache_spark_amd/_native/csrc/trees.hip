@@ -102,6 +102,143 @@ __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __r
   }
 }
 
+// K19 best split, one workgroup per (tree, node) of the level, on the all-reduced fixed-point
+// histogram (exact int64 prefix sums over bins, converted to f64 per candidate). Spark's
+// binsToBestSplit takes the first maximum gain in (feature, bin) order among candidates whose two
+// children reach the minimum weight and whose gain reaches minInfoGain. Small nodes often have
+// EXACT ties (two features separating the same rows), which rounding then breaks arbitrarily, so
+// the rule here is order-independent: G = max gain, then the first (feature, bin) whose gain is
+// within kTreeTieRel·|G| of G (two block reductions) — CPU, GPU and any world size pick the same
+// split. out row: [gain, feature, bin, total S, left S, right S]; gain = -inf and feature = -1 when
+// no valid split exists. Only (f, b) with mask[f] and b < nsplit[f] are candidates. S <= kTreeSMax.
+constexpr int kTreeSMax = 16;
+constexpr double kTreeTieRel = 1e-12;
+
+__device__ double impurity_dev(const double* st, int S, int kind) {
+  if (kind == 0) {
+    const double w = st[0];
+    if (w <= 0.0) return 0.0;
+    const double m = st[1] / w;
+    const double v = st[2] / w - m * m;
+    return v > 0.0 ? v : 0.0;
+  }
+  double tot = 0.0;
+  for (int c = 0; c < S; ++c) tot += st[c];
+  if (tot <= 0.0) return 0.0;
+  double r = kind == 1 ? 1.0 : 0.0;
+  for (int c = 0; c < S; ++c) {
+    const double p = st[c] / tot;
+    if (kind == 1) r -= p * p;
+    else if (p > 0.0) r -= p * log2(p);
+  }
+  return r;
+}
+
+__device__ __forceinline__ double count_dev(const double* st, int S, int kind) {
+  if (kind == 0) return st[0];
+  double t = 0.0;
+  for (int c = 0; c < S; ++c) t += st[c];
+  return t;
+}
+
+__global__ __launch_bounds__(256) void tree_best_split_kernel(const long long* __restrict__ hist, int d, int nbins,
+                                                              int S, const double* __restrict__ scale, int kind,
+                                                              const unsigned char* __restrict__ mask,
+                                                              const int* __restrict__ nsplit, double min_inst,
+                                                              double min_wfrac, double min_gain,
+                                                              double* __restrict__ out) {
+  __shared__ long long tot_i[kTreeSMax];
+  __shared__ double bg[256];
+  __shared__ int bi[256];
+  const int tn = blockIdx.x;  // tree * nodes + node
+  const long long* h = hist + (long long)tn * d * nbins * S;
+  const int tid = threadIdx.x;
+  if (tid < S) {
+    long long t = 0;
+    for (int b = 0; b < nbins; ++b) t += h[(long long)b * S + tid];  // feature 0 covers every row once
+    tot_i[tid] = t;
+  }
+  __syncthreads();
+  double sc[kTreeSMax], tot[kTreeSMax];
+  for (int c = 0; c < S; ++c) {
+    sc[c] = scale[kind == 0 ? c : 0];
+    tot[c] = (double)tot_i[c] / sc[c];
+  }
+  const double wtot = count_dev(tot, S, kind);
+  const double imp = impurity_dev(tot, S, kind);
+  const double min_w = fmax(min_inst, min_wfrac * wtot);
+  // pass 0: G = the maximum valid gain; pass 1: first (f, b) whose gain is within the tie tolerance
+  double G = -__builtin_huge_val();
+  int bidx = 0x7fffffff;
+  for (int pass = 0; pass < 2; ++pass) {
+    const double thr = pass == 0 ? 0.0 : G - kTreeTieRel * fabs(G);
+    double best = -__builtin_huge_val();
+    bidx = 0x7fffffff;
+    for (int f = tid; f < d; f += blockDim.x) {
+      if (!mask[(long long)tn * d + f]) continue;
+      const int ns = nsplit[f];
+      const long long* hf = h + (long long)f * nbins * S;
+      long long cum[kTreeSMax];
+      for (int c = 0; c < S; ++c) cum[c] = 0;
+      for (int b = 0; b < ns; ++b) {
+        double ls[kTreeSMax], rs[kTreeSMax];
+        for (int c = 0; c < S; ++c) {
+          cum[c] += hf[(long long)b * S + c];
+          ls[c] = (double)cum[c] / sc[c];
+          rs[c] = (double)(tot_i[c] - cum[c]) / sc[c];
+        }
+        const double wl = count_dev(ls, S, kind), wr = count_dev(rs, S, kind);
+        if (wl < min_w || wr < min_w || wl <= 0.0 || wr <= 0.0) continue;
+        const double gain = imp - (wl / wtot) * impurity_dev(ls, S, kind) - (wr / wtot) * impurity_dev(rs, S, kind);
+        if (gain < min_gain) continue;
+        if (pass == 0) {
+          best = gain > best ? gain : best;
+        } else if (gain >= thr && f * nbins + b < bidx) {
+          bidx = f * nbins + b;
+          best = gain;
+        }
+      }
+    }
+    bg[tid] = best;
+    bi[tid] = bidx;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if (tid < o) {
+        if (pass == 0) {
+          bg[tid] = bg[tid + o] > bg[tid] ? bg[tid + o] : bg[tid];
+        } else if (bi[tid + o] < bi[tid]) {
+          bg[tid] = bg[tid + o];
+          bi[tid] = bi[tid + o];
+        }
+      }
+      __syncthreads();
+    }
+    if (pass == 0) {
+      G = bg[0];
+      __syncthreads();
+      if (!(G > -__builtin_huge_val())) break;  // no valid candidate (uniform)
+    }
+  }
+  if (tid == 0) {
+    double* o = out + (long long)tn * (3 + 3 * S);
+    const bool valid = G > -__builtin_huge_val() && bi[0] != 0x7fffffff;
+    const int f = valid ? bi[0] / nbins : -1, b = valid ? bi[0] % nbins : -1;
+    o[0] = valid ? bg[0] : -__builtin_huge_val();
+    o[1] = (double)f;
+    o[2] = (double)b;
+    long long cum[kTreeSMax];
+    for (int c = 0; c < S; ++c) cum[c] = 0;
+    if (valid)
+      for (int bb = 0; bb <= b; ++bb)
+        for (int c = 0; c < S; ++c) cum[c] += h[((long long)f * nbins + bb) * S + c];
+    for (int c = 0; c < S; ++c) {
+      o[3 + c] = tot[c];
+      o[3 + S + c] = (double)cum[c] / sc[c];
+      o[3 + 2 * S + c] = (double)(tot_i[c] - cum[c]) / sc[c];
+    }
+  }
+}
+
 // split_feat/split_bin/left_id/right_id: [T][nodes]; split_feat < 0 => node is a leaf (row retires).
 __global__ void tree_route_kernel(const unsigned char* __restrict__ bins, long long n, int d, int T, int nodes,
                                   int* __restrict__ node_of, const int* __restrict__ split_feat,
@@ -173,6 +310,16 @@ CML_API int cml_tree_hist(const unsigned char* bins, long long n, int d, int nbi
   hipFuncSetAttribute((const void*)tree_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   hipLaunchKernelGGL(tree_hist_kernel, dim3(row_blocks, T, fchunks), dim3(256), lds, (hipStream_t)stream, bins, n, d,
                      nbins, node_of, wt, y, cls, S, nodes, fc, scales[0], scales[1], scales[2], out);
+  return cml_status();
+}
+
+// K19: out [T*nodes][3 + 3S] (see tree_best_split_kernel). kind 0 variance, 1 gini, 2 entropy.
+CML_API int cml_tree_best_split(const long long* hist, int tn, int d, int nbins, int S, const double* scale, int kind,
+                                const unsigned char* mask, const int* nsplit, double min_inst, double min_wfrac,
+                                double min_gain, double* out, void* stream) {
+  if (S < 1 || S > kTreeSMax || tn < 1) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(tree_best_split_kernel, dim3(tn), dim3(256), 0, (hipStream_t)stream, hist, d, nbins, S, scale,
+                     kind, mask, nsplit, min_inst, min_wfrac, min_gain, out);
   return cml_status();
 }
 

@@ -28,7 +28,7 @@ import numpy as np
 import torch
 
 from .. import _native
-from .._native import c_int, c_ll, c_vp
+from .._native import c_dbl, c_int, c_ll, c_vp
 from ..parallel.comm import Communicator, local_comm
 from ..utils import rng
 
@@ -36,6 +36,8 @@ _native.register_kernel_sigs({
     "cml_tree_binize": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "cml_tree_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
                               c_int, c_vp]),
+    "cml_tree_best_split": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_dbl, c_dbl,
+                                    c_dbl, c_vp, c_vp]),
     "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
 })
@@ -325,10 +327,16 @@ class ForestEngine:
                 break  # nodes at maxDepth are leaves; their stats came with the parent's split
             hist = self.histogram(bins, node_of, wt, nodes)
             self.comm.allreduce_(hist)
-            h = hist.cpu().numpy()
-            if self.gpu:  # exact integer sums -> float64 statistics
-                sc = self.scales[:3] if self.kind == "variance" else np.full(self.S, self.scales[0])
-                h = h.astype(np.float64) / sc
+            # per-node feature subsets (RF), drawn for every node of the level in order, identically on
+            # every rank (same seed, same draws)
+            masks = np.ones((T, nodes, self.d), dtype=np.uint8)
+            if k_sub < self.d:
+                masks[:] = 0
+                for t in range(T):
+                    for j in range(len(level_nodes[t])):
+                        masks[t, j, rs.choice(self.d, k_sub, replace=False)] = 1
+            res = self.best_splits(hist, masks, nodes)  # [T, nodes, 3 + 3S] (K19)
+            S = self.S
             split_feat = np.full((T, nodes), -1, dtype=np.int32)
             split_bin = np.zeros((T, nodes), dtype=np.int32)
             left_id = np.full((T, nodes), -1, dtype=np.int32)
@@ -336,26 +344,20 @@ class ForestEngine:
             next_level: List[List[Node]] = [[] for _ in range(T)]
             for t in range(T):
                 for j, node in enumerate(level_nodes[t]):
-                    hh = h[t, j]  # [d, nbins, S]
-                    tot = hh[0].sum(0) if self.d else np.zeros(self.S)
+                    r = res[t, j]
                     if node.stats is None:
-                        node.stats = tot
+                        node.stats = r[3:3 + S].copy()
                     node.count = count_of(node.stats, self.kind)
                     node.impurity = impurity_of(node.stats, self.kind)
                     node.prediction = predict_of(node.stats, self.kind)
-                    if depth == p.max_depth or node.count <= 0:
-                        continue
-                    feats = np.arange(self.d)
-                    if k_sub < self.d:
-                        feats = np.sort(rs.choice(self.d, k_sub, replace=False))
-                    best = self._best_split(hh, node, feats)
-                    if best is None:
-                        continue
-                    gain, f, b, lstats, rstats = best
-                    node.gain, node.feature, node.split_bin = gain, int(f), int(b)
+                    gain, f = float(r[0]), int(r[1])
+                    if node.count <= 0 or f < 0 or not gain > 0:
+                        continue  # leaf (Spark: isLeaf = gain <= 0)
+                    b = int(r[2])
+                    node.gain, node.feature, node.split_bin = gain, f, b
                     node.threshold = float(splits[f][b])
-                    node.left = Node(stats=lstats)
-                    node.right = Node(stats=rstats)
+                    node.left = Node(stats=r[3 + S:3 + 2 * S].copy())
+                    node.right = Node(stats=r[3 + 2 * S:3 + 3 * S].copy())
                     for child in (node.left, node.right):
                         child.count = count_of(child.stats, self.kind)
                         child.impurity = impurity_of(child.stats, self.kind)
@@ -376,32 +378,87 @@ class ForestEngine:
             _assign_ids(r)
         return roots
 
-    def _best_split(self, hh: np.ndarray, node: Node, feats: Sequence[int]):
+    def best_splits(self, hist, masks: np.ndarray, nodes: int) -> np.ndarray:
+        """K19: per (tree, node) [gain, feature, bin, total S, left S, right S] of the best split among
+        candidates whose children both reach the minimum weight and whose gain reaches minInfoGain (feature
+        -1: none). Spark's binsToBestSplit takes the first maximum in (feature, bin) order; exact ties (two
+        features separating the same rows of a small node) are common and rounding breaks them arbitrarily,
+        so both paths take the first (feature, bin) within TIE_REL·|G| of the maximum G. GPU: one workgroup
+        per node on the fixed-point histogram; CPU: the same rule vectorised in numpy."""
+        T, S, d, nb = self.p.num_trees, self.S, self.d, self.nbins
         p = self.p
-        total = node.stats
-        wtot = count_of(total, self.kind)
-        imp = impurity_of(total, self.kind)
-        best = None
-        min_w = max(p.min_instances, p.min_weight_fraction * wtot)
-        for f in feats:
-            nsp = len(self.splits[f])
-            if nsp == 0:
-                continue
-            cum = np.cumsum(hh[f], axis=0)  # [nbins, S]: bins <= b go left
-            for b in range(nsp):
-                ls = cum[b]
-                rs_ = total - ls
-                wl, wr = count_of(ls, self.kind), count_of(rs_, self.kind)
-                if wl < min_w or wr < min_w or wl <= 0 or wr <= 0:
-                    continue
-                gain = imp - (wl / wtot) * impurity_of(ls, self.kind) - (wr / wtot) * impurity_of(rs_, self.kind)
-                if gain < p.min_info_gain:
-                    continue
-                if best is None or gain > best[0] + 1e-15:
-                    best = (gain, f, b, ls.copy(), rs_.copy())
-        if best is None or best[0] <= 0:
-            return None
-        return best
+        kind_id = {"variance": 0, "gini": 1, "entropy": 2}[self.kind]
+        nsplit = np.array([len(sp) for sp in self.splits], dtype=np.int32)
+        if self.gpu:
+            out = torch.empty((T * nodes, 3 + 3 * S), dtype=torch.float64, device=self.dev)
+            sc = torch.as_tensor(self.scales, dtype=torch.float64, device=self.dev)
+            mk = torch.as_tensor(masks.reshape(-1), device=self.dev)
+            ns = torch.as_tensor(nsplit, device=self.dev)
+            st = _native.kernels().cml_tree_best_split(hist.data_ptr(), T * nodes, d, nb, S, sc.data_ptr(), kind_id,
+                                                        mk.data_ptr(), ns.data_ptr(), float(p.min_instances),
+                                                        float(p.min_weight_fraction), float(p.min_info_gain),
+                                                        out.data_ptr(), _native.stream_ptr())
+            _native.check(st, "tree_best_split")
+            return out.cpu().numpy().reshape(T, nodes, 3 + 3 * S)
+        h = hist.cpu().numpy().astype(np.float64)                   # [T, nodes, d, nb, S]
+        tot = h[:, :, 0].sum(axis=2) if d else np.zeros((T, nodes, S))  # [T, nodes, S]
+        left = np.cumsum(h, axis=3)
+        right = tot[:, :, None, None, :] - left
+        cnt = (lambda a: a[..., 0]) if self.kind == "variance" else (lambda a: a.sum(-1))
+        wtot, wl, wr = cnt(tot), cnt(left), cnt(right)
+        imp_t, imp_l, imp_r = _impurity_vec(tot, self.kind), _impurity_vec(left, self.kind), _impurity_vec(right,
+                                                                                                       self.kind)
+        with np.errstate(divide="ignore", invalid="ignore"):
+            gain = imp_t[:, :, None, None] - (wl / wtot[:, :, None, None]) * imp_l - (wr / wtot[:, :, None, None]) * imp_r
+        min_w = np.maximum(p.min_instances, p.min_weight_fraction * wtot)[:, :, None, None]
+        ok = (wl >= min_w) & (wr >= min_w) & (wl > 0) & (wr > 0)
+        ok &= np.arange(nb)[None, None, None, :] < nsplit[None, None, :, None]
+        ok &= masks[:, :, :, None].astype(bool)
+        ok &= gain >= p.min_info_gain
+        gain = np.where(ok, gain, -np.inf)
+        flat = gain.reshape(T, nodes, d * nb)
+        if d * nb:
+            # order-independent tie rule (see trees.hip K19): first (feature, bin) within 1e-12·|G| of the max G
+            G = flat.max(-1)
+            near = flat >= (G - TIE_REL * np.abs(G))[..., None]
+            arg = near.argmax(-1)
+            best = np.take_along_axis(flat, arg[..., None], -1)[..., 0]
+            valid = np.isfinite(G)
+        else:
+            arg = np.zeros((T, nodes), dtype=np.int64)
+            best = np.full((T, nodes), -np.inf)
+            valid = np.zeros((T, nodes), dtype=bool)
+        f, b = arg // max(nb, 1), arg % max(nb, 1)
+        ti, ni = np.meshgrid(np.arange(T), np.arange(nodes), indexing="ij")
+        out = np.zeros((T, nodes, 3 + 3 * S))
+        out[..., 0] = np.where(valid, best, -np.inf)
+        out[..., 1] = np.where(valid, f, -1)
+        out[..., 2] = np.where(valid, b, -1)
+        out[..., 3:3 + S] = tot
+        if d * nb:
+            out[..., 3 + S:3 + 2 * S] = left[ti, ni, f, b]
+            out[..., 3 + 2 * S:] = right[ti, ni, f, b]
+        return out
+
+
+TIE_REL = 1e-12  # kTreeTieRel in trees.hip
+
+
+def _impurity_vec(st: np.ndarray, kind: str) -> np.ndarray:
+    """impurity_of over the last axis of a stats array."""
+    with np.errstate(divide="ignore", invalid="ignore"):
+        if kind == "variance":
+            w = st[..., 0]
+            m = st[..., 1] / w
+            v = np.maximum(st[..., 2] / w - m * m, 0.0)
+            return np.where(w > 0, v, 0.0)
+        tot = st.sum(-1)
+        pr = st / tot[..., None]
+        if kind == "gini":
+            r = 1.0 - (pr * pr).sum(-1)
+        else:
+            r = -np.where(pr > 0, pr * np.log2(np.where(pr > 0, pr, 1.0)), 0.0).sum(-1)
+        return np.where(tot > 0, r, 0.0)
 
 
 def _poisson(row_ids, seed, stream, lam):

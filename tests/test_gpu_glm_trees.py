@@ -92,6 +92,31 @@ def test_forest_gpu_matches_cpu(task, trees):
     np.testing.assert_allclose(pg.cpu().numpy(), pc.numpy(), rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("imp", ["variance", "entropy", "gini"])
+def test_forest_gpu_matches_cpu_wide(imp):
+    """40 features, 12 trees with per-node feature subsets: the GPU K19 best-split kernel (fixed-point
+    histogram) and the vectorised CPU rule grow the same forests."""
+    torch.manual_seed(9)
+    n, d = 20000, 40
+    x = torch.randn(n, d, dtype=torch.float64)
+    task = "regression" if imp == "variance" else "classification"
+    if task == "regression":
+        y = x[:, 3] * 2 + (x[:, 17] > 0).double() - x[:, 29] + torch.randn(n, dtype=torch.float64) * 0.1
+    else:
+        y = ((x[:, 5] + x[:, 11] * 0.5) > 0).double() + (x[:, 30] > 0.5).double()
+    p = TR.TreeParams(task=task, num_classes=3, impurity=imp, num_trees=12, seed=5, feature_subset="onethird")
+    cpu = TR.ForestEngine(x, y, p).fit()
+    gpu = TR.ForestEngine(x.cuda(), y.cuda(), p).fit()
+    for a, b in zip(cpu, gpu):
+        na, nb = TR.preorder(a), TR.preorder(b)
+        assert len(na) == len(nb)
+        for u, v in zip(na, nb):
+            assert u.feature == v.feature and u.split_bin == v.split_bin
+            np.testing.assert_allclose(u.stats, v.stats, rtol=1e-9, atol=1e-9)
+            if u.feature >= 0:
+                np.testing.assert_allclose(u.gain, v.gain, rtol=1e-9, atol=1e-12)
+
+
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float64])
 def test_sgd_graph_replay_matches_eager(dtype):
     """The captured SGD step (device-side batch offset, K13 + update in one HIP graph) equals the
