@@ -157,24 +157,39 @@ __device__ __forceinline__ void slot_update(const f32x4 (&acc)[RT], int t, int i
 }
 
 // MFMA chain of centre tile `ct` for all RT sub-tiles into `acc` (each A fragment feeds RT
-// MFMAs; the accumulators start at ||c||² + ||x||², so they end as squared distances), with the
-// slot updates of the previous tile's accumulators interleaved.
-template <int DP, int RT, int RING, bool PREV>
-__device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& xt, const float (&xn)[RT], int ct,
-                                      int g, f32x4 (&acc)[RT], const f32x4 (&prev)[RT], uint4 (&ring)[RING],
-                                      int (&key)[RT][4]) {
+// MFMAs), with the slot updates of the previous tile's accumulators interleaved. The first k-step
+// of every sub-tile takes its C operand from ONE register set, cinit = ||c||² + moff, where moff
+// is the largest ||x||² among the lane's RT rows: the accumulators end as the squared distance
+// plus the row's offset moff − ||x||² >= 0 (the packed-key minimum needs non-negative values; the
+// epilogue subtracts it). Seeding each sub-tile with its own ||x||² cost RT·4 VALU per centre tile
+// in an issue stream where MFMAs leave ~8 of every 16 cycles for everything else.
+// Precision: a row's candidates carry the offset moff − ||x||², so their f32 rounding is on the
+// scale of the tile's largest norm instead of the row's own. That only matters for rows sharing
+// a 64-row tile with an outlier ~100x their norm; bf16 quantisation of x (2^-8 relative in x·c)
+// is the larger error below that.
+// SHARED = false keeps the per-sub-tile seeding (c4 + ||x||² of each row) — the A/B reference of
+// kmeans_ops.set_assign_variant(6); in one process it measured 2.77 vs 2.71 ms full and 2.15 vs
+// 2.07 ms compute-only (profiles/assign_shared_seed_ab_20Mx256.log).
+template <int DP, int RT, int RING, bool PREV, bool SHARED>
+__device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& xt, float moff,
+                                      const float (&xn)[RT], int ct, int g, f32x4 (&acc)[RT],
+                                      const f32x4 (&prev)[RT], uint4 (&ring)[RING], int (&key)[RT][4]) {
   constexpr int KS = AssignShape<DP>::KS;
   constexpr int NSLOT = RT * 4;
   const float4 c4 = *reinterpret_cast<const float4*>(cx.cn + ct * 16 + 4 * g);
+  const f32x4 cinit = {c4.x + moff, c4.y + moff, c4.z + moff, c4.w + moff};
+  if constexpr (!SHARED) {
 #pragma unroll
-  for (int t = 0; t < RT; ++t) acc[t] = f32x4{c4.x + xn[t], c4.y + xn[t], c4.z + xn[t], c4.w + xn[t]};
+    for (int t = 0; t < RT; ++t) acc[t] = f32x4{c4.x + xn[t], c4.y + xn[t], c4.z + xn[t], c4.w + xn[t]};
+  }
 #pragma unroll
   for (int s = 0; s < KS; ++s) {
     const uint4 a = ring[s % RING];
     ring[s % RING] = frag_at<DP>(cx, ct + (s + RING) / KS, (s + RING) % KS);
 #pragma unroll
     for (int t = 0; t < RT; ++t)
-      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), xt.f[t][s], acc[t], 0, 0, 0);
+      acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), xt.f[t][s],
+                                                       (SHARED && s == 0) ? cinit : acc[t], 0, 0, 0);
     if constexpr (PREV) {
 #pragma unroll
       for (int q = (s * NSLOT) / KS; q < ((s + 1) * NSLOT) / KS; ++q)
@@ -197,7 +212,7 @@ struct DeltaOut {
   int* lds_count;  // set in the kernel
 };
 
-template <int DP, int RT, int RINGMAX>
+template <int DP, int RT, int RINGMAX, bool SHARED>
 __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP, RT>& xt, long long tile,
                                             long long n, int r, int g, int c_base, const float* __restrict__ xnorm,
                                             int* __restrict__ labels, float* __restrict__ best_io, int first,
@@ -206,10 +221,12 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
   constexpr int KS = AssignShape<DP>::KS;
   constexpr int RING = KS < RINGMAX ? KS : RINGMAX;
   float xn[RT];
+  float moff = 0.f;  // largest ||x||² of this lane's rows (see chain)
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     const long long row = tile * (16 * RT) + 16 * t + r;
     xn[t] = row < n ? xnorm[row] : 0.f;
+    moff = fmaxf(moff, xn[t]);
   }
   int key[RT][4];
 #pragma unroll
@@ -221,14 +238,14 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
   for (int q = 0; q < RING; ++q) ring[q] = frag_at<DP>(cx, q / KS, q % KS);
   f32x4 acc0[RT], acc1[RT];
   const int nct = cx.nct;
-  chain<DP, RT, RING, false>(cx, xt, xn, 0, g, acc0, acc1, ring, key);
+  chain<DP, RT, RING, false, SHARED>(cx, xt, moff, xn, 0, g, acc0, acc1, ring, key);
   int ct = 1;
   for (; ct + 1 < nct; ct += 2) {
-    chain<DP, RT, RING, true>(cx, xt, xn, ct, g, acc1, acc0, ring, key);
-    chain<DP, RT, RING, true>(cx, xt, xn, ct + 1, g, acc0, acc1, ring, key);
+    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
+    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct + 1, g, acc0, acc1, ring, key);
   }
   if (ct < nct) {
-    chain<DP, RT, RING, true>(cx, xt, xn, ct, g, acc1, acc0, ring, key);
+    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
 #pragma unroll
     for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc1, q >> 2, q & 3, ct, cx.cmask, key);
   } else {
@@ -253,6 +270,7 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
       if (ob < best || (ob == best && oi < bidx)) { best = ob; bidx = oi; }
     }
     bidx += c_base;
+    if constexpr (SHARED) best = best - moff + xn[t];  // remove the row offset: squared distance
     const long long row = tile * (16 * RT) + 16 * t + r;
     const bool mine = g == 0 && row < n;
     if (!first && mine) {
@@ -294,7 +312,7 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
 
 // NT threads; each wave owns super-tiles of RT x 16 rows. PF: the next super-tile's rows are in
 // flight while this one computes (double-buffered X registers).
-template <int DP, int RT, int NT, bool PF, int RINGMAX, bool F8>
+template <int DP, int RT, int NT, bool PF, int RINGMAX, bool F8, bool SHARED = true>
 __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     const void* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
     int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
@@ -366,18 +384,18 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     for (; tile < ntiles; tile += 2 * tw) {
       const long long t1 = tile + tw;
       if (t1 < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1, r, g, xb);
-      assign_tile<DP, RT, RINGMAX>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
       if (t1 >= ntiles) break;
       if (t1 + tw < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1 + tw, r, g, xa);
-      assign_tile<DP, RT, RINGMAX>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
     }
   } else {
     for (; tile < ntiles; tile += tw) {
       XTile<DP, RT> xt;
       load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xt);
-      assign_tile<DP, RT, RINGMAX>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
     }
   }
@@ -1110,6 +1128,11 @@ const void* assign_kernel_ptr() {
     case 3: return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, 2, F8>;
     case 4: return (const void*)kmeans_assign_bf16<DP, 2, 768, false, 4, F8>;
     case 5: return (const void*)kmeans_assign_bf16<DP, 1, 1024, PF, 4, F8>;
+    case 6:  // the default launch with per-sub-tile accumulator seeding (A/B reference of SHARED)
+      if constexpr (DP >= 256)
+        return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8, false>;
+      else
+        return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8, false>;
     default:
       if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8>;
       else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
@@ -1125,6 +1148,7 @@ inline int assign_tile_rows(int Dp) {
     case 3: return Dp >= 512 ? 32 : 64;
     case 4: return 32;
     case 5: return 16;
+    case 6: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
     default: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
   }
 }
@@ -1228,7 +1252,7 @@ CML_API int cml_kmeans_set_assign_sched(int v) {
   return 0;
 }
 CML_API int cml_kmeans_set_assign_variant(int v) {
-  if (v < 0 || v > 5) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 6) return (int)hipErrorInvalidValue;
   g_assign_variant = v;
   return 0;
 }

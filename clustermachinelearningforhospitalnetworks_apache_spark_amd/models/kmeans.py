@@ -65,6 +65,24 @@ def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
     return out
 
 
+def cached_row_sqnorm(x: torch.Tensor, n: int, dp: int) -> torch.Tensor:
+    """||x_i||² of the device matrix's rows, kept on the tensor itself while it is unmodified.
+
+    Spark caches point norms with the vectors (reference KMeans uses VectorWithNorm); here the cache
+    rides on the feature tensor, so a fit followed by ``KMeansModel.transform``/``computeCost`` on the
+    same features reads the matrix once for its norms instead of once per call. The entry is keyed by
+    the tensor's version counter: any in-place write invalidates it."""
+    ent = getattr(x, "_cml_xnorm", None)
+    if ent is not None and ent[0] == x._version and ent[1] == (n, dp):
+        return ent[2]
+    xn = K.row_sqnorm(x, n, dp)
+    try:
+        x._cml_xnorm = (x._version, (n, dp), xn)
+    except (AttributeError, RuntimeError):
+        pass
+    return xn
+
+
 class LloydEngine:
     """Rank-local shard + distributed Lloyd iterations."""
 
@@ -120,7 +138,7 @@ class LloydEngine:
         # distance scratch only when the centres need several LDS chunks (running min through HBM)
         self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev) if self.aplan.kc < self.aplan.kp
                      else None)
-        self.xnorm = K.row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
+        self.xnorm = cached_row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
             self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
@@ -370,6 +388,12 @@ class LloydEngine:
                 out = local_kmeans_pp_device(torch.as_tensor(cand_np, device=self.device), w, k, seed, max_iter=30)
             else:
                 out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30)
+            if self.comm.is_distributed:
+                # every rank ran the same local k-means on the same candidates and weights; rank 0's
+                # result is taken verbatim so last-bit differences of device reductions cannot make
+                # the ranks start (and later decide convergence) from different centres
+                t = torch.as_tensor(np.ascontiguousarray(out, dtype=np.float64), device=self.device)
+                out = self.comm.broadcast_(t, 0).cpu().numpy()
         if out.shape[0] < k:
             # Spark may return fewer centres when there are < k distinct points; pad by repetition so the
             # device buffers keep their shape, and record the real count.
@@ -394,7 +418,7 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: O
     best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     if n:
         if xnorm is None:
-            xnorm = K.row_sqnorm(x, n, dp)
+            xnorm = cached_row_sqnorm(x, n, dp)
         plan = K.plan_assign(n, dp, k, dev.index or 0, fp8=K.is_fp8(x))
         K.assign_bf16(x, n, dp, cb, cn, plan, labels, best, None, xnorm=xnorm)
     return labels[:n], best[:n]

@@ -104,7 +104,7 @@ def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = Fals
 
 
 def set_assign_variant(v: int) -> None:
-    """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD)."""
+    """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD, ..., 6 default shape with per-sub-tile accumulator seeding)."""
     _native.check(_native.kernels().cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
 
 

@@ -94,6 +94,29 @@ def test_incremental_fp8_and_row_chunks():
             np.testing.assert_allclose(mi.cpu().numpy(), mf.cpu().numpy(), rtol=1e-12, atol=1e-9)
 
 
+def test_row_norm_cache_follows_tensor_version():
+    """cached_row_sqnorm: reused for the same unmodified device matrix, recomputed after a write."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import (
+        assign_gpu, cached_row_sqnorm, to_device_matrix)
+    n, d, k = 40_000, 256, 32
+    x = to_device_matrix(_blobs(n, d, k, seed=6), d)
+    eng = LloydEngine(x, d, k, use_graph=False)
+    assert eng.x is x and getattr(x, "_cml_xnorm")[2] is eng.xnorm
+    assert cached_row_sqnorm(x, n, eng.dp) is eng.xnorm
+    c = x[:k, :d].double()
+    _, best0 = assign_gpu(x, eng.dp, d, c)
+    scale = float(eng.xnorm[:k].max().item())
+    assert float(best0[:k].abs().max().item()) <= 1e-5 * scale  # each of the first k rows is its own centre
+    x[0].mul_(2.0)  # in-place write: the cached norms must not be reused
+    xn = cached_row_sqnorm(x, n, eng.dp)
+    assert xn is not eng.xnorm
+    ref = x[:, :d].float().pow(2).sum(1)
+    torch.testing.assert_close(xn, ref, rtol=1e-5, atol=1e-3)
+    _, best1 = assign_gpu(x, eng.dp, d, c)
+    ref0 = (x[0, :d].double() - c).pow(2).sum(1).min().item()
+    assert abs(best1[0].item() - ref0) <= 1e-5 * 4 * scale + 1e-4 * ref0
+
+
 def test_invalidate_forces_full_step():
     n, d, k = 50_000, 64, 16
     x = _blobs(n, d, k, seed=5)

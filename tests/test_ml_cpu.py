@@ -170,6 +170,19 @@ def test_tree_perfect_split_and_spark_split_rule(spark):
     assert len(s) <= 31 and np.all(np.diff(s) > 0)
 
 
+def test_continuous_splits_match_value_walk():
+    """Binary-search split finding == Spark's value-by-value walk (kept as _continuous_splits_loop)."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.trees import (
+        _continuous_splits_loop, continuous_splits)
+    rs = np.random.RandomState(7)
+    cases = [np.repeat(np.arange(100.0), 3), rs.randn(10000), np.round(rs.exponential(3.0, 20000), 1),
+             rs.randint(0, 40, 5000).astype(float), np.concatenate([np.zeros(9000), rs.randn(1000)]),
+             rs.zipf(1.5, 8000).astype(float), np.array([1.0]), np.array([2.0, 2.0, 3.0])]
+    for v in cases:
+        for ns in (1, 3, 7, 31, 63, 127):
+            np.testing.assert_array_equal(continuous_splits(v, ns), _continuous_splits_loop(v, ns))
+
+
 def test_classifiers_on_hospital_binary_label(hosp):
     pdf, fd = hosp
     d = fd.withColumn("LOS_binary", F.when(F.col("length_of_stay") > 5.0, 1).otherwise(0))
