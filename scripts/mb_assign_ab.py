@@ -10,9 +10,15 @@ from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmean
 
 n = int(sys.argv[1]) if len(sys.argv) > 1 else 20_000_000
 variants = [int(v) for v in sys.argv[2].split(",")] if len(sys.argv) > 2 else [0, 6]
-x = bench.make_blobs(n, 256, 256, seed=1000, device=torch.device("cuda"))
-eng = LloydEngine(x, 256, 256, use_graph=False)
-eng.set_centers(x[:256].double().cpu().numpy())
+D = int(sys.argv[3]) if len(sys.argv) > 3 else 256
+KC = int(sys.argv[4]) if len(sys.argv) > 4 else 256
+FP8 = len(sys.argv) > 5 and sys.argv[5] == "fp8"
+x = bench.make_blobs(n, D, KC, seed=1000, device=torch.device("cuda"))
+if FP8:
+    x = x.to(torch.float8_e4m3fn)
+eng = LloydEngine(x, D, KC, use_graph=False)
+eng.set_centers(x[:KC].to(torch.float32).double().cpu().numpy())
+print(f"n={n} d={D} (padded {eng.dp}) k={KC} {'fp8' if FP8 else 'bf16'}", flush=True)
 eng.step()
 x0 = torch.as_strided(eng.x, (n, eng.dp), (0, 1))
 
@@ -51,5 +57,5 @@ for v in variants:
     for m in ("full", "compute"):
         ts = sorted(res[(v, m)])
         t = ts[len(ts) // 2]
-        print(f"variant {v} {m:8s}: median {t:.3f} ms (min {ts[0]:.3f}) -> {2 * n * 256 * 256 / t / 1e9:.0f} TF/s"
+        print(f"variant {v} {m:8s}: median {t:.3f} ms (min {ts[0]:.3f}) -> {2 * n * D * KC / t / 1e9:.0f} TF/s"
               f"  labels equal to variant {variants[0]}: {same}", flush=True)
