@@ -59,8 +59,10 @@ class KMeans(Estimator):
         self._defaultParamMap.pop("weightCol", None)
 
     def _fit(self, df):
-        if self.getOrDefault("distanceMeasure") != "euclidean":
-            raise NotImplementedError("only distanceMeasure='euclidean' runs on the MFMA kernels")
+        measure = self.getOrDefault("distanceMeasure")
+        if measure not in ("euclidean", "cosine"):
+            raise ValueError(f"distanceMeasure must be 'euclidean' or 'cosine', got {measure!r}")
+        spherical = measure == "cosine"
         if self.isSet("weightCol"):
             raise NotImplementedError("weighted KMeans is not supported yet")
         x = df._feature_matrix(self.getFeaturesCol())
@@ -68,20 +70,20 @@ class KMeans(Estimator):
         k = self.getK()
         comm = df._comm
         seed = int(self.getSeed())
-        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids)
+        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical)
         conf = df._session.conf
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
         ckkey = (f"kmeans|n={n_global}|d={d}|k={k}|seed={seed}|init={self.getInitMode()}|"
-                 f"steps={self.getInitSteps()}|tol={self.getTol()}")
+                 f"steps={self.getInitSteps()}|tol={self.getTol()}|measure={measure}")
         resumed = ckpt.load(ckdir, f"kmeans-{self.uid}", ckkey) if ckdir else None
         start = 0
         if resumed is not None:
             start, arrs = resumed
             init = arrs["centers"]
             if init.shape[0] < k:
-                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids)
+                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical)
         elif self.getInitMode() == "random":
             with trace("kmeans.init"):
                 init = eng.init_random(seed)
@@ -91,7 +93,7 @@ class KMeans(Estimator):
             k_eff = getattr(eng, "k_effective", k)
             if k_eff < k:
                 init = init[:k_eff]
-                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids)
+                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical)
         eng.set_centers(init)
 
         def on_iter(it):
@@ -129,19 +131,35 @@ class KMeansModel(Model):
     def numFeatures(self) -> int:
         return int(self._centers.shape[1])
 
+    def _cosine(self) -> bool:
+        return self.getOrDefault("distanceMeasure") == "cosine"
+
     def predict(self, value) -> int:
         v = as_array(value)
+        if self._cosine():  # CosineDistanceMeasure: 1 - cos, centres are unit length
+            nv = np.linalg.norm(v)
+            if nv == 0:
+                raise ValueError("Cosine distance is not defined for zero-length vectors.")
+            return int((1.0 - self._centers @ v / nv).argmin())
         return int(((self._centers - v) ** 2).sum(1).argmin())
 
     def _assign(self, df):
+        """(labels, distance) per local row: squared euclidean, or 1 - cos for distanceMeasure="cosine"
+        (unit rows against the unit centres: ||x - c||² / 2)."""
         x = df._feature_matrix(self.getFeaturesCol())
         c = torch.as_tensor(self._centers, device=x.device)
+        cos = self._cosine()
         if x.is_cuda:
-            from ..models.kmeans import assign_gpu, to_device_matrix
-            xm = to_device_matrix(x, x.shape[1])
+            from ..models.kmeans import assign_gpu, to_device_matrix, unit_rows
+            xm = to_device_matrix(unit_rows(x) if cos else x, x.shape[1])
             lab, dist = assign_gpu(xm, xm.shape[1], x.shape[1], c)
-            return lab.long(), dist.to(torch.float64)
+            dist = dist.to(torch.float64)
+            return lab.long(), (dist / 2.0 if cos else dist)
         from ..ops.kmeans_ops import assign_reference
+        if cos:
+            from ..models.kmeans import unit_rows
+            lab, dist = assign_reference(unit_rows(x), c)
+            return lab, dist / 2.0
         return assign_reference(x, c)
 
     def _transform(self, df):

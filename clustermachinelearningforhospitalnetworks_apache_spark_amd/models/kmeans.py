@@ -65,6 +65,24 @@ def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
     return out
 
 
+def unit_rows(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
+    """Rows scaled to unit length (cosine KMeans). Computed in f32 chunks on the rows' device; bf16 on
+    the GPU (fp8 inputs widen to bf16: unit components need more than e4m3's 3 mantissa bits), f64 on
+    the CPU. Spark rejects zero-length vectors for the cosine measure, and so does this."""
+    d = x.shape[1] if d is None else d
+    out_dtype = torch.bfloat16 if x.is_cuda else torch.float64
+    work = torch.float32 if x.is_cuda else torch.float64
+    out = torch.empty((x.shape[0], d), dtype=out_dtype, device=x.device)
+    step = 1 << 22
+    for s in range(0, x.shape[0], step):
+        v = x[s:s + step, :d].to(work)
+        nrm = v.norm(dim=1, keepdim=True)
+        if bool((nrm == 0).any()):
+            raise ValueError("Cosine distance is not defined for zero-length vectors.")
+        out[s:s + step] = (v / nrm).to(out_dtype)
+    return out
+
+
 def cached_row_sqnorm(x: torch.Tensor, n: int, dp: int) -> torch.Tensor:
     """||x_i||² of the device matrix's rows, kept on the tensor itself while it is unmodified.
 
@@ -89,8 +107,15 @@ class LloydEngine:
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
-                 incremental: Optional[bool] = None):
+                 incremental: Optional[bool] = None, spherical: bool = False):
         self.comm = comm or local_comm()
+        # spherical = Spark's distanceMeasure="cosine": rows are scaled to unit length once, centres
+        # are renormalised after every update (CosineDistanceMeasure.centroid), and on unit vectors
+        # ||x - c||² = 2·(1 - cos), so the euclidean K9/K10 path computes the cosine assignment;
+        # costs and the convergence test are converted back (cost / 2, shift² <= 2·tol).
+        self.spherical = bool(spherical)
+        if self.spherical:
+            x = unit_rows(x, d)
         self._accum_mode = accum_mode
         self._incremental = True if incremental is None else bool(incremental)
         # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
@@ -160,6 +185,7 @@ class LloydEngine:
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         self.shift2 = torch.zeros(k, dtype=torch.float64, device=dev)
+        self._prev_centers = torch.zeros((k, d), dtype=torch.float64, device=dev) if self.spherical else None
 
     @property
     def global_n(self) -> int:
@@ -251,8 +277,14 @@ class LloydEngine:
         for h in handles:
             h.wait()
         self.last_cost = self.msgs[:, -1].sum()
+        if self.spherical:
+            self._prev_centers.copy_(self.centers)
         K.update_centers(self.msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
                          self.shift2)
+        if self.spherical:  # unit-length centres (empty clusters keep their old, already unit, centre)
+            self.centers.div_(self.centers.norm(dim=1, keepdim=True).clamp_(min=1e-300))
+            torch.sum((self.centers - self._prev_centers) ** 2, dim=1, out=self.shift2)
+            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
         self._shift2 = self.shift2
 
     def _step_cpu(self):
@@ -264,6 +296,8 @@ class LloydEngine:
         sums = msg[:kd].reshape(self.k, self.d)
         counts = msg[kd:kd + self.k]
         new = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], self.centers)
+        if self.spherical:
+            new = torch.where(counts[:, None] > 0, new / new.norm(dim=1, keepdim=True).clamp(min=1e-300), new)
         self._shift2 = ((new - self.centers) ** 2).sum(1)
         self.centers = new
         self.last_cost = msg[-1]
@@ -273,7 +307,8 @@ class LloydEngine:
         """Spark's rule: converged iff every centre moved at most tol (euclidean)."""
         if self._shift2 is None:
             return False
-        return bool((self._shift2 <= tol * tol).all().item())
+        lim = 2.0 * tol if self.spherical else tol * tol  # cosine: 1 - cos = ||a - b||² / 2 on unit vectors
+        return bool((self._shift2 <= lim).all().item())
 
     def fit(self, max_iter: int, tol: float, start_iter: int = 0, on_iter=None) -> int:
         """Lloyd iterations until every centre moves <= tol or max_iter. ``start_iter`` resumes a
@@ -300,7 +335,11 @@ class LloydEngine:
         return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers, self.xnorm)
 
     def training_cost(self) -> float:
-        return float(self.last_cost.item()) if self.last_cost is not None else float("nan")
+        """Spark's trainingCost: sum of squared distances, or of cosine distances (spherical)."""
+        if self.last_cost is None:
+            return float("nan")
+        c = float(self.last_cost.item())
+        return c / 2.0 if self.spherical else c
 
     # ------------------------------------------------------------------ initialisation
     def init_random(self, seed: int) -> np.ndarray:
@@ -385,9 +424,10 @@ class LloydEngine:
                 w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)
             if self.gpu:  # the host BLAS is the slow part of init on a busy CPU; same draws on the device
-                out = local_kmeans_pp_device(torch.as_tensor(cand_np, device=self.device), w, k, seed, max_iter=30)
+                out = local_kmeans_pp_device(torch.as_tensor(cand_np, device=self.device), w, k, seed, max_iter=30,
+                                             spherical=self.spherical)
             else:
-                out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30)
+                out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30, spherical=self.spherical)
             if self.comm.is_distributed:
                 # every rank ran the same local k-means on the same candidates and weights; rank 0's
                 # result is taken verbatim so last-bit differences of device reductions cannot make
@@ -424,8 +464,10 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: O
     return labels[:n], best[:n]
 
 
-def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, max_iter: int = 30) -> np.ndarray:
-    """Weighted k-means++ seeding + weighted Lloyd on the candidate set (host, float64)."""
+def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, max_iter: int = 30,
+                    spherical: bool = False) -> np.ndarray:
+    """Weighted k-means++ seeding + weighted Lloyd on the candidate set (host, float64).
+    ``spherical``: unit-length candidates, centres renormalised after every mean (cosine KMeans)."""
     rs = np.random.RandomState(seed & 0x7FFFFFFF)
     n = points.shape[0]
     w = np.maximum(weights.astype(np.float64), 0)
@@ -451,6 +493,8 @@ def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, 
         wsum = np.bincount(lab, weights=w, minlength=k)
         cnt = np.bincount(lab, minlength=k)
         new = sums / np.maximum(wsum, 1e-300)[:, None]
+        if spherical:
+            new = new / np.maximum(np.linalg.norm(new, axis=1), 1e-300)[:, None]
         for j in np.flatnonzero(cnt == 0):  # empty clusters re-seed in index order (same draws as before)
             new[j] = points[rs.randint(n)]
         moved = not np.isclose(new, centers).all()
@@ -461,7 +505,7 @@ def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, 
 
 
 def local_kmeans_pp_device(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
-                           max_iter: int = 30) -> np.ndarray:
+                           max_iter: int = 30, spherical: bool = False) -> np.ndarray:
     """local_kmeans_pp with the float64 arithmetic on ``points.device``: the RandomState draws are
     the same calls in the same order (each D²-weighted pick copies only its n probabilities to the
     host for ``RandomState.choice``), so it picks what the host version picks up to last-bit
@@ -491,6 +535,8 @@ def local_kmeans_pp_device(points: torch.Tensor, weights: torch.Tensor, k: int, 
         wsum = torch.zeros(k, dtype=torch.float64, device=pts.device).index_add_(0, lab, w)
         cnt = torch.bincount(lab, minlength=k)
         new = sums / wsum.clamp(min=1e-300)[:, None]
+        if spherical:
+            new = new / new.norm(dim=1).clamp(min=1e-300)[:, None]
         for j in np.flatnonzero(cnt.cpu().numpy() == 0):
             new[j] = pts[int(rs.randint(n))]
         moved = not bool(torch.isclose(new, centers).all())

@@ -69,3 +69,88 @@ def test_local_kmeans_pp_device_variant_matches_host():
     a = local_kmeans_pp(pts, w, 9, seed=11)
     b = local_kmeans_pp_device(torch.as_tensor(pts), torch.as_tensor(w), 9, seed=11)
     np.testing.assert_allclose(a, b, rtol=1e-12, atol=1e-12)
+
+
+def numpy_spherical_lloyd(x, c, iters):
+    """Spark CosineDistanceMeasure Lloyd: argmax cos, centre = normalised mean of the unit rows."""
+    u = x / np.linalg.norm(x, axis=1, keepdims=True)
+    for _ in range(iters):
+        lab = (u @ c.T).argmax(1)
+        new = c.copy()
+        for j in range(c.shape[0]):
+            m = lab == j
+            if m.any():
+                s = u[m].sum(0)
+                new[j] = s / np.linalg.norm(s)
+        c = new
+    return c, (1.0 - (u * c[lab]).sum(1)).sum()
+
+
+def _directions(n, d, k, seed):
+    rs = np.random.RandomState(seed)
+    dirs = rs.randn(k, d)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    x = dirs[rs.randint(0, k, n)] + 0.15 * rs.randn(n, d)
+    return x * rs.uniform(0.1, 50.0, (n, 1))  # magnitudes must not matter under the cosine measure
+
+
+def test_spherical_engine_matches_numpy():
+    x = _directions(3000, 6, 5, seed=4)
+    u = x / np.linalg.norm(x, axis=1, keepdims=True)
+    init = u[:5].copy()
+    eng = LloydEngine(torch.as_tensor(x), 6, 5, spherical=True)
+    eng.set_centers(init)
+    for _ in range(6):
+        eng.step()
+    ref_c, _ = numpy_spherical_lloyd(x, init, 6)
+    np.testing.assert_allclose(eng.centers.numpy(), ref_c, rtol=1e-10, atol=1e-10)
+    np.testing.assert_allclose(np.linalg.norm(eng.centers.numpy(), axis=1), 1.0, rtol=1e-12)
+    # the reported cost is the cost of the assignment made in the last step (against the step's input centres)
+    prev_c, _ = numpy_spherical_lloyd(x, init, 5)
+    lab = (u @ prev_c.T).argmax(1)
+    np.testing.assert_allclose(eng.training_cost(), (1.0 - (u * prev_c[lab]).sum(1)).sum(), rtol=1e-9)
+
+
+def test_cosine_kmeans_estimator_scale_invariant():
+    import pandas as pd
+    from helpers import session
+    spark = session()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans, KMeansModel
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler
+    x = _directions(2000, 4, 3, seed=5)
+    cols = [f"f{i}" for i in range(4)]
+    rs = np.random.RandomState(9)
+    scaled = x * rs.uniform(0.5, 4.0, (x.shape[0], 1))
+    models = []
+    for data in (x, scaled):
+        df = VectorAssembler(inputCols=cols, outputCol="features").transform(
+            spark.createDataFrame(pd.DataFrame(data, columns=cols)))
+        m = KMeans(k=3, seed=1, distanceMeasure="cosine", maxIter=30).fit(df)
+        pred = np.asarray(m.transform(df).select("prediction").toPandas()["prediction"])
+        models.append((m, pred, df))
+    (m0, p0, df0), (m1, p1, _) = models
+    np.testing.assert_array_equal(p0, p1)
+    np.testing.assert_allclose(np.stack(m0.clusterCenters()), np.stack(m1.clusterCenters()), atol=1e-9)
+    c = np.stack(m0.clusterCenters())
+    np.testing.assert_allclose(np.linalg.norm(c, axis=1), 1.0, rtol=1e-9)
+    u = x / np.linalg.norm(x, axis=1, keepdims=True)
+    np.testing.assert_array_equal(p0, (u @ c.T).argmax(1))
+    cost = (1.0 - (u * c[p0]).sum(1)).sum()
+    np.testing.assert_allclose(m0.computeCost(df0), cost, rtol=1e-9)
+    assert m0.predict(x[0] * 7.0) == p0[0]
+    assert m0.summary.trainingCost >= 0
+    # the measure travels with the saved model
+    import tempfile
+    with tempfile.TemporaryDirectory() as d:
+        m0.write().overwrite().save(d + "/m")
+        m2 = KMeansModel.load(d + "/m")
+        assert m2.getOrDefault("distanceMeasure") == "cosine"
+        np.testing.assert_array_equal(np.asarray(m2.transform(df0).select("prediction").toPandas()["prediction"]), p0)
+
+
+def test_cosine_rejects_zero_rows():
+    import pytest
+    x = np.ones((10, 3))
+    x[4] = 0.0
+    with pytest.raises(ValueError, match="zero-length"):
+        LloydEngine(torch.as_tensor(x), 3, 2, spherical=True)

@@ -129,3 +129,29 @@ def test_invalidate_forces_full_step():
     eng.step()
     torch.cuda.synchronize()
     assert eng.delta.was_full()
+
+
+def test_spherical_gpu_matches_cpu_engine():
+    """distanceMeasure="cosine" on the MFMA path: unit bf16 rows, renormalised centres, vs the f64 CPU engine."""
+    n, d, k = 60_000, 96, 24
+    rs = np.random.RandomState(11)
+    dirs = rs.randn(k, d)
+    dirs /= np.linalg.norm(dirs, axis=1, keepdims=True)
+    x = (dirs[rs.randint(0, k, n)] + 0.2 * rs.randn(n, d)) * rs.uniform(0.2, 30.0, (n, 1))
+    u = x / np.linalg.norm(x, axis=1, keepdims=True)
+    init = u[:k].copy()
+    cpu = LloydEngine(torch.as_tensor(x), d, k, spherical=True)
+    cpu.set_centers(init)
+    gpu = LloydEngine(torch.as_tensor(x, dtype=torch.float32, device="cuda"), d, k, spherical=True)
+    gpu.set_centers(init)
+    for _ in range(8):
+        cpu.step()
+        gpu.step()
+    torch.cuda.synchronize()
+    cg = gpu.centers.cpu().numpy()
+    np.testing.assert_allclose(np.linalg.norm(cg, axis=1), 1.0, rtol=1e-12)
+    np.testing.assert_allclose(cg, cpu.centers.numpy(), atol=1e-2)  # bf16 unit rows vs f64 (2^-9 relative per element)
+    lab_g = gpu.labels[:n].long().cpu().numpy()
+    assert (lab_g == cpu.labels.numpy()).mean() > 0.995
+    assert abs(gpu.training_cost() - cpu.training_cost()) <= 2e-2 * cpu.training_cost()
+    assert gpu.delta is not None and gpu.converged(1.0)
