@@ -766,10 +766,14 @@ template <int CPL> struct SegRaw<CPL, true> { using T = typename RawCols8<CPL>::
 // in earlier slices) goes to slot A[w], its last (may continue in later slices) to slot B[w];
 // kmeans_seg_fixup adds the slots in ascending wave order. The result is bitwise identical
 // run to run (SURVEY.md §5.2 deterministic-reduction mode, here the only mode).
+__device__ __forceinline__ long long seg_chunk(long long filled, long long waves) {
+  return (filled + waves - 1) / waves;
+}
+
 template <int CPL, bool F8>
 __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
-                                                             const int* __restrict__ seg, int k, long long chunk,
+                                                             const int* __restrict__ seg, int k,
                                                              double* __restrict__ msg, double* __restrict__ slots,
                                                              int* __restrict__ slot_c, const int* __restrict__ gate,
                                                              int want) {
@@ -780,8 +784,11 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
   constexpr int ESZ = F8 ? 1 : 2;  // bytes per element
   const int lane = threadIdx.x & 63;
   const long long wave = (long long)blockIdx.x * (kSegThreads / 64) + (threadIdx.x >> 6);
+  // slices follow the positions actually filled (seg[k], on the device): a delta list is bounded by
+  // 2·cap on the host but usually holds far fewer entries, which must still spread over every wave
+  n = n < (long long)seg[k] ? n : (long long)seg[k];
+  const long long chunk = seg_chunk(n, (long long)gridDim.x * (kSegThreads / 64));
   const long long p0 = wave * chunk;
-  n = n < (long long)seg[k] ? n : (long long)seg[k];  // sorted positions actually filled (delta lists: <= bound)
   if (p0 >= n) {
     if (lane == 0) {
       slot_c[2 * wave] = -1;
@@ -878,7 +885,7 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
 
 // msg[c] += Σ over the slices overlapping cluster c, in ascending slice order, of their head
 // (A) / tail (B) partials for c. One workgroup per cluster.
-__global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long chunk,
+__global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long n,
                                                         long long nwaves, const double* __restrict__ slots,
                                                         const int* __restrict__ slot_c, double* __restrict__ msg,
                                                         const int* __restrict__ gate, int want) {
@@ -886,6 +893,7 @@ __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ 
   const int c = blockIdx.x;
   const long long s0 = seg[c], s1 = seg[c + 1];
   if (s1 <= s0) return;
+  const long long chunk = seg_chunk(n < (long long)seg[k] ? n : (long long)seg[k], nwaves);  // as kmeans_segacc
   const long long w0 = s0 / chunk;
   long long w1 = (s1 - 1) / chunk;
   if (w1 >= nwaves) w1 = nwaves - 1;
@@ -1200,10 +1208,9 @@ int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, cons
                   int cpl, int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate, int want,
                   hipStream_t st) {
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
-  const long long chunk = (n + waves - 1) / waves;
 #define CML_SEG(C, F)                                                                                              \
   hipLaunchKernelGGL((kmeans_segacc<C, F>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm, seg, \
-                     k, chunk, msg, slots, slot_c, gate, want)
+                     k, msg, slots, slot_c, gate, want)
   if (xfp8) {
     if (cpl == 4) CML_SEG(4, true);
     else if (cpl == 8) CML_SEG(8, true);
@@ -1216,7 +1223,7 @@ int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, cons
 #undef CML_SEG
   const int e = cml_status();
   if (e) return e;
-  hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, chunk, waves, slots, slot_c, msg, gate,
+  hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, n, waves, slots, slot_c, msg, gate,
                      want);
   return cml_status();
 }

@@ -18,7 +18,7 @@ Per iteration on each rank (E5 in SURVEY.md §3):
 Incremental sums (default on the sort regime): the per-cluster sums of the current labels are kept
 across steps; a step re-reads only the rows whose label changed (new sums = old + moved in − moved
 out, exact in f64 for bf16/fp8 rows), falling back to the full accumulate on the first step and
-whenever more than 1/16 of the rows changed. Every step still assigns every row against every centre.
+whenever more than 1/4 of the rows changed (CML_KMEANS_DELTA_CAP). Every step still assigns every row against every centre.
 
 CPU tensors run the same algorithm with torch float64 ops (``local[n]`` mode and
 the numerical oracle).

@@ -7,6 +7,8 @@ numerical oracle of the tests).
 """
 from __future__ import annotations
 
+import os
+
 from dataclasses import dataclass
 
 import torch
@@ -253,8 +255,10 @@ class DeltaState:
     by ``invalidate()``."""
 
     def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, nblk: int,
-                 fp8: bool = False, cap_fraction: float = 1.0 / 16):
+                 fp8: bool = False, cap_fraction: float | None = None):
         self.k, self.d, self.nblk = k, d, int(nblk)
+        if cap_fraction is None:  # steps with more label changes than this re-accumulate in full
+            cap_fraction = float(os.environ.get("CML_KMEANS_DELTA_CAP", 0.25))
         self.cap = max(1024, int(n * cap_fraction))
         # change lists are per assign workgroup: nblk lists of pcap entries (slack for uneven churn)
         self.pcap = max(64, -(-2 * self.cap // self.nblk))
