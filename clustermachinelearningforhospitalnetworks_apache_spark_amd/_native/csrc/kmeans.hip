@@ -156,6 +156,33 @@ __device__ __forceinline__ void slot_update(const f32x4 (&acc)[RT], int t, int i
   key[t][i] = k < key[t][i] ? k : key[t][i];
 }
 
+// PACK4: the 4 slots of sub-tile t hold the SAME X row against centres 4g+i, so they merge into
+// ONE key per row whose low bits carry (tile, i): 4 v_and_or + 2 v_min3_i32 per 4 distances
+// instead of 4 + 4 (and 4x fewer key registers). Two more mantissa bits are truncated
+// (2^-17 relative for k = 256).
+template <int RT>
+__device__ __forceinline__ void group_update(const f32x4 (&acc)[RT], int t, int ct4, int cmask, int (&key)[RT][4]) {
+  const int k0 = (__float_as_int(acc[t][0]) & ~cmask) | ct4;
+  const int k1 = (__float_as_int(acc[t][1]) & ~cmask) | (ct4 + 1);
+  const int k2 = (__float_as_int(acc[t][2]) & ~cmask) | (ct4 + 2);
+  const int k3 = (__float_as_int(acc[t][3]) & ~cmask) | (ct4 + 3);
+  int m = key[t][0];
+  m = min(m, min(k0, k1));
+  m = min(m, min(k2, k3));
+  key[t][0] = m;
+}
+
+template <int RT, bool PACK4>
+__device__ __forceinline__ void tile_update_all(const f32x4 (&acc)[RT], int ct, int cmask, int (&key)[RT][4]) {
+  if constexpr (PACK4) {
+#pragma unroll
+    for (int t = 0; t < RT; ++t) group_update<RT>(acc, t, ct << 2, cmask, key);
+  } else {
+#pragma unroll
+    for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc, q >> 2, q & 3, ct, cmask, key);
+  }
+}
+
 // MFMA chain of centre tile `ct` for all RT sub-tiles into `acc` (each A fragment feeds RT
 // MFMAs), with the slot updates of the previous tile's accumulators interleaved. The first k-step
 // of every sub-tile takes its C operand from ONE register set, cinit = ||c||² + moff, where moff
@@ -170,7 +197,7 @@ __device__ __forceinline__ void slot_update(const f32x4 (&acc)[RT], int t, int i
 // SHARED = false keeps the per-sub-tile seeding (c4 + ||x||² of each row) — the A/B reference of
 // kmeans_ops.set_assign_variant(6); in one process it measured 2.77 vs 2.71 ms full and 2.15 vs
 // 2.07 ms compute-only (profiles/assign_shared_seed_ab_20Mx256.log).
-template <int DP, int RT, int RING, bool PREV, bool SHARED>
+template <int DP, int RT, int RING, bool PREV, bool SHARED, bool PACK4>
 __device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& xt, float moff,
                                       const float (&xn)[RT], int ct, int g, f32x4 (&acc)[RT],
                                       const f32x4 (&prev)[RT], uint4 (&ring)[RING], int (&key)[RT][4]) {
@@ -190,7 +217,10 @@ __device__ __forceinline__ void chain(const AssignCtx& cx, const XTile<DP, RT>& 
     for (int t = 0; t < RT; ++t)
       acc[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(__builtin_bit_cast(bf16x8, a), xt.f[t][s],
                                                        (SHARED && s == 0) ? cinit : acc[t], 0, 0, 0);
-    if constexpr (PREV) {
+    if constexpr (PREV && PACK4) {
+#pragma unroll
+      for (int t = (s * RT) / KS; t < ((s + 1) * RT) / KS; ++t) group_update<RT>(prev, t, (ct - 1) << 2, cx.cmask, key);
+    } else if constexpr (PREV) {
 #pragma unroll
       for (int q = (s * NSLOT) / KS; q < ((s + 1) * NSLOT) / KS; ++q)
         slot_update<RT>(prev, q >> 2, q & 3, ct - 1, cx.cmask, key);
@@ -212,7 +242,7 @@ struct DeltaOut {
   int* lds_count;  // set in the kernel
 };
 
-template <int DP, int RT, int RINGMAX, bool SHARED>
+template <int DP, int RT, int RINGMAX, bool SHARED, bool PACK4>
 __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP, RT>& xt, long long tile,
                                             long long n, int r, int g, int c_base, const float* __restrict__ xnorm,
                                             int* __restrict__ labels, float* __restrict__ best_io, int first,
@@ -238,30 +268,34 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
   for (int q = 0; q < RING; ++q) ring[q] = frag_at<DP>(cx, q / KS, q % KS);
   f32x4 acc0[RT], acc1[RT];
   const int nct = cx.nct;
-  chain<DP, RT, RING, false, SHARED>(cx, xt, moff, xn, 0, g, acc0, acc1, ring, key);
+  chain<DP, RT, RING, false, SHARED, PACK4>(cx, xt, moff, xn, 0, g, acc0, acc1, ring, key);
   int ct = 1;
   for (; ct + 1 < nct; ct += 2) {
-    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
-    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct + 1, g, acc0, acc1, ring, key);
+    chain<DP, RT, RING, true, SHARED, PACK4>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
+    chain<DP, RT, RING, true, SHARED, PACK4>(cx, xt, moff, xn, ct + 1, g, acc0, acc1, ring, key);
   }
   if (ct < nct) {
-    chain<DP, RT, RING, true, SHARED>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
-#pragma unroll
-    for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc1, q >> 2, q & 3, ct, cx.cmask, key);
+    chain<DP, RT, RING, true, SHARED, PACK4>(cx, xt, moff, xn, ct, g, acc1, acc0, ring, key);
+    tile_update_all<RT, PACK4>(acc1, ct, cx.cmask, key);
   } else {
-#pragma unroll
-    for (int q = 0; q < RT * 4; ++q) slot_update<RT>(acc0, q >> 2, q & 3, ct - 1, cx.cmask, key);
+    tile_update_all<RT, PACK4>(acc0, ct - 1, cx.cmask, key);
   }
 #pragma unroll
   for (int t = 0; t < RT; ++t) {
     // slot (t,i) holding tile c is centre 16c + 4g + i
     float best = __int_as_float(key[t][0] & ~cx.cmask);
-    int bidx = (key[t][0] & cx.cmask) * 16 + 4 * g;
+    int bidx;
+    if constexpr (PACK4) {
+      const int tag = key[t][0] & cx.cmask;  // (tile << 2) | i: centre 16 tile + 4g + i
+      bidx = (tag >> 2) * 16 + 4 * g + (tag & 3);
+    } else {
+      bidx = (key[t][0] & cx.cmask) * 16 + 4 * g;
 #pragma unroll
-    for (int i = 1; i < 4; ++i) {
-      const float v = __int_as_float(key[t][i] & ~cx.cmask);
-      const int idx = (key[t][i] & cx.cmask) * 16 + 4 * g + i;
-      if (v < best || (v == best && idx < bidx)) { best = v; bidx = idx; }
+      for (int i = 1; i < 4; ++i) {
+        const float v = __int_as_float(key[t][i] & ~cx.cmask);
+        const int idx = (key[t][i] & cx.cmask) * 16 + 4 * g + i;
+        if (v < best || (v == best && idx < bidx)) { best = v; bidx = idx; }
+      }
     }
 #pragma unroll
     for (int o = 16; o <= 32; o <<= 1) {
@@ -312,7 +346,7 @@ __device__ __forceinline__ void assign_tile(const AssignCtx& cx, const XTile<DP,
 
 // NT threads; each wave owns super-tiles of RT x 16 rows. PF: the next super-tile's rows are in
 // flight while this one computes (double-buffered X registers).
-template <int DP, int RT, int NT, bool PF, int RINGMAX, bool F8, bool SHARED = true>
+template <int DP, int RT, int NT, bool PF, int RINGMAX, bool F8, bool SHARED = true, bool PACK4 = false>
 __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     const void* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc,
     int kc, int kp, int c_base, const float* __restrict__ cnorm, const float* __restrict__ xnorm,
@@ -367,6 +401,7 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   cx.nct = nct;
   int bits = 1;
   while ((1 << bits) < nct) ++bits;
+  if (PACK4) bits += 2;
   cx.cmask = (1 << bits) - 1;
 
   long long tile = (long long)blockIdx.x * nwaves + wave;
@@ -384,18 +419,18 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
     for (; tile < ntiles; tile += 2 * tw) {
       const long long t1 = tile + tw;
       if (t1 < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1, r, g, xb);
-      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED, PACK4>(cx, xa, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
       if (t1 >= ntiles) break;
       if (t1 + tw < ntiles) load_xtile<DP, RT, F8>(X, n, ldx, t1 + tw, r, g, xa);
-      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED, PACK4>(cx, xb, t1, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
     }
   } else {
     for (; tile < ntiles; tile += tw) {
       XTile<DP, RT> xt;
       load_xtile<DP, RT, F8>(X, n, ldx, tile, r, g, xt);
-      assign_tile<DP, RT, RINGMAX, SHARED>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
+      assign_tile<DP, RT, RINGMAX, SHARED, PACK4>(cx, xt, tile, n, r, g, c_base, xnorm, labels, best_io, first, last, ranking, hist,
                           rank_out, dout, cost);
     }
   }
@@ -1141,6 +1176,11 @@ const void* assign_kernel_ptr() {
         return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8, false>;
       else
         return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8, false>;
+    case 7:  // the default launch with the PACK4 per-row key (4 slots merged by v_min3)
+      if constexpr (DP >= 256)
+        return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8, true, true>;
+      else
+        return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8, true, true>;
     default:
       if constexpr (DP >= 256) return (const void*)kmeans_assign_bf16<DP, RT_BIG, 512, false, DP >= 512 ? 4 : 2, F8>;
       else return (const void*)kmeans_assign_bf16<DP, 1, 512, PF, 4, F8>;
@@ -1157,6 +1197,7 @@ inline int assign_tile_rows(int Dp) {
     case 4: return 32;
     case 5: return 16;
     case 6: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
+    case 7: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
     default: return Dp >= 512 ? 32 : (Dp >= 256 ? 64 : 16);
   }
 }
@@ -1259,7 +1300,7 @@ CML_API int cml_kmeans_set_assign_sched(int v) {
   return 0;
 }
 CML_API int cml_kmeans_set_assign_variant(int v) {
-  if (v < 0 || v > 6) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 7) return (int)hipErrorInvalidValue;
   g_assign_variant = v;
   return 0;
 }
