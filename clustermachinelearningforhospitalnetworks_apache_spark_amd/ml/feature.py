@@ -425,3 +425,211 @@ class IndexToString(Transformer):
         vals = cd.values.cpu().numpy()
         out = np.array([labels[int(v)] if 0 <= int(v) < len(labels) else None for v in vals], dtype=object)
         return _replace_col(df, self.getOutputCol(), ColumnData(out, None, T.StringType()))
+
+
+def _in_out_cols(inst) -> tuple:
+    """(inputCols, outputCols) from either the single- or the multi-column params."""
+    if inst.isSet("inputCols"):
+        ins = list(inst.getInputCols())
+        outs = list(inst.getOrDefault("outputCols")) if inst.isSet("outputCols") else [c + "_out" for c in ins]
+    else:
+        ins = [inst.getInputCol()]
+        outs = [inst.getOutputCol()]
+    if len(ins) != len(outs):
+        raise ValueError(f"{type(inst).__name__}: inputCols and outputCols differ in length")
+    return ins, outs
+
+
+class OneHotEncoder(Estimator):
+    """Category indices (e.g. StringIndexer output for ``hospital_id``, the column the reference
+    imports StringIndexer for but never encodes, ref.py:29) -> one-hot vectors. Spark semantics:
+    ``dropLast`` drops the last category's slot (it becomes all-zero), ``handleInvalid='keep'`` adds a
+    slot for indices outside [0, numCategories). The vector column is a dense [n, size] device tensor
+    (Spark emits sparse vectors; the values are the same). numCategories = max index + 1 over all
+    ranks (one all-reduce)."""
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "inputCols": (NO_DEFAULT, "input column names", "liststr"),
+        "outputCols": (NO_DEFAULT, "output column names", "liststr"),
+        "dropLast": (True, "whether to drop the last category", bool),
+        "handleInvalid": ("error", "how to handle invalid data: 'error' or 'keep'", str),
+    }
+
+    def __init__(self, inputCols=None, outputCols=None, handleInvalid=None, dropLast=None, inputCol=None,
+                 outputCol=None):
+        super().__init__(inputCols=inputCols, outputCols=outputCols, handleInvalid=handleInvalid, dropLast=dropLast,
+                         inputCol=inputCol, outputCol=outputCol)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _fit(self, df):
+        ins, _ = _in_out_cols(self)
+        maxes = []
+        for c in ins:
+            cd = df._column_data(c)
+            v = torch.as_tensor(cd.values).to(torch.float64)
+            vm = torch.as_tensor(cd.valid_mask(), device=v.device)
+            v = v[vm & ~torch.isnan(v)] if v.numel() else v
+            if v.numel() and (bool((v < 0).any()) or bool((v != torch.floor(v)).any())) \
+                    and self.getHandleInvalid() == "error":
+                raise ValueError(f"OneHotEncoder: column {c} holds values that are not category indices")
+            maxes.append(float(v.max()) if v.numel() else -1.0)
+        t = torch.as_tensor(maxes, dtype=torch.float64, device=df._device)
+        df._comm.allreduce_(t, "max")
+        m = OneHotEncoderModel([int(x) + 1 for x in t.cpu().tolist()])
+        self._copyValues(m)
+        return m
+
+
+class OneHotEncoderModel(Model):
+    _params = OneHotEncoder._params
+
+    def __init__(self, categorySizes: Optional[List[int]] = None):
+        super().__init__()
+        self.categorySizes = list(categorySizes or [])
+
+    def _transform(self, df):
+        ins, outs = _in_out_cols(self)
+        keep = self.getHandleInvalid() == "keep"
+        drop = bool(self.getDropLast())
+        for c, o, nc in zip(ins, outs, self.categorySizes):
+            cd = df._column_data(c)
+            v = torch.as_tensor(cd.values).to(torch.float64)
+            valid = torch.as_tensor(cd.valid_mask(), device=v.device)
+            size = nc + (1 if keep else 0) - (1 if drop else 0)
+            bad = ~valid | torch.isnan(v) | (v < 0) | (v >= nc) | (v != torch.floor(v))
+            if bool(bad.any()) and not keep:
+                raise ValueError(f"OneHotEncoder: invalid category index in column {c} "
+                                 "(set handleInvalid='keep' to map it to an extra slot)")
+            idx = torch.where(bad, torch.full_like(v, nc), v).to(torch.int64)  # 'keep' slot = nc
+            out = torch.zeros((v.shape[0], max(size, 0)), dtype=torch.float64, device=v.device)
+            hit = idx < size  # the dropped last slot leaves the row all-zero
+            if size > 0 and bool(hit.any()):
+                rows = torch.nonzero(hit).squeeze(1)
+                out[rows, idx[rows]] = 1.0
+            df = _replace_col(df, o, ColumnData(out, None, T.VectorUDT()))
+        return df
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        U.write_parquet(path, "data", pa.table({"categorySizes": pa.array([self.categorySizes],
+                                                                          type=pa.list_(pa.int32()))}))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(row["categorySizes"])
+        U.apply_params(m, md)
+        return m
+
+
+class Imputer(Estimator):
+    """Fills missing values (null, and ``missingValue`` — NaN by default) per column with the
+    column's mean, median or mode over all ranks (Spark's Imputer). The reference drops every
+    row with a null instead (``na.drop``, ref.py:128); this keeps them. mean: one f64 all-reduce
+    of (sum, count); median / mode: exact, from the all-gathered non-missing values (Spark's median
+    is approxQuantile with relativeError 0.001 — exact is within that bound)."""
+    _params = {
+        "inputCol": (NO_DEFAULT, "input column name", str),
+        "outputCol": ("__auto__", "output column name", str),
+        "inputCols": (NO_DEFAULT, "input column names", "liststr"),
+        "outputCols": (NO_DEFAULT, "output column names", "liststr"),
+        "strategy": ("mean", "strategy for imputation: mean, median or mode", str),
+        "missingValue": (float("nan"), "placeholder for the missing values", float),
+        "relativeError": (0.001, "relative error for approximate quantile computation", float),
+    }
+
+    def __init__(self, strategy=None, missingValue=None, inputCols=None, outputCols=None, inputCol=None,
+                 outputCol=None, relativeError=None):
+        super().__init__(strategy=strategy, missingValue=missingValue, inputCols=inputCols, outputCols=outputCols,
+                         inputCol=inputCol, outputCol=outputCol, relativeError=relativeError)
+        if self.getOutputCol() == "__auto__":
+            self._defaultParamMap["outputCol"] = self.uid + "__output"
+
+    def _present(self, cd) -> torch.Tensor:
+        v = torch.as_tensor(cd.values).to(torch.float64)
+        ok = torch.as_tensor(cd.valid_mask(), device=v.device) & ~torch.isnan(v)
+        mv = float(self.getMissingValue())
+        if not math.isnan(mv):
+            ok &= v != mv
+        return v[ok]
+
+    def _fit(self, df):
+        ins, _ = _in_out_cols(self)
+        strat = self.getStrategy()
+        if strat not in ("mean", "median", "mode"):
+            raise ValueError(f"Imputer: unknown strategy {strat!r}")
+        comm = df._comm
+        surrogates = []
+        for c in ins:
+            v = self._present(df._column_data(c))
+            if strat == "mean":
+                t = torch.as_tensor([float(v.sum()), float(v.numel())], dtype=torch.float64, device=df._device)
+                comm.allreduce_(t)
+                s, n = t.cpu().tolist()
+                if n == 0:
+                    raise ValueError(f"Imputer: surrogate cannot be computed, all values of {c} are missing")
+                surrogates.append(s / n)
+                continue
+            allv = comm.allgather_cat(v.to(df._device)).cpu().numpy()
+            if allv.size == 0:
+                raise ValueError(f"Imputer: surrogate cannot be computed, all values of {c} are missing")
+            if strat == "median":
+                srt = np.sort(allv)
+                surrogates.append(float(srt[(srt.size - 1) // 2]))  # lower median, as approxQuantile(0.5)
+            else:
+                vals, cnt = np.unique(allv, return_counts=True)
+                surrogates.append(float(vals[np.argmax(cnt)]))  # ties -> smallest value (Spark)
+        m = ImputerModel(surrogates)
+        self._copyValues(m)
+        return m
+
+
+class ImputerModel(Model):
+    _params = Imputer._params
+
+    def __init__(self, surrogates: Optional[List[float]] = None):
+        super().__init__()
+        self.surrogates = list(surrogates or [])
+
+    @property
+    def surrogateDF(self):
+        import pandas as pd
+        ins, _ = _in_out_cols(self)
+        return pd.DataFrame({c: [s] for c, s in zip(ins, self.surrogates)})
+
+    def _transform(self, df):
+        ins, outs = _in_out_cols(self)
+        mv = float(self.getMissingValue())
+        for c, o, s in zip(ins, outs, self.surrogates):
+            cd = df._column_data(c)
+            v = torch.as_tensor(cd.values)
+            vf = v.to(torch.float64)
+            miss = ~torch.as_tensor(cd.valid_mask(), device=v.device) | torch.isnan(vf)
+            if not math.isnan(mv):
+                miss |= vf == mv
+            if T.is_integral(cd.dtype):
+                out = torch.where(miss, torch.full_like(v, int(s)), v)
+            else:
+                out = torch.where(miss, torch.full_like(vf, s), vf)
+            dt = cd.dtype if T.is_integral(cd.dtype) else T.DoubleType()
+            df = _replace_col(df, o, ColumnData(out, None, dt))
+        return df
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        ins, _ = _in_out_cols(self)
+        U.write_metadata(self, path)
+        U.write_parquet(path, "data", pa.table({c: pa.array([s], type=pa.float64())
+                                                for c, s in zip(ins, self.surrogates)}))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        m = cls()
+        U.apply_params(m, md)
+        ins, _ = _in_out_cols(m)
+        row = U.read_parquet(path, "data").to_pylist()[0]
+        m.surrogates = [float(row[c]) for c in ins]
+        return m

@@ -122,6 +122,15 @@ class Params:
     def _random_uid(cls) -> str:
         return f"{cls.__name__}_{uuid.uuid4().hex[-12:]}"
 
+    def __getattr__(self, name: str):
+        # pyspark exposes every param as an attribute (``dt.maxDepth`` is a Param), which is what
+        # ParamGridBuilder.addGrid and fit(df, {param: value}) take. Only reached when normal
+        # lookup fails, so real attributes and the generated get*/set* methods win.
+        po = self.__dict__.get("_param_objs")
+        if po is not None and name in po:
+            return po[name]
+        raise AttributeError(f"{type(self).__name__!r} object has no attribute {name!r}")
+
     # ------------------------------------------------------------------ pyspark API
     @property
     def params(self):

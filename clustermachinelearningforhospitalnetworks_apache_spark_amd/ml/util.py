@@ -54,6 +54,14 @@ _JVM = {
     "MulticlassClassificationEvaluator": "org.apache.spark.ml.evaluation.MulticlassClassificationEvaluator",
     "BinaryClassificationEvaluator": "org.apache.spark.ml.evaluation.BinaryClassificationEvaluator",
     "ClusteringEvaluator": "org.apache.spark.ml.evaluation.ClusteringEvaluator",
+    "CrossValidator": "org.apache.spark.ml.tuning.CrossValidator",
+    "CrossValidatorModel": "org.apache.spark.ml.tuning.CrossValidatorModel",
+    "TrainValidationSplit": "org.apache.spark.ml.tuning.TrainValidationSplit",
+    "TrainValidationSplitModel": "org.apache.spark.ml.tuning.TrainValidationSplitModel",
+    "OneHotEncoder": "org.apache.spark.ml.feature.OneHotEncoder",
+    "OneHotEncoderModel": "org.apache.spark.ml.feature.OneHotEncoderModel",
+    "Imputer": "org.apache.spark.ml.feature.Imputer",
+    "ImputerModel": "org.apache.spark.ml.feature.ImputerModel",
 }
 _PY = {
     "LinearRegression": "regression", "LinearRegressionModel": "regression",
@@ -69,6 +77,9 @@ _PY = {
     "Pipeline": "pipeline", "PipelineModel": "pipeline",
     "RegressionEvaluator": "evaluation", "MulticlassClassificationEvaluator": "evaluation",
     "BinaryClassificationEvaluator": "evaluation", "ClusteringEvaluator": "evaluation",
+    "CrossValidator": "tuning", "CrossValidatorModel": "tuning",
+    "TrainValidationSplit": "tuning", "TrainValidationSplitModel": "tuning",
+    "OneHotEncoder": "feature", "OneHotEncoderModel": "feature", "Imputer": "feature", "ImputerModel": "feature",
 }
 
 

@@ -62,6 +62,18 @@ def _workload(out_path, rank, master="local[1]"):
     g = spark.createDataFrame(pdf).groupBy("g").agg(F.sum("y").alias("s")).orderBy("g").collect()
     res["groupby"] = [(r.g, r.s) for r in g]
     res["sql"] = spark.createDataFrame(pdf).filter("a > 0 AND b < 2").count()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import (Imputer, OneHotEncoder,
+                                                                                         StringIndexer)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.tuning import CrossValidator, ParamGridBuilder
+    dte = DecisionTreeRegressor(featuresCol="features", labelCol="y")
+    cv = CrossValidator(estimator=dte, estimatorParamMaps=ParamGridBuilder().addGrid(dte.maxDepth, [2, 4]).build(),
+                        evaluator=RegressionEvaluator(labelCol="y"), numFolds=3, seed=9).fit(f)
+    res["cv"] = cv.avgMetrics
+    gi = StringIndexer(inputCol="g", outputCol="gi").fit(df).transform(df)
+    res["ohe"] = OneHotEncoder(inputCol="gi", outputCol="gv").fit(gi).categorySizes
+    holes = spark.createDataFrame(pdf.assign(a=pdf["a"].where(pdf.index % 7 != 0)))
+    res["imp"] = [Imputer(strategy=s, inputCol="a", outputCol="ai").fit(holes).surrogates[0]
+                  for s in ("mean", "median", "mode")]
     if rank == 0:
         with open(out_path, "w") as fh:
             json.dump(res, fh)
@@ -109,6 +121,9 @@ def _check_invariant(r1, rw, world):
     assert [g for g, _ in rw["groupby"]] == [g for g, _ in r1["groupby"]]
     np.testing.assert_allclose([s for _, s in rw["groupby"]], [s for _, s in r1["groupby"]], rtol=1e-12)
     assert rw["sql"] == r1["sql"]
+    np.testing.assert_allclose(rw["cv"], r1["cv"], rtol=1e-9)
+    assert rw["ohe"] == r1["ohe"] == [5]
+    np.testing.assert_allclose(rw["imp"], r1["imp"], rtol=1e-12)
 
 
 @pytest.mark.parametrize("world", [2, 3])
