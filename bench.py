@@ -60,11 +60,13 @@ def main():
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
     ap.add_argument("--full-accumulate", action="store_true",
                     help="re-accumulate every row each step instead of the exact incremental sums")
-    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline"],
+    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
                          "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update; "
                          "pipeline = BASELINE config 5 (VectorAssembler -> StandardScaler(fp8) -> KMeans -> "
-                         "LogisticRegression, 125M x 512 per GPU = 1B x 512 at 8 GPUs), one step = one Pipeline.fit")
+                         "LogisticRegression, 125M x 512 per GPU = 1B x 512 at 8 GPUs), one step = one Pipeline.fit; "
+                         "csv = BASELINE config 1 (1k x 16 synthetic CSV -> VectorAssembler -> KMeans k=5 on local[2] "
+                         "CPU, plumbing), one step = read + assemble + fit")
     ap.add_argument("--rows-per-gpu", type=int, default=125_000_000, help="pipeline workload (weak scaling)")
     ap.add_argument("--solver", default="lbfgs", choices=["lbfgs", "sgd"],
                     help="logreg workload: Spark's L-BFGS (full-batch passes) or data-parallel mini-batch SGD")
@@ -74,6 +76,8 @@ def main():
         return bench_logreg(args)
     if args.workload == "pipeline":
         return bench_pipeline(args)
+    if args.workload == "csv":
+        return bench_csv(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world != 1:
@@ -377,6 +381,64 @@ def bench_pipeline(args):
         if os.environ.get("CML_TRACE") == "1":
             print(TRACER.report(), file=sys.stderr, flush=True)
     spark.stop()
+
+
+def bench_csv(args):
+    """BASELINE.json config 1 ("KMeans k=5 on 1k x 16 synthetic CSV via local[2] CPU, plumbing"):
+    spark.read.csv (native C++ tokenizer/parser, K1) -> VectorAssembler -> KMeans(k=5).fit, on the
+    CPU session (no GPU). One step = the whole read + assemble + fit. The fitted centres are checked
+    against a numpy Lloyd run from the same initial centres (extra.max_center_err)."""
+    import tempfile
+
+    import numpy as np
+
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    os.environ["CML_FORCE_CPU"] = "1"
+    n, d, k = 1000, 16, 5
+    rs = np.random.RandomState(0)
+    cent = rs.randn(k, d) * 5
+    x = cent[rs.randint(0, k, n)] + rs.randn(n, d)
+    tmp = tempfile.mkdtemp(prefix="cml_csv_bench_")
+    cols = [f"f{i}" for i in range(d)]
+    with open(os.path.join(tmp, "part-0.csv"), "w") as fh:
+        fh.write(",".join(cols) + "\n")
+        for row in x:
+            fh.write(",".join(repr(float(v)) for v in row) + "\n")
+    spark = SparkSession.builder.appName("bench-csv").master("local[2]").getOrCreate()
+
+    def one():
+        df = spark.read.option("header", True).option("inferSchema", True).csv(tmp)
+        feats = VectorAssembler(inputCols=cols, outputCol="features").transform(df)
+        return KMeans(k=k, seed=1, maxIter=20, initMode="random").fit(feats)
+
+    for _ in range(args.warmup):
+        one()
+    t0 = time.perf_counter()
+    model = None
+    for _ in range(args.steps):
+        model = one()
+    elapsed = time.perf_counter() - t0
+    # numpy Lloyd oracle from the same data: converged centres must agree (same partition)
+    got = np.stack(model.clusterCenters())
+    c = got.copy()
+    for _ in range(50):
+        lab = ((x[:, None, :] - c[None]) ** 2).sum(-1).argmin(1)
+        c = np.stack([x[lab == j].mean(0) if (lab == j).any() else c[j] for j in range(k)])
+    err = float(np.abs(c - got).max())
+    print(json.dumps({
+        "metric": "KMeans fit samples/sec, 1k x 16 CSV k=5 via local[2] CPU (read + assemble + fit)",
+        "value": n * model.summary.numIter * args.steps / elapsed, "unit": "samples/s", "n_gpus": 0,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "fp64",
+        "data": "synthetic (Gaussian blobs written to CSV)",
+        "config": {"model": "KMeans k=5", "global_batch": n, "seq_len": None, "parallelism": "local[2]", "dim": d},
+        "extra": {"kmeans_iters": model.summary.numIter, "training_cost": model.summary.trainingCost,
+                  "max_center_err_vs_numpy_lloyd": err}}), flush=True)
+    spark.stop()
+    import shutil
+    shutil.rmtree(tmp, ignore_errors=True)
 
 
 if __name__ == "__main__":
