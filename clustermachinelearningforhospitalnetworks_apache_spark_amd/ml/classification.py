@@ -29,8 +29,8 @@ from .base import Estimator, Model
 from .evaluation import BinaryClassificationEvaluator, MulticlassClassificationEvaluator
 from .feature import _replace_col
 from .linalg import DenseMatrix, DenseVector, as_array
-from .tree_models import (CLASSIF_PARAMS, FOREST_PARAMS, TREE_PARAMS, TreeEstimatorMixin, TreeModelMixin,
-                          _default_seed)
+from .tree_models import (CLASSIF_PARAMS, FOREST_PARAMS, GBT_PARAMS, TREE_PARAMS, GBTEstimatorMixin, GBTModelMixin,
+                          TreeEstimatorMixin, TreeModelMixin, _default_seed)
 
 _LOGREG_PARAMS = {
     "featuresCol": ("features", "features column name", str),
@@ -460,3 +460,41 @@ class RandomForestClassificationModel(TreeModelMixin, Model):
     @staticmethod
     def _single_tree_class():
         return DecisionTreeClassificationModel
+
+
+class GBTClassifier(GBTEstimatorMixin, Estimator):
+    """Gradient-boosted trees for binary labels (Spark ``GBTClassifier``, LogLoss on labels mapped
+    to {-1,+1}; rawPrediction [-F, F], probability 1/(1+exp(-2F)))."""
+    _classification = True
+    _params = dict(TREE_PARAMS, **CLASSIF_PARAMS, **GBT_PARAMS,
+                   lossType=("logistic", "loss function which GBT tries to minimize (logistic)", str),
+                   seed=(_default_seed("org.apache.spark.ml.classification.GBTClassifier"), "random seed", int))
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self._defaultParamMap.pop("thresholds", None)
+
+    def _fit(self, df):
+        trees, tw, d = self._gbt_fit(df)
+        m = GBTClassificationModel()
+        self._copyValues(m)
+        m._init_trees(trees, d, 2, tw)
+        return m
+
+
+class GBTClassificationModel(GBTModelMixin, Model):
+    _classification = True
+    _params = GBTClassifier._params
+
+    def __init__(self):
+        super().__init__()
+        self._init_trees([], 0)
+
+    @property
+    def numClasses(self) -> int:
+        return 2
+
+    @staticmethod
+    def _single_tree_class():
+        from .regression import DecisionTreeRegressionModel
+        return DecisionTreeRegressionModel

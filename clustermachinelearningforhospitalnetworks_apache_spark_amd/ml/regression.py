@@ -25,7 +25,8 @@ from .base import Estimator, Model
 from .evaluation import RegressionEvaluator
 from .feature import _replace_col
 from .linalg import DenseVector, as_array
-from .tree_models import (FOREST_PARAMS, TREE_PARAMS, TreeEstimatorMixin, TreeModelMixin, _default_seed)
+from .tree_models import (FOREST_PARAMS, GBT_PARAMS, TREE_PARAMS, GBTEstimatorMixin, GBTModelMixin,
+                          TreeEstimatorMixin, TreeModelMixin, _default_seed)
 
 _LR_PARAMS = {
     "featuresCol": ("features", "features column name", str),
@@ -371,6 +372,32 @@ class RandomForestRegressionModel(TreeModelMixin, Model):
     _task = "regression"
     _forest = True
     _params = RandomForestRegressor._params
+
+    def __init__(self):
+        super().__init__()
+        self._init_trees([], 0)
+
+    @staticmethod
+    def _single_tree_class():
+        return DecisionTreeRegressionModel
+
+
+class GBTRegressor(GBTEstimatorMixin, Estimator):
+    """Gradient-boosted regression trees (Spark ``GBTRegressor``; lossType squared | absolute)."""
+    _params = dict(TREE_PARAMS, **GBT_PARAMS,
+                   lossType=("squared", "loss function which GBT tries to minimize (squared, absolute)", str),
+                   seed=(_default_seed("org.apache.spark.ml.regression.GBTRegressor"), "random seed", int))
+
+    def _fit(self, df):
+        trees, tw, d = self._gbt_fit(df)
+        m = GBTRegressionModel()
+        self._copyValues(m)
+        m._init_trees(trees, d, 2, tw)
+        return m
+
+
+class GBTRegressionModel(GBTModelMixin, Model):
+    _params = GBTRegressor._params
 
     def __init__(self):
         super().__init__()

@@ -48,6 +48,17 @@ FOREST_PARAMS = {
 }
 
 
+GBT_PARAMS = {
+    "maxIter": (20, "max number of boosting iterations (>= 0)", int),
+    "stepSize": (0.1, "learning rate (a.k.a. shrinkage) in (0, 1]", float),
+    "subsamplingRate": (1.0, "fraction of the training data used for learning each tree", float),
+    "featureSubsetStrategy": ("all", "number of features to consider for splits at each tree node", str),
+    "validationTol": (0.01, "threshold for stopping early when fit with validation is used", float),
+    "validationIndicatorCol": (None, "name of the boolean column marking validation rows", None),
+    "impurity": ("variance", "criterion used for information gain (variance)", str),
+}
+
+
 def _default_seed(jvm_name: str) -> int:
     return java_hash(jvm_name)
 
@@ -82,6 +93,34 @@ class TreeEstimatorMixin:
         eng = TR.ForestEngine(x, y, p, comm, row_ids=df._row_ids, weights=w)
         trees = eng.fit()
         return trees, x.shape[1], num_classes
+
+
+class GBTEstimatorMixin(TreeEstimatorMixin):
+    """Boosted ensembles (Spark ``GBTRegressor`` / ``GBTClassifier``) on the same level-wise
+    histogram kernels as the forests; see ``models.trees.fit_gbt``."""
+    _classification = False
+
+    def _gbt_fit(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        y = df._column_data(self.getLabelCol()).values.to(torch.float64)
+        if self._classification:
+            if y.numel() and bool(((y != 0) & (y != 1)).any()):
+                raise ValueError("GBTClassifier supports binary labels {0, 1} only")
+            y = 2.0 * y - 1.0
+        w = df._column_data(self.getOrDefault("weightCol")).values.to(torch.float64) \
+            if self.isSet("weightCol") else None
+        valid = df._column_data(self.getOrDefault("validationIndicatorCol")).values.to(torch.bool) \
+            if self.isSet("validationIndicatorCol") else None
+        loss = self.getLossType().lower()
+        p = TR.TreeParams(task="regression", impurity="variance", max_depth=self.getMaxDepth(),
+                          max_bins=self.getMaxBins(), min_instances=self.getMinInstancesPerNode(),
+                          min_weight_fraction=self.getMinWeightFractionPerNode(),
+                          min_info_gain=self.getMinInfoGain(), subsampling_rate=self.getSubsamplingRate(),
+                          feature_subset=self.getFeatureSubsetStrategy(), seed=int(self.getSeed()))
+        trees, tw = TR.fit_gbt(x, y, p, self.getMaxIter(), self.getStepSize(), loss, df._comm,
+                               row_ids=df._row_ids, weights=w, valid=valid,
+                               validation_tol=self.getValidationTol())
+        return trees, tw, x.shape[1]
 
 
 class TreeModelMixin:
@@ -279,3 +318,65 @@ def _debug(n: TR.Node, indent: int) -> List[str]:
     out.append(f"{pad}Else (feature {n.feature} > {n.threshold})")
     out += _debug(n.right, indent + 1)
     return out
+
+
+class GBTModelMixin(TreeModelMixin):
+    """Margin F(x) = sum_m w_m tree_m(x) (one K21 launch over all trees, leaf values pre-scaled by
+    the tree weights).  Trees are regression trees, so persistence is the ensemble layout with
+    ``treesMetadata.weights`` = the boosting weights."""
+    _task = "regression"
+    _forest = True
+    _classification = False
+
+    def _margin(self, x):
+        return TR.predict_forest(self._trees, x, "variance", 1, average=False, normalize_leaves=False,
+                                 tree_weights=self._tree_weights)[:, 0]
+
+    def _raw(self, x):
+        return self._margin(x)[:, None]
+
+    @property
+    def featureImportances(self) -> DenseVector:
+        return DenseVector(TR.feature_importances(self._trees, self._num_features, per_tree_normalization=False))
+
+    def predict(self, value) -> float:
+        v = torch.as_tensor(as_array(value), dtype=torch.float64).reshape(1, -1)
+        f = float(self._margin(v)[0])
+        return f if not self._classification else float(f > 0)
+
+    def evaluateEachIteration(self, dataset, loss: Optional[str] = None) -> List[float]:
+        """Mean loss of the first m trees for m = 1..numTrees (Spark ``evaluateEachIteration``)."""
+        x = dataset._feature_matrix(self.getFeaturesCol())
+        y = dataset._column_data(self.getLabelCol()).values.to(torch.float64)
+        if self._classification:
+            y = 2.0 * y - 1.0
+        loss = (loss or self.getLossType()).lower()
+        comm = dataset._comm
+        f = torch.zeros_like(y)
+        den = max(comm.sum_scalar(float(y.numel())), 1.0)
+        out = []
+        for t, w in zip(self._trees, self._tree_weights):
+            f += w * TR.predict_tree(t, x.to(torch.float64))
+            out.append(comm.sum_scalar(float(TR.gbt_loss(loss, f, y).sum().item())) / den)
+        return out
+
+    def _transform(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        f = self._margin(x)
+        if not self._classification:
+            return _replace_col(df, self.getPredictionCol(), ColumnData(f.contiguous(), None, T.DoubleType()))
+        raw = torch.stack([-f, f], 1)
+        p1 = 1.0 / (1.0 + torch.exp(torch.clamp(-2.0 * f, max=700.0)))
+        prob = torch.stack([1.0 - p1, p1], 1)
+        thr = self.getOrDefault("thresholds") if self.isDefined("thresholds") else None
+        if thr:
+            t = torch.as_tensor(np.asarray(thr, dtype=np.float64), device=prob.device)
+            pred = torch.argmax(prob / t.clamp(min=1e-300), 1).to(torch.float64)
+        else:
+            pred = (f > 0).to(torch.float64)
+        out = df
+        if self.getRawPredictionCol():
+            out = _replace_col(out, self.getRawPredictionCol(), ColumnData(raw, None, T.VectorUDT()))
+        if self.getProbabilityCol():
+            out = _replace_col(out, self.getProbabilityCol(), ColumnData(prob, None, T.VectorUDT()))
+        return _replace_col(out, self.getPredictionCol(), ColumnData(pred, None, T.DoubleType()))

@@ -62,6 +62,10 @@ _JVM = {
     "OneHotEncoderModel": "org.apache.spark.ml.feature.OneHotEncoderModel",
     "Imputer": "org.apache.spark.ml.feature.Imputer",
     "ImputerModel": "org.apache.spark.ml.feature.ImputerModel",
+    "GBTRegressor": "org.apache.spark.ml.regression.GBTRegressor",
+    "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
+    "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
+    "GBTClassificationModel": "org.apache.spark.ml.classification.GBTClassificationModel",
 }
 _PY = {
     "LinearRegression": "regression", "LinearRegressionModel": "regression",
@@ -80,6 +84,8 @@ _PY = {
     "CrossValidator": "tuning", "CrossValidatorModel": "tuning",
     "TrainValidationSplit": "tuning", "TrainValidationSplitModel": "tuning",
     "OneHotEncoder": "feature", "OneHotEncoderModel": "feature", "Imputer": "feature", "ImputerModel": "feature",
+    "GBTRegressor": "regression", "GBTRegressionModel": "regression",
+    "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }
 
 

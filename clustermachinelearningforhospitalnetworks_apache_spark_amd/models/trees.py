@@ -322,12 +322,17 @@ class ForestEngine:
             node_of[t] = torch.where(act, new, nd)
 
     # -------------------------------------------------------------- fit
-    def fit(self) -> List[Node]:
+    def fit(self, splits: Optional[List[np.ndarray]] = None, bins: Optional[torch.Tensor] = None) -> List[Node]:
+        """Grow ``num_trees`` trees level-wise.  ``splits``/``bins`` let a caller that fits many
+        trees on the same rows (gradient boosting) find candidates and bin the rows once."""
         p = self.p
         T = p.num_trees
-        splits = self.find_splits()
+        if splits is None:
+            splits = self.find_splits()
         self.splits = splits
-        bins = self.binize(splits)
+        if bins is None:
+            bins = self.binize(splits)
+        self.bins = bins
         # bagging weights (Spark BaggedPoint: Poisson(rate) with replacement, Bernoulli without)
         if T > 1 and p.bootstrap:
             wt = torch.stack([rng.poisson1(self.row_ids, p.seed, 1000 + t).to(torch.float32)
@@ -538,8 +543,9 @@ def num_nodes(root: Node) -> int:
     return len(preorder(root))
 
 
-def feature_importances(trees: List[Node], d: int) -> np.ndarray:
-    """Spark: per tree Σ gain·count over split nodes, normalised; forest = mean, renormalised."""
+def feature_importances(trees: List[Node], d: int, per_tree_normalization: bool = True) -> np.ndarray:
+    """Spark: per tree Σ gain·count over split nodes, normalised; forest = mean, renormalised.
+    GBT models sum the raw per-tree importances (``perTreeNormalization = false``)."""
     total = np.zeros(d)
     for t in trees:
         imp = np.zeros(d)
@@ -547,22 +553,23 @@ def feature_importances(trees: List[Node], d: int) -> np.ndarray:
             if not n.is_leaf:
                 imp[n.feature] += n.gain * n.count
         s = imp.sum()
-        if s > 0:
+        if s > 0 and per_tree_normalization:
             imp /= s
         total += imp
-    if len(trees) > 1:
+    if len(trees) > 1 and per_tree_normalization:
         total /= len(trees)
     s = total.sum()
     return total / s if s > 0 else total
 
 
 def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: int, average: bool,
-                   normalize_leaves: bool) -> torch.Tensor:
+                   normalize_leaves: bool, tree_weights: Optional[Sequence[float]] = None) -> torch.Tensor:
     """[n, S] per-row accumulated leaf values: regression -> prediction (mean if `average`),
     classification -> summed class distributions (normalised per tree when `normalize_leaves`)."""
     S = 1 if kind == "variance" else num_classes
     feats, thrs, lefts, rights, leaves, roots = [], [], [], [], [], []
-    for t in trees:
+    for ti, t in enumerate(trees):
+        tw = 1.0 if tree_weights is None else float(tree_weights[ti])
         nodes = preorder(t)
         base = len(feats)
         roots.append(base)
@@ -573,7 +580,7 @@ def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: i
             lefts.append(index[id(nd.left)] if not nd.is_leaf else -1)
             rights.append(index[id(nd.right)] if not nd.is_leaf else -1)
             if kind == "variance":
-                leaves.append([nd.prediction])
+                leaves.append([nd.prediction * tw])
             else:
                 st = np.asarray(nd.stats, dtype=np.float64)
                 if normalize_leaves:
@@ -615,3 +622,89 @@ def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: i
     if average and len(trees) > 1:
         out /= len(trees)
     return out
+
+
+# ---------------------------------------------------------------------------------------------- boosting
+
+GBT_LOSSES = ("squared", "absolute", "logistic")
+
+
+def gbt_residual(loss: str, f: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    """Pseudo-residual ``-dL/dF`` of Spark's losses (SquaredError 2(y-F), AbsoluteError sign(y-F),
+    LogLoss on labels in {-1,+1}: 4y / (1 + exp(2yF)))."""
+    if loss == "squared":
+        return 2.0 * (y - f)
+    if loss == "absolute":
+        return torch.sign(y - f)
+    return 4.0 * y / (1.0 + torch.exp(torch.clamp(2.0 * y * f, max=700.0)))
+
+
+def gbt_loss(loss: str, f: torch.Tensor, y: torch.Tensor) -> torch.Tensor:
+    if loss == "squared":
+        return (y - f) ** 2
+    if loss == "absolute":
+        return (y - f).abs()
+    m = 2.0 * y * f
+    return 2.0 * torch.where(m < -30, -m, torch.log1p(torch.exp(-m)))  # Spark LogLoss: 2 log(1 + e^(-2yF))
+
+
+def predict_tree(tree: Node, x: torch.Tensor) -> torch.Tensor:
+    return predict_forest([tree], x, "variance", 1, average=False, normalize_leaves=False)[:, 0]
+
+
+def fit_gbt(x: torch.Tensor, y: torch.Tensor, params: TreeParams, max_iter: int, step_size: float, loss: str,
+            comm: Optional[Communicator] = None, row_ids: Optional[torch.Tensor] = None,
+            weights: Optional[torch.Tensor] = None, valid: Optional[torch.Tensor] = None,
+            validation_tol: float = 0.01):
+    """Gradient-boosted regression trees (Spark ``GradientBoostedTrees.boost``): tree 0 is fit on the
+    labels with weight 1, tree m on the pseudo-residuals of the running margin with weight
+    ``step_size``.  Candidate splits and the uint8 bin codes (K16/K17) are built once and reused by
+    every tree; each tree is one level-wise pass of the K18/K19/K20 kernels plus an all-reduce
+    per level; the margin is updated in place by K21.  Labels for ``logistic`` must already be
+    in {-1, +1}.  ``valid`` (bool per row) holds rows out of training and stops early once the
+    validation loss improves by less than ``validation_tol * max(loss, 0.01)`` (Spark's rule).
+    Returns (trees, tree_weights)."""
+    comm = comm or local_comm()
+    if loss not in GBT_LOSSES:
+        raise ValueError(f"unsupported GBT loss {loss!r}")
+    n = int(x.shape[0])
+    row_ids = row_ids if row_ids is not None else torch.arange(n, device=x.device)
+    y = y.to(torch.float64)
+    xv = yv = None
+    if valid is not None:
+        keep = ~valid
+        xv, yv = x[valid].to(torch.float64).contiguous(), y[valid]
+        x, y, row_ids = x[keep], y[keep], row_ids[keep]
+        weights = weights[keep] if weights is not None else None
+    p = TreeParams(**{**params.__dict__, "task": "regression", "impurity": "variance", "num_trees": 1,
+                      "bootstrap": False})
+    eng = ForestEngine(x, y, p, comm, row_ids=row_ids, weights=weights)
+    splits = eng.find_splits()
+    bins = eng.binize(splits)
+    trees: List[Node] = []
+    tw: List[float] = []
+    f = torch.zeros_like(eng.y)
+    fv = torch.zeros_like(yv) if yv is not None else None
+    best_err, best_m = float("inf"), 0
+    for m in range(max_iter):
+        w = 1.0 if m == 0 else step_size
+        if m > 0:
+            eng.y = gbt_residual(loss, f, y).contiguous()
+        eng.p.seed = params.seed + m
+        t = eng.fit(splits, bins)[0]
+        trees.append(t)
+        tw.append(w)
+        f += w * predict_tree(t, eng.x)
+        if fv is not None:
+            fv += w * predict_tree(t, xv)
+            num = comm.sum_scalar(float(gbt_loss(loss, fv, yv).sum().item()))
+            err = num / max(comm.sum_scalar(float(yv.numel())), 1.0)
+            if m == 0:
+                best_err, best_m = err, 1
+            elif best_err - err < validation_tol * max(err, 0.01):
+                break
+            elif err < best_err:
+                best_err, best_m = err, m + 1
+    if fv is not None and best_m:
+        trees, tw = trees[:best_m], tw[:best_m]
+    return trees, tw
