@@ -53,6 +53,14 @@ def _workload(out_path, rank, master="local[1]"):
     res["dt_nodes"] = dt.numNodes
     rf = RandomForestRegressor(featuresCol="features", labelCol="y", numTrees=4).fit(tr)
     res["rf_imp"] = rf.featureImportances.toArray().tolist()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import GBTClassifier
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import GBTRegressor
+    gb = GBTRegressor(featuresCol="features", labelCol="y", maxIter=5).fit(tr)
+    res["gbt"] = gb.featureImportances.toArray().tolist() + [RegressionEvaluator(labelCol="y").evaluate(
+        gb.transform(te))]
+    gbl = f.withColumn("label", F.when(F.col("y") > 1.0, 1).otherwise(0)).withColumn("v", F.col("d") > 5.0)
+    gc = GBTClassifier(maxIter=30, stepSize=0.5, validationIndicatorCol="v").fit(gbl)
+    res["gbtc"] = [gc.getNumTrees] + gc.evaluateEachIteration(gbl)
     km = KMeans(k=3, seed=5, maxIter=10).fit(f)
     res["km"] = np.stack(km.clusterCenters()).tolist()
     res["km_cost"] = km.summary.trainingCost
@@ -115,6 +123,9 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["dt_imp"], r1["dt_imp"], rtol=1e-9, atol=1e-12)
     assert rw["dt_nodes"] == r1["dt_nodes"]
     np.testing.assert_allclose(rw["rf_imp"], r1["rf_imp"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rw["gbt"], r1["gbt"], rtol=1e-9, atol=1e-12)
+    assert rw["gbtc"][0] == r1["gbtc"][0]
+    np.testing.assert_allclose(rw["gbtc"], r1["gbtc"], rtol=1e-9)
     np.testing.assert_allclose(rw["km"], r1["km"], rtol=1e-9, atol=1e-9)
     assert abs(rw["km_cost"] - r1["km_cost"]) < 1e-6 * r1["km_cost"]
     np.testing.assert_allclose(rw["logreg"], r1["logreg"], rtol=1e-6, atol=1e-8)
