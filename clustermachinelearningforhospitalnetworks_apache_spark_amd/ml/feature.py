@@ -633,3 +633,6 @@ class ImputerModel(Model):
         row = U.read_parquet(path, "data").to_pylist()[0]
         m.surrogates = [float(row[c]) for c in ins]
         return m
+
+
+from .feature_extra import Bucketizer, Normalizer, PCA, PCAModel, QuantileDiscretizer  # noqa: E402,F401

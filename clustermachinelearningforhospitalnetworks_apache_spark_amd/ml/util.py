@@ -62,6 +62,11 @@ _JVM = {
     "OneHotEncoderModel": "org.apache.spark.ml.feature.OneHotEncoderModel",
     "Imputer": "org.apache.spark.ml.feature.Imputer",
     "ImputerModel": "org.apache.spark.ml.feature.ImputerModel",
+    "Bucketizer": "org.apache.spark.ml.feature.Bucketizer",
+    "QuantileDiscretizer": "org.apache.spark.ml.feature.QuantileDiscretizer",
+    "Normalizer": "org.apache.spark.ml.feature.Normalizer",
+    "PCA": "org.apache.spark.ml.feature.PCA",
+    "PCAModel": "org.apache.spark.ml.feature.PCAModel",
     "GBTRegressor": "org.apache.spark.ml.regression.GBTRegressor",
     "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
     "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
@@ -84,6 +89,8 @@ _PY = {
     "CrossValidator": "tuning", "CrossValidatorModel": "tuning",
     "TrainValidationSplit": "tuning", "TrainValidationSplitModel": "tuning",
     "OneHotEncoder": "feature", "OneHotEncoderModel": "feature", "Imputer": "feature", "ImputerModel": "feature",
+    "Bucketizer": "feature", "QuantileDiscretizer": "feature", "Normalizer": "feature", "PCA": "feature",
+    "PCAModel": "feature",
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }
