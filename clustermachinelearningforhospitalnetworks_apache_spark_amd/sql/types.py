@@ -129,6 +129,18 @@ class VectorUDT(DataType):
                      "nullable": True, "metadata": {}}]}}
 
 
+class MatrixUDT(DataType):
+    """pyspark.ml.linalg.MatrixUDT: host column of DenseMatrix objects (statistics results)."""
+    host_only = True
+
+    @classmethod
+    def typeName(cls):
+        return "matrix"
+
+    def simpleString(self):
+        return "matrix"
+
+
 class ArrayType(DataType):
     host_only = True
 

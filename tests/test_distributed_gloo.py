@@ -61,6 +61,11 @@ def _workload(out_path, rank, master="local[1]"):
     gbl = f.withColumn("label", F.when(F.col("y") > 1.0, 1).otherwise(0)).withColumn("v", F.col("d") > 5.0)
     gc = GBTClassifier(maxIter=30, stepSize=0.5, validationIndicatorCol="v").fit(gbl)
     res["gbtc"] = [gc.getNumTrees] + gc.evaluateEachIteration(gbl)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import PCA, QuantileDiscretizer
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.stat import Correlation
+    res["corr"] = [Correlation.corr(f, "features", m).head()[0].toArray().tolist() for m in ("pearson", "spearman")]
+    res["pca"] = PCA(k=2, inputCol="features", outputCol="p").fit(f).explainedVariance.toArray().tolist()
+    res["qd"] = QuantileDiscretizer(numBuckets=4, inputCol="b", outputCol="q").fit(f).getSplits()[1:-1]
     km = KMeans(k=3, seed=5, maxIter=10).fit(f)
     res["km"] = np.stack(km.clusterCenters()).tolist()
     res["km_cost"] = km.summary.trainingCost
@@ -126,6 +131,9 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["gbt"], r1["gbt"], rtol=1e-9, atol=1e-12)
     assert rw["gbtc"][0] == r1["gbtc"][0]
     np.testing.assert_allclose(rw["gbtc"], r1["gbtc"], rtol=1e-9)
+    np.testing.assert_allclose(rw["corr"], r1["corr"], rtol=1e-9, atol=1e-12)
+    np.testing.assert_allclose(rw["pca"], r1["pca"], rtol=1e-9)
+    assert rw["qd"] == r1["qd"]
     np.testing.assert_allclose(rw["km"], r1["km"], rtol=1e-9, atol=1e-9)
     assert abs(rw["km_cost"] - r1["km_cost"]) < 1e-6 * r1["km_cost"]
     np.testing.assert_allclose(rw["logreg"], r1["logreg"], rtol=1e-6, atol=1e-8)
