@@ -406,3 +406,7 @@ class GBTRegressionModel(GBTModelMixin, Model):
     @staticmethod
     def _single_tree_class():
         return DecisionTreeRegressionModel
+
+
+from .glr import (GeneralizedLinearRegression, GeneralizedLinearRegressionModel,  # noqa: E402,F401
+                  GeneralizedLinearRegressionTrainingSummary)

@@ -67,6 +67,8 @@ _JVM = {
     "Normalizer": "org.apache.spark.ml.feature.Normalizer",
     "PCA": "org.apache.spark.ml.feature.PCA",
     "PCAModel": "org.apache.spark.ml.feature.PCAModel",
+    "GeneralizedLinearRegression": "org.apache.spark.ml.regression.GeneralizedLinearRegression",
+    "GeneralizedLinearRegressionModel": "org.apache.spark.ml.regression.GeneralizedLinearRegressionModel",
     "GBTRegressor": "org.apache.spark.ml.regression.GBTRegressor",
     "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
     "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
@@ -91,6 +93,7 @@ _PY = {
     "OneHotEncoder": "feature", "OneHotEncoderModel": "feature", "Imputer": "feature", "ImputerModel": "feature",
     "Bucketizer": "feature", "QuantileDiscretizer": "feature", "Normalizer": "feature", "PCA": "feature",
     "PCAModel": "feature",
+    "GeneralizedLinearRegression": "regression", "GeneralizedLinearRegressionModel": "regression",
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }

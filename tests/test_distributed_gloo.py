@@ -65,6 +65,10 @@ def _workload(out_path, rank, master="local[1]"):
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.stat import Correlation
     res["corr"] = [Correlation.corr(f, "features", m).head()[0].toArray().tolist() for m in ("pearson", "spearman")]
     res["pca"] = PCA(k=2, inputCol="features", outputCol="p").fit(f).explainedVariance.toArray().tolist()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import GeneralizedLinearRegression
+    pois = f.withColumn("cnt", F.when(F.col("y") > 1.0, 3).otherwise(1))
+    glr = GeneralizedLinearRegression(family="poisson", labelCol="cnt").fit(pois)
+    res["glr"] = glr.coefficients.toArray().tolist() + [glr.intercept, glr.summary.deviance]
     res["qd"] = QuantileDiscretizer(numBuckets=4, inputCol="b", outputCol="q").fit(f).getSplits()[1:-1]
     km = KMeans(k=3, seed=5, maxIter=10).fit(f)
     res["km"] = np.stack(km.clusterCenters()).tolist()
@@ -134,6 +138,7 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["corr"], r1["corr"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(rw["pca"], r1["pca"], rtol=1e-9)
     assert rw["qd"] == r1["qd"]
+    np.testing.assert_allclose(rw["glr"], r1["glr"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(rw["km"], r1["km"], rtol=1e-9, atol=1e-9)
     assert abs(rw["km_cost"] - r1["km_cost"]) < 1e-6 * r1["km_cost"]
     np.testing.assert_allclose(rw["logreg"], r1["logreg"], rtol=1e-6, atol=1e-8)
