@@ -498,3 +498,6 @@ class GBTClassificationModel(GBTModelMixin, Model):
     def _single_tree_class():
         from .regression import DecisionTreeRegressionModel
         return DecisionTreeRegressionModel
+
+
+from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: E402,F401

@@ -69,6 +69,8 @@ _JVM = {
     "PCAModel": "org.apache.spark.ml.feature.PCAModel",
     "GeneralizedLinearRegression": "org.apache.spark.ml.regression.GeneralizedLinearRegression",
     "GeneralizedLinearRegressionModel": "org.apache.spark.ml.regression.GeneralizedLinearRegressionModel",
+    "NaiveBayes": "org.apache.spark.ml.classification.NaiveBayes",
+    "NaiveBayesModel": "org.apache.spark.ml.classification.NaiveBayesModel",
     "GBTRegressor": "org.apache.spark.ml.regression.GBTRegressor",
     "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
     "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
@@ -94,6 +96,7 @@ _PY = {
     "Bucketizer": "feature", "QuantileDiscretizer": "feature", "Normalizer": "feature", "PCA": "feature",
     "PCAModel": "feature",
     "GeneralizedLinearRegression": "regression", "GeneralizedLinearRegressionModel": "regression",
+    "NaiveBayes": "classification", "NaiveBayesModel": "classification",
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }
