@@ -69,6 +69,9 @@ def _workload(out_path, rank, master="local[1]"):
     pois = f.withColumn("cnt", F.when(F.col("y") > 1.0, 3).otherwise(1))
     glr = GeneralizedLinearRegression(family="poisson", labelCol="cnt").fit(pois)
     res["glr"] = glr.coefficients.toArray().tolist() + [glr.intercept, glr.summary.deviance]
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import NaiveBayes
+    nbm = NaiveBayes(modelType="gaussian").fit(f.withColumn("label", F.when(F.col("y") > 1.0, 1).otherwise(0)))
+    res["nb"] = np.r_[nbm.theta.toArray().ravel(), nbm.sigma.toArray().ravel(), nbm.pi.toArray()].tolist()
     res["qd"] = QuantileDiscretizer(numBuckets=4, inputCol="b", outputCol="q").fit(f).getSplits()[1:-1]
     km = KMeans(k=3, seed=5, maxIter=10).fit(f)
     res["km"] = np.stack(km.clusterCenters()).tolist()
@@ -138,6 +141,7 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["corr"], r1["corr"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(rw["pca"], r1["pca"], rtol=1e-9)
     assert rw["qd"] == r1["qd"]
+    np.testing.assert_allclose(rw["nb"], r1["nb"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(rw["glr"], r1["glr"], rtol=1e-9, atol=1e-12)
     np.testing.assert_allclose(rw["km"], r1["km"], rtol=1e-9, atol=1e-9)
     assert abs(rw["km_cost"] - r1["km_cost"]) < 1e-6 * r1["km_cost"]
