@@ -204,3 +204,6 @@ class KMeansSummary:
     @property
     def cluster(self):
         return self.predictions.select(self.predictionCol)
+
+
+from .bisecting import BisectingKMeans, BisectingKMeansModel  # noqa: E402,F401

@@ -71,6 +71,8 @@ _JVM = {
     "GeneralizedLinearRegressionModel": "org.apache.spark.ml.regression.GeneralizedLinearRegressionModel",
     "NaiveBayes": "org.apache.spark.ml.classification.NaiveBayes",
     "NaiveBayesModel": "org.apache.spark.ml.classification.NaiveBayesModel",
+    "BisectingKMeans": "org.apache.spark.ml.clustering.BisectingKMeans",
+    "BisectingKMeansModel": "org.apache.spark.ml.clustering.BisectingKMeansModel",
     "GBTRegressor": "org.apache.spark.ml.regression.GBTRegressor",
     "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
     "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
@@ -97,6 +99,7 @@ _PY = {
     "PCAModel": "feature",
     "GeneralizedLinearRegression": "regression", "GeneralizedLinearRegressionModel": "regression",
     "NaiveBayes": "classification", "NaiveBayesModel": "classification",
+    "BisectingKMeans": "clustering", "BisectingKMeansModel": "clustering",
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }
