@@ -6,7 +6,8 @@
 // forest at once ("ensemble packing"), splits chosen on the host from the all-reduced
 // histograms, rows routed to children on the device.
 //
-// K17 tree_binize  value -> bin: #thresholds < value (binary search, thresholds in LDS)
+// K17 tree_binize  value -> bin: #thresholds < value (binary search, thresholds in LDS);
+//                  uint8 codes up to 256 bins, uint16 above
 // K18 tree_hist    hist[t][node][f][bin][s] += w_t(row)·stat_s(row) for rows whose node
 //                  at this level is `node`; LDS-privatised per workgroup (one tree ×
 //                  feature chunk per workgroup), 64-bit fixed point (order-independent,
@@ -18,52 +19,68 @@
 
 namespace {
 
+// Bin codes are uint8 while nbins <= 256 (Spark's default maxBins = 32) and uint16 above it, so
+// maxBins > 256 never wraps. Thresholds sit in LDS when d * max_splits doubles fit 64 KiB; wider
+// tables (d = 512 features, large maxBins) are read from global memory (L2-resident, read-only).
+template <typename BinT, bool kLds>
 __global__ void tree_binize_kernel(const double* __restrict__ X, long long n, long long ld, int d,
                                    const double* __restrict__ thr, int max_splits, const int* __restrict__ nsplit,
-                                   unsigned char* __restrict__ bins) {
+                                   BinT* __restrict__ bins) {
   extern __shared__ double sthr[];
-  for (int i = threadIdx.x; i < d * max_splits; i += blockDim.x) sthr[i] = thr[i];
-  __syncthreads();
+  if (kLds) {
+    for (int i = threadIdx.x; i < d * max_splits; i += blockDim.x) sthr[i] = thr[i];
+    __syncthreads();
+  }
+  const double* tab = kLds ? sthr : thr;
   const long long total = n * (long long)d;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total;
        i += (long long)gridDim.x * blockDim.x) {
     const long long r = i / d;
     const int f = (int)(i - r * d);
     const double v = X[r * ld + f];
-    const double* t = sthr + f * max_splits;
+    const double* t = tab + (long long)f * max_splits;
     int lo = 0, hi = nsplit[f];  // first index with t[idx] >= v
     while (lo < hi) {
       const int mid = (lo + hi) >> 1;
       if (t[mid] < v) lo = mid + 1; else hi = mid;
     }
-    bins[r * d + f] = (unsigned char)lo;
+    bins[r * d + f] = (BinT)lo;
   }
 }
 
-// grid: (row blocks, trees, feature chunks). LDS: nodes * fc * nbins * S int64.
+// grid: (row blocks, trees, feature chunks x node chunks). LDS: nc * fc * nbins * S int64.
 // Statistics accumulate as 64-bit FIXED POINT (value * 2^e_s, e_s chosen on the host from the
 // global n, max weight and max |y| so no sum can overflow): integer adds are associative, so the
 // histogram — and every split chosen from it — is bit-identical whatever the row order, the number
 // of workgroups or the number of GPUs, with f64-class precision (Spark aggregates these in f64;
 // f32 partials lost ~1e-7 of Σy² and made splits world-size dependent).
-__global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __restrict__ bins, long long n, int d,
+// A level whose (node, feature) histograms exceed the LDS budget is split into node chunks
+// (blockIdx.z = node chunk * fchunks + feature chunk; each chunk re-reads the row stream); one
+// whose single (node, feature) histogram is larger than LDS (nbins * S > 12288) adds straight into
+// the global histogram (kDirect, integer atomics: still exact and order-independent).
+template <typename BinT, bool kDirect>
+__global__ __launch_bounds__(256) void tree_hist_kernel(const BinT* __restrict__ bins, long long n, int d,
                                                         int nbins, const int* __restrict__ node_of,
                                                         const float* __restrict__ wt, const double* __restrict__ y,
                                                         const int* __restrict__ cls, int S, int nodes, int fc,
-                                                        double sc0, double sc1, double sc2,
+                                                        int nc, int fchunks, double sc0, double sc1, double sc2,
                                                         unsigned long long* __restrict__ out) {
   extern __shared__ unsigned long long h[];
   const int t = blockIdx.y;
-  const int f0 = blockIdx.z * fc;
+  const int f0 = (blockIdx.z % fchunks) * fc;
+  const int n0 = (blockIdx.z / fchunks) * nc;
   const int fcount = min(fc, d - f0);
-  const int hsize = nodes * fc * nbins * S;
-  for (int i = threadIdx.x; i < hsize; i += blockDim.x) h[i] = 0ull;
-  __syncthreads();
+  const int ncount = min(nc, nodes - n0);
+  const int hsize = nc * fc * nbins * S;
+  if (!kDirect) {
+    for (int i = threadIdx.x; i < hsize; i += blockDim.x) h[i] = 0ull;
+    __syncthreads();
+  }
   const int* nd = node_of + (long long)t * n;
   const float* w = wt != nullptr ? wt + (long long)t * n : nullptr;
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
-    const int node = nd[r];
-    if (node < 0) continue;
+    const int node = nd[r] - n0;
+    if (node < 0 || node >= ncount) continue;
     const double wr = w != nullptr ? (double)w[r] : 1.0;
     if (wr == 0.0) continue;
     unsigned long long q0 = (unsigned long long)llrint(wr * sc0), q1 = 0ull, q2 = 0ull;
@@ -75,9 +92,11 @@ __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __r
     } else {
       c = cls[r];
     }
-    const unsigned char* br = bins + r * d + f0;
+    const BinT* br = bins + r * d + f0;
     for (int f = 0; f < fcount; ++f) {
-      unsigned long long* cell = h + ((node * fc + f) * nbins + br[f]) * S;
+      unsigned long long* cell =
+          kDirect ? out + ((((long long)t * nodes + n0 + node) * d + f0 + f) * nbins + br[f]) * S
+                  : h + ((node * fc + f) * nbins + br[f]) * S;
       if (cls == nullptr) {
         atomicAdd(cell + 0, q0);
         atomicAdd(cell + 1, q1);
@@ -87,6 +106,7 @@ __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __r
       }
     }
   }
+  if (kDirect) return;
   __syncthreads();
   for (int i = threadIdx.x; i < hsize; i += blockDim.x) {
     const unsigned long long v = h[i];
@@ -97,8 +117,8 @@ __global__ __launch_bounds__(256) void tree_hist_kernel(const unsigned char* __r
     const int rest2 = rest / nbins;
     const int f = rest2 % fc;
     const int node = rest2 / fc;
-    if (f >= fcount) continue;
-    atomicAdd(out + ((((long long)t * nodes + node) * d + f0 + f) * nbins + b) * S + s, v);
+    if (f >= fcount || node >= ncount) continue;
+    atomicAdd(out + ((((long long)t * nodes + n0 + node) * d + f0 + f) * nbins + b) * S + s, v);
   }
 }
 
@@ -240,7 +260,8 @@ __global__ __launch_bounds__(256) void tree_best_split_kernel(const long long* _
 }
 
 // split_feat/split_bin/left_id/right_id: [T][nodes]; split_feat < 0 => node is a leaf (row retires).
-__global__ void tree_route_kernel(const unsigned char* __restrict__ bins, long long n, int d, int T, int nodes,
+template <typename BinT>
+__global__ void tree_route_kernel(const BinT* __restrict__ bins, long long n, int d, int T, int nodes,
                                   int* __restrict__ node_of, const int* __restrict__ split_feat,
                                   const int* __restrict__ split_bin, const int* __restrict__ left_id,
                                   const int* __restrict__ right_id) {
@@ -257,7 +278,7 @@ __global__ void tree_route_kernel(const unsigned char* __restrict__ bins, long l
       node_of[i] = -1;
       continue;
     }
-    node_of[i] = bins[r * d + f] <= split_bin[k] ? left_id[k] : right_id[k];
+    node_of[i] = (int)bins[r * d + f] <= split_bin[k] ? left_id[k] : right_id[k];
   }
 }
 
@@ -288,28 +309,78 @@ int blocks_for(long long work, int threads, int cap) {
 
 }  // namespace
 
+// bin_bytes: 1 (uint8 codes, nbins <= 256) or 2 (uint16 codes, nbins <= 65536).
 CML_API int cml_tree_binize(const double* X, long long n, long long ld, int d, const double* thr, int max_splits,
-                            const int* nsplit, unsigned char* bins, void* stream) {
+                            const int* nsplit, void* bins, int bin_bytes, void* stream) {
+  if (bin_bytes != 1 && bin_bytes != 2) return (int)hipErrorInvalidValue;
+  if (bin_bytes == 1 && max_splits > 255) return (int)hipErrorInvalidValue;
   const size_t lds = sizeof(double) * (size_t)d * max_splits;
-  if (lds > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(tree_binize_kernel, dim3(blocks_for(n * d, 256, 4096)), dim3(256), lds, (hipStream_t)stream, X,
-                     n, ld, d, thr, max_splits, nsplit, bins);
+  const bool use_lds = lds <= 64 * 1024;
+  const dim3 grid(blocks_for(n * d, 256, 4096));
+  hipStream_t s = (hipStream_t)stream;
+  if (bin_bytes == 1) {
+    if (use_lds)
+      hipLaunchKernelGGL((tree_binize_kernel<unsigned char, true>), grid, dim3(256), lds, s, X, n, ld, d, thr,
+                         max_splits, nsplit, (unsigned char*)bins);
+    else
+      hipLaunchKernelGGL((tree_binize_kernel<unsigned char, false>), grid, dim3(256), 0, s, X, n, ld, d, thr,
+                         max_splits, nsplit, (unsigned char*)bins);
+  } else {
+    if (use_lds)
+      hipLaunchKernelGGL((tree_binize_kernel<unsigned short, true>), grid, dim3(256), lds, s, X, n, ld, d, thr,
+                         max_splits, nsplit, (unsigned short*)bins);
+    else
+      hipLaunchKernelGGL((tree_binize_kernel<unsigned short, false>), grid, dim3(256), 0, s, X, n, ld, d, thr,
+                         max_splits, nsplit, (unsigned short*)bins);
+  }
   return cml_status();
 }
 
-// Returns the feature chunk used (features per workgroup) so the host can size nothing; out must be zeroed.
-CML_API int cml_tree_hist(const unsigned char* bins, long long n, int d, int nbins, const int* node_of, int T,
-                          const float* wt, const double* y, const int* cls, int S, int nodes, const double* scales,
-                          unsigned long long* out, int row_blocks, void* stream) {
-  const long long per_feat = (long long)nodes * nbins * S * 8;
-  int fc = (int)((96 * 1024) / (per_feat > 0 ? per_feat : 1));
-  if (fc < 1) return (int)hipErrorInvalidValue;
-  if (fc > d) fc = d;
+namespace {
+template <typename BinT>
+void launch_hist(const BinT* bins, long long n, int d, int nbins, const int* node_of, int T, const float* wt,
+                 const double* y, const int* cls, int S, int nodes, const double* scales, unsigned long long* out,
+                 int row_blocks, hipStream_t stream) {
+  constexpr long long kBudget = 96 * 1024;
+  const long long per_cell = (long long)nbins * S * 8;  // one (node, feature) histogram
+  if (per_cell > kBudget) {
+    hipLaunchKernelGGL((tree_hist_kernel<BinT, true>), dim3(row_blocks, T, 1), dim3(256), 0, stream, bins, n, d,
+                       nbins, node_of, wt, y, cls, S, nodes, d, nodes, 1, scales[0], scales[1], scales[2], out);
+    return;
+  }
+  int fc, nc;
+  if ((long long)nodes * per_cell <= kBudget) {
+    nc = nodes;
+    fc = (int)(kBudget / ((long long)nodes * per_cell));
+    if (fc > d) fc = d;
+  } else {
+    fc = 1;
+    nc = (int)(kBudget / per_cell);
+  }
   const int fchunks = (d + fc - 1) / fc;
-  const size_t lds = (size_t)per_feat * fc;
-  hipFuncSetAttribute((const void*)tree_hist_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL(tree_hist_kernel, dim3(row_blocks, T, fchunks), dim3(256), lds, (hipStream_t)stream, bins, n, d,
-                     nbins, node_of, wt, y, cls, S, nodes, fc, scales[0], scales[1], scales[2], out);
+  const int nchunks = (nodes + nc - 1) / nc;
+  const size_t lds = (size_t)per_cell * fc * nc;
+  hipFuncSetAttribute((const void*)tree_hist_kernel<BinT, false>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                      (int)lds);
+  hipLaunchKernelGGL((tree_hist_kernel<BinT, false>), dim3(row_blocks, T, fchunks * nchunks), dim3(256), lds, stream,
+                     bins, n, d, nbins, node_of, wt, y, cls, S, nodes, fc, nc, fchunks, scales[0], scales[1],
+                     scales[2], out);
+}
+}  // namespace
+
+// out must be zeroed; bin_bytes as for cml_tree_binize.
+CML_API int cml_tree_hist(const void* bins, long long n, int d, int nbins, const int* node_of, int T,
+                          const float* wt, const double* y, const int* cls, int S, int nodes, const double* scales,
+                          unsigned long long* out, int row_blocks, int bin_bytes, void* stream) {
+  if (nodes < 1 || d < 1 || nbins < 1 || S < 1) return (int)hipErrorInvalidValue;
+  if (bin_bytes == 1)
+    launch_hist((const unsigned char*)bins, n, d, nbins, node_of, T, wt, y, cls, S, nodes, scales, out, row_blocks,
+                (hipStream_t)stream);
+  else if (bin_bytes == 2)
+    launch_hist((const unsigned short*)bins, n, d, nbins, node_of, T, wt, y, cls, S, nodes, scales, out, row_blocks,
+                (hipStream_t)stream);
+  else
+    return (int)hipErrorInvalidValue;
   return cml_status();
 }
 
@@ -323,11 +394,18 @@ CML_API int cml_tree_best_split(const long long* hist, int tn, int d, int nbins,
   return cml_status();
 }
 
-CML_API int cml_tree_route(const unsigned char* bins, long long n, int d, int T, int nodes, int* node_of,
+CML_API int cml_tree_route(const void* bins, long long n, int d, int T, int nodes, int* node_of,
                            const int* split_feat, const int* split_bin, const int* left_id, const int* right_id,
-                           void* stream) {
-  hipLaunchKernelGGL(tree_route_kernel, dim3(blocks_for(n * T, 256, 8192)), dim3(256), 0, (hipStream_t)stream, bins,
-                     n, d, T, nodes, node_of, split_feat, split_bin, left_id, right_id);
+                           int bin_bytes, void* stream) {
+  const dim3 grid(blocks_for(n * T, 256, 8192));
+  if (bin_bytes == 1)
+    hipLaunchKernelGGL(tree_route_kernel<unsigned char>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned char*)bins, n, d, T, nodes, node_of, split_feat, split_bin, left_id, right_id);
+  else if (bin_bytes == 2)
+    hipLaunchKernelGGL(tree_route_kernel<unsigned short>, grid, dim3(256), 0, (hipStream_t)stream,
+                       (const unsigned short*)bins, n, d, T, nodes, node_of, split_feat, split_bin, left_id, right_id);
+  else
+    return (int)hipErrorInvalidValue;
   return cml_status();
 }
 

@@ -25,11 +25,7 @@ from .feature import _replace_col
 from .linalg import DenseVector, as_array
 
 
-def java_hash(s: str) -> int:
-    h = 0
-    for ch in s:
-        h = (31 * h + ord(ch)) & 0xFFFFFFFF
-    return h - (1 << 32) if h >= (1 << 31) else h
+from .util import java_hash  # noqa: E402  (re-exported: Spark's default seeds are class-name hashes)
 
 
 _KMEANS_PARAMS = {
@@ -75,9 +71,16 @@ class KMeans(Estimator):
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
-        ckkey = (f"kmeans|n={n_global}|d={d}|k={k}|seed={seed}|init={self.getInitMode()}|"
-                 f"steps={self.getInitSteps()}|tol={self.getTol()}|measure={measure}")
-        resumed = ckpt.load(ckdir, f"kmeans-{self.uid}", ckkey) if ckdir else None
+        ckname = ckkey = None
+        if ckdir:
+            # the key identifies the fit (shape, params and a data fingerprint), and the checkpoint name
+            # is derived from it: a restarted process, whose estimator has a new uid, finds it again
+            fp = _fingerprint(x, comm)
+            ckkey = (f"kmeans|n={n_global}|d={d}|k={k}|seed={seed}|init={self.getInitMode()}|"
+                     f"steps={self.getInitSteps()}|tol={self.getTol()}|measure={measure}|data={fp}")
+            ckname = ckpt.name_for("kmeans", ckkey)
+        # rank 0 decides and broadcasts, so every rank resumes from the same iteration or none does
+        resumed = ckpt.load_shared(ckdir, ckname, ckkey, comm) if ckdir else None
         start = 0
         if resumed is not None:
             start, arrs = resumed
@@ -98,12 +101,12 @@ class KMeans(Estimator):
 
         def on_iter(it):
             if ckdir and (it % max(every, 1) == 0):
-                ckpt.save(ckdir, f"kmeans-{self.uid}", ckkey, it, {"centers": eng.centers.cpu().numpy()}, comm)
+                ckpt.save(ckdir, ckname, ckkey, it, {"centers": eng.centers.cpu().numpy()}, comm)
 
         iters = eng.fit(self.getMaxIter(), self.getTol(), start_iter=start, on_iter=on_iter)
         if ckdir:
             comm.barrier()
-            ckpt.clear(ckdir, f"kmeans-{self.uid}", comm)
+            ckpt.clear(ckdir, ckname, comm)
         centers = eng.centers.cpu().numpy()
         labels, dist = eng.assign()
         sizes = torch.bincount(labels.long(), minlength=eng.k).to(torch.float64) if eng.n else torch.zeros(
@@ -114,6 +117,19 @@ class KMeans(Estimator):
         model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
                                             [int(s) for s in sizes.cpu().tolist()]))
         return model
+
+
+def _fingerprint(x: torch.Tensor, comm) -> str:
+    """Global (Σx, Σx²) of the feature matrix in float64: two fits with the same shape and
+    params but different data never share a checkpoint."""
+    s = torch.zeros(2, dtype=torch.float64, device=x.device)
+    step = max(1, (1 << 24) // max(int(x.shape[1]), 1))  # row chunks of 16M elements: bounded f64 temporaries
+    for r0 in range(0, int(x.shape[0]), step):
+        xf = x[r0:r0 + step].to(torch.float64)
+        s[0] += xf.sum()
+        s[1] += (xf * xf).sum()
+    comm.allreduce_(s)
+    return f"{float(s[0]):.17g},{float(s[1]):.17g}"
 
 
 class KMeansModel(Model):

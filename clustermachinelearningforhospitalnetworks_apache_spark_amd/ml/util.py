@@ -15,6 +15,7 @@ from __future__ import annotations
 import importlib
 import json
 import os
+import re
 import shutil
 import time
 import uuid
@@ -103,6 +104,14 @@ _PY = {
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
 }
+
+
+def java_hash(s: str) -> int:
+    """``java.lang.String.hashCode`` (Spark seeds default to the estimator class name's hash)."""
+    h = 0
+    for ch in s:
+        h = (31 * h + ord(ch)) & 0xFFFFFFFF
+    return h - (1 << 32) if h >= (1 << 31) else h
 
 
 def jvm_class(obj) -> str:
@@ -251,6 +260,41 @@ def matrix_arrow_type():
 
 # ---------------------------------------------------------------------------------------------- writer/reader
 
+def _pid_alive(pid: int) -> bool:
+    try:
+        os.kill(pid, 0)
+    except ProcessLookupError:
+        return False
+    except (PermissionError, OSError):
+        return True
+    return True
+
+
+def recover_save(path: str) -> None:
+    """Finish or roll back a save that crashed between its two renames. MLWriter.save moves the
+    previous model to ``.<name>.old-<pid>`` only after the new one is complete in
+    ``.<name>.tmp-<pid>``, so when ``path`` is missing, a complete new model (the tmp of the same
+    writer) is promoted, else the old model is restored. Leftovers of dead writers are removed.
+    Writers that are still alive are left alone (they finish their own renames)."""
+    parent = os.path.dirname(os.path.abspath(path)) or "."
+    base = os.path.basename(path)
+    try:
+        entries = os.listdir(parent)
+    except FileNotFoundError:
+        return
+    pat = re.compile(r"^\." + re.escape(base) + r"\.(tmp|old)-(\d+)$")
+    dead = {}
+    for e in entries:
+        m = pat.match(e)
+        if m and not _pid_alive(int(m.group(2))):
+            dead.setdefault(int(m.group(2)), {})[m.group(1)] = os.path.join(parent, e)
+    for pid, parts in sorted(dead.items()):
+        if not os.path.exists(path) and "old" in parts:
+            os.replace(parts.pop("tmp") if "tmp" in parts else parts.pop("old"), path)
+        for leftover in parts.values():
+            shutil.rmtree(leftover, ignore_errors=True)
+
+
 class MLWriter:
     def __init__(self, instance):
         self.instance = instance
@@ -273,6 +317,9 @@ class MLWriter:
         from ..io.reader import strip_scheme
         path = strip_scheme(path).rstrip("/")
         comm = _comm()
+        if comm.is_root:
+            recover_save(path)
+        comm.barrier()
         if os.path.exists(path) and not self._overwrite:
             raise FileExistsError(f"Path {path} already exists. To overwrite it, use write().overwrite().save(path)")
         comm.barrier()
@@ -319,6 +366,8 @@ class MLReader:
     def load(self, path: str):
         from ..io.reader import strip_scheme
         path = strip_scheme(path)
+        if not os.path.exists(path):
+            recover_save(path.rstrip("/"))
         md = read_metadata(path)
         cls = py_class_from_jvm(md["class"]) if self.cls is None else self.cls
         return cls._load_impl(path, md)

@@ -12,7 +12,8 @@ Pipeline per fit (each rank holds a row shard, all trees are grown together):
      max(maxBins², 10000) rows is all-gathered, thresholds per feature follow
      Spark's findSplitsForContinuousFeature rule (midpoints between distinct
      values, or count-stride quantiles when there are more than maxBins-1);
-  2. K17 binize: uint8 bin codes [n, d] resident on the device;
+  2. K17 binize: bin codes [n, d] resident on the device — uint8 up to 256 bins (Spark's default
+     maxBins = 32), 16-bit above (maxBins up to MAX_BINS = 32768), so large maxBins never wrap;
   3. per level: K18 histogram of (tree, node, feature, bin) stats for every tree at
      once, ONE all-reduce of the histogram buffer, best split per node on the host
      (identical on every rank), K20 routes rows to children;
@@ -33,12 +34,12 @@ from ..parallel.comm import Communicator, local_comm
 from ..utils import rng
 
 _native.register_kernel_sigs({
-    "cml_tree_binize": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "cml_tree_binize": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_tree_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp,
-                              c_int, c_vp]),
+                              c_int, c_int, c_vp]),
     "cml_tree_best_split": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_dbl, c_dbl,
                                     c_dbl, c_vp, c_vp]),
-    "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
 })
 
@@ -183,6 +184,16 @@ def subset_size(strategy: str, d: int, task: str, num_trees: int) -> int:
 
 # ---------------------------------------------------------------------------------------------- engine
 
+MAX_BINS = 32768  # 16-bit bin codes (int16 storage, read as uint16 by the kernels)
+
+
+def bin_dtype(nbins: int) -> torch.dtype:
+    """Storage type of the bin codes: one byte while every code fits (nbins <= 256), two above."""
+    if nbins > MAX_BINS:
+        raise ValueError(f"maxBins must be <= {MAX_BINS}, got {nbins}")
+    return torch.uint8 if nbins <= 256 else torch.int16
+
+
 class ForestEngine:
     def __init__(self, x: torch.Tensor, y: torch.Tensor, params: TreeParams, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, weights: Optional[torch.Tensor] = None):
@@ -197,6 +208,8 @@ class ForestEngine:
         self.sample_weight = weights
         self.kind = params.impurity
         self.S = 3 if self.kind == "variance" else params.num_classes
+        if not 2 <= params.max_bins <= MAX_BINS:
+            raise ValueError(f"maxBins must be in [2, {MAX_BINS}], got {params.max_bins}")
 
     # -------------------------------------------------------------- splits
     def find_splits(self) -> List[np.ndarray]:
@@ -220,18 +233,20 @@ class ForestEngine:
             thr[j, : len(s)] = s
             ns[j] = len(s)
         self.nbins = ms + 1
+        bdt = bin_dtype(self.nbins)
         if not self.gpu or self.n == 0:
             t = torch.as_tensor(thr, device=self.dev)
-            bins = torch.empty((self.n, self.d), dtype=torch.uint8, device=self.dev)
+            bins = torch.empty((self.n, self.d), dtype=bdt, device=self.dev)
             for j in range(self.d):
                 bins[:, j] = torch.searchsorted(t[j, : max(ns[j], 0)].contiguous(), self.x[:, j].contiguous(),
-                                                right=False).to(torch.uint8) if ns[j] else 0
+                                                right=False).to(bdt) if ns[j] else 0
             return bins
         thr_t = torch.as_tensor(thr, device=self.dev)
         ns_t = torch.as_tensor(ns, device=self.dev)
-        bins = torch.empty((self.n, self.d), dtype=torch.uint8, device=self.dev)
+        bins = torch.empty((self.n, self.d), dtype=bdt, device=self.dev)
         st = _native.kernels().cml_tree_binize(self.x.data_ptr(), self.n, self.x.stride(0), self.d, thr_t.data_ptr(),
-                                               ms, ns_t.data_ptr(), bins.data_ptr(), _native.stream_ptr())
+                                               ms, ns_t.data_ptr(), bins.data_ptr(), bins.element_size(),
+                                               _native.stream_ptr())
         _native.check(st, "tree_binize")
         return bins
 
@@ -265,7 +280,7 @@ class ForestEngine:
                                                  wt.data_ptr() if wt is not None else 0, self.y.data_ptr(),
                                                  cls.data_ptr() if cls is not None else 0, S, nodes,
                                                  self._scales_host.data_ptr(), out.data_ptr(), rb,
-                                                 _native.stream_ptr())
+                                                 bins.element_size(), _native.stream_ptr())
             _native.check(st, "tree_hist")
             return out
         out = torch.zeros((T, nodes, d, nb, S), dtype=torch.float64, device=self.dev)
@@ -306,7 +321,7 @@ class ForestEngine:
         if self.gpu:
             st = _native.kernels().cml_tree_route(bins.data_ptr(), self.n, self.d, T, nodes, node_of.data_ptr(),
                                                   sf.data_ptr(), sb.data_ptr(), li.data_ptr(), ri.data_ptr(),
-                                                  _native.stream_ptr())
+                                                  bins.element_size(), _native.stream_ptr())
             _native.check(st, "tree_route")
             return
         for t in range(T):
@@ -658,7 +673,7 @@ def fit_gbt(x: torch.Tensor, y: torch.Tensor, params: TreeParams, max_iter: int,
             validation_tol: float = 0.01):
     """Gradient-boosted regression trees (Spark ``GradientBoostedTrees.boost``): tree 0 is fit on the
     labels with weight 1, tree m on the pseudo-residuals of the running margin with weight
-    ``step_size``.  Candidate splits and the uint8 bin codes (K16/K17) are built once and reused by
+    ``step_size``.  Candidate splits and the bin codes (K16/K17) are built once and reused by
     every tree; each tree is one level-wise pass of the K18/K19/K20 kernels plus an all-reduce
     per level; the margin is updated in place by K21.  Labels for ``logistic`` must already be
     in {-1, +1}.  ``valid`` (bool per row) holds rows out of training and stops early once the

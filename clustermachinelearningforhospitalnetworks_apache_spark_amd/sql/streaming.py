@@ -222,19 +222,21 @@ class StreamingQuery:
             ckpt = os.path.join(session.catalog.warehouse, "_checkpoints", table or self.name or uuid.uuid4().hex)
         self._ckpt = strip_scheme(ckpt)
         self.runId = uuid.uuid4().hex
+        self._watermark_ms = 0
         self.id = self._load_or_create_id()
         self._stop = threading.Event()
         self._thread: Optional[threading.Thread] = None
         self._error: Optional[BaseException] = None
         self.recentProgress: List[dict] = []
-        self._watermark_ms = 0
         self._lock = threading.Lock()
         self._next_batch = None
 
     # ------------------------------------------------------------------ checkpoint files
     def _load_or_create_id(self) -> str:
+        """Query id from ``metadata`` (created on first start); also restores the event-time
+        watermark from the last commit, so a restarted query does not fall back to 0."""
         comm = self._session._comm
-        qid = None
+        state = None
         if comm.is_root:
             os.makedirs(os.path.join(self._ckpt, "offsets"), exist_ok=True)
             os.makedirs(os.path.join(self._ckpt, "commits"), exist_ok=True)
@@ -247,7 +249,12 @@ class StreamingQuery:
                 qid = uuid.uuid4().hex
                 with open(meta, "w") as fh:
                     json.dump({"id": qid}, fh)
-        return comm.broadcast_object(qid)
+            commits = self._ids("commits")
+            wm = int(self._read_json("commits", commits[-1]).get("nextBatchWatermarkMs", 0)) if commits else 0
+            state = (qid, wm)
+        qid, wm = comm.broadcast_object(state)
+        self._watermark_ms = wm
+        return qid
 
     def _ids(self, sub: str) -> List[int]:
         d = os.path.join(self._ckpt, sub)
@@ -265,9 +272,12 @@ class StreamingQuery:
         os.replace(tmp, p)
 
     def _seen_files(self) -> List[str]:
+        """Files of every PLANNED batch, in batch order. The offsets log is the write-ahead record
+        of a plan (written first), so a file counts as seen only once its batch has an offsets
+        entry: a crash between the two planning writes can never hide a file."""
         seen: List[str] = []
-        for bid in self._ids(os.path.join("sources", "0")):
-            seen += self._read_json(os.path.join("sources", "0"), bid)["files"]
+        for bid in self._ids("offsets"):
+            seen += self._read_json("offsets", bid)["files"]
         return seen
 
     # ------------------------------------------------------------------ planning (rank 0)
@@ -305,6 +315,8 @@ class StreamingQuery:
                 bid = offs[-1]
                 o = self._read_json("offsets", bid)
                 plan = (bid, o["files"], o["batchTimestampMs"], o["batchWatermarkMs"], True)
+                if not os.path.exists(os.path.join(self._ckpt, "sources", "0", str(bid))):
+                    self._write_json(os.path.join("sources", "0"), bid, {"files": o["files"]})
             else:
                 seen = set(self._seen_files())
                 new = self._list_new(seen)
@@ -312,10 +324,13 @@ class StreamingQuery:
                     bid = last_commit + 1
                     ts = int(time.time() * 1000)
                     plan = (bid, new, ts, self._watermark_ms, False)
-                    self._write_json(os.path.join("sources", "0"), bid, {"files": new})
+                    # offsets (the WAL) first: once it exists the batch replays after any crash;
+                    # sources/0 is the file-source log of the same plan (re-written on replay)
                     self._write_json("offsets", bid, {"batchId": bid, "files": new, "batchTimestampMs": ts,
                                                       "batchWatermarkMs": self._watermark_ms,
                                                       "queryId": self.id})
+                    maybe_fail("stream.between_plan_writes", bid)
+                    self._write_json(os.path.join("sources", "0"), bid, {"files": new})
         return comm.broadcast_object(plan)
 
     # ------------------------------------------------------------------ execution

@@ -1,52 +1,123 @@
 """Iteration checkpoints for long fits ("per-iteration optional estimator
 checkpoint so a killed fit can resume"; the reference has no training checkpoint at all).
 
-A checkpoint is a directory ``<dir>/<name>/`` holding ``state.json`` (iteration, a key that
-identifies the fit: data size, k, seed, params) and one ``<array>.npy`` per state array (loaded
-with ``allow_pickle=False``). Rank 0 writes into a temp directory and renames it over the old
-one, so a crash while checkpointing leaves the previous checkpoint intact. Enabled through the
-session conf ``cml.ml.checkpointDir`` (+ ``cml.ml.checkpointInterval``, default 10 iterations).
+Layout of a checkpoint ``<dir>/<name>/``::
+
+    v-00000012/state.json      iteration, the key that identifies the fit (data size, k, seed, params)
+    v-00000012/<array>.npy     one file per state array (loaded with ``allow_pickle=False``)
+    LATEST                     name of the newest complete version ("v-00000012")
+
+Crash safety: rank 0 writes a new version into ``v-<it>.tmp-<pid>``, renames it to ``v-<it>`` (a
+fresh name, so the rename is atomic and never replaces anything), then atomically replaces the
+``LATEST`` pointer file, and only then deletes older versions.  At every instant at least one
+complete version exists and ``load`` finds it: through ``LATEST``, or — if the pointer is missing,
+torn or names a version that is gone — by scanning for the newest ``v-*`` directory that has its
+``state.json`` (written last inside the version, so its presence means the version is complete).
+
+Names are derived from the fit's key (``name_for``), not from an estimator uid, so a restarted
+process (a new uid) finds the checkpoint of the same fit.  ``load_shared`` makes the resume
+decision on rank 0 and broadcasts it with the arrays, so every rank resumes from the same
+iteration or none does (a per-rank decision would desynchronise the collective sequence).
+Enabled through the session conf ``cml.ml.checkpointDir`` (+ ``cml.ml.checkpointInterval``).
 """
 from __future__ import annotations
 
+import hashlib
 import json
 import os
+import re
 import shutil
 from typing import Dict, Optional, Tuple
 
 import numpy as np
 
+_VER = re.compile(r"^v-(\d{8,})$")
+
+
+def name_for(prefix: str, key: str) -> str:
+    """Stable checkpoint name of a fit: the same key in any process or rank gives the same name."""
+    return f"{prefix}-{hashlib.sha1(key.encode()).hexdigest()[:16]}"
+
+
+def _versions(root: str):
+    """Complete versions under ``root``, newest first."""
+    out = []
+    try:
+        entries = os.listdir(root)
+    except FileNotFoundError:
+        return out
+    for e in entries:
+        m = _VER.match(e)
+        if m and os.path.exists(os.path.join(root, e, "state.json")):
+            out.append((int(m.group(1)), e))
+    return [e for _, e in sorted(out, reverse=True)]
+
 
 def save(directory: str, name: str, key: str, iteration: int, arrays: Dict[str, np.ndarray], comm=None) -> None:
     if comm is not None and not comm.is_root:
         return
-    final = os.path.join(directory, name)
+    root = os.path.join(directory, name)
+    os.makedirs(root, exist_ok=True)
+    ver = f"v-{int(iteration):08d}"
+    final = os.path.join(root, ver)
     tmp = final + f".tmp-{os.getpid()}"
-    if os.path.exists(tmp):
-        shutil.rmtree(tmp)
+    shutil.rmtree(tmp, ignore_errors=True)
     os.makedirs(tmp)
     for k, v in arrays.items():
         np.save(os.path.join(tmp, f"{k}.npy"), np.asarray(v), allow_pickle=False)
-    with open(os.path.join(tmp, "state.json"), "w") as fh:
+    with open(os.path.join(tmp, "state.json"), "w") as fh:  # written last: marks the version complete
         json.dump({"key": key, "iteration": int(iteration), "arrays": sorted(arrays)}, fh)
-    old = final + f".old-{os.getpid()}"
-    if os.path.exists(final):
-        os.replace(final, old)
+    if os.path.exists(final):  # same iteration saved again (a resumed fit): retire the old copy first
+        shutil.rmtree(final)
     os.replace(tmp, final)
-    shutil.rmtree(old, ignore_errors=True)
+    ptr_tmp = os.path.join(root, f"LATEST.tmp-{os.getpid()}")
+    with open(ptr_tmp, "w") as fh:
+        fh.write(ver + "\n")
+    os.replace(ptr_tmp, os.path.join(root, "LATEST"))
+    for e in os.listdir(root):  # older versions and leftovers of crashed writers
+        if e not in (ver, "LATEST"):
+            p = os.path.join(root, e)
+            if os.path.isdir(p):
+                shutil.rmtree(p, ignore_errors=True)
+            else:
+                try:
+                    os.remove(p)
+                except FileNotFoundError:
+                    pass
 
 
 def load(directory: str, name: str, key: str) -> Optional[Tuple[int, Dict[str, np.ndarray]]]:
-    final = os.path.join(directory, name)
-    meta = os.path.join(final, "state.json")
-    if not os.path.exists(meta):
-        return None
-    with open(meta) as fh:
-        st = json.load(fh)
-    if st.get("key") != key:
-        return None
-    arrays = {k: np.load(os.path.join(final, f"{k}.npy"), allow_pickle=False) for k in st["arrays"]}
-    return int(st["iteration"]), arrays
+    root = os.path.join(directory, name)
+    cands = []
+    try:
+        with open(os.path.join(root, "LATEST")) as fh:
+            cands.append(fh.read().strip())
+    except (FileNotFoundError, OSError):
+        pass
+    cands += [v for v in _versions(root) if v not in cands]
+    for ver in cands:
+        meta = os.path.join(root, ver, "state.json")
+        try:
+            with open(meta) as fh:
+                st = json.load(fh)
+        except (FileNotFoundError, ValueError, OSError):
+            continue  # missing or torn: try the next complete version
+        if st.get("key") != key:
+            return None
+        try:
+            arrays = {k: np.load(os.path.join(root, ver, f"{k}.npy"), allow_pickle=False) for k in st["arrays"]}
+        except (FileNotFoundError, ValueError, OSError):
+            continue
+        return int(st["iteration"]), arrays
+    return None
+
+
+def load_shared(directory: str, name: str, key: str, comm=None) -> Optional[Tuple[int, Dict[str, np.ndarray]]]:
+    """``load`` on rank 0, broadcast to every rank (decision and arrays)."""
+    if comm is None or not comm.is_distributed:
+        return load(directory, name, key)
+    res = load(directory, name, key) if comm.is_root else None
+    return comm.broadcast_object(res, src=0)
 
 
 def clear(directory: str, name: str, comm=None) -> None:

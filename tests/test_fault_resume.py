@@ -51,8 +51,11 @@ def test_kmeans_resumes_from_checkpoint(spark, tmp_path, monkeypatch):
     with pytest.raises(InjectedFault):
         km.fit(df)
     saved = os.listdir(tmp_path / "ck")
-    assert saved == [f"kmeans-{km.uid}"]
+    assert len(saved) == 1 and saved[0].startswith("kmeans-")
+    assert sorted(os.listdir(tmp_path / "ck" / saved[0])) == ["LATEST", "v-00000006"]
     monkeypatch.delenv("CML_FAULT")
+    # a restarted process builds a NEW estimator (new uid): the key-derived name still finds it
+    km = KMeans(k=4, seed=3, maxIter=12, tol=0.0)
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models import kmeans as engine_mod
     starts = []
     orig = engine_mod.LloydEngine.fit
@@ -67,6 +70,30 @@ def test_kmeans_resumes_from_checkpoint(spark, tmp_path, monkeypatch):
     np.testing.assert_array_equal(np.stack(model.clusterCenters()), want)
     assert model.summary.numIter == 12
     assert os.listdir(tmp_path / "ck") == []  # cleared after a completed fit
+
+
+def test_checkpoint_survives_crash_between_renames(tmp_path):
+    """A writer killed at any point of save() leaves a loadable checkpoint (the old
+    two-rename scheme left none between its renames)."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import checkpoint as ck
+    d = str(tmp_path)
+    name = ck.name_for("kmeans", "key")
+    assert name == ck.name_for("kmeans", "key") and name != ck.name_for("kmeans", "other")
+    ck.save(d, name, "key", 4, {"centers": np.ones((2, 3))})
+    root = tmp_path / name
+    # crash after the new version was renamed into place but before LATEST moved
+    os.makedirs(root / "v-00000006.tmp-999")
+    (root / "v-00000006.tmp-999" / "centers.npy").write_bytes(b"partial")
+    it, arrs = ck.load(d, name, "key")
+    assert it == 4 and arrs["centers"].shape == (2, 3)
+    ck.save(d, name, "key", 6, {"centers": np.zeros((2, 3))})
+    assert sorted(os.listdir(root)) == ["LATEST", "v-00000006"]
+    # LATEST lost or torn: the newest complete version is found by scanning
+    (root / "LATEST").write_text("v-000")
+    assert ck.load(d, name, "key")[0] == 6
+    os.remove(root / "LATEST")
+    assert ck.load(d, name, "key")[0] == 6
+    assert ck.load(d, name, "different-fit") is None
 
 
 def _start(spark, src, ckpt):
@@ -141,3 +168,58 @@ def test_trace_ranges_and_rank_logger(spark, capsys):
     lg.setLevel(logging.INFO)
     lg.info("hello from rank zero")
     assert "[rank 0/1] cml.test INFO: hello from rank zero" in capsys.readouterr().err
+
+
+def test_model_save_crash_between_renames_recovers(spark, tmp_path):
+    """A writer that died after moving the old model aside but before renaming the new one into
+    place: load() promotes the complete new model."""
+    df = _blobs(spark, n=500)
+    path = str(tmp_path / "model")
+    KMeans(k=2, seed=1).fit(df).write().overwrite().save(path)
+    KMeans(k=3, seed=1).fit(df).write().overwrite().save(str(tmp_path / "new"))
+    dead = 2 ** 22 + 12345  # above pid_max on this box: never a live process
+    os.replace(path, str(tmp_path / f".model.old-{dead}"))
+    os.replace(str(tmp_path / "new"), str(tmp_path / f".model.tmp-{dead}"))
+    back = KMeansModel.load(path)
+    assert len(back.clusterCenters()) == 3
+    assert sorted(os.listdir(tmp_path)) == ["model"]
+    # only the old copy survived (the crash hit before the new one was complete): it is restored
+    os.replace(path, str(tmp_path / f".model.old-{dead}"))
+    assert len(KMeansModel.load(path).clusterCenters()) == 3
+    assert sorted(os.listdir(tmp_path)) == ["model"]
+
+
+def test_stream_crash_between_plan_writes_loses_nothing(spark, tmp_path, monkeypatch):
+    """Killed after offsets/<bid> but before sources/0/<bid>: the restart replays
+    the batch from its offsets entry; no file is hidden or read twice."""
+    src, ck = str(tmp_path / "in"), str(tmp_path / "ck")
+    write_csv_files(hospital_frame(90), src, nfiles=3)
+    monkeypatch.setenv("CML_FAULT", "stream.between_plan_writes=0")
+    with pytest.raises(InjectedFault):
+        _start(spark, src, ck)
+    assert os.path.exists(os.path.join(ck, "offsets", "0"))
+    assert not os.path.exists(os.path.join(ck, "sources", "0", "0"))
+    monkeypatch.delenv("CML_FAULT")
+    write_csv_files(hospital_frame(30, seed=5), src, nfiles=1, prefix="late")
+    q = _start(spark, src, ck)
+    progress = {p["batchId"]: p for p in q.recentProgress}
+    assert progress[0]["replayed"] is True and progress[0]["numInputRows"] == 90
+    assert progress[1]["numInputRows"] == 30
+    assert spark.table("t_fault").count() == 120
+    assert os.path.exists(os.path.join(ck, "sources", "0", "0"))
+
+
+def test_stream_restart_restores_watermark(spark, tmp_path):
+    src, ck = str(tmp_path / "in"), str(tmp_path / "ck")
+    write_csv_files(hospital_frame(60), src, nfiles=1)
+
+    def start():
+        sdf = (spark.readStream.option("header", True).schema(hospital_schema()).csv(src)
+               .withWatermark("event_time", "10 minutes"))
+        return (sdf.writeStream.format("delta").outputMode("append").option("checkpointLocation", ck)
+                .trigger(availableNow=True).toTable("t_wm"))
+
+    wm = start().lastProgress["eventTime"]["watermark"]
+    assert wm > 0
+    q = start()  # nothing new to read: the restarted query still reports the committed watermark
+    assert q._watermark_ms == wm
