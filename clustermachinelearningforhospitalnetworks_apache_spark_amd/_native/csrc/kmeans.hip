@@ -453,6 +453,12 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
   }
 }
 
+}  // namespace
+
+#include "kmeans_rr.h"
+
+namespace {
+
 // ||x_i||² of the bf16 rows (f32), once per fit: the assign epilogue then reads 4 B/row
 // instead of re-deriving the norm from the tile (128 converts + FMAs per lane per tile).
 template <int NCH>
@@ -1156,7 +1162,13 @@ long long assign_lds_bytes(int kc, int kp, int Dp) {
 // RT 1 with the next tile's X in flight and more waves per CU.
 // Variant (tuning/experiments): 0 auto, 1 = RT 2 + X double buffer, 2 = RT 1, 3 = RT 4.
 int g_assign_variant = 0;
-int g_assign_sched = 0;  // kmeans_assign_bf16 `sched` (partner-wave desynchronisation), tuning knob
+int g_assign_sched = 0;
+// K9r (kmeans_rr.h, register-resident centres + LDS-DMA X ring) on variant 8, and by default
+// (variant 0) wherever rr::plan_ct accepts the shape while this is set (CML_KMEANS_RR=0 turns it off).
+// Measured (profiles/r2_assign_rr.md): 100M x 256, k = 256: 12.2 vs 13.2 ms; 10M x 128, k = 64: 0.457 vs
+// 0.509 ms.
+int g_rr_default = 1;
+int g_rr_dbg = 0;  // K9r ablation bits (kmeans_rr.h), 0 in production  // kmeans_assign_bf16 `sched` (partner-wave desynchronisation), tuning knob
 inline int assign_threads(int /*DS*/) {
   return g_assign_variant == 4 ? 768 : (g_assign_variant == 5 ? 1024 : 512);
 }
@@ -1299,8 +1311,32 @@ CML_API int cml_kmeans_set_assign_sched(int v) {
   g_assign_sched = v;
   return 0;
 }
+// K9r plan for (Dp, kc): returns the centre tiles per compute wave (0: K9r not used — variant, fp8 rows
+// or shape), out[0] = LDS bytes, out[1] = rows per tile (= rows per workgroup round), out[2] = threads.
+CML_API int cml_kmeans_assign_rr_plan(int Dp, int kc, int kp, int xfp8, long long* out) {
+  if (xfp8 || kc != kp) return 0;
+  if (!(g_assign_variant == 8 || (g_assign_variant == 0 && g_rr_default))) return 0;
+  const int ct = rr::plan_ct(Dp, kc);
+  if (ct == 0) return 0;
+  const long long lds = rr::lds_for(Dp, kp);
+  if (lds <= 0 || lds > 160 * 1024) return 0;
+  out[0] = lds;
+  out[1] = rr::tile_rows(Dp);
+  out[2] = rr::kThreads;
+  return ct;
+}
+CML_API int cml_kmeans_set_rr_debug(int bits) {
+  g_rr_dbg = bits;
+  return 0;
+}
+CML_API int cml_kmeans_set_rr_default(int on) {
+  g_rr_default = on ? 1 : 0;
+  return 0;
+}
+// Rows per wave tile of the K9 launch the current variant selects (sort-regime scatter geometry).
+CML_API int cml_kmeans_assign_tile_rows(int Dp) { return assign_tile_rows(Dp); }
 CML_API int cml_kmeans_set_assign_variant(int v) {
-  if (v < 0 || v > 7) return (int)hipErrorInvalidValue;
+  if (v < 0 || v > 8) return (int)hipErrorInvalidValue;
   g_assign_variant = v;
   return 0;
 }
@@ -1317,7 +1353,7 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
                                    int kc, int kp, int c_base, const float* cnorm, const float* xnorm, int* labels,
                                    float* best, int first, int last, double* cost_part, int* hist, int* rank,
                                    int grid, int xfp8, int* chg_rows, int* chg_old, int* chg_wg_count,
-                                   int* chg_overflow, int chg_pcap,
+                                   int* chg_overflow, int chg_pcap, int rr_ct,
                                    void* stream) {
   if (kc % 16 != 0 || Dp % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
   if (chg_rows != nullptr && (!(first && last) || chg_old == nullptr || chg_wg_count == nullptr ||
@@ -1330,6 +1366,11 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
   if (xnorm == nullptr) return (int)hipErrorInvalidValue;  // ||x||² seeds the accumulators
   hipStream_t st = (hipStream_t)stream;
   const u16* c = (const u16*)C;
+  if (rr_ct > 0) {  // K9r: single launch over every centre, bf16 rows
+    if (xfp8 || !(first && last) || kc != kp || rr::plan_ct(Dp, kc) != rr_ct) return (int)hipErrorInvalidValue;
+    return rr::dispatch(Dp, rr_ct, (const u16*)X, n, ldx, c, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+                        hist, rank, dout, grid, g_rr_dbg, st);
+  }
   if (xfp8) {
     switch (Dp) {
 #define CML_ASSIGN8(DP)                                                                                          \
@@ -1416,11 +1457,11 @@ CML_API int cml_kmeans_reduce(const float* slab, const int* cslab, const double*
   return cml_status();
 }
 
-// Regime B: scan + scatter + segmented accumulate. `nblk`/`nwaves` describe the assign launch
-// that produced hist/rank. msg = [k*D sums | k counts | cost]. `seg` must hold k+1 ints plus
+// Regime B: scan + scatter + segmented accumulate. `nblk`/`round_rows` describe the assign launch
+// that produced hist/rank (workgroup b ranked rows [b·round_rows + i·nblk·round_rows, +round_rows)). msg = [k*D sums | k counts | cost]. `seg` must hold k+1 ints plus
 // 2k+2 ints of scratch (cml_kmeans_seg_ints).
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
-                                  const int* rank, const int* hist, int nblk, int nwaves, int k, int kp,
+                                  const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
                                   int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
                                   void* stream) {
@@ -1440,7 +1481,7 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
   if (n == 0) return 0;
   hipLaunchKernelGGL(kmeans_scatter, dim3(nblk), dim3(kScatterThreads), sizeof(int) * (size_t)k, st,
                      labels, rank, n,
-                     nblk, nwaves, assign_tile_rows(Dp), k, off, perm, gate, want);
+                     nblk, 1, round_rows, k, off, perm, gate, want);
   e = cml_status();
   if (e) return e;
   return launch_segsum(X, n, ldx, Dp, D, perm, seg, k, cpl, seg_grid, msg, slots, slot_c, xfp8, gate, want, st);

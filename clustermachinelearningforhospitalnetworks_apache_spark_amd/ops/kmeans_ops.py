@@ -7,6 +7,7 @@ numerical oracle of the tests).
 """
 from __future__ import annotations
 
+import ctypes
 import os
 
 from dataclasses import dataclass
@@ -27,7 +28,11 @@ _native.register_kernel_sigs({
     "cml_kmeans_seg_ints": (c_ll, [c_int]),
     "cml_kmeans_assign_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp,
                                        c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp,
-                                       c_int, c_vp]),
+                                       c_int, c_int, c_vp]),
+    "cml_kmeans_assign_rr_plan": (c_int, [c_int, c_int, c_int, c_int, c_vp]),
+    "cml_kmeans_set_rr_default": (c_int, [c_int]),
+    "cml_kmeans_set_rr_debug": (c_int, [c_int]),
+    "cml_kmeans_assign_tile_rows": (c_int, [c_int]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_priv_lds_bytes": (c_ll, [c_int, c_int, c_int]),
@@ -56,6 +61,8 @@ class AssignPlan:
     kc: int            # centres per launch (multiple of 32)
     grid: int
     nwaves: int
+    round_rows: int = 0  # rows a workgroup ranks per round (sort-regime scatter geometry)
+    rr_ct: int = 0       # > 0: K9r (register-resident centres, LDS-DMA X ring), centre tiles per wave
 
 
 @dataclass
@@ -85,9 +92,33 @@ def is_fp8(x: torch.Tensor) -> bool:
     return x.dtype == FP8
 
 
+_ENV_APPLIED = False
+
+
+def _apply_env_knobs(lib) -> None:
+    """CML_KMEANS_ASSIGN_VARIANT / CML_KMEANS_RR (0/1) set the K9 launch knobs once per process."""
+    global _ENV_APPLIED
+    if _ENV_APPLIED:
+        return
+    _ENV_APPLIED = True
+    v = os.environ.get("CML_KMEANS_ASSIGN_VARIANT")
+    if v:
+        _native.check(lib.cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
+    rr = os.environ.get("CML_KMEANS_RR")
+    if rr:
+        _native.check(lib.cml_kmeans_set_rr_default(int(rr)), "set_rr_default")
+
+
 def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = False) -> AssignPlan:
     lib = _native.kernels()
+    _apply_env_knobs(lib)
     kp = round_up(max(k, 1), 32)
+    out = (ctypes.c_longlong * 3)()
+    ct = lib.cml_kmeans_assign_rr_plan(dp, kp, kp, int(fp8), ctypes.addressof(out))
+    if ct > 0:  # K9r: one 512-thread workgroup per CU, TR-row tiles dealt round-robin
+        tr = int(out[1])
+        grid = max(1, min((n + tr - 1) // tr, num_cus(device_index)))
+        return AssignPlan(n=n, dp=dp, kp=kp, kc=kp, grid=grid, nwaves=1, round_rows=tr, rr_ct=int(ct))
     kc = kp
     while kc > 32 and lib.cml_kmeans_assign_lds_bytes(kc, kp, dp) > LDS_BUDGET:
         kc -= 32
@@ -102,12 +133,20 @@ def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = Fals
             per_cu = max(1, min(per_cu, occ))
     ntiles = (n + 31) // 32
     grid = max(1, min((ntiles + waves - 1) // waves, num_cus(device_index) * per_cu))
-    return AssignPlan(n=n, dp=dp, kp=kp, kc=kc, grid=grid, nwaves=waves)
+    return AssignPlan(n=n, dp=dp, kp=kp, kc=kc, grid=grid, nwaves=waves,
+                      round_rows=waves * lib.cml_kmeans_assign_tile_rows(dp))
 
 
 def set_assign_variant(v: int) -> None:
-    """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD, ..., 6 default shape with per-sub-tile accumulator seeding)."""
+    """Tuning knob for the K9 launch shape (0 auto, 1 one wave/SIMD, 2 two waves/SIMD, ..., 6 default shape with
+    per-sub-tile accumulator seeding, 7 PACK4 keys, 8 K9r register-resident centres + LDS-DMA X ring).
+    Plans made before a change keep the kernel they were made for."""
     _native.check(_native.kernels().cml_kmeans_set_assign_variant(int(v)), "set_assign_variant")
+
+
+def set_rr_default(on: bool) -> None:
+    """Whether variant 0 (auto) picks K9r wherever it applies."""
+    _native.check(_native.kernels().cml_kmeans_set_rr_default(int(bool(on))), "set_rr_default")
 
 
 def set_assign_sched(v: int) -> None:
@@ -188,7 +227,8 @@ def assign_bf16(x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch
             plan.grid, int(is_fp8(x)),
             delta.rows.data_ptr() if delta is not None else 0, delta.old.data_ptr() if delta is not None else 0,
             delta.wg_count.data_ptr() if delta is not None else 0,
-            delta.overflow.data_ptr() if delta is not None else 0, delta.pcap if delta is not None else 0, st)
+            delta.overflow.data_ptr() if delta is not None else 0, delta.pcap if delta is not None else 0,
+            plan.rr_ct, st)
         _native.check(status, "kmeans_assign_bf16")
 
 
@@ -238,7 +278,7 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
     With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full."""
     lib = _native.kernels()
     status = lib.cml_kmeans_sort_accum(x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(),
-                                       hist.data_ptr(), aplan.grid, aplan.nwaves, k, aplan.kp,
+                                       hist.data_ptr(), aplan.grid, aplan.round_rows, k, aplan.kp,
                                        cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
                                        perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
                                        slots[0].data_ptr(), slots[1].data_ptr(), int(is_fp8(x)),

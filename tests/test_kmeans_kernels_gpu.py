@@ -46,12 +46,18 @@ def test_assign_matches_reference(n, d, k, cached_norm):
 
 @pytest.fixture
 def assign_variant(request):
-    K.set_assign_variant(request.param)
-    yield request.param
+    """Variant 0 here is the default dispatch (K9r where it applies, else K9); 9 = K9 forced (variant 0
+    with the K9r default switched off)."""
+    v = request.param
+    K.set_assign_variant(0 if v == 9 else v)
+    if v == 9:
+        K.set_rr_default(False)
+    yield v
     K.set_assign_variant(0)
+    K.set_rr_default(True)
 
 
-@pytest.mark.parametrize("assign_variant", [0, 1, 2, 3], indirect=True)
+@pytest.mark.parametrize("assign_variant", [0, 1, 2, 3, 8, 9], indirect=True)
 @pytest.mark.parametrize("mode", [None, "sort"])
 @pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (50000, 256, 256), (9999, 100, 70), (2000, 16, 3),
                                    (3000, 512, 40), (40000, 128, 64)])
@@ -182,3 +188,94 @@ def test_graph_replay_matches_eager(n, d, k, mode):
         assert (eng._graph is not None) == use_graph
     assert torch.equal(out[False][0], out[True][0]) and torch.equal(out[False][1], out[True][1])
     assert out[False][2] == out[True][2]
+
+
+@pytest.mark.parametrize("n,d,k", [(20000, 256, 256), (50_001, 128, 64), (3001, 512, 40), (777, 200, 33),
+                                   (100_000, 256, 250), (65, 128, 64), (130_000, 100, 100)])
+def test_rr_assign_matches_k9(n, d, k):
+    """K9r (register-resident centres, LDS-DMA X ring; variant 8) against K9 and the f64 reference:
+    same labels up to near ties, same distances, cost and counting-sort histogram/ranks."""
+    torch.manual_seed(11)
+    dev = torch.device("cuda")
+    x = torch.randn(n, d, device=dev) * 2
+    c = x[torch.randperm(n, device=dev)[:k]] + 0.1 * torch.randn(k, d, device=dev)
+    xm = to_device_matrix(x, d)
+    dp = xm.shape[1]
+    xn = K.row_sqnorm(xm, n, dp)
+    out = {}
+    for v in (0, 8):
+        K.set_assign_variant(v)
+        K.set_rr_default(False)  # variant 0 = K9 here
+        try:
+            plan = K.plan_assign(n, dp, k)
+            assert (plan.rr_ct > 0) == (v == 8)
+            cb = torch.zeros((plan.kp, dp), dtype=torch.bfloat16, device=dev)
+            cn = torch.zeros(plan.kp, dtype=torch.float32, device=dev)
+            cent = c.double().contiguous().clone()
+            K.update_centers(None, k, d, cent, cb, dp, plan.kp, cn, None)
+            labels = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            best = torch.zeros(n, dtype=torch.float32, device=dev)
+            cost = torch.zeros(plan.grid, dtype=torch.float64, device=dev)
+            hist = torch.zeros(plan.grid * plan.kp, dtype=torch.int32, device=dev)
+            rank = torch.zeros(n, dtype=torch.int32, device=dev)
+            K.assign_bf16(xm, n, dp, cb, cn, plan, labels, best, cost, hist, rank, xnorm=xn)
+            torch.cuda.synchronize()
+            out[v] = (labels.cpu().long(), best.cpu().double(), float(cost.sum()), hist.view(plan.grid, plan.kp).cpu(),
+                      rank.cpu(), plan)
+        finally:
+            K.set_assign_variant(0)
+            K.set_rr_default(True)
+    lab, best, cost, hist, rank, plan = out[8]
+    ref_lab, ref_d, gap = _ref_assign(x.to(torch.bfloat16), c.to(torch.bfloat16))
+    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
+    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
+    assert (lab == out[0][0]).float().mean() > 0.999
+    np.testing.assert_allclose(best.numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
+    assert abs(cost - best.sum().item()) <= 1e-6 * abs(cost) + 1e-6
+    # counting-sort first pass: per-workgroup histograms sum to the label counts, ranks are a
+    # permutation of 0..count-1 inside every (workgroup, label) run of the rows that workgroup owns
+    np.testing.assert_array_equal(hist.sum(0)[:k].numpy(), torch.bincount(lab, minlength=k).numpy())
+    rows = torch.arange(n)
+    blk = (rows // plan.round_rows) % plan.grid
+    key = blk * plan.kp + lab
+    order = torch.argsort(key * n + rank.long())
+    ks, rs = key[order], rank.long()[order]
+    first = torch.ones(n, dtype=torch.bool)
+    first[1:] = ks[1:] != ks[:-1]
+    start = torch.cummax(torch.where(first, torch.arange(n), torch.zeros(n, dtype=torch.long)), 0).values
+    assert torch.equal(rs, torch.arange(n) - start)
+
+
+@pytest.mark.parametrize("n,d,k", [(300_000, 256, 256), (200_000, 128, 64)])
+def test_rr_lloyd_fit_matches_k9(n, d, k):
+    """Whole fits with K9r (incremental sums, graph replay): after every step the centres are exactly
+    the means of the rows under the engine's own labels (the incremental sums stay exact), and the fit
+    tracks the K9 fit (near-tie label flips make the two trajectories drift apart slightly)."""
+    torch.manual_seed(12)
+    cen = torch.randn(k, d, device="cuda") * 4
+    x = (cen[torch.randint(0, k, (n,), device="cuda")] + torch.randn(n, d, device="cuda")).to(torch.bfloat16)
+    init = x[:k].double().cpu().numpy()
+    xs = x.double().cpu()
+    res = {}
+    for v in (0, 8):
+        K.set_assign_variant(v)
+        K.set_rr_default(False)  # variant 0 = K9 here
+        try:
+            eng = LloydEngine(x, d, k)
+            assert (eng.aplan.rr_ct > 0) == (v == 8)
+            eng.set_centers(init)
+            for _ in range(6):
+                prev = eng.centers.cpu().clone()
+                eng.step()
+                torch.cuda.synchronize()
+                lab = eng.labels[:n].cpu().long()
+                sums, counts = K.sums_reference(xs, lab, k)
+                want = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], prev)
+                np.testing.assert_allclose(eng.centers.cpu().numpy(), want.numpy(), rtol=1e-9, atol=1e-9)
+            res[v] = (eng.centers.cpu(), eng.training_cost(), eng.labels[:n].cpu())
+        finally:
+            K.set_assign_variant(0)
+            K.set_rr_default(True)
+    agree = (res[0][2] == res[8][2]).float().mean().item()
+    assert agree > 0.99, agree
+    assert abs(res[8][1] - res[0][1]) <= 1e-3 * abs(res[0][1])
