@@ -1314,14 +1314,14 @@ CML_API int cml_kmeans_set_assign_sched(int v) {
 // K9r plan for (Dp, kc): returns the centre tiles per compute wave (0: K9r not used — variant, fp8 rows
 // or shape), out[0] = LDS bytes, out[1] = rows per tile (= rows per workgroup round), out[2] = threads.
 CML_API int cml_kmeans_assign_rr_plan(int Dp, int kc, int kp, int xfp8, long long* out) {
-  if (xfp8 || kc != kp) return 0;
+  if (kc != kp) return 0;
   if (!(g_assign_variant == 8 || (g_assign_variant == 0 && g_rr_default))) return 0;
-  const int ct = rr::plan_ct(Dp, kc);
+  const int ct = rr::plan_ct(Dp, kc, xfp8 != 0);
   if (ct == 0) return 0;
-  const long long lds = rr::lds_for(Dp, kp);
+  const long long lds = rr::lds_for(Dp, kp, xfp8 != 0);
   if (lds <= 0 || lds > 160 * 1024) return 0;
   out[0] = lds;
-  out[1] = rr::tile_rows(Dp);
+  out[1] = rr::tile_rows(Dp, xfp8 != 0);
   out[2] = rr::kThreads;
   return ct;
 }
@@ -1366,9 +1366,9 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
   if (xnorm == nullptr) return (int)hipErrorInvalidValue;  // ||x||² seeds the accumulators
   hipStream_t st = (hipStream_t)stream;
   const u16* c = (const u16*)C;
-  if (rr_ct > 0) {  // K9r: single launch over every centre, bf16 rows
-    if (xfp8 || !(first && last) || kc != kp || rr::plan_ct(Dp, kc) != rr_ct) return (int)hipErrorInvalidValue;
-    return rr::dispatch(Dp, rr_ct, (const u16*)X, n, ldx, c, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+  if (rr_ct > 0) {  // K9r: single launch over every centre
+    if (!(first && last) || kc != kp || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
+    return rr::dispatch(Dp, rr_ct, xfp8 != 0, X, n, ldx, c, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
                         hist, rank, dout, grid, g_rr_dbg, st);
   }
   if (xfp8) {

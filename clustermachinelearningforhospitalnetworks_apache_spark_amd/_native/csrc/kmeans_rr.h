@@ -44,10 +44,10 @@ constexpr int kCompute = 4;
 constexpr int kRedStride = 17;  // dwords per row of the key exchange: 16 keys + 1 pad (conflict-free writes)
 constexpr int kNS = 4;          // X ring slots
 
-template <int DP>
+template <int DP, bool F8 = false>
 struct Geo {
   static constexpr int KS = DP / 32;            // MFMA k-steps per row
-  static constexpr int ROWB = DP * 2;           // bytes per bf16 row
+  static constexpr int ROWB = F8 ? DP : DP * 2; // bytes per row (bf16, or OCP e4m3fn bytes)
   static constexpr int TR = 32768 / ROWB;       // rows per tile (32 KiB of X)
   static constexpr int NSUB = TR / 16;          // 16-row MFMA sub-tiles per tile
   static constexpr int SLOT = TR * ROWB;        // 32 KiB
@@ -61,9 +61,9 @@ struct Geo {
 };
 
 // LDS layout (bytes): [X ring NS*SLOT | trailers NTR*TRB | keys 2*RED | hist kp ints | misc 64 B]
-template <int DP>
+template <int DP, bool F8 = false>
 __host__ __device__ constexpr long long lds_bytes(int kp) {
-  using G = Geo<DP>;
+  using G = Geo<DP, F8>;
   return (long long)kNS * G::SLOT + (long long)G::NTR * G::TRB + 2LL * G::RED + 4LL * ((kp + 3) & ~3) + 64;
 }
 
@@ -91,12 +91,13 @@ __device__ __forceinline__ void glds4(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
 
-template <int DP>
-__device__ __forceinline__ void issue_tile(const u16* __restrict__ X, long long ldx, long long n,
+// ldx in BYTES; rows are 16-B aligned.
+template <int DP, bool F8>
+__device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, long long ldx, long long n,
                                            const float* __restrict__ xnorm, const int* __restrict__ labels,
                                            long long tile, int slot, int tr, int dw, int lane,
                                            unsigned char* smem) {
-  using G = Geo<DP>;
+  using G = Geo<DP, F8>;
   const long long row0 = tile * G::TR;
   unsigned char* sdst = smem + slot * G::SLOT;
 #pragma unroll
@@ -107,7 +108,7 @@ __device__ __forceinline__ void issue_tile(const u16* __restrict__ X, long long 
     const int gch = pos ^ (R & 15);                      // global chunk stored there
     long long grow = row0 + R;
     grow = grow < n ? grow : n - 1;                      // rows past n: any valid row (discarded)
-    glds16(X + grow * ldx + 8 * gch, sdst + p * 1024);
+    glds16(X + grow * ldx + 16 * gch, sdst + p * 1024);
   }
   unsigned char* tdst = smem + kNS * G::SLOT + tr * G::TRB + (dw ? G::TR * 4 : 0);
 #pragma unroll
@@ -122,15 +123,19 @@ __device__ __forceinline__ void issue_tile(const u16* __restrict__ X, long long 
   }
 }
 
-template <int DP, int CT>
+// F8: X rows are OCP e4m3fn bytes (SURVEY config 5). They travel through the ring as bytes (half the
+// HBM and LDS traffic) and every compute wave widens its fragments with v_cvt_scalef32_pk_bf16_fp8
+// (exact: e4m3 values are a subset of bf16); one 16-B read then covers TWO k-steps, step 2v+h of lane
+// (r, g) holding k = 64v + 16g + 8h + j, and the centre fragments follow the same k order.
+template <int DP, int CT, bool F8>
 __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
-    const u16* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc, int kc,
+    const unsigned char* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc, int kc,
     int kp, const float* __restrict__ cnorm, const float* __restrict__ xnorm, int* __restrict__ labels,
     float* __restrict__ best_out, double* __restrict__ cost_part, int* __restrict__ hist_out,
     int* __restrict__ rank_out, DeltaOut dout, int dbg) {
   // dbg (ablation only, 0 in production): bit 0 DMA waves issue nothing, bit 1 compute waves skip
   // their MFMAs/keys, bit 2 finalize waves skip the epilogue
-  using G = Geo<DP>;
+  using G = Geo<DP, F8>;
   constexpr int KS = G::KS;
   constexpr int CPW = CT * 16;  // centres per compute wave
   constexpr int TAGB = 2 + (CT > 1) + (CT > 2) + (CT > 4);
@@ -160,7 +165,8 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
 #pragma unroll
       for (int s = 0; s < KS; ++s) {
         uint4 v = make_uint4(0u, 0u, 0u, 0u);
-        if (c < kc) v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + 32 * s + 8 * g);
+        const int k0 = F8 ? 64 * (s >> 1) + 16 * g + 8 * (s & 1) : 32 * s + 8 * g;
+        if (c < kc) v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + k0);
         const unsigned w4[4] = {v.x, v.y, v.z, v.w};
         unsigned o[4];
 #pragma unroll
@@ -196,39 +202,61 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       // fragment of step u+PF is read while step u's MFMAs issue (a scheduling barrier per step pins
       // it: left alone, the scheduler issued each read one step ahead, 4 MFMAs = 64 cycles, under the
       // LDS latency), and the previous sub-tile's key updates ride in the VALU gaps.
-      constexpr int NST = G::NSUB * KS;
+      constexpr int SPU = F8 ? 2 : 1;      // k-steps per 16-B LDS read unit
+      constexpr int UPS = KS / SPU;        // read units per sub-tile
+      constexpr int NU = G::NSUB * UPS;
       constexpr int PF = 3;
       float xnv[G::NSUB];
 #pragma unroll
       for (int t = 0; t < G::NSUB; ++t) xnv[t] = tn[16 * t + r];
       auto xaddr = [&](int u) {
-        const int t = u / KS, s = u % KS;
-        return xs + 16 * t * G::ROWB + 256 * (s >> 2) + boff[s & 3];
+        const int t = u / UPS, v = u % UPS;
+        return xs + 16 * t * G::ROWB + 256 * (v >> 2) + boff[v & 3];
       };
-      bf16x8 xf[PF + 1];
+      uint4 xr[PF + 1];
 #pragma unroll
-      for (int u = 0; u < PF && u < NST; ++u) xf[u] = *reinterpret_cast<const bf16x8*>(xaddr(u));
+      for (int u = 0; u < PF && u < NU; ++u) xr[u] = *reinterpret_cast<const uint4*>(xaddr(u));
       f32x4 acc[2][CT];
       int key[2] = {0x7fffffff, 0x7fffffff};
 #pragma unroll
-      for (int u = 0; u < NST; ++u) {
-        const int t = u / KS, s = u % KS, cur = t & 1, prv = cur ^ 1;
-        if (u + PF < NST) xf[(u + PF) % (PF + 1)] = *reinterpret_cast<const bf16x8*>(xaddr(u + PF));
-        if (s == 0) key[cur] = 0x7fffffff;
+      for (int u = 0; u < NU; ++u) {
+        const int t = u / UPS, v = u % UPS, cur = t & 1, prv = cur ^ 1;
+        if (u + PF < NU) xr[(u + PF) % (PF + 1)] = *reinterpret_cast<const uint4*>(xaddr(u + PF));
+        bf16x8 xb[SPU];
+        if constexpr (F8) {
+          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
+          const uint4 w = xr[u % (PF + 1)];
+          const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+          unsigned o[8];
 #pragma unroll
-        for (int ct = 0; ct < CT; ++ct)
-          acc[cur][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
-              creg[ct][s], xf[u % (PF + 1)], s == 0 ? (c4[ct] + xnv[t]) : acc[cur][ct], 0, 0, 0);
-        if (t > 0) {  // keys of the previous sub-tile, spread over this one's k-steps
-#pragma unroll
-          for (int e = (s * CT * 4) / KS; e < ((s + 1) * CT * 4) / KS; ++e) {
-            const int ct = e >> 2, i = e & 3;
-            const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
-            key[prv] = kv < key[prv] ? kv : key[prv];
+          for (int q = 0; q < 4; ++q) {
+            o[2 * q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(ws[q], 1.0f, false));
+            o[2 * q + 1] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(ws[q], 1.0f, true));
           }
-          if (s == KS - 1) kred[(16 * (t - 1) + r) * kRedStride + wave * 4 + g] = key[prv];
+          xb[0] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+          xb[SPU - 1] = __builtin_bit_cast(bf16x8, make_uint4(o[4], o[5], o[6], o[7]));
+        } else {
+          xb[0] = __builtin_bit_cast(bf16x8, xr[u % (PF + 1)]);
         }
-        __builtin_amdgcn_sched_barrier(0);  // keep every step's read PF steps ahead of its use
+#pragma unroll
+        for (int h = 0; h < SPU; ++h) {
+          const int s = v * SPU + h;
+          if (s == 0) key[cur] = 0x7fffffff;
+#pragma unroll
+          for (int ct = 0; ct < CT; ++ct)
+            acc[cur][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                creg[ct][s], xb[h], s == 0 ? (c4[ct] + xnv[t]) : acc[cur][ct], 0, 0, 0);
+          if (t > 0) {  // keys of the previous sub-tile, spread over this one's k-steps
+#pragma unroll
+            for (int e = (s * CT * 4) / KS; e < ((s + 1) * CT * 4) / KS; ++e) {
+              const int ct = e >> 2, i = e & 3;
+              const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
+              key[prv] = kv < key[prv] ? kv : key[prv];
+            }
+            if (s == KS - 1) kred[(16 * (t - 1) + r) * kRedStride + wave * 4 + g] = key[prv];
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);  // keep every unit's read PF units ahead of its use
       }
       {
         constexpr int t = G::NSUB - 1, cur = t & 1;
@@ -247,14 +275,14 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     // ------------------------------------------------------------------ LDS-DMA waves
     const int dw = wave - kCompute;
     for (long long j = 0; j < kNS - 1 && j < nt && !(dbg & 1); ++j)
-      issue_tile<DP>(X, ldx, n, xnorm, labels, tile_of(j), (int)j, (int)j, dw, lane, smem);
+      issue_tile<DP, F8>(X, ldx, n, xnorm, labels, tile_of(j), (int)j, (int)j, dw, lane, smem);
     if (nt >= kNS - 1) wait_vm<(kNS - 2) * G::CNT>();
     else wait_vm<0>();
     barrier();  // B(-1)
     for (long long j = 0; j < nt; ++j) {
       const long long jn = j + kNS - 1;
       if (jn < nt && !(dbg & 1)) {
-        issue_tile<DP>(X, ldx, n, xnorm, labels, tile_of(jn), (int)(jn % kNS), (int)(jn % G::NTR), dw, lane,
+        issue_tile<DP, F8>(X, ldx, n, xnorm, labels, tile_of(jn), (int)(jn % kNS), (int)(jn % G::NTR), dw, lane,
                        smem);
         wait_vm<(kNS - 2) * G::CNT>();  // tile j+1 has landed; j+2 .. j+NS-1 stay in flight
       } else {
@@ -351,9 +379,10 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
 }
 
 // Centre tiles per compute wave for kc centres (kc <= 64·CT), or 0 when K9r does not apply
-// (fp8 rows, D outside {128, 256, 512}, or the centres do not fit 128 VGPRs per lane).
-inline int plan_ct(int Dp, int kc) {
+// (D outside {128, 256, 512} — {256, 512} for fp8 rows —, or the centres do not fit 128 VGPRs per lane).
+inline int plan_ct(int Dp, int kc, bool f8 = false) {
   if (Dp != 128 && Dp != 256 && Dp != 512) return 0;
+  if (f8 && Dp < 256) return 0;
   const int ct = (kc + 63) / 64;
   if (ct > 4) return 0;  // CT = 8 spills at 256 VGPRs
   const int c = ct <= 1 ? 1 : (ct <= 2 ? 2 : 4);
@@ -361,7 +390,14 @@ inline int plan_ct(int Dp, int kc) {
   return c;
 }
 
-inline long long lds_for(int Dp, int kp) {
+inline long long lds_for(int Dp, int kp, bool f8 = false) {
+  if (f8) {
+    switch (Dp) {
+      case 256: return lds_bytes<256, true>(kp);
+      case 512: return lds_bytes<512, true>(kp);
+      default: return 0;
+    }
+  }
   switch (Dp) {
     case 128: return lds_bytes<128>(kp);
     case 256: return lds_bytes<256>(kp);
@@ -370,31 +406,36 @@ inline long long lds_for(int Dp, int kp) {
   }
 }
 
-inline int tile_rows(int Dp) { return Dp > 0 ? 32768 / (2 * Dp) : 0; }
+inline int tile_rows(int Dp, bool f8 = false) { return Dp > 0 ? 32768 / ((f8 ? 1 : 2) * Dp) : 0; }
 
-template <int DP, int CT>
-int launch(const u16* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp, const float* cnorm,
+// X: bf16 rows (ldx elements) or, with f8, e4m3fn rows (ldx bytes).
+template <int DP, int CT, bool F8>
+int launch(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp, const float* cnorm,
            const float* xnorm, int* labels, float* best, double* cost_part, int* hist, int* rank, DeltaOut dout,
            int grid, int dbg, hipStream_t st) {
-  const size_t lds = (size_t)lds_bytes<DP>(kp);
+  const size_t lds = (size_t)lds_bytes<DP, F8>(kp);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const void* fn = (const void*)kmeans_assign_rr<DP, CT>;
+  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT>), dim3(grid), dim3(kThreads), lds, st, X, n, ldx, C, ldc, kc, kp,
-                     cnorm, xnorm, labels, best, cost_part, hist, rank, dout, dbg);
+  const long long ldb = F8 ? ldx : 2 * ldx;
+  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8>), dim3(grid), dim3(kThreads), lds, st,
+                     (const unsigned char*)X, n, ldb, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist,
+                     rank, dout, dbg);
   return cml_status();
 }
 
-inline int dispatch(int Dp, int ct, const u16* X, long long n, long long ldx, const u16* C, long long ldc, int kc,
-                    int kp, const float* cnorm, const float* xnorm, int* labels, float* best, double* cost_part,
-                    int* hist, int* rank, DeltaOut dout, int grid, int dbg, hipStream_t st) {
-#define CML_RR(D, T)                                                                                             \
-  if (Dp == D && ct == T)                                                                                        \
-  return launch<D, T>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, grid, dbg, \
-                      st)
-  CML_RR(128, 1); CML_RR(128, 2); CML_RR(128, 4);
-  CML_RR(256, 1); CML_RR(256, 2); CML_RR(256, 4);
-  CML_RR(512, 1); CML_RR(512, 2);
+inline int dispatch(int Dp, int ct, bool f8, const void* X, long long n, long long ldx, const u16* C, long long ldc,
+                    int kc, int kp, const float* cnorm, const float* xnorm, int* labels, float* best,
+                    double* cost_part, int* hist, int* rank, DeltaOut dout, int grid, int dbg, hipStream_t st) {
+#define CML_RR(D, T, F)                                                                                             \
+  if (Dp == D && ct == T && f8 == F)                                                                                \
+  return launch<D, T, F>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, grid, \
+                         dbg, st)
+  CML_RR(128, 1, false); CML_RR(128, 2, false); CML_RR(128, 4, false);
+  CML_RR(256, 1, false); CML_RR(256, 2, false); CML_RR(256, 4, false);
+  CML_RR(512, 1, false); CML_RR(512, 2, false);
+  CML_RR(256, 1, true); CML_RR(256, 2, true); CML_RR(256, 4, true);
+  CML_RR(512, 1, true); CML_RR(512, 2, true);
 #undef CML_RR
   return (int)hipErrorInvalidValue;
 }

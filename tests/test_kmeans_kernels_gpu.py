@@ -279,3 +279,43 @@ def test_rr_lloyd_fit_matches_k9(n, d, k):
     agree = (res[0][2] == res[8][2]).float().mean().item()
     assert agree > 0.99, agree
     assert abs(res[8][1] - res[0][1]) <= 1e-3 * abs(res[0][1])
+
+
+@pytest.mark.parametrize("n,d,k", [(40_000, 512, 128), (30_001, 256, 256), (5_000, 300, 40)])
+def test_rr_fp8_assign_matches_k9(n, d, k):
+    """K9r on OCP e4m3fn rows (SURVEY config 5): fragments widened in registers by
+    v_cvt_scalef32_pk_bf16_fp8 give the labels/distances of K9's fp8 path and of the bf16 reference
+    on the dequantised values."""
+    torch.manual_seed(13)
+    dev = torch.device("cuda")
+    x8 = (torch.randn(n, d, device=dev) * 1.5).to(torch.float8_e4m3fn)
+    xd = x8.to(torch.float32)
+    c = xd[torch.randperm(n, device=dev)[:k]] + 0.05 * torch.randn(k, d, device=dev)
+    xm = to_device_matrix(x8, d)
+    dp = xm.shape[1]
+    xn = K.row_sqnorm(xm, n, dp)
+    out = {}
+    for v in (0, 8):
+        K.set_assign_variant(v)
+        K.set_rr_default(False)
+        try:
+            plan = K.plan_assign(n, dp, k, fp8=True)
+            assert (plan.rr_ct > 0) == (v == 8)
+            cb = torch.zeros((plan.kp, dp), dtype=torch.bfloat16, device=dev)
+            cn = torch.zeros(plan.kp, dtype=torch.float32, device=dev)
+            K.update_centers(None, k, d, c.double().contiguous().clone(), cb, dp, plan.kp, cn, None)
+            labels = torch.full((n,), -1, dtype=torch.int32, device=dev)
+            best = torch.zeros(n, dtype=torch.float32, device=dev)
+            cost = torch.zeros(plan.grid, dtype=torch.float64, device=dev)
+            K.assign_bf16(xm, n, dp, cb, cn, plan, labels, best, cost, xnorm=xn)
+            torch.cuda.synchronize()
+            out[v] = (labels.cpu().long(), best.cpu().double())
+        finally:
+            K.set_assign_variant(0)
+            K.set_rr_default(True)
+    ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), c.to(torch.bfloat16))
+    lab, best = out[8]
+    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
+    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
+    assert (lab == out[0][0]).float().mean() > 0.999
+    np.testing.assert_allclose(best.numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
