@@ -5,6 +5,7 @@ from .dataframe import DataFrame, DataFrameNaFunctions
 from .group import GroupedData
 from .session import SparkSession, Session
 from .types import Row
+from .window import Window, WindowSpec
 
 __all__ = ["SparkSession", "Session", "DataFrame", "DataFrameNaFunctions", "Column", "Row", "GroupedData",
-           "functions", "types"]
+           "functions", "types", "Window", "WindowSpec"]

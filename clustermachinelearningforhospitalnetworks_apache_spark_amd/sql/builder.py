@@ -62,7 +62,8 @@ def column_from_values(values, dtype: T.DataType, device) -> ColumnData:
                 valid[i] = False
                 out[i] = None
             else:
-                out[i] = v if isinstance(dtype, T.ArrayType) else (v if isinstance(v, str) else str(v))
+                keep = isinstance(dtype, (T.ArrayType, T.StructType, T.MapType, T.MatrixUDT))
+                out[i] = v if keep or isinstance(v, str) else str(v)
         return ColumnData(out, None if valid.all() else valid, dtype)
     valid = np.ones(n, dtype=bool)
     if isinstance(dtype, T.TimestampType):

@@ -685,6 +685,11 @@ class Column:
             raise ValueError("otherwise() can only be applied on a Column previously generated by when()")
         return Column(When(self._expr.branches, _expr(value)))
 
+    def over(self, window):
+        """Window function / aggregate evaluated over ``window`` (``sql.window.WindowSpec``)."""
+        from .window import over
+        return over(self, window)
+
     def asc(self): return SortOrder(self._expr, True)
     def desc(self): return SortOrder(self._expr, False)
     def asc_nulls_last(self): return SortOrder(self._expr, True, False)

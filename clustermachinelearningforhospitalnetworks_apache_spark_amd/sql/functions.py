@@ -252,6 +252,80 @@ def first(c: ColumnOrName) -> Column:
     return Column(AggExpr("first", _c(c)))
 
 
+def last(c: ColumnOrName) -> Column:
+    return Column(AggExpr("last", _c(c)))
+
+
+def collect_list(c: ColumnOrName) -> Column:
+    return Column(AggExpr("collect_list", _c(c)))
+
+
+def collect_set(c: ColumnOrName) -> Column:
+    return Column(AggExpr("collect_set", _c(c)))
+
+
+def approx_count_distinct(c: ColumnOrName, rsd: float = 0.05) -> Column:
+    """Exact distinct count (a valid answer for any rsd; Spark uses HyperLogLog++)."""
+    return Column(AggExpr("count", _c(c), distinct=True))
+
+
+def percentile_approx(c: ColumnOrName, percentage, accuracy: int = 10000) -> Column:
+    """Spark's percentile_approx on the exact sorted values: the smallest value whose rank reaches
+    ceil(p * n) (what the approximate algorithm converges to). ``percentage`` may be a list."""
+    e = AggExpr("percentile", _c(c))
+    e.arg = percentage
+    return Column(e)
+
+
+# ------------------------------------------------------------------------------------------------ window functions
+
+def window(timeColumn: ColumnOrName, windowDuration: str, slideDuration: str = None, startTime: str = None) -> Column:
+    """Event-time buckets (tumbling, or sliding with ``slideDuration``) as struct<start, end>."""
+    from .window import TimeWindow, parse_duration_us
+    dur = parse_duration_us(windowDuration)
+    slide = parse_duration_us(slideDuration) if slideDuration else dur
+    start = parse_duration_us(startTime) if startTime else 0
+    return Column(TimeWindow(_c(timeColumn), dur, slide, start))
+
+def _wf(fn, child=None, arg=None, default=None) -> Column:
+    from .window import WindowFunc
+    return Column(WindowFunc(fn, child, arg, default))
+
+
+def row_number() -> Column:
+    return _wf("row_number")
+
+
+def rank() -> Column:
+    return _wf("rank")
+
+
+def dense_rank() -> Column:
+    return _wf("dense_rank")
+
+
+def percent_rank() -> Column:
+    return _wf("percent_rank")
+
+
+def cume_dist() -> Column:
+    return _wf("cume_dist")
+
+
+def ntile(n: int) -> Column:
+    if int(n) < 1:
+        raise ValueError("ntile needs n >= 1")
+    return _wf("ntile", None, int(n))
+
+
+def lag(c: ColumnOrName, offset: int = 1, default=None) -> Column:
+    return _wf("lag", _c(c), int(offset), default)
+
+
+def lead(c: ColumnOrName, offset: int = 1, default=None) -> Column:
+    return _wf("lead", _c(c), int(offset), default)
+
+
 # ------------------------------------------------------------------------------------------------ UDFs
 
 def _return_type(rt) -> T.DataType:

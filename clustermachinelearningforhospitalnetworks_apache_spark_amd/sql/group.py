@@ -25,9 +25,13 @@ def _agg_name(e: Expr) -> str:
     return e.name()
 
 
-def _result_type(fn: str, in_type: Optional[T.DataType]) -> T.DataType:
+def _result_type(fn: str, in_type: Optional[T.DataType], arg=None) -> T.DataType:
     if fn == "count":
         return T.LongType()
+    if fn in ("collect_list", "collect_set"):
+        return T.ArrayType(in_type or T.StringType())
+    if fn == "percentile" and isinstance(arg, (list, tuple)):
+        return T.ArrayType(in_type or T.DoubleType())
     if fn in ("avg", "stddev", "stddev_pop", "variance", "var_pop"):
         return T.DoubleType()
     if fn == "sum":
@@ -48,6 +52,10 @@ def _partial(values: List[Any], fn: str, distinct: bool):
         return ("set", set(vals)) if distinct else ("n", len(vals))
     if fn == "first":
         return ("first", vals[0] if vals else None)
+    if fn == "last":
+        return ("last", vals[-1] if vals else None)
+    if fn in ("collect_list", "collect_set", "percentile"):
+        return ("list", [_hashable(v) for v in values if v is not None])
     if fn in ("min", "max"):
         if not vals:
             return (fn, None)
@@ -76,6 +84,23 @@ def _merge(parts, fn: str):
             if p[1] is not None:
                 return p[1]
         return None
+    if kind == "last":
+        for p in reversed(parts):
+            if p[1] is not None:
+                return p[1]
+        return None
+    if kind == "list":
+        vals = [v for p in parts for v in p[1]]
+        if fn == "collect_list":
+            return vals
+        if fn == "collect_set":
+            out, seen = [], set()
+            for v in vals:
+                if v not in seen:
+                    seen.add(v)
+                    out.append(v)
+            return out
+        return vals  # percentile: finished by _percentile with the requested fractions
     if kind in ("min", "max"):
         vals = [p[1] for p in parts if p[1] is not None]
         if not vals:
@@ -113,10 +138,31 @@ def _merge(parts, fn: str):
 
 
 def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
+    from .window import _WINDOW_TYPE, TimeWindow
     comm = df._comm
     key_names = [k.name() for k in keys]
-    key_vals = [column_to_python(k.eval(df)) for k in keys]
-    key_types = [k.eval(df).dtype for k in keys] if keys else []
+    # time-window keys (functions.window) may put a row into several buckets: expand rows first
+    src = list(range(df._nrows))
+    key_vals, key_types = [], []
+    for k in keys:
+        if isinstance(k, TimeWindow):
+            key_vals.append(("tw", k.buckets(df)))
+            key_types.append(_WINDOW_TYPE)
+        else:
+            cd = k.eval(df)
+            key_vals.append(("col", column_to_python(cd)))
+            key_types.append(cd.dtype)
+    if any(kind == "tw" for kind, _ in key_vals):
+        # expanded row list: one entry per (row, bucket) of the first time-window key
+        tw = next(v for kind, v in key_vals if kind == "tw")
+        src = [i for i in range(df._nrows) for _ in tw[i]]
+        which = []
+        for i in range(df._nrows):
+            which += list(range(len(tw[i])))
+        key_vals = [[v[i] for i in src] if kind == "col" else [v[i][w] for i, w in zip(src, which)]
+                    for kind, v in key_vals]
+    else:
+        key_vals = [v for _, v in key_vals]
     specs = []
     for e in exprs:
         alias, inner = _unwrap(e)
@@ -126,17 +172,18 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
                 continue
             raise ValueError(f"expression {e} is neither an aggregate nor a grouping column")
         if inner.child is None:
-            vals = [1] * df._nrows
+            vals = [1] * len(src)
             itype = T.LongType()
         else:
             cd = inner.child.eval(df)
             vals = column_to_python(cd)
+            vals = [vals[i] for i in src] if len(src) != df._nrows or src != list(range(df._nrows)) else vals
             itype = cd.dtype
         specs.append(("agg", alias or _agg_name(inner), inner, vals, itype))
     # local partials per group
     groups: Dict[tuple, List[Any]] = {}
     order: List[tuple] = []
-    for i in range(df._nrows):
+    for i in range(len(src)):
         key = tuple(kv[i] for kv in key_vals)
         if key not in groups:
             groups[key] = []
@@ -174,14 +221,17 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
             if sp[0] == "key":
                 row.append(key[sp[2]])
             else:
-                row.append(_merge(merged[key][j], sp[2].fn))
+                v = _merge(merged[key][j], sp[2].fn)
+                if sp[2].fn == "percentile":
+                    v = _percentile(v, getattr(sp[2], "arg", 0.5))
+                row.append(v)
         rows.append(row)
     fields = []
     for sp in specs:
         if sp[0] == "key":
             fields.append(T.StructField(sp[1], key_types[sp[2]], True))
         else:
-            fields.append(T.StructField(sp[1], _result_type(sp[2].fn, sp[4]), True))
+            fields.append(T.StructField(sp[1], _result_type(sp[2].fn, sp[4], getattr(sp[2], "arg", None)), True))
     schema = T.StructType(fields)
     for j, f in enumerate(fields):
         if isinstance(f.dataType, T.LongType):
@@ -271,6 +321,23 @@ def drop_duplicates(df: DataFrame, subset: Optional[Sequence[str]]) -> DataFrame
         keep_rows.append(r)
         keep_ids.append(i)
     return rows_contiguous(df._session, df.schema, keep_rows, keep_ids)
+
+
+def _percentile(vals: List[Any], p):
+    """Smallest value whose rank reaches ceil(p·n) (Spark percentile_approx's exact limit)."""
+    if not vals:
+        return None
+    srt = sorted(vals)
+
+    def one(q):
+        q = float(q)
+        if not 0.0 <= q <= 1.0:
+            raise ValueError("percentage must be in [0, 1]")
+        i = max(int(math.ceil(q * len(srt))) - 1, 0)
+        return srt[i]
+    if isinstance(p, (list, tuple)):
+        return [one(q) for q in p]
+    return one(p)
 
 
 def _hashable(v):

@@ -88,6 +88,17 @@ class Parser:
         self.i += 1
         return tok
 
+    def at_word(self, *words) -> bool:
+        """A keyword or identifier spelled like one of ``words`` (window-clause words are not reserved)."""
+        p = self.peek()
+        return p is not None and p.kind in ("kw", "ident") and p.val.upper() in words
+
+    def expect_word(self, word):
+        if not self.at_word(word):
+            tok = self.peek()
+            raise SyntaxError(f"expected {word}, got {tok.val if tok else 'end of SQL'!r}")
+        self.take()
+
     def expect_kw(self, kw):
         tok = self.take()
         if tok.kind != "kw" or tok.val != kw:
@@ -276,13 +287,96 @@ class Parser:
                 self.take()
                 args.append(self.expr())
         self.expect_op(")")
+        e = self._call_expr(name, lname, args, distinct)
+        if self.at_word("OVER"):
+            self.take()
+            from .window import WindowExpr
+            e = WindowExpr(e, self.window_spec())
+        return e
+
+    def window_spec(self):
+        """OVER ( [PARTITION BY e, ...] [ORDER BY e [ASC|DESC] [NULLS FIRST|LAST], ...]
+                  [ROWS|RANGE BETWEEN bound AND bound] )"""
+        from .window import Window, WindowSpec
+        self.expect_op("(")
+        part, orders, frame = [], [], None
+        if self.at_word("PARTITION"):
+            self.take()
+            self.expect_kw("BY")
+            part.append(self.expr())
+            while self.at_op(","):
+                self.take()
+                part.append(self.expr())
+        if self.at_kw("ORDER"):
+            self.take()
+            self.expect_kw("BY")
+            while True:
+                e = self.expr()
+                asc = True
+                if self.at_kw("ASC", "DESC"):
+                    asc = self.take().val == "ASC"
+                nulls_first = None
+                if self.at_kw("NULLS"):
+                    self.take()
+                    nulls_first = self.take().val == "FIRST"
+                orders.append(SortOrder(e, asc, nulls_first))
+                if not self.at_op(","):
+                    break
+                self.take()
+        if self.at_word("ROWS", "RANGE"):
+            kind = self.take().val.lower()
+            self.expect_kw("BETWEEN")
+            lo = self._frame_bound()
+            self.expect_kw("AND")
+            hi = self._frame_bound()
+            frame = (kind, lo, hi)
+        self.expect_op(")")
+        spec = WindowSpec(part, orders)
+        if frame is not None:
+            spec = spec.rowsBetween(frame[1], frame[2]) if frame[0] == "rows" else spec.rangeBetween(frame[1],
+                                                                                                     frame[2])
+        return spec
+
+    def _frame_bound(self) -> int:
+        from .window import Window
+        if self.at_word("UNBOUNDED"):
+            self.take()
+            if self.at_word("PRECEDING"):
+                self.take()
+                return Window.unboundedPreceding
+            self.expect_word("FOLLOWING")
+            return Window.unboundedFollowing
+        if self.at_word("CURRENT"):
+            self.take()
+            self.expect_word("ROW")
+            return Window.currentRow
+        tok = self.take()
+        if tok.kind != "num":
+            raise SyntaxError(f"expected a frame bound, got {tok.val!r}")
+        v = float(tok.val)
+        v = int(v) if v.is_integer() else v
+        if self.at_word("PRECEDING"):
+            self.take()
+            return -v
+        self.expect_word("FOLLOWING")
+        return v
+
+    def _call_expr(self, name: str, lname: str, args: List[Expr], distinct: bool) -> Expr:
+        from . import functions as F
         if lname == "count":
             return AggExpr("count", args[0] if args else None, distinct)
         aggs = {"sum": "sum", "avg": "avg", "mean": "avg", "min": "min", "max": "max", "stddev": "stddev",
                 "stddev_samp": "stddev", "stddev_pop": "stddev_pop", "variance": "variance",
-                "var_samp": "variance", "var_pop": "var_pop", "first": "first"}
+                "var_samp": "variance", "var_pop": "var_pop", "first": "first", "last": "last",
+                "collect_list": "collect_list", "collect_set": "collect_set"}
         if lname in aggs:
             return AggExpr(aggs[lname], args[0], distinct)
+        if lname in ("lag", "lead"):
+            off = int(args[1].value) if len(args) > 1 else 1
+            default = args[2].value if len(args) > 2 else None
+            return getattr(F, lname)(Column(args[0]), off, default)._expr
+        if lname == "ntile":
+            return F.ntile(int(args[0].value))._expr
         fn = getattr(F, lname, None)
         if fn is None:
             raise SyntaxError(f"unknown function {name}")

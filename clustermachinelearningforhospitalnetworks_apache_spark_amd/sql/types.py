@@ -161,6 +161,46 @@ class ArrayType(DataType):
         return hash(("array", self.elementType))
 
 
+class MapType(DataType):
+    host_only = True
+
+    def __init__(self, keyType: DataType, valueType: DataType, valueContainsNull: bool = True):
+        self.keyType, self.valueType, self.valueContainsNull = keyType, valueType, valueContainsNull
+
+    def simpleString(self):
+        return f"map<{self.keyType.simpleString()},{self.valueType.simpleString()}>"
+
+    def jsonValue(self):
+        return {"type": "map", "keyType": self.keyType.jsonValue(), "valueType": self.valueType.jsonValue(),
+                "valueContainsNull": self.valueContainsNull}
+
+    def __eq__(self, other):
+        return isinstance(other, MapType) and (other.keyType, other.valueType) == (self.keyType, self.valueType)
+
+    def __hash__(self):
+        return hash(("map", self.keyType, self.valueType))
+
+
+class DecimalType(DataType):
+    """Fixed-point decimal; computed as float64 on the device (precision/scale kept for the schema)."""
+    torch_dtype = torch.float64
+
+    def __init__(self, precision: int = 10, scale: int = 0):
+        self.precision, self.scale = precision, scale
+
+    def simpleString(self):
+        return f"decimal({self.precision},{self.scale})"
+
+    def jsonValue(self):
+        return self.simpleString()
+
+    def __eq__(self, other):
+        return isinstance(other, DecimalType) and (other.precision, other.scale) == (self.precision, self.scale)
+
+    def __hash__(self):
+        return hash(("decimal", self.precision, self.scale))
+
+
 class StructField:
     def __init__(self, name: str, dataType: DataType, nullable: bool = True, metadata: Optional[Dict] = None):
         self.name = name
@@ -269,7 +309,7 @@ def parse_ddl_schema(ddl: str) -> StructType:
 
 
 def is_numeric(t: DataType) -> bool:
-    return isinstance(t, (ByteType, ShortType, IntegerType, LongType, FloatType, DoubleType))
+    return isinstance(t, (ByteType, ShortType, IntegerType, LongType, FloatType, DoubleType, DecimalType))
 
 
 def is_integral(t: DataType) -> bool:

@@ -94,6 +94,14 @@ def _workload(out_path, rank, master="local[1]"):
     holes = spark.createDataFrame(pdf.assign(a=pdf["a"].where(pdf.index % 7 != 0)))
     res["imp"] = [Imputer(strategy=s, inputCol="a", outputCol="ai").fit(holes).surrogates[0]
                   for s in ("mean", "median", "mode")]
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import Window
+    w = Window.partitionBy("g").orderBy("a")
+    wd = spark.createDataFrame(pdf).select("g", "a", F.row_number().over(w).alias("rn"),
+                                           F.sum("y").over(w.rowsBetween(-3, 0)).alias("s"),
+                                           F.lag("b", 1).over(w).alias("lb")).orderBy("g", "a").collect()
+    res["win"] = [[r.g, r.rn, r.s, r.lb] for r in wd][:300]
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
+    res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
     if rank == 0:
         with open(out_path, "w") as fh:
             json.dump(res, fh)
@@ -152,6 +160,10 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["cv"], r1["cv"], rtol=1e-9)
     assert rw["ohe"] == r1["ohe"] == [5]
     np.testing.assert_allclose(rw["imp"], r1["imp"], rtol=1e-12)
+    assert [x[:2] for x in rw["win"]] == [x[:2] for x in r1["win"]]
+    np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
+    assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
+    np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)
 
 
 @pytest.mark.parametrize("world", [2, 3])
