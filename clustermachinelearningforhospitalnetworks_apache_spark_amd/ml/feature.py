@@ -76,7 +76,7 @@ class VectorAssembler(Transformer):
                     bad_any = bool(torch.isnan(x).any().item())
                 if bad_any:
                     raise ValueError("VectorAssembler: encountered NaN values with handleInvalid='error'")
-            return _replace_col(df, self.getOutputCol(), ColumnData(x, None, T.VectorUDT()))
+            return self._named(df, _replace_col(df, self.getOutputCol(), ColumnData(x, None, T.VectorUDT())))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags
             from ..ops import frame_ops
@@ -94,7 +94,22 @@ class VectorAssembler(Transformer):
                 idx = df._mask_index(keep)
                 df = df._take_rows(idx)
                 x = x[idx]
-        return _replace_col(df, self.getOutputCol(), ColumnData(x.contiguous(), None, T.VectorUDT()))
+        return self._named(df, _replace_col(df, self.getOutputCol(), ColumnData(x.contiguous(), None, T.VectorUDT())))
+
+    def _named(self, src, out):
+        """Attach Spark's ``ml_attr`` feature names: scalar columns by name, vector columns by their
+        own attribute names or ``<col>_<i>``."""
+        from .feature_more import _vector_meta, vector_attr_names
+        names = []
+        for c in self.getInputCols():
+            cd = src._column_data(c)
+            if isinstance(cd.dtype, T.VectorUDT):
+                sub = vector_attr_names(src, c)
+                names += sub if sub is not None else [f"{c}_{i}" for i in range(cd.values.shape[1])]
+            else:
+                names.append(c)
+        out.schema[self.getOutputCol()].metadata = _vector_meta(names)
+        return out
 
     @staticmethod
     def _assemble_torch(df, cds):
@@ -636,3 +651,8 @@ class ImputerModel(Model):
 
 
 from .feature_extra import Bucketizer, Normalizer, PCA, PCAModel, QuantileDiscretizer  # noqa: E402,F401
+from .feature_more import (ChiSqSelector, ChiSqSelectorModel, ElementwiseProduct, Interaction,  # noqa: E402,F401
+                           MaxAbsScaler, MaxAbsScalerModel, PolynomialExpansion, RFormula, RFormulaModel,
+                           RobustScaler, RobustScalerModel, SQLTransformer, UnivariateFeatureSelector,
+                           UnivariateFeatureSelectorModel, VarianceThresholdSelector, VarianceThresholdSelectorModel,
+                           VectorIndexer, VectorIndexerModel, VectorSlicer)

@@ -78,6 +78,26 @@ _JVM = {
     "GBTRegressionModel": "org.apache.spark.ml.regression.GBTRegressionModel",
     "GBTClassifier": "org.apache.spark.ml.classification.GBTClassifier",
     "GBTClassificationModel": "org.apache.spark.ml.classification.GBTClassificationModel",
+    "MaxAbsScaler": "org.apache.spark.ml.feature.MaxAbsScaler",
+    "MaxAbsScalerModel": "org.apache.spark.ml.feature.MaxAbsScalerModel",
+    "RobustScaler": "org.apache.spark.ml.feature.RobustScaler",
+    "RobustScalerModel": "org.apache.spark.ml.feature.RobustScalerModel",
+    "ElementwiseProduct": "org.apache.spark.ml.feature.ElementwiseProduct",
+    "PolynomialExpansion": "org.apache.spark.ml.feature.PolynomialExpansion",
+    "Interaction": "org.apache.spark.ml.feature.Interaction",
+    "VectorSlicer": "org.apache.spark.ml.feature.VectorSlicer",
+    "VectorIndexer": "org.apache.spark.ml.feature.VectorIndexer",
+    "VectorIndexerModel": "org.apache.spark.ml.feature.VectorIndexerModel",
+    "SQLTransformer": "org.apache.spark.ml.feature.SQLTransformer",
+    "VarianceThresholdSelector": "org.apache.spark.ml.feature.VarianceThresholdSelector",
+    "VarianceThresholdSelectorModel": "org.apache.spark.ml.feature.VarianceThresholdSelectorModel",
+    "UnivariateFeatureSelector": "org.apache.spark.ml.feature.UnivariateFeatureSelector",
+    "UnivariateFeatureSelectorModel": "org.apache.spark.ml.feature.UnivariateFeatureSelectorModel",
+    "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
+    "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
+    "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "RFormulaModel": "org.apache.spark.ml.feature.RFormulaModel",
+    "IndexToString": "org.apache.spark.ml.feature.IndexToString",
 }
 _PY = {
     "LinearRegression": "regression", "LinearRegressionModel": "regression",
@@ -103,6 +123,26 @@ _PY = {
     "BisectingKMeans": "clustering", "BisectingKMeansModel": "clustering",
     "GBTRegressor": "regression", "GBTRegressionModel": "regression",
     "GBTClassifier": "classification", "GBTClassificationModel": "classification",
+    "MaxAbsScaler": "feature",
+    "MaxAbsScalerModel": "feature",
+    "RobustScaler": "feature",
+    "RobustScalerModel": "feature",
+    "ElementwiseProduct": "feature",
+    "PolynomialExpansion": "feature",
+    "Interaction": "feature",
+    "VectorSlicer": "feature",
+    "VectorIndexer": "feature",
+    "VectorIndexerModel": "feature",
+    "SQLTransformer": "feature",
+    "VarianceThresholdSelector": "feature",
+    "VarianceThresholdSelectorModel": "feature",
+    "UnivariateFeatureSelector": "feature",
+    "UnivariateFeatureSelectorModel": "feature",
+    "ChiSqSelector": "feature",
+    "ChiSqSelectorModel": "feature",
+    "RFormula": "feature",
+    "RFormulaModel": "feature",
+    "IndexToString": "feature",
 }
 
 

@@ -142,10 +142,12 @@ class DataFrame:
     def _from_columns(self, names: Sequence[str], datas: Sequence[ColumnData]) -> "DataFrame":
         fields, cols = [], {}
         for n, d in zip(names, datas):
-            nullable = True
+            nullable, meta = True, None
             if n in self._schema.names:
                 nullable = self._schema[n].nullable
-            fields.append(T.StructField(n, d.dtype, nullable))
+                if self._cols.get(n) is d:  # the column itself: keep its metadata (ML attributes)
+                    meta = dict(self._schema[n].metadata)
+            fields.append(T.StructField(n, d.dtype, nullable, meta))
             cols[n] = d
         return self._new(T.StructType(fields), cols, self._nrows, self._row_ids)
 

@@ -171,6 +171,10 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
                 specs.append(("key", alias or inner.col, key_names.index(inner.col), None))
                 continue
             raise ValueError(f"expression {e} is neither an aggregate nor a grouping column")
+        if getattr(inner, "custom", False):
+            # device-side aggregate (e.g. ml.stat.Summarizer): prepare / partial / merge hooks
+            specs.append(("agg", alias or _agg_name(inner), inner, inner.prepare(df), None))
+            continue
         if inner.child is None:
             vals = [1] * len(src)
             itype = T.LongType()
@@ -201,7 +205,10 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
                 parts.append(None)
             else:
                 _, _, agg, vals, _ = sp
-                parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct))
+                if getattr(agg, "custom", False):
+                    parts.append(agg.partial(vals, [src[i] for i in idx]))
+                else:
+                    parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct))
         local[key] = parts
     gathered = comm.allgather_object(local)
     merged: Dict[tuple, List[List[Any]]] = {}
@@ -221,6 +228,9 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
             if sp[0] == "key":
                 row.append(key[sp[2]])
             else:
+                if getattr(sp[2], "custom", False):
+                    row.append(sp[2].merge(merged[key][j]))
+                    continue
                 v = _merge(merged[key][j], sp[2].fn)
                 if sp[2].fn == "percentile":
                     v = _percentile(v, getattr(sp[2], "arg", 0.5))
@@ -230,6 +240,8 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
     for sp in specs:
         if sp[0] == "key":
             fields.append(T.StructField(sp[1], key_types[sp[2]], True))
+        elif getattr(sp[2], "custom", False):
+            fields.append(T.StructField(sp[1], sp[2].result_type(), True))
         else:
             fields.append(T.StructField(sp[1], _result_type(sp[2].fn, sp[4], getattr(sp[2], "arg", None)), True))
     schema = T.StructType(fields)
