@@ -5,7 +5,9 @@
 // K8  scale_apply     (x - μ)·(1/σ) with optional centring, any in/out dtype (bf16/f32/f64)
 // K13 logreg_grad     fused binomial logistic pass: margin = x·w + b, p = σ(margin),
 //                     ∇w += (p − y)·x, ∇b += p − y, loss += softplus(margin) − y·margin,
-//                     X read ONCE per pass (L-BFGS full batch or an SGD mini-batch)
+//                     X read ONCE per pass (L-BFGS full batch or an SGD mini-batch); the same
+//                     pass with loss LS = 1 is the hinge loss of LinearSVC (labels {0,1} -> ±1,
+//                     r = −w·y± where 1 − y±·m > 0) and LS = 2 the squared loss ½(m − y)²
 // K13b partial_colsum  fixed-order sum of the per-block partials (device-side, capturable)
 // K14 sgd_update      momentum SGD step on the device (mini-batch LogisticRegression)
 // K15 gram            [X 1 y]ᵀ[X 1 y] upper triangle in f64 (LinearRegression normal equations)
@@ -383,7 +385,7 @@ __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __re
 // ---------------------------------------------------------------------------- K13 logistic gradient
 // Per row group: margin m = x·w + b (CT), p = σ(m), r = wt·(p − y); the lane's chunk of r·x goes
 // into CT accumulators that are folded into f64 every FLUSH rows; loss and weights in f64.
-template <typename T, int NCH, int U>
+template <typename T, int NCH, int U, int LS = 0>
 __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     const T* __restrict__ X, long long n, long long ld, int d, int lpr, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[d+1], last = intercept*/,
@@ -450,15 +452,28 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
 #pragma unroll
         for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
       m = group_sum_ct<CT>(m, lpr) + b;
-      const CT p = sigmoid_ct(m);
-      const CT r = (CT)wi * (p - (CT)yi);
+      CT r;
+      double lrow;
+      if constexpr (LS == 0) {  // logistic
+        r = (CT)wi * (sigmoid_ct(m) - (CT)yi);
+        lrow = (double)softplus_ct(m) - yi * (double)m;
+      } else if constexpr (LS == 1) {  // hinge, labels {0, 1}
+        const CT ys = yi > 0.5 ? (CT)1 : (CT)-1;
+        const CT t = (CT)1 - ys * m;
+        r = t > (CT)0 ? -(CT)wi * ys : (CT)0;
+        lrow = t > (CT)0 ? (double)t : 0.0;
+      } else {  // squared
+        const CT e = m - (CT)yi;
+        r = (CT)wi * e;
+        lrow = 0.5 * (double)e * (double)e;
+      }
 #pragma unroll
       for (int c = 0; c < NCH; ++c)
 #pragma unroll
         for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
       if (li == 0) {
         gb += (double)r;
-        loss += wi * ((double)softplus_ct(m) - yi * (double)m);
+        loss += wi * lrow;
         wsum += wi;
       }
       if constexpr (sizeof(CT) == 4) {
@@ -930,6 +945,30 @@ CML_API int cml_logreg_grad(const void* X, long long n, long long ld, int d, int
                            logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld,
                            d, lpr, y, wt, coef, out, row_base);
       });
+    });
+  });
+  return cml_status();
+}
+
+// K13 with the hinge (LS = 1) or squared (LS = 2) loss; one group ahead (U = 1, the K13 optimum).
+CML_API int cml_glm_loss_grad(const void* X, long long n, long long ld, int d, int dtype, const double* y,
+                              const double* wt, const double* coef, double* out, int grid, int loss, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  if (loss < 0 || loss > 2) return (int)hipErrorInvalidValue;
+  if (loss == 0) return cml_logreg_grad(X, n, ld, d, dtype, y, wt, coef, out, grid, nullptr, stream);
+  CML_T_SWITCH(dtype, {
+    int lpr = 0;
+    int nch = 0;
+    if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
+    CML_NCH_SWITCH(nch, {
+      if (loss == 1)
+        hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 1, 1>), dim3(grid), dim3(kGlmThreads),
+                           logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
+                           nullptr);
+      else
+        hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 1, 2>), dim3(grid), dim3(kGlmThreads),
+                           logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
+                           nullptr);
     });
   });
   return cml_status();

@@ -501,3 +501,6 @@ class GBTClassificationModel(GBTModelMixin, Model):
 
 
 from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: E402,F401
+from .classification_more import (LinearSVC, LinearSVCModel, LinearSVCSummary,  # noqa: E402,F401
+                                  LinearSVCTrainingSummary, MultilayerPerceptronClassificationModel,
+                                  MultilayerPerceptronClassifier, OneVsRest, OneVsRestModel)

@@ -1,0 +1,519 @@
+"""More pyspark.ml.classification: LinearSVC, OneVsRest and MultilayerPerceptronClassifier.
+
+The reference trains tree ensembles on the assembled hospital features (ref.py:182-190); these
+are the other MLlib classifiers such a pipeline swaps in (readmission / high-LOS flags).
+MI355X-first:
+
+* LinearSVC: every L-BFGS function evaluation is ONE fused device pass of the K13 kernel in its
+  hinge-loss instantiation (margin, sub-gradient and loss; X read once) + one all-reduce of the
+  (d+3)-vector; the optimizer runs on the host like Spark's driver-side Breeze OWL-QN.
+* OneVsRest: k binary fits of any classifier over the same device-resident feature matrix
+  (only the 0/1 label column changes); scoring stacks the k margins into one [n, k] tensor.
+* MultilayerPerceptronClassifier: sigmoid hidden layers + softmax/cross-entropy output (Spark's
+  topology); the full-batch loss and gradient of the flat weight vector come from device GEMMs
+  (hipBLASLt) with autograd, all-reduced, and fed to the same L-BFGS (solver 'l-bfgs') or to plain
+  gradient descent (solver 'gd'). Weight layout = Spark's: per layer W (out x in, column-major)
+  then b.
+"""
+from __future__ import annotations
+
+import os
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..models.optim import lbfgs
+from ..ops import glm_ops
+from ..sql import types as T
+from ..sql.column import ColumnData
+from . import util as U
+from .base import Estimator, Model
+from .feature import _replace_col
+from .linalg import DenseVector, as_array
+from .param import NO_DEFAULT
+
+_PRED_PARAMS = {
+    "featuresCol": ("features", "features column name", str),
+    "labelCol": ("label", "label column name", str),
+    "predictionCol": ("prediction", "prediction column name", str),
+    "rawPredictionCol": ("rawPrediction", "raw prediction (a.k.a. confidence) column name", str),
+}
+
+
+def _labels_weights(est, df):
+    y = df._column_data(est.getLabelCol()).values.to(torch.float64)
+    w = df._column_data(est.getOrDefault("weightCol")).values.to(torch.float64) \
+        if est.isSet("weightCol") and est.getOrDefault("weightCol") else None
+    return y, w
+
+
+def _std(df, x: torch.Tensor) -> np.ndarray:
+    from .stat import _moments
+    _, _, var = _moments(df, x)
+    return np.sqrt(var)
+
+
+# ------------------------------------------------------------------------------------------ LinearSVC
+
+_SVC_PARAMS = dict(_PRED_PARAMS, **{
+    "maxIter": (100, "max number of iterations (>= 0)", int),
+    "regParam": (0.0, "regularization parameter (>= 0)", float),
+    "tol": (1e-6, "convergence tolerance for iterative algorithms (>= 0)", float),
+    "fitIntercept": (True, "whether to fit an intercept term", bool),
+    "standardization": (True, "whether to standardize the training features before fitting the model", bool),
+    "threshold": (0.0, "threshold in binary classification prediction applied to rawPrediction", float),
+    "weightCol": (None, "weight column name", None),
+    "aggregationDepth": (2, "suggested depth for treeAggregate (>= 2)", int),
+    "maxBlockSizeInMB": (0.0, "maximum memory in MB for stacking input data into blocks", float),
+})
+
+
+class LinearSVC(Estimator):
+    """Linear SVM: minimises the mean (weighted) hinge loss + ½·regParam·‖β‖² (β in standardized
+    space when ``standardization``), Spark's defaults (maxIter 100, tol 1e-6, threshold 0)."""
+    _params = _SVC_PARAMS
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _fit(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        d = x.shape[1]
+        y, w = _labels_weights(self, df)
+        comm = df._comm
+        bad = comm.max_scalar(float(((y != 0) & (y != 1)).any().item()) if y.numel() else 0.0)
+        if bad:
+            raise ValueError("LinearSVC only supports binary classification with labels 0 and 1")
+        std = _std(df, x)
+        sd = np.where(std > 0, std, 1.0)
+        active = std > 0
+        fi = self.getFitIntercept()
+        standardize = self.getStandardization()
+        lam = self.getRegParam()
+        dev = x.device
+
+        def fg(p):
+            wp, b = p[:d], (p[d] if fi else 0.0)
+            coef = np.where(active, wp / sd, 0.0)
+            out = glm_ops.loss_grad(x, d, y, torch.as_tensor(np.r_[coef, b], device=dev), w, loss="hinge")
+            comm.allreduce_(out)
+            o = out.cpu().numpy()
+            wsum = max(o[d + 2], 1e-300)
+            g = np.zeros(d + 1)
+            g[:d] = np.where(active, o[:d] / sd, 0.0) / wsum
+            g[d] = o[d] / wsum if fi else 0.0
+            f = o[d + 1] / wsum
+            if lam > 0:
+                pen = wp if standardize else wp / sd
+                f += 0.5 * lam * float(np.sum(np.where(active, pen * pen, 0.0)))
+                g[:d] += lam * np.where(active, pen if standardize else pen / sd, 0.0)
+            return f, g
+
+        p, hist, iters = lbfgs(fg, np.zeros(d + 1), self.getMaxIter(), self.getTol())
+        coef = np.where(active, p[:d] / sd, 0.0)
+        model = LinearSVCModel(coef, float(p[d]) if fi else 0.0)
+        self._copyValues(model)
+        model._attach_summary(LinearSVCTrainingSummary(model, df, hist, iters))
+        return model
+
+
+class LinearSVCModel(Model):
+    _params = _SVC_PARAMS
+
+    def __init__(self, coefficients=None, intercept: float = 0.0):
+        super().__init__()
+        self._coef = np.asarray(coefficients if coefficients is not None else [], dtype=np.float64)
+        self._icpt = float(intercept)
+        self._summary = None
+
+    @property
+    def coefficients(self) -> DenseVector:
+        return DenseVector(self._coef)
+
+    @property
+    def intercept(self) -> float:
+        return self._icpt
+
+    @property
+    def numClasses(self) -> int:
+        return 2
+
+    @property
+    def numFeatures(self) -> int:
+        return int(self._coef.size)
+
+    def _margin(self, x: torch.Tensor) -> torch.Tensor:
+        coef = torch.as_tensor(np.r_[self._coef, self._icpt], device=x.device)
+        return glm_ops.linear_predict(x, x.shape[1], coef, "identity")
+
+    def _transform(self, df):
+        x = df._feature_matrix(self.getFeaturesCol())
+        m = self._margin(x).to(torch.float64)
+        out = df
+        if self.getRawPredictionCol():
+            out = _replace_col(out, self.getRawPredictionCol(), ColumnData(torch.stack([-m, m], 1), None,
+                                                                          T.VectorUDT()))
+        pred = (m > self.getThreshold()).to(torch.float64)
+        return _replace_col(out, self.getPredictionCol(), ColumnData(pred, None, T.DoubleType()))
+
+    def predict(self, value) -> float:
+        v = np.asarray(as_array(value), dtype=np.float64)
+        return float(v @ self._coef + self._icpt > self.getThreshold())
+
+    def predictRaw(self, value) -> DenseVector:
+        m = float(np.asarray(as_array(value), dtype=np.float64) @ self._coef + self._icpt)
+        return DenseVector([-m, m])
+
+    def evaluate(self, df):
+        return LinearSVCSummary(self, df)
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        U.write_parquet(path, "data", pa.Table.from_pylist(
+            [{"coefficients": U.vector_struct(self._coef), "intercept": self._icpt}],
+            schema=pa.schema([("coefficients", U.vector_arrow_type()),
+                              pa.field("intercept", pa.float64(), nullable=False)])))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        r = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(U.vector_from_struct(r["coefficients"]), r["intercept"])
+        U.apply_params(m, md)
+        return m
+
+
+class LinearSVCSummary:
+    def __init__(self, model, df):
+        self._model, self._df, self._pred = model, df, None
+        self.labelCol = model.getLabelCol()
+        self.predictionCol = model.getPredictionCol()
+
+    @property
+    def predictions(self):
+        if self._pred is None:
+            self._pred = self._model.transform(self._df)
+        return self._pred
+
+    def _mc(self, metric):
+        from .evaluation import MulticlassClassificationEvaluator
+        return MulticlassClassificationEvaluator(labelCol=self.labelCol, predictionCol=self.predictionCol,
+                                                 metricName=metric).evaluate(self.predictions)
+
+    @property
+    def accuracy(self):
+        return self._mc("accuracy")
+
+    @property
+    def weightedPrecision(self):
+        return self._mc("weightedPrecision")
+
+    @property
+    def weightedRecall(self):
+        return self._mc("weightedRecall")
+
+    @property
+    def areaUnderROC(self):
+        from .evaluation import BinaryClassificationEvaluator
+        return BinaryClassificationEvaluator(rawPredictionCol=self._model.getRawPredictionCol(),
+                                             labelCol=self.labelCol).evaluate(self.predictions)
+
+
+class LinearSVCTrainingSummary(LinearSVCSummary):
+    def __init__(self, model, df, hist, iters):
+        super().__init__(model, df)
+        self.objectiveHistory = list(hist)
+        self.totalIterations = int(iters)
+
+
+# ------------------------------------------------------------------------------------------ OneVsRest
+
+_OVR_PARAMS = dict(_PRED_PARAMS, **{
+    "classifier": (NO_DEFAULT, "base binary classifier", None),
+    "weightCol": (None, "weight column name", None),
+    "parallelism": (1, "the number of threads to use when running parallel algorithms (>= 1)", int),
+})
+
+
+def _raw_confidence(model, df):
+    """[n] confidence of the positive class of a fitted binary model: rawPrediction[:, 1]."""
+    rc = model.getRawPredictionCol() if model.hasParam("rawPredictionCol") else ""
+    out = model.transform(df)
+    if rc and rc in out.columns:
+        return out._feature_matrix(rc)[:, 1].to(torch.float64)
+    pc = model.getProbabilityCol() if model.hasParam("probabilityCol") else ""
+    if pc and pc in out.columns:
+        return out._feature_matrix(pc)[:, 1].to(torch.float64)
+    raise ValueError(f"OneVsRest: {type(model).__name__} produces no rawPrediction / probability column")
+
+
+class OneVsRest(Estimator):
+    """Multiclass by k binary fits of ``classifier`` (class c vs the rest); prediction = argmax of the
+    k positive-class confidences."""
+    _params = _OVR_PARAMS
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        self._defaultParamMap.pop("weightCol", None)
+
+    def _fit(self, df):
+        clf = self.getClassifier()
+        y = df._column_data(self.getLabelCol()).values.to(torch.float64)
+        k = int(df._comm.max_scalar(float(y.max().item()) if y.numel() else 0.0)) + 1
+        tmp = f"mc2b_{self.uid}"
+        models = []
+        for c in range(k):
+            yc = (y == c).to(torch.float64)
+            dfc = _replace_col(df, tmp, ColumnData(yc, None, T.DoubleType()))
+            pm = {clf.getParam("labelCol"): tmp, clf.getParam("featuresCol"): self.getFeaturesCol()}
+            if self.isSet("weightCol") and clf.hasParam("weightCol"):
+                pm[clf.getParam("weightCol")] = self.getOrDefault("weightCol")
+            m = clf.copy(pm).fit(dfc)
+            m._set(labelCol=self.getLabelCol())
+            models.append(m)
+        model = OneVsRestModel(models)
+        self._copyValues(model)
+        return model
+
+    def _save_impl(self, path):
+        U.write_metadata(self, path, param_map={k: v for k, v in self._paramMap.items() if k != "classifier"})
+        self.getClassifier()._save_impl(_sub(path, "classifier"))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        inst = cls()
+        U.apply_params(inst, md)
+        inst._set(classifier=U.load(os.path.join(path, "classifier")))
+        return inst
+
+
+def _sub(path: str, name: str) -> str:
+    d = os.path.join(path, name)
+    os.makedirs(d, exist_ok=True)
+    return d
+
+
+class OneVsRestModel(Model):
+    _params = _OVR_PARAMS
+
+    def __init__(self, models: Optional[List] = None):
+        super().__init__()
+        self.models = list(models or [])
+
+    @property
+    def numClasses(self) -> int:
+        return len(self.models)
+
+    def _transform(self, df):
+        conf = torch.stack([_raw_confidence(m, df) for m in self.models], 1)
+        out = df
+        if self.getRawPredictionCol():
+            out = _replace_col(out, self.getRawPredictionCol(), ColumnData(conf.contiguous(), None, T.VectorUDT()))
+        pred = torch.argmax(conf, 1).to(torch.float64)
+        return _replace_col(out, self.getPredictionCol(), ColumnData(pred, None, T.DoubleType()))
+
+    def _save_impl(self, path):
+        U.write_metadata(self, path, param_map={k: v for k, v in self._paramMap.items() if k != "classifier"},
+                         extra={"numClasses": len(self.models), "labelMetadata": "{}"})
+        clf = self.getOrDefault("classifier") if self.isSet("classifier") else None
+        if clf is not None:
+            clf._save_impl(_sub(path, "classifier"))
+        for i, m in enumerate(self.models):
+            m._save_impl(_sub(path, f"model_{i}"))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        models = [U.load(os.path.join(path, f"model_{i}")) for i in range(int(md["numClasses"]))]
+        m = cls(models)
+        U.apply_params(m, md)
+        if os.path.isdir(os.path.join(path, "classifier")):
+            m._set(classifier=U.load(os.path.join(path, "classifier")))
+        return m
+
+
+# -------------------------------------------------------------------- MultilayerPerceptronClassifier
+
+_MLP_PARAMS = dict(_PRED_PARAMS, **{
+    "probabilityCol": ("probability", "column name for predicted class conditional probabilities", str),
+    "layers": (NO_DEFAULT, "sizes of layers from input layer to output layer", None),
+    "blockSize": (128, "block size for stacking input data in matrices", int),
+    "seed": (None, "random seed", None),
+    "maxIter": (100, "max number of iterations (>= 0)", int),
+    "tol": (1e-6, "convergence tolerance for iterative algorithms (>= 0)", float),
+    "stepSize": (0.03, "step size to be used for each iteration of optimization (> 0)", float),
+    "solver": ("l-bfgs", "the solver algorithm for optimization: l-bfgs, gd", str),
+    "initialWeights": (None, "the initial weights of the model", None),
+    "thresholds": (None, "thresholds in multi-class classification", None),
+})
+
+
+def _mlp_unpack(p: torch.Tensor, layers: List[int]):
+    """Spark's flat layout: per layer W (out x in, column-major) then b (out)."""
+    out, off = [], 0
+    for a, b in zip(layers[:-1], layers[1:]):
+        W = p[off:off + a * b].reshape(a, b).T  # column-major [out, in]
+        off += a * b
+        out.append((W, p[off:off + b]))
+        off += b
+    return out
+
+
+def _mlp_forward(x: torch.Tensor, params) -> torch.Tensor:
+    h = x
+    for i, (W, b) in enumerate(params):
+        h = h @ W.T + b
+        if i < len(params) - 1:
+            h = torch.sigmoid(h)
+    return h  # pre-softmax scores
+
+
+def _mlp_size(layers: List[int]) -> int:
+    return sum(a * b + b for a, b in zip(layers[:-1], layers[1:]))
+
+
+class MultilayerPerceptronClassifier(Estimator):
+    """Feed-forward network: sigmoid hidden layers, softmax output with cross-entropy loss, trained
+    full-batch (L-BFGS or gradient descent); weights initialised uniformly in ±sqrt(6/(in+out))
+    per layer from ``seed`` (Spark's initialisation range)."""
+    _params = _MLP_PARAMS
+
+    def __init__(self, **kwargs):
+        super().__init__(**kwargs)
+        for k in ("seed", "initialWeights", "thresholds"):
+            self._defaultParamMap.pop(k, None)
+
+    def _fit(self, df):
+        from .tree_models import _default_seed
+        layers = [int(v) for v in self.getLayers()]
+        if len(layers) < 2:
+            raise ValueError("MultilayerPerceptronClassifier: layers needs an input and an output size")
+        x = df._feature_matrix(self.getFeaturesCol()).to(torch.float64)
+        if x.shape[1] != layers[0]:
+            raise ValueError(f"MultilayerPerceptronClassifier: input layer {layers[0]} != feature size {x.shape[1]}")
+        y = df._column_data(self.getLabelCol()).values.to(torch.int64)
+        comm = df._comm
+        k = layers[-1]
+        if y.numel() and (int(y.max()) >= k or int(y.min()) < 0):
+            raise ValueError(f"MultilayerPerceptronClassifier: labels must be in [0, {k})")
+        cnt = torch.tensor([float(y.numel())], dtype=torch.float64, device=x.device)
+        comm.allreduce_(cnt)
+        N = max(float(cnt.item()), 1.0)
+        if self.isSet("initialWeights"):
+            p0 = np.asarray(as_array(self.getOrDefault("initialWeights")), dtype=np.float64)
+            if p0.size != _mlp_size(layers):
+                raise ValueError(f"initialWeights has {p0.size} entries, the topology needs {_mlp_size(layers)}")
+        else:
+            seed = self.getOrDefault("seed") if self.isSet("seed") else _default_seed(U.jvm_class(self))
+            rng = np.random.default_rng(int(seed) & 0xFFFFFFFF)
+            parts = []
+            for a, b in zip(layers[:-1], layers[1:]):
+                lim = np.sqrt(6.0 / (a + b))
+                parts += [rng.uniform(-lim, lim, a * b), rng.uniform(-lim, lim, b)]
+            p0 = np.concatenate(parts)
+        Y = torch.nn.functional.one_hot(y, k).to(torch.float64) if y.numel() else torch.zeros(
+            (0, k), dtype=torch.float64, device=x.device)
+
+        def fg(p):
+            pt = torch.as_tensor(p, device=x.device).requires_grad_(True)
+            z = _mlp_forward(x, _mlp_unpack(pt, layers))
+            loss = (torch.logsumexp(z, 1) - (z * Y).sum(1)).sum()
+            g, = torch.autograd.grad(loss, pt)
+            msg = torch.cat([g.detach(), loss.detach().reshape(1)])
+            comm.allreduce_(msg)
+            o = msg.cpu().numpy()
+            return float(o[-1]) / N, o[:-1] / N
+
+        if self.getSolver() == "l-bfgs":
+            p, hist, iters = lbfgs(fg, p0, self.getMaxIter(), self.getTol())
+        elif self.getSolver() == "gd":
+            p, hist = p0.copy(), []
+            f, g = fg(p)
+            hist.append(f)
+            iters = 0
+            for iters in range(1, self.getMaxIter() + 1):
+                p = p - self.getStepSize() * g
+                fn, g = fg(p)
+                hist.append(fn)
+                if abs(f - fn) < self.getTol() * max(abs(f), 1e-12):
+                    break
+                f = fn
+        else:
+            raise ValueError(f"MultilayerPerceptronClassifier: unknown solver {self.getSolver()!r}")
+        model = MultilayerPerceptronClassificationModel(layers, p)
+        self._copyValues(model)
+        model._attach_summary(_MLPTrainingSummary(model, df, hist, iters))
+        return model
+
+
+class _MLPTrainingSummary(LinearSVCSummary):
+    def __init__(self, model, df, hist, iters):
+        super().__init__(model, df)
+        self.objectiveHistory = list(hist)
+        self.totalIterations = int(iters)
+
+
+class MultilayerPerceptronClassificationModel(Model):
+    _params = _MLP_PARAMS
+
+    def __init__(self, layers: Optional[List[int]] = None, weights=None):
+        super().__init__()
+        self._layers = [int(v) for v in (layers or [])]
+        self._w = np.asarray(weights if weights is not None else [], dtype=np.float64)
+        self._summary = None
+
+    @property
+    def weights(self) -> DenseVector:
+        return DenseVector(self._w)
+
+    @property
+    def numFeatures(self) -> int:
+        return self._layers[0]
+
+    @property
+    def numClasses(self) -> int:
+        return self._layers[-1]
+
+    def _scores(self, x: torch.Tensor) -> torch.Tensor:
+        p = torch.as_tensor(self._w, device=x.device)
+        return _mlp_forward(x.to(torch.float64), _mlp_unpack(p, self._layers))
+
+    def _transform(self, df):
+        z = self._scores(df._feature_matrix(self.getFeaturesCol()))
+        prob = torch.softmax(z, 1)
+        out = df
+        if self.getRawPredictionCol():
+            out = _replace_col(out, self.getRawPredictionCol(), ColumnData(z.contiguous(), None, T.VectorUDT()))
+        if self.getProbabilityCol():
+            out = _replace_col(out, self.getProbabilityCol(), ColumnData(prob.contiguous(), None, T.VectorUDT()))
+        thr = self.getOrDefault("thresholds") if self.isSet("thresholds") else None
+        sc = prob / torch.as_tensor(np.asarray(thr, dtype=np.float64), device=prob.device) if thr else prob
+        return _replace_col(out, self.getPredictionCol(),
+                            ColumnData(torch.argmax(sc, 1).to(torch.float64), None, T.DoubleType()))
+
+    def predict(self, value) -> float:
+        z = self._scores(torch.as_tensor(as_array(value), dtype=torch.float64).reshape(1, -1))
+        return float(torch.argmax(z, 1)[0])
+
+    def predictProbability(self, value) -> DenseVector:
+        z = self._scores(torch.as_tensor(as_array(value), dtype=torch.float64).reshape(1, -1))
+        return DenseVector(torch.softmax(z, 1)[0].cpu().numpy())
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        U.write_metadata(self, path)
+        U.write_parquet(path, "data", pa.Table.from_pylist(
+            [{"layers": self._layers, "weights": U.vector_struct(self._w)}],
+            schema=pa.schema([("layers", pa.list_(pa.int32())), ("weights", U.vector_arrow_type())])))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        r = U.read_parquet(path, "data").to_pylist()[0]
+        m = cls(r["layers"], U.vector_from_struct(r["weights"]))
+        U.apply_params(m, md)
+        return m
+
+
+__all__ = ["LinearSVC", "LinearSVCModel", "LinearSVCSummary", "LinearSVCTrainingSummary", "OneVsRest",
+           "OneVsRestModel", "MultilayerPerceptronClassifier", "MultilayerPerceptronClassificationModel"]

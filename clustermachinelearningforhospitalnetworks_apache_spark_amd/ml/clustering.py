@@ -223,3 +223,4 @@ class KMeansSummary:
 
 
 from .bisecting import BisectingKMeans, BisectingKMeansModel  # noqa: E402,F401
+from .gmm import GaussianMixture, GaussianMixtureModel, GaussianMixtureSummary  # noqa: E402,F401

@@ -410,3 +410,5 @@ class GBTRegressionModel(GBTModelMixin, Model):
 
 from .glr import (GeneralizedLinearRegression, GeneralizedLinearRegressionModel,  # noqa: E402,F401
                   GeneralizedLinearRegressionTrainingSummary)
+from .regression_more import (AFTSurvivalRegression, AFTSurvivalRegressionModel,  # noqa: E402,F401
+                              IsotonicRegression, IsotonicRegressionModel)

@@ -96,6 +96,18 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "AFTSurvivalRegression": "org.apache.spark.ml.regression.AFTSurvivalRegression",
+    "AFTSurvivalRegressionModel": "org.apache.spark.ml.regression.AFTSurvivalRegressionModel",
+    "IsotonicRegression": "org.apache.spark.ml.regression.IsotonicRegression",
+    "IsotonicRegressionModel": "org.apache.spark.ml.regression.IsotonicRegressionModel",
+    "GaussianMixture": "org.apache.spark.ml.clustering.GaussianMixture",
+    "GaussianMixtureModel": "org.apache.spark.ml.clustering.GaussianMixtureModel",
+    "LinearSVC": "org.apache.spark.ml.classification.LinearSVC",
+    "LinearSVCModel": "org.apache.spark.ml.classification.LinearSVCModel",
+    "OneVsRest": "org.apache.spark.ml.classification.OneVsRest",
+    "OneVsRestModel": "org.apache.spark.ml.classification.OneVsRestModel",
+    "MultilayerPerceptronClassifier": "org.apache.spark.ml.classification.MultilayerPerceptronClassifier",
+    "MultilayerPerceptronClassificationModel": "org.apache.spark.ml.classification.MultilayerPerceptronClassificationModel",
     "RFormulaModel": "org.apache.spark.ml.feature.RFormulaModel",
     "IndexToString": "org.apache.spark.ml.feature.IndexToString",
 }
@@ -141,6 +153,18 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "AFTSurvivalRegression": "regression",
+    "AFTSurvivalRegressionModel": "regression",
+    "IsotonicRegression": "regression",
+    "IsotonicRegressionModel": "regression",
+    "GaussianMixture": "clustering",
+    "GaussianMixtureModel": "clustering",
+    "LinearSVC": "classification",
+    "LinearSVCModel": "classification",
+    "OneVsRest": "classification",
+    "OneVsRestModel": "classification",
+    "MultilayerPerceptronClassifier": "classification",
+    "MultilayerPerceptronClassificationModel": "classification",
     "RFormulaModel": "feature",
     "IndexToString": "feature",
 }

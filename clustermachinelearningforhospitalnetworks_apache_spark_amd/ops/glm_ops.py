@@ -24,6 +24,7 @@ _native.register_kernel_sigs({
     "cml_linear_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "cml_gram": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_partial_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "cml_glm_loss_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
                                c_vp, c_ll, c_ll, c_vp]),
 })
@@ -164,6 +165,48 @@ def logreg_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
                                            ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
                                            g, 0, _native.stream_ptr())
     _native.check(st, "logreg_grad")
+    return partial_colsum(out)
+
+
+_LOSS = {"logistic": 0, "hinge": 1, "squared": 2}
+
+
+def loss_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor, weight: Optional[torch.Tensor] = None,
+              loss: str = "hinge") -> torch.Tensor:
+    """K13 with a selectable per-row loss of the margin m = x·w + b: 'logistic' (= logreg_grad),
+    'hinge' (LinearSVC; labels {0, 1} mapped to ±1) or 'squared' (½(m − y)²).  Returns the float64
+    [grad_w (d) | grad_b | loss | weight_sum] sums of the local shard, X read once."""
+    code_l = _LOSS[loss]
+    n = x.shape[0]
+    coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    if not x.is_cuda or n == 0:
+        xf = x[:, :d].to(torch.float64)
+        m = xf @ coef[:d] + coef[d]
+        yy = y.to(torch.float64)
+        ww = torch.ones_like(yy) if weight is None else weight.to(torch.float64)
+        if code_l == 0:
+            r = ww * (torch.sigmoid(m) - yy)
+            lr = torch.nn.functional.softplus(m) - yy * m
+        elif code_l == 1:
+            ys = torch.where(yy > 0.5, 1.0, -1.0).to(torch.float64)
+            t = 1.0 - ys * m
+            r = torch.where(t > 0, -ww * ys, torch.zeros_like(t))
+            lr = t.clamp(min=0.0)
+        else:
+            e = m - yy
+            r = ww * e
+            lr = 0.5 * e * e
+        return torch.cat([xf.T @ r, r.sum().reshape(1), (ww * lr).sum().reshape(1), ww.sum().reshape(1)])
+    xx = _prep(x)
+    code = _CODE[xx.dtype]
+    g = _grid(n, d, code, xx.device, "logreg")
+    out = torch.empty((g, d + 3), dtype=torch.float64, device=xx.device)
+    yy = y.to(torch.float64).contiguous()
+    ww = weight.to(torch.float64).contiguous() if weight is not None else None
+    st = _native.kernels().cml_glm_loss_grad(xx.data_ptr(), n, xx.stride(0), d, code, yy.data_ptr(),
+                                             ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
+                                             g, code_l, _native.stream_ptr())
+    _native.check(st, "glm_loss_grad")
     return partial_colsum(out)
 
 
