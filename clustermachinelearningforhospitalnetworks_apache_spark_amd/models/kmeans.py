@@ -26,6 +26,7 @@ the numerical oracle).
 from __future__ import annotations
 
 import math
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -121,7 +122,10 @@ class LloydEngine:
         # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
         # removes the per-launch host cost that dominates small shards. Default: single rank (a
         # multi-rank step contains RCCL collectives, which stay eagerly launched).
-        self.use_graph = (self.comm.world_size == 1) if use_graph is None else bool(use_graph)
+        if use_graph is None:
+            env = os.environ.get("CML_KMEANS_GRAPH")  # "0": eager steps on one rank (the multi-rank launch path)
+            use_graph = (self.comm.world_size == 1) if env is None else (env == "1" and self.comm.world_size == 1)
+        self.use_graph = bool(use_graph)
         self._graph = None
         self.k = int(k)
         self.d = int(d)

@@ -671,7 +671,8 @@ class Column:
     astype = cast
 
     def alias(self, *names):
-        return Column(Alias(self._expr, names[0]))
+        # several names: the columns of a multi-column generator (posexplode -> pos, col)
+        return Column(Alias(self._expr, names[0] if len(names) == 1 else tuple(names)))
 
     name = alias
 

@@ -133,6 +133,9 @@ class DataFrame:
         if any(e.is_aggregate() for e in exprs):
             from .group import aggregate
             return aggregate(self, [], exprs)
+        from .functions_more import Generator, select_with_generator
+        if any(isinstance(e.child if isinstance(e, Alias) else e, Generator) for e in exprs):
+            return select_with_generator(self, exprs)
         names, datas = [], []
         for e in exprs:
             names.append(e.name())
@@ -158,7 +161,13 @@ class DataFrame:
     def withColumn(self, name: str, col: Column) -> "DataFrame":
         if self._stream is not None:
             return self._lazy("withColumn", name, col)
-        data = _as_expr(col).eval(self)
+        e = _as_expr(col)
+        from .functions_more import Generator
+        if isinstance(e, Generator) or (isinstance(e, Alias) and isinstance(e.child, Generator)):
+            inner = e.child if isinstance(e, Alias) else e
+            keep = [ColRef(c) for c in self.columns if c != name]
+            return self.select(*keep, Alias(inner, name))
+        data = e.eval(self)
         fields = list(self._schema.fields)
         cols = dict(self._cols)
         if name in cols:

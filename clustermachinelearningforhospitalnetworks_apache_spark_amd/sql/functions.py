@@ -545,3 +545,6 @@ def from_unixtime(c: ColumnOrName, fmt: str = "yyyy-MM-dd HH:mm:ss") -> Column:
     py = _spark_to_strftime(fmt)
     return _host_map("from_unixtime", [c], lambda s: _dt.datetime.utcfromtimestamp(int(s)).strftime(py),
                      T.StringType())
+
+
+from .functions_more import *  # noqa: E402,F401,F403  (statistical aggregates, math/date/string, arrays, explode)

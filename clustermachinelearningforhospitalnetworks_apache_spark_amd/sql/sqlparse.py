@@ -380,12 +380,25 @@ class Parser:
         fn = getattr(F, lname, None)
         if fn is None:
             raise SyntaxError(f"unknown function {name}")
-        cols = [Column(a) for a in args]
+        lit_pos = _LIT_ARGS.get(lname, ())
+        cols = [a.value if (i in lit_pos and isinstance(a, Lit)) else Column(a) for i, a in enumerate(args)]
         if lname == "round" and len(args) == 2:
             return F.round(cols[0], int(args[1].value))._expr
         if lname in ("current_timestamp", "current_date", "now"):
             return fn()._expr
         return fn(*cols)._expr
+
+
+# argument positions that the Python builders take as plain values (SQL passes literals there)
+_LIT_ARGS = {
+    "percentile": (1,), "percentile_approx": (1, 2), "sha2": (1,), "repeat": (1,), "instr": (1,), "locate": (0, 2),
+    "translate": (1, 2), "add_months": (1,), "date_trunc": (0,), "trunc": (1,), "bround": (1,), "element_at": (1,),
+    "array_contains": (1,), "array_join": (1, 2), "sort_array": (1,), "date_add": (1,), "date_sub": (1,),
+    "substring": (1, 2), "substr": (1, 2), "lpad": (1, 2), "rpad": (1, 2), "regexp_replace": (1, 2),
+    "regexp_extract": (1, 2), "split": (1,), "date_format": (1,), "concat_ws": (0,), "from_unixtime": (1,),
+    "to_date": (1,), "to_timestamp": (1,), "unix_timestamp": (1,), "months_between": (2,),
+    "approx_count_distinct": (1,),
+}
 
 
 def _like(e: Expr, pattern: str) -> Expr:

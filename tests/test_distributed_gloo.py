@@ -102,6 +102,26 @@ def _workload(out_path, rank, master="local[1]"):
     res["win"] = [[r.g, r.rn, r.s, r.lb] for r in wd][:300]
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
     res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
+    # round-2 additions: device aggregates merged across ranks, selectors, SVM, GMM, AFT, isotonic
+    st = spark.createDataFrame(pdf).select(F.skewness("a"), F.kurtosis("b"), F.corr("a", "y"), F.covar_samp("c", "d"),
+                                           F.median("d"), F.percentile("a", [0.25, 0.75])).collect()[0]
+    res["stat_aggs"] = [st[0], st[1], st[2], st[3], st[4]] + list(st[5])
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.stat import Summarizer
+    sm = f.select(Summarizer.metrics("mean", "variance", "max").summary(F.col("features"))).collect()[0][0]
+    res["summ"] = np.r_[sm.mean.toArray(), sm.variance.toArray(), sm.max.toArray()].tolist()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LinearSVC
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import GaussianMixture
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import RobustScaler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import (AFTSurvivalRegression,
+                                                                                            IsotonicRegression)
+    sv = LinearSVC(maxIter=30, regParam=0.01).fit(lab)
+    res["svc"] = sv.coefficients.toArray().tolist() + [sv.intercept]
+    res["gmm"] = GaussianMixture(k=2, seed=4, maxIter=10).fit(f).weights
+    res["robust"] = RobustScaler(inputCol="features", outputCol="r").fit(f).range.toArray().tolist()
+    surv = f.withColumn("t", F.exp(F.col("a") * 0.3)).withColumn("cens", F.when(F.col("b") > 0.0, 1.0).otherwise(0.0))
+    aft = AFTSurvivalRegression(labelCol="t", censorCol="cens", maxIter=30).fit(surv)
+    res["aft"] = aft.coefficients.toArray().tolist() + [aft.intercept, aft.scale]
+    res["iso"] = IsotonicRegression(labelCol="y", featureIndex=3).fit(f).predictions.toArray().tolist()[:50]
     if rank == 0:
         with open(out_path, "w") as fh:
             json.dump(res, fh)
@@ -164,6 +184,13 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
     assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
     np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)
+    np.testing.assert_allclose(rw["stat_aggs"], r1["stat_aggs"], rtol=1e-9)
+    np.testing.assert_allclose(rw["summ"], r1["summ"], rtol=1e-10)
+    np.testing.assert_allclose(rw["robust"], r1["robust"], rtol=1e-12)
+    np.testing.assert_allclose(rw["iso"], r1["iso"], rtol=1e-10)
+    np.testing.assert_allclose(rw["svc"], r1["svc"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(rw["aft"], r1["aft"], rtol=1e-5, atol=1e-7)
+    np.testing.assert_allclose(rw["gmm"], r1["gmm"], rtol=1e-6)
 
 
 @pytest.mark.parametrize("world", [2, 3])
