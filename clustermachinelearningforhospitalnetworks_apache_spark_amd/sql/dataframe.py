@@ -24,6 +24,7 @@ import torch
 from . import types as T
 from .column import (AggExpr, Alias, ColRef, Column, ColumnData, Expr, Lit, SortOrder, _expr, _to_host,
                      micros_to_datetime, ts_to_micros)
+from .dataframe_more import DataFrameMoreMixin
 
 
 def _as_expr(c) -> Expr:
@@ -36,7 +37,7 @@ def _as_expr(c) -> Expr:
     return Lit(c)
 
 
-class DataFrame:
+class DataFrame(DataFrameMoreMixin):
     def __init__(self, session, schema: T.StructType, cols: Dict[str, ColumnData], nrows: int,
                  row_ids: torch.Tensor, device: torch.device, stream=None):
         self._session = session
@@ -534,7 +535,6 @@ class DataFrame:
             cols = tuple(cols[0])
         return describe(self, list(cols))
 
-    summary = describe
 
     def join(self, other: "DataFrame", on=None, how: str = "inner") -> "DataFrame":
         from .group import join_frames

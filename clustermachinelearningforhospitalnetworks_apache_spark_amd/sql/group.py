@@ -253,10 +253,25 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
     return rows_round_robin(df._session, schema, rows)
 
 
+def _as_key_exprs(cols) -> List[Expr]:
+    from .dataframe import _as_expr
+    if len(cols) == 1 and isinstance(cols[0], (list, tuple)):
+        cols = tuple(cols[0])
+    return [_as_expr(c) for c in cols]
+
+
 class GroupedData:
     def __init__(self, df: DataFrame, keys: List[Expr]):
         self.df = df
         self.keys = keys
+
+    def pivot(self, pivot_col, values=None):
+        from .dataframe_more import PivotedData
+        return PivotedData(self.df, self.keys, pivot_col, list(values) if values is not None else None)
+
+    def applyInPandas(self, func, schema):
+        from .dataframe_more import apply_in_pandas
+        return apply_in_pandas(self, func, schema)
 
     def agg(self, *exprs) -> DataFrame:
         if len(exprs) == 1 and isinstance(exprs[0], dict):

@@ -1,0 +1,81 @@
+"""Set operations, summary, df.stat, pivot, rollup / cube, applyInPandas / mapInPandas."""
+import numpy as np
+import pandas as pd
+import pytest
+
+from helpers import session
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+
+
+@pytest.fixture(scope="module")
+def spark():
+    return session()
+
+
+def test_set_operations(spark):
+    a = spark.createDataFrame([(1, "x"), (1, "x"), (2, "y"), (3, "z")], "i INT, s STRING")
+    b = spark.createDataFrame([(1, "x"), (3, "z"), (3, "z"), (4, "w")], "i INT, s STRING")
+    rows = lambda df: sorted(tuple(r) for r in df.collect())  # noqa: E731
+    assert rows(a.intersect(b)) == [(1, "x"), (3, "z")]
+    assert rows(a.intersectAll(b)) == [(1, "x"), (3, "z")]
+    assert rows(a.subtract(b)) == [(2, "y")]
+    assert rows(a.exceptAll(b)) == [(1, "x"), (2, "y")]
+
+
+def test_summary_and_stat(spark):
+    rs = np.random.RandomState(0)
+    x = rs.normal(size=101)
+    y = 2 * x + rs.normal(size=101)
+    df = spark.createDataFrame([(float(a), float(b), "g" + str(i % 3)) for i, (a, b) in enumerate(zip(x, y))],
+                               "x DOUBLE, y DOUBLE, g STRING")
+    s = {r.summary: r for r in df.summary().collect()}
+    assert s["count"].x == "101" and float(s["mean"].x) == pytest.approx(x.mean())
+    srt = np.sort(x)
+    assert float(s["50%"].x) == pytest.approx(srt[50]) and float(s["25%"].x) == pytest.approx(srt[25])
+    assert s["mean"].g is None and s["min"].g == "g0"
+    assert df.stat.approxQuantile("x", [0.0, 0.5, 1.0], 0.0) == [srt[0], srt[50], srt[-1]]
+    assert df.stat.corr("x", "y") == pytest.approx(np.corrcoef(x, y)[0, 1])
+    assert df.cov("x", "y") == pytest.approx(np.cov(x, y)[0, 1])
+    ct = df.withColumn("pos", F.col("x") > 0).stat.crosstab("g", "pos")
+    assert ct.columns == ["g_pos", "false", "true"]
+    tot = sum(r[1] + r[2] for r in ct.collect())
+    assert tot == 101
+    fi = df.stat.freqItems(["g"], 0.3).collect()[0][0]
+    assert sorted(fi) == ["g0", "g1", "g2"]
+    sb = df.stat.sampleBy("g", {"g0": 1.0, "g1": 0.0}, seed=3)
+    assert set(r.g for r in sb.collect()) == {"g0"} and sb.count() == 34
+
+
+def test_pivot_rollup_cube(spark):
+    df = spark.createDataFrame([("a", 2024, 1.0), ("a", 2025, 2.0), ("b", 2024, 3.0), ("a", 2024, 4.0)],
+                               "h STRING, yr INT, v DOUBLE")
+    p = df.groupBy("h").pivot("yr").agg(F.sum("v"))
+    assert p.columns == ["h", "2024", "2025"]
+    got = {r.h: (r["2024"], r["2025"]) for r in p.collect()}
+    assert got == {"a": (5.0, 2.0), "b": (3.0, None)}
+    p2 = df.groupBy("h").pivot("yr", [2025]).agg(F.sum("v").alias("s"), F.count("v").alias("n"))
+    assert p2.columns == ["h", "2025_s", "2025_n"]
+    r = df.rollup("h", "yr").agg(F.sum("v").alias("s"))
+    res = {(x.h, x.yr): x.s for x in r.collect()}
+    assert res[(None, None)] == 10.0 and res[("a", None)] == 7.0 and res[("a", 2024)] == 5.0
+    assert len(res) == 1 + 2 + 3
+    c = df.cube("h", "yr").agg(F.sum("v").alias("s"))
+    resc = {(x.h, x.yr): x.s for x in c.collect()}
+    assert resc[(None, 2024)] == 8.0 and len(resc) == 1 + 2 + 2 + 3
+
+
+def test_pandas_functions(spark):
+    df = spark.createDataFrame([("a", 1.0), ("a", 3.0), ("b", 5.0)], "g STRING, v DOUBLE")
+
+    def center(pdf):
+        return pdf.assign(v=pdf.v - pdf.v.mean())
+    out = df.groupBy("g").applyInPandas(center, "g STRING, v DOUBLE")
+    assert sorted((r.g, r.v) for r in out.collect()) == [("a", -1.0), ("a", 1.0), ("b", 0.0)]
+
+    def double(it):
+        for pdf in it:
+            yield pdf.assign(v=pdf.v * 2)
+    m = df.mapInPandas(double, "g STRING, v DOUBLE")
+    assert sorted(r.v for r in m.collect()) == [2.0, 6.0, 10.0]
+    assert df.checkpoint() is df and df.hint("broadcast") is df
+    assert df.toJSON()[0] == '{"g": "a", "v": 1.0}'
