@@ -504,3 +504,4 @@ from .naive_bayes import NaiveBayes, NaiveBayesModel  # noqa: E402,F401
 from .classification_more import (LinearSVC, LinearSVCModel, LinearSVCSummary,  # noqa: E402,F401
                                   LinearSVCTrainingSummary, MultilayerPerceptronClassificationModel,
                                   MultilayerPerceptronClassifier, OneVsRest, OneVsRestModel)
+from .fm import FMClassificationModel, FMClassifier  # noqa: E402,F401

@@ -412,3 +412,4 @@ from .glr import (GeneralizedLinearRegression, GeneralizedLinearRegressionModel,
                   GeneralizedLinearRegressionTrainingSummary)
 from .regression_more import (AFTSurvivalRegression, AFTSurvivalRegressionModel,  # noqa: E402,F401
                               IsotonicRegression, IsotonicRegressionModel)
+from .fm import FMRegressionModel, FMRegressor  # noqa: E402,F401

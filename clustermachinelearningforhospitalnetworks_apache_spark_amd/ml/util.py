@@ -96,6 +96,12 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "FPGrowth": "org.apache.spark.ml.fpm.FPGrowth",
+    "FPGrowthModel": "org.apache.spark.ml.fpm.FPGrowthModel",
+    "FMRegressor": "org.apache.spark.ml.regression.FMRegressor",
+    "FMRegressionModel": "org.apache.spark.ml.regression.FMRegressionModel",
+    "FMClassifier": "org.apache.spark.ml.classification.FMClassifier",
+    "FMClassificationModel": "org.apache.spark.ml.classification.FMClassificationModel",
     "AFTSurvivalRegression": "org.apache.spark.ml.regression.AFTSurvivalRegression",
     "AFTSurvivalRegressionModel": "org.apache.spark.ml.regression.AFTSurvivalRegressionModel",
     "IsotonicRegression": "org.apache.spark.ml.regression.IsotonicRegression",
@@ -153,6 +159,9 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "FPGrowth": "fpm", "FPGrowthModel": "fpm",
+    "FMRegressor": "regression", "FMRegressionModel": "regression",
+    "FMClassifier": "classification", "FMClassificationModel": "classification",
     "AFTSurvivalRegression": "regression",
     "AFTSurvivalRegressionModel": "regression",
     "IsotonicRegression": "regression",

@@ -116,3 +116,34 @@ def test_gaussian_mixture(spark, tmp_path):
     m50.write().overwrite().save(p)
     back = U.load(p)
     np.testing.assert_allclose(_col(back.transform(df), "probability"), _col(m50.transform(df), "probability"))
+
+
+def test_factorization_machines(spark, tmp_path):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import FMClassifier
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import FMRegressor
+    rs = np.random.RandomState(5)
+    n, d, f = 600, 4, 2
+    X = rs.normal(size=(n, d))
+    V = rs.normal(scale=0.7, size=(d, f))
+    w = np.array([0.5, -0.3, 0.0, 0.2])
+    inter = 0.5 * (((X @ V) ** 2) - (X ** 2) @ (V ** 2)).sum(1)
+    y = 1.0 + X @ w + inter + 0.05 * rs.normal(size=n)
+    df = _frame(spark, X, {"label": y})
+    m = FMRegressor(factorSize=2, stepSize=0.05, maxIter=400, seed=3).fit(df)
+    pred = _col(m.transform(df), "prediction")
+    assert np.mean((pred - y) ** 2) < 0.1 * np.var(y)
+    # prediction formula
+    W, Vm = m.linear.toArray(), m.factors.toArray()
+    ref = m.intercept + X @ W + 0.5 * (((X @ Vm) ** 2) - (X ** 2) @ (Vm ** 2)).sum(1)
+    np.testing.assert_allclose(pred, ref, rtol=1e-10)
+    p = str(tmp_path / "fm")
+    m.write().overwrite().save(p)
+    back = U.load(p)
+    np.testing.assert_allclose(_col(back.transform(df), "prediction"), pred)
+    yc = (inter > np.median(inter)).astype(float)
+    mc = FMClassifier(factorSize=2, stepSize=0.05, maxIter=300, seed=1).fit(_frame(spark, X, {"label": yc}))
+    out = mc.transform(_frame(spark, X, {"label": yc}))
+    assert (_col(out, "prediction") == yc).mean() > 0.85
+    np.testing.assert_allclose(_col(out, "probability").sum(1), 1.0)
+    nolin = FMRegressor(factorSize=2, fitLinear=False, fitIntercept=False, maxIter=5, seed=3).fit(df)
+    assert np.all(nolin.linear.toArray() == 0) and nolin.intercept == 0.0
