@@ -96,6 +96,8 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "ALS": "org.apache.spark.ml.recommendation.ALS",
+    "ALSModel": "org.apache.spark.ml.recommendation.ALSModel",
     "FPGrowth": "org.apache.spark.ml.fpm.FPGrowth",
     "FPGrowthModel": "org.apache.spark.ml.fpm.FPGrowthModel",
     "FMRegressor": "org.apache.spark.ml.regression.FMRegressor",
@@ -159,6 +161,7 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "ALS": "recommendation", "ALSModel": "recommendation",
     "FPGrowth": "fpm", "FPGrowthModel": "fpm",
     "FMRegressor": "regression", "FMRegressionModel": "regression",
     "FMClassifier": "classification", "FMClassificationModel": "classification",

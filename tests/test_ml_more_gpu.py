@@ -59,6 +59,7 @@ def test_ml_more_gpu_equals_cpu():
     pdf["cat"] = rs.randint(0, 3, n).astype(float)
     outs = {}
     for master in ("mi355x", "local[1]"):
+        rs2 = np.random.RandomState(11)
         spark = SparkSession.builder.appName("mlmore").master(master).getOrCreate()
         df = VectorAssembler(inputCols=list("abcd"), outputCol="features").transform(spark.createDataFrame(pdf))
         r = {}
@@ -80,6 +81,14 @@ def test_ml_more_gpu_equals_cpu():
         r["aft"] = np.r_[aft.coefficients.toArray(), aft.intercept, aft.scale]
         iso = IsotonicRegression(labelCol="y").fit(df)
         r["iso"] = iso.predictions.toArray()
+        from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import FMRegressor
+        from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.recommendation import ALS
+        fm = FMRegressor(labelCol="t", factorSize=3, maxIter=30, stepSize=0.05, seed=2).fit(df)
+        r["fm"] = np.r_[fm.intercept, fm.linear.toArray(), fm.factors.toArray().ravel()]
+        rt = spark.createDataFrame(pd.DataFrame({"user": rs2.randint(0, 50, 2000), "item": rs2.randint(0, 40, 2000),
+                                                 "rating": rs2.rand(2000) * 5}))
+        als = ALS(rank=4, maxIter=5, seed=3).fit(rt)
+        r["als"] = np.stack([np.array(x.features) for x in sorted(als.userFactors.collect(), key=lambda x: x.id)])
         s = df.select(Summarizer.metrics("mean", "variance", "max").summary(F.col("features"))).collect()[0][0]
         r["summ"] = np.r_[s.mean.toArray(), s.variance.toArray(), s.max.toArray()]
         outs[master] = r
@@ -92,3 +101,5 @@ def test_ml_more_gpu_equals_cpu():
         np.testing.assert_allclose(g[key], c[key], rtol=1e-4, atol=1e-5, err_msg=key)
     np.testing.assert_allclose(g["ovr"], c["ovr"], rtol=1e-5, atol=1e-5, err_msg="ovr")
     np.testing.assert_allclose(g["mlp"], c["mlp"], rtol=1e-4, atol=1e-4, err_msg="mlp")
+    np.testing.assert_allclose(g["fm"], c["fm"], rtol=1e-5, atol=1e-7, err_msg="fm")
+    np.testing.assert_allclose(g["als"], c["als"], rtol=1e-4, atol=1e-5, err_msg="als")
