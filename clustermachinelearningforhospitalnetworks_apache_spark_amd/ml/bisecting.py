@@ -44,27 +44,12 @@ from . import util as U
 from .util import java_hash
 from .base import Estimator, Model
 from .feature import _replace_col
+from .util import JavaRandom  # noqa: F401 (re-exported)
 from .linalg import as_array
 
 EPSILON = np.finfo(np.float64).eps  # MLUtils.EPSILON: 2.220446049250313e-16
 LEVEL_LIMIT = 63                    # log2(Long.MaxValue): raw indices stay below 2^63
 _CHUNK = 1 << 24                    # elements per f64 row chunk (bounded temporaries)
-
-
-class JavaRandom:
-    """``java.util.Random``: the 48-bit LCG and nextDouble, bit-exact."""
-
-    _MUL, _ADD, _MASK = 0x5DEECE66D, 0xB, (1 << 48) - 1
-
-    def __init__(self, seed: int):
-        self._s = (int(seed) ^ self._MUL) & self._MASK
-
-    def _next(self, bits: int) -> int:
-        self._s = (self._s * self._MUL + self._ADD) & self._MASK
-        return self._s >> (48 - bits)
-
-    def next_double(self) -> float:
-        return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
 
 
 class _Node:

@@ -656,3 +656,5 @@ from .feature_more import (ChiSqSelector, ChiSqSelectorModel, ElementwiseProduct
                            RobustScaler, RobustScalerModel, SQLTransformer, UnivariateFeatureSelector,
                            UnivariateFeatureSelectorModel, VarianceThresholdSelector, VarianceThresholdSelectorModel,
                            VectorIndexer, VectorIndexerModel, VectorSlicer)
+from .lsh import (BucketedRandomProjectionLSH, BucketedRandomProjectionLSHModel, MinHashLSH,  # noqa: E402,F401
+                  MinHashLSHModel)

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import importlib
 import json
+import math
 import os
 import re
 import shutil
@@ -96,6 +97,10 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "BucketedRandomProjectionLSH": "org.apache.spark.ml.feature.BucketedRandomProjectionLSH",
+    "BucketedRandomProjectionLSHModel": "org.apache.spark.ml.feature.BucketedRandomProjectionLSHModel",
+    "MinHashLSH": "org.apache.spark.ml.feature.MinHashLSH",
+    "MinHashLSHModel": "org.apache.spark.ml.feature.MinHashLSHModel",
     "ALS": "org.apache.spark.ml.recommendation.ALS",
     "ALSModel": "org.apache.spark.ml.recommendation.ALSModel",
     "FPGrowth": "org.apache.spark.ml.fpm.FPGrowth",
@@ -161,6 +166,10 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "BucketedRandomProjectionLSH": "feature",
+    "BucketedRandomProjectionLSHModel": "feature",
+    "MinHashLSH": "feature",
+    "MinHashLSHModel": "feature",
     "ALS": "recommendation", "ALSModel": "recommendation",
     "FPGrowth": "fpm", "FPGrowthModel": "fpm",
     "FMRegressor": "regression", "FMRegressionModel": "regression",
@@ -180,6 +189,52 @@ _PY = {
     "RFormulaModel": "feature",
     "IndexToString": "feature",
 }
+
+
+class JavaRandom:
+    """``java.util.Random``: the 48-bit LCG and nextDouble, bit-exact."""
+
+    _MUL, _ADD, _MASK = 0x5DEECE66D, 0xB, (1 << 48) - 1
+
+    def __init__(self, seed: int):
+        self._s = (int(seed) ^ self._MUL) & self._MASK
+
+    def _next(self, bits: int) -> int:
+        self._s = (self._s * self._MUL + self._ADD) & self._MASK
+        return self._s >> (48 - bits)
+
+    def next_double(self) -> float:
+        return ((self._next(26) << 27) + self._next(27)) * (1.0 / (1 << 53))
+
+    def next_int(self, bound: int) -> int:
+        """``nextInt(bound)`` including Java's 32-bit overflow test in the rejection loop."""
+        r = self._next(31)
+        m = bound - 1
+        if bound & m == 0:
+            return (bound * r) >> 31
+        u = r
+        while True:
+            r = u % bound
+            v = (u - r + m) & 0xFFFFFFFF
+            if v < 0x80000000:  # non-negative as a Java int
+                return r
+            u = self._next(31)
+
+    def next_gaussian(self) -> float:
+        """``nextGaussian``: Marsaglia's polar method, the second deviate cached."""
+        g = getattr(self, "_gauss", None)
+        if g is not None:
+            self._gauss = None
+            return g
+        while True:
+            v1 = 2.0 * self.next_double() - 1.0
+            v2 = 2.0 * self.next_double() - 1.0
+            s = v1 * v1 + v2 * v2
+            if 0.0 < s < 1.0:
+                break
+        mul = math.sqrt(-2.0 * math.log(s) / s)
+        self._gauss = v2 * mul
+        return v1 * mul
 
 
 def java_hash(s: str) -> int:
