@@ -284,3 +284,151 @@ class ClusteringEvaluator(Evaluator):
             part = torch.stack([s.sum(), torch.tensor(float(len(lab)), dtype=torch.float64, device=x.device)])
         df._comm.allreduce_(part)
         return float(part[0] / part[1]) if part[1] > 0 else float("nan")
+
+
+# ------------------------------------------------------------------------- multilabel / ranking
+
+def _array_pairs(df, pred_col: str, label_col: str):
+    """This rank's (prediction list, label list) pairs; metrics merge per-rank sums."""
+    from ..sql.dataframe import column_to_python
+    p = column_to_python(df._column_data(pred_col))
+    lab = column_to_python(df._column_data(label_col))
+    return [(list(a or []), list(b or [])) for a, b in zip(p, lab)]
+
+
+class MultilabelClassificationEvaluator(Evaluator):
+    """Spark's MultilabelMetrics over array columns of predicted and true labels: subsetAccuracy,
+    accuracy, hammingLoss, precision, recall, f1Measure (default), micro*, and *ByLabel for
+    ``metricLabel``. Per-rank sums, one all-gather of the small count maps."""
+    _params = {
+        "predictionCol": ("prediction", "prediction column name", str),
+        "labelCol": ("label", "label column name", str),
+        "metricName": ("f1Measure", "metric name in evaluation", str),
+        "metricLabel": (0.0, "the class whose metric will be computed in *ByLabel", float),
+    }
+
+    def __init__(self, predictionCol=None, labelCol=None, metricName=None, metricLabel=None):
+        super().__init__(predictionCol=predictionCol, labelCol=labelCol, metricName=metricName,
+                         metricLabel=metricLabel)
+
+    def _evaluate(self, df) -> float:
+        pairs = _array_pairs(df, self.getPredictionCol(), self.getLabelCol())
+        s = np.zeros(8)  # n, subset, acc, prec, rec, f1, sumTp, sumFp (sumFn below)
+        fn = 0.0
+        by: dict = {}
+        labels = set()
+        for p, lab in pairs:
+            P, L = set(p), set(lab)
+            inter = len(P & L)
+            s[0] += 1
+            s[1] += P == L
+            den = len(P) + len(L) - inter
+            s[2] += inter / den if den else float("nan")
+            s[3] += inter / len(P) if P else 0.0
+            s[4] += inter / len(L) if L else float("nan")
+            s[5] += 2.0 * inter / (len(P) + len(L)) if (P or L) else float("nan")
+            s[6] += inter
+            s[7] += len(P - L)
+            fn += len(L - P)
+            labels |= L
+            for x in P | L:
+                t = by.setdefault(x, [0, 0, 0])
+                t[0] += x in P and x in L
+                t[1] += x in P and x not in L
+                t[2] += x in L and x not in P
+        parts = df._comm.allgather_object((s.tolist(), fn, by, sorted(labels, key=str)))
+        S = np.sum([np.asarray(q[0]) for q in parts], 0)
+        FN = sum(q[1] for q in parts)
+        allby: dict = {}
+        all_labels = set()
+        for _, _, b, labs in parts:
+            all_labels |= set(labs)
+            for k, v in b.items():
+                t = allby.setdefault(k, [0, 0, 0])
+                for i in range(3):
+                    t[i] += v[i]
+        n = S[0]
+        m = self.getMetricName()
+        if m == "subsetAccuracy":
+            return S[1] / n
+        if m == "accuracy":
+            return S[2] / n
+        if m == "hammingLoss":
+            return (S[7] + FN) / (n * max(len(all_labels), 1))
+        if m == "precision":
+            return S[3] / n
+        if m == "recall":
+            return S[4] / n
+        if m == "f1Measure":
+            return S[5] / n
+        tp, fp = S[6], S[7]
+        if m == "microPrecision":
+            return tp / (tp + fp)
+        if m == "microRecall":
+            return tp / (tp + FN)
+        if m == "microF1Measure":
+            return 2 * tp / (2 * tp + fp + FN)
+        t = allby.get(self.getMetricLabel(), [0, 0, 0])
+        prec = t[0] / (t[0] + t[1]) if t[0] + t[1] else 0.0
+        rec = t[0] / (t[0] + t[2]) if t[0] + t[2] else 0.0
+        if m == "precisionByLabel":
+            return prec
+        if m == "recallByLabel":
+            return rec
+        if m == "f1MeasureByLabel":
+            return 2 * prec * rec / (prec + rec) if prec + rec else 0.0
+        raise ValueError(f"unknown multilabel metric {m!r}")
+
+    def isLargerBetter(self) -> bool:
+        return self.getMetricName() != "hammingLoss"
+
+
+class RankingEvaluator(Evaluator):
+    """Spark's RankingMetrics with binary relevance: meanAveragePrecision (default),
+    meanAveragePrecisionAtK, precisionAtK, ndcgAtK, recallAtK over ranked prediction arrays and
+    ground-truth label arrays."""
+    _params = {
+        "predictionCol": ("prediction", "prediction column name", str),
+        "labelCol": ("label", "label column name", str),
+        "metricName": ("meanAveragePrecision", "metric name in evaluation", str),
+        "k": (10, "the ranking position value used in the *AtK metrics (> 0)", int),
+    }
+
+    def __init__(self, predictionCol=None, labelCol=None, metricName=None, k=None):
+        super().__init__(predictionCol=predictionCol, labelCol=labelCol, metricName=metricName, k=k)
+
+    def _evaluate(self, df) -> float:
+        pairs = _array_pairs(df, self.getPredictionCol(), self.getLabelCol())
+        m, k = self.getMetricName(), self.getK()
+        tot = 0.0
+        for pred, lab in pairs:
+            L = set(lab)
+            if m == "meanAveragePrecision":
+                hits, acc = 0, 0.0
+                for i, x in enumerate(pred):
+                    if x in L:
+                        hits += 1
+                        acc += hits / (i + 1)
+                tot += acc / len(L) if L else 0.0
+            elif m == "meanAveragePrecisionAtK":
+                hits, acc = 0, 0.0
+                for i, x in enumerate(pred[:k]):
+                    if x in L:
+                        hits += 1
+                        acc += hits / (i + 1)
+                tot += acc / min(len(L), k) if L else 0.0
+            elif m == "precisionAtK":
+                tot += sum(1 for x in pred[:k] if x in L) / k if L else 0.0
+            elif m == "recallAtK":
+                tot += sum(1 for x in pred[:k] if x in L) / len(L) if L else 0.0
+            elif m == "ndcgAtK":
+                if not L:
+                    continue
+                dcg = sum(1.0 / math.log2(i + 2) for i, x in enumerate(pred[:k]) if x in L)
+                idcg = sum(1.0 / math.log2(i + 2) for i in range(min(k, len(L))))
+                tot += dcg / idcg
+            else:
+                raise ValueError(f"unknown ranking metric {m!r}")
+        t = torch.tensor([tot, float(len(pairs))], dtype=torch.float64, device=df._device)
+        df._comm.allreduce_(t)
+        return float(t[0] / t[1]) if t[1] > 0 else float("nan")

@@ -97,6 +97,8 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "MultilabelClassificationEvaluator": "org.apache.spark.ml.evaluation.MultilabelClassificationEvaluator",
+    "RankingEvaluator": "org.apache.spark.ml.evaluation.RankingEvaluator",
     "BucketedRandomProjectionLSH": "org.apache.spark.ml.feature.BucketedRandomProjectionLSH",
     "BucketedRandomProjectionLSHModel": "org.apache.spark.ml.feature.BucketedRandomProjectionLSHModel",
     "MinHashLSH": "org.apache.spark.ml.feature.MinHashLSH",
@@ -166,6 +168,7 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "MultilabelClassificationEvaluator": "evaluation", "RankingEvaluator": "evaluation",
     "BucketedRandomProjectionLSH": "feature",
     "BucketedRandomProjectionLSHModel": "feature",
     "MinHashLSH": "feature",
