@@ -283,6 +283,31 @@ __device__ inline CT group_sum_ct(CT v, int lpr) {
   }
 }
 
+// A lane's share of a row dot product. f32: packed FMAs (v_pk_fma_f32) into two independent 2-wide
+// partial sums — half the VALU issue of scalar FMAs and no CPT-long dependency chain (fp8 rows give
+// a lane 16 columns per chunk; the scalar chain made K13 VALU-latency bound at 4.1 TB/s).
+template <typename CT, int NCH, int CPT>
+__device__ inline CT dot_ct(const CT (&v)[NCH][CPT], const CT (&w)[NCH][CPT]) {
+  if constexpr (sizeof(CT) == 4 && CPT % 4 == 0) {
+    f32x2_t ma = {0.f, 0.f}, mb = {0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < CPT; j += 4) {
+        ma = __builtin_elementwise_fma(f32x2_t{v[c][j], v[c][j + 1]}, f32x2_t{w[c][j], w[c][j + 1]}, ma);
+        mb = __builtin_elementwise_fma(f32x2_t{v[c][j + 2], v[c][j + 3]}, f32x2_t{w[c][j + 2], w[c][j + 3]}, mb);
+      }
+    return (ma.x + mb.x) + (ma.y + mb.y);
+  } else {
+    CT m = 0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
+    return m;
+  }
+}
+
 __device__ inline float sigmoid_ct(float m) { return 1.f / (1.f + __expf(-m)); }
 __device__ inline double sigmoid_ct(double m) {
   const double e = exp(-fabs(m));
@@ -446,11 +471,7 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
         yn[q] = ok ? y[row] : 0.0;
         wn[q] = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
       }
-      CT m = 0;
-#pragma unroll
-      for (int c = 0; c < NCH; ++c)
-#pragma unroll
-        for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
+      CT m = dot_ct<CT, NCH, CPT>(v, w);
       m = group_sum_ct<CT>(m, lpr) + b;
       CT r;
       double lrow;
@@ -467,10 +488,23 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
         r = (CT)wi * e;
         lrow = 0.5 * (double)e * (double)e;
       }
+      if constexpr (sizeof(CT) == 4 && CPT % 2 == 0) {
+        const f32x2_t r2 = {r, r};
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
+        for (int c = 0; c < NCH; ++c)
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
+          for (int j = 0; j < CPT; j += 2) {
+            const f32x2_t gg = __builtin_elementwise_fma(r2, f32x2_t{v[c][j], v[c][j + 1]},
+                                                         f32x2_t{g[c][j], g[c][j + 1]});
+            g[c][j] = gg.x;
+            g[c][j + 1] = gg.y;
+          }
+      } else {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
+      }
       if (li == 0) {
         gb += (double)r;
         loss += wi * lrow;
@@ -627,11 +661,7 @@ __global__ __launch_bounds__(kGlmThreads) void linear_predict_kernel(const T* __
     CT v[NCH][CPT];
     decode_group<T, CT, NCH>(raw, lpr, li, d, v);
     load_raw_group<T, NCH>(X, row + step, ld, lpr, li, d, row + step < n, raw);  // prefetch
-    CT m = 0;
-#pragma unroll
-    for (int c = 0; c < NCH; ++c)
-#pragma unroll
-      for (int j = 0; j < CPT; ++j) m = fma(v[c][j], w[c][j], m);
+    const CT m = dot_ct<CT, NCH, CPT>(v, w);
     const double mm = (double)group_sum_ct<CT>(m, lpr) + b;
     if (ok && li == 0) out[row] = link == 1 ? sigmoid_ct(mm) : mm;
   }
