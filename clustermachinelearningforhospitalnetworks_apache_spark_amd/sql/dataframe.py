@@ -524,8 +524,20 @@ class DataFrame(DataFrameMoreMixin):
         return self.dropDuplicates()
 
     def dropDuplicates(self, subset: Optional[Sequence[str]] = None) -> "DataFrame":
+        if self._stream is not None:
+            return self._lazy("_stream_dedup", list(subset) if subset else None)
         from .group import drop_duplicates
         return drop_duplicates(self, subset)
+
+    def _stream_dedup(self, subset) -> "DataFrame":
+        """Batch semantics of a streaming dropDuplicates (used for the plan's schema)."""
+        from .group import drop_duplicates
+        return drop_duplicates(self, subset)
+
+    def _stream_aggregate(self, keys, exprs) -> "DataFrame":
+        """Batch semantics of a streaming groupBy().agg() (used for the plan's schema)."""
+        from .group import aggregate
+        return aggregate(self, keys, exprs)
 
     drop_duplicates = dropDuplicates
 

@@ -137,9 +137,10 @@ def _merge(parts, fn: str):
     return var if fn == "variance" else math.sqrt(var)
 
 
-def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
+def local_partials(df: DataFrame, keys: List[Expr], exprs: List[Expr]):
+    """This rank's per-group partial aggregates: (specs, key_types, {key tuple: [partial per spec]}).
+    A spec is ("key", name, key index, None) or ("agg", name, AggExpr, values, input type)."""
     from .window import _WINDOW_TYPE, TimeWindow
-    comm = df._comm
     key_names = [k.name() for k in keys]
     # time-window keys (functions.window) may put a row into several buckets: expand rows first
     src = list(range(df._nrows))
@@ -184,7 +185,6 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
             vals = [vals[i] for i in src] if len(src) != df._nrows or src != list(range(df._nrows)) else vals
             itype = cd.dtype
         specs.append(("agg", alias or _agg_name(inner), inner, vals, itype))
-    # local partials per group
     groups: Dict[tuple, List[Any]] = {}
     order: List[tuple] = []
     for i in range(len(src)):
@@ -210,32 +210,40 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
                 else:
                     parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct))
         local[key] = parts
-    gathered = comm.allgather_object(local)
+    return specs, key_types, local
+
+
+def gather_partials(comm, local, nspecs: int):
+    """All ranks' partials per group, in first-seen (rank, local) order: ({key: [[partials] per spec]}, keys)."""
     merged: Dict[tuple, List[List[Any]]] = {}
     morder: List[tuple] = []
-    for part in gathered:
+    for part in comm.allgather_object(local):
         for key, parts in part.items():
             if key not in merged:
-                merged[key] = [[] for _ in specs]
+                merged[key] = [[] for _ in range(nspecs)]
                 morder.append(key)
             for j, p in enumerate(parts):
                 if p is not None:
                     merged[key][j].append(p)
-    rows = []
-    for key in morder:
-        row = []
-        for j, sp in enumerate(specs):
-            if sp[0] == "key":
-                row.append(key[sp[2]])
-            else:
-                if getattr(sp[2], "custom", False):
-                    row.append(sp[2].merge(merged[key][j]))
-                    continue
-                v = _merge(merged[key][j], sp[2].fn)
-                if sp[2].fn == "percentile":
-                    v = _percentile(v, getattr(sp[2], "arg", 0.5))
-                row.append(v)
-        rows.append(row)
+    return merged, morder
+
+
+def final_row(key: tuple, parts: List[List[Any]], specs) -> List[Any]:
+    row = []
+    for j, sp in enumerate(specs):
+        if sp[0] == "key":
+            row.append(key[sp[2]])
+        elif getattr(sp[2], "custom", False):
+            row.append(sp[2].merge(parts[j]))
+        else:
+            v = _merge(parts[j], sp[2].fn)
+            if sp[2].fn == "percentile":
+                v = _percentile(v, getattr(sp[2], "arg", 0.5))
+            row.append(v)
+    return row
+
+
+def result_schema(specs, key_types) -> T.StructType:
     fields = []
     for sp in specs:
         if sp[0] == "key":
@@ -244,12 +252,62 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
             fields.append(T.StructField(sp[1], sp[2].result_type(), True))
         else:
             fields.append(T.StructField(sp[1], _result_type(sp[2].fn, sp[4], getattr(sp[2], "arg", None)), True))
-    schema = T.StructType(fields)
-    for j, f in enumerate(fields):
+    return T.StructType(fields)
+
+
+def fix_long_columns(schema: T.StructType, rows: List[List[Any]]) -> None:
+    for j, f in enumerate(schema.fields):
         if isinstance(f.dataType, T.LongType):
             for r in rows:
                 if r[j] is not None:
                     r[j] = int(r[j])
+
+
+def combine_partials(parts: List[Any], fn: str):
+    """Several partials of one built-in aggregate -> one partial of the same kind (streaming state)."""
+    if not parts:
+        return None
+    kind = parts[0][0]
+    if kind == "n":
+        return ("n", sum(p[1] for p in parts))
+    if kind == "set":
+        out = set()
+        for p in parts:
+            out |= p[1]
+        return ("set", out)
+    if kind in ("first", "last"):
+        return (kind, _merge(parts, fn))
+    if kind == "list":
+        return ("list", [v for p in parts for v in p[1]])
+    if kind in ("min", "max"):
+        return (kind, _merge(parts, fn))
+    live = [p for p in parts if not (p[0] == "mom" and p[1] == 0)]
+    if not live:
+        return ("mom", 0, 0.0, 0.0, 0.0)
+    if all(p[0] == "isum" for p in live):
+        return ("isum", sum(p[1] for p in live), sum(p[2] for p in live))
+    n, mean, m2, s = 0, 0.0, 0.0, 0.0
+    for p in live:
+        if p[0] == "isum":
+            nb, sb = p[1], float(p[2])
+            mb, m2b = (sb / nb if nb else 0.0), 0.0
+        else:
+            nb, sb, mb, m2b = p[1], p[2], p[3], p[4]
+        delta = mb - mean
+        tot = n + nb
+        mean = mean + delta * nb / tot
+        m2 = m2 + m2b + delta * delta * n * nb / tot
+        n = tot
+        s += sb
+    return ("mom", n, s, mean, m2)
+
+
+def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
+    specs, key_types, local = local_partials(df, keys, exprs)
+    merged, morder = gather_partials(df._comm, local, len(specs))
+    rows = [final_row(key, merged[key], specs) for key in morder]
+    schema = result_schema(specs, key_types)
+    fix_long_columns(schema, rows)
     return rows_round_robin(df._session, schema, rows)
 
 
@@ -279,6 +337,8 @@ class GroupedData:
             exprs = tuple(getattr(F, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})")
                           for c, fn in exprs[0].items())
         es = [ColRef(k.name()) for k in self.keys] + [_as_expr(e) for e in exprs]
+        if self.df.isStreaming:
+            return self.df._lazy("_stream_aggregate", self.keys, es)
         return aggregate(self.df, self.keys, es)
 
     def _simple(self, fn: str, cols) -> DataFrame:

@@ -10,6 +10,12 @@ its sink finished.  On restart an offsets entry without a commit is re-run with 
 transaction is already in the table log, so a crash between the sink commit and the
 checkpoint commit cannot duplicate rows.
 
+Stateful operators: a streaming ``groupBy().agg()`` keeps per-group partial aggregates (the same
+partials the batch aggregation merges across ranks) in a versioned state checkpoint
+(``state/<id>``, written before the commit) and emits all groups (``complete``), the updated
+groups (``update``) or the groups whose event-time window the watermark passed (``append``);
+``dropDuplicates`` keeps the seen keys. Late rows (event time behind the watermark) are dropped.
+
 Defects of the reference are not reproduced: ``foreachBatch``
 calls ``fn(df, batch_id)``; ``.table(name)`` is accepted as an alias of
 ``toTable``; when both a foreachBatch function and a table target are given, each
@@ -141,8 +147,6 @@ class DataStreamWriter:
         m = mode.lower()
         if m not in ("append", "update", "complete"):
             raise ValueError(f"unknown output mode {mode}")
-        if m != "append":
-            raise NotImplementedError("only outputMode('append') is supported (the reference's mode, ref.py:113)")
         self._mode = m
         return self
 
@@ -202,6 +206,16 @@ class DataStreamWriter:
 
     def _start(self, table: Optional[str] = None, path: Optional[str] = None):
         session = self._df._session
+        plan = self._df._stream
+        has_agg = any(m == "_stream_aggregate" for m, _, _ in plan.ops)
+        if self._mode == "complete" and not has_agg:
+            raise ValueError("Complete output mode not supported when there are no streaming aggregations")
+        if self._mode == "append" and has_agg and not plan.watermark:
+            raise ValueError("Append output mode not supported when there are streaming aggregations without "
+                             "watermark")
+        if self._mode == "update" and has_agg and (table is not None or path is not None):
+            raise ValueError("update output mode is not supported by table / file sinks; use foreachBatch or "
+                             "the memory / console sinks")
         q = StreamingQuery(session, self._df._stream, self, table=table, path=path)
         session.streams._register(q)
         q._launch()
@@ -230,6 +244,9 @@ class StreamingQuery:
         self.recentProgress: List[dict] = []
         self._lock = threading.Lock()
         self._next_batch = None
+        self._batch_wm = 0          # watermark (ms) the running batch started with
+        self._wm_source = None      # frame the watermark column is read from (pre-aggregation)
+        self._state = self._load_state()  # stateful operators: {op index: state}
 
     # ------------------------------------------------------------------ checkpoint files
     def _load_or_create_id(self) -> str:
@@ -270,6 +287,37 @@ class StreamingQuery:
         with open(tmp, "w") as fh:
             json.dump(obj, fh)
         os.replace(tmp, p)
+
+    def _load_state(self) -> Dict[int, Any]:
+        """State of the stateful operators after the last committed batch (``state/<batch id>``,
+        written by this engine before the commit), identical on every rank."""
+        import pickle
+        comm = self._session._comm
+        st = None
+        if comm.is_root:
+            commits = self._ids("commits")
+            p = os.path.join(self._ckpt, "state", str(commits[-1])) if commits else None
+            if p and os.path.exists(p):
+                with open(p, "rb") as fh:
+                    st = pickle.load(fh)  # this engine's own checkpoint file
+        return comm.broadcast_object(st) or {}
+
+    def _save_state(self, bid: int) -> None:
+        import pickle
+        if not self._state or not self._session._comm.is_root:
+            return
+        d = os.path.join(self._ckpt, "state")
+        os.makedirs(d, exist_ok=True)
+        tmp = os.path.join(d, f"{bid}.tmp")
+        with open(tmp, "wb") as fh:
+            pickle.dump(self._state, fh)
+        os.replace(tmp, os.path.join(d, str(bid)))
+        for old in self._ids("state"):
+            if old < bid - 2:  # keep a short history (replays only ever need the last committed one)
+                try:
+                    os.remove(os.path.join(d, str(old)))
+                except OSError:
+                    pass
 
     def _seen_files(self) -> List[str]:
         """Files of every PLANNED batch, in batch order. The offsets log is the write-ahead record
@@ -362,12 +410,131 @@ class StreamingQuery:
         else:
             raise ValueError(f"unsupported streaming source format {self._plan.fmt}")
         df._batch_time_us = int(ts_ms) * 1000
-        for method, args, kwargs in self._plan.ops:
+        self._wm_source = None
+        for i, (method, args, kwargs) in enumerate(self._plan.ops):
             if method == "withWatermark":
+                self._wm_source = df
                 continue
-            df = getattr(df, method)(*args, **kwargs)
+            if method == "_stream_aggregate":
+                if self._wm_source is None:
+                    self._wm_source = df
+                df = self._stateful_aggregate(i, df, *args)
+            elif method == "_stream_dedup":
+                df = self._stateful_dedup(i, df, *args)
+            else:
+                df = getattr(df, method)(*args, **kwargs)
             df._batch_time_us = int(ts_ms) * 1000
         return df
+
+    # ------------------------------------------------------------------ stateful operators
+    def _late_mask(self, df):
+        """Rows at or after the batch's watermark (late rows are dropped by stateful operators)."""
+        import torch
+        wm = self._plan.watermark
+        if not wm or self._batch_wm <= 0 or wm[0] not in df.columns:
+            return None
+        cd = df._column_data(wm[0])
+        if cd.is_host:
+            return None
+        return cd.values.to(torch.int64) >= self._batch_wm * 1000
+
+    def _expired(self, key: tuple, key_exprs) -> bool:
+        """A group whose event time is behind the watermark: its time-window ends at or before it, or
+        its key is the watermark column itself and is older."""
+        from .column import ColRef, ts_to_micros
+        wm = self._plan.watermark
+        if not wm:
+            return False
+        lim = self._batch_wm * 1000
+        for v, e in zip(key, key_exprs):
+            end = getattr(v, "end", None) if hasattr(v, "__fields__") else None
+            if end is not None:
+                return ts_to_micros(end) <= lim
+            if isinstance(e, ColRef) and e.col == wm[0] and v is not None:
+                return ts_to_micros(v) < lim
+        return False
+
+    def _stateful_aggregate(self, idx: int, df, keys, exprs):
+        """Streaming groupBy().agg(): this batch's partials are merged into the per-group state; the
+        output is every group (complete), the groups this batch touched (update), or the groups whose
+        event-time window the watermark has passed, which then leave the state (append)."""
+        from .builder import rows_round_robin
+        from .group import (combine_partials, final_row, fix_long_columns, gather_partials, local_partials,
+                            result_schema)
+        keep = self._late_mask(df)
+        if keep is not None:
+            df = df._mask_rows(keep)
+        specs, key_types, local = local_partials(df, keys, exprs)
+        merged, morder = gather_partials(self._session._comm, local, len(specs))
+        st = self._state.setdefault(idx, {})
+        touched = []
+        for key in morder:
+            cur = st.get(key)
+            new = []
+            for j, sp in enumerate(specs):
+                if sp[0] == "key":
+                    new.append(None)
+                elif getattr(sp[2], "custom", False):
+                    new.append((cur[j] if cur else []) + merged[key][j])
+                else:
+                    prev = [cur[j]] if cur is not None and cur[j] is not None else []
+                    new.append(combine_partials(prev + merged[key][j], sp[2].fn))
+            st[key] = new
+            touched.append(key)
+        mode = self._writer._mode
+        if mode == "complete":
+            out = list(st)
+        elif mode == "update":
+            out = touched
+        else:
+            out = [k for k in st if self._expired(k, keys)]
+
+        def parts_of(key):
+            return [[] if sp[0] == "key" else (st[key][j] if getattr(sp[2], "custom", False)
+                                              else [st[key][j]] if st[key][j] is not None else [])
+                    for j, sp in enumerate(specs)]
+        rows = [final_row(k, parts_of(k), specs) for k in out]
+        if mode != "complete":  # evict groups the watermark has passed
+            for k in [k for k in st if self._expired(k, keys)]:
+                del st[k]
+        schema = result_schema(specs, key_types)
+        fix_long_columns(schema, rows)
+        return rows_round_robin(self._session, schema, rows)
+
+    def _stateful_dedup(self, idx: int, df, subset):
+        """Streaming dropDuplicates: a row passes if its key was never seen in an earlier batch and it
+        is the key's first row in this batch (rank order, then row order). With a watermark on a key
+        column, keys older than the watermark leave the state and late rows are dropped."""
+        import torch
+        from .dataframe import column_to_python
+        from .group import _hashable
+        keep_late = self._late_mask(df)
+        if keep_late is not None:
+            df = df._mask_rows(keep_late)
+        cols = list(subset) if subset else df.columns
+        vals = [column_to_python(df._column_data(c)) for c in cols]
+        keys = [tuple(_hashable(v[i]) for v in vals) for i in range(df._nrows)]
+        seen = self._state.setdefault(idx, {})
+        comm = self._session._comm
+        allk = comm.allgather_object(keys)
+        mask_all, newseen = [], {}
+        for r, ks in enumerate(allk):
+            m = []
+            for k in ks:
+                ok = k not in seen and k not in newseen
+                if ok:
+                    newseen[k] = True
+                m.append(ok)
+            mask_all.append(m)
+        seen.update(newseen)
+        wm = self._plan.watermark
+        if wm and wm[0] in cols and self._batch_wm > 0:
+            from .column import ts_to_micros
+            j = cols.index(wm[0])
+            for k in [k for k in seen if k[j] is not None and ts_to_micros(k[j]) < self._batch_wm * 1000]:
+                del seen[k]
+        mask = torch.as_tensor(mask_all[comm.rank], dtype=torch.bool, device=df._device)
+        return df._mask_rows(mask) if df._nrows else df
 
     def _advance_watermark(self, df) -> None:
         wm = self._plan.watermark
@@ -393,17 +560,21 @@ class StreamingQuery:
 
     def _run_batch_impl(self, plan) -> dict:
         bid, files, ts_ms, wm_ms, replay = plan
+        if replay:
+            self._state = self._load_state()
         maybe_fail("stream.after_offsets", bid)  # crash point: batch planned (offsets logged), nothing written
         t0 = time.time()
         self._watermark_ms = max(self._watermark_ms, wm_ms)
+        self._batch_wm = wm_ms
         df = self._read_batch(files, ts_ms)
-        nrows = df.count()
+        nrows = (self._wm_source if self._wm_source is not None else df).count()
         w = self._writer
+        complete = w._mode == "complete"
         if self._table is not None:
             from ..io import table as tbl
             root = self._session.catalog._table_path(self._table)
             if tbl.committed_txn(root, self.id) < bid:
-                tbl.write_frame(df, root, "append", operation="STREAMING UPDATE",
+                tbl.write_frame(df, root, "overwrite" if complete else "append", operation="STREAMING UPDATE",
                                 txn={"appId": self.id, "version": bid})
         elif self._path is not None or (w._format not in (None, "console", "memory", "delta", "noop")):
             if self._path is None:
@@ -422,13 +593,14 @@ class StreamingQuery:
             df.show()
         elif w._format == "memory":
             name = self.name or "memory_sink"
-            prev = self._session.catalog._views.get(name)
+            prev = None if complete else self._session.catalog._views.get(name)
             self._session.catalog._register_view(name, df if prev is None else prev.union(df), True)
         if w._foreach_batch is not None:
             w._foreach_batch(df, bid)
-        self._advance_watermark(df)
+        self._advance_watermark(self._wm_source if self._wm_source is not None else df)
         comm = self._session._comm
         comm.barrier()
+        self._save_state(bid)
         maybe_fail("stream.before_commit", bid)  # crash point: sink done, commit not yet logged
         if comm.is_root:
             self._write_json("commits", bid, {"nextBatchWatermarkMs": self._watermark_ms})
