@@ -122,6 +122,23 @@ def _workload(out_path, rank, master="local[1]"):
     aft = AFTSurvivalRegression(labelCol="t", censorCol="cens", maxIter=30).fit(surv)
     res["aft"] = aft.coefficients.toArray().tolist() + [aft.intercept, aft.scale]
     res["iso"] = IsotonicRegression(labelCol="y", featureIndex=3).fit(f).predictions.toArray().tolist()[:50]
+    # stateful streaming: a complete-mode aggregation over CSV uploads planned by rank 0
+    sdir = os.path.join(os.path.dirname(out_path), f"stream_w{spark.world_size}")
+    if rank == 0:
+        os.makedirs(sdir, exist_ok=True)
+        for i in range(3):
+            part = pdf.iloc[i * 200:(i + 1) * 200]
+            pd.DataFrame({"hospital_id": part["g"], "event_time": "2025-04-01 10:00:00", "v": part["y"]}).to_csv(
+                os.path.join(sdir, f"up_{i}.csv"), index=False)
+    spark._comm.barrier()
+    got = []
+    q = (spark.readStream.option("header", True).schema("hospital_id STRING, event_time TIMESTAMP, v DOUBLE")
+         .csv(sdir).groupBy("hospital_id").agg(F.count("*").alias("n"), F.sum("v").alias("s"))
+         .writeStream.outputMode("complete")
+         .foreachBatch(lambda d, b: got.append(sorted([r.hospital_id, r.n, r.s] for r in d.collect())))
+         .option("checkpointLocation", sdir + "_ck").trigger(availableNow=True).start())
+    q.awaitTermination()
+    res["stream_agg"] = got[-1]
     if rank == 0:
         with open(out_path, "w") as fh:
             json.dump(res, fh)
@@ -191,6 +208,9 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["svc"], r1["svc"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(rw["aft"], r1["aft"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(rw["gmm"], r1["gmm"], rtol=1e-6)
+    assert [x[:2] for x in rw["stream_agg"]] == [x[:2] for x in r1["stream_agg"]]
+    np.testing.assert_allclose([x[2] for x in rw["stream_agg"]], [x[2] for x in r1["stream_agg"]], rtol=1e-12)
+    assert sum(x[1] for x in r1["stream_agg"]) == 600
 
 
 @pytest.mark.parametrize("world", [2, 3])
