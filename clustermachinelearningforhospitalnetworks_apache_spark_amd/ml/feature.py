@@ -22,23 +22,13 @@ from .base import Estimator, Model, Transformer
 from .linalg import DenseVector
 from .param import NO_DEFAULT
 from . import util as U
+from .colutil import _auto_output, _replace_col  # noqa: F401 (re-exported)
 
 
 def features_dtype(session) -> torch.dtype:
     name = session.conf.get("cml.ml.features.dtype", "float64")
     return {"float64": torch.float64, "double": torch.float64, "float32": torch.float32, "float": torch.float32,
             "bfloat16": torch.bfloat16, "bf16": torch.bfloat16}[str(name).lower()]
-
-
-def _replace_col(df, name: str, data: ColumnData):
-    fields = list(df.schema.fields)
-    cols = dict(df._cols)
-    if name in cols:
-        fields[df.schema.names.index(name)] = T.StructField(name, data.dtype, True)
-    else:
-        fields.append(T.StructField(name, data.dtype, True))
-    cols[name] = data
-    return df._new(T.StructType(fields), cols, df._nrows, df._row_ids)
 
 
 class VectorAssembler(Transformer):
@@ -658,3 +648,5 @@ from .feature_more import (ChiSqSelector, ChiSqSelectorModel, ElementwiseProduct
                            VectorIndexer, VectorIndexerModel, VectorSlicer)
 from .lsh import (BucketedRandomProjectionLSH, BucketedRandomProjectionLSHModel, MinHashLSH,  # noqa: E402,F401
                   MinHashLSHModel)
+from .feature_text import (CountVectorizer, CountVectorizerModel, HashingTF, IDF, IDFModel, NGram,  # noqa: E402,F401
+                           RegexTokenizer, StopWordsRemover, Tokenizer)

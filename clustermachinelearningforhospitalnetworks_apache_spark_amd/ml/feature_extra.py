@@ -27,14 +27,9 @@ from ..sql import types as T
 from ..sql.column import ColumnData
 from . import util as U
 from .base import Estimator, Model, Transformer
-from .feature import _replace_col
+from .colutil import _auto_output, _replace_col
 from .linalg import DenseMatrix, DenseVector
 from .param import NO_DEFAULT
-
-
-def _auto_output(obj) -> None:
-    if obj.getOutputCol() == "__auto__":
-        obj._defaultParamMap["outputCol"] = obj.uid + "__output"
 
 
 class Bucketizer(Transformer):

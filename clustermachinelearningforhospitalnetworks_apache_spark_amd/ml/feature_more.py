@@ -24,8 +24,7 @@ from ..sql import types as T
 from ..sql.column import ColumnData
 from . import util as U
 from .base import Estimator, Model, Transformer
-from .feature import _replace_col
-from .feature_extra import _auto_output
+from .colutil import _auto_output, _replace_col
 from .linalg import DenseVector
 from .param import NO_DEFAULT
 

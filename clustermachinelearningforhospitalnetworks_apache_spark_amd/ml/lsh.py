@@ -20,8 +20,7 @@ from ..sql.column import ColumnData
 from . import util as U
 from .util import JavaRandom
 from .base import Estimator, Model
-from .feature import _replace_col
-from .feature_extra import _auto_output
+from .colutil import _auto_output, _replace_col
 from .linalg import DenseVector, as_array
 from .param import NO_DEFAULT
 

@@ -97,6 +97,15 @@ _JVM = {
     "ChiSqSelector": "org.apache.spark.ml.feature.ChiSqSelector",
     "ChiSqSelectorModel": "org.apache.spark.ml.feature.ChiSqSelectorModel",
     "RFormula": "org.apache.spark.ml.feature.RFormula",
+    "CountVectorizer": "org.apache.spark.ml.feature.CountVectorizer",
+    "CountVectorizerModel": "org.apache.spark.ml.feature.CountVectorizerModel",
+    "HashingTF": "org.apache.spark.ml.feature.HashingTF",
+    "IDF": "org.apache.spark.ml.feature.IDF",
+    "IDFModel": "org.apache.spark.ml.feature.IDFModel",
+    "NGram": "org.apache.spark.ml.feature.NGram",
+    "RegexTokenizer": "org.apache.spark.ml.feature.RegexTokenizer",
+    "StopWordsRemover": "org.apache.spark.ml.feature.StopWordsRemover",
+    "Tokenizer": "org.apache.spark.ml.feature.Tokenizer",
     "MultilabelClassificationEvaluator": "org.apache.spark.ml.evaluation.MultilabelClassificationEvaluator",
     "RankingEvaluator": "org.apache.spark.ml.evaluation.RankingEvaluator",
     "BucketedRandomProjectionLSH": "org.apache.spark.ml.feature.BucketedRandomProjectionLSH",
@@ -168,6 +177,15 @@ _PY = {
     "ChiSqSelector": "feature",
     "ChiSqSelectorModel": "feature",
     "RFormula": "feature",
+    "CountVectorizer": "feature",
+    "CountVectorizerModel": "feature",
+    "HashingTF": "feature",
+    "IDF": "feature",
+    "IDFModel": "feature",
+    "NGram": "feature",
+    "RegexTokenizer": "feature",
+    "StopWordsRemover": "feature",
+    "Tokenizer": "feature",
     "MultilabelClassificationEvaluator": "evaluation", "RankingEvaluator": "evaluation",
     "BucketedRandomProjectionLSH": "feature",
     "BucketedRandomProjectionLSHModel": "feature",
