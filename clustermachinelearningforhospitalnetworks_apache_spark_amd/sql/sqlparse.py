@@ -150,6 +150,12 @@ class Parser:
             elif self.at_kw("IN"):
                 self.take()
                 self.expect_op("(")
+                if self.at_kw("SELECT"):
+                    q = _query(self)
+                    self.expect_op(")")
+                    e2 = InSubquery(e, q)
+                    e = Unary("not", e2) if neg else e2
+                    continue
                 items = [self.expr()]
                 while self.at_op(","):
                     self.take()
@@ -246,8 +252,10 @@ class Parser:
         if tok.kind == "ident":
             if self.at_op("("):
                 return self.call(tok.val)
-            name = tok.val.split(".")[-1] if "." in tok.val else tok.val
-            return ColRef(name)
+            if "." in tok.val:
+                q, c = tok.val.rsplit(".", 1)
+                return QualRef(q, c)
+            return ColRef(tok.val)
         raise SyntaxError(f"unexpected token {tok.val!r}")
 
     def case(self) -> Expr:
@@ -418,6 +426,68 @@ def _like(e: Expr, pattern: str) -> Expr:
     return Func(f"like({pattern})", [e], impl)
 
 
+class QualRef(ColRef):
+    """``alias.column``: resolves to the join output column ``alias.column`` when the join had to
+    qualify it (the name exists on both sides), else to ``column``."""
+
+    def __init__(self, qual: str, col: str):
+        super().__init__(col)
+        self.qual = qual
+
+    def eval(self, frame):
+        full = f"{self.qual}.{self.col}"
+        return frame._column_data(full if full in frame._cols else self.col)
+
+    def __str__(self):
+        return f"{self.qual}.{self.col}"
+
+
+class InSubquery(Expr):
+    """``e IN (SELECT ...)``: the subquery runs once per evaluation; its single column's distinct
+    values become the IN list."""
+
+    def __init__(self, child: Expr, query):
+        self.child, self.query = child, query
+
+    def refs(self):
+        return self.child.refs()
+
+    def __str__(self):
+        return f"({self.child} IN (subquery))"
+
+    def eval(self, frame):
+        from .dataframe import column_to_python
+        sub = _run_query(frame._session, self.query)
+        if len(sub.columns) != 1:
+            raise ValueError("IN subquery must return exactly one column")
+        vals = []
+        seen = set()
+        for part in frame._comm.allgather_object(column_to_python(sub._column_data(sub.columns[0]))):
+            for v in part:
+                if v not in seen:
+                    seen.add(v)
+                    vals.append(v)
+        acc = Lit(False)
+        for v in vals:
+            acc = BinOp("or", acc, BinOp("==", self.child, Lit(v)))
+        return acc.eval(frame)
+
+
+@dataclass
+class Source:
+    name: Optional[str] = None
+    sub: Optional[object] = None  # a query
+    alias: Optional[str] = None
+
+
+@dataclass
+class JoinClause:
+    how: str
+    right: Source
+    on: Optional[Expr] = None
+    using: Optional[List[str]] = None
+
+
 @dataclass
 class Select:
     items: List[Tuple[Expr, Optional[str]]]
@@ -429,17 +499,108 @@ class Select:
     limit: Optional[int] = None
     distinct: bool = False
     subquery: Optional["Select"] = None
+    source: Optional[Source] = None
+    joins: List[JoinClause] = field(default_factory=list)
 
 
-def parse_select(sql: str) -> Select:
+@dataclass
+class SetOp:
+    op: str          # union | union all | intersect | except
+    left: object
+    right: object
+    order_by: List[SortOrder] = field(default_factory=list)
+    limit: Optional[int] = None
+
+
+def parse_select(sql: str):
     p = Parser(tokenize(sql))
-    sel = _select(p)
+    q = _query(p)
     if p.peek() is not None:
         raise SyntaxError(f"unexpected trailing SQL: {p.peek().val!r}")
-    return sel
+    return q
+
+
+def _query(p: Parser):
+    """select (UNION [ALL] | INTERSECT | EXCEPT | MINUS) select ... ; a trailing ORDER BY / LIMIT of
+    the last select applies to the whole set operation."""
+    left = _select(p)
+    while p.at_word("UNION", "INTERSECT", "EXCEPT", "MINUS"):
+        op = p.take().val.upper()
+        if op == "UNION" and p.at_word("ALL"):
+            p.take()
+            op = "UNION ALL"
+        elif p.at_kw("DISTINCT"):
+            p.take()
+        right = _select(p)
+        left = SetOp(op.lower().replace("minus", "except"), left, right)
+        if isinstance(right, Select) and (right.order_by or right.limit is not None):
+            left.order_by, left.limit = right.order_by, right.limit
+            right.order_by, right.limit = [], None
+    return left
+
+
+def _source(p: Parser) -> Source:
+    if p.at_op("("):
+        p.take()
+        sub = _query(p)
+        p.expect_op(")")
+        src = Source(sub=sub)
+    else:
+        src = Source(name=p.take().val)
+    if p.at_kw("AS"):
+        p.take()
+        src.alias = p.take().val
+    elif p.peek() is not None and p.peek().kind == "ident" and not p.at_word(
+            "JOIN", "INNER", "LEFT", "RIGHT", "FULL", "CROSS", "SEMI", "ANTI", "ON", "USING", "UNION", "INTERSECT",
+            "EXCEPT", "MINUS", "OUTER", "NATURAL"):
+        src.alias = p.take().val
+    return src
+
+
+_JOIN_WORDS = ("JOIN", "INNER", "LEFT", "RIGHT", "FULL", "CROSS", "SEMI", "ANTI")
+
+
+def _join(p: Parser) -> Optional[JoinClause]:
+    if not p.at_word(*_JOIN_WORDS) and not p.at_op(","):
+        return None
+    if p.at_op(","):  # FROM a, b  ==  CROSS JOIN
+        p.take()
+        return JoinClause("cross", _source(p))
+    words = []
+    while not p.at_word("JOIN"):
+        words.append(p.take().val.upper())
+    p.take()
+    words = [w for w in words if w != "OUTER"]
+    how = {(): "inner", ("INNER",): "inner", ("LEFT",): "left", ("RIGHT",): "right", ("FULL",): "full",
+           ("CROSS",): "cross", ("LEFT", "SEMI"): "leftsemi", ("SEMI",): "leftsemi", ("LEFT", "ANTI"): "leftanti",
+           ("ANTI",): "leftanti"}.get(tuple(words))
+    if how is None:
+        raise SyntaxError(f"unsupported join type {' '.join(words)}")
+    right = _source(p)
+    jc = JoinClause(how, right)
+    if p.at_word("ON"):
+        p.take()
+        jc.on = p.expr()
+    elif p.at_word("USING"):
+        p.take()
+        p.expect_op("(")
+        cols = [p.take().val]
+        while p.at_op(","):
+            p.take()
+            cols.append(p.take().val)
+        p.expect_op(")")
+        jc.using = cols
+    elif how != "cross":
+        raise SyntaxError("JOIN needs ON or USING")
+    return jc
 
 
 def _select(p: Parser) -> Select:
+    if p.at_op("("):
+        p.take()
+        q = _query(p)
+        p.expect_op(")")
+        return q
     p.expect_kw("SELECT")
     distinct = False
     if p.at_kw("DISTINCT"):
@@ -449,21 +610,16 @@ def _select(p: Parser) -> Select:
     while p.at_op(","):
         p.take()
         items.append(_select_item(p))
-    table, sub = None, None
+    sel = Select(items, None, distinct=distinct)
     if p.at_kw("FROM"):
         p.take()
-        if p.at_op("("):
-            p.take()
-            sub = _select(p)
-            p.expect_op(")")
-        else:
-            table = p.take().val
-        if p.at_kw("AS"):
-            p.take()
-            p.take()
-        elif p.peek() is not None and p.peek().kind == "ident":
-            p.take()  # table alias
-    sel = Select(items, table, distinct=distinct, subquery=sub)
+        sel.source = _source(p)
+        sel.table = sel.source.name
+        while True:
+            jc = _join(p)
+            if jc is None:
+                break
+            sel.joins.append(jc)
     if p.at_kw("WHERE"):
         p.take()
         sel.where = p.expr()
@@ -499,13 +655,29 @@ def _select(p: Parser) -> Select:
     return sel
 
 
+class _QualStar(Expr):
+    def __init__(self, qual: str):
+        self.qual = qual
+
+    def refs(self):
+        return []
+
+    def __str__(self):
+        return f"{self.qual}.*"
+
+
 def _select_item(p: Parser):
+    tok, nxt = p.peek(), p.peek(1)
+    if tok is not None and tok.kind == "ident" and nxt is not None and nxt.kind == "op" and nxt.val == "." \
+            and p.peek(2) is not None and p.peek(2).val == "*":
+        p.take(), p.take(), p.take()
+        return _QualStar(tok.val), None
     e = p.expr()
     alias = None
     if p.at_kw("AS"):
         p.take()
         alias = p.take().val
-    elif p.peek() is not None and p.peek().kind == "ident":
+    elif p.peek() is not None and p.peek().kind == "ident" and not p.at_word("FROM"):
         alias = p.take().val
     return e, alias
 
@@ -524,16 +696,356 @@ def parse_select_item(sql: str) -> Expr:
     return Alias(e, alias) if alias else e
 
 
+# ---------------------------------------------------------------------------------------- statements
+
 def execute(session, sql: str):
-    """Run a SELECT against the session catalog; returns a DataFrame."""
-    sel = parse_select(sql)
-    return _run(session, sel)
+    """Run one SQL statement against the session catalog; returns a DataFrame.
+
+    Queries: SELECT with joins (INNER / LEFT / RIGHT / FULL [OUTER], CROSS, LEFT SEMI / ANTI, ON or
+    USING), set operations (UNION [ALL], INTERSECT, EXCEPT), WITH common table expressions, IN
+    subqueries, GROUP BY with expressions. Statements: CREATE [OR REPLACE] [TEMP] VIEW .. AS,
+    CREATE TABLE .. AS, INSERT INTO / OVERWRITE, DROP TABLE / VIEW, SHOW TABLES, DESCRIBE."""
+    p = Parser(tokenize(sql))
+    if p.at_word("WITH"):
+        p.take()
+        ctes = []
+        while True:
+            name = p.take().val
+            p.expect_kw("AS")
+            p.expect_op("(")
+            ctes.append((name, _query(p)))
+            p.expect_op(")")
+            if not p.at_op(","):
+                break
+            p.take()
+        q = _query(p)
+        _expect_end(p)
+        cat = session.catalog
+        saved = {n: cat._views.get(n) for n, _ in ctes}
+        try:
+            for n, cq in ctes:
+                cat._register_view(n, _run_query(session, cq), True)
+            return _run_query(session, q)
+        finally:
+            for n, v in saved.items():
+                if v is None:
+                    cat._views.pop(n, None)
+                else:
+                    cat._views[n] = v
+    if p.at_word("CREATE"):
+        return _create(session, p)
+    if p.at_word("INSERT"):
+        p.take()
+        mode = "append"
+        if p.at_word("OVERWRITE"):
+            p.take()
+            mode = "overwrite"
+        else:
+            p.expect_word("INTO")
+        if p.at_word("TABLE"):
+            p.take()
+        name = p.take().val
+        df = _run_query(session, _query(p))
+        _expect_end(p)
+        target = session.table(name)
+        df = df.toDF(*target.columns) if len(df.columns) == len(target.columns) else df
+        session.catalog._save_table(name, df, mode)
+        return session.createDataFrame([], T.StructType([]))
+    if p.at_word("DROP"):
+        p.take()
+        kind = p.take().val.upper()
+        if p.at_word("IF"):
+            p.take()
+            p.expect_word("EXISTS")
+        name = p.take().val
+        _expect_end(p)
+        if kind == "VIEW":
+            session.catalog.dropTempView(name)
+        else:
+            session.catalog.dropTable(name)
+        return session.createDataFrame([], T.StructType([]))
+    if p.at_word("SHOW"):
+        p.take()
+        p.take()  # TABLES | VIEWS
+        _expect_end(p)
+        rows = [(t.database or "", t.name, t.isTemporary) for t in session.catalog.listTables()]
+        return session.createDataFrame(rows, "namespace STRING, tableName STRING, isTemporary BOOLEAN")
+    if p.at_word("DESCRIBE", "DESC"):
+        p.take()
+        if p.at_word("TABLE"):
+            p.take()
+        name = p.take().val
+        _expect_end(p)
+        df = session.table(name)
+        rows = [(f.name, f.dataType.simpleString(), None) for f in df.schema.fields]
+        return session.createDataFrame(rows, "col_name STRING, data_type STRING, comment STRING")
+    q = _query(p)
+    _expect_end(p)
+    return _run_query(session, q)
+
+
+def _expect_end(p: Parser) -> None:
+    if p.peek() is not None:
+        raise SyntaxError(f"unexpected trailing SQL: {p.peek().val!r}")
+
+
+def _create(session, p: Parser):
+    p.take()  # CREATE
+    replace = False
+    if p.at_kw("OR"):
+        p.take()
+        p.expect_word("REPLACE")
+        replace = True
+    if p.at_word("GLOBAL"):
+        p.take()
+    if p.at_word("TEMP", "TEMPORARY"):
+        p.take()
+    kind = p.take().val.upper()
+    if_not_exists = False
+    if p.at_word("IF"):
+        p.take()
+        p.expect_kw("NOT")
+        p.expect_word("EXISTS")
+        if_not_exists = True
+    name = p.take().val
+    if p.at_word("USING"):
+        p.take()
+        p.take()
+    p.expect_kw("AS")
+    q = _query(p)
+    _expect_end(p)
+    df = _run_query(session, q)
+    if kind == "VIEW":
+        session.catalog._register_view(name, df, replace)
+    elif kind == "TABLE":
+        if session.catalog.tableExists(name):
+            if if_not_exists:
+                return session.createDataFrame([], T.StructType([]))
+            raise ValueError(f"table {name} already exists")
+        session.catalog._save_table(name, df, "overwrite")
+    else:
+        raise SyntaxError(f"CREATE {kind} is not supported")
+    return session.createDataFrame([], T.StructType([]))
+
+
+def _run_query(session, q):
+    if isinstance(q, SetOp):
+        left, right = _run_query(session, q.left), _run_query(session, q.right)
+        if q.op == "union all":
+            df = left.union(right)
+        elif q.op == "union":
+            df = left.union(right).distinct()
+        elif q.op == "intersect":
+            df = left.intersect(right)
+        else:
+            df = left.subtract(right)
+        if q.order_by:
+            df = df.orderBy(*q.order_by)
+        if q.limit is not None:
+            df = df.limit(q.limit)
+        return df
+    return _run(session, q)
+
+
+def _source_frame(session, src: Source):
+    df = _run_query(session, src.sub) if src.sub is not None else session.table(src.name)
+    return df, (src.alias or src.name)
+
+
+def _split_on(cond: Expr, lcols, rcols):
+    """ON condition -> ([(left col, right col)] equi keys, residual conjuncts)."""
+    conj = []
+
+    def flat(e):
+        if isinstance(e, BinOp) and e.op == "and":
+            flat(e.left)
+            flat(e.right)
+        else:
+            conj.append(e)
+    flat(cond)
+    keys, rest = [], []
+    for c in conj:
+        if isinstance(c, BinOp) and c.op == "==" and isinstance(c.left, ColRef) and isinstance(c.right, ColRef):
+            a, b = c.left, c.right
+            side = lambda r, cols: (getattr(r, "qual", None), r.col, r.col in cols)  # noqa: E731
+            la, lb = side(a, lcols), side(b, rcols)
+            if la[2] and lb[2]:
+                keys.append((a, b))
+                continue
+            la, lb = side(b, lcols), side(a, rcols)
+            if la[2] and lb[2]:
+                keys.append((b, a))
+                continue
+        rest.append(c)
+    return keys, rest
+
+
+def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[str], using: bool):
+    """Host hash join keeping both sides' columns; names present on both sides become
+    ``alias.column`` (USING keys appear once). Right side gathered to every rank (reference-scale
+    tables, as ``DataFrame.join``)."""
+    from .builder import frame_from_pycolumns
+    from .dataframe import column_to_python
+    from .group import _hashable
+    rnames, rrows, _ = right._gather_host()
+    lnames = left.columns
+    lcols = left._local_rows_host()
+    ridx = [rnames.index(k) for k in rkeys]
+    index = {}
+    for j, r in enumerate(rrows):
+        key = tuple(_hashable(r[i]) for i in ridx)
+        if any(v is None for v in key):
+            continue
+        index.setdefault(key, []).append(j)
+    r_out = [n for n in rnames if not (using and n in rkeys)]
+    both = set(lnames) & set(r_out)
+    lq, rq = lq or "l", rq or "r"
+    out_l = [f"{lq}.{n}" if n in both else n for n in lnames]
+    out_r = [f"{rq}.{n}" if n in both else n for n in r_out]
+    r_pos = [rnames.index(n) for n in r_out]
+    semi = how in ("leftsemi", "leftanti")
+    rows, matched = [], set()
+    for i in range(left._nrows):
+        lrow = [lcols[n][i] for n in lnames]
+        key = tuple(_hashable(lcols[k][i]) for k in lkeys)
+        hits = list(range(len(rrows))) if how == "cross" else ([] if any(v is None for v in key)
+                                                               else index.get(key, []))
+        if semi:
+            if bool(hits) == (how == "leftsemi"):
+                rows.append(lrow)
+            continue
+        if hits:
+            for j in hits:
+                matched.add(j)
+                rows.append(lrow + [rrows[j][t] for t in r_pos])
+        elif how in ("left", "full"):
+            rows.append(lrow + [None] * len(r_pos))
+    if how in ("right", "full"):
+        allm = set()
+        for part in left._comm.allgather_object(sorted(matched)):
+            allm |= set(part)
+        if left._comm.rank == 0:
+            for j, r in enumerate(rrows):
+                if j not in allm:
+                    lrow = [None] * len(lnames)
+                    if using:
+                        for k_l, k_r in zip(lkeys, rkeys):
+                            lrow[lnames.index(k_l)] = r[rnames.index(k_r)]
+                    rows.append(lrow + [r[t] for t in r_pos])
+    names = out_l if semi else out_l + out_r
+    fields = [T.StructField(n, left.schema[o].dataType, True) for n, o in zip(out_l, lnames)]
+    if not semi:
+        fields += [T.StructField(n, right.schema[o].dataType, True) for n, o in zip(out_r, r_out)]
+    schema = T.StructType(fields)
+    pycols = {f.name: [r[j] for r in rows] for j, f in enumerate(schema.fields)}
+    counts = left._comm.allgather_object(len(rows))
+    off = sum(counts[: left._comm.rank])
+    df = frame_from_pycolumns(left._session, schema, pycols, list(range(off, off + len(rows))))
+    src = dict(getattr(left, "_sql_sources", {}) or {lq: out_l})
+    if not semi:
+        src[rq] = out_r
+    df._sql_sources = src
+    return df
+
+
+def _apply_join(session, df, lq, jc: JoinClause):
+    right, rq = _source_frame(session, jc.right)
+    if jc.how == "cross":
+        out = _join_frames(df, lq, right, rq, "cross", [], [], False)
+        return out if jc.on is None else out.filter(Column(jc.on))
+    if jc.using is not None:
+        return _join_frames(df, lq, right, rq, jc.how, jc.using, jc.using, True)
+    keys, rest = _split_on(jc.on, set(df.columns), set(right.columns))
+    if not keys:
+        if jc.how != "inner":
+            raise NotImplementedError("non-equi outer joins are not supported")
+        return _join_frames(df, lq, right, rq, "cross", [], [], False).filter(Column(jc.on))
+    if rest and jc.how != "inner":
+        raise NotImplementedError("outer joins with non-equality ON conditions are not supported")
+    out = _join_frames(df, lq, right, rq, jc.how, [a.col for a, _ in keys], [b.col for _, b in keys], False)
+    for c in rest:
+        out = out.filter(Column(c))
+    return out
+
+
+def _transform(e: Expr, fn) -> Expr:
+    """Bottom-up rewrite of an expression tree (fn returns a replacement or None)."""
+    from .column import Func
+    r = fn(e)
+    if r is not None:
+        return r
+    if isinstance(e, BinOp):
+        return BinOp(e.op, _transform(e.left, fn), _transform(e.right, fn))
+    if isinstance(e, Unary):
+        return Unary(e.op, _transform(e.child, fn))
+    if isinstance(e, Alias):
+        return Alias(_transform(e.child, fn), e.alias)
+    if isinstance(e, Cast):
+        return Cast(_transform(e.child, fn), e.to)
+    if isinstance(e, When):
+        return When([(_transform(c, fn), _transform(v, fn)) for c, v in e.branches],
+                    _transform(e.other, fn) if e.other is not None else None)
+    if isinstance(e, Func):
+        return Func(e.fname, [_transform(a, fn) for a in e.args], e.impl)
+    return e
+
+
+def _grouped(df, sel: Select, exprs: List[Expr]):
+    """GROUP BY with arbitrary expressions: aggregates and non-column keys are computed first under
+    internal names, then the select items (expressions over keys and aggregates), HAVING and ORDER
+    BY are evaluated on that frame."""
+    from .group import aggregate
+    keys, key_names = [], []
+    for j, k in enumerate(sel.group_by):
+        if isinstance(k, ColRef) and not isinstance(k, QualRef):
+            keys.append(k)
+            key_names.append(k.col)
+        else:
+            nm = f"__key{j}"
+            keys.append(Alias(k, nm))
+            key_names.append(nm)
+    key_str = {str(k.child if isinstance(k, Alias) else k): n for k, n in zip(keys, key_names)}
+    aggs: List[Expr] = []
+
+    def grab(e):
+        if isinstance(e, AggExpr):
+            s_ = str(e)
+            for i, a in enumerate(aggs):
+                if str(a) == s_:
+                    return ColRef(f"__agg{i}")
+            aggs.append(e)
+            return ColRef(f"__agg{len(aggs) - 1}")
+        if not isinstance(e, (Lit,)) and str(e) in key_str and not isinstance(e, Alias):
+            return ColRef(key_str[str(e)])
+        if isinstance(e, QualRef) and e.col in key_str:
+            return ColRef(key_str[e.col])
+        return None
+    items = [_transform(x, grab) for x in exprs]
+    having = _transform(sel.having, grab) if sel.having is not None else None
+    orders = [SortOrder(_transform(o.expr, grab), o.ascending, o.nulls_first) for o in sel.order_by]
+    # ORDER BY an output alias
+    out_names = {x.name(): x for x in items}
+    orders = [SortOrder(ColRef(o.expr.col), o.ascending, o.nulls_first)
+              if isinstance(o.expr, ColRef) and o.expr.col in out_names else o for o in orders]
+    agg_df = aggregate(df, keys, [ColRef(n) for n in key_names] + [Alias(a, f"__agg{i}") for i, a in enumerate(aggs)])
+    if having is not None:
+        agg_df = agg_df.filter(Column(having))
+    if orders:
+        tmp = agg_df.select(*[Column(c) for c in agg_df.columns], *[Column(x) for x in items
+                                                                    if x.name() not in agg_df.columns])
+        tmp = tmp.orderBy(*orders)
+        return tmp.select(*[Column(ColRef(x.name())) for x in items]), True
+    return agg_df.select(*[Column(x) for x in items]), False
 
 
 def _run(session, sel: Select):
-    from .dataframe import DataFrame
-    if sel.subquery is not None:
-        df = _run(session, sel.subquery)
+    if sel.source is not None:
+        df, lq = _source_frame(session, sel.source)
+        for jc in sel.joins:
+            df = _apply_join(session, df, lq, jc)
+            lq = None
+    elif sel.subquery is not None:
+        df = _run_query(session, sel.subquery)
     elif sel.table is not None:
         df = session.table(sel.table)
     else:
@@ -541,18 +1053,23 @@ def _run(session, sel: Select):
     if sel.where is not None:
         df = df.filter(Column(sel.where))
     exprs: List[Expr] = []
+    sources = getattr(df, "_sql_sources", None) or {}
     for e, alias in sel.items:
-        if isinstance(e, ColRef) and e.col == "*":
+        if isinstance(e, ColRef) and e.col == "*" and not isinstance(e, QualRef):
             exprs += [ColRef(n) for n in df.columns]
+        elif isinstance(e, _QualStar):
+            cols = sources.get(e.qual)
+            if cols is None:
+                if e.qual in (sel.table, getattr(sel.source, "alias", None)):
+                    cols = df.columns
+                else:
+                    raise ValueError(f"unknown table alias {e.qual!r}")
+            exprs += [Alias(ColRef(c), c.split(".", 1)[1]) if c.startswith(e.qual + ".") else ColRef(c) for c in cols]
         else:
             exprs.append(Alias(e, alias) if alias else e)
     ordered = False
     if sel.group_by or any(x.is_aggregate() for x in exprs):
-        from .group import aggregate
-        out = aggregate(df, sel.group_by, exprs)
-        if sel.having is not None:
-            out = out.filter(Column(_rewrite_aggs(sel.having, exprs)))
-        df = out
+        df, ordered = _grouped(df, sel, exprs)
     else:
         out_names = {x.name() for x in exprs}
         if sel.order_by and not sel.distinct and any(

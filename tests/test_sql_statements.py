@@ -1,0 +1,103 @@
+"""SQL front end: joins, set operations, CTEs, IN subqueries, GROUP BY expressions and the DDL/DML
+statements, checked against sqlite3 (Python's stdlib) running the same queries on the same rows."""
+import sqlite3
+
+import pytest
+
+from helpers import session
+
+
+@pytest.fixture()
+def spark(tmp_path):
+    s = session()
+    s.conf.set("spark.sql.warehouse.dir", str(tmp_path / "wh"))
+    return s
+
+
+ADM = [(1, "H0", 3.0, 10), (2, "H1", 5.5, 20), (3, "H0", 1.0, 10), (4, "H2", 8.0, 30), (5, "H3", 2.0, None)]
+HOS = [("H0", "north", 100), ("H1", "south", 80), ("H2", "north", 50), ("H9", "east", 10)]
+
+
+@pytest.fixture()
+def db(spark):
+    spark.createDataFrame(ADM, "id INT, hid STRING, los DOUBLE, ward INT").createOrReplaceTempView("adm")
+    spark.createDataFrame(HOS, "hid STRING, region STRING, beds INT").createOrReplaceTempView("hos")
+    con = sqlite3.connect(":memory:")
+    con.execute("CREATE TABLE adm (id INT, hid TEXT, los REAL, ward INT)")
+    con.execute("CREATE TABLE hos (hid TEXT, region TEXT, beds INT)")
+    con.executemany("INSERT INTO adm VALUES (?,?,?,?)", ADM)
+    con.executemany("INSERT INTO hos VALUES (?,?,?)", HOS)
+    return con
+
+
+def _norm(rows):
+    out = [tuple(None if v is None else (round(v, 9) if isinstance(v, float) else v) for v in r) for r in rows]
+    return sorted(out, key=lambda t: tuple((v is None, str(type(v)), v if v is not None else 0) for v in t))
+
+
+def _same(spark, con, q, sq=None):
+    got = _norm(tuple(r) for r in spark.sql(q).collect())
+    want = _norm(tuple(r) for r in con.execute(sq or q).fetchall())
+    assert got == want, q
+
+
+@pytest.mark.parametrize("q", [
+    "SELECT a.id, h.region FROM adm a JOIN hos h ON a.hid = h.hid",
+    "SELECT a.id, h.region, h.beds FROM adm a LEFT JOIN hos h ON a.hid = h.hid",
+    "SELECT a.id, h.hid FROM adm AS a INNER JOIN hos AS h ON h.hid = a.hid AND h.beds > 60",
+    "SELECT a.id, h.region FROM adm a, hos h WHERE a.hid = h.hid AND a.los > 2",
+    "SELECT h.region, COUNT(*) AS n, SUM(a.los) AS total FROM adm a JOIN hos h ON a.hid = h.hid GROUP BY h.region",
+    "SELECT hid, id FROM adm UNION SELECT hid, beds FROM hos",
+    "SELECT hid FROM adm UNION ALL SELECT hid FROM hos",
+    "SELECT hid FROM adm INTERSECT SELECT hid FROM hos",
+    "SELECT hid FROM hos EXCEPT SELECT hid FROM adm",
+    "SELECT id FROM adm WHERE hid IN (SELECT hid FROM hos WHERE region = 'north')",
+    "SELECT id FROM adm WHERE hid NOT IN (SELECT hid FROM hos WHERE region = 'north')",
+    "SELECT hid, COUNT(*) * 2 AS c2, MAX(los) - MIN(los) AS spread FROM adm GROUP BY hid",
+    "SELECT ward * 10 AS w10, COUNT(*) AS n FROM adm GROUP BY ward * 10",
+    "SELECT hid, AVG(los) AS m FROM adm GROUP BY hid HAVING COUNT(*) > 1",
+    "SELECT UPPER(hid) AS u, SUM(los) AS s FROM adm GROUP BY hid",
+])
+def test_queries_match_sqlite(spark, db, q):
+    _same(spark, db, q)
+
+
+def test_join_variants(spark, db):
+    # FULL / RIGHT joins and USING (sqlite in this image may predate RIGHT/FULL JOIN: checked directly)
+    full = _norm((r.id, r.region) for r in spark.sql(
+        "SELECT a.id, h.region FROM adm a FULL OUTER JOIN hos h ON a.hid = h.hid").collect())
+    assert full == _norm([(1, "north"), (2, "south"), (3, "north"), (4, "north"), (5, None), (None, "east")])
+    right = spark.sql("SELECT a.id, h.hid FROM adm a RIGHT JOIN hos h ON a.hid = h.hid").collect()
+    assert sorted((r.id is None, r.hid) for r in right) == sorted(
+        [(False, "H0"), (False, "H0"), (False, "H1"), (False, "H2"), (True, "H9")])
+    using = spark.sql("SELECT * FROM adm JOIN hos USING (hid)")
+    assert using.columns == ["id", "hid", "los", "ward", "region", "beds"] and using.count() == 4
+    semi = sorted(r.id for r in spark.sql("SELECT id FROM adm a LEFT SEMI JOIN hos h ON a.hid = h.hid").collect())
+    anti = sorted(r.id for r in spark.sql("SELECT id FROM adm a LEFT ANTI JOIN hos h ON a.hid = h.hid").collect())
+    assert semi == [1, 2, 3, 4] and anti == [5]
+    star = spark.sql("SELECT a.*, h.region FROM adm a JOIN hos h ON a.hid = h.hid")
+    assert star.columns == ["id", "hid", "los", "ward", "region"]
+    both = spark.sql("SELECT a.hid, h.hid FROM adm a JOIN hos h ON a.hid = h.hid").collect()
+    assert all(r[0] == r[1] for r in both)
+
+
+def test_cte_and_statements(spark, db):
+    q = ("WITH big AS (SELECT hid FROM hos WHERE beds >= 80), "
+         "l AS (SELECT * FROM adm WHERE los > 1.5) SELECT l.id FROM l JOIN big ON l.hid = big.hid")
+    assert sorted(r.id for r in spark.sql(q).collect()) == [1, 2]
+    assert "big" not in spark.catalog._views  # CTE views are scoped to the statement
+    spark.sql("CREATE OR REPLACE TEMP VIEW north AS SELECT * FROM hos WHERE region = 'north'")
+    assert spark.table("north").count() == 2
+    spark.sql("CREATE TABLE stays AS SELECT id, los FROM adm WHERE los > 2")
+    assert spark.table("stays").count() == 3
+    spark.sql("INSERT INTO stays SELECT id, los FROM adm WHERE los <= 2")
+    assert spark.table("stays").count() == 5
+    spark.sql("INSERT OVERWRITE TABLE stays SELECT id, los FROM adm WHERE id = 1")
+    assert [tuple(r) for r in spark.table("stays").collect()] == [(1, 3.0)]
+    names = {r.tableName for r in spark.sql("SHOW TABLES").collect()}
+    assert {"stays", "north", "adm"} <= names
+    desc = {r.col_name: r.data_type for r in spark.sql("DESCRIBE adm").collect()}
+    assert desc == {"id": "int", "hid": "string", "los": "double", "ward": "int"}
+    spark.sql("DROP TABLE IF EXISTS stays")
+    spark.sql("DROP VIEW north")
+    assert not spark.catalog.tableExists("stays") and not spark.catalog.tableExists("north")
