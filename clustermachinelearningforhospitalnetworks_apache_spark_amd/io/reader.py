@@ -83,6 +83,10 @@ class DataFrameReader:
             return self.parquet(path)
         if f == "json":
             return self.json(path)
+        if f == "orc":
+            return self.orc(path)
+        if f == "text":
+            return self.text(path)
         if f in ("delta", "table"):
             from . import table
             return table.read_table(self._session, strip_scheme(path), self._options.get("versionasof"))
@@ -99,9 +103,41 @@ class DataFrameReader:
         if inferSchema is not None:
             self.option("inferschema", inferSchema)
         files = expand_paths(path)
-        return read_csv_files(self._session, files, self._schema, self._bool("header"),
-                              sep=str(self._options.get("sep", self._options.get("delimiter", ","))),
-                              quote=str(self._options.get("quote", '"')), infer=self._bool("inferschema"))
+        sch = self._schema
+
+        def read(fs, ids=None):
+            return read_csv_files(self._session, fs, sch, self._bool("header"),
+                                  sep=str(self._options.get("sep", self._options.get("delimiter", ","))),
+                                  quote=str(self._options.get("quote", '"')), infer=self._bool("inferschema"),
+                                  file_ids=ids)
+        return self._maybe_partitioned(path, files, read)
+
+    def _maybe_partitioned(self, path, files, read):
+        """Hive partition discovery: ``col=value`` directories become typed columns."""
+        from .partition import read_partitioned
+        bases = [strip_scheme(p) for p in ([path] if isinstance(path, str) else list(path))]
+        bases = [b for b in bases if os.path.isdir(b)]
+        if bases and files:
+            out = read_partitioned(self._session, files, bases, read)
+            if out is not None:
+                return out
+        return read(files)
+
+    def orc(self, path):
+        import pyarrow as pa
+        import pyarrow.orc as orc
+        from .arrow import frame_from_arrow
+        from ..sql.builder import shard_range
+        files = expand_paths(path, exts=[".orc"])
+
+        def read(fs, ids=None):
+            tabs = [orc.read_table(f) for f in fs]
+            table = pa.concat_tables(tabs) if len(tabs) > 1 else (tabs[0] if tabs else pa.table({}))
+            comm = self._session._comm
+            a, b = shard_range(table.num_rows, comm.rank, comm.world_size)
+            base = (min(ids) << 40) if ids else 0
+            return frame_from_arrow(self._session, table.slice(a, b - a), list(range(base + a, base + b)))
+        return self._maybe_partitioned(path, files, read)
 
     def parquet(self, *paths):
         from .arrow import read_parquet_files
@@ -112,7 +148,9 @@ class DataFrameReader:
             if os.path.isdir(sp) and table.exists(sp):
                 return table.read_table(self._session, sp)
             files += expand_paths(p, exts=[".parquet"])
-        return read_parquet_files(self._session, files, self._schema)
+        sch = self._schema
+        return self._maybe_partitioned(list(paths), files,
+                                       lambda fs, ids=None: read_parquet_files(self._session, fs, sch, file_ids=ids))
 
     def json(self, path, schema=None):
         import pandas as pd

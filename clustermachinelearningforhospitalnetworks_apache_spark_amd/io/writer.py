@@ -1,4 +1,5 @@
-"""df.write — DataFrameWriter (parquet / csv / json / table / saveAsTable)."""
+"""df.write — DataFrameWriter (parquet / csv / json / orc / text / table / saveAsTable; Hive-style
+``partitionBy`` directories)."""
 from __future__ import annotations
 
 import os
@@ -75,9 +76,50 @@ class DataFrameWriter:
             return self.csv(path)
         if f == "json":
             return self.json(path)
+        if f == "orc":
+            return self.orc(path)
+        if f == "text":
+            return self.text(path)
         raise ValueError(f"unsupported format {f}")
 
-    def _part(self, path: str, ext: str) -> str:
+    def _write(self, path: str, write_part) -> None:
+        """Save mode, optional Hive partitioning (``partitionBy``), one part file per rank, _SUCCESS."""
+        path = strip_scheme(path)
+        if not self._prepare_dir(path):
+            return
+        if self._partition_by:
+            from .partition import write_partitioned
+
+            def one(sub, d):
+                os.makedirs(d, exist_ok=True)
+                if sub._nrows:
+                    write_part(sub, d)
+            write_partitioned(self._df, path, list(self._partition_by), one)
+        else:
+            write_part(self._df, path)
+        self._success(path)
+
+    def orc(self, path: str, mode: Optional[str] = None):
+        import pyarrow.orc as orc
+        from .arrow import frame_to_arrow
+        if mode:
+            self.mode(mode)
+        self._write(path, lambda df, d: orc.write_table(frame_to_arrow(df), self._part(d, "orc", df)))
+
+    def text(self, path: str, mode: Optional[str] = None):
+        from ..sql.dataframe import column_to_python
+        if mode:
+            self.mode(mode)
+        if len(self._df.columns) - len(self._partition_by or ()) != 1:
+            raise ValueError("text data source supports only a single column")
+
+        def w(df, d):
+            with open(self._part(d, "txt", df), "w") as fh:
+                for v in column_to_python(df._column_data(df.columns[0])):
+                    fh.write(("" if v is None else str(v)) + "\n")
+        self._write(path, w)
+
+    def _part(self, path: str, ext: str, df=None) -> str:
         comm = self._df._comm
         import uuid
         return os.path.join(path, f"part-{comm.rank:05d}-{uuid.uuid4().hex[:8]}.{ext}")
@@ -94,11 +136,10 @@ class DataFrameWriter:
         from .arrow import frame_to_arrow
         if mode:
             self.mode(mode)
-        path = strip_scheme(path)
-        if not self._prepare_dir(path):
-            return
-        pq.write_table(frame_to_arrow(self._df), self._part(path, "parquet"))
-        self._success(path)
+        comp = self._options.get("compression", "snappy")
+        self._write(path, lambda df, d: pq.write_table(frame_to_arrow(df), self._part(d, "parquet", df),
+                                                      compression=None if comp in ("none", "uncompressed")
+                                                      else comp))
 
     def csv(self, path: str, mode: Optional[str] = None, header=None, sep=None):
         if mode:
@@ -107,27 +148,20 @@ class DataFrameWriter:
             self.option("header", header)
         if sep is not None:
             self.option("sep", sep)
-        path = strip_scheme(path)
-        if not self._prepare_dir(path):
-            return
-        pdf = self._local_pandas()
         hdr = str(self._options.get("header", "false")).lower() == "true"
-        pdf.to_csv(self._part(path, "csv"), index=False, header=hdr, sep=self._options.get("sep", ","))
-        self._success(path)
+        self._write(path, lambda df, d: self._local_pandas(df).to_csv(self._part(d, "csv", df), index=False,
+                                                                     header=hdr, sep=self._options.get("sep", ",")))
 
     def json(self, path: str, mode: Optional[str] = None):
         if mode:
             self.mode(mode)
-        path = strip_scheme(path)
-        if not self._prepare_dir(path):
-            return
-        self._local_pandas().to_json(self._part(path, "json"), orient="records", lines=True, date_format="iso")
-        self._success(path)
+        self._write(path, lambda df, d: self._local_pandas(df).to_json(self._part(d, "json", df), orient="records",
+                                                                      lines=True, date_format="iso"))
 
-    def _local_pandas(self):
+    def _local_pandas(self, df=None):
         import pandas as pd
         from ..sql.dataframe import column_to_python
-        df = self._df
+        df = self._df if df is None else df
         data = {}
         for f in df.schema.fields:
             vals = column_to_python(df._cols[f.name])
