@@ -81,6 +81,62 @@ bool parse_timestamp(const char* p, const char* e, long long& us, bool date_only
   return true;
 }
 
+// Decimal integer without a copy: [+-]digits. False on anything else or overflow of 18+ digits.
+inline bool fast_int(const char* b, const char* e, long long& out) {
+  bool neg = false;
+  if (b < e && (*b == '-' || *b == '+')) { neg = *b == '-'; ++b; }
+  if (b == e || e - b > 18) return false;
+  long long v = 0;
+  for (; b < e; ++b) {
+    const unsigned d = (unsigned)(*b - '0');
+    if (d > 9) return false;
+    v = v * 10 + d;
+  }
+  out = neg ? -v : v;
+  return true;
+}
+
+// Clinger's fast path: [+-]digits[.digits][(e|E)[+-]digits] with at most 19 significant digits whose
+// value fits 2^53 and a decimal exponent in [-22, 22] is exactly one correctly rounded multiply or
+// divide by an exact power of ten. Anything else returns false (the caller uses strtod).
+inline bool fast_double(const char* b, const char* e, double& out) {
+  static const double kPow10[] = {1e0, 1e1, 1e2, 1e3, 1e4, 1e5, 1e6, 1e7, 1e8, 1e9, 1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+  bool neg = false;
+  if (b < e && (*b == '-' || *b == '+')) { neg = *b == '-'; ++b; }
+  unsigned long long m = 0;
+  int nd = 0, ex = 0;
+  bool any = false;
+  for (; b < e && (unsigned)(*b - '0') <= 9; ++b) {
+    any = true;
+    if (nd < 19) { m = m * 10 + (unsigned)(*b - '0'); if (m) ++nd; }
+    else ++ex;
+  }
+  if (b < e && *b == '.') {
+    ++b;
+    for (; b < e && (unsigned)(*b - '0') <= 9; ++b) {
+      any = true;
+      if (nd < 19) { m = m * 10 + (unsigned)(*b - '0'); if (m) ++nd; --ex; }
+    }
+  }
+  if (!any) return false;
+  if (b < e && (*b == 'e' || *b == 'E')) {
+    ++b;
+    bool eneg = false;
+    if (b < e && (*b == '-' || *b == '+')) { eneg = *b == '-'; ++b; }
+    if (b == e) return false;
+    int x = 0;
+    for (; b < e && (unsigned)(*b - '0') <= 9; ++b) { if (x < 10000) x = x * 10 + (*b - '0'); }
+    ex += eneg ? -x : x;
+  }
+  if (b != e) return false;
+  if (m > (1ULL << 53) || ex < -22 || ex > 22) return false;
+  double v = (double)m;
+  v = ex < 0 ? v / kPow10[-ex] : v * kPow10[ex];
+  out = neg ? -v : v;
+  return true;
+}
+
 inline void trim(const char*& b, const char*& e) {
   while (b < e && (*b == ' ' || *b == '\t')) ++b;
   while (e > b && (e[-1] == ' ' || e[-1] == '\t' || e[-1] == '\r')) --e;
@@ -96,7 +152,7 @@ struct Outputs {
 void store_cell(const Outputs& o, int c, long long r, const char* b, const char* e, bool quoted, bool has_esc) {
   unsigned char* v = o.valid[c];
   if (o.types[c] != kString) trim(b, e);
-  if (b == e && !quoted) {
+  if (b == e && (!quoted || o.types[c] != kString)) {  // "" is an empty string, but a null number
     v[r] = 0;
     if (o.types[c] == kString) {
       long long* t = static_cast<long long*>(o.data[c]) + 3 * r;
@@ -116,6 +172,17 @@ void store_cell(const Outputs& o, int c, long long r, const char* b, const char*
     }
     case kInt32:
     case kInt64: {
+      long long fi;
+      if (fast_int(b, e, fi)) {
+        if (o.types[c] == kInt32) {
+          if (fi < INT32_MIN || fi > INT32_MAX) { v[r] = 0; return; }
+          static_cast<int32_t*>(o.data[c])[r] = (int32_t)fi;
+        } else {
+          static_cast<int64_t*>(o.data[c])[r] = fi;
+        }
+        v[r] = 1;
+        return;
+      }
       const size_t n = std::min<size_t>(e - b, sizeof(buf) - 1);
       memcpy(buf, b, n);
       buf[n] = 0;
@@ -138,6 +205,13 @@ void store_cell(const Outputs& o, int c, long long r, const char* b, const char*
     }
     case kFloat64:
     case kFloat32: {
+      double fx;
+      if (fast_double(b, e, fx)) {
+        if (o.types[c] == kFloat64) static_cast<double*>(o.data[c])[r] = fx;
+        else static_cast<float*>(o.data[c])[r] = (float)fx;
+        v[r] = 1;
+        return;
+      }
       const size_t n = std::min<size_t>(e - b, sizeof(buf) - 1);
       memcpy(buf, b, n);
       buf[n] = 0;
@@ -236,6 +310,77 @@ CML_HOST_API long long cml_csv_index(const char* buf, long long len, char quote,
     if (n < cap && starts) starts[n] = s;
     ++n;
   }
+  return n;
+}
+
+// Multithreaded record index. Phase 1: each thread counts the quote characters of its byte range;
+// the prefix parity gives the quoting state at every range start. Phase 2: each thread lists the
+// record starts (first byte after an unquoted newline) of its range. The header / blank-line rules
+// of cml_csv_index then run over the merged list. `starts` needs room for (#newlines + 1) entries.
+CML_HOST_API long long cml_csv_index_mt(const char* buf, long long len, char quote, int skip_header,
+                                        long long* starts, long long cap, int nthreads) {
+  if (nthreads < 1) nthreads = 1;
+  if (len < (1LL << 20)) nthreads = 1;
+  const long long per = (len + nthreads - 1) / nthreads;
+  std::vector<long long> nq(nthreads, 0);
+  std::vector<std::vector<long long>> brk(nthreads);
+  auto count_q = [&](int t) {
+    const long long a = t * per, b = std::min(len, a + per);
+    long long q = 0;
+    for (long long i = a; i < b; ++i) q += buf[i] == quote;
+    nq[t] = q;
+  };
+  auto scan = [&](int t, bool inq) {
+    const long long a = t * per, b = std::min(len, a + per);
+    std::vector<long long>& out = brk[t];
+    out.reserve((size_t)((b - a) / 32 + 16));
+    if (nq[t] == 0 && !inq) {  // no quotes in this range: memchr over the newlines
+      const char* p = buf + a;
+      const char* end = buf + b;
+      while (p < end) {
+        const void* hit = std::memchr(p, '\n', (size_t)(end - p));
+        if (hit == nullptr) break;
+        const char* q = static_cast<const char*>(hit);
+        out.push_back(q - buf);
+        p = q + 1;
+      }
+      return;
+    }
+    for (long long i = a; i < b; ++i) {
+      const char ch = buf[i];
+      if (ch == quote) inq = !inq;
+      else if (ch == '\n' && !inq) out.push_back(i);
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(count_q, t);
+    count_q(0);
+    for (auto& x : th) x.join();
+  }
+  {
+    std::vector<std::thread> th;
+    long long q = 0;
+    std::vector<bool> state(nthreads);
+    for (int t = 0; t < nthreads; ++t) { state[t] = (q & 1) != 0; q += nq[t]; }
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(scan, t, (bool)state[t]);
+    scan(0, false);
+    for (auto& x : th) x.join();
+  }
+  // records: [prev newline + 1, newline) in order; trailing record without a newline
+  long long n = 0, s = 0;
+  int skipped = 0;
+  auto emit = [&](long long a, long long e) {
+    long long ee = e;
+    while (ee > a && (buf[ee - 1] == '\r' || buf[ee - 1] == ' ')) --ee;
+    if (ee == a) return;
+    if (skipped < skip_header) { ++skipped; return; }
+    if (n < cap && starts) starts[n] = a;
+    ++n;
+  };
+  for (int t = 0; t < nthreads; ++t)
+    for (long long nl : brk[t]) { emit(s, nl); s = nl + 1; }
+  if (s < len) emit(s, len);
   return n;
 }
 

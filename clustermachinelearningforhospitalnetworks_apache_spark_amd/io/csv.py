@@ -21,6 +21,7 @@ from ..sql.column import ColumnData
 
 _native.register_host_sigs({
     "cml_csv_index": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll]),
+    "cml_csv_index_mt": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll, c_int]),
     "cml_csv_gather_strings": (c_ll, [ctypes.c_char_p, c_vp, c_vp, c_ll, ctypes.c_char, c_vp, c_vp]),
     "cml_csv_parse": (c_int, [ctypes.c_char_p, c_ll, c_vp, c_ll, c_int, ctypes.c_char, ctypes.c_char, c_vp, c_vp,
                               c_vp, c_int]),
@@ -43,10 +44,7 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
                     rows: Optional[slice] = None, nthreads: Optional[int] = None):
     """Parse a CSV image into host arrays: {name: (values np.ndarray, valid np.ndarray)}, nrecords."""
     lib = _native.host()
-    n_all = lib.cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, None, 0)
-    starts = np.zeros(max(n_all, 1), dtype=np.int64)
-    lib.cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, starts.ctypes.data, n_all)
-    starts = starts[:n_all]
+    starts = record_starts(buf, header, quote, nthreads)
     if rows is not None:
         starts = starts[rows]
     n = int(starts.shape[0])
@@ -72,6 +70,18 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
         else:
             out[f.name] = (d[:n], valid)
     return out, n
+
+
+def record_starts(buf: bytes, header: bool, quote: str = '"', nthreads: Optional[int] = None) -> np.ndarray:
+    """Byte offsets of the records (one multithreaded native pass). A record takes at least two
+    bytes with its newline, so len/2 + 1 entries always suffice; the untouched tail of the
+    allocation is never paged in."""
+    cap = len(buf) // 2 + 2
+    starts = np.empty(cap, dtype=np.int64)
+    nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+    n = _native.host().cml_csv_index_mt(buf, len(buf), quote.encode(), 1 if header else 0, starts.ctypes.data, cap,
+                                         nthreads)
+    return starts[:n].copy()
 
 
 def _strings(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int, quote: str) -> np.ndarray:
@@ -163,7 +173,7 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
         if whole_files:
             sl = None
         else:
-            n_all = _native.host().cml_csv_index(buf, len(buf), quote.encode(), 1 if header else 0, None, 0)
+            n_all = int(record_starts(buf, header, quote).shape[0])
             a, b = shard_range(n_all, rank, W)
             sl = slice(a, b)
         parsed, n = parse_csv_bytes(buf, schema, header, sep, quote, rows=sl)
