@@ -242,3 +242,16 @@ def test_rformula(spark, tmp_path):
     pm = Pipeline(stages=[RFormula(formula="readmit ~ ward + age")]).fit(df)
     scored = pm.transform(df.select("ward", "age"))
     assert "label" not in scored.columns and _vec(scored, "features").shape == (5, 3)
+
+
+def test_ml_functions_vector_array(spark):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.functions import array_to_vector, vector_to_array
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+    X = np.array([[1.0, 2.0], [3.5, -1.0]])
+    df = _frame(spark, X)
+    arr = df.select(vector_to_array(F.col("f")).alias("a"))
+    assert [r.a for r in arr.collect()] == [[1.0, 2.0], [3.5, -1.0]]
+    back = arr.select(array_to_vector("a").alias("v"))
+    np.testing.assert_allclose(_vec(back, "v"), X)
+    f32 = df.select(vector_to_array("f", "float32").alias("a")).schema["a"].dataType.simpleString()
+    assert f32 == "array<float>"
