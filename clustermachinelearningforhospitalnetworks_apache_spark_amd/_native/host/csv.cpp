@@ -18,7 +18,10 @@
 #include <cstdint>
 #include <cstdlib>
 #include <cstring>
+#include <string>
+#include <string_view>
 #include <thread>
+#include <unordered_map>
 #include <vector>
 
 #define CML_HOST_API extern "C" __attribute__((visibility("default")))
@@ -446,3 +449,124 @@ CML_HOST_API long long cml_csv_gather_strings(const char* buf, const long long* 
   if (offsets != nullptr) offsets[n] = pos;
   return pos;
 }
+
+// ------------------------------------------------------------------------------------------ dictionary
+// Dictionary encoding of a parsed string column (strings are dictionary-encoded). Each thread
+// hashes a contiguous block of rows into a local dictionary (first-appearance order); the blocks'
+// dictionaries are merged in block order, so code c is the c-th distinct string in row order for any
+// thread count, and local codes are remapped in parallel. Nulls get code -1.
+namespace {
+struct DictResult {
+  std::vector<int> codes;
+  std::vector<std::vector<std::string>> owned;  // per-thread unescaped strings ("" -> "), never moved
+  std::vector<std::string_view> values;    // global dictionary in code order
+};
+}  // namespace
+
+CML_HOST_API void* cml_dict_build(const char* buf, const long long* trip, const unsigned char* valid, long long n,
+                                  char quote, int nthreads) {
+  auto* res = new DictResult();
+  res->codes.assign((size_t)n, -1);
+  if (nthreads < 1) nthreads = 1;
+  if (n < 65536) nthreads = 1;
+  const long long per = (n + nthreads - 1) / nthreads;
+  std::vector<std::vector<std::string_view>> ldict(nthreads);
+  res->owned.resize((size_t)nthreads);
+  auto& lowned = res->owned;
+  auto work = [&](int t) {
+    const long long r0 = t * per, r1 = std::min(n, r0 + per);
+    std::unordered_map<std::string_view, int> m;
+    m.reserve(1024);
+    std::vector<std::string>& own = lowned[t];
+    // reserve so that string_views into `own` stay valid while it grows
+    long long nesc = 0;
+    for (long long r = r0; r < r1; ++r) nesc += valid[r] && trip[3 * r + 2];
+    own.reserve((size_t)nesc);
+    for (long long r = r0; r < r1; ++r) {
+      if (!valid[r]) continue;
+      const char* p = buf + trip[3 * r];
+      const long long len = trip[3 * r + 1];
+      std::string_view key(p, (size_t)len);
+      if (trip[3 * r + 2]) {
+        std::string u;
+        u.reserve((size_t)len);
+        for (long long i = 0; i < len; ++i) {
+          if (p[i] == quote && i + 1 < len && p[i + 1] == quote) ++i;
+          u.push_back(p[i]);
+        }
+        own.push_back(std::move(u));
+        key = std::string_view(own.back());
+      }
+      auto it = m.find(key);
+      int code;
+      if (it == m.end()) {
+        code = (int)ldict[t].size();
+        ldict[t].push_back(key);
+        m.emplace(key, code);
+      } else {
+        code = it->second;
+      }
+      res->codes[(size_t)r] = code;
+    }
+  };
+  {
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(work, t);
+    work(0);
+    for (auto& x : th) x.join();
+  }
+  std::unordered_map<std::string_view, int> g;
+  std::vector<std::vector<int>> remap(nthreads);
+  for (int t = 0; t < nthreads; ++t) {
+    remap[t].resize(ldict[t].size());
+    for (size_t i = 0; i < ldict[t].size(); ++i) {
+      auto it = g.find(ldict[t][i]);
+      if (it == g.end()) {
+        const int c = (int)res->values.size();
+        res->values.push_back(ldict[t][i]);
+        g.emplace(ldict[t][i], c);
+        remap[t][i] = c;
+      } else {
+        remap[t][i] = it->second;
+      }
+    }
+  }
+  {
+    auto fix = [&](int t) {
+      const long long r0 = t * per, r1 = std::min(n, r0 + per);
+      for (long long r = r0; r < r1; ++r) {
+        int& c = res->codes[(size_t)r];
+        if (c >= 0) c = remap[t][(size_t)c];
+      }
+    };
+    std::vector<std::thread> th;
+    for (int t = 1; t < nthreads; ++t) th.emplace_back(fix, t);
+    fix(0);
+    for (auto& x : th) x.join();
+  }
+  return res;
+}
+
+// dictionary size: entries and total bytes
+CML_HOST_API void cml_dict_size(void* h, long long* count, long long* bytes) {
+  auto* res = static_cast<DictResult*>(h);
+  long long b = 0;
+  for (auto& v : res->values) b += (long long)v.size();
+  *count = (long long)res->values.size();
+  *bytes = b;
+}
+
+// codes [n] (int32), dictionary as Arrow large-string offsets [count+1] + data
+CML_HOST_API void cml_dict_fill(void* h, int* codes, long long* offsets, char* data) {
+  auto* res = static_cast<DictResult*>(h);
+  std::memcpy(codes, res->codes.data(), res->codes.size() * sizeof(int));
+  long long pos = 0;
+  for (size_t c = 0; c < res->values.size(); ++c) {
+    offsets[c] = pos;
+    std::memcpy(data + pos, res->values[c].data(), res->values[c].size());
+    pos += (long long)res->values[c].size();
+  }
+  offsets[res->values.size()] = pos;
+}
+
+CML_HOST_API void cml_dict_free(void* h) { delete static_cast<DictResult*>(h); }

@@ -23,6 +23,10 @@ _native.register_host_sigs({
     "cml_csv_index": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll]),
     "cml_csv_index_mt": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll, c_int]),
     "cml_csv_gather_strings": (c_ll, [ctypes.c_char_p, c_vp, c_vp, c_ll, ctypes.c_char, c_vp, c_vp]),
+    "cml_dict_build": (c_vp, [ctypes.c_char_p, c_vp, c_vp, c_ll, ctypes.c_char, c_int]),
+    "cml_dict_size": (None, [c_vp, c_vp, c_vp]),
+    "cml_dict_fill": (None, [c_vp, c_vp, c_vp, c_vp]),
+    "cml_dict_free": (None, [c_vp]),
     "cml_csv_parse": (c_int, [ctypes.c_char_p, c_ll, c_vp, c_ll, c_int, ctypes.c_char, ctypes.c_char, c_vp, c_vp,
                               c_vp, c_int]),
 })
@@ -41,8 +45,10 @@ def _np_dtype(code: int):
 
 
 def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = ",", quote: str = '"',
-                    rows: Optional[slice] = None, nthreads: Optional[int] = None):
-    """Parse a CSV image into host arrays: {name: (values np.ndarray, valid np.ndarray)}, nrecords."""
+                    rows: Optional[slice] = None, nthreads: Optional[int] = None, dicts: Optional[dict] = None):
+    """Parse a CSV image into host arrays: {name: (values np.ndarray, valid np.ndarray)}, nrecords.
+    Low-cardinality string columns are dictionary-encoded (values share one str object per
+    distinct string); with ``dicts`` given, it receives {name: (int32 codes, dictionary)} for them."""
     lib = _native.host()
     starts = record_starts(buf, header, quote, nthreads)
     if rows is not None:
@@ -64,7 +70,14 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
     for f, c, d, v in zip(schema.fields, codes, datas, valids):
         valid = v[:n].astype(bool)
         if c == 0:
-            out[f.name] = (_strings(lib, buf, d, v, n, quote), valid)
+            enc = _dictionary(lib, buf, d, v, n, quote, nthreads)
+            if enc is None:
+                out[f.name] = (_strings(lib, buf, d, v, n, quote), valid)
+            else:
+                codes, dictionary = enc
+                out[f.name] = (np.append(dictionary, None)[codes], valid)
+                if dicts is not None:
+                    dicts[f.name] = enc
         elif c == 5:
             out[f.name] = (d[:n].astype(bool), valid)
         else:
@@ -82,6 +95,56 @@ def record_starts(buf: bytes, header: bool, quote: str = '"', nthreads: Optional
     n = _native.host().cml_csv_index_mt(buf, len(buf), quote.encode(), 1 if header else 0, starts.ctypes.data, cap,
                                          nthreads)
     return starts[:n].copy()
+
+
+_DICT_SAMPLE = 16384
+
+
+def _dict_run(lib, buf, trip, valid_u8, n, quote, nthreads):
+    h = lib.cml_dict_build(buf, trip.ctypes.data, valid_u8.ctypes.data, n, quote.encode(), nthreads)
+    try:
+        cnt, nb = ctypes.c_longlong(), ctypes.c_longlong()
+        lib.cml_dict_size(h, ctypes.byref(cnt), ctypes.byref(nb))
+        codes = np.empty(n, dtype=np.int32)
+        offsets = np.empty(cnt.value + 1, dtype=np.int64)
+        data = np.empty(max(nb.value, 1), dtype=np.uint8)
+        lib.cml_dict_fill(h, codes.ctypes.data, offsets.ctypes.data, data.ctypes.data)
+    finally:
+        lib.cml_dict_free(h)
+    return codes, offsets, data, cnt.value
+
+
+def _dictionary(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int, quote: str,
+                nthreads: Optional[int]):
+    """(int32 codes with -1 for null, object array of the distinct strings in first-appearance
+    order) when the column looks low-cardinality on a leading sample, else None. The native
+    encoder hashes row blocks on several threads and merges the block dictionaries, so only one
+    Python str per distinct value is ever created."""
+    import pyarrow as pa
+    if n < 2 * _DICT_SAMPLE:
+        return None
+    nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+    _, _, _, k = _dict_run(lib, buf, trip, valid_u8, _DICT_SAMPLE, quote, 1)
+    if k > _DICT_SAMPLE // 4:
+        return None
+    codes, offsets, data, k = _dict_run(lib, buf, trip, valid_u8, n, quote, nthreads)
+    if k > n // 4:
+        return None
+    arr = pa.LargeStringArray.from_buffers(k, pa.py_buffer(offsets), pa.py_buffer(data))
+    return codes, arr.to_numpy(zero_copy_only=False)
+
+
+def merge_dictionaries(parts):
+    """Concatenate per-chunk (codes, dictionary) into one code space (first-appearance order)."""
+    index: Dict[str, int] = {}
+    out = []
+    for codes, dictionary in parts:
+        remap = np.empty(len(dictionary) + 1, dtype=np.int32)
+        for i, v in enumerate(dictionary):
+            remap[i] = index.setdefault(v, len(index))
+        remap[-1] = -1
+        out.append(remap[codes])
+    return np.concatenate(out) if out else np.zeros(0, dtype=np.int32)
 
 
 def _strings(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int, quote: str) -> np.ndarray:
@@ -164,6 +227,7 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
     whole_files = len(paths) >= W
     cols: Dict[str, List] = {f.name: [] for f in schema.fields}
     valids: Dict[str, List] = {f.name: [] for f in schema.fields}
+    encs: Dict[str, List] = {f.name: [] for f in schema.fields}
     ids: List[np.ndarray] = []
     for i, (p, fid) in enumerate(zip(paths, fids)):
         if whole_files and i % W != rank:
@@ -176,13 +240,15 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
             n_all = int(record_starts(buf, header, quote).shape[0])
             a, b = shard_range(n_all, rank, W)
             sl = slice(a, b)
-        parsed, n = parse_csv_bytes(buf, schema, header, sep, quote, rows=sl)
+        dicts: Dict[str, tuple] = {}
+        parsed, n = parse_csv_bytes(buf, schema, header, sep, quote, rows=sl, dicts=dicts)
         start = 0 if sl is None else sl.start
         ids.append((np.int64(fid) << np.int64(40)) + np.arange(start, start + n, dtype=np.int64))
         for f in schema.fields:
             v, ok = parsed[f.name]
             cols[f.name].append(v)
             valids[f.name].append(ok)
+            encs[f.name].append(dicts.get(f.name))
     dev = session._device
     from ..sql.dataframe import DataFrame
     out_cols = {}
@@ -195,6 +261,8 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
             vals = np.zeros(0, dtype=object if isinstance(f.dataType, T.StringType) else np.float64)
             ok = np.zeros(0, dtype=bool)
         out_cols[f.name] = _to_column(vals, ok, f.dataType, dev)
+        if encs[f.name] and all(e is not None for e in encs[f.name]):
+            out_cols[f.name].codes = merge_dictionaries(encs[f.name])
     rid = torch.as_tensor(np.concatenate(ids) if ids else np.zeros(0, dtype=np.int64), device=dev)
     return DataFrame(session, schema, out_cols, n_total, rid, dev)
 

@@ -27,6 +27,9 @@ class ColumnData:
     values: Any                      # torch.Tensor (device) or np.ndarray (host, object/str)
     valid: Any                       # None (all valid) | bool torch.Tensor | bool np.ndarray
     dtype: T.DataType
+    # dictionary codes of a host string column (int32, -1 = null; values[i] is the codes[i]-th
+    # distinct string, shared objects) — set by ingest, kept by row subsets, used by group-by
+    codes: Any = None
 
     @property
     def is_host(self) -> bool:
@@ -47,7 +50,8 @@ class ColumnData:
         """Row subset by index tensor (device) / array."""
         if self.is_host:
             ii = idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)
-            return ColumnData(self.values[ii], None if self.valid is None else self.valid[ii], self.dtype)
+            return ColumnData(self.values[ii], None if self.valid is None else self.valid[ii], self.dtype,
+                              None if self.codes is None else self.codes[ii])
         ti = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=self.values.device)
         ti = ti.to(self.values.device)
         return ColumnData(self.values[ti], None if self.valid is None else self.valid[ti], self.dtype)
@@ -55,7 +59,8 @@ class ColumnData:
     def mask(self, m) -> "ColumnData":
         if self.is_host:
             mm = m.cpu().numpy() if isinstance(m, torch.Tensor) else np.asarray(m, dtype=bool)
-            return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype)
+            return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype,
+                              None if self.codes is None else self.codes[mm])
         mm = m if isinstance(m, torch.Tensor) else torch.as_tensor(m, device=self.values.device)
         mm = mm.to(self.values.device)
         return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype)
@@ -515,6 +520,17 @@ class When(Expr):
         vals = [v.eval(frame) for _, v in self.branches]
         other = self.other.eval(frame) if self.other is not None else None
         all_cols = vals + ([other] if other is not None else [])
+        typed = [x for x in all_cols if not isinstance(x.dtype, T.NullType)]
+        if typed and not any(x.is_host for x in typed):
+            # NULL literal branches (when(c, None)) take the device type of the others
+            def _dev(x):
+                if not isinstance(x.dtype, T.NullType):
+                    return x
+                return ColumnData(torch.zeros(n, dtype=torch.float64, device=dev),
+                                  torch.zeros(n, dtype=torch.bool, device=dev), x.dtype)
+            vals = [_dev(v) for v in vals]
+            other = None if other is None else _dev(other)
+            all_cols = vals + ([other] if other is not None else [])
         if any(x.is_host for x in all_cols):
             out = np.empty(n, dtype=object)
             vm = np.zeros(n, dtype=bool)

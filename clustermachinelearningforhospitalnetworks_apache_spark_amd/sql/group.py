@@ -140,7 +140,12 @@ def _merge(parts, fn: str):
 def local_partials(df: DataFrame, keys: List[Expr], exprs: List[Expr]):
     """This rank's per-group partial aggregates: (specs, key_types, {key tuple: [partial per spec]}).
     A spec is ("key", name, key index, None) or ("agg", name, AggExpr, values, input type)."""
+    from . import group_fast
     from .window import _WINDOW_TYPE, TimeWindow
+    if group_fast.ENABLED:
+        fast = group_fast.fast_local_partials(df, keys, exprs)
+        if fast is not None:
+            return fast
     key_names = [k.name() for k in keys]
     # time-window keys (functions.window) may put a row into several buckets: expand rows first
     src = list(range(df._nrows))
