@@ -650,3 +650,4 @@ from .lsh import (BucketedRandomProjectionLSH, BucketedRandomProjectionLSHModel,
                   MinHashLSHModel)
 from .feature_text import (CountVectorizer, CountVectorizerModel, HashingTF, IDF, IDFModel, NGram,  # noqa: E402,F401
                            RegexTokenizer, StopWordsRemover, Tokenizer)
+from .feature_misc import DCT, FeatureHasher, VectorSizeHint  # noqa: E402,F401

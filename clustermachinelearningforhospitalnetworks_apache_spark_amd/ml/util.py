@@ -90,6 +90,14 @@ _JVM = {
     "VectorIndexer": "org.apache.spark.ml.feature.VectorIndexer",
     "VectorIndexerModel": "org.apache.spark.ml.feature.VectorIndexerModel",
     "SQLTransformer": "org.apache.spark.ml.feature.SQLTransformer",
+    "DCT": "org.apache.spark.ml.feature.DCT",
+    "FeatureHasher": "org.apache.spark.ml.feature.FeatureHasher",
+    "VectorSizeHint": "org.apache.spark.ml.feature.VectorSizeHint",
+    "Word2Vec": "org.apache.spark.ml.feature.Word2Vec",
+    "Word2VecModel": "org.apache.spark.ml.feature.Word2VecModel",
+    "LDA": "org.apache.spark.ml.clustering.LDA",
+    "LocalLDAModel": "org.apache.spark.ml.clustering.LocalLDAModel",
+    "PowerIterationClustering": "org.apache.spark.ml.clustering.PowerIterationClustering",
     "VarianceThresholdSelector": "org.apache.spark.ml.feature.VarianceThresholdSelector",
     "VarianceThresholdSelectorModel": "org.apache.spark.ml.feature.VarianceThresholdSelectorModel",
     "UnivariateFeatureSelector": "org.apache.spark.ml.feature.UnivariateFeatureSelector",
@@ -170,6 +178,14 @@ _PY = {
     "VectorIndexer": "feature",
     "VectorIndexerModel": "feature",
     "SQLTransformer": "feature",
+    "DCT": "feature",
+    "FeatureHasher": "feature",
+    "VectorSizeHint": "feature",
+    "Word2Vec": "feature",
+    "Word2VecModel": "feature",
+    "LDA": "clustering",
+    "LocalLDAModel": "clustering",
+    "PowerIterationClustering": "clustering",
     "VarianceThresholdSelector": "feature",
     "VarianceThresholdSelectorModel": "feature",
     "UnivariateFeatureSelector": "feature",
@@ -551,3 +567,28 @@ DefaultParamsReadable = MLReadable
 def load(path: str):
     """Load any saved estimator/model/pipeline by its metadata class."""
     return MLReader(None).load(path)
+
+
+def java_double_str(v: float) -> str:
+    """``java.lang.Double.toString``: shortest round-trip digits, plain notation for
+    1e-3 <= |v| < 1e7 (at least one fractional digit), ``d.dddE±n`` otherwise."""
+    import decimal
+    v = float(v)
+    if math.isnan(v):
+        return "NaN"
+    if math.isinf(v):
+        return "Infinity" if v > 0 else "-Infinity"
+    if v == 0.0:
+        return "-0.0" if math.copysign(1.0, v) < 0 else "0.0"
+    sign, digits, exp = decimal.Decimal(repr(v)).as_tuple()
+    ds = "".join(map(str, digits)).rstrip("0") or "0"
+    point = len(digits) + exp          # decimal point position relative to the digit string
+    a = abs(v)
+    neg = "-" if sign else ""
+    if 1e-3 <= a < 1e7:
+        if point <= 0:
+            return f"{neg}0.{'0' * -point}{ds}"
+        if point >= len(ds):
+            return f"{neg}{ds}{'0' * (point - len(ds))}.0"
+        return f"{neg}{ds[:point]}.{ds[point:]}"
+    return f"{neg}{ds[0]}.{ds[1:] or '0'}E{point - 1}"
