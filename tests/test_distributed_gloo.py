@@ -122,6 +122,18 @@ def _workload(out_path, rank, master="local[1]"):
     aft = AFTSurvivalRegression(labelCol="t", censorCol="cens", maxIter=30).fit(surv)
     res["aft"] = aft.coefficients.toArray().tolist() + [aft.intercept, aft.scale]
     res["iso"] = IsotonicRegression(labelCol="y", featureIndex=3).fit(f).predictions.toArray().tolist()[:50]
+    # LDA (online VB: counter-based mini-batches and γ init) and power iteration clustering
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import (LDA,
+                                                                                          PowerIterationClustering)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler as VA
+    cnt = pd.DataFrame(np.floor(np.abs(pdf[["a", "b", "c", "d"]].to_numpy()) * 3), columns=list("pqrs"))
+    cdf = VA(inputCols=list("pqrs"), outputCol="features").transform(spark.createDataFrame(cnt))
+    lda = LDA(k=2, maxIter=5, seed=3, subsamplingRate=0.3).fit(cdf)
+    res["lda"] = lda.topicsMatrix().toArray().ravel().tolist()
+    edges = [(i, j, 1.0 if i < 6 else 3.0) for b in (0, 6) for i in range(b, b + 6) for j in range(i + 1, b + 6)]
+    edges.append((5, 6, 0.01))
+    res["pic"] = sorted([r.id, r.cluster] for r in PowerIterationClustering(k=2, weightCol="weight").assignClusters(
+        spark.createDataFrame(edges, "src long, dst long, weight double")).collect())
     # stateful streaming: a complete-mode aggregation over CSV uploads planned by rank 0
     sdir = os.path.join(os.path.dirname(out_path), f"stream_w{spark.world_size}")
     if rank == 0:
@@ -208,6 +220,8 @@ def _check_invariant(r1, rw, world):
     np.testing.assert_allclose(rw["svc"], r1["svc"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(rw["aft"], r1["aft"], rtol=1e-5, atol=1e-7)
     np.testing.assert_allclose(rw["gmm"], r1["gmm"], rtol=1e-6)
+    np.testing.assert_allclose(rw["lda"], r1["lda"], rtol=1e-6)
+    assert rw["pic"] == r1["pic"]
     assert [x[:2] for x in rw["stream_agg"]] == [x[:2] for x in r1["stream_agg"]]
     np.testing.assert_allclose([x[2] for x in rw["stream_agg"]], [x[2] for x in r1["stream_agg"]], rtol=1e-12)
     assert sum(x[1] for x in r1["stream_agg"]) == 600
