@@ -651,3 +651,4 @@ from .lsh import (BucketedRandomProjectionLSH, BucketedRandomProjectionLSHModel,
 from .feature_text import (CountVectorizer, CountVectorizerModel, HashingTF, IDF, IDFModel, NGram,  # noqa: E402,F401
                            RegexTokenizer, StopWordsRemover, Tokenizer)
 from .feature_misc import DCT, FeatureHasher, VectorSizeHint  # noqa: E402,F401
+from .word2vec import Word2Vec, Word2VecModel  # noqa: E402,F401
