@@ -62,7 +62,8 @@ def column_from_values(values, dtype: T.DataType, device) -> ColumnData:
                 valid[i] = False
                 out[i] = None
             else:
-                keep = isinstance(dtype, (T.ArrayType, T.StructType, T.MapType, T.MatrixUDT))
+                keep = isinstance(dtype, (T.ArrayType, T.StructType, T.MapType, T.MatrixUDT)) or (
+                    isinstance(dtype, T.BinaryType) and isinstance(v, (bytes, bytearray)))
                 out[i] = v if keep or isinstance(v, str) else str(v)
         return ColumnData(out, None if valid.all() else valid, dtype)
     valid = np.ones(n, dtype=bool)
@@ -99,6 +100,9 @@ def column_from_values(values, dtype: T.DataType, device) -> ColumnData:
                     if isinstance(dtype, T.BooleanType):
                         arr[i] = (v.lower() == "true") if isinstance(v, str) else bool(v)
                     elif T.is_integral(dtype):
+                        if isinstance(v, (int, np.integer)):
+                            arr[i] = int(v)  # exact: no float round trip for 64-bit values
+                            continue
                         fv = float(v)
                         if math.isnan(fv):
                             valid[i] = False

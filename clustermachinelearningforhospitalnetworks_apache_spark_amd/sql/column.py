@@ -586,7 +586,8 @@ class Func(Expr):
         return any(a.is_aggregate() for a in self.args)
 
     def __str__(self):
-        return f"{self.fname}({', '.join(str(a) for a in self.args)})"
+        parts = [str(a) for a in self.args] + [str(p) for p in getattr(self, "params", ())]
+        return f"{self.fname}({', '.join(parts)})"
 
     def eval(self, frame):
         return self.impl(frame, [a.eval(frame) for a in self.args])
@@ -709,8 +710,10 @@ class Column:
 
     def asc(self): return SortOrder(self._expr, True)
     def desc(self): return SortOrder(self._expr, False)
+    def asc_nulls_first(self): return SortOrder(self._expr, True, True)
     def asc_nulls_last(self): return SortOrder(self._expr, True, False)
     def desc_nulls_first(self): return SortOrder(self._expr, False, True)
+    def desc_nulls_last(self): return SortOrder(self._expr, False, False)
 
     def __getattr__(self, item):
         if item.startswith("_"):

@@ -63,7 +63,14 @@ def current_date() -> Column:
 
 
 def to_timestamp(c: ColumnOrName, fmt: str = None) -> Column:
-    return Column(Cast(_c(c), T.TimestampType()))
+    """Cast to timestamp; with ``fmt`` parse strings with that Spark datetime pattern (null when a
+    value does not match)."""
+    if fmt is None:
+        return Column(Cast(_c(c), T.TimestampType()))
+    from .datetimefmt import parser
+    p = parser(fmt)
+    return _host_map("to_timestamp", [c], lambda s: p(s) if isinstance(s, str) else _as_datetime(s),
+                     T.TimestampType(), params=[fmt])
 
 
 def monotonically_increasing_id() -> Column:
@@ -393,11 +400,32 @@ def pandas_udf(f=None, returnType=None, functionType=None):
 
 # ------------------------------------------------------------------------------------------------ strings / dates
 
-def _host_map(name, cols, fn, rt):
-    """Row-wise host function over one or more columns (null in -> null out unless fn handles it)."""
+def _closure_params(fn) -> list:
+    """Scalar parameters a row function closes over (used to make output column names unique, e.g.
+    ``substring_index(s, ., 2)`` vs ``substring_index(s, ., -3)``)."""
+    out = []
+    for cell in (getattr(fn, "__closure__", None) or ()):
+        try:
+            v = cell.cell_contents
+        except ValueError:
+            continue
+        if isinstance(v, (str, int, float, bool)):
+            out.append(v)
+        elif isinstance(getattr(v, "pattern", None), str):
+            out.append(v.pattern)
+    return out
+
+
+def _host_map(name, cols, fn, rt, params=None):
+    """Row-wise host function over one or more columns (null in -> null out unless fn handles it).
+    ``params`` (default: the scalars ``fn`` closes over) are shown in the column name."""
     def wrapped(*vals):
         return None if any(v is None for v in vals) else fn(*vals)
-    return UserDefinedFunction(wrapped, rt, name=name)(*cols)
+    col = UserDefinedFunction(wrapped, rt, name=name)(*cols)
+    ps = _closure_params(fn) if params is None else list(params)
+    if ps:
+        col._expr.params = ps
+    return col
 
 
 def substring(c: ColumnOrName, pos: int, length: int) -> Column:
@@ -447,17 +475,26 @@ def rpad(c: ColumnOrName, width: int, pad: str) -> Column:
     return _host_map("rpad", [c], lambda s: (str(s) + pad * width)[:width], T.StringType())
 
 
-def _spark_to_strftime(fmt: str) -> str:
-    out = fmt
-    for a, b in (("yyyy", "%Y"), ("MM", "%m"), ("dd", "%d"), ("HH", "%H"), ("mm", "%M"), ("ss", "%S"),
-                 ("yy", "%y"), ("EEE", "%a"), ("MMM", "%b")):
-        out = out.replace(a, b)
-    return out
+def _as_datetime(t):
+    import datetime as _dt
+    from .column import micros_to_datetime, ts_to_micros
+    if isinstance(t, str):
+        try:
+            return micros_to_datetime(ts_to_micros(t))
+        except (ValueError, TypeError):
+            return None
+    return t if isinstance(t, (_dt.datetime, _dt.date)) else None
 
 
 def date_format(c: ColumnOrName, fmt: str) -> Column:
-    py = _spark_to_strftime(fmt)
-    return _host_map("date_format", [c], lambda t: t.strftime(py), T.StringType())
+    """Format a date / timestamp (or a timestamp string) with a Spark datetime pattern."""
+    from .datetimefmt import formatter
+    f = formatter(fmt)
+
+    def g(t):
+        t = _as_datetime(t)
+        return None if t is None else f(t)
+    return _host_map("date_format", [c], g, T.StringType(), params=[fmt])
 
 
 def _days(cd: ColumnData) -> torch.Tensor:
@@ -469,6 +506,15 @@ def _days(cd: ColumnData) -> torch.Tensor:
 
 
 def to_date(c: ColumnOrName, fmt: str = None) -> Column:
+    if fmt is not None:
+        from .datetimefmt import parser
+        p = parser(fmt)
+
+        def g(s):
+            t = p(s) if isinstance(s, str) else _as_datetime(s)
+            return None if t is None else (t.date() if hasattr(t, "date") else t)
+        return _host_map("to_date", [c], g, T.DateType(), params=[fmt])
+
     def impl(frame, args):
         a = args[0]
         if a.is_host or isinstance(a.dtype, T.StringType):
@@ -517,6 +563,16 @@ def unix_timestamp(c: ColumnOrName = None, fmt: str = None) -> Column:
             torch.full((frame._nrows,), int(time.time()), dtype=torch.int64, device=frame._device), None,
             T.LongType())))
 
+    if fmt is not None:
+        from .column import ts_to_micros
+        from .datetimefmt import parser
+        p = parser(fmt)
+
+        def g(s):
+            t = p(s) if isinstance(s, str) else _as_datetime(s)
+            return None if t is None else ts_to_micros(t) // 1_000_000
+        return _host_map("unix_timestamp", [c], g, T.LongType(), params=[fmt])
+
     def impl(frame, args):
         a = args[0]
         if isinstance(a.dtype, T.DateType):
@@ -542,9 +598,11 @@ def _cast_host_ts(frame, a):
 
 def from_unixtime(c: ColumnOrName, fmt: str = "yyyy-MM-dd HH:mm:ss") -> Column:
     import datetime as _dt
-    py = _spark_to_strftime(fmt)
-    return _host_map("from_unixtime", [c], lambda s: _dt.datetime.utcfromtimestamp(int(s)).strftime(py),
-                     T.StringType())
+    from .datetimefmt import formatter
+    f = formatter(fmt)
+    return _host_map("from_unixtime", [c], lambda s: f(_dt.datetime(1970, 1, 1) + _dt.timedelta(seconds=int(s))),
+                     T.StringType(), params=[fmt])
 
 
 from .functions_more import *  # noqa: E402,F401,F403  (statistical aggregates, math/date/string, arrays, explode)
+from .functions_extra import *  # noqa: E402,F401,F403  (null helpers, hashes, time zones, collections, lambdas, JSON)

@@ -755,6 +755,55 @@ def posexplode_outer(c: ColumnOrName) -> Column:
     return Column(Generator("posexplode_outer", _c(c)))
 
 
+def _generator_plan(ge: "Generator", cd: ColumnData):
+    """(output names, output types, value -> list of output tuples) for one generator."""
+    outer = ge.fn.endswith("_outer")
+    if ge.fn == "json_tuple":
+        import json as _json
+        fields = list(getattr(ge, "fields", []))
+
+        def expand_json(v):
+            try:
+                obj = _json.loads(v) if v is not None else None
+            except (ValueError, TypeError):
+                obj = None
+            if not isinstance(obj, dict):
+                return [tuple(None for _ in fields)]
+            out = []
+            for f in fields:
+                x = obj.get(f)
+                out.append(None if x is None else (x if isinstance(x, str) else _json.dumps(x, separators=(",", ":"))))
+            return [tuple(out)]
+        return [f"c{i}" for i in range(len(fields))], [T.StringType()] * len(fields), expand_json
+    if ge.fn.startswith("inline"):
+        st = cd.dtype.elementType if isinstance(cd.dtype, T.ArrayType) else None
+        if not isinstance(st, T.StructType):
+            raise TypeError("inline() needs an array of structs")
+        width = len(st.fields)
+
+        def expand_inline(v):
+            items = [tuple(e) if e is not None else tuple([None] * width) for e in (v or [])]
+            return items if items else ([tuple([None] * width)] if outer else [])
+        return [f.name for f in st.fields], [f.dataType for f in st.fields], expand_inline
+    is_map = isinstance(cd.dtype, T.MapType)
+    pos = ge.fn.startswith("pos")
+    names = ge.output_names(is_map)
+    if is_map:
+        types = ([T.IntegerType()] if pos else []) + [cd.dtype.keyType, cd.dtype.valueType]
+    else:
+        types = ([T.IntegerType()] if pos else []) + [cd.dtype.elementType if isinstance(cd.dtype, T.ArrayType)
+                                                      else T.StringType()]
+
+    def expand(v):
+        items = list(v.items()) if (is_map and v is not None) else (list(v) if v is not None else [])
+        if not items:
+            if not outer:
+                return []
+            return [((None,) if pos else ()) + ((None, None) if is_map else (None,))]
+        return [((p,) if pos else ()) + (tuple(e) if is_map else (e,)) for p, e in enumerate(items)]
+    return names, types, expand
+
+
 def select_with_generator(df, exprs: List[Expr]):
     """``df.select(...)`` where one item is a Generator: each input row is repeated once per element
     (``_outer``: at least once, with null elements for null / empty inputs); the other items are
@@ -772,23 +821,15 @@ def select_with_generator(df, exprs: List[Expr]):
         alias, ge = ge.alias, ge.child
     cd = ge.child.eval(df)
     vals = column_to_python(cd)
-    is_map = isinstance(cd.dtype, T.MapType)
-    outer = ge.fn.endswith("_outer")
-    rep, elems = [], []
+    gnames, gtypes, expand = _generator_plan(ge, cd)
+    rep, rows = [], []
     for i, v in enumerate(vals):
-        items = list(v.items()) if (is_map and v is not None) else (list(v) if v is not None else [])
-        if not items and outer:
+        for r in expand(v):
             rep.append(i)
-            elems.append((None, (None, None) if is_map else None))
-            continue
-        for p, e in enumerate(items):
-            rep.append(i)
-            elems.append((p, e))
+            rows.append(r)
     idx = torch.as_tensor(rep, dtype=torch.int64, device=df._device)
     base = df._take_rows(idx)
     names, datas = [], []
-    et = cd.dtype.elementType if isinstance(cd.dtype, T.ArrayType) else T.StringType()
-    gnames = ge.output_names(is_map)
     if alias is not None:
         al = alias if isinstance(alias, (list, tuple)) else [alias]
         if len(al) != len(gnames):
@@ -799,16 +840,9 @@ def select_with_generator(df, exprs: List[Expr]):
             names.append(e.name())
             datas.append(e.eval(base))
             continue
-        gen_cols = []
-        if ge.fn.startswith("pos"):
-            gen_cols.append(column_from_values([p for p, _ in elems], T.IntegerType(), df._device))
-        if is_map:
-            gen_cols.append(column_from_values([kv[0] for _, kv in elems], cd.dtype.keyType, df._device))
-            gen_cols.append(column_from_values([kv[1] for _, kv in elems], cd.dtype.valueType, df._device))
-        else:
-            gen_cols.append(column_from_values([x for _, x in elems], et, df._device))
-        names += gnames
-        datas += gen_cols
+        for k, (gn, gt) in enumerate(zip(gnames, gtypes)):
+            names.append(gn)
+            datas.append(column_from_values([r[k] for r in rows], gt, df._device))
     out = base._from_columns(names, datas)
     counts = df._comm.allgather_object(len(rep))
     off = builtins.sum(counts[:df._comm.rank])

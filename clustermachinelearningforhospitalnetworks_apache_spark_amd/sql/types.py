@@ -285,26 +285,83 @@ _SIMPLE = {
 }
 
 
+def _split_top(s: str, sep: str = ",") -> List[str]:
+    """Split on ``sep`` outside <...> / (...) nesting."""
+    out, depth, cur = [], 0, []
+    for ch in s:
+        if ch in "<(":
+            depth += 1
+        elif ch in ">)":
+            depth -= 1
+        if ch == sep and depth == 0:
+            out.append("".join(cur))
+            cur = []
+        else:
+            cur.append(ch)
+    out.append("".join(cur))
+    return [p.strip() for p in out if p.strip()]
+
+
+def _name_type(part: str):
+    """'name TYPE' / 'name: TYPE' / '`na me` TYPE' -> (name, type string)."""
+    part = part.strip()
+    if part.startswith("`"):
+        end = part.index("`", 1)
+        name, rest = part[1:end], part[end + 1:]
+    else:
+        i = 0
+        while i < len(part) and not part[i].isspace() and part[i] != ":":
+            i += 1
+        name, rest = part[:i], part[i:]
+    rest = rest.strip()
+    if rest.startswith(":"):
+        rest = rest[1:].strip()
+    # drop trailing column constraints / comments
+    up = rest.upper()
+    for kw in (" NOT NULL", " COMMENT "):
+        j = up.find(kw)
+        if j >= 0:
+            rest, up = rest[:j], up[:j]
+    return name, rest.strip()
+
+
 def parse_type(s) -> DataType:
+    """Spark SQL type strings: simple names, decimal(p,s), array<T>, map<K,V>, struct<a:T,...>."""
     if isinstance(s, DataType):
         return s
-    t = str(s).strip().lower()
-    if t.startswith("array<") and t.endswith(">"):
+    t = str(s).strip()
+    low = t.lower()
+    if low.startswith("array<") and low.endswith(">"):
         return ArrayType(parse_type(t[6:-1]))
-    if t in _SIMPLE:
-        return _SIMPLE[t]()
+    if low.startswith("map<") and low.endswith(">"):
+        kv = _split_top(t[4:-1])
+        if len(kv) != 2:
+            raise ValueError(f"bad map type {s!r}")
+        return MapType(parse_type(kv[0]), parse_type(kv[1]))
+    if low.startswith("struct<") and low.endswith(">"):
+        st = StructType()
+        for part in _split_top(t[7:-1]):
+            name, typ = _name_type(part)
+            st.add(name, parse_type(typ))
+        return st
+    if low.startswith("decimal") or low.startswith("numeric") or low.startswith("dec"):
+        if "(" in low:
+            args = [int(x) for x in low[low.index("(") + 1:low.rindex(")")].split(",")]
+            return DecimalType(*args)
+        return DecimalType()
+    if low in _SIMPLE:
+        return _SIMPLE[low]()
+    if low.startswith("varchar") or low.startswith("char"):
+        return StringType()
     raise ValueError(f"unknown type {s!r}")
 
 
 def parse_ddl_schema(ddl: str) -> StructType:
-    """'a INT, b DOUBLE' -> StructType."""
+    """'a INT, b DOUBLE, c ARRAY<STRING>, d STRUCT<x: INT, y: MAP<STRING, DOUBLE>>' -> StructType."""
     st = StructType()
-    for part in ddl.split(","):
-        part = part.strip()
-        if not part:
-            continue
-        name, typ = part.replace(":", " ").split(None, 1)
-        st.add(name.strip("`"), parse_type(typ))
+    for part in _split_top(ddl):
+        name, typ = _name_type(part)
+        st.add(name, parse_type(typ), nullable="NOT NULL" not in part.upper())
     return st
 
 
