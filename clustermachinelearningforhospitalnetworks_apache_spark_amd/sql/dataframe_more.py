@@ -344,13 +344,20 @@ class MultiGroupedData:
         self.df, self.keys, self.sets = df, keys, sets
 
     def agg(self, *exprs):
-        from .column import Column, Lit
+        from .column import Alias, Column, Lit
         from .dataframe import _as_expr
+        from .functions_extra import GroupingMarker
         from .group import GroupedData
         names = [k.name() for k in self.keys]
+        if len(exprs) == 1 and isinstance(exprs[0], dict):
+            from . import functions as F
+            exprs = tuple(getattr(F, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})")
+                          for c, fn in exprs[0].items())
+        es = [_as_expr(e) for e in exprs]
+        plain = [Column(e) for e in es if not isinstance(e.child if isinstance(e, Alias) else e, GroupingMarker)]
         out = None
         for s in self.sets:
-            part = GroupedData(self.df, list(s)).agg(*exprs)
+            part = GroupedData(self.df, list(s)).agg(*plain)
             sn = [k.name() for k in s]
             sel = []
             for nm, k in zip(names, self.keys):
@@ -359,7 +366,15 @@ class MultiGroupedData:
                 else:
                     dt = k.eval(self.df).dtype
                     sel.append(Column(Lit(None)).cast(dt).alias(nm))
-            sel += [Column(_as_expr(c)) for c in part.columns if c not in sn]
+            agg_cols = [c for c in part.columns if c not in sn]
+            it = iter(agg_cols)
+            for e in es:
+                inner = e.child if isinstance(e, Alias) else e
+                if isinstance(inner, GroupingMarker):
+                    v, dt = inner.value(names, sn)
+                    sel.append(Column(Lit(v)).cast(dt).alias(e.alias if isinstance(e, Alias) else inner.name()))
+                else:
+                    sel.append(Column(_as_expr(next(it))))
             part = part.select(*sel)
             out = part if out is None else out.union(part)
         return out

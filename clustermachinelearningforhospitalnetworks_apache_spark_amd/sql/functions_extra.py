@@ -635,6 +635,12 @@ def current_timezone() -> Column:
     return lit("UTC")
 
 
+def session_window(timeColumn: ColumnOrName, gapDuration) -> Column:
+    """Session windows for groupBy: events of one key closer than ``gapDuration`` share a session."""
+    from .window import SessionWindow, parse_duration_us
+    return Column(SessionWindow(_e(timeColumn), parse_duration_us(gapDuration)))
+
+
 def window_time(windowColumn: ColumnOrName) -> Column:
     """The event time of a window struct: its end minus 1 microsecond."""
     def f(w):
@@ -1346,6 +1352,47 @@ def json_array_length(col: ColumnOrName) -> Column:
             return None
         return len(v) if isinstance(v, list) else None
     return _host_map("json_array_length", [col], f, T.IntegerType())
+
+
+# ------------------------------------------------------------------------------------------ grouping sets
+
+class GroupingMarker(Expr):
+    """``grouping(col)`` / ``grouping_id(cols...)`` inside ``rollup`` / ``cube`` aggregations: resolved
+    per grouping set by MultiGroupedData (1 where the column is rolled up)."""
+
+    def __init__(self, kind: str, cols: List[str]):
+        self.kind, self.cols = kind, cols
+
+    def refs(self):
+        return list(self.cols)
+
+    def name(self):
+        return f"{self.kind}({', '.join(self.cols)})"
+
+    __str__ = name
+
+    def is_aggregate(self):
+        return True
+
+    def eval(self, frame):
+        raise ValueError(f"{self.kind}() can only be used with GroupingSets/Cube/Rollup")
+
+    def value(self, keys: List[str], in_set: List[str]):
+        if self.kind == "grouping":
+            return (0 if self.cols[0] in in_set else 1), T.ByteType()
+        cols = self.cols or keys
+        v = 0
+        for c in cols:
+            v = (v << 1) | (0 if c in in_set else 1)
+        return v, T.LongType()
+
+
+def grouping(col: ColumnOrName) -> Column:
+    return Column(GroupingMarker("grouping", [col if isinstance(col, str) else _e(col).name()]))
+
+
+def grouping_id(*cols: ColumnOrName) -> Column:
+    return Column(GroupingMarker("grouping_id", [c if isinstance(c, str) else _e(c).name() for c in cols]))
 
 
 # ------------------------------------------------------------------------------------------ misc

@@ -24,9 +24,10 @@ from __future__ import annotations
 
 import math
 import sys
-from typing import Any, List, Optional, Sequence
+from typing import Any, Dict, List, Optional, Sequence
 
 import numpy as np
+import torch
 
 from . import types as T
 from .column import AggExpr, ColRef, Column, ColumnData, Expr, SortOrder, _expr
@@ -421,6 +422,78 @@ class TimeWindow(Expr):
         if self.slide != self.dur:
             raise ValueError("a sliding window() yields several buckets per row: use it in groupBy")
         return column_from_values([w[0] if w else None for w in b], _WINDOW_TYPE, frame._device)
+
+
+class SessionWindow(Expr):
+    """``functions.session_window(timeColumn, gapDuration)``: per group of the other grouping keys,
+    events closer than ``gap`` form one session [first event, last event + gap). Sessions can span
+    ranks, so the (key, event time) pairs are gathered, swept in time order once, and every rank
+    maps its rows to their session (``materialize``, called by GroupedData before aggregating)."""
+
+    def __init__(self, child: Expr, gap_us: int):
+        if gap_us <= 0:
+            raise ValueError("session_window needs a positive gap duration")
+        self.child, self.gap = child, gap_us
+
+    def refs(self):
+        return self.child.refs()
+
+    def name(self):
+        return "session_window"
+
+    def __str__(self):
+        return f"session_window({self.child}, {self.gap}us)"
+
+    def eval(self, frame) -> ColumnData:
+        raise ValueError("session_window() is only supported as a groupBy key")
+
+    def materialize(self, frame, other_keys: List[Expr]) -> ColumnData:
+        from .builder import column_from_values
+        from .column import micros_to_datetime
+        from .dataframe import column_to_python
+        from .types import Row
+        cd = self.child.eval(frame)
+        if not isinstance(cd.dtype, T.TimestampType) or cd.is_host:
+            raise TypeError("session_window() needs a timestamp column")
+        ts = cd.values.to(torch.int64).cpu().tolist()
+        vm = cd.valid_mask().cpu().tolist()
+        kv = [column_to_python(k.eval(frame)) for k in other_keys]
+        keys = [tuple(_hashable_key(k[i]) for k in kv) for i in range(len(ts))]
+        local = sorted({(k, t) for k, t, ok in zip(keys, ts, vm) if ok}, key=lambda x: (repr(x[0]), x[1]))
+        events: Dict[tuple, List[int]] = {}
+        for part in frame._comm.allgather_object(local):
+            for k, t in part:
+                events.setdefault(k, []).append(t)
+        session: Dict[tuple, tuple] = {}
+        for k, tl in events.items():
+            tl = sorted(set(tl))
+            start, end, members = tl[0], tl[0] + self.gap, [tl[0]]
+            for t in tl[1:]:
+                if t < end:
+                    end = max(end, t + self.gap)
+                    members.append(t)
+                    continue
+                for m in members:
+                    session[(k, m)] = (start, end)
+                start, end, members = t, t + self.gap, [t]
+            for m in members:
+                session[(k, m)] = (start, end)
+        vals = []
+        for k, t, ok in zip(keys, ts, vm):
+            if not ok:
+                vals.append(None)
+                continue
+            a, b = session[(k, t)]
+            vals.append(Row(start=micros_to_datetime(a), end=micros_to_datetime(b)))
+        return column_from_values(vals, _WINDOW_TYPE, frame._device)
+
+
+def _hashable_key(v):
+    if isinstance(v, list):
+        return tuple(_hashable_key(x) for x in v)
+    if isinstance(v, dict):
+        return tuple(sorted((k, _hashable_key(x)) for k, x in v.items()))
+    return v
 
 
 def parse_duration_us(s) -> int:

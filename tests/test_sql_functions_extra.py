@@ -194,3 +194,27 @@ def test_inline_and_misc(spark):
     o = spark.createDataFrame([(None,), (2,), (1,)], "x int").orderBy(F.desc_nulls_last("x")).collect()
     assert [r.x for r in o] == [2, 1, None]
     assert spark.range(1).select(F.input_file_name()).collect()[0][0] == ""
+
+
+def test_grouping_in_rollup_and_cube(spark):
+    df = spark.createDataFrame([("a", "x", 1), ("a", "y", 2), ("b", "x", 3)], "g string, h string, v int")
+    rows = df.rollup("g", "h").agg(F.sum("v").alias("s"), F.grouping("g").alias("gg"), F.grouping_id().alias("gid")) \
+        .orderBy("gid", "g", "h").collect()
+    got = [(r.g, r.h, r.s, r.gg, r.gid) for r in rows]
+    assert got == [("a", "x", 1, 0, 0), ("a", "y", 2, 0, 0), ("b", "x", 3, 0, 0),
+                   ("a", None, 3, 0, 1), ("b", None, 3, 0, 1), (None, None, 6, 1, 3)]
+    cube = df.cube("g", "h").agg(F.grouping_id("g", "h").alias("gid"), F.count("*").alias("n")).collect()
+    assert sorted({r.gid for r in cube}) == [0, 1, 2, 3]
+    with pytest.raises(ValueError):
+        df.select(F.grouping("g")).collect()
+
+
+def test_session_window(spark):
+    t0 = dt.datetime(2024, 1, 1, 10, 0)
+    m = lambda k: t0 + dt.timedelta(minutes=k)
+    rows = [("h1", m(0)), ("h1", m(3)), ("h1", m(7)), ("h1", m(20)), ("h2", m(1)), ("h2", m(30)), ("h2", None)]
+    df = spark.createDataFrame(rows, "h string, t timestamp")
+    out = df.groupBy("h", F.session_window("t", "5 minutes")).agg(F.count("*").alias("n")).collect()
+    got = sorted((r.h, r.session_window.start if r.session_window else None,
+                  r.session_window.end if r.session_window else None, r.n) for r in out if r.session_window)
+    assert got == [("h1", m(0), m(12), 3), ("h1", m(20), m(25), 1), ("h2", m(1), m(6), 1), ("h2", m(30), m(35), 1)]
