@@ -89,6 +89,16 @@ class DenseVector(Vector):
     def __truediv__(self, o):
         return DenseVector(self.array / np.asarray(o, dtype=np.float64))
 
+    def __neg__(self):
+        return DenseVector(-self.array)
+
+    __radd__ = __add__
+    __rmul__ = __mul__
+
+    def toSparse(self) -> "SparseVector":
+        nz = np.nonzero(self.array)[0]
+        return SparseVector(self.size, nz.tolist(), self.array[nz].tolist())
+
 
 class SparseVector(Vector):
     def __init__(self, size: int, *args):
@@ -116,6 +126,13 @@ class SparseVector(Vector):
 
     def numNonzeros(self) -> int:
         return int(np.count_nonzero(self.values))
+
+    def toDense(self) -> DenseVector:
+        return DenseVector(self.toArray())
+
+    def dot(self, other) -> float:
+        o = as_array(other)
+        return float(np.dot(self.values, o[self.indices]))
 
     def __getitem__(self, i):
         return self.toArray()[i]
@@ -180,16 +197,75 @@ class DenseMatrix(Matrix):
         return self.values.reshape(self.numCols, self.numRows).T
 
     def __eq__(self, other):
-        return isinstance(other, DenseMatrix) and np.array_equal(self.toArray(), other.toArray())
+        return isinstance(other, Matrix) and np.array_equal(self.toArray(), other.toArray())
+
+    def __getitem__(self, ij):
+        i, j = ij
+        return float(self.toArray()[i, j])
+
+    def toSparse(self) -> "SparseMatrix":
+        return SparseMatrix.from_dense(self.toArray())
 
     def __repr__(self):
         return f"DenseMatrix({self.numRows}, {self.numCols}, {self.values.tolist()}, {self.isTransposed})"
+
+
+class SparseMatrix(Matrix):
+    """Compressed sparse column matrix (Spark's layout; isTransposed => compressed rows)."""
+
+    def __init__(self, numRows: int, numCols: int, colPtrs, rowIndices, values, isTransposed: bool = False):
+        super().__init__(numRows, numCols, isTransposed)
+        self.colPtrs = np.asarray(colPtrs, dtype=np.int32)
+        self.rowIndices = np.asarray(rowIndices, dtype=np.int32)
+        self.values = np.asarray(values, dtype=np.float64)
+        major = numRows if isTransposed else numCols
+        if self.colPtrs.shape[0] != major + 1:
+            raise ValueError(f"colPtrs must have {major + 1} entries")
+        if self.rowIndices.shape[0] != self.values.shape[0]:
+            raise ValueError("rowIndices and values differ in length")
+
+    @staticmethod
+    def from_dense(a: np.ndarray) -> "SparseMatrix":
+        a = np.asarray(a, dtype=np.float64)
+        ptrs, rows, vals = [0], [], []
+        for j in range(a.shape[1]):
+            nz = np.nonzero(a[:, j])[0]
+            rows.extend(nz.tolist())
+            vals.extend(a[nz, j].tolist())
+            ptrs.append(len(rows))
+        return SparseMatrix(a.shape[0], a.shape[1], ptrs, rows, vals)
+
+    def toArray(self) -> np.ndarray:
+        major, minor = (self.numRows, self.numCols) if self.isTransposed else (self.numCols, self.numRows)
+        out = np.zeros((minor, major))
+        for j in range(major):
+            a, b = self.colPtrs[j], self.colPtrs[j + 1]
+            out[self.rowIndices[a:b], j] = self.values[a:b]
+        return out.T if self.isTransposed else out
+
+    def toDense(self) -> DenseMatrix:
+        return Matrices.from_numpy(self.toArray())
+
+    def __getitem__(self, ij):
+        i, j = ij
+        return float(self.toArray()[i, j])
+
+    def __eq__(self, other):
+        return isinstance(other, Matrix) and np.array_equal(self.toArray(), other.toArray())
+
+    def __repr__(self):
+        return (f"SparseMatrix({self.numRows}, {self.numCols}, {self.colPtrs.tolist()}, {self.rowIndices.tolist()}, "
+                f"{self.values.tolist()}, {self.isTransposed})")
 
 
 class Matrices:
     @staticmethod
     def dense(numRows: int, numCols: int, values) -> DenseMatrix:
         return DenseMatrix(numRows, numCols, values)
+
+    @staticmethod
+    def sparse(numRows: int, numCols: int, colPtrs, rowIndices, values) -> SparseMatrix:
+        return SparseMatrix(numRows, numCols, colPtrs, rowIndices, values)
 
     @staticmethod
     def from_numpy(a: np.ndarray) -> DenseMatrix:
