@@ -77,6 +77,16 @@ def column_to_arrow(cd: ColumnData):
         mat = cd.values.detach().double().cpu().numpy()
         valid = None if cd.valid is None else cd.valid_mask().cpu().numpy()
         return vectors_to_arrow(mat, valid)
+    if cd.is_host and cd.codes is not None and isinstance(cd.dtype, T.StringType):
+        # dictionary-encoded strings: codes + one object per distinct value, expanded by Arrow in C++
+        codes = np.asarray(cd.codes, dtype=np.int32)
+        k = int(codes.max(initial=-1)) + 1
+        first = np.full(k, -1, dtype=np.int64)
+        pos = np.nonzero(codes >= 0)[0]
+        first[codes[pos][::-1]] = pos[::-1]
+        dictionary = pa.array(list(cd.values[first]) if k else [], type=pa.string())
+        idx = pa.array(codes, mask=codes < 0)
+        return pa.DictionaryArray.from_arrays(idx, dictionary).cast(pa.string())
     if cd.is_host:
         return pa.array(column_to_python(cd), type=spark_type_to_arrow(cd.dtype))
     arr = cd.values.detach().cpu().numpy()

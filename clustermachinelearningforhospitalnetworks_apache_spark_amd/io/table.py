@@ -137,6 +137,56 @@ def write_frame(df, root: str, mode: str, operation: str = "WRITE", txn: Optiona
     return comm.broadcast_object(version)
 
 
+class PendingWrite:
+    """A table append whose Parquet file is being written by a background thread (Arrow's writer
+    releases the GIL), so the caller can run other work — the streaming query runs the user's
+    foreachBatch function — before ``finish()`` joins it and commits (collectives happen in
+    ``finish``, at the same point on every rank)."""
+
+    def __init__(self, df, root: str, mode: str, operation: str, txn: Optional[dict]):
+        import threading
+
+        import pyarrow.parquet as pq
+        from .arrow import frame_to_arrow
+        self.df, self.root, self.mode, self.operation, self.txn = df, root, mode, operation, txn
+        self.path = new_data_file(root, df._comm.rank) if df._nrows > 0 else None
+        self.error: Optional[BaseException] = None
+        self.thread = None
+        if self.path:
+            table = frame_to_arrow(df)  # device -> host on the calling thread
+
+            def run():
+                try:
+                    pq.write_table(table, self.path)
+                except BaseException as e:  # noqa: BLE001 — re-raised in finish()
+                    self.error = e
+            self.thread = threading.Thread(target=run, name="cml-table-write", daemon=True)
+            self.thread.start()
+
+    def finish(self) -> Optional[int]:
+        if self.thread is not None:
+            self.thread.join()
+        comm = self.df._comm
+        failed = comm.allgather_object(self.error is not None)
+        if any(failed):
+            raise self.error if self.error is not None else RuntimeError("table write failed on another rank")
+        paths = comm.allgather_object(self.path)
+        added = [p for p in paths if p]
+        version = None
+        if comm.is_root:
+            removed = snapshot(self.root)[0] if self.mode == "overwrite" else []
+            version = commit(self.root, added, removed, self.df.schema, self.operation, self.txn)
+        return comm.broadcast_object(version)
+
+
+def write_frame_async(df, root: str, mode: str, operation: str = "WRITE",
+                      txn: Optional[dict] = None) -> PendingWrite:
+    """Append / overwrite like ``write_frame`` with the file write overlapped (``.finish()``)."""
+    if mode not in ("append", "overwrite"):
+        raise ValueError("write_frame_async supports append / overwrite")
+    return PendingWrite(df, root, mode, operation, txn)
+
+
 def read_table(session, root: str, version: Optional[int] = None):
     from .arrow import read_parquet_files
     files, schema, _ = snapshot(root, version)

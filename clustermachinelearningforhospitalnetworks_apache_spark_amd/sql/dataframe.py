@@ -664,6 +664,8 @@ class DataFrameNaFunctions:
 # ---------------------------------------------------------------------------------------------- helpers
 
 def _non_null_mask(cd: ColumnData) -> torch.Tensor:
+    if cd.is_host and cd.codes is not None:
+        return torch.as_tensor(np.asarray(cd.codes) >= 0)  # dictionary codes: -1 is null
     if cd.is_host:
         import pandas as pd
         m = cd.valid_mask() & ~pd.isna(cd.values)  # None / NaN test in C, not a Python loop
@@ -696,8 +698,11 @@ def column_to_python(cd: ColumnData) -> List[Any]:
     from ..ml.linalg import DenseVector
     n = len(cd)
     if cd.is_host:
-        vm = cd.valid_mask()
-        return [v if vm[i] else None for i, v in enumerate(cd.values)]
+        if cd.valid is None:
+            return cd.values.tolist() if isinstance(cd.values, np.ndarray) and cd.values.dtype == object \
+                else list(cd.values)
+        vals = np.asarray(cd.values, dtype=object)
+        return np.where(np.asarray(cd.valid, dtype=bool), vals, None).tolist()
     vals = cd.values.detach()
     if vals.dtype in (torch.bfloat16, torch.float8_e4m3fn):
         vals = vals.float()

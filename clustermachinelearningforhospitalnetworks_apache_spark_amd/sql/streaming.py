@@ -570,12 +570,14 @@ class StreamingQuery:
         nrows = (self._wm_source if self._wm_source is not None else df).count()
         w = self._writer
         complete = w._mode == "complete"
+        pending = None
         if self._table is not None:
             from ..io import table as tbl
             root = self._session.catalog._table_path(self._table)
             if tbl.committed_txn(root, self.id) < bid:
-                tbl.write_frame(df, root, "overwrite" if complete else "append", operation="STREAMING UPDATE",
-                                txn={"appId": self.id, "version": bid})
+                # the Parquet write runs in the background while foreachBatch trains on the batch
+                pending = tbl.write_frame_async(df, root, "overwrite" if complete else "append",
+                                                operation="STREAMING UPDATE", txn={"appId": self.id, "version": bid})
         elif self._path is not None or (w._format not in (None, "console", "memory", "delta", "noop")):
             if self._path is None:
                 raise ValueError("file sink needs a path")
@@ -595,8 +597,12 @@ class StreamingQuery:
             name = self.name or "memory_sink"
             prev = None if complete else self._session.catalog._views.get(name)
             self._session.catalog._register_view(name, df if prev is None else prev.union(df), True)
-        if w._foreach_batch is not None:
-            w._foreach_batch(df, bid)
+        try:
+            if w._foreach_batch is not None:
+                w._foreach_batch(df, bid)
+        finally:
+            if pending is not None:
+                pending.finish()
         self._advance_watermark(self._wm_source if self._wm_source is not None else df)
         comm = self._session._comm
         comm.barrier()
