@@ -566,8 +566,9 @@ class StreamingQuery:
         t0 = time.time()
         self._watermark_ms = max(self._watermark_ms, wm_ms)
         self._batch_wm = wm_ms
-        df = self._read_batch(files, ts_ms)
-        nrows = (self._wm_source if self._wm_source is not None else df).count()
+        with trace("stream.read"):
+            df = self._read_batch(files, ts_ms)
+            nrows = (self._wm_source if self._wm_source is not None else df).count()
         w = self._writer
         complete = w._mode == "complete"
         pending = None
@@ -599,10 +600,12 @@ class StreamingQuery:
             self._session.catalog._register_view(name, df if prev is None else prev.union(df), True)
         try:
             if w._foreach_batch is not None:
-                w._foreach_batch(df, bid)
+                with trace("stream.foreachBatch"):
+                    w._foreach_batch(df, bid)
         finally:
             if pending is not None:
-                pending.finish()
+                with trace("stream.sink_commit"):
+                    pending.finish()
         self._advance_watermark(self._wm_source if self._wm_source is not None else df)
         comm = self._session._comm
         comm.barrier()
