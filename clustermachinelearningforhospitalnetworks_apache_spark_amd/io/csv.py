@@ -56,7 +56,8 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
     n = int(starts.shape[0])
     ncols = len(schema.fields)
     codes = np.array([_code(f.dataType) for f in schema.fields], dtype=np.int32)
-    datas = [np.zeros(n * 3 if c == 0 else n, dtype=_np_dtype(c)) for c in codes]
+    # string columns get (offset, length, escaped) triples, read only for valid rows: no zero-fill
+    datas = [np.empty(n * 3, dtype=np.int64) if c == 0 else np.zeros(n, dtype=_np_dtype(c)) for c in codes]
     valids = [np.zeros(max(n, 1), dtype=np.uint8) for _ in codes]
     dptr = (ctypes.c_void_p * ncols)(*[d.ctypes.data for d in datas])
     vptr = (ctypes.c_void_p * ncols)(*[v.ctypes.data for v in valids])
@@ -68,7 +69,7 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
             raise RuntimeError("CSV parse failed")
     out = {}
     for f, c, d, v in zip(schema.fields, codes, datas, valids):
-        valid = v[:n].astype(bool)
+        valid = v[:n].view(bool)  # 0/1 bytes: a zero-copy bool view
         if c == 0:
             enc = _dictionary(lib, buf, d, v, n, quote, nthreads)
             if enc is None:
@@ -79,7 +80,7 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
                 if dicts is not None:
                     dicts[f.name] = enc
         elif c == 5:
-            out[f.name] = (d[:n].astype(bool), valid)
+            out[f.name] = (d[:n].view(bool), valid)
         else:
             out[f.name] = (d[:n], valid)
     return out, n
@@ -254,7 +255,9 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
     out_cols = {}
     n_total = int(sum(a.shape[0] for a in ids)) if ids else 0
     for f in schema.fields:
-        if cols[f.name]:
+        if len(cols[f.name]) == 1:
+            vals, ok = cols[f.name][0], valids[f.name][0]
+        elif cols[f.name]:
             vals = np.concatenate(cols[f.name])
             ok = np.concatenate(valids[f.name])
         else:
@@ -269,7 +272,7 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
 
 def _to_column(vals: np.ndarray, ok: np.ndarray, dt: T.DataType, dev) -> ColumnData:
     if isinstance(dt, (T.StringType, T.BinaryType)) or dt.torch_dtype is None:
-        return ColumnData(vals.astype(object), None if ok.all() else ok, dt)
+        return ColumnData(vals if vals.dtype == object else vals.astype(object), None if ok.all() else ok, dt)
     t = torch.as_tensor(np.ascontiguousarray(vals)).to(device=dev, dtype=dt.torch_dtype)
     valid = None if ok.all() else torch.as_tensor(ok, device=dev)
     return ColumnData(t, valid, dt)
