@@ -21,7 +21,7 @@ _TOKEN = re.compile(r"""
     | (?P<str>'(?:[^']|'')*')
     | (?P<dstr>"(?:[^"]|"")*")
     | (?P<ident>`[^`]+`|[A-Za-z_][A-Za-z_0-9]*(?:\.[A-Za-z_][A-Za-z_0-9]*)*)
-    | (?P<op><=>|<=|>=|<>|!=|==|\|\||[-+*/%(),=<>.])
+    | (?P<op><=>|<=|>=|<>|!=|==|->|\|\||[-+*/%(),=<>.\[\]])
     )""", re.VERBOSE)
 
 _KEYWORDS = {"SELECT", "FROM", "WHERE", "GROUP", "BY", "ORDER", "LIMIT", "AND", "OR", "NOT", "BETWEEN", "IN",
@@ -212,7 +212,47 @@ class Parser:
         if self.at_op("+"):
             self.take()
             return self.unary()
-        return self.primary()
+        return self._postfix(self.primary())
+
+    def _postfix(self, e: Expr) -> Expr:
+        """``e[i]`` (0-based array index / map key) and ``e.field`` (struct field)."""
+        while True:
+            if self.at_op("["):
+                self.take()
+                idx = self.expr()
+                self.expect_op("]")
+                e = Subscript(e, idx)
+            elif self.at_op(".") and self.peek(1) is not None and self.peek(1).kind == "ident":
+                self.take()
+                e = GetField(e, self.take().val)
+            else:
+                return e
+
+    def _try_lambda(self) -> Optional[Expr]:
+        """``x -> body`` or ``(x, y) -> body`` as a higher-order function argument."""
+        t0, t1 = self.peek(), self.peek(1)
+        if t0 is not None and t0.kind == "ident" and t1 is not None and t1.kind == "op" and t1.val == "->":
+            self.take(), self.take()
+            return SqlLambda([t0.val], self.expr())
+        if t0 is not None and t0.kind == "op" and t0.val == "(":
+            k, names = 1, []
+            while True:
+                t = self.peek(k)
+                if t is None or t.kind != "ident":
+                    return None
+                names.append(t.val)
+                t = self.peek(k + 1)
+                if t is not None and t.kind == "op" and t.val == ",":
+                    k += 2
+                    continue
+                if t is not None and t.kind == "op" and t.val == ")":
+                    arrow = self.peek(k + 2)
+                    if arrow is not None and arrow.kind == "op" and arrow.val == "->":
+                        for _ in range(k + 3):
+                            self.take()
+                        return SqlLambda(names, self.expr())
+                return None
+        return None
 
     def primary(self) -> Expr:
         tok = self.take()
@@ -290,10 +330,10 @@ class Parser:
             self.take()
             args = []
         elif not self.at_op(")"):
-            args.append(self.expr())
+            args.append(self._try_lambda() or self.expr())
             while self.at_op(","):
                 self.take()
-                args.append(self.expr())
+                args.append(self._try_lambda() or self.expr())
         self.expect_op(")")
         e = self._call_expr(name, lname, args, distinct)
         if self.at_word("OVER"):
@@ -389,7 +429,8 @@ class Parser:
         if fn is None:
             raise SyntaxError(f"unknown function {name}")
         lit_pos = _LIT_ARGS.get(lname, ())
-        cols = [a.value if (i in lit_pos and isinstance(a, Lit)) else Column(a) for i, a in enumerate(args)]
+        cols = [a.callable() if isinstance(a, SqlLambda) else
+                a.value if (i in lit_pos and isinstance(a, Lit)) else Column(a) for i, a in enumerate(args)]
         if lname == "round" and len(args) == 2:
             return F.round(cols[0], int(args[1].value))._expr
         if lname in ("current_timestamp", "current_date", "now"):
@@ -436,10 +477,112 @@ class QualRef(ColRef):
 
     def eval(self, frame):
         full = f"{self.qual}.{self.col}"
-        return frame._column_data(full if full in frame._cols else self.col)
+        if full in frame._cols or self.col in frame._cols:
+            return frame._column_data(full if full in frame._cols else self.col)
+        head = self.qual.split(".")[0]
+        if head in frame._cols:  # struct column: s.a / s.a.b
+            e: Expr = ColRef(head)
+            for part in self.qual.split(".")[1:] + [self.col]:
+                e = GetField(e, part)
+            return e.eval(frame)
+        return frame._column_data(self.col)
 
     def __str__(self):
         return f"{self.qual}.{self.col}"
+
+
+class GetField(Expr):
+    """``struct_expr.field``."""
+
+    def __init__(self, child: Expr, field: str):
+        self.child, self.field = child, field
+
+    def refs(self):
+        return self.child.refs()
+
+    def name(self):
+        return self.field
+
+    def __str__(self):
+        return f"{self.child}.{self.field}"
+
+    def eval(self, frame):
+        from .builder import column_from_values
+        from .dataframe import column_to_python
+        cd = self.child.eval(frame)
+        st = cd.dtype
+        if not isinstance(st, T.StructType):
+            raise TypeError(f"cannot extract field {self.field!r} from {st.simpleString()}")
+        ft = next((f.dataType for f in st.fields if f.name == self.field), None)
+        if ft is None:
+            raise ValueError(f"no field {self.field!r} in {st.simpleString()}")
+        vals = [None if v is None else (v[self.field] if isinstance(v, dict) else getattr(v, self.field))
+                for v in column_to_python(cd)]
+        return column_from_values(vals, ft, frame._device)
+
+
+class Subscript(Expr):
+    """``array[i]`` (0-based, null when out of range) / ``map[key]``."""
+
+    def __init__(self, child: Expr, index: Expr):
+        self.child, self.index = child, index
+
+    def refs(self):
+        return self.child.refs() + self.index.refs()
+
+    def __str__(self):
+        return f"{self.child}[{self.index}]"
+
+    def eval(self, frame):
+        from .builder import column_from_values
+        from .dataframe import column_to_python
+        cd = self.child.eval(frame)
+        keys = column_to_python(self.index.eval(frame))
+        vals = column_to_python(cd)
+        out = []
+        for v, k in zip(vals, keys):
+            if v is None or k is None:
+                out.append(None)
+            elif isinstance(v, dict):
+                out.append(v.get(k))
+            else:
+                i = int(k)
+                out.append(v[i] if 0 <= i < len(v) else None)
+        dt = cd.dtype.valueType if isinstance(cd.dtype, T.MapType) else (
+            cd.dtype.elementType if isinstance(cd.dtype, T.ArrayType) else T.StringType())
+        return column_from_values(out, dt, frame._device)
+
+
+class SqlLambda(Expr):
+    """``(x, y) -> body`` argument of a SQL higher-order function; becomes a Python callable over
+    Columns whose parameters replace the body's references to x, y."""
+
+    def __init__(self, params: List[str], body: Expr):
+        self.params, self.body = params, body
+
+    def refs(self):
+        return []
+
+    def __str__(self):
+        return f"lambdafunction({self.body}, {', '.join(self.params)})"
+
+    def eval(self, frame):
+        raise ValueError("a lambda is only valid as a higher-order function argument")
+
+    def callable(self):
+        params, body = self.params, self.body
+
+        def bind(*cols):
+            mapping = {p: c._expr for p, c in zip(params, cols)}
+            return Column(_transform(body, lambda e: mapping.get(e.col) if isinstance(e, ColRef) and not isinstance(
+                e, QualRef) and e.col in mapping else None))
+        if len(params) == 1:
+            return lambda a: bind(a)
+        if len(params) == 2:
+            return lambda a, b: bind(a, b)
+        if len(params) == 3:
+            return lambda a, b, c: bind(a, b, c)
+        raise SyntaxError("lambdas take 1 to 3 parameters")
 
 
 class InSubquery(Expr):
@@ -478,6 +621,7 @@ class Source:
     name: Optional[str] = None
     sub: Optional[object] = None  # a query
     alias: Optional[str] = None
+    sample: Optional[tuple] = None  # TABLESAMPLE: ("percent", p) | ("rows", n)
 
 
 @dataclass
@@ -501,6 +645,7 @@ class Select:
     subquery: Optional["Select"] = None
     source: Optional[Source] = None
     joins: List[JoinClause] = field(default_factory=list)
+    grouping_sets: Optional[List[List[Expr]]] = None  # ROLLUP / CUBE / GROUPING SETS
 
 
 @dataclass
@@ -547,6 +692,15 @@ def _source(p: Parser) -> Source:
         src = Source(sub=sub)
     else:
         src = Source(name=p.take().val)
+    if p.at_word("TABLESAMPLE"):
+        p.take()
+        p.expect_op("(")
+        v = float(p.take().val)
+        unit = p.take().val.upper()
+        if unit not in ("PERCENT", "ROWS"):
+            raise SyntaxError("TABLESAMPLE supports (n PERCENT) and (n ROWS)")
+        p.expect_op(")")
+        src.sample = ("percent", v) if unit == "PERCENT" else ("rows", int(v))
     if p.at_kw("AS"):
         p.take()
         src.alias = p.take().val
@@ -626,10 +780,7 @@ def _select(p: Parser) -> Select:
     if p.at_kw("GROUP"):
         p.take()
         p.expect_kw("BY")
-        sel.group_by.append(p.expr())
-        while p.at_op(","):
-            p.take()
-            sel.group_by.append(p.expr())
+        _group_by(p, sel)
     if p.at_kw("HAVING"):
         p.take()
         sel.having = p.expr()
@@ -653,6 +804,63 @@ def _select(p: Parser) -> Select:
         p.take()
         sel.limit = int(p.take().val)
     return sel
+
+
+def _paren_list(p: Parser) -> List[Expr]:
+    p.expect_op("(")
+    out: List[Expr] = []
+    if not p.at_op(")"):
+        out.append(p.expr())
+        while p.at_op(","):
+            p.take()
+            out.append(p.expr())
+    p.expect_op(")")
+    return out
+
+
+def _rollup_sets(keys: List[Expr]) -> List[List[Expr]]:
+    return [keys[:i] for i in range(len(keys), -1, -1)]
+
+
+def _cube_sets(keys: List[Expr]) -> List[List[Expr]]:
+    n = len(keys)
+    return [[k for j, k in enumerate(keys) if not (mask >> (n - 1 - j)) & 1] for mask in range(2 ** n)]
+
+
+def _group_by(p: Parser, sel: Select) -> None:
+    """GROUP BY e, ... | ROLLUP(e, ...) | CUBE(e, ...) | GROUPING SETS ((e, ...), e, ()) | e, ... WITH ROLLUP|CUBE."""
+    nxt = p.peek(1)
+    if p.at_word("ROLLUP", "CUBE") and nxt is not None and nxt.kind == "op" and nxt.val == "(":
+        kind = p.take().val.upper()
+        keys = _paren_list(p)
+        sel.group_by = keys
+        sel.grouping_sets = _rollup_sets(keys) if kind == "ROLLUP" else _cube_sets(keys)
+        return
+    if p.at_word("GROUPING") and nxt is not None and nxt.kind == "ident" and nxt.val.upper() == "SETS":
+        p.take(), p.take()
+        p.expect_op("(")
+        sets: List[List[Expr]] = []
+        while True:
+            sets.append(_paren_list(p) if p.at_op("(") else [p.expr()])
+            if not p.at_op(","):
+                break
+            p.take()
+        p.expect_op(")")
+        keys: List[Expr] = []
+        for st in sets:
+            for k in st:
+                if str(k) not in {str(x) for x in keys}:
+                    keys.append(k)
+        sel.group_by, sel.grouping_sets = keys, sets
+        return
+    sel.group_by.append(p.expr())
+    while p.at_op(","):
+        p.take()
+        sel.group_by.append(p.expr())
+    if p.at_word("WITH") and p.peek(1) is not None and p.peek(1).val.upper() in ("ROLLUP", "CUBE"):
+        p.take()
+        kind = p.take().val.upper()
+        sel.grouping_sets = _rollup_sets(sel.group_by) if kind == "ROLLUP" else _cube_sets(sel.group_by)
 
 
 class _QualStar(Expr):
@@ -849,6 +1057,9 @@ def _run_query(session, q):
 
 def _source_frame(session, src: Source):
     df = _run_query(session, src.sub) if src.sub is not None else session.table(src.name)
+    if src.sample is not None:
+        kind, v = src.sample
+        df = df.sample(fraction=min(max(v / 100.0, 0.0), 1.0), seed=0) if kind == "percent" else df.limit(v)
     return df, (src.alias or src.name)
 
 
@@ -986,15 +1197,29 @@ def _transform(e: Expr, fn) -> Expr:
         return When([(_transform(c, fn), _transform(v, fn)) for c, v in e.branches],
                     _transform(e.other, fn) if e.other is not None else None)
     if isinstance(e, Func):
-        return Func(e.fname, [_transform(a, fn) for a in e.args], e.impl)
+        nf = Func(e.fname, [_transform(a, fn) for a in e.args], e.impl)
+        if hasattr(e, "params"):
+            nf.params = e.params
+        return nf
+    if isinstance(e, GetField):
+        return GetField(_transform(e.child, fn), e.field)
+    if isinstance(e, Subscript):
+        return Subscript(_transform(e.child, fn), _transform(e.index, fn))
     return e
 
 
-def _grouped(df, sel: Select, exprs: List[Expr]):
+def _grouped(df, sel: Select, exprs: List[Expr], null_keys=(), all_keys=None):
     """GROUP BY with arbitrary expressions: aggregates and non-column keys are computed first under
     internal names, then the select items (expressions over keys and aggregates), HAVING and ORDER
-    BY are evaluated on that frame."""
+    BY are evaluated on that frame. For one grouping set of ROLLUP / CUBE / GROUPING SETS,
+    ``null_keys`` are the keys rolled up (null in the output) and ``grouping()`` / ``grouping_id()``
+    resolve against ``all_keys``."""
+    from .functions_extra import GroupingMarker
     from .group import aggregate
+    null_str = {str(k): k for k in null_keys}
+    null_types = {sk: k.eval(df).dtype for sk, k in null_str.items()}
+    all_names = [str(k) for k in (all_keys if all_keys is not None else sel.group_by)]
+    in_set = [str(k) for k in sel.group_by]
     keys, key_names = [], []
     for j, k in enumerate(sel.group_by):
         if isinstance(k, ColRef) and not isinstance(k, QualRef):
@@ -1008,6 +1233,11 @@ def _grouped(df, sel: Select, exprs: List[Expr]):
     aggs: List[Expr] = []
 
     def grab(e):
+        if isinstance(e, GroupingMarker):
+            v, dt = e.value(all_names, in_set)
+            return Cast(Lit(v), dt)
+        if not isinstance(e, (Lit, Alias)) and str(e) in null_str:
+            return Cast(Lit(None), null_types[str(e)])
         if isinstance(e, AggExpr):
             s_ = str(e)
             for i, a in enumerate(aggs):
@@ -1021,6 +1251,9 @@ def _grouped(df, sel: Select, exprs: List[Expr]):
             return ColRef(key_str[e.col])
         return None
     items = [_transform(x, grab) for x in exprs]
+    # unaliased items keep their SQL text as the column name (e.g. "sum(v)"), not the internal one
+    items = [Alias(it, x.name()) if not isinstance(x, Alias) and it.name() != x.name() else it
+             for x, it in zip(exprs, items)]
     having = _transform(sel.having, grab) if sel.having is not None else None
     orders = [SortOrder(_transform(o.expr, grab), o.ascending, o.nulls_first) for o in sel.order_by]
     # ORDER BY an output alias
@@ -1068,7 +1301,17 @@ def _run(session, sel: Select):
         else:
             exprs.append(Alias(e, alias) if alias else e)
     ordered = False
-    if sel.group_by or any(x.is_aggregate() for x in exprs):
+    if sel.grouping_sets is not None:
+        import dataclasses
+        out = None
+        for gs in sel.grouping_sets:
+            in_set = {str(k) for k in gs}
+            sub = dataclasses.replace(sel, group_by=list(gs), grouping_sets=None, order_by=[], limit=None)
+            part, _ = _grouped(df, sub, exprs, null_keys=[k for k in sel.group_by if str(k) not in in_set],
+                               all_keys=sel.group_by)
+            out = part if out is None else out.union(part)
+        df = out
+    elif sel.group_by or any(x.is_aggregate() for x in exprs):
         df, ordered = _grouped(df, sel, exprs)
     else:
         out_names = {x.name() for x in exprs}

@@ -101,3 +101,32 @@ def test_cte_and_statements(spark, db):
     spark.sql("DROP TABLE IF EXISTS stays")
     spark.sql("DROP VIEW north")
     assert not spark.catalog.tableExists("stays") and not spark.catalog.tableExists("north")
+
+
+def test_sql_grouping_sets_lambdas_and_access():
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    spark = SparkSession.builder.appName("sqlx").master("local[1]").getOrCreate()
+    df = spark.createDataFrame([("a", "x", 1, [1, 2, 3]), ("a", "y", 2, [4]), ("b", "x", 3, [])],
+                               "g string, h string, v int, arr array<int>")
+    df.createOrReplaceTempView("gs")
+    q = spark.sql("SELECT g, h, SUM(v) AS s, GROUPING_ID() AS gid FROM gs GROUP BY ROLLUP(g, h)")
+    got = sorted((r.gid, r.g or "", r.h or "", r.s) for r in q.collect())
+    assert got == [(0, "a", "x", 1), (0, "a", "y", 2), (0, "b", "x", 3), (1, "a", "", 3), (1, "b", "", 3),
+                   (3, "", "", 6)]
+    cube = spark.sql("SELECT g, h, COUNT(*) AS n FROM gs GROUP BY CUBE(g, h)").collect()
+    assert len(cube) == 3 + 2 + 2 + 1
+    sets = spark.sql("SELECT g, h, SUM(v) AS s, grouping(h) AS gh FROM gs GROUP BY GROUPING SETS ((g), (h), ())")
+    assert sorted((r.g or "", r.h or "", r.s, r.gh) for r in sets.collect()) == [
+        ("", "", 6, 1), ("", "x", 4, 0), ("", "y", 2, 0), ("a", "", 3, 1), ("b", "", 3, 1)]
+    wr = spark.sql("SELECT g, SUM(v) FROM gs GROUP BY g WITH ROLLUP")
+    assert wr.columns == ["g", "sum(v)"] and sorted((r[0] or "", r[1]) for r in wr.collect()) == [
+        ("", 6), ("a", 3), ("b", 3)]
+    lam = spark.sql("SELECT transform(arr, x -> x + v) AS a, filter(arr, (x, i) -> i > 0) AS f, "
+                    "aggregate(arr, 0, (acc, x) -> acc + x) AS s, exists(arr, x -> x > 3) AS e, "
+                    "arr[0] AS first, named_struct('k', v).k AS k FROM gs").collect()
+    assert [tuple(r) for r in lam] == [([2, 3, 4], [2, 3], 6, False, 1, 1), ([6], [], 4, True, 4, 2),
+                                       ([], [], 0, False, None, 3)]
+    nested = spark.sql("SELECT s.g AS sg, s.v FROM (SELECT struct(g, v) AS s FROM gs)").collect()
+    assert [tuple(r) for r in nested] == [("a", 1), ("a", 2), ("b", 3)]
+    assert spark.sql("SELECT COUNT(*) AS n FROM gs TABLESAMPLE (2 ROWS)").collect()[0].n == 2
+    spark.stop()
