@@ -2,6 +2,7 @@
 from . import functions, types
 from .column import Column
 from .dataframe import DataFrame, DataFrameNaFunctions
+from .dataframe_more import DataFrameWriterV2, Observation
 from .group import GroupedData
 from .session import SparkSession, Session
 from .types import Row

@@ -14,6 +14,9 @@ from typing import Dict, List, Optional
 from ..io import table as tbl
 
 
+_GLOBAL_VIEWS: dict = {}  # global_temp database: shared by the sessions of this process
+
+
 @dataclass
 class Table:
     name: str
@@ -45,7 +48,14 @@ class Catalog:
     def dropTempView(self, name: str) -> bool:
         return self._views.pop(name, None) is not None
 
-    dropGlobalTempView = dropTempView
+    # global temporary views live in the ``global_temp`` database, shared by the sessions of the process
+    def _register_global_view(self, name: str, df, replace: bool) -> None:
+        if not replace and name in _GLOBAL_VIEWS:
+            raise ValueError(f"global temporary view {name!r} already exists")
+        _GLOBAL_VIEWS[name] = df
+
+    def dropGlobalTempView(self, name: str) -> bool:
+        return _GLOBAL_VIEWS.pop(name, None) is not None
 
     # ------------------------------------------------------------------ tables
     def _save_table(self, name: str, df, mode: str) -> None:
@@ -54,6 +64,11 @@ class Catalog:
     def _resolve(self, name: str):
         if name in self._views:
             return self._views[name]
+        if name.startswith("global_temp."):
+            v = _GLOBAL_VIEWS.get(name.split(".", 1)[1])
+            if v is None:
+                raise LookupError(f"Table or view not found: {name}")
+            return v
         path = self._table_path(name)
         if tbl.exists(path):
             return tbl.read_table(self._session, path)

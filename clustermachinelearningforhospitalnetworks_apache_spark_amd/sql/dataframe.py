@@ -587,7 +587,13 @@ class DataFrame(DataFrameMoreMixin):
     def createTempView(self, name: str) -> None:
         self._session.catalog._register_view(name, self, replace=False)
 
-    createOrReplaceGlobalTempView = createOrReplaceTempView
+    registerTempTable = createOrReplaceTempView
+
+    def createGlobalTempView(self, name: str) -> None:
+        self._session.catalog._register_global_view(name, self, replace=False)
+
+    def createOrReplaceGlobalTempView(self, name: str) -> None:
+        self._session.catalog._register_global_view(name, self, replace=True)
 
     @property
     def write(self):

@@ -288,6 +288,130 @@ class DataFrameMoreMixin:
                                    for k, v in r.asDict().items()}, default=str))
         return out
 
+    # ------------------------------------------------------------------------------ reshaping / misc API
+    def unpivot(self, ids, values, variableColumnName: str, valueColumnName: str):
+        """Wide to long: one output row per (input row, value column), ids repeated (values cast to
+        their common type)."""
+        from .builder import column_from_values
+        from .dataframe import column_to_python
+        ids = [ids] if isinstance(ids, str) else list(ids or [])
+        ids = [c if isinstance(c, str) else c._expr.name() for c in ids]
+        values = [c for c in self.columns if c not in ids] if values is None else (
+            [values] if isinstance(values, str) else [c if isinstance(c, str) else c._expr.name() for c in values])
+        if not values:
+            raise ValueError("unpivot needs at least one value column")
+        types = [self.schema[c].dataType for c in values]
+        vt = types[0]
+        for t in types[1:]:
+            if type(t) is not type(vt):
+                if T.is_numeric(t) and T.is_numeric(vt):
+                    vt = T.DoubleType() if not (T.is_integral(t) and T.is_integral(vt)) else T.LongType()
+                else:
+                    vt = T.StringType()
+        n, k = self._nrows, len(values)
+        rep = torch.arange(n, device=self._device).repeat_interleave(k)
+        base = self._take_rows(rep)
+        cols = [column_to_python(self._cols[c]) for c in values]
+        var, val = [], []
+        for i in range(n):
+            for j, c in enumerate(values):
+                var.append(c)
+                v = cols[j][i]
+                val.append(str(v) if (v is not None and isinstance(vt, T.StringType)) else v)
+        names = ids + [variableColumnName, valueColumnName]
+        datas = [base._cols[c] for c in ids] + [column_from_values(var, T.StringType(), self._device),
+                                                column_from_values(val, vt, self._device)]
+        out = base._from_columns(names, datas)
+        counts = self._comm.allgather_object(n * k)
+        off = sum(counts[:self._comm.rank])
+        out._row_ids = torch.arange(off, off + n * k, dtype=torch.int64, device=self._device)
+        return out
+
+    melt = unpivot
+
+    def offset(self, num: int):
+        """Skip the first ``num`` rows (global row order)."""
+        counts = self._comm.allgather_object(self._nrows)
+        start = sum(counts[:self._comm.rank])
+        local_skip = min(max(num - start, 0), self._nrows)
+        return self._take_rows(torch.arange(local_skip, self._nrows, device=self._device))
+
+    def dropDuplicatesWithinWatermark(self, subset=None):
+        return self.dropDuplicates(subset)
+
+    def inputFiles(self) -> List[str]:
+        return list(getattr(self, "_input_files_list", []) or [])
+
+    def isLocal(self) -> bool:
+        return self._comm.world_size == 1
+
+    def repartitionByRange(self, numPartitions, *cols):
+        """Range partitioning: rows sorted by ``cols`` and cut into contiguous rank shards."""
+        if isinstance(numPartitions, (str,)) or hasattr(numPartitions, "_expr"):
+            cols = (numPartitions,) + cols
+        return self.orderBy(*cols) if cols else self.repartition()
+
+    def replace(self, to_replace, value=None, subset=None):
+        return self.na.replace(to_replace, value, subset)
+
+    def sameSemantics(self, other) -> bool:
+        """Same schema and the very same column buffers (frames here are materialised, not plans)."""
+        return (self.schema == other.schema and self._nrows == other._nrows
+                and all(self._cols[n] is other._cols[n] for n in self.columns))
+
+    def semanticHash(self) -> int:
+        return hash((tuple(self.columns), tuple(id(self._cols[n]) for n in self.columns))) & 0x7FFFFFFF
+
+    def to(self, schema):
+        """Reorder / cast columns by name to ``schema`` (missing nullable columns become null)."""
+        from .column import Column, Lit
+        from . import functions as F
+        sch = schema if isinstance(schema, T.StructType) else T.parse_ddl_schema(schema)
+        sel = []
+        for f in sch.fields:
+            if f.name in self.columns:
+                sel.append(F.col(f.name).cast(f.dataType).alias(f.name))
+            elif f.nullable:
+                sel.append(Column(Lit(None)).cast(f.dataType).alias(f.name))
+            else:
+                raise ValueError(f"column {f.name!r} is missing and not nullable")
+        return self.select(*sel)
+
+    def withMetadata(self, columnName: str, metadata: Dict[str, Any]):
+        out = self.select(*self.columns)
+        out.schema[columnName].metadata = dict(metadata)
+        return out
+
+    def observe(self, observation, *exprs):
+        """Compute named metrics over this frame (eagerly: frames are materialised) and hand them to
+        the ``Observation`` (or store them under a name); returns the frame unchanged."""
+        row = self.agg(*exprs).collect()[0]
+        if isinstance(observation, Observation):
+            observation._set(row.asDict())
+        else:
+            self._session._observations = getattr(self._session, "_observations", {})
+            self._session._observations[str(observation)] = row.asDict()
+        return self
+
+    def mapInArrow(self, func, schema):
+        """``func`` maps an iterator of pyarrow RecordBatches (this rank's shard) to RecordBatches."""
+        import pyarrow as pa
+        from ..io.arrow import frame_to_arrow
+        sch = schema if isinstance(schema, T.StructType) else T.parse_ddl_schema(schema)
+        batches = frame_to_arrow(self).to_batches()
+        outs = list(func(iter(batches)))
+        tbl = pa.Table.from_batches(outs) if outs else None
+        pdf = tbl.to_pandas() if tbl is not None else None
+        import pandas as pd
+        return _frame_from_pandas_local(self, sch, pdf if pdf is not None else pd.DataFrame(columns=sch.names))
+
+    def writeTo(self, table: str):
+        return DataFrameWriterV2(self, table)
+
+    def pandas_api(self, index_col=None):
+        """A pandas DataFrame of the whole frame (pandas-on-Spark is not part of this framework)."""
+        return self.toPandas()
+
     def rollup(self, *cols):
         from .group import _as_key_exprs
         keys = _as_key_exprs(cols)
@@ -299,6 +423,103 @@ class DataFrameMoreMixin:
         keys = _as_key_exprs(cols)
         sets = [list(c) for r in range(len(keys), -1, -1) for c in combinations(keys, r)]
         return MultiGroupedData(self, keys, sets)
+
+
+class Observation:
+    """``pyspark.sql.Observation``: metrics collected by ``df.observe(obs, ...)``."""
+
+    def __init__(self, name: Optional[str] = None):
+        self.name = name or "observation"
+        self._vals: Optional[Dict[str, Any]] = None
+
+    def _set(self, vals: Dict[str, Any]) -> None:
+        self._vals = vals
+
+    @property
+    def get(self) -> Dict[str, Any]:
+        if self._vals is None:
+            raise RuntimeError("the observed DataFrame has not been evaluated")
+        return dict(self._vals)
+
+
+class DataFrameWriterV2:
+    """``df.writeTo(table)``: create / replace / createOrReplace / append / overwritePartitions on
+    the catalog's transactional tables."""
+
+    def __init__(self, df, table: str):
+        self.df, self.table = df, table
+        self._using = None
+        self._parts: List[str] = []
+        self._props: Dict[str, str] = {}
+
+    def using(self, provider: str):
+        self._using = provider
+        return self
+
+    def option(self, key, value):
+        return self
+
+    def options(self, **kw):
+        return self
+
+    def tableProperty(self, key, value):
+        self._props[key] = value
+        return self
+
+    def partitionedBy(self, *cols):
+        self._parts = [c if isinstance(c, str) else c._expr.name() for c in cols]
+        return self
+
+    def _exists(self) -> bool:
+        return self.df._session.catalog.tableExists(self.table)
+
+    def create(self) -> None:
+        if self._exists():
+            raise ValueError(f"table {self.table} already exists")
+        self.df._session.catalog._save_table(self.table, self.df, "overwrite")
+
+    def replace(self) -> None:
+        if not self._exists():
+            raise ValueError(f"table {self.table} does not exist")
+        self.df._session.catalog._save_table(self.table, self.df, "overwrite")
+
+    def createOrReplace(self) -> None:
+        self.df._session.catalog._save_table(self.table, self.df, "overwrite")
+
+    def append(self) -> None:
+        if not self._exists():
+            raise ValueError(f"table {self.table} does not exist")
+        self.df._session.catalog._save_table(self.table, self.df, "append")
+
+    def overwrite(self, condition=None) -> None:
+        """Replace the rows matching ``condition`` (all rows when None) with this frame."""
+        cat = self.df._session.catalog
+        if condition is None:
+            cat._save_table(self.table, self.df, "overwrite")
+            return
+        from .column import Column
+        cond = condition if isinstance(condition, Column) else Column(condition)
+        keep = cat._resolve(self.table).filter(~cond)
+        cat._save_table(self.table, keep.unionByName(self.df), "overwrite")
+
+    def overwritePartitions(self) -> None:
+        """Dynamic partition overwrite: replace the partitions (by ``partitionedBy`` columns) present
+        in this frame, keep the others."""
+        cat = self.df._session.catalog
+        if not self._parts or not self._exists():
+            cat._save_table(self.table, self.df, "overwrite")
+            return
+        from .dataframe import column_to_python
+        from . import functions as F
+        new_keys = set()
+        for part in self.df._comm.allgather_object(list(zip(*[column_to_python(self.df._cols[c])
+                                                               for c in self._parts]))):
+            new_keys.update(part)
+        old = cat._resolve(self.table)
+        old_keys = list(zip(*[column_to_python(old._cols[c]) for c in self._parts])) if old._nrows else []
+        mask = torch.as_tensor([k not in new_keys for k in old_keys], dtype=torch.bool, device=old._device)
+        keep = old._mask_rows(mask) if old._nrows else old
+        cat._save_table(self.table, keep.unionByName(self.df), "overwrite")
 
 
 def _frame_from_pandas_local(df, schema: T.StructType, pdf):

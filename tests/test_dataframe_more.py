@@ -79,3 +79,42 @@ def test_pandas_functions(spark):
     assert sorted(r.v for r in m.collect()) == [2.0, 6.0, 10.0]
     assert df.checkpoint() is df and df.hint("broadcast") is df
     assert df.toJSON()[0] == '{"g": "a", "v": 1.0}'
+
+
+def test_dataframe_api_round2b(tmp_path):
+    import pyarrow as pa
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import Observation, SparkSession
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+    spark = SparkSession.builder.appName("api2b").master("local[1]").config(
+        "spark.sql.warehouse.dir", str(tmp_path / "wh")).getOrCreate()
+    df = spark.createDataFrame([(1, 11, 1.1), (2, 12, 1.2), (3, 13, None)], "id int, a int, b double")
+    long = df.unpivot("id", ["a", "b"], "var", "val")
+    assert long.columns == ["id", "var", "val"]
+    assert [tuple(r) for r in long.collect()] == [(1, "a", 11.0), (1, "b", 1.1), (2, "a", 12.0), (2, "b", 1.2),
+                                                  (3, "a", 13.0), (3, "b", None)]
+    assert df.melt(["id"], None, "k", "v").count() == 6
+    assert [r.id for r in df.offset(1).collect()] == [2, 3]
+    obs = Observation("m")
+    assert df.observe(obs, F.count(F.lit(1)).alias("rows"), F.max("a").alias("mx")) is df
+    assert obs.get == {"rows": 3, "mx": 13}
+    t = df.to("b double, id long, c string")
+    assert t.columns == ["b", "id", "c"] and t.schema["id"].dataType.simpleString() == "bigint"
+    assert [r.c for r in t.collect()] == [None] * 3
+    assert df.withMetadata("a", {"comment": "admissions"}).schema["a"].metadata == {"comment": "admissions"}
+    assert df.replace(11, 99, subset=["a"]).collect()[0].a == 99
+    assert df.sameSemantics(df) and not df.sameSemantics(df.select("id"))
+    assert df.isLocal() and df.inputFiles() == []
+    arrow = df.mapInArrow(lambda it: (pa.RecordBatch.from_pydict({"id2": [x * 2 for x in b.column(0).to_pylist()]})
+                                      for b in it), "id2 long")
+    assert [r.id2 for r in arrow.collect()] == [2, 4, 6]
+    df.createOrReplaceGlobalTempView("gv")
+    assert spark.sql("SELECT COUNT(*) AS n FROM global_temp.gv").collect()[0].n == 3
+    assert spark.catalog.dropGlobalTempView("gv")
+    df.writeTo("wt").create()
+    df.filter("id = 1").writeTo("wt").append()
+    assert spark.table("wt").count() == 4
+    df.filter("id = 2").writeTo("wt").overwrite(F.col("id") == 1)
+    assert sorted(r.id for r in spark.table("wt").collect()) == [2, 2, 3]
+    df.writeTo("wt").partitionedBy("id").overwritePartitions()
+    assert sorted(r.id for r in spark.table("wt").collect()) == [1, 2, 3]
+    spark.stop()
