@@ -103,8 +103,147 @@ class Catalog:
     def listDatabases(self):
         return ["default"]
 
-    def cacheTable(self, name: str) -> None:  # data is resident already
-        return None
+    def cacheTable(self, name: str, storageLevel=None) -> None:  # data is resident already
+        self._resolve(name)
 
     def clearCache(self) -> None:
         return None
+
+    def isCached(self, tableName: str) -> bool:
+        """Frames are materialised in device memory, so a resolvable table is always "cached"."""
+        try:
+            self._resolve(tableName)
+            return True
+        except LookupError:
+            return False
+
+    def uncacheTable(self, tableName: str) -> None:
+        return None
+
+    def refreshTable(self, tableName: str) -> None:
+        return None
+
+    def refreshByPath(self, path: str) -> None:
+        return None
+
+    def recoverPartitions(self, tableName: str) -> None:
+        return None
+
+    # ------------------------------------------------------------------ metadata
+    def currentCatalog(self) -> str:
+        return "spark_catalog"
+
+    def setCurrentCatalog(self, catalogName: str) -> None:
+        if catalogName != "spark_catalog":
+            raise ValueError(f"catalog {catalogName!r} not found")
+
+    def listCatalogs(self, pattern: Optional[str] = None):
+        return [CatalogMetadata("spark_catalog", None)]
+
+    def setCurrentDatabase(self, dbName: str) -> None:
+        if dbName != "default":
+            raise ValueError(f"database {dbName!r} not found (only 'default' and 'global_temp' exist)")
+
+    def databaseExists(self, dbName: str) -> bool:
+        return dbName in ("default", "global_temp")
+
+    def getDatabase(self, dbName: str):
+        if not self.databaseExists(dbName):
+            raise LookupError(f"database {dbName!r} not found")
+        return Database(dbName, "spark_catalog", None, self.warehouse if dbName == "default" else None)
+
+    def getTable(self, tableName: str) -> Table:
+        name = tableName.split(".")[-1]
+        if tableName in self._views:
+            return Table(tableName, None, None, "TEMPORARY", True)
+        if tableName.startswith("global_temp.") and name in _GLOBAL_VIEWS:
+            return Table(name, "global_temp", None, "TEMPORARY", True)
+        if tbl.exists(self._table_path(tableName)):
+            return Table(name, "default", None, "MANAGED", False)
+        raise LookupError(f"Table or view not found: {tableName}")
+
+    def listColumns(self, tableName: str, dbName: Optional[str] = None):
+        df = self._resolve(tableName if dbName in (None, "default") else f"{dbName}.{tableName}")
+        return [CatalogColumn(f.name, f.metadata.get("comment") if f.metadata else None, f.dataType.simpleString(),
+                              f.nullable, False, False) for f in df.schema.fields]
+
+    def listFunctions(self, dbName: Optional[str] = None, pattern: Optional[str] = None):
+        import fnmatch
+        from . import functions as F
+        names = sorted({n for n in dir(F) if not n.startswith("_") and callable(getattr(F, n)) and n[0].islower()}
+                       | set(_registered_udfs()))
+        if pattern:
+            names = [n for n in names if fnmatch.fnmatch(n, pattern.replace("*", "*"))]
+        return [Function(n, None, None, None, "TEMPORARY" if n in _registered_udfs() else "BUILTIN",
+                         n in _registered_udfs()) for n in names]
+
+    def functionExists(self, functionName: str, dbName: Optional[str] = None) -> bool:
+        from . import functions as F
+        return functionName in _registered_udfs() or callable(getattr(F, functionName.lower(), None))
+
+    def getFunction(self, functionName: str):
+        if not self.functionExists(functionName):
+            raise LookupError(f"function {functionName!r} not found")
+        tmp = functionName in _registered_udfs()
+        return Function(functionName, None, None, None, "TEMPORARY" if tmp else "BUILTIN", tmp)
+
+    def registerFunction(self, name: str, f, returnType=None):
+        return self._session.udf.register(name, f, returnType)
+
+    def createTable(self, tableName: str, path: Optional[str] = None, source: Optional[str] = None,
+                    schema=None, description: Optional[str] = None, **options):
+        """A managed table (empty, with ``schema``) or, with ``path``, an external table: the files
+        at ``path`` are registered under the name."""
+        if path is not None:
+            df = self._session.read.format(source or "parquet").options(**options).load(path) if schema is None \
+                else self._session.read.format(source or "parquet").schema(schema).options(**options).load(path)
+            self._register_view(tableName, df, replace=False)
+            return df
+        if schema is None:
+            raise ValueError("createTable needs a schema or a path")
+        from .types import StructType, parse_ddl_schema
+        st = schema if isinstance(schema, StructType) else parse_ddl_schema(schema)
+        df = self._session._empty_frame(st)
+        tbl.write_frame(df, self._table_path(tableName), "error", operation="CREATE TABLE")
+        return self._resolve(tableName)
+
+    createExternalTable = createTable
+
+
+@dataclass
+class Database:
+    name: str
+    catalog: Optional[str]
+    description: Optional[str]
+    locationUri: Optional[str]
+
+
+@dataclass
+class CatalogMetadata:
+    name: str
+    description: Optional[str]
+
+
+@dataclass
+class CatalogColumn:
+    name: str
+    description: Optional[str]
+    dataType: str
+    nullable: bool
+    isPartition: bool
+    isBucket: bool
+
+
+@dataclass
+class Function:
+    name: str
+    catalog: Optional[str]
+    namespace: Optional[str]
+    description: Optional[str]
+    className: str
+    isTemporary: bool
+
+
+def _registered_udfs() -> Dict[str, object]:
+    from .functions import REGISTERED_UDFS
+    return REGISTERED_UDFS

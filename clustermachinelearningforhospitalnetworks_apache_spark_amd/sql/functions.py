@@ -382,6 +382,23 @@ class UserDefinedFunction:
         return self
 
 
+REGISTERED_UDFS: dict = {}  # name -> UserDefinedFunction, callable from SQL (spark.udf.register)
+
+
+class UDFRegistration:
+    """``spark.udf``: register Python functions under a SQL name."""
+
+    def register(self, name: str, f, returnType=None):
+        u = f if isinstance(f, UserDefinedFunction) else UserDefinedFunction(f, returnType, name=name)
+        if returnType is not None and isinstance(f, UserDefinedFunction):
+            u = UserDefinedFunction(f.func, returnType, f.vectorized, name=name)
+        REGISTERED_UDFS[name.lower()] = u
+        return u
+
+    def registerJavaFunction(self, name, javaClassName, returnType=None):
+        raise NotImplementedError("JVM functions are not available in this framework")
+
+
 def udf(f=None, returnType=None):
     """``udf(f, returnType)`` or ``@udf(returnType=...)`` / ``@udf``."""
     if f is None or isinstance(f, (str, T.DataType)):

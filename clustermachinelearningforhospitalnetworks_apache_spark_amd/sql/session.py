@@ -123,6 +123,8 @@ class SparkSession:
         self._device = self._comm.device
         self._stopped = False
         self.catalog = Catalog(self)
+        from .functions import UDFRegistration
+        self.udf = UDFRegistration()
         self._streams = None
         self._start_time = time.time()
         self.sparkContext = _Context(self)

@@ -425,7 +425,7 @@ class Parser:
             return getattr(F, lname)(Column(args[0]), off, default)._expr
         if lname == "ntile":
             return F.ntile(int(args[0].value))._expr
-        fn = getattr(F, lname, None)
+        fn = F.REGISTERED_UDFS.get(lname) or getattr(F, lname, None)
         if fn is None:
             raise SyntaxError(f"unknown function {name}")
         lit_pos = _LIT_ARGS.get(lname, ())

@@ -130,3 +130,24 @@ def test_sql_grouping_sets_lambdas_and_access():
     assert [tuple(r) for r in nested] == [("a", 1), ("a", 2), ("b", 3)]
     assert spark.sql("SELECT COUNT(*) AS n FROM gs TABLESAMPLE (2 ROWS)").collect()[0].n == 2
     spark.stop()
+
+
+def test_catalog_metadata_and_sql_udf(tmp_path):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    spark = SparkSession.builder.appName("cat").master("local[1]").config(
+        "spark.sql.warehouse.dir", str(tmp_path / "wh")).getOrCreate()
+    df = spark.createDataFrame([(1, "a"), (2, "b")], "id int, s string")
+    df.createOrReplaceTempView("v")
+    cols = spark.catalog.listColumns("v")
+    assert [(c.name, c.dataType, c.nullable) for c in cols] == [("id", "int", True), ("s", "string", True)]
+    assert spark.catalog.getTable("v").isTemporary and spark.catalog.isCached("v")
+    assert spark.catalog.databaseExists("default") and spark.catalog.currentCatalog() == "spark_catalog"
+    spark.catalog.createTable("empty_t", schema="x double, y string")
+    assert spark.table("empty_t").count() == 0 and spark.table("empty_t").columns == ["x", "y"]
+    assert spark.catalog.functionExists("sqrt") and not spark.catalog.functionExists("nope_fn")
+    spark.udf.register("plus_one", lambda x: x + 1, T.IntegerType())
+    assert spark.catalog.functionExists("plus_one")
+    assert [r.p for r in spark.sql("SELECT plus_one(id) AS p FROM v").collect()] == [2, 3]
+    assert any(f.name == "plus_one" and f.isTemporary for f in spark.catalog.listFunctions())
+    spark.stop()
