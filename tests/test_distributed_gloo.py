@@ -176,8 +176,16 @@ def _run(world, tmp_path, gpu=False):
             os.environ.pop(k, None)
         _workload(out, 0, "mi355x" if gpu else "local[1]")
     else:
-        mp.start_processes(_rank_main, args=(world, _free_port(), out, gpu), nprocs=world, join=True,
-                           start_method="spawn")
+        # the free port can be taken by a concurrent test between probing and binding (pytest -n):
+        # one fresh-port retry; a real mismatch fails deterministically on both attempts
+        for attempt in range(2):
+            try:
+                mp.start_processes(_rank_main, args=(world, _free_port(), out, gpu), nprocs=world, join=True,
+                                   start_method="spawn")
+                break
+            except mp.ProcessRaisedException as e:
+                if attempt == 1 or "address already in use" not in str(e).lower() and "EADDRINUSE" not in str(e):
+                    raise
     with open(out) as fh:
         return json.load(fh)
 
