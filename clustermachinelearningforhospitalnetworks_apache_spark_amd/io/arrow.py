@@ -80,11 +80,15 @@ def column_to_arrow(cd: ColumnData):
     if cd.is_host and cd.codes is not None and isinstance(cd.dtype, T.StringType):
         # dictionary-encoded strings: codes + one object per distinct value, expanded by Arrow in C++
         codes = np.asarray(cd.codes, dtype=np.int32)
-        k = int(codes.max(initial=-1)) + 1
-        first = np.full(k, -1, dtype=np.int64)
-        pos = np.nonzero(codes >= 0)[0]
-        first[codes[pos][::-1]] = pos[::-1]
-        dictionary = pa.array(list(cd.values[first]) if k else [], type=pa.string())
+        dict_vals = getattr(cd, "dictionary", None)
+        if dict_vals is not None:
+            dictionary = pa.array(list(dict_vals[:-1]), type=pa.string())
+        else:
+            k = int(codes.max(initial=-1)) + 1
+            first = np.full(k, -1, dtype=np.int64)
+            pos = np.nonzero(codes >= 0)[0]
+            first[codes[pos][::-1]] = pos[::-1]
+            dictionary = pa.array(list(cd.values[first]) if k else [], type=pa.string())
         idx = pa.array(codes, mask=codes < 0)
         return pa.DictionaryArray.from_arrays(idx, dictionary).cast(pa.string())
     if cd.is_host:

@@ -17,7 +17,7 @@ from .. import _native
 from .._native import c_int, c_ll, c_vp
 from ..sql import types as T
 from ..sql.builder import column_from_values, shard_range
-from ..sql.column import ColumnData
+from ..sql.column import ColumnData, DictColumnData
 
 _native.register_host_sigs({
     "cml_csv_index": (c_ll, [ctypes.c_char_p, c_ll, ctypes.c_char, c_int, c_vp, c_ll]),
@@ -62,7 +62,7 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
     dptr = (ctypes.c_void_p * ncols)(*[d.ctypes.data for d in datas])
     vptr = (ctypes.c_void_p * ncols)(*[v.ctypes.data for v in valids])
     if n:
-        nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+        nthreads = nthreads or host_threads()
         st = lib.cml_csv_parse(buf, len(buf), starts.ctypes.data, n, ncols, sep.encode(), quote.encode(),
                                codes.ctypes.data, dptr, vptr, nthreads)
         if st != 0:
@@ -76,9 +76,11 @@ def parse_csv_bytes(buf: bytes, schema: T.StructType, header: bool, sep: str = "
                 out[f.name] = (_strings(lib, buf, d, v, n, quote), valid)
             else:
                 codes, dictionary = enc
-                out[f.name] = (np.append(dictionary, None)[codes], valid)
+                out[f.name] = (None, valid)  # values are built lazily from the dictionary
                 if dicts is not None:
                     dicts[f.name] = enc
+                else:
+                    out[f.name] = (np.append(dictionary, None)[codes], valid)
         elif c == 5:
             out[f.name] = (d[:n].view(bool), valid)
         else:
@@ -92,13 +94,26 @@ def record_starts(buf: bytes, header: bool, quote: str = '"', nthreads: Optional
     allocation is never paged in."""
     cap = len(buf) // 2 + 2
     starts = np.empty(cap, dtype=np.int64)
-    nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+    nthreads = nthreads or host_threads()
     n = _native.host().cml_csv_index_mt(buf, len(buf), quote.encode(), 1 if header else 0, starts.ctypes.data, cap,
                                          nthreads)
     return starts[:n].copy()
 
 
 _DICT_SAMPLE = 16384
+
+
+def host_threads() -> int:
+    """Worker threads for the native parser: the CPUs this process may run on (cgroup / affinity),
+    bounded by OMP_NUM_THREADS when set and by 16."""
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        n = min(n, int(env))
+    return max(1, min(16, n))
 
 
 def _dict_run(lib, buf, trip, valid_u8, n, quote, nthreads):
@@ -124,7 +139,7 @@ def _dictionary(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int,
     import pyarrow as pa
     if n < 2 * _DICT_SAMPLE:
         return None
-    nthreads = nthreads or min(8, max(1, (os.cpu_count() or 1)))
+    nthreads = nthreads or host_threads()
     _, _, _, k = _dict_run(lib, buf, trip, valid_u8, _DICT_SAMPLE, quote, 1)
     if k > _DICT_SAMPLE // 4:
         return None
@@ -136,7 +151,10 @@ def _dictionary(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int,
 
 
 def merge_dictionaries(parts):
-    """Concatenate per-chunk (codes, dictionary) into one code space (first-appearance order)."""
+    """Concatenate per-chunk (codes, dictionary) into one code space (first-appearance order):
+    (int32 codes, object array of the distinct strings)."""
+    if len(parts) == 1:
+        return parts[0][0], np.asarray(parts[0][1], dtype=object)
     index: Dict[str, int] = {}
     out = []
     for codes, dictionary in parts:
@@ -145,7 +163,10 @@ def merge_dictionaries(parts):
             remap[i] = index.setdefault(v, len(index))
         remap[-1] = -1
         out.append(remap[codes])
-    return np.concatenate(out) if out else np.zeros(0, dtype=np.int32)
+    merged = np.empty(len(index), dtype=object)
+    for v, i in index.items():
+        merged[i] = v
+    return (np.concatenate(out) if out else np.zeros(0, dtype=np.int32)), merged
 
 
 def _strings(lib, buf: bytes, trip: np.ndarray, valid_u8: np.ndarray, n: int, quote: str) -> np.ndarray:
@@ -255,6 +276,15 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
     out_cols = {}
     n_total = int(sum(a.shape[0] for a in ids)) if ids else 0
     for f in schema.fields:
+        if encs[f.name] and all(e is not None for e in encs[f.name]):
+            codes, dictionary = merge_dictionaries(encs[f.name])
+            ok = np.concatenate(valids[f.name]) if len(valids[f.name]) > 1 else valids[f.name][0]
+            out_cols[f.name] = DictColumnData(codes, np.append(dictionary, None), None if ok.all() else ok,
+                                              f.dataType)
+            continue
+        if any(v is None for v in cols[f.name]):  # mixed chunks: materialise the encoded ones
+            cols[f.name] = [np.append(e[1], None)[e[0]] if v is None else v
+                            for v, e in zip(cols[f.name], encs[f.name])]
         if len(cols[f.name]) == 1:
             vals, ok = cols[f.name][0], valids[f.name][0]
         elif cols[f.name]:
@@ -264,8 +294,6 @@ def read_csv_files(session, paths: Sequence[str], schema: Optional[T.StructType]
             vals = np.zeros(0, dtype=object if isinstance(f.dataType, T.StringType) else np.float64)
             ok = np.zeros(0, dtype=bool)
         out_cols[f.name] = _to_column(vals, ok, f.dataType, dev)
-        if encs[f.name] and all(e is not None for e in encs[f.name]):
-            out_cols[f.name].codes = merge_dictionaries(encs[f.name])
     rid = torch.as_tensor(np.concatenate(ids) if ids else np.zeros(0, dtype=np.int64), device=dev)
     return DataFrame(session, schema, out_cols, n_total, rid, dev)
 

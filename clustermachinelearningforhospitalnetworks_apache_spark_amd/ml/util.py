@@ -482,6 +482,11 @@ class MLWriter:
         """Crash-consistent save: the model is written into a sibling temp directory and renamed
         into place, so a failure mid-save never leaves a half-written model and,
         with overwrite, the previous model survives until the new one is complete."""
+        from ..utils.trace import trace
+        with trace("MLWriter.save"):
+            self._save(path)
+
+    def _save(self, path: str) -> None:
         from ..io.reader import strip_scheme
         path = strip_scheme(path).rstrip("/")
         comm = _comm()

@@ -66,6 +66,46 @@ class ColumnData:
         return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype)
 
 
+class DictColumnData(ColumnData):
+    """A dictionary-encoded host string column: int32 ``codes`` (-1 = null) into
+    ``dictionary`` (distinct strings followed by a trailing None). Row subsets gather the codes only;
+    the object array of values is built on first access and cached."""
+
+    def __init__(self, codes, dictionary, valid, dtype):
+        self.codes = np.asarray(codes, dtype=np.int32)
+        self.dictionary = dictionary
+        self.valid = valid
+        self.dtype = dtype
+        self._values = None
+
+    @property
+    def values(self):
+        if self._values is None:
+            self._values = self.dictionary[self.codes]
+        return self._values
+
+    @values.setter
+    def values(self, v):
+        self._values = v
+
+    @property
+    def is_host(self) -> bool:
+        return True
+
+    def __len__(self):
+        return int(self.codes.shape[0])
+
+    def take(self, idx) -> "ColumnData":
+        ii = idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)
+        return DictColumnData(self.codes[ii], self.dictionary, None if self.valid is None else self.valid[ii],
+                              self.dtype)
+
+    def mask(self, m) -> "ColumnData":
+        mm = m.cpu().numpy() if isinstance(m, torch.Tensor) else np.asarray(m, dtype=bool)
+        return DictColumnData(self.codes[mm], self.dictionary, None if self.valid is None else self.valid[mm],
+                              self.dtype)
+
+
 # ------------------------------------------------------------------------------------------------
 # conversion helpers
 # ------------------------------------------------------------------------------------------------

@@ -301,6 +301,11 @@ class DataFrame(DataFrameMoreMixin):
         names = self.columns if subset is None else ([subset] if isinstance(subset, str) else list(subset))
         if not names or self._nrows == 0:
             return self
+        from ..utils.trace import trace
+        with trace("DataFrame.dropna"):
+            return self._dropna(names, how, thresh)
+
+    def _dropna(self, names, how, thresh) -> "DataFrame":
         good = torch.zeros((self._nrows,), dtype=torch.int32, device=self._device)
         for n in names:
             cd = self._cols[n]
