@@ -317,6 +317,8 @@ class DataFrame(DataFrameMoreMixin):
             keep = good > 0
         else:
             keep = good == len(names)
+        if bool(keep.all()):
+            return self  # nothing to drop: no gather, the frame is returned as is
         return self._mask_rows(keep)
 
     def fillna(self, value, subset=None) -> "DataFrame":
