@@ -224,5 +224,5 @@ class KMeansSummary:
 
 from .bisecting import BisectingKMeans, BisectingKMeansModel  # noqa: E402,F401
 from .gmm import GaussianMixture, GaussianMixtureModel, GaussianMixtureSummary  # noqa: E402,F401
-from .lda import LDA, LocalLDAModel  # noqa: E402,F401
+from .lda import LDA, DistributedLDAModel, LocalLDAModel  # noqa: E402,F401
 from .pic import PowerIterationClustering  # noqa: E402,F401

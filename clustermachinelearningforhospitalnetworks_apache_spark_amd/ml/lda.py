@@ -116,9 +116,11 @@ class LDA(Estimator):
         return int(self.getOrDefault("seed")) if self.isSet("seed") else _default_seed(U.jvm_class(self))
 
     def _fit(self, df):
-        if self.getOptimizer().lower() != "online":
-            raise ValueError("LDA: only optimizer='online' is provided (the EM optimizer's DistributedLDAModel "
-                             "graph is not part of this framework)")
+        opt = self.getOptimizer().lower()
+        if opt == "em":
+            return self._fit_em(df)
+        if opt != "online":
+            raise ValueError(f"LDA: optimizer must be 'online' or 'em', got {opt!r}")
         k = self.getK()
         if k < 2:
             raise ValueError("LDA: k must be > 1")
@@ -163,6 +165,59 @@ class LDA(Estimator):
             if self.getOptimizeDocConcentration():
                 alpha = _update_alpha(alpha, logphat / nb, nb, rho)
         model = LocalLDAModel(lam.T.cpu().numpy(), alpha.cpu().numpy(), eta, V)
+        self._copyValues(model)
+        model._gamma_seed = seed
+        return model
+
+    def _fit_em(self, df):
+        """Spark's EMLDAOptimizer (MAP EM on the document-term graph) in dense form: with
+        A = N_doc + (alpha - 1) and B = (N_term + (eta - 1)) / (N_k + V (eta - 1)), the token
+        responsibilities are A_jk B_wk / (A B^T)_jw, so one EM iteration is two GEMMs,
+        N_doc <- A * ((X / A B^T) B) and N_term <- B * ((X / A B^T)^T A), the latter all-reduced.
+        Initial counts come from a uniform random soft assignment per (document, term) token."""
+        k = self.getK()
+        if k < 2:
+            raise ValueError("LDA: k must be > 1")
+        comm = df._comm
+        X = df._feature_matrix(self.getFeaturesCol()).to(torch.float64)
+        n, V = X.shape
+        dev = X.device
+        seed = self._seed()
+        a = self.getOrDefault("docConcentration") if self.isSet("docConcentration") else None
+        if a is None:
+            alpha = 50.0 / k + 1.0
+        else:
+            av = [float(v) for v in (a if isinstance(a, (list, tuple, np.ndarray)) else [a])]
+            if len(set(av)) != 1:
+                raise ValueError("LDA(optimizer='em') needs a symmetric docConcentration")
+            alpha = av[0] if av[0] >= 0 else 50.0 / k + 1.0
+        eta = self.getOrDefault("topicConcentration") if self.isSet("topicConcentration") else None
+        eta = 1.1 if eta is None or eta < 0 else float(eta)
+        if alpha <= 1.0 or eta <= 1.0:
+            raise ValueError("LDA(optimizer='em') needs docConcentration > 1 and topicConcentration > 1")
+        # random soft assignment per token: gamma_jw ~ normalised uniform(k), one per (doc, term) pair
+        nz = torch.nonzero(X > 0)
+        ndoc = torch.zeros((n, k), dtype=torch.float64, device=dev)
+        nterm = torch.zeros((V, k), dtype=torch.float64, device=dev)
+        if nz.numel():
+            rows, cols = nz[:, 0], nz[:, 1]
+            key_ids = df._row_ids[rows] * V + cols
+            g = torch.stack([R.uniform(key_ids, seed, 500 + t) for t in range(k)], 1)
+            g = g / g.sum(1, keepdim=True) * X[rows, cols][:, None]
+            ndoc.index_add_(0, rows, g)
+            nterm.index_add_(0, cols, g)
+        comm.allreduce_(nterm)
+        for _ in range(self.getMaxIter()):
+            nk = nterm.sum(0)
+            A = ndoc + (alpha - 1.0)
+            B = (nterm + (eta - 1.0)) / (nk + V * (eta - 1.0))[None, :]
+            Z = A @ B.T
+            Q = torch.where(X > 0, X / Z, torch.zeros_like(X))
+            ndoc = A * (Q @ B)
+            nterm = B * (Q.T @ A)
+            comm.allreduce_(nterm)
+        model = DistributedLDAModel(nterm.cpu().numpy(), np.full(k, alpha), eta, V)
+        model._train_stats = _em_training_stats(X, ndoc, nterm, alpha, eta, comm)
         self._copyValues(model)
         model._gamma_seed = seed
         return model
@@ -305,4 +360,68 @@ class LocalLDAModel(Model):
         return m
 
 
-__all__: List[str] = ["LDA", "LocalLDAModel", "dirichlet_expectation", "e_step"]
+def _em_training_stats(X, ndoc, nterm, alpha: float, eta: float, comm):
+    """(trainingLogLikelihood, logPrior) of an EM fit, as Spark's DistributedLDAModel defines them."""
+    k = ndoc.shape[1]
+    V = nterm.shape[0]
+    nk = nterm.sum(0)
+    phi = (nterm + (eta - 1.0)) / (nk + V * (eta - 1.0))[None, :]            # [V, k]
+    nj = ndoc.sum(1, keepdim=True)
+    theta = (ndoc + (alpha - 1.0)) / (nj + k * (alpha - 1.0))                 # [n, k]
+    p = theta @ phi.T                                                          # [n, V]
+    ll = torch.where(X > 0, X * torch.log(p.clamp(min=1e-300)), torch.zeros_like(X)).sum()
+    doc_prior = ((alpha - 1.0) * torch.log(theta.clamp(min=1e-300))).sum()
+    msg = torch.stack([ll, doc_prior]).clone()
+    comm.allreduce_(msg)
+    term_prior = ((eta - 1.0) * torch.log(phi.clamp(min=1e-300))).sum()
+    return float(msg[0]), float(msg[1] + term_prior)
+
+
+class DistributedLDAModel(LocalLDAModel):
+    """The EM optimizer's model: term-topic counts N_wk as ``topicsMatrix`` plus the training
+    statistics; inference on new documents uses the same variational E-step as ``toLocal()``."""
+
+    def __init__(self, topics=None, alpha=None, eta: float = 0.0, vocab_size: int = 0):
+        super().__init__(topics, alpha, eta, vocab_size)
+        self._train_stats = (float("nan"), float("nan"))
+
+    def isDistributed(self) -> bool:
+        return True
+
+    def toLocal(self) -> LocalLDAModel:
+        m = LocalLDAModel(self._topics, self._alpha, self._eta, self._V)
+        self._copyValues(m)
+        m._gamma_seed = self._gamma_seed
+        return m
+
+    @property
+    def trainingLogLikelihood(self) -> float:
+        return self._train_stats[0]
+
+    def logPrior(self) -> float:
+        return self._train_stats[1]
+
+    def getCheckpointFiles(self) -> List[str]:
+        return []
+
+    def deleteCheckpointFiles(self) -> None:
+        return None
+
+    def _save_impl(self, path):
+        import pyarrow as pa
+        super()._save_impl(path)
+        U.write_parquet(path, "training", pa.table({"trainingLogLikelihood": [self._train_stats[0]],
+                                                    "logPrior": [self._train_stats[1]]}))
+
+    @classmethod
+    def _load_impl(cls, path, md):
+        m = super()._load_impl(path, md)
+        try:
+            r = U.read_parquet(path, "training").to_pylist()[0]
+            m._train_stats = (r["trainingLogLikelihood"], r["logPrior"])
+        except (OSError, FileNotFoundError, IndexError):
+            pass
+        return m
+
+
+__all__: List[str] = ["LDA", "LocalLDAModel", "DistributedLDAModel", "dirichlet_expectation", "e_step"]

@@ -97,6 +97,7 @@ _JVM = {
     "Word2VecModel": "org.apache.spark.ml.feature.Word2VecModel",
     "LDA": "org.apache.spark.ml.clustering.LDA",
     "LocalLDAModel": "org.apache.spark.ml.clustering.LocalLDAModel",
+    "DistributedLDAModel": "org.apache.spark.ml.clustering.DistributedLDAModel",
     "PowerIterationClustering": "org.apache.spark.ml.clustering.PowerIterationClustering",
     "VarianceThresholdSelector": "org.apache.spark.ml.feature.VarianceThresholdSelector",
     "VarianceThresholdSelectorModel": "org.apache.spark.ml.feature.VarianceThresholdSelectorModel",
@@ -185,6 +186,7 @@ _PY = {
     "Word2VecModel": "feature",
     "LDA": "clustering",
     "LocalLDAModel": "clustering",
+    "DistributedLDAModel": "clustering",
     "PowerIterationClustering": "clustering",
     "VarianceThresholdSelector": "feature",
     "VarianceThresholdSelectorModel": "feature",

@@ -112,10 +112,66 @@ def test_lda_recovers_planted_topics(spark, tmp_path):
     np.testing.assert_allclose(td2, td, rtol=1e-12)
 
 
-def test_lda_rejects_em(spark):
+def test_lda_rejects_bad_optimizer(spark):
     df, _, _ = _corpus(spark, n_docs=12)
     with pytest.raises(ValueError):
-        LDA(k=2, optimizer="em").fit(df)
+        LDA(k=2, optimizer="gibbs").fit(df)
+    with pytest.raises(ValueError):
+        LDA(k=2, optimizer="em", docConcentration=[0.5]).fit(df)
+
+
+def _spark_em_iteration(X, ndoc, nterm, alpha, eta):
+    """One EMLDAOptimizer iteration written per edge (computePTopic), in numpy."""
+    V, k = nterm.shape
+    nk = nterm.sum(0)
+    nd, nt = np.zeros_like(ndoc), np.zeros_like(nterm)
+    for j, w in zip(*np.nonzero(X)):
+        g = (nterm[w] + eta - 1) * (ndoc[j] + alpha - 1) / (nk + V * (eta - 1))
+        g = g / g.sum() * X[j, w]
+        nd[j] += g
+        nt[w] += g
+    return nd, nt
+
+
+def test_em_dense_update_matches_edge_loop():
+    rs = np.random.RandomState(1)
+    n, V, k, alpha, eta = 9, 7, 3, 50.0 / 3 + 1, 1.1
+    X = rs.poisson(1.0, size=(n, V)).astype(float)
+    ndoc = rs.rand(n, k) * 3
+    nterm = rs.rand(V, k) * 3
+    A = ndoc + alpha - 1
+    B = (nterm + eta - 1) / (nterm.sum(0) + V * (eta - 1))
+    Q = np.where(X > 0, X / (A @ B.T), 0.0)
+    nd_ref, nt_ref = _spark_em_iteration(X, ndoc, nterm, alpha, eta)
+    np.testing.assert_allclose(A * (Q @ B), nd_ref, rtol=1e-12)
+    np.testing.assert_allclose(B * (Q.T @ A), nt_ref, rtol=1e-12)
+
+
+def test_lda_em_distributed_model(spark, tmp_path):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import DistributedLDAModel
+    df, topic, V = _corpus(spark)
+    m = LDA(k=3, maxIter=30, seed=4, optimizer="em").fit(df)
+    assert isinstance(m, DistributedLDAModel) and m.isDistributed()
+    tops = m.describeTopics(8).collect()
+    assert sorted({min(r.termIndices) // 8 for r in tops}) == [0, 1, 2]
+    for r in tops:
+        assert len({i // 8 for i in r.termIndices}) == 1
+    # counts: every token is assigned once
+    assert m.topicsMatrix().toArray().sum() == pytest.approx(240 * 40, rel=1e-9)
+    few = LDA(k=3, maxIter=2, seed=4, optimizer="em").fit(df)
+    assert m.trainingLogLikelihood + m.logPrior() >= few.trainingLogLikelihood + few.logPrior()
+    loc = m.toLocal()
+    assert not loc.isDistributed()
+    td = np.stack([v.toArray() for v in loc.transform(df).toPandas()["topicDistribution"]])
+    lab = td.argmax(1)
+    for t in range(3):
+        vals, cnt = np.unique(lab[topic == t], return_counts=True)
+        assert cnt.max() / cnt.sum() > 0.95
+    p = str(tmp_path / "em")
+    m.save(p)
+    m2 = DistributedLDAModel.load(p)
+    np.testing.assert_array_equal(m2.topicsMatrix().toArray(), m.topicsMatrix().toArray())
+    assert m2.trainingLogLikelihood == m.trainingLogLikelihood
 
 
 def _two_cliques(spark, weak=0.01):
