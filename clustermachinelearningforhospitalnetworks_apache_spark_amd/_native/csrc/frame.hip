@@ -20,6 +20,8 @@
 // CDF thresholds are computed on the host once), so CPU and GPU runs make identical decisions.
 #include "common.h"
 
+#include <type_traits>
+
 namespace {
 
 constexpr int kThreads = 256;
@@ -203,6 +205,58 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmCol* __rest
   }
 }
 
+// Scalar-columns fast path (every column width 1, at most 16 of them, row width ldo <= 16): the
+// column table is staged in LDS once per block, each thread builds its whole output row in registers
+// (the per-column loads of a wave are coalesced) and writes it with 16-byte stores.
+constexpr int kAsmMax = 16;
+
+template <int OUT>
+__global__ __launch_bounds__(kThreads) void assemble_scalar_kernel(const AsmCol* __restrict__ cols, int ncols,
+                                                                   long long n, void* __restrict__ out, long long ldo,
+                                                                   unsigned char* __restrict__ invalid, int nan_keep) {
+  __shared__ AsmCol sc[kAsmMax];
+  if (threadIdx.x < ncols) sc[threadIdx.x] = cols[threadIdx.x];
+  __syncthreads();
+  using OT = typename std::conditional<OUT == 0, double, typename std::conditional<OUT == 1, float, u16>::type>::type;
+  constexpr int PER16 = 16 / (int)sizeof(OT);
+  const bool vec = (ldo % PER16) == 0 && (reinterpret_cast<size_t>(out) & 15) == 0;
+  for (long long r = (long long)blockIdx.x * kThreads + threadIdx.x; r < n; r += (long long)gridDim.x * kThreads) {
+    OT row[kAsmMax];
+    bool bad = false;
+#pragma unroll
+    for (int c = 0; c < kAsmMax; ++c) {
+      if (c < ncols) {
+        const AsmCol& col = sc[c];
+        const bool ok = col.valid == nullptr || col.valid[r] != 0;
+        double v = ok ? load_as_f64(col.ptr, col.type, r) : __builtin_nan("");
+        bad |= !ok || v != v;
+        if (!nan_keep && v != v) v = 0.0;
+        if constexpr (OUT == 0) row[c] = v;
+        else if constexpr (OUT == 1) row[c] = (float)v;
+        else row[c] = f64_to_bf16(v);
+      } else {
+        row[c] = (OT)0;
+      }
+    }
+    OT* o = reinterpret_cast<OT*>(out) + r * ldo;
+    if (vec) {
+#pragma unroll
+      for (int q = 0; q < kAsmMax / PER16; ++q) {
+        if (q * PER16 < ldo) {
+          uint4 w;
+          __builtin_memcpy(&w, &row[q * PER16], 16);
+          *reinterpret_cast<uint4*>(o + q * PER16) = w;
+        }
+      }
+    } else {
+#pragma unroll
+      for (int c = 0; c < kAsmMax; ++c)
+        if (c < ldo) o[c] = row[c];
+    }
+    if (invalid != nullptr) invalid[r] = bad ? 1 : 0;
+  }
+}
+
 // --------------------------------------------------------------------------------------------- K6
 __global__ __launch_bounds__(kThreads) void binarize_kernel(const void* __restrict__ x, int type, long long n,
                                                             double thr, double* __restrict__ out) {
@@ -277,6 +331,80 @@ __global__ __launch_bounds__(kThreads) void col_absmax_kernel(const T* __restric
     float m = 0.f;
     for (long long r = r0; r < r1; ++r) m = fmaxf(m, fabsf(ld_f32<T>(x, r * ldx + j)));
     partial[(long long)blockIdx.x * d + j] = m;
+  }
+}
+
+// 16-byte fast path: a row is cpr = d / E chunks of E = 16 / sizeof(T) values; thread t of the block
+// takes chunk t % cpr of rows t / cpr + k * (kThreads / cpr) (1 KiB per wave instruction), keeps E
+// running maxima and the block folds its row groups through LDS at the end.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void col_absmax16_kernel(const T* __restrict__ x, long long n, int d,
+                                                                long long ldx, int rows_per_block,
+                                                                float* __restrict__ partial) {
+  constexpr int E = 16 / (int)sizeof(T);
+  __shared__ float sh[2048];  // (kThreads / cpr) x d floats = 8 KiB
+  const int cpr = d / E;
+  const int rpi = kThreads / cpr;
+  const int t = threadIdx.x, ch = t % cpr, rg = t / cpr;
+  const long long r0 = (long long)blockIdx.x * rows_per_block;
+  const long long r1 = r0 + rows_per_block < n ? r0 + rows_per_block : n;
+  float m[E];
+#pragma unroll
+  for (int e = 0; e < E; ++e) m[e] = 0.f;
+  if (rg < rpi) {
+    for (long long r = r0 + rg; r < r1; r += rpi) {
+      const uint4 w = *reinterpret_cast<const uint4*>(x + r * ldx + ch * E);
+      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int e = 0; e < E; ++e) {
+        float v;
+        if constexpr (sizeof(T) == 2) v = bf16_to_f32((u16)((ws[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+        else v = __uint_as_float(ws[e]);
+        m[e] = fmaxf(m[e], fabsf(v));
+      }
+    }
+#pragma unroll
+    for (int e = 0; e < E; ++e) sh[rg * d + ch * E + e] = m[e];
+  }
+  __syncthreads();
+  for (int j = t; j < d; j += kThreads) {
+    float v = 0.f;
+    for (int q = 0; q < rpi; ++q) v = fmaxf(v, sh[q * d + j]);
+    partial[(long long)blockIdx.x * d + j] = v;
+  }
+}
+
+// 8 values per thread -> one 8-byte store of e4m3fn bytes (rows of d = ldo values, d % 8 == 0,
+// cpr = d / 8 a power of two: row and chunk by shift / mask, no 64-bit division per element).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void quant_fp8_v8_kernel(const T* __restrict__ x, long long n, int d,
+                                                                long long ldx, const float* __restrict__ scale,
+                                                                unsigned char* __restrict__ out, int cpr_shift) {
+  const long long total = n << cpr_shift;
+  const long long cmask = (1LL << cpr_shift) - 1;
+  for (long long t = (long long)blockIdx.x * kThreads + threadIdx.x; t < total; t += (long long)gridDim.x * kThreads) {
+    const long long r = t >> cpr_shift;
+    const int j = (int)(t & cmask) * 8;
+    float v[8];
+    if constexpr (sizeof(T) == 2) {
+      const uint4 w = *reinterpret_cast<const uint4*>(x + r * ldx + j);
+      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = bf16_to_f32((u16)((ws[e >> 1] >> (16 * (e & 1))) & 0xffffu));
+    } else {
+      const float4 a = *reinterpret_cast<const float4*>(x + r * ldx + j);
+      const float4 b = *reinterpret_cast<const float4*>(x + r * ldx + j + 4);
+      v[0] = a.x; v[1] = a.y; v[2] = a.z; v[3] = a.w; v[4] = b.x; v[5] = b.y; v[6] = b.z; v[7] = b.w;
+    }
+    const float4 s0 = *reinterpret_cast<const float4*>(scale + j);
+    const float4 s1 = *reinterpret_cast<const float4*>(scale + j + 4);
+    const float sc[8] = {s0.x, s0.y, s0.z, s0.w, s1.x, s1.y, s1.z, s1.w};
+    unsigned lo = 0, hi = 0;
+    lo = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[0] * sc[0], v[1] * sc[1], (int)lo, false);
+    lo = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[2] * sc[2], v[3] * sc[3], (int)lo, true);
+    hi = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[4] * sc[4], v[5] * sc[5], (int)hi, false);
+    hi = (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v[6] * sc[6], v[7] * sc[7], (int)hi, true);
+    *reinterpret_cast<uint2*>(out + r * (long long)d + j) = make_uint2(lo, hi);
   }
 }
 
@@ -397,10 +525,19 @@ CML_API int cml_compact(const unsigned char* mask, long long n, long long* idx, 
 
 // cols: device array of AsmCol (see struct layout: ptr, valid, ld, type, width, out_off, pad).
 CML_API int cml_assemble(const void* cols, int ncols, long long n, void* out, int out_dtype, long long ldo, int dout,
-                         unsigned char* invalid, int nan_keep, void* stream) {
+                         unsigned char* invalid, int nan_keep, int scalar_only, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const AsmCol* c = (const AsmCol*)cols;
   if (n <= 0) return 0;
+  if (scalar_only && ncols <= kAsmMax && ldo <= kAsmMax) {
+    switch (out_dtype) {
+      case 0: hipLaunchKernelGGL(assemble_scalar_kernel<0>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
+      case 1: hipLaunchKernelGGL(assemble_scalar_kernel<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
+      case 2: hipLaunchKernelGGL(assemble_scalar_kernel<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
+      default: return (int)hipErrorInvalidValue;
+    }
+    return cml_status();
+  }
   switch (out_dtype) {
     case 0: hipLaunchKernelGGL(assemble_kernel<0>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
     case 1: hipLaunchKernelGGL(assemble_kernel<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
@@ -440,6 +577,18 @@ CML_API int cml_col_absmax(const void* x, int dtype, long long n, int d, long lo
   const long long nb = (n + rows_per_block - 1) / rows_per_block;
   if (nb <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int E = dtype == 0 ? 8 : 4;
+  const bool fast = (dtype == 0 || dtype == 1) && d % E == 0 && ldx % E == 0 && d / E <= kThreads && d <= 2048 &&
+                    (reinterpret_cast<size_t>(x) & 15) == 0;
+  if (fast) {
+    if (dtype == 1)
+      hipLaunchKernelGGL(col_absmax16_kernel<float>, dim3((unsigned)nb), dim3(kThreads), 0, st, (const float*)x, n, d,
+                         ldx, rows_per_block, partial);
+    else
+      hipLaunchKernelGGL(col_absmax16_kernel<u16>, dim3((unsigned)nb), dim3(kThreads), 0, st, (const u16*)x, n, d,
+                         ldx, rows_per_block, partial);
+    return cml_status();
+  }
   if (dtype == 1)
     hipLaunchKernelGGL(col_absmax_kernel<float>, dim3((unsigned)nb), dim3(kThreads), 0, st, (const float*)x, n, d,
                        ldx, rows_per_block, partial);
@@ -455,6 +604,22 @@ CML_API int cml_quant_fp8(const void* x, int dtype, long long n, int d, long lon
                           unsigned char* out, long long ldo, void* stream) {
   if (n <= 0) return 0;
   hipStream_t st = (hipStream_t)stream;
+  const int cpr = d / 8;
+  const bool pow2 = cpr > 0 && (cpr & (cpr - 1)) == 0;
+  const int align = dtype == 0 ? 8 : 4;
+  if (ldo == d && d % 8 == 0 && pow2 && ldx % align == 0 && (reinterpret_cast<size_t>(x) & 15) == 0 &&
+      (reinterpret_cast<size_t>(scale) & 15) == 0 && (reinterpret_cast<size_t>(out) & 7) == 0 &&
+      (dtype == 0 || dtype == 1)) {
+    const int sh = __builtin_ctz((unsigned)cpr);
+    const long long chunks = n * cpr;
+    if (dtype == 1)
+      hipLaunchKernelGGL(quant_fp8_v8_kernel<float>, dim3(grid_for(chunks)), dim3(kThreads), 0, st, (const float*)x,
+                         n, d, ldx, scale, out, sh);
+    else
+      hipLaunchKernelGGL(quant_fp8_v8_kernel<u16>, dim3(grid_for(chunks)), dim3(kThreads), 0, st, (const u16*)x, n,
+                         d, ldx, scale, out, sh);
+    return cml_status();
+  }
   const long long total = n * ((ldo + 1) / 2);
   if (dtype == 1)
     hipLaunchKernelGGL(quant_fp8_kernel<float>, dim3(grid_for(total)), dim3(kThreads), 0, st, (const float*)x, n, d,

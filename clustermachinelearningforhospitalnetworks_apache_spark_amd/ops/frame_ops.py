@@ -24,7 +24,7 @@ _native.register_kernel_sigs({
     "cml_counter_uniform": (c_int, [c_vp, c_ll, c_ull, c_vp, c_vp]),
     "cml_compact_blocks": (c_ll, [c_ll]),
     "cml_compact": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
-    "cml_assemble": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_ll, c_int, c_vp, c_int, c_vp]),
+    "cml_assemble": (c_int, [c_vp, c_int, c_ll, c_vp, c_int, c_ll, c_int, c_vp, c_int, c_int, c_vp]),
     "cml_assemble_col_bytes": (c_int, []),
     "cml_binarize": (c_int, [c_vp, c_int, c_ll, c_double, c_vp, c_vp]),
     "cml_metric_grid": (c_int, [c_ll]),
@@ -164,8 +164,9 @@ def assemble(parts: List[Tuple[torch.Tensor, Optional[torch.Tensor]]], out_dtype
     cols = torch.from_numpy(rec.view(np.uint8).copy()).to(dev)
     out = torch.empty((n, ld), dtype=out_dtype, device=dev)
     invalid = torch.empty(n, dtype=torch.uint8, device=dev)
+    scalar_only = int(all(int(r["width"]) == 1 for r in rec))
     _native.check(lib.cml_assemble(cols.data_ptr(), len(parts), n, out.data_ptr(), _OUT_TYPES[out_dtype], ld, d,
-                                   invalid.data_ptr(), int(keep_nan), _st(stream)), "assemble")
+                                   invalid.data_ptr(), int(keep_nan), scalar_only, _st(stream)), "assemble")
     del keep  # stream-ordered: any reuse of these blocks by the caching allocator runs after the launch
     return out, invalid.view(torch.bool)
 

@@ -135,3 +135,49 @@ def test_has_nan(dtype):
     xp[7777, 39] = 0
     xp[5, 50] = float("nan")  # beyond d: ignored
     assert not F.has_nan(xp.cuda(), 40)
+
+
+@pytest.mark.parametrize("out_dtype", [torch.float64, torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("ld", [0, 8, 7])
+def test_assemble_scalar_fast_path(out_dtype, ld):
+    """Scalar-only columns take the register-row / 16-byte-store kernel; padded and odd row widths too."""
+    n = 20_011
+    g = torch.Generator().manual_seed(3)
+    cols = [torch.randint(-100, 100, (n,), generator=g, dtype=torch.int32),
+            torch.randn(n, generator=g, dtype=torch.float64),
+            torch.randn(n, generator=g).to(torch.float32),
+            torch.randint(0, 2, (n,), generator=g).to(torch.bool),
+            torch.randint(-5, 5, (n,), generator=g, dtype=torch.int64)]
+    cols[1][::89] = float("nan")
+    valid = [None, None, torch.rand(n, generator=g) > 0.05, None, torch.rand(n, generator=g) > 0.02]
+    got, gbad = F.assemble([(v.cuda(), None if m is None else m.cuda()) for v, m in zip(cols, valid)],
+                           out_dtype=out_dtype, ld=ld)
+    want = torch.stack([c.double() for c in cols], 1)
+    bad = torch.zeros(n, dtype=torch.bool)
+    for j, m in enumerate(valid):
+        if m is not None:
+            want[~m, j] = float("nan")
+    bad |= torch.isnan(want).any(1)
+    assert torch.equal(gbad.cpu(), bad)
+    width = max(ld, 5)
+    assert got.shape == (n, width)
+    g64 = got.double().cpu()
+    np.testing.assert_array_equal(np.isnan(g64[:, :5].numpy()), np.isnan(want.numpy()))
+    ok = ~torch.isnan(want)
+    assert torch.equal(g64[:, :5][ok], want.to(out_dtype).double()[ok]) or out_dtype == torch.bfloat16
+    if width > 5:
+        assert (g64[:, 5:] == 0).all()
+
+
+@pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
+@pytest.mark.parametrize("d", [128, 256])
+def test_fp8_quantisation_vector_paths(src, d):
+    n = 9_001
+    g = torch.Generator().manual_seed(11)
+    x = (torch.randn(n, d, generator=g) * torch.logspace(-2, 2, d)).to(src)
+    amax = F.col_absmax(x.cuda(), d).cpu()
+    np.testing.assert_array_equal(amax.numpy(), x.float().abs().amax(0).numpy())
+    scale = 448.0 / amax.clamp(min=1e-12)
+    q = F.quant_fp8(x.cuda(), d, scale).cpu()
+    want = (x.float() * scale).clamp(-448, 448).to(torch.float8_e4m3fn)
+    assert torch.equal(q.view(torch.uint8), want.view(torch.uint8))
