@@ -210,50 +210,72 @@ __global__ __launch_bounds__(kThreads) void assemble_kernel(const AsmCol* __rest
 // (the per-column loads of a wave are coalesced) and writes it with 16-byte stores.
 constexpr int kAsmMax = 16;
 
-template <int OUT>
+template <int OUT, int MAXC>
 __global__ __launch_bounds__(kThreads) void assemble_scalar_kernel(const AsmCol* __restrict__ cols, int ncols,
                                                                    long long n, void* __restrict__ out, long long ldo,
                                                                    unsigned char* __restrict__ invalid, int nan_keep) {
-  __shared__ AsmCol sc[kAsmMax];
+  // RPT rows per thread per pass (rows r, r + 256, ...): their loads are all issued before the first
+  // store, so a wave keeps RPT x ncols loads in flight (Little's law at ~2 us HBM latency).
+  constexpr int RPT = 4;
+  __shared__ AsmCol sc[MAXC];
   if (threadIdx.x < ncols) sc[threadIdx.x] = cols[threadIdx.x];
   __syncthreads();
   using OT = typename std::conditional<OUT == 0, double, typename std::conditional<OUT == 1, float, u16>::type>::type;
   constexpr int PER16 = 16 / (int)sizeof(OT);
   const bool vec = (ldo % PER16) == 0 && (reinterpret_cast<size_t>(out) & 15) == 0;
-  for (long long r = (long long)blockIdx.x * kThreads + threadIdx.x; r < n; r += (long long)gridDim.x * kThreads) {
-    OT row[kAsmMax];
-    bool bad = false;
+  const long long step = (long long)gridDim.x * kThreads * RPT;
+  for (long long r0 = (long long)blockIdx.x * kThreads * RPT + threadIdx.x; r0 < n; r0 += step) {
+    double v[RPT][MAXC];
+    bool bad[RPT];
 #pragma unroll
-    for (int c = 0; c < kAsmMax; ++c) {
+    for (int q = 0; q < RPT; ++q) bad[q] = false;
+#pragma unroll
+    for (int c = 0; c < MAXC; ++c) {
       if (c < ncols) {
         const AsmCol& col = sc[c];
-        const bool ok = col.valid == nullptr || col.valid[r] != 0;
-        double v = ok ? load_as_f64(col.ptr, col.type, r) : __builtin_nan("");
-        bad |= !ok || v != v;
-        if (!nan_keep && v != v) v = 0.0;
-        if constexpr (OUT == 0) row[c] = v;
-        else if constexpr (OUT == 1) row[c] = (float)v;
-        else row[c] = f64_to_bf16(v);
-      } else {
-        row[c] = (OT)0;
-      }
-    }
-    OT* o = reinterpret_cast<OT*>(out) + r * ldo;
-    if (vec) {
 #pragma unroll
-      for (int q = 0; q < kAsmMax / PER16; ++q) {
-        if (q * PER16 < ldo) {
-          uint4 w;
-          __builtin_memcpy(&w, &row[q * PER16], 16);
-          *reinterpret_cast<uint4*>(o + q * PER16) = w;
+        for (int q = 0; q < RPT; ++q) {
+          const long long r = r0 + (long long)q * kThreads;
+          const bool inr = r < n;
+          const bool ok = col.valid == nullptr || (inr && col.valid[r] != 0);
+          double x = (ok && inr) ? load_as_f64(col.ptr, col.type, r) : __builtin_nan("");
+          bad[q] |= !ok || x != x;
+          if (!nan_keep && x != x) x = 0.0;
+          v[q][c] = x;
         }
-      }
-    } else {
+      } else {
 #pragma unroll
-      for (int c = 0; c < kAsmMax; ++c)
-        if (c < ldo) o[c] = row[c];
+        for (int q = 0; q < RPT; ++q) v[q][c] = 0.0;
+      }
     }
-    if (invalid != nullptr) invalid[r] = bad ? 1 : 0;
+#pragma unroll
+    for (int q = 0; q < RPT; ++q) {
+      const long long r = r0 + (long long)q * kThreads;
+      if (r >= n) break;
+      OT row[MAXC];
+#pragma unroll
+      for (int c = 0; c < MAXC; ++c) {
+        if constexpr (OUT == 0) row[c] = v[q][c];
+        else if constexpr (OUT == 1) row[c] = (float)v[q][c];
+        else row[c] = f64_to_bf16(v[q][c]);
+      }
+      OT* o = reinterpret_cast<OT*>(out) + r * ldo;
+      if (vec) {
+#pragma unroll
+        for (int k = 0; k < MAXC / PER16; ++k) {
+          if (k * PER16 < ldo) {
+            uint4 w;
+            __builtin_memcpy(&w, &row[k * PER16], 16);
+            *reinterpret_cast<uint4*>(o + k * PER16) = w;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int c = 0; c < MAXC; ++c)
+          if (c < ldo) o[c] = row[c];
+      }
+      if (invalid != nullptr) invalid[r] = bad[q] ? 1 : 0;
+    }
   }
 }
 
@@ -523,6 +545,22 @@ CML_API int cml_compact(const unsigned char* mask, long long n, long long* idx, 
   return cml_status();
 }
 
+// the smallest row capacity (4, 8 or 16 values) that holds both the columns and the output width
+template <int OUT>
+int launch_asm_scalar(const AsmCol* c, int ncols, long long n, void* out, long long ldo, unsigned char* invalid,
+                      int nan_keep, hipStream_t st) {
+  const long long need = ncols > ldo ? ncols : ldo;
+  const dim3 grid(grid_for(n, 4LL * kThreads)), block(kThreads);
+  if (need <= 4)
+    hipLaunchKernelGGL((assemble_scalar_kernel<OUT, 4>), grid, block, 0, st, c, ncols, n, out, ldo, invalid, nan_keep);
+  else if (need <= 8)
+    hipLaunchKernelGGL((assemble_scalar_kernel<OUT, 8>), grid, block, 0, st, c, ncols, n, out, ldo, invalid, nan_keep);
+  else
+    hipLaunchKernelGGL((assemble_scalar_kernel<OUT, 16>), grid, block, 0, st, c, ncols, n, out, ldo, invalid,
+                       nan_keep);
+  return cml_status();
+}
+
 // cols: device array of AsmCol (see struct layout: ptr, valid, ld, type, width, out_off, pad).
 CML_API int cml_assemble(const void* cols, int ncols, long long n, void* out, int out_dtype, long long ldo, int dout,
                          unsigned char* invalid, int nan_keep, int scalar_only, void* stream) {
@@ -531,12 +569,11 @@ CML_API int cml_assemble(const void* cols, int ncols, long long n, void* out, in
   if (n <= 0) return 0;
   if (scalar_only && ncols <= kAsmMax && ldo <= kAsmMax) {
     switch (out_dtype) {
-      case 0: hipLaunchKernelGGL(assemble_scalar_kernel<0>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
-      case 1: hipLaunchKernelGGL(assemble_scalar_kernel<1>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
-      case 2: hipLaunchKernelGGL(assemble_scalar_kernel<2>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, invalid, nan_keep); break;
+      case 0: return launch_asm_scalar<0>(c, ncols, n, out, ldo, invalid, nan_keep, st);
+      case 1: return launch_asm_scalar<1>(c, ncols, n, out, ldo, invalid, nan_keep, st);
+      case 2: return launch_asm_scalar<2>(c, ncols, n, out, ldo, invalid, nan_keep, st);
       default: return (int)hipErrorInvalidValue;
     }
-    return cml_status();
   }
   switch (out_dtype) {
     case 0: hipLaunchKernelGGL(assemble_kernel<0>, dim3(grid_for(n)), dim3(kThreads), 0, st, c, ncols, n, out, ldo, dout, invalid, nan_keep); break;
