@@ -104,13 +104,29 @@ __device__ __forceinline__ int block_exclusive_scan(int v, int* sh, int& total) 
   return wbase + incl - v;
 }
 
+// 16 mask bytes of the thread's 16 consecutive rows as a bit set (one 16-byte load when the tile is
+// whole and aligned, byte loads for the tail)
+__device__ __forceinline__ unsigned mask_bits16(const unsigned char* __restrict__ mask, long long base, long long n) {
+  unsigned bits = 0;
+  if (base + kCompactItems <= n && (reinterpret_cast<size_t>(mask + base) & 15) == 0) {
+    const uint4 w = *reinterpret_cast<const uint4*>(mask + base);
+    const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+    for (int q = 0; q < 4; ++q)
+#pragma unroll
+      for (int b = 0; b < 4; ++b) bits |= ((ws[q] >> (8 * b)) & 0xffu) ? (1u << (4 * q + b)) : 0u;
+  } else {
+#pragma unroll
+    for (int j = 0; j < kCompactItems; ++j) bits |= (base + j < n && mask[base + j]) ? (1u << j) : 0u;
+  }
+  return bits;
+}
+
 __global__ __launch_bounds__(kThreads) void compact_count_kernel(const unsigned char* __restrict__ mask, long long n,
                                                                  long long* __restrict__ bcount) {
   __shared__ int sh[kThreads / 64];
   const long long base = (long long)blockIdx.x * kCompactTile + (long long)threadIdx.x * kCompactItems;
-  int c = 0;
-#pragma unroll
-  for (int j = 0; j < kCompactItems; ++j) c += (base + j < n && mask[base + j]) ? 1 : 0;
+  const int c = __popc(mask_bits16(mask, base, n));
   int total;
   block_exclusive_scan(c, sh, total);
   if (threadIdx.x == 0) bcount[blockIdx.x] = total;
@@ -132,19 +148,24 @@ __global__ __launch_bounds__(kThreads) void compact_scan_kernel(long long* __res
   if (threadIdx.x == 0) *count_out = carry;
 }
 
+// The tile's kept indices are placed in LDS at their scanned positions, then copied out by the whole
+// block with consecutive 8-byte stores (coalesced) instead of per-thread runs.
 __global__ __launch_bounds__(kThreads) void compact_scatter_kernel(const unsigned char* __restrict__ mask, long long n,
                                                                    const long long* __restrict__ boff,
                                                                    long long* __restrict__ idx) {
   __shared__ int sh[kThreads / 64];
-  const long long base = (long long)blockIdx.x * kCompactTile + (long long)threadIdx.x * kCompactItems;
-  unsigned bits = 0;
-#pragma unroll
-  for (int j = 0; j < kCompactItems; ++j) bits |= (base + j < n && mask[base + j]) ? (1u << j) : 0u;
+  __shared__ long long buf[kCompactTile];
+  const long long tile0 = (long long)blockIdx.x * kCompactTile;
+  const long long base = tile0 + (long long)threadIdx.x * kCompactItems;
+  const unsigned bits = mask_bits16(mask, base, n);
   int total;
-  long long pos = boff[blockIdx.x] + block_exclusive_scan(__popc(bits), sh, total);
+  int pos = block_exclusive_scan(__popc(bits), sh, total);
 #pragma unroll
   for (int j = 0; j < kCompactItems; ++j)
-    if (bits & (1u << j)) idx[pos++] = base + j;
+    if (bits & (1u << j)) buf[pos++] = base + j;
+  __syncthreads();
+  const long long o = boff[blockIdx.x];
+  for (int i = threadIdx.x; i < total; i += kThreads) idx[o + i] = buf[i];
 }
 
 // --------------------------------------------------------------------------------------------- K2
