@@ -623,3 +623,4 @@ def from_unixtime(c: ColumnOrName, fmt: str = "yyyy-MM-dd HH:mm:ss") -> Column:
 
 from .functions_more import *  # noqa: E402,F401,F403  (statistical aggregates, math/date/string, arrays, explode)
 from .functions_extra import *  # noqa: E402,F401,F403  (null helpers, hashes, time zones, collections, lambdas, JSON)
+from .functions_tail import *  # noqa: E402,F401,F403  (regr_* / string_agg / bit aggregates, try_*, regex, url, date aliases)

@@ -239,6 +239,8 @@ class _ValuesAgg(_DevAgg):
     statistics, Spark's ``percentile``), mode (most frequent, ties -> smallest), sum_distinct."""
 
     def __init__(self, fn, children, arg=None, label=None):
+        if label is None and arg is not None:  # distinct names for different percentages
+            label = f"{fn}({', '.join(str(c) for c in children)}, {arg})"
         super().__init__(fn, children, label)
         self.arg = arg
         if fn == "percentile" and isinstance(arg, (list, tuple)):
