@@ -13,7 +13,7 @@ from dataclasses import dataclass, field
 from typing import List, Optional, Tuple
 
 from . import types as T
-from .column import AggExpr, Alias, BinOp, Cast, ColRef, Column, Expr, Lit, SortOrder, Unary, When
+from .column import AggExpr, Alias, BinOp, Cast, ColRef, Column, ColumnData, Expr, Lit, SortOrder, Unary, When
 
 _TOKEN = re.compile(r"""
     \s*(?:
@@ -179,9 +179,13 @@ class Parser:
                     isnot = True
                 self.expect_kw("NULL")
                 e = Unary("isnotnull" if isnot else "isnull", e)
+            elif self.at_op("<=>"):  # null-safe equality
+                self.take()
+                from .functions_tail import equal_null
+                e = equal_null(Column(e), Column(self.additive()))._expr
             elif self.at_op("=", "==", "!=", "<>", "<", "<=", ">", ">=", "<=>"):
                 op = self.take().val
-                op = {"=": "==", "<>": "!=", "<=>": "=="}.get(op, op)
+                op = {"=": "==", "<>": "!="}.get(op, op)
                 e = BinOp(op, e, self.additive())
             else:
                 return e
@@ -194,9 +198,33 @@ class Parser:
             if op == "||":
                 from .functions import concat
                 e = concat(Column(e), Column(rhs))._expr
+            elif isinstance(rhs, IntervalLit):
+                e = rhs.add_to(e, -1 if op == "-" else 1)
             else:
                 e = BinOp(op, e, rhs)
         return e
+
+    def interval(self) -> "IntervalLit":
+        """INTERVAL n unit [n unit ...] / INTERVAL 'n' unit (units: year, month, week, day, hour, minute,
+        second, millisecond, microsecond; plural forms accepted)."""
+        months, micros = 0, 0
+        while self.peek() is not None and self.peek().kind in ("num", "str") or self.at_op("-"):
+            neg = False
+            if self.at_op("-"):
+                self.take()
+                neg = True
+            v = float(self.take().val)
+            unit = self.take().val.upper().rstrip("S")
+            v = -v if neg else v
+            if unit in ("YEAR", "MONTH"):
+                months += int(v) * (12 if unit == "YEAR" else 1)
+            else:
+                scale = {"WEEK": 7 * 86400e6, "DAY": 86400e6, "HOUR": 3600e6, "MINUTE": 60e6, "SECOND": 1e6,
+                         "MILLISECOND": 1e3, "MICROSECOND": 1.0}.get(unit)
+                if scale is None:
+                    raise SyntaxError(f"unsupported interval unit {unit}")
+                micros += int(round(v * scale))
+        return IntervalLit(months, micros)
 
     def mult(self):
         e = self.unary()
@@ -276,6 +304,8 @@ class Parser:
                 return Cast(Lit(self.take().val), T.TimestampType() if tok.val == "TIMESTAMP" else T.DateType())
             if tok.val == "CASE":
                 return self.case()
+            if tok.val == "INTERVAL":
+                return self.interval()
             if tok.val == "CAST":
                 self.expect_op("(")
                 e = self.expr()
@@ -321,6 +351,9 @@ class Parser:
         from . import functions as F
         self.expect_op("(")
         lname = name.lower()
+        special = self._special_call(lname)
+        if special is not None:
+            return special
         distinct = False
         if self.at_kw("DISTINCT"):
             self.take()
@@ -341,6 +374,75 @@ class Parser:
             from .window import WindowExpr
             e = WindowExpr(e, self.window_spec())
         return e
+
+    def _special_call(self, lname: str) -> Optional[Expr]:
+        """SQL-standard argument syntax: EXTRACT(f FROM e), POSITION(a IN b), TRIM([BOTH|LEADING|TRAILING]
+        [chars] FROM s), SUBSTRING(s FROM p [FOR n]). Returns None (nothing consumed) otherwise."""
+        from . import functions as F
+        if lname in ("extract", "date_part") and self.peek(1) is not None and self.peek(1).kind == "kw" \
+                and self.peek(1).val == "FROM":
+            field_ = self.take().val
+            self.expect_kw("FROM")
+            src = self.expr()
+            self.expect_op(")")
+            return F.date_part(field_, Column(src))._expr
+        if lname == "position":
+            sub = self.additive()
+            if not self.at_kw("IN"):
+                args = [sub]
+                while self.at_op(","):
+                    self.take()
+                    args.append(self.expr())
+                self.expect_op(")")
+                start = int(args[2].value) if len(args) > 2 else 1
+                return F.locate(args[0].value, Column(args[1]), start)._expr
+            self.take()
+            src = self.expr()
+            self.expect_op(")")
+            return F.locate(sub.value if isinstance(sub, Lit) else str(sub), Column(src))._expr
+        if lname == "trim" and (self.at_word("BOTH", "LEADING", "TRAILING") or self._trim_from_ahead()):
+            mode = self.take().val.upper() if self.at_word("BOTH", "LEADING", "TRAILING") else "BOTH"
+            chars = None
+            if not self.at_kw("FROM"):
+                chars = self.additive()
+            self.expect_kw("FROM")
+            src = self.expr()
+            self.expect_op(")")
+            cs = " " if chars is None else (chars.value if isinstance(chars, Lit) else str(chars))
+            fn = {"BOTH": str.strip, "LEADING": str.lstrip, "TRAILING": str.rstrip}[mode]
+            return F._host_map(f"trim_{mode.lower()}", [Column(src)], lambda v: fn(str(v), cs), T.StringType(),
+                               params=[cs])._expr
+        if lname in ("substring", "substr"):
+            save = self.i
+            first = self.expr()
+            if self.at_kw("FROM"):
+                self.take()
+                pos = self.expr()
+                ln = None
+                if self.at_word("FOR"):
+                    self.take()
+                    ln = self.expr()
+                self.expect_op(")")
+                return F.substring(Column(first), int(pos.value), int(ln.value) if ln is not None else 2 ** 31 - 1)._expr
+            self.i = save
+        return None
+
+    def _trim_from_ahead(self) -> bool:
+        """TRIM('x' FROM s) / TRIM(FROM s): a FROM keyword inside the parentheses."""
+        depth, k = 0, 0
+        while True:
+            t = self.peek(k)
+            if t is None:
+                return False
+            if t.kind == "op" and t.val == "(":
+                depth += 1
+            elif t.kind == "op" and t.val == ")":
+                if depth == 0:
+                    return False
+                depth -= 1
+            elif t.kind == "kw" and t.val == "FROM" and depth == 0:
+                return True
+            k += 1
 
     def window_spec(self):
         """OVER ( [PARTITION BY e, ...] [ORDER BY e [ASC|DESC] [NULLS FIRST|LAST], ...]
@@ -489,6 +591,57 @@ class QualRef(ColRef):
 
     def __str__(self):
         return f"{self.qual}.{self.col}"
+
+
+class IntervalLit(Expr):
+    """An INTERVAL literal: months + microseconds, added to dates / timestamps by ``+`` / ``-``."""
+
+    def __init__(self, months: int, micros: int):
+        self.months, self.micros = months, micros
+
+    def refs(self):
+        return []
+
+    def __str__(self):
+        return f"INTERVAL {self.months} MONTHS {self.micros} MICROSECONDS"
+
+    def eval(self, frame):
+        raise ValueError("an INTERVAL is only valid added to or subtracted from a date / timestamp")
+
+    def add_to(self, e: Expr, sign: int) -> Expr:
+        months, micros = sign * self.months, sign * self.micros
+        from .column import Func
+
+        def impl(frame, args):
+            import torch
+            a = args[0]
+            if months:
+                from .functions_more import _add_months
+                from .column import micros_to_datetime, ts_to_micros
+                from .dataframe import column_to_python
+                from .builder import column_from_values
+                import datetime as _dt
+                vals = []
+                for v in column_to_python(a):
+                    if v is None:
+                        vals.append(None)
+                        continue
+                    t = v if isinstance(v, _dt.datetime) else _dt.datetime.combine(v, _dt.time())
+                    d = _add_months(t.date(), months)
+                    vals.append(_dt.datetime.combine(d, t.time()) + _dt.timedelta(microseconds=micros))
+                out = column_from_values(vals, T.TimestampType(), frame._device)
+                if isinstance(a.dtype, T.DateType) and micros % 86_400_000_000 == 0:
+                    out = ColumnData(torch.div(out.values, 86_400_000_000, rounding_mode="floor").to(torch.int32),
+                                     out.valid, T.DateType())
+                return out
+            if isinstance(a.dtype, T.DateType):
+                if micros % 86_400_000_000 == 0:
+                    return ColumnData(a.values + micros // 86_400_000_000, a.valid, T.DateType())
+                return ColumnData(a.values.to(torch.int64) * 86_400_000_000 + micros, a.valid, T.TimestampType())
+            if isinstance(a.dtype, T.TimestampType):
+                return ColumnData(a.values + micros, a.valid, T.TimestampType())
+            raise TypeError(f"cannot add an INTERVAL to {a.dtype.simpleString()}")
+        return Func(f"({e} {'+' if sign > 0 else '-'} INTERVAL)", [e], impl)
 
 
 class GetField(Expr):

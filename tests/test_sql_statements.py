@@ -151,3 +151,19 @@ def test_catalog_metadata_and_sql_udf(tmp_path):
     assert [r.p for r in spark.sql("SELECT plus_one(id) AS p FROM v").collect()] == [2, 3]
     assert any(f.name == "plus_one" and f.isTemporary for f in spark.catalog.listFunctions())
     spark.stop()
+
+
+def test_sql_standard_forms_and_intervals():
+    import datetime as dt
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    spark = SparkSession.builder.appName("sqlf").master("local[1]").getOrCreate()
+    spark.createDataFrame([(dt.datetime(2024, 1, 31, 3, 4, 5), "  ab  ", dt.date(2024, 1, 31), None)],
+                          "t timestamp, s string, d date, n int").createOrReplaceTempView("sf")
+    r = spark.sql("SELECT EXTRACT(YEAR FROM t) AS y, t + INTERVAL 1 DAY 2 HOURS AS t2, t - INTERVAL '2' HOUR AS t3, "
+                  "d + INTERVAL 1 MONTH AS d2, d - INTERVAL 3 DAYS AS d3, POSITION('b' IN s) AS p, "
+                  "TRIM(BOTH ' ' FROM s) AS z1, TRIM(LEADING FROM s) AS z2, SUBSTRING(s FROM 3 FOR 2) AS z3, "
+                  "n <=> NULL AS ns, regr_count(1.0, 2.0) AS rc FROM sf").collect()[0]
+    assert r.y == 2024 and r.t2 == dt.datetime(2024, 2, 1, 5, 4, 5) and r.t3 == dt.datetime(2024, 1, 31, 1, 4, 5)
+    assert r.d2 == dt.date(2024, 2, 29) and r.d3 == dt.date(2024, 1, 28) and r.p == 4
+    assert (r.z1, r.z2, r.z3) == ("ab", "ab  ", "ab") and r.ns is True and r.rc == 1
+    spark.stop()
