@@ -32,6 +32,7 @@ import torch
 from . import types as T
 from .column import AggExpr, ColRef, Column, ColumnData, Expr, SortOrder, _expr
 
+DEVICE_WINDOWS = True  # window_fast.device_window first; tests flip this to compare with the host path
 _UNB_PREC = -sys.maxsize - 1
 _UNB_FOLL = sys.maxsize
 
@@ -143,6 +144,11 @@ class WindowExpr(Expr):
     def eval(self, frame) -> ColumnData:
         from .builder import column_from_values
         from .dataframe import column_to_python
+        if DEVICE_WINDOWS:
+            from .window_fast import device_window
+            fast = device_window(frame, self.func, self.spec)
+            if fast is not None:
+                return fast
         comm = frame._comm
         child = self.func.child
         pk = [column_to_python(e.eval(frame)) for e in self.spec._partition]
