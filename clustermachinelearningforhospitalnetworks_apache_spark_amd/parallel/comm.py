@@ -144,6 +144,24 @@ class Communicator:
         parts = self.allgather(t)
         return parts[0] if len(parts) == 1 else torch.cat(parts, 0)
 
+    def alltoallv(self, t: torch.Tensor, send_counts: List[int]) -> torch.Tensor:
+        """Variable all-to-all along dim 0: rows ``t[sum(send_counts[:r]) : ... + send_counts[r]]`` go
+        to rank r; the result is what every rank sent here, in source-rank order (one
+        ``all_to_all_single`` for the counts, one for the payload — the shuffle of sort / repartition)."""
+        if not self.is_distributed:
+            return t
+        sc = torch.tensor([int(c) for c in send_counts], dtype=torch.int64, device=t.device)
+        rc = torch.empty_like(sc)
+        dist.all_to_all_single(self._coerce(rc), sc, group=self.group)
+        recv = [int(x) for x in rc.tolist()]
+        src = t.contiguous()
+        is_bool = src.dtype == torch.bool
+        if is_bool:
+            src = src.view(torch.uint8)
+        out = torch.empty((sum(recv),) + tuple(src.shape[1:]), dtype=src.dtype, device=src.device)
+        dist.all_to_all_single(self._coerce(out), src, recv, [int(c) for c in send_counts], group=self.group)
+        return out.view(torch.bool) if is_bool else out
+
     def sum_scalar(self, v: float, dtype=torch.float64) -> float:
         if not self.is_distributed:
             return v

@@ -400,6 +400,10 @@ class _Neg:
 
 
 def sort_frame(df: DataFrame, orders: List[SortOrder]) -> DataFrame:
+    from .relational_fast import device_sort
+    out = device_sort(df, orders)
+    if out is not None:
+        return out
     names, rows, ids = df._gather_host()
     keyvals = []
     for o in orders:
@@ -414,6 +418,10 @@ def sort_frame(df: DataFrame, orders: List[SortOrder]) -> DataFrame:
 
 
 def drop_duplicates(df: DataFrame, subset: Optional[Sequence[str]]) -> DataFrame:
+    from .relational_fast import device_dedup
+    out = device_dedup(df, subset)
+    if out is not None:
+        return out
     names, rows, ids = df._gather_host()
     cols = list(range(len(names))) if subset is None else [names.index(c) for c in subset]
     seen = set()
@@ -476,12 +484,14 @@ def describe(df: DataFrame, cols: List[str]) -> DataFrame:
 
 
 def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
-    """Broadcast hash join: the right side is gathered to every rank (reference-scale tables)."""
+    """Equi-join on column names. Device path: relational_fast (joint key codes, sorted right side,
+    searchsorted match ranges); the row loop below (broadcast hash join, right side gathered to
+    every rank) handles keys without device codes. Null keys never match (Spark equality).
+    Right non-key columns whose names clash with left ones get an ``_r`` suffix."""
     how = how.lower().replace("_", "")
-    how = {"leftouter": "left", "rightouter": "right", "fullouter": "full", "outer": "full"}.get(how, how)
-    rnames, rrows, _ = right._gather_host()
+    how = {"leftouter": "left", "rightouter": "right", "fullouter": "full", "outer": "full",
+           "semi": "leftsemi", "anti": "leftanti"}.get(how, how)
     lnames = left.columns
-    lcols = left._local_rows_host()
     if on is None:
         keys = []
     elif isinstance(on, str):
@@ -490,24 +500,36 @@ def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
         keys = list(on)
     else:
         raise NotImplementedError("join supports column-name keys")
+    if not keys and how != "cross":
+        how = "cross"
+    r_extra = [n for n in right.columns if n not in keys]
+    semi = how in ("leftanti", "leftsemi")
+    out_names = lnames if semi else lnames + [n + "_r" if n in lnames else n for n in r_extra]
+    fields = [T.StructField(n, left.schema[n].dataType) for n in lnames]
+    if not semi:
+        fields += [T.StructField(o, right.schema[n].dataType) for o, n in zip(out_names[len(lnames):], r_extra)]
+    schema = T.StructType(fields)
+    from .relational_fast import device_join
+    out = device_join(left, right, keys, how, out_names, schema)
+    if out is not None:
+        return out
+    rnames, rrows, _ = right._gather_host()
+    lcols = left._local_rows_host()
     index: Dict[tuple, List[int]] = {}
     for j, r in enumerate(rrows):
-        index.setdefault(tuple(r[rnames.index(k)] for k in keys), []).append(j)
-    r_extra = [n for n in rnames if n not in keys]
-    out_names = lnames + [n for n in r_extra if n not in lnames] + [n + "_r" for n in r_extra if n in lnames]
+        key = tuple(_hashable(r[rnames.index(k)]) for k in keys)
+        if any(v is None for v in key):
+            continue
+        index.setdefault(key, []).append(j)
     r_out_idx = [rnames.index(n) for n in r_extra]
     out_rows = []
     matched_right = set()
     for i in range(left._nrows):
         lrow = [lcols[n][i] for n in lnames]
-        key = tuple(lcols[k][i] for k in keys)
+        key = tuple(_hashable(lcols[k][i]) for k in keys)
         hits = list(range(len(rrows))) if how == "cross" else index.get(key, [])
-        if how == "leftanti":
-            if not hits:
-                out_rows.append(lrow)
-            continue
-        if how == "leftsemi":
-            if hits:
+        if semi:
+            if bool(hits) == (how == "leftsemi"):
                 out_rows.append(lrow)
             continue
         if hits:
@@ -516,25 +538,16 @@ def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
                 out_rows.append(lrow + [rrows[j][t] for t in r_out_idx])
         elif how in ("left", "full"):
             out_rows.append(lrow + [None] * len(r_out_idx))
-    if how in ("leftanti", "leftsemi"):
-        out_names = lnames
     if how in ("right", "full"):
         allm = left._comm.allgather_object(sorted(matched_right))
         m = set()
         for a in allm:
             m |= set(a)
-        if left._comm.rank == 0:
+        if left._comm.rank == left._comm.world_size - 1:
             for j, r in enumerate(rrows):
                 if j not in m:
                     lrow = [r[rnames.index(n)] if n in keys else None for n in lnames]
                     out_rows.append(lrow + [r[t] for t in r_out_idx])
-        if how == "right":
-            out_rows = [r for r in out_rows if any(v is not None for v in r[len(lnames):]) or True]
-    fields = [T.StructField(n, left.schema[n].dataType) for n in lnames]
-    if how not in ("leftanti", "leftsemi"):
-        fields += [T.StructField(n if n in out_names else n + "_r", right.schema[n].dataType) for n in r_extra]
-        fields = [T.StructField(nm, f.dataType) for nm, f in zip(out_names, fields)]
-    schema = T.StructType(fields)
     # gather-free placement: keep this rank's output rows local
     from .builder import frame_from_pycolumns
     pycols = {f.name: [r[j] for r in out_rows] for j, f in enumerate(schema.fields)}
@@ -544,5 +557,9 @@ def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
 
 
 def rebalance(df: DataFrame) -> DataFrame:
+    from .relational_fast import device_rebalance
+    out = device_rebalance(df)
+    if out is not None:
+        return out
     names, rows, ids = df._gather_host()
     return rows_contiguous(df._session, df.schema, rows, ids)

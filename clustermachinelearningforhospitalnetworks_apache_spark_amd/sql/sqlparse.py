@@ -1245,14 +1245,45 @@ def _split_on(cond: Expr, lcols, rcols):
 
 
 def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[str], using: bool):
-    """Host hash join keeping both sides' columns; names present on both sides become
-    ``alias.column`` (USING keys appear once). Right side gathered to every rank (reference-scale
-    tables, as ``DataFrame.join``)."""
+    """Equi-join keeping both sides' columns; names present on both sides become
+    ``alias.column`` (USING keys appear once). Device path: relational_fast (joint key codes,
+    searchsorted match ranges; right side broadcast as ``DataFrame.join``), row loop otherwise."""
+    from . import relational_fast as RF
+    lnames = left.columns
+    rnames = right.columns
+    r_out = [n for n in rnames if not (using and n in rkeys)]
+    both = set(lnames) & set(r_out)
+    lq, rq = lq or "l", rq or "r"
+    out_l = [f"{lq}.{n}" if n in both else n for n in lnames]
+    out_r = [f"{rq}.{n}" if n in both else n for n in r_out]
+    semi = how in ("leftsemi", "leftanti")
+    fields = [T.StructField(n, left.schema[o].dataType, True) for n, o in zip(out_l, lnames)]
+    if not semi:
+        fields += [T.StructField(n, right.schema[o].dataType, True) for n, o in zip(out_r, r_out)]
+    schema = T.StructType(fields)
+    df = None
+    if RF.ENABLED:
+        rcols, n_right = RF._gather_frame(right)
+        r = RF.join_indices(left, rcols, n_right, list(lkeys), list(rkeys), how)
+        if r is not None:
+            li, ri = r
+            fill = list(zip(lkeys, rkeys)) if using else []
+            df = RF.build_join(left, rcols, li, ri, list(zip(out_l, lnames)),
+                               [] if semi else list(zip(out_r, r_out)), fill, schema)
+    if df is None:
+        df = _join_rows(left, right, how, lkeys, rkeys, using, lnames, r_out, schema, semi)
+    src = dict(getattr(left, "_sql_sources", {}) or {lq: out_l})
+    if not semi:
+        src[rq] = out_r
+    df._sql_sources = src
+    return df
+
+
+def _join_rows(left, right, how, lkeys, rkeys, using, lnames, r_out, schema, semi):
+    """Row-loop join for keys without device codes (vectors, arrays, ...)."""
     from .builder import frame_from_pycolumns
-    from .dataframe import column_to_python
     from .group import _hashable
     rnames, rrows, _ = right._gather_host()
-    lnames = left.columns
     lcols = left._local_rows_host()
     ridx = [rnames.index(k) for k in rkeys]
     index = {}
@@ -1261,13 +1292,7 @@ def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[st
         if any(v is None for v in key):
             continue
         index.setdefault(key, []).append(j)
-    r_out = [n for n in rnames if not (using and n in rkeys)]
-    both = set(lnames) & set(r_out)
-    lq, rq = lq or "l", rq or "r"
-    out_l = [f"{lq}.{n}" if n in both else n for n in lnames]
-    out_r = [f"{rq}.{n}" if n in both else n for n in r_out]
     r_pos = [rnames.index(n) for n in r_out]
-    semi = how in ("leftsemi", "leftanti")
     rows, matched = [], set()
     for i in range(left._nrows):
         lrow = [lcols[n][i] for n in lnames]
@@ -1288,7 +1313,7 @@ def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[st
         allm = set()
         for part in left._comm.allgather_object(sorted(matched)):
             allm |= set(part)
-        if left._comm.rank == 0:
+        if left._comm.rank == left._comm.world_size - 1:
             for j, r in enumerate(rrows):
                 if j not in allm:
                     lrow = [None] * len(lnames)
@@ -1296,20 +1321,10 @@ def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[st
                         for k_l, k_r in zip(lkeys, rkeys):
                             lrow[lnames.index(k_l)] = r[rnames.index(k_r)]
                     rows.append(lrow + [r[t] for t in r_pos])
-    names = out_l if semi else out_l + out_r
-    fields = [T.StructField(n, left.schema[o].dataType, True) for n, o in zip(out_l, lnames)]
-    if not semi:
-        fields += [T.StructField(n, right.schema[o].dataType, True) for n, o in zip(out_r, r_out)]
-    schema = T.StructType(fields)
     pycols = {f.name: [r[j] for r in rows] for j, f in enumerate(schema.fields)}
     counts = left._comm.allgather_object(len(rows))
     off = sum(counts[: left._comm.rank])
-    df = frame_from_pycolumns(left._session, schema, pycols, list(range(off, off + len(rows))))
-    src = dict(getattr(left, "_sql_sources", {}) or {lq: out_l})
-    if not semi:
-        src[rq] = out_r
-    df._sql_sources = src
-    return df
+    return frame_from_pycolumns(left._session, schema, pycols, list(range(off, off + len(rows))))
 
 
 def _apply_join(session, df, lq, jc: JoinClause):

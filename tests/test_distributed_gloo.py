@@ -100,6 +100,22 @@ def _workload(out_path, rank, master="local[1]"):
                                            F.sum("y").over(w.rowsBetween(-3, 0)).alias("s"),
                                            F.lag("b", 1).over(w).alias("lb")).orderBy("g", "a").collect()
     res["win"] = [[r.g, r.rn, r.s, r.lb] for r in wd][:300]
+    # relational shuffles: sort (all-to-all exchange), dedup, joins, repartition
+    rel = spark.createDataFrame(pdf.assign(k=(pdf.index * 7) % 13, q=pdf["g"].where(pdf.index % 11 != 0)))
+    srt = rel.orderBy(F.col("q").desc_nulls_first(), "k", F.col("a").desc())
+    res["sort_rows"] = [[r.q, r.k, r.a] for r in srt.select("q", "k", "a").collect()]
+    res["dedup"] = [[r.q, r.k] for r in rel.select("q", "k").distinct().collect()]
+    dim = spark.createDataFrame(pd.DataFrame({"k": list(range(0, 15, 2)) + [4],
+                                              "kname": [f"n{i}" for i in range(9)]}))
+    res["join"] = {h: [[r.a, r.k, r.kname] for r in rel.join(dim, "k", h).select("a", "k", "kname").collect()]
+                   for h in ("inner", "left", "right", "full")}
+    res["semi"] = [rel.join(dim, "k", h).count() for h in ("leftsemi", "leftanti")]
+    rel.createOrReplaceTempView("rel")
+    dim.createOrReplaceTempView("dim")
+    res["sql_join"] = [[r.a, r.kname] for r in spark.sql(
+        "SELECT rel.a, dim.kname FROM rel JOIN dim ON rel.k = dim.k WHERE rel.a > 0").collect()]
+    rp = rel.filter("a > 1").repartition(4)
+    res["repart"] = [[r.a, r.k] for r in rp.select("a", "k").collect()]
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
     res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
     # round-2 additions: device aggregates merged across ranks, selectors, SVM, GMM, AFT, isotonic
@@ -220,6 +236,8 @@ def _check_invariant(r1, rw, world):
     assert [x[:2] for x in rw["win"]] == [x[:2] for x in r1["win"]]
     np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
     assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
+    for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart"):
+        assert rw[key] == r1[key], key
     np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(rw["stat_aggs"], r1["stat_aggs"], rtol=1e-9)
     np.testing.assert_allclose(rw["summ"], r1["summ"], rtol=1e-10)
