@@ -308,6 +308,10 @@ def combine_partials(parts: List[Any], fn: str):
 
 
 def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
+    from .window import SessionWindow, materialize_sessions
+    if any(isinstance(k, SessionWindow) for k in keys):
+        # sessions depend on the other keys: materialise them as a column, then group by it
+        df, keys, _ = materialize_sessions(df, keys)
     specs, key_types, local = local_partials(df, keys, exprs)
     merged, morder = gather_partials(df._comm, local, len(specs))
     rows = [final_row(key, merged[key], specs) for key in morder]
@@ -344,19 +348,6 @@ class GroupedData:
         es = [ColRef(k.name()) for k in self.keys] + [_as_expr(e) for e in exprs]
         if self.df.isStreaming:
             return self.df._lazy("_stream_aggregate", self.keys, es)
-        from .window import SessionWindow
-        if any(isinstance(k, SessionWindow) for k in self.keys):
-            # sessions depend on the other keys: materialise them as a column, then group by it
-            df, keys = self.df, []
-            for k in self.keys:
-                if isinstance(k, SessionWindow):
-                    cd = k.materialize(df, [o for o in self.keys if o is not k])
-                    df = df._from_columns(list(df.columns) + ["session_window"],
-                                          [df._cols[c] for c in df.columns] + [cd])
-                    keys.append(ColRef("session_window"))
-                else:
-                    keys.append(k)
-            return aggregate(df, keys, es)
         return aggregate(self.df, self.keys, es)
 
     def _simple(self, fn: str, cols) -> DataFrame:

@@ -464,10 +464,13 @@ class StreamingQuery:
         keep = self._late_mask(df)
         if keep is not None:
             df = df._mask_rows(keep)
-        specs, key_types, local = local_partials(df, keys, exprs)
-        merged, morder = gather_partials(self._session._comm, local, len(specs))
         st = self._state.setdefault(idx, {})
         touched = []
+        from .window import SessionWindow
+        if any(isinstance(k, SessionWindow) for k in keys):
+            df, keys, touched = self._merge_sessions(st, df, keys, exprs)
+        specs, key_types, local = local_partials(df, keys, exprs)
+        merged, morder = gather_partials(self._session._comm, local, len(specs))
         for key in morder:
             cur = st.get(key)
             new = []
@@ -480,7 +483,8 @@ class StreamingQuery:
                     prev = [cur[j]] if cur is not None and cur[j] is not None else []
                     new.append(combine_partials(prev + merged[key][j], sp[2].fn))
             st[key] = new
-            touched.append(key)
+            if key not in touched:
+                touched.append(key)
         mode = self._writer._mode
         if mode == "complete":
             out = list(st)
@@ -500,6 +504,49 @@ class StreamingQuery:
         schema = result_schema(specs, key_types)
         fix_long_columns(schema, rows)
         return rows_round_robin(self._session, schema, rows)
+
+    def _merge_sessions(self, st, df, keys, exprs):
+        """Session windows across micro-batches (Spark's merging session state store): the state's
+        sessions of every key are merged with this batch's events — an event inside a session
+        extends it, one between two sessions joins them — and the state is re-keyed to the merged
+        sessions (their partials combined) before this batch's partials are added."""
+        from .column import micros_to_datetime, ts_to_micros
+        from .group import combine_partials, local_partials
+        from .types import Row
+        from .window import SessionWindow, materialize_sessions
+        j = next(i for i, k in enumerate(keys) if isinstance(k, SessionWindow))
+        prior = {}
+        for key in st:
+            sw = key[j]
+            prior.setdefault(key[:j] + key[j + 1:], []).append((ts_to_micros(sw.start), ts_to_micros(sw.end)))
+        df, keys2, remap = materialize_sessions(df, keys, prior)
+        specs = local_partials(df._session._empty_frame(df.schema), keys2, exprs)[0]
+        touched = []
+        for key in list(st):
+            ok = key[:j] + key[j + 1:]
+            old = (ts_to_micros(key[j].start), ts_to_micros(key[j].end))
+            new = remap.get((ok, old), old)
+            if new == old:
+                continue
+            nk = key[:j] + (Row(start=micros_to_datetime(new[0]), end=micros_to_datetime(new[1])),) + key[j + 1:]
+            cur, add = st.pop(key), None
+            add = st.get(nk)
+            if add is None:
+                st[nk] = cur
+            else:
+                comb = []
+                for i, sp in enumerate(specs):
+                    if sp[0] == "key":
+                        comb.append(None)
+                    elif getattr(sp[2], "custom", False):
+                        comb.append(add[i] + cur[i])
+                    else:
+                        parts = [p for p in (add[i], cur[i]) if p is not None]
+                        comb.append(combine_partials(parts, sp[2].fn) if parts else None)
+                st[nk] = comb
+            if nk not in touched:
+                touched.append(nk)
+        return df, keys2, touched
 
     def _stateful_dedup(self, idx: int, df, subset):
         """Streaming dropDuplicates: a row passes if its key was never seen in an earlier batch and it

@@ -453,7 +453,11 @@ class SessionWindow(Expr):
     def eval(self, frame) -> ColumnData:
         raise ValueError("session_window() is only supported as a groupBy key")
 
-    def materialize(self, frame, other_keys: List[Expr]) -> ColumnData:
+    def materialize(self, frame, other_keys: List[Expr], prior=None):
+        """Session column of ``frame``. ``prior`` ({other-key tuple: [(start_us, end_us), ...]}) are
+        sessions already held in a streaming state store: this batch's events merge with them (an
+        event can extend a session or bridge two). Returns the column, and with ``prior`` also the
+        {(key, (start, end)) -> (start', end')} remap of the prior sessions."""
         from .builder import column_from_values
         from .column import micros_to_datetime
         from .dataframe import column_to_python
@@ -466,24 +470,36 @@ class SessionWindow(Expr):
         kv = [column_to_python(k.eval(frame)) for k in other_keys]
         keys = [tuple(_hashable_key(k[i]) for k in kv) for i in range(len(ts))]
         local = sorted({(k, t) for k, t, ok in zip(keys, ts, vm) if ok}, key=lambda x: (repr(x[0]), x[1]))
-        events: Dict[tuple, List[int]] = {}
+        spans: Dict[tuple, List[tuple]] = {}
         for part in frame._comm.allgather_object(local):
             for k, t in part:
-                events.setdefault(k, []).append(t)
+                spans.setdefault(k, []).append((t, t + self.gap, "e"))
+        for k, lst in (prior or {}).items():
+            for s_, e_ in lst:
+                spans.setdefault(k, []).append((s_, e_, "p"))
         session: Dict[tuple, tuple] = {}
-        for k, tl in events.items():
-            tl = sorted(set(tl))
-            start, end, members = tl[0], tl[0] + self.gap, [tl[0]]
-            for t in tl[1:]:
-                if t < end:
-                    end = max(end, t + self.gap)
-                    members.append(t)
+        remap: Dict[tuple, tuple] = {}
+        for k, sl in spans.items():
+            sl = sorted(set(sl))
+            cur = None
+            members: List[tuple] = []
+
+            def close():
+                for s_, e_, kind in members:
+                    if kind == "e":
+                        session[(k, s_)] = cur
+                    else:
+                        remap[(k, (s_, e_))] = cur
+            for s_, e_, kind in sl:
+                if cur is not None and s_ < cur[1]:
+                    cur = (cur[0], max(cur[1], e_))
+                    members.append((s_, e_, kind))
                     continue
-                for m in members:
-                    session[(k, m)] = (start, end)
-                start, end, members = t, t + self.gap, [t]
-            for m in members:
-                session[(k, m)] = (start, end)
+                if cur is not None:
+                    close()
+                cur, members = (s_, e_), [(s_, e_, kind)]
+            if cur is not None:
+                close()
         vals = []
         for k, t, ok in zip(keys, ts, vm):
             if not ok:
@@ -491,7 +507,25 @@ class SessionWindow(Expr):
                 continue
             a, b = session[(k, t)]
             vals.append(Row(start=micros_to_datetime(a), end=micros_to_datetime(b)))
-        return column_from_values(vals, _WINDOW_TYPE, frame._device)
+        col = column_from_values(vals, _WINDOW_TYPE, frame._device)
+        return col if prior is None else (col, remap)
+
+
+def materialize_sessions(df, keys: List[Expr], prior=None):
+    """Replace a ``session_window`` grouping key by a materialised ``session_window`` column:
+    (frame with the column, keys referring to it, prior-session remap or None)."""
+    from .column import ColRef
+    out_keys, remap = [], None
+    for k in keys:
+        if isinstance(k, SessionWindow):
+            others = [o for o in keys if o is not k]
+            r = k.materialize(df, others, prior) if prior is not None else (k.materialize(df, others), None)
+            cd, remap = r
+            df = df._from_columns(list(df.columns) + ["session_window"], [df._cols[c] for c in df.columns] + [cd])
+            out_keys.append(ColRef("session_window"))
+        else:
+            out_keys.append(k)
+    return df, out_keys, remap
 
 
 def _hashable_key(v):

@@ -122,3 +122,60 @@ def test_output_mode_validation(spark, tmp_path):
     with pytest.raises(ValueError):
         _src(spark, src).writeStream.outputMode("complete").format("memory").queryName("y").option(
             "checkpointLocation", str(tmp_path / "c2")).start()
+
+
+def _session_rows(df):
+    return sorted((r.hospital_id, str(r.session_window.start), str(r.session_window.end), r.n) for r in df.collect())
+
+
+def test_session_window_merges_across_batches(spark, tmp_path):
+    """Streaming session_window: a later event bridges two sessions of earlier batches; complete
+    mode equals the batch groupBy over everything seen, update mode emits only merged / new sessions."""
+    src, ck = str(tmp_path / "in"), str(tmp_path / "ck")
+    base = hospital_frame(1)
+    mk = lambda hs: pd.DataFrame([dict(base.iloc[0], hospital_id=h, event_time=pd.Timestamp(t))  # noqa: E731
+                                  for h, t in hs])
+    b1 = mk([("H0", "2025-04-01 10:00:00"), ("H0", "2025-04-01 10:03:00"), ("H0", "2025-04-01 10:20:00"),
+             ("H1", "2025-04-01 10:00:00")])
+    b2 = mk([("H0", "2025-04-01 10:11:00"), ("H1", "2025-04-01 11:00:00")])
+    b3 = mk([("H0", "2025-04-01 10:24:00")])
+    sess = F.session_window("event_time", "10 minutes")
+    agg = _src(spark, src).groupBy("hospital_id", sess).agg(F.count("*").alias("n"))
+    outs = {"complete": [], "update": []}
+    for mode in outs:
+        d = str(tmp_path / f"in_{mode}")
+        ckm = ck + mode
+        for i, b in enumerate((b1, b2, b3)):
+            write_csv_files(b, d, 1, f"p{i}")
+            a = _src(spark, d).groupBy("hospital_id", sess).agg(F.count("*").alias("n"))
+            _run(a, ckm, mode, fn=lambda df, bid, m=mode: outs[m].append(_session_rows(df)))
+    allrows = pd.concat([b1, b2, b3])
+    batch = spark.createDataFrame(allrows[["hospital_id", "event_time"]])
+    ref = _session_rows(batch.groupBy("hospital_id", sess).agg(F.count("*").alias("n")))
+    assert outs["complete"][-1] == ref
+    # 10:00, 10:03 | 10:20 merge through 10:11 -> one session [10:00, 10:30); 10:24 extends it to 10:34
+    assert ("H0", "2025-04-01 10:00:00", "2025-04-01 10:34:00", 5) in ref
+    assert outs["update"][1] == [("H0", "2025-04-01 10:00:00", "2025-04-01 10:30:00", 4),
+                                 ("H1", "2025-04-01 11:00:00", "2025-04-01 11:10:00", 1)]
+    assert outs["update"][2] == [("H0", "2025-04-01 10:00:00", "2025-04-01 10:34:00", 5)]
+    assert agg.isStreaming
+
+
+def test_session_window_append_mode_emits_closed_sessions(spark, tmp_path):
+    src, ck = str(tmp_path / "in"), str(tmp_path / "ck")
+    base = hospital_frame(1)
+    mk = lambda ts: pd.DataFrame([dict(base.iloc[0], hospital_id="H0", event_time=pd.Timestamp(t))  # noqa: E731
+                                  for t in ts])
+    out = []
+    for i, ts in enumerate((["2025-04-01 10:00:00", "2025-04-01 10:04:00"], ["2025-04-01 10:30:00"],
+                            ["2025-04-01 11:00:00"], ["2025-04-01 11:30:00"])):
+        write_csv_files(mk(ts), src, 1, f"p{i}")
+        a = (_src(spark, src).withWatermark("event_time", "5 minutes")
+             .groupBy("hospital_id", F.session_window("event_time", "10 minutes")).agg(F.count("*").alias("n")))
+        _run(a, ck, "append", fn=lambda df, bid: out.append(_session_rows(df)))
+    emitted = [r for b in out for r in b]
+    # a session closes in the first batch whose watermark (max event of earlier batches - 5 min)
+    # has passed its end: 10:00-10:14 in batch 2, 10:30-10:40 in batch 3
+    assert ("H0", "2025-04-01 10:00:00", "2025-04-01 10:14:00", 2) in emitted
+    assert ("H0", "2025-04-01 10:30:00", "2025-04-01 10:40:00", 1) in emitted
+    assert len(emitted) == len(set(emitted)) == 2 and out[0] == []
