@@ -408,8 +408,8 @@ class DataFrame(DataFrameMoreMixin):
         rows: List[List[Any]] = []
         all_ids: List[int] = []
         for loc, pid, n in parts:
-            for i in range(n):
-                rows.append([loc[nm][i] for nm in names])
+            if n:
+                rows.extend(map(list, zip(*[loc[nm] for nm in names])) if names else ([] for _ in range(n)))
             all_ids += pid
         return names, rows, all_ids
 
@@ -439,9 +439,18 @@ class DataFrame(DataFrameMoreMixin):
         return iter(self.collect())
 
     def toPandas(self):
+        """All rows as a pandas DataFrame (collect-to-driver, ref.py:204). Numeric, boolean and
+        timestamp columns move as numpy arrays (one device-to-host copy per column); other types
+        go through Python values."""
         import pandas as pd
-        names, rows, _ = self._gather_host()
-        data = {n: [r[i] for r in rows] for i, n in enumerate(names)}
+        names = self.columns
+        local = {n: _pandas_array(self._cols[n]) for n in names}
+        parts = self._comm.allgather_object(local) if self._comm.is_distributed else [local]
+        data = {}
+        for n in names:
+            arrs = [p[n] for p in parts]
+            data[n] = np.concatenate(arrs) if all(isinstance(a, np.ndarray) for a in arrs) else \
+                [v for a in arrs for v in (a.tolist() if isinstance(a, np.ndarray) else a)]
         pdf = pd.DataFrame(data, columns=names)
         for f in self._schema.fields:
             if isinstance(f.dataType, T.TimestampType):
@@ -706,6 +715,33 @@ def concat_column_data(parts: List[ColumnData], device) -> ColumnData:
     return ColumnData(vals, valid, dt)
 
 
+def _pandas_array(cd: ColumnData):
+    """The pandas representation of one local column: a numpy array where pandas would infer the
+    same dtype from the Python values (int64 / float64 with NaN for nulls / bool / datetime64 with
+    NaT), else the list of Python values."""
+    dt = cd.dtype
+    if cd.is_host or cd.values.dim() != 1 or not (T.is_numeric(dt) or isinstance(dt, (T.BooleanType,
+                                                                                        T.TimestampType))):
+        return column_to_python(cd)
+    v = cd.values.detach()
+    ok = None if cd.valid is None else cd.valid.detach().cpu().numpy().astype(bool)
+    nulls = ok is not None and not ok.all()
+    if isinstance(dt, T.TimestampType):
+        a = v.to(torch.int64).cpu().numpy().astype("datetime64[us]").astype("datetime64[ns]")
+        if nulls:
+            a[~ok] = np.datetime64("NaT")
+        return a
+    if isinstance(dt, T.BooleanType):
+        return column_to_python(cd) if nulls else v.cpu().numpy().astype(bool)
+    if T.is_integral(dt) and not nulls:
+        return v.to(torch.int64).cpu().numpy()
+    a = v.to(torch.float64).cpu().numpy()
+    if nulls:
+        a = a.copy()
+        a[~ok] = np.nan
+    return a
+
+
 def column_to_python(cd: ColumnData) -> List[Any]:
     """Host python values of a column (nulls -> None)."""
     from ..ml.linalg import DenseVector
@@ -724,14 +760,20 @@ def column_to_python(cd: ColumnData) -> List[Any]:
     dt = cd.dtype
     if isinstance(dt, T.VectorUDT):
         return [DenseVector(arr[i].astype(np.float64)) if vm[i] else None for i in range(n)]
+    # vectorised conversions: numpy builds the Python objects (datetime64[us] -> datetime.datetime,
+    # datetime64[D] -> datetime.date), nulls are patched in with one masked select
     if isinstance(dt, T.TimestampType):
-        return [micros_to_datetime(arr[i]) if vm[i] else None for i in range(n)]
-    if isinstance(dt, T.DateType):
-        return [(_dt.date(1970, 1, 1) + _dt.timedelta(days=int(arr[i]))) if vm[i] else None for i in range(n)]
-    if isinstance(dt, T.BooleanType):
-        return [bool(arr[i]) if vm[i] else None for i in range(n)]
-    if T.is_integral(dt):
-        return [int(arr[i]) if vm[i] else None for i in range(n)]
-    if isinstance(dt, (T.FloatType, T.DoubleType)):
-        return [float(arr[i]) if vm[i] else None for i in range(n)]
-    return [arr[i] if vm[i] else None for i in range(n)]
+        obj = arr.astype(np.int64).astype("datetime64[us]").astype(object)
+    elif isinstance(dt, T.DateType):
+        obj = arr.astype(np.int64).astype("datetime64[D]").astype(object)
+    elif isinstance(dt, T.BooleanType):
+        obj = arr.astype(bool)
+    elif T.is_integral(dt):
+        obj = arr.astype(np.int64)
+    elif isinstance(dt, (T.FloatType, T.DoubleType)):
+        obj = arr.astype(np.float64)
+    else:
+        return [arr[i] if vm[i] else None for i in range(n)]
+    if vm.all():
+        return obj.tolist()
+    return np.where(vm, obj.astype(object), None).tolist()

@@ -36,10 +36,14 @@ def _key(row) -> tuple:
 
 class DataFrameMoreMixin:
     # ------------------------------------------------------------------------------ set operations
-    def _set_op(self, other, keep_fn):
+    def _set_op(self, other, keep_fn, kind: str):
         from .builder import rows_contiguous
+        from .relational_fast import device_set_op
         if len(other.columns) != len(self.columns):
             raise ValueError("set operations need the same number of columns")
+        out = device_set_op(self, other, kind)
+        if out is not None:
+            return out
         _, left, _ = self._gather_host()
         _, right, _ = other._gather_host()
         rows = keep_fn(left, right)
@@ -56,7 +60,7 @@ class DataFrameMoreMixin:
                     seen.add(k)
                     out.append(r)
             return out
-        return self._set_op(other, f)
+        return self._set_op(other, f, "intersect")
 
     def intersectAll(self, other):
         """Rows in both frames, with multiplicity min(count_left, count_right)."""
@@ -72,7 +76,7 @@ class DataFrameMoreMixin:
                     cnt[k] -= 1
                     out.append(r)
             return out
-        return self._set_op(other, f)
+        return self._set_op(other, f, "intersectAll")
 
     def subtract(self, other):
         """Distinct rows of this frame that are not in ``other`` (SQL EXCEPT DISTINCT)."""
@@ -85,7 +89,7 @@ class DataFrameMoreMixin:
                     seen.add(k)
                     out.append(r)
             return out
-        return self._set_op(other, f)
+        return self._set_op(other, f, "subtract")
 
     def exceptAll(self, other):
         """Rows of this frame minus ``other`` with multiplicity (SQL EXCEPT ALL)."""
@@ -102,7 +106,7 @@ class DataFrameMoreMixin:
                 else:
                     out.append(r)
             return out
-        return self._set_op(other, f)
+        return self._set_op(other, f, "exceptAll")
 
     # ------------------------------------------------------------------------------ statistics
     @property

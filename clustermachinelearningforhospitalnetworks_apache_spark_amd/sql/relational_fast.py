@@ -253,17 +253,8 @@ def device_dedup(df, subset: Optional[Sequence[str]]):
         counts = _counts(comm, n)
         off = sum(counts[:comm.rank])
         surv = torch.nonzero(keep).flatten()
-        sub = [c.take(surv) for c in cds]
         # every rank codes the same concatenation of survivors (rank order)
-        blocks = [[] for _ in cds]
-        for j, c in enumerate(sub):
-            if c.is_host:
-                allv = comm.allgather_object(_host_values(c))
-                blocks[j] = [ColumnData(v, None, c.dtype) for v in allv]
-            else:
-                vs = comm.allgather(c.values.to(dev).contiguous())
-                oks = comm.allgather(c.valid_mask().to(dev).contiguous())
-                blocks[j] = [ColumnData(v, o, c.dtype) for v, o in zip(vs, oks)]
+        blocks = [_blocks(c.take(surv), comm, dev) for c in cds]
         gidx = _gather(comm, surv + off)
         if gidx.numel():
             gcode = _tuple_codes(blocks, dev, null_equal=True)
@@ -278,6 +269,60 @@ def device_dedup(df, subset: Optional[Sequence[str]]):
     if bool(keep.all()):
         return df
     return df._mask_rows(keep)
+
+
+def _blocks(cd: ColumnData, comm, dev) -> List[ColumnData]:
+    """The column's per-rank blocks (rank order), on every rank."""
+    if not comm.is_distributed:
+        return [cd]
+    if cd.is_host:
+        return [ColumnData(v, None, cd.dtype) for v in comm.allgather_object(_host_values(cd))]
+    vs = comm.allgather(cd.values.to(dev).contiguous())
+    oks = comm.allgather(cd.valid_mask().to(dev).contiguous())
+    return [ColumnData(v, o, cd.dtype) for v, o in zip(vs, oks)]
+
+
+def _occurrence(code: torch.Tensor) -> torch.Tensor:
+    """0-based rank of every row among the earlier rows with the same code."""
+    n = code.numel()
+    srt, perm = torch.sort(code, stable=True)
+    pos = torch.arange(n, device=code.device)
+    start = torch.ones(n, dtype=torch.bool, device=code.device)
+    start[1:] = srt[1:] != srt[:-1]
+    first = torch.cummax(torch.where(start, pos, torch.zeros_like(pos)), 0).values
+    occ = torch.empty_like(pos)
+    occ[perm] = pos - first
+    return occ
+
+
+def device_set_op(left, right, kind: str):
+    """``intersect`` / ``subtract`` (distinct) and ``intersectAll`` / ``exceptAll`` (multiset) on
+    whole-row equality codes (nulls equal, as Spark's set operations); the kept rows are this
+    rank's left rows, in order. None when a column has no device code."""
+    if not ENABLED or len(left.columns) != len(right.columns):
+        return None
+    comm, dev = left._comm, left._device
+    lc = [left._cols[n] for n in left.columns]
+    rc = [right._cols[n] for n in right.columns]
+    ok = all(_key_kind(a) is not None and _key_kind(a) == _key_kind(b) for a, b in zip(lc, rc))
+    if comm.is_distributed:
+        ok = all(comm.allgather_object(ok))
+    if not ok:
+        return None
+    lcounts = _counts(comm, left._nrows)
+    NL = sum(lcounts)
+    if NL == 0:
+        return left
+    code = _tuple_codes([_blocks(a, comm, dev) + _blocks(b, comm, dev) for a, b in zip(lc, rc)], dev,
+                        null_equal=True)
+    lcode, rcode = code[:NL], code[NL:]
+    rcnt = torch.bincount(rcode, minlength=int(code.max()) + 1)[lcode]
+    occ = _occurrence(lcode)
+    keep = {"intersect": (occ == 0) & (rcnt > 0), "subtract": (occ == 0) & (rcnt == 0),
+            "intersectAll": occ < rcnt, "exceptAll": occ >= rcnt}[kind]
+    off = sum(lcounts[:comm.rank])
+    mine = keep[off:off + left._nrows]
+    return left if bool(mine.all()) else left._mask_rows(mine)
 
 
 # ------------------------------------------------------------------------------------------------ join

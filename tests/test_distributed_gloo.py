@@ -116,6 +116,10 @@ def _workload(out_path, rank, master="local[1]"):
         "SELECT rel.a, dim.kname FROM rel JOIN dim ON rel.k = dim.k WHERE rel.a > 0").collect()]
     rp = rel.filter("a > 1").repartition(4)
     res["repart"] = [[r.a, r.k] for r in rp.select("a", "k").collect()]
+    kq = rel.select("k", "q")
+    other = spark.createDataFrame(pdf.assign(k=(pdf.index * 5) % 13, q=pdf["g"]).iloc[::3][["k", "q"]])
+    res["setops"] = [[tuple(r) for r in getattr(kq, m)(other).collect()]
+                     for m in ("intersect", "intersectAll", "subtract", "exceptAll")]
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
     res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
     # round-2 additions: device aggregates merged across ranks, selectors, SVM, GMM, AFT, isotonic
@@ -236,7 +240,7 @@ def _check_invariant(r1, rw, world):
     assert [x[:2] for x in rw["win"]] == [x[:2] for x in r1["win"]]
     np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
     assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
-    for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart"):
+    for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart", "setops"):
         assert rw[key] == r1[key], key
     np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(rw["stat_aggs"], r1["stat_aggs"], rtol=1e-9)

@@ -173,3 +173,11 @@ def test_device_paths_do_not_gather_rows(spark, monkeypatch):
     df.dropDuplicates(["g", "w"]).count()
     df.join(right, "g", "full").count()
     df.repartition(2).count()
+
+
+@pytest.mark.parametrize("op", ["intersect", "intersectAll", "subtract", "exceptAll"])
+def test_set_ops_match_row_loop(spark, op):
+    a = _frame(spark, 400, seed=1).select("g", "w", "b")
+    b = _frame(spark, 300, seed=2).select("g", "w", "b")
+    dev, host = _both(lambda: _rows(getattr(a, op)(b)))
+    assert dev == host and len(dev) > 0
