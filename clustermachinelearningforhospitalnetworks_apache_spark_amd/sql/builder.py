@@ -38,6 +38,14 @@ def column_from_values(values, dtype: T.DataType, device) -> ColumnData:
             arr = np.where(nan, 0, arr)
         t = torch.as_tensor(np.ascontiguousarray(arr)).to(device=device, dtype=dtype.torch_dtype)
         return ColumnData(t, valid, dtype)
+    if isinstance(dtype, T.TimestampType) and isinstance(values, np.ndarray) and values.dtype.kind == "M":
+        nat = np.isnat(values)
+        us = values.astype("datetime64[us]").astype(np.int64)
+        us = np.where(nat, 0, us)
+        return ColumnData(torch.as_tensor(us).to(device), None if not nat.any() else
+                          torch.as_tensor(~nat, device=device), dtype)
+    if isinstance(dtype, T.StringType):
+        return _string_column(values, dtype)
     vals = list(values) if not isinstance(values, list) else values
     n = len(vals)
     if isinstance(dtype, T.VectorUDT):
@@ -132,6 +140,44 @@ def frame_from_pycolumns(session, schema: T.StructType, pycols: Dict[str, Sequen
     elif not isinstance(row_ids, torch.Tensor):
         row_ids = torch.as_tensor(np.asarray(row_ids, dtype=np.int64), device=dev)
     return DataFrame(session, schema, cols, n, row_ids.to(dev), dev)
+
+
+DICT_MIN_ROWS = 32768  # below this a plain object array is as cheap as codes + dictionary
+
+
+def _string_column(values, dtype) -> ColumnData:
+    """A host string column without a per-row Python loop: nulls (None / NaN / NaT) found by
+    ``pandas.isna``, non-string values stringified, and — for large columns with few distinct
+    values (hospital ids, wards, regions) — dictionary encoding (``DictColumnData``: int32 codes +
+    distinct strings), which the group-by, sort, join and take paths use instead of the objects."""
+    import pandas as pd
+    from .column import DictColumnData
+    arr = values if isinstance(values, np.ndarray) and values.dtype == object else np.asarray(
+        list(values) if not isinstance(values, list) else values, dtype=object)
+    if arr.ndim != 1:  # e.g. a list of equal-length tuples
+        out = np.empty(len(values), dtype=object)
+        out[:] = list(values)
+        arr = out
+    n = arr.shape[0]
+    null = np.asarray(pd.isna(arr), dtype=bool) if n else np.zeros(0, dtype=bool)
+    if pd.api.types.infer_dtype(arr, skipna=True) not in ("string", "empty"):
+        arr = arr.copy()
+        for i in np.flatnonzero(~null):
+            v = arr[i]
+            if not isinstance(v, str):
+                arr[i] = v.decode() if isinstance(v, (bytes, bytearray)) else str(v)
+    valid = None if not null.any() else ~null
+    if n >= DICT_MIN_ROWS:
+        codes, uniq = pd.factorize(arr, use_na_sentinel=True)
+        if 4 * len(uniq) <= n:
+            dictionary = np.empty(len(uniq) + 1, dtype=object)
+            dictionary[:-1] = np.asarray(uniq, dtype=object)
+            dictionary[-1] = None
+            return DictColumnData(codes.astype(np.int32), dictionary, valid, dtype)
+    if valid is not None:
+        arr = arr.copy() if arr is values else arr
+        arr[null] = None
+    return ColumnData(arr, valid, dtype)
 
 
 def shard_range(n: int, rank: int, world: int):

@@ -35,15 +35,88 @@ import numpy as np
 import torch
 
 from . import types as T
-from .column import ColumnData
+from .column import ColumnData, DictColumnData
 
 ENABLED = True  # tests flip this to compare against the row-loop paths
 
 
 # ------------------------------------------------------------------------------------------------ codes
 def _rerank(v: torch.Tensor) -> Tuple[torch.Tensor, int]:
+    """Order-preserving dense ranks of int64 values: a presence bincount + prefix sum when the value
+    range is small (O(n + range), no sort), a sort-based unique otherwise."""
+    n = v.numel()
+    if n == 0:
+        return v.to(torch.int64), 0
+    lo, hi = int(v.min()), int(v.max())
+    if hi - lo < max(4 * n, 1 << 20):
+        x = v - lo
+        present = torch.bincount(x, minlength=hi - lo + 1) > 0
+        remap = torch.cumsum(present, 0) - 1
+        return remap[x], int(remap[-1]) + 1
     uniq, inv = torch.unique(v, sorted=True, return_inverse=True)
     return inv.to(torch.int64), int(uniq.numel())
+
+
+_I64_MASK = 0x7FFFFFFFFFFFFFFF
+
+
+def _order_key(v: torch.Tensor, ok: Optional[torch.Tensor], ascending: bool, nulls_first: bool):
+    """Order-preserving int64 sort keys of one column: a list of (key, range) to sort by, most
+    significant first; ``range`` (keys in [0, range)) is None for full-width keys. Floats map to
+    their total-order bit pattern (NaN canonical and largest, -0.0 == 0.0), descending is the bitwise
+    complement, nulls go below / above every value."""
+    if v.is_floating_point():
+        x = v.to(torch.float64) + 0.0
+        x = torch.where(torch.isnan(x), torch.full_like(x, float("nan")), x)
+        b = x.view(torch.int64)
+        k = b ^ ((b >> 63) & _I64_MASK)
+    else:
+        k = v.to(torch.int64)
+    if not ascending:
+        k = ~k
+    has_null = ok is not None and not bool(ok.all())
+    valid = k[ok] if has_null else k
+    if valid.numel() == 0:
+        return [(torch.zeros_like(k), 1)]
+    lo, hi = int(valid.min()), int(valid.max())
+    span = hi - lo + 1 + (1 if has_null else 0)
+    if span < (1 << 62):
+        key = k - lo + (1 if has_null and nulls_first else 0)
+        if has_null:
+            key = torch.where(ok, key, torch.full_like(key, 0 if nulls_first else hi - lo + 1))
+        return [(key, span)]
+    if not has_null:
+        return [(k, None)]
+    flag = (ok if nulls_first else ~ok).to(torch.int64)  # 0 sorts first
+    return [(flag, 2), (torch.where(ok, k, torch.zeros_like(k)), None)]
+
+
+def _lex_perm(keys: List[Tuple[torch.Tensor, Optional[int]]], n: int, dev) -> torch.Tensor:
+    """Stable lexicographic permutation: bounded keys are packed by mixed radix into as few int64
+    words as fit, then one stable sort per word, least significant word first."""
+    words, cur, radix = [], None, 1
+    for key, rng in keys:
+        if rng is None:
+            if cur is not None:
+                words.append(cur)
+            words.append(key)
+            cur, radix = None, 1
+            continue
+        if cur is not None and radix * rng < (1 << 62):
+            cur, radix = cur * rng + key, radix * rng
+        else:
+            if cur is not None:
+                words.append(cur)
+            cur, radix = key, rng
+    if cur is not None:
+        words.append(cur)
+    perm = None
+    for w in reversed(words):
+        if perm is None:
+            perm = torch.sort(w, stable=True).indices
+        else:
+            perm = perm[torch.sort(w[perm], stable=True).indices]
+    return perm if perm is not None else torch.arange(n, device=dev)
 
 
 def _fold(parts: List[Tuple[torch.Tensor, int]]) -> torch.Tensor:
@@ -59,6 +132,44 @@ def _host_values(cd: ColumnData) -> np.ndarray:
     if cd.valid is not None:
         vals = np.where(np.asarray(cd.valid, dtype=bool), vals, None)
     return vals
+
+
+def _str_parts(cd: ColumnData) -> Tuple[np.ndarray, np.ndarray]:
+    """(int64 codes with -1 = null, distinct strings) of a host string column: the ingest
+    dictionary when the column has one, one ``pandas.factorize`` otherwise."""
+    if isinstance(cd, DictColumnData):
+        codes = cd.codes.astype(np.int64)
+        if cd.valid is not None:
+            codes = np.where(np.asarray(cd.valid, dtype=bool), codes, -1)
+        return codes, np.asarray(cd.dictionary[:-1], dtype=object)
+    import pandas as pd
+    codes, uniq = pd.factorize(_host_values(cd), use_na_sentinel=True)
+    return codes.astype(np.int64), np.asarray(uniq, dtype=object)
+
+
+def _merge_str(blocks: List[ColumnData]) -> Tuple[np.ndarray, np.ndarray]:
+    """Codes of several string blocks against one merged dictionary: only the (small)
+    dictionaries are factorised together, the per-row codes are remapped by a gather."""
+    import pandas as pd
+    parts = [_str_parts(c) for c in blocks]
+    if len(parts) == 1:
+        return parts[0]
+    alld = np.concatenate([d for _, d in parts]) if parts else np.zeros(0, dtype=object)
+    gmap, guniq = pd.factorize(alld)
+    out, off = [], 0
+    for codes, d in parts:
+        m = gmap[off:off + len(d)]
+        out.append(np.where(codes >= 0, m[np.clip(codes, 0, None)] if len(d) else -1, -1))
+        off += len(d)
+    return (np.concatenate(out) if out else np.zeros(0, dtype=np.int64)), np.asarray(guniq, dtype=object)
+
+
+def _dict_column(codes: np.ndarray, uniq: np.ndarray, dtype) -> ColumnData:
+    dictionary = np.empty(len(uniq) + 1, dtype=object)
+    dictionary[:-1] = uniq
+    dictionary[-1] = None
+    ok = codes >= 0
+    return DictColumnData(codes.astype(np.int32), dictionary, None if ok.all() else ok, dtype)
 
 
 def _numeric_like(dt) -> bool:
@@ -90,10 +201,8 @@ def _eq_codes(cols: List[ColumnData], dev) -> Optional[Tuple[torch.Tensor, int]]
     if len(kinds) != 1 or None in kinds:
         return None
     if kinds == {"str"}:
-        import pandas as pd
-        vals = np.concatenate([_host_values(c) for c in cols]) if cols else np.zeros(0, dtype=object)
-        codes, uniq = pd.factorize(vals, use_na_sentinel=True)
-        return torch.as_tensor(np.asarray(codes, dtype=np.int64), device=dev), len(uniq)
+        codes, uniq = _merge_str(cols)
+        return torch.as_tensor(codes, device=dev), len(uniq)
     as_float = any(c.values.is_floating_point() for c in cols)
     bits = torch.cat([_eq_bits(c.values.to(dev), as_float) for c in cols])
     ok = torch.cat([c.valid_mask().to(dev) for c in cols])
@@ -120,23 +229,22 @@ def _tuple_codes(keycols: List[List[ColumnData]], dev, null_equal: bool) -> Opti
 
 
 def _order_codes(cd: ColumnData, comm, dev, ascending: bool, nulls_first: bool):
-    """(order-preserving dense code over all ranks in rank order, cardinality) or None."""
-    from .window_fast import _order_code
+    """Sort keys (``_order_key``) of a column over all ranks in rank order, or None."""
     if cd.is_host:
         if not isinstance(cd.dtype, T.StringType):
             return None
-        import pandas as pd
-        loc = _host_values(cd)
-        allv = np.concatenate(comm.allgather_object(loc)) if comm.is_distributed else loc
-        codes, _ = pd.factorize(allv, sort=True, use_na_sentinel=True)
-        v = torch.as_tensor(np.asarray(codes, dtype=np.int64), device=dev)
+        codes, uniq = _merge_str(_blocks(cd, comm, dev))
+        rank = np.empty(len(uniq), dtype=np.int64)
+        rank[np.argsort(uniq, kind="stable")] = np.arange(len(uniq))  # code-point (= UTF-8 byte) order
+        v = torch.as_tensor(np.where(codes >= 0, rank[np.clip(codes, 0, None)] if len(uniq) else 0, -1),
+                            device=dev)
         ok = v >= 0
     else:
         if cd.values.dim() != 1 or not _numeric_like(cd.dtype):
             return None
         v = _gather(comm, cd.values.to(dev))
-        ok = _gather(comm, cd.valid_mask().to(dev))
-    return _order_code(v, ok, ascending, nulls_first)
+        ok = _gather(comm, cd.valid_mask().to(dev)) if (cd.valid is not None or comm.is_distributed) else None
+    return _order_key(v, ok, ascending, nulls_first)
 
 
 def _gather(comm, t: torch.Tensor) -> torch.Tensor:
@@ -174,7 +282,15 @@ def _exchange(df, perm: torch.Tensor, counts: List[int]):
     inv[order] = torch.arange(order.numel(), device=dev)
     cols = {}
     for name, cd in df._cols.items():
-        if cd.is_host:
+        if cd.is_host and isinstance(cd.dtype, T.StringType):
+            codes, uniq = _str_parts(cd)
+            codes = codes[send_idx.cpu().numpy()]
+            cut = np.cumsum([0] + send_counts)
+            parts = comm.allgather_object(([codes[cut[r]:cut[r + 1]] for r in range(W)], uniq))
+            blocks = [_dict_column(p[0][me], p[1], cd.dtype) for p in parts]
+            rc, ru = _merge_str(blocks)
+            cols[name] = _dict_column(rc[inv.cpu().numpy()], ru, cd.dtype)
+        elif cd.is_host:
             vals = _host_values(cd)[send_idx.cpu().numpy()]
             cut = np.cumsum([0] + send_counts)
             parts = comm.allgather_object([vals[cut[r]:cut[r + 1]] for r in range(W)])
@@ -205,16 +321,15 @@ def device_sort(df, orders) -> Optional[object]:
     comm, dev = df._comm, df._device
     counts = _counts(comm, df._nrows)
     N = sum(counts)
-    parts = []
+    if N == 0:
+        return df
+    keys = []
     for o in orders:
         r = _order_codes(o.expr.eval(df), comm, dev, o.ascending, o.nulls_first)
         if r is None:
             return None
-        parts.append(r)
-    if N == 0:
-        return df
-    perm = torch.sort(_fold(parts), stable=True).indices
-    return _exchange(df, perm, counts)
+        keys += r
+    return _exchange(df, _lex_perm(keys, N, dev), counts)
 
 
 # ------------------------------------------------------------------------------------------------ dedup
@@ -275,6 +390,8 @@ def _blocks(cd: ColumnData, comm, dev) -> List[ColumnData]:
     """The column's per-rank blocks (rank order), on every rank."""
     if not comm.is_distributed:
         return [cd]
+    if cd.is_host and isinstance(cd.dtype, T.StringType):
+        return [_dict_column(c, u, cd.dtype) for c, u in comm.allgather_object(_str_parts(cd))]
     if cd.is_host:
         return [ColumnData(v, None, cd.dtype) for v in comm.allgather_object(_host_values(cd))]
     vs = comm.allgather(cd.values.to(dev).contiguous())
@@ -333,7 +450,9 @@ def _gather_frame(df) -> Tuple[Dict[str, ColumnData], int]:
         return dict(df._cols), df._nrows
     out = {}
     for name, cd in df._cols.items():
-        if cd.is_host:
+        if cd.is_host and isinstance(cd.dtype, T.StringType):
+            out[name] = _dict_column(*_merge_str(_blocks(cd, comm, df._device)), cd.dtype)
+        elif cd.is_host:
             vals = np.concatenate(comm.allgather_object(_host_values(cd)))
             ok = np.asarray([x is not None for x in vals], dtype=bool)
             out[name] = ColumnData(vals, None if ok.all() else ok, cd.dtype)
@@ -353,6 +472,11 @@ def _take_nullable(cd: ColumnData, idx: torch.Tensor) -> ColumnData:
         shape = (idx.numel(),) + tuple(cd.values.shape[1:])
         return ColumnData(torch.zeros(shape, dtype=cd.values.dtype, device=cd.values.device),
                           torch.zeros(idx.numel(), dtype=torch.bool, device=cd.values.device), cd.dtype)
+    if isinstance(cd, DictColumnData):
+        codes, uniq = _str_parts(cd)
+        c = codes[safe.cpu().numpy()]
+        c[miss.cpu().numpy()] = -1
+        return _dict_column(c, uniq, cd.dtype)
     if cd.is_host:
         ii = safe.cpu().numpy()
         mm = miss.cpu().numpy()

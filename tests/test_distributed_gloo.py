@@ -100,7 +100,10 @@ def _workload(out_path, rank, master="local[1]"):
                                            F.sum("y").over(w.rowsBetween(-3, 0)).alias("s"),
                                            F.lag("b", 1).over(w).alias("lb")).orderBy("g", "a").collect()
     res["win"] = [[r.g, r.rn, r.s, r.lb] for r in wd][:300]
-    # relational shuffles: sort (all-to-all exchange), dedup, joins, repartition
+    # relational shuffles: sort (all-to-all exchange), dedup, joins, repartition; strings
+    # dictionary-encoded (per-rank dictionaries merged by the shuffles)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import builder as _B
+    _B.DICT_MIN_ROWS = 64
     rel = spark.createDataFrame(pdf.assign(k=(pdf.index * 7) % 13, q=pdf["g"].where(pdf.index % 11 != 0)))
     srt = rel.orderBy(F.col("q").desc_nulls_first(), "k", F.col("a").desc())
     res["sort_rows"] = [[r.q, r.k, r.a] for r in srt.select("q", "k", "a").collect()]
@@ -120,6 +123,8 @@ def _workload(out_path, rank, master="local[1]"):
     other = spark.createDataFrame(pdf.assign(k=(pdf.index * 5) % 13, q=pdf["g"]).iloc[::3][["k", "q"]])
     res["setops"] = [[tuple(r) for r in getattr(kq, m)(other).collect()]
                      for m in ("intersect", "intersectAll", "subtract", "exceptAll")]
+    assert type(rel._cols["q"]).__name__ == "DictColumnData"
+    _B.DICT_MIN_ROWS = 32768
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
     res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
     # round-2 additions: device aggregates merged across ranks, selectors, SVM, GMM, AFT, isotonic

@@ -181,3 +181,26 @@ def test_set_ops_match_row_loop(spark, op):
     b = _frame(spark, 300, seed=2).select("g", "w", "b")
     dev, host = _both(lambda: _rows(getattr(a, op)(b)))
     assert dev == host and len(dev) > 0
+
+
+def test_dictionary_encoded_strings_match_row_loop(spark, monkeypatch):
+    """String columns dictionary-encoded at creation (codes + distinct strings) go through the
+    same sort / dedup / join / set-operation results as plain object columns."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import builder
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.column import DictColumnData
+    monkeypatch.setattr(builder, "DICT_MIN_ROWS", 16)
+    df = _frame(spark, 500, seed=5)
+    assert isinstance(df._cols["w"], DictColumnData)
+    right = spark.createDataFrame([(w, f"t{j}") for j, w in enumerate(["icu", "er", "er", None, "onc"] * 5)],
+                                  "w string, tag string")
+    other = _frame(spark, 300, seed=6).select("w", "g")
+    cases = [lambda: _rows(df.orderBy(F.col("w").desc_nulls_last(), "id")),
+             lambda: _rows(df.dropDuplicates(["w", "b"])),
+             lambda: _rows(df.join(right, "w", "full")),
+             lambda: _rows(df.select("w", "g").exceptAll(other)),
+             lambda: _rows(df.orderBy("w", "id").join(right, "w", "leftanti"))]
+    for fn in cases:
+        dev, host = _both(fn)
+        assert dev == host
+    out = df.orderBy("w")
+    assert isinstance(out._cols["w"], DictColumnData)
