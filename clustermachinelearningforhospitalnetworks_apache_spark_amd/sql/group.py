@@ -476,7 +476,7 @@ def describe(df: DataFrame, cols: List[str]) -> DataFrame:
 
 def join_frames(left: DataFrame, right: DataFrame, on, how: str) -> DataFrame:
     """Equi-join on column names. Device path: relational_fast (joint key codes, sorted right side,
-    searchsorted match ranges); the row loop below (broadcast hash join, right side gathered to
+    per-code count and prefix-sum match ranges); the row loop below (broadcast hash join, right side gathered to
     every rank) handles keys without device codes. Null keys never match (Spark equality).
     Right non-key columns whose names clash with left ones get an ``_r`` suffix."""
     how = how.lower().replace("_", "")

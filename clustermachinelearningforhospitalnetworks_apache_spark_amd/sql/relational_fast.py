@@ -18,8 +18,8 @@ streaming job). Here:
   first dropped rank-locally, then only the surviving keys are all-gathered to resolve
   cross-rank duplicates in global order. Rows stay on their rank.
 * **join** — left and right keys are coded jointly (one ``torch.unique`` over both sides; null
-  keys never match), the right side is sorted by code and ``searchsorted`` gives every left
-  row's match range; ``repeat_interleave`` expands the pairs in (left row, right row) order.
+  keys never match), the right side is sorted by code and per-code counts / prefix sums give
+  every left row's match range; ``repeat_interleave`` expands the pairs in (left row, right row) order.
   inner / left / right / full / semi / anti / cross are index arithmetic on those ranges; the
   right side is broadcast to every rank (the reference's tables are small dimensions), the
   unmatched right rows of right / full joins are emitted once, by rank 0.
@@ -533,10 +533,14 @@ def join_indices(left, rcols: Dict[str, ColumnData], n_right: int, lkeys: List[s
     if code is None:
         return None
     lc, rc = code[:n_left], code[n_left:]
-    rs, rperm = torch.sort(rc, stable=True)
-    lo = torch.searchsorted(rs, lc, right=False)
-    hi = torch.searchsorted(rs, lc, right=True)
-    cnt = torch.where(lc >= 0, hi - lo, torch.zeros_like(lo))
+    # codes are dense: per-code counts and starts of the code-sorted right side replace a binary search
+    card = int(code.max()) + 2 if code.numel() else 1
+    rperm = torch.sort(rc, stable=True).indices
+    rcount = torch.bincount(rc + 1, minlength=card)[1:]           # slot 0 = null keys
+    rstart = torch.cumsum(rcount, 0) - rcount + int((rc < 0).sum())  # null right keys sort first
+    lsafe = torch.clamp(lc, min=0)
+    lo = rstart[lsafe]
+    cnt = torch.where(lc >= 0, rcount[lsafe], torch.zeros_like(lo))
     if how in ("leftsemi", "leftanti"):
         keep = cnt > 0 if how == "leftsemi" else cnt == 0
         li = torch.nonzero(keep).flatten()

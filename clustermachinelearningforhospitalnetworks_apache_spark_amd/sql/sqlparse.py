@@ -1247,7 +1247,7 @@ def _split_on(cond: Expr, lcols, rcols):
 def _join_frames(left, lq, right, rq, how: str, lkeys: List[str], rkeys: List[str], using: bool):
     """Equi-join keeping both sides' columns; names present on both sides become
     ``alias.column`` (USING keys appear once). Device path: relational_fast (joint key codes,
-    searchsorted match ranges; right side broadcast as ``DataFrame.join``), row loop otherwise."""
+    per-code match ranges; right side broadcast as ``DataFrame.join``), row loop otherwise."""
     from . import relational_fast as RF
     lnames = left.columns
     rnames = right.columns
