@@ -31,8 +31,12 @@ from . import types as T
 from .column import AggExpr, ColumnData, Expr
 
 def _dense_codes(vals: torch.Tensor) -> Tuple[torch.Tensor, int]:
-    uniq, inv = torch.unique(vals, sorted=True, return_inverse=True)
-    return inv.to(torch.int64), int(uniq.numel())
+    """Order-preserving dense ranks (bincount + prefix sum for small integer ranges, else unique)."""
+    if vals.is_floating_point():
+        uniq, inv = torch.unique(vals, sorted=True, return_inverse=True)
+        return inv.to(torch.int64), int(uniq.numel())
+    from .relational_fast import _rerank
+    return _rerank(vals.to(torch.int64))
 
 
 def _gather(comm, t: torch.Tensor) -> torch.Tensor:
