@@ -532,9 +532,238 @@ def _frame_from_pandas_local(df, schema: T.StructType, pdf):
     n = len(pdf)
     counts = df._comm.allgather_object(n)
     off = sum(counts[:df._comm.rank])
-    pycols = {f.name: [None if (isinstance(v, float) and v != v and not isinstance(f.dataType, (T.DoubleType,
-                                                                                                T.FloatType)))
-                       else v for v in pdf[f.name].tolist()] for f in schema.fields}
+    pycols = {}
+    for f in schema.fields:
+        col = pdf[f.name]
+        if (col.dtype.kind in "biuf" and not isinstance(f.dataType, (T.StringType, T.VectorUDT, T.DateType,
+                                                                     T.TimestampType))) or \
+                (col.dtype.kind == "M" and isinstance(f.dataType, T.TimestampType)):
+            pycols[f.name] = col.to_numpy()  # numpy fast path (NaN in integral columns -> null)
+        else:
+            pycols[f.name] = [None if (isinstance(v, float) and v != v and not isinstance(f.dataType, (
+                T.DoubleType, T.FloatType))) else v for v in col.tolist()]
+    return frame_from_pycolumns(df._session, schema, pycols, list(range(off, off + n)))
+
+
+class DataFrameStatFunctions:
+    def __init__(self, df):
+        self.df = df
+
+    def approxQuantile(self, col, probabilities, relativeError):
+        return self.df.approxQuantile(col, probabilities, relativeError)
+
+    def corr(self, col1, col2, method=None):
+        return self.df.corr(col1, col2, method)
+
+    def cov(self, col1, col2):
+        return self.df.cov(col1, col2)
+
+    def crosstab(self, col1, col2):
+        return self.df.crosstab(col1, col2)
+
+    def freqItems(self, cols, support=None):
+        return self.df.freqItems(cols, support)
+
+    def sampleBy(self, col, fractions, seed=None):
+        return self.df.sampleBy(col, fractions, seed)
+
+
+class MultiGroupedData:
+    """rollup / cube: one aggregation per grouping set, keys outside the set are null, results
+    unioned (Spark's GROUPING SETS)."""
+
+    def __init__(self, df, keys, sets):
+        self.df, self.keys, self.sets = df, keys, sets
+
+    def agg(self, *exprs):
+        from .column import Alias, Column, Lit
+        from .dataframe import _as_expr
+        from .functions_extra import GroupingMarker
+        from .group import GroupedData
+        names = [k.name() for k in self.keys]
+        if len(exprs) == 1 and isinstance(exprs[0], dict):
+            from . import functions as F
+            exprs = tuple(getattr(F, fn if fn != "mean" else "avg")(c).alias(f"{fn}({c})")
+                          for c, fn in exprs[0].items())
+        es = [_as_expr(e) for e in exprs]
+        plain = [Column(e) for e in es if not isinstance(e.child if isinstance(e, Alias) else e, GroupingMarker)]
+        out = None
+        for s in self.sets:
+            part = GroupedData(self.df, list(s)).agg(*plain)
+            sn = [k.name() for k in s]
+            sel = []
+            for nm, k in zip(names, self.keys):
+                if nm in sn:
+                    sel.append(Column(_as_expr(nm)))
+                else:
+                    dt = k.eval(self.df).dtype
+                    sel.append(Column(Lit(None)).cast(dt).alias(nm))
+            agg_cols = [c for c in part.columns if c not in sn]
+            it = iter(agg_cols)
+            for e in es:
+                inner = e.child if isinstance(e, Alias) else e
+                if isinstance(inner, GroupingMarker):
+                    v, dt = inner.value(names, sn)
+                    sel.append(Column(Lit(v)).cast(dt).alias(e.alias if isinstance(e, Alias) else inner.name()))
+                else:
+                    sel.append(Column(_as_expr(next(it))))
+            part = part.select(*sel)
+            out = part if out is None else out.union(part)
+        return out
+
+    def count(self):
+        from . import functions as F
+        return self.agg(F.count("*").alias("count"))
+
+
+class PivotedData:
+    """``groupBy(keys).pivot(col, values).agg(...)``: one output column per (pivot value, aggregate)."""
+
+    def __init__(self, df, keys, pivot, values):
+        self.df, self.keys, self.pivot, self.values = df, keys, pivot, values
+
+    def agg(self, *exprs):
+        from .builder import rows_round_robin
+        from .column import Alias
+        from .dataframe import _as_expr, column_to_python
+        from .group import aggregate, _agg_name
+        pv_expr = _as_expr(self.pivot)
+        values = self.values
+        if values is None:
+            vals = column_to_python(pv_expr.eval(self.df))
+            allv = set()
+            for part in self.df._comm.allgather_object(sorted({v for v in vals if v is not None}, key=str)):
+                allv |= set(part)
+            values = sorted(allv, key=lambda v: (str(type(v)), v))
+            if len(values) > 10000:
+                raise ValueError("pivot: more than 10000 distinct values; pass them explicitly")
+        from .column import ColRef
+        agg_exprs = [_as_expr(e) for e in exprs]
+        key_names = [k.name() for k in self.keys]
+        res = aggregate(self.df, self.keys + [pv_expr], [ColRef(n) for n in key_names] + [ColRef(pv_expr.name())]
+                        + agg_exprs)
+        rows = res.collect()
+        nk = len(key_names)
+        agg_names = [a.alias if isinstance(a, Alias) else _agg_name(a) for a in agg_exprs]
+        agg_types = [res.schema.fields[nk + 1 + j].dataType for j in range(len(agg_exprs))]
+        table: Dict[tuple, Dict[Any, list]] = {}
+        order: List[tuple] = []
+        for r in rows:
+            k = tuple(r[:nk])
+            if k not in table:
+                table[k] = {}
+                order.append(k)
+            table[k][r[nk]] = list(r[nk + 1:])
+        fields = [T.StructField(n, res.schema.fields[i].dataType) for i, n in enumerate(key_names)]
+        for v in values:
+            for j, an in enumerate(agg_names):
+                nm = str(v) if len(agg_names) == 1 else f"{v}_{an}"
+                fields.append(T.StructField(nm, agg_types[j]))
+        out_rows = []
+        for k in order:
+            row = list(k)
+            for v in values:
+                got = table[k].get(v)
+                row += got if got is not None else [None] * len(agg_names)
+            out_rows.append(row)
+        return rows_round_robin(self.df._session, T.StructType(fields), out_rows)
+
+    def count(self):
+        from . import functions as F
+        return self.agg(F.count("*").alias("count"))
+
+    def sum(self, *cols):
+        from . import functions as F
+        return self.agg(*[F.sum(c) for c in cols])
+
+    def avg(self, *cols):
+        from . import functions as F
+        return self.agg(*[F.avg(c) for c in cols])
+
+    mean = avg
+
+
+def apply_in_pandas(grouped, func, schema):
+    """GroupedData.applyInPandas: every group's rows become one pandas DataFrame handed to ``func``.
+    Groups get global dense codes (sql/relational_fast.py); group g's rows are shuffled to rank
+    g % world (one all-to-all), each rank converts its rows to pandas column-wise once and calls
+    ``func`` per group, in key order. Output rows stay on that rank."""
+    import pandas as pd
+    from . import relational_fast as RF
+    df = grouped.df
+    sch = schema if isinstance(schema, T.StructType) else T.parse_ddl_schema(schema)
+    comm = df._comm
+    kc = [k.eval(df) for k in grouped.keys]
+    ok = all(RF._key_kind(c) is not None for c in kc)
+    if comm.is_distributed:
+        ok = all(comm.allgather_object(ok))
+    if not ok:
+        return _apply_in_pandas_rows(grouped, func, sch)
+    if comm.is_distributed:
+        counts = RF._counts(comm, df._nrows)
+        off = sum(counts[:comm.rank])
+        code = RF._tuple_codes([RF._blocks(c, comm, df._device) for c in kc], df._device, null_equal=True) \
+            if sum(counts) else torch.zeros(0, dtype=torch.int64, device=df._device)
+        dest = code[off:off + df._nrows] % comm.world_size
+        df = RF.shuffle_to(df, dest)
+        kc = [k.eval(df) for k in grouped.keys]
+    from .dataframe import _pandas_array, column_to_python
+    names = df.columns
+    pdf_all = pd.DataFrame({n: _pandas_array(df._cols[n]) for n in names}, columns=names)
+    mine = []
+    if df._nrows:
+        code = RF._tuple_codes([[c] for c in kc], df._device, null_equal=True).cpu().numpy()
+        order = np.argsort(code, kind="stable")
+        bounds = np.flatnonzero(np.diff(code[order])) + 1
+        groups = np.split(order, bounds)
+        kv = [column_to_python(c) for c in kc]
+        groups.sort(key=lambda g: tuple(str(v[g[0]]) for v in kv))
+        for g in groups:
+            mine.append(func(pdf_all.iloc[g].reset_index(drop=True)))
+    res = pd.concat(mine, ignore_index=True) if mine else pd.DataFrame(columns=sch.names)
+    return _frame_from_pandas_local(df, sch, res)
+
+
+def _apply_in_pandas_rows(grouped, func, sch):
+    """Row-gathering applyInPandas for keys without device codes: group g is processed by rank
+    crc32(g) % world (deterministic), whose output rows stay on that rank."""
+    import pandas as pd
+    df = grouped.df
+    names, rows, _ = df._gather_host()
+    from .dataframe import column_to_python
+    keyvals = [df._comm.allgather_object(column_to_python(k.eval(df))) for k in grouped.keys]
+    flat = [[v for part in kv for v in part] for kv in keyvals]
+    groups: Dict[tuple, List[int]] = {}
+    for i in range(len(rows)):
+        groups.setdefault(tuple(f[i] for f in flat), []).append(i)
+    import zlib
+    mine = []
+    W, r = df._comm.world_size, df._comm.rank
+    for key in sorted(groups, key=lambda t: tuple(str(v) for v in t)):
+        if zlib.crc32(repr(key).encode()) % W != r:
+            continue
+        pdf = pd.DataFrame([rows[i] for i in groups[key]], columns=names)
+        mine.append(func(pdf))
+    res = pd.concat(mine, ignore_index=True) if mine else pd.DataFrame(columns=sch.names)
+    return _frame_from_pandas_local(df, sch, res)
+
+
+def _frame_from_pandas_local(df, schema: T.StructType, pdf):
+    """A frame whose rows are this rank's pandas rows (row ids renumbered globally)."""
+    from .builder import frame_from_pycolumns
+    n = len(pdf)
+    counts = df._comm.allgather_object(n)
+    off = sum(counts[:df._comm.rank])
+    pycols = {}
+    for f in schema.fields:
+        col = pdf[f.name]
+        if (col.dtype.kind in "biuf" and not isinstance(f.dataType, (T.StringType, T.VectorUDT, T.DateType,
+                                                                     T.TimestampType))) or \
+                (col.dtype.kind == "M" and isinstance(f.dataType, T.TimestampType)):
+            pycols[f.name] = col.to_numpy()  # numpy fast path (NaN in integral columns -> null)
+        else:
+            pycols[f.name] = [None if (isinstance(v, float) and v != v and not isinstance(f.dataType, (
+                T.DoubleType, T.FloatType))) else v for v in col.tolist()]
     return frame_from_pycolumns(df._session, schema, pycols, list(range(off, off + n)))
 
 

@@ -280,6 +280,34 @@ def _exchange(df, perm: torch.Tensor, counts: List[int]):
     order = torch.sort(src_rank[a:b], stable=True).indices
     inv = torch.empty_like(order)
     inv[order] = torch.arange(order.numel(), device=dev)
+    return _move(df, send_idx, send_counts, inv)
+
+
+def shuffle_to(df, dest: torch.Tensor):
+    """Send every local row to rank ``dest[i]``; a rank's result holds what it received in source-rank
+    order, each source's rows in their original order (the exchange of applyInPandas)."""
+    comm = df._comm
+    if not comm.is_distributed:
+        return df
+    dest = dest.to(df._device)
+    send_idx = torch.sort(dest, stable=True).indices
+    send_counts = torch.bincount(dest, minlength=comm.world_size).tolist()
+    return _move(df, send_idx, send_counts, None)
+
+
+def _move(df, send_idx: torch.Tensor, send_counts: List[int], inv: Optional[torch.Tensor]):
+    """Row exchange: local rows ``send_idx`` (grouped by destination, ``send_counts`` per rank) go out,
+    the received rows (source-rank order) are permuted by ``inv`` when given."""
+    comm = df._comm
+    W, me = comm.world_size, comm.rank
+    dev = df._device
+    inv_np = None if inv is None else inv.cpu().numpy()
+
+    def perm_np(a):
+        return a if inv_np is None else a[inv_np]
+
+    def perm_t(t):
+        return t if inv is None else t[inv]
     cols = {}
     for name, cd in df._cols.items():
         if cd.is_host and isinstance(cd.dtype, T.StringType):
@@ -289,21 +317,21 @@ def _exchange(df, perm: torch.Tensor, counts: List[int]):
             parts = comm.allgather_object(([codes[cut[r]:cut[r + 1]] for r in range(W)], uniq))
             blocks = [_dict_column(p[0][me], p[1], cd.dtype) for p in parts]
             rc, ru = _merge_str(blocks)
-            cols[name] = _dict_column(rc[inv.cpu().numpy()], ru, cd.dtype)
+            cols[name] = _dict_column(perm_np(rc), ru, cd.dtype)
         elif cd.is_host:
             vals = _host_values(cd)[send_idx.cpu().numpy()]
             cut = np.cumsum([0] + send_counts)
             parts = comm.allgather_object([vals[cut[r]:cut[r + 1]] for r in range(W)])
             recv = np.concatenate([p[me] for p in parts]) if parts else np.zeros(0, dtype=object)
-            out = recv[inv.cpu().numpy()]
+            out = perm_np(recv)
             ok = np.asarray([x is not None for x in out], dtype=bool)
             cols[name] = ColumnData(out, None if ok.all() else ok, cd.dtype)
         else:
-            v = comm.alltoallv(cd.values[send_idx], send_counts)[inv]
-            ok = comm.alltoallv(cd.valid_mask().to(dev)[send_idx], send_counts)[inv]
+            v = perm_t(comm.alltoallv(cd.values[send_idx], send_counts))
+            ok = perm_t(comm.alltoallv(cd.valid_mask().to(dev)[send_idx], send_counts))
             cols[name] = ColumnData(v, None if cd.valid is None and bool(ok.all()) else ok, cd.dtype)
-    ids = comm.alltoallv(df._row_ids.to(dev)[send_idx], send_counts)[inv]
-    return df._new(df._schema, cols, b - a, ids)
+    ids = perm_t(comm.alltoallv(df._row_ids.to(dev)[send_idx], send_counts))
+    return df._new(df._schema, cols, int(ids.numel()), ids)
 
 
 def device_rebalance(df):

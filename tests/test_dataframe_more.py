@@ -118,3 +118,26 @@ def test_dataframe_api_round2b(tmp_path):
     df.writeTo("wt").partitionedBy("id").overwritePartitions()
     assert sorted(r.id for r in spark.table("wt").collect()) == [1, 2, 3]
     spark.stop()
+
+
+def test_apply_in_pandas_many_groups_matches_pandas(spark):
+    """Column-wise conversion and code-based grouping: every group handed to ``func`` exactly once, in
+    key order, with the pandas dtypes of the columns (ints stay int64, strings object)."""
+    import numpy as np
+    rs = np.random.RandomState(4)
+    n = 3000
+    pdf = pd.DataFrame({"h": [f"H{i % 37}" for i in range(n)], "w": rs.randint(0, 3, n).astype(np.int32),
+                        "los": rs.gamma(2.0, 2.0, n)})
+    df = spark.createDataFrame(pdf)
+    seen = []
+
+    def fn(g):
+        seen.append((g.h.iloc[0], int(g.w.iloc[0])))
+        assert g.w.dtype == np.int32 or g.w.dtype == np.int64
+        return pd.DataFrame({"h": [g.h.iloc[0]], "w": [int(g.w.iloc[0])], "n": [len(g)], "m": [g.los.mean()]})
+    out = df.groupBy("h", "w").applyInPandas(fn, "h string, w int, n long, m double").collect()
+    ref = pdf.groupby(["h", "w"]).los.agg(["size", "mean"])
+    assert len(out) == len(ref) == len(seen) == len(set(seen))
+    assert [(r.h, r.w) for r in out] == sorted(((r.h, r.w) for r in out), key=lambda t: (str(t[0]), str(t[1])))
+    for r in out:
+        assert r.n == ref.loc[(r.h, r.w), "size"] and abs(r.m - ref.loc[(r.h, r.w), "mean"]) < 1e-12

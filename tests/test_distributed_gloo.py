@@ -124,6 +124,10 @@ def _workload(out_path, rank, master="local[1]"):
     res["setops"] = [[tuple(r) for r in getattr(kq, m)(other).collect()]
                      for m in ("intersect", "intersectAll", "subtract", "exceptAll")]
     assert type(rel._cols["q"]).__name__ == "DictColumnData"
+    aip = rel.groupBy("q", "k").applyInPandas(
+        lambda g: pd.DataFrame({"q": [g.q.iloc[0]], "k": [int(g.k.iloc[0])], "n": [len(g)], "s": [float(g.a.sum())]}),
+        "q string, k long, n long, s double").collect()
+    res["aip"] = sorted([[r.q, r.k, r.n, round(r.s, 9)] for r in aip], key=str)
     _B.DICT_MIN_ROWS = 32768
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import BisectingKMeans
     res["bkm"] = np.stack(BisectingKMeans(k=4, seed=2).fit(f).clusterCenters()).tolist()
@@ -245,7 +249,7 @@ def _check_invariant(r1, rw, world):
     assert [x[:2] for x in rw["win"]] == [x[:2] for x in r1["win"]]
     np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
     assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
-    for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart", "setops"):
+    for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart", "setops", "aip"):
         assert rw[key] == r1[key], key
     np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)
     np.testing.assert_allclose(rw["stat_aggs"], r1["stat_aggs"], rtol=1e-9)
