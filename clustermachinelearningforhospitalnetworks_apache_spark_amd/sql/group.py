@@ -312,6 +312,10 @@ def aggregate(df: DataFrame, keys: List[Expr], exprs: List[Expr]) -> DataFrame:
     if any(isinstance(k, SessionWindow) for k in keys):
         # sessions depend on the other keys: materialise them as a column, then group by it
         df, keys, _ = materialize_sessions(df, keys)
+    from .aggregate_fast import device_aggregate
+    out = device_aggregate(df, keys, exprs)
+    if out is not None:
+        return out
     specs, key_types, local = local_partials(df, keys, exprs)
     merged, morder = gather_partials(df._comm, local, len(specs))
     rows = [final_row(key, merged[key], specs) for key in morder]

@@ -106,8 +106,26 @@ def _python_values(cd: ColumnData) -> List[Any]:
     return column_to_python(cd)
 
 
+class TensorPartials:
+    """Per-group partial aggregates of one rank as device tensors (group g = g-th group in first-
+    appearance order): ``parts[j]`` is None for a key spec, else a dict with ``kind`` and tensors
+    ("n": cnt; "min"/"max": cnt, val; "first"/"last": cnt, rows; "isum": cnt, sum; "mom": cnt, sum,
+    mu, m2; "custom": computed from the group row lists)."""
+
+    def __init__(self, **kw):
+        self.__dict__.update(kw)
+
+
 def fast_local_partials(df, keys, exprs):
     """Same result as ``group.local_partials`` or None when this path does not apply."""
+    tp = tensor_partials(df, keys, exprs)
+    if tp is None:
+        return None
+    return tp.specs, tp.key_types, _to_python(tp, df)
+
+
+def tensor_partials(df, keys, exprs) -> Optional[TensorPartials]:
+    """The device stage of ``fast_local_partials``; None when this path does not apply."""
     from .group import _agg_name, _unwrap
     from .window import _WINDOW_TYPE, TimeWindow
     n = df._nrows
@@ -202,43 +220,22 @@ def fast_local_partials(df, keys, exprs):
     specs = [("agg", sp[1], sp[2], sp[2].prepare(df), None) if inp is not None and inp[0] == "custom" else sp
              for sp, inp in zip(specs, agg_inputs)]
     first_rows = first if src is None else src[first]
-    # ---- key tuples (python values of each group's first entry, as the row loop sees them)
-    key_lists = []
-    for k, cd in zip(keys, key_cols):
-        if cd is None:
-            from .column import micros_to_datetime
-            from .types import Row
-            s0 = win_start[first].cpu().tolist()
-            key_lists.append([Row(start=micros_to_datetime(s), end=micros_to_datetime(s + k.dur)) for s in s0])
-        else:
-            key_lists.append(_python_values(cd.take(first_rows)))
-    group_keys = [tuple(kl[g] for kl in key_lists) for g in range(G)]
-    # ---- per-group partials
-    per_spec: List[Optional[List[Any]]] = []
-    rows_of_group = None
+    # ---- per-group partials (tensors)
+    parts: List[Optional[dict]] = []
     all_count = None
     for sp, inp in zip(specs, agg_inputs):
         if sp[0] == "key":
-            per_spec.append(None)
+            parts.append(None)
             continue
         agg = sp[2]
         kind = inp[0]
         if kind == "custom":
-            if rows_of_group is None:
-                srows = (torch.arange(n, device=dev) if src is None else src)
-                perm = torch.argsort(gid, stable=True)
-                counts = torch.bincount(gid, minlength=G).cpu().tolist()
-                flat = srows[perm].cpu().tolist()
-                rows_of_group, at = [], 0
-                for c in counts:
-                    rows_of_group.append(flat[at:at + c])
-                    at += c
-            per_spec.append([agg.partial(sp[3], rows_of_group[g]) for g in range(G)])
+            parts.append({"kind": "custom"})
             continue
         if kind == "star":
             if all_count is None:
                 all_count = torch.bincount(gid, minlength=G)
-            per_spec.append([("n", c) for c in all_count.cpu().tolist()])
+            parts.append({"kind": "n", "cnt": all_count})
             continue
         cd = inp[1]
         fn = agg.fn
@@ -261,9 +258,8 @@ def fast_local_partials(df, keys, exprs):
             cnt = all_count
         else:
             cnt = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, gid, vm.to(torch.int64))
-        cnt_l = cnt.cpu().tolist()
         if fn == "count":
-            per_spec.append([("n", c) for c in cnt_l])
+            parts.append({"kind": "n", "cnt": cnt})
             continue
         if fn in ("min", "max"):
             if vals.is_floating_point():
@@ -274,8 +270,7 @@ def fast_local_partials(df, keys, exprs):
             v = vals if vm is None else torch.where(vm, vals, torch.full_like(vals, fill))
             out = torch.full((G,), fill, dtype=vals.dtype, device=dev)
             out.scatter_reduce_(0, gid, v, "amin" if fn == "min" else "amax", include_self=True)
-            py = _python_values(ColumnData(out, None, cd.dtype))
-            per_spec.append([(fn, py[g] if cnt_l[g] else None) for g in range(G)])
+            parts.append({"kind": fn, "cnt": cnt, "val": out, "cd": cd})
             continue
         if fn in ("first", "last"):
             pos = torch.arange(m, device=dev)
@@ -285,18 +280,15 @@ def fast_local_partials(df, keys, exprs):
             pick = torch.full((G,), fill, dtype=torch.int64, device=dev)
             pick.scatter_reduce_(0, gid, pos, "amin" if fn == "first" else "amax", include_self=True)
             pick = pick.clamp(0, m - 1)
-            rows = pick if src is None else src[pick]
-            py = _python_values(cd.take(rows))
-            per_spec.append([(fn, py[g] if cnt_l[g] else None) for g in range(G)])
+            parts.append({"kind": fn, "cnt": cnt, "rows": pick if src is None else src[pick], "cd": cd})
             continue
         # sum / avg / variance family
         if fn == "sum" and T.is_integral(cd.dtype):
             v = vals.to(torch.int64)
             if vm is not None:
                 v = torch.where(vm, v, torch.zeros_like(v))
-            s = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, gid, v)
-            per_spec.append([("isum", c, int(x)) if c else ("mom", 0, 0.0, 0.0, 0.0)
-                             for c, x in zip(cnt_l, s.cpu().tolist())])
+            parts.append({"kind": "isum", "cnt": cnt,
+                          "sum": torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, gid, v)})
             continue
         v = vals.to(torch.float64)
         if vm is not None:
@@ -307,10 +299,61 @@ def fast_local_partials(df, keys, exprs):
         if vm is not None:
             d = torch.where(vm, d, torch.zeros_like(d))
         m2 = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, d * d)
-        st = torch.stack([s, mu, m2]).cpu().tolist()
-        per_spec.append([("mom", c, st[0][g], st[1][g], st[2][g]) if c else ("mom", 0, 0.0, 0.0, 0.0)
-                         for g, c in enumerate(cnt_l)])
+        parts.append({"kind": "mom", "cnt": cnt, "sum": s, "mu": mu, "m2": m2})
+    return TensorPartials(specs=specs, key_types=key_types, keys=keys, key_cols=key_cols, G=G, gid=gid,
+                          first=first, first_rows=first_rows, src=src, win_start=win_start, n=n, m=m, parts=parts)
+
+
+def _to_python(tp: TensorPartials, df):
+    """{key tuple: [partial per spec]} in the shapes ``group._partial`` produces."""
+    G, dev = tp.G, df._device
+    # ---- key tuples (python values of each group's first entry, as the row loop sees them)
+    key_lists = []
+    for k, cd in zip(tp.keys, tp.key_cols):
+        if cd is None:
+            from .column import micros_to_datetime
+            from .types import Row
+            s0 = tp.win_start[tp.first].cpu().tolist()
+            key_lists.append([Row(start=micros_to_datetime(s), end=micros_to_datetime(s + k.dur)) for s in s0])
+        else:
+            key_lists.append(_python_values(cd.take(tp.first_rows)))
+    group_keys = [tuple(kl[g] for kl in key_lists) for g in range(G)]
+    per_spec: List[Optional[List[Any]]] = []
+    rows_of_group = None
+    for sp, pt in zip(tp.specs, tp.parts):
+        if pt is None:
+            per_spec.append(None)
+            continue
+        kind = pt["kind"]
+        if kind == "custom":
+            if rows_of_group is None:
+                srows = (torch.arange(tp.n, device=dev) if tp.src is None else tp.src)
+                perm = torch.argsort(tp.gid, stable=True)
+                counts = torch.bincount(tp.gid, minlength=G).cpu().tolist()
+                flat = srows[perm].cpu().tolist()
+                rows_of_group, at = [], 0
+                for c in counts:
+                    rows_of_group.append(flat[at:at + c])
+                    at += c
+            per_spec.append([sp[2].partial(sp[3], rows_of_group[g]) for g in range(G)])
+            continue
+        cnt_l = pt["cnt"].cpu().tolist()
+        if kind == "n":
+            per_spec.append([("n", c) for c in cnt_l])
+        elif kind in ("min", "max"):
+            py = _python_values(ColumnData(pt["val"], None, pt["cd"].dtype))
+            per_spec.append([(kind, py[g] if cnt_l[g] else None) for g in range(G)])
+        elif kind in ("first", "last"):
+            py = _python_values(pt["cd"].take(pt["rows"]))
+            per_spec.append([(kind, py[g] if cnt_l[g] else None) for g in range(G)])
+        elif kind == "isum":
+            per_spec.append([("isum", c, int(x)) if c else ("mom", 0, 0.0, 0.0, 0.0)
+                             for c, x in zip(cnt_l, pt["sum"].cpu().tolist())])
+        else:
+            st = torch.stack([pt["sum"], pt["mu"], pt["m2"]]).cpu().tolist()
+            per_spec.append([("mom", c, st[0][g], st[1][g], st[2][g]) if c else ("mom", 0, 0.0, 0.0, 0.0)
+                             for g, c in enumerate(cnt_l)])
     local = {}
     for g, key in enumerate(group_keys):
         local[key] = [None if ps is None else ps[g] for ps in per_spec]
-    return specs, key_types, local
+    return local

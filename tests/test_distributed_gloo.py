@@ -82,6 +82,14 @@ def _workload(out_path, rank, master="local[1]"):
     g = spark.createDataFrame(pdf).groupBy("g").agg(F.sum("y").alias("s")).orderBy("g").collect()
     res["groupby"] = [(r.g, r.s) for r in g]
     res["sql"] = spark.createDataFrame(pdf).filter("a > 0 AND b < 2").count()
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import aggregate_fast as _AF
+    rich = lambda: [list(r) for r in spark.createDataFrame(pdf.assign(h=(pdf.index * 13) % 97)).groupBy(  # noqa: E731
+        "g", "h").agg(F.sum("y"), F.avg("a"), F.stddev("b"), F.min("c"), F.max("d"), F.count("*"),
+                      F.first("a"), F.last("b")).collect()]
+    res["agg_dev"] = rich()
+    _AF.ENABLED = False
+    res["agg_py"] = rich()
+    _AF.ENABLED = True
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import (Imputer, OneHotEncoder,
                                                                                          StringIndexer)
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.tuning import CrossValidator, ParamGridBuilder
@@ -249,6 +257,7 @@ def _check_invariant(r1, rw, world):
     assert [x[:2] for x in rw["win"]] == [x[:2] for x in r1["win"]]
     np.testing.assert_allclose([x[2] for x in rw["win"]], [x[2] for x in r1["win"]], rtol=1e-12)
     assert [x[3] for x in rw["win"]] == [x[3] for x in r1["win"]]
+    assert rw["agg_dev"] == rw["agg_py"] and r1["agg_dev"] == r1["agg_py"]  # device merge == Python merge
     for key in ("sort_rows", "dedup", "join", "semi", "sql_join", "repart", "setops", "aip"):
         assert rw[key] == r1[key], key
     np.testing.assert_allclose(rw["bkm"], r1["bkm"], rtol=1e-9, atol=1e-9)

@@ -171,3 +171,42 @@ def test_fast_equals_row_loop_gpu():
             _same(fast, slow)
     finally:
         s.stop()
+
+
+@pytest.mark.parametrize("qi", [0, 1, 2, 5, 6, 7])
+def test_columnar_merge_bitwise_equals_python_merge(spark, qi):
+    """aggregate_fast (device merge of the tensor partials) against group.gather_partials /
+    final_row over the same partials: identical values, bit for bit, and identical order."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import aggregate_fast
+    df = _frame(spark)
+    q = QUERIES[qi]
+    dev = _rows(q(df))
+    aggregate_fast.ENABLED = False
+    try:
+        py = _rows(q(df))
+    finally:
+        aggregate_fast.ENABLED = True
+    assert len(dev) == len(py)
+    for a, b in zip(dev, py):
+        for u, v in zip(a, b):
+            if isinstance(u, float) and isinstance(v, float) and math.isnan(u):
+                assert math.isnan(v)
+            else:
+                assert u == v and type(u) is type(v), (a, b)
+
+
+def test_high_cardinality_groupby(spark):
+    import numpy as np
+    import pandas as pd
+    n = 50000
+    rs = np.random.RandomState(1)
+    pdf = pd.DataFrame({"pid": rs.randint(0, 20000, n), "v": rs.rand(n)})
+    got = spark.createDataFrame(pdf).groupBy("pid").agg(F.count("*").alias("c"), F.sum("v").alias("s"),
+                                                         F.max("v").alias("m"))
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.column import ColumnData
+    assert all(not c.is_host for c in got._cols.values())  # device columns, no per-group Python rows
+    ref = pdf.groupby("pid").v.agg(["size", "sum", "max"])
+    rows = got.collect()
+    assert len(rows) == len(ref)
+    for r in rows[:500]:
+        assert r.c == ref.loc[r.pid, "size"] and abs(r.s - ref.loc[r.pid, "sum"]) < 1e-9 and r.m == ref.loc[r.pid, "max"]
