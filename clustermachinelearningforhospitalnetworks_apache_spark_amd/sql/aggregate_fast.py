@@ -12,8 +12,9 @@ first-appearance order). Instead of turning them into Python tuples and merging 
    min / max reduce, first / last pick the earliest / latest rank holding a value, and
    (count, sum, mean, M2) follow the same sequential Chan et al. update as ``group._merge`` — the
    results are the row-loop path's, bit for bit;
-3. finishes sum / avg / variance / stddev on the device and places global group g on rank
-   g % world (``rows_round_robin``'s placement) as device columns.
+3. finishes sum / avg / variance / stddev (the moment merge and the final division / square root
+   run in numpy over one value per group and rank: IEEE-rounded f64, identical on every device)
+   and places global group g on rank g % world (``rows_round_robin``'s placement) as device columns.
 
 High-cardinality aggregations (a group per patient or per admission, not per hospital) therefore
 never build per-group Python objects. Time-window and session keys, custom aggregates
@@ -44,12 +45,6 @@ def _concat(blocks: List[ColumnData], dtype) -> ColumnData:
     v = torch.cat([b.values for b in blocks])
     ok = torch.cat([b.valid_mask().to(v.device) for b in blocks])
     return ColumnData(v, ok, dtype)
-
-
-def _sqrt(x: torch.Tensor) -> torch.Tensor:
-    """Correctly rounded square root (numpy's, as ``math.sqrt``): the vectorised CPU kernel of
-    ``torch.sqrt`` may differ in the last bit. One value per group, so the host round trip is small."""
-    return torch.from_numpy(np.sqrt(x.cpu().numpy())).to(x.device)
 
 
 def device_aggregate(df, keys, exprs):
@@ -138,43 +133,47 @@ def device_aggregate(df, keys, exprs):
             s = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, fid, gathered(pt["sum"]))
             val, valid = s, has
         else:
-            # sequential Chan et al. merge over rank blocks (group._merge's order and arithmetic)
-            s_e, mu_e, m2_e = gathered(pt["sum"]), gathered(pt["mu"]), gathered(pt["m2"])
-            n = torch.zeros(G, dtype=torch.float64, device=dev)
-            mean = torch.zeros(G, dtype=torch.float64, device=dev)
-            m2 = torch.zeros(G, dtype=torch.float64, device=dev)
-            s = torch.zeros(G, dtype=torch.float64, device=dev)
+            # sequential Chan et al. merge over rank blocks (group._merge's order and arithmetic), in
+            # numpy on the host: IEEE-rounded f64 division and sqrt, so the values are the Python
+            # merge's bit for bit on any device (one value per group and rank crosses the link)
+            s_e, mu_e, m2_e = (gathered(pt[k]).cpu().numpy() for k in ("sum", "mu", "m2"))
+            ce = cnt_e.cpu().numpy().astype(np.float64)
+            fid_h = fid.cpu().numpy()
+            n = np.zeros(G)
+            mean = np.zeros(G)
+            m2 = np.zeros(G)
+            s = np.zeros(G)
             for b in blk:
                 if b.stop == b.start:
                     continue
-                g = fid[b]
-                nb = cnt_e[b].to(torch.float64)
+                g = fid_h[b]
+                nb = ce[b]
                 live = nb > 0
                 n0, mean0, m20 = n[g], mean[g], m2[g]
                 delta = mu_e[b] - mean0
                 tot = n0 + nb
-                safe = torch.where(live, tot, torch.ones_like(tot))
-                mean_new = mean0 + delta * nb / safe
-                m2_new = m20 + m2_e[b] + delta * delta * n0 * nb / safe
-                n[g] = torch.where(live, tot, n0)
-                mean[g] = torch.where(live, mean_new, mean0)
-                m2[g] = torch.where(live, m2_new, m20)
-                s[g] = torch.where(live, s[g] + s_e[b], s[g])
-            nz = torch.where(has, n, torch.ones_like(n))
+                safe = np.where(live, tot, 1.0)
+                n[g] = np.where(live, tot, n0)
+                mean[g] = np.where(live, mean0 + delta * nb / safe, mean0)
+                m2[g] = np.where(live, m20 + m2_e[b] + delta * delta * n0 * nb / safe, m20)
+                s[g] = np.where(live, s[g] + s_e[b], s[g])
+            has_h = n > 0
+            nz = np.where(has_h, n, 1.0)
+            valid = has
             if fn == "sum":
-                val, valid = s, has
+                res = s
             elif fn == "avg":
-                val, valid = s / nz, has
+                res = s / nz
             else:
-                var_pop = torch.clamp(m2 / nz, min=0.0)
+                var_pop = np.maximum(m2 / nz, 0.0)
                 if fn in ("var_pop", "stddev_pop"):
-                    val = var_pop if fn == "var_pop" else _sqrt(var_pop)
-                    valid = has
+                    res = var_pop if fn == "var_pop" else np.sqrt(var_pop)
                 else:
                     big = n >= 2
-                    var = var_pop * n / torch.where(big, n - 1, torch.ones_like(n))
-                    val = var if fn == "variance" else _sqrt(var)
-                    valid = big
+                    var = var_pop * n / np.where(big, n - 1, 1.0)
+                    res = var if fn == "variance" else np.sqrt(var)
+                    valid = torch.as_tensor(big, device=dev)
+            val = torch.from_numpy(res).to(dev)
         out = val[mine]
         tdt = rtype.torch_dtype
         if tdt is not None and out.dtype != tdt:
