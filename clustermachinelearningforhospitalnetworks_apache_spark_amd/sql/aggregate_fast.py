@@ -10,8 +10,9 @@ first-appearance order). Instead of turning them into Python tuples and merging 
 2. all-gathers the partial tensors and merges them rank block by rank block (inside a block every
    group appears once, so each step is a duplicate-free scatter): counts and integer sums add,
    min / max reduce, first / last pick the earliest / latest rank holding a value, and
-   (count, sum, mean, M2) follow the same sequential Chan et al. update as ``group._merge`` — the
-   results are the row-loop path's, bit for bit;
+   (count, sum, mean, M2) follow the same sequential Chan et al. update as ``group._merge`` — from
+   the same partials the results are the Python merge's, bit for bit (the local float partials are
+   ``index_add_`` sums: on the GPU their last bits depend on atomic order);
 3. finishes sum / avg / variance / stddev (the moment merge and the final division / square root
    run in numpy over one value per group and rank: IEEE-rounded f64, identical on every device)
    and places global group g on rank g % world (``rows_round_robin``'s placement) as device columns.
