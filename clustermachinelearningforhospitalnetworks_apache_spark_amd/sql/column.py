@@ -626,6 +626,9 @@ class Func(Expr):
         return any(a.is_aggregate() for a in self.args)
 
     def __str__(self):
+        label = getattr(self, "label", None)
+        if label is not None:
+            return label
         parts = [str(a) for a in self.args] + [str(p) for p in getattr(self, "params", ())]
         return f"{self.fname}({', '.join(parts)})"
 
@@ -754,6 +757,95 @@ class Column:
     def asc_nulls_last(self): return SortOrder(self._expr, True, False)
     def desc_nulls_first(self): return SortOrder(self._expr, False, True)
     def desc_nulls_last(self): return SortOrder(self._expr, False, False)
+
+    # ---- pyspark Column methods built on sql.functions (string predicates / regex / substr run
+    # once per distinct value on dictionary-encoded columns, see functions._host_map)
+    def __pow__(self, o):
+        from .functions import pow as _pow
+        return _pow(self, o)
+
+    def __rpow__(self, o):
+        from .functions import pow as _pow
+        return _pow(Column(_expr(o)), self)
+
+    def __rmod__(self, o): return Column(BinOp("%", _expr(o), self._expr))
+
+    def contains(self, other):
+        from .functions_tail import contains
+        return contains(self, other)
+
+    def startswith(self, other):
+        from .functions_tail import startswith
+        return startswith(self, other)
+
+    def endswith(self, other):
+        from .functions_tail import endswith
+        return endswith(self, other)
+
+    def like(self, pattern: str):
+        from .functions_tail import like
+        return like(self, pattern)
+
+    def ilike(self, pattern: str):
+        from .functions_tail import ilike
+        return ilike(self, pattern)
+
+    def rlike(self, pattern: str):
+        from .functions_tail import regexp_like
+        return regexp_like(self, pattern)
+
+    def substr(self, startPos, length):
+        from .functions import substring
+        if isinstance(startPos, Column) or isinstance(length, Column):
+            from .functions_tail import substr
+            return substr(self, startPos, length)
+        return substring(self, int(startPos), int(length))
+
+    def getItem(self, key):
+        from .sqlparse import Subscript
+        return Column(Subscript(self._expr, _expr(key)))
+
+    def getField(self, name: str):
+        from .sqlparse import GetField
+        return Column(GetField(self._expr, name))
+
+    def __getitem__(self, k):
+        if isinstance(k, slice):
+            if k.step is not None:
+                raise ValueError("slice with step is not supported")
+            return self.substr(k.start, k.stop)
+        from .functions_tail import _ItemOrField
+        return Column(_ItemOrField(self._expr, k))
+
+    def eqNullSafe(self, other):
+        from .functions_tail import equal_null
+        return equal_null(self, other if isinstance(other, Column) else Column(Lit(other)))
+
+    def bitwiseAND(self, other):
+        from .functions_tail import _bitwise
+        return _bitwise("&", self, other)
+
+    def bitwiseOR(self, other):
+        from .functions_tail import _bitwise
+        return _bitwise("|", self, other)
+
+    def bitwiseXOR(self, other):
+        from .functions_tail import _bitwise
+        return _bitwise("^", self, other)
+
+    def isNaN(self): return Column(Unary("isnan", self._expr))
+
+    def try_cast(self, to):
+        """Cast with null for values that do not convert (the engine's casts already do)."""
+        return self.cast(to)
+
+    def withField(self, fieldName: str, col):
+        from .functions_tail import _with_field
+        return _with_field(self, fieldName, col)
+
+    def dropFields(self, *fieldNames: str):
+        from .functions_tail import _drop_fields
+        return _drop_fields(self, fieldNames)
 
     def __getattr__(self, item):
         if item.startswith("_"):

@@ -442,7 +442,50 @@ def _host_map(name, cols, fn, rt, params=None):
     ps = _closure_params(fn) if params is None else list(params)
     if ps:
         col._expr.params = ps
+    col._expr.impl = _per_distinct(col._expr.impl, wrapped, rt, [isinstance(a, Lit) for a in col._expr.args])
     return col
+
+
+_DISTINCT_MIN_ROWS = 1024
+
+
+def _per_distinct(impl, fn, rt, lits):
+    """Evaluate a deterministic row function once per distinct value when its only column argument
+    is dictionary-encoded (ingest / createDataFrame ``DictColumnData``): ``fn`` runs over the
+    dictionary, the rows gather the results by code. String results stay dictionary-encoded."""
+    col_args = [i for i, lit_ in enumerate(lits) if not lit_]
+
+    def run(frame, args):
+        from .builder import column_from_values
+        from .column import DictColumnData
+        from .dataframe import column_to_python
+        if len(col_args) != 1 or not isinstance(args[col_args[0]], DictColumnData) or \
+                len(args[col_args[0]]) < _DISTINCT_MIN_ROWS:
+            return impl(frame, args)
+        j = col_args[0]
+        cd = args[j]
+        consts = [None if i == j else (column_to_python(a)[0] if len(a) else None) for i, a in enumerate(args)]
+        outs = []
+        for v in cd.dictionary[:-1]:
+            call = list(consts)
+            call[j] = v
+            outs.append(fn(*call))
+        codes = cd.codes.astype(np.int64)
+        if cd.valid is not None:
+            codes = np.where(np.asarray(cd.valid, dtype=bool), codes, -1)
+        null_out = fn(*[None if i == j else c for i, c in enumerate(consts)])
+        if isinstance(rt, T.StringType):
+            import pandas as pd
+            from .relational_fast import _dict_column
+            vals = np.empty(len(outs) + 1, dtype=object)
+            vals[:-1] = outs
+            vals[-1] = null_out
+            rc, uniq = pd.factorize(vals, use_na_sentinel=True)
+            return _dict_column(rc[codes], np.asarray(uniq, dtype=object), rt)
+        table = column_from_values(outs + [null_out], rt, frame._device)
+        idx = np.where(codes >= 0, codes, len(outs))
+        return table.take(torch.as_tensor(idx, device=table.values.device) if not table.is_host else idx)
+    return run
 
 
 def substring(c: ColumnOrName, pos: int, length: int) -> Column:
@@ -451,7 +494,7 @@ def substring(c: ColumnOrName, pos: int, length: int) -> Column:
         s = str(s)
         start = builtins.max(pos - 1 if pos > 0 else (len(s) + pos if pos < 0 else 0), 0)
         return s[start:start + length]
-    return _host_map(f"substring({pos},{length})", [c], f, T.StringType())
+    return _host_map("substring", [c], f, T.StringType(), params=[pos, length])
 
 
 def concat_ws(sep: str, *cols: ColumnOrName) -> Column:

@@ -738,6 +738,451 @@ def input_file_block_length() -> Column:
     return lit(-1).cast("bigint")
 
 
+# ------------------------------------------------------------------ Column-method helpers, misc
+def _like_rx(pattern: str, escape: str = "\\", flags=0):
+    out, i = [], 0
+    while i < len(pattern):
+        ch = pattern[i]
+        if ch == escape and i + 1 < len(pattern):
+            out.append(re.escape(pattern[i + 1]))
+            i += 2
+            continue
+        out.append(".*" if ch == "%" else "." if ch == "_" else re.escape(ch))
+        i += 1
+    return re.compile("".join(out), re.S | flags)
+
+
+def like(s: ColumnOrName, pattern, escapeChar=None) -> Column:
+    """SQL LIKE: ``%`` any run, ``_`` one character, ``escapeChar`` (default ``\``) escapes."""
+    pat = pattern._expr.value if isinstance(pattern, Column) else str(pattern)
+    rx = _like_rx(pat, escapeChar or "\\")
+    return _host_map("like", [s], lambda v: rx.fullmatch(str(v)) is not None, T.BooleanType(), params=[pat])
+
+
+def ilike(s: ColumnOrName, pattern, escapeChar=None) -> Column:
+    pat = pattern._expr.value if isinstance(pattern, Column) else str(pattern)
+    rx = _like_rx(pat, escapeChar or "\\", re.IGNORECASE)
+    return _host_map("ilike", [s], lambda v: rx.fullmatch(str(v)) is not None, T.BooleanType(), params=[pat])
+
+
+def substr(s: ColumnOrName, pos, len=None) -> Column:  # noqa: A002
+    """``substr(str, pos[, len])`` with column or literal position / length (1-based, Spark)."""
+    lit_ = (lambda x: x if isinstance(x, Column) else Column(Lit(x)))
+    args = [s, lit_(pos)] + ([] if len is None else [lit_(len)])
+
+    def f(v, p, n=None):
+        v = str(v)
+        p = int(p)
+        start = builtins.max(p - 1 if p > 0 else (builtins.len(v) + p if p < 0 else 0), 0)
+        return v[start:] if n is None else v[start:start + builtins.max(int(n), 0)]
+    return _host_map("substr", args, f, T.StringType())
+
+
+class _ItemOrField(Func):
+    """``col[key]``: a struct field for struct columns, ``getItem`` (array index / map key) otherwise."""
+
+    def __init__(self, child, key):
+        super().__init__("getitem", [child], None)
+        self.key = key
+
+    def __str__(self):
+        return f"{self.args[0]}[{self.key}]"
+
+    def name(self):
+        return str(self)
+
+    def eval(self, frame):
+        from .sqlparse import GetField, Subscript
+        cd = self.args[0].eval(frame)
+        if isinstance(cd.dtype, T.StructType) and isinstance(self.key, str):
+            return GetField(self.args[0], self.key).eval(frame)
+        return Subscript(self.args[0], Lit(self.key)).eval(frame)
+
+
+def _bitwise(op: str, a: Column, b) -> Column:
+    fn = {"&": torch.bitwise_and, "|": torch.bitwise_or, "^": torch.bitwise_xor}[op]
+    bb = b if isinstance(b, Column) else Column(Lit(b))
+
+    def impl(frame, args):
+        x, y = args
+        if x.is_host or y.is_host:
+            raise TypeError("bitwise operators need integral columns")
+        dt = x.dtype if T.is_integral(x.dtype) else T.LongType()
+        v = fn(x.values.to(torch.int64), y.values.to(torch.int64).to(x.values.device))
+        ok = None if x.valid is None and y.valid is None else x.valid_mask() & y.valid_mask().to(x.values.device)
+        return ColumnData(v.to(dt.torch_dtype), ok, dt)
+    f = Func(op, [a._expr, bb._expr], impl)
+    f.label = f"({a._expr} {op} {bb._expr})"
+    return Column(f)
+
+
+def _struct_rows(cd):
+    from .dataframe import column_to_python
+    return column_to_python(cd)
+
+
+def _with_field(c: Column, name: str, value: Column) -> Column:
+    from .builder import column_from_values
+    from .dataframe import column_to_python
+    from .types import Row
+    v = value if isinstance(value, Column) else Column(Lit(value))
+
+    def impl(frame, args):
+        st, val = args
+        if not isinstance(st.dtype, T.StructType):
+            raise TypeError("withField needs a struct column")
+        fields = [f for f in st.dtype.fields if f.name != name]
+        pos = next((i for i, f in enumerate(st.dtype.fields) if f.name == name), len(fields))
+        fields.insert(pos, T.StructField(name, val.dtype, True))
+        dt = T.StructType(fields)
+        out = []
+        for r, x in zip(column_to_python(st), column_to_python(val)):
+            if r is None:
+                out.append(None)
+                continue
+            d = r.asDict() if isinstance(r, Row) else dict(r)
+            d[name] = x
+            out.append(Row(**{f.name: d.get(f.name) for f in fields}))
+        return column_from_values(out, dt, frame._device)
+    f = Func("update_fields", [c._expr, v._expr], impl)
+    f.label = f"update_fields({c._expr}, WithField({name}, {v._expr}))"
+    return Column(f)
+
+
+def _drop_fields(c: Column, names) -> Column:
+    from .builder import column_from_values
+    from .dataframe import column_to_python
+    from .types import Row
+
+    def impl(frame, args):
+        st = args[0]
+        if not isinstance(st.dtype, T.StructType):
+            raise TypeError("dropFields needs a struct column")
+        fields = [f for f in st.dtype.fields if f.name not in names]
+        dt = T.StructType(fields)
+        out = [None if r is None else Row(**{f.name: (r.asDict() if isinstance(r, Row) else r).get(f.name)
+                                                for f in fields}) for r in column_to_python(st)]
+        return column_from_values(out, dt, frame._device)
+    f = Func("drop_fields", [c._expr], impl)
+    f.label = f"update_fields({c._expr}, {', '.join(f'dropfield({n})' for n in names)})"
+    return Column(f)
+
+
+def find_in_set(s: ColumnOrName, strArray: ColumnOrName) -> Column:
+    """1-based index of ``s`` in the comma-separated list (0 when absent or ``s`` contains a comma)."""
+    return _host_map("find_in_set", [s, strArray], lambda a, b: 0 if "," in str(a) else (
+        str(b).split(",").index(str(a)) + 1 if str(a) in str(b).split(",") else 0), T.IntegerType())
+
+
+def elt(*inputs: ColumnOrName) -> Column:
+    """``elt(n, s1, s2, ...)``: the n-th string (1-based), null when out of range."""
+    def f(n, *vals):
+        if n is None:
+            return None
+        n = int(n)
+        return vals[n - 1] if 1 <= n <= len(vals) else None
+    return UserDefinedFunction(f, T.StringType(), name="elt")(*inputs)
+
+
+def get(col: ColumnOrName, index) -> Column:
+    """Array element at a 0-based index, null when out of range."""
+    from .sqlparse import Subscript
+    ix = index if isinstance(index, Column) else Column(Lit(index))
+    return Column(Subscript(_c(col), ix._expr))
+
+
+def negate(c: ColumnOrName) -> Column:
+    return -Column(_c(c))
+
+
+def position(substr: ColumnOrName, str: ColumnOrName, start=None) -> Column:  # noqa: A002
+    """1-based position of ``substr`` in ``str`` at or after ``start`` (0 when absent)."""
+    args = [substr, str] + ([] if start is None else [start if isinstance(start, Column) else Column(Lit(start))])
+
+    def f(sub, s, st=1):
+        st = int(st)
+        if st < 1:
+            return 0
+        return builtins.str(s).find(builtins.str(sub), st - 1) + 1
+    return _host_map("position", args, f, T.IntegerType())
+
+
+def raise_error(errMsg) -> Column:
+    msg = errMsg._expr.value if isinstance(errMsg, Column) and isinstance(errMsg._expr, Lit) else errMsg
+
+    def impl(frame, args):
+        if frame._nrows:
+            raise RuntimeError(str(msg))
+        return ColumnData(np.empty(0, dtype=object), None, T.NullType())
+    return Column(Func("raise_error", [], impl))
+
+
+def assert_true(col: ColumnOrName, errMsg=None) -> Column:
+    def impl(frame, args):
+        from .dataframe import column_to_python
+        vals = column_to_python(args[0])
+        if any(not v for v in vals):
+            raise RuntimeError(str(errMsg) if errMsg is not None else f"'{args[0]}' is not true!")
+        return ColumnData(np.full(frame._nrows, None, dtype=object), np.zeros(frame._nrows, dtype=bool),
+                          T.NullType())
+    return Column(Func("assert_true", [_c(col)], impl))
+
+
+def str_to_map(text: ColumnOrName, pairDelim=None, keyValueDelim=None) -> Column:
+    pd_ = pairDelim._expr.value if isinstance(pairDelim, Column) else (pairDelim or ",")
+    kd = keyValueDelim._expr.value if isinstance(keyValueDelim, Column) else (keyValueDelim or ":")
+
+    def f(s):
+        out = {}
+        for part in re.split(pd_, str(s)):
+            kv = re.split(kd, part, maxsplit=1)
+            out[kv[0]] = kv[1] if len(kv) > 1 else None
+        return out
+    return _host_map("str_to_map", [text], f, T.MapType(T.StringType(), T.StringType()))
+
+
+def sha(col: ColumnOrName) -> Column:
+    from .functions_more import sha1
+    return sha1(col)
+
+
+def replace(src: ColumnOrName, search, replace=None) -> Column:  # noqa: A002
+    s_ = search._expr.value if isinstance(search, Column) else search
+    r_ = "" if replace is None else (replace._expr.value if isinstance(replace, Column) else replace)
+    return _host_map("replace", [src], lambda v: str(v).replace(s_, r_) if s_ else str(v), T.StringType())
+
+
+def regexp_extract_all(s: ColumnOrName, regexp, idx=1) -> Column:
+    rx = _rx(regexp)
+    i = idx._expr.value if isinstance(idx, Column) else int(idx)
+
+    def f(v):
+        return [(m.group(i) or "") for m in rx.finditer(str(v))]
+    return _host_map("regexp_extract_all", [s], f, T.ArrayType(T.StringType()))
+
+
+def call_function(funcName: str, *cols) -> Column:
+    """Call a built-in or registered function by name."""
+    from . import functions as F
+    from .functions import REGISTERED_UDFS
+    if funcName in REGISTERED_UDFS:
+        return REGISTERED_UDFS[funcName](*cols)
+    fn = getattr(F, funcName, None) or getattr(F, funcName.lower(), None)
+    if fn is None or not callable(fn):
+        raise ValueError(f"unknown function {funcName}")
+    return fn(*cols)
+
+
+def call_udf(udfName: str, *cols) -> Column:
+    from .functions import REGISTERED_UDFS
+    if udfName not in REGISTERED_UDFS:
+        raise ValueError(f"no registered UDF {udfName}")
+    return REGISTERED_UDFS[udfName](*cols)
+
+
+def _const_str(name, getter):
+    def impl(frame, args):
+        v = getter(frame)
+        out = np.empty(frame._nrows, dtype=object)
+        out[:] = v
+        return ColumnData(out, None, T.StringType())
+    return Column(Func(name, [], impl))
+
+
+def current_catalog() -> Column:
+    return _const_str("current_catalog", lambda f: "spark_catalog")
+
+
+def current_database() -> Column:
+    return _const_str("current_database", lambda f: f._session.catalog.currentDatabase())
+
+
+current_schema = current_database
+
+
+def _csv_line(vals, sep=","):
+    import csv
+    import io
+    buf = io.StringIO()
+    csv.writer(buf, delimiter=sep, lineterminator="").writerow(["" if v is None else v for v in vals])
+    return buf.getvalue()
+
+
+def to_csv(col: ColumnOrName, options=None) -> Column:
+    from .types import Row
+    sep = (options or {}).get("sep", ",")
+
+    def f(v):
+        vals = list(v.asDict().values()) if isinstance(v, Row) else list(v.values()) if isinstance(v, dict) \
+            else list(v)
+        return _csv_line(vals, sep)
+    return _host_map("to_csv", [col], f, T.StringType())
+
+
+def from_csv(col: ColumnOrName, schema, options=None) -> Column:
+    import csv
+    from .functions_extra import _typed
+    from .types import Row
+    dt = T.parse_ddl_schema(schema) if isinstance(schema, str) else schema
+    if isinstance(schema, Column):
+        dt = T.parse_ddl_schema(schema._expr.value)
+    sep = (options or {}).get("sep", ",")
+
+    def f(s):
+        fields = next(csv.reader([str(s)], delimiter=sep), [])
+        vals = {}
+        for i, fl in enumerate(dt.fields):
+            raw = fields[i] if i < len(fields) else None
+            vals[fl.name] = None if raw in (None, "") else _typed(_parse_scalar(raw, fl.dataType), fl.dataType)
+        return Row(**vals)
+    return _host_map("from_csv", [col], f, dt)
+
+
+def _parse_scalar(raw: str, dt):
+    try:
+        if T.is_integral(dt):
+            return int(raw)
+        if isinstance(dt, (T.DoubleType, T.FloatType)):
+            return float(raw)
+        if isinstance(dt, T.BooleanType):
+            return raw.strip().lower() == "true"
+    except ValueError:
+        return None
+    return raw
+
+
+def schema_of_csv(csv_str, options=None) -> Column:
+    text = csv_str._expr.value if isinstance(csv_str, Column) else str(csv_str)
+    import csv
+    sep = (options or {}).get("sep", ",")
+    fields = next(csv.reader([text], delimiter=sep), [])
+
+    def kind(x):
+        for cast, name in ((int, "INT"), (float, "DOUBLE")):
+            try:
+                cast(x)
+                return name
+            except ValueError:
+                pass
+        return "BOOLEAN" if x.lower() in ("true", "false") else "STRING"
+    ddl = "STRUCT<" + ", ".join(f"_c{i}: {kind(x)}" for i, x in enumerate(fields)) + ">"
+    return _const_str("schema_of_csv", lambda f: ddl)
+
+
+class _PartitionTransform(Func):
+    """``years`` / ``months`` / ``days`` / ``hours`` / ``bucket`` partition transforms
+    (``writeTo(...).partitionedBy``); evaluated they give the partition value."""
+
+    def __init__(self, kind, child, n=None):
+        super().__init__(kind, [child], None)
+        self.kind, self.n = kind, n
+
+    def eval(self, frame):
+        cd = self.args[0].eval(frame)
+        if self.kind == "bucket":
+            from .hashing import device_hash
+            h = device_hash([cd], 42) if not cd.is_host else None
+            if h is None:
+                from .functions_extra import hash as _hash
+                h = _hash(Column(self.args[0]))._expr.eval(frame).values
+            return ColumnData(torch.remainder(h.to(torch.int64), self.n).to(torch.int32), cd.valid, T.IntegerType())
+        us = cd.values.to(torch.int64) * (86_400_000_000 if isinstance(cd.dtype, T.DateType) else 1)
+        if self.kind == "hours":
+            return ColumnData(torch.div(us, 3_600_000_000, rounding_mode="floor").to(torch.int32), cd.valid,
+                              T.IntegerType())
+        days = torch.div(us, 86_400_000_000, rounding_mode="floor")
+        if self.kind == "days":
+            return ColumnData(days.to(torch.int32), cd.valid, T.DateType())
+        d = np.asarray(days.cpu().numpy(), dtype="datetime64[D]")
+        y = d.astype("datetime64[Y]").astype(np.int64)
+        if self.kind == "years":
+            return ColumnData(torch.as_tensor(y.astype(np.int32), device=cd.values.device), cd.valid,
+                              T.IntegerType())
+        m = d.astype("datetime64[M]").astype(np.int64)
+        return ColumnData(torch.as_tensor(m.astype(np.int32), device=cd.values.device), cd.valid, T.IntegerType())
+
+
+def years(col: ColumnOrName) -> Column:
+    return Column(_PartitionTransform("years", _c(col)))
+
+
+def months(col: ColumnOrName) -> Column:
+    return Column(_PartitionTransform("months", _c(col)))
+
+
+def days(col: ColumnOrName) -> Column:
+    return Column(_PartitionTransform("days", _c(col)))
+
+
+def hours(col: ColumnOrName) -> Column:
+    return Column(_PartitionTransform("hours", _c(col)))
+
+
+def bucket(numBuckets, col: ColumnOrName) -> Column:
+    n = numBuckets._expr.value if isinstance(numBuckets, Column) else int(numBuckets)
+    return Column(_PartitionTransform("bucket", _c(col), n))
+
+
+def to_timestamp_ltz(timestamp: ColumnOrName, format=None) -> Column:  # noqa: A002
+    from .functions import to_timestamp
+    return to_timestamp(timestamp, format._expr.value if isinstance(format, Column) else format)
+
+
+to_timestamp_ntz = to_timestamp_ltz
+
+
+def make_timestamp_ltz(years, months, days, hours, mins, secs, timezone=None) -> Column:
+    from .functions_extra import make_timestamp
+    return make_timestamp(years, months, days, hours, mins, secs, timezone)
+
+
+def make_timestamp_ntz(years, months, days, hours, mins, secs) -> Column:
+    from .functions_extra import make_timestamp
+    return make_timestamp(years, months, days, hours, mins, secs)
+
+
+def to_unix_timestamp(timestamp: ColumnOrName, format=None) -> Column:  # noqa: A002
+    from .functions import unix_timestamp
+    return unix_timestamp(timestamp, format._expr.value if isinstance(format, Column) else format)
+
+
+class _HistogramNumeric(_HostValuesAgg):
+    """``histogram_numeric(col, nBins)``: Spark's streaming histogram (Ben-Haim & Tom-Tov): merge the
+    two closest centroids until ``nBins`` remain; result array<struct<x, y>>."""
+
+    def result_type(self):
+        return T.ArrayType(T.StructType([T.StructField("x", T.DoubleType()), T.StructField("y", T.DoubleType())]))
+
+    def merge(self, parts):
+        from .types import Row
+        vals = [v for p in parts for v in p]
+        if not vals:
+            return None
+        nb = int(self.arg)
+        pts = {}
+        for v in vals:
+            pts[float(v)] = pts.get(float(v), 0.0) + 1.0
+        cs = sorted(pts.items())
+        while len(cs) > nb:
+            i = builtins.min(range(len(cs) - 1), key=lambda j: cs[j + 1][0] - cs[j][0])
+            (x1, y1), (x2, y2) = cs[i], cs[i + 1]
+            cs[i:i + 2] = [((x1 * y1 + x2 * y2) / (y1 + y2), y1 + y2)]
+        return [Row(x=x, y=y) for x, y in cs]
+
+
+def histogram_numeric(col: ColumnOrName, nBins) -> Column:
+    n = nBins._expr.value if isinstance(nBins, Column) else int(nBins)
+    a = _HistogramNumeric("histogram_numeric", _c(col))
+    a.arg = n
+    return Column(a)
+
+
+def nth_value(col: ColumnOrName, offset: int, ignoreNulls: bool = False) -> Column:
+    """Window function: the ``offset``-th value (1-based) of the window frame, null if it has fewer rows."""
+    from .window import WindowFunc
+    return Column(WindowFunc("nth_value", _c(col), int(offset), bool(ignoreNulls)))
+
+
 __all__ = [n for n in dir() if not n.startswith("_") and n not in (
     "annotations", "builtins", "getpass", "math", "np", "re", "torch", "T", "Any", "List", "Optional", "urllib",
     "AggExpr", "Column", "ColumnData", "Func", "Lit", "UserDefinedFunction", "ColumnOrName")]

@@ -110,6 +110,8 @@ class WindowFunc(Expr):
             inner += f", {self.arg}, {self.default}"
         elif self.fn == "ntile":
             inner = str(self.arg)
+        elif self.fn == "nth_value":
+            inner += f", {self.arg}" + (", true" if self.default else "")
         return f"{self.fn}({inner})"
 
     def eval(self, frame):
@@ -234,13 +236,30 @@ def _evaluate(func, spec: WindowSpec, pk, ok, arg, n: int) -> list:
         idx = perm[a:b]
         ov = okey[a:b]
         m = b - a
-        if isinstance(func, WindowFunc):
+        if isinstance(func, WindowFunc) and fn == "nth_value":
+            res = _nth_value(func, spec, ov, [arg[i] for i in idx], m)
+        elif isinstance(func, WindowFunc):
             res = _rank_like(func, ov, [arg[i] for i in idx] if arg is not None else None, m)
         else:
             res = _frame_agg(fn, spec, ov, [arg[i] for i in idx] if arg is not None else [1] * m, m,
                              count_star=func.child is None)
         for j, i in enumerate(idx):
             out[i] = res[j]
+    return out
+
+
+def _nth_value(func: WindowFunc, spec: WindowSpec, ov: list, vals: list, m: int) -> list:
+    """``nth_value(col, k[, ignoreNulls])``: the k-th (non-null) value of each row's frame."""
+    k, skip_nulls = int(func.arg), bool(func.default)
+    lo, hi = _frame_bounds(spec, ov, m)
+    out = []
+    for i in range(m):
+        if skip_nulls:
+            seen = [v for v in vals[lo[i]:hi[i] + 1] if v is not None]
+            out.append(seen[k - 1] if len(seen) >= k else None)
+        else:
+            j = lo[i] + k - 1
+            out.append(vals[j] if j <= hi[i] else None)
     return out
 
 

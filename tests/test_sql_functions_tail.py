@@ -95,3 +95,27 @@ def test_timestamp_arithmetic(spark):
     assert r[8] == dt.datetime(2016, 3, 11, 0, 0, 7)
     assert r[9] == (dt.date(2024, 4, 1) - dt.date(2016, 3, 11)).days
     assert len(spark.range(3).select(F.uuid()).collect()[0][0]) == 36
+
+
+def test_string_functions_per_distinct_on_dictionary_columns(monkeypatch):
+    """Row functions over a dictionary-encoded column run once per distinct value and give the
+    same rows as the per-row evaluation."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession, builder
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as Fm
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.column import DictColumnData
+    s = SparkSession.builder.master("local[1]").getOrCreate()
+    rows = [(["icu-a", "er-b", None, "gen-c", "icu-d"][i % 5], i) for i in range(3000)]
+    monkeypatch.setattr(Fm, "_DISTINCT_MIN_ROWS", 16)
+    monkeypatch.setattr(builder, "DICT_MIN_ROWS", 16)
+    dd = s.createDataFrame(rows, "w string, i int")
+    assert isinstance(dd._cols["w"], DictColumnData)
+    monkeypatch.setattr(builder, "DICT_MIN_ROWS", 1 << 30)
+    plain = s.createDataFrame(rows, "w string, i int")
+    q = lambda d: [tuple(r) for r in d.select(F.upper("w"), F.col("w").startswith("icu"), F.length("w"),  # noqa
+                                                F.regexp_replace("w", "-", "_"), F.col("w").like("%-_"),
+                                                F.substring("w", 2, 3)).collect()]
+    assert q(dd) == q(plain)
+    out = dd.select(F.regexp_replace("w", "-", "_").alias("u"))
+    assert isinstance(out._cols["u"], DictColumnData)
+    assert dd.filter(F.col("w").contains("icu")).count() == 1200
