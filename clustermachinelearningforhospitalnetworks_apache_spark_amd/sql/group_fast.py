@@ -26,6 +26,7 @@ import numpy as np
 import torch
 
 from . import types as T
+from ..ops.group_ops import group_reduce
 from .column import AggExpr, ColRef, ColumnData
 
 _FAST_FNS = {"count", "sum", "avg", "min", "max", "stddev", "stddev_pop", "variance", "var_pop", "first", "last"}
@@ -252,53 +253,40 @@ def tensor_partials(df, keys, exprs) -> Optional[TensorPartials]:
             if vals.is_floating_point():
                 nn = ~torch.isnan(vals)
                 vm = nn if vm is None else vm & nn
+        # per-group reductions: K25 group_reduce (LDS-privatised, few groups) on the GPU, torch
+        # scatter otherwise; masked-off entries (nulls, NaN) are skipped
         if vm is None:
             if all_count is None:
                 all_count = torch.bincount(gid, minlength=G)
             cnt = all_count
         else:
-            cnt = torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, gid, vm.to(torch.int64))
+            cnt = group_reduce(gid, vm.to(torch.uint8), G, "sum", floating=False)
         if fn == "count":
             parts.append({"kind": "n", "cnt": cnt})
             continue
         if fn in ("min", "max"):
-            if vals.is_floating_point():
-                fill = float("inf") if fn == "min" else float("-inf")
-            else:
-                info = torch.iinfo(vals.dtype)
-                fill = info.max if fn == "min" else info.min
-            v = vals if vm is None else torch.where(vm, vals, torch.full_like(vals, fill))
-            out = torch.full((G,), fill, dtype=vals.dtype, device=dev)
-            out.scatter_reduce_(0, gid, v, "amin" if fn == "min" else "amax", include_self=True)
+            out = group_reduce(gid, vals, G, fn, mask=vm)
+            if out.dtype != vals.dtype:
+                if not vals.is_floating_point():
+                    info = torch.iinfo(vals.dtype)
+                    out = out.clamp(info.min, info.max)
+                out = out.to(vals.dtype)
             parts.append({"kind": fn, "cnt": cnt, "val": out, "cd": cd})
             continue
         if fn in ("first", "last"):
-            pos = torch.arange(m, device=dev)
-            fill = m if fn == "first" else -1
-            if vm is not None:
-                pos = torch.where(vm, pos, torch.full_like(pos, fill))
-            pick = torch.full((G,), fill, dtype=torch.int64, device=dev)
-            pick.scatter_reduce_(0, gid, pos, "amin" if fn == "first" else "amax", include_self=True)
+            pick = group_reduce(gid, None, G, "min" if fn == "first" else "max", mask=vm, floating=False)
             pick = pick.clamp(0, m - 1)
             parts.append({"kind": fn, "cnt": cnt, "rows": pick if src is None else src[pick], "cd": cd})
             continue
         # sum / avg / variance family
         if fn == "sum" and T.is_integral(cd.dtype):
-            v = vals.to(torch.int64)
-            if vm is not None:
-                v = torch.where(vm, v, torch.zeros_like(v))
-            parts.append({"kind": "isum", "cnt": cnt,
-                          "sum": torch.zeros(G, dtype=torch.int64, device=dev).index_add_(0, gid, v)})
+            parts.append({"kind": "isum", "cnt": cnt, "sum": group_reduce(gid, vals, G, "sum", mask=vm,
+                                                                          floating=False)})
             continue
-        v = vals.to(torch.float64)
-        if vm is not None:
-            v = torch.where(vm, v, torch.zeros_like(v))
-        s = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, v)
+        s = group_reduce(gid, vals, G, "sum", mask=vm, floating=True)
         mu = s / cnt.clamp(min=1).to(torch.float64)
-        d = v - mu[gid]
-        if vm is not None:
-            d = torch.where(vm, d, torch.zeros_like(d))
-        m2 = torch.zeros(G, dtype=torch.float64, device=dev).index_add_(0, gid, d * d)
+        d = vals.to(torch.float64) - mu[gid]
+        m2 = group_reduce(gid, d * d, G, "sum", mask=vm, floating=True)
         parts.append({"kind": "mom", "cnt": cnt, "sum": s, "mu": mu, "m2": m2})
     return TensorPartials(specs=specs, key_types=key_types, keys=keys, key_cols=key_cols, G=G, gid=gid,
                           first=first, first_rows=first_rows, src=src, win_start=win_start, n=n, m=m, parts=parts)
