@@ -207,8 +207,7 @@ def tensor_partials(df, keys, exprs) -> Optional[TensorPartials]:
         else:
             _, inv = torch.unique(torch.stack([c for c, _ in key_codes], 1), dim=0, return_inverse=True)
         G = int(inv.max()) + 1
-        pos = torch.arange(m, device=dev)
-        first = torch.full((G,), m, dtype=torch.int64, device=dev).scatter_reduce_(0, inv, pos, "amin")
+        first = group_reduce(inv, None, G, "min", floating=False)  # first entry of every group
         order = torch.argsort(first)
         rank = torch.empty_like(order)
         rank[order] = torch.arange(G, device=dev)

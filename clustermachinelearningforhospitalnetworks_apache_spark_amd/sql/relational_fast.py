@@ -365,8 +365,8 @@ def _first_of(code: torch.Tensor, key: torch.Tensor) -> torch.Tensor:
     """Bool mask of the rows holding the smallest ``key`` of their code."""
     n = code.numel()
     card = int(code.max()) + 1 if n else 0
-    best = torch.full((card,), torch.iinfo(torch.int64).max, dtype=torch.int64, device=code.device)
-    best.scatter_reduce_(0, code, key, reduce="amin")
+    from ..ops.group_ops import group_reduce
+    best = group_reduce(code, key.to(torch.int64), card, "min", floating=False)
     return best[code] == key
 
 

@@ -289,10 +289,9 @@ def device_window(frame, func, spec) -> Optional[ColumnData]:
             else:
                 okx = ok
                 fill = torch.iinfo(torch.int64).max if fn == "min" else torch.iinfo(torch.int64).min
-            xv = torch.where(okx, x, torch.full_like(x, fill))
-            red = torch.full((nseg,), fill, dtype=x.dtype, device=dev)
-            red.scatter_reduce_(0, sid, xv, "amin" if fn == "min" else "amax", include_self=True)
-            has = torch.zeros(nseg, dtype=torch.int64, device=dev).index_add_(0, sid, okx.to(torch.int64)) > 0
+            from ..ops.group_ops import group_reduce
+            red = group_reduce(sid, x, nseg, fn, mask=okx)  # K25 on the GPU for few partitions
+            has = group_reduce(sid, okx.to(torch.uint8), nseg, "sum", floating=False) > 0
             res = red[sid].to(vs.dtype)
             res_valid = has[sid]
             out_type = in_type
