@@ -43,7 +43,7 @@ __device__ __forceinline__ T combine(T a, T b) {
 }
 
 template <typename T, int VT>
-__device__ __forceinline__ T load_val(const void* vals, long long r) {
+__device__ __forceinline__ T load_val(const void* vals, long long r) {  // VT != kRowIndex
   if constexpr (VT == kF64) return (T)static_cast<const double*>(vals)[r];
   else if constexpr (VT == kF32) return (T)static_cast<const float*>(vals)[r];
   else if constexpr (VT == kI32) return (T)static_cast<const int*>(vals)[r];
@@ -52,21 +52,29 @@ __device__ __forceinline__ T load_val(const void* vals, long long r) {
   else return (T)r;
 }
 
-template <typename T, int VT, int OP>
+// Elements e in [0, n * d): row e / d, column e % d, accumulator slot gid[row] * d + column (d > 1:
+// the per-group column sums of a row-major [n, d] matrix, read coalesced). G counts slots (groups * d).
+template <typename T, int VT, int OP, bool MULTI>
 __global__ __launch_bounds__(kThreads) void group_reduce_kernel(const int* __restrict__ gid, const void* __restrict__ vals,
-                                                                const unsigned char* __restrict__ mask, long long n, int G,
-                                                                long long rows_per_block, T ident,
+                                                                const unsigned char* __restrict__ mask, long long n, int d,
+                                                                int G, long long rows_per_block, T ident,
                                                                 T* __restrict__ partial) {
   extern __shared__ __align__(16) unsigned char smem[];
   T* acc = reinterpret_cast<T*>(smem);  // [kWaves][G]
   for (int i = threadIdx.x; i < kWaves * G; i += kThreads) acc[i] = ident;
   __syncthreads();
   T* mine = acc + (size_t)(threadIdx.x >> 6) * G;
+  const long long ne = MULTI ? n * d : n;
   const long long start = (long long)blockIdx.x * rows_per_block;
-  const long long end = start + rows_per_block < n ? start + rows_per_block : n;
-  for (long long r = start + threadIdx.x; r < end; r += kThreads) {
+  const long long end = start + rows_per_block < ne ? start + rows_per_block : ne;
+  for (long long e = start + threadIdx.x; e < end; e += kThreads) {
+    const long long r = MULTI ? e / d : e;
     if (mask != nullptr && mask[r] == 0) continue;
-    lds_apply<T, OP>(mine + gid[r], load_val<T, VT>(vals, r));
+    const int slot = MULTI ? gid[r] * d + (int)(e - r * d) : gid[r];
+    T v;
+    if constexpr (VT == kRowIndex) v = (T)r;
+    else v = load_val<T, VT>(vals, e);
+    lds_apply<T, OP>(mine + slot, v);
   }
   __syncthreads();
   for (int g = threadIdx.x; g < G; g += kThreads) {
@@ -96,26 +104,30 @@ __global__ __launch_bounds__(kThreads) void group_reduce_final_kernel(const T* _
 }
 
 template <typename T, int VT, int OP>
-int launch(const int* gid, const void* vals, const unsigned char* mask, long long n, int G, long long rpb, long long nb,
-           T ident, T* scratch, T* out, hipStream_t st) {
+int launch(const int* gid, const void* vals, const unsigned char* mask, long long n, int d, int G, long long rpb,
+           long long nb, T ident, T* scratch, T* out, hipStream_t st) {
   const size_t lds = (size_t)kWaves * G * sizeof(T);
-  hipLaunchKernelGGL((group_reduce_kernel<T, VT, OP>), dim3((unsigned)nb), dim3(kThreads), lds, st, gid, vals, mask, n,
-                     G, rpb, ident, scratch);
+  if (d > 1)
+    hipLaunchKernelGGL((group_reduce_kernel<T, VT, OP, true>), dim3((unsigned)nb), dim3(kThreads), lds, st, gid, vals,
+                       mask, n, d, G, rpb, ident, scratch);
+  else
+    hipLaunchKernelGGL((group_reduce_kernel<T, VT, OP, false>), dim3((unsigned)nb), dim3(kThreads), lds, st, gid, vals,
+                       mask, n, 1, G, rpb, ident, scratch);
   hipLaunchKernelGGL((group_reduce_final_kernel<T, OP>), dim3((unsigned)G), dim3(kThreads), 0, st, scratch, nb, G,
                      ident, out);
   return cml_status();
 }
 
 template <typename T, int OP>
-int by_type(int vtype, const int* gid, const void* vals, const unsigned char* mask, long long n, int G, long long rpb,
-            long long nb, T ident, T* scratch, T* out, hipStream_t st) {
+int by_type(int vtype, const int* gid, const void* vals, const unsigned char* mask, long long n, int d, int G,
+            long long rpb, long long nb, T ident, T* scratch, T* out, hipStream_t st) {
   switch (vtype) {
-    case kF64: return launch<T, kF64, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
-    case kF32: return launch<T, kF32, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
-    case kI32: return launch<T, kI32, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
-    case kI64: return launch<T, kI64, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
-    case kU8: return launch<T, kU8, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
-    case kRowIndex: return launch<T, kRowIndex, OP>(gid, vals, mask, n, G, rpb, nb, ident, scratch, out, st);
+    case kF64: return launch<T, kF64, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
+    case kF32: return launch<T, kF32, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
+    case kI32: return launch<T, kI32, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
+    case kI64: return launch<T, kI64, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
+    case kU8: return launch<T, kU8, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
+    case kRowIndex: return launch<T, kRowIndex, OP>(gid, vals, mask, n, d, G, rpb, nb, ident, scratch, out, st);
     default: return (int)hipErrorInvalidValue;
   }
 }
@@ -125,29 +137,31 @@ int by_type(int vtype, const int* gid, const void* vals, const unsigned char* ma
 // Largest group count the LDS-privatised path takes (4 wave copies of G 8-byte accumulators).
 CML_API int cml_group_reduce_max_groups() { return 2048; }
 
-// out[g] = op over rows r with gid[r] == g (and mask[r] != 0) of vals[r]; acc: 0 = f64, 1 = i64.
-// scratch holds nb * G accumulators; rows_per_block * nb >= n.
-CML_API int cml_group_reduce(const int* gid, const void* vals, int vtype, const unsigned char* mask, long long n, int G,
-                             int op, int acc, long long rows_per_block, long long nb, void* scratch, void* out,
+// out[g * d + j] = op over rows r with gid[r] == g (and mask[r] != 0) of vals[r * d + j]; acc: 0 = f64,
+// 1 = i64. G counts accumulator slots (groups * d); scratch holds nb * G of them; every block covers
+// rows_per_block elements and rows_per_block * nb >= n * d.
+CML_API int cml_group_reduce(const int* gid, const void* vals, int vtype, const unsigned char* mask, long long n, int d,
+                             int G, int op, int acc, long long rows_per_block, long long nb, void* scratch, void* out,
                              void* stream) {
-  if (G <= 0 || G > 2048 || nb <= 0 || rows_per_block * nb < n) return (int)hipErrorInvalidValue;
+  if (G <= 0 || G > 2048 || d <= 0 || G % d != 0 || nb <= 0 || rows_per_block * nb < n * d)
+    return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   if (acc == 0) {
     double* s = (double*)scratch;
     double* o = (double*)out;
     switch (op) {
-      case kSum: return by_type<double, kSum>(vtype, gid, vals, mask, n, G, rows_per_block, nb, 0.0, s, o, st);
-      case kMin: return by_type<double, kMin>(vtype, gid, vals, mask, n, G, rows_per_block, nb, __builtin_inf(), s, o, st);
-      case kMax: return by_type<double, kMax>(vtype, gid, vals, mask, n, G, rows_per_block, nb, -__builtin_inf(), s, o, st);
+      case kSum: return by_type<double, kSum>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, 0.0, s, o, st);
+      case kMin: return by_type<double, kMin>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, __builtin_inf(), s, o, st);
+      case kMax: return by_type<double, kMax>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, -__builtin_inf(), s, o, st);
       default: return (int)hipErrorInvalidValue;
     }
   }
   long long* s = (long long*)scratch;
   long long* o = (long long*)out;
   switch (op) {
-    case kSum: return by_type<long long, kSum>(vtype, gid, vals, mask, n, G, rows_per_block, nb, 0LL, s, o, st);
-    case kMin: return by_type<long long, kMin>(vtype, gid, vals, mask, n, G, rows_per_block, nb, (long long)0x7FFFFFFFFFFFFFFFLL, s, o, st);
-    case kMax: return by_type<long long, kMax>(vtype, gid, vals, mask, n, G, rows_per_block, nb, (long long)(-0x7FFFFFFFFFFFFFFFLL - 1), s, o, st);
+    case kSum: return by_type<long long, kSum>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, 0LL, s, o, st);
+    case kMin: return by_type<long long, kMin>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, (long long)0x7FFFFFFFFFFFFFFFLL, s, o, st);
+    case kMax: return by_type<long long, kMax>(vtype, gid, vals, mask, n, d, G, rows_per_block, nb, (long long)(-0x7FFFFFFFFFFFFFFFLL - 1), s, o, st);
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -259,9 +259,10 @@ class ClusteringEvaluator(Evaluator):
         cnt = torch.zeros(K, dtype=torch.float64, device=x.device)
         sq = torch.zeros(K, dtype=torch.float64, device=x.device)
         if lab.numel():
-            sums.index_add_(0, lab, x)
-            cnt.index_add_(0, lab, torch.ones_like(lab, dtype=torch.float64))
-            sq.index_add_(0, lab, (x * x).sum(1))
+            from ..ops.group_ops import group_reduce, group_sum_rows  # K25 on the GPU (few clusters)
+            sums = group_sum_rows(lab, x, K)
+            cnt = group_reduce(lab, torch.ones_like(lab, dtype=torch.uint8), K, "sum", floating=True)
+            sq = group_reduce(lab, (x * x).sum(1), K, "sum")
         msg = torch.cat([sums.reshape(-1), cnt, sq])
         df._comm.allreduce_(msg)
         sums = msg[: K * d].reshape(K, d)

@@ -65,8 +65,10 @@ class NaiveBayes(Estimator):
         msg = torch.zeros(C * (d + 1), dtype=torch.float64, device=x.device)
         sums = msg[:C * d].view(C, d)
         cnt = msg[C * d:]
-        sums.index_add_(0, yi, x * w[:, None])
-        cnt.index_add_(0, yi, w)
+        from ..ops.group_ops import group_reduce, group_sum_rows  # K25 on the GPU (few classes)
+        if yi.numel():
+            sums.copy_(group_sum_rows(yi, x * w[:, None], C))
+            cnt.copy_(group_reduce(yi, w, C, "sum", floating=True))
         comm.allreduce_(msg)
         S, n = sums.cpu().numpy(), cnt.cpu().numpy()
         lam = self.getSmoothing()
@@ -77,7 +79,8 @@ class NaiveBayes(Estimator):
             mean = S / nz[:, None]
             mean_t = torch.as_tensor(mean, device=x.device)
             sq = torch.zeros(C * d, dtype=torch.float64, device=x.device).view(C, d)
-            sq.index_add_(0, yi, (x - mean_t[yi]) ** 2 * w[:, None])
+            if yi.numel():
+                sq.copy_(group_sum_rows(yi, (x - mean_t[yi]) ** 2 * w[:, None], C))
             comm.allreduce_(sq)
             var = sq.cpu().numpy() / nz[:, None]
             # Spark: epsilon = 1e-9 * max variance of any feature over all rows

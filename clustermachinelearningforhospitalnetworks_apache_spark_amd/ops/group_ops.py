@@ -15,8 +15,8 @@ from .. import _native
 from .._native import c_int, c_ll, c_vp
 
 _native.register_kernel_sigs({
-    "cml_group_reduce": (c_int, [c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_int, c_ll, c_ll, c_vp, c_vp,
-                                 c_vp]),
+    "cml_group_reduce": (c_int, [c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_int, c_int, c_ll, c_ll, c_vp,
+                                 c_vp, c_vp]),
     "cml_group_reduce_max_groups": (c_int, []),
 })
 
@@ -83,13 +83,43 @@ def group_reduce(gid: torch.Tensor, vals: Optional[torch.Tensor], G: int, op: st
         if mask.shape[0] != n:
             raise ValueError("group_reduce: gid and mask differ in length")
         mp = mask.data_ptr()
-    rpb = max(_ROWS_PER_BLOCK, -(-n // 65535))
-    nb = -(-n // rpb)
+    return _launch(gid32, vp, vt, mp, n, 1, G, op, floating)
+
+
+def _launch(gid32, vp, vt, mp, n: int, d: int, G: int, op: str, floating: bool) -> torch.Tensor:
+    ne = n * d
+    rpb = max(_ROWS_PER_BLOCK, -(-ne // 65535))
+    nb = -(-ne // rpb)
     dt = torch.float64 if floating else torch.int64
-    scratch = torch.empty(nb * G, dtype=dt, device=gid.device)
-    out = torch.empty(G, dtype=dt, device=gid.device)
-    stream = torch.cuda.current_stream(gid.device).cuda_stream
-    _native.check(_native.kernels().cml_group_reduce(gid32.data_ptr(), vp, vt, mp, n, G, _OPS[op],
+    slots = G * d
+    scratch = torch.empty(nb * slots, dtype=dt, device=gid32.device)
+    out = torch.empty(slots, dtype=dt, device=gid32.device)
+    stream = torch.cuda.current_stream(gid32.device).cuda_stream
+    _native.check(_native.kernels().cml_group_reduce(gid32.data_ptr(), vp, vt, mp, n, d, slots, _OPS[op],
                                                      0 if floating else 1, rpb, nb, scratch.data_ptr(),
                                                      out.data_ptr(), stream), "group_reduce")
     return out
+
+
+def group_sum_rows(gid: torch.Tensor, x: torch.Tensor, G: int, mask: Optional[torch.Tensor] = None) -> torch.Tensor:
+    """[G, d] f64 per-group column sums of a row-major [n, d] matrix (class / cluster sums of the
+    evaluators and NaiveBayes): K25 over the n*d elements when G*d fits the LDS path."""
+    n, d = int(x.shape[0]), int(x.shape[1])
+    if not x.is_cuda or G * d > 2048 or n * d < _MIN_ROWS or G <= 0 or d == 0:
+        g = gid.to(torch.int64)
+        v = x.to(torch.float64)
+        if mask is not None:
+            v = torch.where(mask.to(torch.bool)[:, None], v, torch.zeros_like(v))
+        return torch.zeros(G, d, dtype=torch.float64, device=x.device).index_add_(0, g, v)
+    gid32 = (gid if gid.dtype == torch.int32 else gid.to(torch.int32)).contiguous()
+    lo, hi = torch.aminmax(gid32)
+    if int(lo) < 0 or int(hi) >= G:
+        raise ValueError(f"group_sum_rows: group ids outside [0, {G})")
+    x = x.contiguous()
+    if x.dtype not in (torch.float64, torch.float32):
+        x = x.to(torch.float64)
+    mp = None
+    if mask is not None:
+        mask = (mask.view(torch.uint8) if mask.dtype == torch.bool else mask.to(torch.uint8)).contiguous()
+        mp = mask.data_ptr()
+    return _launch(gid32, x.data_ptr(), _VTYPES[x.dtype], mp, n, d, G, "sum", True).view(G, d)

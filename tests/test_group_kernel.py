@@ -60,3 +60,20 @@ def test_group_reduce_rejects_out_of_range_ids():
     gid = torch.full((1 << 15,), 5, device="cuda", dtype=torch.int64)
     with pytest.raises(ValueError):
         group_ops.group_reduce(gid, torch.ones(1 << 15, device="cuda", dtype=torch.float64), 5, "sum")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("G,d", [(3, 4), (10, 128), (256, 8)])
+def test_group_sum_rows_matches_torch(G, d):
+    dev = torch.device("cuda")
+    gen = torch.Generator(device=dev).manual_seed(G * d)
+    n = 300_001
+    gid = torch.randint(0, G, (n,), device=dev, generator=gen)
+    for dt in (torch.float64, torch.float32):
+        x = torch.randn(n, d, device=dev, dtype=dt, generator=gen)
+        mask = torch.rand(n, device=dev, generator=gen) < 0.8
+        got = group_ops.group_sum_rows(gid, x, G, mask=mask)
+        ref = torch.zeros(G, d, dtype=torch.float64, device=dev).index_add_(
+            0, gid, torch.where(mask[:, None], x.double(), torch.zeros_like(x.double())))
+        torch.testing.assert_close(got, ref, rtol=1e-11, atol=1e-9)
+        assert torch.equal(got, group_ops.group_sum_rows(gid, x, G, mask=mask))
