@@ -38,6 +38,8 @@ from typing import Dict, List, Optional
 import numpy as np
 import torch
 
+from ..ops.group_ops import group_sum_rows
+
 from ..sql import types as T
 from ..sql.column import ColumnData
 from . import util as U
@@ -83,7 +85,7 @@ def _summarize(x: torch.Tensor, idx: torch.Tensor, keys: List[int], comm) -> Dic
             xs = x[r0:r0 + step][sel].to(torch.float64)
             part = torch.cat([xs, torch.ones((xs.shape[0], 1), dtype=torch.float64, device=x.device),
                               (xs * xs).sum(1, keepdim=True)], 1)
-            acc.index_add_(0, slot[sel], part)
+            acc += group_sum_rows(slot[sel], part, m)  # K25 per-cluster column sums on the GPU
     comm.allreduce_(acc)
     a = acc.cpu().numpy()
     out = {}
