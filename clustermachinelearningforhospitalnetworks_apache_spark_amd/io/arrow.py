@@ -143,7 +143,21 @@ def arrow_column_to_data(arr, dt: T.DataType, device) -> ColumnData:
         return ColumnData(torch.as_tensor(mat, device=device), None if valid_np is None else torch.as_tensor(
             valid_np, device=device), dt)
     if dt.torch_dtype is None or dt.host_only:
+        if isinstance(dt, T.StringType) and pa.types.is_dictionary(arr.type):
+            arr = arr.cast(arr.type.value_type)
         if isinstance(dt, T.StringType) and (pa.types.is_string(arr.type) or pa.types.is_large_string(arr.type)):
+            from ..sql.builder import DICT_MIN_ROWS
+            if n >= DICT_MIN_ROWS:
+                # repetitive strings (ids, wards, regions) stay dictionary-encoded: Arrow's hash
+                # encoder in C++, then int32 codes + the distinct strings (sql.column.DictColumnData)
+                enc = arr.dictionary_encode()
+                if 4 * len(enc.dictionary) <= n:
+                    from ..sql.column import DictColumnData
+                    codes = enc.indices.fill_null(-1).to_numpy(zero_copy_only=False).astype(np.int32)
+                    dictionary = np.empty(len(enc.dictionary) + 1, dtype=object)
+                    dictionary[:-1] = enc.dictionary.to_numpy(zero_copy_only=False)
+                    dictionary[-1] = None
+                    return DictColumnData(codes, dictionary, valid_np, dt)
             vals = arr.to_numpy(zero_copy_only=False)  # Arrow builds the str objects in C++
             if vals.dtype != object:
                 vals = vals.astype(object)

@@ -43,3 +43,16 @@ def test_text_format(spark, tmp_path):
     assert sorted(r.value for r in back.collect()) == ["first line", "second"]
     with pytest.raises(ValueError):
         spark.createDataFrame([(1, 2)], "a INT, b INT").write.text(str(tmp_path / "t2"))
+
+
+def test_parquet_strings_dictionary_encoded_on_read(tmp_path, monkeypatch):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession, builder
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.column import DictColumnData
+    s = SparkSession.builder.master("local[1]").getOrCreate()
+    rows = [([None, "H1", "H2", "H3"][i % 4], i) for i in range(400)]
+    s.createDataFrame(rows, "h string, i int").write.mode("overwrite").parquet(str(tmp_path / "p"))
+    monkeypatch.setattr(builder, "DICT_MIN_ROWS", 16)
+    df = s.read.parquet(str(tmp_path / "p"))
+    assert isinstance(df._cols["h"], DictColumnData)
+    assert sorted((r.h or "", r.i) for r in df.collect()) == sorted((h or "", i) for h, i in rows)
+    assert df.na.drop().count() == 300 and df.groupBy("h").count().count() == 4
