@@ -58,6 +58,9 @@ def main():
     ap.add_argument("--k", type=int, default=256)
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
+    ap.add_argument("--prune", action="store_true",
+                    help="time the exact bound-pruned Lloyd step (LloydEngine(prune=True)) instead of the full "
+                         "assignment; without it the pruned step is still reported in extra")
     ap.add_argument("--full-accumulate", action="store_true",
                     help="re-accumulate every row each step instead of the exact incremental sums")
     ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv"],
@@ -99,7 +102,8 @@ def main():
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
 
-    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks, incremental=not args.full_accumulate)
+    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks, incremental=not args.full_accumulate,
+                      prune=args.prune)
     t0 = time.perf_counter()
     init = eng.init_kmeans_parallel(seed=42) if args.init == "k-means||" else eng.init_random(seed=42)
     eng.set_centers(init)
@@ -121,7 +125,30 @@ def main():
     elapsed = time.perf_counter() - t0
     elapsed = comm.max_scalar(elapsed)
     cost = eng.training_cost()
-    acc = {"accumulate": "incremental (exact)" if eng.delta is not None else "full"}
+    acc = {"accumulate": "incremental (exact)" if eng.delta is not None else "full",
+           "assign": "pruned (exact bounds)" if args.prune else "full (every row x every centre)"}
+    if args.prune:
+        acc["last_step_prune_rank0"] = eng.prune_stats()
+    elif gpu:
+        # the exact bound-pruned step (LloydEngine(prune=True)) from the same start, same step count:
+        # its ms/step and whether its labels equal the full step's after warmup + steps iterations
+        lab_full = eng.labels[: eng.n].clone()
+        pe = LloydEngine(x, args.dim, args.k, comm, prune=True)
+        pe.set_centers(init)
+        for _ in range(args.warmup):
+            pe.step()
+        comm.barrier()
+        torch.cuda.synchronize()
+        t1 = time.perf_counter()
+        for _ in range(args.steps):
+            pe.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        acc["pruned_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - t1) / args.steps
+        same = float(torch.equal(pe.labels[: pe.n], lab_full))
+        acc["pruned_labels_equal_full"] = comm.max_scalar(1.0 - same) == 0.0
+        acc["pruned_last_step_rank0"] = pe.prune_stats()
+        del pe, lab_full
     if eng.delta is not None and gpu:
         # transparency: the same steps with every step forced to re-accumulate all rows
         acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()

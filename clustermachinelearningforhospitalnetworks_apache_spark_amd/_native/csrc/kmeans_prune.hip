@@ -1,0 +1,131 @@
+// K9p: bounds pass of the exact pruned Lloyd step (models/kmeans.py ``LloydEngine(prune=True)``).
+//
+// Spark's EuclideanDistanceMeasure.findClosest (mllib/clustering/DistanceMeasure.scala) skips a
+// centre when the triangle inequality proves it cannot be the closest one (centre-to-centre
+// distances precomputed once per iteration). This is the same idea carried across iterations
+// (Hamerly's upper bound + half the distance to the nearest other centre):
+//
+//   ub[i] >= ||x_i - c_{a(i)}||  (a(i) = current label), lb[i] <= min_{j != a(i)} ||x_i - c_j||,
+//   kept per row in HBM (8 B / row);
+//   after a centre update:  ub[i] += drift[a(i)], lb[i] -= max_{j != a(i)} drift[j]
+//   (drift[j] = ||c_j_new - c_j_old||; ub rounded up, lb rounded down);
+//   the label provably stays if ub[i] <= thr[a(i)] (thr[j] = half the distance from c_j to its
+//   nearest other centre less a slack) or ub[i] <= lb[i] - c2 / lb[i]. Both slacks keep the
+//   squared-distance gap above twice the f32 error of the full assign's MFMA distance, so the full
+//   assign would pick the same centre. Such rows are not read at all; every other row is appended
+//   to `cand` and re-assigned against all centres by K9 on a gathered copy.
+//
+// One pass reads 12 B and writes 8 B per row (100M rows: 2 GB, ~0.35 ms at HBM speed) instead of
+// the 51 GB X stream of the full assign. Rows are read 4 per lane with 16-byte loads; each block
+// compacts its candidates through one LDS scan and one global atomic (the candidate ORDER depends
+// on block scheduling, the candidate SET does not; everything downstream is per-row or an exact
+// f64 sum, so results do not depend on it).
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block
+
+// Moves one row's bounds to the new centres; true when they still prove its label.
+__device__ __forceinline__ bool bound_step(int a, float& u, float& w, const float* sd, const float* st, float dm1,
+                                           float dm2, int jm, float c2) {
+  u = (u + sd[a]) * (1.0f + 2.4e-7f);                           // rounded up (inf stays inf)
+  w = fmaxf((w - (a == jm ? dm2 : dm1)) * (1.0f - 2.4e-7f), 0.f);  // rounded down
+  const float lt = w > 0.f ? (w - c2 / w) * (1.0f - 1e-6f) : -1.f;
+  return u <= st[a] || u <= lt;
+}
+
+__global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
+                                                                       float* __restrict__ ub,
+                                                                       float* __restrict__ lb,
+                                                                       const float* __restrict__ drift,
+                                                                       const float* __restrict__ dmax,
+                                                                       const float* __restrict__ thr, float c2,
+                                                                       int k, long long n, int* __restrict__ cand,
+                                                                       int* __restrict__ count) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  float* sd = reinterpret_cast<float*>(smem);  // [k] drift
+  float* st = sd + k;                          // [k] threshold
+  __shared__ int wsum[kThreads / 64];
+  __shared__ int base;
+  for (int i = threadIdx.x; i < k; i += kThreads) {
+    sd[i] = drift[i];
+    st[i] = thr[i];
+  }
+  __syncthreads();
+  // largest drift, second largest, index of the largest: the lower bound moves by the largest drift
+  // of any OTHER centre
+  const float dm1 = dmax[0], dm2 = dmax[1];
+  const int jm = (int)dmax[2];
+  const long long blk0 = (long long)blockIdx.x * kThreads * kIters * 4;
+  unsigned mask = 0;  // bit it*4+j: row blk0 + (it*kThreads + tid)*4 + j is a candidate
+#pragma unroll
+  for (int it = 0; it < kIters; ++it) {
+    const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+    if (r0 >= n) break;
+    if (r0 + 3 < n) {
+      const int4 l = *reinterpret_cast<const int4*>(lab + r0);
+      const float4 u = *reinterpret_cast<const float4*>(ub + r0);
+      const float4 w = *reinterpret_cast<const float4*>(lb + r0);
+      const int ls[4] = {l.x, l.y, l.z, l.w};
+      float us[4] = {u.x, u.y, u.z, u.w};
+      float ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int j = 0; j < 4; ++j)
+        if (!bound_step(ls[j], us[j], ws[j], sd, st, dm1, dm2, jm, c2)) mask |= 1u << (it * 4 + j);
+      *reinterpret_cast<float4*>(ub + r0) = make_float4(us[0], us[1], us[2], us[3]);
+      *reinterpret_cast<float4*>(lb + r0) = make_float4(ws[0], ws[1], ws[2], ws[3]);
+    } else {
+      for (int j = 0; j < 4 && r0 + j < n; ++j) {
+        float u = ub[r0 + j], w = lb[r0 + j];
+        if (!bound_step(lab[r0 + j], u, w, sd, st, dm1, dm2, jm, c2)) mask |= 1u << (it * 4 + j);
+        ub[r0 + j] = u;
+        lb[r0 + j] = w;
+      }
+    }
+  }
+  // block-wide exclusive scan of the per-lane candidate counts
+  const int mine = __popc(mask);
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  int incl = mine;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const int v = __shfl_up(incl, o, 64);
+    if (lane >= o) incl += v;
+  }
+  if (lane == 63) wsum[wave] = incl;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    int t = 0;
+    for (int w = 0; w < kThreads / 64; ++w) t += wsum[w];
+    base = t ? atomicAdd(count, t) : 0;
+  }
+  __syncthreads();
+  int off = base + incl - mine;
+  for (int w = 0; w < wave; ++w) off += wsum[w];
+  while (mask) {
+    const int b = __ffs(mask) - 1;
+    mask &= mask - 1;
+    cand[off++] = (int)(blk0 + ((long long)(b >> 2) * kThreads + threadIdx.x) * 4 + (b & 3));
+  }
+}
+
+}  // namespace
+
+// Moves every row's bounds by the centre drifts; rows whose bounds no longer prove the label are
+// appended to cand, their number added to *count (zeroed by the caller). dmax = {largest drift,
+// second largest, index of the largest}. lab / ub / lb 16-byte aligned, k <= 8192.
+CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
+                                    const float* thr, float c2, int k, long long n, int* cand, int* count,
+                                    void* stream) {
+  if (k <= 0 || k > 8192 || n < 0 || n >= (1LL << 31) || ((uintptr_t)lab & 15) || ((uintptr_t)ub & 15) ||
+      ((uintptr_t)lb & 15))
+    return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  const long long per = (long long)kThreads * kIters * 4;
+  const unsigned grid = (unsigned)((n + per - 1) / per);
+  hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads), (size_t)2 * k * sizeof(float),
+                     (hipStream_t)stream, lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count);
+  return cml_status();
+}

@@ -20,6 +20,13 @@ across steps; a step re-reads only the rows whose label changed (new sums = old 
 out, exact in f64 for bf16/fp8 rows), falling back to the full accumulate on the first step and
 whenever more than 1/4 of the rows changed (CML_KMEANS_DELTA_CAP). Every step still assigns every row against every centre.
 
+Pruned steps (``prune=True`` / ``CML_KMEANS_PRUNE=1``, opt-in): the exact bound-pruned form of the
+same iteration (``_step_prune``). Spark's own findClosest skips centres the triangle inequality rules
+out (mllib/clustering/DistanceMeasure.scala); here a per-row upper bound on the distance to the
+assigned centre is carried across iterations (Hamerly), so rows whose bound proves the label are not
+read at all and only the others are re-assigned against every centre. Labels, sums and centres are
+those of the full step (tests/test_kmeans_prune.py); the headline bench keeps the full assignment.
+
 CPU tensors run the same algorithm with torch float64 ops (``local[n]`` mode and
 the numerical oracle).
 """
@@ -27,12 +34,14 @@ from __future__ import annotations
 
 import math
 import os
+import types
 from typing import List, Optional
 
 import numpy as np
 import torch
 
 from ..ops import kmeans_ops as K
+from ..ops.group_ops import group_reduce
 from ..parallel.comm import Communicator, local_comm
 from ..utils import rng
 from ..utils.device import padded_dim, round_up
@@ -108,8 +117,13 @@ class LloydEngine:
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
-                 incremental: Optional[bool] = None, spherical: bool = False):
+                 incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None):
         self.comm = comm or local_comm()
+        if prune is None:
+            prune = os.environ.get("CML_KMEANS_PRUNE") == "1"
+        self.prune = bool(prune)
+        if self.prune:  # one chunk, no graph (the candidate count is read back every step), own sums
+            row_chunks, use_graph, incremental = 1, False, False
         # spherical = Spark's distanceMeasure="cosine": rows are scaled to unit length once, centres
         # are renormalised after every update (CosineDistanceMeasure.centroid), and on unit vectors
         # ||x - c||² = 2·(1 - cos), so the euclidean K9/K10 path computes the cosine assignment;
@@ -147,6 +161,7 @@ class LloydEngine:
         self.last_cost = None
         self._shift2 = None
         self.delta = None  # incremental-sums state (GPU sort regime), see _alloc_gpu
+        self._pst = None  # pruned-step state, see _step_prune
         if self.gpu:
             self._alloc_gpu()
 
@@ -165,8 +180,8 @@ class LloydEngine:
         self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode, fp8=fp8)
         self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         # distance scratch only when the centres need several LDS chunks (running min through HBM)
-        self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev) if self.aplan.kc < self.aplan.kp
-                     else None)
+        self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+                     if (self.aplan.kc < self.aplan.kp or self.prune) else None)
         self.xnorm = cached_row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
@@ -212,11 +227,16 @@ class LloydEngine:
             self.centers = c.contiguous().clone()
         if self.gpu:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+        if self._pst is not None:  # bounds were relative to the old centres
+            self._pst.valid = False
+            self._prune_centre_stats()
 
     # ------------------------------------------------------------------ iteration
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
-        if self.gpu and self.use_graph:
+        if self.prune:
+            self._step_prune()
+        elif self.gpu and self.use_graph:
             self._step_graph()
         elif self.gpu:
             self._step_gpu()
@@ -281,9 +301,13 @@ class LloydEngine:
         for h in handles:
             h.wait()
         self.last_cost = self.msgs[:, -1].sum()
+        self._update_gpu(self.msgs)
+
+    def _update_gpu(self, msgs: torch.Tensor) -> None:
+        """K11 from the all-reduced [sums | counts | cost] rows (one per chunk)."""
         if self.spherical:
             self._prev_centers.copy_(self.centers)
-        K.update_centers(self.msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
+        K.update_centers(msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
                          self.shift2)
         if self.spherical:  # unit-length centres (empty clusters keep their old, already unit, centre)
             self.centers.div_(self.centers.norm(dim=1, keepdim=True).clamp_(min=1e-300))
@@ -296,6 +320,10 @@ class LloydEngine:
         sums, counts = K.sums_reference(self.x, labels, self.k)
         msg = torch.cat([sums.reshape(-1), counts, best.sum().reshape(1)])
         self.comm.allreduce_(msg)
+        self._update_cpu(msg)
+        self.labels = labels
+
+    def _update_cpu(self, msg: torch.Tensor) -> None:
         kd = self.k * self.d
         sums = msg[:kd].reshape(self.k, self.d)
         counts = msg[kd:kd + self.k]
@@ -305,7 +333,215 @@ class LloydEngine:
         self._shift2 = ((new - self.centers) ** 2).sum(1)
         self.centers = new
         self.last_cost = msg[-1]
-        self.labels = labels
+
+    # ------------------------------------------------------------------ pruned (exact) steps
+    # Error allowance of a squared distance from the full assign, relative to |x|² + |c|²: f32
+    # accumulation of exact bf16 products is within D·2^-24·Σ|x_j c_j| <= 0.77e-5·(|x|² + |c|²) at D = 256.
+    _PRUNE_TAU = 3e-5
+    _PRUNE_CAP = 0.3  # a rank re-assigns all of its rows when more than this fraction are candidates
+
+    def _prune_init(self) -> None:
+        n, k, d, dev = self.n, self.k, self.d, self.device
+        bdt = torch.float32 if self.gpu else torch.float64
+        idt = torch.int32 if self.gpu else torch.int64
+        st = types.SimpleNamespace(valid=False, last=(True, 0))
+        st.ub = torch.full((max(n, 1),), float("inf"), dtype=bdt, device=dev)  # >= |x_i - c_label(i)|
+        st.lb = torch.zeros(max(n, 1), dtype=bdt, device=dev)  # <= distance to the nearest other centre
+        st.dmax = torch.zeros(3, dtype=bdt, device=dev)  # [largest drift, second largest, its index]
+        st.cand = torch.zeros(max(n, 1), dtype=idt, device=dev)
+        st.count = torch.zeros(1, dtype=idt, device=dev)
+        st.L = torch.zeros(k * d + 2 * k, dtype=torch.float64, device=dev)  # local [Σx | count | Σ|x|²] per centre
+        st.G = torch.zeros_like(st.L)  # all ranks' L summed (kept by adding the all-reduced deltas)
+        st.drift = torch.zeros(k, dtype=bdt, device=dev)
+        st.thr = torch.zeros(k, dtype=bdt, device=dev)
+        if self.gpu:
+            xn = self.xnorm[:n]
+        else:
+            self._xn64 = (self.x * self.x).sum(1)
+            xn = self._xn64
+        st.mx = self.comm.max_scalar(float(xn.max()) if n else 0.0)
+        if not self.gpu and getattr(self, "labels", None) is None:
+            self.labels = torch.zeros(max(n, 1), dtype=torch.int64)
+        self._pst = st
+
+    def _assign_centres64(self) -> torch.Tensor:
+        """The centres the assignment compares against (bf16-rounded on the GPU), as f64."""
+        return self.cb[: self.k, : self.d].to(torch.float64) if self.gpu else self.centers
+
+    def _prune_centre_stats(self, old: Optional[torch.Tensor] = None) -> None:
+        """drift[j] = |c_j - old_j| (rounded up) and thr[j] = half the distance from c_j to its nearest
+        other centre less the slack that keeps a pruned row's label strictly best under the full
+        assign's rounding: |x - c_j'|² - |x - c_j|² >= 4·s_j·(s_j - ub) >= 2·tau·(max|x|² + max|c|²)."""
+        st = self._pst
+        c = self._assign_centres64()
+        cn = (c * c).sum(1)
+        st.cn = cn
+        st.mc = float(cn.max()) if self.k else 0.0
+        st.c2 = 2.0 * self._PRUNE_TAU * (st.mx + st.mc)
+        if old is not None:
+            dr = (c - old).pow(2).sum(1).sqrt() * (1.0 + 1e-6)
+            st.drift.copy_(dr)
+            top = torch.topk(dr, min(2, self.k))
+            st.dmax.copy_(torch.stack([top.values[0], top.values[-1],
+                                       top.indices[0].to(torch.float64)]).to(st.dmax.dtype))
+        if self.k > 1:
+            d2 = (cn[:, None] + cn[None, :] - 2.0 * (c @ c.T)).clamp_(min=0.0)
+            d2.fill_diagonal_(float("inf"))
+            half = 0.5 * d2.min(1).values.sqrt()
+            slack = self._PRUNE_TAU * (st.mx + st.mc) / (2.0 * half)
+            thr = torch.where(half > 0, (half - slack) * (1.0 - 1e-6), torch.full_like(half, -math.inf))
+        else:
+            thr = torch.full((self.k,), math.inf, dtype=torch.float64, device=self.device)
+        st.thr.copy_(thr)
+
+    def _prune_bound(self, best: torch.Tensor, xn: torch.Tensor) -> torch.Tensor:
+        """Upper bound on the exact distance from the assign's squared distance (rounded up)."""
+        return (best.clamp(min=0) + self._PRUNE_TAU * (xn + self._pst.mc)).sqrt() * (1.0 + 1e-6)
+
+    def _prune_lower(self, xg: torch.Tensor, xng: torch.Tensor, lab: torch.Tensor, out: torch.Tensor,
+                     chunk: int = 1 << 19) -> None:
+        """out[i] = lower bound on the distance from row i to its nearest centre other than lab[i].
+        GPU: one bf16 GEMM with the |c|² bias fused (hipBLASLt, f32 accumulation, bf16 output), the
+        label's column masked, min over centres. Rounding the bias and the output to bf16 costs at
+        most 2^-9·(3·|c|² + |x|²) per entry, covered by subtracting 1e-2·(|x|² + max|c|²) before the
+        square root. CPU: the same in f64."""
+        st, k = self._pst, self.k
+        if self.gpu:
+            cbt = self.cb[:k].t()
+            bias = st.cn.to(torch.bfloat16)
+            err = 1e-2
+        else:
+            cbt = self.centers.t()
+            bias = st.cn
+            err = self._PRUNE_TAU
+        for s0 in range(0, xg.shape[0], chunk):
+            xc = xg[s0:s0 + chunk]
+            if self.gpu and xc.dtype != torch.bfloat16:
+                xc = xc.to(torch.bfloat16)
+            xn = xng[s0:s0 + chunk].to(out.dtype)
+            if k > 1:
+                dist = torch.addmm(bias, xc, cbt, alpha=-2.0)  # |c_j|² - 2 x·c_j
+                dist.scatter_(1, lab[s0:s0 + chunk].long()[:, None], math.inf)
+                sec = dist.min(1).values.to(out.dtype) + xn
+            else:
+                sec = torch.full_like(xn, math.inf)
+            out[s0:s0 + chunk] = (sec - err * (xn + st.mc)).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6)
+
+    def _step_prune(self) -> None:
+        """One exact Lloyd iteration: bounds pass (K9p), the rows it cannot prove are gathered and
+        assigned against every centre (K9), the per-centre sums move by the rows whose label changed,
+        and the deltas are all-reduced. A rank whose candidates exceed _PRUNE_CAP of its rows, or
+        whose bounds are stale (first step, set_centers), assigns all of its rows instead; the
+        collective sequence is the same either way."""
+        if self._pst is None:
+            self._prune_init()
+            self._prune_centre_stats()
+        st = self._pst
+        n, k, d = self.n, self.k, self.d
+        full, m = not st.valid, n
+        if not full and n:
+            K.prune_bounds(self.labels[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count)
+            m = int(st.count[0].item())
+            full = m > self._PRUNE_CAP * n
+        delta = self._prune_local_full() if full else self._prune_local_cands(m)
+        st.last = (full, m)
+        self.comm.allreduce_(delta)
+        st.G += delta
+        kd = k * d
+        c = self._assign_centres64()
+        s_, cnt, q = st.G[:kd].view(k, d), st.G[kd:kd + k], st.G[kd + k:]
+        # cost of this assignment: Σ_j Σ_{i in j} |x_i - c_j|² = Σ_j (Q_j - 2 c_j·S_j + n_j |c_j|²)
+        cost = (q.sum() - 2.0 * (c * s_).sum() + (cnt * st.cn).sum()).clamp(min=0.0)
+        msg = torch.cat([st.G[:kd + k], cost.reshape(1)])
+        old = c.clone()
+        if self.gpu:
+            self.last_cost = msg[-1]
+            self._update_gpu(msg.view(1, -1))
+        else:
+            self._update_cpu(msg)
+        st.valid = True
+        self._prune_centre_stats(old)
+
+    def _prune_local_full(self) -> torch.Tensor:
+        st = self._pst
+        n, k, d = self.n, self.k, self.d
+        kd = k * d
+        new = torch.zeros_like(st.L)
+        if n and self.gpu:
+            msg, xc, lab, best = self.msgs[0], self.x[:n], self.labels[:n], self.best[:n]
+            if self.cplan.mode == "priv":
+                K.assign_bf16(xc, n, self.dp, self.cb, self.cnorm, self.aplan, lab, best, self.cost_part,
+                              xnorm=self.xnorm[:n])
+                K.accumulate_priv(xc, n, lab, k, self.cplan, self.slab, self.cslab)
+                K.reduce_slabs(self.slab, self.cslab, self.cost_part, self.aplan.grid, k, d, self.cplan, msg)
+            else:
+                rank = self.rank[:n]
+                K.assign_bf16(xc, n, self.dp, self.cb, self.cnorm, self.aplan, lab, best, self.cost_part,
+                              self.hist, rank, xnorm=self.xnorm[:n])
+                K.accumulate_sort(xc, n, self.dp, d, lab, rank, self.hist, self.aplan, k, self.cost_part,
+                                  self.off, self.seg, self.perm, self.cplan, msg, self.slots)
+            new[:kd + k] = msg[:kd + k]
+            new[kd + k:] = group_reduce(lab, self.xnorm[:n], k, "sum")
+            st.ub[:n] = self._prune_bound(best, self.xnorm[:n])
+            self._prune_lower(xc, self.xnorm[:n], lab, st.lb)
+        elif n:
+            lab, best = K.assign_reference(self.x, self.centers)
+            self.labels = lab
+            sums, counts = K.sums_reference(self.x, lab, k)
+            new[:kd] = sums.reshape(-1)
+            new[kd:kd + k] = counts
+            new[kd + k:].index_add_(0, lab, self._xn64)
+            st.ub[:n] = self._prune_bound(best, self._xn64)
+            self._prune_lower(self.x, self._xn64, lab, st.lb)
+        delta = new - st.L
+        st.L = new
+        return delta
+
+    def _prune_local_cands(self, m: int) -> torch.Tensor:
+        st = self._pst
+        k, d = self.k, self.d
+        kd = k * d
+        delta = torch.zeros_like(st.L)
+        if m == 0:
+            return delta
+        cand = st.cand[:m].long()
+        if self.gpu:
+            fp8 = K.is_fp8(self.x)
+            xg = self.x.view(torch.uint8)[cand].view(self.x.dtype) if fp8 else self.x[cand]
+            xng = self.xnorm[cand]
+            labg = torch.empty(m, dtype=torch.int32, device=self.device)
+            bestg = torch.empty(m, dtype=torch.float32, device=self.device)
+            plan = K.plan_assign(m, self.dp, k, self.device.index or 0, fp8=fp8)
+            K.assign_bf16(xg, m, self.dp, self.cb, self.cnorm, plan, labg, bestg, None, xnorm=xng)
+        else:
+            xg, xng = self.x[cand], self._xn64[cand]
+            labg, bestg = K.assign_reference(xg, self.centers)
+        old = self.labels[cand]
+        labg = labg.to(old.dtype)
+        self.labels[cand] = labg
+        st.ub[cand] = self._prune_bound(bestg, xng).to(st.ub.dtype)
+        lo = torch.empty(m, dtype=st.lb.dtype, device=self.device)
+        self._prune_lower(xg, xng, labg, lo)
+        st.lb[cand] = lo
+        ch = torch.nonzero(labg != old).flatten()
+        if ch.numel():
+            o, nw = old[ch].long(), labg[ch].long()
+            xs = xg[ch, :d].to(torch.float64)
+            xq = xng[ch].to(torch.float64)
+            ones = torch.ones(ch.numel(), dtype=torch.float64, device=self.device)
+            sums, cnt, q = delta[:kd].view(k, d), delta[kd:kd + k], delta[kd + k:]
+            sums.index_add_(0, nw, xs).index_add_(0, o, -xs)
+            cnt.index_add_(0, nw, ones).index_add_(0, o, -ones)
+            q.index_add_(0, nw, xq).index_add_(0, o, -xq)
+        st.L += delta
+        return delta
+
+    def prune_stats(self) -> dict:
+        """Last pruned step: whether this rank re-assigned all rows, and how many it re-assigned."""
+        if self._pst is None:
+            return {}
+        full, m = self._pst.last
+        return {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
 
     def converged(self, tol: float) -> bool:
         """Spark's rule: converged iff every centre moved at most tol (euclidean)."""

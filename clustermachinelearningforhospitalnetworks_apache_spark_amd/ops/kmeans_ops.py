@@ -50,6 +50,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                   c_vp]),
+    "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_int, c_ll, c_vp,
+                                        c_vp, c_vp]),
 })
 
 
@@ -344,6 +346,34 @@ class DeltaState:
 
     def was_full(self, chunk: int = 0) -> bool:
         return bool(self.mode[chunk, 0].item())
+
+
+def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift: torch.Tensor,
+                 dmax: torch.Tensor, thr: torch.Tensor, c2: float, k: int, cand: torch.Tensor,
+                 count: torch.Tensor, stream=None) -> None:
+    """K9p (``kmeans_prune.hip``): moves the per-row distance bounds by the centre drifts
+    (ub += drift[label], lb -= largest drift of another centre) and appends to ``cand`` the rows whose
+    bounds no longer prove the label (neither ub <= thr[label] nor ub <= lb - c2 / lb); ``count[0]`` =
+    their number. ``dmax`` = [largest drift, second largest, index of the largest]. CPU tensors: the
+    same pass in torch (f64 bounds), candidates in row order."""
+    n = int(labels.shape[0])
+    if labels.is_cuda:
+        count.zero_()
+        _native.check(_native.kernels().cml_kmeans_prune_bounds(
+            labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
+            float(c2), int(k), n, cand.data_ptr(), count.data_ptr(), _native.stream_ptr(stream)),
+            "kmeans_prune_bounds")
+        return
+    lab = labels[:n].long()
+    ub[:n] += drift[lab]
+    other = torch.where(lab == int(dmax[2]), dmax[1], dmax[0])
+    lb[:n] = (lb[:n] - other).clamp_(min=0.0)
+    w = lb[:n]
+    lt = torch.where(w > 0, w - c2 / w.clamp(min=1e-300), torch.full_like(w, -1.0))
+    keep = (ub[:n] <= thr[lab]) | (ub[:n] <= lt)
+    idx = torch.nonzero(~keep).flatten()
+    cand[: idx.numel()] = idx.to(cand.dtype)
+    count[0] = idx.numel()
 
 
 def seg_buffer_ints(k: int) -> int:
