@@ -66,8 +66,11 @@ class KMeans(Estimator):
         k = self.getK()
         comm = df._comm
         seed = int(self.getSeed())
-        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical)
         conf = df._session.conf
+        # exact bound-pruned Lloyd steps (models/kmeans.py _step_prune): same centres, fewer rows read
+        pv = conf.get("cml.ml.kmeans.prune", None)
+        prune = None if pv is None else str(pv).lower() in ("1", "true")
+        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
@@ -86,7 +89,7 @@ class KMeans(Estimator):
             start, arrs = resumed
             init = arrs["centers"]
             if init.shape[0] < k:
-                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical)
+                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
         elif self.getInitMode() == "random":
             with trace("kmeans.init"):
                 init = eng.init_random(seed)
@@ -96,7 +99,7 @@ class KMeans(Estimator):
             k_eff = getattr(eng, "k_effective", k)
             if k_eff < k:
                 init = init[:k_eff]
-                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical)
+                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
         eng.set_centers(init)
 
         def on_iter(it):

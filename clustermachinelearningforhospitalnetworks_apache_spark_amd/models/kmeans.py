@@ -399,33 +399,56 @@ class LloydEngine:
         return (best.clamp(min=0) + self._PRUNE_TAU * (xn + self._pst.mc)).sqrt() * (1.0 + 1e-6)
 
     def _prune_lower(self, xg: torch.Tensor, xng: torch.Tensor, lab: torch.Tensor, out: torch.Tensor,
-                     chunk: int = 1 << 19) -> None:
+                     chunk: Optional[int] = None) -> None:
         """out[i] = lower bound on the distance from row i to its nearest centre other than lab[i].
-        GPU: one bf16 GEMM with the |c|² bias fused (hipBLASLt, f32 accumulation, bf16 output), the
-        label's column masked, min over centres. Rounding the bias and the output to bf16 costs at
-        most 2^-9·(3·|c|² + |x|²) per entry, covered by subtracting 1e-2·(|x|² + max|c|²) before the
-        square root. CPU: the same in f64."""
+        GPU: one bf16 GEMM against the centres with f32 accumulation and f32 output (hipBLASLt), the
+        label's column masked, min over centres; its rounding is that of the full assign, covered
+        by subtracting tau·(|x|² + max|c|²) before the square root. CPU: the same in f64."""
         st, k = self._pst, self.k
         if self.gpu:
             cbt = self.cb[:k].t()
-            bias = st.cn.to(torch.bfloat16)
-            err = 1e-2
+            cn = st.cn.to(torch.float32)
         else:
             cbt = self.centers.t()
-            bias = st.cn
-            err = self._PRUNE_TAU
+            cn = st.cn
+        if chunk is None:  # [chunk, k] f32 blocks of 512 MiB at k = 256 (64 MiB blocks measured slower)
+            chunk = max(1024, (512 << 20) // (4 * max(k, 1)))
         for s0 in range(0, xg.shape[0], chunk):
             xc = xg[s0:s0 + chunk]
-            if self.gpu and xc.dtype != torch.bfloat16:
-                xc = xc.to(torch.bfloat16)
-            xn = xng[s0:s0 + chunk].to(out.dtype)
+            xn = xng[s0:s0 + chunk].to(cn.dtype)
             if k > 1:
-                dist = torch.addmm(bias, xc, cbt, alpha=-2.0)  # |c_j|² - 2 x·c_j
+                if self.gpu:
+                    if xc.dtype != torch.bfloat16:
+                        xc = xc.to(torch.bfloat16)
+                    # |c_j|² - 2 x·c_j with the bias and scale in the GEMM epilogue (one f32 write)
+                    dist = torch.addmm(cn, xc, cbt, out_dtype=torch.float32, alpha=-2.0)
+                else:
+                    dist = torch.addmm(cn, xc, cbt, alpha=-2.0)
                 dist.scatter_(1, lab[s0:s0 + chunk].long()[:, None], math.inf)
-                sec = dist.min(1).values.to(out.dtype) + xn
+                sec = dist.min(1).values + xn
             else:
                 sec = torch.full_like(xn, math.inf)
-            out[s0:s0 + chunk] = (sec - err * (xn + st.mc)).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6)
+            lo = (sec - self._PRUNE_TAU * (xn + st.mc)).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6)
+            out[s0:s0 + chunk] = lo.to(out.dtype)
+
+    @staticmethod
+    def _moved_sums(delta: torch.Tensor, k: int, d: int, xs: torch.Tensor, xq: torch.Tensor, new: torch.Tensor,
+                    old: torch.Tensor, chunk: int = 1 << 17) -> None:
+        """delta += the per-centre [Σx | count | Σ|x|²] change of rows moving old -> new, as one f64 GEMM
+        per chunk with a {-1, 0, +1} move matrix (sums of bf16 / fp8 rows are exact in f64, so the
+        result does not depend on the GEMM's summation order; scatter-add atomics on 256 rows of
+        centres serialise)."""
+        kd = k * d
+        sums, cnt, q = delta[:kd].view(k, d), delta[kd:kd + k], delta[kd + k:]
+        for s0 in range(0, xs.shape[0], chunk):
+            nw, o = new[s0:s0 + chunk], old[s0:s0 + chunk]
+            w = torch.zeros((nw.shape[0], k), dtype=torch.float64, device=xs.device)
+            w.scatter_(1, nw[:, None], 1.0)
+            w.scatter_(1, o[:, None], -1.0)
+            wt = w.t()
+            sums += wt @ xs[s0:s0 + chunk]
+            cnt += w.sum(0)
+            q += wt @ xq[s0:s0 + chunk]
 
     def _step_prune(self) -> None:
         """One exact Lloyd iteration: bounds pass (K9p), the rows it cannot prove are gathered and
@@ -440,11 +463,20 @@ class LloydEngine:
         n, k, d = self.n, self.k, self.d
         full, m = not st.valid, n
         if not full and n:
-            K.prune_bounds(self.labels[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count)
-            m = int(st.count[0].item())
+            with trace("prune.bounds"):
+                K.prune_bounds(self.labels[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand,
+                               st.count)
+                m = int(st.count[0].item())
             full = m > self._PRUNE_CAP * n
-        delta = self._prune_local_full() if full else self._prune_local_cands(m)
+        with trace("prune.full" if full else "prune.candidates"):
+            delta = self._prune_local_full() if full else self._prune_local_cands(m)
         st.last = (full, m)
+        with trace("prune.allreduce_update"):
+            self._prune_apply(delta)
+
+    def _prune_apply(self, delta: torch.Tensor) -> None:
+        st = self._pst
+        k, d = self.k, self.d
         self.comm.allreduce_(delta)
         st.G += delta
         kd = k * d
@@ -460,7 +492,8 @@ class LloydEngine:
         else:
             self._update_cpu(msg)
         st.valid = True
-        self._prune_centre_stats(old)
+        with trace("prune.centre_stats"):
+            self._prune_centre_stats(old)
 
     def _prune_local_full(self) -> torch.Tensor:
         st = self._pst
@@ -500,11 +533,31 @@ class LloydEngine:
     def _prune_local_cands(self, m: int) -> torch.Tensor:
         st = self._pst
         k, d = self.k, self.d
-        kd = k * d
         delta = torch.zeros_like(st.L)
         if m == 0:
             return delta
         cand = st.cand[:m].long()
+        with trace("prune.gather_assign"):
+            xg, xng, labg, bestg = self._prune_assign_rows(cand, m)
+        old = self.labels[cand]
+        labg = labg.to(old.dtype)
+        self.labels[cand] = labg
+        st.ub[cand] = self._prune_bound(bestg, xng).to(st.ub.dtype)
+        lo = torch.empty(m, dtype=st.lb.dtype, device=self.device)
+        with trace("prune.lower"):
+            self._prune_lower(xg, xng, labg, lo)
+        st.lb[cand] = lo
+        with trace("prune.delta"):
+            ch = torch.nonzero(labg != old).flatten()
+            if ch.numel():
+                o, nw = old[ch].long(), labg[ch].long()
+                self._moved_sums(delta, k, d, xg[ch, :d].to(torch.float64), xng[ch].to(torch.float64), nw, o)
+        st.L += delta
+        return delta
+
+    def _prune_assign_rows(self, cand: torch.Tensor, m: int):
+        """Gathered candidate rows, their |x|², labels and squared distances against every centre."""
+        k = self.k
         if self.gpu:
             fp8 = K.is_fp8(self.x)
             xg = self.x.view(torch.uint8)[cand].view(self.x.dtype) if fp8 else self.x[cand]
@@ -516,25 +569,7 @@ class LloydEngine:
         else:
             xg, xng = self.x[cand], self._xn64[cand]
             labg, bestg = K.assign_reference(xg, self.centers)
-        old = self.labels[cand]
-        labg = labg.to(old.dtype)
-        self.labels[cand] = labg
-        st.ub[cand] = self._prune_bound(bestg, xng).to(st.ub.dtype)
-        lo = torch.empty(m, dtype=st.lb.dtype, device=self.device)
-        self._prune_lower(xg, xng, labg, lo)
-        st.lb[cand] = lo
-        ch = torch.nonzero(labg != old).flatten()
-        if ch.numel():
-            o, nw = old[ch].long(), labg[ch].long()
-            xs = xg[ch, :d].to(torch.float64)
-            xq = xng[ch].to(torch.float64)
-            ones = torch.ones(ch.numel(), dtype=torch.float64, device=self.device)
-            sums, cnt, q = delta[:kd].view(k, d), delta[kd:kd + k], delta[kd + k:]
-            sums.index_add_(0, nw, xs).index_add_(0, o, -xs)
-            cnt.index_add_(0, nw, ones).index_add_(0, o, -ones)
-            q.index_add_(0, nw, xq).index_add_(0, o, -xq)
-        st.L += delta
-        return delta
+        return xg, xng, labg, bestg
 
     def prune_stats(self) -> dict:
         """Last pruned step: whether this rank re-assigned all rows, and how many it re-assigned."""

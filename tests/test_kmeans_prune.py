@@ -35,7 +35,9 @@ def _pair(x, d, k, init, steps, **kw):
         n = a.n
         assert torch.equal(a.labels[:n].long(), b.labels[:n].long())
         torch.testing.assert_close(b.centers, a.centers, rtol=1e-12, atol=1e-12)
-        assert abs(float(b.last_cost) - float(a.last_cost)) <= 1e-9 * max(1.0, abs(float(a.last_cost)))
+        # full step: Σ of the assign's f32 row distances; pruned: Σ_j (Q_j - 2 c_j·S_j + n_j |c_j|²) in f64
+        rtol = 1e-5 if x.is_cuda else 1e-9
+        assert abs(float(b.last_cost) - float(a.last_cost)) <= rtol * max(1.0, abs(float(a.last_cost)))
         assert torch.equal(a._shift2 <= 1e-8, b._shift2 <= 1e-8)
     return a, b, stats
 
@@ -129,13 +131,15 @@ def test_pruned_distributed_gloo_matches_single_rank(tmp_path):
 
 # ------------------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d,k", [(300_001, 256, 256), (200_000, 128, 64), (50_000, 64, 300)])
-def test_pruned_equals_full_gpu(n, d, k):
-    x = _blobs(n, d, k, seed=7, scale=1.0, device="cuda", dtype=torch.bfloat16)
+@pytest.mark.parametrize("n,d,k,scale", [(300_001, 256, 256, 1.0), (200_000, 128, 64, 1.0), (50_000, 64, 300, 3.0),
+                                         (60_000, 64, 200, 0.5)])
+def test_pruned_equals_full_gpu(n, d, k, scale):
+    x = _blobs(n, d, k, seed=7, scale=scale, device="cuda", dtype=torch.bfloat16)
     init = x[torch.randperm(n, device="cuda")[:k]].double().cpu().numpy()
     _, b, stats = _pair(x, d, k, init, 10, use_graph=False)
     assert b._pst.ub.dtype == torch.float32
-    assert any(not s["full"] for s in stats[1:]), stats
+    if scale >= 1.0:  # separated blobs: the bounds prune; overlapping ones (0.5) re-assign in full
+        assert any(not s["full"] for s in stats[1:]), stats
 
 
 @pytest.mark.gpu
@@ -175,3 +179,26 @@ def test_bounds_kernel_matches_torch_pass():
     # the kernel rounds its bounds outwards: it may keep a few more candidates, never fewer
     assert want <= got and len(got - want) <= max(10, m // 10000)
     assert len(got) == m
+
+
+def test_kmeans_estimator_prune_conf_cpu():
+    import pandas as pd
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    x = _blobs(5_000, 4, 5, seed=21, scale=4.0).numpy()
+    df = spark.createDataFrame(pd.DataFrame(x, columns=list("abcd")))
+    df = VectorAssembler(inputCols=list("abcd"), outputCol="features").transform(df)
+    try:
+        spark.conf.set("cml.ml.kmeans.prune", "false")
+        full = KMeans(k=5, seed=3, maxIter=30).fit(df)
+        spark.conf.set("cml.ml.kmeans.prune", "true")
+        pruned = KMeans(k=5, seed=3, maxIter=30).fit(df)
+    finally:
+        spark.conf.unset("cml.ml.kmeans.prune")
+    np.testing.assert_allclose(np.array(pruned.clusterCenters()), np.array(full.clusterCenters()), rtol=1e-12,
+                               atol=1e-12)
+    assert pruned.summary.numIter == full.summary.numIter
+    assert pruned.summary.clusterSizes == full.summary.clusterSizes
+    assert abs(pruned.summary.trainingCost - full.summary.trainingCost) <= 1e-9 * full.summary.trainingCost
