@@ -129,7 +129,7 @@ def main():
            "assign": "pruned (exact bounds)" if args.prune else "full (every row x every centre)"}
     if args.prune:
         acc["last_step_prune_rank0"] = eng.prune_stats()
-    elif gpu:
+    elif gpu and W == 1:
         # the exact bound-pruned step (LloydEngine(prune=True)) from the same start, same step count:
         # its ms/step and whether its labels equal the full step's after warmup + steps iterations
         lab_full = eng.labels[: eng.n].clone()
