@@ -149,7 +149,7 @@ class DataFrameWriter:
         if sep is not None:
             self.option("sep", sep)
         hdr = str(self._options.get("header", "false")).lower() == "true"
-        self._write(path, lambda df, d: self._local_pandas(df).to_csv(self._part(d, "csv", df), index=False,
+        self._write(path, lambda df, d: self._local_pandas(df, csv=True).to_csv(self._part(d, "csv", df), index=False,
                                                                      header=hdr, sep=self._options.get("sep", ",")))
 
     def json(self, path: str, mode: Optional[str] = None):
@@ -158,14 +158,20 @@ class DataFrameWriter:
         self._write(path, lambda df, d: self._local_pandas(df).to_json(self._part(d, "json", df), orient="records",
                                                                       lines=True, date_format="iso"))
 
-    def _local_pandas(self, df=None):
+    def _local_pandas(self, df=None, csv: bool = False):
         import pandas as pd
         from ..sql.dataframe import column_to_python
         df = self._df if df is None else df
+        from ..sql import types as T
         data = {}
         for f in df.schema.fields:
             vals = column_to_python(df._cols[f.name])
-            data[f.name] = [v.toArray().tolist() if hasattr(v, "toArray") else v for v in vals]
+            vals = [v.toArray().tolist() if hasattr(v, "toArray") else v for v in vals]
+            if isinstance(f.dataType, (T.ByteType, T.ShortType, T.IntegerType, T.LongType)):
+                vals = pd.array(vals, dtype="Int64")  # nulls stay empty cells, integers stay integers (not 0.0)
+            elif csv and isinstance(f.dataType, T.BooleanType):
+                vals = [None if v is None else ("true" if v else "false") for v in vals]  # Spark's spelling
+            data[f.name] = vals
         return pd.DataFrame(data, columns=df.columns)
 
     def saveAsTable(self, name: str, format: Optional[str] = None, mode: Optional[str] = None):

@@ -753,7 +753,7 @@ def _like_rx(pattern: str, escape: str = "\\", flags=0):
 
 
 def like(s: ColumnOrName, pattern, escapeChar=None) -> Column:
-    """SQL LIKE: ``%`` any run, ``_`` one character, ``escapeChar`` (default ``\``) escapes."""
+    r"""SQL LIKE: ``%`` any run, ``_`` one character, ``escapeChar`` (default ``\``) escapes."""
     pat = pattern._expr.value if isinstance(pattern, Column) else str(pattern)
     rx = _like_rx(pat, escapeChar or "\\")
     return _host_map("like", [s], lambda v: rx.fullmatch(str(v)) is not None, T.BooleanType(), params=[pat])

@@ -1,0 +1,143 @@
+"""Property-based tests (hypothesis) of the frame operations of the reference workflow (SURVEY.md §4.2,
+unit tier): na.drop, BETWEEN, when/otherwise, randomSplit, groupBy aggregates and the CSV round trip,
+each against a pandas / numpy statement of the same semantics on generated tables with nulls; plus the
+exact pruned Lloyd step against the full one on generated data."""
+import math
+
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+from hypothesis import HealthCheck, given, settings
+from hypothesis import strategies as st
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
+
+SETTINGS = settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+
+
+@pytest.fixture(scope="module")
+def spark():
+    return SparkSession.builder.master("local[1]").getOrCreate()
+
+
+_val = st.one_of(st.none(), st.integers(-50, 50))
+_dbl = st.one_of(st.none(), st.floats(-1e3, 1e3, allow_nan=False, width=32))
+
+
+@st.composite
+def tables(draw, min_rows=0, max_rows=40):
+    n = draw(st.integers(min_rows, max_rows))
+    return pd.DataFrame({
+        "h": draw(st.lists(st.sampled_from(["h1", "h2", "h3", None]), min_size=n, max_size=n)),
+        "a": pd.array(draw(st.lists(_val, min_size=n, max_size=n)), dtype="Int64"),
+        "x": pd.array(draw(st.lists(_dbl, min_size=n, max_size=n)), dtype="Float64"),
+    })
+
+
+def _df(spark, pdf):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    schema = T.StructType([T.StructField("h", T.StringType(), True), T.StructField("a", T.LongType(), True),
+                           T.StructField("x", T.DoubleType(), True)])
+    rows = [tuple(None if (v is pd.NA or v is None or (isinstance(v, float) and math.isnan(v))) else v
+                  for v in r) for r in pdf.astype(object).itertuples(index=False)]
+    return spark.createDataFrame(rows, schema)
+
+
+def _rows(df):
+    return sorted((tuple(r) for r in df.collect()), key=repr)
+
+
+def _py(v):
+    return None if v is pd.NA or v is None else (int(v) if isinstance(v, (np.integer,)) else v)
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_na_drop_keeps_exactly_the_complete_rows(spark, pdf):
+    got = _rows(_df(spark, pdf).na.drop())
+    want = sorted((tuple(_py(v) for v in r) for r in pdf.dropna().astype(object).itertuples(index=False)), key=repr)
+    assert [(h, a, None if x is None else float(x)) for h, a, x in got] == \
+        [(h, a, None if x is None else float(x)) for h, a, x in want]
+
+
+@SETTINGS
+@given(pdf=tables(), lo=st.integers(-60, 60), width=st.integers(0, 60))
+def test_between_is_inclusive_and_drops_nulls(spark, pdf, lo, width):
+    hi = lo + width
+    got = _df(spark, pdf).filter(F.col("a").between(lo, hi)).count()
+    want = int(((pdf["a"] >= lo) & (pdf["a"] <= hi)).fillna(False).sum())
+    assert got == want
+
+
+@SETTINGS
+@given(pdf=tables(), thr=st.floats(-1e3, 1e3, allow_nan=False, width=32))
+def test_when_otherwise_matches_three_valued_logic(spark, pdf, thr):
+    out = _df(spark, pdf).withColumn("b", F.when(F.col("x") > thr, 1).otherwise(0)).select("b").collect()
+    got = sorted(r[0] for r in out)
+    # a null comparison is not true: otherwise() applies (Spark CASE WHEN semantics)
+    want = sorted(int(v is not pd.NA and v > thr) for v in pdf["x"])
+    assert got == want
+
+
+@SETTINGS
+@given(pdf=tables(min_rows=1), w=st.lists(st.floats(0.1, 5.0), min_size=2, max_size=4), seed=st.integers(0, 2**31))
+def test_random_split_partitions_rows_deterministically(spark, pdf, w, seed):
+    df = _df(spark, pdf).withColumn("id", F.monotonically_increasing_id())
+    parts = df.randomSplit(w, seed=seed)
+    again = df.randomSplit(w, seed=seed)
+    ids = [sorted(r["id"] for r in p.select("id").collect()) for p in parts]
+    assert ids == [sorted(r["id"] for r in p.select("id").collect()) for p in again]
+    flat = [i for p in ids for i in p]
+    assert sorted(flat) == sorted(r["id"] for r in df.select("id").collect())  # disjoint and complete
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_groupby_count_sum_avg_max_match_pandas(spark, pdf):
+    got = {r["h"]: (r["n"], r["s"], r["m"], r["mx"]) for r in
+           _df(spark, pdf).groupBy("h").agg(F.count("a").alias("n"), F.sum("a").alias("s"),
+                                            F.avg("x").alias("m"), F.max("x").alias("mx")).collect()}
+    g = pdf.astype({"h": object}).fillna({"h": "__null__"}).groupby("h", dropna=False)
+    assert len(got) == g.ngroups
+    for key, sub in g:
+        k = None if key == "__null__" else key
+        n, s, m, mx = got[k]
+        assert n == int(sub["a"].notna().sum())
+        assert s == (None if sub["a"].notna().sum() == 0 else int(sub["a"].sum()))
+        xs = sub["x"].dropna().astype(float)
+        if len(xs) == 0:
+            assert m is None and mx is None
+        else:
+            assert math.isclose(m, float(xs.mean()), rel_tol=1e-9, abs_tol=1e-9)
+            assert mx == float(xs.max())
+
+
+@SETTINGS
+@given(pdf=tables(min_rows=1))
+def test_csv_round_trip(spark, pdf, tmp_path_factory):
+    path = str(tmp_path_factory.mktemp("csv") / "t")
+    df = _df(spark, pdf)
+    df.write.mode("overwrite").option("header", True).csv(path)
+    back = spark.read.option("header", True).schema(df.schema).csv(path)
+    assert _rows(back) == _rows(df)
+
+
+@settings(max_examples=15, deadline=None)
+@given(n=st.integers(50, 3000), d=st.integers(1, 12), k=st.integers(1, 9), scale=st.floats(0.3, 8.0),
+       seed=st.integers(0, 10_000))
+def test_pruned_lloyd_equals_full_lloyd(n, d, k, scale, seed):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    g = torch.Generator().manual_seed(seed)
+    cen = torch.randn(k, d, generator=g, dtype=torch.float64) * scale
+    x = cen[torch.randint(0, k, (n,), generator=g)] + torch.randn(n, d, generator=g, dtype=torch.float64)
+    init = x[torch.randperm(n, generator=g)[:k]].numpy()
+    a, b = LloydEngine(x, d, k), LloydEngine(x, d, k, prune=True)
+    a.set_centers(init)
+    b.set_centers(init)
+    for _ in range(6):
+        a.step()
+        b.step()
+        assert torch.equal(a.labels, b.labels)
+        torch.testing.assert_close(b.centers, a.centers, rtol=1e-12, atol=1e-12)
