@@ -160,14 +160,18 @@ class DataFrameReader:
         if schema is not None:
             self.schema(schema)
         files = expand_paths(path)
-        frames = [pd.read_json(f, lines=True) for f in files]
+        # precise_float: exact round trip of the writer's shortest-repr doubles (the default parser rounds)
+        frames = [pd.read_json(f, lines=True, precise_float=True) for f in files]
         pdf = pd.concat(frames, ignore_index=True) if frames else pd.DataFrame()
         comm = self._session._comm
         a, b = shard_range(len(pdf), comm.rank, comm.world_size)
         table = pa.Table.from_pandas(pdf.iloc[a:b], preserve_index=False)
         df = frame_from_arrow(self._session, table, list(range(a, b)))
         if self._schema is not None:
-            df = df.select(*[df[f.name].cast(f.dataType).alias(f.name) for f in self._schema.fields])
+            from ..sql import functions as F
+            # a field no record carries (Spark omits null fields when writing) reads as an all-null column
+            df = df.select(*[(df[f.name] if f.name in df.columns else F.lit(None)).cast(f.dataType).alias(f.name)
+                             for f in self._schema.fields])
         return df
 
     def table(self, name: str):

@@ -155,8 +155,50 @@ class DataFrameWriter:
     def json(self, path: str, mode: Optional[str] = None):
         if mode:
             self.mode(mode)
-        self._write(path, lambda df, d: self._local_pandas(df).to_json(self._part(d, "json", df), orient="records",
-                                                                      lines=True, date_format="iso"))
+        self._write(path, lambda df, d: self._json_lines(df, self._part(d, "json", df)))
+
+    @staticmethod
+    def _json_lines(df, path: str) -> None:
+        """JSON Lines as Spark writes them: one object per row, null fields omitted (ignoreNullFields),
+        doubles with every significant digit (shortest repr round-trips; pandas' to_json keeps 10)."""
+        import datetime
+        import decimal
+        import json
+        import math
+        from ..sql.dataframe import column_to_python
+
+        def conv(v):
+            if isinstance(v, float):
+                return None if math.isnan(v) else v
+            if isinstance(v, datetime.datetime):
+                return v.isoformat(timespec="milliseconds")
+            if isinstance(v, datetime.date):
+                return v.isoformat()
+            if isinstance(v, decimal.Decimal):
+                return float(v)
+            if hasattr(v, "toArray"):
+                return v.toArray().tolist()
+            if hasattr(v, "asDict"):
+                return {k: conv(x) for k, x in v.asDict().items()}
+            if isinstance(v, dict):
+                return {str(k): conv(x) for k, x in v.items()}
+            if isinstance(v, (list, tuple)):
+                return [conv(x) for x in v]
+            if isinstance(v, (bytes, bytearray)):
+                import base64
+                return base64.b64encode(bytes(v)).decode()
+            return v
+
+        cols = [(f.name, column_to_python(df._cols[f.name])) for f in df.schema.fields]
+        n = len(cols[0][1]) if cols else 0
+        with open(path, "w") as fh:
+            for i in range(n):
+                rec = {}
+                for name, vals in cols:
+                    v = conv(vals[i])
+                    if v is not None:
+                        rec[name] = v
+                fh.write(json.dumps(rec, allow_nan=True) + "\n")
 
     def _local_pandas(self, df=None, csv: bool = False):
         import pandas as pd

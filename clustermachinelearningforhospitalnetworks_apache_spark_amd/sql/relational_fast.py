@@ -562,7 +562,8 @@ def join_indices(left, rcols: Dict[str, ColumnData], n_right: int, lkeys: List[s
         return None
     lc, rc = code[:n_left], code[n_left:]
     # codes are dense: per-code counts and starts of the code-sorted right side replace a binary search
-    card = int(code.max()) + 2 if code.numel() else 1
+    # (at least one code slot: with every key null, or an empty side, the lookups below still index slot 0)
+    card = max(int(code.max()) + 2 if code.numel() else 0, 2)
     rperm = torch.sort(rc, stable=True).indices
     rcount = torch.bincount(rc + 1, minlength=card)[1:]           # slot 0 = null keys
     rstart = torch.cumsum(rcount, 0) - rcount + int((rc < 0).sum())  # null right keys sort first

@@ -141,3 +141,104 @@ def test_pruned_lloyd_equals_full_lloyd(n, d, k, scale, seed):
         b.step()
         assert torch.equal(a.labels, b.labels)
         torch.testing.assert_close(b.centers, a.centers, rtol=1e-12, atol=1e-12)
+
+
+def _key(v):
+    """Spark's default ascending order: nulls first."""
+    return (0,) if v is None else (1, v)
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_order_by_two_keys_with_nulls(spark, pdf):
+    got = [(r["h"], r["a"]) for r in _df(spark, pdf).orderBy(F.col("h").asc(), F.col("a").desc()).collect()]
+    rows = [(_py(h), _py(a)) for h, a in zip(pdf["h"], pdf["a"])]
+    # h ascending nulls first; a descending nulls last (Spark's defaults for asc() / desc())
+    want = sorted(rows, key=lambda r: (_key(r[0]), (1,) if r[1] is None else (0, -r[1])))
+    assert got == want
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_drop_duplicates_and_distinct(spark, pdf):
+    df = _df(spark, pdf).select("h", "a")
+    rows = {(_py(h), _py(a)) for h, a in zip(pdf["h"], pdf["a"])}
+    assert sorted((tuple(r) for r in df.distinct().collect()), key=repr) == sorted(rows, key=repr)
+    assert sorted((tuple(r) for r in df.dropDuplicates(["h"]).select("h").collect()), key=lambda t: _key(t[0])) == \
+        sorted(((h,) for h in {r[0] for r in rows}), key=lambda t: _key(t[0]))
+
+
+@SETTINGS
+@given(left=tables(max_rows=25), right=tables(max_rows=25), how=st.sampled_from(["inner", "left", "left_semi",
+                                                                                 "left_anti"]))
+def test_equi_join_null_keys_never_match(spark, left, right, how):
+    ldf = _df(spark, left).select(F.col("a").alias("k"), F.col("h").alias("lh"))
+    rdf = _df(spark, right).select(F.col("a").alias("k"), F.col("x").alias("rx"))
+    got = sorted((tuple(r) for r in ldf.join(rdf, on="k", how=how).collect()), key=repr)
+    L = [(_py(a), _py(h)) for a, h in zip(left["a"], left["h"])]
+    R = [(_py(a), None if x is pd.NA else float(x)) for a, x in zip(right["a"], right["x"])]
+    want = []
+    for k, lh in L:
+        m = [rx for k2, rx in R if k is not None and k2 == k]
+        if how == "inner":
+            want += [(k, lh, rx) for rx in m]
+        elif how == "left":
+            want += [(k, lh, rx) for rx in m] or [(k, lh, None)]
+        elif how == "left_semi":
+            want += [(k, lh)] if m else []
+        else:
+            want += [] if m else [(k, lh)]
+    assert got == sorted(want, key=repr)
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_window_row_number_and_rank(spark, pdf):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.window import Window
+    w = Window.partitionBy("h").orderBy(F.col("a").asc())
+    out = _df(spark, pdf).select("h", "a", F.row_number().over(w).alias("rn"), F.rank().over(w).alias("rk")).collect()
+    by = {}
+    for r in out:
+        by.setdefault(r["h"], []).append((r["a"], r["rn"], r["rk"]))
+    for h, lst in by.items():
+        lst.sort(key=lambda t: t[1])
+        assert [t[1] for t in lst] == list(range(1, len(lst) + 1))
+        keys = [t[0] for t in lst]
+        assert keys == sorted(keys, key=_key)  # nulls first
+        for i, (a, rn, rk) in enumerate(lst):
+            first = next(j for j, t in enumerate(lst) if t[0] == a)
+            assert rk == first + 1
+
+
+@SETTINGS
+@given(pdf=tables(min_rows=1), fmt=st.sampled_from(["parquet", "json"]))
+def test_parquet_json_round_trip(spark, pdf, fmt, tmp_path_factory):
+    path = str(tmp_path_factory.mktemp(fmt) / "t")
+    df = _df(spark, pdf)
+    getattr(df.write.mode("overwrite"), fmt)(path)
+    back = getattr(spark.read.schema(df.schema), fmt)(path) if fmt == "json" else spark.read.parquet(path)
+    assert _rows(back.select("h", "a", "x")) == _rows(df)
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_sql_group_by_equals_dataframe_api(spark, pdf):
+    df = _df(spark, pdf)
+    df.createOrReplaceTempView("prop_t")
+    got = sorted((tuple(r) for r in spark.sql(
+        "SELECT h, count(*) AS n, sum(a) AS s FROM prop_t WHERE a IS NOT NULL GROUP BY h").collect()), key=repr)
+    want = sorted((tuple(r) for r in df.filter(F.col("a").isNotNull()).groupBy("h").agg(
+        F.count(F.lit(1)).alias("n"), F.sum("a").alias("s")).collect()), key=repr)
+    assert got == want
+
+
+@SETTINGS
+@given(a=tables(max_rows=20), b=tables(max_rows=20))
+def test_set_operations(spark, a, b):
+    da, db = _df(spark, a).select("h", "a"), _df(spark, b).select("h", "a")
+    A = [(_py(h), _py(v)) for h, v in zip(a["h"], a["a"])]
+    B = [(_py(h), _py(v)) for h, v in zip(b["h"], b["a"])]
+    rs = lambda df: sorted((tuple(r) for r in df.collect()), key=repr)  # noqa: E731
+    assert rs(da.union(db)) == sorted(A + B, key=repr)
+    assert rs(da.intersect(db)) == sorted(set(A) & set(B), key=repr)
+    assert rs(da.subtract(db)) == sorted(set(A) - set(B), key=repr)
