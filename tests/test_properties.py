@@ -242,3 +242,132 @@ def test_set_operations(spark, a, b):
     assert rs(da.union(db)) == sorted(A + B, key=repr)
     assert rs(da.intersect(db)) == sorted(set(A) & set(B), key=repr)
     assert rs(da.subtract(db)) == sorted(set(A) - set(B), key=repr)
+
+
+# ------------------------------------------------------------------ expressions and ML transformers
+@SETTINGS
+@given(pdf=tables())
+def test_arithmetic_coalesce_and_case_propagate_nulls(spark, pdf):
+    out = _df(spark, pdf).select(
+        (F.col("a") * 2 + 1).alias("p"), F.coalesce(F.col("a"), F.lit(-1)).alias("c"),
+        F.when(F.col("a").isNull(), "none").when(F.col("a") < 0, "neg").otherwise("pos").alias("w"),
+        (F.col("a") / F.lit(4)).alias("q"), F.abs(F.col("a")).alias("ab")).collect()
+    for r, a in zip(out, pdf["a"]):
+        a = _py(a)
+        assert r["p"] == (None if a is None else a * 2 + 1)
+        assert r["c"] == (-1 if a is None else a)
+        assert r["w"] == ("none" if a is None else "neg" if a < 0 else "pos")
+        assert r["q"] == (None if a is None else a / 4)
+        assert r["ab"] == (None if a is None else abs(a))
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_fillna_and_isin(spark, pdf):
+    df = _df(spark, pdf)
+    got = [tuple(r) for r in df.fillna({"a": 7, "h": "zz"}).select("h", "a").collect()]
+    want = [("zz" if _py(h) is None else h, 7 if _py(a) is None else _py(a)) for h, a in zip(pdf["h"], pdf["a"])]
+    assert got == want
+    n = df.filter(F.col("h").isin("h1", "h3")).count()
+    assert n == sum(1 for h in pdf["h"] if h in ("h1", "h3"))
+
+
+@SETTINGS
+@given(pdf=tables(min_rows=1))
+def test_string_indexer_frequency_order_and_round_trip(spark, pdf):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import IndexToString, StringIndexer
+    df = _df(spark, pdf).na.drop(subset=["h"])
+    vals = [h for h in pdf["h"] if h is not None]
+    if not vals:
+        return
+    model = StringIndexer(inputCol="h", outputCol="hi").fit(df)
+    # Spark's frequencyDesc: most frequent first, ties alphabetical
+    cnt = {v: vals.count(v) for v in set(vals)}
+    assert list(model.labels) == sorted(cnt, key=lambda v: (-cnt[v], v))
+    out = IndexToString(inputCol="hi", outputCol="hb", labels=model.labels).transform(model.transform(df))
+    assert [r["hb"] for r in out.select("hb").collect()] == vals
+
+
+@SETTINGS
+@given(xs=st.lists(st.floats(-1e3, 1e3, allow_nan=False), min_size=2, max_size=40),
+       splits=st.lists(st.floats(-500, 500, allow_nan=False), min_size=1, max_size=5, unique=True))
+def test_bucketizer_matches_numpy_digitize(spark, xs, splits):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import Bucketizer
+    edges = [-math.inf] + sorted(splits) + [math.inf]
+    df = spark.createDataFrame(pd.DataFrame({"x": xs}))
+    got = [r["b"] for r in Bucketizer(splits=edges, inputCol="x", outputCol="b").transform(df).select("b").collect()]
+    # buckets [e_i, e_{i+1}); the last bucket also holds its upper edge
+    want = [float(min(np.searchsorted(edges, v, side="right") - 1, len(edges) - 2)) for v in xs]
+    assert got == want
+
+
+@SETTINGS
+@given(data=st.lists(st.lists(st.floats(-100, 100, allow_nan=False), min_size=3, max_size=3), min_size=2,
+                     max_size=30), with_mean=st.booleans())
+def test_standard_scaler_matches_numpy(spark, data, with_mean):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import StandardScaler, VectorAssembler
+    X = np.array(data)
+    df = VectorAssembler(inputCols=["a", "b", "c"], outputCol="f").transform(
+        spark.createDataFrame(pd.DataFrame(X, columns=["a", "b", "c"])))
+    m = StandardScaler(inputCol="f", outputCol="s", withMean=with_mean, withStd=True).fit(df)
+    std = X.std(0, ddof=1)
+    np.testing.assert_allclose(m.std.toArray(), std, rtol=1e-9, atol=1e-12)
+    out = np.array([r["s"].toArray() for r in m.transform(df).select("s").collect()])
+    ref = (X - X.mean(0)) if with_mean else X.copy()
+    ref = np.where(std > 0, ref / np.where(std > 0, std, 1.0), 0.0)
+    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-9)
+
+
+@SETTINGS
+@given(pdf=tables(), lo=st.integers(-3, 0), hi=st.integers(0, 3))
+def test_window_rows_frame_sum_matches_python(spark, pdf, lo, hi):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql.window import Window
+    df = _df(spark, pdf).withColumn("id", F.monotonically_increasing_id())
+    w = Window.partitionBy("h").orderBy("id").rowsBetween(lo, hi)
+    out = df.select("h", "id", "a", F.sum("a").over(w).alias("s"), F.count("a").over(w).alias("c")).collect()
+    by = {}
+    for r in sorted(out, key=lambda r: r["id"]):
+        by.setdefault(r["h"], []).append(r)
+    for rows in by.values():
+        for i, r in enumerate(rows):
+            win = [x["a"] for x in rows[max(0, i + lo): i + hi + 1] if x["a"] is not None]
+            assert r["c"] == len(win)
+            assert r["s"] == (sum(win) if win else None)
+
+
+@SETTINGS
+@given(pdf=tables())
+def test_pivot_sum_matches_pandas(spark, pdf):
+    df = _df(spark, pdf).na.drop(subset=["h"]).withColumn("p", F.when(F.col("a") > 0, "pos").otherwise("npos"))
+    got = {r["h"]: (r["npos"] if "npos" in r.asDict() else None, r["pos"] if "pos" in r.asDict() else None)
+           for r in df.groupBy("h").pivot("p", ["npos", "pos"]).agg(F.sum("a")).collect()}
+    for h in {x for x in pdf["h"] if x is not None}:
+        sub = pdf[pdf["h"] == h]
+        for j, sel in enumerate([~(sub["a"] > 0).fillna(False), (sub["a"] > 0).fillna(False)]):
+            vals = [int(v) for v in sub["a"][sel] if v is not pd.NA]
+            assert got[h][j] == (sum(vals) if vals else None)
+
+
+@SETTINGS
+@given(vals=st.lists(st.one_of(st.none(), st.integers(-10**6, 10**6), st.text("0123456789.-e ", max_size=6)),
+                     max_size=30))
+def test_string_to_numeric_casts_are_null_on_garbage(spark, vals):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    strs = [None if v is None else str(v) for v in vals]
+    df = spark.createDataFrame([(s,) for s in strs], T.StructType([T.StructField("s", T.StringType(), True)]))
+    got = [r[0] for r in df.select(F.col("s").cast("int")).collect()]
+    for s, g in zip(strs, got):
+        if s is None:
+            assert g is None
+            continue
+        t = s.strip()
+        try:
+            want = int(t) if t and (t.lstrip("-").isdigit() and t.count("-") <= 1) else None
+        except ValueError:
+            want = None
+        if want is not None and not (-2**31 <= want < 2**31):
+            want = None
+        if want is not None or g is not None:
+            # Spark also accepts a decimal string for int (truncating): only check the digit-only strings
+            if want is not None:
+                assert g == want, (s, g)
