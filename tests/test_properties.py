@@ -1,8 +1,10 @@
 """Property-based tests (hypothesis) of the frame operations of the reference workflow (SURVEY.md §4.2,
 unit tier): na.drop, BETWEEN, when/otherwise, randomSplit, groupBy aggregates and the CSV round trip,
 each against a pandas / numpy statement of the same semantics on generated tables with nulls; plus the
-exact pruned Lloyd step against the full one on generated data."""
+exact pruned Lloyd step against the full one on generated data. Tables run on host columns and, on a
+GPU box, on device columns."""
 import math
+import os
 
 import numpy as np
 import pandas as pd
@@ -14,12 +16,24 @@ from hypothesis import strategies as st
 from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
 from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import functions as F
 
-SETTINGS = settings(max_examples=20, deadline=None, suppress_health_check=[HealthCheck.function_scoped_fixture])
+# CML_PROP_EXAMPLES raises the example count for a deeper search (default 20 keeps the suite fast)
+SETTINGS = settings(max_examples=int(os.environ.get("CML_PROP_EXAMPLES", 20)), deadline=None,
+                    suppress_health_check=[HealthCheck.function_scoped_fixture])
 
 
-@pytest.fixture(scope="module")
-def spark():
-    return SparkSession.builder.master("local[1]").getOrCreate()
+@pytest.fixture(scope="module", params=["local[1]", pytest.param("mi355x", marks=pytest.mark.gpu)])
+def spark(request):
+    """The same properties on host columns and on HBM-resident device columns (device sort / join /
+    group-by / window paths)."""
+    if request.param == "local[1]":  # any active host session will do (other modules share it)
+        yield SparkSession.builder.master(request.param).getOrCreate()
+        return
+    act = SparkSession.getActiveSession()
+    if act is not None and not act._stopped and act.conf.get("spark.master", None) != request.param:
+        act.stop()
+    s = SparkSession.builder.master(request.param).getOrCreate()
+    yield s
+    s.stop()
 
 
 _val = st.one_of(st.none(), st.integers(-50, 50))
@@ -310,7 +324,7 @@ def test_standard_scaler_matches_numpy(spark, data, with_mean):
     df = VectorAssembler(inputCols=["a", "b", "c"], outputCol="f").transform(
         spark.createDataFrame(pd.DataFrame(X, columns=["a", "b", "c"])))
     m = StandardScaler(inputCol="f", outputCol="s", withMean=with_mean, withStd=True).fit(df)
-    std = X.std(0, ddof=1)
+    std = np.where(np.ptp(X, 0) == 0, 0.0, X.std(0, ddof=1))  # constant column: exactly 0, as Spark's summarizer
     np.testing.assert_allclose(m.std.toArray(), std, rtol=1e-9, atol=1e-12)
     out = np.array([r["s"].toArray() for r in m.transform(df).select("s").collect()])
     ref = (X - X.mean(0)) if with_mean else X.copy()
