@@ -388,3 +388,79 @@ def test_string_to_numeric_casts_are_null_on_garbage(spark, vals):
             # Spark also accepts a decimal string for int (truncating): only check the digit-only strings
             if want is not None:
                 assert g == want, (s, g)
+
+
+# ------------------------------------------------------------------ evaluators and linear models vs oracles
+@SETTINGS
+@given(y=st.lists(st.floats(-50, 50, allow_nan=False), min_size=2, max_size=40), noise=st.integers(0, 10_000))
+def test_regression_evaluator_metrics(spark, y, noise):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.evaluation import RegressionEvaluator
+    rs = np.random.RandomState(noise)
+    yt = np.array(y)
+    yp = yt + rs.randn(len(yt)) * rs.choice([0.0, 0.5, 5.0])
+    df = spark.createDataFrame(pd.DataFrame({"label": yt, "prediction": yp}))
+    err = yp - yt
+    want = {"rmse": math.sqrt(np.mean(err ** 2)), "mse": np.mean(err ** 2), "mae": np.mean(np.abs(err))}
+    sst = np.sum((yt - yt.mean()) ** 2)
+    for name, v in want.items():
+        got = RegressionEvaluator(metricName=name).evaluate(df)
+        assert math.isclose(got, v, rel_tol=1e-9, abs_tol=1e-9), (name, got, v)
+    if sst > 1e-9:
+        got = RegressionEvaluator(metricName="r2").evaluate(df)
+        assert math.isclose(got, 1 - np.sum(err ** 2) / sst, rel_tol=1e-7, abs_tol=1e-7)
+
+
+@SETTINGS
+@given(labels=st.lists(st.integers(0, 3), min_size=1, max_size=50), flip=st.integers(0, 10_000))
+def test_multiclass_evaluator_matches_sklearn(spark, labels, flip):
+    from sklearn import metrics as skm
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.evaluation import \
+        MulticlassClassificationEvaluator
+    rs = np.random.RandomState(flip)
+    yt = np.array(labels, dtype=float)
+    yp = np.where(rs.rand(len(yt)) < 0.3, rs.randint(0, 4, len(yt)), yt).astype(float)
+    df = spark.createDataFrame(pd.DataFrame({"label": yt, "prediction": yp}))
+    ev = MulticlassClassificationEvaluator
+    assert math.isclose(ev(metricName="accuracy").evaluate(df), skm.accuracy_score(yt, yp), rel_tol=1e-12)
+    # Spark's weighted metrics weight each label class by its frequency in the LABEL column
+    assert math.isclose(ev(metricName="weightedPrecision").evaluate(df),
+                        skm.precision_score(yt, yp, average="weighted", zero_division=0), rel_tol=1e-9, abs_tol=1e-12)
+    assert math.isclose(ev(metricName="weightedRecall").evaluate(df),
+                        skm.recall_score(yt, yp, average="weighted", zero_division=0), rel_tol=1e-9, abs_tol=1e-12)
+
+
+@SETTINGS
+@given(n=st.integers(5, 60), scores=st.integers(0, 10_000), ties=st.booleans())
+def test_binary_auc_matches_sklearn(spark, n, scores, ties):
+    from sklearn import metrics as skm
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.evaluation import \
+        BinaryClassificationEvaluator
+    rs = np.random.RandomState(scores)
+    y = rs.randint(0, 2, n).astype(float)
+    if y.min() == y.max():
+        y[0] = 1.0 - y[0]
+    s = rs.randn(n) + y
+    if ties:
+        s = np.round(s)  # tied scores: Spark's curve takes every distinct threshold once
+    df = spark.createDataFrame(pd.DataFrame({"label": y, "rawPrediction": s}))
+    got = BinaryClassificationEvaluator(rawPredictionCol="rawPrediction").evaluate(df)
+    assert math.isclose(got, skm.roc_auc_score(y, s), rel_tol=1e-9, abs_tol=1e-12)
+
+
+@SETTINGS
+@given(n=st.integers(8, 80), d=st.integers(1, 4), seed=st.integers(0, 10_000))
+def test_linear_regression_normal_equations_match_lstsq(spark, n, d, seed):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import LinearRegression
+    rs = np.random.RandomState(seed)
+    X = rs.randn(n, d) * rs.uniform(0.5, 5, d) + rs.uniform(-3, 3, d)
+    y = X @ rs.randn(d) + 2.0 + rs.randn(n) * 0.1
+    cols = [f"c{i}" for i in range(d)]
+    pdf = pd.DataFrame(X, columns=cols)
+    pdf["y"] = y
+    df = VectorAssembler(inputCols=cols, outputCol="features").transform(spark.createDataFrame(pdf))
+    m = LinearRegression(labelCol="y", solver="normal").fit(df)
+    A = np.hstack([X, np.ones((n, 1))])
+    coef = np.linalg.lstsq(A, y, rcond=None)[0]
+    np.testing.assert_allclose(m.coefficients.toArray(), coef[:d], rtol=1e-6, atol=1e-8)
+    assert math.isclose(m.intercept, coef[d], rel_tol=1e-6, abs_tol=1e-8)
