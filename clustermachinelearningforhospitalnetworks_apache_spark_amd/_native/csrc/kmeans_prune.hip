@@ -111,7 +111,50 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   }
 }
 
+// Lower bounds of the candidate rows from their GEMM block dist[r][j] = |c_j|² - 2 x_r·c_j (f32, k
+// columns): lb[r] = sqrt(max(min_{j != lab[r]} dist[r][j] + xn[r] - tau·(xn[r] + mc), 0)) rounded down.
+// 16 lanes per row read its k floats as 16-byte loads (one contiguous 1 KiB row at k = 256), then a
+// 4-step xor-shuffle min; one launch replaces the mask / row-min / bound elementwise passes.
+__global__ __launch_bounds__(kThreads) void kmeans_prune_lower_kernel(const float* __restrict__ dist, int k,
+                                                                      const int* __restrict__ lab,
+                                                                      const float* __restrict__ xn, float mc,
+                                                                      float tau, long long m,
+                                                                      float* __restrict__ lb) {
+  const long long r = (long long)blockIdx.x * (kThreads / 16) + (threadIdx.x >> 4);
+  const int sub = threadIdx.x & 15;
+  float best = __builtin_huge_valf();
+  const int a = r < m ? lab[r] : -1;
+  if (r < m) {
+    const float4* row = reinterpret_cast<const float4*>(dist + r * (long long)k);
+    for (int c4 = sub; c4 < (k >> 2); c4 += 16) {
+      const float4 v = row[c4];
+      const int c = c4 << 2;
+      best = fminf(best, c + 0 == a ? best : v.x);
+      best = fminf(best, c + 1 == a ? best : v.y);
+      best = fminf(best, c + 2 == a ? best : v.z);
+      best = fminf(best, c + 3 == a ? best : v.w);
+    }
+  }
+#pragma unroll
+  for (int o = 8; o > 0; o >>= 1) best = fminf(best, __shfl_xor(best, o, 64));
+  if (r < m && sub == 0) {
+    const float x = xn[r];
+    const float sec = best + x - tau * (x + mc);
+    lb[r] = sqrtf(fmaxf(sec, 0.f)) * (1.0f - 1e-6f);
+  }
+}
+
 }  // namespace
+
+CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, const float* xn, float mc, float tau,
+                                   long long m, float* lb, void* stream) {
+  if (k <= 0 || (k & 3) || ((uintptr_t)dist & 15) || m < 0) return (int)hipErrorInvalidValue;
+  if (m == 0) return 0;
+  const long long rows_per_block = kThreads / 16;
+  hipLaunchKernelGGL(kmeans_prune_lower_kernel, dim3((unsigned)((m + rows_per_block - 1) / rows_per_block)),
+                     dim3(kThreads), 0, (hipStream_t)stream, dist, k, lab, xn, mc, tau, m, lb);
+  return cml_status();
+}
 
 // Moves every row's bounds by the centre drifts; rows whose bounds no longer prove the label are
 // appended to cand, their number added to *count (zeroed by the caller). dmax = {largest drift,

@@ -411,8 +411,8 @@ class LloydEngine:
         else:
             cbt = self.centers.t()
             cn = st.cn
-        if chunk is None:  # [chunk, k] f32 blocks of 512 MiB at k = 256 (64 MiB blocks measured slower)
-            chunk = max(1024, (512 << 20) // (4 * max(k, 1)))
+        if chunk is None:  # [chunk, k] f32 blocks (CML_PRUNE_CHUNK_MB, default 512 MiB)
+            chunk = max(1024, (int(os.environ.get("CML_PRUNE_CHUNK_MB", 512)) << 20) // (4 * max(k, 1)))
         for s0 in range(0, xg.shape[0], chunk):
             xc = xg[s0:s0 + chunk]
             xn = xng[s0:s0 + chunk].to(cn.dtype)
@@ -422,6 +422,12 @@ class LloydEngine:
                         xc = xc.to(torch.bfloat16)
                     # |c_j|² - 2 x·c_j with the bias and scale in the GEMM epilogue (one f32 write)
                     dist = torch.addmm(cn, xc, cbt, out_dtype=torch.float32, alpha=-2.0)
+                    if k % 4 == 0 and out.dtype == torch.float32:  # masked row min + bound in one pass
+                        labc = lab[s0:s0 + chunk]
+                        labc = labc if labc.dtype == torch.int32 else labc.to(torch.int32)
+                        K.prune_lower(dist, labc.contiguous(), xn.contiguous(), st.mc, self._PRUNE_TAU,
+                                      out[s0:s0 + chunk])
+                        continue
                 else:
                     dist = torch.addmm(cn, xc, cbt, alpha=-2.0)
                 dist.scatter_(1, lab[s0:s0 + chunk].long()[:, None], math.inf)
@@ -433,22 +439,30 @@ class LloydEngine:
 
     @staticmethod
     def _moved_sums(delta: torch.Tensor, k: int, d: int, xs: torch.Tensor, xq: torch.Tensor, new: torch.Tensor,
-                    old: torch.Tensor, chunk: int = 1 << 17) -> None:
-        """delta += the per-centre [Σx | count | Σ|x|²] change of rows moving old -> new, as one f64 GEMM
-        per chunk with a {-1, 0, +1} move matrix (sums of bf16 / fp8 rows are exact in f64, so the
-        result does not depend on the GEMM's summation order; scatter-add atomics on 256 rows of
-        centres serialise)."""
+                    old: torch.Tensor, chunk: int = 1 << 17, split: int = 64) -> None:
+        """delta += the per-centre [Σx | count | Σ|x|²] change of rows moving old -> new: an f64 GEMM of
+        a {-1, 0, +1} move matrix with [x | 1 | |x|²] (sums of bf16 / fp8 rows are exact in f64, so the
+        result does not depend on the summation order; scatter-add atomics onto k rows serialise). The
+        row dimension is split into ``split`` batches so the tiny k x (d + 2) output still spreads over
+        every CU (one plain GEMM ran 4 workgroups: 14 ms per 128K rows)."""
         kd = k * d
-        sums, cnt, q = delta[:kd].view(k, d), delta[kd:kd + k], delta[kd + k:]
         for s0 in range(0, xs.shape[0], chunk):
             nw, o = new[s0:s0 + chunk], old[s0:s0 + chunk]
-            w = torch.zeros((nw.shape[0], k), dtype=torch.float64, device=xs.device)
-            w.scatter_(1, nw[:, None], 1.0)
-            w.scatter_(1, o[:, None], -1.0)
-            wt = w.t()
-            sums += wt @ xs[s0:s0 + chunk]
-            cnt += w.sum(0)
-            q += wt @ xq[s0:s0 + chunk]
+            c = nw.shape[0]
+            b = max(1, min(split, c // 256))
+            cp = -(-c // b) * b
+            w = torch.zeros((cp, k), dtype=torch.float64, device=xs.device)
+            ar = torch.arange(c, device=xs.device)
+            w[ar, nw] = 1.0
+            w[ar, o] = -1.0
+            v = torch.zeros((cp, d + 2), dtype=torch.float64, device=xs.device)
+            v[:c, :d] = xs[s0:s0 + chunk]
+            v[:c, d] = 1.0
+            v[:c, d + 1] = xq[s0:s0 + chunk]
+            part = torch.bmm(w.view(b, cp // b, k).transpose(1, 2), v.view(b, cp // b, d + 2)).sum(0)
+            delta[:kd].view(k, d).add_(part[:, :d])
+            delta[kd:kd + k].add_(part[:, d])
+            delta[kd + k:].add_(part[:, d + 1])
 
     def _step_prune(self) -> None:
         """One exact Lloyd iteration: bounds pass (K9p), the rows it cannot prove are gathered and

@@ -50,6 +50,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                   c_vp]),
+    "cml_kmeans_prune_lower": (c_int, [c_vp, c_int, c_vp, c_vp, ctypes.c_float, ctypes.c_float, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_int, c_ll, c_vp,
                                         c_vp, c_vp]),
 })
@@ -374,6 +375,16 @@ def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift
     idx = torch.nonzero(~keep).flatten()
     cand[: idx.numel()] = idx.to(cand.dtype)
     count[0] = idx.numel()
+
+
+def prune_lower(dist: torch.Tensor, lab: torch.Tensor, xn: torch.Tensor, mc: float, tau: float,
+                out: torch.Tensor, stream=None) -> None:
+    """K9p lower bounds (``kmeans_prune.hip``) from a [m, k] f32 block of |c_j|² - 2 x·c_j:
+    out = sqrt(max(min_{j != lab} dist + xn - tau·(xn + mc), 0)), rounded down."""
+    m, k = dist.shape
+    _native.check(_native.kernels().cml_kmeans_prune_lower(
+        dist.data_ptr(), int(k), lab.data_ptr(), xn.data_ptr(), float(mc), float(tau), int(m), out.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_prune_lower")
 
 
 def seg_buffer_ints(k: int) -> int:

@@ -202,3 +202,19 @@ def test_kmeans_estimator_prune_conf_cpu():
     assert pruned.summary.numIter == full.summary.numIter
     assert pruned.summary.clusterSizes == full.summary.clusterSizes
     assert abs(pruned.summary.trainingCost - full.summary.trainingCost) <= 1e-9 * full.summary.trainingCost
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("m,k", [(100_003, 256), (777, 64), (5, 12)])
+def test_lower_bound_kernel_matches_torch(m, k):
+    g = torch.Generator(device="cuda")
+    g.manual_seed(m)
+    dist = torch.randn(m, k, device="cuda", generator=g) * 100
+    lab = torch.randint(0, k, (m,), device="cuda", generator=g, dtype=torch.int32)
+    xn = torch.rand(m, device="cuda", generator=g) * 500 + 200
+    out = torch.empty(m, device="cuda")
+    K.prune_lower(dist, lab, xn, 300.0, 3e-5, out)
+    ref = dist.double().scatter(1, lab.long()[:, None], float("inf")).min(1).values + xn.double()
+    ref = (ref - 3e-5 * (xn.double() + 300.0)).clamp(min=0).sqrt()
+    torch.testing.assert_close(out.double(), ref, rtol=2e-6, atol=1e-5)
+    assert bool((out.double() <= ref * (1 + 1e-7) + 1e-6).all())
