@@ -216,6 +216,10 @@ class DataStreamWriter:
         if self._mode == "update" and has_agg and (table is not None or path is not None):
             raise ValueError("update output mode is not supported by table / file sinks; use foreachBatch or "
                              "the memory / console sinks")
+        if table is not None and not has_agg and not session.catalog.tableExists(table):
+            # like Spark's toTable: the sink table exists (empty, with the stream's schema) from the start,
+            # so readers of the unbounded table do not fail before the first file arrives
+            session.catalog.createTable(table, schema=self._df.schema)
         q = StreamingQuery(session, self._df._stream, self, table=table, path=path)
         session.streams._register(q)
         q._launch()
