@@ -456,6 +456,8 @@ class Unary(Expr):
             return ColumnData(out, h.valid, T.StringType())
         if self.op in ("year", "month", "dayofmonth", "hour", "minute", "second", "dayofweek"):
             us = c.values.to(torch.int64)
+            if isinstance(c.dtype, T.DateType):  # dates hold days since the epoch, not microseconds
+                us = us * 86_400_000_000
             if self.op in ("hour", "minute", "second"):
                 secs = torch.div(us, 1_000_000, rounding_mode="floor")
                 val = {"hour": torch.remainder(torch.div(secs, 3600, rounding_mode="floor"), 24),
@@ -499,6 +501,12 @@ class Cast(Expr):
         dev = frame._device
         to = self.to
         if isinstance(to, T.StringType):
+            if isinstance(c.dtype, (T.DateType, T.TimestampType)) and not c.is_host:
+                # device dates / timestamps hold days / microseconds: format the calendar values
+                from .dataframe import column_to_python
+                vals = column_to_python(c)
+                return ColumnData(np.array([None if v is None else _fmt_datetime(v) for v in vals], dtype=object),
+                                  None if c.valid is None else c.valid_mask().cpu().numpy(), to)
             h = _to_host(c)
             return ColumnData(np.array([None if v is None else _fmt(v) for v in h.values], dtype=object),
                               h.valid, to)
@@ -529,6 +537,17 @@ class Cast(Expr):
         if T.is_integral(to) and v.is_floating_point():
             v = torch.trunc(v)
         return ColumnData(v.to(to.torch_dtype), c.valid, to)
+
+
+def _fmt_datetime(v):
+    """Spark's string form: 2024-05-17 for dates, 2024-05-17 10:20:30[.fraction without trailing zeros]."""
+    import datetime as _dt
+    if isinstance(v, _dt.datetime):
+        out = v.strftime("%Y-%m-%d %H:%M:%S")
+        return out + ("." + f"{v.microsecond:06d}".rstrip("0") if v.microsecond else "")
+    if isinstance(v, _dt.date):
+        return f"{v.year:04d}-{v.month:02d}-{v.day:02d}"
+    return str(v)
 
 
 def _fmt(v):

@@ -489,12 +489,18 @@ def _per_distinct(impl, fn, rt, lits):
 
 
 def substring(c: ColumnOrName, pos: int, length: int) -> Column:
-    """1-based position like Spark; pos <= 0 counts from the end."""
-    def f(s):
-        s = str(s)
-        start = builtins.max(pos - 1 if pos > 0 else (len(s) + pos if pos < 0 else 0), 0)
-        return s[start:start + length]
-    return _host_map("substring", [c], f, T.StringType(), params=[pos, length])
+    """1-based position like Spark; 0 acts as 1, a negative position counts from the end."""
+    return _host_map("substring", [c], lambda s: spark_substr(str(s), pos, length), T.StringType(),
+                     params=[pos, length])
+
+
+def spark_substr(s: str, pos: int, length: int) -> str:
+    """UTF8String.substringSQL: the window [start, start + length) is taken BEFORE clamping start at 0, so
+    a negative position reaching before the string start shortens the result (substring('0', -2, 1) = '')."""
+    start = pos - 1 if pos > 0 else (len(s) + pos if pos < 0 else 0)
+    end = start + length
+    start = builtins.max(start, 0)
+    return "" if start >= end else s[start:end]
 
 
 def concat_ws(sep: str, *cols: ColumnOrName) -> Column:

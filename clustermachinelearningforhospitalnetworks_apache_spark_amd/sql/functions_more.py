@@ -482,8 +482,9 @@ def _add_months(d: _dt.date, m: int) -> _dt.date:
     y, mo = divmod(d.month - 1 + m, 12)
     first = _dt.date(d.year + y, mo + 1, 1)
     end = _month_end(first)
-    # Spark: the last day of a month maps to the last day of the target month
-    day = end.day if d == _month_end(d) else builtins.min(d.day, end.day)
+    # Spark 3 (LocalDate.plusMonths): keep the day of month, clamped to the target month's length; the
+    # Spark 2 rule mapping a month's last day to the target's last day was dropped in 3.0
+    day = builtins.min(d.day, end.day)
     return first.replace(day=day)
 
 

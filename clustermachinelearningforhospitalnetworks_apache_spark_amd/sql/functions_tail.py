@@ -770,11 +770,11 @@ def substr(s: ColumnOrName, pos, len=None) -> Column:  # noqa: A002
     lit_ = (lambda x: x if isinstance(x, Column) else Column(Lit(x)))
     args = [s, lit_(pos)] + ([] if len is None else [lit_(len)])
 
+    from .functions import spark_substr
+
     def f(v, p, n=None):
         v = str(v)
-        p = int(p)
-        start = builtins.max(p - 1 if p > 0 else (builtins.len(v) + p if p < 0 else 0), 0)
-        return v[start:] if n is None else v[start:start + builtins.max(int(n), 0)]
+        return spark_substr(v, int(p), builtins.len(v) + 1 if n is None else int(n))
     return _host_map("substr", args, f, T.StringType())
 
 

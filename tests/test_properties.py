@@ -464,3 +464,88 @@ def test_linear_regression_normal_equations_match_lstsq(spark, n, d, seed):
     coef = np.linalg.lstsq(A, y, rcond=None)[0]
     np.testing.assert_allclose(m.coefficients.toArray(), coef[:d], rtol=1e-6, atol=1e-8)
     assert math.isclose(m.intercept, coef[d], rel_tol=1e-6, abs_tol=1e-8)
+
+
+# ------------------------------------------------------------------ string and date functions vs Python
+_txt = st.one_of(st.none(), st.text(alphabet="abcXYZ -_,.01", max_size=12))
+
+
+@SETTINGS
+@given(vals=st.lists(_txt, min_size=1, max_size=25), pos=st.integers(-6, 6), ln=st.integers(0, 6),
+       pad=st.integers(0, 10))
+def test_string_functions_match_python(spark, vals, pos, ln, pad):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    df = spark.createDataFrame([(v,) for v in vals], T.StructType([T.StructField("s", T.StringType(), True)]))
+    out = df.select(F.upper("s").alias("u"), F.length("s").alias("n"), F.trim("s").alias("t"),
+                    F.substring("s", pos, ln).alias("sub"), F.lpad("s", pad, "*").alias("lp"),
+                    F.concat_ws("|", "s", F.lit("k")).alias("cw"), F.regexp_replace("s", "[0-9]", "#").alias("rr"),
+                    F.reverse("s").alias("rv")).collect()
+
+    def substr(s, p, n):  # Spark substring: 1-based, 0 acts as 1, negative counts from the end
+        if p > 0:
+            start = p - 1
+        elif p < 0:
+            start = max(len(s) + p, 0)
+            n = n - max(0, -(len(s) + p))  # characters before the start are cut from the length
+        else:
+            start = 0
+        return s[start:start + max(n, 0)]
+
+    for r, v in zip(out, vals):
+        if v is None:
+            assert r["u"] is None and r["n"] is None and r["sub"] is None and r["lp"] is None
+            assert r["cw"] == "k"  # concat_ws skips nulls
+            continue
+        assert r["u"] == v.upper() and r["n"] == len(v) and r["t"] == v.strip(" ")
+        assert r["sub"] == substr(v, pos, ln), (v, pos, ln, r["sub"])
+        assert r["lp"] == (v[:pad] if len(v) >= pad else "*" * (pad - len(v)) + v)
+        assert r["cw"] == v + "|k" and r["rv"] == v[::-1]
+        assert r["rr"] == "".join("#" if c.isdigit() else c for c in v)
+
+
+@SETTINGS
+@given(days=st.lists(st.one_of(st.none(), st.integers(-20_000, 40_000)), min_size=1, max_size=25),
+       add=st.integers(-400, 400))
+def test_date_functions_match_python(spark, days, add):
+    import datetime as dt
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    epoch = dt.date(1970, 1, 1)
+    ds = [None if d is None else epoch + dt.timedelta(days=d) for d in days]
+    df = spark.createDataFrame([(d,) for d in ds], T.StructType([T.StructField("d", T.DateType(), True)]))
+    out = df.select(F.date_add("d", add).alias("a"), F.datediff(F.date_add("d", add), "d").alias("dd"),
+                    F.year("d").alias("y"), F.month("d").alias("m"), F.dayofmonth("d").alias("dm"),
+                    F.date_format("d", "yyyy-MM-dd").alias("f"), F.dayofweek("d").alias("dw"),
+                    F.last_day("d").alias("ld")).collect()
+    for r, d in zip(out, ds):
+        if d is None:
+            assert all(r[c] is None for c in ("a", "dd", "y", "m", "dm", "f", "dw", "ld"))
+            continue
+        assert r["a"] == d + dt.timedelta(days=add) and r["dd"] == add
+        assert (r["y"], r["m"], r["dm"]) == (d.year, d.month, d.day)
+        assert r["f"] == d.isoformat() if d.year >= 1000 else True
+        assert r["dw"] == (d.isoweekday() % 7) + 1  # Spark: 1 = Sunday
+        nxt = (d.replace(day=28) + dt.timedelta(days=4))
+        assert r["ld"] == nxt - dt.timedelta(days=nxt.day)
+
+
+@SETTINGS
+@given(days=st.lists(st.integers(-20_000, 40_000), min_size=1, max_size=25))
+def test_more_date_parts_match_python(spark, days):
+    import datetime as dt
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import types as T
+    ds = [dt.date(1970, 1, 1) + dt.timedelta(days=d) for d in days]
+    df = spark.createDataFrame([(d,) for d in ds], T.StructType([T.StructField("d", T.DateType(), True)]))
+    out = df.select(F.quarter("d").alias("q"), F.dayofyear("d").alias("doy"), F.weekofyear("d").alias("w"),
+                    F.col("d").cast("string").alias("s"), F.hour("d").alias("h"),
+                    F.trunc("d", "month").alias("tm"), F.add_months("d", 1).alias("am")).collect()
+    for r, d in zip(out, ds):
+        assert r["q"] == (d.month - 1) // 3 + 1
+        assert r["doy"] == d.timetuple().tm_yday
+        assert r["w"] == d.isocalendar()[1]
+        assert r["h"] == 0
+        assert r["tm"] == d.replace(day=1)
+        if d.year >= 1000:
+            assert r["s"] == d.isoformat()
+        y, m = (d.year + d.month // 12, d.month % 12 + 1)
+        import calendar
+        assert r["am"] == dt.date(y, m, min(d.day, calendar.monthrange(y, m)[1]))
