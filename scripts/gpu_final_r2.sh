@@ -12,4 +12,4 @@ timeout -k 10 300 python bench.py --steps 20 --warmup 3 > gpurun_out/final/bench
 cat gpurun_out/final/bench.json
 timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d /tmp/prof_final -o bench -- python3 bench.py --steps 10 --warmup 2 > gpurun_out/final/prof_bench.log 2>&1 || { tail -20 gpurun_out/final/prof_bench.log; exit 1; }
 for f in $(find /tmp/prof_final -name "*kernel_stats.csv"); do cp $f gpurun_out/final/bench_kernel_stats.csv; done
-cut -d, -f1-8 gpurun_out/final/bench_kernel_stats.csv | head -14 | cut -c1-200
+python3 -c "import csv;[print(r[\"Name\"][:100], r[\"Calls\"], r[\"Percentage\"]) for r in list(csv.DictReader(open(\"gpurun_out/final/bench_kernel_stats.csv\")))[:14]]"
