@@ -2,16 +2,16 @@
 """Headline benchmark: KMeans fit samples/sec (whole job), BASELINE.json config
 "KMeans k=256 on 100M×256, DP across MI355X with RCCL all-reduce of centroid sums".
 
-One step = one full distributed Lloyd iteration on the whole 100M-row dataset:
-K9 MFMA distance GEMM + argmin of EVERY row against EVERY centre, K10 per-cluster
-sums, RCCL all-reduce of the f64 [k·D sums | k counts | cost] message, K11 centre
-update.  K10 is the engine's default incremental form (sums of the current labels
-kept across steps, only rows whose label changed re-read; exact in f64, equal to
-the full re-accumulation — tests/test_kmeans_incremental_gpu.py); the JSON line
-also reports the same steps forced to re-accumulate every row
-(extra.full_accumulate_ms_per_step, or run with --full-accumulate).  The dataset is fixed (100M rows total) and sharded
-over the N ranks, so scaling is *strong*.  Data: synthetic Gaussian blobs
-generated on the GPU, bf16 features, random-init k-means|| centres (no network).
+The timed region is ONE WHOLE FIT from scratch, the metric SURVEY.md §6 / BASELINE.md define
+(samples/s = N_rows x Lloyd iterations / fit wall time): LloydEngine construction (device
+layout + row norms), k-means|| initialisation (initSteps=2, as Spark's KMeans.fit runs it) and
+--steps Lloyd iterations with tol=0, i.e. what ``KMeans(k=256, maxIter=steps, tol=0).fit`` runs
+(ml/clustering.py). A step = one distributed Lloyd iteration: K9r MFMA distance GEMM + argmin,
+K10 per-cluster sums, RCCL all-reduce of the f64 [k·D sums | k counts | cost] message, K11 centre
+update. --warmup runs an untimed warm-up fit of that many iterations first. The steady-state
+step rate after the fit is reported in extra (not the headline). The dataset is fixed (100M rows
+total) and sharded over the N ranks, so scaling is *strong*. Data: synthetic Gaussian blobs
+generated on the GPU, bf16 features (no network).
 
 Usage (driver contract):
     python bench.py --gpus 1 --steps 20 --warmup 3
@@ -48,21 +48,54 @@ def make_blobs(n: int, d: int, k_true: int, seed: int, device, dtype=torch.bfloa
     return x
 
 
+def _drop_norm_cache(x: torch.Tensor) -> None:
+    """The engine caches ||x||² on the feature tensor (Spark's VectorWithNorm); a timed fit must
+    compute them itself, so the cache of an earlier fit on the same tensor is dropped."""
+    if hasattr(x, "_cml_xnorm"):
+        del x._cml_xnorm
+
+
+def kmeans_fit(x, args, comm, seed: int = 42, iters: int = 20, breakdown: bool = False):
+    """One whole KMeans fit, as ``KMeans(k, maxIter=iters, tol=0).fit`` runs it (ml/clustering.py):
+    engine construction (device layout, row norms), k-means|| init (initSteps=2) and ``iters``
+    Lloyd iterations. Returns (engine, init seconds, per-iteration seconds or None)."""
+    gpu = x.is_cuda
+    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks,
+                      incremental=not args.full_accumulate, prune=args.prune)
+    eng.track_prune = breakdown
+    init = eng.init_kmeans_parallel(seed=seed) if args.init == "k-means||" else eng.init_random(seed=seed)
+    eng.set_centers(init)
+    if gpu and breakdown:
+        torch.cuda.synchronize()
+    t_init = time.perf_counter()
+    per = [] if breakdown else None
+    for _ in range(iters):
+        t = time.perf_counter()
+        eng.step()
+        if breakdown:
+            if gpu:
+                torch.cuda.synchronize()
+            per.append(time.perf_counter() - t)
+    return eng, t_init, per
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20)
-    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--steps", type=int, default=20, help="Lloyd iterations of the timed fit")
+    ap.add_argument("--warmup", type=int, default=3, help="Lloyd iterations of the untimed warm-up fit")
     ap.add_argument("--rows", type=int, default=100_000_000, help="total rows (strong scaling)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--k", type=int, default=256)
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
-    ap.add_argument("--prune", action="store_true",
-                    help="time the exact bound-pruned Lloyd step (LloydEngine(prune=True)) instead of the full "
-                         "assignment; without it the pruned step is still reported in extra")
+    ap.add_argument("--prune", default=None, choices=["on", "off"],
+                    help="force the exact bound-pruned Lloyd step on or off (default: what KMeans.fit uses)")
     ap.add_argument("--full-accumulate", action="store_true",
                     help="re-accumulate every row each step instead of the exact incremental sums")
+    ap.add_argument("--breakdown", action="store_true",
+                    help="also run one fit with a device sync after every iteration and report per-iteration "
+                         "times (extra.breakdown); the headline fit is never synchronised inside")
     ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
                          "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update; "
@@ -75,6 +108,7 @@ def main():
                     help="logreg workload: Spark's L-BFGS (full-batch passes) or data-parallel mini-batch SGD")
     ap.add_argument("--batch", type=int, default=1 << 20, help="logreg SGD rows per rank per step")
     args = ap.parse_args()
+    args.prune = None if args.prune is None else args.prune == "on"
     if args.workload == "logreg":
         return bench_logreg(args)
     if args.workload == "pipeline":
@@ -102,66 +136,61 @@ def main():
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
 
-    eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks, incremental=not args.full_accumulate,
-                      prune=args.prune)
-    t0 = time.perf_counter()
-    init = eng.init_kmeans_parallel(seed=42) if args.init == "k-means||" else eng.init_random(seed=42)
-    eng.set_centers(init)
-    if gpu:
-        torch.cuda.synchronize()
-    init_s = time.perf_counter() - t0
+    # untimed warm-up fit: code objects, allocator pools, RCCL channels (its results are discarded)
+    if args.warmup > 0:
+        eng, _, _ = kmeans_fit(x, args, comm, seed=7, iters=args.warmup)
+        del eng
+        _drop_norm_cache(x)
 
-    for _ in range(args.warmup):
-        eng.step()
+    # the timed region: one whole fit from scratch, bracketed by barrier + device sync on both sides
     comm.barrier()
     if gpu:
         torch.cuda.synchronize()
     t0 = time.perf_counter()
-    for _ in range(args.steps):
-        eng.step()
+    eng, t_init, _ = kmeans_fit(x, args, comm, seed=42, iters=args.steps)
     if gpu:
         torch.cuda.synchronize()
     comm.barrier()
-    elapsed = time.perf_counter() - t0
-    elapsed = comm.max_scalar(elapsed)
+    t1 = time.perf_counter()
+    elapsed = comm.max_scalar(t1 - t0)
+    init_s = comm.max_scalar(t_init - t0)
     cost = eng.training_cost()
     acc = {"accumulate": "incremental (exact)" if eng.delta is not None else "full",
-           "assign": "pruned (exact bounds)" if args.prune else "full (every row x every centre)"}
-    if args.prune:
+           "assign": "pruned (exact bounds)" if eng.prune else "full (every row x every centre)"}
+    if eng.prune:
         acc["last_step_prune_rank0"] = eng.prune_stats()
-    elif gpu and W == 1:
-        # the exact bound-pruned step (LloydEngine(prune=True)) from the same start, same step count:
-        # its ms/step and whether its labels equal the full step's after warmup + steps iterations
-        lab_full = eng.labels[: eng.n].clone()
-        pe = LloydEngine(x, args.dim, args.k, comm, prune=True)
-        pe.set_centers(init)
-        for _ in range(args.warmup):
-            pe.step()
+    if gpu:
+        # steady-state rate of the same step after the timed fit (not part of the headline)
         comm.barrier()
         torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            pe.step()
-        torch.cuda.synchronize()
-        comm.barrier()
-        acc["pruned_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - t1) / args.steps
-        same = float(torch.equal(pe.labels[: pe.n], lab_full))
-        acc["pruned_labels_equal_full"] = comm.max_scalar(1.0 - same) == 0.0
-        acc["pruned_last_step_rank0"] = pe.prune_stats()
-        del pe, lab_full
-    if eng.delta is not None and gpu:
-        # transparency: the same steps with every step forced to re-accumulate all rows
-        acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
-        acc["last_step_full_rank0"] = eng.delta.was_full()
-        comm.barrier()
-        torch.cuda.synchronize()
-        t1 = time.perf_counter()
-        for _ in range(args.steps):
-            eng.delta.invalidate()
+        ts = time.perf_counter()
+        for _ in range(5):
             eng.step()
         torch.cuda.synchronize()
         comm.barrier()
-        acc["full_accumulate_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - t1) / args.steps
+        acc["steady_state_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 5
+        if eng.delta is not None and not eng.prune:
+            acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
+            comm.barrier()
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            for _ in range(3):
+                eng.delta.invalidate()
+                eng.step()
+            torch.cuda.synchronize()
+            comm.barrier()
+            acc["full_accumulate_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
+    del eng
+    if args.breakdown:
+        _drop_norm_cache(x)
+        comm.barrier()
+        tb = time.perf_counter()
+        eng, tbi, per_it = kmeans_fit(x, args, comm, seed=42, iters=args.steps, breakdown=True)
+        acc["breakdown"] = {"init_ms": round(1000.0 * (tbi - tb), 3),
+                            "iteration_ms": [round(1000.0 * t, 3) for t in per_it]}
+        if eng.prune:
+            acc["breakdown"]["prune_history_rank0"] = eng.prune_history()
+        del eng
 
     total_rows = args.rows
     value = total_rows * args.steps / elapsed
@@ -181,16 +210,16 @@ def main():
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16" if gpu else "fp64",
-            "data": "synthetic (Gaussian blobs generated on device, random-init k-means|| centres)",
+            "data": "synthetic (Gaussian blobs generated on device; centres from k-means|| init inside the timed fit)",
             "config": {
                 "model": f"KMeans k={args.k}, {args.rows}x{args.dim}",
                 "global_batch": total_rows,
                 "seq_len": None,
                 "parallelism": f"dp{W}",
                 "k": args.k, "rows": total_rows, "dim": args.dim,
-                "row_chunks_per_rank": eng.row_chunks,
+                "timed": f"whole fit: engine + norms, k-means|| init, {args.steps} Lloyd iterations (tol=0)",
             },
-            "extra": {"datagen_s": round(gen_s, 3), "init_s": round(init_s, 3),
+            "extra": {"fit_s": round(elapsed, 4), "datagen_s": round(gen_s, 3), "init_s": round(init_s, 4),
                       "training_cost": cost, "device": torch.cuda.get_device_name(dev) if gpu else "cpu", **acc},
         }
         print(json.dumps(out), flush=True)

@@ -738,7 +738,10 @@ __global__ __launch_bounds__(kScatterThreads) void kmeans_scatter(const int* __r
       }
 #pragma unroll
       for (int u = 0; u < kScatterU; ++u)
-        if (lab[u] >= 0) perm[soff[lab[u]] + rk[u]] = (int)(r0 + u * stride + o);
+        if (lab[u] >= 0) {
+          const long long pos = (long long)soff[lab[u]] + rk[u];
+          if (pos < n) perm[pos] = (int)(r0 + u * stride + o);  // ranks from this step's assign: always
+        }
     }
   }
 }
@@ -1368,8 +1371,8 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
   const u16* c = (const u16*)C;
   if (rr_ct > 0) {  // K9r: single launch over every centre
     if (!(first && last) || kc != kp || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
-    return rr::dispatch(Dp, rr_ct, xfp8 != 0, X, n, ldx, c, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
-                        hist, rank, dout, grid, g_rr_dbg, st);
+    return rr::dispatch(0, Dp, rr_ct, xfp8 != 0, X, n, ldx, c, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+                        hist, rank, dout, rr::Ext{}, grid, g_rr_dbg, st);
   }
   if (xfp8) {
     switch (Dp) {
@@ -1392,6 +1395,34 @@ CML_API int cml_kmeans_assign_bf16(const void* X, long long n, long long ldx, in
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_ASSIGN
+}
+
+// K9r with the pruned-step extensions (kmeans_rr.h modes): mode 1 = every row + top-2 bounds
+// (ub/lb), mode 2 = the positions of a candidate list (idx, compacted xn/lab, count on the device)
+// + top-2 bounds. gate/want: the launch returns at once unless *gate == want (null: always runs).
+// hist/rank (counting-sort ranks) and the change log as for cml_kmeans_assign_bf16; mode 2 takes no
+// hist/rank. n is the row count (mode 1) or the capacity the grid is sized for (mode 2).
+CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long long ldx, int Dp, const void* C,
+                                     long long ldc, int kc, int kp, const float* cnorm, const float* xnorm,
+                                     int* labels, double* cost_part, int* hist, int* rank, int grid, int xfp8,
+                                     int* chg_rows, int* chg_old, int* chg_wg_count, int* chg_overflow, int chg_pcap,
+                                     int rr_ct, const int* idx, const int* n_dev, const int* lab_in, float* ub,
+                                     float* lb, const float* mc, float tau, const int* gate, int want, void* stream) {
+  if (mode < 1 || mode > 2 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
+  if (rr_ct <= 0 || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
+  if (xnorm == nullptr || ub == nullptr || lb == nullptr || mc == nullptr) return (int)hipErrorInvalidValue;
+  if ((hist == nullptr) != (rank == nullptr)) return (int)hipErrorInvalidValue;
+  if (mode == 2 && (idx == nullptr || n_dev == nullptr || lab_in == nullptr || hist != nullptr))
+    return (int)hipErrorInvalidValue;
+  if (chg_rows != nullptr && (chg_old == nullptr || chg_wg_count == nullptr || chg_overflow == nullptr || chg_pcap < 0))
+    return (int)hipErrorInvalidValue;
+  const long long lds = rr::lds_for(Dp, kp, xfp8 != 0, mode);
+  if (lds <= 0 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
+  const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
+  const rr::Ext ext{idx, n_dev, lab_in, ub, lb, mc, tau, gate, want};
+  return rr::dispatch(mode, Dp, rr_ct, xfp8 != 0, X, n, ldx, (const u16*)C, ldc, kc, kp, cnorm, xnorm, labels,
+                      nullptr, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }
 
 CML_API int cml_row_sqnorm_fp8(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {

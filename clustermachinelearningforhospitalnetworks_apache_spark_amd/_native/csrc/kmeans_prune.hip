@@ -41,10 +41,18 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
                                                                        float* __restrict__ lb,
                                                                        const float* __restrict__ drift,
                                                                        const float* __restrict__ dmax,
-                                                                       const float* __restrict__ thr, float c2,
-                                                                       int k, long long n, int* __restrict__ cand,
-                                                                       int* __restrict__ count) {
+                                                                       const float* __restrict__ thr,
+                                                                       const float* __restrict__ c2p, int k,
+                                                                       long long n, int* __restrict__ cand,
+                                                                       int* __restrict__ count,
+                                                                       const float* __restrict__ xn,
+                                                                       int* __restrict__ cand_lab,
+                                                                       float* __restrict__ cand_xn,
+                                                                       const int* __restrict__ skip,
+                                                                       long long cap) {
+  if (skip != nullptr && *skip != 0) return;  // bounds invalid this step (full pass instead)
   extern __shared__ __align__(16) unsigned char smem[];
+  const float c2 = *c2p;
   float* sd = reinterpret_cast<float*>(smem);  // [k] drift
   float* st = sd + k;                          // [k] threshold
   __shared__ int wsum[kThreads / 64];
@@ -107,7 +115,145 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   while (mask) {
     const int b = __ffs(mask) - 1;
     mask &= mask - 1;
-    cand[off++] = (int)(blk0 + ((long long)(b >> 2) * kThreads + threadIdx.x) * 4 + (b & 3));
+    const int row = (int)(blk0 + ((long long)(b >> 2) * kThreads + threadIdx.x) * 4 + (b & 3));
+    if (off >= cap) break;  // list full: *count still gets every candidate (the step then runs in full)
+    cand[off] = row;
+    if (cand_lab != nullptr) {  // compacted label / norm of the candidate (trailer of the K9r mode-2 pass)
+      cand_lab[off] = lab[row];
+      cand_xn[off] = xn[row];
+    }
+    ++off;
+  }
+}
+
+// Pruned-step mode: full pass (1) when the bounds are invalid (*force) or more than cap rows are
+// candidates, else the candidate pass (0); mode[1] keeps the candidate count. One thread.
+__global__ void kmeans_prune_gate_kernel(const int* __restrict__ count, long long cap, const int* __restrict__ force,
+                                         int* __restrict__ mode) {
+  const int full = (*force != 0 || (long long)*count > cap) ? 1 : 0;
+  mode[0] = full;
+  mode[1] = full ? 0 : *count;  // re-assigned rows of a candidate pass (stats; count is reset later)
+}
+
+// Centre statistics of the pruned step, part 1 (one workgroup per centre j, over the bf16 centres
+// the assign compares against, in f64): ||c_j||², drift_j = |c_j - old_j| rounded up, and
+// half_j = half the distance from c_j to its nearest other centre.
+__global__ __launch_bounds__(256) void kmeans_centre_stats_kernel(const u16* __restrict__ cb,
+                                                                  const u16* __restrict__ cb_old, long long ldc, int k,
+                                                                  int d, double* __restrict__ cn,
+                                                                  float* __restrict__ drift,
+                                                                  double* __restrict__ half) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* cj = reinterpret_cast<double*>(smem);  // [d]
+  __shared__ double red[256];
+  __shared__ double red2[256];
+  const int j = blockIdx.x, tid = threadIdx.x;
+  double nrm = 0.0, dr = 0.0;
+  for (int t = tid; t < d; t += 256) {
+    const double v = (double)bf16_to_f32(cb[(long long)j * ldc + t]);
+    cj[t] = v;
+    nrm += v * v;
+    if (cb_old != nullptr) {
+      const double o = v - (double)bf16_to_f32(cb_old[(long long)j * ldc + t]);
+      dr += o * o;
+    }
+  }
+  red[tid] = nrm;
+  red2[tid] = dr;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) {
+      red[tid] += red[tid + o];
+      red2[tid] += red2[tid + o];
+    }
+    __syncthreads();
+  }
+  if (tid == 0) {
+    cn[j] = red[0];
+    if (cb_old != nullptr) drift[j] = (float)(sqrt(red2[0]) * (1.0 + 1e-6));
+  }
+  __syncthreads();
+  // nearest other centre: thread t walks centres t, t+256, ... (each distance summed over d in f64)
+  double best = __builtin_huge_val();
+  for (int i = tid; i < k; i += 256) {
+    if (i == j) continue;
+    double s = 0.0;
+    for (int t = 0; t < d; ++t) {
+      const double e = (double)bf16_to_f32(cb[(long long)i * ldc + t]) - cj[t];
+      s += e * e;
+    }
+    best = s < best ? s : best;
+  }
+  red[tid] = best;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = red[tid + o] < red[tid] ? red[tid + o] : red[tid];
+    __syncthreads();
+  }
+  if (tid == 0) half[j] = 0.5 * sqrt(red[0]);
+}
+
+// Part 2 (one workgroup): mc = max ||c||², c2 = 2·tau·(mx + mc), thr_j = (half_j - tau·(mx + mc) /
+// (2 half_j))·(1 - 1e-6) (or -inf / +inf), dmax = {largest drift, second largest, its index};
+// resets the candidate count and the force flag for the next step.
+__global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double* __restrict__ cn,
+                                                                   const double* __restrict__ half,
+                                                                   const float* __restrict__ drift, int k,
+                                                                   const float* __restrict__ mx, float tau,
+                                                                   int have_drift, float* __restrict__ thr,
+                                                                   float* __restrict__ dmax, float* __restrict__ mc,
+                                                                   float* __restrict__ c2, int* __restrict__ count,
+                                                                   int* __restrict__ force) {
+  __shared__ double smax[256];
+  __shared__ float d1[256], d2[256];
+  __shared__ int i1[256];
+  const int tid = threadIdx.x;
+  double m = 0.0;
+  float a = -1.f, b = -1.f;
+  int ia = 0;
+  for (int j = tid; j < k; j += 256) {
+    m = cn[j] > m ? cn[j] : m;
+    if (have_drift) {
+      const float v = drift[j];
+      if (v > a) { b = a; a = v; ia = j; }
+      else if (v > b) { b = v; }
+    }
+  }
+  smax[tid] = m;
+  d1[tid] = a;
+  d2[tid] = b;
+  i1[tid] = ia;
+  __syncthreads();
+  if (tid == 0) {
+    double mm = 0.0;
+    float ta = -1.f, tb = -1.f;
+    int ti = 0;
+    for (int t = 0; t < 256; ++t) {
+      mm = smax[t] > mm ? smax[t] : mm;
+      // merge (d1[t], d2[t]) into (ta, tb): lowest index wins ties of the largest drift
+      if (d1[t] > ta) { tb = ta > d2[t] ? ta : d2[t]; ta = d1[t]; ti = i1[t]; }
+      else { const float c = d1[t]; tb = c > tb ? c : tb; }
+    }
+    smax[0] = mm;
+    const float mcf = (float)mm;
+    *mc = mcf;
+    *c2 = (float)(2.0 * (double)tau * ((double)*mx + mm));
+    if (have_drift) {
+      dmax[0] = ta < 0.f ? 0.f : ta;
+      dmax[1] = tb < 0.f ? 0.f : tb;
+      dmax[2] = (float)ti;
+    }
+    *count = 0;
+    *force = 0;
+  }
+  __syncthreads();
+  const double sl = (double)tau * ((double)*mx + smax[0]);
+  for (int j = tid; j < k; j += 256) {
+    float t;
+    if (k == 1) t = __builtin_huge_valf();
+    else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
+    else t = -__builtin_huge_valf();
+    thr[j] = t;
   }
 }
 
@@ -157,11 +303,15 @@ CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, con
 }
 
 // Moves every row's bounds by the centre drifts; rows whose bounds no longer prove the label are
-// appended to cand, their number added to *count (zeroed by the caller). dmax = {largest drift,
+// appended to cand (at most cap entries are written), their number added to *count (zeroed by the
+// caller). dmax = {largest drift,
 // second largest, index of the largest}. lab / ub / lb 16-byte aligned, k <= 8192.
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
-                                    const float* thr, float c2, int k, long long n, int* cand, int* count,
-                                    void* stream) {
+                                    const float* thr, const float* c2, int k, long long n, int* cand, int* count,
+                                    const float* xn, int* cand_lab, float* cand_xn, const int* skip,
+                                    long long cap, void* stream) {
+  if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
+    return (int)hipErrorInvalidValue;
   if (k <= 0 || k > 8192 || n < 0 || n >= (1LL << 31) || ((uintptr_t)lab & 15) || ((uintptr_t)ub & 15) ||
       ((uintptr_t)lb & 15))
     return (int)hipErrorInvalidValue;
@@ -169,6 +319,27 @@ CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const 
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
   hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads), (size_t)2 * k * sizeof(float),
-                     (hipStream_t)stream, lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count);
+                     (hipStream_t)stream, lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab,
+                     cand_xn, skip, cap);
+  return cml_status();
+}
+
+CML_API int cml_kmeans_prune_gate(const int* count, long long cap, const int* force, int* mode, void* stream) {
+  hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, cap, force, mode);
+  return cml_status();
+}
+
+// cb / cb_old: bf16 centres [>= k rows, ldc]; cb_old may be null (no drift: the bounds start over).
+// mx: device scalar max ||x||² (all ranks). Outputs: cn (f64 [k]), half (f64 [k] scratch), drift/thr
+// (f32 [k]), dmax (f32 [3]), mc / c2 (f32 scalars); count and force are reset to 0.
+CML_API int cml_kmeans_centre_stats(const void* cb, const void* cb_old, long long ldc, int k, int d, const float* mx,
+                                    float tau, double* cn, double* half, float* drift, float* thr, float* dmax,
+                                    float* mc, float* c2, int* count, int* force, void* stream) {
+  if (k <= 0 || d <= 0 || d > 8192) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  hipLaunchKernelGGL(kmeans_centre_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(double), st,
+                     (const u16*)cb, (const u16*)cb_old, ldc, k, d, cn, drift, half);
+  hipLaunchKernelGGL(kmeans_centre_stats2_kernel, dim3(1), dim3(256), 0, st, cn, half, drift, k, mx, tau,
+                     cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force);
   return cml_status();
 }

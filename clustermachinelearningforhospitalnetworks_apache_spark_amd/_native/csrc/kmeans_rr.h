@@ -9,7 +9,7 @@
 //   * the k centres are split over the 4 COMPUTE waves (one per SIMD): wave w keeps centres
 //     [w·kc/4, (w+1)·kc/4) as MFMA A fragments in VGPRs for the whole launch (k = 256, D = 256:
 //     64 centres x 256 x bf16 = 128 VGPRs per lane), pre-scaled by -2;
-//   * X streams through a 4-slot LDS ring of 32-KiB tiles filled by LDS-DMA
+//   * X streams through an NS-slot LDS ring of 32-KiB tiles filled by LDS-DMA
 //     (global_load_lds_dwordx4) issued by 2 DMA waves that do nothing else, so the loads never stall
 //     a computing wave and ~96 KiB per CU stay in flight;
 //   * every compute wave reads each X tile from LDS (B operand of v_mfma_f32_16x16x32_bf16, one
@@ -17,6 +17,22 @@
 //     centres goes to an exchange buffer;
 //   * 2 FINALIZE waves take the minimum over the 4 compute waves one tile later and run the
 //     epilogue K9 runs inline (labels, cost, label-change lists, counting-sort ranks).
+//
+// Modes (template MODE):
+//   0  the plain assign above;
+//   1  + TOP-2: compute waves keep the two smallest keys per row, the finalize waves merge them and
+//        write the exact-pruning bounds of every row (models/kmeans.py pruned step):
+//        ub = sqrt(best + tau·(|x|²+max|c|²)) rounded up, lb = sqrt(second - tau·(...)) rounded down.
+//        The second-best distance is what the Hamerly lower bound needs, so a full step leaves valid
+//        bounds behind with no extra pass (it replaced a [n, k] GEMM + row-min over every row);
+//   2  TOP-2 over a CANDIDATE list: position p of the launch is row idx[p]; the position count is
+//        read on the device (*n_dev), so the pruned step needs no host synchronisation. X rows are
+//        fetched through the index (the DMA waves read each tile's indices with scalar loads, which
+//        do not count against the vmcnt that paces the LDS-DMA ring); norms/labels/indices of the
+//        positions are compacted arrays (written by the bounds pass) that ride the trailer ring.
+//        Outputs (labels, bounds, change log) go to the real rows.
+// Any mode can be gated by a device flag (*gate == want, else every workgroup returns at once), so
+// a step can enqueue both the full and the candidate launch and let the device pick one.
 //
 // Tile rows are stored in LDS row-major with the 16-byte chunks of row R permuted (chunk c at
 // position c ^ (R & 15)): one DMA instruction then reads 1 KiB of whole rows from HBM (2 rows of
@@ -41,30 +57,52 @@ namespace rr {
 
 constexpr int kThreads = 512;   // waves 0-3 compute, 4-5 LDS-DMA, 6-7 finalize
 constexpr int kCompute = 4;
-constexpr int kRedStride = 17;  // dwords per row of the key exchange: 16 keys + 1 pad (conflict-free writes)
-constexpr int kNS = 4;          // X ring slots
 
-template <int DP, bool F8 = false>
+// Extra inputs/outputs of modes 1 and 2 and of the device gate.
+struct Ext {
+  const int* idx;     // MODE 2: real row of every position (compacted, >= roundup(n, TR) readable entries)
+  const int* n_dev;   // MODE 2: number of positions
+  const int* lab_in;  // MODE 2: labels of the positions (compacted)
+  float* ub;          // MODE >= 1: upper bound of |x - c_label| per row
+  float* lb;          // MODE >= 1: lower bound of the distance to every other centre per row
+  const float* mc;    // MODE >= 1: max ||c||² (device scalar)
+  float tau;          // MODE >= 1: error allowance relative to ||x||² + max||c||²
+  const int* gate;    // launch runs only when gate == nullptr || *gate == want
+  int want;
+};
+
+template <int DP, bool F8 = false, int MODE = 0>
 struct Geo {
   static constexpr int KS = DP / 32;            // MFMA k-steps per row
   static constexpr int ROWB = F8 ? DP : DP * 2; // bytes per row (bf16, or OCP e4m3fn bytes)
   static constexpr int TR = 32768 / ROWB;       // rows per tile (32 KiB of X)
   static constexpr int NSUB = TR / 16;          // 16-row MFMA sub-tiles per tile
   static constexpr int SLOT = TR * ROWB;        // 32 KiB
-  static constexpr int NTR = kNS + 1;           // trailer ring entries
   static constexpr int PIECES = SLOT / 1024;    // 1-KiB DMA pieces per tile (32)
+  static constexpr int RPP = 1024 / ROWB;       // rows per piece
   static constexpr int LPR = ROWB / 16;         // lanes (16-B chunks) per row in a piece
   static constexpr int TRAIL_Q = TR >= 64 ? TR / 64 : 1;  // dword DMA instructions per trailer array
-  static constexpr int CNT = PIECES / 2 + TRAIL_Q;        // DMA instructions per DMA wave per tile
-  static constexpr int TRB = TR * 8;            // trailer entry bytes (norms f32 + labels i32)
-  static constexpr int RED = TR * kRedStride * 4;
+  static constexpr int NARR = MODE == 2 ? 3 : 2;          // trailer arrays: norms, labels (, rows)
+  // DMA instructions per tile: wave 0 carries the norms, wave 1 the labels (and rows)
+  static constexpr int CNT0 = PIECES / 2 + TRAIL_Q;
+  static constexpr int CNT1 = PIECES / 2 + (NARR - 1) * TRAIL_Q;
+  static constexpr int TRB = TR * 4 * NARR;     // trailer entry bytes
+  static constexpr int NK = MODE >= 1 ? 2 : 1;  // keys per (row, wave, lane group)
+  static constexpr int STRIDE = 16 * NK + 1;    // dwords per row of the key exchange (+1: conflict-free writes)
+  static constexpr int RED = TR * STRIDE * 4;
+  static constexpr long long fixed_bytes(int ns, int kp) {
+    return (long long)(ns + 1) * TRB + 2LL * RED + 4LL * ((kp + 3) & ~3) + 64;
+  }
+  // ring depth: 4 slots where LDS allows, 3 for the 128-row tiles of the top-2 modes
+  static constexpr int NS = (4LL * SLOT + fixed_bytes(4, 1024)) <= 160 * 1024 ? 4 : 3;
+  static constexpr int NTR = NS + 1;            // trailer ring entries
 };
 
 // LDS layout (bytes): [X ring NS*SLOT | trailers NTR*TRB | keys 2*RED | hist kp ints | misc 64 B]
-template <int DP, bool F8 = false>
+template <int DP, bool F8 = false, int MODE = 0>
 __host__ __device__ constexpr long long lds_bytes(int kp) {
-  using G = Geo<DP, F8>;
-  return (long long)kNS * G::SLOT + (long long)G::NTR * G::TRB + 2LL * G::RED + 4LL * ((kp + 3) & ~3) + 64;
+  using G = Geo<DP, F8, MODE>;
+  return (long long)G::NS * G::SLOT + G::fixed_bytes(G::NS, kp);
 }
 
 // s_waitcnt with only vmcnt = N (expcnt, lgkmcnt at their maxima: not waited for). gfx9 encoding.
@@ -91,34 +129,82 @@ __device__ __forceinline__ void glds4(const void* src, unsigned char* lds) {
   __builtin_amdgcn_global_load_lds(src, (__attribute__((address_space(3))) void*)lds, 4, 0, 0);
 }
 
-// ldx in BYTES; rows are 16-B aligned.
-template <int DP, bool F8>
+typedef const __attribute__((address_space(4))) int* cidx_t;  // constant address space: scalar loads
+
+// ldx in BYTES; rows are 16-B aligned. Positions past n load row n-1 (discarded).
+template <int DP, bool F8, int MODE>
 __device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, long long ldx, long long n,
                                            const float* __restrict__ xnorm, const int* __restrict__ labels,
-                                           long long tile, int slot, int tr, int dw, int lane,
-                                           unsigned char* smem) {
-  using G = Geo<DP, F8>;
+                                           const int* __restrict__ idx, long long tile, int slot, int tr, int dw,
+                                           int lane, unsigned char* smem) {
+  using G = Geo<DP, F8, MODE>;
   const long long row0 = tile * G::TR;
   unsigned char* sdst = smem + slot * G::SLOT;
+  if constexpr (MODE == 2) {
+    // this wave's TR/2 positions start at row0 + dw*TR/2: their rows come in as uniform scalar loads
+    // (the index buffer is padded to whole tiles, entries past n are stale but valid rows), in
+    // batches of 16 with the next batch's loads in flight while the current one's pieces issue
+    // (a whole tile's 64 indices at once ran out of SGPRs and fell back to vector loads, whose
+    // vmcnt wait would drain the ring)
+    constexpr int NR = G::TR / 2;
+    constexpr int BAT = NR < 16 ? NR : 16;
+    constexpr int NBAT = NR / BAT;
+    constexpr int PPB = BAT / G::RPP;  // pieces per batch
+    const cidx_t ci = (cidx_t)(idx + row0 + dw * NR);
+    const int sub = lane / G::LPR;  // row within the piece
+    int cur[BAT];
 #pragma unroll
-  for (int q = 0; q < G::PIECES / 2; ++q) {
-    const int p = dw * (G::PIECES / 2) + q;
-    const int R = p * (1024 / G::ROWB) + lane / G::LPR;  // row within the tile
-    const int pos = lane % G::LPR;                       // LDS chunk position in the row
-    const int gch = pos ^ (R & 15);                      // global chunk stored there
-    long long grow = row0 + R;
-    grow = grow < n ? grow : n - 1;                      // rows past n: any valid row (discarded)
-    glds16(X + grow * ldx + 16 * gch, sdst + p * 1024);
+    for (int i = 0; i < BAT; ++i) cur[i] = ci[i];
+#pragma unroll
+    for (int b = 0; b < NBAT; ++b) {
+      int nxt[BAT];
+      if (b + 1 < NBAT) {
+#pragma unroll
+        for (int i = 0; i < BAT; ++i) nxt[i] = ci[(b + 1) * BAT + i];
+      }
+#pragma unroll
+      for (int qq = 0; qq < PPB; ++qq) {
+        const int q = b * PPB + qq;
+        const int p = dw * (G::PIECES / 2) + q;
+        const int R = p * G::RPP + sub;
+        int grow = cur[qq * G::RPP];
+#pragma unroll
+        for (int s = 1; s < G::RPP; ++s) grow = sub == s ? cur[qq * G::RPP + s] : grow;
+        const int pos = lane % G::LPR;
+        const int gch = pos ^ (R & 15);
+        glds16(X + (long long)grow * ldx + 16 * gch, sdst + p * 1024);
+      }
+      __builtin_amdgcn_sched_barrier(0);
+      if (b + 1 < NBAT) {
+#pragma unroll
+        for (int i = 0; i < BAT; ++i) cur[i] = nxt[i];
+      }
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < G::PIECES / 2; ++q) {
+      const int p = dw * (G::PIECES / 2) + q;
+      const int R = p * G::RPP + lane / G::LPR;  // row within the tile
+      const int pos = lane % G::LPR;             // LDS chunk position in the row
+      const int gch = pos ^ (R & 15);            // global chunk stored there
+      long long grow = row0 + R;
+      grow = grow < n ? grow : n - 1;            // rows past n: any valid row (discarded)
+      glds16(X + grow * ldx + 16 * gch, sdst + p * 1024);
+    }
   }
-  unsigned char* tdst = smem + kNS * G::SLOT + tr * G::TRB + (dw ? G::TR * 4 : 0);
+  unsigned char* tbase = smem + G::NS * G::SLOT + tr * G::TRB;
 #pragma unroll
   for (int q = 0; q < G::TRAIL_Q; ++q) {
     const int R = q * 64 + lane;
     long long grow = row0 + R;
     grow = grow < n ? grow : n - 1;
     if (R < G::TR) {
-      if (dw == 0) glds4(xnorm + grow, tdst + q * 256);
-      else glds4(labels + grow, tdst + q * 256);
+      if (dw == 0) {
+        glds4(xnorm + grow, tbase + q * 256);
+      } else {
+        glds4(labels + grow, tbase + G::TR * 4 + q * 256);
+        if constexpr (MODE == 2) glds4(idx + grow, tbase + G::TR * 8 + q * 256);
+      }
     }
   }
 }
@@ -127,27 +213,34 @@ __device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, 
 // HBM and LDS traffic) and every compute wave widens its fragments with v_cvt_scalef32_pk_bf16_fp8
 // (exact: e4m3 values are a subset of bf16); one 16-B read then covers TWO k-steps, step 2v+h of lane
 // (r, g) holding k = 64v + 16g + 8h + j, and the centre fragments follow the same k order.
-template <int DP, int CT, bool F8>
+template <int DP, int CT, bool F8, int MODE>
 __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     const unsigned char* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc, int kc,
     int kp, const float* __restrict__ cnorm, const float* __restrict__ xnorm, int* __restrict__ labels,
     float* __restrict__ best_out, double* __restrict__ cost_part, int* __restrict__ hist_out,
-    int* __restrict__ rank_out, DeltaOut dout, int dbg) {
+    int* __restrict__ rank_out, DeltaOut dout, Ext ext, int dbg) {
   // dbg (ablation only, 0 in production): bit 0 DMA waves issue nothing, bit 1 compute waves skip
   // their MFMAs/keys, bit 2 finalize waves skip the epilogue
-  using G = Geo<DP, F8>;
+  using G = Geo<DP, F8, MODE>;
   constexpr int KS = G::KS;
+  constexpr int NS = G::NS;
   constexpr int CPW = CT * 16;  // centres per compute wave
   constexpr int TAGB = 2 + (CT > 1) + (CT > 2) + (CT > 4);
   constexpr int TAGM = (1 << TAGB) - 1;
+  constexpr bool TOP2 = MODE >= 1;
+  if (ext.gate != nullptr && *ext.gate != ext.want) return;  // uniform: before any barrier
+  if constexpr (MODE == 2) n = *ext.n_dev;
+  const int* lab_src = MODE == 2 ? ext.lab_in : labels;  // trailer source of the previous labels
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
-  unsigned char* trail = smem + kNS * G::SLOT;
+  unsigned char* trail = smem + NS * G::SLOT;
   int* red = reinterpret_cast<int*>(trail + G::NTR * G::TRB);
-  int* hist = red + 2 * G::TR * kRedStride;
+  int* hist = red + 2 * G::TR * G::STRIDE;
   int* misc = hist + ((kp + 3) & ~3);  // [0] change counter, [2..5] two f64 cost partials
   double* cost_sh = reinterpret_cast<double*>(misc + 2);
 
-  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  // the role index is wave-uniform: readfirstlane lets the compiler branch on it with scalar
+  // instructions and keep addresses derived from it (the MODE 2 index loads) in SGPRs
+  const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
   const long long ntiles = (n + G::TR - 1) / G::TR;
   const long long nt = ntiles > blockIdx.x ? (ntiles - 1 - blockIdx.x) / gridDim.x + 1 : 0;
   const bool ranking = rank_out != nullptr;
@@ -195,9 +288,9 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         barrier();
         continue;
       }
-      const unsigned char* xs = smem + (int)(j % kNS) * G::SLOT;
+      const unsigned char* xs = smem + (int)(j % NS) * G::SLOT;
       const float* tn = reinterpret_cast<const float*>(trail + (int)(j % G::NTR) * G::TRB);
-      int* kred = red + (int)(j & 1) * G::TR * kRedStride;
+      int* kred = red + (int)(j & 1) * G::TR * G::STRIDE;
       // The tile is one flat, fully unrolled sequence of NSUB*KS steps (sub-tile t, k-step s). The B
       // fragment of step u+PF is read while step u's MFMAs issue (a scheduling barrier per step pins
       // it: left alone, the scheduler issued each read one step ahead, 4 MFMAs = 64 cycles, under the
@@ -218,13 +311,13 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       for (int u = 0; u < PF && u < NU; ++u) xr[u] = *reinterpret_cast<const uint4*>(xaddr(u));
       f32x4 acc[2][CT];
       int key[2] = {0x7fffffff, 0x7fffffff};
+      int key2[2] = {0x7fffffff, 0x7fffffff};  // TOP2: second smallest key
 #pragma unroll
       for (int u = 0; u < NU; ++u) {
         const int t = u / UPS, v = u % UPS, cur = t & 1, prv = cur ^ 1;
         if (u + PF < NU) xr[(u + PF) % (PF + 1)] = *reinterpret_cast<const uint4*>(xaddr(u + PF));
         bf16x8 xb[SPU];
         if constexpr (F8) {
-          typedef __bf16 bf16x2 __attribute__((ext_vector_type(2)));
           const uint4 w = xr[u % (PF + 1)];
           const unsigned ws[4] = {w.x, w.y, w.z, w.w};
           unsigned o[8];
@@ -241,7 +334,10 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
 #pragma unroll
         for (int h = 0; h < SPU; ++h) {
           const int s = v * SPU + h;
-          if (s == 0) key[cur] = 0x7fffffff;
+          if (s == 0) {
+            key[cur] = 0x7fffffff;
+            if constexpr (TOP2) key2[cur] = 0x7fffffff;
+          }
 #pragma unroll
           for (int ct = 0; ct < CT; ++ct)
             acc[cur][ct] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
@@ -251,9 +347,16 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
             for (int e = (s * CT * 4) / KS; e < ((s + 1) * CT * 4) / KS; ++e) {
               const int ct = e >> 2, i = e & 3;
               const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
+              if constexpr (TOP2) {
+                const int hi = kv > key[prv] ? kv : key[prv];
+                key2[prv] = hi < key2[prv] ? hi : key2[prv];
+              }
               key[prv] = kv < key[prv] ? kv : key[prv];
             }
-            if (s == KS - 1) kred[(16 * (t - 1) + r) * kRedStride + wave * 4 + g] = key[prv];
+            if (s == KS - 1) {
+              kred[(16 * (t - 1) + r) * G::STRIDE + wave * 4 + g] = key[prv];
+              if constexpr (TOP2) kred[(16 * (t - 1) + r) * G::STRIDE + 16 + wave * 4 + g] = key2[prv];
+            }
           }
         }
         __builtin_amdgcn_sched_barrier(0);  // keep every unit's read PF units ahead of its use
@@ -264,9 +367,14 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         for (int e = 0; e < CT * 4; ++e) {
           const int ct = e >> 2, i = e & 3;
           const int kv = (__float_as_int(acc[cur][ct][i]) & ~TAGM) | (ct << 2 | i);
+          if constexpr (TOP2) {
+            const int hi = kv > key[cur] ? kv : key[cur];
+            key2[cur] = hi < key2[cur] ? hi : key2[cur];
+          }
           key[cur] = kv < key[cur] ? kv : key[cur];
         }
-        kred[(16 * t + r) * kRedStride + wave * 4 + g] = key[cur];
+        kred[(16 * t + r) * G::STRIDE + wave * 4 + g] = key[cur];
+        if constexpr (TOP2) kred[(16 * t + r) * G::STRIDE + 16 + wave * 4 + g] = key2[cur];
       }
       wait_lgkm0();
       barrier();  // B(j)
@@ -274,17 +382,23 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   } else if (wave < kCompute + 2) {
     // ------------------------------------------------------------------ LDS-DMA waves
     const int dw = wave - kCompute;
-    for (long long j = 0; j < kNS - 1 && j < nt && !(dbg & 1); ++j)
-      issue_tile<DP, F8>(X, ldx, n, xnorm, labels, tile_of(j), (int)j, (int)j, dw, lane, smem);
-    if (nt >= kNS - 1) wait_vm<(kNS - 2) * G::CNT>();
-    else wait_vm<0>();
+    for (long long j = 0; j < NS - 1 && j < nt && !(dbg & 1); ++j)
+      issue_tile<DP, F8, MODE>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(j), (int)j, (int)j, dw, lane, smem);
+    if (nt >= NS - 1) {
+      if (dw == 0) wait_vm<(NS - 2) * G::CNT0>();
+      else wait_vm<(NS - 2) * G::CNT1>();
+    } else {
+      wait_vm<0>();
+    }
     barrier();  // B(-1)
     for (long long j = 0; j < nt; ++j) {
-      const long long jn = j + kNS - 1;
+      const long long jn = j + NS - 1;
       if (jn < nt && !(dbg & 1)) {
-        issue_tile<DP, F8>(X, ldx, n, xnorm, labels, tile_of(jn), (int)(jn % kNS), (int)(jn % G::NTR), dw, lane,
-                       smem);
-        wait_vm<(kNS - 2) * G::CNT>();  // tile j+1 has landed; j+2 .. j+NS-1 stay in flight
+        issue_tile<DP, F8, MODE>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(jn), (int)(jn % NS),
+                                 (int)(jn % G::NTR), dw, lane, smem);
+        // tile j+1 has landed; j+2 .. j+NS-1 stay in flight
+        if (dw == 0) wait_vm<(NS - 2) * G::CNT0>();
+        else wait_vm<(NS - 2) * G::CNT1>();
       } else {
         wait_vm<0>();
       }
@@ -299,37 +413,61 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       if (lane == 0) misc[0] = 0;
     }
     double cost = 0.0;
+    float mcv = 0.f;
+    if constexpr (TOP2) mcv = *ext.mc;
     // LPR_F lanes per row, each taking 16 / LPR_F of the 16 (wave, lane-group) keys; keys are loaded
     // in one batch and reduced branch-free on a 64-bit (value, centre index) composite
     constexpr int LPR_F = 64 / RPF;
     constexpr int QPL = 16 / LPR_F;
     const int rl = lane % RPF, part = lane / RPF;
     auto finalize = [&](long long j) {
-      const int* kr = red + (int)(j & 1) * G::TR * kRedStride;
+      const int* kr = red + (int)(j & 1) * G::TR * G::STRIDE;
       const unsigned char* te = trail + (int)(j % G::NTR) * G::TRB;
       const int R = fw * RPF + rl;
-      const long long row = tile_of(j) * G::TR + R;
-      int kv[QPL];
+      const long long pos = tile_of(j) * G::TR + R;
+      int kv[QPL], kv2[QPL];
 #pragma unroll
-      for (int q = 0; q < QPL; ++q) kv[q] = kr[R * kRedStride + part * QPL + q];
+      for (int q = 0; q < QPL; ++q) {
+        kv[q] = kr[R * G::STRIDE + part * QPL + q];
+        if constexpr (TOP2) kv2[q] = kr[R * G::STRIDE + 16 + part * QPL + q];
+      }
       const int old = reinterpret_cast<const int*>(te + G::TR * 4)[R];
+      long long row = pos;
+      if constexpr (MODE == 2) row = reinterpret_cast<const int*>(te + G::TR * 8)[R];
       unsigned long long best = ~0ull;
+      unsigned sec = ~0u;  // TOP2: second smallest value, order-preserving unsigned form
 #pragma unroll
       for (int q = 0; q < QPL; ++q) {  // qq = w*4 + g: centres w*CPW + ct*16 + 4g + i
         const int qq = part * QPL + q;
         const int tag = kv[q] & TAGM;
         const unsigned idx = (unsigned)((qq >> 2) * CPW + (qq & 3) * 4 + (tag >> 2) * 16 + (tag & 3));
-        const unsigned long long c = ((unsigned long long)((unsigned)(kv[q] & ~TAGM) ^ 0x80000000u) << 32) | idx;
+        const unsigned u1 = (unsigned)(kv[q] & ~TAGM) ^ 0x80000000u;
+        const unsigned long long c = ((unsigned long long)u1 << 32) | idx;
+        if constexpr (TOP2) {
+          // second of the union = min(larger of the two firsts, smaller of the two seconds)
+          const unsigned u2 = (unsigned)(kv2[q] & ~TAGM) ^ 0x80000000u;
+          const unsigned bv = (unsigned)(best >> 32);
+          const unsigned mx = u1 > bv ? u1 : bv;
+          const unsigned s2 = u2 < sec ? u2 : sec;
+          sec = mx < s2 ? mx : s2;
+        }
         best = c < best ? c : best;
       }
 #pragma unroll
       for (int o = RPF; o < 64; o <<= 1) {
         const unsigned long long ob = __shfl_xor(best, o, 64);
+        if constexpr (TOP2) {
+          const unsigned os = __shfl_xor(sec, o, 64);
+          const unsigned bv = (unsigned)(best >> 32), obv = (unsigned)(ob >> 32);
+          const unsigned mx = obv > bv ? obv : bv;
+          const unsigned s2 = os < sec ? os : sec;
+          sec = mx < s2 ? mx : s2;
+        }
         best = ob < best ? ob : best;
       }
       const int bi = (int)(best & 0xffffffffu);
       const float dist = fmaxf(__int_as_float((int)((unsigned)(best >> 32) ^ 0x80000000u)), 0.f);
-      const bool mine = part == 0 && row < n;
+      const bool mine = part == 0 && pos < n;
       const bool ch = mine && old != bi;
       if (dout.rows != nullptr) {
         const unsigned long long bal = __ballot(ch);
@@ -351,6 +489,13 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         cost += (double)dist;
         if (best_out != nullptr) best_out[row] = dist;
         if (ranking) rank_out[row] = atomicAdd(hist + bi, 1);
+        if constexpr (TOP2) {
+          const float xn = reinterpret_cast<const float*>(te)[R];
+          const float slack = ext.tau * (xn + mcv);
+          const float sd = __int_as_float((int)(sec ^ 0x80000000u));
+          ext.ub[row] = sqrtf(dist + slack) * (1.0f + 1e-6f);
+          ext.lb[row] = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
+        }
       }
     };
     wait_lgkm0();
@@ -390,18 +535,28 @@ inline int plan_ct(int Dp, int kc, bool f8 = false) {
   return c;
 }
 
-inline long long lds_for(int Dp, int kp, bool f8 = false) {
+template <int MODE>
+inline long long lds_for_mode(int Dp, int kp, bool f8) {
   if (f8) {
     switch (Dp) {
-      case 256: return lds_bytes<256, true>(kp);
-      case 512: return lds_bytes<512, true>(kp);
+      case 256: return lds_bytes<256, true, MODE>(kp);
+      case 512: return lds_bytes<512, true, MODE>(kp);
       default: return 0;
     }
   }
   switch (Dp) {
-    case 128: return lds_bytes<128>(kp);
-    case 256: return lds_bytes<256>(kp);
-    case 512: return lds_bytes<512>(kp);
+    case 128: return lds_bytes<128, false, MODE>(kp);
+    case 256: return lds_bytes<256, false, MODE>(kp);
+    case 512: return lds_bytes<512, false, MODE>(kp);
+    default: return 0;
+  }
+}
+
+inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
+  switch (mode) {
+    case 0: return lds_for_mode<0>(Dp, kp, f8);
+    case 1: return lds_for_mode<1>(Dp, kp, f8);
+    case 2: return lds_for_mode<2>(Dp, kp, f8);
     default: return 0;
   }
 }
@@ -409,28 +564,30 @@ inline long long lds_for(int Dp, int kp, bool f8 = false) {
 inline int tile_rows(int Dp, bool f8 = false) { return Dp > 0 ? 32768 / ((f8 ? 1 : 2) * Dp) : 0; }
 
 // X: bf16 rows (ldx elements) or, with f8, e4m3fn rows (ldx bytes).
-template <int DP, int CT, bool F8>
+template <int DP, int CT, bool F8, int MODE>
 int launch(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp, const float* cnorm,
            const float* xnorm, int* labels, float* best, double* cost_part, int* hist, int* rank, DeltaOut dout,
-           int grid, int dbg, hipStream_t st) {
-  const size_t lds = (size_t)lds_bytes<DP, F8>(kp);
+           Ext ext, int grid, int dbg, hipStream_t st) {
+  const size_t lds = (size_t)lds_bytes<DP, F8, MODE>(kp);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8>;
+  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8, MODE>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const long long ldb = F8 ? ldx : 2 * ldx;
-  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8>), dim3(grid), dim3(kThreads), lds, st,
+  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8, MODE>), dim3(grid), dim3(kThreads), lds, st,
                      (const unsigned char*)X, n, ldb, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist,
-                     rank, dout, dbg);
+                     rank, dout, ext, dbg);
   return cml_status();
 }
 
-inline int dispatch(int Dp, int ct, bool f8, const void* X, long long n, long long ldx, const u16* C, long long ldc,
-                    int kc, int kp, const float* cnorm, const float* xnorm, int* labels, float* best,
-                    double* cost_part, int* hist, int* rank, DeltaOut dout, int grid, int dbg, hipStream_t st) {
-#define CML_RR(D, T, F)                                                                                             \
-  if (Dp == D && ct == T && f8 == F)                                                                                \
-  return launch<D, T, F>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, grid, \
-                         dbg, st)
+template <int MODE>
+inline int dispatch_mode(int Dp, int ct, bool f8, const void* X, long long n, long long ldx, const u16* C,
+                         long long ldc, int kc, int kp, const float* cnorm, const float* xnorm, int* labels,
+                         float* best, double* cost_part, int* hist, int* rank, DeltaOut dout, Ext ext, int grid,
+                         int dbg, hipStream_t st) {
+#define CML_RR(D, T, F)                                                                                            \
+  if (Dp == D && ct == T && f8 == F)                                                                               \
+  return launch<D, T, F, MODE>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, \
+                               ext, grid, dbg, st)
   CML_RR(128, 1, false); CML_RR(128, 2, false); CML_RR(128, 4, false);
   CML_RR(256, 1, false); CML_RR(256, 2, false); CML_RR(256, 4, false);
   CML_RR(512, 1, false); CML_RR(512, 2, false);
@@ -438,6 +595,21 @@ inline int dispatch(int Dp, int ct, bool f8, const void* X, long long n, long lo
   CML_RR(512, 1, true); CML_RR(512, 2, true);
 #undef CML_RR
   return (int)hipErrorInvalidValue;
+}
+
+inline int dispatch(int mode, int Dp, int ct, bool f8, const void* X, long long n, long long ldx, const u16* C,
+                    long long ldc, int kc, int kp, const float* cnorm, const float* xnorm, int* labels, float* best,
+                    double* cost_part, int* hist, int* rank, DeltaOut dout, Ext ext, int grid, int dbg,
+                    hipStream_t st) {
+  switch (mode) {
+    case 0: return dispatch_mode<0>(Dp, ct, f8, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+                                    hist, rank, dout, ext, grid, dbg, st);
+    case 1: return dispatch_mode<1>(Dp, ct, f8, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+                                    hist, rank, dout, ext, grid, dbg, st);
+    case 2: return dispatch_mode<2>(Dp, ct, f8, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
+                                    hist, rank, dout, ext, grid, dbg, st);
+    default: return (int)hipErrorInvalidValue;
+  }
 }
 
 }  // namespace rr

@@ -119,11 +119,14 @@ class LloydEngine:
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
                  incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None):
         self.comm = comm or local_comm()
-        if prune is None:
-            prune = os.environ.get("CML_KMEANS_PRUNE") == "1"
+        if prune is None:  # default on GPU rows: exact pruned steps (CML_KMEANS_PRUNE=0 turns them off)
+            env = os.environ.get("CML_KMEANS_PRUNE")
+            prune = (env != "0") if env is not None else x.is_cuda
         self.prune = bool(prune)
-        if self.prune:  # one chunk, no graph (the candidate count is read back every step), own sums
-            row_chunks, use_graph, incremental = 1, False, False
+        self.track_prune = False  # record (full?, re-assigned rows) of every pruned step (host reads)
+        self._pdev = False  # the device pruned step (_step_prune_dev) is in use, decided in _alloc_gpu
+        if self.prune:  # one row chunk; the device form keeps incremental sums, the torch form its own
+            row_chunks = 1
         # spherical = Spark's distanceMeasure="cosine": rows are scaled to unit length once, centres
         # are renormalised after every update (CosineDistanceMeasure.centroid), and on unit vectors
         # ||x - c||² = 2·(1 - cos), so the euclidean K9/K10 path computes the cosine assignment;
@@ -158,6 +161,7 @@ class LloydEngine:
         self.row_chunks = max(1, min(int(row_chunks), max(1, self.n)))
         self.centers = torch.zeros((self.k, self.d), dtype=torch.float64, device=self.device)
         self.iterations = 0
+        self._cost_fn = None
         self.last_cost = None
         self._shift2 = None
         self.delta = None  # incremental-sums state (GPU sort regime), see _alloc_gpu
@@ -180,8 +184,9 @@ class LloydEngine:
         self.cplan = K.plan_accum(max(maxn, 1), dp, k, dev.index or 0, force=self._accum_mode, fp8=fp8)
         self.labels = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         # distance scratch only when the centres need several LDS chunks (running min through HBM)
+        pdev_ok = self.aplan.rr_ct > 0 and self.aplan.kc == self.aplan.kp and self.cplan.mode == "sort"
         self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
-                     if (self.aplan.kc < self.aplan.kp or self.prune) else None)
+                     if (self.aplan.kc < self.aplan.kp or (self.prune and not pdev_ok)) else None)
         self.xnorm = cached_row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
@@ -205,6 +210,12 @@ class LloydEngine:
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         self.shift2 = torch.zeros(k, dtype=torch.float64, device=dev)
         self._prev_centers = torch.zeros((k, d), dtype=torch.float64, device=dev) if self.spherical else None
+        # the device pruned step needs the K9r assign (every centre in one launch) and the sort-regime sums
+        if self.prune and pdev_ok:
+            self._pdev = True
+            self._pdev_alloc()
+        elif self.prune:
+            self.use_graph, self.delta = False, None  # torch form: host-synchronised, its own sums
 
     @property
     def global_n(self) -> int:
@@ -227,14 +238,27 @@ class LloydEngine:
             self.centers = c.contiguous().clone()
         if self.gpu:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
-        if self._pst is not None:  # bounds were relative to the old centres
+        if self._pdev:  # bounds and incremental sums were relative to the old centres: a full step next
+            st = self._pst
+            K.centre_stats(self.cb, None, self.k, self.d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax,
+                           st.mc, st.c2, st.count, st.force)
+            st.force.fill_(1)
+            self.delta.invalidate()
+        elif self._pst is not None:  # bounds were relative to the old centres
             self._pst.valid = False
             self._prune_centre_stats()
 
     # ------------------------------------------------------------------ iteration
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
-        if self.prune:
+        if self._pdev:
+            if self.use_graph:
+                self._step_graph()
+            else:
+                self._step_prune_dev()
+            if self.track_prune:
+                self._pst.history.append(self._pdev_last())
+        elif self.prune:
             self._step_prune()
         elif self.gpu and self.use_graph:
             self._step_graph()
@@ -251,14 +275,17 @@ class LloydEngine:
         if self._graph is None:
             if not getattr(self, "_graph_warm", False):
                 self._graph_warm = True
-                self._step_gpu()
+                (self._step_prune_dev if self._pdev else self._step_gpu)()
                 return
             torch.cuda.synchronize(self.device)
             g = torch.cuda.CUDAGraph()
+            body = self._step_prune_dev if self._pdev else self._step_gpu
             with torch.cuda.graph(g):
-                self._step_gpu()
+                body()
             self._graph = g
         self._graph.replay()
+        if self._pdev:
+            self._cost_fn = self._pdev_cost
 
     def _best(self, r0: int, r1: int):
         return None if self.best is None else self.best[r0:r1]
@@ -334,6 +361,100 @@ class LloydEngine:
         self.centers = new
         self.last_cost = msg[-1]
 
+    # ------------------------------------------------------------------ device pruned step
+    @staticmethod
+    def prune_tau(dp: int) -> float:
+        """Error allowance of the assign's squared distances, relative to |x|² + max|c|²: the f32
+        accumulation of dp exact bf16 products (dp·2^-25 of Σ|x_j c_j| <= (|x|² + |c|²)/2 each way)
+        plus the key truncation of the K9r argmin (2^-18 of a distance <= 2(|x|² + |c|²)), doubled."""
+        return max(3e-5, 2.0 * (dp * 2.0 ** -25 + 2.0 ** -17))
+
+    def _pdev_alloc(self) -> None:
+        """State of the device pruned step (_step_prune_dev): per-row bounds, candidate lists sized for
+        _PRUNE_CAP of the rows, centre statistics, and incremental sums whose change lists can hold
+        every candidate of a workgroup (a candidate pass never overflows into a full re-accumulation)."""
+        n, k, d, dev, ap = self.n, self.k, self.d, self.device, self.aplan
+        tr = ap.round_rows
+        st = types.SimpleNamespace(history=[])
+        st.cap_m = max(tr, int(math.ceil(self._PRUNE_CAP * n)))
+        st.tau = self.prune_tau(self.dp)
+        per_wg = -(-(-(-st.cap_m // tr)) // ap.grid) * tr
+        pad = round_up(st.cap_m, tr) + tr
+        st.cand = torch.zeros(pad, dtype=torch.int32, device=dev)
+        st.cand_lab = torch.zeros(pad, dtype=torch.int32, device=dev)
+        st.cand_xn = torch.zeros(pad, dtype=torch.float32, device=dev)
+        st.count = torch.zeros(1, dtype=torch.int32, device=dev)
+        st.pmode = torch.zeros(2, dtype=torch.int32, device=dev)  # [full pass?, re-assigned rows]
+        st.force = torch.ones(1, dtype=torch.int32, device=dev)
+        st.ub = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        st.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        st.drift = torch.zeros(k, dtype=torch.float32, device=dev)
+        st.thr = torch.zeros(k, dtype=torch.float32, device=dev)
+        st.dmax = torch.zeros(3, dtype=torch.float32, device=dev)
+        st.cn = torch.zeros(k, dtype=torch.float64, device=dev)
+        st.half = torch.zeros(k, dtype=torch.float64, device=dev)
+        st.mc = torch.zeros(1, dtype=torch.float32, device=dev)
+        st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
+        mx = self.comm.max_scalar(float(self.xnorm[:n].max()) if n else 0.0)
+        st.mx = torch.full((1,), mx, dtype=torch.float32, device=dev)
+        st.cb_old = torch.zeros_like(self.cb)
+        self._pst = st
+        self.delta = K.DeltaState(max(n, 1), k, d, self.dp, 1, self.msg_len, dev, ap.grid, fp8=K.is_fp8(self.x),
+                                  cap=max(st.cap_m, 1024), pcap=max(per_wg, 64))
+
+    def _step_prune_dev(self) -> None:
+        """One exact Lloyd iteration with no host synchronisation (HIP-graph capturable):
+        K9p moves every row's bounds by the centre drifts and compacts the rows they no longer prove
+        (label, norm beside each); a one-thread gate picks the full pass (bounds invalid, or more than
+        _PRUNE_CAP of the rows are candidates) or the candidate pass; both K9r launches are enqueued
+        and the device runs one — mode 1 over every row, mode 2 over the candidate positions, each
+        writing new labels and top-2 bounds and logging label changes; the incremental sums move by
+        the changed rows (exact f64 sums, as the full path); all-reduce; K11; centre statistics for
+        the next step's bounds."""
+        st, dl = self._pst, self.delta
+        n, k, d, ap = self.n, self.k, self.d, self.aplan
+        x, lab, msg = self.x, self.labels, self.msgs[0]
+        K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
+                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.force, zero_count=False) \
+            if n else None
+        K.prune_gate(st.count, st.cap_m, st.force, st.pmode)
+        K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                        st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1)
+        K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
+                        st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
+                        gate=st.pmode, want=0)
+        dl.gate(0)
+        K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
+                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0])
+        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
+        self.comm.allreduce_async(msg).wait()
+        st.cb_old.copy_(self.cb)
+        self._update_gpu(self.msgs)
+        K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
+                       st.c2, st.count, st.force)
+        self._cost_fn = self._pdev_cost
+
+    def _pdev_cost(self) -> torch.Tensor:
+        """Cost of the last step's assignment (Spark's per-iteration cost): Σ_j (Q_j - 2 c_j·S_j +
+        n_j |c_j|²) over the centres it assigned against (cb_old), S/n its all-reduced sums, Q_j the
+        per-centre Σ|x|² of the current labels (one group-sum over the rows, all-reduced)."""
+        st, k, d, n = self._pst, self.k, self.d, self.n
+        kd = k * d
+        q = group_reduce(self.labels[:n], self.xnorm[:n].to(torch.float64), k, "sum") if n else torch.zeros(
+            k, dtype=torch.float64, device=self.device)
+        q = q.to(torch.float64).contiguous()
+        self.comm.allreduce_(q)
+        c = st.cb_old[:k, :d].to(torch.float64)
+        msg = self.msgs[0]
+        s_, cnt = msg[:kd].view(k, d), msg[kd:kd + k]
+        cost = q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()
+        return cost.clamp(min=0.0)
+
+    def _pdev_last(self) -> tuple:
+        """(full pass?, re-assigned rows) of the last device pruned step (synchronises)."""
+        pm = self._pst.pmode.cpu().tolist()
+        return (bool(pm[0]), int(self.n if pm[0] else pm[1]))
+
     # ------------------------------------------------------------------ pruned (exact) steps
     # Error allowance of a squared distance from the full assign, relative to |x|² + |c|²: f32
     # accumulation of exact bf16 products is within D·2^-24·Σ|x_j c_j| <= 0.77e-5·(|x|² + |c|²) at D = 256.
@@ -344,7 +465,7 @@ class LloydEngine:
         n, k, d, dev = self.n, self.k, self.d, self.device
         bdt = torch.float32 if self.gpu else torch.float64
         idt = torch.int32 if self.gpu else torch.int64
-        st = types.SimpleNamespace(valid=False, last=(True, 0))
+        st = types.SimpleNamespace(valid=False, last=(True, 0), history=[])
         st.ub = torch.full((max(n, 1),), float("inf"), dtype=bdt, device=dev)  # >= |x_i - c_label(i)|
         st.lb = torch.zeros(max(n, 1), dtype=bdt, device=dev)  # <= distance to the nearest other centre
         st.dmax = torch.zeros(3, dtype=bdt, device=dev)  # [largest drift, second largest, its index]
@@ -485,6 +606,7 @@ class LloydEngine:
         with trace("prune.full" if full else "prune.candidates"):
             delta = self._prune_local_full() if full else self._prune_local_cands(m)
         st.last = (full, m)
+        st.history.append((bool(full), int(m)))
         with trace("prune.allreduce_update"):
             self._prune_apply(delta)
 
@@ -589,8 +711,12 @@ class LloydEngine:
         """Last pruned step: whether this rank re-assigned all rows, and how many it re-assigned."""
         if self._pst is None:
             return {}
-        full, m = self._pst.last
+        full, m = self._pdev_last() if self._pdev else self._pst.last
         return {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
+
+    def prune_history(self) -> list:
+        """(full step?, re-assigned rows) of every pruned step of this engine, rank-local."""
+        return [] if self._pst is None else list(self._pst.history)
 
     def converged(self, tol: float) -> bool:
         """Spark's rule: converged iff every centre moved at most tol (euclidean)."""
@@ -622,6 +748,20 @@ class LloydEngine:
         if not self.gpu:
             return K.assign_reference(self.x, self.centers if centers is None else centers)
         return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers, self.xnorm)
+
+    @property
+    def last_cost(self):
+        """Cost of the last step's assignment (a device scalar); the device pruned step evaluates it
+        on first access (a collective: every rank reads it together)."""
+        if self._cost_fn is not None:
+            fn, self._cost_fn = self._cost_fn, None
+            self._last_cost = fn()
+        return self._last_cost
+
+    @last_cost.setter
+    def last_cost(self, v) -> None:
+        self._cost_fn = None
+        self._last_cost = v
 
     def training_cost(self) -> float:
         """Spark's trainingCost: sum of squared distances, or of cosine distances (spherical)."""

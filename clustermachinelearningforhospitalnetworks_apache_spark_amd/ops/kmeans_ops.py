@@ -51,9 +51,20 @@ _native.register_kernel_sigs({
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                   c_vp]),
     "cml_kmeans_prune_lower": (c_int, [c_vp, c_int, c_vp, c_vp, ctypes.c_float, ctypes.c_float, c_ll, c_vp, c_vp]),
-    "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_int, c_ll, c_vp,
-                                        c_vp, c_vp]),
+    "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]),
+    "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_centre_stats": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
+                                         c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
+                                         c_vp]),
 })
+
+
+def _ptr(t) -> int:
+    return 0 if t is None else t.data_ptr()
 
 
 @dataclass
@@ -298,13 +309,14 @@ class DeltaState:
     by ``invalidate()``."""
 
     def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, nblk: int,
-                 fp8: bool = False, cap_fraction: float | None = None):
+                 fp8: bool = False, cap_fraction: float | None = None, cap: int | None = None,
+                 pcap: int | None = None):
         self.k, self.d, self.nblk = k, d, int(nblk)
         if cap_fraction is None:  # steps with more label changes than this re-accumulate in full
             cap_fraction = float(os.environ.get("CML_KMEANS_DELTA_CAP", 0.25))
-        self.cap = max(1024, int(n * cap_fraction))
+        self.cap = max(1024, int(n * cap_fraction)) if cap is None else int(cap)
         # change lists are per assign workgroup: nblk lists of pcap entries (slack for uneven churn)
-        self.pcap = max(64, -(-2 * self.cap // self.nblk))
+        self.pcap = max(64, -(-2 * self.cap // self.nblk)) if pcap is None else int(pcap)
         self.rows = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
         self.old = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
         self.wg_count = torch.zeros(self.nblk, dtype=torch.int32, device=device)
@@ -350,21 +362,30 @@ class DeltaState:
 
 
 def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift: torch.Tensor,
-                 dmax: torch.Tensor, thr: torch.Tensor, c2: float, k: int, cand: torch.Tensor,
-                 count: torch.Tensor, stream=None) -> None:
+                 dmax: torch.Tensor, thr: torch.Tensor, c2, k: int, cand: torch.Tensor,
+                 count: torch.Tensor, stream=None, xn: torch.Tensor | None = None,
+                 cand_lab: torch.Tensor | None = None, cand_xn: torch.Tensor | None = None,
+                 skip: torch.Tensor | None = None, zero_count: bool = True) -> None:
     """K9p (``kmeans_prune.hip``): moves the per-row distance bounds by the centre drifts
     (ub += drift[label], lb -= largest drift of another centre) and appends to ``cand`` the rows whose
     bounds no longer prove the label (neither ub <= thr[label] nor ub <= lb - c2 / lb); ``count[0]`` =
-    their number. ``dmax`` = [largest drift, second largest, index of the largest]. CPU tensors: the
-    same pass in torch (f64 bounds), candidates in row order."""
+    their number (on the GPU at most ``len(cand)`` of them are written). ``dmax`` = [largest drift, second largest, index of the largest]. GPU: ``c2`` is a
+    device scalar; with ``cand_lab``/``cand_xn`` the candidates' labels and norms are written compacted
+    beside ``cand`` (the K9r candidate pass reads them); ``skip`` (device flag) turns the launch into a
+    no-op; ``zero_count=False`` leaves the zeroing of ``count`` to the caller (the centre-stats pass).
+    CPU tensors: the same pass in torch (f64 bounds), candidates in row order."""
     n = int(labels.shape[0])
     if labels.is_cuda:
-        count.zero_()
+        if zero_count:
+            count.zero_()
+        if not torch.is_tensor(c2):
+            c2 = torch.tensor([float(c2)], dtype=torch.float32, device=labels.device)
         _native.check(_native.kernels().cml_kmeans_prune_bounds(
             labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
-            float(c2), int(k), n, cand.data_ptr(), count.data_ptr(), _native.stream_ptr(stream)),
-            "kmeans_prune_bounds")
+            c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
+            _ptr(skip), int(cand.shape[0]), _native.stream_ptr(stream)), "kmeans_prune_bounds")
         return
+    c2 = float(c2)
     lab = labels[:n].long()
     ub[:n] += drift[lab]
     other = torch.where(lab == int(dmax[2]), dmax[1], dmax[0])
@@ -375,6 +396,49 @@ def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift
     idx = torch.nonzero(~keep).flatten()
     cand[: idx.numel()] = idx.to(cand.dtype)
     count[0] = idx.numel()
+
+
+def prune_gate(count: torch.Tensor, cap: int, force: torch.Tensor, mode: torch.Tensor, stream=None) -> None:
+    """mode[0] = 1 (full pass) when force[0] or count[0] > cap, else 0 (candidate pass). Device only."""
+    _native.check(_native.kernels().cml_kmeans_prune_gate(count.data_ptr(), int(cap), force.data_ptr(),
+                                                          mode.data_ptr(), _native.stream_ptr(stream)),
+                  "kmeans_prune_gate")
+
+
+def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, mx: torch.Tensor, tau: float,
+                 cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor, thr: torch.Tensor, dmax: torch.Tensor,
+                 mc: torch.Tensor, c2: torch.Tensor, count: torch.Tensor, force: torch.Tensor, stream=None) -> None:
+    """Centre statistics of the device pruned step (``kmeans_prune.hip``) over the bf16 centres: norms,
+    drifts against ``cb_old`` (None: no drift), half nearest-centre distances -> thr, dmax, mc, c2;
+    resets ``count`` and ``force``. No host synchronisation."""
+    _native.check(_native.kernels().cml_kmeans_centre_stats(
+        cb.data_ptr(), _ptr(cb_old), cb.stride(0), int(k), int(d), mx.data_ptr(), float(tau), cn.data_ptr(),
+        half.data_ptr(), drift.data_ptr(), thr.data_ptr(), dmax.data_ptr(), mc.data_ptr(), c2.data_ptr(),
+        count.data_ptr(), force.data_ptr(), _native.stream_ptr(stream)), "kmeans_centre_stats")
+
+
+def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor,
+                  plan: AssignPlan, xnorm: torch.Tensor, labels: torch.Tensor, cost_part: torch.Tensor | None,
+                  ub: torch.Tensor, lb: torch.Tensor, mc: torch.Tensor, tau: float,
+                  hist: torch.Tensor | None = None, rank: torch.Tensor | None = None,
+                  delta: "DeltaState | None" = None, idx: torch.Tensor | None = None,
+                  n_dev: torch.Tensor | None = None, lab_in: torch.Tensor | None = None,
+                  gate: torch.Tensor | None = None, want: int = 0, stream=None) -> None:
+    """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
+    the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
+    ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
+    rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag."""
+    if plan.rr_ct <= 0 or plan.kc != plan.kp:
+        raise ValueError("the pruned-step assign needs the K9r plan (Dp in {128, 256, 512}, k <= 256)")
+    _native.check(_native.kernels().cml_kmeans_assign_rr_ext(
+        int(mode), x.data_ptr(), int(n), x.stride(0), int(dp), cb.data_ptr(), cb.stride(0), plan.kc, plan.kp,
+        cnorm.data_ptr(), xnorm.data_ptr(), labels.data_ptr(), _ptr(cost_part), _ptr(hist), _ptr(rank),
+        plan.grid, int(is_fp8(x)),
+        _ptr(delta.rows if delta is not None else None), _ptr(delta.old if delta is not None else None),
+        _ptr(delta.wg_count if delta is not None else None), _ptr(delta.overflow if delta is not None else None),
+        delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
+        lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _native.stream_ptr(stream)),
+        f"kmeans_assign_rr_ext(mode={mode})")
 
 
 def prune_lower(dist: torch.Tensor, lab: torch.Tensor, xn: torch.Tensor, mc: float, tau: float,

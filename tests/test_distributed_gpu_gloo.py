@@ -36,7 +36,8 @@ def _fit(x_local, comm, chunks):
     import torch
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
     full = _data()
-    eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D, K, comm, row_chunks=chunks)
+    eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D, K, comm, row_chunks=chunks,
+                      prune=False)
     eng.set_centers(full[:K])
     modes = []
     for _ in range(6):

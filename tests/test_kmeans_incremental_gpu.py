@@ -13,6 +13,12 @@ from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans im
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _full_steps_only(monkeypatch):
+    """These tests target the full / incremental step machinery: pruned steps off by default."""
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "0")
+
+
 def _blobs(n, d, k, seed, grid=True, dtype=torch.bfloat16):
     g = torch.Generator(device="cuda")
     g.manual_seed(seed)

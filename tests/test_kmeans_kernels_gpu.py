@@ -10,6 +10,12 @@ from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmean
 pytestmark = pytest.mark.gpu
 
 
+@pytest.fixture(autouse=True)
+def _full_steps_only(monkeypatch):
+    """These tests target the full / incremental step machinery: pruned steps off by default."""
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "0")
+
+
 def _ref_assign(xb, cb):
     x = xb.double().cpu()
     c = cb.double().cpu()

@@ -1,7 +1,9 @@
 """Exact bound-pruned Lloyd steps (``LloydEngine(prune=True)``, K9p ``kmeans_prune.hip``) against the
 full step: the same labels, sums and centres at every iteration, with most rows pruned once the
-centres settle. CPU tests run the torch form of every pass; GPU tests the HIP bounds kernel, the
-gathered K9 re-assignment and the hipBLASLt lower bounds."""
+centres settle. CPU tests run the torch form of every pass; GPU tests the device pruned step (K9p
+bounds + gate, K9r top-2 full pass and candidate pass, incremental sums, centre statistics) where
+the K9r assign applies, and the torch-bounds form (gathered K9 re-assignment, GEMM lower bounds)
+for the other shapes."""
 import os
 import socket
 
@@ -23,7 +25,7 @@ def _blobs(n, d, k, seed, scale=3.0, device="cpu", dtype=torch.float64):
 
 
 def _pair(x, d, k, init, steps, **kw):
-    a = LloydEngine(x, d, k, **kw)
+    a = LloydEngine(x, d, k, prune=False, **kw)
     b = LloydEngine(x, d, k, prune=True, **kw)
     a.set_centers(init)
     b.set_centers(init)
@@ -67,7 +69,7 @@ def test_pruned_spherical_cpu():
 def test_pruned_fit_converges_like_full_cpu():
     x = _blobs(8_000, 4, 6, seed=9, scale=5.0)
     init = x[:6].numpy()
-    a = LloydEngine(x, 4, 6)
+    a = LloydEngine(x, 4, 6, prune=False)
     b = LloydEngine(x, 4, 6, prune=True)
     a.set_centers(init)
     b.set_centers(init)
@@ -218,3 +220,162 @@ def test_lower_bound_kernel_matches_torch(m, k):
     ref = (ref - 3e-5 * (xn.double() + 300.0)).clamp(min=0).sqrt()
     torch.testing.assert_close(out.double(), ref, rtol=2e-6, atol=1e-5)
     assert bool((out.double() <= ref * (1 + 1e-7) + 1e-6).all())
+
+
+# ---------------------------------------------------------------- device pruned-step kernels
+def _rr_setup(n, d, k, seed):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import to_device_matrix
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.device import padded_dim, round_up
+    x = to_device_matrix(_blobs(n, d, k, seed=seed, device="cuda", dtype=torch.bfloat16), d)
+    dp = x.shape[1]
+    kp = round_up(k, 32)
+    pick = torch.randint(0, n, (k,), device="cuda", generator=torch.Generator(device="cuda").manual_seed(seed))
+    cent = x[pick, :d]
+    cent = cent.double().contiguous()
+    cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device="cuda")
+    cn = torch.zeros(kp, dtype=torch.float32, device="cuda")
+    K.update_centers(None, k, d, cent.clone(), cb, dp, kp, cn, None)
+    xn = K.row_sqnorm(x, n, dp)
+    return x, dp, kp, cb, cn, xn
+
+
+def _exact_top2(x, d, cb, k):
+    xf = x[:, :d].double()
+    c = cb[:k, :d].double()
+    dist = (xf * xf).sum(1, keepdim=True) - 2 * xf @ c.T + (c * c).sum(1)[None]
+    top = torch.topk(dist, min(2, k), dim=1, largest=False)
+    return dist, top.values, top.indices
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,k", [(70_001, 256, 256), (33_333, 128, 64), (20_000, 512, 100), (1, 256, 2),
+                                   (4_097, 256, 1)])
+def test_rr_top2_full_pass_bounds(n, d, k):
+    """K9r mode 1: labels equal the plain K9r pass; ub >= the exact distance to the label's centre and
+    lb <= the exact distance to every other centre (f64 over the same bf16 operands), tight within tau."""
+    x, dp, kp, cb, cn, xn = _rr_setup(n, d, k, seed=n)
+    plan = K.plan_assign(n, dp, k)
+    assert plan.rr_ct > 0
+    lab0 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    K.assign_bf16(x, n, dp, cb, cn, plan, lab0, None, torch.zeros(plan.grid, dtype=torch.float64, device="cuda"),
+                  xnorm=xn)
+    lab = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ub = torch.zeros(n, device="cuda")
+    lb = torch.zeros(n, device="cuda")
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    tau = LloydEngine.prune_tau(dp)
+    mc = torch.tensor([float(cn[:k].max())], device="cuda")
+    K.assign_rr_ext(1, x, n, dp, cb, cn, plan, xn, lab, None, ub, lb, mc, tau)
+    torch.cuda.synchronize()
+    assert torch.equal(lab, lab0)
+    dist, vals, _ = _exact_top2(x, d, cb, k)
+    own = dist.gather(1, lab.long()[:, None]).squeeze(1).clamp(min=0).sqrt()
+    assert bool((ub.double() >= own * (1 - 1e-12)).all())
+    if k > 1:
+        other = dist.scatter(1, lab.long()[:, None], float("inf")).min(1).values.clamp(min=0).sqrt()
+        assert bool((lb.double() <= other * (1 + 1e-12)).all())
+        slack = (tau * (xn.double() + float(mc)) + 1e-6 * other ** 2).sqrt() * 2 + 1e-3
+        assert bool(((other - lb.double()) <= slack).all())
+    else:
+        assert bool(torch.isinf(lb).all())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n,d,k,m", [(90_000, 256, 256, 5_000), (90_000, 256, 256, 0), (50_000, 128, 64, 49_999),
+                                     (30_000, 512, 128, 777), (64, 256, 33, 64)])
+def test_rr_candidate_pass_matches_full(n, d, k, m):
+    """K9r mode 2 on a scattered candidate list (count read on the device): the candidates get the
+    labels and bounds mode 1 gives them; every other row is untouched; the change log lists exactly
+    the candidates whose label changed, with their old label."""
+    x, dp, kp, cb, cn, xn = _rr_setup(n, d, k, seed=n + m)
+    plan = K.plan_assign(n, dp, k)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    tau = LloydEngine.prune_tau(dp)
+    mc = torch.tensor([float(cn[:k].max())], device="cuda")
+    ref_lab = torch.zeros(n, dtype=torch.int32, device="cuda")
+    ref_ub, ref_lb = torch.zeros(n, device="cuda"), torch.zeros(n, device="cuda")
+    K.assign_rr_ext(1, x, n, dp, cb, cn, plan, xn, ref_lab, None, ref_ub, ref_lb, mc, tau)
+    g = torch.Generator(device="cuda").manual_seed(m)
+    old = torch.randint(0, k, (n,), device="cuda", generator=g, dtype=torch.int32)
+    cand = torch.randperm(n, device="cuda", generator=g)[:m].to(torch.int32)
+    tr = plan.round_rows
+    cap = max(m, 1)
+    pad = -(-cap // tr) * tr + tr
+    idx = torch.zeros(pad, dtype=torch.int32, device="cuda")
+    idx[:m] = cand
+    clab = torch.zeros(pad, dtype=torch.int32, device="cuda")
+    clab[:m] = old[cand.long()]
+    cxn = torch.zeros(pad, device="cuda")
+    cxn[:m] = xn[cand.long()]
+    cnt = torch.tensor([m], dtype=torch.int32, device="cuda")
+    lab = old.clone()
+    ub = torch.full((n,), -1.0, device="cuda")
+    lb = torch.full((n,), -1.0, device="cuda")
+    per_wg = -(-(-(-cap // tr)) // plan.grid) * tr
+    dl = K.DeltaState(n, k, d, dp, 1, k * d + k + 1, x.device, plan.grid, cap=max(cap, 1024), pcap=max(per_wg, 64))
+    K.assign_rr_ext(2, x, cap, dp, cb, cn, plan, cxn, lab, None, ub, lb, mc, tau, delta=dl, idx=idx, n_dev=cnt,
+                    lab_in=clab)
+    torch.cuda.synchronize()
+    sel = torch.zeros(n, dtype=torch.bool, device="cuda")
+    sel[cand.long()] = True
+    assert torch.equal(lab[sel], ref_lab[sel]) and torch.equal(lab[~sel], old[~sel])
+    assert torch.equal(ub[sel], ref_ub[sel]) and torch.equal(lb[sel], ref_lb[sel])
+    assert bool((ub[~sel] == -1).all()) and bool((lb[~sel] == -1).all())
+    assert int(dl.overflow.item()) == 0
+    rows, olds = [], []
+    for b in range(plan.grid):
+        c = int(dl.wg_count[b].item())
+        rows.append(dl.rows[b * dl.pcap: b * dl.pcap + c])
+        olds.append(dl.old[b * dl.pcap: b * dl.pcap + c])
+    rows = torch.cat(rows).long()
+    olds = torch.cat(olds)
+    changed = sel & (ref_lab != old)
+    assert sorted(rows.tolist()) == sorted(torch.nonzero(changed).flatten().tolist())
+    assert torch.equal(olds, old[rows])
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("k,d", [(256, 256), (37, 100), (1, 16), (2, 512)])
+def test_centre_stats_kernel_matches_torch(k, d):
+    g = torch.Generator(device="cuda").manual_seed(k * d)
+    dp = -(-d // 16) * 16
+    cb = (torch.randn(k + 3, dp, device="cuda", generator=g) * 3).to(torch.bfloat16)
+    cb[:, d:] = 0
+    old = (cb.float() + torch.randn(k + 3, dp, device="cuda", generator=g) * 0.1).to(torch.bfloat16)
+    old[:, d:] = 0
+    if k > 2:
+        cb[2] = cb[1]  # coincident centres: half distance 0 -> thr = -inf
+    f = dict(cn=torch.zeros(k, dtype=torch.float64, device="cuda"),
+             half=torch.zeros(k, dtype=torch.float64, device="cuda"),
+             drift=torch.zeros(k, device="cuda"), thr=torch.zeros(k, device="cuda"), dmax=torch.zeros(3, device="cuda"),
+             mc=torch.zeros(1, device="cuda"), c2=torch.zeros(1, device="cuda"),
+             count=torch.full((1,), 7, dtype=torch.int32, device="cuda"),
+             force=torch.ones(1, dtype=torch.int32, device="cuda"))
+    mx = torch.tensor([1234.5], device="cuda")
+    tau = 3e-5
+    K.centre_stats(cb, old, k, d, mx, tau, f["cn"], f["half"], f["drift"], f["thr"], f["dmax"], f["mc"], f["c2"],
+                   f["count"], f["force"])
+    torch.cuda.synchronize()
+    c = cb[:k, :d].double()
+    o = old[:k, :d].double()
+    cn = (c * c).sum(1)
+    torch.testing.assert_close(f["cn"], cn, rtol=1e-12, atol=1e-9)
+    dr = (c - o).pow(2).sum(1).sqrt()
+    assert bool((f["drift"].double() >= dr * (1 - 1e-7)).all())
+    torch.testing.assert_close(f["drift"].double(), dr, rtol=2e-6, atol=1e-7)
+    top = torch.topk(dr, min(2, k)).values
+    assert abs(float(f["dmax"][0]) - float(top[0])) <= 2e-6 * float(top[0]) + 1e-7
+    if k > 1:
+        assert abs(float(f["dmax"][1]) - float(top[-1])) <= 2e-6 * float(top[-1]) + 1e-7
+        d2 = (cn[:, None] + cn[None, :] - 2 * c @ c.T).clamp(min=0)
+        d2 = ((c[:, None, :] - c[None, :, :]) ** 2).sum(-1)
+        d2.fill_diagonal_(float("inf"))
+        half = 0.5 * d2.min(1).values.sqrt()
+        sl = tau * (1234.5 + float(cn.max()))
+        ref = torch.where(half > 0, (half - sl / (2 * half)) * (1 - 1e-6), torch.full_like(half, -float("inf")))
+        torch.testing.assert_close(f["thr"].double(), ref, rtol=1e-6, atol=1e-6)
+    else:
+        assert bool(torch.isinf(f["thr"]).all())
+    assert abs(float(f["mc"]) - float(cn.max())) <= 1e-6 * float(cn.max())
+    assert abs(float(f["c2"]) - 2 * tau * (1234.5 + float(cn.max()))) <= 1e-6 * float(f["c2"])
+    assert int(f["count"]) == 0 and int(f["force"]) == 0

@@ -147,7 +147,7 @@ def test_pruned_lloyd_equals_full_lloyd(n, d, k, scale, seed):
     cen = torch.randn(k, d, generator=g, dtype=torch.float64) * scale
     x = cen[torch.randint(0, k, (n,), generator=g)] + torch.randn(n, d, generator=g, dtype=torch.float64)
     init = x[torch.randperm(n, generator=g)[:k]].numpy()
-    a, b = LloydEngine(x, d, k), LloydEngine(x, d, k, prune=True)
+    a, b = LloydEngine(x, d, k, prune=False), LloydEngine(x, d, k, prune=True)
     a.set_centers(init)
     b.set_centers(init)
     for _ in range(6):
