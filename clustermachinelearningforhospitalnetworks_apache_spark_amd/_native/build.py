@@ -97,7 +97,8 @@ def build_host(force: bool = False, verbose: bool = False) -> Path:
     if not srcs:
         return HOST_LIB
     cxx = os.environ.get("CXX", shutil.which("g++") or "c++")
-    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden"]
+    # -ffp-contract=off: kmeans_local.cpp reproduces the device kernels' explicitly rounded f64 math
+    flags = ["-O3", "-std=c++17", "-fPIC", "-shared", "-pthread", "-fvisibility=hidden", "-ffp-contract=off"]
     digest = _digest(srcs + hdrs, " ".join(flags))
     if not force and _stamp_ok(HOST_LIB, digest):
         return HOST_LIB

@@ -459,67 +459,6 @@ __global__ __launch_bounds__(NT, 1) void kmeans_assign_bf16(
 
 namespace {
 
-// ||x_i||² of the bf16 rows (f32), once per fit: the assign epilogue then reads 4 B/row
-// instead of re-deriving the norm from the tile (128 converts + FMAs per lane per tile).
-template <int NCH>
-__global__ __launch_bounds__(256) void row_sqnorm_bf16(const u16* __restrict__ X, long long n, long long ldx,
-                                                       float* __restrict__ out) {
-  constexpr int RPW = 64 / NCH;
-  const int lane = threadIdx.x & 63;
-  const int sub = lane / NCH, c = lane - sub * NCH;
-  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW) {
-    const long long row = r0 + sub;
-    float s = 0.f;
-    if (row < n) {
-      const uint4 v = *reinterpret_cast<const uint4*>(X + row * ldx + 8 * c);
-      const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float lo = bf16_to_f32((u16)(w[q] & 0xffffu)), hi = bf16_to_f32((u16)(w[q] >> 16));
-        s = fmaf(lo, lo, s);
-        s = fmaf(hi, hi, s);
-      }
-    }
-#pragma unroll
-    for (int o = NCH / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (c == 0 && row < n) out[row] = s;
-  }
-}
-
-// ||x_i||² of OCP e4m3fn rows (f32): NCH 16-byte chunks per row.
-template <int NCH>
-__global__ __launch_bounds__(256) void row_sqnorm_fp8(const unsigned char* __restrict__ X, long long n, long long ldx,
-                                                      float* __restrict__ out) {
-  typedef float f2 __attribute__((ext_vector_type(2)));
-  constexpr int RPW = 64 / NCH;
-  const int lane = threadIdx.x & 63;
-  const int sub = lane / NCH, c = lane - sub * NCH;
-  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
-  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW) {
-    const long long row = r0 + sub;
-    float s = 0.f;
-    if (row < n) {
-      const uint4 v = *reinterpret_cast<const uint4*>(X + row * ldx + 16 * c);
-      const unsigned w[4] = {v.x, v.y, v.z, v.w};
-#pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], false);
-        const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], true);
-        s = fmaf(a.x, a.x, s);
-        s = fmaf(a.y, a.y, s);
-        s = fmaf(b.x, b.x, s);
-        s = fmaf(b.y, b.y, s);
-      }
-    }
-#pragma unroll
-    for (int o = NCH / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
-    if (c == 0 && row < n) out[row] = s;
-  }
-}
-
 template <int CPL>
 __device__ __forceinline__ void load_cols(const u16* p, float (&v)[CPL]) {
   if constexpr (CPL == 2) {
@@ -1425,41 +1364,18 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
                       nullptr, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }
 
+// ||x||² of the device matrix: the row pass of kmeans_init.hip (norms only), the one definition of
+// the cached norms.
+extern "C" int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, float* xn,
+                                   const float* c0, float c0n, float* cost, int* near, unsigned* xn_max,
+                                   int* erange, void* stream);
+
 CML_API int cml_row_sqnorm_fp8(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
-  if (Dp % 64 != 0 || Dp > 1024 || ldx % 16 != 0) return (int)hipErrorInvalidValue;
-  const unsigned char* x = (const unsigned char*)X;
-  hipStream_t st = (hipStream_t)stream;
-  const long long rows_per_block = 4LL * (64 / (Dp / 16));
-  const long long blocks = std::min<long long>((n + rows_per_block - 1) / rows_per_block, 256LL * 16);
-  const dim3 g((unsigned)std::max<long long>(blocks, 1));
-  switch (Dp / 16) {
-    case 4: hipLaunchKernelGGL(row_sqnorm_fp8<4>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 8: hipLaunchKernelGGL(row_sqnorm_fp8<8>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 16: hipLaunchKernelGGL(row_sqnorm_fp8<16>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 32: hipLaunchKernelGGL(row_sqnorm_fp8<32>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 64: hipLaunchKernelGGL(row_sqnorm_fp8<64>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-  return cml_status();
+  return cml_kmeans_row_pass(X, n, ldx, Dp, 1, out, nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 CML_API int cml_row_sqnorm_bf16(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
-  if (Dp % 16 != 0 || Dp > 512 || ldx % 8 != 0) return (int)hipErrorInvalidValue;
-  const u16* x = (const u16*)X;
-  hipStream_t st = (hipStream_t)stream;
-  const long long rows_per_block = 4LL * (64 / (Dp / 8));
-  const long long blocks = std::min<long long>((n + rows_per_block - 1) / rows_per_block, 256LL * 16);
-  const dim3 g((unsigned)std::max<long long>(blocks, 1));
-  switch (Dp / 8) {
-    case 2: hipLaunchKernelGGL(row_sqnorm_bf16<2>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 4: hipLaunchKernelGGL(row_sqnorm_bf16<4>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 8: hipLaunchKernelGGL(row_sqnorm_bf16<8>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 16: hipLaunchKernelGGL(row_sqnorm_bf16<16>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 32: hipLaunchKernelGGL(row_sqnorm_bf16<32>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    case 64: hipLaunchKernelGGL(row_sqnorm_bf16<64>, g, dim3(256), 0, st, x, n, ldx, out); break;
-    default: return (int)hipErrorInvalidValue;
-  }
-  return cml_status();
+  return cml_kmeans_row_pass(X, n, ldx, Dp, 0, out, nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, stream);
 }
 
 // Regime A. rpw rows per wave-instruction, private copies; dw <= cpl*64/rpw.

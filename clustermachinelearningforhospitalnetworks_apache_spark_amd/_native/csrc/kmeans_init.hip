@@ -1,0 +1,496 @@
+// K12 — k-means|| initialisation on the device (models/kmeans.py ``init_kmeans_parallel``).
+//
+// The reference has no KMeans; this is Spark MLlib's default initMode
+// ("k-means||", initSteps = 2: mllib/clustering/KMeans.scala initKMeansParallel), re-designed so the
+// init of the 100M x 256 headline fit costs a few memory passes instead of ~80 host round trips:
+//
+//   row pass      one read of X: ||x||² (THE row-norm kernel: cml_row_sqnorm_* run it too, so cached
+//                 norms are the same bits whichever path made them), the distance to the first
+//                 centre (the first k-means|| cost), max ||x||² (pruning bounds) and the range of
+//                 the bf16 exponents (exactness guard of the incremental sums) — fused: the init
+//                 used to read X twice for these;
+//   sample        u(seed, round, global row) < 2k·cost/Σcost (utils/rng.py counter uniform, the same
+//                 splitmix64 as K5), compacted to a row list;
+//   merge         cost/nearest-candidate update from one K9r pass over a candidate chunk (strict <:
+//                 the earlier candidate keeps ties, i.e. argmin order over the candidate list);
+//   local k-means weighted k-means++ seeding + weighted Lloyd (Spark LocalKMeans.kMeansPlusPlus)
+//                 on the ~2k·initSteps candidates, as a few small kernels with no host round trip
+//                 per pick. Every value is formed in a fixed order with explicitly rounded f64
+//                 operations (_rn intrinsics, no contraction), and host/kmeans_local.cpp performs the
+//                 same operations in the same order: the CPU session and the GPU pick the same
+//                 centres bit for bit.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+
+__device__ __forceinline__ unsigned long long splitmix64(unsigned long long x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+// u in [0, 1) of counter c under key (utils/rng.py uniform)
+__device__ __forceinline__ double cu(unsigned long long c, unsigned long long key) {
+  return (double)(splitmix64(c ^ key) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+// ----------------------------------------------------------------------------------------- row pass
+// A row of NCH 16-byte chunks is read by LPR = NCH / CPL lanes, lane l taking chunks l, l + LPR, ...
+// (CPL of them: each load instruction covers LPR·16 contiguous bytes of RPW = 64 / LPR rows). Each lane
+// folds its values in chunk order with f32 fma, then a butterfly over the row's lanes: that fold is
+// THE definition of the cached ||x||² (cml_row_sqnorm_* run this same kernel). 8 lanes per 512-B row
+// (CPL = 4) instead of one lane per chunk keep the shuffle count per byte low; the first version
+// (32 lanes per row, 5 butterfly steps for each of the two sums) ran 13 ms for 51 GB, VALU-bound.
+// U row groups are in flight per lane. c0 (f32 [Dp], the bf16-rounded first centre) may be null.
+// Exponent range of the bf16 magnitudes, branch-free: max of |bits|, min of (|bits| - 1) mod 2^16.
+template <int NCH, int CPL, bool F8, int U>
+__global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char* __restrict__ X, long long n,
+                                                            long long ldb, float* __restrict__ xn_out,
+                                                            const float* __restrict__ c0, float c0n,
+                                                            float* __restrict__ cost_out, int* __restrict__ near_out,
+                                                            unsigned* __restrict__ xn_max,
+                                                            int* __restrict__ erange) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int LPR = NCH / CPL;
+  static_assert(LPR >= 1 && LPR <= 64 && NCH % CPL == 0, "row split");
+  constexpr int RPW = 64 / LPR;
+  constexpr int VPC = F8 ? 16 : 8;  // values per chunk
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, c = lane - sub * LPR;
+  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  const bool dot = c0 != nullptr;
+  unsigned umx = 0u, umn = 0xffffu;
+  unsigned mxb = 0;
+  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW * U) {
+    uint4 v[U][CPL];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + (long long)u * nw * RPW + sub;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        v[u][i] = row < n ? *reinterpret_cast<const uint4*>(X + row * ldb + 16 * (c + LPR * i))
+                          : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + (long long)u * nw * RPW + sub;
+      float s = 0.f, dt = 0.f;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const unsigned w[4] = {v[u][i].x, v[u][i].y, v[u][i].z, v[u][i].w};
+        float xs[VPC];
+        if constexpr (F8) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], false);
+            const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], true);
+            xs[4 * q] = a.x;
+            xs[4 * q + 1] = a.y;
+            xs[4 * q + 2] = b.x;
+            xs[4 * q + 3] = b.y;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            xs[2 * q] = bf16_to_f32((u16)(w[q] & 0xffffu));
+            xs[2 * q + 1] = bf16_to_f32((u16)(w[q] >> 16));
+            const unsigned lo = w[q] & 0x7fffu, hi = (w[q] >> 16) & 0x7fffu;  // rows past n load zeros
+            umx = max(umx, max(lo, hi));
+            umn = min(umn, min((lo + 0xffffu) & 0xffffu, (hi + 0xffffu) & 0xffffu));
+          }
+        }
+#pragma unroll
+        for (int e = 0; e < VPC; ++e) s = fmaf(xs[e], xs[e], s);
+        if (dot) {
+          const float* cc = c0 + VPC * (c + LPR * i);
+#pragma unroll
+          for (int e = 0; e < VPC; ++e) dt = fmaf(xs[e], cc[e], dt);
+        }
+      }
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) {
+        s += __shfl_xor(s, o, 64);
+        if (dot) dt += __shfl_xor(dt, o, 64);
+      }
+      if (c == 0 && row < n) {
+        xn_out[row] = s;
+        mxb = __float_as_uint(s) > mxb ? __float_as_uint(s) : mxb;
+        if (dot) {
+          cost_out[row] = fmaxf(fmaf(-2.f, dt, s + c0n), 0.f);
+          near_out[row] = 0;
+        }
+      }
+    }
+  }
+  // wave reductions, one atomic per wave (integer min/max: the result does not depend on order)
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    mxb = max(mxb, (unsigned)__shfl_xor(mxb, o, 64));
+    umx = max(umx, (unsigned)__shfl_xor(umx, o, 64));
+    umn = min(umn, (unsigned)__shfl_xor(umn, o, 64));
+  }
+  if (lane == 0) {
+    if (xn_max != nullptr) atomicMax(xn_max, mxb);  // non-negative floats order as their bits
+    if (erange != nullptr && !F8 && umx != 0u) {
+      atomicMin(erange, (int)((umn + 1u) >> 7));
+      atomicMax(erange + 1, (int)(umx >> 7));
+    }
+  }
+}
+
+// cost/nearest from one candidate chunk's K9r pass (best distance + label within the chunk)
+__global__ __launch_bounds__(kThreads) void init_merge_kernel(float* __restrict__ cost, int* __restrict__ near,
+                                                              const float* __restrict__ best,
+                                                              const int* __restrict__ lab, int off, long long n) {
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += (long long)gridDim.x * blockDim.x) {
+    const float b = best[i];
+    if (b < cost[i]) {
+      cost[i] = b;
+      near[i] = lab[i] + off;
+    }
+  }
+}
+
+// rows with u(row id) < scale·cost (Spark: rand < 2·k·cost / Σcost), appended to out (unordered)
+__global__ __launch_bounds__(kThreads) void init_sample_kernel(const float* __restrict__ cost,
+                                                               const long long* __restrict__ ids, long long n,
+                                                               unsigned long long key, double scale,
+                                                               int* __restrict__ out, int* __restrict__ count,
+                                                               long long cap) {
+  const int lane = threadIdx.x & 63;
+  for (long long i0 = (long long)blockIdx.x * blockDim.x; i0 < n; i0 += (long long)gridDim.x * blockDim.x) {
+    const long long i = i0 + threadIdx.x;
+    bool take = false;
+    if (i < n) take = cu((unsigned long long)ids[i], key) < scale * (double)cost[i];
+    const unsigned long long bal = __ballot(take);
+    if (bal) {
+      const int leader = __builtin_ctzll(bal);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(count, (int)__popcll(bal));
+      base = __shfl(base, leader, 64);
+      const long long at = base + (long long)__popcll(bal & ((1ull << lane) - 1ull));
+      if (take && at < cap) out[at] = (int)i;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------- local k-means
+// dist(p, c) = fold over t of fma(p_t - c_t, p_t - c_t, acc), acc from 0 (host twin: kmeans_local.cpp)
+__device__ __forceinline__ double dist_seq(const double* __restrict__ p, const double* c, int d) {
+  double acc = 0.0;
+  for (int t = 0; t < d; ++t) {
+    const double e = __dsub_rn(p[t], c[t]);
+    acc = __fma_rn(e, e, acc);
+  }
+  return acc;
+}
+
+constexpr int kBlocks = 256;  // fixed block count of the weighted prefix sums (host twin: the same)
+
+// Weighted k-means++ seeding (Spark LocalKMeans.kMeansPlusPlus): pick 0 ∝ w, pick i ∝ w·d²; the
+// cumulative weight is summed in kBlocks contiguous blocks (fixed order), the pick walks it.
+// One workgroup of kKppThreads; the points are read transposed (PT[t*m + q]: a wave's reads are
+// contiguous), the chosen centre sits in LDS (d doubles). One thread per point and dimension-
+// sequential distance folds keep the host twin's order.
+constexpr int kKppThreads = 1024;
+
+__global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __restrict__ P,
+                                                                const double* __restrict__ PT, int m, int d,
+                                                                const double* __restrict__ w, int k,
+                                                                unsigned long long key, double* __restrict__ C,
+                                                                double* __restrict__ CT, double* __restrict__ d2) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* crow = reinterpret_cast<double*>(smem);
+  __shared__ double part[kBlocks];
+  __shared__ int pick_sh;
+  const int tid = threadIdx.x;
+  const int L = (m + kBlocks - 1) / kBlocks;
+  for (int i = 0; i < k; ++i) {
+    if (tid < kBlocks) {
+      double s = 0.0;
+      const int q1 = min(m, (tid + 1) * L);
+      for (int q = tid * L; q < q1; ++q) s = __dadd_rn(s, i == 0 ? w[q] : __dmul_rn(w[q], d2[q]));
+      part[tid] = s;
+    }
+    __syncthreads();
+    if (tid == 0) {
+      double total = 0.0;
+      for (int b = 0; b < kBlocks; ++b) total = __dadd_rn(total, part[b]);
+      const double u = cu((unsigned long long)i, key);
+      int pick = -1;
+      if (!(total > 0.0)) {
+        pick = (int)__dmul_rn(u, (double)m);
+        pick = pick < m - 1 ? pick : m - 1;
+      } else {
+        const double r = __dmul_rn(u, total);
+        double cum = 0.0;
+        for (int b = 0; b < kBlocks && pick < 0; ++b) {
+          const double nxt = __dadd_rn(cum, part[b]);
+          if (nxt > r) {
+            double c2 = cum;
+            const int q1 = min(m, (b + 1) * L);
+            int lastpos = -1;
+            for (int q = b * L; q < q1; ++q) {
+              const double pw = i == 0 ? w[q] : __dmul_rn(w[q], d2[q]);
+              if (pw > 0.0) lastpos = q;
+              c2 = __dadd_rn(c2, pw);
+              if (c2 > r) { pick = q; break; }
+            }
+            if (pick < 0) pick = lastpos;
+            if (pick < 0) break;
+          }
+          cum = nxt;
+        }
+        if (pick < 0) {  // rounding: the last point of positive weight
+          for (int q = m - 1; q >= 0 && pick < 0; --q)
+            if ((i == 0 ? w[q] : __dmul_rn(w[q], d2[q])) > 0.0) pick = q;
+        }
+        if (pick < 0) pick = 0;
+      }
+      pick_sh = pick;
+    }
+    __syncthreads();
+    const int pk = pick_sh;
+    for (int t = tid; t < d; t += kKppThreads) {
+      const double v = P[(long long)pk * d + t];
+      crow[t] = v;
+      C[(long long)i * d + t] = v;
+      CT[(long long)t * k + i] = v;
+    }
+    __syncthreads();
+    for (int q = tid; q < m; q += kKppThreads) {
+      double acc = 0.0;
+      for (int t = 0; t < d; ++t) {
+        const double e = __dsub_rn(PT[(long long)t * m + q], crow[t]);
+        acc = __fma_rn(e, e, acc);
+      }
+      d2[q] = (i == 0 || acc < d2[q]) ? acc : d2[q];
+    }
+    __syncthreads();
+  }
+}
+
+// labels[q] = argmin_j dist(P_q, C_j) (ties: lowest j); *moved = 1 if any label changed.
+// One workgroup per point; centres read transposed (CT[t*k + j]) so a wave's reads are contiguous.
+__global__ __launch_bounds__(kThreads) void local_assign_kernel(const double* __restrict__ P, int m, int d,
+                                                                const double* __restrict__ CT, int k,
+                                                                int* __restrict__ labels, int* __restrict__ moved) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* prow = reinterpret_cast<double*>(smem);
+  __shared__ double bd[kThreads];
+  __shared__ int bj[kThreads];
+  const int q = blockIdx.x, tid = threadIdx.x;
+  for (int t = tid; t < d; t += kThreads) prow[t] = P[(long long)q * d + t];
+  __syncthreads();
+  double best = __builtin_huge_val();
+  int bi = 0x7fffffff;
+  for (int j = tid; j < k; j += kThreads) {
+    double acc = 0.0;
+    for (int t = 0; t < d; ++t) {
+      const double e = __dsub_rn(prow[t], CT[(long long)t * k + j]);
+      acc = __fma_rn(e, e, acc);
+    }
+    if (acc < best) { best = acc; bi = j; }  // j ascending: strict < keeps the lowest index
+  }
+  bd[tid] = best;
+  bj[tid] = bi;
+  __syncthreads();
+  for (int o = kThreads / 2; o > 0; o >>= 1) {
+    if (tid < o) {
+      const double a = bd[tid], b = bd[tid + o];
+      const int ia = bj[tid], ib = bj[tid + o];
+      if (b < a || (b == a && ib < ia)) { bd[tid] = b; bj[tid] = ib; }
+    }
+    __syncthreads();
+  }
+  if (tid == 0 && labels[q] != bj[0]) {
+    labels[q] = bj[0];
+    *moved = 1;
+  }
+}
+
+// C_j = Σ_{label q = j, q ascending} w_q·P_q (fma folds) · (1 / Σ w_q); cnt[j] = Σ w_q. One workgroup
+// per cluster; spherical: the mean is divided by its norm (sequential fold, correctly rounded sqrt).
+__global__ __launch_bounds__(kThreads) void local_update_kernel(const double* __restrict__ P, int m, int d,
+                                                                const double* __restrict__ w,
+                                                                const int* __restrict__ labels, int k,
+                                                                double* __restrict__ C, double* __restrict__ CT,
+                                                                double* __restrict__ cnt, int spherical) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  int* lab = reinterpret_cast<int*>(smem);                          // [m]
+  double* cvals = reinterpret_cast<double*>(smem + (((size_t)m * 4 + 15) & ~(size_t)15));  // [d]
+  __shared__ double inv_sh, nrm_sh;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  for (int q = tid; q < m; q += kThreads) lab[q] = labels[q];
+  __syncthreads();
+  double c = 0.0;
+  for (int q = 0; q < m; ++q)
+    if (lab[q] == j) c = __dadd_rn(c, w[q]);
+  if (tid == 0) {
+    cnt[j] = c;
+    inv_sh = c > 0.0 ? __ddiv_rn(1.0, c) : 0.0;
+  }
+  __syncthreads();
+  if (!(c > 0.0)) return;  // empty: local_empty_kernel reseeds it
+  const double inv = inv_sh;
+  for (int t = tid; t < d; t += kThreads) {
+    double s = 0.0;
+    for (int q = 0; q < m; ++q)
+      if (lab[q] == j) s = __fma_rn(w[q], P[(long long)q * d + t], s);
+    cvals[t] = __dmul_rn(s, inv);
+  }
+  __syncthreads();
+  if (spherical) {
+    if (tid == 0) {
+      double a = 0.0;
+      for (int t = 0; t < d; ++t) a = __fma_rn(cvals[t], cvals[t], a);
+      const double nr = __dsqrt_rn(a);
+      nrm_sh = nr > 1e-300 ? nr : 1e-300;
+    }
+    __syncthreads();
+    for (int t = tid; t < d; t += kThreads) cvals[t] = __ddiv_rn(cvals[t], nrm_sh);
+    __syncthreads();
+  }
+  for (int t = tid; t < d; t += kThreads) {
+    C[(long long)j * d + t] = cvals[t];
+    CT[(long long)t * k + j] = cvals[t];
+  }
+}
+
+// Empty clusters (cnt == 0), in index order, take point floor(u·m) of the next counter draw
+// (Spark: points(rand.nextInt(points.length))). ctr persists across iterations. One workgroup.
+__global__ __launch_bounds__(kThreads) void local_empty_kernel(const double* __restrict__ P, int m, int d,
+                                                               const double* __restrict__ cnt, int k,
+                                                               unsigned long long key,
+                                                               unsigned long long* __restrict__ ctr,
+                                                               double* __restrict__ C, double* __restrict__ CT,
+                                                               int* __restrict__ picks) {
+  __shared__ int nsh;
+  const int tid = threadIdx.x;
+  if (tid == 0) {
+    unsigned long long cc = *ctr;
+    int ne = 0;
+    for (int j = 0; j < k; ++j) {
+      if (!(cnt[j] > 0.0)) {
+        int q = (int)__dmul_rn(cu(cc++, key), (double)m);
+        q = q < m - 1 ? q : m - 1;
+        picks[2 * ne] = j;
+        picks[2 * ne + 1] = q;
+        ++ne;
+      }
+    }
+    *ctr = cc;
+    nsh = ne;
+  }
+  __syncthreads();
+  const int ne = nsh;
+  for (int e = 0; e < ne; ++e) {
+    const int j = picks[2 * e], q = picks[2 * e + 1];
+    for (int t = tid; t < d; t += kThreads) {
+      const double v = P[(long long)q * d + t];
+      C[(long long)j * d + t] = v;
+      CT[(long long)t * k + j] = v;
+    }
+  }
+}
+
+inline unsigned grid_for(long long n, long long per) {
+  long long g = (n + per - 1) / per;
+  g = g < 1 ? 1 : g;
+  return (unsigned)(g > 4096 ? 4096 : g);
+}
+
+}  // namespace
+
+// X: bf16 [n, ldx elements] (Dp = 16..512) or e4m3fn [n, ldx bytes] (Dp = 64..1024). c0/cost/near may
+// be null together (norms only); xn_max (f32 bits, zero-initialised) and erange (int[2], {INT_MAX, -1}
+// initialised) may be null.
+CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, float* xn,
+                                const float* c0, float c0n, float* cost, int* near, unsigned* xn_max, int* erange,
+                                void* stream) {
+  if (n < 0 || ((c0 == nullptr) != (cost == nullptr)) || ((cost == nullptr) != (near == nullptr)))
+    return (int)hipErrorInvalidValue;
+  if (n == 0) return 0;
+  hipStream_t st = (hipStream_t)stream;
+  const unsigned char* x = (const unsigned char*)X;
+  constexpr int U = 2;
+  const long long rowb = xfp8 ? (long long)Dp : 2LL * Dp;
+  if (xfp8 ? (Dp % 64 != 0 || Dp > 1024 || ldx % 16 != 0) : (Dp % 16 != 0 || Dp > 512 || ldx % 8 != 0))
+    return (int)hipErrorInvalidValue;
+  const long long ldb = xfp8 ? ldx : 2 * ldx;
+#define CML_RP(NCH, CPL, F)                                                                                   \
+  hipLaunchKernelGGL((row_pass_kernel<NCH, CPL, F, U>), dim3(grid_for(n, 4LL * (64 / ((NCH) / (CPL))) * U)), \
+                     dim3(kThreads), 0, st, x, n, ldb, xn, c0, c0n, cost, near, xn_max, erange)
+  switch ((int)(rowb / 16) * (xfp8 ? -1 : 1)) {
+    case 2: CML_RP(2, 2, false); break;        // bf16 Dp = 16
+    case 4: CML_RP(4, 4, false); break;        // 32
+    case 8: CML_RP(8, 4, false); break;        // 64
+    case 16: CML_RP(16, 4, false); break;      // 128
+    case 32: CML_RP(32, 4, false); break;      // 256
+    case 64: CML_RP(64, 4, false); break;      // 512
+    case -4: CML_RP(4, 4, true); break;        // fp8 Dp = 64
+    case -8: CML_RP(8, 4, true); break;        // 128
+    case -16: CML_RP(16, 4, true); break;      // 256
+    case -32: CML_RP(32, 4, true); break;      // 512
+    case -64: CML_RP(64, 4, true); break;      // 1024
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef CML_RP
+  return cml_status();
+}
+
+CML_API int cml_kmeans_init_merge(float* cost, int* near, const float* best, const int* lab, int off, long long n,
+                                  void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(init_merge_kernel, dim3(grid_for(n, kThreads * 4LL)), dim3(kThreads), 0, (hipStream_t)stream,
+                     cost, near, best, lab, off, n);
+  return cml_status();
+}
+
+// count must be zeroed by the caller; at most cap rows are written (count holds the total).
+CML_API int cml_kmeans_init_sample(const float* cost, const long long* ids, long long n, unsigned long long key,
+                                   double scale, int* out, int* count, long long cap, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(init_sample_kernel, dim3(grid_for(n, kThreads * 8LL)), dim3(kThreads), 0, (hipStream_t)stream,
+                     cost, ids, n, key, scale, out, count, cap);
+  return cml_status();
+}
+
+// P: f64 [m, d] candidates, PT: the same transposed [d, m], w: f64 [m]; C: f64 [k, d], CT: f64 [d, k],
+// d2: f64 [m] scratch.
+CML_API int cml_local_kpp(const double* P, const double* PT, int m, int d, const double* w, int k,
+                          unsigned long long key, double* C, double* CT, double* d2, void* stream) {
+  if (m <= 0 || d <= 0 || k <= 0 || (long long)d * 8 > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(local_kpp_kernel, dim3(1), dim3(kKppThreads), (size_t)d * 8, (hipStream_t)stream, P, PT, m, d,
+                     w, k, key, C, CT, d2);
+  return cml_status();
+}
+
+CML_API int cml_local_assign(const double* P, int m, int d, const double* CT, int k, int* labels, int* moved,
+                             void* stream) {
+  if (m <= 0 || (long long)d * 8 > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(local_assign_kernel, dim3(m), dim3(kThreads), (size_t)d * 8, (hipStream_t)stream, P, m, d, CT,
+                     k, labels, moved);
+  return cml_status();
+}
+
+CML_API int cml_local_update(const double* P, int m, int d, const double* w, const int* labels, int k, double* C,
+                             double* CT, double* cnt, int spherical, double* /*unused*/, void* stream) {
+  const size_t lds = (((size_t)m * 4 + 15) & ~(size_t)15) + (size_t)d * 8;
+  if (m <= 0 || lds > 150 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(local_update_kernel, dim3(k), dim3(kThreads), lds, (hipStream_t)stream, P, m, d, w, labels, k,
+                     C, CT, cnt, spherical);
+  return cml_status();
+}
+
+// picks: int [2k] scratch.
+CML_API int cml_local_empty(const double* P, int m, int d, const double* cnt, int k, unsigned long long key,
+                            unsigned long long* ctr, double* C, double* CT, int* picks, void* stream) {
+  hipLaunchKernelGGL(local_empty_kernel, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, P, m, d, cnt, k, key, ctr,
+                     C, CT, picks);
+  return cml_status();
+}

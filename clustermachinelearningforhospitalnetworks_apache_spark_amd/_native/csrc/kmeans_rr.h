@@ -131,6 +131,13 @@ __device__ __forceinline__ void glds4(const void* src, unsigned char* lds) {
 
 typedef const __attribute__((address_space(4))) int* cidx_t;  // constant address space: scalar loads
 
+// median of three (one v_med3_i32): with a <= c it is the second smallest of {a, b, c}
+__device__ __forceinline__ int med3(int a, int b, int c) {
+  const int lo = a < b ? a : b, hi = a < b ? b : a;
+  const int m = hi < c ? hi : c;
+  return lo > m ? lo : m;
+}
+
 // ldx in BYTES; rows are 16-B aligned. Positions past n load row n-1 (discarded).
 template <int DP, bool F8, int MODE>
 __device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, long long ldx, long long n,
@@ -347,10 +354,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
             for (int e = (s * CT * 4) / KS; e < ((s + 1) * CT * 4) / KS; ++e) {
               const int ct = e >> 2, i = e & 3;
               const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
-              if constexpr (TOP2) {
-                const int hi = kv > key[prv] ? kv : key[prv];
-                key2[prv] = hi < key2[prv] ? hi : key2[prv];
-              }
+              if constexpr (TOP2) key2[prv] = med3(key[prv], kv, key2[prv]);  // key <= key2: new second
               key[prv] = kv < key[prv] ? kv : key[prv];
             }
             if (s == KS - 1) {
@@ -367,10 +371,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         for (int e = 0; e < CT * 4; ++e) {
           const int ct = e >> 2, i = e & 3;
           const int kv = (__float_as_int(acc[cur][ct][i]) & ~TAGM) | (ct << 2 | i);
-          if constexpr (TOP2) {
-            const int hi = kv > key[cur] ? kv : key[cur];
-            key2[cur] = hi < key2[cur] ? hi : key2[cur];
-          }
+          if constexpr (TOP2) key2[cur] = med3(key[cur], kv, key2[cur]);
           key[cur] = kv < key[cur] ? kv : key[cur];
         }
         kred[(16 * t + r) * G::STRIDE + wave * 4 + g] = key[cur];

@@ -1,0 +1,148 @@
+// Host twin of the local k-means kernels of csrc/kmeans_init.hip (weighted k-means++ seeding +
+// weighted Lloyd on the k-means|| candidates, Spark LocalKMeans.kMeansPlusPlus semantics).
+//
+// The CPU session (local[n]) and the GPU must start Lloyd from the same centres, so every value is
+// formed here with the operations, in the order, the device kernels use: distances as a fold of
+// fma(p_t - c_t, p_t - c_t, acc) over t; the cumulative pick weight summed in kBlocks contiguous
+// blocks; weighted sums as fma folds in point order; a division for 1 / Σw then a product; IEEE
+// correctly-rounded operations everywhere (this file is built with -ffp-contract=off, and std::fma /
+// std::sqrt are correctly rounded), so both produce the same bits.
+#include <cmath>
+#include <cstdint>
+#include <cstring>
+#include <vector>
+
+#define CML_HOST_API extern "C" __attribute__((visibility("default")))
+
+namespace {
+
+constexpr int kBlocks = 256;
+
+inline uint64_t splitmix64(uint64_t x) {
+  x += 0x9E3779B97F4A7C15ull;
+  x = (x ^ (x >> 30)) * 0xBF58476D1CE4E5B9ull;
+  x = (x ^ (x >> 27)) * 0x94D049BB133111EBull;
+  return x ^ (x >> 31);
+}
+
+inline double cu(uint64_t c, uint64_t key) {
+  return (double)(splitmix64(c ^ key) >> 11) * (1.0 / 9007199254740992.0);
+}
+
+inline double dist_seq(const double* p, const double* c, int d) {
+  double acc = 0.0;
+  for (int t = 0; t < d; ++t) {
+    const double e = p[t] - c[t];
+    acc = std::fma(e, e, acc);
+  }
+  return acc;
+}
+
+void kpp(const double* P, int m, int d, const double* w, int k, uint64_t key, double* C, double* d2) {
+  const int L = (m + kBlocks - 1) / kBlocks;
+  std::vector<double> part(kBlocks);
+  for (int i = 0; i < k; ++i) {
+    auto pw = [&](int q) { return i == 0 ? w[q] : w[q] * d2[q]; };
+    for (int b = 0; b < kBlocks; ++b) {
+      double s = 0.0;
+      const int q1 = std::min(m, (b + 1) * L);
+      for (int q = b * L; q < q1; ++q) s = s + pw(q);
+      part[b] = s;
+    }
+    double total = 0.0;
+    for (int b = 0; b < kBlocks; ++b) total = total + part[b];
+    const double u = cu((uint64_t)i, key);
+    int pick = -1;
+    if (!(total > 0.0)) {
+      pick = (int)(u * (double)m);
+      pick = pick < m - 1 ? pick : m - 1;
+    } else {
+      const double r = u * total;
+      double cum = 0.0;
+      for (int b = 0; b < kBlocks && pick < 0; ++b) {
+        const double nxt = cum + part[b];
+        if (nxt > r) {
+          double c2 = cum;
+          const int q1 = std::min(m, (b + 1) * L);
+          int lastpos = -1;
+          for (int q = b * L; q < q1; ++q) {
+            const double p = pw(q);
+            if (p > 0.0) lastpos = q;
+            c2 = c2 + p;
+            if (c2 > r) { pick = q; break; }
+          }
+          if (pick < 0) pick = lastpos;
+          if (pick < 0) break;
+        }
+        cum = nxt;
+      }
+      if (pick < 0)
+        for (int q = m - 1; q >= 0 && pick < 0; --q)
+          if (pw(q) > 0.0) pick = q;
+      if (pick < 0) pick = 0;
+    }
+    std::memcpy(C + (size_t)i * d, P + (size_t)pick * d, sizeof(double) * (size_t)d);
+    for (int q = 0; q < m; ++q) {
+      const double dd = dist_seq(P + (size_t)q * d, C + (size_t)i * d, d);
+      d2[q] = (i == 0 || dd < d2[q]) ? dd : d2[q];
+    }
+  }
+}
+
+}  // namespace
+
+// Weighted k-means++ + up to max_iter weighted Lloyd iterations; C: f64 [k, d] out. Returns the
+// number of Lloyd assignments run.
+CML_HOST_API int cml_local_kmeans_host(const double* P, int m, int d, const double* w, int k, uint64_t key_pp,
+                                       uint64_t key_empty, int max_iter, int spherical, double* C) {
+  if (m <= 0 || d <= 0 || k <= 0) return -1;
+  std::vector<double> d2(m);
+  kpp(P, m, d, w, k, key_pp, C, d2.data());
+  std::vector<int> lab(m, -1);
+  std::vector<double> cnt(k), cvals(d);
+  uint64_t ctr = 0;
+  int it = 0;
+  for (; it < max_iter; ++it) {
+    bool moved = false;
+    for (int q = 0; q < m; ++q) {
+      double best = HUGE_VAL;
+      int bi = 0x7fffffff;
+      for (int j = 0; j < k; ++j) {
+        const double a = dist_seq(P + (size_t)q * d, C + (size_t)j * d, d);
+        if (a < best) { best = a; bi = j; }
+      }
+      if (lab[q] != bi) { lab[q] = bi; moved = true; }
+    }
+    if (!moved) break;
+    for (int j = 0; j < k; ++j) {
+      double c = 0.0;
+      for (int q = 0; q < m; ++q)
+        if (lab[q] == j) c = c + w[q];
+      cnt[j] = c;
+      if (!(c > 0.0)) continue;
+      const double inv = 1.0 / c;
+      for (int t = 0; t < d; ++t) {
+        double s = 0.0;
+        for (int q = 0; q < m; ++q)
+          if (lab[q] == j) s = std::fma(w[q], P[(size_t)q * d + t], s);
+        cvals[t] = s * inv;
+      }
+      if (spherical) {
+        double a = 0.0;
+        for (int t = 0; t < d; ++t) a = std::fma(cvals[t], cvals[t], a);
+        double nr = std::sqrt(a);
+        nr = nr > 1e-300 ? nr : 1e-300;
+        for (int t = 0; t < d; ++t) cvals[t] = cvals[t] / nr;
+      }
+      std::memcpy(C + (size_t)j * d, cvals.data(), sizeof(double) * (size_t)d);
+    }
+    for (int j = 0; j < k; ++j) {
+      if (!(cnt[j] > 0.0)) {
+        int q = (int)(cu(ctr++, key_empty) * (double)m);
+        q = q < m - 1 ? q : m - 1;
+        std::memcpy(C + (size_t)j * d, P + (size_t)q * d, sizeof(double) * (size_t)d);
+      }
+    }
+  }
+  return it;
+}

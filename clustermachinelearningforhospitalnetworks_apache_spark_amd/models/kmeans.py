@@ -187,7 +187,15 @@ class LloydEngine:
         pdev_ok = self.aplan.rr_ct > 0 and self.aplan.kc == self.aplan.kp and self.cplan.mode == "sort"
         self.best = (torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
                      if (self.aplan.kc < self.aplan.kp or (self.prune and not pdev_ok)) else None)
-        self.xnorm = cached_row_sqnorm(self.x, n, dp)  # constant over the fit, like Spark's cached point norms
+        # ||x||² are constant over the fit, like Spark's cached point norms: reused from the feature
+        # tensor's cache, else computed lazily (_ensure_norms) — k-means|| init fuses them into its
+        # first pass over X
+        ent = getattr(self.x, "_cml_xnorm", None)
+        if ent is not None and ent[0] == self.x._version and ent[1] == (n, dp):
+            self.xnorm, self._norms_ready = ent[2], True
+        else:
+            self.xnorm, self._norms_ready = torch.empty(max(n, 1), dtype=torch.float32, device=dev), False
+        self._erange = None  # bf16 exponent range of X (exactness of the f64 sums), from the row pass
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
             self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
@@ -217,6 +225,38 @@ class LloydEngine:
         elif self.prune:
             self.use_graph, self.delta = False, None  # torch form: host-synchronised, its own sums
 
+    def _set_mx(self) -> None:
+        """Device max ||x||² over every rank (pruning slack), from the cached norms."""
+        st = self._pst
+        if self.n:
+            st.mx.copy_(self.xnorm[: self.n].max().reshape(1))
+        else:
+            st.mx.zero_()
+        if self.comm.is_distributed:
+            self.comm.allreduce_(st.mx, op="max")
+
+    def _row_pass(self, c0: Optional[torch.Tensor] = None, c0n: float = 0.0, cost=None, near=None) -> None:
+        """The one pass over X that fills the norms (and max norm, exponent range; with c0 the first
+        k-means|| costs), then caches the norms on the feature tensor."""
+        n, dp = self.n, self.dp
+        self._erange = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device=self.device)
+        mxv = self._pst.mx if self._pdev else None
+        if mxv is not None:
+            mxv.zero_()
+        if n:
+            K.row_pass(self.x, n, dp, self.xnorm, c0, c0n, cost, near, xn_max=mxv, erange=self._erange)
+        if mxv is not None and self.comm.is_distributed:
+            self.comm.allreduce_(mxv, op="max")
+        self._norms_ready = True
+        try:
+            self.x._cml_xnorm = (self.x._version, (n, dp), self.xnorm)
+        except (AttributeError, RuntimeError):
+            pass
+
+    def _ensure_norms(self) -> None:
+        if self.gpu and not self._norms_ready:
+            self._row_pass()
+
     @property
     def global_n(self) -> int:
         return int(self.comm.sum_scalar(float(self.n)))
@@ -229,6 +269,7 @@ class LloydEngine:
         return self._row_ids
 
     def set_centers(self, centers) -> None:
+        self._ensure_norms()
         c = torch.as_tensor(np.asarray(centers, dtype=np.float64), device=self.device)
         if c.shape != (self.k, self.d):
             raise ValueError(f"centers shape {tuple(c.shape)} != {(self.k, self.d)}")
@@ -251,6 +292,7 @@ class LloydEngine:
     # ------------------------------------------------------------------ iteration
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
+        self._ensure_norms()
         if self._pdev:
             if self.use_graph:
                 self._step_graph()
@@ -395,8 +437,9 @@ class LloydEngine:
         st.half = torch.zeros(k, dtype=torch.float64, device=dev)
         st.mc = torch.zeros(1, dtype=torch.float32, device=dev)
         st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
-        mx = self.comm.max_scalar(float(self.xnorm[:n].max()) if n else 0.0)
-        st.mx = torch.full((1,), mx, dtype=torch.float32, device=dev)
+        st.mx = torch.zeros(1, dtype=torch.float32, device=dev)  # max ||x||² over all ranks (_ensure_norms)
+        if self._norms_ready:
+            self._set_mx()
         st.cb_old = torch.zeros_like(self.cb)
         self._pst = st
         self.delta = K.DeltaState(max(n, 1), k, d, self.dp, 1, self.msg_len, dev, ap.grid, fp8=K.is_fp8(self.x),
@@ -462,6 +505,7 @@ class LloydEngine:
     _PRUNE_CAP = 0.3  # a rank re-assigns all of its rows when more than this fraction are candidates
 
     def _prune_init(self) -> None:
+        self._ensure_norms()
         n, k, d, dev = self.n, self.k, self.d, self.device
         bdt = torch.float32 if self.gpu else torch.float64
         idt = torch.int32 if self.gpu else torch.int64
@@ -747,6 +791,7 @@ class LloydEngine:
             centers = torch.as_tensor(centers, dtype=torch.float64, device=self.device)
         if not self.gpu:
             return K.assign_reference(self.x, self.centers if centers is None else centers)
+        self._ensure_norms()
         return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers, self.xnorm)
 
     @property
@@ -794,11 +839,22 @@ class LloydEngine:
         if not self.gpu:
             lab, best = K.assign_reference(self.x, cands)
             return best, lab
+        self._ensure_norms()
         lab, best = assign_gpu(self.x, self.dp, self.d, cands, self.xnorm)
         return best.to(torch.float64), lab.long()
 
     def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
-        """k-means|| (Bahmani et al.), Spark's default initMode, then weighted local k-means++."""
+        """k-means|| (Bahmani et al.), Spark's default initMode (initSteps rounds sampling each row with
+        probability 2k·cost/Σcost), then weighted local k-means++ + Lloyd on the distinct candidates.
+
+        GPU ranks stay on the device: the first pass over X computes the row norms and the costs
+        against the first centre together (K12 row pass), a round samples with one kernel over the
+        costs, the new candidates' distances run on K9r in chunks of at most 256 centres merged into
+        (cost, nearest candidate), and the local k-means runs as HIP kernels. The nearest candidate of
+        every row is carried across rounds (strict improvement keeps the earlier candidate: argmin's
+        first-index rule over the concatenated list), so the candidate weights need no extra pass.
+        The CPU path runs the same algorithm in f64, with the same distinct-candidate order (sorted
+        rows) and the bitwise-identical local k-means (host twin of the kernels)."""
         k = self.k
         ids = self.row_ids()
         gn = self.global_n
@@ -813,56 +869,55 @@ class LloydEngine:
                                                                       device=self.device)
         row = self.comm.allgather(row)[owner] if self.comm.is_distributed else row
         centers = [row.reshape(1, self.d)]
-        # nearest-candidate index is tracked across rounds (strict improvement keeps the earlier
-        # candidate, i.e. argmin's first-index rule over the concatenated candidate list), so the
-        # candidate weights need no extra assignment pass over the data at the end
-        if self.n:
+        if self.gpu:
+            costs, nearest = self._init_first_pass(centers[0])
+        elif self.n:
             costs, nearest = self._min_dist_idx(centers[0])
         else:
             costs = torch.zeros(0, dtype=torch.float64, device=self.device)
             nearest = torch.zeros(0, dtype=torch.int64, device=self.device)
         ncand = 1
         for step in range(steps):
-            sum_cost = self.comm.sum_scalar(float(costs.sum().item()) if self.n else 0.0)
+            sum_cost = self.comm.sum_scalar(float(costs[: self.n].sum(dtype=torch.float64).item()) if self.n else 0.0)
             if sum_cost <= 0:
                 break
-            us = rng.uniform(ids, seed, stream=100 + step)
-            prob = 2.0 * k * costs / sum_cost
-            chosen = torch.nonzero(us < prob).flatten()
+            if self.gpu:
+                chosen = self._init_sample(costs, ids, rng.key(seed, 100 + step), 2.0 * k / sum_cost)
+            else:
+                us = rng.uniform(ids, seed, stream=100 + step)  # the sample kernel's test: u < scale·cost
+                chosen = torch.nonzero(us < (2.0 * k / sum_cost) * costs).flatten()
             new = self._rows_f64(chosen) if chosen.numel() else torch.zeros((0, self.d), dtype=torch.float64,
                                                                             device=self.device)
             new = self.comm.allgather_cat(new)
             if new.shape[0] == 0:
                 continue
             centers.append(new)
-            if self.n:
+            if self.gpu:
+                self._init_candidate_pass(new, costs, nearest, ncand)
+            elif self.n:
                 d_new, i_new = self._min_dist_idx(new)
                 better = d_new < costs
                 costs = torch.where(better, d_new, costs)
                 nearest = torch.where(better, i_new + ncand, nearest)
             ncand += new.shape[0]
         cand = torch.cat(centers, 0)
-        cand_np, inverse = np.unique(cand.cpu().numpy(), axis=0, return_inverse=True)
-        if cand_np.shape[0] <= k:
-            out = cand_np
+        # distinct candidates in sorted-row order (np.unique's order; identical on every device)
+        uniq, inverse = torch.unique(cand, dim=0, return_inverse=True)
+        if uniq.shape[0] <= k:
+            out = uniq.cpu().numpy()
         else:
             if self.n:
-                inv = torch.as_tensor(inverse.reshape(-1), dtype=torch.int64, device=self.device)
-                w = torch.bincount(inv[nearest], minlength=cand_np.shape[0]).to(torch.float64)
+                w = torch.bincount(inverse.reshape(-1)[nearest[: self.n].long()], minlength=uniq.shape[0])
+                w = w.to(torch.float64)
             else:
-                w = torch.zeros(cand_np.shape[0], dtype=torch.float64, device=self.device)
+                w = torch.zeros(uniq.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)
-            if self.gpu:  # the host BLAS is the slow part of init on a busy CPU; same draws on the device
-                out = local_kmeans_pp_device(torch.as_tensor(cand_np, device=self.device), w, k, seed, max_iter=30,
-                                             spherical=self.spherical)
-            else:
-                out = local_kmeans_pp(cand_np, w.cpu().numpy(), k, seed, max_iter=30, spherical=self.spherical)
+            out = K.local_kmeans(uniq, w, k, seed, max_iter=30, spherical=self.spherical)
             if self.comm.is_distributed:
                 # every rank ran the same local k-means on the same candidates and weights; rank 0's
-                # result is taken verbatim so last-bit differences of device reductions cannot make
-                # the ranks start (and later decide convergence) from different centres
-                t = torch.as_tensor(np.ascontiguousarray(out, dtype=np.float64), device=self.device)
-                out = self.comm.broadcast_(t, 0).cpu().numpy()
+                # result is taken verbatim (one source of truth for the centres every rank starts from)
+                out = self.comm.broadcast_(out.contiguous(), 0)
+            out = out.cpu().numpy()
         if out.shape[0] < k:
             # Spark may return fewer centres when there are < k distinct points; pad by repetition so the
             # device buffers keep their shape, and record the real count.
@@ -871,6 +926,56 @@ class LloydEngine:
         else:
             self.k_effective = k
         return out
+
+    def _init_first_pass(self, c0: torch.Tensor):
+        """(cost f32, nearest i32) of every local row against the first centre, from the row pass that
+        also fills the norms (one read of X; a second read only if the norms were cached already)."""
+        n, d, dp, dev = self.n, self.d, self.dp, self.device
+        cb0 = torch.zeros((32, dp), dtype=torch.bfloat16, device=dev)
+        cn0 = torch.zeros(32, dtype=torch.float32, device=dev)
+        K.update_centers(None, 1, d, c0.reshape(1, d).to(torch.float64).contiguous().clone(), cb0, dp, 32, cn0, None)
+        costs = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        nearest = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        self._row_pass(cb0[0].to(torch.float32).contiguous(), float(cn0[0].item()), costs, nearest)
+        return costs, nearest
+
+    def _init_sample(self, costs: torch.Tensor, ids: torch.Tensor, key: int, scale: float) -> torch.Tensor:
+        """Sorted local rows chosen by one k-means|| round (K12 sample kernel)."""
+        n = self.n
+        if n == 0:
+            return torch.zeros(0, dtype=torch.int64, device=self.device)
+        ids = ids if ids.dtype == torch.int64 and ids.is_contiguous() else ids.to(torch.int64).contiguous()
+        cap = min(n, max(4096, 8 * self.k))
+        for _ in range(2):
+            out = torch.empty(cap, dtype=torch.int32, device=self.device)
+            cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
+            K.init_sample(costs, ids, n, key, scale, out, cnt)
+            m = int(cnt.item())
+            if m <= cap:
+                return torch.sort(out[:m]).values.long()
+            cap = m  # rare: more than the expected ~2k·(share of the cost) rows; run again with room
+        raise RuntimeError("k-means|| sample did not fit its buffer")
+
+    def _init_candidate_pass(self, new: torch.Tensor, costs: torch.Tensor, nearest: torch.Tensor,
+                             off: int) -> None:
+        """Merge the distances to the new candidates (K9r, at most 256 centres per launch) into
+        (cost, nearest)."""
+        n, d, dp, dev = self.n, self.d, self.dp, self.device
+        if n == 0:
+            return
+        lab = torch.zeros(n, dtype=torch.int32, device=dev)
+        best = torch.empty(n, dtype=torch.float32, device=dev)
+        step = 256
+        for c0 in range(0, new.shape[0], step):
+            ch = new[c0:c0 + step].to(torch.float64).contiguous()
+            kc = ch.shape[0]
+            kp = round_up(kc, 32)
+            cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
+            cn = torch.zeros(kp, dtype=torch.float32, device=dev)
+            K.update_centers(None, kc, d, ch.clone(), cb, dp, kp, cn, None)
+            plan = K.plan_assign(n, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
+            K.assign_bf16(self.x, n, dp, cb, cn, plan, lab, best, None, xnorm=self.xnorm)
+            K.init_merge(costs, nearest, best, lab, off + c0, n)
 
 
 def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: Optional[torch.Tensor] = None):
@@ -895,81 +1000,15 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: O
 
 def local_kmeans_pp(points: np.ndarray, weights: np.ndarray, k: int, seed: int, max_iter: int = 30,
                     spherical: bool = False) -> np.ndarray:
-    """Weighted k-means++ seeding + weighted Lloyd on the candidate set (host, float64).
-    ``spherical``: unit-length candidates, centres renormalised after every mean (cosine KMeans)."""
-    rs = np.random.RandomState(seed & 0x7FFFFFFF)
-    n = points.shape[0]
-    w = np.maximum(weights.astype(np.float64), 0)
-    if w.sum() <= 0:
-        w = np.ones(n)
-    centers = np.empty((k, points.shape[1]))
-    centers[0] = points[rs.choice(n, p=w / w.sum())]
-    d2 = ((points - centers[0]) ** 2).sum(1)
-    for i in range(1, k):
-        p = w * d2
-        s = p.sum()
-        idx = rs.choice(n, p=p / s) if s > 0 else rs.randint(n)
-        centers[i] = points[idx]
-        d2 = np.minimum(d2, ((points - centers[i]) ** 2).sum(1))
-    pn = (points * points).sum(1)
-    wp = points * w[:, None]
-    for _ in range(max_iter):
-        dist = pn[:, None] - 2.0 * points @ centers.T + (centers * centers).sum(1)[None, :]
-        lab = dist.argmin(1)
-        # weighted means of every cluster at once (one scatter-add, no per-cluster Python loop)
-        sums = np.zeros_like(centers)
-        np.add.at(sums, lab, wp)
-        wsum = np.bincount(lab, weights=w, minlength=k)
-        cnt = np.bincount(lab, minlength=k)
-        new = sums / np.maximum(wsum, 1e-300)[:, None]
-        if spherical:
-            new = new / np.maximum(np.linalg.norm(new, axis=1), 1e-300)[:, None]
-        for j in np.flatnonzero(cnt == 0):  # empty clusters re-seed in index order (same draws as before)
-            new[j] = points[rs.randint(n)]
-        moved = not np.isclose(new, centers).all()
-        centers = new
-        if not moved:
-            break
-    return centers
+    """Weighted k-means++ seeding + weighted Lloyd on the candidate set (host, float64): the native
+    host twin of the device kernels (``ops.kmeans_ops.local_kmeans``). ``spherical``: centres are
+    renormalised after every mean (cosine KMeans)."""
+    return K.local_kmeans(torch.as_tensor(np.ascontiguousarray(points, dtype=np.float64)),
+                          torch.as_tensor(np.ascontiguousarray(weights, dtype=np.float64)), k, seed,
+                          max_iter=max_iter, spherical=spherical).numpy()
 
 
 def local_kmeans_pp_device(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
                            max_iter: int = 30, spherical: bool = False) -> np.ndarray:
-    """local_kmeans_pp with the float64 arithmetic on ``points.device``: the RandomState draws are
-    the same calls in the same order (each D²-weighted pick copies only its n probabilities to the
-    host for ``RandomState.choice``), so it picks what the host version picks up to last-bit
-    differences of the distance sums."""
-    rs = np.random.RandomState(seed & 0x7FFFFFFF)
-    pts = points.to(torch.float64)
-    n = pts.shape[0]
-    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0)
-    if float(w.sum()) <= 0:
-        w = torch.ones(n, dtype=torch.float64, device=pts.device)
-    w_np = w.cpu().numpy()
-    centers = torch.empty((k, pts.shape[1]), dtype=torch.float64, device=pts.device)
-    centers[0] = pts[int(rs.choice(n, p=w_np / w_np.sum()))]
-    d2 = ((pts - centers[0]) ** 2).sum(1)
-    for i in range(1, k):
-        pr = (w * d2).cpu().numpy()
-        s = pr.sum()
-        idx = rs.choice(n, p=pr / s) if s > 0 else rs.randint(n)
-        centers[i] = pts[int(idx)]
-        d2 = torch.minimum(d2, ((pts - centers[i]) ** 2).sum(1))
-    pn = (pts * pts).sum(1)
-    wp = pts * w[:, None]
-    for _ in range(max_iter):
-        dist = pn[:, None] - 2.0 * pts @ centers.T + (centers * centers).sum(1)[None, :]
-        lab = dist.argmin(1)
-        sums = torch.zeros_like(centers).index_add_(0, lab, wp)
-        wsum = torch.zeros(k, dtype=torch.float64, device=pts.device).index_add_(0, lab, w)
-        cnt = torch.bincount(lab, minlength=k)
-        new = sums / wsum.clamp(min=1e-300)[:, None]
-        if spherical:
-            new = new / new.norm(dim=1).clamp(min=1e-300)[:, None]
-        for j in np.flatnonzero(cnt.cpu().numpy() == 0):
-            new[j] = pts[int(rs.randint(n))]
-        moved = not bool(torch.isclose(new, centers).all())
-        centers = new
-        if not moved:
-            break
-    return centers.cpu().numpy()
+    """local_kmeans_pp on ``points.device`` (HIP kernels on a GPU tensor); bitwise the host result."""
+    return K.local_kmeans(points, weights, k, seed, max_iter=max_iter, spherical=spherical).cpu().numpy()

@@ -63,8 +63,112 @@ _native.register_kernel_sigs({
 })
 
 
+_native.register_kernel_sigs({
+    "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
+                                    c_vp, c_vp]),
+    "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
+    "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
+                                       c_vp]),
+    "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp]),
+    "cml_local_assign": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
+    "cml_local_update": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "cml_local_empty": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+})
+_native.register_host_sigs({
+    "cml_local_kmeans_host": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, ctypes.c_uint64, c_int,
+                                      c_int, c_vp]),
+})
+
+
 def _ptr(t) -> int:
     return 0 if t is None else t.data_ptr()
+
+
+def _u64(v: int) -> int:
+    return int(v) & ((1 << 64) - 1)
+
+
+def row_pass(x: torch.Tensor, n: int, dp: int, xn: torch.Tensor, c0: torch.Tensor | None = None, c0n: float = 0.0,
+             cost: torch.Tensor | None = None, near: torch.Tensor | None = None,
+             xn_max: torch.Tensor | None = None, erange: torch.Tensor | None = None, stream=None) -> None:
+    """One read of X (``kmeans_init.hip``): ``xn`` = ||x||² (bitwise ``row_sqnorm``), optionally the
+    first k-means|| cost against the bf16-rounded centre ``c0`` (f32 [dp], norm ``c0n``) with
+    ``near`` = 0, the max ||x||² (``xn_max``: f32 [1], zero-initialised, updated by bit-pattern
+    atomicMax) and the range of bf16 exponents (``erange``: int32 [2] = {INT_MAX, -1} initialised)."""
+    _native.check(_native.kernels().cml_kmeans_row_pass(
+        x.data_ptr(), int(n), x.stride(0), int(dp), int(is_fp8(x)), xn.data_ptr(), _ptr(c0), float(c0n), _ptr(cost),
+        _ptr(near), _ptr(xn_max), _ptr(erange), _native.stream_ptr(stream)), "kmeans_row_pass")
+
+
+def init_merge(cost: torch.Tensor, near: torch.Tensor, best: torch.Tensor, lab: torch.Tensor, off: int,
+               n: int, stream=None) -> None:
+    """cost/near <- best/lab+off where best < cost (a k-means|| candidate chunk's assign pass)."""
+    _native.check(_native.kernels().cml_kmeans_init_merge(cost.data_ptr(), near.data_ptr(), best.data_ptr(),
+                                                          lab.data_ptr(), int(off), int(n),
+                                                          _native.stream_ptr(stream)), "kmeans_init_merge")
+
+
+def init_sample(cost: torch.Tensor, ids: torch.Tensor, n: int, key: int, scale: float, out: torch.Tensor,
+                count: torch.Tensor, stream=None) -> None:
+    """Rows with counter-uniform(ids[i]) < scale·cost[i] appended (unordered) to ``out`` (at most
+    len(out)); ``count`` (zeroed by the caller) receives their number."""
+    _native.check(_native.kernels().cml_kmeans_init_sample(
+        cost.data_ptr(), ids.data_ptr(), int(n), _u64(key), float(scale), out.data_ptr(), count.data_ptr(),
+        int(out.shape[0]), _native.stream_ptr(stream)), "kmeans_init_sample")
+
+
+def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int, max_iter: int = 30,
+                 spherical: bool = False) -> torch.Tensor:
+    """Weighted k-means++ seeding + weighted Lloyd on a small candidate set (Spark
+    LocalKMeans.kMeansPlusPlus), f64 [k, d]. GPU tensors run the ``kmeans_init.hip`` kernels (one
+    host read per Lloyd iteration, for the moved flag); CPU tensors the host twin
+    (``host/kmeans_local.cpp``), which performs the same rounded operations in the same order: both
+    return the same bits. Draws: counter uniforms under (seed, 200) for the picks and (seed, 201) for
+    empty-cluster reseeds."""
+    from ..utils import rng
+    pts = points.to(torch.float64).contiguous()
+    m, d = pts.shape
+    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0).contiguous()
+    if float(w.sum()) <= 0:
+        w = torch.ones(m, dtype=torch.float64, device=pts.device)
+    key_pp, key_e = rng.key(seed, 200), rng.key(seed, 201)
+    lds_update = ((m * 4 + 15) & ~15) + d * 8
+    if pts.is_cuda and d * 8 <= 64 * 1024 and lds_update <= 150 * 1024:
+        lib = _native.kernels()
+        st = _native.stream_ptr(None)
+        dev = pts.device
+        C = torch.empty((k, d), dtype=torch.float64, device=dev)
+        CT = torch.empty((d, k), dtype=torch.float64, device=dev)
+        d2 = torch.empty(m, dtype=torch.float64, device=dev)
+        lab = torch.full((m,), -1, dtype=torch.int32, device=dev)
+        moved = torch.zeros(1, dtype=torch.int32, device=dev)
+        cnt = torch.zeros(k, dtype=torch.float64, device=dev)
+        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
+        picks = torch.zeros(2 * k, dtype=torch.int32, device=dev)
+        PT = pts.t().contiguous()
+        _native.check(lib.cml_local_kpp(pts.data_ptr(), PT.data_ptr(), m, d, w.data_ptr(), int(k), _u64(key_pp),
+                                        C.data_ptr(), CT.data_ptr(), d2.data_ptr(), st), "local_kpp")
+        for _ in range(max_iter):
+            moved.zero_()
+            _native.check(lib.cml_local_assign(pts.data_ptr(), m, d, CT.data_ptr(), int(k), lab.data_ptr(),
+                                               moved.data_ptr(), st), "local_assign")
+            if int(moved.item()) == 0:
+                break
+            _native.check(lib.cml_local_update(pts.data_ptr(), m, d, w.data_ptr(), lab.data_ptr(), int(k),
+                                               C.data_ptr(), CT.data_ptr(), cnt.data_ptr(), int(bool(spherical)), 0,
+                                               st), "local_update")
+            _native.check(lib.cml_local_empty(pts.data_ptr(), m, d, cnt.data_ptr(), int(k), _u64(key_e),
+                                              ctr.data_ptr(), C.data_ptr(), CT.data_ptr(), picks.data_ptr(), st),
+                          "local_empty")
+        return C
+    P = pts.cpu().contiguous()
+    W = w.cpu().contiguous()
+    C = torch.empty((k, d), dtype=torch.float64)
+    r = _native.host().cml_local_kmeans_host(P.data_ptr(), m, d, W.data_ptr(), int(k), _u64(key_pp), _u64(key_e),
+                                             int(max_iter), int(bool(spherical)), C.data_ptr())
+    if r < 0:
+        raise ValueError("local k-means: empty candidate set")
+    return C.to(pts.device)
 
 
 @dataclass

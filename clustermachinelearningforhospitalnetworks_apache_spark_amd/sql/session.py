@@ -109,8 +109,20 @@ class SparkSession:
         SparkSession.builder = SparkSession.Builder()
         opts = dict(opts or {})
         self.conf = RuntimeConfig(opts)
-        kind, n = parse_master(opts.get("spark.master", os.environ.get("CML_MASTER", "auto")))
+        master = opts.get("spark.master", os.environ.get("CML_MASTER", "auto"))
+        kind, n = parse_master(master)
         self._kind = kind
+        if kind == "gpu" and n is not None:
+            # mi355x[N] names the cluster the way the reference's .master(...) does (ref.py:55-58): N
+            # ranks, one per GPU. A session must not silently run with another world size.
+            world = int(os.environ.get("WORLD_SIZE", "1"))
+            if world != n:
+                raise ValueError(
+                    f"master {master!r} asks for {n} GPU ranks but this process is rank "
+                    f"{os.environ.get('RANK', '0')} of WORLD_SIZE={world}. Start one process per GPU with "
+                    f"`python -m clustermachinelearningforhospitalnetworks_apache_spark_amd.launch "
+                    f"--nproc-per-node {n} your_app.py` (or torchrun --nproc-per-node {n}), or use "
+                    f"master('mi355x') to take the world size from the launcher.")
         if kind == "local" and n:
             torch.set_num_threads(max(1, n))
         # collective watchdog: a rank that stops participating fails the job after the timeout

@@ -295,26 +295,34 @@ class StreamingQuery:
     def _load_state(self) -> Dict[int, Any]:
         """State of the stateful operators after the last committed batch (``state/<batch id>``,
         written by this engine before the commit), identical on every rank."""
-        import pickle
+        from ..utils import jsonstate
         comm = self._session._comm
         st = None
         if comm.is_root:
             commits = self._ids("commits")
             p = os.path.join(self._ckpt, "state", str(commits[-1])) if commits else None
             if p and os.path.exists(p):
-                with open(p, "rb") as fh:
-                    st = pickle.load(fh)  # this engine's own checkpoint file
+                # tagged JSON (utils/jsonstate.py): a shared checkpoint directory can never run code
+                with open(p, encoding="utf-8") as fh:
+                    try:
+                        st = jsonstate.loads(fh.read())
+                    except (ValueError, UnicodeDecodeError) as e:
+                        raise ValueError(f"streaming state file {p} is not a state record of this engine "
+                                         f"(tagged JSON): {e}") from None
+                st = {int(k): v for k, v in st.items()}
         return comm.broadcast_object(st) or {}
 
     def _save_state(self, bid: int) -> None:
-        import pickle
+        from ..utils import jsonstate
         if not self._state or not self._session._comm.is_root:
             return
         d = os.path.join(self._ckpt, "state")
         os.makedirs(d, exist_ok=True)
         tmp = os.path.join(d, f"{bid}.tmp")
-        with open(tmp, "wb") as fh:
-            pickle.dump(self._state, fh)
+        with open(tmp, "w", encoding="utf-8") as fh:
+            fh.write(jsonstate.dumps(self._state))
+            fh.flush()
+            os.fsync(fh.fileno())
         os.replace(tmp, os.path.join(d, str(bid)))
         for old in self._ids("state"):
             if old < bid - 2:  # keep a short history (replays only ever need the last committed one)

@@ -1,0 +1,131 @@
+"""Device k-means|| initialisation (``kmeans_init.hip``) against torch / host references: the fused
+row pass (norms vs f64, bitwise equal between the fused and the norms-only launch; first costs,
+max norm, exponent range), the
+sampling and merge kernels, the local k-means kernels against their host twin (bit for bit), and a
+whole init on exactly-representable data equal to the CPU session's."""
+import numpy as np
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine, to_device_matrix
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import rng
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.mark.parametrize("n,d,fp8", [(100_003, 256, False), (7, 16, False), (65_537, 128, False),
+                                     (30_001, 512, False), (50_000, 256, True), (9_999, 512, True)])
+def test_row_pass_matches_norm_kernel(n, d, fp8):
+    g = torch.Generator(device="cuda").manual_seed(n)
+    xf = torch.randn(n, d, device="cuda", generator=g) * 3
+    xf[::7, 3] = 0.0
+    xf[5, 1] = 1e-30  # a tiny exponent
+    x = to_device_matrix(xf.to(torch.float8_e4m3fn) if fp8 else xf, d)
+    dp = x.shape[1]
+    ref = K.row_sqnorm(x, n, dp)  # norms-only launch of the same kernel
+    xd0 = (x.view(torch.uint8)[:, :d].view(torch.float8_e4m3fn) if fp8 else x[:, :d]).double()
+    torch.testing.assert_close(ref.double(), (xd0 * xd0).sum(1), rtol=2e-6, atol=1e-30)
+    xn = torch.empty(n, device="cuda")
+    c0 = torch.zeros(dp, device="cuda")
+    c0[:d] = xf[1].to(torch.bfloat16).float()
+    c0n = float((c0.double() ** 2).sum())
+    cost = torch.empty(n, device="cuda")
+    near = torch.full((n,), 5, dtype=torch.int32, device="cuda")
+    mx = torch.zeros(1, device="cuda")
+    er = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device="cuda")
+    K.row_pass(x, n, dp, xn, c0, c0n, cost, near, xn_max=mx, erange=er)
+    torch.cuda.synchronize()
+    assert torch.equal(xn, ref)
+    assert float(mx) == float(ref.max())
+    assert bool((near == 0).all())
+    xd = (x.view(torch.uint8)[:, :d].view(torch.float8_e4m3fn) if fp8 else x[:, :d]).double()
+    want = ((xd - c0[:d].double()) ** 2).sum(1)
+    torch.testing.assert_close(cost.double(), want, rtol=1e-5, atol=1e-5 * float(ref.max()))
+    if not fp8:
+        bits = x[:, :d].contiguous().view(torch.int16).to(torch.int32) & 0x7FFF
+        nz = bits[bits != 0]
+        e = (nz >> 7) & 0xFF
+        assert er.tolist() == [int(e.min()), int(e.max())]
+
+
+def test_init_sample_and_merge_match_torch():
+    n = 1_000_003
+    g = torch.Generator(device="cuda").manual_seed(3)
+    cost = torch.rand(n, device="cuda", generator=g) * 10
+    ids = torch.arange(17, 17 + n, device="cuda", dtype=torch.int64)
+    key = rng.key(42, 100)
+    scale = 2 * 256 / float(cost.double().sum())
+    out = torch.empty(n, dtype=torch.int32, device="cuda")
+    cnt = torch.zeros(1, dtype=torch.int32, device="cuda")
+    K.init_sample(cost, ids, n, key, scale, out, cnt)
+    m = int(cnt.item())
+    got = torch.sort(out[:m]).values.long().cpu()
+    u = rng.uniform(ids.cpu(), 42, 100)
+    want = torch.nonzero(u < scale * cost.cpu().double()).flatten()
+    assert torch.equal(got, want)
+    # capacity: the count is the total, only cap rows are written
+    small = torch.full((5,), -7, dtype=torch.int32, device="cuda")
+    cnt.zero_()
+    K.init_sample(cost, ids, n, key, scale, small, cnt)
+    assert int(cnt.item()) == m and bool((small >= 0).all())
+    near = torch.zeros(n, dtype=torch.int32, device="cuda")
+    best = torch.rand(n, device="cuda", generator=g) * 10
+    lab = torch.randint(0, 100, (n,), device="cuda", generator=g, dtype=torch.int32)
+    c2, n2 = cost.clone(), near.clone()
+    K.init_merge(c2, n2, best, lab, 1000, n)
+    better = best < cost
+    assert torch.equal(c2, torch.where(better, best, cost))
+    assert torch.equal(n2, torch.where(better, lab + 1000, near))
+
+
+@pytest.mark.parametrize("m,d,k,spherical", [(1025, 256, 256, False), (300, 7, 20, False), (50, 3, 49, False),
+                                             (2000, 64, 5, False), (600, 32, 40, True), (12, 5, 12, False)])
+def test_local_kmeans_device_equals_host_bitwise(m, d, k, spherical):
+    rs = np.random.RandomState(m + k)
+    pts = rs.randn(m, d) * 3 + rs.randint(0, 8, (m, 1))
+    pts[1] = pts[0]  # duplicate candidate
+    w = rs.randint(0, 50, m).astype(np.float64)
+    w[:3] = 0.0
+    if spherical:
+        pts /= np.linalg.norm(pts, axis=1, keepdims=True)
+    host = K.local_kmeans(torch.as_tensor(pts), torch.as_tensor(w), k, seed=9, spherical=spherical)
+    dev = K.local_kmeans(torch.as_tensor(pts, device="cuda"), torch.as_tensor(w, device="cuda"), k, seed=9,
+                         spherical=spherical)
+    assert np.array_equal(host.numpy(), dev.cpu().numpy())
+    assert np.isfinite(host.numpy()).all()
+
+
+def _integer_blobs(n, d, k, seed):
+    rs = np.random.RandomState(seed)
+    cen = rs.randint(0, 12, (k, d))
+    x = np.clip(cen[rs.randint(0, k, n)] + rs.randint(-1, 2, (n, d)), 0, 15)
+    return x.astype(np.float64)  # small integers: exact in bf16, every squared distance exact in f32
+
+
+@pytest.mark.parametrize("n,d,k", [(40_000, 16, 24), (20_011, 128, 64), (8_000, 256, 200)])
+def test_init_device_equals_cpu_on_exact_data(n, d, k):
+    """With exactly representable data every cost, sampling decision, candidate and weight is the same
+    on both sessions, and the local k-means is the same arithmetic: the init centres are bitwise equal."""
+    x = _integer_blobs(n, d, k, seed=d)
+    cpu = LloydEngine(torch.as_tensor(x), d, k).init_kmeans_parallel(seed=5)
+    gpu = LloydEngine(torch.as_tensor(x, device="cuda"), d, k).init_kmeans_parallel(seed=5)
+    assert np.array_equal(cpu, gpu)
+
+
+def test_init_then_fit_on_blobs_gpu():
+    """Engine path end to end: the fused first pass fills the norms; the fit recovers the blobs."""
+    n, d, k = 200_000, 256, 32
+    g = torch.Generator(device="cuda").manual_seed(1)
+    cen = torch.randn(k, d, device="cuda", generator=g) * 6
+    x = (cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randn(n, d, device="cuda", generator=g))
+    eng = LloydEngine(x.to(torch.bfloat16), d, k)
+    assert not eng._norms_ready
+    init = eng.init_kmeans_parallel(seed=3)
+    assert eng._norms_ready
+    torch.testing.assert_close(eng.xnorm[:n], K.row_sqnorm(eng.x, n, eng.dp)[:n], rtol=0, atol=0)
+    eng.set_centers(init)
+    eng.fit(20, 0.0)
+    got = eng.centers
+    dmin = torch.cdist(cen.double(), got).min(1).values
+    assert float(dmin.max()) < 0.5
