@@ -199,7 +199,8 @@ constexpr int kBlocks = 256;  // fixed block count of the weighted prefix sums (
 constexpr int kKppThreads = 1024;
 
 __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __restrict__ P,
-                                                                const double* __restrict__ PT, int m, int d,
+                                                                const double* __restrict__ PT,
+                                                                const double* __restrict__ D, int m, int d,
                                                                 const double* __restrict__ w, int k,
                                                                 unsigned long long key, double* __restrict__ C,
                                                                 double* __restrict__ CT, double* __restrict__ d2) {
@@ -262,16 +263,51 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
       CT[(long long)t * k + i] = v;
     }
     __syncthreads();
-    for (int q = tid; q < m; q += kKppThreads) {
-      double acc = 0.0;
-      for (int t = 0; t < d; ++t) {
-        const double e = __dsub_rn(PT[(long long)t * m + q], crow[t]);
-        acc = __fma_rn(e, e, acc);
+    if (D != nullptr) {  // precomputed pairwise distances: the update is one contiguous row read
+      const double* dr = D + (long long)pk * m;
+      for (int q = tid; q < m; q += kKppThreads) {
+        const double acc = dr[q];
+        d2[q] = (i == 0 || acc < d2[q]) ? acc : d2[q];
       }
-      d2[q] = (i == 0 || acc < d2[q]) ? acc : d2[q];
+    } else {
+      for (int q = tid; q < m; q += kKppThreads) {
+        double acc = 0.0;
+        for (int t = 0; t < d; ++t) {
+          const double e = __dsub_rn(PT[(long long)t * m + q], crow[t]);
+          acc = __fma_rn(e, e, acc);
+        }
+        d2[q] = (i == 0 || acc < d2[q]) ? acc : d2[q];
+      }
     }
     __syncthreads();
   }
+}
+
+// D[i][q] = dist(P_q, P_i) (the fold of the k-means++ update: e = P_q[t] - P_i[t], acc = fma(e, e,
+// acc)) for every candidate pair, 16 x 16 pairs per workgroup with both row blocks staged in LDS
+// in 64-dimension slices; each thread folds its pair over the dimensions in order.
+constexpr int kPairT = 16, kPairS = 64;
+__global__ __launch_bounds__(kThreads) void local_pairdist_kernel(const double* __restrict__ P, int m, int d,
+                                                                  double* __restrict__ D) {
+  __shared__ double ri[kPairT][kPairS + 1], rq[kPairT][kPairS + 1];
+  const int tid = threadIdx.x, ti = tid / kPairT, tq = tid % kPairT;
+  const int i0 = blockIdx.y * kPairT, q0 = blockIdx.x * kPairT;
+  double acc = 0.0;
+  for (int s0 = 0; s0 < d; s0 += kPairS) {
+    const int w = min(kPairS, d - s0);
+    for (int e = tid; e < kPairT * kPairS; e += kThreads) {
+      const int r = e / kPairS, t = e % kPairS;
+      ri[r][t] = (i0 + r < m && t < w) ? P[(long long)(i0 + r) * d + s0 + t] : 0.0;
+      rq[r][t] = (q0 + r < m && t < w) ? P[(long long)(q0 + r) * d + s0 + t] : 0.0;
+    }
+    __syncthreads();
+    for (int t = 0; t < w; ++t) {
+      const double e = __dsub_rn(rq[tq][t], ri[ti][t]);
+      acc = __fma_rn(e, e, acc);
+    }
+    __syncthreads();
+  }
+  if (i0 + ti < m && q0 + tq < m) D[(long long)(i0 + ti) * m + q0 + tq] = acc;
 }
 
 // labels[q] = argmin_j dist(P_q, C_j) (ties: lowest j); *moved = 1 if any label changed.
@@ -462,11 +498,17 @@ CML_API int cml_kmeans_init_sample(const float* cost, const long long* ids, long
 
 // P: f64 [m, d] candidates, PT: the same transposed [d, m], w: f64 [m]; C: f64 [k, d], CT: f64 [d, k],
 // d2: f64 [m] scratch.
+// D: f64 [m, m] scratch for the pairwise distances, or null (then each pick folds its distances from PT).
 CML_API int cml_local_kpp(const double* P, const double* PT, int m, int d, const double* w, int k,
-                          unsigned long long key, double* C, double* CT, double* d2, void* stream) {
+                          unsigned long long key, double* C, double* CT, double* d2, double* D, void* stream) {
   if (m <= 0 || d <= 0 || k <= 0 || (long long)d * 8 > 64 * 1024) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(local_kpp_kernel, dim3(1), dim3(kKppThreads), (size_t)d * 8, (hipStream_t)stream, P, PT, m, d,
-                     w, k, key, C, CT, d2);
+  hipStream_t st = (hipStream_t)stream;
+  if (D != nullptr) {
+    const unsigned g = (unsigned)((m + kPairT - 1) / kPairT);
+    hipLaunchKernelGGL(local_pairdist_kernel, dim3(g, g), dim3(kThreads), 0, st, P, m, d, D);
+  }
+  hipLaunchKernelGGL(local_kpp_kernel, dim3(1), dim3(kKppThreads), (size_t)d * 8, st, P, PT, D, m, d, w, k, key, C,
+                     CT, d2);
   return cml_status();
 }
 

@@ -526,13 +526,16 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
 
 // Centre tiles per compute wave for kc centres (kc <= 64·CT), or 0 when K9r does not apply
 // (D outside {128, 256, 512} — {256, 512} for fp8 rows —, or the centres do not fit 128 VGPRs per lane).
+// CT = 3 and 5 exist for bf16 Dp <= 256 (CT = 5 holds 160 VGPRs of centres at Dp = 256): a 320-centre
+// chunk is one pass where 256 + 64 took two (k-means|| candidate rounds of 2k = 512-640 centres).
 inline int plan_ct(int Dp, int kc, bool f8 = false) {
   if (Dp != 128 && Dp != 256 && Dp != 512) return 0;
   if (f8 && Dp < 256) return 0;
   const int ct = (kc + 63) / 64;
-  if (ct > 4) return 0;  // CT = 8 spills at 256 VGPRs
-  const int c = ct <= 1 ? 1 : (ct <= 2 ? 2 : 4);
-  if (c * (Dp / 32) > 32) return 0;
+  if (ct > 5) return 0;  // CT = 8 spills at 256 VGPRs
+  const int c = ct <= 2 ? (ct < 1 ? 1 : ct) : (Dp <= 256 ? ct : 4);
+  if (ct > 4 && (Dp > 256 || f8)) return 0;  // fp8 CT = 5 spills (the widening needs registers)
+  if (c * (Dp / 32) > 40) return 0;
   return c;
 }
 
@@ -589,10 +592,10 @@ inline int dispatch_mode(int Dp, int ct, bool f8, const void* X, long long n, lo
   if (Dp == D && ct == T && f8 == F)                                                                               \
   return launch<D, T, F, MODE>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, \
                                ext, grid, dbg, st)
-  CML_RR(128, 1, false); CML_RR(128, 2, false); CML_RR(128, 4, false);
-  CML_RR(256, 1, false); CML_RR(256, 2, false); CML_RR(256, 4, false);
+  CML_RR(128, 1, false); CML_RR(128, 2, false); CML_RR(128, 3, false); CML_RR(128, 4, false); CML_RR(128, 5, false);
+  CML_RR(256, 1, false); CML_RR(256, 2, false); CML_RR(256, 3, false); CML_RR(256, 4, false); CML_RR(256, 5, false);
   CML_RR(512, 1, false); CML_RR(512, 2, false);
-  CML_RR(256, 1, true); CML_RR(256, 2, true); CML_RR(256, 4, true);
+  CML_RR(256, 1, true); CML_RR(256, 2, true); CML_RR(256, 3, true); CML_RR(256, 4, true);
   CML_RR(512, 1, true); CML_RR(512, 2, true);
 #undef CML_RR
   return (int)hipErrorInvalidValue;

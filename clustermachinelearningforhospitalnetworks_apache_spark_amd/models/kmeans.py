@@ -965,9 +965,9 @@ class LloydEngine:
             return
         lab = torch.zeros(n, dtype=torch.int32, device=dev)
         best = torch.empty(n, dtype=torch.float32, device=dev)
-        step = 256
-        for c0 in range(0, new.shape[0], step):
-            ch = new[c0:c0 + step].to(torch.float64).contiguous()
+        c0 = 0
+        for size in self._candidate_chunks(new.shape[0]):
+            ch = new[c0:c0 + size].to(torch.float64).contiguous()
             kc = ch.shape[0]
             kp = round_up(kc, 32)
             cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
@@ -976,6 +976,33 @@ class LloydEngine:
             plan = K.plan_assign(n, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
             K.assign_bf16(self.x, n, dp, cb, cn, plan, lab, best, None, xnorm=self.xnorm)
             K.init_merge(costs, nearest, best, lab, off + c0, n)
+            c0 += size
+
+    # Time of one K9r pass over 20M x 256 bf16 rows by centre tiles per compute wave (64 centres each),
+    # ms, measured on MI355X (profiles/r3/mb_rr_modes.log): CT <= 2 is HBM-bound, then the MFMA work
+    # grows with CT (under the power-limited clock, not linearly).
+    _CT_COST = {1: 1.72, 2: 1.78, 3: 2.06, 4: 2.45, 5: 2.78}
+
+    def _candidate_chunks(self, m: int) -> list:
+        """Split m candidate centres into K9r launches (multiples of 64, at most 256 — 320 where CT = 5
+        exists) minimising the summed pass cost: 520 candidates run as 256 + 264 (two passes, ~27.5)
+        rather than 256 + 256 + 8 (three, ~34)."""
+        big = 320 if (K.plan_assign(1, self.dp, 320, fp8=K.is_fp8(self.x)).rr_ct == 5) else 256
+        units = -(-m // 64)
+        best = [0.0] + [math.inf] * units  # best[u]: cheapest cover of u units of 64
+        pick = [0] * (units + 1)
+        for u in range(1, units + 1):
+            for c in range(1, big // 64 + 1):
+                v = best[max(0, u - c)] + self._CT_COST.get(c, 20.0)
+                if v < best[u]:
+                    best[u], pick[u] = v, c
+        sizes, u = [], units
+        while u > 0:
+            sizes.append(pick[u] * 64)
+            u = max(0, u - pick[u])
+        sizes.sort(reverse=True)
+        sizes[-1] -= sum(sizes) - m  # the last chunk takes the remainder
+        return [s for s in sizes if s > 0]
 
 
 def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: Optional[torch.Tensor] = None):

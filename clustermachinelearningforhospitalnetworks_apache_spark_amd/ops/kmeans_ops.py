@@ -69,7 +69,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
                                        c_vp]),
-    "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp]),
+    "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
+                              c_vp]),
     "cml_local_assign": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
     "cml_local_update": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_local_empty": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -146,8 +147,12 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         picks = torch.zeros(2 * k, dtype=torch.int32, device=dev)
         PT = pts.t().contiguous()
+        # pairwise candidate distances up front (one parallel pass) when they fit 1 GiB: each pick is
+        # then a row read instead of m dimension folds on the one seeding workgroup
+        D = torch.empty((m, m), dtype=torch.float64, device=dev) if m * m * 8 <= (1 << 30) else None
         _native.check(lib.cml_local_kpp(pts.data_ptr(), PT.data_ptr(), m, d, w.data_ptr(), int(k), _u64(key_pp),
-                                        C.data_ptr(), CT.data_ptr(), d2.data_ptr(), st), "local_kpp")
+                                        C.data_ptr(), CT.data_ptr(), d2.data_ptr(), _ptr(D), st), "local_kpp")
+        del D
         for _ in range(max_iter):
             moved.zero_()
             _native.check(lib.cml_local_assign(pts.data_ptr(), m, d, CT.data_ptr(), int(k), lab.data_ptr(),

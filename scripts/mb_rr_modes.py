@@ -82,3 +82,15 @@ for frac in (0.02, 0.05, 0.2):
                                         lab_in=cl))
     print(f"K9r mode 2, {100 * frac:4.1f} % rows     {t2:8.3f} ms  ({m * dp * 2 / t2 / 1e9:5.2f} TB/s of candidate rows;"
           f" full-pass share {t2 / t0:.3f})")
+
+# centre tiles per wave: the k-means|| candidate chunk sizes
+for kk in (64, 128, 192, 256, 320):
+    kpp_ = -(-kk // 32) * 32
+    cbk = torch.zeros((kpp_, dp), dtype=torch.bfloat16, device="cuda")
+    cnk = torch.zeros(kpp_, device="cuda")
+    cen2 = torch.randn(kk, d, device="cuda", generator=g).double() * 4
+    K.update_centers(None, kk, d, cen2.clone(), cbk, dp, kpp_, cnk, None)
+    pl = K.plan_assign(n, dp, kk)
+    bst = torch.empty(n, device="cuda")
+    t = timeit(lambda: K.assign_bf16(x, n, dp, cbk, cnk, pl, lab, bst, None, xnorm=xn))
+    print(f"K9r mode 0, k={kk:3d} (CT={pl.rr_ct})     {t:8.3f} ms")
