@@ -1,0 +1,190 @@
+// Source-precision KMeans kernels: the f64 reference algorithm on device-resident f32/f64 features.
+//
+// The reference's feature vectors are DoubleType/IntegerType columns assembled into f64 vectors
+// (ref.py:64-72, ref.py:134-136) and Spark's KMeans works in f64. The bf16 MFMA path rounds rows to
+// 8 mantissa bits (a hospital occupancy of 387 becomes 388), so for f32/f64 input the engine runs
+// these kernels instead (models/kmeans.py, precision "exact"; cml.ml.kmeans.precision = bf16 opts
+// into the fast path):
+//
+//   exact_assign   label/distance of every row against f64 centres: one thread per row, centres
+//                  staged in LDS tiles, distances as a dimension-ordered fold of (x_t - c_t)² in f64,
+//                  ties to the lowest centre index;
+//   exact_segsum   per-cluster f64 sums of the rows in label-sorted order (a stable sort of the
+//                  labels): fixed 1024-position chunks summed sequentially, chunk partials of the
+//                  clusters crossing a chunk edge combined in chunk order — deterministic, no atomics.
+#include "common.h"
+
+namespace {
+
+constexpr int kThreads = 256;
+constexpr int kChunk = 1024;  // sorted positions per segmented-sum chunk
+
+template <typename T, int DREG>
+__global__ __launch_bounds__(kThreads) void exact_assign_kernel(const T* __restrict__ X, long long n, long long ldx,
+                                                                int d, const double* __restrict__ C, int k, int kt,
+                                                                int* __restrict__ labels, double* __restrict__ best,
+                                                                int* __restrict__ changed) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* ct = reinterpret_cast<double*>(smem);  // [kt][d]
+  const long long r = (long long)blockIdx.x * kThreads + threadIdx.x;
+  const bool live = r < n;
+  double xr[DREG > 0 ? DREG : 1];
+  if constexpr (DREG > 0) {
+#pragma unroll
+    for (int t = 0; t < DREG; ++t) xr[t] = (live && t < d) ? (double)X[r * ldx + t] : 0.0;
+  }
+  double bd = __builtin_huge_val();
+  int bi = 0;
+  for (int c0 = 0; c0 < k; c0 += kt) {
+    const int kc = min(kt, k - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < kc * d; e += kThreads) ct[e] = C[(long long)c0 * d + e];
+    __syncthreads();
+    if (live) {
+      for (int j = 0; j < kc; ++j) {
+        const double* cj = ct + (long long)j * d;
+        double acc = 0.0;
+        if constexpr (DREG > 0) {
+#pragma unroll
+          for (int t = 0; t < DREG; ++t) {
+            if (t < d) {
+              const double e = xr[t] - cj[t];
+              acc = __fma_rn(e, e, acc);
+            }
+          }
+        } else {
+          for (int t = 0; t < d; ++t) {
+            const double e = (double)X[r * ldx + t] - cj[t];
+            acc = __fma_rn(e, e, acc);
+          }
+        }
+        if (acc < bd) {  // centres ascending: strict < keeps the lowest index
+          bd = acc;
+          bi = c0 + j;
+        }
+      }
+    }
+  }
+  if (live) {
+    if (changed != nullptr && labels[r] != bi) atomicAdd(changed, 1);
+    labels[r] = bi;
+    best[r] = bd;
+  }
+}
+
+// seg[c] = first sorted position of cluster c (seg[k] = n); perm[p] = row at sorted position p.
+// Chunk ch covers positions [ch*kChunk, ...): clusters strictly inside it are stored complete into S;
+// the cluster open at its start goes to slot 2ch, the one open at its end (if another) to 2ch+1.
+template <typename T>
+__global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restrict__ X, long long ldx, int d,
+                                                               const int* __restrict__ perm,
+                                                               const int* __restrict__ seg, int k, long long n,
+                                                               double* __restrict__ S, double* __restrict__ slots,
+                                                               int* __restrict__ slot_c) {
+  const long long ch = blockIdx.x;
+  const int col = blockIdx.y * 64 + threadIdx.x;
+  const long long p0 = ch * kChunk, p1 = min(n, p0 + kChunk);
+  int lo = 0, hi = k;  // seg[lo] <= p0 < seg[hi]
+  while (hi - lo > 1) {
+    const int mid = (lo + hi) >> 1;
+    if (seg[mid] <= p0) lo = mid; else hi = mid;
+  }
+  int c = lo;
+  while (seg[c + 1] <= p0) ++c;  // skip empty clusters
+  const int ca = c;
+  double acc = 0.0;
+  long long next = seg[c + 1];
+  for (long long p = p0; p < p1; ++p) {
+    while (p >= next) {  // cluster c ended: first one -> slot A, a middle one is complete
+      if (col < d) {
+        if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
+        else S[(long long)c * d + col] = acc;
+      }
+      acc = 0.0;
+      ++c;
+      next = seg[c + 1];
+    }
+    if (col < d) acc += (double)X[(long long)perm[p] * ldx + col];
+  }
+  if (col < d) {
+    if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
+    else slots[(2 * ch + 1) * (long long)d + col] = acc;
+  }
+  if (blockIdx.y == 0 && threadIdx.x == 0) {
+    slot_c[2 * ch] = ca;
+    slot_c[2 * ch + 1] = c == ca ? -1 : c;
+  }
+}
+
+// S[c] for the clusters that touch a chunk edge: the slot partials in chunk order (A before B).
+__global__ __launch_bounds__(kThreads) void exact_seg_fix_kernel(const int* __restrict__ seg, int k, int d,
+                                                                 double* __restrict__ S,
+                                                                 const double* __restrict__ slots,
+                                                                 const int* __restrict__ slot_c) {
+  const int c = blockIdx.x;
+  const long long s0 = seg[c], s1 = seg[c + 1];
+  if (s1 <= s0) {
+    for (int t = threadIdx.x; t < d; t += kThreads) S[(long long)c * d + t] = 0.0;
+    return;
+  }
+  const long long ch0 = s0 / kChunk, ch1 = (s1 - 1) / kChunk;
+  bool edge = false;
+  for (long long ch = ch0; ch <= ch1; ++ch) edge |= slot_c[2 * ch] == c || slot_c[2 * ch + 1] == c;
+  if (!edge) return;  // complete inside one chunk: stored by the partial kernel
+  for (int t = threadIdx.x; t < d; t += kThreads) {
+    double s = 0.0;
+    for (long long ch = ch0; ch <= ch1; ++ch) {
+      if (slot_c[2 * ch] == c) s += slots[(2 * ch) * (long long)d + t];
+      if (slot_c[2 * ch + 1] == c) s += slots[(2 * ch + 1) * (long long)d + t];
+    }
+    S[(long long)c * d + t] = s;
+  }
+}
+
+}  // namespace
+
+// X: f64 (xf64 = 1) or f32 rows [n, ldx elements]; C: f64 [k, d]; labels (int32, read for the change
+// count when `changed` is given) and best (f64) [n].
+CML_API int cml_kmeans_exact_assign(const void* X, int xf64, long long n, long long ldx, int d, const double* C,
+                                    int k, int* labels, double* best, int* changed, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  const int kt = max(1, min(k, 8192 / d));  // centres per LDS tile (<= 64 KiB)
+  const size_t lds = (size_t)kt * d * sizeof(double);
+  const dim3 g((unsigned)((n + kThreads - 1) / kThreads));
+  hipStream_t st = (hipStream_t)stream;
+#define CML_EA(T, R)                                                                                        \
+  hipLaunchKernelGGL((exact_assign_kernel<T, R>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, k, kt, \
+                     labels, best, changed)
+  if (xf64) {
+    if (d <= 4) CML_EA(double, 4);
+    else if (d <= 16) CML_EA(double, 16);
+    else CML_EA(double, 0);
+  } else {
+    if (d <= 4) CML_EA(float, 4);
+    else if (d <= 16) CML_EA(float, 16);
+    else CML_EA(float, 0);
+  }
+#undef CML_EA
+  return cml_status();
+}
+
+// Slot scratch: slots f64 [2 * nchunks * d], slot_c int [2 * nchunks], nchunks = ceil(n / 1024).
+CML_API long long cml_kmeans_exact_chunks(long long n) { return (n + kChunk - 1) / kChunk; }
+
+CML_API int cml_kmeans_exact_segsum(const void* X, int xf64, long long ldx, int d, const int* perm, const int* seg,
+                                    int k, long long n, double* S, double* slots, int* slot_c, void* stream) {
+  if (d <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (n > 0) {
+    const dim3 g((unsigned)((n + kChunk - 1) / kChunk), (unsigned)((d + 63) / 64));
+    if (xf64)
+      hipLaunchKernelGGL((exact_seg_partial_kernel<double>), g, dim3(64), 0, st, (const double*)X, ldx, d, perm, seg,
+                         k, n, S, slots, slot_c);
+    else
+      hipLaunchKernelGGL((exact_seg_partial_kernel<float>), g, dim3(64), 0, st, (const float*)X, ldx, d, perm, seg,
+                         k, n, S, slots, slot_c);
+  }
+  hipLaunchKernelGGL(exact_seg_fix_kernel, dim3(k), dim3(kThreads), 0, st, seg, k, d, S, slots, slot_c);
+  return cml_status();
+}

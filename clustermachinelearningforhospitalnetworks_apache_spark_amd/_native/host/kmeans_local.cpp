@@ -7,9 +7,11 @@
 // blocks; weighted sums as fma folds in point order; a division for 1 / Σw then a product; IEEE
 // correctly-rounded operations everywhere (this file is built with -ffp-contract=off, and std::fma /
 // std::sqrt are correctly rounded), so both produce the same bits.
+#include <algorithm>
 #include <cmath>
 #include <cstdint>
 #include <cstring>
+#include <thread>
 #include <vector>
 
 #define CML_HOST_API extern "C" __attribute__((visibility("default")))
@@ -145,4 +147,74 @@ CML_HOST_API int cml_local_kmeans_host(const double* P, int m, int d, const doub
     }
   }
   return it;
+}
+
+// ---- host twins of csrc/kmeans_exact.hip (the CPU session's KMeans assignment and sums) ----------
+// exact_assign: dimension-ordered fold of fma(x_t - c_t, x_t - c_t, acc), ties to the lowest index —
+// the device kernel's arithmetic, so CPU and GPU sessions label rows identically. Rows are split over
+// `threads` std::threads (each row's result does not depend on the split).
+CML_HOST_API int cml_exact_assign_host(const double* X, long long n, long long ldx, int d, const double* C, int k,
+                                       long long* labels, double* best, int threads) {
+  if (n < 0 || d <= 0 || k <= 0) return -1;
+  auto work = [&](long long r0, long long r1) {
+    for (long long r = r0; r < r1; ++r) {
+      const double* x = X + r * ldx;
+      double bd = HUGE_VAL;
+      int bi = 0;
+      for (int j = 0; j < k; ++j) {
+        const double* c = C + (long long)j * d;
+        double acc = 0.0;
+        for (int t = 0; t < d; ++t) {
+          const double e = x[t] - c[t];
+          acc = std::fma(e, e, acc);
+        }
+        if (acc < bd) { bd = acc; bi = j; }
+      }
+      labels[r] = bi;
+      best[r] = bd;
+    }
+  };
+  threads = std::max(1, std::min(threads, (int)std::max(1LL, n / 4096)));
+  std::vector<std::thread> ts;
+  const long long per = (n + threads - 1) / threads;
+  for (int i = 1; i < threads; ++i) ts.emplace_back(work, std::min(n, i * per), std::min(n, (i + 1) * per));
+  work(0, std::min(n, per));
+  for (auto& t : ts) t.join();
+  return 0;
+}
+
+// exact_sums: per-cluster sums in the device kernel's order — rows of cluster c in ascending row
+// order occupy sorted positions [seg[c], seg[c+1]); the positions are cut into 1024-position chunks,
+// each chunk's run of the cluster is folded from 0, and the runs are added in chunk order.
+CML_HOST_API int cml_exact_sums_host(const double* X, long long n, long long ldx, int d, const long long* labels,
+                                     int k, double* S, double* counts) {
+  if (n < 0 || d <= 0 || k <= 0) return -1;
+  constexpr long long kChunk = 1024;
+  std::vector<long long> cnt(k, 0), seg(k + 1, 0);
+  for (long long r = 0; r < n; ++r) {
+    if (labels[r] < 0 || labels[r] >= k) return -2;
+    ++cnt[labels[r]];
+  }
+  for (int c = 0; c < k; ++c) seg[c + 1] = seg[c] + cnt[c];
+  std::vector<std::vector<long long>> rows(k);
+  for (int c = 0; c < k; ++c) rows[c].reserve(cnt[c]);
+  for (long long r = 0; r < n; ++r) rows[labels[r]].push_back(r);
+  std::vector<double> part(d);
+  for (int c = 0; c < k; ++c) {
+    double* s = S + (long long)c * d;
+    for (int t = 0; t < d; ++t) s[t] = 0.0;
+    counts[c] = (double)cnt[c];
+    long long i = 0;
+    while (i < cnt[c]) {
+      const long long ch = (seg[c] + i) / kChunk;
+      const long long end = std::min(cnt[c], (ch + 1) * kChunk - seg[c]);
+      for (int t = 0; t < d; ++t) part[t] = 0.0;
+      for (; i < end; ++i) {
+        const double* x = X + rows[c][i] * ldx;
+        for (int t = 0; t < d; ++t) part[t] = part[t] + x[t];
+      }
+      for (int t = 0; t < d; ++t) s[t] = s[t] + part[t];
+    }
+  }
+  return 0;
 }

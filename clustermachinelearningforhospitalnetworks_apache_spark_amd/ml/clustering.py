@@ -3,9 +3,15 @@ SURVEY.md §0.3) on the distributed Lloyd engine of ``models/kmeans.py``.
 
 Spark defaults: k=2, maxIter=20, tol=1e-4, initMode="k-means||", initSteps=2,
 distanceMeasure="euclidean", seed = Java hashCode of the class name.
-On GPU ranks the assignment runs on the bf16 MFMA kernel (K9) — centres are kept
-in float64, sums are exact-f64 (K10), so only near-ties between two centres can
-differ from a float64 evaluation.
+Precision (session conf ``cml.ml.kmeans.precision``, default "auto"): f32/f64 feature
+vectors — the reference's assembled DoubleType/IntegerType columns (ref.py:64-72,
+ref.py:134-136), and this engine's default ``cml.ml.features.dtype`` — run the f64
+reference algorithm on the device (``kmeans_exact.hip``: f64 distances, deterministic
+f64 sums of the rows as given), so GPU fits agree with the CPU f64 fit
+(tests/test_kmeans_exact_gpu.py). bf16 / fp8 feature vectors (or ``precision=bf16``)
+run the MFMA path: distances of the bf16-rounded rows and centres, exact f64 sums of
+those rounded rows — values outside bf16's 8 mantissa bits are rounded first (an
+occupancy of 387 becomes 388).
 """
 from __future__ import annotations
 
@@ -70,7 +76,9 @@ class KMeans(Estimator):
         # exact bound-pruned Lloyd steps (models/kmeans.py _step_prune): same centres, fewer rows read
         pv = conf.get("cml.ml.kmeans.prune", None)
         prune = None if pv is None else str(pv).lower() in ("1", "true")
-        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
+        precision = conf.get("cml.ml.kmeans.precision", "auto")
+        eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
+                          precision=precision)
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
@@ -89,7 +97,8 @@ class KMeans(Estimator):
             start, arrs = resumed
             init = arrs["centers"]
             if init.shape[0] < k:
-                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
+                eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
+                                  precision=precision)
         elif self.getInitMode() == "random":
             with trace("kmeans.init"):
                 init = eng.init_random(seed)
@@ -99,7 +108,8 @@ class KMeans(Estimator):
             k_eff = getattr(eng, "k_effective", k)
             if k_eff < k:
                 init = init[:k_eff]
-                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical, prune=prune)
+                eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
+                                  precision=precision)
         eng.set_centers(init)
 
         def on_iter(it):
@@ -168,7 +178,8 @@ class KMeansModel(Model):
         x = df._feature_matrix(self.getFeaturesCol())
         c = torch.as_tensor(self._centers, device=x.device)
         cos = self._cosine()
-        if x.is_cuda:
+        prec = df._session.conf.get("cml.ml.kmeans.precision", "auto").lower()
+        if x.is_cuda and (prec == "bf16" or x.dtype not in (torch.float32, torch.float64)):
             from ..models.kmeans import assign_gpu, to_device_matrix, unit_rows
             xm = to_device_matrix(unit_rows(x) if cos else x, x.shape[1])
             lab, dist = assign_gpu(xm, xm.shape[1], x.shape[1], c)

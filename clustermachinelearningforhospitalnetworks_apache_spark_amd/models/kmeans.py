@@ -75,13 +75,16 @@ def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
     return out
 
 
-def unit_rows(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
-    """Rows scaled to unit length (cosine KMeans). Computed in f32 chunks on the rows' device; bf16 on
-    the GPU (fp8 inputs widen to bf16: unit components need more than e4m3's 3 mantissa bits), f64 on
-    the CPU. Spark rejects zero-length vectors for the cosine measure, and so does this."""
+def unit_rows(x: torch.Tensor, d: Optional[int] = None, exact: Optional[bool] = None) -> torch.Tensor:
+    """Rows scaled to unit length (cosine KMeans). bf16 on the GPU's MFMA path (computed in f32; fp8
+    inputs widen to bf16: unit components need more than e4m3's 3 mantissa bits), f64 on the CPU and
+    on the GPU's source-precision path (``exact``, default: f32/f64 input). Spark rejects zero-length
+    vectors for the cosine measure, and so does this."""
     d = x.shape[1] if d is None else d
-    out_dtype = torch.bfloat16 if x.is_cuda else torch.float64
-    work = torch.float32 if x.is_cuda else torch.float64
+    if exact is None:
+        exact = (not x.is_cuda) or x.dtype in (torch.float32, torch.float64)
+    out_dtype = torch.float64 if exact else torch.bfloat16
+    work = torch.float64 if exact else torch.float32
     out = torch.empty((x.shape[0], d), dtype=out_dtype, device=x.device)
     step = 1 << 22
     for s in range(0, x.shape[0], step):
@@ -117,8 +120,25 @@ class LloydEngine:
     def __init__(self, x: torch.Tensor, d: int, k: int, comm: Optional[Communicator] = None,
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
-                 incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None):
+                 incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None,
+                 precision: Optional[str] = None):
         self.comm = comm or local_comm()
+        # precision (cml.ml.kmeans.precision): "bf16" = the MFMA path (bf16 rows in the distance GEMM,
+        # exact f64 sums of those rows); "exact" = the f64 reference algorithm on the rows as given
+        # (kmeans_exact.hip on the GPU); "auto" = exact for f32/f64 device rows — the reference's f64
+        # feature vectors (ref.py:134-136) are not silently rounded to 8 mantissa bits — and the MFMA
+        # path for bf16 / fp8 rows.
+        precision = (precision or os.environ.get("CML_KMEANS_PRECISION") or "auto").lower()
+        if precision not in ("auto", "bf16", "exact"):
+            raise ValueError(f"KMeans precision must be 'auto', 'bf16' or 'exact', got {precision!r}")
+        if precision == "auto":
+            precision = "exact" if (not x.is_cuda or x.dtype in (torch.float32, torch.float64)) else "bf16"
+        if precision == "exact" and x.is_cuda and x.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"precision 'exact' needs f32/f64 rows, got {x.dtype}")
+        self.precision = precision
+        exact_dev = x.is_cuda and precision == "exact"
+        if exact_dev:
+            prune = False  # the reference algorithm (the torch bounds form would need host syncs anyway)
         if prune is None:  # default on GPU rows: exact pruned steps (CML_KMEANS_PRUNE=0 turns them off)
             env = os.environ.get("CML_KMEANS_PRUNE")
             prune = (env != "0") if env is not None else x.is_cuda
@@ -133,7 +153,7 @@ class LloydEngine:
         # costs and the convergence test are converted back (cost / 2, shift² <= 2·tol).
         self.spherical = bool(spherical)
         if self.spherical:
-            x = unit_rows(x, d)
+            x = unit_rows(x, d, exact=(precision == "exact"))
         self._accum_mode = accum_mode
         self._incremental = True if incremental is None else bool(incremental)
         # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
@@ -146,7 +166,9 @@ class LloydEngine:
         self._graph = None
         self.k = int(k)
         self.d = int(d)
-        self.gpu = x.is_cuda
+        # the MFMA kernels run only on the bf16 path; the exact path runs the reference algorithm (the
+        # torch f64 ops, with the f64 HIP kernels for assignment and sums) on the rows' device
+        self.gpu = x.is_cuda and precision == "bf16"
         self.n = int(x.shape[0])
         self.device = x.device
         if self.gpu:
@@ -192,9 +214,9 @@ class LloydEngine:
         # first pass over X
         ent = getattr(self.x, "_cml_xnorm", None)
         if ent is not None and ent[0] == self.x._version and ent[1] == (n, dp):
-            self.xnorm, self._norms_ready = ent[2], True
+            self._xnorm, self._norms_ready = ent[2], True
         else:
-            self.xnorm, self._norms_ready = torch.empty(max(n, 1), dtype=torch.float32, device=dev), False
+            self._xnorm, self._norms_ready = torch.empty(max(n, 1), dtype=torch.float32, device=dev), False
         self._erange = None  # bf16 exponent range of X (exactness of the f64 sums), from the row pass
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
@@ -229,7 +251,7 @@ class LloydEngine:
         """Device max ||x||² over every rank (pruning slack), from the cached norms."""
         st = self._pst
         if self.n:
-            st.mx.copy_(self.xnorm[: self.n].max().reshape(1))
+            st.mx.copy_(self._xnorm[: self.n].max().reshape(1))
         else:
             st.mx.zero_()
         if self.comm.is_distributed:
@@ -244,18 +266,25 @@ class LloydEngine:
         if mxv is not None:
             mxv.zero_()
         if n:
-            K.row_pass(self.x, n, dp, self.xnorm, c0, c0n, cost, near, xn_max=mxv, erange=self._erange)
+            K.row_pass(self.x, n, dp, self._xnorm, c0, c0n, cost, near, xn_max=mxv, erange=self._erange)
         if mxv is not None and self.comm.is_distributed:
             self.comm.allreduce_(mxv, op="max")
         self._norms_ready = True
         try:
-            self.x._cml_xnorm = (self.x._version, (n, dp), self.xnorm)
+            self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm)
         except (AttributeError, RuntimeError):
             pass
 
     def _ensure_norms(self) -> None:
         if self.gpu and not self._norms_ready:
             self._row_pass()
+
+    @property
+    def xnorm(self) -> torch.Tensor:
+        """||x||² of the device rows (f32), computed on first use unless the k-means|| init's first
+        pass over X already produced them."""
+        self._ensure_norms()
+        return self._xnorm
 
     @property
     def global_n(self) -> int:

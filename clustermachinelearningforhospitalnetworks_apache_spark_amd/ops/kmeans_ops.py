@@ -75,9 +75,16 @@ _native.register_kernel_sigs({
     "cml_local_update": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_local_empty": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
 })
+_native.register_kernel_sigs({
+    "cml_kmeans_exact_assign": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_exact_chunks": (c_ll, [c_ll]),
+    "cml_kmeans_exact_segsum": (c_int, [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
+})
 _native.register_host_sigs({
     "cml_local_kmeans_host": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, ctypes.c_uint64, c_int,
                                       c_int, c_vp]),
+    "cml_exact_assign_host": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_int]),
+    "cml_exact_sums_host": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp]),
 })
 
 
@@ -582,8 +589,74 @@ def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor
 # CPU reference implementations (torch, float64) — identical semantics, used by local[n] mode.
 # ----------------------------------------------------------------------------------------------
 
+def exact_assign(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor | None = None,
+                 changed: torch.Tensor | None = None, stream=None):
+    """(labels int32, squared distance f64) of device f32/f64 rows against f64 centres in f64
+    (``kmeans_exact.hip``): the source-precision assignment (ties: lowest centre index)."""
+    n, d = int(x.shape[0]), int(centers.shape[1])
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    c = centers.to(device=x.device, dtype=torch.float64).contiguous()
+    lab = labels if labels is not None else torch.zeros(max(n, 1), dtype=torch.int32, device=x.device)
+    best = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
+    _native.check(_native.kernels().cml_kmeans_exact_assign(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), int(c.shape[0]),
+        lab.data_ptr(), best.data_ptr(), _ptr(changed), _native.stream_ptr(stream)), "kmeans_exact_assign")
+    return lab[:n], best[:n]
+
+
+def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = None, stream=None):
+    """Deterministic per-cluster f64 sums [k, d] and counts [k] of device f32/f64 rows: a stable sort
+    of the labels, then fixed-chunk sequential sums combined in chunk order (no atomics)."""
+    n = int(labels.shape[0])
+    d = int(x.shape[1]) if d is None else d
+    if x.dtype not in (torch.float32, torch.float64):
+        x = x.to(torch.float64)
+    lab = labels[:n].long()
+    counts = torch.bincount(lab, minlength=k)[:k] if n else torch.zeros(k, dtype=torch.int64, device=x.device)
+    seg = torch.zeros(k + 1, dtype=torch.int32, device=x.device)
+    seg[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    perm = torch.sort(lab, stable=True).indices.to(torch.int32) if n else torch.zeros(1, dtype=torch.int32,
+                                                                                         device=x.device)
+    lib = _native.kernels()
+    nch = max(1, int(lib.cml_kmeans_exact_chunks(n)))
+    slots = torch.empty(2 * nch * d, dtype=torch.float64, device=x.device)
+    slot_c = torch.full((2 * nch,), -1, dtype=torch.int32, device=x.device)
+    S = torch.zeros((k, d), dtype=torch.float64, device=x.device)
+    _native.check(lib.cml_kmeans_exact_segsum(x.data_ptr(), int(x.dtype == torch.float64), x.stride(0), d,
+                                              perm.data_ptr(), seg.data_ptr(), int(k), n, S.data_ptr(),
+                                              slots.data_ptr(), slot_c.data_ptr(), _native.stream_ptr(stream)),
+                  "kmeans_exact_segsum")
+    return S, counts.to(torch.float64)
+
+
 def assign_reference(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 16):
-    """Return (labels int64, min squared distance f64) with first-index tie breaking."""
+    """Return (labels int64, min squared distance f64) with first-index tie breaking. Device f32/f64
+    rows run the f64 kernel (exact_assign); host rows the torch f64 form."""
+    if x.is_cuda:
+        lab, best = exact_assign(x, centers)
+        return lab.long(), best
+    # host twin of the device kernel (same fold, same ties): CPU and GPU sessions label rows alike
+    x = x.to(torch.float64)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    c = centers.to(torch.float64).contiguous()
+    n = int(x.shape[0])
+    labels = torch.empty(n, dtype=torch.int64)
+    best = torch.empty(n, dtype=torch.float64)
+    if n:
+        r = _native.host().cml_exact_assign_host(x.data_ptr(), n, x.stride(0), int(c.shape[1]), c.data_ptr(),
+                                                 int(c.shape[0]), labels.data_ptr(), best.data_ptr(),
+                                                 max(1, torch.get_num_threads()))
+        if r != 0:
+            raise ValueError("assign_reference: invalid shapes")
+    return labels, best
+
+
+def _assign_reference_blas(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 16):
+    """The BLAS (expansion) form of the f64 assignment, kept as a cross-check of the fold kernels."""
     x = x.to(torch.float64)
     c = centers.to(torch.float64)
     cn = (c * c).sum(1)
@@ -599,6 +672,23 @@ def assign_reference(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 1
 
 
 def sums_reference(x: torch.Tensor, labels: torch.Tensor, k: int):
+    if x.is_cuda:
+        return exact_sums(x, labels, k)
+    x = x.to(torch.float64)
+    if x.stride(-1) != 1:
+        x = x.contiguous()
+    n, d = int(x.shape[0]), int(x.shape[1])
+    lab = labels.to(torch.int64).contiguous()
+    S = torch.empty((k, d), dtype=torch.float64)
+    cnt = torch.empty(k, dtype=torch.float64)
+    r = _native.host().cml_exact_sums_host(x.data_ptr(), n, x.stride(0), d, lab.data_ptr(), int(k), S.data_ptr(),
+                                           cnt.data_ptr())
+    if r != 0:
+        raise ValueError("sums_reference: labels outside [0, k)")
+    return S, cnt
+
+
+def _sums_reference_torch(x: torch.Tensor, labels: torch.Tensor, k: int):
     x = x.to(torch.float64)
     sums = torch.zeros(k, x.shape[1], dtype=torch.float64, device=x.device)
     sums.index_add_(0, labels, x)

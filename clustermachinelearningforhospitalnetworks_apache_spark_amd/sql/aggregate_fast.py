@@ -83,7 +83,7 @@ def device_aggregate(df, keys, exprs):
     fid = fid_of_code[code]                        # final group of every entry
     G = card
     first_entry = firstpos[order]                  # entry holding each final group's key
-    mine = torch.arange(me, G, W, device=dev)      # round-robin placement
+    mine = torch.arange(me, max(G, me), W, device=dev)  # round-robin placement (none when me >= G)
     cols, fields = {}, []
 
     def gathered(t):

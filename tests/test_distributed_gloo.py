@@ -278,7 +278,7 @@ def _check_invariant(r1, rw, world):
     assert sum(x[1] for x in r1["stream_agg"]) == 600
 
 
-@pytest.mark.parametrize("world", [2, 3])
+@pytest.mark.parametrize("world", [2, 3, 4, 8])
 def test_spmd_results_invariant_to_world_size(tmp_path, world):
     _check_invariant(_run(1, tmp_path), _run(world, tmp_path), world)
 

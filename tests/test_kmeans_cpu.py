@@ -154,3 +154,21 @@ def test_cosine_rejects_zero_rows():
     x[4] = 0.0
     with pytest.raises(ValueError, match="zero-length"):
         LloydEngine(torch.as_tensor(x), 3, 2, spherical=True)
+
+
+def test_precision_modes_cpu():
+    import pytest
+    x = torch.as_tensor(np.random.RandomState(0).randn(100, 3))
+    assert LloydEngine(x, 3, 2).precision == "exact"
+    with pytest.raises(ValueError):
+        LloydEngine(x, 3, 2, precision="fp16")
+
+
+def test_candidate_chunks_cover_and_respect_limits():
+    e = LloydEngine(torch.zeros(10, 4, dtype=torch.float64), 4, 2)
+    e.dp = 256
+    e.x = torch.zeros(1, 256, dtype=torch.bfloat16)
+    for m in (1, 63, 64, 255, 256, 300, 511, 512, 520, 641, 1025, 3000):
+        ch = LloydEngine._candidate_chunks(e, m)
+        assert sum(ch) == m and all(0 < c <= 320 for c in ch)
+        assert all(c % 64 == 0 for c in ch[:-1])

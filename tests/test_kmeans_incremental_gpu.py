@@ -15,8 +15,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _full_steps_only(monkeypatch):
-    """These tests target the full / incremental step machinery: pruned steps off by default."""
+    """These tests target the full / incremental MFMA step machinery: pruned steps off by default, and
+    f32/f64 rows take the bf16 path (not the source-precision one, tests/test_kmeans_exact_gpu.py)."""
     monkeypatch.setenv("CML_KMEANS_PRUNE", "0")
+    monkeypatch.setenv("CML_KMEANS_PRECISION", "bf16")
 
 
 def _blobs(n, d, k, seed, grid=True, dtype=torch.bfloat16):
@@ -107,7 +109,8 @@ def test_row_norm_cache_follows_tensor_version():
     n, d, k = 40_000, 256, 32
     x = to_device_matrix(_blobs(n, d, k, seed=6), d)
     eng = LloydEngine(x, d, k, use_graph=False)
-    assert eng.x is x and getattr(x, "_cml_xnorm")[2] is eng.xnorm
+    xn0 = eng.xnorm  # computed on first use (or by the k-means|| first pass), then cached on the tensor
+    assert eng.x is x and getattr(x, "_cml_xnorm")[2] is xn0
     assert cached_row_sqnorm(x, n, eng.dp) is eng.xnorm
     c = x[:k, :d].double()
     _, best0 = assign_gpu(x, eng.dp, d, c)

@@ -12,8 +12,10 @@ pytestmark = pytest.mark.gpu
 
 @pytest.fixture(autouse=True)
 def _full_steps_only(monkeypatch):
-    """These tests target the full / incremental step machinery: pruned steps off by default."""
+    """These tests target the full / incremental MFMA step machinery: pruned steps off by default, and
+    f32/f64 rows take the bf16 path (not the source-precision one, tests/test_kmeans_exact_gpu.py)."""
     monkeypatch.setenv("CML_KMEANS_PRUNE", "0")
+    monkeypatch.setenv("CML_KMEANS_PRECISION", "bf16")
 
 
 def _ref_assign(xb, cb):
