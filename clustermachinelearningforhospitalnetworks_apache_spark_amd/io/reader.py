@@ -163,9 +163,13 @@ class DataFrameReader:
         # precise_float: exact round trip of the writer's shortest-repr doubles (the default parser rounds)
         frames = [pd.read_json(f, lines=True, precise_float=True) for f in files]
         pdf = pd.concat(frames, ignore_index=True) if frames else pd.DataFrame()
+        special = _non_numeric_numbers(pdf, files)
         comm = self._session._comm
         a, b = shard_range(len(pdf), comm.rank, comm.world_size)
         table = pa.Table.from_pandas(pdf.iloc[a:b], preserve_index=False)
+        for c, vals in special.items():  # NaN is a value there, not a null: build the column directly
+            i = table.schema.get_field_index(c)
+            table = table.set_column(i, c, pa.array(vals[a:b], type=pa.float64(), from_pandas=False))
         df = frame_from_arrow(self._session, table, list(range(a, b)))
         if self._schema is not None:
             from ..sql import functions as F
@@ -187,3 +191,38 @@ class DataFrameReader:
         a, b = shard_range(len(lines), comm.rank, comm.world_size)
         schema = T.StructType([T.StructField("value", T.StringType())])
         return frame_from_pycolumns(self._session, schema, {"value": lines[a:b]}, list(range(a, b)))
+
+
+_NON_NUMERIC = {"NaN": float("nan"), "Infinity": float("inf"), "+Infinity": float("inf"), "-Infinity": float("-inf"),
+                "INF": float("inf"), "+INF": float("inf"), "-INF": float("-inf")}
+
+
+def _non_numeric_numbers(pdf, files) -> dict:
+    """Spark's allowNonNumericNumbers (default on): non-finite doubles written as "NaN" / "Infinity" /
+    "-Infinity" strings read back as those values. pandas parses them but cannot keep a NaN apart from
+    a missing field (both become NaN), so when a file carries such strings the numeric columns are
+    rebuilt from the records: {column: python values, None for a missing or null field}."""
+    import json
+    import math
+    import numbers
+    texts = []
+    for f in files:
+        with open(f, encoding="utf-8") as fh:
+            texts.append(fh.read())
+    if not any(any(f'"{w}"' in t for w in _NON_NUMERIC) for t in texts):
+        return {}
+    recs = [json.loads(line) for t in texts for line in t.splitlines() if line.strip()]
+    if len(recs) != len(pdf):
+        return {}
+    out = {}
+    for c in pdf.columns:
+        vals = [r.get(c) for r in recs]
+        present = [v for v in vals if v is not None]
+        if not any(isinstance(v, str) and v in _NON_NUMERIC for v in present):
+            continue
+        if not all((isinstance(v, str) and v in _NON_NUMERIC) or
+                   (isinstance(v, numbers.Number) and not isinstance(v, bool)) for v in present):
+            continue
+        out[c] = [None if v is None else (_NON_NUMERIC[v] if isinstance(v, str) else float(v)) for v in vals]
+        pdf[c] = [0.0 if v is None or (isinstance(v, float) and math.isnan(v)) else v for v in out[c]]
+    return out

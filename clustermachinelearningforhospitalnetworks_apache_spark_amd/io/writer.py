@@ -160,7 +160,8 @@ class DataFrameWriter:
     @staticmethod
     def _json_lines(df, path: str) -> None:
         """JSON Lines as Spark writes them: one object per row, null fields omitted (ignoreNullFields),
-        doubles with every significant digit (shortest repr round-trips; pandas' to_json keeps 10)."""
+        doubles with every significant digit (shortest repr round-trips; pandas' to_json keeps 10),
+        NaN / ±Infinity as the quoted strings Spark writes."""
         import datetime
         import decimal
         import json
@@ -169,7 +170,13 @@ class DataFrameWriter:
 
         def conv(v):
             if isinstance(v, float):
-                return None if math.isnan(v) else v
+                # Spark writes non-finite doubles as the strings "NaN" / "Infinity" / "-Infinity" and
+                # reads them back (allowNonNumericNumbers): NaN must not turn into a missing field
+                if math.isnan(v):
+                    return "NaN"
+                if math.isinf(v):
+                    return "Infinity" if v > 0 else "-Infinity"
+                return v
             if isinstance(v, datetime.datetime):
                 return v.isoformat(timespec="milliseconds")
             if isinstance(v, datetime.date):
@@ -198,7 +205,7 @@ class DataFrameWriter:
                     v = conv(vals[i])
                     if v is not None:
                         rec[name] = v
-                fh.write(json.dumps(rec, allow_nan=True) + "\n")
+                fh.write(json.dumps(rec, allow_nan=False, separators=(",", ":"), ensure_ascii=False) + "\n")
 
     def _local_pandas(self, df=None, csv: bool = False):
         import pandas as pd

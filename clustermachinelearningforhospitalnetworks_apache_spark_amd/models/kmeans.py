@@ -178,6 +178,9 @@ class LloydEngine:
             self.x = x[:, :d].to(torch.float64)
             self.dp = d
         self._row_ids = row_ids
+        # error allowance of the assign's squared distances (pruning bounds), scaled with the padded
+        # width: the f32 accumulation error grows with D; f64 rows keep the fixed floor
+        self._tau = self.prune_tau(self.dp) if self.gpu else self._PRUNE_TAU
         if row_chunks is None:
             row_chunks = 2 if (self.comm.is_distributed and self.n >= (1 << 20)) else 1
         self.row_chunks = max(1, min(int(row_chunks), max(1, self.n)))
@@ -571,7 +574,7 @@ class LloydEngine:
         cn = (c * c).sum(1)
         st.cn = cn
         st.mc = float(cn.max()) if self.k else 0.0
-        st.c2 = 2.0 * self._PRUNE_TAU * (st.mx + st.mc)
+        st.c2 = 2.0 * self._tau * (st.mx + st.mc)
         if old is not None:
             dr = (c - old).pow(2).sum(1).sqrt() * (1.0 + 1e-6)
             st.drift.copy_(dr)
@@ -582,7 +585,7 @@ class LloydEngine:
             d2 = (cn[:, None] + cn[None, :] - 2.0 * (c @ c.T)).clamp_(min=0.0)
             d2.fill_diagonal_(float("inf"))
             half = 0.5 * d2.min(1).values.sqrt()
-            slack = self._PRUNE_TAU * (st.mx + st.mc) / (2.0 * half)
+            slack = self._tau * (st.mx + st.mc) / (2.0 * half)
             thr = torch.where(half > 0, (half - slack) * (1.0 - 1e-6), torch.full_like(half, -math.inf))
         else:
             thr = torch.full((self.k,), math.inf, dtype=torch.float64, device=self.device)
@@ -590,7 +593,7 @@ class LloydEngine:
 
     def _prune_bound(self, best: torch.Tensor, xn: torch.Tensor) -> torch.Tensor:
         """Upper bound on the exact distance from the assign's squared distance (rounded up)."""
-        return (best.clamp(min=0) + self._PRUNE_TAU * (xn + self._pst.mc)).sqrt() * (1.0 + 1e-6)
+        return (best.clamp(min=0) + self._tau * (xn + self._pst.mc)).sqrt() * (1.0 + 1e-6)
 
     def _prune_lower(self, xg: torch.Tensor, xng: torch.Tensor, lab: torch.Tensor, out: torch.Tensor,
                      chunk: Optional[int] = None) -> None:
@@ -619,7 +622,7 @@ class LloydEngine:
                     if k % 4 == 0 and out.dtype == torch.float32:  # masked row min + bound in one pass
                         labc = lab[s0:s0 + chunk]
                         labc = labc if labc.dtype == torch.int32 else labc.to(torch.int32)
-                        K.prune_lower(dist, labc.contiguous(), xn.contiguous(), st.mc, self._PRUNE_TAU,
+                        K.prune_lower(dist, labc.contiguous(), xn.contiguous(), st.mc, self._tau,
                                       out[s0:s0 + chunk])
                         continue
                 else:
@@ -628,7 +631,7 @@ class LloydEngine:
                 sec = dist.min(1).values + xn
             else:
                 sec = torch.full_like(xn, math.inf)
-            lo = (sec - self._PRUNE_TAU * (xn + st.mc)).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6)
+            lo = (sec - self._tau * (xn + st.mc)).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6)
             out[s0:s0 + chunk] = lo.to(out.dtype)
 
     @staticmethod

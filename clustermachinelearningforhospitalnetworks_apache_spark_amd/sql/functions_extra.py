@@ -266,7 +266,8 @@ def _row_hash(name: str, algo: str, cols) -> Column:
         for a in args:
             if isinstance(a.dtype, T.NullType):
                 continue
-            if not a.is_host and a.values.dim() == 1 and (T.is_numeric(a.dtype) or isinstance(
+            wide_dec = isinstance(a.dtype, T.DecimalType) and a.dtype.precision > 18
+            if not a.is_host and a.values.dim() == 1 and not wide_dec and (T.is_numeric(a.dtype) or isinstance(
                     a.dtype, (T.BooleanType, T.DateType, T.TimestampType))):
                 nh = device_hash(a.values, a.dtype, h, algo)
                 h = nh if a.valid is None else torch.where(a.valid.to(dev), nh, h)

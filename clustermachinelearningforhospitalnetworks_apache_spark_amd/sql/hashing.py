@@ -174,6 +174,12 @@ def _float_bits(v: float) -> int:
     return _struct.unpack("<i", _struct.pack("<f", v))[0]
 
 
+def _unscaled(v: Any, scale: int) -> int:
+    from decimal import ROUND_HALF_UP, Decimal
+    d = v if isinstance(v, Decimal) else Decimal(repr(float(v)))
+    return int(d.scaleb(scale).to_integral_value(rounding=ROUND_HALF_UP))
+
+
 def hash_value(v: Any, dt: T.DataType, seed: int, algo: str) -> int:
     """Hash one Python value of Spark type ``dt`` (unsigned result in the algorithm's width)."""
     from .column import ts_to_micros
@@ -194,7 +200,14 @@ def hash_value(v: Any, dt: T.DataType, seed: int, algo: str) -> int:
         return fl(ts_to_micros(v), seed)
     if isinstance(dt, T.FloatType):
         return fi(_float_bits(float(v)), seed)
-    if isinstance(dt, (T.DoubleType, T.DecimalType)):
+    if isinstance(dt, T.DecimalType):
+        # Spark: the unscaled value, as a long when precision <= 18, else the two's-complement
+        # big-endian bytes of the unscaled BigInteger (BigInteger.toByteArray, minimal length)
+        unscaled = _unscaled(v, dt.scale)
+        if dt.precision <= 18:
+            return fl(unscaled, seed)
+        return fb(unscaled.to_bytes((unscaled.bit_length() + 8) // 8, "big", signed=True), seed)
+    if isinstance(dt, T.DoubleType):
         return fl(_double_bits(float(v)), seed)
     if isinstance(dt, T.BinaryType):
         return fb(bytes(v), seed)
@@ -267,7 +280,12 @@ def device_hash(vals: torch.Tensor, dt: T.DataType, seed: torch.Tensor, algo: st
         f = vals.to(torch.float32) + 0.0
         f = torch.where(torch.isnan(f), torch.full_like(f, float("nan")), f)
         lane, width = f.view(torch.int32).to(torch.int64), 4
-    elif isinstance(dt, (T.DoubleType, T.DecimalType)):
+    elif isinstance(dt, T.DecimalType):
+        if dt.precision > 18:
+            raise ValueError("decimal(precision > 18) hashes on the host (unscaled BigInteger bytes)")
+        # device decimals are f64: the unscaled long is the value at the column's scale, rounded
+        lane, width = torch.round(vals.to(torch.float64) * (10.0 ** dt.scale)).to(torch.int64), 8
+    elif isinstance(dt, T.DoubleType):
         f = vals.to(torch.float64) + 0.0
         f = torch.where(torch.isnan(f), torch.full_like(f, float("nan")), f)
         lane, width = f.view(torch.int64), 8

@@ -7,12 +7,15 @@ Layout of a checkpoint ``<dir>/<name>/``::
     v-00000012/<array>.npy     one file per state array (loaded with ``allow_pickle=False``)
     LATEST                     name of the newest complete version ("v-00000012")
 
-Crash safety: rank 0 writes a new version into ``v-<it>.tmp-<pid>``, renames it to ``v-<it>`` (a
-fresh name, so the rename is atomic and never replaces anything), then atomically replaces the
-``LATEST`` pointer file, and only then deletes older versions.  At every instant at least one
-complete version exists and ``load`` finds it: through ``LATEST``, or — if the pointer is missing,
-torn or names a version that is gone — by scanning for the newest ``v-*`` directory that has its
-``state.json`` (written last inside the version, so its presence means the version is complete).
+Crash safety: rank 0 writes a new version into ``v-<it>.tmp-<pid>``, fsyncs its files and the
+directory, renames it to a name no earlier save used (``v-<it>``, or ``v-<it>-<generation>`` when
+that iteration was saved before — a resumed fit — so a rename never replaces or deletes anything),
+fsyncs the parent, then atomically replaces the ``LATEST`` pointer file (written, fsynced, renamed,
+parent fsynced), and only then deletes versions older than the previous one. At every instant —
+power loss included — at least one complete, durable version exists and ``load`` finds it: through
+``LATEST``, or — if the pointer is missing, torn or names a version that is gone — by scanning for the
+newest ``v-*`` directory that has its ``state.json`` (written last inside the version, so its
+presence means the version is complete).
 
 Names are derived from the fit's key (``name_for``), not from an estimator uid, so a restarted
 process (a new uid) finds the checkpoint of the same fit.  ``load_shared`` makes the resume
@@ -31,7 +34,7 @@ from typing import Dict, Optional, Tuple
 
 import numpy as np
 
-_VER = re.compile(r"^v-(\d{8,})$")
+_VER = re.compile(r"^v-(\d{8,})(?:-(\d+))?$")
 
 
 def name_for(prefix: str, key: str) -> str:
@@ -49,8 +52,28 @@ def _versions(root: str):
     for e in entries:
         m = _VER.match(e)
         if m and os.path.exists(os.path.join(root, e, "state.json")):
-            out.append((int(m.group(1)), e))
+            out.append(((int(m.group(1)), int(m.group(2) or 0)), e))
     return [e for _, e in sorted(out, reverse=True)]
+
+
+def _fsync_dir(path: str) -> None:
+    try:
+        fd = os.open(path, os.O_RDONLY)
+    except OSError:
+        return
+    try:
+        os.fsync(fd)
+    except OSError:
+        pass
+    finally:
+        os.close(fd)
+
+
+def _write_durable(path: str, write) -> None:
+    with open(path, "wb") as fh:
+        write(fh)
+        fh.flush()
+        os.fsync(fh.fileno())
 
 
 def save(directory: str, name: str, key: str, iteration: int, arrays: Dict[str, np.ndarray], comm=None) -> None:
@@ -58,24 +81,28 @@ def save(directory: str, name: str, key: str, iteration: int, arrays: Dict[str, 
         return
     root = os.path.join(directory, name)
     os.makedirs(root, exist_ok=True)
-    ver = f"v-{int(iteration):08d}"
+    base = f"v-{int(iteration):08d}"
+    gens = [int(m.group(2) or 0) for m in (_VER.match(e) for e in os.listdir(root)) if m and
+            int(m.group(1)) == int(iteration)]
+    ver = base if not gens else f"{base}-{max(gens) + 1}"  # never an existing name
     final = os.path.join(root, ver)
-    tmp = final + f".tmp-{os.getpid()}"
+    tmp = os.path.join(root, f"{ver}.tmp-{os.getpid()}")
     shutil.rmtree(tmp, ignore_errors=True)
     os.makedirs(tmp)
     for k, v in arrays.items():
-        np.save(os.path.join(tmp, f"{k}.npy"), np.asarray(v), allow_pickle=False)
-    with open(os.path.join(tmp, "state.json"), "w") as fh:  # written last: marks the version complete
-        json.dump({"key": key, "iteration": int(iteration), "arrays": sorted(arrays)}, fh)
-    if os.path.exists(final):  # same iteration saved again (a resumed fit): retire the old copy first
-        shutil.rmtree(final)
-    os.replace(tmp, final)
+        _write_durable(os.path.join(tmp, f"{k}.npy"), lambda fh, v=v: np.save(fh, np.asarray(v), allow_pickle=False))
+    meta = json.dumps({"key": key, "iteration": int(iteration), "arrays": sorted(arrays)}).encode()
+    _write_durable(os.path.join(tmp, "state.json"), lambda fh: fh.write(meta))  # last: marks the version complete
+    _fsync_dir(tmp)
+    os.rename(tmp, final)
+    _fsync_dir(root)
     ptr_tmp = os.path.join(root, f"LATEST.tmp-{os.getpid()}")
-    with open(ptr_tmp, "w") as fh:
-        fh.write(ver + "\n")
+    _write_durable(ptr_tmp, lambda fh: fh.write((ver + "\n").encode()))
     os.replace(ptr_tmp, os.path.join(root, "LATEST"))
+    _fsync_dir(root)
+    keep = set(_versions(root)[:2]) | {ver, "LATEST"}  # the new version and the one before it
     for e in os.listdir(root):  # older versions and leftovers of crashed writers
-        if e not in (ver, "LATEST"):
+        if e not in keep:
             p = os.path.join(root, e)
             if os.path.isdir(p):
                 shutil.rmtree(p, ignore_errors=True)

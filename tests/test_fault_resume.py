@@ -52,7 +52,7 @@ def test_kmeans_resumes_from_checkpoint(spark, tmp_path, monkeypatch):
         km.fit(df)
     saved = os.listdir(tmp_path / "ck")
     assert len(saved) == 1 and saved[0].startswith("kmeans-")
-    assert sorted(os.listdir(tmp_path / "ck" / saved[0])) == ["LATEST", "v-00000006"]
+    assert sorted(os.listdir(tmp_path / "ck" / saved[0])) == ["LATEST", "v-00000004", "v-00000006"]
     monkeypatch.delenv("CML_FAULT")
     # a restarted process builds a NEW estimator (new uid): the key-derived name still finds it
     km = KMeans(k=4, seed=3, maxIter=12, tol=0.0)
@@ -87,7 +87,14 @@ def test_checkpoint_survives_crash_between_renames(tmp_path):
     it, arrs = ck.load(d, name, "key")
     assert it == 4 and arrs["centers"].shape == (2, 3)
     ck.save(d, name, "key", 6, {"centers": np.zeros((2, 3))})
-    assert sorted(os.listdir(root)) == ["LATEST", "v-00000006"]
+    # the new version and the one before it are kept; crashed writers' leftovers are gone
+    assert sorted(os.listdir(root)) == ["LATEST", "v-00000004", "v-00000006"]
+    # the same iteration saved again (a resumed fit) lands under a fresh name: the old copy is never
+    # removed before the new one is complete and LATEST names it
+    ck.save(d, name, "key", 6, {"centers": np.full((2, 3), 7.0)})
+    assert sorted(os.listdir(root)) == ["LATEST", "v-00000006", "v-00000006-1"]
+    assert (root / "LATEST").read_text().strip() == "v-00000006-1"
+    assert float(ck.load(d, name, "key")[1]["centers"][0, 0]) == 7.0
     # LATEST lost or torn: the newest complete version is found by scanning
     (root / "LATEST").write_text("v-000")
     assert ck.load(d, name, "key")[0] == 6

@@ -133,7 +133,8 @@ def test_pruned_distributed_gloo_matches_single_rank(tmp_path):
 
 # ------------------------------------------------------------------------------------------- GPU
 @pytest.mark.gpu
-@pytest.mark.parametrize("n,d,k,scale", [(300_001, 256, 256, 1.0), (200_000, 128, 64, 1.0), (50_000, 64, 300, 3.0),
+@pytest.mark.parametrize("n,d,k,scale", [(300_001, 256, 256, 1.0), (200_000, 128, 64, 1.0), (120_000, 512, 128, 1.0),
+                                         (50_000, 64, 300, 3.0),
                                          (60_000, 64, 200, 0.5)])
 def test_pruned_equals_full_gpu(n, d, k, scale):
     x = _blobs(n, d, k, seed=7, scale=scale, device="cuda", dtype=torch.bfloat16)
