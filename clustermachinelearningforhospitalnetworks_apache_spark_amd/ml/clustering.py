@@ -65,9 +65,10 @@ class KMeans(Estimator):
         if measure not in ("euclidean", "cosine"):
             raise ValueError(f"distanceMeasure must be 'euclidean' or 'cosine', got {measure!r}")
         spherical = measure == "cosine"
-        if self.isSet("weightCol"):
-            raise NotImplementedError("weighted KMeans is not supported yet")
         x = df._feature_matrix(self.getFeaturesCol())
+        weights = None
+        if self.isSet("weightCol") and self.getOrDefault("weightCol"):
+            weights = _weights(df, self.getOrDefault("weightCol"), x.device)
         d = x.shape[1]
         k = self.getK()
         comm = df._comm
@@ -78,7 +79,7 @@ class KMeans(Estimator):
         prune = None if pv is None else str(pv).lower() in ("1", "true")
         precision = conf.get("cml.ml.kmeans.precision", "auto")
         eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                          precision=precision)
+                          precision=precision, weights=weights)
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
@@ -87,6 +88,8 @@ class KMeans(Estimator):
             # the key identifies the fit (shape, params and a data fingerprint), and the checkpoint name
             # is derived from it: a restarted process, whose estimator has a new uid, finds it again
             fp = _fingerprint(x, comm)
+            if weights is not None:
+                fp += "|w=" + _fingerprint(weights.reshape(-1, 1), comm)
             ckkey = (f"kmeans|n={n_global}|d={d}|k={k}|seed={seed}|init={self.getInitMode()}|"
                      f"steps={self.getInitSteps()}|tol={self.getTol()}|measure={measure}|data={fp}")
             ckname = ckpt.name_for("kmeans", ckkey)
@@ -98,7 +101,7 @@ class KMeans(Estimator):
             init = arrs["centers"]
             if init.shape[0] < k:
                 eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                                  precision=precision)
+                                  precision=precision, weights=weights)
         elif self.getInitMode() == "random":
             with trace("kmeans.init"):
                 init = eng.init_random(seed)
@@ -109,7 +112,7 @@ class KMeans(Estimator):
             if k_eff < k:
                 init = init[:k_eff]
                 eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                                  precision=precision)
+                                  precision=precision, weights=weights)
         eng.set_centers(init)
 
         def on_iter(it):
@@ -130,6 +133,24 @@ class KMeans(Estimator):
         model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
                                             [int(s) for s in sizes.cpu().tolist()]))
         return model
+
+
+def _weights(df, col: str, device) -> torch.Tensor:
+    """The weight column as f64 (Spark's checkNonNegativeWeight: finite, >= 0, not null)."""
+    cd = df._column_data(col)
+    if cd.is_host:
+        from ..sql.dataframe import column_to_python
+        vals = column_to_python(cd)
+        if any(v is None for v in vals):
+            raise ValueError(f"weight column {col!r} contains nulls")
+        w = torch.as_tensor(np.asarray(vals, dtype=np.float64), device=device)
+    else:
+        if cd.valid is not None and not bool(cd.valid.all()):
+            raise ValueError(f"weight column {col!r} contains nulls")
+        w = cd.values.to(device=device, dtype=torch.float64).reshape(-1)
+    if w.numel() and not bool(((w >= 0) & torch.isfinite(w)).all()):
+        raise ValueError(f"weights must be finite and non-negative (column {col!r})")
+    return w
 
 
 def _fingerprint(x: torch.Tensor, comm) -> str:

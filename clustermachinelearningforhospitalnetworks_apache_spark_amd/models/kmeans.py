@@ -121,8 +121,17 @@ class LloydEngine:
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
                  incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None,
-                 precision: Optional[str] = None):
+                 precision: Optional[str] = None, weights: Optional[torch.Tensor] = None):
         self.comm = comm or local_comm()
+        # weights (Spark's weightCol, KMeans.scala runAlgorithm): centre = Σ w·x / Σ w, cost = Σ w·d²,
+        # k-means|| candidates weighted by the summed weight of their rows. Weighted fits run the
+        # source-precision path (f64 rows, deterministic f64 sums of [w·x | w]).
+        if weights is not None:
+            if str(precision or "auto").lower() == "bf16":
+                raise ValueError("weighted KMeans runs at source precision; precision 'bf16' is not supported")
+            precision, prune = "exact", False
+            if x.is_cuda and x.dtype not in (torch.float32, torch.float64):
+                x = x.to(torch.float32)
         # precision (cml.ml.kmeans.precision): "bf16" = the MFMA path (bf16 rows in the distance GEMM,
         # exact f64 sums of those rows); "exact" = the f64 reference algorithm on the rows as given
         # (kmeans_exact.hip on the GPU); "auto" = exact for f32/f64 device rows — the reference's f64
@@ -178,6 +187,13 @@ class LloydEngine:
             self.x = x[:, :d].to(torch.float64)
             self.dp = d
         self._row_ids = row_ids
+        self.w = self._wx = None
+        if weights is not None:
+            w = torch.as_tensor(weights, dtype=torch.float64, device=self.device).reshape(-1)
+            if w.shape[0] != self.n:
+                raise ValueError(f"{w.shape[0]} weights for {self.n} rows")
+            self.w = w
+            self._wx = torch.cat([self.x * w[:, None], w[:, None]], 1)  # [w·x | w]: one sums pass
         # error allowance of the assign's squared distances (pruning bounds), scaled with the padded
         # width: the f32 accumulation error grows with D; f64 rows keep the fixed floor
         self._tau = self.prune_tau(self.dp) if self.gpu else self._PRUNE_TAU
@@ -418,8 +434,13 @@ class LloydEngine:
 
     def _step_cpu(self):
         labels, best = K.assign_reference(self.x, self.centers)
-        sums, counts = K.sums_reference(self.x, labels, self.k)
-        msg = torch.cat([sums.reshape(-1), counts, best.sum().reshape(1)])
+        if self.w is not None:
+            aug, _ = K.sums_reference(self._wx, labels, self.k)
+            sums, counts, cost = aug[:, : self.d], aug[:, self.d], (best * self.w).sum()
+        else:
+            sums, counts = K.sums_reference(self.x, labels, self.k)
+            cost = best.sum()
+        msg = torch.cat([sums.reshape(-1), counts, cost.reshape(1)])
         self.comm.allreduce_(msg)
         self._update_cpu(msg)
         self.labels = labels
@@ -938,7 +959,11 @@ class LloydEngine:
         if uniq.shape[0] <= k:
             out = uniq.cpu().numpy()
         else:
-            if self.n:
+            if self.n and self.w is not None:
+                # summed row weights per candidate (deterministic f64 sums, as the Lloyd sums)
+                w = K.sums_reference(self.w[:, None], inverse.reshape(-1)[nearest[: self.n].long()],
+                                     uniq.shape[0])[0][:, 0].contiguous()
+            elif self.n:
                 w = torch.bincount(inverse.reshape(-1)[nearest[: self.n].long()], minlength=uniq.shape[0])
                 w = w.to(torch.float64)
             else:

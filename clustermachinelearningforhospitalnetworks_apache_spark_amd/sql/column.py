@@ -658,8 +658,9 @@ class Func(Expr):
 class AggExpr(Expr):
     """Aggregate (count/sum/avg/min/max/stddev/variance/count_distinct) — evaluated by groupBy/agg."""
 
-    def __init__(self, fn: str, child: Optional[Expr], distinct: bool = False):
+    def __init__(self, fn: str, child: Optional[Expr], distinct: bool = False, ignore_nulls: bool = False):
         self.fn, self.child, self.distinct = fn, child, distinct
+        self.ignore_nulls = bool(ignore_nulls)  # first / last: Spark's ignoreNulls (default False)
 
     def is_aggregate(self):
         return True

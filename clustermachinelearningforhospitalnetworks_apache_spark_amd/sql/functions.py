@@ -255,12 +255,16 @@ def var_pop(c: ColumnOrName) -> Column:
     return Column(AggExpr("var_pop", _c(c)))
 
 
-def first(c: ColumnOrName) -> Column:
-    return Column(AggExpr("first", _c(c)))
+def first(c: ColumnOrName, ignorenulls: bool = False) -> Column:
+    """Spark's first(col, ignorenulls=False): the value of the group's first row in row order (null
+    included); with ignorenulls the first non-null value."""
+    return Column(AggExpr("first", _c(c), ignore_nulls=ignorenulls))
 
 
-def last(c: ColumnOrName) -> Column:
-    return Column(AggExpr("last", _c(c)))
+def last(c: ColumnOrName, ignorenulls: bool = False) -> Column:
+    """Spark's last(col, ignorenulls=False): the group's last row's value (null included); with
+    ignorenulls the last non-null value."""
+    return Column(AggExpr("last", _c(c), ignore_nulls=ignorenulls))
 
 
 def collect_list(c: ColumnOrName) -> Column:

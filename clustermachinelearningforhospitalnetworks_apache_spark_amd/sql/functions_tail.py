@@ -193,17 +193,17 @@ def array_agg(c: ColumnOrName) -> Column:
 
 def any_value(c: ColumnOrName, ignoreNulls: bool = False) -> Column:
     from .functions import first
-    return first(c)
+    return first(c, ignorenulls=bool(ignoreNulls))
 
 
 def first_value(c: ColumnOrName, ignoreNulls: bool = False) -> Column:
     from .functions import first
-    return first(c)
+    return first(c, ignorenulls=bool(ignoreNulls))
 
 
 def last_value(c: ColumnOrName, ignoreNulls: bool = False) -> Column:
     from .functions import last
-    return last(c)
+    return last(c, ignorenulls=bool(ignoreNulls))
 
 
 def std(c: ColumnOrName) -> Column:
@@ -212,13 +212,18 @@ def std(c: ColumnOrName) -> Column:
 
 
 def try_sum(c: ColumnOrName) -> Column:
-    from .functions import sum as _sum
-    return _sum(c)
+    """Spark's try_sum: sum, but null (instead of a wrapped 64-bit value) when an integral total
+    leaves the LongType range. Floating sums behave as sum (overflow to ±Infinity)."""
+    from .column import AggExpr
+    return Column(AggExpr("try_sum", _c(c)))
 
 
 def try_avg(c: ColumnOrName) -> Column:
-    from .functions import avg
-    return avg(c)
+    """Spark's try_avg. Average accumulates integral and floating input in a double (Average's
+    sumDataType), which cannot overflow to an error; only decimal/interval sums differ from avg, and
+    decimals here are averaged in f64 too — so the value is avg's, named try_avg."""
+    from .column import AggExpr
+    return Column(AggExpr("try_avg", _c(c)))
 
 
 # ------------------------------------------------------------------------------------------ try_* / null-safe

@@ -34,8 +34,10 @@ def _result_type(fn: str, in_type: Optional[T.DataType], arg=None) -> T.DataType
         return T.ArrayType(in_type or T.DoubleType())
     if fn in ("avg", "stddev", "stddev_pop", "variance", "var_pop"):
         return T.DoubleType()
-    if fn == "sum":
+    if fn in ("sum", "try_sum"):
         return T.LongType() if in_type is not None and T.is_integral(in_type) else T.DoubleType()
+    if fn == "try_avg":
+        return T.DoubleType()
     return in_type or T.DoubleType()
 
 
@@ -46,14 +48,16 @@ def _unwrap(e: Expr):
     return alias, e
 
 
-def _partial(values: List[Any], fn: str, distinct: bool):
+def _partial(values: List[Any], fn: str, distinct: bool, ignore_nulls: bool = True):
+    if fn in ("first", "last"):
+        # (kind, value, rows seen): without ignoreNulls the first / last ROW decides, null or not
+        vals = values if not ignore_nulls else [v for v in values if v is not None]
+        if not vals:
+            return (fn, None, False)
+        return (fn, vals[0] if fn == "first" else vals[-1], True)
     vals = [v for v in values if v is not None and not (isinstance(v, float) and math.isnan(v) and fn != "count")]
     if fn == "count":
         return ("set", set(vals)) if distinct else ("n", len(vals))
-    if fn == "first":
-        return ("first", vals[0] if vals else None)
-    if fn == "last":
-        return ("last", vals[-1] if vals else None)
     if fn in ("collect_list", "collect_set", "percentile"):
         return ("list", [_hashable(v) for v in values if v is not None])
     if fn in ("min", "max"):
@@ -61,8 +65,11 @@ def _partial(values: List[Any], fn: str, distinct: bool):
             return (fn, None)
         return (fn, min(vals) if fn == "min" else max(vals))
     nums = [float(v) for v in vals]
-    if fn == "sum" and vals and all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in vals):
-        return ("isum", len(nums), int(np.sum(np.asarray(vals, dtype=np.int64))))
+    if fn in ("sum", "try_sum") and vals and \
+            all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in vals):
+        # exact (unbounded) integer sum: the merge wraps it to 64 bits (sum, Spark's non-ANSI
+        # overflow) or turns an out-of-range total into null (try_sum)
+        return ("isum", len(nums), sum(int(v) for v in vals))
     if not nums:
         return ("mom", 0, 0.0, 0.0, 0.0)
     a = np.asarray(nums, dtype=np.float64)
@@ -81,12 +88,12 @@ def _merge(parts, fn: str):
         return len(s)
     if kind == "first":
         for p in parts:
-            if p[1] is not None:
+            if p[2]:
                 return p[1]
         return None
     if kind == "last":
         for p in reversed(parts):
-            if p[1] is not None:
+            if p[2]:
                 return p[1]
         return None
     if kind == "list":
@@ -109,7 +116,11 @@ def _merge(parts, fn: str):
     if kind == "isum" or all(p[0] == "isum" for p in parts):
         n = sum(p[1] for p in parts if p[0] == "isum")
         s = sum(p[2] for p in parts if p[0] == "isum") + sum(p[2] for p in parts if p[0] == "mom")
-        return s if n else None
+        if not n:
+            return None
+        if fn == "try_sum":
+            return s if -2 ** 63 <= s < 2 ** 63 else None
+        return (s + 2 ** 63) % 2 ** 64 - 2 ** 63  # two's-complement wrap, as Spark's LongType sum
     # Chan et al. parallel merge of (count, mean, M2)
     n, mean, m2, s = 0, 0.0, 0.0, 0.0
     for p in parts:
@@ -124,9 +135,9 @@ def _merge(parts, fn: str):
         s += sb
     if n == 0:
         return None
-    if fn == "sum":
+    if fn in ("sum", "try_sum"):
         return s
-    if fn == "avg":
+    if fn in ("avg", "try_avg"):
         return s / n
     var_pop = max(m2 / n, 0.0)
     if fn in ("var_pop", "stddev_pop"):
@@ -213,7 +224,8 @@ def local_partials(df: DataFrame, keys: List[Expr], exprs: List[Expr]):
                 if getattr(agg, "custom", False):
                     parts.append(agg.partial(vals, [src[i] for i in idx]))
                 else:
-                    parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct))
+                    parts.append(_partial([vals[i] for i in idx], agg.fn, agg.distinct,
+                                          getattr(agg, "ignore_nulls", False)))
         local[key] = parts
     return specs, key_types, local
 
@@ -281,7 +293,8 @@ def combine_partials(parts: List[Any], fn: str):
             out |= p[1]
         return ("set", out)
     if kind in ("first", "last"):
-        return (kind, _merge(parts, fn))
+        rows = any(p[2] for p in parts)
+        return (kind, _merge(parts, fn), rows)
     if kind == "list":
         return ("list", [v for p in parts for v in p[1]])
     if kind in ("min", "max"):

@@ -166,6 +166,8 @@ def tensor_partials(df, keys, exprs) -> Optional[TensorPartials]:
             agg_inputs.append(("star", None))
             continue
         cd = inner.child.eval(df)
+        if inner.fn in ("first", "last") and not inner.ignore_nulls and cd.valid is not None:
+            return None  # first/last ROW with nulls present (Spark's default): the row-loop merge
         if inner.fn in ("first", "last") and (cd.is_host or cd.values.dim() == 1):
             pass  # positions are computed on the device, values taken from the column as stored
         elif inner.fn != "count" and (cd.is_host or not _numeric(cd.dtype) or cd.values.dim() != 1):
@@ -332,7 +334,7 @@ def _to_python(tp: TensorPartials, df):
             per_spec.append([(kind, py[g] if cnt_l[g] else None) for g in range(G)])
         elif kind in ("first", "last"):
             py = _python_values(pt["cd"].take(pt["rows"]))
-            per_spec.append([(kind, py[g] if cnt_l[g] else None) for g in range(G)])
+            per_spec.append([(kind, py[g] if cnt_l[g] else None, bool(cnt_l[g])) for g in range(G)])
         elif kind == "isum":
             per_spec.append([("isum", c, int(x)) if c else ("mom", 0, 0.0, 0.0, 0.0)
                              for c, x in zip(cnt_l, pt["sum"].cpu().tolist())])

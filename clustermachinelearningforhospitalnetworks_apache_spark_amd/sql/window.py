@@ -180,11 +180,11 @@ def _result_type(func, in_type: Optional[T.DataType]) -> T.DataType:
     fn = func.fn
     if fn in ("row_number", "rank", "dense_rank", "ntile"):
         return T.IntegerType()
-    if fn in ("percent_rank", "cume_dist", "avg", "stddev", "stddev_pop", "variance", "var_pop"):
+    if fn in ("percent_rank", "cume_dist", "avg", "try_avg", "stddev", "stddev_pop", "variance", "var_pop"):
         return T.DoubleType()
     if fn == "count":
         return T.LongType()
-    if fn == "sum":
+    if fn in ("sum", "try_sum"):
         return T.LongType() if in_type is not None and T.is_integral(in_type) else T.DoubleType()
     return in_type or T.DoubleType()
 
@@ -242,7 +242,7 @@ def _evaluate(func, spec: WindowSpec, pk, ok, arg, n: int) -> list:
             res = _rank_like(func, ov, [arg[i] for i in idx] if arg is not None else None, m)
         else:
             res = _frame_agg(fn, spec, ov, [arg[i] for i in idx] if arg is not None else [1] * m, m,
-                             count_star=func.child is None)
+                             count_star=func.child is None, ignore_nulls=getattr(func, "ignore_nulls", False))
         for j, i in enumerate(idx):
             out[i] = res[j]
     return out
@@ -340,9 +340,12 @@ def _frame_bounds(spec: WindowSpec, ov: list, m: int):
     return lo, hi
 
 
-def _frame_agg(fn: str, spec: WindowSpec, ov: list, vals: list, m: int, count_star: bool) -> list:
+def _frame_agg(fn: str, spec: WindowSpec, ov: list, vals: list, m: int, count_star: bool,
+               ignore_nulls: bool = False) -> list:
     lo, hi = _frame_bounds(spec, ov, m)
     present = np.array([v is not None for v in vals], dtype=bool)
+    try_sum = fn == "try_sum"
+    fn = {"try_sum": "sum", "try_avg": "avg"}.get(fn, fn)
     if fn in ("sum", "avg", "count"):
         if count_star:
             present = np.ones(m, dtype=bool)
@@ -351,9 +354,21 @@ def _frame_agg(fn: str, spec: WindowSpec, ov: list, vals: list, m: int, count_st
             return [int(cnt[h + 1] - cnt[l]) if h >= l else 0 for l, h in zip(lo, hi)]
         integral = all(isinstance(v, (int, np.integer)) and not isinstance(v, bool) for v in vals if v is not None)
         if fn == "sum" and integral:
-            acc = np.concatenate([[0], np.cumsum([int(v) if v is not None else 0 for v in vals], dtype=np.int64)])
-            return [int(acc[h + 1] - acc[l]) if h >= l and cnt[h + 1] - cnt[l] > 0 else None
-                    for l, h in zip(lo, hi)]
+            # exact prefix sums (Python ints); sum wraps to 64 bits, try_sum turns overflow into null
+            acc = [0]
+            for v in vals:
+                acc.append(acc[-1] + (int(v) if v is not None else 0))
+            out = []
+            for l, h in zip(lo, hi):
+                if h < l or cnt[h + 1] - cnt[l] == 0:
+                    out.append(None)
+                    continue
+                t = acc[h + 1] - acc[l]
+                if try_sum:
+                    out.append(t if -2 ** 63 <= t < 2 ** 63 else None)
+                else:
+                    out.append((t + 2 ** 63) % 2 ** 64 - 2 ** 63)
+            return out
         x = np.array([float(v) if v is not None else 0.0 for v in vals], dtype=np.float64)
         out = []
         for l, h in zip(lo, hi):
@@ -367,7 +382,9 @@ def _frame_agg(fn: str, spec: WindowSpec, ov: list, vals: list, m: int, count_st
     out = []
     for l, h in zip(lo, hi):
         seg = [v for v in vals[l:h + 1] if v is not None] if h >= l else []
-        if fn == "first":
+        if fn in ("first", "last") and ignore_nulls:
+            out.append((seg[0] if fn == "first" else seg[-1]) if seg else None)
+        elif fn == "first":
             out.append(vals[l] if h >= l else None)
         elif fn == "last":
             out.append(vals[h] if h >= l else None)

@@ -104,6 +104,8 @@ def device_window(frame, func, spec) -> Optional[ColumnData]:
     elif isinstance(func, AggExpr):
         if fn not in agg_fns or getattr(func, "custom", False) or func.distinct:
             return None
+        if getattr(func, "ignore_nulls", False):
+            return None  # first / last ignoreNulls over a frame: host path
     else:
         return None
     frame_spec = spec._frame
