@@ -739,6 +739,56 @@ __device__ __forceinline__ void add_raw8_f32(float (&acc)[CPL], const typename R
 template <int CPL, bool F8> struct SegRaw { using T = typename RawCols<CPL>::T; };
 template <int CPL> struct SegRaw<CPL, true> { using T = typename RawCols8<CPL>::T; };
 
+// Σ (x_j - c_j)² over this lane's CPL columns of a raw row (bf16 or e4m3 bytes), f32.
+template <int CPL, bool F8>
+__device__ __forceinline__ float sqdist_raw(const typename SegRaw<CPL, F8>::T& w, const float (&cv)[CPL]) {
+  const unsigned* ws = reinterpret_cast<const unsigned*>(&w);
+  float s = 0.f;
+  if constexpr (F8) {
+    typedef float f2 __attribute__((ext_vector_type(2)));
+#pragma unroll
+    for (int q = 0; q < CPL / 4; ++q) {
+      const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], false);
+      const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[q], true);
+      const float e0 = a.x - cv[4 * q], e1 = a.y - cv[4 * q + 1], e2 = b.x - cv[4 * q + 2], e3 = b.y - cv[4 * q + 3];
+      s = fmaf(e0, e0, s);
+      s = fmaf(e1, e1, s);
+      s = fmaf(e2, e2, s);
+      s = fmaf(e3, e3, s);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL / 2; ++q) {
+      const float e0 = bf16_to_f32((u16)(ws[q] & 0xffffu)) - cv[2 * q];
+      const float e1 = bf16_to_f32((u16)(ws[q] >> 16)) - cv[2 * q + 1];
+      s = fmaf(e0, e0, s);
+      s = fmaf(e1, e1, s);
+    }
+  }
+  return s;
+}
+
+// Wave total of v by DPP (quad swaps, half-row and row mirrors, row broadcasts 15 / 31): six vector
+// adds and no LDS traffic; the total is read from lane 63 into a scalar register.
+__device__ __forceinline__ float wave_total_dpp(float v) {
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));   // quad [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));   // quad [2,3,0,1]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x141, 0xf, 0xf, false));  // row_half_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x140, 0xf, 0xf, false));  // row_mirror
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));  // row_bcast15
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));  // row_bcast31
+  return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// Optional side output of the segmented accumulate (UB): ub[row] = an upper bound of |x - c_label|
+// over the bf16 centres `cb` (row stride ldc) the labels were assigned against — the exact-pruning
+// upper bound of every row, formed while the rows stream through (models/kmeans.py _step_seeded).
+struct SegUB {
+  const u16* cb;
+  long long ldc;
+  float* ub;
+};
+
 // Sort regime, pass 4: segmented sum over the label-sorted order. Wave w streams sorted
 // positions [w*chunk, (w+1)*chunk): ONE vector load fetches the next U row ids, U whole-row
 // gathers (CPL*2 bytes per lane) are in flight, the running sum stays in f64 registers, and
@@ -753,13 +803,13 @@ __device__ __forceinline__ long long seg_chunk(long long filled, long long waves
   return (filled + waves - 1) / waves;
 }
 
-template <int CPL, bool F8>
+template <int CPL, bool F8, bool UB = false>
 __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k,
                                                              double* __restrict__ msg, double* __restrict__ slots,
                                                              int* __restrict__ slot_c, const int* __restrict__ gate,
-                                                             int want) {
+                                                             int want, SegUB sub) {
   using raw_t = typename SegRaw<CPL, F8>::T;
   constexpr int U = 16;
   if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
@@ -796,9 +846,18 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
   double acc[CPL];
 #pragma unroll
   for (int j = 0; j < CPL; ++j) acc[j] = 0.0;
+  float cv[CPL];  // UB: this lane's columns of centre c
+  auto load_cv = [&](int cc) {
+#pragma unroll
+    for (int j = 0; j < CPL; ++j) cv[j] = active ? bf16_to_f32(sub.cb[(long long)cc * sub.ldc + col + j]) : 0.f;
+  };
+  if constexpr (UB) load_cv(c);
+  // f32 sum of <= 512 rounded squares of exact differences: relative error < 2^-14; rounded up
+  auto ub_of = [](float s) { return sqrtf(s * (1.0f + 1.0f / 8192.0f)) * (1.0f + 1e-6f); };
   for (long long p = p0; p < p1; p += U) {
     const int cnt = (int)(p1 - p < U ? p1 - p : U);
     const int pr = lane < cnt ? perm[p + lane] : 0;
+    float mine = 0.f;  // UB: squared distance of the batch's row `lane`
     raw_t w[U];
 #pragma unroll
     for (int u = 0; u < U; ++u) {
@@ -811,6 +870,14 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
     }
     const long long pe = p + cnt;
     if (next >= pe) {
+      if constexpr (UB) {
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+          const float t = wave_total_dpp(sqdist_raw<CPL, F8>(w[u], cv));
+          mine = lane == u ? t : mine;
+        }
+        if (lane < cnt) sub.ub[pr] = ub_of(mine);
+      }
       if constexpr (F8) {
         // e4m3 values are multiples of 2^-9 below 2^9: 16 of them sum EXACTLY in f32, so the rows
         // are added in f32 and folded into f64 once per batch (half the f64 adds and conversions)
@@ -846,12 +913,20 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
           ++c;
           next = seg[c + 1];
           while (next <= pos && c < k - 1) { ++c; next = seg[c + 1]; }
+          if constexpr (UB) load_cv(c);
         }
         const long long row = __builtin_amdgcn_readlane(pr, u);
         raw_t v = raw_t{};
         if (active) v = *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ);
+        if constexpr (UB) {
+          const float t = wave_total_dpp(sqdist_raw<CPL, F8>(v, cv));
+          mine = lane == u ? t : mine;
+        }
         if constexpr (F8) add_raw8<CPL>(acc, v);
         else add_raw<CPL>(acc, v);
+      }
+      if constexpr (UB) {
+        if (lane < cnt) sub.ub[pr] = ub_of(mine);
       }
     }
   }
@@ -1201,11 +1276,15 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
 // bound of the filled positions (the kernels clamp to seg[k]).
 int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, const int* perm, const int* seg, int k,
                   int cpl, int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate, int want,
-                  hipStream_t st) {
+                  hipStream_t st, SegUB sub = SegUB{nullptr, 0, nullptr}) {
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
-#define CML_SEG(C, F)                                                                                              \
-  hipLaunchKernelGGL((kmeans_segacc<C, F>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm, seg, \
-                     k, msg, slots, slot_c, gate, want)
+#define CML_SEG(C, F)                                                                                               \
+  if (sub.ub != nullptr)                                                                                            \
+    hipLaunchKernelGGL((kmeans_segacc<C, F, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D,    \
+                       perm, seg, k, msg, slots, slot_c, gate, want, sub);                                          \
+  else                                                                                                              \
+    hipLaunchKernelGGL((kmeans_segacc<C, F, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D,   \
+                       perm, seg, k, msg, slots, slot_c, gate, want, sub)
   if (xfp8) {
     if (cpl == 4) CML_SEG(4, true);
     else if (cpl == 8) CML_SEG(8, true);
@@ -1269,6 +1348,10 @@ CML_API int cml_kmeans_assign_rr_plan(int Dp, int kc, int kp, int xfp8, long lon
 }
 CML_API int cml_kmeans_set_rr_debug(int bits) {
   g_rr_dbg = bits;
+  return 0;
+}
+CML_API int cml_kmeans_set_rr_m32(int on) {
+  rr::g_m32 = on ? 1 : 0;
   return 0;
 }
 CML_API int cml_kmeans_set_rr_default(int on) {
@@ -1407,11 +1490,32 @@ CML_API int cml_kmeans_reduce(const float* slab, const int* cslab, const double*
 // Regime B: scan + scatter + segmented accumulate. `nblk`/`round_rows` describe the assign launch
 // that produced hist/rank (workgroup b ranked rows [b·round_rows + i·nblk·round_rows, +round_rows)). msg = [k*D sums | k counts | cost]. `seg` must hold k+1 ints plus
 // 2k+2 ints of scratch (cml_kmeans_seg_ints).
+static int sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels, const int* rank,
+                      const int* hist, int nblk, int round_rows, int k, int kp, const double* cost_part, int ncost,
+                      int* off, int* seg, int* perm, int cpl, int seg_grid, double* msg, double* slots, int* slot_c,
+                      int xfp8, const int* gate, void* stream, SegUB sub);
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                   const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
                                   int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
                                   void* stream) {
+  return sort_accum(X, n, ldx, Dp, D, labels, rank, hist, nblk, round_rows, k, kp, cost_part, ncost, off, seg, perm,
+                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{nullptr, 0, nullptr});
+}
+// The same, also writing ub[row] >= |x_row - cb[label]| (bf16 centres, row stride ldc) for every row.
+CML_API int cml_kmeans_sort_accum_ub(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
+                                     const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
+                                     const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
+                                     int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
+                                     const void* cb, long long ldc, float* ub, void* stream) {
+  if (cb == nullptr || ub == nullptr || ldc < Dp) return (int)hipErrorInvalidValue;
+  return sort_accum(X, n, ldx, Dp, D, labels, rank, hist, nblk, round_rows, k, kp, cost_part, ncost, off, seg, perm,
+                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{(const u16*)cb, ldc, ub});
+}
+static int sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels, const int* rank,
+                      const int* hist, int nblk, int round_rows, int k, int kp, const double* cost_part, int ncost,
+                      int* off, int* seg, int* perm, int cpl, int seg_grid, double* msg, double* slots, int* slot_c,
+                      int xfp8, const int* gate, void* stream, SegUB sub) {
   hipStream_t st = (hipStream_t)stream;
   long long* tot = reinterpret_cast<long long*>(seg + k + 1 + ((k + 1) & 1));  // scratch after seg (8-B aligned)
   const int want = 1;  // gated launches run on full-accumulate steps only
@@ -1431,7 +1535,7 @@ CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int
                      nblk, 1, round_rows, k, off, perm, gate, want);
   e = cml_status();
   if (e) return e;
-  return launch_segsum(X, n, ldx, Dp, D, perm, seg, k, cpl, seg_grid, msg, slots, slot_c, xfp8, gate, want, st);
+  return launch_segsum(X, n, ldx, Dp, D, perm, seg, k, cpl, seg_grid, msg, slots, slot_c, xfp8, gate, want, st, sub);
 }
 
 // ---- incremental sums (see kmeans_delta_gate). Per step, after the single-launch assign that

@@ -290,6 +290,44 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_lower_kernel(const floa
   }
 }
 
+
+// Bounds of the first Lloyd step seeded by the k-means|| init (models/kmeans.py _seed_from_init):
+// row x's nearest init candidate p = qmap[nearest[x]] lies within r = sqrt(cost + slack) of x, and p's
+// nearest / second-nearest centres are a(p) at d1(p) / d2(p) (exact f64 over the bf16 operands, rounded
+// outward), so |x - c_a| <= r + d1 and |x - c_j| >= d2 - r for every other j: label a(p), ub, lb.
+__global__ __launch_bounds__(256) void kmeans_seed_bounds_kernel(
+    const int* __restrict__ nearest, const float* __restrict__ cost, const float* __restrict__ xn,
+    const int* __restrict__ qmap, const int* __restrict__ a, const float* __restrict__ d1,
+    const float* __restrict__ d2, const float* __restrict__ pn, float tau, long long n, int* __restrict__ labels,
+    float* __restrict__ ub, float* __restrict__ lb) {
+  const long long row = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (row >= n) return;
+  const int q = qmap[nearest[row]];
+  const float r = sqrtf(fmaxf(cost[row], 0.f) + tau * (xn[row] + pn[q])) * (1.0f + 1e-6f);
+  labels[row] = a[q];
+  ub[row] = (r + d1[q]) * (1.0f + 1e-6f);
+  lb[row] = fmaxf(d2[q] - r, 0.f) * (1.0f - 1e-6f);
+}
+
+// Counting-sort ranks of the current labels in the K9r workgroup geometry (row -> workgroup
+// (row / tr) % grid), for a full accumulate after a step that ran only the candidate pass:
+// hist[b][label] and rank[row] = the row's position among its workgroup's rows of that label.
+// 1024 threads = 1024 / tr of the workgroup's tiles per sweep (tr <= 1024 rows per tile).
+__global__ __launch_bounds__(1024) void kmeans_label_hist_kernel(const int* __restrict__ labels, long long n, int tr,
+                                                                 int kp, int* __restrict__ hist,
+                                                                 int* __restrict__ rank) {
+  extern __shared__ int h[];
+  for (int i = threadIdx.x; i < kp; i += 1024) h[i] = 0;
+  __syncthreads();
+  const int per = 1024 / tr, t = threadIdx.x / tr, i = threadIdx.x % tr;
+  for (long long j0 = 0; ((long long)blockIdx.x + j0 * gridDim.x) * tr < n; j0 += per) {
+    const long long row = ((long long)blockIdx.x + (j0 + t) * gridDim.x) * tr + i;
+    if (t < per && row < n) rank[row] = atomicAdd(&h[labels[row]], 1);
+  }
+  __syncthreads();
+  for (int i2 = threadIdx.x; i2 < kp; i2 += 1024) hist[(long long)blockIdx.x * kp + i2] = h[i2];
+}
+
 }  // namespace
 
 CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, const float* xn, float mc, float tau,
@@ -341,5 +379,22 @@ CML_API int cml_kmeans_centre_stats(const void* cb, const void* cb_old, long lon
                      (const u16*)cb, (const u16*)cb_old, ldc, k, d, cn, drift, half);
   hipLaunchKernelGGL(kmeans_centre_stats2_kernel, dim3(1), dim3(256), 0, st, cn, half, drift, k, mx, tau,
                      cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force);
+  return cml_status();
+}
+
+CML_API int cml_kmeans_seed_bounds(const int* nearest, const float* cost, const float* xn, const int* qmap,
+                                   const int* a, const float* d1, const float* d2, const float* pn, float tau,
+                                   long long n, int* labels, float* ub, float* lb, void* stream) {
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(kmeans_seed_bounds_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     nearest, cost, xn, qmap, a, d1, d2, pn, tau, n, labels, ub, lb);
+  return cml_status();
+}
+
+CML_API int cml_kmeans_label_hist(const int* labels, long long n, int tr, int grid, int kp, int* hist, int* rank,
+                                  void* stream) {
+  if (tr <= 0 || tr > 1024 || grid <= 0 || kp <= 0 || (size_t)kp * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_label_hist_kernel, dim3(grid), dim3(1024), (size_t)kp * 4, (hipStream_t)stream, labels,
+                     n, tr, kp, hist, rank);
   return cml_status();
 }

@@ -71,7 +71,9 @@ struct Ext {
   int want;
 };
 
-template <int DP, bool F8 = false, int MODE = 0>
+__host__ __device__ constexpr int cn_slots(int kp) { return ((kp + 3) & ~3) > 256 ? ((kp + 3) & ~3) : 256; }
+
+template <int DP, bool F8 = false, int MODE = 0, bool M32 = false>
 struct Geo {
   static constexpr int KS = DP / 32;            // MFMA k-steps per row
   static constexpr int ROWB = F8 ? DP : DP * 2; // bytes per row (bf16, or OCP e4m3fn bytes)
@@ -88,20 +90,31 @@ struct Geo {
   static constexpr int CNT1 = PIECES / 2 + (NARR - 1) * TRAIL_Q;
   static constexpr int TRB = TR * 4 * NARR;     // trailer entry bytes
   static constexpr int NK = MODE >= 1 ? 2 : 1;  // keys per (row, wave, lane group)
-  static constexpr int STRIDE = 16 * NK + 1;    // dwords per row of the key exchange (+1: conflict-free writes)
+  // key entries per row: (compute wave, lane group) = 4 x 4 for the 16x16 MFMA tiles, 4 x 2 (lane
+  // halves) for the 32x32 ones
+  static constexpr int NQ = M32 ? 8 : 16;
+  static constexpr int STRIDE = NQ * NK + 1;    // dwords per row of the key exchange (+1: conflict-free writes)
   static constexpr int RED = TR * STRIDE * 4;
+  // M32: the finalize waves run two tiles behind the compute waves (the last sub-tile's keys of tile j
+  // are formed during tile j+1), so keys are triple-buffered and the trailer ring is one entry deeper;
+  // the centre norms sit in LDS (kp floats) instead of registers
+  static constexpr int LAG = M32 ? 2 : 1;
+  static constexpr int NKB = LAG + 1;           // key exchange buffers
   static constexpr long long fixed_bytes(int ns, int kp) {
-    return (long long)(ns + 1) * TRB + 2LL * RED + 4LL * ((kp + 3) & ~3) + 64;
+    // (M32) the centre norms cover every centre slot a compute wave reads (4 waves x 64), padded with +inf
+    const long long kp4 = (kp + 3) & ~3;
+    return (long long)(ns + LAG) * TRB + (long long)NKB * RED + 4LL * kp4 + (M32 ? 4LL * cn_slots(kp) : 0LL) + 64;
   }
   // ring depth: 4 slots where LDS allows, 3 for the 128-row tiles of the top-2 modes
   static constexpr int NS = (4LL * SLOT + fixed_bytes(4, 1024)) <= 160 * 1024 ? 4 : 3;
-  static constexpr int NTR = NS + 1;            // trailer ring entries
+  static constexpr int NTR = NS + LAG;          // trailer ring entries
 };
 
-// LDS layout (bytes): [X ring NS*SLOT | trailers NTR*TRB | keys 2*RED | hist kp ints | misc 64 B]
-template <int DP, bool F8 = false, int MODE = 0>
+// LDS layout (bytes): [X ring NS*SLOT | trailers NTR*TRB | keys NKB*RED | hist kp ints | (M32) centre
+// norms kp floats | misc 64 B]
+template <int DP, bool F8 = false, int MODE = 0, bool M32 = false>
 __host__ __device__ constexpr long long lds_bytes(int kp) {
-  using G = Geo<DP, F8, MODE>;
+  using G = Geo<DP, F8, MODE, M32>;
   return (long long)G::NS * G::SLOT + G::fixed_bytes(G::NS, kp);
 }
 
@@ -139,12 +152,12 @@ __device__ __forceinline__ int med3(int a, int b, int c) {
 }
 
 // ldx in BYTES; rows are 16-B aligned. Positions past n load row n-1 (discarded).
-template <int DP, bool F8, int MODE>
+template <int DP, bool F8, int MODE, bool M32>
 __device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, long long ldx, long long n,
                                            const float* __restrict__ xnorm, const int* __restrict__ labels,
                                            const int* __restrict__ idx, long long tile, int slot, int tr, int dw,
                                            int lane, unsigned char* smem) {
-  using G = Geo<DP, F8, MODE>;
+  using G = Geo<DP, F8, MODE, M32>;
   const long long row0 = tile * G::TR;
   unsigned char* sdst = smem + slot * G::SLOT;
   if constexpr (MODE == 2) {
@@ -216,11 +229,186 @@ __device__ __forceinline__ void issue_tile(const unsigned char* __restrict__ X, 
   }
 }
 
+// Compute waves on 32x32 MFMA tiles (v_mfma_f32_32x32x16_bf16), CT even: wave w holds centres
+// [w·16CT, (w+1)·16CT) as NT = CT/2 A tiles of 32 centres; a 32-row sub-tile of X is the B operand
+// (lane: row l&31, k half l>>5), so every output lane holds ONE X row against 16 centres per tile.
+// Why: with 16x16 tiles the key epilogue (and-or tag, min3, med3) and the accumulator seeding filled
+// every vector-issue slot the 16-cycle MFMAs leave (2-3 vector instructions per MFMA, ISA count of
+// the steady loop), so the pass ran at ~60 % of MFMA peak even without HBM traffic; a 32x32x16 MFMA
+// holds vector issue for 8 of its 32 cycles, so the same epilogue per output fits beside it.
+// Accumulators start at ||c||² (read from LDS into the free buffer during the previous sub-tile's
+// second half); ||x||² (one value per lane) is added when the keys are formed, in the first half of
+// the NEXT sub-tile's k-steps — across tiles too, so tile j's last keys land during tile j+1 and the
+// finalize waves run two tiles behind (Geo::LAG). Tags: a·16 + reg (increasing with the centre index
+// for a lane, ties to the lowest centre); the finalize decodes centre = w·16CT + 32a + (reg&3) +
+// 8(reg>>2) + 4h.
+template <int DP, int CT, bool F8, int MODE>
+__device__ __forceinline__ void compute_m32(const u16* __restrict__ C, long long ldc, int kc, long long nt,
+                                            int wave, int lane, unsigned char* smem, const float* cnl, int dbg) {
+  using G = Geo<DP, F8, MODE, true>;
+  constexpr int NT = CT / 2;            // 32-centre A tiles per wave
+  constexpr int KS2 = DP / 16;          // 32x32x16 k-steps per row
+  constexpr int SPU = F8 ? 2 : 1;       // k-steps per 16-B LDS read unit
+  constexpr int UPS = KS2 / SPU;        // read units per sub-tile
+  constexpr int NSUB = G::TR / 32;      // 32-row sub-tiles per tile (even)
+  constexpr int NU = NSUB * UPS;
+  constexpr int NE = NT * 16;           // key elements per lane per sub-tile
+  constexpr int HALF = KS2 / 2 < NE / 2 ? KS2 / 2 : NE / 2;  // keys are formed in the first HALF k-steps
+  constexpr int EPS = NE / HALF;        // key elements per k-step (even)
+  constexpr int TAGB = 4 + (NT > 1);
+  constexpr int TAGM = (1 << TAGB) - 1;
+  constexpr bool TOP2 = MODE >= 1;
+  constexpr int PF = 2;
+  static_assert(NSUB % 2 == 0 && NE % HALF == 0 && EPS % 2 == 0, "M32 geometry");
+  unsigned char* trail = smem + G::NS * G::SLOT;
+  int* red = reinterpret_cast<int*>(trail + G::NTR * G::TRB);
+  const int r = lane & 31, hh = lane >> 5;
+  const int cw0 = wave * (CT * 16);
+  bf16x8 creg[NT][KS2];
+#pragma unroll
+  for (int a = 0; a < NT; ++a) {
+    const int c = cw0 + 32 * a + r;
+#pragma unroll
+    for (int s = 0; s < KS2; ++s) {
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      // bf16: step s, lane half h holds k = 16s + 8h + j; fp8: the 16-B unit v = s/2 of lane half h
+      // holds k = 32v + 16h + (0..15), its low / high 8 are steps 2v / 2v+1
+      const int k0 = F8 ? 32 * (s >> 1) + 16 * hh + 8 * (s & 1) : 16 * s + 8 * hh;
+      if (c < kc) v = *reinterpret_cast<const uint4*>(C + (long long)c * ldc + k0);
+      const unsigned w4[4] = {v.x, v.y, v.z, v.w};
+      unsigned o[4];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {  // x -2, exact
+        const float lo = -2.f * bf16_to_f32((u16)(w4[e] & 0xffffu));
+        const float hi = -2.f * bf16_to_f32((u16)(w4[e] >> 16));
+        o[e] = (unsigned)f32_to_bf16(lo) | ((unsigned)f32_to_bf16(hi) << 16);
+      }
+      creg[a][s] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+    }
+  }
+  __builtin_amdgcn_s_setprio(1);
+  // B fragment of unit v, sub-tile t: row 32t + r, 16-B chunk 2v + h stored at (2v + h) ^ (r & 15)
+  int boff[8];
+#pragma unroll
+  for (int m = 0; m < 8; ++m) boff[m] = r * G::ROWB + (((2 * m + hh) ^ (r & 15)) << 4);
+  const float* cnp = cnl + cw0 + 4 * hh;
+  auto load_cn = [&](f32x16(&dst)[NT]) {
+#pragma unroll
+    for (int a = 0; a < NT; ++a)
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const f32x4 v = *reinterpret_cast<const f32x4*>(cnp + 32 * a + 8 * q);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) dst[a][4 * q + i] = v[i];
+      }
+  };
+  f32x16 acc[2][NT];
+  wait_lgkm0();
+  barrier();  // B(-1): first tile landed, centre norms in LDS
+  load_cn(acc[0]);
+  int key = 0x7fffffff, key2 = 0x7fffffff;
+  // forms key elements [e0, e1) of the pending sub-tile (accumulators pa, row norm xv)
+  auto keys = [&](const f32x16(&pa)[NT], float xv, int e0, int e1) {
+#pragma unroll
+    for (int e = e0; e < e1; e += 2) {
+      const int a = e >> 4, i = e & 15;
+      typedef float f32x2 __attribute__((ext_vector_type(2)));
+      const f32x2 v = f32x2{pa[a][i], pa[a][i + 1]} + f32x2{xv, xv};  // one v_pk_add_f32
+      const int k0 = (__float_as_int(v[0]) & ~TAGM) | (a << 4 | i);
+      const int k1 = (__float_as_int(v[1]) & ~TAGM) | (a << 4 | (i + 1));
+      if constexpr (TOP2) {
+        key2 = med3(key, k0, key2);
+        key = k0 < key ? k0 : key;
+        key2 = med3(key, k1, key2);
+        key = k1 < key ? k1 : key;
+      } else {
+        const int m = k0 < k1 ? k0 : k1;
+        key = m < key ? m : key;
+      }
+    }
+  };
+  auto put_keys = [&](int* kred, int row) {
+    kred[row * G::STRIDE + wave * 2 + hh] = key;
+    if constexpr (TOP2) kred[row * G::STRIDE + 8 + wave * 2 + hh] = key2;
+    key = 0x7fffffff;
+    key2 = 0x7fffffff;
+  };
+  for (long long j = 0; j < nt; ++j) {
+    if (dbg & 2) {
+      wait_lgkm0();
+      barrier();
+      continue;
+    }
+    const unsigned char* xs = smem + (int)(j % G::NS) * G::SLOT;
+    const float* tn = reinterpret_cast<const float*>(trail + (int)(j % G::NTR) * G::TRB);
+    const float* tnp = reinterpret_cast<const float*>(trail + (int)((j + G::NTR - 1) % G::NTR) * G::TRB);
+    int* kr = red + (int)(j % G::NKB) * G::TR * G::STRIDE;
+    int* krp = red + (int)((j + G::NKB - 1) % G::NKB) * G::TR * G::STRIDE;
+    auto xaddr = [&](int u) {
+      const int t = u / UPS, v = u % UPS;
+      return xs + 32 * t * G::ROWB + 256 * (v >> 3) + boff[v & 7];
+    };
+    uint4 xr[PF + 1];
+#pragma unroll
+    for (int u = 0; u < PF && u < NU; ++u) xr[u] = *reinterpret_cast<const uint4*>(xaddr(u));
+    // the pending sub-tile at t = 0 is the previous tile's last one (none before the first tile)
+    float xpend = j > 0 ? tnp[32 * (NSUB - 1) + r] : 0.f;
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int t = u / UPS, v = u % UPS, cur = t & 1, prv = cur ^ 1;
+      if (u + PF < NU) xr[(u + PF) % (PF + 1)] = *reinterpret_cast<const uint4*>(xaddr(u + PF));
+      if (v == 0 && t > 0) xpend = tn[32 * (t - 1) + r];
+      bf16x8 xb[SPU];
+      if constexpr (F8) {
+        const uint4 w = xr[u % (PF + 1)];
+        const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+        unsigned o[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) {
+          o[2 * q] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(ws[q], 1.0f, false));
+          o[2 * q + 1] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(ws[q], 1.0f, true));
+        }
+        xb[0] = __builtin_bit_cast(bf16x8, make_uint4(o[0], o[1], o[2], o[3]));
+        xb[SPU - 1] = __builtin_bit_cast(bf16x8, make_uint4(o[4], o[5], o[6], o[7]));
+      } else {
+        xb[0] = __builtin_bit_cast(bf16x8, xr[u % (PF + 1)]);
+      }
+#pragma unroll
+      for (int h = 0; h < SPU; ++h) {
+        const int s = v * SPU + h;
+#pragma unroll
+        for (int a = 0; a < NT; ++a)
+          acc[cur][a] = __builtin_amdgcn_mfma_f32_32x32x16_bf16(creg[a][s], xb[h], acc[cur][a], 0, 0, 0);
+        const bool pending = t > 0 || j > 0;
+        if (s < HALF) {
+          if (pending) keys(acc[prv], xpend, s * EPS, (s + 1) * EPS);
+          if (s == HALF - 1 && pending) {
+            if (t > 0) put_keys(kr, 32 * (t - 1) + r);
+            else put_keys(krp, 32 * (NSUB - 1) + r);
+          }
+        } else if (s == HALF) {
+          load_cn(acc[prv]);  // seeds of the next sub-tile (its accumulators are free now)
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    wait_lgkm0();
+    barrier();  // B(j)
+  }
+  if (nt > 0 && !(dbg & 2)) {  // keys of the very last sub-tile (accumulator parity (NSUB-1)&1 = 1)
+    const float* tn = reinterpret_cast<const float*>(trail + (int)((nt - 1) % G::NTR) * G::TRB);
+    keys(acc[1], tn[32 * (NSUB - 1) + r], 0, NE);
+    put_keys(red + (int)((nt - 1) % G::NKB) * G::TR * G::STRIDE, 32 * (NSUB - 1) + r);
+  }
+  wait_lgkm0();
+  barrier();  // B(nt)
+}
+
 // F8: X rows are OCP e4m3fn bytes (SURVEY config 5). They travel through the ring as bytes (half the
 // HBM and LDS traffic) and every compute wave widens its fragments with v_cvt_scalef32_pk_bf16_fp8
 // (exact: e4m3 values are a subset of bf16); one 16-B read then covers TWO k-steps, step 2v+h of lane
 // (r, g) holding k = 64v + 16g + 8h + j, and the centre fragments follow the same k order.
-template <int DP, int CT, bool F8, int MODE>
+template <int DP, int CT, bool F8, int MODE, bool M32>
 __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     const unsigned char* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc, int kc,
     int kp, const float* __restrict__ cnorm, const float* __restrict__ xnorm, int* __restrict__ labels,
@@ -228,7 +416,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     int* __restrict__ rank_out, DeltaOut dout, Ext ext, int dbg) {
   // dbg (ablation only, 0 in production): bit 0 DMA waves issue nothing, bit 1 compute waves skip
   // their MFMAs/keys, bit 2 finalize waves skip the epilogue
-  using G = Geo<DP, F8, MODE>;
+  using G = Geo<DP, F8, MODE, M32>;
   constexpr int KS = G::KS;
   constexpr int NS = G::NS;
   constexpr int CPW = CT * 16;  // centres per compute wave
@@ -241,8 +429,10 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
   unsigned char* trail = smem + NS * G::SLOT;
   int* red = reinterpret_cast<int*>(trail + G::NTR * G::TRB);
-  int* hist = red + 2 * G::TR * G::STRIDE;
-  int* misc = hist + ((kp + 3) & ~3);  // [0] change counter, [2..5] two f64 cost partials
+  int* hist = red + G::NKB * G::TR * G::STRIDE;
+  float* cnl = reinterpret_cast<float*>(hist + ((kp + 3) & ~3));  // M32: centre norms [cn_slots(kp)]
+  int* misc = M32 ? reinterpret_cast<int*>(cnl + cn_slots(kp)) : hist + ((kp + 3) & ~3);
+  // misc: [0] change counter, [2..5] two f64 cost partials
   double* cost_sh = reinterpret_cast<double*>(misc + 2);
 
   // the role index is wave-uniform: readfirstlane lets the compiler branch on it with scalar
@@ -254,6 +444,10 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   auto tile_of = [&](long long j) { return (long long)blockIdx.x + j * gridDim.x; };
 
   if (wave < kCompute) {
+   if constexpr (M32) {
+    for (int i = tid; i < cn_slots(kp); i += kCompute * 64) cnl[i] = i < kc ? cnorm[i] : __builtin_huge_valf();
+    compute_m32<DP, CT, F8, MODE>(C, ldc, kc, nt, wave, lane, smem, cnl, dbg);
+   } else {
     // ------------------------------------------------------------------ compute waves
     const int r = lane & 15, g = lane >> 4;
     const int cw0 = wave * CPW;
@@ -380,11 +574,12 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       wait_lgkm0();
       barrier();  // B(j)
     }
+   }
   } else if (wave < kCompute + 2) {
     // ------------------------------------------------------------------ LDS-DMA waves
     const int dw = wave - kCompute;
     for (long long j = 0; j < NS - 1 && j < nt && !(dbg & 1); ++j)
-      issue_tile<DP, F8, MODE>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(j), (int)j, (int)j, dw, lane, smem);
+      issue_tile<DP, F8, MODE, M32>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(j), (int)j, (int)j, dw, lane, smem);
     if (nt >= NS - 1) {
       if (dw == 0) wait_vm<(NS - 2) * G::CNT0>();
       else wait_vm<(NS - 2) * G::CNT1>();
@@ -395,8 +590,8 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     for (long long j = 0; j < nt; ++j) {
       const long long jn = j + NS - 1;
       if (jn < nt && !(dbg & 1)) {
-        issue_tile<DP, F8, MODE>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(jn), (int)(jn % NS),
-                                 (int)(jn % G::NTR), dw, lane, smem);
+        issue_tile<DP, F8, MODE, M32>(X, ldx, n, xnorm, lab_src, ext.idx, tile_of(jn), (int)(jn % NS),
+                                      (int)(jn % G::NTR), dw, lane, smem);
         // tile j+1 has landed; j+2 .. j+NS-1 stay in flight
         if (dw == 0) wait_vm<(NS - 2) * G::CNT0>();
         else wait_vm<(NS - 2) * G::CNT1>();
@@ -405,6 +600,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       }
       barrier();  // B(j)
     }
+    if constexpr (M32) barrier();  // B(nt)
   } else {
     // ------------------------------------------------------------------ finalize waves
     const int fw = wave - kCompute - 2;
@@ -419,10 +615,10 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     // LPR_F lanes per row, each taking 16 / LPR_F of the 16 (wave, lane-group) keys; keys are loaded
     // in one batch and reduced branch-free on a 64-bit (value, centre index) composite
     constexpr int LPR_F = 64 / RPF;
-    constexpr int QPL = 16 / LPR_F;
+    constexpr int QPL = G::NQ / LPR_F;
     const int rl = lane % RPF, part = lane / RPF;
     auto finalize = [&](long long j) {
-      const int* kr = red + (int)(j & 1) * G::TR * G::STRIDE;
+      const int* kr = red + (int)(j % G::NKB) * G::TR * G::STRIDE;
       const unsigned char* te = trail + (int)(j % G::NTR) * G::TRB;
       const int R = fw * RPF + rl;
       const long long pos = tile_of(j) * G::TR + R;
@@ -430,7 +626,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
 #pragma unroll
       for (int q = 0; q < QPL; ++q) {
         kv[q] = kr[R * G::STRIDE + part * QPL + q];
-        if constexpr (TOP2) kv2[q] = kr[R * G::STRIDE + 16 + part * QPL + q];
+        if constexpr (TOP2) kv2[q] = kr[R * G::STRIDE + G::NQ + part * QPL + q];
       }
       const int old = reinterpret_cast<const int*>(te + G::TR * 4)[R];
       long long row = pos;
@@ -438,15 +634,23 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       unsigned long long best = ~0ull;
       unsigned sec = ~0u;  // TOP2: second smallest value, order-preserving unsigned form
 #pragma unroll
-      for (int q = 0; q < QPL; ++q) {  // qq = w*4 + g: centres w*CPW + ct*16 + 4g + i
+      for (int q = 0; q < QPL; ++q) {
         const int qq = part * QPL + q;
-        const int tag = kv[q] & TAGM;
-        const unsigned idx = (unsigned)((qq >> 2) * CPW + (qq & 3) * 4 + (tag >> 2) * 16 + (tag & 3));
-        const unsigned u1 = (unsigned)(kv[q] & ~TAGM) ^ 0x80000000u;
+        unsigned idx;
+        if constexpr (M32) {  // qq = w*2 + h, tag = a*16 + reg: centre w*CPW + 32a + (reg&3) + 8(reg>>2) + 4h
+          const int tag = kv[q] & ((1 << (4 + (CT > 2))) - 1);
+          const int rg = tag & 15;
+          idx = (unsigned)((qq >> 1) * CPW + 32 * (tag >> 4) + (rg & 3) + 8 * (rg >> 2) + 4 * (qq & 1));
+        } else {  // qq = w*4 + g: centres w*CPW + ct*16 + 4g + i
+          const int tag = kv[q] & TAGM;
+          idx = (unsigned)((qq >> 2) * CPW + (qq & 3) * 4 + (tag >> 2) * 16 + (tag & 3));
+        }
+        const int tagm = M32 ? ((1 << (4 + (CT > 2))) - 1) : TAGM;
+        const unsigned u1 = (unsigned)(kv[q] & ~tagm) ^ 0x80000000u;
         const unsigned long long c = ((unsigned long long)u1 << 32) | idx;
         if constexpr (TOP2) {
           // second of the union = min(larger of the two firsts, smaller of the two seconds)
-          const unsigned u2 = (unsigned)(kv2[q] & ~TAGM) ^ 0x80000000u;
+          const unsigned u2 = (unsigned)(kv2[q] & ~tagm) ^ 0x80000000u;
           const unsigned bv = (unsigned)(best >> 32);
           const unsigned mx = u1 > bv ? u1 : bv;
           const unsigned s2 = u2 < sec ? u2 : sec;
@@ -501,10 +705,16 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     };
     wait_lgkm0();
     barrier();  // B(-1)
+    constexpr int LAG = G::LAG;  // tile j's keys are complete at B(j + LAG - 1)
     for (long long j = 0; j < nt; ++j) {
-      if (j > 0 && !(dbg & 4)) finalize(j - 1);
+      if (j >= LAG && !(dbg & 4)) finalize(j - LAG);
       wait_lgkm0();
       barrier();  // B(j)
+    }
+    if constexpr (LAG == 2) {
+      if (nt >= 2 && !(dbg & 4)) finalize(nt - 2);
+      wait_lgkm0();
+      barrier();  // B(nt)
     }
     if (nt > 0 && !(dbg & 4)) finalize(nt - 1);
     cost = wave_sum_f64(cost);
@@ -539,45 +749,60 @@ inline int plan_ct(int Dp, int kc, bool f8 = false) {
   return c;
 }
 
-template <int MODE>
+inline int tile_rows(int Dp, bool f8 = false) { return Dp > 0 ? 32768 / ((f8 ? 1 : 2) * Dp) : 0; }
+
+// 32x32 MFMA compute waves (compute_m32) for even CT where a tile holds an even number of 32-row
+// sub-tiles (not bf16 D = 512), selected by cml_kmeans_set_rr_m32(1) / CML_KMEANS_RR_M32=1. Off by
+// default: measured on MI355X (profiles/r3/k9r_m32_vs_m16.txt) the 16x16 form is faster — 2.45 vs
+// 2.71 ms for 20M x 256, k = 256 — because the pass is bound by the MFMA pipe under the power-limited
+// clock (MFMA-only ablation 1.86 ms either way), not by vector issue slots.
+inline int g_m32 = 0;
+inline bool use_m32(int Dp, int ct, bool f8) {
+  const int tr = tile_rows(Dp, f8);
+  return g_m32 && (ct == 2 || ct == 4) && tr >= 64 && (tr / 32) % 2 == 0;
+}
+
+template <int MODE, bool M32>
 inline long long lds_for_mode(int Dp, int kp, bool f8) {
   if (f8) {
     switch (Dp) {
-      case 256: return lds_bytes<256, true, MODE>(kp);
-      case 512: return lds_bytes<512, true, MODE>(kp);
+      case 256: return lds_bytes<256, true, MODE, M32>(kp);
+      case 512: return lds_bytes<512, true, MODE, M32>(kp);
       default: return 0;
     }
   }
   switch (Dp) {
-    case 128: return lds_bytes<128, false, MODE>(kp);
-    case 256: return lds_bytes<256, false, MODE>(kp);
-    case 512: return lds_bytes<512, false, MODE>(kp);
+    case 128: return lds_bytes<128, false, MODE, M32>(kp);
+    case 256: return lds_bytes<256, false, MODE, M32>(kp);
+    case 512: return lds_bytes<512, false, MODE, M32>(kp);
     default: return 0;
   }
 }
 
 inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
-  switch (mode) {
-    case 0: return lds_for_mode<0>(Dp, kp, f8);
-    case 1: return lds_for_mode<1>(Dp, kp, f8);
-    case 2: return lds_for_mode<2>(Dp, kp, f8);
+  const bool m32 = use_m32(Dp, plan_ct(Dp, kp, f8), f8);
+  switch (mode * 2 + (m32 ? 1 : 0)) {
+    case 0: return lds_for_mode<0, false>(Dp, kp, f8);
+    case 1: return lds_for_mode<0, true>(Dp, kp, f8);
+    case 2: return lds_for_mode<1, false>(Dp, kp, f8);
+    case 3: return lds_for_mode<1, true>(Dp, kp, f8);
+    case 4: return lds_for_mode<2, false>(Dp, kp, f8);
+    case 5: return lds_for_mode<2, true>(Dp, kp, f8);
     default: return 0;
   }
 }
 
-inline int tile_rows(int Dp, bool f8 = false) { return Dp > 0 ? 32768 / ((f8 ? 1 : 2) * Dp) : 0; }
-
 // X: bf16 rows (ldx elements) or, with f8, e4m3fn rows (ldx bytes).
-template <int DP, int CT, bool F8, int MODE>
+template <int DP, int CT, bool F8, int MODE, bool M32>
 int launch(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp, const float* cnorm,
            const float* xnorm, int* labels, float* best, double* cost_part, int* hist, int* rank, DeltaOut dout,
            Ext ext, int grid, int dbg, hipStream_t st) {
-  const size_t lds = (size_t)lds_bytes<DP, F8, MODE>(kp);
+  const size_t lds = (size_t)lds_bytes<DP, F8, MODE, M32>(kp);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8, MODE>;
+  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8, MODE, M32>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const long long ldb = F8 ? ldx : 2 * ldx;
-  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8, MODE>), dim3(grid), dim3(kThreads), lds, st,
+  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8, MODE, M32>), dim3(grid), dim3(kThreads), lds, st,
                      (const unsigned char*)X, n, ldb, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist,
                      rank, dout, ext, dbg);
   return cml_status();
@@ -588,15 +813,22 @@ inline int dispatch_mode(int Dp, int ct, bool f8, const void* X, long long n, lo
                          long long ldc, int kc, int kp, const float* cnorm, const float* xnorm, int* labels,
                          float* best, double* cost_part, int* hist, int* rank, DeltaOut dout, Ext ext, int grid,
                          int dbg, hipStream_t st) {
-#define CML_RR(D, T, F)                                                                                            \
-  if (Dp == D && ct == T && f8 == F)                                                                               \
-  return launch<D, T, F, MODE>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank, dout, \
-                               ext, grid, dbg, st)
-  CML_RR(128, 1, false); CML_RR(128, 2, false); CML_RR(128, 3, false); CML_RR(128, 4, false); CML_RR(128, 5, false);
-  CML_RR(256, 1, false); CML_RR(256, 2, false); CML_RR(256, 3, false); CML_RR(256, 4, false); CML_RR(256, 5, false);
-  CML_RR(512, 1, false); CML_RR(512, 2, false);
-  CML_RR(256, 1, true); CML_RR(256, 2, true); CML_RR(256, 3, true); CML_RR(256, 4, true);
-  CML_RR(512, 1, true); CML_RR(512, 2, true);
+  const bool m32 = use_m32(Dp, ct, f8);
+#define CML_RR(D, T, F, M)                                                                                          \
+  if (Dp == D && ct == T && f8 == F && m32 == M)                                                                    \
+  return launch<D, T, F, MODE, M>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank,    \
+                                  dout, ext, grid, dbg, st)
+  CML_RR(128, 1, false, false); CML_RR(128, 2, false, false); CML_RR(128, 3, false, false);
+  CML_RR(128, 4, false, false); CML_RR(128, 5, false, false);
+  CML_RR(256, 1, false, false); CML_RR(256, 2, false, false); CML_RR(256, 3, false, false);
+  CML_RR(256, 4, false, false); CML_RR(256, 5, false, false);
+  CML_RR(512, 1, false, false); CML_RR(512, 2, false, false);
+  CML_RR(256, 1, true, false); CML_RR(256, 2, true, false); CML_RR(256, 3, true, false); CML_RR(256, 4, true, false);
+  CML_RR(512, 1, true, false); CML_RR(512, 2, true, false);
+  CML_RR(128, 2, false, true); CML_RR(128, 4, false, true);
+  CML_RR(256, 2, false, true); CML_RR(256, 4, false, true);
+  CML_RR(256, 2, true, true); CML_RR(256, 4, true, true);
+  CML_RR(512, 2, true, true);
 #undef CML_RR
   return (int)hipErrorInvalidValue;
 }

@@ -327,12 +327,20 @@ class LloydEngine:
             self.centers = c.contiguous().clone()
         if self.gpu:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+        seed, self._seed = getattr(self, "_seed", None), None
         if self._pdev:  # bounds and incremental sums were relative to the old centres: a full step next
             st = self._pst
             K.centre_stats(self.cb, None, self.k, self.d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax,
                            st.mc, st.c2, st.count, st.force)
-            st.force.fill_(1)
             self.delta.invalidate()
+            # centres straight from this engine's k-means|| init: the first step starts from bounds the
+            # init already implies (no full assign pass); anything else takes a full step
+            self._seeded = (seed is not None and seed.out.shape == tuple(c.shape) and
+                            np.array_equal(seed.out, np.asarray(centers, dtype=np.float64)))
+            if self._seeded:
+                self._seed_from_init(seed)
+            else:
+                st.force.fill_(1)
         elif self._pst is not None:  # bounds were relative to the old centres
             self._pst.valid = False
             self._prune_centre_stats()
@@ -342,7 +350,10 @@ class LloydEngine:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
         self._ensure_norms()
         if self._pdev:
-            if self.use_graph:
+            if getattr(self, "_seeded", False):
+                self._seeded = False
+                self._step_seeded()
+            elif self.use_graph:
                 self._step_graph()
             else:
                 self._step_prune_dev()
@@ -491,10 +502,10 @@ class LloydEngine:
         st.mc = torch.zeros(1, dtype=torch.float32, device=dev)
         st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
         st.mx = torch.zeros(1, dtype=torch.float32, device=dev)  # max ||x||² over all ranks (_ensure_norms)
-        if self._norms_ready:
-            self._set_mx()
         st.cb_old = torch.zeros_like(self.cb)
         self._pst = st
+        if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
+            self._set_mx()
         self.delta = K.DeltaState(max(n, 1), k, d, self.dp, 1, self.msg_len, dev, ap.grid, fp8=K.is_fp8(self.x),
                                   cap=max(st.cap_m, 1024), pcap=max(per_wg, 64))
 
@@ -522,6 +533,73 @@ class LloydEngine:
         dl.gate(0)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0])
+        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
+        self.comm.allreduce_async(msg).wait()
+        st.cb_old.copy_(self.cb)
+        self._update_gpu(self.msgs)
+        K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
+                       st.c2, st.count, st.force)
+        self._cost_fn = self._pdev_cost
+
+    def _seed_from_init(self, sd) -> None:
+        """Labels and bounds of every row from the k-means|| init (kmeans_seed_bounds): row x's nearest
+        candidate p is within r = sqrt(cost + slack) of it (the candidate pass's f32 distance, slack for
+        its rounding), and p's nearest / second-nearest bf16 centre lie at d1 / d2 (f64, rounded
+        outward), so the label is a(p) with ub = r + d1 and lb = d2 - r. The first pruned step then
+        re-assigns only the rows these bounds do not prove (_step_seeded)."""
+        st, n, k, d = self._pst, self.n, self.k, self.d
+        if n == 0:
+            return
+        cbd = self.cb[:k, :d].to(torch.float64)
+        U = sd.uniq.to(device=self.device, dtype=torch.float64)
+        pn = (U * U).sum(1)
+        cnn = (cbd * cbd).sum(1)
+        d2m = (pn[:, None] + cnn[None, :] - 2.0 * (U @ cbd.T)).clamp_(min=0.0)
+        eps = 1e-12 * float(pn.max() + cnn.max())  # f64 rounding of the expansion
+        top = torch.topk(d2m, min(2, k), dim=1, largest=False)
+        a = top.indices[:, 0].to(torch.int32).contiguous()
+        d1 = ((top.values[:, 0] + eps).sqrt() * (1.0 + 1e-6)).to(torch.float32).contiguous()
+        if k > 1:
+            d2 = ((top.values[:, 1] - eps).clamp(min=0.0).sqrt() * (1.0 - 1e-6)).to(torch.float32).contiguous()
+        else:
+            d2 = torch.full_like(d1, math.inf)
+        pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
+        qmap = sd.inverse.reshape(-1).to(torch.int32).contiguous()
+        K.seed_bounds(sd.nearest[:n], sd.costs[:n], self.xnorm[:n], qmap, a, d1, d2, pn32, 2.0 * self._tau, n,
+                      self.labels[:n], st.ub[:n], st.lb[:n])
+
+    def _step_seeded(self) -> None:
+        """First Lloyd step after _seed_from_init: the bounds pass (no drift yet) lists the rows the
+        init's bounds leave open, the K9r candidate pass re-assigns them, and the sums of every row's
+        label are accumulated in full (counting-sort ranks from the labels; the incremental sums start
+        from them). Same labels and centres as a full step; more than _PRUNE_CAP candidates on a rank
+        fall back to the full pass there (the collectives are the same either way)."""
+        st, dl = self._pst, self.delta
+        n, k, d, ap = self.n, self.k, self.d, self.aplan
+        x, lab, msg = self.x, self.labels, self.msgs[0]
+        m = 0
+        if n:
+            K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
+                           xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, zero_count=True)
+            m = int(st.count.item())
+        if m > st.cap_m:
+            st.force.fill_(1)
+            self._step_prune_dev()
+            return
+        st.pmode.copy_(torch.tensor([0, m], dtype=torch.int32))
+        if n:
+            K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, None, st.ub, st.lb,
+                            st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab)
+            K.label_hist(lab, n, ap, self.hist, self.rank)
+        self.cost_part.zero_()
+        dl.invalidate()
+        dl.gate(0)
+        # the seeded upper bounds (r + d1) are loose; the accumulate streams every row anyway and leaves
+        # the exact one, |x - c_label| rounded up, so the next step's bounds prove as many rows as after a
+        # full pass (the seeded lower bounds stay: d2 - r is far below what they are compared with)
+        K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
+                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], ub_centres=self.cb,
+                          ub=st.ub)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
         self.comm.allreduce_async(msg).wait()
         st.cb_old.copy_(self.cb)
@@ -982,6 +1060,10 @@ class LloydEngine:
             out = np.concatenate([out, np.repeat(out[-1:], k - out.shape[0], 0)], 0)
         else:
             self.k_effective = k
+        if self._pdev and self.n and self.k_effective == k and os.environ.get("CML_KMEANS_SEED_BOUNDS", "1") != "0":
+            # what the first Lloyd step needs to start from bounds instead of a full pass (set_centers)
+            self._seed = types.SimpleNamespace(nearest=nearest, costs=costs, inverse=inverse, uniq=uniq,
+                                               out=np.array(out, dtype=np.float64, copy=True))
         return out
 
     def _init_first_pass(self, c0: torch.Tensor):

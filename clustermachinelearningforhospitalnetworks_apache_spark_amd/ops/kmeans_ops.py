@@ -32,6 +32,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_rr_plan": (c_int, [c_int, c_int, c_int, c_int, c_vp]),
     "cml_kmeans_set_rr_default": (c_int, [c_int]),
     "cml_kmeans_set_rr_debug": (c_int, [c_int]),
+    "cml_kmeans_set_rr_m32": (c_int, [c_int]),
     "cml_kmeans_assign_tile_rows": (c_int, [c_int]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
@@ -42,6 +43,9 @@ _native.register_kernel_sigs({
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
                                       c_vp]),
+    "cml_kmeans_sort_accum_ub": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int,
+                                         c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
+                                         c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                                        c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -54,6 +58,9 @@ _native.register_kernel_sigs({
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]),
     "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
+                                       c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "cml_kmeans_centre_stats": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
@@ -237,6 +244,9 @@ def _apply_env_knobs(lib) -> None:
     rr = os.environ.get("CML_KMEANS_RR")
     if rr:
         _native.check(lib.cml_kmeans_set_rr_default(int(rr)), "set_rr_default")
+    m32 = os.environ.get("CML_KMEANS_RR_M32")
+    if m32:
+        _native.check(lib.cml_kmeans_set_rr_m32(int(m32)), "set_rr_m32")
 
 
 def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = False) -> AssignPlan:
@@ -277,6 +287,12 @@ def set_assign_variant(v: int) -> None:
 def set_rr_default(on: bool) -> None:
     """Whether variant 0 (auto) picks K9r wherever it applies."""
     _native.check(_native.kernels().cml_kmeans_set_rr_default(int(bool(on))), "set_rr_default")
+
+
+def set_rr_m32(on: bool) -> None:
+    """K9r compute waves on 32x32x16 MFMA tiles (even centre-tile counts; CML_KMEANS_RR_M32=1) or the
+    16x16x32 form (default, faster on MI355X). Both give the same labels up to the distance rounding."""
+    _native.check(_native.kernels().cml_kmeans_set_rr_m32(int(bool(on))), "set_rr_m32")
 
 
 def set_assign_sched(v: int) -> None:
@@ -403,16 +419,24 @@ def seg_slots(plan: AccumPlan, d: int, device) -> tuple:
 def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tensor, rank: torch.Tensor,
                     hist: torch.Tensor, aplan: AssignPlan, k: int, cost_part: torch.Tensor, off: torch.Tensor,
                     seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor,
-                    slots: tuple, stream=None, gate: torch.Tensor | None = None) -> None:
+                    slots: tuple, stream=None, gate: torch.Tensor | None = None,
+                    ub_centres: torch.Tensor | None = None, ub: torch.Tensor | None = None) -> None:
     """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic).
-    With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full."""
+    With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full. With
+    ``ub_centres`` (bf16 [kp, dp]) and ``ub`` (f32 [n]) the segmented pass also writes every row's upper
+    bound of |x - c_label| (the exact-pruning bound) as the rows stream through."""
     lib = _native.kernels()
-    status = lib.cml_kmeans_sort_accum(x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(),
-                                       hist.data_ptr(), aplan.grid, aplan.round_rows, k, aplan.kp,
-                                       cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
-                                       perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(),
-                                       slots[0].data_ptr(), slots[1].data_ptr(), int(is_fp8(x)),
-                                       gate.data_ptr() if gate is not None else 0, _native.stream_ptr(stream))
+    args = (x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(), hist.data_ptr(), aplan.grid,
+            aplan.round_rows, k, aplan.kp, cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
+            perm.data_ptr(), plan.cpl, plan.seg_grid, msg.data_ptr(), slots[0].data_ptr(), slots[1].data_ptr(),
+            int(is_fp8(x)), gate.data_ptr() if gate is not None else 0)
+    if ub is not None:
+        if ub_centres is None or ub_centres.dtype != torch.bfloat16 or ub.dtype != torch.float32 or ub.numel() < n:
+            raise ValueError("accumulate_sort: ub needs bf16 centres and an f32 [n] output")
+        status = lib.cml_kmeans_sort_accum_ub(*args, ub_centres.data_ptr(), ub_centres.stride(0), ub.data_ptr(),
+                                              _native.stream_ptr(stream))
+    else:
+        status = lib.cml_kmeans_sort_accum(*args, _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
 
 
@@ -512,6 +536,35 @@ def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift
     idx = torch.nonzero(~keep).flatten()
     cand[: idx.numel()] = idx.to(cand.dtype)
     count[0] = idx.numel()
+
+
+def seed_bounds(nearest: torch.Tensor, cost: torch.Tensor, xn: torch.Tensor, qmap: torch.Tensor, a: torch.Tensor,
+                d1: torch.Tensor, d2: torch.Tensor, pn: torch.Tensor, tau: float, n: int, labels: torch.Tensor,
+                ub: torch.Tensor, lb: torch.Tensor, stream=None) -> None:
+    """Labels and exact-pruning bounds of every row from the k-means|| init (kmeans_prune.hip): nearest
+    candidate (int32 index into qmap), its squared distance (f32) and the candidate -> (centre a, d1, d2,
+    |p|²) tables (int32 / f32). Device only."""
+    for t, dt in ((nearest, torch.int32), (cost, torch.float32), (xn, torch.float32), (qmap, torch.int32),
+                  (a, torch.int32), (d1, torch.float32), (d2, torch.float32), (pn, torch.float32),
+                  (labels, torch.int32), (ub, torch.float32), (lb, torch.float32)):
+        if t.dtype != dt or not t.is_contiguous():
+            raise ValueError("seed_bounds: operand dtype/layout")
+    _native.check(_native.kernels().cml_kmeans_seed_bounds(
+        nearest.data_ptr(), cost.data_ptr(), xn.data_ptr(), qmap.data_ptr(), a.data_ptr(), d1.data_ptr(),
+        d2.data_ptr(), pn.data_ptr(), float(tau), int(n), labels.data_ptr(), ub.data_ptr(), lb.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_seed_bounds")
+
+
+def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Tensor, rank: torch.Tensor,
+               stream=None) -> None:
+    """Counting-sort ranks of the current labels in the K9r workgroup geometry (what a full K9r pass
+    leaves in hist/rank for the sort-regime accumulate). Device only."""
+    if labels.dtype != torch.int32 or hist.numel() < plan.grid * plan.kp or rank.numel() < n:
+        raise ValueError("label_hist: operand shapes")
+    _native.check(_native.kernels().cml_kmeans_label_hist(labels.data_ptr(), int(n), int(plan.round_rows),
+                                                          int(plan.grid), int(plan.kp), hist.data_ptr(),
+                                                          rank.data_ptr(), _native.stream_ptr(stream)),
+                  "kmeans_label_hist")
 
 
 def prune_gate(count: torch.Tensor, cap: int, force: torch.Tensor, mode: torch.Tensor, stream=None) -> None:

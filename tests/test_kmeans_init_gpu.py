@@ -129,3 +129,46 @@ def test_init_then_fit_on_blobs_gpu():
     got = eng.centers
     dmin = torch.cdist(cen.double(), got).min(1).values
     assert float(dmin.max()) < 0.5
+
+
+@pytest.mark.parametrize("n,d,k,scale", [(300_001, 256, 64, 4.0), (120_013, 128, 100, 3.0), (50_000, 256, 256, 0.3)])
+def test_seeded_first_step_equals_full_step(monkeypatch, n, d, k, scale):
+    """The first Lloyd step after the device k-means|| init starts from the bounds the init implies
+    (kmeans_seed_bounds + candidate pass + full accumulate) instead of a full assign pass: labels after
+    step 1, the centres over a whole fit and the costs are bitwise those of the full first step; on
+    separated blobs most rows are proven by the seeded bounds. (scale 0.3: overlapping blobs, few rows
+    proven.)"""
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
+    monkeypatch.setenv("CML_KMEANS_PRECISION", "bf16")
+    g = torch.Generator(device="cuda").manual_seed(n)
+    cen = torch.randn(k, d, device="cuda", generator=g) * scale
+    x = (cen[torch.randint(0, k, (n,), device="cuda", generator=g)] +
+         torch.randn(n, d, device="cuda", generator=g)).to(torch.bfloat16)
+    res = []
+    for seeded in ("1", "0"):
+        monkeypatch.setenv("CML_KMEANS_SEED_BOUNDS", seeded)
+        eng = LloydEngine(x, d, k)
+        eng.track_prune = True
+        init = eng.init_kmeans_parallel(seed=11)
+        eng.set_centers(init)
+        assert eng._seeded == (seeded == "1")
+        eng.step()
+        lab1 = eng.labels[:n].clone()
+        st = eng._pst
+        idx = torch.arange(0, n, 7, device="cuda")
+        xs = eng.x[idx, :d].double()
+        own = ((xs - st.cb_old[lab1[idx].long(), :d].double()) ** 2).sum(1).sqrt()
+        assert bool((st.ub[idx].double() >= own * (1 - 1e-12)).all())  # valid upper bounds after step 1
+        c1 = eng.training_cost()
+        eng.fit(12, 0.0, start_iter=1)
+        res.append((init, lab1, c1, eng.centers.cpu().numpy(), eng.training_cost(), eng.prune_history()))
+    (i_s, l_s, c_s, C_s, f_s, h_s), (i_f, l_f, c_f, C_f, f_f, h_f) = res
+    assert np.array_equal(i_s, i_f)
+    assert torch.equal(l_s, l_f)
+    assert c_s == c_f and f_s == f_f
+    assert np.array_equal(C_s, C_f)
+    assert h_f[0] == (True, n)  # the unseeded engine ran a full first pass
+    full, m = h_s[0]
+    assert 0 <= m <= n and (not full or m == n)  # more than _PRUNE_CAP candidates: the full pass instead
+    if scale >= 4.0:
+        assert not full and m < 0.5 * n, m
