@@ -190,6 +190,8 @@ def main():
                             "iteration_ms": [round(1000.0 * t, 3) for t in per_it]}
         if eng.prune:
             acc["breakdown"]["prune_history_rank0"] = eng.prune_history()
+        # pruned k-means|| rounds: (rows, rows with a few relevant candidates, rows sent to the K9r pass)
+        acc["breakdown"]["init_pruned_rounds_rank0"] = getattr(eng, "_init_prune_history", None)
         del eng
 
     total_rows = args.rows

@@ -799,8 +799,11 @@ struct SegUB {
 // in earlier slices) goes to slot A[w], its last (may continue in later slices) to slot B[w];
 // kmeans_seg_fixup adds the slots in ascending wave order. The result is bitwise identical
 // run to run (SURVEY.md §5.2 deterministic-reduction mode, here the only mode).
+// Positions per wave slice: an even split, but at least 128 (a short delta list — the incremental
+// steps' moved rows — then occupies few waves, so a cluster spans few slices and the fixup stays short).
 __device__ __forceinline__ long long seg_chunk(long long filled, long long waves) {
-  return (filled + waves - 1) / waves;
+  const long long c = (filled + waves - 1) / waves;
+  return c > 128 ? c : 128;
 }
 
 template <int CPL, bool F8, bool UB = false>
@@ -941,6 +944,201 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
   }
 }
 
+// ---------------------------------------------------------------------------------------------------
+// Pruned k-means|| candidate pass (models/kmeans.py _init_candidate_pass_pruned). A row x whose
+// nearest candidate so far is p at distance r (cost, plus the slack of the pass that measured it) can
+// only move to a new candidate y with |p - y| < 2r (else |x - y| >= |p - y| - r >= r). tab_v[p] holds
+// the distances from p to the m new candidates sorted ascending (rounded down), tab_j their indices:
+// L(x) = #{y : tab_v[p][y] < 2r} new candidates are relevant. L = 0: nothing to do; L <= lmax: the
+// few distances are computed here (one wave per row, DPP sums); otherwise the row goes to the K9r
+// candidate pass (list B).
+__device__ __forceinline__ float init_reach(float cost, float xn, float pn, float tau) {
+  return 2.0f * sqrtf(fmaxf(cost, 0.f) + tau * (xn + pn)) * (1.0f + 2e-6f);
+}
+
+// Each block classifies a contiguous chunk of kClsRows rows (kClsPer per thread) and reserves its
+// list slots with ONE atomic per list: per-wave atomics on two counters serialised at the L2 and cost
+// ~30 ms for 100M rows (1.6M waves).
+constexpr int kClsPer = 16;
+constexpr int kClsRows = 256 * kClsPer;
+
+__global__ __launch_bounds__(256) void init_classify_kernel(const float* __restrict__ cost,
+                                                            const int* __restrict__ near, const float* __restrict__ xn,
+                                                            const float* __restrict__ pn,
+                                                            const float* __restrict__ tab_v, int m, float tau,
+                                                            long long n, int lmax, int* __restrict__ list_a,
+                                                            int* __restrict__ cnt_a, int* __restrict__ list_b,
+                                                            int* __restrict__ cnt_b) {
+  __shared__ int wa[4], wb[4], base[2];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  for (long long c0 = (long long)blockIdx.x * kClsRows; c0 < n; c0 += (long long)gridDim.x * kClsRows) {
+    unsigned cls = 0;  // 2 bits per row: 0 skip, 1 list A, 2 list B
+#pragma unroll
+    for (int q = 0; q < kClsPer; ++q) {
+      const long long i = c0 + (long long)q * 256 + threadIdx.x;
+      unsigned k = 0;
+      if (i < n) {  // the sorted row only needs two probes: L == 0 iff v[0] >= t, L <= lmax iff v[lmax] >= t
+        const int p = near[i];
+        const float t = init_reach(cost[i], xn[i], pn[p], tau);
+        const float* v = tab_v + (long long)p * m;
+        const float v0 = v[0], vl = lmax < m ? v[lmax] : __builtin_huge_valf();
+        k = v0 >= t ? 0u : (vl >= t ? 1u : 2u);
+      }
+      cls |= k << (2 * q);
+    }
+    int na = 0, nb = 0;
+#pragma unroll
+    for (int q = 0; q < kClsPer; ++q) {
+      const unsigned c = (cls >> (2 * q)) & 3u;
+      na += (int)__popcll(__ballot(c == 1));
+      nb += (int)__popcll(__ballot(c == 2));
+    }
+    if (lane == 0) {
+      wa[wv] = na;
+      wb[wv] = nb;
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      const int ta = wa[0] + wa[1] + wa[2] + wa[3], tb = wb[0] + wb[1] + wb[2] + wb[3];
+      base[0] = ta ? atomicAdd(cnt_a, ta) : 0;
+      base[1] = tb ? atomicAdd(cnt_b, tb) : 0;
+    }
+    __syncthreads();
+    int pa = base[0], pb = base[1];
+    for (int w = 0; w < wv; ++w) {
+      pa += wa[w];
+      pb += wb[w];
+    }
+    const unsigned long long below = (1ull << lane) - 1ull;
+#pragma unroll
+    for (int q = 0; q < kClsPer; ++q) {
+      const unsigned c = (cls >> (2 * q)) & 3u;
+      const unsigned long long ba = __ballot(c == 1), bb = __ballot(c == 2);
+      const long long i = c0 + (long long)q * 256 + threadIdx.x;
+      if (c == 1) list_a[pa + (int)__popcll(ba & below)] = (int)i;
+      if (c == 2) list_b[pb + (int)__popcll(bb & below)] = (int)i;
+      pa += (int)__popcll(ba);
+      pb += (int)__popcll(bb);
+    }
+    __syncthreads();  // wa/wb/base reused by the next chunk
+  }
+}
+
+// List A: one wave per batch of 16 rows. Lane u looks up row u (nearest candidate, reach, its relevant
+// new candidates: at most LMAX) so the dependent lookups of the 16 rows overlap; then every row's
+// distances are computed by the whole wave (CPL columns per lane, DPP sums), the relevant candidates'
+// slices loaded together. Strict improvement over the current cost moves the row; among the new
+// candidates ties go to the lowest index (K9r's argmin rule).
+template <int CPL, bool F8, int LMAX>
+__global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restrict__ X, long long ldx, int Dp,
+                                                             float* __restrict__ cost, int* __restrict__ near,
+                                                             const float* __restrict__ xn,
+                                                             const float* __restrict__ pn,
+                                                             const float* __restrict__ tab_v,
+                                                             const int* __restrict__ tab_j, int m,
+                                                             const u16* __restrict__ Y, int off, float tau,
+                                                             const int* __restrict__ list, const int* __restrict__ cnt) {
+  using raw_t = typename SegRaw<CPL, F8>::T;
+  using yraw_t = typename RawCols<CPL>::T;
+  constexpr int U = 16;
+  constexpr int ESZ = F8 ? 1 : 2;
+  const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
+  const int lane = threadIdx.x & 63;
+  const int col = CPL * lane;
+  const bool active = col < Dp;
+  const long long nwaves = (long long)gridDim.x * (blockDim.x / 64);
+  const long long total = *cnt;
+  for (long long b0 = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * U; b0 < total;
+       b0 += nwaves * U) {
+    const int c = (int)(total - b0 < U ? total - b0 : U);
+    const int pr = lane < c ? list[b0 + lane] : 0;
+    // lane u < c: row u's lookups
+    float cr = 0.f;
+    int L = 0, jl[LMAX];
+    if (lane < c) {
+      const int p = near[pr];
+      cr = cost[pr];
+      const float t = init_reach(cr, xn[pr], pn[p], tau);
+      const float* v = tab_v + (long long)p * m;
+      const int* tj = tab_j + (long long)p * m;
+#pragma unroll
+      for (int l = 0; l < LMAX; ++l) {
+        const bool in = l < m && v[l] < t;
+        L += in ? 1 : 0;
+        jl[l] = in ? tj[l] : 0;
+      }
+    } else {
+#pragma unroll
+      for (int l = 0; l < LMAX; ++l) jl[l] = 0;
+    }
+    raw_t w[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = __builtin_amdgcn_readlane(pr, u);
+      w[u] = (u < c && active) ? *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ) : raw_t{};
+    }
+    float nbest = 0.f;
+    int nbj = -1;
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (u < c) {
+      const int Lu = __builtin_amdgcn_readlane(L, u);
+      float best = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr), u));
+      int bj = -1;
+      yraw_t yv[LMAX];
+#pragma unroll
+      for (int l = 0; l < LMAX; ++l) {
+        const int j = __builtin_amdgcn_readlane(jl[l], u);
+        yv[l] = (l < Lu && active) ? *reinterpret_cast<const yraw_t*>(Y + (long long)j * Dp + col) : yraw_t{};
+      }
+#pragma unroll
+      for (int l = 0; l < LMAX; ++l) {
+        if (l < Lu) {
+        const int j = __builtin_amdgcn_readlane(jl[l], u);
+        const unsigned* ys = reinterpret_cast<const unsigned*>(&yv[l]);
+        float cv[CPL];
+#pragma unroll
+        for (int q = 0; q < CPL / 2; ++q) {
+          cv[2 * q] = bf16_to_f32((u16)(ys[q] & 0xffffu));
+          cv[2 * q + 1] = bf16_to_f32((u16)(ys[q] >> 16));
+        }
+        const float d = wave_total_dpp(sqdist_raw<CPL, F8>(w[u], cv));
+        if (d < best || (d == best && bj >= 0 && j < bj)) {
+          best = d;
+          bj = j;
+        }
+        }
+      }
+      if (lane == u) {
+        nbest = best;
+        nbj = bj;
+      }
+      }
+    }
+    if (lane < c && nbj >= 0) {
+      cost[pr] = nbest;
+      near[pr] = off + nbj;
+    }
+  }
+}
+
+// List B after a K9r candidate pass over a chunk of the new candidates (labels relative to the chunk).
+__global__ __launch_bounds__(256) void init_merge_list_kernel(float* __restrict__ cost, int* __restrict__ near,
+                                                              const float* __restrict__ best,
+                                                              const int* __restrict__ lab, int off,
+                                                              const int* __restrict__ list,
+                                                              const int* __restrict__ cnt) {
+  const long long total = *cnt;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < total; i += (long long)gridDim.x * blockDim.x) {
+    const int row = list[i];
+    const float b = best[row];
+    if (b < cost[row]) {
+      cost[row] = b;
+      near[row] = lab[row] + off;
+    }
+  }
+}
+
 // msg[c] += Σ over the slices overlapping cluster c, in ascending slice order, of their head
 // (A) / tail (B) partials for c. One workgroup per cluster.
 __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long n,
@@ -957,7 +1155,22 @@ __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ 
   if (w1 >= nwaves) w1 = nwaves - 1;
   for (int d = threadIdx.x; d < D; d += blockDim.x) {
     double t = 0.0;
-    for (long long w = w0; w <= w1; ++w) {
+    long long w = w0;
+    // 8 slices per round, loads issued together (a cluster can span thousands of slices)
+    for (; w + 8 <= w1 + 1; w += 8) {
+      double v[8];
+#pragma unroll
+      for (int q = 0; q < 8; ++q) {
+        const long long ww = w + q;
+        const int ca = slot_c[2 * ww], cb = slot_c[2 * ww + 1];
+        const double a = slots[(2 * ww) * (long long)D + d], b = slots[(2 * ww + 1) * (long long)D + d];
+        v[q] = ca == c ? a : 0.0;
+        v[q] = cb == c ? v[q] + b : v[q];
+      }
+#pragma unroll
+      for (int q = 0; q < 8; ++q) t += v[q];
+    }
+    for (; w <= w1; ++w) {
       if (slot_c[2 * w] == c) t += slots[(2 * w) * (long long)D + d];
       if (slot_c[2 * w + 1] == c) t += slots[(2 * w + 1) * (long long)D + d];
     }
@@ -1429,7 +1642,8 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
                                      int* labels, double* cost_part, int* hist, int* rank, int grid, int xfp8,
                                      int* chg_rows, int* chg_old, int* chg_wg_count, int* chg_overflow, int chg_pcap,
                                      int rr_ct, const int* idx, const int* n_dev, const int* lab_in, float* ub,
-                                     float* lb, const float* mc, float tau, const int* gate, int want, void* stream) {
+                                     float* lb, const float* mc, float tau, const int* gate, int want, float* best,
+                                     void* stream) {
   if (mode < 1 || mode > 2 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if (rr_ct <= 0 || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
@@ -1444,7 +1658,7 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
   const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
   const rr::Ext ext{idx, n_dev, lab_in, ub, lb, mc, tau, gate, want};
   return rr::dispatch(mode, Dp, rr_ct, xfp8 != 0, X, n, ldx, (const u16*)C, ldc, kc, kp, cnorm, xnorm, labels,
-                      nullptr, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
+                      best, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }
 
 // ||x||² of the device matrix: the row pass of kmeans_init.hip (norms only), the one definition of
@@ -1587,5 +1801,53 @@ CML_API int cml_kmeans_update(const double* bufs, int nbuf, long long bstride, i
                               long long ldc, int Dp, int Kp, float* cnorm, double* shift2, void* stream) {
   hipLaunchKernelGGL(kmeans_update_kernel, dim3(Kp), dim3(256), 0, (hipStream_t)stream, bufs, nbuf, bstride, k, D,
                      cent, (u16*)cb, ldc, Dp, cnorm, shift2);
+  return cml_status();
+}
+
+// Pruned k-means|| candidate pass: classification (list A / list B, counters zeroed by the caller).
+CML_API int cml_kmeans_init_classify(const float* cost, const int* near, const float* xn, const float* pn,
+                                     const float* tab_v, int m, float tau, long long n, int lmax, int* list_a,
+                                     int* cnt_a, int* list_b, int* cnt_b, void* stream) {
+  if (n <= 0) return 0;
+  if (m <= 0) return (int)hipErrorInvalidValue;
+  const long long blocks = std::min<long long>((n + kClsRows - 1) / kClsRows, 4096);
+  hipLaunchKernelGGL(init_classify_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, cost, near, xn,
+                     pn, tab_v, m, tau, n, lmax, list_a, cnt_a, list_b, cnt_b);
+  return cml_status();
+}
+
+// List A distances. X: bf16 rows (ldx elements) or e4m3 bytes (ldx bytes); Y: bf16 [m, Dp] new
+// candidates; n_cap: an upper bound of *cnt (sizes the grid).
+constexpr int kInitLmax = 8;  // models/kmeans.py _INIT_LMAX
+CML_API int cml_kmeans_init_lmax() { return kInitLmax; }
+CML_API int cml_kmeans_init_near_list(const void* X, long long ldx, int Dp, int xfp8, float* cost, int* near,
+                                      const float* xn, const float* pn, const float* tab_v, const int* tab_j, int m,
+                                      const void* Y, int off, float tau, const int* list, const int* cnt,
+                                      long long n_cap, void* stream) {
+  if (n_cap <= 0) return 0;
+  const int cpl = Dp / 64;
+  const long long blocks = std::max<long long>(1, std::min<long long>((n_cap + 63) / 64, 4096));
+  hipStream_t st = (hipStream_t)stream;
+#define CML_NL(C, F)                                                                                                \
+  hipLaunchKernelGGL((init_near_list_kernel<C, F, kInitLmax>), dim3((unsigned)blocks), dim3(256), 0, st, X, ldx, Dp, \
+                     cost, near, xn, pn, tab_v, tab_j, m, (const u16*)Y, off, tau, list, cnt)
+  if (xfp8) {
+    if (cpl == 4) CML_NL(4, true);
+    else if (cpl == 8) CML_NL(8, true);
+    else return (int)hipErrorInvalidValue;
+  } else if (cpl == 2) CML_NL(2, false);
+  else if (cpl == 4) CML_NL(4, false);
+  else if (cpl == 8) CML_NL(8, false);
+  else return (int)hipErrorInvalidValue;
+#undef CML_NL
+  return cml_status();
+}
+
+CML_API int cml_kmeans_init_merge_list(float* cost, int* near, const float* best, const int* lab, int off,
+                                       const int* list, const int* cnt, long long n_cap, void* stream) {
+  if (n_cap <= 0) return 0;
+  const long long blocks = std::max<long long>(1, std::min<long long>((n_cap + 255) / 256, 4096));
+  hipLaunchKernelGGL(init_merge_list_kernel, dim3((unsigned)blocks), dim3(256), 0, (hipStream_t)stream, cost, near,
+                     best, lab, off, list, cnt);
   return cml_status();
 }

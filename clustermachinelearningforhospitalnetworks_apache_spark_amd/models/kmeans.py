@@ -1024,7 +1024,17 @@ class LloydEngine:
                 continue
             centers.append(new)
             if self.gpu:
-                self._init_candidate_pass(new, costs, nearest, ncand)
+                # once most rows sit near a candidate, only the new candidates close to a row's nearest one
+                # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
+                # round (only the first centre so far) everything after the first K9r chunk
+                first = new.shape[0] if step > 0 else self._candidate_chunks(new.shape[0])[0]
+                if step == 0:
+                    self._init_candidate_pass(new[:first], costs, nearest, ncand)
+                rest = new[first:] if step == 0 else new
+                if rest.shape[0] and not self._init_candidate_pass_pruned(
+                        torch.cat(centers[:-1] + ([new[:first]] if step == 0 else []), 0), rest, costs, nearest,
+                        ncand + (first if step == 0 else 0)):
+                    self._init_candidate_pass(rest, costs, nearest, ncand + (first if step == 0 else 0))
             elif self.n:
                 d_new, i_new = self._min_dist_idx(new)
                 better = d_new < costs
@@ -1116,6 +1126,70 @@ class LloydEngine:
             K.assign_bf16(self.x, n, dp, cb, cn, plan, lab, best, None, xnorm=self.xnorm)
             K.init_merge(costs, nearest, best, lab, off + c0, n)
             c0 += size
+
+    _INIT_LMAX = 8  # relevant new candidates a row may have to take the per-row path (else the K9r pass)
+
+    def _init_candidate_pass_pruned(self, prev: torch.Tensor, new: torch.Tensor, costs: torch.Tensor,
+                                    nearest: torch.Tensor, off: int) -> bool:
+        """A k-means|| candidate pass that skips what the triangle inequality rules out: a row at distance
+        r from its nearest candidate p can only move to a new candidate y with |p - y| < 2r. With the
+        distances from every existing candidate to the new ones sorted (a small f64 table), each row
+        counts its relevant candidates (kmeans init_classify); rows with none are done, rows with at
+        most _INIT_LMAX get those distances from a per-row kernel, the rest run the K9r candidate pass
+        over their positions (mode 2). Same nearest candidates as the full pass up to the rounding of
+        near-ties. Returns False (nothing changed) when too many rows need the K9r pass to gain."""
+        n, d, dp, dev = self.n, self.d, self.dp, self.device
+        if not self._pdev or os.environ.get("CML_KMEANS_INIT_PRUNE", "1") == "0":
+            return False
+        if n == 0:
+            return True
+        m = int(new.shape[0])
+        P = prev.to(device=dev, dtype=torch.float64)
+        Y = new.to(device=dev, dtype=torch.float64)
+        pn, yn = (P * P).sum(1), (Y * Y).sum(1)
+        d2 = pn[:, None] + yn[None, :] - 2.0 * (P @ Y.T)
+        eps = 1e-12 * float(pn.max() + yn.max())
+        vals, order = torch.sort((d2 - eps).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6), dim=1)
+        tab_v = vals.to(torch.float32).contiguous()
+        tab_j = order.to(torch.int32).contiguous()
+        pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
+        tau = 2.0 * self._tau
+        tr = self.aplan.round_rows
+        list_a = torch.empty(n, dtype=torch.int32, device=dev)
+        list_b = torch.zeros(n + tr, dtype=torch.int32, device=dev)  # padded: whole tiles of valid rows
+        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        K.init_classify(costs, nearest, self.xnorm, pn32, tab_v, tau, n, self._INIT_LMAX, list_a, cnt[0:1], list_b,
+                        cnt[1:2])
+        ca, cb = (int(v) for v in cnt.tolist())
+        if cb > 0.6 * n:
+            return False
+        yb = torch.zeros((m, dp), dtype=torch.bfloat16, device=dev)
+        yb[:, :d] = Y.to(torch.bfloat16)
+        if ca:
+            K.init_near_list(self.x, dp, costs, nearest, self.xnorm, pn32, tab_v, tab_j, yb, off, tau, list_a,
+                             cnt[0:1], ca)
+        if cb:
+            st = self._pst
+            pad = -(-cb // tr) * tr + tr
+            cxn = torch.zeros(pad, dtype=torch.float32, device=dev)
+            cxn[:cb] = self.xnorm[list_b[:cb].long()]
+            lab_in = torch.full((pad,), -1, dtype=torch.int32, device=dev)
+            best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+            c0 = 0
+            for size in self._candidate_chunks(m):
+                kp = round_up(size, 32)
+                cbk = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
+                cnk = torch.zeros(kp, dtype=torch.float32, device=dev)
+                K.update_centers(None, size, d, Y[c0:c0 + size].contiguous().clone(), cbk, dp, kp, cnk, None)
+                plan = K.plan_assign(cb, dp, size, dev.index or 0, fp8=K.is_fp8(self.x))
+                mc = cnk[:size].max().reshape(1)
+                K.assign_rr_ext(2, self.x, cb, dp, cbk, cnk, plan, cxn, self.labels, None, st.ub, st.lb, mc,
+                                self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, best=best)
+                K.init_merge_list(costs, nearest, best, self.labels, off + c0, list_b, cnt[1:2], cb)
+                c0 += size
+        if self.track_prune:
+            self._init_prune_history = getattr(self, "_init_prune_history", []) + [(n, ca, cb)]
+        return True
 
     # Time of one K9r pass over 20M x 256 bf16 rows by centre tiles per compute wave (64 centres each),
     # ms, measured on MI355X (profiles/r3/mb_rr_modes.log): CT <= 2 is HBM-bound, then the MFMA work

@@ -66,7 +66,12 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
-                                         c_vp]),
+                                         c_vp, c_vp]),
+    "cml_kmeans_init_classify": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, ctypes.c_float, c_ll, c_int, c_vp,
+                                         c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_init_near_list": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
+                                          c_int, ctypes.c_float, c_vp, c_vp, c_ll, c_vp]),
+    "cml_kmeans_init_merge_list": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp, c_ll, c_vp]),
 })
 
 
@@ -592,11 +597,13 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
                   hist: torch.Tensor | None = None, rank: torch.Tensor | None = None,
                   delta: "DeltaState | None" = None, idx: torch.Tensor | None = None,
                   n_dev: torch.Tensor | None = None, lab_in: torch.Tensor | None = None,
-                  gate: torch.Tensor | None = None, want: int = 0, stream=None) -> None:
+                  gate: torch.Tensor | None = None, want: int = 0, stream=None,
+                  best: torch.Tensor | None = None) -> None:
     """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
     the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
     ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
-    rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag."""
+    rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag;
+    ``best`` (f32, real rows) receives the squared distance to the new label."""
     if plan.rr_ct <= 0 or plan.kc != plan.kp:
         raise ValueError("the pruned-step assign needs the K9r plan (Dp in {128, 256, 512}, k <= 256)")
     _native.check(_native.kernels().cml_kmeans_assign_rr_ext(
@@ -606,8 +613,40 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
         _ptr(delta.rows if delta is not None else None), _ptr(delta.old if delta is not None else None),
         _ptr(delta.wg_count if delta is not None else None), _ptr(delta.overflow if delta is not None else None),
         delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
-        lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _native.stream_ptr(stream)),
+        lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _native.stream_ptr(stream)),
         f"kmeans_assign_rr_ext(mode={mode})")
+
+
+def init_classify(cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor, pn: torch.Tensor, tab_v: torch.Tensor,
+                  tau: float, n: int, lmax: int, list_a: torch.Tensor, cnt_a: torch.Tensor, list_b: torch.Tensor,
+                  cnt_b: torch.Tensor, stream=None) -> None:
+    """Pruned k-means|| pass, step 1 (kmeans.hip init_classify_kernel): rows with no relevant new
+    candidate are dropped, rows with at most ``lmax`` go to ``list_a``, the others to ``list_b``
+    (counters zeroed by the caller, lists of capacity n)."""
+    m = int(tab_v.shape[1])
+    _native.check(_native.kernels().cml_kmeans_init_classify(
+        cost.data_ptr(), near.data_ptr(), xn.data_ptr(), pn.data_ptr(), tab_v.data_ptr(), m, float(tau), int(n),
+        int(lmax), list_a.data_ptr(), cnt_a.data_ptr(), list_b.data_ptr(), cnt_b.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_init_classify")
+
+
+def init_near_list(x: torch.Tensor, dp: int, cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor,
+                   pn: torch.Tensor, tab_v: torch.Tensor, tab_j: torch.Tensor, y: torch.Tensor, off: int, tau: float,
+                   lst: torch.Tensor, cnt: torch.Tensor, n_cap: int, stream=None) -> None:
+    """Pruned k-means|| pass, step 2: the relevant new candidates of every ``lst`` row (y: bf16 [m, dp])."""
+    m = int(tab_v.shape[1])
+    _native.check(_native.kernels().cml_kmeans_init_near_list(
+        x.data_ptr(), x.stride(0), int(dp), int(is_fp8(x)), cost.data_ptr(), near.data_ptr(), xn.data_ptr(),
+        pn.data_ptr(), tab_v.data_ptr(), tab_j.data_ptr(), m, y.data_ptr(), int(off), float(tau), lst.data_ptr(),
+        cnt.data_ptr(), int(n_cap), _native.stream_ptr(stream)), "kmeans_init_near_list")
+
+
+def init_merge_list(cost: torch.Tensor, near: torch.Tensor, best: torch.Tensor, lab: torch.Tensor, off: int,
+                    lst: torch.Tensor, cnt: torch.Tensor, n_cap: int, stream=None) -> None:
+    """cost/near of the ``lst`` rows <- best/lab+off where best < cost."""
+    _native.check(_native.kernels().cml_kmeans_init_merge_list(
+        cost.data_ptr(), near.data_ptr(), best.data_ptr(), lab.data_ptr(), int(off), lst.data_ptr(), cnt.data_ptr(),
+        int(n_cap), _native.stream_ptr(stream)), "kmeans_init_merge_list")
 
 
 def prune_lower(dist: torch.Tensor, lab: torch.Tensor, xn: torch.Tensor, mc: float, tau: float,

@@ -172,3 +172,24 @@ def test_seeded_first_step_equals_full_step(monkeypatch, n, d, k, scale):
     assert 0 <= m <= n and (not full or m == n)  # more than _PRUNE_CAP candidates: the full pass instead
     if scale >= 4.0:
         assert not full and m < 0.5 * n, m
+
+
+@pytest.mark.parametrize("n,d,k", [(120_000, 128, 64), (60_013, 256, 100)])
+def test_pruned_candidate_pass_equals_full_on_exact_data(monkeypatch, n, d, k):
+    """The second k-means|| round skips the (row, candidate) pairs the triangle inequality rules out
+    (init_classify / init_near_list / K9r candidate pass on the remaining rows). On exactly representable
+    data every distance is exact, so the init centres equal those of the full candidate passes, and the
+    pruned pass really skipped rows."""
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
+    monkeypatch.setenv("CML_KMEANS_PRECISION", "bf16")
+    x = torch.as_tensor(_integer_blobs(n, d, k, seed=n), device="cuda")
+    res = []
+    for pruned in ("1", "0"):
+        monkeypatch.setenv("CML_KMEANS_INIT_PRUNE", pruned)
+        eng = LloydEngine(x, d, k)
+        eng.track_prune = True
+        res.append((eng.init_kmeans_parallel(seed=21), getattr(eng, "_init_prune_history", [])))
+    assert np.array_equal(res[0][0], res[1][0])
+    assert res[1][1] == [] and len(res[0][1]) == 1
+    rows, ca, cb = res[0][1][0]
+    assert rows == n and ca + cb < n
