@@ -1024,12 +1024,13 @@ __global__ __launch_bounds__(256) void init_classify_kernel(const float* __restr
   }
 }
 
-// List A: one wave per batch of 16 rows. Lane u looks up row u (nearest candidate, reach, its relevant
-// new candidates: at most LMAX) so the dependent lookups of the 16 rows overlap; then every row's
-// distances are computed by the whole wave (CPL columns per lane, DPP sums), the relevant candidates'
-// slices loaded together. Strict improvement over the current cost moves the row; among the new
-// candidates ties go to the lowest index (K9r's argmin rule).
-template <int CPL, bool F8, int LMAX>
+// List A: 16 lanes per row (NCOL = Dp/16 columns each, one 16-lane DPP row), 4 rows per wave step.
+// Each lane group looks up its own row (nearest candidate, reach), walks the sorted relevant new
+// candidates (at most LMAX; the wave stops at the longest list of its 4 rows) and keeps the nearest.
+// Strict improvement over the current cost moves the row; ties among the new candidates go to the
+// lowest index (K9r's argmin rule). A 16-lane sum is 4 DPP steps (no row broadcasts), and the f32
+// math is on packed pairs, so a (row, candidate) pair costs ~a dozen vector instructions.
+template <int NCOL, bool F8, int LMAX>
 __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restrict__ X, long long ldx, int Dp,
                                                              float* __restrict__ cost, int* __restrict__ near,
                                                              const float* __restrict__ xn,
@@ -1038,86 +1039,74 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
                                                              const int* __restrict__ tab_j, int m,
                                                              const u16* __restrict__ Y, int off, float tau,
                                                              const int* __restrict__ list, const int* __restrict__ cnt) {
-  using raw_t = typename SegRaw<CPL, F8>::T;
-  using yraw_t = typename RawCols<CPL>::T;
-  constexpr int U = 16;
-  constexpr int ESZ = F8 ? 1 : 2;
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int XB = F8 ? NCOL : 2 * NCOL;  // bytes of this lane's X slice
+  static_assert(XB % 16 == 0 && (2 * NCOL) % 16 == 0, "16-B slices");
   const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
-  const int lane = threadIdx.x & 63;
-  const int col = CPL * lane;
-  const bool active = col < Dp;
+  const int lane = threadIdx.x & 63, g = lane >> 4, sl = lane & 15;
   const long long nwaves = (long long)gridDim.x * (blockDim.x / 64);
   const long long total = *cnt;
-  for (long long b0 = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * U; b0 < total;
-       b0 += nwaves * U) {
-    const int c = (int)(total - b0 < U ? total - b0 : U);
-    const int pr = lane < c ? list[b0 + lane] : 0;
-    // lane u < c: row u's lookups
-    float cr = 0.f;
-    int L = 0, jl[LMAX];
-    if (lane < c) {
-      const int p = near[pr];
-      cr = cost[pr];
-      const float t = init_reach(cr, xn[pr], pn[p], tau);
-      const float* v = tab_v + (long long)p * m;
-      const int* tj = tab_j + (long long)p * m;
+  for (long long base = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 4; base < total;
+       base += nwaves * 4) {
+    const long long idx = base + g;
+    const bool act = idx < total;
+    const int row = act ? list[idx] : list[base];
+    const int p = near[row];
+    const float cr = cost[row];
+    const float t = init_reach(cr, xn[row], pn[p], tau);
+    const float* v = tab_v + (long long)p * m;
+    const int* tj = tab_j + (long long)p * m;
+    f2 xf[NCOL / 2];  // this lane's columns as f32 pairs, in column order
+    {
+      const uint4* src =
+          reinterpret_cast<const uint4*>(xb + (long long)row * ldx * (F8 ? 1 : 2) + (long long)sl * XB);
 #pragma unroll
-      for (int l = 0; l < LMAX; ++l) {
-        const bool in = l < m && v[l] < t;
-        L += in ? 1 : 0;
-        jl[l] = in ? tj[l] : 0;
-      }
-    } else {
+      for (int b = 0; b < XB / 16; ++b) {
+        const uint4 q4 = src[b];
+        const unsigned ws[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
-      for (int l = 0; l < LMAX; ++l) jl[l] = 0;
-    }
-    raw_t w[U];
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long row = __builtin_amdgcn_readlane(pr, u);
-      w[u] = (u < c && active) ? *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ) : raw_t{};
-    }
-    float nbest = 0.f;
-    int nbj = -1;
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      if (u < c) {
-      const int Lu = __builtin_amdgcn_readlane(L, u);
-      float best = __int_as_float(__builtin_amdgcn_readlane(__float_as_int(cr), u));
-      int bj = -1;
-      yraw_t yv[LMAX];
-#pragma unroll
-      for (int l = 0; l < LMAX; ++l) {
-        const int j = __builtin_amdgcn_readlane(jl[l], u);
-        yv[l] = (l < Lu && active) ? *reinterpret_cast<const yraw_t*>(Y + (long long)j * Dp + col) : yraw_t{};
-      }
-#pragma unroll
-      for (int l = 0; l < LMAX; ++l) {
-        if (l < Lu) {
-        const int j = __builtin_amdgcn_readlane(jl[l], u);
-        const unsigned* ys = reinterpret_cast<const unsigned*>(&yv[l]);
-        float cv[CPL];
-#pragma unroll
-        for (int q = 0; q < CPL / 2; ++q) {
-          cv[2 * q] = bf16_to_f32((u16)(ys[q] & 0xffffu));
-          cv[2 * q + 1] = bf16_to_f32((u16)(ys[q] >> 16));
-        }
-        const float d = wave_total_dpp(sqdist_raw<CPL, F8>(w[u], cv));
-        if (d < best || (d == best && bj >= 0 && j < bj)) {
-          best = d;
-          bj = j;
-        }
+        for (int e = 0; e < 4; ++e) {
+          if constexpr (F8) {
+            xf[8 * b + 2 * e] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e], false);
+            xf[8 * b + 2 * e + 1] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e], true);
+          } else {
+            xf[4 * b + e] = f2{__uint_as_float(ws[e] << 16), __uint_as_float(ws[e] & 0xffff0000u)};
+          }
         }
       }
-      if (lane == u) {
-        nbest = best;
-        nbj = bj;
+    }
+    float best = cr;
+    int bj = -1;
+#pragma unroll 1
+    for (int l = 0; l < LMAX && l < m; ++l) {
+      const bool rel = act && v[l] < t;
+      if (__ballot(rel) == 0ull) break;  // sorted: no later candidate is relevant to any of the 4 rows
+      const int j = rel ? tj[l] : 0;
+      const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)j * Dp + (long long)sl * NCOL);
+      f2 acc2 = f2{0.f, 0.f};
+#pragma unroll
+      for (int b = 0; b < (2 * NCOL) / 16; ++b) {
+        const uint4 q4 = ysrc[b];
+        const unsigned ys[4] = {q4.x, q4.y, q4.z, q4.w};
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          const f2 dv = xf[4 * b + e] - f2{__uint_as_float(ys[e] << 16), __uint_as_float(ys[e] & 0xffff0000u)};
+          acc2 = dv * dv + acc2;
+        }
       }
+      float d = acc2.x + acc2.y;  // 16-lane sum: quad swaps, half-row mirror, row mirror
+      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0xB1, 0xf, 0xf, false));
+      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xf, 0xf, false));
+      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xf, 0xf, false));
+      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x140, 0xf, 0xf, false));
+      if (rel && (d < best || (d == best && bj >= 0 && j < bj))) {
+        best = d;
+        bj = j;
       }
     }
-    if (lane < c && nbj >= 0) {
-      cost[pr] = nbest;
-      near[pr] = off + nbj;
+    if (act && sl == 0 && bj >= 0) {
+      cost[row] = best;
+      near[row] = off + bj;
     }
   }
 }
@@ -1825,19 +1814,19 @@ CML_API int cml_kmeans_init_near_list(const void* X, long long ldx, int Dp, int 
                                       const void* Y, int off, float tau, const int* list, const int* cnt,
                                       long long n_cap, void* stream) {
   if (n_cap <= 0) return 0;
-  const int cpl = Dp / 64;
-  const long long blocks = std::max<long long>(1, std::min<long long>((n_cap + 63) / 64, 4096));
+  const int ncol = Dp / 16;
+  const long long blocks = std::max<long long>(1, std::min<long long>((n_cap + 15) / 16, 8192));
   hipStream_t st = (hipStream_t)stream;
 #define CML_NL(C, F)                                                                                                \
   hipLaunchKernelGGL((init_near_list_kernel<C, F, kInitLmax>), dim3((unsigned)blocks), dim3(256), 0, st, X, ldx, Dp, \
                      cost, near, xn, pn, tab_v, tab_j, m, (const u16*)Y, off, tau, list, cnt)
   if (xfp8) {
-    if (cpl == 4) CML_NL(4, true);
-    else if (cpl == 8) CML_NL(8, true);
+    if (ncol == 16) CML_NL(16, true);
+    else if (ncol == 32) CML_NL(32, true);
     else return (int)hipErrorInvalidValue;
-  } else if (cpl == 2) CML_NL(2, false);
-  else if (cpl == 4) CML_NL(4, false);
-  else if (cpl == 8) CML_NL(8, false);
+  } else if (ncol == 8) CML_NL(8, false);
+  else if (ncol == 16) CML_NL(16, false);
+  else if (ncol == 32) CML_NL(32, false);
   else return (int)hipErrorInvalidValue;
 #undef CML_NL
   return cml_status();

@@ -203,18 +203,28 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
                                                                 const double* __restrict__ D, int m, int d,
                                                                 const double* __restrict__ w, int k,
                                                                 unsigned long long key, double* __restrict__ C,
-                                                                double* __restrict__ CT, double* __restrict__ d2) {
+                                                                double* __restrict__ CT, double* __restrict__ d2,
+                                                                bool lds_pw) {
   extern __shared__ __align__(16) unsigned char smem[];
   double* crow = reinterpret_cast<double*>(smem);
+  // with room in LDS the pick weights w·d2 and the distances live there (the serial scans of a pick
+  // then read LDS, not L2); same values and order as the global form
+  const bool in_lds = lds_pw;
+  double* pwl = crow + d;      // [m] pick weights (in_lds)
+  double* d2l = pwl + m;       // [m] running distances (in_lds)
   __shared__ double part[kBlocks];
   __shared__ int pick_sh;
   const int tid = threadIdx.x;
   const int L = (m + kBlocks - 1) / kBlocks;
+  if (in_lds)
+    for (int q = tid; q < m; q += kKppThreads) pwl[q] = w[q];
+  __syncthreads();
   for (int i = 0; i < k; ++i) {
+    auto pw_at = [&](int q) { return in_lds ? pwl[q] : (i == 0 ? w[q] : __dmul_rn(w[q], d2[q])); };
     if (tid < kBlocks) {
       double s = 0.0;
       const int q1 = min(m, (tid + 1) * L);
-      for (int q = tid * L; q < q1; ++q) s = __dadd_rn(s, i == 0 ? w[q] : __dmul_rn(w[q], d2[q]));
+      for (int q = tid * L; q < q1; ++q) s = __dadd_rn(s, pw_at(q));
       part[tid] = s;
     }
     __syncthreads();
@@ -236,7 +246,7 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
             const int q1 = min(m, (b + 1) * L);
             int lastpos = -1;
             for (int q = b * L; q < q1; ++q) {
-              const double pw = i == 0 ? w[q] : __dmul_rn(w[q], d2[q]);
+              const double pw = pw_at(q);
               if (pw > 0.0) lastpos = q;
               c2 = __dadd_rn(c2, pw);
               if (c2 > r) { pick = q; break; }
@@ -248,7 +258,7 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
         }
         if (pick < 0) {  // rounding: the last point of positive weight
           for (int q = m - 1; q >= 0 && pick < 0; --q)
-            if ((i == 0 ? w[q] : __dmul_rn(w[q], d2[q])) > 0.0) pick = q;
+            if (pw_at(q) > 0.0) pick = q;
         }
         if (pick < 0) pick = 0;
       }
@@ -263,7 +273,15 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
       CT[(long long)t * k + i] = v;
     }
     __syncthreads();
-    if (D != nullptr) {  // precomputed pairwise distances: the update is one contiguous row read
+    if (D != nullptr && in_lds) {
+      const double* dr = D + (long long)pk * m;
+      for (int q = tid; q < m; q += kKppThreads) {
+        const double acc = dr[q];
+        const double nd = (i == 0 || acc < d2l[q]) ? acc : d2l[q];
+        d2l[q] = nd;
+        pwl[q] = __dmul_rn(w[q], nd);
+      }
+    } else if (D != nullptr) {  // precomputed pairwise distances: the update is one contiguous row read
       const double* dr = D + (long long)pk * m;
       for (int q = tid; q < m; q += kKppThreads) {
         const double acc = dr[q];
@@ -507,8 +525,12 @@ CML_API int cml_local_kpp(const double* P, const double* PT, int m, int d, const
     const unsigned g = (unsigned)((m + kPairT - 1) / kPairT);
     hipLaunchKernelGGL(local_pairdist_kernel, dim3(g, g), dim3(kThreads), 0, st, P, m, d, D);
   }
-  hipLaunchKernelGGL(local_kpp_kernel, dim3(1), dim3(kKppThreads), (size_t)d * 8, st, P, PT, D, m, d, w, k, key, C,
-                     CT, d2);
+  const size_t big = ((size_t)d + 2 * (size_t)m) * 8;
+  const bool lds_pw = D != nullptr && big <= 150 * 1024;
+  const size_t lds = lds_pw ? big : (size_t)d * 8;
+  if (lds_pw) hipFuncSetAttribute((const void*)local_kpp_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(local_kpp_kernel, dim3(1), dim3(kKppThreads), lds, st, P, PT, D, m, d, w, k, key, C, CT, d2,
+                     lds_pw);
   return cml_status();
 }
 
