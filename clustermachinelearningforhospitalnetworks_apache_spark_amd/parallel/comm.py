@@ -201,6 +201,13 @@ class Communicator:
     def shutdown(self) -> None:
         if self._owns and dist.is_initialized():
             try:
+                # every rank reaches the teardown before any destroys its group: a rank that tore its
+                # gloo transport down while a peer still had traffic in flight aborted under load
+                # (std::terminate from a joinable transport thread)
+                dist.barrier()
+            except Exception:  # pragma: no cover - teardown best effort
+                pass
+            try:
                 dist.destroy_process_group()
             except Exception:  # pragma: no cover - teardown best effort
                 pass
