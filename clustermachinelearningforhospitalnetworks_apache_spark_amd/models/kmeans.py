@@ -168,9 +168,11 @@ class LloydEngine:
         # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
         # removes the per-launch host cost that dominates small shards. Default: single rank (a
         # multi-rank step contains RCCL collectives, which stay eagerly launched).
+        # Multi-rank: the device pruned step is captured as two graphs around its all-reduce (the RCCL
+        # call stays eager between the replays); the chunked full-step path stays eager there.
         if use_graph is None:
-            env = os.environ.get("CML_KMEANS_GRAPH")  # "0": eager steps on one rank (the multi-rank launch path)
-            use_graph = (self.comm.world_size == 1) if env is None else (env == "1" and self.comm.world_size == 1)
+            env = os.environ.get("CML_KMEANS_GRAPH")  # "0": eager steps
+            use_graph = True if env is None else env == "1"
         self.use_graph = bool(use_graph)
         self._graph = None
         self.k = int(k)
@@ -361,7 +363,7 @@ class LloydEngine:
                 self._pst.history.append(self._pdev_last())
         elif self.prune:
             self._step_prune()
-        elif self.gpu and self.use_graph:
+        elif self.gpu and self.use_graph and not self.comm.is_distributed:
             self._step_graph()
         elif self.gpu:
             self._step_gpu()
@@ -373,18 +375,32 @@ class LloydEngine:
         """Replay the captured step (captured on the first call after one eager warm-up step,
         which also settles every lazily allocated buffer). All step state lives in buffers the
         graph reads in place: new centres from set_centers/update are picked up by the replay."""
+        split = self._pdev and self.comm.is_distributed  # graph | all-reduce | graph
         if self._graph is None:
             if not getattr(self, "_graph_warm", False):
                 self._graph_warm = True
                 (self._step_prune_dev if self._pdev else self._step_gpu)()
                 return
             torch.cuda.synchronize(self.device)
-            g = torch.cuda.CUDAGraph()
-            body = self._step_prune_dev if self._pdev else self._step_gpu
-            with torch.cuda.graph(g):
-                body()
-            self._graph = g
-        self._graph.replay()
+            if split:
+                ga, gb = torch.cuda.CUDAGraph(), torch.cuda.CUDAGraph()
+                with torch.cuda.graph(ga):
+                    self._pdev_pre()
+                with torch.cuda.graph(gb):
+                    self._pdev_post()
+                self._graph = (ga, gb)
+            else:
+                g = torch.cuda.CUDAGraph()
+                body = self._step_prune_dev if self._pdev else self._step_gpu
+                with torch.cuda.graph(g):
+                    body()
+                self._graph = g
+        if split:
+            self._graph[0].replay()
+            self.comm.allreduce_async(self.msgs[0]).wait()
+            self._graph[1].replay()
+        else:
+            self._graph.replay()
         if self._pdev:
             self._cost_fn = self._pdev_cost
 
@@ -518,6 +534,12 @@ class LloydEngine:
         writing new labels and top-2 bounds and logging label changes; the incremental sums move by
         the changed rows (exact f64 sums, as the full path); all-reduce; K11; centre statistics for
         the next step's bounds."""
+        self._pdev_pre()
+        self.comm.allreduce_async(self.msgs[0]).wait()
+        self._pdev_post()
+
+    def _pdev_pre(self) -> None:
+        """The device pruned step up to its all-reduce (bounds, gate, K9r passes, sums -> msg)."""
         st, dl = self._pst, self.delta
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
@@ -534,7 +556,10 @@ class LloydEngine:
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0])
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
-        self.comm.allreduce_async(msg).wait()
+
+    def _pdev_post(self) -> None:
+        """The device pruned step after its all-reduce: K11 and the centre statistics of the next bounds."""
+        st, k, d = self._pst, self.k, self.d
         st.cb_old.copy_(self.cb)
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,

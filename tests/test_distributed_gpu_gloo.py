@@ -82,3 +82,74 @@ def test_two_ranks_on_one_gpu_match_single_rank(tmp_path):
     np.testing.assert_array_equal(np.asarray(res["centers"]), ref_centers)
     assert abs(res["cost"] - ref_cost) <= 1e-9 * abs(ref_cost)
     assert res["modes"][0] and not all(res["modes"]), "incremental path not exercised on the ranks"
+
+
+# ---- the default GPU path on two ranks: device k-means|| (pruned candidate passes), the seeded first
+# step and graph-captured pruned steps split around the all-reduce (graph | all-reduce | graph)
+
+N2, D2, K2 = 200_000, 128, 64
+
+
+def _data2():
+    rs = np.random.RandomState(11)
+    cen = rs.randn(K2, D2) * 4
+    x = cen[rs.randint(0, K2, N2)] + rs.randn(N2, D2)
+    return np.round(x * 8) / 8
+
+
+def _fit2(x_local, comm):
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D2, K2, comm, prune=True,
+                      precision="bf16")
+    eng.track_prune = True
+    init = eng.init_kmeans_parallel(seed=5)
+    eng.set_centers(init)
+    seeded = bool(eng._seeded)
+    eng.fit(10, 0.0)
+    torch.cuda.synchronize()
+    return {"init": np.asarray(init).tolist(), "centers": eng.centers.cpu().numpy().tolist(),
+            "cost": eng.training_cost(), "pdev": bool(eng._pdev), "seeded": seeded,
+            "graph": isinstance(eng._graph, tuple) if comm.is_distributed else eng._graph is not None,
+            "hist": eng.prune_history()}
+
+
+def _rank_main2(rank, world, port, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1"})
+    import torch
+    import torch.distributed as dist
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
+    x = _data2()
+    lo, hi = rank * N2 // world, (rank + 1) * N2 // world
+    res = _fit2(x[lo:hi], comm)
+    if rank == 0:
+        with open(out_path, "w") as fh:
+            json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch):
+    """Two ranks on the default GPU path (pruned init, seeded step, split graphs) give the single-rank
+    fit bit for bit: init centres, final centres and cost (1/8-grid data: every f64 sum is exact)."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
+    out = str(tmp_path / "w2d.json")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main2, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = json.load(open(out))
+    ref = _fit2(_data2(), local_comm())
+    assert res["pdev"] and ref["pdev"] and res["seeded"] and res["graph"], res
+    np.testing.assert_array_equal(np.asarray(res["init"]), np.asarray(ref["init"]))
+    np.testing.assert_array_equal(np.asarray(res["centers"]), np.asarray(ref["centers"]))
+    assert abs(res["cost"] - ref["cost"]) <= 1e-9 * abs(ref["cost"])
