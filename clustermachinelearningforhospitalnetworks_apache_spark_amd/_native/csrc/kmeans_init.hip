@@ -228,9 +228,22 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
       part[tid] = s;
     }
     __syncthreads();
-    if (tid == 0) {
-      double total = 0.0;
-      for (int b = 0; b < kBlocks; ++b) total = __dadd_rn(total, part[b]);
+    if (tid < 64) {
+      // wave 0: lane l folds parts 4l..4l+3 in order, an inclusive Hillis-Steele scan over the 64 lane
+      // sums (S[l] = S[l - off] + S[l] at off = 1, 2, ..., 32) gives the total and the prefixes; the
+      // first lane whose prefix exceeds r walks its 4 parts and then the points of the block
+      // (kpp_pick in the host twin: the same operations in the same order)
+      const int l = tid;
+      double q4 = part[4 * l];
+#pragma unroll
+      for (int j = 1; j < 4; ++j) q4 = __dadd_rn(q4, part[4 * l + j]);
+      double S = q4;
+#pragma unroll
+      for (int off = 1; off < 64; off <<= 1) {
+        const double o = __shfl_up(S, off, 64);
+        if (l >= off) S = __dadd_rn(o, S);
+      }
+      const double total = __shfl(S, 63, 64);
       const double u = cu((unsigned long long)i, key);
       int pick = -1;
       if (!(total > 0.0)) {
@@ -238,31 +251,46 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
         pick = pick < m - 1 ? pick : m - 1;
       } else {
         const double r = __dmul_rn(u, total);
-        double cum = 0.0;
-        for (int b = 0; b < kBlocks && pick < 0; ++b) {
-          const double nxt = __dadd_rn(cum, part[b]);
-          if (nxt > r) {
-            double c2 = cum;
-            const int q1 = min(m, (b + 1) * L);
-            int lastpos = -1;
-            for (int q = b * L; q < q1; ++q) {
-              const double pw = pw_at(q);
-              if (pw > 0.0) lastpos = q;
-              c2 = __dadd_rn(c2, pw);
-              if (c2 > r) { pick = q; break; }
+        const unsigned long long over = __ballot(S > r);
+        if (over != 0ull) {
+          const int ls = __builtin_ctzll(over);
+          const double prev = __shfl(S, ls > 0 ? ls - 1 : 0, 64);
+          if (l == ls) {
+            double cum = ls > 0 ? prev : 0.0;
+            int lastb = -1;
+            for (int j = 0; j < 4 && pick < 0; ++j) {
+              const int b = 4 * l + j;
+              const double nxt = __dadd_rn(cum, part[b]);
+              if (part[b] > 0.0) lastb = b;
+              if (nxt > r) {
+                double c2 = cum;
+                const int q1 = min(m, (b + 1) * L);
+                int lastpos = -1;
+                for (int q = b * L; q < q1; ++q) {
+                  const double pw = pw_at(q);
+                  if (pw > 0.0) lastpos = q;
+                  c2 = __dadd_rn(c2, pw);
+                  if (c2 > r) { pick = q; break; }
+                }
+                if (pick < 0) pick = lastpos;
+              }
+              cum = nxt;
             }
-            if (pick < 0) pick = lastpos;
-            if (pick < 0) break;
+            if (pick < 0 && lastb >= 0) {  // rounding between the lane prefix and the part walk
+              const int q1 = min(m, (lastb + 1) * L);
+              for (int q = lastb * L; q < q1; ++q)
+                if (pw_at(q) > 0.0) pick = q;
+            }
           }
-          cum = nxt;
+          pick = __shfl(pick, ls, 64);
         }
-        if (pick < 0) {  // rounding: the last point of positive weight
+        if (pick < 0 && l == 0) {  // rounding: the last point of positive weight
           for (int q = m - 1; q >= 0 && pick < 0; --q)
             if (pw_at(q) > 0.0) pick = q;
         }
         if (pick < 0) pick = 0;
       }
-      pick_sh = pick;
+      if (l == 0) pick_sh = pick;
     }
     __syncthreads();
     const int pk = pick_sh;

@@ -51,8 +51,18 @@ void kpp(const double* P, int m, int d, const double* w, int k, uint64_t key, do
       for (int q = b * L; q < q1; ++q) s = s + pw(q);
       part[b] = s;
     }
-    double total = 0.0;
-    for (int b = 0; b < kBlocks; ++b) total = total + part[b];
+    // lane sums of 4 parts, inclusive Hillis-Steele scan over the 64 lanes (the device's wave 0)
+    double S[64], T[64];
+    for (int l = 0; l < 64; ++l) {
+      double q4 = part[4 * l];
+      for (int j = 1; j < 4; ++j) q4 = q4 + part[4 * l + j];
+      S[l] = q4;
+    }
+    for (int off = 1; off < 64; off <<= 1) {
+      for (int l = 0; l < 64; ++l) T[l] = l >= off ? S[l - off] + S[l] : S[l];
+      std::memcpy(S, T, sizeof(S));
+    }
+    const double total = S[63];
     const double u = cu((uint64_t)i, key);
     int pick = -1;
     if (!(total > 0.0)) {
@@ -60,23 +70,35 @@ void kpp(const double* P, int m, int d, const double* w, int k, uint64_t key, do
       pick = pick < m - 1 ? pick : m - 1;
     } else {
       const double r = u * total;
-      double cum = 0.0;
-      for (int b = 0; b < kBlocks && pick < 0; ++b) {
-        const double nxt = cum + part[b];
-        if (nxt > r) {
-          double c2 = cum;
-          const int q1 = std::min(m, (b + 1) * L);
-          int lastpos = -1;
-          for (int q = b * L; q < q1; ++q) {
-            const double p = pw(q);
-            if (p > 0.0) lastpos = q;
-            c2 = c2 + p;
-            if (c2 > r) { pick = q; break; }
+      int ls = -1;
+      for (int l = 0; l < 64 && ls < 0; ++l)
+        if (S[l] > r) ls = l;
+      if (ls >= 0) {
+        double cum = ls > 0 ? S[ls - 1] : 0.0;
+        int lastb = -1;
+        for (int j = 0; j < 4 && pick < 0; ++j) {
+          const int b = 4 * ls + j;
+          const double nxt = cum + part[b];
+          if (part[b] > 0.0) lastb = b;
+          if (nxt > r) {
+            double c2 = cum;
+            const int q1 = std::min(m, (b + 1) * L);
+            int lastpos = -1;
+            for (int q = b * L; q < q1; ++q) {
+              const double p = pw(q);
+              if (p > 0.0) lastpos = q;
+              c2 = c2 + p;
+              if (c2 > r) { pick = q; break; }
+            }
+            if (pick < 0) pick = lastpos;
           }
-          if (pick < 0) pick = lastpos;
-          if (pick < 0) break;
+          cum = nxt;
         }
-        cum = nxt;
+        if (pick < 0 && lastb >= 0) {
+          const int q1 = std::min(m, (lastb + 1) * L);
+          for (int q = lastb * L; q < q1; ++q)
+            if (pw(q) > 0.0) pick = q;
+        }
       }
       if (pick < 0)
         for (int q = m - 1; q >= 0 && pick < 0; --q)
