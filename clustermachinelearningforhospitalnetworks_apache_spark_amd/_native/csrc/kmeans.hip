@@ -700,6 +700,18 @@ __device__ __forceinline__ void add_raw(double (&acc)[CPL], const typename RawCo
   }
 }
 
+// The same on the sum grid: every value scaled by qs = 2^S and rounded to an integer (exact in f64),
+// so the f64 sums are exact integers whatever the data's exponent span (models/kmeans.py _sum_grid).
+template <int CPL>
+__device__ __forceinline__ void add_raw_q(double (&acc)[CPL], const typename RawCols<CPL>::T& w, double qs) {
+  const unsigned* ws = reinterpret_cast<const unsigned*>(&w);
+#pragma unroll
+  for (int q = 0; q < CPL / 2; ++q) {
+    acc[2 * q] += rint((double)bf16_to_f32((u16)(ws[q] & 0xffffu)) * qs);
+    acc[2 * q + 1] += rint((double)bf16_to_f32((u16)(ws[q] >> 16)) * qs);
+  }
+}
+
 // OCP e4m3fn rows: CPL bytes per lane.
 template <int CPL> struct RawCols8;
 template <> struct RawCols8<4> { using T = unsigned; };
@@ -787,6 +799,7 @@ struct SegUB {
   const u16* cb;
   long long ldc;
   float* ub;
+  double qs;  // sum grid scale (0: plain f64 sums of the raw values)
 };
 
 // Sort regime, pass 4: segmented sum over the label-sorted order. Wave w streams sorted
@@ -806,7 +819,7 @@ __device__ __forceinline__ long long seg_chunk(long long filled, long long waves
   return c > 128 ? c : 128;
 }
 
-template <int CPL, bool F8, bool UB = false>
+template <int CPL, bool F8, bool UB = false, bool Q = false>
 __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k,
@@ -893,7 +906,10 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
         for (int j = 0; j < CPL; ++j) acc[j] += (double)part[j];
       } else {
 #pragma unroll
-        for (int u = 0; u < U; ++u) add_raw<CPL>(acc, w[u]);
+        for (int u = 0; u < U; ++u) {
+          if constexpr (Q) add_raw_q<CPL>(acc, w[u], sub.qs);
+          else add_raw<CPL>(acc, w[u]);
+        }
       }
     } else {
       // a cluster boundary inside this batch (~k + #waves batches per pass): walk its rows one at a
@@ -926,6 +942,7 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
           mine = lane == u ? t : mine;
         }
         if constexpr (F8) add_raw8<CPL>(acc, v);
+        else if constexpr (Q) add_raw_q<CPL>(acc, v, sub.qs);
         else add_raw<CPL>(acc, v);
       }
       if constexpr (UB) {
@@ -1173,7 +1190,7 @@ __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ 
 __global__ void kmeans_update_kernel(const double* __restrict__ bufs, int nbuf, long long bstride,
                                      int k, int D, double* __restrict__ cent, u16* __restrict__ cb,
                                      long long ldc, int Dp, float* __restrict__ cnorm,
-                                     double* __restrict__ shift2) {
+                                     double* __restrict__ shift2, double unit) {
   __shared__ double rn[16], rs[16];
   const int c = blockIdx.x, tid = threadIdx.x;
   const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
@@ -1193,7 +1210,7 @@ __global__ void kmeans_update_kernel(const double* __restrict__ bufs, int nbuf, 
       if (bufs != nullptr && cnt > 0.0) {
         double s = 0.0;
         for (int b = 0; b < nbuf; ++b) s += bufs[b * bstride + (long long)c * D + d];
-        nv = s / cnt;
+        nv = (s * unit) / cnt;  // unit: the sum grid step (a power of two: exact), 1 for plain sums
       }
       sh += (nv - old) * (nv - old);
       cent[(long long)c * D + d] = nv;
@@ -1478,25 +1495,30 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
 // bound of the filled positions (the kernels clamp to seg[k]).
 int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, const int* perm, const int* seg, int k,
                   int cpl, int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate, int want,
-                  hipStream_t st, SegUB sub = SegUB{nullptr, 0, nullptr}) {
+                  hipStream_t st, SegUB sub = SegUB{nullptr, 0, nullptr, 0.0}) {
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
-#define CML_SEG(C, F)                                                                                               \
-  if (sub.ub != nullptr)                                                                                            \
-    hipLaunchKernelGGL((kmeans_segacc<C, F, true>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D,    \
-                       perm, seg, k, msg, slots, slot_c, gate, want, sub);                                          \
-  else                                                                                                              \
-    hipLaunchKernelGGL((kmeans_segacc<C, F, false>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D,   \
-                       perm, seg, k, msg, slots, slot_c, gate, want, sub)
+#define CML_SEG_L(C, F, U, Q)                                                                                       \
+  hipLaunchKernelGGL((kmeans_segacc<C, F, U, Q>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm, \
+                     seg, k, msg, slots, slot_c, gate, want, sub)
+#define CML_SEG(C, F)                                                  \
+  if (sub.ub != nullptr) {                                             \
+    if (!F && sub.qs != 0.0) CML_SEG_L(C, F, true, !F);               \
+    else CML_SEG_L(C, F, true, false);                                 \
+  } else {                                                             \
+    if (!F && sub.qs != 0.0) CML_SEG_L(C, F, false, !F);              \
+    else CML_SEG_L(C, F, false, false);                                \
+  }
   if (xfp8) {
-    if (cpl == 4) CML_SEG(4, true);
-    else if (cpl == 8) CML_SEG(8, true);
-    else if (cpl == 16) CML_SEG(16, true);
+    if (cpl == 4) CML_SEG(4, true)
+    else if (cpl == 8) CML_SEG(8, true)
+    else if (cpl == 16) CML_SEG(16, true)
     else return (int)hipErrorInvalidValue;
-  } else if (cpl == 2) CML_SEG(2, false);
-  else if (cpl == 4) CML_SEG(4, false);
-  else if (cpl == 8) CML_SEG(8, false);
+  } else if (cpl == 2) CML_SEG(2, false)
+  else if (cpl == 4) CML_SEG(4, false)
+  else if (cpl == 8) CML_SEG(8, false)
   else return (int)hipErrorInvalidValue;
 #undef CML_SEG
+#undef CML_SEG_L
   const int e = cml_status();
   if (e) return e;
   hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, n, waves, slots, slot_c, msg, gate,
@@ -1697,23 +1719,24 @@ static int sort_accum(const void* X, long long n, long long ldx, int Dp, int D, 
                       const int* hist, int nblk, int round_rows, int k, int kp, const double* cost_part, int ncost,
                       int* off, int* seg, int* perm, int cpl, int seg_grid, double* msg, double* slots, int* slot_c,
                       int xfp8, const int* gate, void* stream, SegUB sub);
+// qscale: the sum grid (0 = plain f64 sums); see add_raw_q.
 CML_API int cml_kmeans_sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                   const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
                                   const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
                                   int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
-                                  void* stream) {
+                                  double qscale, void* stream) {
   return sort_accum(X, n, ldx, Dp, D, labels, rank, hist, nblk, round_rows, k, kp, cost_part, ncost, off, seg, perm,
-                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{nullptr, 0, nullptr});
+                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{nullptr, 0, nullptr, qscale});
 }
 // The same, also writing ub[row] >= |x_row - cb[label]| (bf16 centres, row stride ldc) for every row.
 CML_API int cml_kmeans_sort_accum_ub(const void* X, long long n, long long ldx, int Dp, int D, const int* labels,
                                      const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
                                      const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
                                      int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
-                                     const void* cb, long long ldc, float* ub, void* stream) {
+                                     const void* cb, long long ldc, float* ub, double qscale, void* stream) {
   if (cb == nullptr || ub == nullptr || ldc < Dp) return (int)hipErrorInvalidValue;
   return sort_accum(X, n, ldx, Dp, D, labels, rank, hist, nblk, round_rows, k, kp, cost_part, ncost, off, seg, perm,
-                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{(const u16*)cb, ldc, ub});
+                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{(const u16*)cb, ldc, ub, qscale});
 }
 static int sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels, const int* rank,
                       const int* hist, int nblk, int round_rows, int k, int kp, const double* cost_part, int ncost,
@@ -1758,7 +1781,7 @@ CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, 
                                    const int* mode, int k, int* dh, int* dseg,
                                    int* cursor, int* dperm, int cpl, int seg_grid, double* dsum, double* slots,
                                    int* slot_c, double* acc, const double* cost_part, int ncost, double* msg, int xfp8,
-                                   void* stream) {
+                                   double qscale, void* stream) {
   hipStream_t st = (hipStream_t)stream;
   const size_t lh = sizeof(int) * 2 * (size_t)k;
   hipLaunchKernelGGL(kmeans_delta_hist, dim3(nblk), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
@@ -1771,7 +1794,7 @@ CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, 
   if (e) return e;
   if (cap > 0) {
     e = launch_segsum(X, 2LL * cap, ldx, Dp, D, dperm, dseg, 2 * k, cpl, seg_grid, dsum, slots, slot_c, xfp8, mode, 0,
-                      st);
+                      st, SegUB{nullptr, 0, nullptr, qscale});
     if (e) return e;
   }
   const long long total = (long long)k * D + k + 1;
@@ -1787,9 +1810,10 @@ CML_API long long cml_kmeans_seg_slot_doubles(int seg_grid, int D) {
 CML_API long long cml_kmeans_seg_slot_ints(int seg_grid) { return 2LL * seg_grid * (kSegThreads / 64); }
 
 CML_API int cml_kmeans_update(const double* bufs, int nbuf, long long bstride, int k, int D, double* cent, void* cb,
-                              long long ldc, int Dp, int Kp, float* cnorm, double* shift2, void* stream) {
+                              long long ldc, int Dp, int Kp, float* cnorm, double* shift2, double unit,
+                              void* stream) {
   hipLaunchKernelGGL(kmeans_update_kernel, dim3(Kp), dim3(256), 0, (hipStream_t)stream, bufs, nbuf, bstride, k, D,
-                     cent, (u16*)cb, ldc, Dp, cnorm, shift2);
+                     cent, (u16*)cb, ldc, Dp, cnorm, shift2, unit);
   return cml_status();
 }
 

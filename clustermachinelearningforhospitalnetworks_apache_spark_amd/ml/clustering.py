@@ -78,8 +78,12 @@ class KMeans(Estimator):
         pv = conf.get("cml.ml.kmeans.prune", None)
         prune = None if pv is None else str(pv).lower() in ("1", "true")
         precision = conf.get("cml.ml.kmeans.precision", "auto")
+        rv = conf.get("cml.ml.kmeans.refreshInterval", None)
+        refresh = None if rv is None else int(rv)
+        # an out-of-core feature column (host rows on a GPU session): streamed Lloyd passes
+        dev = df._device if (not x.is_cuda and df._device.type == "cuda") else None
         eng = LloydEngine(x, d, k, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                          precision=precision, weights=weights)
+                          precision=precision, weights=weights, refresh_interval=refresh, device=dev)
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
         n_global = int(comm.sum_scalar(float(eng.n)))
@@ -101,7 +105,7 @@ class KMeans(Estimator):
             init = arrs["centers"]
             if init.shape[0] < k:
                 eng = LloydEngine(x, d, init.shape[0], comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                                  precision=precision, weights=weights)
+                                  precision=precision, weights=weights, refresh_interval=refresh, device=dev)
         elif self.getInitMode() == "random":
             with trace("kmeans.init"):
                 init = eng.init_random(seed)
@@ -112,7 +116,7 @@ class KMeans(Estimator):
             if k_eff < k:
                 init = init[:k_eff]
                 eng = LloydEngine(x, d, k_eff, comm, row_ids=df._row_ids, spherical=spherical, prune=prune,
-                                  precision=precision, weights=weights)
+                                  precision=precision, weights=weights, device=dev)
         eng.set_centers(init)
 
         def on_iter(it):
@@ -197,6 +201,12 @@ class KMeansModel(Model):
         """(labels, distance) per local row: squared euclidean, or 1 - cos for distanceMeasure="cosine"
         (unit rows against the unit centres: ||x - c||² / 2)."""
         x = df._feature_matrix(self.getFeaturesCol())
+        if not x.is_cuda and df._device.type == "cuda" and not self._cosine():
+            # out-of-core column: the streamed MFMA assign (models/kmeans.py _assign_all)
+            from ..models.kmeans import LloydEngine
+            eng = LloydEngine(x, x.shape[1], len(self._centers), df._comm, device=df._device)
+            lab, dist = eng.assign(torch.as_tensor(self._centers))
+            return lab.long(), dist.to(torch.float64)
         c = torch.as_tensor(self._centers, device=x.device)
         cos = self._cosine()
         prec = df._session.conf.get("cml.ml.kmeans.precision", "auto").lower()

@@ -106,9 +106,12 @@ def cached_row_sqnorm(x: torch.Tensor, n: int, dp: int) -> torch.Tensor:
     ent = getattr(x, "_cml_xnorm", None)
     if ent is not None and ent[0] == x._version and ent[1] == (n, dp):
         return ent[2]
-    xn = K.row_sqnorm(x, n, dp)
+    xn = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
+    er = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device=x.device)
+    if n:
+        K.row_pass(x, n, dp, xn, erange=er)
     try:
-        x._cml_xnorm = (x._version, (n, dp), xn)
+        x._cml_xnorm = (x._version, (n, dp), xn, er)
     except (AttributeError, RuntimeError):
         pass
     return xn
@@ -121,8 +124,27 @@ class LloydEngine:
                  row_ids: Optional[torch.Tensor] = None, row_chunks: Optional[int] = None,
                  accum_mode: Optional[str] = None, use_graph: Optional[bool] = None,
                  incremental: Optional[bool] = None, spherical: bool = False, prune: Optional[bool] = None,
-                 precision: Optional[str] = None, weights: Optional[torch.Tensor] = None):
+                 precision: Optional[str] = None, weights: Optional[torch.Tensor] = None,
+                 refresh_interval: Optional[int] = None, device: Optional[torch.device] = None,
+                 stream_chunk_rows: Optional[int] = None):
         self.comm = comm or local_comm()
+        # out-of-core rows (utils/hoststream.py): host rows with a GPU `device` stay in pinned host memory
+        # and every pass over X streams them through two device buffers (full steps; the per-row state —
+        # norms, labels, k-means|| costs — lives on the device)
+        self._hs = None
+        streamed = device is not None and torch.device(device).type == "cuda" and not x.is_cuda
+        if streamed:
+            if weights is not None or spherical:
+                raise ValueError("streamed (out-of-core) KMeans supports unweighted euclidean fits")
+            if x.dtype not in (torch.bfloat16, torch.float8_e4m3fn):
+                x = to_device_matrix(x, d)  # bf16 on the host
+            precision, prune, incremental, use_graph = "bf16", False, False, False
+        # full re-accumulation of the incremental sums every refresh_interval steps (0 = never: the sum
+        # grid of _sum_grid already keeps incremental == full bit for bit; conf
+        # cml.ml.kmeans.refreshInterval / env CML_KMEANS_REFRESH turn on the belt-and-braces refresh)
+        if refresh_interval is None:
+            refresh_interval = int(os.environ.get("CML_KMEANS_REFRESH", "0") or 0)
+        self.refresh_interval = max(0, int(refresh_interval))
         # weights (Spark's weightCol, KMeans.scala runAlgorithm): centre = Σ w·x / Σ w, cost = Σ w·d²,
         # k-means|| candidates weighted by the summed weight of their rows. Weighted fits run the
         # source-precision path (f64 rows, deterministic f64 sums of [w·x | w]).
@@ -142,6 +164,8 @@ class LloydEngine:
             raise ValueError(f"KMeans precision must be 'auto', 'bf16' or 'exact', got {precision!r}")
         if precision == "auto":
             precision = "exact" if (not x.is_cuda or x.dtype in (torch.float32, torch.float64)) else "bf16"
+        if streamed:
+            precision = "bf16"
         if precision == "exact" and x.is_cuda and x.dtype not in (torch.float32, torch.float64):
             raise ValueError(f"precision 'exact' needs f32/f64 rows, got {x.dtype}")
         self.precision = precision
@@ -179,10 +203,19 @@ class LloydEngine:
         self.d = int(d)
         # the MFMA kernels run only on the bf16 path; the exact path runs the reference algorithm (the
         # torch f64 ops, with the f64 HIP kernels for assignment and sums) on the rows' device
-        self.gpu = x.is_cuda and precision == "bf16"
+        self.gpu = (x.is_cuda or streamed) and precision == "bf16"
         self.n = int(x.shape[0])
-        self.device = x.device
-        if self.gpu:
+        self.device = torch.device(device) if streamed else x.device
+        if streamed:
+            from ..utils.hoststream import HostRowStream, pinned_rows
+            self.x = pinned_rows(to_device_matrix(x, d))
+            self.dp = self.x.shape[1]
+            if stream_chunk_rows is None:  # ~1 GiB per buffer
+                stream_chunk_rows = max(1024, (1 << 30) // (self.dp * self.x.element_size()))
+            bounds = HostRowStream.chunk_bounds(self.n, stream_chunk_rows)
+            row_chunks = len(bounds) - 1
+            self._hs = HostRowStream(self.x, bounds[1] - bounds[0] if self.n else 1, self.device)
+        elif self.gpu:
             self.x = to_device_matrix(x, d)
             self.dp = self.x.shape[1]
         else:
@@ -202,6 +235,8 @@ class LloydEngine:
         if row_chunks is None:
             row_chunks = 2 if (self.comm.is_distributed and self.n >= (1 << 20)) else 1
         self.row_chunks = max(1, min(int(row_chunks), max(1, self.n)))
+        if self._hs is not None:
+            self.row_chunks = len(bounds) - 1
         self.centers = torch.zeros((self.k, self.d), dtype=torch.float64, device=self.device)
         self.iterations = 0
         self._cost_fn = None
@@ -209,6 +244,9 @@ class LloydEngine:
         self._shift2 = None
         self.delta = None  # incremental-sums state (GPU sort regime), see _alloc_gpu
         self._pst = None  # pruned-step state, see _step_prune
+        # sum grid of the device sort-regime accumulates (_sum_grid): qscale 0 / unit 1 = plain f64 sums
+        self._qscale, self._unit, self._grid_done = 0.0, 1.0, False
+        self.sum_grid = None  # the grid step when the rows are summed on a grid
         if self.gpu:
             self._alloc_gpu()
 
@@ -217,9 +255,13 @@ class LloydEngine:
         dev = self.device
         k, d, dp, n = self.k, self.d, self.dp, self.n
         self.kp = round_up(k, 32)
-        bounds = [round(i * n / self.row_chunks) for i in range(self.row_chunks + 1)]
-        # keep chunk boundaries on 32-row tiles
-        bounds = [min(n, round_up(b, 32)) if 0 < i < self.row_chunks else b for i, b in enumerate(bounds)]
+        if self._hs is not None:
+            from ..utils.hoststream import HostRowStream
+            bounds = HostRowStream.chunk_bounds(n, self._hs.chunk_rows)
+        else:
+            bounds = [round(i * n / self.row_chunks) for i in range(self.row_chunks + 1)]
+            # keep chunk boundaries on 32-row tiles
+            bounds = [min(n, round_up(b, 32)) if 0 < i < self.row_chunks else b for i, b in enumerate(bounds)]
         self.bounds = bounds
         maxn = max(bounds[i + 1] - bounds[i] for i in range(self.row_chunks)) if n else 0
         fp8 = K.is_fp8(self.x)
@@ -234,11 +276,12 @@ class LloydEngine:
         # tensor's cache, else computed lazily (_ensure_norms) — k-means|| init fuses them into its
         # first pass over X
         ent = getattr(self.x, "_cml_xnorm", None)
+        self._erange = None  # bf16 exponent range of X (exactness of the f64 sums), from the row pass
         if ent is not None and ent[0] == self.x._version and ent[1] == (n, dp):
             self._xnorm, self._norms_ready = ent[2], True
+            self._erange = ent[3] if len(ent) > 3 else None
         else:
             self._xnorm, self._norms_ready = torch.empty(max(n, 1), dtype=torch.float32, device=dev), False
-        self._erange = None  # bf16 exponent range of X (exactness of the f64 sums), from the row pass
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
             self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
@@ -287,14 +330,27 @@ class LloydEngine:
         if mxv is not None:
             mxv.zero_()
         if n:
-            K.row_pass(self.x, n, dp, self._xnorm, c0, c0n, cost, near, xn_max=mxv, erange=self._erange)
+            for _, r0, r1, xc in self._x_chunks(whole=True):
+                K.row_pass(xc, r1 - r0, dp, self._xnorm[r0:r1], c0, c0n, None if cost is None else cost[r0:r1],
+                           None if near is None else near[r0:r1], xn_max=mxv, erange=self._erange)
         if mxv is not None and self.comm.is_distributed:
             self.comm.allreduce_(mxv, op="max")
         self._norms_ready = True
         try:
-            self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm)
+            self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm, self._erange)
         except (AttributeError, RuntimeError):
             pass
+
+    def _x_chunks(self, whole: bool = False):
+        """(chunk, r0, r1, device rows) over the row chunks: slices of the resident matrix (one slice of
+        every row with ``whole``), or the host rows streamed through the double buffer."""
+        if self._hs is not None:
+            yield from self._hs.chunks(self.bounds)
+        elif whole:
+            yield 0, 0, self.n, self.x
+        else:
+            for c in range(self.row_chunks):
+                yield c, self.bounds[c], self.bounds[c + 1], self.x[self.bounds[c]:self.bounds[c + 1]]
 
     def _ensure_norms(self) -> None:
         if self.gpu and not self._norms_ready:
@@ -351,6 +407,12 @@ class LloydEngine:
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
         self._ensure_norms()
+        self._sum_grid()
+        if (self.delta is not None and self.refresh_interval and self.iterations
+                and self.iterations % self.refresh_interval == 0):
+            self.delta.invalidate()  # device flag: graph replays take the full accumulate too
+            if self._pdev:  # a pruned step has no counting-sort ranks of every row: a full step
+                self._pst.force.fill_(1)
         if self._pdev:
             if getattr(self, "_seeded", False):
                 self._seeded = False
@@ -370,6 +432,43 @@ class LloydEngine:
         else:
             self._step_cpu()
         self.iterations += 1
+
+    def _sum_grid(self) -> None:
+        """Exactness of the device f64 sums (once per fit, a collective). The incremental sums are only
+        equal to a full re-accumulation while every f64 sum is exact: a bf16 row value is a multiple of
+        2^(emin - 134) below 2^(emax - 126) (biased exponents over the data, from the row pass), so
+        n of them sum exactly while log2(n) + (emax - emin) + 8 <= 53. When the data's exponent span
+        breaks that (tiny values beside large ones), every value is summed on the grid
+        g = 2^(emax - 126 + ceil(log2(n + 1)) - 52) instead — scaled by 1/g and rounded to an integer, so
+        the sums are exact integers in any order and K11 scales them back. The rounding (at most g/2
+        per value, at the headline scale 2^-20 against values up to 2^5) happens once per value and in
+        the same way on every path, so full, incremental, pruned and multi-rank sums stay equal bit for
+        bit. fp8 rows (multiples of 2^-9 below 2^9) are always exact."""
+        if self._grid_done:
+            return
+        self._grid_done = True
+        if not self.gpu or K.is_fp8(self.x) or self.cplan.mode != "sort" or (self.prune and not self._pdev):
+            return
+        if self._erange is None:  # norms came from a cache without the range: one more pass for it
+            er = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device=self.device)
+            if self.n:
+                tmp = torch.empty(self.n, dtype=torch.float32, device=self.device)
+                for _, r0, r1, xc in self._x_chunks(whole=True):
+                    K.row_pass(xc, r1 - r0, self.dp, tmp[r0:r1], erange=er)
+            self._erange = er
+        lo = self._erange[0:1].to(torch.int64).clone()
+        hi = self._erange[1:2].to(torch.int64).clone()
+        if self.comm.is_distributed:
+            self.comm.allreduce_(lo, op="min")
+            self.comm.allreduce_(hi, op="max")
+        lo, hi, gn = int(lo.item()), int(hi.item()), self.global_n
+        if hi < 0 or gn == 0:  # every value is zero
+            return
+        lg = math.ceil(math.log2(gn + 1))
+        if lg + (hi - max(lo, 1)) + 8 <= 53:
+            return  # plain f64 sums are exact
+        g = (hi - 126) + lg - 52
+        self._qscale, self._unit, self.sum_grid = 2.0 ** -g, 2.0 ** g, 2.0 ** g
 
     def _step_graph(self):
         """Replay the captured step (captured on the first call after one eager warm-up step,
@@ -409,12 +508,10 @@ class LloydEngine:
 
     def _step_gpu(self):
         handles = []
-        for c in range(self.row_chunks):
-            r0, r1 = self.bounds[c], self.bounds[c + 1]
+        for c, r0, r1, xc in self._x_chunks():
             nrow = r1 - r0
             msg = self.msgs[c]
             if nrow > 0:
-                xc = self.x[r0:r1]
                 lab = self.labels[r0:r1]
                 if self.cplan.mode == "priv":
                     K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
@@ -431,14 +528,15 @@ class LloydEngine:
                     dl.gate(c)
                     K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
                                       self.cost_part, self.off, self.seg, self.perm, self.cplan, dl.acc[c],
-                                      self.slots, gate=dl.mode[c])
-                    dl.accumulate(xc, self.dp, lab, c, self.cost_part, self.aplan.grid, msg)
+                                      self.slots, gate=dl.mode[c], qscale=self._qscale)
+                    dl.accumulate(xc, self.dp, lab, c, self.cost_part, self.aplan.grid, msg, qscale=self._qscale)
                 else:
                     rank = self.rank[r0:r1]
                     K.assign_bf16(xc, nrow, self.dp, self.cb, self.cnorm, self.aplan, lab, self._best(r0, r1),
                                   self.cost_part, self.hist, rank, xnorm=self.xnorm[r0:r1])
                     K.accumulate_sort(xc, nrow, self.dp, self.d, lab, rank, self.hist, self.aplan, self.k,
-                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, msg, self.slots)
+                                      self.cost_part, self.off, self.seg, self.perm, self.cplan, msg, self.slots,
+                                      qscale=self._qscale)
             else:
                 msg.zero_()
             handles.append(self.comm.allreduce_async(msg))
@@ -452,7 +550,7 @@ class LloydEngine:
         if self.spherical:
             self._prev_centers.copy_(self.centers)
         K.update_centers(msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
-                         self.shift2)
+                         self.shift2, unit=self._unit)
         if self.spherical:  # unit-length centres (empty clusters keep their old, already unit, centre)
             self.centers.div_(self.centers.norm(dim=1, keepdim=True).clamp_(min=1e-300))
             torch.sum((self.centers - self._prev_centers) ** 2, dim=1, out=self.shift2)
@@ -554,8 +652,8 @@ class LloydEngine:
                         gate=st.pmode, want=0)
         dl.gate(0)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
-                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0])
-        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
+                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
+        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
 
     def _pdev_post(self) -> None:
         """The device pruned step after its all-reduce: K11 and the centre statistics of the next bounds."""
@@ -624,8 +722,8 @@ class LloydEngine:
         # full pass (the seeded lower bounds stay: d2 - r is far below what they are compared with)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], ub_centres=self.cb,
-                          ub=st.ub)
-        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg)
+                          ub=st.ub, qscale=self._qscale)
+        dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
         self.comm.allreduce_async(msg).wait()
         st.cb_old.copy_(self.cb)
         self._update_gpu(self.msgs)
@@ -645,7 +743,7 @@ class LloydEngine:
         self.comm.allreduce_(q)
         c = st.cb_old[:k, :d].to(torch.float64)
         msg = self.msgs[0]
-        s_, cnt = msg[:kd].view(k, d), msg[kd:kd + k]
+        s_, cnt = msg[:kd].view(k, d) * self._unit, msg[kd:kd + k]
         cost = q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()
         return cost.clamp(min=0.0)
 
@@ -948,7 +1046,19 @@ class LloydEngine:
         if not self.gpu:
             return K.assign_reference(self.x, self.centers if centers is None else centers)
         self._ensure_norms()
-        return assign_gpu(self.x, self.dp, self.d, self.centers if centers is None else centers, self.xnorm)
+        return self._assign_all(self.centers if centers is None else centers)
+
+    def _assign_all(self, centers: torch.Tensor):
+        """(labels, distances) of every local row on the MFMA path (streamed chunk by chunk out of core)."""
+        if self._hs is None:
+            return assign_gpu(self.x, self.dp, self.d, centers, self.xnorm)
+        lab = torch.empty(max(self.n, 1), dtype=torch.int32, device=self.device)
+        best = torch.empty(max(self.n, 1), dtype=torch.float32, device=self.device)
+        for _, r0, r1, xc in self._x_chunks():
+            if r1 > r0:
+                lc, bc = assign_gpu(xc, self.dp, self.d, centers, self._xnorm[r0:r1])
+                lab[r0:r1], best[r0:r1] = lc, bc
+        return lab[: self.n], best[: self.n]
 
     @property
     def last_cost(self):
@@ -986,6 +1096,8 @@ class LloydEngine:
         return all_rows[order].cpu().numpy()
 
     def _rows_f64(self, idx: torch.Tensor) -> torch.Tensor:
+        if self._hs is not None:  # host rows
+            return self.x[idx.long().cpu(), : self.d].to(torch.float64).to(self.device)
         if self.gpu:
             return self.x[idx.long(), : self.d].to(torch.float64)
         return self.x[idx.long()]
@@ -996,7 +1108,7 @@ class LloydEngine:
             lab, best = K.assign_reference(self.x, cands)
             return best, lab
         self._ensure_norms()
-        lab, best = assign_gpu(self.x, self.dp, self.d, cands, self.xnorm)
+        lab, best = self._assign_all(cands)
         return best.to(torch.float64), lab.long()
 
     def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
@@ -1139,7 +1251,8 @@ class LloydEngine:
             return
         lab = torch.zeros(n, dtype=torch.int32, device=dev)
         best = torch.empty(n, dtype=torch.float32, device=dev)
-        c0 = 0
+        xn = self.xnorm
+        parts, c0 = [], 0
         for size in self._candidate_chunks(new.shape[0]):
             ch = new[c0:c0 + size].to(torch.float64).contiguous()
             kc = ch.shape[0]
@@ -1147,10 +1260,18 @@ class LloydEngine:
             cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
             cn = torch.zeros(kp, dtype=torch.float32, device=dev)
             K.update_centers(None, kc, d, ch.clone(), cb, dp, kp, cn, None)
-            plan = K.plan_assign(n, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
-            K.assign_bf16(self.x, n, dp, cb, cn, plan, lab, best, None, xnorm=self.xnorm)
-            K.init_merge(costs, nearest, best, lab, off + c0, n)
+            parts.append((c0, kc, cb, cn))
             c0 += size
+        # rows outer (one read of X per pass, streamed out of core), candidate chunks inner: the merges
+        # of a row run in candidate order either way
+        for _, r0, r1, xc in self._x_chunks(whole=True):
+            m = r1 - r0
+            if m == 0:
+                continue
+            for c0, kc, cb, cn in parts:
+                plan = K.plan_assign(m, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
+                K.assign_bf16(xc, m, dp, cb, cn, plan, lab[r0:r1], best[r0:r1], None, xnorm=xn[r0:r1])
+                K.init_merge(costs[r0:r1], nearest[r0:r1], best[r0:r1], lab[r0:r1], off + c0, m)
 
     _INIT_LMAX = 8  # relevant new candidates a row may have to take the per-row path (else the K9r pass)
 

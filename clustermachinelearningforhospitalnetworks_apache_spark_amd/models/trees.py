@@ -267,8 +267,11 @@ class ForestEngine:
         return out
 
     def histogram(self, bins, node_of, wt, nodes: int) -> torch.Tensor:
-        """(T, nodes, d, nbins, S) statistics of this rank's rows. GPU: int64 fixed point (scale
-        ``self.scales``), converted by ``to_stats`` after the all-reduce; CPU: float64."""
+        """(T, nodes, d, nbins, S) statistics of this rank's rows in int64 fixed point (scale
+        ``self.scales``; converted in best_splits after the all-reduce). Both paths quantise each row's
+        w, w·y, w·y² the same way (f64 product, exact power-of-two scale, round half to even), so the
+        integer histograms — and every node's statistics — are bit-identical between the GPU kernel
+        (K18), the CPU form and any world size."""
         T, S, d, nb = self.p.num_trees, self.S, self.d, self.nbins
         if self.gpu:
             out = torch.zeros((T, nodes, d, nb, S), dtype=torch.int64, device=self.dev)
@@ -283,10 +286,11 @@ class ForestEngine:
                                                  bins.element_size(), _native.stream_ptr())
             _native.check(st, "tree_hist")
             return out
-        out = torch.zeros((T, nodes, d, nb, S), dtype=torch.float64, device=self.dev)
+        out = torch.zeros((T, nodes, d, nb, S), dtype=torch.int64, device=self.dev)
         if self.n == 0 or nodes == 0:
             return out
         flat = out.view(-1)
+        sc = [float(v) for v in self.scales]
         for t in range(T):
             nd = node_of[t]
             active = nd >= 0
@@ -303,11 +307,14 @@ class ForestEngine:
             feat = torch.arange(d, device=self.dev)
             base = (((t * nodes + nsel)[:, None] * d + feat[None, :]) * nb + b) * S
             if self.kind == "variance":
-                for s, v in enumerate((w, w * yy, w * yy * yy)):
-                    flat.index_add_(0, (base + s).reshape(-1), v[:, None].expand(-1, d).reshape(-1))
+                wy = w * yy
+                for s, v in enumerate((w, wy, wy * yy)):
+                    q = torch.round(v * sc[s]).to(torch.int64)
+                    flat.index_add_(0, (base + s).reshape(-1), q[:, None].expand(-1, d).reshape(-1))
             else:
                 c = yy.long()
-                flat.index_add_(0, (base + c[:, None]).reshape(-1), w[:, None].expand(-1, d).reshape(-1))
+                q = torch.round(w * sc[0]).to(torch.int64)
+                flat.index_add_(0, (base + c[:, None]).reshape(-1), q[:, None].expand(-1, d).reshape(-1))
         return out
 
     def route(self, bins, node_of, split_feat, split_bin, left_id, right_id, nodes: int) -> None:
@@ -364,8 +371,8 @@ class ForestEngine:
         if wt is not None:
             wt = wt.to(self.dev).contiguous()
         node_of = torch.zeros((T, self.n), dtype=torch.int32, device=self.dev)
+        self.scales = self.fixed_point_scales(wt)
         if self.gpu:
-            self.scales = self.fixed_point_scales(wt)
             self._scales_host = torch.as_tensor(self.scales, dtype=torch.float64).contiguous()
         k_sub = subset_size(p.feature_subset, self.d, p.task, T)
         roots = [Node() for _ in range(T)]
@@ -450,10 +457,14 @@ class ForestEngine:
                                                         out.data_ptr(), _native.stream_ptr())
             _native.check(st, "tree_best_split")
             return out.cpu().numpy().reshape(T, nodes, 3 + 3 * S)
-        h = hist.cpu().numpy().astype(np.float64)                   # [T, nodes, d, nb, S]
-        tot = h[:, :, 0].sum(axis=2) if d else np.zeros((T, nodes, S))  # [T, nodes, S]
-        left = np.cumsum(h, axis=3)
-        right = tot[:, :, None, None, :] - left
+        hi = hist.cpu().numpy()                                   # [T, nodes, d, nb, S] int64
+        tot_i = hi[:, :, 0].sum(axis=2) if d else np.zeros((T, nodes, S), dtype=np.int64)  # [T, nodes, S]
+        left_i = np.cumsum(hi, axis=3)
+        # to f64 exactly as K19 does: (double)integer / 2^e
+        scv = np.asarray(self.scales[:S] if self.kind == "variance" else [self.scales[0]] * S, dtype=np.float64)
+        tot = tot_i.astype(np.float64) / scv
+        left = left_i.astype(np.float64) / scv
+        right = (tot_i[:, :, None, None, :] - left_i).astype(np.float64) / scv
         cnt = (lambda a: a[..., 0]) if self.kind == "variance" else (lambda a: a.sum(-1))
         wtot, wl, wr = cnt(tot), cnt(left), cnt(right)
         imp_t, imp_l, imp_r = _impurity_vec(tot, self.kind), _impurity_vec(left, self.kind), _impurity_vec(right,
@@ -635,7 +646,8 @@ def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: i
                 k = torch.where(inner, nxt, k)
             out += lv[k]
     if average and len(trees) > 1:
-        out /= len(trees)
+        # true division on every device (a python-scalar divisor becomes a reciprocal multiply on the GPU)
+        out /= torch.full((1,), float(len(trees)), dtype=torch.float64, device=dev)
     return out
 
 

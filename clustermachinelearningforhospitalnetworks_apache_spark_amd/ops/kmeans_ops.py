@@ -42,18 +42,18 @@ _native.register_kernel_sigs({
     "cml_kmeans_reduce": (c_int, [c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int, c_int, c_vp, c_vp]),
     "cml_kmeans_sort_accum": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_int,
                                       c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp,
-                                      c_vp]),
+                                      ctypes.c_double, c_vp]),
     "cml_kmeans_sort_accum_ub": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                                          c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
-                                         c_vp, c_vp, c_ll, c_vp, c_vp]),
+                                         c_vp, c_vp, c_ll, c_vp, ctypes.c_double, c_vp]),
     "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                                        c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                       c_int, c_vp, c_int, c_vp]),
+                                       c_int, c_vp, c_int, ctypes.c_double, c_vp]),
     "cml_kmeans_seg_slot_doubles": (c_ll, [c_int, c_int]),
     "cml_kmeans_seg_slot_ints": (c_ll, [c_int]),
     "cml_kmeans_update": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
-                                  c_vp]),
+                                  ctypes.c_double, c_vp]),
     "cml_kmeans_prune_lower": (c_int, [c_vp, c_int, c_vp, c_vp, ctypes.c_float, ctypes.c_float, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]),
@@ -425,11 +425,14 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
                     hist: torch.Tensor, aplan: AssignPlan, k: int, cost_part: torch.Tensor, off: torch.Tensor,
                     seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor,
                     slots: tuple, stream=None, gate: torch.Tensor | None = None,
-                    ub_centres: torch.Tensor | None = None, ub: torch.Tensor | None = None) -> None:
+                    ub_centres: torch.Tensor | None = None, ub: torch.Tensor | None = None,
+                    qscale: float = 0.0) -> None:
     """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic).
     With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full. With
     ``ub_centres`` (bf16 [kp, dp]) and ``ub`` (f32 [n]) the segmented pass also writes every row's upper
-    bound of |x - c_label| (the exact-pruning bound) as the rows stream through."""
+    bound of |x - c_label| (the exact-pruning bound) as the rows stream through. ``qscale`` (a power of
+    two, 0 = off) sums the rows on the grid 1/qscale: every value is scaled and rounded to an integer,
+    so the f64 sums are exact integers (LloydEngine._sum_grid) and K11 scales them back."""
     lib = _native.kernels()
     args = (x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(), hist.data_ptr(), aplan.grid,
             aplan.round_rows, k, aplan.kp, cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
@@ -439,9 +442,9 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
         if ub_centres is None or ub_centres.dtype != torch.bfloat16 or ub.dtype != torch.float32 or ub.numel() < n:
             raise ValueError("accumulate_sort: ub needs bf16 centres and an f32 [n] output")
         status = lib.cml_kmeans_sort_accum_ub(*args, ub_centres.data_ptr(), ub_centres.stride(0), ub.data_ptr(),
-                                              _native.stream_ptr(stream))
+                                              float(qscale), _native.stream_ptr(stream))
     else:
-        status = lib.cml_kmeans_sort_accum(*args, _native.stream_ptr(stream))
+        status = lib.cml_kmeans_sort_accum(*args, float(qscale), _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
 
 
@@ -489,14 +492,14 @@ class DeltaState:
             self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(), _native.stream_ptr(stream)), "kmeans_delta_gate")
 
     def accumulate(self, x: torch.Tensor, dp: int, labels: torch.Tensor, chunk: int, cost_part: torch.Tensor,
-                   ncost: int, msg: torch.Tensor, stream=None) -> None:
+                   ncost: int, msg: torch.Tensor, stream=None, qscale: float = 0.0) -> None:
         _native.check(_native.kernels().cml_kmeans_delta_accum(
             x.data_ptr(), x.stride(0), dp, self.d, labels.data_ptr(), self.rows.data_ptr(), self.old.data_ptr(),
             self.wg_count.data_ptr(), self.nblk, self.pcap, self.cap, self.mode[chunk].data_ptr(), self.k,
             self.dh.data_ptr(), self.dseg.data_ptr(),
             self.cursor.data_ptr(), self.dperm.data_ptr(), self.plan.cpl, self.plan.seg_grid, self.dsum.data_ptr(),
             self.slots[0].data_ptr(), self.slots[1].data_ptr(), self.acc[chunk].data_ptr(), cost_part.data_ptr(),
-            ncost, msg.data_ptr(), int(is_fp8(x)), _native.stream_ptr(stream)), "kmeans_delta_accum")
+            ncost, msg.data_ptr(), int(is_fp8(x)), float(qscale), _native.stream_ptr(stream)), "kmeans_delta_accum")
 
     def changed_rows(self, chunk: int = 0) -> int:
         """Label changes of the last step (0 on a full step). Synchronises."""
@@ -664,15 +667,16 @@ def seg_buffer_ints(k: int) -> int:
 
 
 def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int,
-                   kp: int, cnorm: torch.Tensor, shift2: torch.Tensor | None, stream=None) -> None:
-    """K11: cent <- Σx/count (empty clusters keep their centre), cb <- bf16(cent), cnorm <- ||cb||²."""
+                   kp: int, cnorm: torch.Tensor, shift2: torch.Tensor | None, stream=None, unit: float = 1.0) -> None:
+    """K11: cent <- Σx·unit/count (empty clusters keep their centre), cb <- bf16(cent), cnorm <- ||cb||²;
+    ``unit`` is the sum grid step (accumulate_sort ``qscale`` = 1/unit), 1 for plain sums."""
     lib = _native.kernels()
     if msgs is not None:
         nbuf, bstride, mp = msgs.shape[0], msgs.stride(0), msgs.data_ptr()
     else:
         nbuf, bstride, mp = 0, 0, 0
     status = lib.cml_kmeans_update(mp, nbuf, bstride, k, d, cent.data_ptr(), cb.data_ptr(), cb.stride(0), dp, kp,
-                                   cnorm.data_ptr(), shift2.data_ptr() if shift2 is not None else 0,
+                                   cnorm.data_ptr(), shift2.data_ptr() if shift2 is not None else 0, float(unit),
                                    _native.stream_ptr(stream))
     _native.check(status, "kmeans_update")
 

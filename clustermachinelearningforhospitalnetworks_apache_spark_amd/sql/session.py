@@ -202,10 +202,18 @@ class SparkSession:
         fields, cols = [], {}
         kinds = {torch.float64: T.DoubleType(), torch.float32: T.FloatType(), torch.int32: T.IntegerType(),
                  torch.int64: T.LongType(), torch.bool: T.BooleanType(), torch.int16: T.ShortType()}
+        from ..utils.hoststream import hbm_budget_bytes, pinned_rows
+        budget = hbm_budget_bytes(self._device, self.conf.get("cml.hbm.budgetBytes", None))
         for name, t in columns.items():
             if int(t.shape[0]) != n:
                 raise ValueError("all columns need the same number of rows")
-            t = t.to(self._device)
+            if (t.dim() == 2 and not t.is_cuda and self._device.type == "cuda"
+                    and t.numel() * t.element_size() > budget):
+                # out of core: a vector column larger than cml.hbm.budgetBytes stays in pinned
+                # host memory; KMeans streams it through the GPU chunk by chunk (utils/hoststream.py)
+                t = pinned_rows(t)
+            else:
+                t = t.to(self._device)
             if t.dim() == 2:
                 dt = T.VectorUDT()
             elif t.dtype in kinds:

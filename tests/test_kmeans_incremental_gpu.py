@@ -164,3 +164,37 @@ def test_spherical_gpu_matches_cpu_engine():
     assert (lab_g == cpu.labels.numpy()).mean() > 0.995
     assert abs(gpu.training_cost() - cpu.training_cost()) <= 2e-2 * cpu.training_cost()
     assert gpu.delta is not None and gpu.converged(1.0)
+
+
+@pytest.mark.parametrize("wide", [True, False])
+def test_sum_grid_keeps_incremental_equal_to_full(wide):
+    """Exactness guard of the incremental sums (models/kmeans.py _sum_grid): rows whose values span
+    2^-30 .. 2^20 break the f64 window (log2 n + span + 8 > 53), so the rows are summed on a grid and
+    the full, incremental and pruned fits stay equal bit for bit after 20 steps; a narrow span keeps
+    plain f64 sums (no grid). A periodic full re-accumulation (refresh_interval) gives the same bits."""
+    n, d, k = 200_000, 128, 16
+    g = torch.Generator(device="cuda").manual_seed(3)
+    if wide:
+        mag = torch.exp2(torch.rand(n, d, device="cuda", generator=g) * 50 - 30)
+        sgn = torch.where(torch.rand(n, d, device="cuda", generator=g) < 0.5, -1.0, 1.0)
+        cen = torch.randn(k, d, device="cuda", generator=g) * 2 ** 18
+        x = cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + sgn * mag
+    else:
+        cen = torch.randn(k, d, device="cuda", generator=g) * 4
+        x = cen[torch.randint(0, k, (n,), device="cuda", generator=g)] + torch.randint(
+            -8, 9, (n, d), device="cuda", generator=g).float() / 4
+    x = x.to(torch.bfloat16)
+    init = x[:k].double().cpu().numpy()
+    res = {}
+    for name, kw in (("incremental", dict(prune=False)), ("full", dict(prune=False, incremental=False)),
+                     ("pruned", dict(prune=True)), ("refresh", dict(prune=True, refresh_interval=3))):
+        eng = LloydEngine(x, d, k, precision="bf16", accum_mode="sort", **kw)
+        eng.set_centers(init)
+        for _ in range(20):
+            eng.step()
+        torch.cuda.synchronize()
+        res[name] = (eng.centers.cpu().numpy(), eng.sum_grid)
+    assert np.array_equal(res["incremental"][0], res["full"][0])
+    assert np.array_equal(res["pruned"][0], res["full"][0])
+    assert np.array_equal(res["refresh"][0], res["full"][0])  # periodic full re-accumulation changes nothing
+    assert (res["full"][1] is not None) == wide and (res["incremental"][1] is not None) == wide

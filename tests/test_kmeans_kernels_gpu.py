@@ -19,13 +19,34 @@ def _full_steps_only(monkeypatch):
 
 
 def _ref_assign(xb, cb):
-    x = xb.double().cpu()
-    c = cb.double().cpu()
+    """Exact (f64, on the rows' device) argmin over the bf16/fp8 operands: label, distance, top-2 gap."""
+    x = xb.double()
+    c = cb.double().to(x.device)
     sc = (c * c).sum(1)[None, :] - 2 * x @ c.T
-    srt, idx = torch.sort(sc, 1)
-    d = (x * x).sum(1) + srt[:, 0]
-    gap = srt[:, 1] - srt[:, 0] if c.shape[0] > 1 else torch.full_like(d, 1e9)
-    return idx[:, 0], d.clamp(min=0), gap
+    top = torch.topk(sc, min(2, c.shape[0]), dim=1, largest=False)
+    d = (x * x).sum(1) + top.values[:, 0]
+    gap = top.values[:, 1] - top.values[:, 0] if c.shape[0] > 1 else torch.full_like(d, 1e9)
+    return top.indices[:, 0].cpu(), d.clamp(min=0).cpu(), gap.cpu()
+
+
+def _band(xb, cb, dp):
+    """The assign's own error bound on a squared distance, tau·(|x|² + max|c|²) per row (tau =
+    LloydEngine.prune_tau: f32 accumulation of dp bf16 products plus the argmin key truncation). Two
+    labels may differ only where the exact top-2 gap is within 2·band."""
+    tau = LloydEngine.prune_tau(dp)
+    x = xb.double()
+    c = cb.double().to(x.device)
+    return (tau * ((x * x).sum(1) + float((c * c).sum(1).max()))).cpu()
+
+
+def _check_labels(lab, ref_lab, gap, band):
+    bad = (lab != ref_lab) & (gap > 2 * band)
+    assert not bool(bad.any()), f"{int(bad.sum())} label mismatches outside the 2·tau band"
+
+
+def _check_dist(best, ref_d, band):
+    err = (best.double().cpu() - ref_d).abs()
+    assert bool((err <= band).all()), f"max distance error {float((err / band).max()):.3g} x the tau band"
 
 
 @pytest.mark.parametrize("n,d,k", [(1000, 4, 5), (4097, 100, 70), (20000, 256, 256), (3000, 512, 200),
@@ -46,10 +67,9 @@ def test_assign_matches_reference(n, d, k, cached_norm):
     torch.cuda.synchronize()
     cb = c.to(torch.bfloat16)
     ref_lab, ref_d, gap = _ref_assign(x.to(torch.bfloat16), cb)
-    lab = lab.cpu().long()
-    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
-    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
-    np.testing.assert_allclose(best.cpu().double().numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
+    band = _band(x.to(torch.bfloat16), cb, xm.shape[1])
+    _check_labels(lab.cpu().long(), ref_lab, gap, band)
+    _check_dist(best, ref_d, band)
 
 
 @pytest.fixture
@@ -87,10 +107,10 @@ def test_lloyd_step_matches_reference(n, d, k, mode, assign_variant):
     np.testing.assert_allclose(eng.centers.cpu().numpy(), want.numpy(), rtol=1e-4, atol=1e-4)
     msg = eng.msgs[0].cpu()
     np.testing.assert_array_equal(msg[k * d:k * d + k].numpy(), counts.numpy())
-    # label agreement with the exact reference (allowing bf16 near-ties)
-    ref_lab, ref_d, gap = _ref_assign(x, torch.as_tensor(init).to(torch.bfloat16))
-    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
-    assert ok.all()
+    # label agreement with the exact argmin outside the kernels' own rounding band
+    cb0 = torch.as_tensor(init).to(torch.bfloat16)
+    ref_lab, ref_d, gap = _ref_assign(x, cb0)
+    _check_labels(lab, ref_lab, gap, _band(x, cb0, eng.dp))
     assert abs(eng.training_cost() - ref_d.sum().item()) <= 1e-3 * ref_d.sum().item() + 1e-3
 
 
@@ -144,8 +164,12 @@ def test_sort_regime_bitwise_deterministic(n, d, k):
         msgs.append(eng.msgs[0].clone())
     assert torch.equal(msgs[0], msgs[1])
     lab = eng.labels[:n].cpu().long()
-    sums, counts = K.sums_reference(x.double().cpu(), lab, k)
-    np.testing.assert_allclose(msgs[0][:k * d].cpu().numpy(), sums.reshape(-1).numpy(), rtol=1e-9, atol=1e-6)
+    # the sums are exact: plain f64 sums, or (wide exponent span: models/kmeans.py _sum_grid) integer
+    # sums of the rows rounded to the grid, scaled back by the grid step
+    unit = eng.sum_grid or 1.0
+    xq = x.double().cpu() if eng.sum_grid is None else torch.round(x.double().cpu() / unit) * unit
+    sums, counts = K.sums_reference(xq, lab, k)
+    assert torch.equal(msgs[0][:k * d].cpu() * unit, sums.reshape(-1))
 
 
 @pytest.mark.parametrize("n,d,k", [(30_000, 37, 5), (50_000, 256, 256), (20_000, 512, 64), (9_999, 200, 33)])
@@ -169,9 +193,9 @@ def test_fp8_features_lloyd_step(n, d, k, mode):
     msg = eng.msgs[0].cpu()
     np.testing.assert_array_equal(msg[k * d:k * d + k].numpy(), counts.numpy())
     np.testing.assert_allclose(msg[:k * d].numpy(), sums.reshape(-1).numpy(), rtol=1e-9, atol=1e-6)
-    ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), torch.as_tensor(init).to(torch.bfloat16))
-    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
-    assert ok.all()
+    cb0 = torch.as_tensor(init).to(torch.bfloat16)
+    ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), cb0)
+    _check_labels(lab, ref_lab, gap, _band(xd.to(torch.bfloat16), cb0, eng.dp))
 
 
 @pytest.mark.parametrize("n,d,k,mode", [(200_000, 64, 16, None), (100_000, 256, 256, "sort"), (50_000, 16, 5, None)])
@@ -198,8 +222,12 @@ def test_graph_replay_matches_eager(n, d, k, mode):
     assert out[False][2] == out[True][2]
 
 
+# partial last 64-row tiles and partial last workgroup rounds (round = grid x 64 rows): n = 1, 63, 65 mod
+# 64 and mod the round, k not a multiple of the 32-centre tile
 @pytest.mark.parametrize("n,d,k", [(20000, 256, 256), (50_001, 128, 64), (3001, 512, 40), (777, 200, 33),
-                                   (100_000, 256, 250), (65, 128, 64), (130_000, 100, 100)])
+                                   (100_000, 256, 250), (65, 128, 64), (130_000, 100, 100), (63, 256, 40),
+                                   (16_385, 256, 256), (16_447, 256, 129), (16_449, 128, 64), (32_831, 256, 200),
+                                   (49_153, 512, 97), (1_048_641, 256, 256)])
 def test_rr_assign_matches_k9(n, d, k):
     """K9r (register-resident centres, LDS-DMA X ring; variant 8) against K9 and the f64 reference:
     same labels up to near ties, same distances, cost and counting-sort histogram/ranks."""
@@ -235,10 +263,14 @@ def test_rr_assign_matches_k9(n, d, k):
             K.set_rr_default(True)
     lab, best, cost, hist, rank, plan = out[8]
     ref_lab, ref_d, gap = _ref_assign(x.to(torch.bfloat16), c.to(torch.bfloat16))
-    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
-    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
-    assert (lab == out[0][0]).float().mean() > 0.999
-    np.testing.assert_allclose(best.numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
+    band = _band(x.to(torch.bfloat16), c.to(torch.bfloat16), dp)
+    _check_labels(lab, ref_lab, gap, band)
+    _check_labels(out[0][0], ref_lab, gap, band)
+    clear = gap > 2 * band  # K9r == K9 on every row whose label the rounding cannot decide
+    assert torch.equal(lab[clear], out[0][0][clear])
+    assert lab.min() >= 0 and lab.max() < k  # every row (tail tile / last workgroup included) written
+    _check_dist(best, ref_d, band)
+    _check_dist(out[0][1], ref_d, band)
     assert abs(cost - best.sum().item()) <= 1e-6 * abs(cost) + 1e-6
     # counting-sort first pass: per-workgroup histograms sum to the label counts, ranks are a
     # permutation of 0..count-1 inside every (workgroup, label) run of the rows that workgroup owns
@@ -274,9 +306,13 @@ def test_rr_lloyd_fit_matches_k9(n, d, k):
             eng.set_centers(init)
             for _ in range(6):
                 prev = eng.centers.cpu().clone()
+                cb0 = eng.cb[:k, :d].clone()
                 eng.step()
                 torch.cuda.synchronize()
                 lab = eng.labels[:n].cpu().long()
+                # every step's labels: the exact argmin for the step's bf16 centres outside the band
+                ref_lab, _, gap = _ref_assign(x, cb0)
+                _check_labels(lab, ref_lab, gap, _band(x, cb0, eng.dp))
                 sums, counts = K.sums_reference(xs, lab, k)
                 want = torch.where(counts[:, None] > 0, sums / counts.clamp(min=1)[:, None], prev)
                 np.testing.assert_allclose(eng.centers.cpu().numpy(), want.numpy(), rtol=1e-9, atol=1e-9)
@@ -285,7 +321,7 @@ def test_rr_lloyd_fit_matches_k9(n, d, k):
             K.set_assign_variant(0)
             K.set_rr_default(True)
     agree = (res[0][2] == res[8][2]).float().mean().item()
-    assert agree > 0.99, agree
+    assert agree > 0.99, agree  # trajectories: a near-tie flip in one step moves later centres slightly
     assert abs(res[8][1] - res[0][1]) <= 1e-3 * abs(res[0][1])
 
 
@@ -322,8 +358,11 @@ def test_rr_fp8_assign_matches_k9(n, d, k):
             K.set_assign_variant(0)
             K.set_rr_default(True)
     ref_lab, ref_d, gap = _ref_assign(xd.to(torch.bfloat16), c.to(torch.bfloat16))
+    band = _band(xd.to(torch.bfloat16), c.to(torch.bfloat16), dp)
     lab, best = out[8]
-    ok = (lab == ref_lab) | (gap < 1e-2 * (1 + ref_d.abs()))
-    assert ok.all(), f"{(~ok).sum().item()} label mismatches beyond near-ties"
-    assert (lab == out[0][0]).float().mean() > 0.999
-    np.testing.assert_allclose(best.numpy(), ref_d.numpy(), rtol=2e-3, atol=2e-2 * d ** 0.5)
+    _check_labels(lab, ref_lab, gap, band)
+    _check_labels(out[0][0], ref_lab, gap, band)
+    clear = gap > 2 * band
+    assert torch.equal(lab[clear], out[0][0][clear])
+    _check_dist(best, ref_d, band)
+    _check_dist(out[0][1], ref_d, band)
