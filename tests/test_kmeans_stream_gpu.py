@@ -46,7 +46,9 @@ def test_streamed_fit_equals_resident(n, d, k, dtype, chunk):
         torch.cuda.synchronize()
         assert torch.equal(res.centers, st.centers), f"step {it}"
         assert torch.equal(res.labels[:n], st.labels[:n]), f"step {it}"
-    assert st.training_cost() == pytest.approx(res.training_cost(), rel=1e-12)
+    # same labels and centres; the resident fit's pruned steps evaluate the cost by the per-centre expansion
+    # (sum|x|^2 - 2 c.S + n|c|^2 from the exact sums), the streamed full steps sum per-row f32 distances
+    assert st.training_cost() == pytest.approx(res.training_cost(), rel=1e-6)
     lab_r, d_r = res.assign()
     lab_s, d_s = st.assign()
     assert torch.equal(lab_r[:n], lab_s[:n]) and torch.equal(d_r[:n], d_s[:n])
@@ -87,5 +89,5 @@ def test_budget_conf_streams_the_feature_column():
     spark.conf.unset("cml.hbm.budgetBytes")
     assert np.array_equal(out["resident"][0], out["streamed"][0])
     assert out["resident"][1] == out["streamed"][1]
-    assert out["streamed"][2] == pytest.approx(out["resident"][2], rel=1e-12)
+    assert out["streamed"][2] == pytest.approx(out["resident"][2], rel=1e-6)  # cost formulas differ (above)
     assert torch.equal(out["resident"][3], out["streamed"][3])
