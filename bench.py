@@ -96,7 +96,7 @@ def main():
     ap.add_argument("--breakdown", action="store_true",
                     help="also run one fit with a device sync after every iteration and report per-iteration "
                          "times (extra.breakdown); the headline fit is never synchronised inside")
-    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv"],
+    ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv", "kmeans_ooc"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
                          "LogisticRegression, 100M x 256), one step = one distributed gradient pass + L-BFGS update; "
                          "pipeline = BASELINE config 5 (VectorAssembler -> StandardScaler(fp8) -> KMeans -> "
@@ -104,6 +104,8 @@ def main():
                          "csv = BASELINE config 1 (1k x 16 synthetic CSV -> VectorAssembler -> KMeans k=5 on local[2] "
                          "CPU, plumbing), one step = read + assemble + fit")
     ap.add_argument("--rows-per-gpu", type=int, default=125_000_000, help="pipeline workload (weak scaling)")
+    ap.add_argument("--ooc-rows", type=int, default=250_000_000,
+                    help="kmeans_ooc workload: fp8 rows (x 512) kept in pinned host memory")
     ap.add_argument("--solver", default="lbfgs", choices=["lbfgs", "sgd"],
                     help="logreg workload: Spark's L-BFGS (full-batch passes) or data-parallel mini-batch SGD")
     ap.add_argument("--batch", type=int, default=1 << 20, help="logreg SGD rows per rank per step")
@@ -115,6 +117,8 @@ def main():
         return bench_pipeline(args)
     if args.workload == "csv":
         return bench_csv(args)
+    if args.workload == "kmeans_ooc":
+        return bench_kmeans_ooc(args)
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world != 1:
@@ -355,6 +359,69 @@ def bench_logreg(args):
             "extra": {"datagen_s": round(gen_s, 3), "scaler_s": round(scaler_s, 3), "final_loss": hist[-1] if hist
                       else None}}), flush=True)
     comm.shutdown()
+
+
+def bench_kmeans_ooc(args):
+    """Out-of-core KMeans (SURVEY §5.7, config 5's row scale on ONE GPU): 250M x 512 e4m3 rows = 128 GB
+    live in pinned host memory (more than the HBM budget the pipeline leaves) and every pass over X
+    streams them through two device buffers (utils/hoststream.py). Timed: one whole fit (k-means|| init,
+    ``--steps`` Lloyd iterations, k = 128, tol = 0). Reports rows·iterations/s like the headline, the
+    streamed bytes, and the copy engine's H2D rate of one pass with no kernels attached."""
+    gpu = torch.cuda.is_available()
+    n, d, k = args.ooc_rows, 512, 128
+    if not gpu:
+        n = min(n, 50_000)
+    dev = torch.device("cuda", 0) if gpu else torch.device("cpu")
+    t0 = time.perf_counter()
+    xh = torch.empty((n, d), dtype=torch.uint8, pin_memory=gpu)
+    g = torch.Generator(device=dev)
+    g.manual_seed(7)
+    cen = torch.randn((64, d), generator=g, device=dev) * 3
+    step = 1 << 22
+    for s0 in range(0, n, step):
+        m = min(step, n - s0)
+        z = cen[torch.randint(0, 64, (m,), generator=g, device=dev)] + torch.randn((m, d), generator=g, device=dev)
+        xh[s0:s0 + m].copy_(z.clamp_(-440.0, 440.0).to(torch.float8_e4m3fn).view(torch.uint8))
+        del z
+    x8 = xh.view(torch.float8_e4m3fn)
+    gen_s = time.perf_counter() - t0
+    if not gpu:
+        x8 = x8.to(torch.float32)
+    mk = (lambda rows: LloydEngine(rows, d, k, device=dev)) if gpu else (lambda rows: LloydEngine(rows, d, k))
+    # untimed warm-up on a slice (code objects, pinned staging buffers)
+    w = mk(x8[: min(n, 1 << 20)])
+    w.set_centers(w.init_kmeans_parallel(seed=3))
+    w.step()
+    del w
+    if gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    eng = mk(x8)
+    eng.set_centers(eng.init_kmeans_parallel(seed=42))
+    t_init = time.perf_counter()
+    for _ in range(args.steps):
+        eng.step()
+    if gpu:
+        torch.cuda.synchronize()
+    elapsed = time.perf_counter() - t0
+    extra = {"fit_s": round(elapsed, 3), "init_s": round(t_init - t0, 3), "datagen_s": round(gen_s, 2),
+             "training_cost": eng.training_cost(), "host_bytes": n * d}
+    if gpu and eng._hs is not None:
+        hs = eng._hs
+        extra["streamed_GB"] = round(hs.bytes / 1e9, 2)
+        extra["passes_over_x"] = hs.passes
+        extra["streamed_GB_per_s_in_fit"] = round(hs.bytes / 1e9 / elapsed, 2)
+        for _ in hs.chunks(eng.bounds, timed=True):
+            pass
+        extra["h2d_GB_per_s_copy_only"] = round(hs.last_h2d_gbps() or 0.0, 2)
+        extra["chunk_rows"] = hs.chunk_rows
+    print(json.dumps({
+        "metric": f"Out-of-core KMeans fit samples/sec, {n / 1e6:g}M x {d} fp8 in pinned host memory, k={k}",
+        "value": n * args.steps / elapsed, "unit": "samples/s", "n_gpus": 1 if gpu else 0, "steps": args.steps,
+        "warmup": 1, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "fp8 rows (e4m3fn), bf16 MFMA", "data": "synthetic Gaussian blobs",
+        "config": {"model": f"KMeans k={k}", "global_batch": n, "seq_len": None, "parallelism": "dp1 (streamed)",
+                   "rows": n, "dim": d}, "extra": extra}), flush=True)
 
 
 def bench_pipeline(args):

@@ -702,14 +702,31 @@ __device__ __forceinline__ void add_raw(double (&acc)[CPL], const typename RawCo
 
 // The same on the sum grid: every value scaled by qs = 2^S and rounded to an integer (exact in f64),
 // so the f64 sums are exact integers whatever the data's exponent span (models/kmeans.py _sum_grid).
+// qsf = qs as an f32 normal (0 when qs is outside f32's normal range): a bf16 value times a power of
+// two is then exact in f32 (|x·qs| <= 2^(53 - log2 n) by the grid's choice, far inside the range; a
+// result below the normal range rounds to 0 either way), and rintf rounds it half-to-even as rint
+// does, so the f32 form gives the same integers at full-rate f32 instead of f64 mul + round.
 template <int CPL>
-__device__ __forceinline__ void add_raw_q(double (&acc)[CPL], const typename RawCols<CPL>::T& w, double qs) {
+__device__ __forceinline__ void add_raw_q(double (&acc)[CPL], const typename RawCols<CPL>::T& w, double qs,
+                                          float qsf) {
   const unsigned* ws = reinterpret_cast<const unsigned*>(&w);
+  if (qsf != 0.f) {
 #pragma unroll
-  for (int q = 0; q < CPL / 2; ++q) {
-    acc[2 * q] += rint((double)bf16_to_f32((u16)(ws[q] & 0xffffu)) * qs);
-    acc[2 * q + 1] += rint((double)bf16_to_f32((u16)(ws[q] >> 16)) * qs);
+    for (int q = 0; q < CPL / 2; ++q) {
+      acc[2 * q] += (double)rintf(bf16_to_f32((u16)(ws[q] & 0xffffu)) * qsf);
+      acc[2 * q + 1] += (double)rintf(bf16_to_f32((u16)(ws[q] >> 16)) * qsf);
+    }
+  } else {
+#pragma unroll
+    for (int q = 0; q < CPL / 2; ++q) {
+      acc[2 * q] += rint((double)bf16_to_f32((u16)(ws[q] & 0xffffu)) * qs);
+      acc[2 * q + 1] += rint((double)bf16_to_f32((u16)(ws[q] >> 16)) * qs);
+    }
   }
+}
+
+__device__ __forceinline__ float grid_scale_f32(double qs) {
+  return (qs >= 0x1p-126 && qs <= 0x1p126) ? (float)qs : 0.f;
 }
 
 // OCP e4m3fn rows: CPL bytes per lane.
@@ -792,6 +809,27 @@ __device__ __forceinline__ float wave_total_dpp(float v) {
   return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
 }
 
+// Row totals of a batch of 16 rows by a transposing butterfly: s[u] is this lane's partial of row u.
+// Each xor level halves the values a lane carries (it keeps one half of the rows and adds its
+// partner's partials of them), so 8 + 4 + 2 + 1 shuffles and two quad DPP steps leave row
+// 8·b5 + 4·b4 + 2·b3 + b2 (bits of the lane id) summed over the wave, and lane u < 16 reads row u
+// from lane 4u: 18 cross-lane ops for 16 rows instead of 16 wave totals of 6 DPP steps each.
+__device__ __forceinline__ float batch16_totals(const float (&s)[16]) {
+  const int lane = threadIdx.x & 63;
+  const bool h5 = lane & 32, h4 = lane & 16, h3 = lane & 8, h2 = lane & 4;
+  float a[8], b[4], c[2];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) a[i] = (h5 ? s[8 + i] : s[i]) + __shfl_xor(h5 ? s[i] : s[8 + i], 32, 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i) b[i] = (h4 ? a[4 + i] : a[i]) + __shfl_xor(h4 ? a[i] : a[4 + i], 16, 64);
+#pragma unroll
+  for (int i = 0; i < 2; ++i) c[i] = (h3 ? b[2 + i] : b[i]) + __shfl_xor(h3 ? b[i] : b[2 + i], 8, 64);
+  float v = (h2 ? c[1] : c[0]) + __shfl_xor(h2 ? c[0] : c[1], 4, 64);
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0xB1, 0xf, 0xf, false));  // quad [1,0,3,2]
+  v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x4E, 0xf, 0xf, false));  // quad [2,3,0,1]
+  return __shfl(v, 4 * (lane & 15), 64);
+}
+
 // Optional side output of the segmented accumulate (UB): ub[row] = an upper bound of |x - c_label|
 // over the bf16 centres `cb` (row stride ldc) the labels were assigned against — the exact-pruning
 // upper bound of every row, formed while the rows stream through (models/kmeans.py _step_seeded).
@@ -820,7 +858,7 @@ __device__ __forceinline__ long long seg_chunk(long long filled, long long waves
 }
 
 template <int CPL, bool F8, bool UB = false, bool Q = false>
-__global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
+__global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc(const void* __restrict__ X, long long n, long long ldx,
                                                              int Dp, int D, const int* __restrict__ perm,
                                                              const int* __restrict__ seg, int k,
                                                              double* __restrict__ msg, double* __restrict__ slots,
@@ -868,11 +906,16 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
     for (int j = 0; j < CPL; ++j) cv[j] = active ? bf16_to_f32(sub.cb[(long long)cc * sub.ldc + col + j]) : 0.f;
   };
   if constexpr (UB) load_cv(c);
+  const float qsf = grid_scale_f32(sub.qs);
   // f32 sum of <= 512 rounded squares of exact differences: relative error < 2^-14; rounded up
   auto ub_of = [](float s) { return sqrtf(s * (1.0f + 1.0f / 8192.0f)) * (1.0f + 1e-6f); };
+  // the next batch's row ids are loaded one batch ahead: the row gathers then wait for one memory
+  // round trip per batch instead of two dependent ones (the pass was latency-bound at 3.7 TB/s)
+  int pr_next = (lane < U && p0 + lane < p1) ? perm[p0 + lane] : 0;
   for (long long p = p0; p < p1; p += U) {
     const int cnt = (int)(p1 - p < U ? p1 - p : U);
-    const int pr = lane < cnt ? perm[p + lane] : 0;
+    const int pr = pr_next;
+    pr_next = (lane < U && p + U + lane < p1) ? perm[p + U + lane] : 0;
     float mine = 0.f;  // UB: squared distance of the batch's row `lane`
     raw_t w[U];
 #pragma unroll
@@ -887,10 +930,18 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
     const long long pe = p + cnt;
     if (next >= pe) {
       if constexpr (UB) {
+        static_assert(U == 16, "batch16_totals");
+        if constexpr (CPL <= 8) {
+          float sq[U];
 #pragma unroll
-        for (int u = 0; u < U; ++u) {
-          const float t = wave_total_dpp(sqdist_raw<CPL, F8>(w[u], cv));
-          mine = lane == u ? t : mine;
+          for (int u = 0; u < U; ++u) sq[u] = sqdist_raw<CPL, F8>(w[u], cv);
+          mine = batch16_totals(sq);
+        } else {  // 16 B per lane per row: the 16 partials would not fit beside the batch
+#pragma unroll
+          for (int u = 0; u < U; ++u) {
+            const float t = wave_total_dpp(sqdist_raw<CPL, F8>(w[u], cv));
+            mine = lane == u ? t : mine;
+          }
         }
         if (lane < cnt) sub.ub[pr] = ub_of(mine);
       }
@@ -907,7 +958,7 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
       } else {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
-          if constexpr (Q) add_raw_q<CPL>(acc, w[u], sub.qs);
+          if constexpr (Q) add_raw_q<CPL>(acc, w[u], sub.qs, qsf);
           else add_raw<CPL>(acc, w[u]);
         }
       }
@@ -942,7 +993,7 @@ __global__ __launch_bounds__(kSegThreads) void kmeans_segacc(const void* __restr
           mine = lane == u ? t : mine;
         }
         if constexpr (F8) add_raw8<CPL>(acc, v);
-        else if constexpr (Q) add_raw_q<CPL>(acc, v, sub.qs);
+        else if constexpr (Q) add_raw_q<CPL>(acc, v, sub.qs, qsf);
         else add_raw<CPL>(acc, v);
       }
       if constexpr (UB) {
@@ -1042,8 +1093,12 @@ __global__ __launch_bounds__(256) void init_classify_kernel(const float* __restr
 }
 
 // List A: 16 lanes per row (NCOL = Dp/16 columns each, one 16-lane DPP row), 4 rows per wave step.
-// Each lane group looks up its own row (nearest candidate, reach), walks the sorted relevant new
-// candidates (at most LMAX; the wave stops at the longest list of its 4 rows) and keeps the nearest.
+// Each lane group looks up its own row (nearest candidate, reach) and keeps the nearest of its relevant
+// new candidates (a prefix of the sorted table row, at most LMAX). The table lookups are taken off the
+// candidate loop: lane sl of a group loads entry sl of its row's table (one load per lane, issued with
+// the X slice), a ballot gives every group's relevant count, and candidate l's index comes from lane
+// g*16 + l by ds_bpermute; the next candidate's Y slice is loaded while the current one is reduced, so
+// a candidate costs one global round trip instead of three dependent ones (the loop was latency-bound).
 // Strict improvement over the current cost moves the row; ties among the new candidates go to the
 // lowest index (K9r's argmin rule). A 16-lane sum is 4 DPP steps (no row broadcasts), and the f32
 // math is on packed pairs, so a (row, candidate) pair costs ~a dozen vector instructions.
@@ -1058,11 +1113,14 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
                                                              const int* __restrict__ list, const int* __restrict__ cnt) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int XB = F8 ? NCOL : 2 * NCOL;  // bytes of this lane's X slice
+  constexpr int YQ = (2 * NCOL) / 16;       // uint4s of this lane's Y slice
   static_assert(XB % 16 == 0 && (2 * NCOL) % 16 == 0, "16-B slices");
+  static_assert(LMAX <= 16, "one table entry per lane of a 16-lane group");
   const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
   const int lane = threadIdx.x & 63, g = lane >> 4, sl = lane & 15;
   const long long nwaves = (long long)gridDim.x * (blockDim.x / 64);
   const long long total = *cnt;
+  const int lm = LMAX < m ? LMAX : m;
   for (long long base = ((long long)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6)) * 4; base < total;
        base += nwaves * 4) {
     const long long idx = base + g;
@@ -1071,8 +1129,9 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
     const int p = near[row];
     const float cr = cost[row];
     const float t = init_reach(cr, xn[row], pn[p], tau);
-    const float* v = tab_v + (long long)p * m;
-    const int* tj = tab_j + (long long)p * m;
+    const bool own = sl < lm;
+    const float vv = own ? tab_v[(long long)p * m + sl] : __builtin_huge_valf();
+    const int jj = own ? tab_j[(long long)p * m + sl] : 0;
     f2 xf[NCOL / 2];  // this lane's columns as f32 pairs, in column order
     {
       const uint4* src =
@@ -1092,19 +1151,41 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
         }
       }
     }
+    // relevant candidates of each group: a prefix of its sorted row (v ascending), so a popcount
+    const unsigned long long relb = __ballot(act && vv < t);
+    const int L = __popcll((relb >> (16 * g)) & 0xffffull);
+    int lw = 0;  // the wave's longest list (uniform)
+#pragma unroll
+    for (int q = 0; q < 4; ++q) {
+      const int c = __popcll((relb >> (16 * q)) & 0xffffull);
+      lw = c > lw ? c : lw;
+    }
     float best = cr;
     int bj = -1;
-#pragma unroll 1
-    for (int l = 0; l < LMAX && l < m; ++l) {
-      const bool rel = act && v[l] < t;
-      if (__ballot(rel) == 0ull) break;  // sorted: no later candidate is relevant to any of the 4 rows
-      const int j = rel ? tj[l] : 0;
+    uint4 yq[YQ];
+    int j = 0;
+    if (lw > 0) {
+      j = __shfl(jj, 16 * g, 64);
       const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)j * Dp + (long long)sl * NCOL);
+#pragma unroll
+      for (int b = 0; b < YQ; ++b) yq[b] = ysrc[b];
+    }
+#pragma unroll 1
+    for (int l = 0; l < lw; ++l) {
+      uint4 yc[YQ];
+#pragma unroll
+      for (int b = 0; b < YQ; ++b) yc[b] = yq[b];
+      const int jc = j;
+      if (l + 1 < lw) {  // prefetch the next candidate's slice
+        j = __shfl(jj, 16 * g + l + 1, 64);
+        const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)j * Dp + (long long)sl * NCOL);
+#pragma unroll
+        for (int b = 0; b < YQ; ++b) yq[b] = ysrc[b];
+      }
       f2 acc2 = f2{0.f, 0.f};
 #pragma unroll
-      for (int b = 0; b < (2 * NCOL) / 16; ++b) {
-        const uint4 q4 = ysrc[b];
-        const unsigned ys[4] = {q4.x, q4.y, q4.z, q4.w};
+      for (int b = 0; b < YQ; ++b) {
+        const unsigned ys[4] = {yc[b].x, yc[b].y, yc[b].z, yc[b].w};
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
           const f2 dv = xf[4 * b + e] - f2{__uint_as_float(ys[e] << 16), __uint_as_float(ys[e] & 0xffff0000u)};
@@ -1116,9 +1197,9 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
       d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xf, 0xf, false));
       d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xf, 0xf, false));
       d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x140, 0xf, 0xf, false));
-      if (rel && (d < best || (d == best && bj >= 0 && j < bj))) {
+      if (l < L && (d < best || (d == best && bj >= 0 && jc < bj))) {
         best = d;
-        bj = j;
+        bj = jc;
       }
     }
     if (act && sl == 0 && bj >= 0) {

@@ -65,6 +65,13 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
   const bool dot = c0 != nullptr;
   unsigned umx = 0u, umn = 0xffffu;
   unsigned mxb = 0;
+  // this lane's columns of the first centre, in registers for the whole pass (re-reading them from
+  // the cache every row tripled the pass's load traffic)
+  float cr[CPL][VPC];
+#pragma unroll
+  for (int i = 0; i < CPL; ++i)
+#pragma unroll
+    for (int e = 0; e < VPC; ++e) cr[i][e] = dot ? c0[VPC * (c + LPR * i) + e] : 0.f;
   for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW * U) {
     uint4 v[U][CPL];
 #pragma unroll
@@ -106,9 +113,8 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
 #pragma unroll
         for (int e = 0; e < VPC; ++e) s = fmaf(xs[e], xs[e], s);
         if (dot) {
-          const float* cc = c0 + VPC * (c + LPR * i);
 #pragma unroll
-          for (int e = 0; e < VPC; ++e) dt = fmaf(xs[e], cc[e], dt);
+          for (int e = 0; e < VPC; ++e) dt = fmaf(xs[e], cr[i][e], dt);
         }
       }
 #pragma unroll

@@ -178,6 +178,7 @@ class LloydEngine:
         self.prune = bool(prune)
         self.track_prune = False  # record (full?, re-assigned rows) of every pruned step (host reads)
         self._pdev = False  # the device pruned step (_step_prune_dev) is in use, decided in _alloc_gpu
+        self._seed_ub = os.environ.get("CML_KMEANS_SEED_UB", "1") != "0"  # A/B knob: exact ubs from the seeded sums
         if self.prune:  # one row chunk; the device form keeps incremental sums, the torch form its own
             row_chunks = 1
         # spherical = Spark's distanceMeasure="cosine": rows are scaled to unit length once, centres
@@ -215,6 +216,7 @@ class LloydEngine:
             bounds = HostRowStream.chunk_bounds(self.n, stream_chunk_rows)
             row_chunks = len(bounds) - 1
             self._hs = HostRowStream(self.x, bounds[1] - bounds[0] if self.n else 1, self.device)
+            self._hs_bounds = bounds  # (re-deriving them from the first chunk's size splits a lone short chunk)
         elif self.gpu:
             self.x = to_device_matrix(x, d)
             self.dp = self.x.shape[1]
@@ -256,8 +258,7 @@ class LloydEngine:
         k, d, dp, n = self.k, self.d, self.dp, self.n
         self.kp = round_up(k, 32)
         if self._hs is not None:
-            from ..utils.hoststream import HostRowStream
-            bounds = HostRowStream.chunk_bounds(n, self._hs.chunk_rows)
+            bounds = self._hs_bounds
         else:
             bounds = [round(i * n / self.row_chunks) for i in range(self.row_chunks + 1)]
             # keep chunk boundaries on 32-row tiles
@@ -721,8 +722,9 @@ class LloydEngine:
         # the exact one, |x - c_label| rounded up, so the next step's bounds prove as many rows as after a
         # full pass (the seeded lower bounds stay: d2 - r is far below what they are compared with)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
-                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], ub_centres=self.cb,
-                          ub=st.ub, qscale=self._qscale)
+                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0],
+                          ub_centres=self.cb if self._seed_ub else None, ub=st.ub if self._seed_ub else None,
+                          qscale=self._qscale)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
         self.comm.allreduce_async(msg).wait()
         st.cb_old.copy_(self.cb)
@@ -1189,8 +1191,11 @@ class LloydEngine:
                 w = K.sums_reference(self.w[:, None], inverse.reshape(-1)[nearest[: self.n].long()],
                                      uniq.shape[0])[0][:, 0].contiguous()
             elif self.n:
-                w = torch.bincount(inverse.reshape(-1)[nearest[: self.n].long()], minlength=uniq.shape[0])
-                w = w.to(torch.float64)
+                # rows per candidate (a histogram of the int32 nearest ids), folded onto the distinct
+                # candidates: integer counts, so the f64 sums are exact in any order
+                per = torch.bincount(nearest[: self.n], minlength=cand.shape[0]).to(torch.float64)
+                w = torch.zeros(uniq.shape[0], dtype=torch.float64, device=self.device)
+                w.index_add_(0, inverse.reshape(-1), per)
             else:
                 w = torch.zeros(uniq.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)
