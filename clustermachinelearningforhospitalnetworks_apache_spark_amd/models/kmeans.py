@@ -190,14 +190,15 @@ class LloydEngine:
             x = unit_rows(x, d, exact=(precision == "exact"))
         self._accum_mode = accum_mode
         self._incremental = True if incremental is None else bool(incremental)
-        # One Lloyd step = ~8 kernel launches per row chunk; replaying it as a captured HIP graph
-        # removes the per-launch host cost that dominates small shards. Default: single rank (a
-        # multi-rank step contains RCCL collectives, which stay eagerly launched).
-        # Multi-rank: the device pruned step is captured as two graphs around its all-reduce (the RCCL
-        # call stays eager between the replays); the chunked full-step path stays eager there.
+        # One Lloyd step = ~8-15 kernel launches; with use_graph it is replayed as a captured HIP graph
+        # (single rank: one graph; multi-rank: the device pruned step as two graphs around its
+        # all-reduce, the RCCL call eager between the replays; the chunked full step stays eager).
+        # Measured on MI355X (profiles/r3/graph_ab/): the pruned step has no host synchronisation, so eager
+        # launches run ahead of the GPU and a 20-step fit is as fast eagerly (100.9 vs 102.6 ms at 100M
+        # rows, 19.6 vs 20.9 ms at the 8-GPU shard of 12.5M) — the capture costs more than the replays
+        # save. Default eager; CML_KMEANS_GRAPH=1 (or use_graph=True) captures.
         if use_graph is None:
-            env = os.environ.get("CML_KMEANS_GRAPH")  # "0": eager steps
-            use_graph = True if env is None else env == "1"
+            use_graph = os.environ.get("CML_KMEANS_GRAPH") == "1"
         self.use_graph = bool(use_graph)
         self._graph = None
         self.k = int(k)

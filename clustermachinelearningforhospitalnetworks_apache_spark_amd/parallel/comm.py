@@ -68,7 +68,11 @@ class Communicator:
             device = torch.device("cuda", dev_index)
         else:
             device = torch.device("cpu")
-        if world == 1:
+        # CML_COMM_SELF=1: a one-rank RCCL (or gloo) process group whose collectives really run, so the
+        # multi-rank code paths (split step graphs around the all-reduce, chunk-overlapped all-reduces,
+        # object broadcasts) execute — and show up in a rocprofv3 trace — on a single GPU
+        self_group = world == 1 and os.environ.get("CML_COMM_SELF") == "1"
+        if world == 1 and not self_group:
             return cls(0, 1, device, None)
         # CML_COMM_BACKEND=gloo keeps GPU-resident shards but runs the collectives over gloo: several
         # ranks can then share one device (tests on a 1-GPU box; RCCL needs a device per rank)
@@ -76,17 +80,22 @@ class Communicator:
         owns = False
         if not dist.is_initialized():
             os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+            os.environ.setdefault("MASTER_PORT", "29517")
             kwargs = dict(backend=backend, rank=rank, world_size=world,
                           timeout=datetime.timedelta(seconds=timeout_s))
             if use_gpu and backend == "nccl":
                 kwargs["device_id"] = device
             dist.init_process_group(**kwargs)
             owns = True
-        return cls(rank, world, device, dist.get_backend(), dist.group.WORLD, owns)
+        c = cls(rank, world, device, dist.get_backend(), dist.group.WORLD, owns)
+        c._self_group = self_group
+        return c
+
+    _self_group = False
 
     @property
     def is_distributed(self) -> bool:
-        return self.world_size > 1
+        return self.world_size > 1 or self._self_group
 
     @property
     def is_root(self) -> bool:

@@ -101,7 +101,7 @@ def _fit2(x_local, comm):
     import torch
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
     eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D2, K2, comm, prune=True,
-                      precision="bf16")
+                      precision="bf16", use_graph=True)
     eng.track_prune = True
     init = eng.init_kmeans_parallel(seed=5)
     eng.set_centers(init)
