@@ -666,20 +666,28 @@ __global__ __launch_bounds__(kScatterThreads) void kmeans_scatter(const int* __r
   __syncthreads();
   const long long grp = (long long)nwaves * tile_rows;  // rows b owns per round
   const long long stride = grp * nblk;                  // rows between two of b's rounds
-  for (long long r0 = (long long)b * grp; r0 < n; r0 += stride * kScatterU) {
-    for (long long o = threadIdx.x; o < grp; o += blockDim.x) {
+  // every thread of the block works: `per` of b's rounds side by side (K9r's rounds are one 64-row
+  // tile, so a one-round-at-a-time walk left 448 of the 512 threads idle and the pass latency-bound)
+  const int per = (long long)blockDim.x >= grp ? (int)(blockDim.x / grp) : 1;
+  const int ro = per > 1 ? (int)(threadIdx.x / grp) : 0;
+  if (ro >= per) return;
+  const long long o0 = per > 1 ? (long long)threadIdx.x - ro * grp : (long long)threadIdx.x;
+  const long long ostep = per > 1 ? grp : (long long)blockDim.x;
+  for (long long q0 = ro; (long long)b * grp + q0 * stride < n; q0 += (long long)per * kScatterU) {
+    for (long long o = o0; o < grp; o += ostep) {
       int lab[kScatterU], rk[kScatterU];
+      long long rows[kScatterU];
 #pragma unroll
       for (int u = 0; u < kScatterU; ++u) {
-        const long long row = r0 + u * stride + o;
-        lab[u] = row < n ? labels[row] : -1;
-        rk[u] = row < n ? rank[row] : 0;
+        rows[u] = (long long)b * grp + (q0 + (long long)u * per) * stride + o;
+        lab[u] = rows[u] < n ? labels[rows[u]] : -1;
+        rk[u] = rows[u] < n ? rank[rows[u]] : 0;
       }
 #pragma unroll
       for (int u = 0; u < kScatterU; ++u)
         if (lab[u] >= 0) {
           const long long pos = (long long)soff[lab[u]] + rk[u];
-          if (pos < n) perm[pos] = (int)(r0 + u * stride + o);  // ranks from this step's assign: always
+          if (pos < n) perm[pos] = (int)rows[u];  // ranks from this step's assign: always
         }
     }
   }
@@ -1083,7 +1091,12 @@ __global__ __launch_bounds__(256) void init_classify_kernel(const float* __restr
       const unsigned c = (cls >> (2 * q)) & 3u;
       const unsigned long long ba = __ballot(c == 1), bb = __ballot(c == 2);
       const long long i = c0 + (long long)q * 256 + threadIdx.x;
-      if (c == 1) list_a[pa + (int)__popcll(ba & below)] = (int)i;
+      if (c == 1) {  // list A entry: the row with its nearest candidate, reach and cost (int4; re-read: cache hits)
+        const int p = near[i];
+        const float cst = cost[i];
+        reinterpret_cast<int4*>(list_a)[pa + (int)__popcll(ba & below)] =
+            make_int4((int)i, p, __float_as_int(init_reach(cst, xn[i], pn[p], tau)), __float_as_int(cst));
+      }
       if (c == 2) list_b[pb + (int)__popcll(bb & below)] = (int)i;
       pa += (int)__popcll(ba);
       pb += (int)__popcll(bb);
@@ -1093,29 +1106,29 @@ __global__ __launch_bounds__(256) void init_classify_kernel(const float* __restr
 }
 
 // List A: 16 lanes per row (NCOL = Dp/16 columns each, one 16-lane DPP row), 4 rows per wave step.
-// Each lane group looks up its own row (nearest candidate, reach) and keeps the nearest of its relevant
-// new candidates (a prefix of the sorted table row, at most LMAX). The table lookups are taken off the
-// candidate loop: lane sl of a group loads entry sl of its row's table (one load per lane, issued with
-// the X slice), a ballot gives every group's relevant count, and candidate l's index comes from lane
-// g*16 + l by ds_bpermute; the next candidate's Y slice is loaded while the current one is reduced, so
-// a candidate costs one global round trip instead of three dependent ones (the loop was latency-bound).
+// Each lane group takes one list entry (row, nearest candidate p, reach t, cost: written by the
+// classify kernel, so no per-row lookups) and keeps the nearest of its relevant new candidates (a
+// prefix of p's sorted table row, at most LMAX). Lane sl of a group loads entry sl of the table row
+// with the X slice; a ballot gives every group's relevant count; candidate l's index comes from lane
+// g*16 + l by ds_bpermute, and the Y slices of 4 candidates are loaded together — the pass was
+// latency-bound on dependent loads (list -> row state -> table -> each candidate), now a row costs
+// three memory round trips for up to 4 relevant candidates.
 // Strict improvement over the current cost moves the row; ties among the new candidates go to the
 // lowest index (K9r's argmin rule). A 16-lane sum is 4 DPP steps (no row broadcasts), and the f32
 // math is on packed pairs, so a (row, candidate) pair costs ~a dozen vector instructions.
 template <int NCOL, bool F8, int LMAX>
 __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restrict__ X, long long ldx, int Dp,
                                                              float* __restrict__ cost, int* __restrict__ near,
-                                                             const float* __restrict__ xn,
-                                                             const float* __restrict__ pn,
                                                              const float* __restrict__ tab_v,
                                                              const int* __restrict__ tab_j, int m,
-                                                             const u16* __restrict__ Y, int off, float tau,
-                                                             const int* __restrict__ list, const int* __restrict__ cnt) {
+                                                             const u16* __restrict__ Y, int off,
+                                                             const int4* __restrict__ list, const int* __restrict__ cnt) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int XB = F8 ? NCOL : 2 * NCOL;  // bytes of this lane's X slice
   constexpr int YQ = (2 * NCOL) / 16;       // uint4s of this lane's Y slice
+  constexpr int CB = 4;                     // candidates loaded together
   static_assert(XB % 16 == 0 && (2 * NCOL) % 16 == 0, "16-B slices");
-  static_assert(LMAX <= 16, "one table entry per lane of a 16-lane group");
+  static_assert(LMAX <= 16 && LMAX % CB == 0, "one table entry per lane of a 16-lane group");
   const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
   const int lane = threadIdx.x & 63, g = lane >> 4, sl = lane & 15;
   const long long nwaves = (long long)gridDim.x * (blockDim.x / 64);
@@ -1125,10 +1138,9 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
        base += nwaves * 4) {
     const long long idx = base + g;
     const bool act = idx < total;
-    const int row = act ? list[idx] : list[base];
-    const int p = near[row];
-    const float cr = cost[row];
-    const float t = init_reach(cr, xn[row], pn[p], tau);
+    const int4 e = list[act ? idx : base];
+    const int row = e.x, p = e.y;
+    const float t = __int_as_float(e.z), cr = __int_as_float(e.w);
     const bool own = sl < lm;
     const float vv = own ? tab_v[(long long)p * m + sl] : __builtin_huge_valf();
     const int jj = own ? tab_j[(long long)p * m + sl] : 0;
@@ -1141,12 +1153,12 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
         const uint4 q4 = src[b];
         const unsigned ws[4] = {q4.x, q4.y, q4.z, q4.w};
 #pragma unroll
-        for (int e = 0; e < 4; ++e) {
+        for (int e4 = 0; e4 < 4; ++e4) {
           if constexpr (F8) {
-            xf[8 * b + 2 * e] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e], false);
-            xf[8 * b + 2 * e + 1] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e], true);
+            xf[8 * b + 2 * e4] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e4], false);
+            xf[8 * b + 2 * e4 + 1] = __builtin_amdgcn_cvt_pk_f32_fp8((int)ws[e4], true);
           } else {
-            xf[4 * b + e] = f2{__uint_as_float(ws[e] << 16), __uint_as_float(ws[e] & 0xffff0000u)};
+            xf[4 * b + e4] = f2{__uint_as_float(ws[e4] << 16), __uint_as_float(ws[e4] & 0xffff0000u)};
           }
         }
       }
@@ -1162,44 +1174,42 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
     }
     float best = cr;
     int bj = -1;
-    uint4 yq[YQ];
-    int j = 0;
-    if (lw > 0) {
-      j = __shfl(jj, 16 * g, 64);
-      const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)j * Dp + (long long)sl * NCOL);
-#pragma unroll
-      for (int b = 0; b < YQ; ++b) yq[b] = ysrc[b];
-    }
 #pragma unroll 1
-    for (int l = 0; l < lw; ++l) {
-      uint4 yc[YQ];
+    for (int l0 = 0; l0 < lw; l0 += CB) {
+      uint4 yq[CB][YQ];
+      int jc[CB];
 #pragma unroll
-      for (int b = 0; b < YQ; ++b) yc[b] = yq[b];
-      const int jc = j;
-      if (l + 1 < lw) {  // prefetch the next candidate's slice
-        j = __shfl(jj, 16 * g + l + 1, 64);
-        const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)j * Dp + (long long)sl * NCOL);
+      for (int q = 0; q < CB; ++q) {
+        jc[q] = __shfl(jj, 16 * g + l0 + q, 64);
+        if (l0 + q < lw) {
+          const uint4* ysrc = reinterpret_cast<const uint4*>(Y + (long long)jc[q] * Dp + (long long)sl * NCOL);
 #pragma unroll
-        for (int b = 0; b < YQ; ++b) yq[b] = ysrc[b];
-      }
-      f2 acc2 = f2{0.f, 0.f};
-#pragma unroll
-      for (int b = 0; b < YQ; ++b) {
-        const unsigned ys[4] = {yc[b].x, yc[b].y, yc[b].z, yc[b].w};
-#pragma unroll
-        for (int e = 0; e < 4; ++e) {
-          const f2 dv = xf[4 * b + e] - f2{__uint_as_float(ys[e] << 16), __uint_as_float(ys[e] & 0xffff0000u)};
-          acc2 = dv * dv + acc2;
+          for (int b = 0; b < YQ; ++b) yq[q][b] = ysrc[b];
         }
       }
-      float d = acc2.x + acc2.y;  // 16-lane sum: quad swaps, half-row mirror, row mirror
-      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0xB1, 0xf, 0xf, false));
-      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xf, 0xf, false));
-      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xf, 0xf, false));
-      d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x140, 0xf, 0xf, false));
-      if (l < L && (d < best || (d == best && bj >= 0 && jc < bj))) {
-        best = d;
-        bj = jc;
+#pragma unroll
+      for (int q = 0; q < CB; ++q) {
+        if (l0 + q < lw) {
+          f2 acc2 = f2{0.f, 0.f};
+#pragma unroll
+          for (int b = 0; b < YQ; ++b) {
+            const unsigned ys[4] = {yq[q][b].x, yq[q][b].y, yq[q][b].z, yq[q][b].w};
+#pragma unroll
+            for (int e4 = 0; e4 < 4; ++e4) {
+              const f2 dv = xf[4 * b + e4] - f2{__uint_as_float(ys[e4] << 16), __uint_as_float(ys[e4] & 0xffff0000u)};
+              acc2 = dv * dv + acc2;
+            }
+          }
+          float d = acc2.x + acc2.y;  // 16-lane sum: quad swaps, half-row mirror, row mirror
+          d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0xB1, 0xf, 0xf, false));
+          d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x4E, 0xf, 0xf, false));
+          d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x141, 0xf, 0xf, false));
+          d += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(d), 0x140, 0xf, 0xf, false));
+          if (l0 + q < L && (d < best || (d == best && bj >= 0 && jc[q] < bj))) {
+            best = d;
+            bj = jc[q];
+          }
+        }
       }
     }
     if (act && sl == 0 && bj >= 0) {
@@ -1911,7 +1921,8 @@ CML_API int cml_kmeans_init_classify(const float* cost, const int* near, const f
 }
 
 // List A distances. X: bf16 rows (ldx elements) or e4m3 bytes (ldx bytes); Y: bf16 [m, Dp] new
-// candidates; n_cap: an upper bound of *cnt (sizes the grid).
+// candidates; list: the classify kernel's int4 entries (xn, pn and tau are folded into them and are
+// not read); n_cap: an upper bound of *cnt (sizes the grid).
 constexpr int kInitLmax = 8;  // models/kmeans.py _INIT_LMAX
 CML_API int cml_kmeans_init_lmax() { return kInitLmax; }
 CML_API int cml_kmeans_init_near_list(const void* X, long long ldx, int Dp, int xfp8, float* cost, int* near,
@@ -1924,7 +1935,7 @@ CML_API int cml_kmeans_init_near_list(const void* X, long long ldx, int Dp, int 
   hipStream_t st = (hipStream_t)stream;
 #define CML_NL(C, F)                                                                                                \
   hipLaunchKernelGGL((init_near_list_kernel<C, F, kInitLmax>), dim3((unsigned)blocks), dim3(256), 0, st, X, ldx, Dp, \
-                     cost, near, xn, pn, tab_v, tab_j, m, (const u16*)Y, off, tau, list, cnt)
+                     cost, near, tab_v, tab_j, m, (const u16*)Y, off, reinterpret_cast<const int4*>(list), cnt)
   if (xfp8) {
     if (ncol == 16) CML_NL(16, true);
     else if (ncol == 32) CML_NL(32, true);

@@ -1307,7 +1307,7 @@ class LloydEngine:
         pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
         tau = 2.0 * self._tau
         tr = self.aplan.round_rows
-        list_a = torch.empty(n, dtype=torch.int32, device=dev)
+        list_a = torch.empty((n, 4), dtype=torch.int32, device=dev)  # (row, nearest, reach, cost) entries
         list_b = torch.zeros(n + tr, dtype=torch.int32, device=dev)  # padded: whole tiles of valid rows
         cnt = torch.zeros(2, dtype=torch.int32, device=dev)
         K.init_classify(costs, nearest, self.xnorm, pn32, tab_v, tau, n, self._INIT_LMAX, list_a, cnt[0:1], list_b,

@@ -624,8 +624,11 @@ def init_classify(cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor, pn: 
                   tau: float, n: int, lmax: int, list_a: torch.Tensor, cnt_a: torch.Tensor, list_b: torch.Tensor,
                   cnt_b: torch.Tensor, stream=None) -> None:
     """Pruned k-means|| pass, step 1 (kmeans.hip init_classify_kernel): rows with no relevant new
-    candidate are dropped, rows with at most ``lmax`` go to ``list_a``, the others to ``list_b``
-    (counters zeroed by the caller, lists of capacity n)."""
+    candidate are dropped, rows with at most ``lmax`` go to ``list_a`` as int32 [n, 4] entries (row,
+    nearest candidate, reach and cost as f32 bits), the others to ``list_b`` (row ids; counters zeroed
+    by the caller, lists of capacity n)."""
+    if list_a.dtype != torch.int32 or list_a.numel() < 4 * n:
+        raise ValueError("list_a: int32 [n, 4] entries")
     m = int(tab_v.shape[1])
     _native.check(_native.kernels().cml_kmeans_init_classify(
         cost.data_ptr(), near.data_ptr(), xn.data_ptr(), pn.data_ptr(), tab_v.data_ptr(), m, float(tau), int(n),
