@@ -1167,7 +1167,7 @@ class LloydEngine:
                 # once most rows sit near a candidate, only the new candidates close to a row's nearest one
                 # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
                 # round (only the first centre so far) everything after the first K9r chunk
-                first = new.shape[0] if step > 0 else self._candidate_chunks(new.shape[0])[0]
+                first = new.shape[0] if step > 0 else self._first_chunk(new.shape[0])
                 if step == 0:
                     self._init_candidate_pass(new[:first], costs, nearest, ncand)
                 rest = new[first:] if step == 0 else new
@@ -1347,6 +1347,16 @@ class LloydEngine:
     # ms, measured on MI355X (profiles/r3/mb_rr_modes.log): CT <= 2 is HBM-bound, then the MFMA work
     # grows with CT (under the power-limited clock, not linearly).
     _CT_COST = {1: 1.72, 2: 1.78, 3: 2.06, 4: 2.45, 5: 2.78}
+
+    def _first_chunk(self, m: int) -> int:
+        """Candidates of the first k-means|| round that take a full K9r pass before the rest are pruned
+        against them (CML_KMEANS_INIT_FIRST caps it, a multiple of 64; default: the first chunk of
+        _candidate_chunks)."""
+        first = self._candidate_chunks(m)[0]
+        cap = os.environ.get("CML_KMEANS_INIT_FIRST")
+        if cap:
+            first = min(first, max(64, int(cap) // 64 * 64), m)
+        return first
 
     def _candidate_chunks(self, m: int) -> list:
         """Split m candidate centres into K9r launches (multiples of 64, at most 256 — 320 where CT = 5
