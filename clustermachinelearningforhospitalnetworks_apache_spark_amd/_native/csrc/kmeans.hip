@@ -845,7 +845,8 @@ struct SegUB {
   const u16* cb;
   long long ldc;
   float* ub;
-  double qs;  // sum grid scale (0: plain f64 sums of the raw values)
+  double qs;             // sum grid scale (0: plain f64 sums of the raw values)
+  const float* cu = nullptr;  // offset-form bounds: ub - cu[label] is stored (kmeans_prune.hip)
 };
 
 // Sort regime, pass 4: segmented sum over the label-sorted order. Wave w streams sorted
@@ -917,6 +918,12 @@ __global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc
   const float qsf = grid_scale_f32(sub.qs);
   // f32 sum of <= 512 rounded squares of exact differences: relative error < 2^-14; rounded up
   auto ub_of = [](float s) { return sqrtf(s * (1.0f + 1.0f / 8192.0f)) * (1.0f + 1e-6f); };
+  // offset form: ub - cu[label], rounded up
+  auto ub_store = [&](float u, int cc) {
+    if (sub.cu == nullptr) return u;
+    const float cu = sub.cu[cc];
+    return (u - cu) + 1e-6f * (u + cu);
+  };
   // the next batch's row ids are loaded one batch ahead: the row gathers then wait for one memory
   // round trip per batch instead of two dependent ones (the pass was latency-bound at 3.7 TB/s)
   int pr_next = (lane < U && p0 + lane < p1) ? perm[p0 + lane] : 0;
@@ -951,7 +958,7 @@ __global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc
             mine = lane == u ? t : mine;
           }
         }
-        if (lane < cnt) sub.ub[pr] = ub_of(mine);
+        if (lane < cnt) sub.ub[pr] = ub_store(ub_of(mine), c);
       }
       if constexpr (F8) {
         // e4m3 values are multiples of 2^-9 below 2^9: 16 of them sum EXACTLY in f32, so the rows
@@ -974,6 +981,7 @@ __global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc
       // a cluster boundary inside this batch (~k + #waves batches per pass): walk its rows one at a
       // time, re-reading each (cache hits) instead of keeping the batch's registers live — the
       // unrolled predicated form doubled the kernel's VGPRs and halved its occupancy
+      int rc = c;  // UB: the cluster of the batch's row `lane`
 #pragma unroll 1
       for (int u = 0; u < cnt; ++u) {
         const long long pos = p + u;
@@ -999,13 +1007,14 @@ __global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc
         if constexpr (UB) {
           const float t = wave_total_dpp(sqdist_raw<CPL, F8>(v, cv));
           mine = lane == u ? t : mine;
+          rc = lane == u ? c : rc;
         }
         if constexpr (F8) add_raw8<CPL>(acc, v);
         else if constexpr (Q) add_raw_q<CPL>(acc, v, sub.qs, qsf);
         else add_raw<CPL>(acc, v);
       }
       if constexpr (UB) {
-        if (lane < cnt) sub.ub[pr] = ub_of(mine);
+        if (lane < cnt) sub.ub[pr] = ub_store(ub_of(mine), rc);
       }
     }
   }
@@ -1745,7 +1754,7 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
                                      int* chg_rows, int* chg_old, int* chg_wg_count, int* chg_overflow, int chg_pcap,
                                      int rr_ct, const int* idx, const int* n_dev, const int* lab_in, float* ub,
                                      float* lb, const float* mc, float tau, const int* gate, int want, float* best,
-                                     void* stream) {
+                                     const float* cum, int k_cum, void* stream) {
   if (mode < 1 || mode > 2 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if (rr_ct <= 0 || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
@@ -1758,7 +1767,7 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
   const long long lds = rr::lds_for(Dp, kp, xfp8 != 0, mode);
   if (lds <= 0 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
   const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
-  const rr::Ext ext{idx, n_dev, lab_in, ub, lb, mc, tau, gate, want};
+  const rr::Ext ext{idx, n_dev, lab_in, ub, lb, mc, tau, gate, want, cum, cum != nullptr ? cum + k_cum : nullptr};
   return rr::dispatch(mode, Dp, rr_ct, xfp8 != 0, X, n, ldx, (const u16*)C, ldc, kc, kp, cnorm, xnorm, labels,
                       best, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }
@@ -1824,10 +1833,11 @@ CML_API int cml_kmeans_sort_accum_ub(const void* X, long long n, long long ldx, 
                                      const int* rank, const int* hist, int nblk, int round_rows, int k, int kp,
                                      const double* cost_part, int ncost, int* off, int* seg, int* perm, int cpl,
                                      int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate,
-                                     const void* cb, long long ldc, float* ub, double qscale, void* stream) {
+                                     const void* cb, long long ldc, float* ub, double qscale, const float* cu,
+                                     void* stream) {
   if (cb == nullptr || ub == nullptr || ldc < Dp) return (int)hipErrorInvalidValue;
   return sort_accum(X, n, ldx, Dp, D, labels, rank, hist, nblk, round_rows, k, kp, cost_part, ncost, off, seg, perm,
-                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{(const u16*)cb, ldc, ub, qscale});
+                    cpl, seg_grid, msg, slots, slot_c, xfp8, gate, stream, SegUB{(const u16*)cb, ldc, ub, qscale, cu});
 }
 static int sort_accum(const void* X, long long n, long long ldx, int Dp, int D, const int* labels, const int* rank,
                       const int* hist, int nblk, int round_rows, int k, int kp, const double* cost_part, int ncost,

@@ -27,6 +27,21 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block
 
+// Offset form (cum != null): the stored values are us = ub - cu[a] and ls = lb + cl[a] against the
+// per-centre cumulative drifts cu[j] = Σ drift_j and cl[j] = Σ (largest drift of a centre other than
+// j), both rounded up as they accumulate (kmeans_centre_stats2_kernel). The effective bounds are
+// us + cu[a] (rounded up) and ls - cl[a] (rounded down), so a row whose label holds is only READ — the
+// pass drops its 8 B/row of bound writes — and the writers (K9r epilogue, the seeded accumulate) store
+// the offsets of the bounds they compute.
+__device__ __forceinline__ bool bound_lazy(int a, float us, float ls, const float* cu, const float* cl,
+                                           const float* st, float c2) {
+  const float ca = cu[a], la = cl[a];
+  const float u = (us + ca) + 1e-6f * (fabsf(us) + ca);                     // rounded up (inf stays inf)
+  const float w = fmaxf((ls - la) - 1e-6f * (fabsf(ls) + la), 0.f);        // rounded down
+  const float lt = w > 0.f ? (w - c2 / w) * (1.0f - 1e-6f) : -1.f;
+  return u <= st[a] || u <= lt;
+}
+
 // Moves one row's bounds to the new centres; true when they still prove its label.
 __device__ __forceinline__ bool bound_step(int a, float& u, float& w, const float* sd, const float* st, float dm1,
                                            float dm2, int jm, float c2) {
@@ -49,17 +64,24 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
                                                                        int* __restrict__ cand_lab,
                                                                        float* __restrict__ cand_xn,
                                                                        const int* __restrict__ skip,
-                                                                       long long cap) {
+                                                                       long long cap, const float* __restrict__ cum) {
   if (skip != nullptr && *skip != 0) return;  // bounds invalid this step (full pass instead)
   extern __shared__ __align__(16) unsigned char smem[];
   const float c2 = *c2p;
   float* sd = reinterpret_cast<float*>(smem);  // [k] drift
   float* st = sd + k;                          // [k] threshold
+  float* scu = st + k;                         // [k] cumulative drifts (offset form)
+  float* scl = scu + k;                        // [k]
   __shared__ int wsum[kThreads / 64];
   __shared__ int base;
+  const bool lazy = cum != nullptr;
   for (int i = threadIdx.x; i < k; i += kThreads) {
     sd[i] = drift[i];
     st[i] = thr[i];
+    if (lazy) {
+      scu[i] = cum[i];
+      scl[i] = cum[k + i];
+    }
   }
   __syncthreads();
   // largest drift, second largest, index of the largest: the lower bound moves by the largest drift
@@ -72,6 +94,23 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   for (int it = 0; it < kIters; ++it) {
     const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
     if (r0 >= n) break;
+    if (lazy) {  // read-only: rows whose label holds keep their stored offsets
+      if (r0 + 3 < n) {
+        const int4 l = *reinterpret_cast<const int4*>(lab + r0);
+        const float4 u = *reinterpret_cast<const float4*>(ub + r0);
+        const float4 w = *reinterpret_cast<const float4*>(lb + r0);
+        const int ls[4] = {l.x, l.y, l.z, l.w};
+        const float us[4] = {u.x, u.y, u.z, u.w};
+        const float ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (!bound_lazy(ls[j], us[j], ws[j], scu, scl, st, c2)) mask |= 1u << (it * 4 + j);
+      } else {
+        for (int j = 0; j < 4 && r0 + j < n; ++j)
+          if (!bound_lazy(lab[r0 + j], ub[r0 + j], lb[r0 + j], scu, scl, st, c2)) mask |= 1u << (it * 4 + j);
+      }
+      continue;
+    }
     if (r0 + 3 < n) {
       const int4 l = *reinterpret_cast<const int4*>(lab + r0);
       const float4 u = *reinterpret_cast<const float4*>(ub + r0);
@@ -203,8 +242,9 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
                                                                    int have_drift, float* __restrict__ thr,
                                                                    float* __restrict__ dmax, float* __restrict__ mc,
                                                                    float* __restrict__ c2, int* __restrict__ count,
-                                                                   int* __restrict__ force) {
+                                                                   int* __restrict__ force, float* __restrict__ cum) {
   __shared__ double smax[256];
+  __shared__ float sdm[3];
   __shared__ float d1[256], d2[256];
   __shared__ int i1[256];
   const int tid = threadIdx.x;
@@ -243,6 +283,9 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
       dmax[1] = tb < 0.f ? 0.f : tb;
       dmax[2] = (float)ti;
     }
+    sdm[0] = ta < 0.f ? 0.f : ta;
+    sdm[1] = tb < 0.f ? 0.f : tb;
+    sdm[2] = (float)ti;
     *count = 0;
     *force = 0;
   }
@@ -254,6 +297,10 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
     else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
     else t = -__builtin_huge_valf();
     thr[j] = t;
+    if (have_drift && cum != nullptr) {  // cumulative drifts of the offset-form bounds, rounded up
+      cum[j] = (cum[j] + drift[j]) * (1.0f + 2.4e-7f);
+      cum[k + j] = (cum[k + j] + (j == (int)sdm[2] ? sdm[1] : sdm[0])) * (1.0f + 2.4e-7f);
+    }
   }
 }
 
@@ -347,18 +394,19 @@ CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, con
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
                                     const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                     const float* xn, int* cand_lab, float* cand_xn, const int* skip,
-                                    long long cap, void* stream) {
+                                    long long cap, const float* cum, void* stream) {
   if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
     return (int)hipErrorInvalidValue;
+  if (cum != nullptr && k > 4096) return (int)hipErrorInvalidValue;  // 4k floats of LDS
   if (k <= 0 || k > 8192 || n < 0 || n >= (1LL << 31) || ((uintptr_t)lab & 15) || ((uintptr_t)ub & 15) ||
       ((uintptr_t)lb & 15))
     return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
-  hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads), (size_t)2 * k * sizeof(float),
-                     (hipStream_t)stream, lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab,
-                     cand_xn, skip, cap);
+  hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
+                     (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
+                     dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum);
   return cml_status();
 }
 
@@ -372,13 +420,13 @@ CML_API int cml_kmeans_prune_gate(const int* count, long long cap, const int* fo
 // (f32 [k]), dmax (f32 [3]), mc / c2 (f32 scalars); count and force are reset to 0.
 CML_API int cml_kmeans_centre_stats(const void* cb, const void* cb_old, long long ldc, int k, int d, const float* mx,
                                     float tau, double* cn, double* half, float* drift, float* thr, float* dmax,
-                                    float* mc, float* c2, int* count, int* force, void* stream) {
+                                    float* mc, float* c2, int* count, int* force, float* cum, void* stream) {
   if (k <= 0 || d <= 0 || d > 8192) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(kmeans_centre_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(double), st,
                      (const u16*)cb, (const u16*)cb_old, ldc, k, d, cn, drift, half);
   hipLaunchKernelGGL(kmeans_centre_stats2_kernel, dim3(1), dim3(256), 0, st, cn, half, drift, k, mx, tau,
-                     cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force);
+                     cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force, cum);
   return cml_status();
 }
 

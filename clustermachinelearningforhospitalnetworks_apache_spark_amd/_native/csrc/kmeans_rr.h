@@ -69,6 +69,10 @@ struct Ext {
   float tau;          // MODE >= 1: error allowance relative to ||x||² + max||c||²
   const int* gate;    // launch runs only when gate == nullptr || *gate == want
   int want;
+  // offset-form bounds (kmeans_prune.hip): stored ub - cu[label] (rounded up) and lb + cl[label]
+  // (rounded down) against the per-centre cumulative drifts; null: absolute bounds
+  const float* cu = nullptr;
+  const float* cl = nullptr;
 };
 
 __host__ __device__ constexpr int cn_slots(int kp) { return ((kp + 3) & ~3) > 256 ? ((kp + 3) & ~3) : 256; }
@@ -698,8 +702,15 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
           const float xn = reinterpret_cast<const float*>(te)[R];
           const float slack = ext.tau * (xn + mcv);
           const float sd = __int_as_float((int)(sec ^ 0x80000000u));
-          ext.ub[row] = sqrtf(dist + slack) * (1.0f + 1e-6f);
-          ext.lb[row] = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
+          float u = sqrtf(dist + slack) * (1.0f + 1e-6f);
+          float w = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
+          if (ext.cu != nullptr) {
+            const float cu = ext.cu[bi], cl = ext.cl[bi];
+            u = (u - cu) + 1e-6f * (u + cu);
+            w = (w + cl) - 1e-6f * (w + cl);
+          }
+          ext.ub[row] = u;
+          ext.lb[row] = w;
         }
       }
     };

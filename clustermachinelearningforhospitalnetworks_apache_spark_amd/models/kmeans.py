@@ -619,6 +619,11 @@ class LloydEngine:
         st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
         st.mx = torch.zeros(1, dtype=torch.float32, device=dev)  # max ||x||² over all ranks (_ensure_norms)
         st.cb_old = torch.zeros_like(self.cb)
+        # offset-form bounds (kmeans_prune.hip bound_lazy): ub/lb hold ub - cu[label] / lb + cl[label]
+        # against these cumulative drifts [cu | cl], so the bounds pass only reads the rows whose label
+        # holds; CML_KMEANS_LAZY_BOUNDS=0 keeps the absolute bounds rewritten every step
+        st.cum = (torch.zeros(2 * k, dtype=torch.float32, device=dev)
+                  if os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096 else None)
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
@@ -644,14 +649,14 @@ class LloydEngine:
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
         K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
-                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.force, zero_count=False) \
-            if n else None
+                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.force, zero_count=False,
+                       cum=st.cum) if n else None
         K.prune_gate(st.count, st.cap_m, st.force, st.pmode)
         K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
-                        st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1)
+                        st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
-                        gate=st.pmode, want=0)
+                        gate=st.pmode, want=0, cum=st.cum)
         dl.gate(0)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
@@ -663,7 +668,7 @@ class LloydEngine:
         st.cb_old.copy_(self.cb)
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
-                       st.c2, st.count, st.force)
+                       st.c2, st.count, st.force, cum=st.cum)
         self._cost_fn = self._pdev_cost
 
     def _seed_from_init(self, sd) -> None:
@@ -690,6 +695,8 @@ class LloydEngine:
             d2 = torch.full_like(d1, math.inf)
         pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
         qmap = sd.inverse.reshape(-1).to(torch.int32).contiguous()
+        if st.cum is not None:
+            st.cum.zero_()  # every row's bounds are written here: offsets against zero drift
         K.seed_bounds(sd.nearest[:n], sd.costs[:n], self.xnorm[:n], qmap, a, d1, d2, pn32, 2.0 * self._tau, n,
                       self.labels[:n], st.ub[:n], st.lb[:n])
 
@@ -705,7 +712,7 @@ class LloydEngine:
         m = 0
         if n:
             K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
-                           xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, zero_count=True)
+                           xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, zero_count=True, cum=st.cum)
             m = int(st.count.item())
         if m > st.cap_m:
             st.force.fill_(1)
@@ -714,7 +721,7 @@ class LloydEngine:
         st.pmode.copy_(torch.tensor([0, m], dtype=torch.int32))
         if n:
             K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, None, st.ub, st.lb,
-                            st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab)
+                            st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab, cum=st.cum)
             K.label_hist(lab, n, ap, self.hist, self.rank)
         self.cost_part.zero_()
         dl.invalidate()
@@ -725,13 +732,13 @@ class LloydEngine:
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0],
                           ub_centres=self.cb if self._seed_ub else None, ub=st.ub if self._seed_ub else None,
-                          qscale=self._qscale)
+                          qscale=self._qscale, cum=st.cum)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
         self.comm.allreduce_async(msg).wait()
         st.cb_old.copy_(self.cb)
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
-                       st.c2, st.count, st.force)
+                       st.c2, st.count, st.force, cum=st.cum)
         self._cost_fn = self._pdev_cost
 
     def _pdev_cost(self) -> torch.Tensor:

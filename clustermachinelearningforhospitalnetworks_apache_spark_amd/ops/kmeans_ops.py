@@ -45,7 +45,7 @@ _native.register_kernel_sigs({
                                       ctypes.c_double, c_vp]),
     "cml_kmeans_sort_accum_ub": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_int,
                                          c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int,
-                                         c_vp, c_vp, c_ll, c_vp, ctypes.c_double, c_vp]),
+                                         c_vp, c_vp, c_ll, c_vp, ctypes.c_double, c_vp, c_vp]),
     "cml_kmeans_delta_gate": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
     "cml_kmeans_delta_accum": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_int, c_vp,
                                        c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -56,17 +56,17 @@ _native.register_kernel_sigs({
                                   ctypes.c_double, c_vp]),
     "cml_kmeans_prune_lower": (c_int, [c_vp, c_int, c_vp, c_vp, ctypes.c_float, ctypes.c_float, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
-                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp]),
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
                                        c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
     "cml_kmeans_centre_stats": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
-                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
-                                         c_vp, c_vp]),
+                                         c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_init_classify": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, ctypes.c_float, c_ll, c_int, c_vp,
                                          c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_near_list": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
@@ -426,13 +426,14 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
                     seg: torch.Tensor, perm: torch.Tensor, plan: AccumPlan, msg: torch.Tensor,
                     slots: tuple, stream=None, gate: torch.Tensor | None = None,
                     ub_centres: torch.Tensor | None = None, ub: torch.Tensor | None = None,
-                    qscale: float = 0.0) -> None:
+                    qscale: float = 0.0, cum: torch.Tensor | None = None) -> None:
     """K10 regime B: counting sort by label, then segmented f64 sums -> msg (deterministic).
     With ``gate`` (DeltaState.mode) the launches only run on steps the gate marks as full. With
     ``ub_centres`` (bf16 [kp, dp]) and ``ub`` (f32 [n]) the segmented pass also writes every row's upper
     bound of |x - c_label| (the exact-pruning bound) as the rows stream through. ``qscale`` (a power of
     two, 0 = off) sums the rows on the grid 1/qscale: every value is scaled and rounded to an integer,
-    so the f64 sums are exact integers (LloydEngine._sum_grid) and K11 scales them back."""
+    so the f64 sums are exact integers (LloydEngine._sum_grid) and K11 scales them back. ``cum``
+    (f32 [2k], the offset-form bounds' cumulative drifts) stores ub - cum[label] instead of ub."""
     lib = _native.kernels()
     args = (x.data_ptr(), n, x.stride(0), dp, d, labels.data_ptr(), rank.data_ptr(), hist.data_ptr(), aplan.grid,
             aplan.round_rows, k, aplan.kp, cost_part.data_ptr(), aplan.grid, off.data_ptr(), seg.data_ptr(),
@@ -442,7 +443,7 @@ def accumulate_sort(x: torch.Tensor, n: int, dp: int, d: int, labels: torch.Tens
         if ub_centres is None or ub_centres.dtype != torch.bfloat16 or ub.dtype != torch.float32 or ub.numel() < n:
             raise ValueError("accumulate_sort: ub needs bf16 centres and an f32 [n] output")
         status = lib.cml_kmeans_sort_accum_ub(*args, ub_centres.data_ptr(), ub_centres.stride(0), ub.data_ptr(),
-                                              float(qscale), _native.stream_ptr(stream))
+                                              float(qscale), _ptr(cum), _native.stream_ptr(stream))
     else:
         status = lib.cml_kmeans_sort_accum(*args, float(qscale), _native.stream_ptr(stream))
     _native.check(status, "kmeans_sort_accum")
@@ -513,14 +514,16 @@ def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift
                  dmax: torch.Tensor, thr: torch.Tensor, c2, k: int, cand: torch.Tensor,
                  count: torch.Tensor, stream=None, xn: torch.Tensor | None = None,
                  cand_lab: torch.Tensor | None = None, cand_xn: torch.Tensor | None = None,
-                 skip: torch.Tensor | None = None, zero_count: bool = True) -> None:
+                 skip: torch.Tensor | None = None, zero_count: bool = True, cum: torch.Tensor | None = None) -> None:
     """K9p (``kmeans_prune.hip``): moves the per-row distance bounds by the centre drifts
     (ub += drift[label], lb -= largest drift of another centre) and appends to ``cand`` the rows whose
     bounds no longer prove the label (neither ub <= thr[label] nor ub <= lb - c2 / lb); ``count[0]`` =
     their number (on the GPU at most ``len(cand)`` of them are written). ``dmax`` = [largest drift, second largest, index of the largest]. GPU: ``c2`` is a
     device scalar; with ``cand_lab``/``cand_xn`` the candidates' labels and norms are written compacted
     beside ``cand`` (the K9r candidate pass reads them); ``skip`` (device flag) turns the launch into a
-    no-op; ``zero_count=False`` leaves the zeroing of ``count`` to the caller (the centre-stats pass).
+    no-op; ``zero_count=False`` leaves the zeroing of ``count`` to the caller (the centre-stats pass);
+    ``cum`` (f32 [2k] cumulative drifts) selects the offset-form bounds: ``ub``/``lb`` hold ub - cu[label]
+    and lb + cl[label], the drifts are already in ``cum``, and the pass only reads them (no bound writes).
     CPU tensors: the same pass in torch (f64 bounds), candidates in row order."""
     n = int(labels.shape[0])
     if labels.is_cuda:
@@ -531,7 +534,7 @@ def prune_bounds(labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor, drift
         _native.check(_native.kernels().cml_kmeans_prune_bounds(
             labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
             c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
-            _ptr(skip), int(cand.shape[0]), _native.stream_ptr(stream)), "kmeans_prune_bounds")
+            _ptr(skip), int(cand.shape[0]), _ptr(cum), _native.stream_ptr(stream)), "kmeans_prune_bounds")
         return
     c2 = float(c2)
     lab = labels[:n].long()
@@ -584,14 +587,15 @@ def prune_gate(count: torch.Tensor, cap: int, force: torch.Tensor, mode: torch.T
 
 def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, mx: torch.Tensor, tau: float,
                  cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor, thr: torch.Tensor, dmax: torch.Tensor,
-                 mc: torch.Tensor, c2: torch.Tensor, count: torch.Tensor, force: torch.Tensor, stream=None) -> None:
+                 mc: torch.Tensor, c2: torch.Tensor, count: torch.Tensor, force: torch.Tensor, stream=None,
+                 cum: torch.Tensor | None = None) -> None:
     """Centre statistics of the device pruned step (``kmeans_prune.hip``) over the bf16 centres: norms,
     drifts against ``cb_old`` (None: no drift), half nearest-centre distances -> thr, dmax, mc, c2;
     resets ``count`` and ``force``. No host synchronisation."""
     _native.check(_native.kernels().cml_kmeans_centre_stats(
         cb.data_ptr(), _ptr(cb_old), cb.stride(0), int(k), int(d), mx.data_ptr(), float(tau), cn.data_ptr(),
         half.data_ptr(), drift.data_ptr(), thr.data_ptr(), dmax.data_ptr(), mc.data_ptr(), c2.data_ptr(),
-        count.data_ptr(), force.data_ptr(), _native.stream_ptr(stream)), "kmeans_centre_stats")
+        count.data_ptr(), force.data_ptr(), _ptr(cum), _native.stream_ptr(stream)), "kmeans_centre_stats")
 
 
 def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor,
@@ -601,7 +605,7 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
                   delta: "DeltaState | None" = None, idx: torch.Tensor | None = None,
                   n_dev: torch.Tensor | None = None, lab_in: torch.Tensor | None = None,
                   gate: torch.Tensor | None = None, want: int = 0, stream=None,
-                  best: torch.Tensor | None = None) -> None:
+                  best: torch.Tensor | None = None, cum: torch.Tensor | None = None) -> None:
     """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
     the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
     ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
@@ -616,7 +620,8 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
         _ptr(delta.rows if delta is not None else None), _ptr(delta.old if delta is not None else None),
         _ptr(delta.wg_count if delta is not None else None), _ptr(delta.overflow if delta is not None else None),
         delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
-        lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _native.stream_ptr(stream)),
+        lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _ptr(cum),
+        int(cum.shape[0] // 2) if cum is not None else 0, _native.stream_ptr(stream)),
         f"kmeans_assign_rr_ext(mode={mode})")
 
 
