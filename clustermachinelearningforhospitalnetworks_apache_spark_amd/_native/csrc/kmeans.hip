@@ -1754,8 +1754,10 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
                                      int* chg_rows, int* chg_old, int* chg_wg_count, int* chg_overflow, int chg_pcap,
                                      int rr_ct, const int* idx, const int* n_dev, const int* lab_in, float* ub,
                                      float* lb, const float* mc, float tau, const int* gate, int want, float* best,
-                                     const float* cum, int k_cum, void* stream) {
+                                     const float* cum, int k_cum, float* mcost, int* mnear, int moff,
+                                     void* stream) {
   if (mode < 1 || mode > 2 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  if ((mcost == nullptr) != (mnear == nullptr) || (mcost != nullptr && mode != 2)) return (int)hipErrorInvalidValue;
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if (rr_ct <= 0 || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
   if (xnorm == nullptr || ub == nullptr || lb == nullptr || mc == nullptr) return (int)hipErrorInvalidValue;
@@ -1767,7 +1769,8 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
   const long long lds = rr::lds_for(Dp, kp, xfp8 != 0, mode);
   if (lds <= 0 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
   const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
-  const rr::Ext ext{idx, n_dev, lab_in, ub, lb, mc, tau, gate, want, cum, cum != nullptr ? cum + k_cum : nullptr};
+  const rr::Ext ext{idx,  n_dev, lab_in, ub,    lb,    mc,   tau, gate, want, cum, cum != nullptr ? cum + k_cum : nullptr,
+                    mcost, mnear, moff};
   return rr::dispatch(mode, Dp, rr_ct, xfp8 != 0, X, n, ldx, (const u16*)C, ldc, kc, kp, cnorm, xnorm, labels,
                       best, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }

@@ -90,18 +90,28 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   const int jm = (int)dmax[2];
   const long long blk0 = (long long)blockIdx.x * kThreads * kIters * 4;
   unsigned mask = 0;  // bit it*4+j: row blk0 + (it*kThreads + tid)*4 + j is a candidate
+  if (lazy) {
+    // read-only: rows whose label holds keep their stored offsets. All kIters groups' loads are issued
+    // before any test (48 B in flight per lane; one group at a time ran the pass at 3.3 TB/s)
+    int4 L[kIters];
+    float4 U[kIters], W[kIters];
 #pragma unroll
-  for (int it = 0; it < kIters; ++it) {
-    const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
-    if (r0 >= n) break;
-    if (lazy) {  // read-only: rows whose label holds keep their stored offsets
+    for (int it = 0; it < kIters; ++it) {
+      const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
       if (r0 + 3 < n) {
-        const int4 l = *reinterpret_cast<const int4*>(lab + r0);
-        const float4 u = *reinterpret_cast<const float4*>(ub + r0);
-        const float4 w = *reinterpret_cast<const float4*>(lb + r0);
-        const int ls[4] = {l.x, l.y, l.z, l.w};
-        const float us[4] = {u.x, u.y, u.z, u.w};
-        const float ws[4] = {w.x, w.y, w.z, w.w};
+        L[it] = *reinterpret_cast<const int4*>(lab + r0);
+        U[it] = *reinterpret_cast<const float4*>(ub + r0);
+        W[it] = *reinterpret_cast<const float4*>(lb + r0);
+      }
+    }
+#pragma unroll
+    for (int it = 0; it < kIters; ++it) {
+      const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+      if (r0 >= n) break;
+      if (r0 + 3 < n) {
+        const int ls[4] = {L[it].x, L[it].y, L[it].z, L[it].w};
+        const float us[4] = {U[it].x, U[it].y, U[it].z, U[it].w};
+        const float ws[4] = {W[it].x, W[it].y, W[it].z, W[it].w};
 #pragma unroll
         for (int j = 0; j < 4; ++j)
           if (!bound_lazy(ls[j], us[j], ws[j], scu, scl, st, c2)) mask |= 1u << (it * 4 + j);
@@ -109,8 +119,12 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
         for (int j = 0; j < 4 && r0 + j < n; ++j)
           if (!bound_lazy(lab[r0 + j], ub[r0 + j], lb[r0 + j], scu, scl, st, c2)) mask |= 1u << (it * 4 + j);
       }
-      continue;
     }
+  }
+#pragma unroll
+  for (int it = 0; it < kIters && !lazy; ++it) {
+    const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+    if (r0 >= n) break;
     if (r0 + 3 < n) {
       const int4 l = *reinterpret_cast<const int4*>(lab + r0);
       const float4 u = *reinterpret_cast<const float4*>(ub + r0);

@@ -73,6 +73,12 @@ struct Ext {
   // (rounded down) against the per-centre cumulative drifts; null: absolute bounds
   const float* cu = nullptr;
   const float* cl = nullptr;
+  // k-means|| candidate merge (MODE 2): a row whose distance to its nearest centre of this launch is
+  // strictly below mcost[row] takes it (mcost = dist, mnear = label + moff) — the init's merge kernel
+  // folded into the epilogue
+  float* mcost = nullptr;
+  int* mnear = nullptr;
+  int moff = 0;
 };
 
 __host__ __device__ constexpr int cn_slots(int kp) { return ((kp + 3) & ~3) > 256 ? ((kp + 3) & ~3) : 256; }
@@ -697,6 +703,12 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       if (mine) {
         cost += (double)dist;
         if (best_out != nullptr) best_out[row] = dist;
+        if constexpr (MODE == 2) {
+          if (ext.mcost != nullptr && dist < ext.mcost[row]) {
+            ext.mcost[row] = dist;
+            ext.mnear[row] = bi + ext.moff;
+          }
+        }
         if (ranking) rank_out[row] = atomicAdd(hist + bi, 1);
         if constexpr (TOP2) {
           const float xn = reinterpret_cast<const float*>(te)[R];

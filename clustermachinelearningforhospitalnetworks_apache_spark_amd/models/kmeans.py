@@ -1333,7 +1333,6 @@ class LloydEngine:
             cxn = torch.zeros(pad, dtype=torch.float32, device=dev)
             cxn[:cb] = self.xnorm[list_b[:cb].long()]
             lab_in = torch.full((pad,), -1, dtype=torch.int32, device=dev)
-            best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
             c0 = 0
             for size in self._candidate_chunks(m):
                 kp = round_up(size, 32)
@@ -1343,8 +1342,8 @@ class LloydEngine:
                 plan = K.plan_assign(cb, dp, size, dev.index or 0, fp8=K.is_fp8(self.x))
                 mc = cnk[:size].max().reshape(1)
                 K.assign_rr_ext(2, self.x, cb, dp, cbk, cnk, plan, cxn, self.labels, None, st.ub, st.lb, mc,
-                                self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, best=best)
-                K.init_merge_list(costs, nearest, best, self.labels, off + c0, list_b, cnt[1:2], cb)
+                                self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, merge_cost=costs,
+                                merge_near=nearest, merge_off=off + c0)
                 c0 += size
         if self.track_prune:
             self._init_prune_history = getattr(self, "_init_prune_history", []) + [(n, ca, cb)]

@@ -66,7 +66,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
-                                         c_vp, c_vp, c_int, c_vp]),
+                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_init_classify": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, ctypes.c_float, c_ll, c_int, c_vp,
                                          c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_near_list": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
@@ -605,12 +605,16 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
                   delta: "DeltaState | None" = None, idx: torch.Tensor | None = None,
                   n_dev: torch.Tensor | None = None, lab_in: torch.Tensor | None = None,
                   gate: torch.Tensor | None = None, want: int = 0, stream=None,
-                  best: torch.Tensor | None = None, cum: torch.Tensor | None = None) -> None:
+                  best: torch.Tensor | None = None, cum: torch.Tensor | None = None,
+                  merge_cost: torch.Tensor | None = None, merge_near: torch.Tensor | None = None,
+                  merge_off: int = 0) -> None:
     """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
     the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
     ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
     rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag;
-    ``best`` (f32, real rows) receives the squared distance to the new label."""
+    ``best`` (f32, real rows) receives the squared distance to the new label; ``merge_cost``/``merge_near``
+    (mode 2, f32/int32 per real row) take the k-means|| merge: strictly nearer rows get (distance, label +
+    ``merge_off``)."""
     if plan.rr_ct <= 0 or plan.kc != plan.kp:
         raise ValueError("the pruned-step assign needs the K9r plan (Dp in {128, 256, 512}, k <= 256)")
     _native.check(_native.kernels().cml_kmeans_assign_rr_ext(
@@ -621,7 +625,8 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
         _ptr(delta.wg_count if delta is not None else None), _ptr(delta.overflow if delta is not None else None),
         delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
         lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _ptr(cum),
-        int(cum.shape[0] // 2) if cum is not None else 0, _native.stream_ptr(stream)),
+        int(cum.shape[0] // 2) if cum is not None else 0, _ptr(merge_cost), _ptr(merge_near), int(merge_off),
+        _native.stream_ptr(stream)),
         f"kmeans_assign_rr_ext(mode={mode})")
 
 
