@@ -97,11 +97,11 @@ def _data2():
     return np.round(x * 8) / 8
 
 
-def _fit2(x_local, comm):
+def _fit2(x_local, comm, use_graph=True):
     import torch
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
     eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D2, K2, comm, prune=True,
-                      precision="bf16", use_graph=True)
+                      precision="bf16", use_graph=use_graph)
     eng.track_prune = True
     init = eng.init_kmeans_parallel(seed=5)
     eng.set_centers(init)
@@ -114,7 +114,7 @@ def _fit2(x_local, comm):
             "hist": eng.prune_history()}
 
 
-def _rank_main2(rank, world, port, out_path):
+def _rank_main2(rank, world, port, out_path, use_graph=True):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1"})
     import torch
@@ -125,7 +125,7 @@ def _rank_main2(rank, world, port, out_path):
     comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
     x = _data2()
     lo, hi = rank * N2 // world, (rank + 1) * N2 // world
-    res = _fit2(x[lo:hi], comm)
+    res = _fit2(x[lo:hi], comm, use_graph)
     if rank == 0:
         with open(out_path, "w") as fh:
             json.dump(res, fh)
@@ -133,23 +133,25 @@ def _rank_main2(rank, world, port, out_path):
     dist.destroy_process_group()
 
 
-def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch):
-    """Two ranks on the default GPU path (pruned init, seeded step, split graphs) give the single-rank
-    fit bit for bit: init centres, final centres and cost (1/8-grid data: every f64 sum is exact)."""
+@pytest.mark.parametrize("use_graph", [False, True])
+def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch, use_graph):
+    """Two ranks on the default GPU path (pruned init, seeded step, eager pruned steps around the
+    all-reduce — or split graphs) give the single-rank fit bit for bit: init centres, final centres and
+    cost (1/8-grid data: every f64 sum is exact)."""
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
     monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
     out = str(tmp_path / "w2d.json")
     ctx = mp.get_context("spawn")
     port = _free_port()
-    procs = [ctx.Process(target=_rank_main2, args=(r, 2, port, out)) for r in range(2)]
+    procs = [ctx.Process(target=_rank_main2, args=(r, 2, port, out, use_graph)) for r in range(2)]
     for p in procs:
         p.start()
     for p in procs:
         p.join(240)
     assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
     res = json.load(open(out))
-    ref = _fit2(_data2(), local_comm())
-    assert res["pdev"] and ref["pdev"] and res["seeded"] and res["graph"], res
+    ref = _fit2(_data2(), local_comm(), use_graph)
+    assert res["pdev"] and ref["pdev"] and res["seeded"] and res["graph"] == use_graph, res
     np.testing.assert_array_equal(np.asarray(res["init"]), np.asarray(ref["init"]))
     np.testing.assert_array_equal(np.asarray(res["centers"]), np.asarray(ref["centers"]))
     assert abs(res["cost"] - ref["cost"]) <= 1e-9 * abs(ref["cost"])
