@@ -173,6 +173,19 @@ def main():
         torch.cuda.synchronize()
         comm.barrier()
         acc["steady_state_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 5
+        if eng._pdev:
+            # a forced full step (bounds invalid): K9r over every row with top-2 bounds + the full
+            # counting-sort f64 accumulate (what a fit pays when most rows move)
+            comm.barrier()
+            torch.cuda.synchronize()
+            ts = time.perf_counter()
+            for _ in range(3):
+                eng._pst.force.fill_(1)
+                eng.delta.invalidate()
+                eng.step()
+            torch.cuda.synchronize()
+            comm.barrier()
+            acc["full_step_ms"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
         if eng.delta is not None and not eng.prune:
             acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
             comm.barrier()
