@@ -1298,7 +1298,7 @@ class LloydEngine:
         over their positions (mode 2). Same nearest candidates as the full pass up to the rounding of
         near-ties. Returns False (nothing changed) when too many rows need the K9r pass to gain."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
-        if not self._pdev or os.environ.get("CML_KMEANS_INIT_PRUNE", "1") == "0":
+        if not self._pdev or os.environ.get("CML_KMEANS_INIT_PRUNE", "1") == "0" or not self._rr_max_chunk():
             return False
         if n == 0:
             return True
@@ -1364,11 +1364,23 @@ class LloydEngine:
             first = min(first, max(64, int(cap) // 64 * 64), m)
         return first
 
+    def _rr_max_chunk(self) -> int:
+        """Most centres one K9r launch takes at this row width (320 at Dp = 256 bf16, 128 at Dp = 512:
+        (k/64)·(Dp/32) bounded by the compute waves' VGPRs); 0 when K9r does not apply."""
+        if getattr(self, "_rr_max", None) is None:
+            self._rr_max = 0
+            for c in (320, 256, 192, 128, 64):
+                p = K.plan_assign(1, self.dp, c, fp8=K.is_fp8(self.x))
+                if p.rr_ct > 0 and p.kc == p.kp:
+                    self._rr_max = c
+                    break
+        return self._rr_max
+
     def _candidate_chunks(self, m: int) -> list:
         """Split m candidate centres into K9r launches (multiples of 64, at most 256 — 320 where CT = 5
         exists) minimising the summed pass cost: 520 candidates run as 256 + 264 (two passes, ~27.5)
         rather than 256 + 256 + 8 (three, ~34)."""
-        big = 320 if (K.plan_assign(1, self.dp, 320, fp8=K.is_fp8(self.x)).rr_ct == 5) else 256
+        big = self._rr_max_chunk() or 256  # 256: K9 launches (no K9r plan at this width)
         units = -(-m // 64)
         best = [0.0] + [math.inf] * units  # best[u]: cheapest cover of u units of 64
         pick = [0] * (units + 1)
