@@ -1156,7 +1156,13 @@ class LloydEngine:
             nearest = torch.zeros(0, dtype=torch.int64, device=self.device)
         ncand = 1
         for step in range(steps):
-            sum_cost = self.comm.sum_scalar(float(costs[: self.n].sum(dtype=torch.float64).item()) if self.n else 0.0)
+            if not self.n:
+                local = 0.0
+            elif self.gpu and costs.dtype == torch.float32:
+                local = float(K.sum_f64(costs, self.n).item())  # no f64 copy of the costs
+            else:
+                local = float(costs[: self.n].sum(dtype=torch.float64).item())
+            sum_cost = self.comm.sum_scalar(local)
             if sum_cost <= 0:
                 break
             if self.gpu:

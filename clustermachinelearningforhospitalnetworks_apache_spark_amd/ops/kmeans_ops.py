@@ -79,6 +79,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
                                     c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
+    "cml_sum_f32_f64_parts": (c_int, []),
+    "cml_sum_f32_f64": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
                                        c_vp]),
     "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
@@ -118,6 +120,19 @@ def row_pass(x: torch.Tensor, n: int, dp: int, xn: torch.Tensor, c0: torch.Tenso
     _native.check(_native.kernels().cml_kmeans_row_pass(
         x.data_ptr(), int(n), x.stride(0), int(dp), int(is_fp8(x)), xn.data_ptr(), _ptr(c0), float(c0n), _ptr(cost),
         _ptr(near), _ptr(xn_max), _ptr(erange), _native.stream_ptr(stream)), "kmeans_row_pass")
+
+
+def sum_f64(x: torch.Tensor, n: int, stream=None) -> torch.Tensor:
+    """Σ x[:n] of a contiguous f32 device vector as an f64 device scalar (kmeans_init.hip: fixed-order
+    block partials, no f64 copy of the input)."""
+    if x.dtype != torch.float32 or not x.is_cuda or not x.is_contiguous() or x.data_ptr() % 16:
+        raise ValueError("sum_f64: a 16-byte aligned contiguous f32 device vector")
+    lib = _native.kernels()
+    part = torch.empty(int(lib.cml_sum_f32_f64_parts()), dtype=torch.float64, device=x.device)
+    out = torch.empty(1, dtype=torch.float64, device=x.device)
+    _native.check(lib.cml_sum_f32_f64(x.data_ptr(), int(n), part.data_ptr(), out.data_ptr(),
+                                      _native.stream_ptr(stream)), "sum_f32_f64")
+    return out[0]
 
 
 def init_merge(cost: torch.Tensor, near: torch.Tensor, best: torch.Tensor, lab: torch.Tensor, off: int,

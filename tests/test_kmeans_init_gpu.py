@@ -195,3 +195,14 @@ def test_pruned_candidate_pass_equals_full_on_exact_data(monkeypatch, n, d, k):
     assert res[1][1] == [] and len(res[0][1]) >= 1
     rows, ca, cb = res[0][1][-1]
     assert rows == n and ca + cb < n
+
+
+@pytest.mark.parametrize("n", [1, 5, 4096, 1_000_003])
+def test_sum_f64_matches_torch(n):
+    """Σ of f32 values in f64 (the k-means|| cost total) against torch's f64 sum of the same values."""
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = torch.rand(n + 3, device="cuda", generator=g) * 1000
+    got = float(K.sum_f64(x, n))
+    want = float(x[:n].double().sum())
+    assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
+    assert float(K.sum_f64(x, n)) == got  # deterministic
