@@ -3,7 +3,7 @@
 set -o pipefail
 cd "$GRAFT_REPO_ROOT"
 export PYTHONPATH="$GRAFT_REPO_ROOT${PYTHONPATH:+:$PYTHONPATH}"
-out=gpurun_out/r3/check4
+out=gpurun_out/r3/check5
 mkdir -p $out
 timeout -k 10 900 python -u -m pytest tests -x -m gpu -q --timeout 300 --timeout-method thread > $out/tests.log 2>&1
 rc=$?; tail -6 $out/tests.log; [ $rc -eq 0 ] || [ $rc -eq 1 ] || exit $rc
