@@ -163,9 +163,9 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
     from ..utils import rng
     pts = points.to(torch.float64).contiguous()
     m, d = pts.shape
-    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0).contiguous()
-    if float(w.sum()) <= 0:
-        w = torch.ones(m, dtype=torch.float64, device=pts.device)
+    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0)
+    # all-zero weights -> uniform, decided on the device (no host read before the seeding kernels)
+    w = torch.where(w.sum() > 0, w, torch.ones_like(w)).contiguous()
     key_pp, key_e = rng.key(seed, 200), rng.key(seed, 201)
     lds_update = ((m * 4 + 15) & ~15) + d * 8
     if pts.is_cuda and d * 8 <= 64 * 1024 and lds_update <= 150 * 1024:
