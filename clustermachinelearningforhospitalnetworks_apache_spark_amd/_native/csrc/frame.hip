@@ -340,20 +340,48 @@ __global__ __launch_bounds__(kThreads) void reg_metrics_kernel(const double* __r
 }
 
 // partial[b][C*C]: weighted confusion counts cm[label][pred], labels/preds in [0, C).
-// Per-thread register-free: each block accumulates into LDS f64 with ds_add_f64 (C <= 32).
+// Deterministic (no float atomics): a wave takes 64 rows at a time and folds them cell by cell — the
+// first pending lane's cell, the masked weights of every lane holding that cell summed by a fixed
+// butterfly, added by that lane into the wave's private LDS histogram — so each cell's partial is a
+// fixed-order sum for a given n and grid; the block then adds its waves' histograms in wave order.
+// (Binary labels: at most 4 distinct cells per 64 rows, so ~4 butterflies per 64 rows.)
 __global__ __launch_bounds__(kThreads) void cls_confusion_kernel(const long long* __restrict__ y,
                                                                  const long long* __restrict__ p,
                                                                  const double* __restrict__ w, long long n, int C,
                                                                  double* __restrict__ partial) {
-  extern __shared__ double cm[];
-  for (int i = threadIdx.x; i < C * C; i += kThreads) cm[i] = 0.0;
+  extern __shared__ double cm[];  // [kThreads / 64][C * C]
+  const int CC = C * C, lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  constexpr int kWaves = kThreads / 64;
+  for (int i = threadIdx.x; i < kWaves * CC; i += kThreads) cm[i] = 0.0;
   __syncthreads();
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const long long a = y[i], b = p[i];
-    if (a >= 0 && a < C && b >= 0 && b < C) atomicAdd(&cm[a * C + b], w != nullptr ? w[i] : 1.0);
+  double* mine = cm + wv * CC;
+  for (long long base = ((long long)blockIdx.x * kWaves + wv) * 64; base < n; base += (long long)gridDim.x * kThreads) {
+    const long long i = base + lane;
+    int cell = -1;
+    double wi = 0.0;
+    if (i < n) {
+      const long long a = y[i], b = p[i];
+      if (a >= 0 && a < C && b >= 0 && b < C) {
+        cell = (int)(a * C + b);
+        wi = w != nullptr ? w[i] : 1.0;
+      }
+    }
+    unsigned long long pending = __ballot(cell >= 0);
+    while (pending) {
+      const int leader = __builtin_ctzll(pending);
+      const int lc = __shfl(cell, leader, 64);
+      const bool same = cell == lc;
+      const double v = wave_sum_f64(same ? wi : 0.0);
+      if (lane == leader) mine[lc] += v;
+      pending &= ~__ballot(same);
+    }
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < C * C; i += kThreads) partial[(long long)blockIdx.x * C * C + i] = cm[i];
+  for (int c = threadIdx.x; c < CC; c += kThreads) {
+    double t = 0.0;
+    for (int q = 0; q < kWaves; ++q) t += cm[q * CC + c];
+    partial[(long long)blockIdx.x * CC + c] = t;
+  }
 }
 
 // --------------------------------------------------------------------------------------------- K4
@@ -625,8 +653,11 @@ CML_API int cml_reg_metrics(const double* y, const double* p, const double* w, l
 CML_API int cml_cls_confusion(const long long* y, const long long* p, const double* w, long long n, int C,
                               double* partial, int grid, void* stream) {
   if (C < 1 || C > 64) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(cls_confusion_kernel, dim3(grid), dim3(kThreads), (size_t)C * C * sizeof(double),
-                     (hipStream_t)stream, y, p, w, n, C, partial);
+  const size_t lds = (size_t)(kThreads / 64) * C * C * sizeof(double);  // <= 128 KiB (C = 64)
+  if (lds > 64 * 1024)
+    hipFuncSetAttribute((const void*)cls_confusion_kernel, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  hipLaunchKernelGGL(cls_confusion_kernel, dim3(grid), dim3(kThreads), lds, (hipStream_t)stream, y, p, w, n, C,
+                     partial);
   return cml_status();
 }
 

@@ -151,6 +151,97 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
   }
 }
 
+// Exact training cost of an assignment: Σ_i |x_i - c_lab(i)|² with every difference and square in f64
+// (the values are bf16 / e4m3 and the centres the bf16 copies the assign compared against, so each
+// term is exact up to the f64 sum). The expanded form Σ(Q_j - 2c_j·S_j + n_j|c_j|²) of the pruned step
+// cancels catastrophically for data far from the origin (|x|² >> cost); this pass
+// reads X once instead, in the row-pass layout (LPR lanes per row, CPL 16-B chunks per lane), and
+// leaves fixed-order block partials (deterministic for a given n).
+template <int NCH, int CPL, bool F8, int U>
+__global__ __launch_bounds__(kThreads) void cost_pass_kernel(const unsigned char* __restrict__ X, long long n,
+                                                             long long ldb, const int* __restrict__ lab,
+                                                             const u16* __restrict__ cb, long long ldc,
+                                                             double* __restrict__ part) {
+  typedef float f2 __attribute__((ext_vector_type(2)));
+  constexpr int LPR = NCH / CPL;
+  constexpr int RPW = 64 / LPR;
+  constexpr int VPC = F8 ? 16 : 8;
+  const int lane = threadIdx.x & 63;
+  const int sub = lane / LPR, c = lane - sub * LPR;
+  const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
+  double acc = 0.0;
+  for (long long r0 = w0 * RPW; r0 < n; r0 += nw * RPW * U) {
+    uint4 v[U][CPL];
+    int lb[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + (long long)u * nw * RPW + sub;
+      lb[u] = row < n ? lab[row] : 0;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i)
+        v[u][i] = row < n ? *reinterpret_cast<const uint4*>(X + row * ldb + 16 * (c + LPR * i))
+                          : make_uint4(0u, 0u, 0u, 0u);
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long row = r0 + (long long)u * nw * RPW + sub;
+      const u16* cr = cb + (long long)lb[u] * ldc;
+      double s = 0.0;
+#pragma unroll
+      for (int i = 0; i < CPL; ++i) {
+        const unsigned w[4] = {v[u][i].x, v[u][i].y, v[u][i].z, v[u][i].w};
+        float xs[VPC];
+        if constexpr (F8) {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const f2 a = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], false);
+            const f2 b = __builtin_amdgcn_cvt_pk_f32_fp8((int)w[q], true);
+            xs[4 * q] = a.x;
+            xs[4 * q + 1] = a.y;
+            xs[4 * q + 2] = b.x;
+            xs[4 * q + 3] = b.y;
+          }
+        } else {
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            xs[2 * q] = bf16_to_f32((u16)(w[q] & 0xffffu));
+            xs[2 * q + 1] = bf16_to_f32((u16)(w[q] >> 16));
+          }
+        }
+        const int col0 = VPC * (c + LPR * i);
+        unsigned cw[VPC / 2];
+#pragma unroll
+        for (int h = 0; h < VPC / 8; ++h) {
+          const uint4 t = row < n ? *reinterpret_cast<const uint4*>(cr + col0 + 8 * h) : make_uint4(0u, 0u, 0u, 0u);
+          cw[4 * h] = t.x;
+          cw[4 * h + 1] = t.y;
+          cw[4 * h + 2] = t.z;
+          cw[4 * h + 3] = t.w;
+        }
+#pragma unroll
+        for (int e = 0; e < VPC; ++e) {
+          const float cv = bf16_to_f32((u16)((e & 1) ? (cw[e >> 1] >> 16) : (cw[e >> 1] & 0xffffu)));
+          const double df = (double)xs[e] - (double)cv;
+          s = fma(df, df, s);
+        }
+      }
+#pragma unroll
+      for (int o = LPR / 2; o > 0; o >>= 1) s += __shfl_xor(s, o, 64);
+      if (c == 0 && row < n) acc += s;
+    }
+  }
+  acc = wave_sum_f64(acc);
+  __shared__ double ws[kThreads / 64];
+  if (lane == 0) ws[threadIdx.x >> 6] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double t = 0.0;
+    for (int w = 0; w < kThreads / 64; ++w) t += ws[w];
+    part[blockIdx.x] = t;
+  }
+}
+
 // cost/nearest from one candidate chunk's K9r pass (best distance + label within the chunk)
 __global__ __launch_bounds__(kThreads) void init_merge_kernel(float* __restrict__ cost, int* __restrict__ near,
                                                               const float* __restrict__ best,
@@ -563,6 +654,46 @@ CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int D
     default: return (int)hipErrorInvalidValue;
   }
 #undef CML_RP
+  return cml_status();
+}
+
+// out[0] = Σ_i |x_i - cb[lab[i]]|² in f64 (exact terms, fixed-order sum). X as in cml_kmeans_row_pass;
+// cb: bf16 [*, ldc elements] with ldc >= Dp (zero beyond the real columns, as X), 16-byte aligned rows;
+// lab: int32 [n], every value a valid row of cb; part: cml_kmeans_cost_parts() doubles of scratch.
+CML_API int cml_kmeans_cost_parts() { return 4096; }
+CML_API int cml_kmeans_cost_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, const int* lab,
+                                 const void* cb, long long ldc, double* part, double* out, void* stream) {
+  if (n < 0 || ldc < Dp || ldc % 8 != 0) return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (n == 0) return (int)hipMemsetAsync(out, 0, sizeof(double), st);
+  const unsigned char* x = (const unsigned char*)X;
+  const u16* c = (const u16*)cb;
+  constexpr int U = 2;
+  const long long rowb = xfp8 ? (long long)Dp : 2LL * Dp;
+  if (xfp8 ? (Dp % 64 != 0 || Dp > 1024 || ldx % 16 != 0) : (Dp % 16 != 0 || Dp > 512 || ldx % 8 != 0))
+    return (int)hipErrorInvalidValue;
+  const long long ldb = xfp8 ? ldx : 2 * ldx;
+  unsigned nb = 0;
+#define CML_CP(NCH, CPL, F)                                                                                  \
+  nb = grid_for(n, 4LL * (64 / ((NCH) / (CPL))) * U);                                                        \
+  hipLaunchKernelGGL((cost_pass_kernel<NCH, CPL, F, U>), dim3(nb), dim3(kThreads), 0, st, x, n, ldb, lab, c, \
+                     ldc, part)
+  switch ((int)(rowb / 16) * (xfp8 ? -1 : 1)) {
+    case 2: CML_CP(2, 2, false); break;
+    case 4: CML_CP(4, 4, false); break;
+    case 8: CML_CP(8, 4, false); break;
+    case 16: CML_CP(16, 4, false); break;
+    case 32: CML_CP(32, 4, false); break;
+    case 64: CML_CP(64, 4, false); break;
+    case -4: CML_CP(4, 4, true); break;
+    case -8: CML_CP(8, 4, true); break;
+    case -16: CML_CP(16, 4, true); break;
+    case -32: CML_CP(32, 4, true); break;
+    case -64: CML_CP(64, 4, true); break;
+    default: return (int)hipErrorInvalidValue;
+  }
+#undef CML_CP
+  hipLaunchKernelGGL(sum_partials_kernel, dim3(1), dim3(1), 0, st, part, (int)nb, out);
   return cml_status();
 }
 

@@ -205,6 +205,21 @@ def _non_numeric_numbers(pdf, files) -> dict:
     import json
     import math
     import numbers
+    # only columns pandas typed float-with-NaN or object-holding-such-a-string can be affected: with none,
+    # the files are not read a second time (any quoted "NaN" inside an ordinary string value
+    # used to trigger a full re-parse of every record)
+    cand = []
+    for c in pdf.columns:
+        col = pdf[c]
+        if col.dtype.kind == "f":
+            if bool(col.isna().any()):
+                cand.append(c)
+        elif col.dtype == object:
+            if any((isinstance(v, str) and v in _NON_NUMERIC) or (isinstance(v, float) and math.isnan(v))
+                   for v in col):
+                cand.append(c)
+    if not cand:
+        return {}
     texts = []
     for f in files:
         with open(f, encoding="utf-8") as fh:
@@ -215,7 +230,7 @@ def _non_numeric_numbers(pdf, files) -> dict:
     if len(recs) != len(pdf):
         return {}
     out = {}
-    for c in pdf.columns:
+    for c in cand:
         vals = [r.get(c) for r in recs]
         present = [v for v in vals if v is not None]
         if not any(isinstance(v, str) and v in _NON_NUMERIC for v in present):
@@ -223,6 +238,16 @@ def _non_numeric_numbers(pdf, files) -> dict:
         if not all((isinstance(v, str) and v in _NON_NUMERIC) or
                    (isinstance(v, numbers.Number) and not isinstance(v, bool)) for v in present):
             continue
+        if not any(isinstance(v, numbers.Number) for v in present):
+            # only strings (no JSON number at all): Spark's inference keeps a string column
+            pdf[c] = pd_object(vals)
+            continue
         out[c] = [None if v is None else (_NON_NUMERIC[v] if isinstance(v, str) else float(v)) for v in vals]
         pdf[c] = [0.0 if v is None or (isinstance(v, float) and math.isnan(v)) else v for v in out[c]]
     return out
+
+
+def pd_object(vals):
+    """A pandas object column holding exactly ``vals`` (strings and None, no NaN coercion)."""
+    import pandas as pd
+    return pd.Series(vals, dtype=object)

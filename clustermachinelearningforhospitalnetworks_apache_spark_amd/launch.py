@@ -64,6 +64,30 @@ def _terminate(procs: List[subprocess.Popen], grace: float) -> None:
             p.wait()
 
 
+def visible_gpu_count(sysfs: str = "/sys/class/kfd/kfd/topology/nodes") -> int:
+    """GPUs this job may use, counted WITHOUT touching the HIP runtime (the launcher forks and execs the
+    ranks, and a process that initialised the GPU must not do that): the KFD topology nodes with SIMDs
+    (CPU nodes report simd_count 0), narrowed by HIP/ROCR/CUDA_VISIBLE_DEVICES when set."""
+    n = 0
+    try:
+        for node in sorted(os.listdir(sysfs)):
+            try:
+                with open(os.path.join(sysfs, node, "properties")) as fh:
+                    props = dict(line.split()[:2] for line in fh if len(line.split()) >= 2)
+            except OSError:
+                continue
+            if int(props.get("simd_count", "0")) > 0:
+                n += 1
+    except OSError:
+        n = 0
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        v = os.environ.get(var)
+        if v is not None:
+            ids = [t for t in v.split(",") if t.strip() != ""]
+            n = min(n, len(ids)) if n else len(ids)
+    return n
+
+
 def run_job(cmd: List[str], nproc: int, grace: float = 10.0, port: Optional[int] = None,
             env: Optional[dict] = None) -> int:
     """Start ``nproc`` ranks of ``cmd`` and supervise them; returns the job's exit code."""
@@ -110,11 +134,7 @@ def main(argv: Optional[List[str]] = None) -> int:
         ap.error("give a script or -m module")
     nproc = a.nproc_per_node
     if nproc is None:
-        try:  # counting devices does not initialise the GPU on this image
-            import torch
-            nproc = max(1, torch.cuda.device_count())
-        except Exception:
-            nproc = 1
+        nproc = max(1, visible_gpu_count())
     cmd = [sys.executable] + (["-m", a.module] if a.module else [a.script]) + \
         ([a.script] if a.module and a.script else []) + list(a.args)
     rc = 1

@@ -140,19 +140,29 @@ class KMeans(Estimator):
 
 
 def _weights(df, col: str, device) -> torch.Tensor:
-    """The weight column as f64 (Spark's checkNonNegativeWeight: finite, >= 0, not null)."""
+    """The weight column as f64 (Spark's checkNonNegativeWeight: finite, >= 0, not null).
+
+    The check is agreed over every rank before anything is raised (one max all-reduce of a
+    [has null, has bad value] flag pair): a bad weight on one shard makes every rank raise the same
+    ValueError instead of leaving the others blocked in the init collectives."""
     cd = df._column_data(col)
+    nulls = False
     if cd.is_host:
         from ..sql.dataframe import column_to_python
         vals = column_to_python(cd)
-        if any(v is None for v in vals):
-            raise ValueError(f"weight column {col!r} contains nulls")
-        w = torch.as_tensor(np.asarray(vals, dtype=np.float64), device=device)
+        nulls = any(v is None for v in vals)
+        w = torch.as_tensor(np.asarray([0.0 if v is None else v for v in vals], dtype=np.float64), device=device)
     else:
-        if cd.valid is not None and not bool(cd.valid.all()):
-            raise ValueError(f"weight column {col!r} contains nulls")
+        nulls = cd.valid is not None and not bool(cd.valid.all())
         w = cd.values.to(device=device, dtype=torch.float64).reshape(-1)
-    if w.numel() and not bool(((w >= 0) & torch.isfinite(w)).all()):
+    bad = bool(w.numel()) and not bool(((w >= 0) & torch.isfinite(w)).all())
+    comm = df._comm
+    flags = torch.tensor([float(nulls), float(bad)], dtype=torch.float64, device=comm.device)
+    if comm.is_distributed:
+        comm.allreduce_(flags, op="max")
+    if flags[0].item() > 0:
+        raise ValueError(f"weight column {col!r} contains nulls")
+    if flags[1].item() > 0:
         raise ValueError(f"weights must be finite and non-negative (column {col!r})")
     return w
 

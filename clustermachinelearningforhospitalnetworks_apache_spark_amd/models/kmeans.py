@@ -75,6 +75,44 @@ def to_device_matrix(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
     return out
 
 
+def host_layout(x: torch.Tensor, d: Optional[int] = None) -> torch.Tensor:
+    """The pinned host copy of an out-of-core feature matrix in the kernels' layout (bf16
+    [n, padded_dim(d)], or e4m3fn [n, padded_dim_fp8(d)] for fp8 rows), written straight into page-locked
+    memory chunk by chunk (no unpinned intermediate) and cached on ``x`` while it is unmodified, so the
+    fits and transforms of one column share one copy — and, through it, the cached row norms and stream
+    buffers (every transform used to make a new bf16 copy plus a pinned copy of it). A matrix
+    already in that layout and pinned is used as is."""
+    from ..utils.hoststream import pinned_rows
+    d = x.shape[1] if d is None else d
+    fp8 = x.dtype == torch.float8_e4m3fn
+    dp = padded_dim_fp8(d) if fp8 else padded_dim(d)
+    want = torch.float8_e4m3fn if fp8 else torch.bfloat16
+    layout = x.dtype == want and x.shape[1] == dp and x.is_contiguous()
+    if layout and (x.is_pinned() or not torch.cuda.is_available()):
+        return x
+    ent = getattr(x, "_cml_hostlayout", None)
+    if ent is not None and ent[0] == x._version and ent[1] == d:
+        return ent[2]
+    pin = torch.cuda.is_available()
+    n = x.shape[0]
+    if layout:
+        out = pinned_rows(x)
+    elif fp8:
+        out = torch.zeros((n, dp), dtype=torch.uint8, pin_memory=pin)
+        out[:, :d] = x[:, :d].view(torch.uint8)
+        out = out.view(torch.float8_e4m3fn)
+    else:
+        out = torch.zeros((n, dp), dtype=torch.bfloat16, pin_memory=pin)
+        step = 1 << 20
+        for s in range(0, n, step):
+            out[s:s + step, :d] = x[s:s + step, :d].to(torch.bfloat16)
+    try:
+        x._cml_hostlayout = (x._version, d, out)
+    except (AttributeError, RuntimeError):
+        pass
+    return out
+
+
 def unit_rows(x: torch.Tensor, d: Optional[int] = None, exact: Optional[bool] = None) -> torch.Tensor:
     """Rows scaled to unit length (cosine KMeans). bf16 on the GPU's MFMA path (computed in f32; fp8
     inputs widen to bf16: unit components need more than e4m3's 3 mantissa bits), f64 on the CPU and
@@ -136,8 +174,9 @@ class LloydEngine:
         if streamed:
             if weights is not None or spherical:
                 raise ValueError("streamed (out-of-core) KMeans supports unweighted euclidean fits")
-            if x.dtype not in (torch.bfloat16, torch.float8_e4m3fn):
-                x = to_device_matrix(x, d)  # bf16 on the host
+            # the pinned bf16/fp8 padded copy, made once per column and reused by every later fit and
+            # transform of it (with its cached norms and its stream buffers)
+            x = host_layout(x, d)
             precision, prune, incremental, use_graph = "bf16", False, False, False
         # full re-accumulation of the incremental sums every refresh_interval steps (0 = never: the sum
         # grid of _sum_grid already keeps incremental == full bit for bit; conf
@@ -209,14 +248,14 @@ class LloydEngine:
         self.n = int(x.shape[0])
         self.device = torch.device(device) if streamed else x.device
         if streamed:
-            from ..utils.hoststream import HostRowStream, pinned_rows
-            self.x = pinned_rows(to_device_matrix(x, d))
+            from ..utils.hoststream import HostRowStream, cached_stream
+            self.x = x
             self.dp = self.x.shape[1]
             if stream_chunk_rows is None:  # ~1 GiB per buffer
                 stream_chunk_rows = max(1024, (1 << 30) // (self.dp * self.x.element_size()))
             bounds = HostRowStream.chunk_bounds(self.n, stream_chunk_rows)
             row_chunks = len(bounds) - 1
-            self._hs = HostRowStream(self.x, bounds[1] - bounds[0] if self.n else 1, self.device)
+            self._hs = cached_stream(self.x, bounds[1] - bounds[0] if self.n else 1, self.device)
             self._hs_bounds = bounds  # (re-deriving them from the first chunk's size splits a lone short chunk)
         elif self.gpu:
             self.x = to_device_matrix(x, d)
@@ -303,6 +342,7 @@ class LloydEngine:
                       if self._incremental and self.cplan.mode == "sort" and self.aplan.kc == self.aplan.kp else None)
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
+        self._cb_cost = torch.zeros_like(self.cb)  # centres of the last full/torch-pruned step's assignment
         self.cnorm = torch.zeros(self.kp, dtype=torch.float32, device=dev)
         self.shift2 = torch.zeros(k, dtype=torch.float64, device=dev)
         self._prev_centers = torch.zeros((k, d), dtype=torch.float64, device=dev) if self.spherical else None
@@ -502,8 +542,7 @@ class LloydEngine:
             self._graph[1].replay()
         else:
             self._graph.replay()
-        if self._pdev:
-            self._cost_fn = self._pdev_cost
+        self._cost_fn = self._exact_cost
 
     def _best(self, r0: int, r1: int):
         return None if self.best is None else self.best[r0:r1]
@@ -544,7 +583,13 @@ class LloydEngine:
             handles.append(self.comm.allreduce_async(msg))
         for h in handles:
             h.wait()
-        self.last_cost = self.msgs[:, -1].sum()
+        if self._hs is None:
+            # the exact cost of this assignment is evaluated on first read (_exact_cost) against a copy of
+            # the centres it was made with; streamed rows keep the assign's per-row f32 distances
+            self._cb_cost.copy_(self.cb)
+            self._cost_fn = self._exact_cost
+        else:
+            self.last_cost = self.msgs[:, -1].sum()
         self._update_gpu(self.msgs)
 
     def _update_gpu(self, msgs: torch.Tensor) -> None:
@@ -669,7 +714,7 @@ class LloydEngine:
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
                        st.c2, st.count, st.force, cum=st.cum)
-        self._cost_fn = self._pdev_cost
+        self._cost_fn = self._exact_cost
 
     def _seed_from_init(self, sd) -> None:
         """Labels and bounds of every row from the k-means|| init (kmeans_seed_bounds): row x's nearest
@@ -739,23 +784,21 @@ class LloydEngine:
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
                        st.c2, st.count, st.force, cum=st.cum)
-        self._cost_fn = self._pdev_cost
+        self._cost_fn = self._exact_cost
 
-    def _pdev_cost(self) -> torch.Tensor:
-        """Cost of the last step's assignment (Spark's per-iteration cost): Σ_j (Q_j - 2 c_j·S_j +
-        n_j |c_j|²) over the centres it assigned against (cb_old), S/n its all-reduced sums, Q_j the
-        per-centre Σ|x|² of the current labels (one group-sum over the rows, all-reduced)."""
-        st, k, d, n = self._pst, self.k, self.d, self.n
-        kd = k * d
-        q = group_reduce(self.labels[:n], self.xnorm[:n].to(torch.float64), k, "sum") if n else torch.zeros(
-            k, dtype=torch.float64, device=self.device)
-        q = q.to(torch.float64).contiguous()
-        self.comm.allreduce_(q)
-        c = st.cb_old[:k, :d].to(torch.float64)
-        msg = self.msgs[0]
-        s_, cnt = msg[:kd].view(k, d) * self._unit, msg[kd:kd + k]
-        cost = q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()
-        return cost.clamp(min=0.0)
+    def _exact_cost(self) -> torch.Tensor:
+        """Cost of the last step's assignment (Spark's per-iteration cost) on the device rows: one exact
+        pass Σ_i |x_i - c_lab(i)|² (f64 differences and squares, K.cost_pass) against the bf16 centres that
+        assignment compared with (the pruned step's cb_old, else the copy _step_gpu keeps), all-reduced.
+        Read lazily — a fit whose cost is never read never pays the pass. The expanded per-centre form
+        Σ(Q_j - 2c_j·S_j + n_j|c_j|²) it replaces lost percents for data far from the origin (|x|² >> cost)."""
+        cb = self._pst.cb_old if self._pdev else self._cb_cost
+        if self.n:
+            cost = K.cost_pass(self.x, self.n, self.dp, self.labels, cb)
+        else:
+            cost = torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.comm.allreduce_(cost)
+        return cost[0]
 
     def _pdev_last(self) -> tuple:
         """(full pass?, re-assigned rows) of the last device pruned step (synchronises)."""
@@ -931,8 +974,9 @@ class LloydEngine:
         msg = torch.cat([st.G[:kd + k], cost.reshape(1)])
         old = c.clone()
         if self.gpu:
-            self.last_cost = msg[-1]
+            self._cb_cost.copy_(self.cb)  # exact cost on first read (the expanded form above cancels)
             self._update_gpu(msg.view(1, -1))
+            self._cost_fn = self._exact_cost
         else:
             self._update_cpu(msg)
         st.valid = True

@@ -80,6 +80,8 @@ _native.register_kernel_sigs({
                                     c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_sum_f32_f64_parts": (c_int, []),
+    "cml_kmeans_cost_parts": (c_int, []),
+    "cml_kmeans_cost_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_sum_f32_f64": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
                                        c_vp]),
@@ -133,6 +135,24 @@ def sum_f64(x: torch.Tensor, n: int, stream=None) -> torch.Tensor:
     _native.check(lib.cml_sum_f32_f64(x.data_ptr(), int(n), part.data_ptr(), out.data_ptr(),
                                       _native.stream_ptr(stream)), "sum_f32_f64")
     return out[0]
+
+
+def cost_pass(x: torch.Tensor, n: int, dp: int, lab: torch.Tensor, cb: torch.Tensor, stream=None) -> torch.Tensor:
+    """Σ_i |x_i - cb[lab_i]|² over the first n device rows as an f64 device tensor [1] (``kmeans_init.hip``):
+    every difference and square in f64, fixed-order block partials — the exact cost of an assignment
+    against the bf16 centres ``cb`` [kp, >= dp] it was made with, with no cancellation for data far from
+    the origin (the expanded Σ(Q - 2c·S + n|c|²) form loses ~(|x|²/cost)·2^-24)."""
+    if lab.dtype != torch.int32 or not lab.is_contiguous() or cb.dtype != torch.bfloat16 or cb.stride(1) != 1:
+        raise ValueError("cost_pass: int32 labels and bf16 centres")
+    if lab.numel() < n or cb.shape[1] < dp or x.shape[0] < n:
+        raise ValueError("cost_pass: operand shapes")
+    lib = _native.kernels()
+    part = torch.empty(int(lib.cml_kmeans_cost_parts()), dtype=torch.float64, device=x.device)
+    out = torch.empty(1, dtype=torch.float64, device=x.device)
+    _native.check(lib.cml_kmeans_cost_pass(x.data_ptr(), int(n), x.stride(0), int(dp), int(is_fp8(x)),
+                                           lab.data_ptr(), cb.data_ptr(), cb.stride(0), part.data_ptr(),
+                                           out.data_ptr(), _native.stream_ptr(stream)), "kmeans_cost_pass")
+    return out
 
 
 def init_merge(cost: torch.Tensor, near: torch.Tensor, best: torch.Tensor, lab: torch.Tensor, off: int,

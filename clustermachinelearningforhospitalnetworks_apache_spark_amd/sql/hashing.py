@@ -206,7 +206,9 @@ def hash_value(v: Any, dt: T.DataType, seed: int, algo: str) -> int:
         unscaled = _unscaled(v, dt.scale)
         if dt.precision <= 18:
             return fl(unscaled, seed)
-        return fb(unscaled.to_bytes((unscaled.bit_length() + 8) // 8, "big", signed=True), seed)
+        # Java's bitLength ignores the sign bit: for negatives it is that of ~v (-128 -> 7 bits, 1 byte)
+        nbits = (unscaled if unscaled >= 0 else ~unscaled).bit_length()
+        return fb(unscaled.to_bytes(nbits // 8 + 1, "big", signed=True), seed)
     if isinstance(dt, T.DoubleType):
         return fl(_double_bits(float(v)), seed)
     if isinstance(dt, T.BinaryType):

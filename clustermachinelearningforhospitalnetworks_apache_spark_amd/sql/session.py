@@ -209,9 +209,13 @@ class SparkSession:
                 raise ValueError("all columns need the same number of rows")
             if (t.dim() == 2 and not t.is_cuda and self._device.type == "cuda"
                     and t.numel() * t.element_size() > budget):
-                # out of core: a vector column larger than cml.hbm.budgetBytes stays in pinned
-                # host memory; KMeans streams it through the GPU chunk by chunk (utils/hoststream.py)
-                t = pinned_rows(t)
+                # out of core: a vector column larger than cml.hbm.budgetBytes stays in host
+                # memory; KMeans streams it through the GPU chunk by chunk (utils/hoststream.py). bf16 / fp8
+                # rows are pinned here; other dtypes get their pinned bf16 copy on first use (one copy,
+                # cached on the column: models/kmeans.py host_layout) — pinning the f32 source too would
+                # hold twice the page-locked memory
+                if t.dtype in (torch.bfloat16, torch.float8_e4m3fn):
+                    t = pinned_rows(t)
             else:
                 t = t.to(self._device)
             if t.dim() == 2:

@@ -46,6 +46,25 @@ def pinned_rows(x: torch.Tensor) -> torch.Tensor:
     return x.pin_memory()
 
 
+def cached_stream(xh: torch.Tensor, chunk_rows: int, device: torch.device) -> "HostRowStream":
+    """One HostRowStream (two device chunk buffers + copy stream) per pinned matrix, chunk size and
+    device, kept on the matrix: repeated fits / transforms of an out-of-core column reuse its buffers
+    instead of allocating 2 x ~1 GiB of HBM per call."""
+    key = (str(device), int(chunk_rows))
+    cache = getattr(xh, "_cml_streams", None)
+    if cache is None:
+        cache = {}
+        try:
+            xh._cml_streams = cache
+        except (AttributeError, RuntimeError):
+            pass
+    hs = cache.get(key)
+    if hs is None or hs.xh is not xh:
+        hs = HostRowStream(xh, chunk_rows, device)
+        cache[key] = hs
+    return hs
+
+
 class HostRowStream:
     """Double-buffered H2D streaming of a pinned host matrix [n, dp] in row chunks."""
 

@@ -110,6 +110,27 @@ def test_binarize_and_metric_sums():
                                rtol=1e-10)
 
 
+@pytest.mark.parametrize("C", [2, 7, 33, 64])
+def test_weighted_confusion_deterministic(C):
+    """Fractional weights: the confusion counts are a fixed-order sum (no float atomics), bitwise equal
+    across runs, and equal to the f64 oracle at 1e-12."""
+    n = 2_000_003
+    g = torch.Generator().manual_seed(C)
+    yl = torch.randint(0, C, (n,), generator=g)
+    pl = torch.where(torch.rand(n, generator=g) < 0.7, yl, torch.randint(0, C, (n,), generator=g))
+    w = torch.rand(n, generator=g, dtype=torch.float64) * 3.3 + 1e-3
+    a = F.confusion(yl.cuda(), pl.cuda(), C, w.cuda()).cpu()
+    b = F.confusion(yl.cuda(), pl.cuda(), C, w.cuda()).cpu()
+    assert torch.equal(a, b)
+    cm = torch.zeros(C * C, dtype=torch.float64).index_add_(0, yl * C + pl, w).reshape(C, C)
+    np.testing.assert_allclose(a.numpy(), cm.numpy(), rtol=1e-12)
+    # out-of-range ids are skipped
+    yl[:10] = -1
+    pl[10:20] = C
+    c = F.confusion(yl.cuda(), pl.cuda(), C, None).cpu()
+    assert float(c.sum()) == n - 20
+
+
 @pytest.mark.parametrize("src", [torch.float32, torch.bfloat16])
 def test_fp8_quantisation(src):
     n, d = 4099, 37

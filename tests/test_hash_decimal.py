@@ -20,6 +20,12 @@ def test_decimal_hash_uses_unscaled_value():
     assert hash_value(v, wide, 42, "murmur3") == m3_bytes(u.to_bytes((u.bit_length() + 8) // 8, "big", signed=True),
                                                           42)
     assert hash_value(Decimal("-1.000"), wide, 42, "xxhash64") == xx_bytes(b"\xfc\x18", 42)  # -1000
+    # BigInteger.toByteArray is minimal for negative powers of two: -128 -> [0x80], -32768 -> [0x80, 0x00]
+    w2 = T.DecimalType(38, 2)
+    assert hash_value(Decimal("-1.28"), w2, 42, "murmur3") == m3_bytes(b"\x80", 42)
+    assert hash_value(Decimal("-327.68"), w2, 42, "xxhash64") == xx_bytes(b"\x80\x00", 42)
+    assert hash_value(Decimal("-1.29"), w2, 42, "murmur3") == m3_bytes(b"\xff\x7f", 42)
+    assert hash_value(Decimal("1.28"), w2, 42, "murmur3") == m3_bytes(b"\x00\x80", 42)
 
 
 def test_decimal_column_hash_matches_host():

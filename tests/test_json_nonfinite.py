@@ -21,3 +21,18 @@ def test_json_nan_inf_round_trip(tmp_path):
         got = {r["id"]: r["v"] for r in back.collect()}
         assert got[1] == 1.5 and math.isnan(got[2]) and got[3] == math.inf and got[4] == -math.inf
         assert got[5] is None
+
+
+def test_json_nan_strings_without_numbers_stay_strings(tmp_path):
+    """a column whose present values are only such strings (no JSON number at all) is a
+    string column, as Spark infers it; a "NaN" inside an ordinary string value changes nothing."""
+    p = tmp_path / "s.json"
+    p.write_text('{"a":"NaN","b":1.5,"c":"x \\"NaN\\" y"}\n{"a":"Infinity","b":2.0,"c":"z"}\n{"b":3.0,"c":"w"}\n')
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    df = spark.read.json(str(p))
+    types = {f.name: f.dataType for f in df.schema.fields}
+    assert isinstance(types["a"], T.StringType), types
+    assert isinstance(types["b"], T.DoubleType) and isinstance(types["c"], T.StringType)
+    rows = sorted(df.collect(), key=lambda r: r["b"])
+    assert [r["a"] for r in rows] == ["NaN", "Infinity", None]
+    assert rows[0]["c"] == 'x "NaN" y'

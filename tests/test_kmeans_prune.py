@@ -37,8 +37,9 @@ def _pair(x, d, k, init, steps, **kw):
         n = a.n
         assert torch.equal(a.labels[:n].long(), b.labels[:n].long())
         torch.testing.assert_close(b.centers, a.centers, rtol=1e-12, atol=1e-12)
-        # full step: Σ of the assign's f32 row distances; pruned: Σ_j (Q_j - 2 c_j·S_j + n_j |c_j|²) in f64
-        rtol = 1e-5 if x.is_cuda else 1e-9
+        # GPU: both evaluate the exact f64 cost pass over the same labels and bf16 centres (bit for bit);
+        # CPU: full = Σ of the f64 row distances, pruned = Σ_j (Q_j - 2 c_j·S_j + n_j |c_j|²) in f64
+        rtol = 0.0 if x.is_cuda else 1e-9
         assert abs(float(b.last_cost) - float(a.last_cost)) <= rtol * max(1.0, abs(float(a.last_cost)))
         assert torch.equal(a._shift2 <= 1e-8, b._shift2 <= 1e-8)
     return a, b, stats
@@ -380,3 +381,29 @@ def test_centre_stats_kernel_matches_torch(k, d):
     assert abs(float(f["mc"]) - float(cn.max())) <= 1e-6 * float(cn.max())
     assert abs(float(f["c2"]) - 2 * tau * (1234.5 + float(cn.max()))) <= 1e-6 * float(f["c2"])
     assert int(f["count"]) == 0 and int(f["force"]) == 0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fp8,prune", [(False, True), (False, False), (True, True)])
+def test_training_cost_exact_on_offset_data_gpu(fp8, prune):
+    """trainingCost on data far from the origin (blobs + 300: |x|² ~ 2.3e7 per row against a cost of ~256
+    per row) equals the f64 oracle Σ|x_i - c_lab(i)|² over the same labels and bf16 centres at 1e-9 (the
+    expanded Σ(Q - 2c·S + n|c|²) form with f32 norms was off by percents here)."""
+    n, d, k = 200_000, 256, 64
+    x = _blobs(n, d, k, seed=17, scale=1.0, device="cuda", dtype=torch.float32) + 300.0
+    x = x.clamp(-440, 440).to(torch.float8_e4m3fn) if fp8 else x.to(torch.bfloat16)
+    eng = LloydEngine(x, d, k, prune=prune, use_graph=False)
+    eng.set_centers(x[:k].float().double().cpu().numpy())
+    for _ in range(4):
+        eng.step()
+    cb = (eng._pst.cb_old if eng._pdev else eng._cb_cost)[:k, :d].double()
+    lab = eng.labels[:n].long()
+    xf = x[:, :d].float().double()
+    ref = float(((xf - cb[lab]) ** 2).sum())
+    got = eng.training_cost()
+    assert abs(got - ref) <= 1e-9 * ref, (got, ref)
+    # the kernel alone, on the padded device matrix
+    xm = eng.x
+    c1 = float(K.cost_pass(xm, n, eng.dp, eng.labels, eng.cb).item())
+    ref1 = float(((xf - eng.cb[:k, :d].double()[lab]) ** 2).sum())
+    assert abs(c1 - ref1) <= 1e-9 * ref1

@@ -46,8 +46,8 @@ def test_streamed_fit_equals_resident(n, d, k, dtype, chunk):
         torch.cuda.synchronize()
         assert torch.equal(res.centers, st.centers), f"step {it}"
         assert torch.equal(res.labels[:n], st.labels[:n]), f"step {it}"
-    # same labels and centres; the resident fit's pruned steps evaluate the cost by the per-centre expansion
-    # (sum|x|^2 - 2 c.S + n|c|^2 from the exact sums), the streamed full steps sum per-row f32 distances
+    # same labels and centres; the resident fit evaluates the cost by the exact f64 cost pass, the streamed
+    # full steps sum the assign's per-row f32 distances
     assert st.training_cost() == pytest.approx(res.training_cost(), rel=1e-6)
     lab_r, d_r = res.assign()
     lab_s, d_s = st.assign()
@@ -91,3 +91,36 @@ def test_budget_conf_streams_the_feature_column():
     assert out["resident"][1] == out["streamed"][1]
     assert out["streamed"][2] == pytest.approx(out["resident"][2], rel=1e-6)  # cost formulas differ (above)
     assert torch.equal(out["resident"][3], out["streamed"][3])
+
+
+def test_f32_out_of_core_column_converted_once():
+    """an f32 out-of-core column is converted to the pinned bf16 layout ONCE — fit, transform
+    and computeCost reuse that copy (and its stream buffers) instead of making a bf16 copy plus a pinned
+    copy per call; the host RSS growth over repeated transforms stays far below one matrix."""
+    import psutil
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    spark = SparkSession.builder.master("mi355x").getOrCreate()
+    n, d, k = 400_000, 200, 16
+    xh = _blobs(n, d, k, seed=12, dtype=torch.float32)
+    spark.conf.set("cml.hbm.budgetBytes", str(1 << 20))
+    try:
+        df = spark.createDataFrameFromTensors({"features": xh})
+        col = df._feature_matrix("features")
+        assert not col.is_cuda and col.dtype == torch.float32
+        m = KMeans(k=k, seed=4, maxIter=4, tol=0.0).fit(df)
+        layout = col._cml_hostlayout[2]
+        assert layout.is_pinned() and layout.dtype == torch.bfloat16 and layout.shape == (n, 256)
+        ptr = layout.data_ptr()
+        m.transform(df)._numeric("prediction")
+        proc = psutil.Process()
+        rss0 = proc.memory_info().rss
+        for _ in range(3):
+            m.transform(df)._numeric("prediction")
+            m.computeCost(df)
+        grown = proc.memory_info().rss - rss0
+        assert col._cml_hostlayout[2].data_ptr() == ptr
+        assert len(layout._cml_streams) == 1
+        assert grown < 0.25 * layout.numel() * layout.element_size(), grown
+    finally:
+        spark.conf.unset("cml.hbm.budgetBytes")

@@ -171,3 +171,32 @@ def test_weighted_gpu_fit_equals_cpu_fit():
     assert np.array_equal(res[0][0], res[1][0])
     assert np.array_equal(res[0][1], res[1][1])
     assert res[0][2] == res[1][2]
+
+
+def _bad_weight_rank(rank, world, port, out):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "LOCAL_RANK": str(rank),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port), "CML_FORCE_CPU": "1"})
+    torch.set_num_threads(1)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    x, rs = _blobs(400, seed=6)
+    w = rs.uniform(0.1, 2.0, len(x))
+    w[-1] = -1.0  # one bad weight: it lands on exactly one rank's shard
+    try:
+        KMeans(k=3, seed=1, weightCol="w", maxIter=3).fit(_frame(spark, x, w))
+        msg = "no error"
+    except ValueError as e:
+        msg = str(e)
+    with open(f"{out}.{rank}", "w") as fh:
+        fh.write(msg)
+    spark.stop()
+
+
+def test_bad_weight_on_one_rank_raises_on_every_rank(tmp_path):
+    """the weight check is agreed across ranks, so every rank raises the same ValueError at
+    once instead of the clean ranks blocking in the init collectives until the watchdog fires."""
+    out = str(tmp_path / "bad")
+    mp.start_processes(_bad_weight_rank, args=(2, _free_port(), out), nprocs=2, join=True, start_method="spawn")
+    for r in range(2):
+        assert "finite and non-negative" in open(f"{out}.{r}").read()

@@ -61,3 +61,21 @@ def test_launch_restarts_failed_job(tmp_path):
     """)
     assert launch.main(["--nproc-per-node", "2", "--max-restarts", "1", app]) == 0
     assert marker.exists()
+
+
+def test_visible_gpu_count_from_kfd_sysfs(tmp_path, monkeypatch):
+    """The launcher counts GPUs from the KFD topology (nodes with SIMDs), never through the HIP runtime,
+    and honours the *_VISIBLE_DEVICES masks."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.launch import visible_gpu_count
+    for i, simds in enumerate([0, 0, 1024, 1024, 1024]):  # two CPU nodes, three GPUs
+        d = tmp_path / str(i)
+        d.mkdir()
+        (d / "properties").write_text(f"cpu_cores_count 0\nsimd_count {simds}\nmax_waves_per_simd 8\n")
+    for var in ("ROCR_VISIBLE_DEVICES", "HIP_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"):
+        monkeypatch.delenv(var, raising=False)
+    assert visible_gpu_count(str(tmp_path)) == 3
+    monkeypatch.setenv("HIP_VISIBLE_DEVICES", "0,2")
+    assert visible_gpu_count(str(tmp_path)) == 2
+    assert visible_gpu_count(str(tmp_path / "missing")) == 2
+    monkeypatch.delenv("HIP_VISIBLE_DEVICES")
+    assert visible_gpu_count(str(tmp_path / "missing")) == 0
