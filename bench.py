@@ -2,16 +2,19 @@
 """Headline benchmark: KMeans fit samples/sec (whole job), BASELINE.json config
 "KMeans k=256 on 100M×256, DP across MI355X with RCCL all-reduce of centroid sums".
 
-The timed region is ONE WHOLE FIT from scratch, the metric SURVEY.md §6 / BASELINE.md define
-(samples/s = N_rows x Lloyd iterations / fit wall time): LloydEngine construction (device
-layout + row norms), k-means|| initialisation (initSteps=2, as Spark's KMeans.fit runs it) and
---steps Lloyd iterations with tol=0, i.e. what ``KMeans(k=256, maxIter=steps, tol=0).fit`` runs
-(ml/clustering.py). A step = one distributed Lloyd iteration: K9r MFMA distance GEMM + argmin,
-K10 per-cluster sums, RCCL all-reduce of the f64 [k·D sums | k counts | cost] message, K11 centre
-update. --warmup runs an untimed warm-up fit of that many iterations first. The steady-state
-step rate after the fit is reported in extra (not the headline). The dataset is fixed (100M rows
-total) and sharded over the N ranks, so scaling is *strong*. Data: synthetic Gaussian blobs
-generated on the GPU, bf16 features (no network).
+The timed region is ONE WHOLE ``KMeans(k=256, maxIter=steps, tol=0, seed=42).fit(df)`` through the
+public pyspark.ml-compatible Estimator API (ml/clustering.py; the reference's ``lr.fit(train_data)``
+contract, ref.py:147) on a frame of this rank's HBM-resident shard (``createDataFrameFromTensors``) —
+the metric SURVEY.md §6 / BASELINE.md define (samples/s = N_rows x Lloyd iterations / fit wall time):
+engine construction (device layout + row norms), k-means|| initialisation (initSteps=2, as Spark's
+KMeans.fit runs it), ``steps`` Lloyd iterations and the model + summary (trainingCost; clusterSizes is
+lazy, as Spark's). A step = one distributed Lloyd iteration: exact bound-pruned K9r MFMA assign, K10
+incremental f64 sums, RCCL all-reduce of the [k·D sums | k counts | cost] message, K11 update.
+--warmup runs an untimed warm-up fit of that many iterations first. The same fit driven on the
+LloydEngine directly, the steady-state step and a forced full step are reported in extra (not the
+headline), and with --data blobs (the headline) also a fit on overlapping blobs (extra.overlap), where
+the bounds prune little. The dataset is fixed (100M rows total) and sharded over the N ranks, so
+scaling is *strong*. Data: synthetic Gaussian blobs generated on the GPU, bf16 features (no network).
 
 Usage (driver contract):
     python bench.py --gpus 1 --steps 20 --warmup 3
@@ -34,15 +37,23 @@ from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm im
 METRIC = "KMeans fit samples/sec (whole node), 100M×256 k=256 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
 
+# --data: centre spread of the Gaussian blobs (unit noise); "uniform" has no cluster structure
+_DATA = {"blobs": 4.0, "overlap": 0.5, "uniform": None}
 
-def make_blobs(n: int, d: int, k_true: int, seed: int, device, dtype=torch.bfloat16, chunk: int = 1 << 22):
+
+def make_blobs(n: int, d: int, k_true: int, seed: int, device, dtype=torch.bfloat16, chunk: int = 1 << 22,
+               spread=4.0):
+    """n rows of k_true Gaussian blobs (centres randn·spread, unit noise), or U(-2, 2) rows (spread None)."""
     g = torch.Generator(device=device)
     g.manual_seed(1234)  # identical blob centres on every rank
-    centers = torch.randn((k_true, d), generator=g, device=device) * 4.0
+    centers = torch.randn((k_true, d), generator=g, device=device) * (spread or 0.0)
     g.manual_seed(seed)
     x = torch.empty((n, d), dtype=dtype, device=device)
     for s in range(0, n, chunk):
         m = min(chunk, n - s)
+        if spread is None:
+            x[s:s + m] = (torch.rand((m, d), generator=g, device=device) * 4.0 - 2.0).to(dtype)
+            continue
         lab = torch.randint(0, k_true, (m,), generator=g, device=device)
         x[s:s + m] = (centers[lab] + torch.randn((m, d), generator=g, device=device)).to(dtype)
     return x
@@ -56,9 +67,9 @@ def _drop_norm_cache(x: torch.Tensor) -> None:
 
 
 def kmeans_fit(x, args, comm, seed: int = 42, iters: int = 20, breakdown: bool = False):
-    """One whole KMeans fit, as ``KMeans(k, maxIter=iters, tol=0).fit`` runs it (ml/clustering.py):
-    engine construction (device layout, row norms), k-means|| init (initSteps=2) and ``iters``
-    Lloyd iterations. Returns (engine, init seconds, per-iteration seconds or None)."""
+    """One whole KMeans fit on the LloydEngine directly (what ``KMeans.fit`` drives): engine
+    construction (device layout, row norms), k-means|| init (initSteps=2) and ``iters`` Lloyd
+    iterations. Returns (engine, init seconds, per-iteration seconds or None)."""
     gpu = x.is_cuda
     eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks,
                       incremental=not args.full_accumulate, prune=args.prune)
@@ -79,22 +90,48 @@ def kmeans_fit(x, args, comm, seed: int = 42, iters: int = 20, breakdown: bool =
     return eng, t_init, per
 
 
+def api_fit(df, args, seed: int, iters: int):
+    """The public Estimator fit: ``KMeans(k, maxIter=iters, tol, seed).fit(df)``."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+    km = KMeans(k=args.k, maxIter=iters, tol=args.tol, seed=seed, initMode=args.init,
+                featuresCol="features")
+    return km.fit(df)
+
+
+def _timed(comm, gpu, fn):
+    """Run fn bracketed by barrier + device sync on both sides; (result, max seconds over ranks)."""
+    comm.barrier()
+    if gpu:
+        torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    out = fn()
+    if gpu:
+        torch.cuda.synchronize()
+    comm.barrier()
+    return out, comm.max_scalar(time.perf_counter() - t0)
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
-    ap.add_argument("--steps", type=int, default=20, help="Lloyd iterations of the timed fit")
+    ap.add_argument("--steps", type=int, default=20, help="Lloyd iterations of the timed fit (maxIter)")
     ap.add_argument("--warmup", type=int, default=3, help="Lloyd iterations of the untimed warm-up fit")
     ap.add_argument("--rows", type=int, default=100_000_000, help="total rows (strong scaling)")
     ap.add_argument("--dim", type=int, default=256)
     ap.add_argument("--k", type=int, default=256)
+    ap.add_argument("--tol", type=float, default=0.0, help="KMeans tol of the timed fit (headline: 0)")
+    ap.add_argument("--data", default="blobs", choices=sorted(_DATA),
+                    help="blobs = the headline data (separated blobs); overlap = blob centres 8x closer; "
+                         "uniform = no cluster structure")
+    ap.add_argument("--no-overlap", action="store_true", help="skip the extra overlap-data fit")
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
     ap.add_argument("--prune", default=None, choices=["on", "off"],
-                    help="force the exact bound-pruned Lloyd step on or off (default: what KMeans.fit uses)")
+                    help="engine measurements: force the exact bound-pruned Lloyd step on or off")
     ap.add_argument("--full-accumulate", action="store_true",
-                    help="re-accumulate every row each step instead of the exact incremental sums")
+                    help="engine measurements: re-accumulate every row each step instead of the exact incremental sums")
     ap.add_argument("--breakdown", action="store_true",
-                    help="also run one fit with a device sync after every iteration and report per-iteration "
+                    help="also run one engine fit with a device sync after every iteration and report per-iteration "
                          "times (extra.breakdown); the headline fit is never synchronised inside")
     ap.add_argument("--workload", default="kmeans", choices=["kmeans", "logreg", "pipeline", "csv", "kmeans_ooc"],
                     help="kmeans = the BASELINE headline; logreg = BASELINE config 4 (StandardScaler + "
@@ -120,6 +157,7 @@ def main():
     if args.workload == "kmeans_ooc":
         return bench_kmeans_ooc(args)
 
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
     world = int(os.environ.get("WORLD_SIZE", "1"))
     if world != args.gpus and world != 1:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}", file=sys.stderr)
@@ -127,7 +165,9 @@ def main():
     if not gpu:
         # CPU plumbing run only (no MI355X here): shrink so it finishes.
         args.rows, args.dim, args.k = min(args.rows, 200_000), min(args.dim, 32), min(args.k, 16)
-    comm = Communicator.from_env(want_gpu=gpu)
+    spark = (SparkSession.builder.appName("bench-kmeans").master("mi355x" if gpu else "local[1]")
+             .config("cml.ml.features.dtype", "bf16" if gpu else "float64").getOrCreate())
+    comm = spark._comm
     rank, W = comm.rank, comm.world_size
     dev = comm.device
 
@@ -135,71 +175,38 @@ def main():
     n_local = per + (1 if rank < args.rows - per * W else 0)
     t0 = time.perf_counter()
     x = make_blobs(n_local, args.dim, args.k, seed=1000 + rank, device=dev,
-                   dtype=torch.bfloat16 if gpu else torch.float64)
+                   dtype=torch.bfloat16 if gpu else torch.float64, spread=_DATA[args.data])
     if gpu:
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
+    df = spark.createDataFrameFromTensors({"features": x})
 
     # untimed warm-up fit: code objects, allocator pools, RCCL channels (its results are discarded)
     if args.warmup > 0:
-        eng, _, _ = kmeans_fit(x, args, comm, seed=7, iters=args.warmup)
-        del eng
+        api_fit(df, args, seed=7, iters=args.warmup)
         _drop_norm_cache(x)
 
-    # the timed region: one whole fit from scratch, bracketed by barrier + device sync on both sides
-    comm.barrier()
-    if gpu:
-        torch.cuda.synchronize()
-    t0 = time.perf_counter()
-    eng, t_init, _ = kmeans_fit(x, args, comm, seed=42, iters=args.steps)
-    if gpu:
-        torch.cuda.synchronize()
-    comm.barrier()
-    t1 = time.perf_counter()
-    elapsed = comm.max_scalar(t1 - t0)
-    init_s = comm.max_scalar(t_init - t0)
-    cost = eng.training_cost()
-    acc = {"accumulate": "incremental (exact)" if eng.delta is not None else "full",
-           "assign": "pruned (exact bounds)" if eng.prune else "full (every row x every centre)"}
+    # the timed region: one whole public-API fit from scratch, bracketed by barrier + device sync
+    model, elapsed = _timed(comm, gpu, lambda: api_fit(df, args, seed=42, iters=args.steps))
+    summ = model.summary
+    acc = {"api": f"KMeans(k={args.k}, maxIter={args.steps}, tol={args.tol:g}, seed=42).fit(df)",
+           "iterations": summ.numIter, "training_cost": summ.trainingCost}
+    del model, summ
+    _drop_norm_cache(x)
+
+    # the same fit on the engine directly (no Estimator layer), then its steady-state and full steps
+    (eng, t_init), eng_s = _timed(comm, gpu, lambda: kmeans_fit(x, args, comm, seed=42, iters=args.steps)[:2])
+    acc["engine_fit_ms"] = round(1000.0 * eng_s, 3)
+    acc["api_over_engine"] = round(elapsed / eng_s, 4) if eng_s > 0 else None
+    acc["accumulate"] = "incremental (exact)" if eng.delta is not None else "full"
+    acc["assign"] = "pruned (exact bounds)" if eng.prune else "full (every row x every centre)"
     if eng.prune:
         acc["last_step_prune_rank0"] = eng.prune_stats()
     if gpu:
-        # steady-state rate of the same step after the timed fit (not part of the headline)
-        comm.barrier()
-        torch.cuda.synchronize()
-        ts = time.perf_counter()
-        for _ in range(5):
-            eng.step()
-        torch.cuda.synchronize()
-        comm.barrier()
-        acc["steady_state_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 5
-        if eng._pdev:
-            # a forced full step (bounds invalid): K9r over every row with top-2 bounds + the full
-            # counting-sort f64 accumulate (what a fit pays when most rows move)
-            comm.barrier()
-            torch.cuda.synchronize()
-            ts = time.perf_counter()
-            for _ in range(3):
-                eng._pst.force.fill_(1)
-                eng.delta.invalidate()
-                eng.step()
-            torch.cuda.synchronize()
-            comm.barrier()
-            acc["full_step_ms"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
-        if eng.delta is not None and not eng.prune:
-            acc["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
-            comm.barrier()
-            torch.cuda.synchronize()
-            ts = time.perf_counter()
-            for _ in range(3):
-                eng.delta.invalidate()
-                eng.step()
-            torch.cuda.synchronize()
-            comm.barrier()
-            acc["full_accumulate_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
+        acc.update(_step_rates(eng, comm))
     del eng
+    _drop_norm_cache(x)
     if args.breakdown:
-        _drop_norm_cache(x)
         comm.barrier()
         tb = time.perf_counter()
         eng, tbi, per_it = kmeans_fit(x, args, comm, seed=42, iters=args.steps, breakdown=True)
@@ -210,12 +217,31 @@ def main():
         # pruned k-means|| rounds: (rows, rows with a few relevant candidates, rows sent to the K9r pass)
         acc["breakdown"]["init_pruned_rounds_rank0"] = getattr(eng, "_init_prune_history", None)
         del eng
+        _drop_norm_cache(x)
+
+    if gpu and args.data == "blobs" and not args.no_overlap:
+        # the same public-API fit on overlapping blobs (centres 8x closer), where the exact bounds prune
+        # little: the robustness of the headline. Same shape, separate data.
+        del df
+        x2 = make_blobs(n_local, args.dim, args.k, seed=2000 + rank, device=dev, spread=_DATA["overlap"])
+        df2 = spark.createDataFrameFromTensors({"features": x2})
+        api_fit(df2, args, seed=7, iters=max(1, args.warmup))
+        _drop_norm_cache(x2)
+        m2, el2 = _timed(comm, gpu, lambda: api_fit(df2, args, seed=42, iters=args.steps))
+        ov = {"fit_ms": round(1000.0 * el2, 3), "samples_per_s": args.rows * args.steps / el2,
+              "iterations": m2.summary.numIter}
+        del m2
+        _drop_norm_cache(x2)
+        e2, _, _ = kmeans_fit(x2, args, comm, seed=42, iters=args.steps)
+        ov.update(_step_rates(e2, comm))
+        del e2, df2, x2
+        acc["overlap"] = ov
 
     total_rows = args.rows
     value = total_rows * args.steps / elapsed
-    headline = (args.rows, args.dim, args.k) == (100_000_000, 256, 256)
+    headline = (args.rows, args.dim, args.k, args.data) == (100_000_000, 256, 256, "blobs")
     metric = METRIC if headline else (f"KMeans fit samples/sec (whole node), {args.rows / 1e6:g}M×{args.dim} "
-                                      f"k={args.k}")
+                                      f"k={args.k}" + ("" if args.data == "blobs" else f", {args.data} data"))
     if rank == 0:
         out = {
             "metric": metric,
@@ -229,20 +255,58 @@ def main():
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
             "dtype": "bf16" if gpu else "fp64",
-            "data": "synthetic (Gaussian blobs generated on device; centres from k-means|| init inside the timed fit)",
+            "data": f"synthetic ({args.data}: generated on device; centres from k-means|| init inside the timed fit)",
             "config": {
                 "model": f"KMeans k={args.k}, {args.rows}x{args.dim}",
                 "global_batch": total_rows,
                 "seq_len": None,
                 "parallelism": f"dp{W}",
                 "k": args.k, "rows": total_rows, "dim": args.dim,
-                "timed": f"whole fit: engine + norms, k-means|| init, {args.steps} Lloyd iterations (tol=0)",
+                "timed": f"whole public-API fit: KMeans(k={args.k}, maxIter={args.steps}, tol={args.tol:g}).fit(df) "
+                         "= engine + norms, k-means|| init, Lloyd iterations, model + summary",
             },
-            "extra": {"fit_s": round(elapsed, 4), "datagen_s": round(gen_s, 3), "init_s": round(init_s, 4),
-                      "training_cost": cost, "device": torch.cuda.get_device_name(dev) if gpu else "cpu", **acc},
+            "extra": {"fit_s": round(elapsed, 4), "datagen_s": round(gen_s, 3),
+                      "device": torch.cuda.get_device_name(dev) if gpu else "cpu", **acc},
         }
         print(json.dumps(out), flush=True)
-    comm.shutdown()
+    spark.stop()
+
+
+def _step_rates(eng, comm) -> dict:
+    """Steady-state step time of a fitted engine (5 more pruned steps) and a forced full step (bounds
+    invalid: K9r over every row with top-2 bounds + the full counting-sort f64 accumulate)."""
+    out = {}
+    comm.barrier()
+    torch.cuda.synchronize()
+    ts = time.perf_counter()
+    for _ in range(5):
+        eng.step()
+    torch.cuda.synchronize()
+    comm.barrier()
+    out["steady_state_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 5
+    if eng._pdev:
+        comm.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(3):
+            eng._pst.force.fill_(1)
+            eng.delta.invalidate()
+            eng.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        out["full_step_ms"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
+    if eng.delta is not None and not eng.prune:
+        out["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
+        comm.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(3):
+            eng.delta.invalidate()
+            eng.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        out["full_accumulate_ms_per_step"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
+    return out
 
 
 def bench_logreg(args):

@@ -55,10 +55,11 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
                                                             const float* __restrict__ c0, float c0n,
                                                             float* __restrict__ cost_out, int* __restrict__ near_out,
                                                             unsigned* __restrict__ xn_max,
-                                                            int* __restrict__ erange) {
+                                                            int* __restrict__ erange, double* __restrict__ xn64) {
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int LPR = NCH / CPL;
   static_assert(LPR >= 1 && LPR <= 64 && NCH % CPL == 0, "row split");
+  const bool wide = xn64 != nullptr;
   constexpr int RPW = 64 / LPR;
   constexpr int VPC = F8 ? 16 : 8;  // values per chunk
   const int lane = threadIdx.x & 63;
@@ -89,6 +90,7 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
     for (int u = 0; u < U; ++u) {
       const long long row = r0 + (long long)u * nw * RPW + sub;
       float s = 0.f, dt = 0.f;
+      double s64 = 0.0;
 #pragma unroll
       for (int i = 0; i < CPL; ++i) {
         const unsigned w[4] = {v[u][i].x, v[u][i].y, v[u][i].z, v[u][i].w};
@@ -115,6 +117,10 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
         }
 #pragma unroll
         for (int e = 0; e < VPC; ++e) s = fmaf(xs[e], xs[e], s);
+        if (wide) {  // x² of a bf16 / e4m3 value is exact in f32; the f64 sum is exact up to its own rounding
+#pragma unroll
+          for (int e = 0; e < VPC; ++e) s64 += (double)(xs[e] * xs[e]);
+        }
         if (dot) {
 #pragma unroll
           for (int e = 0; e < VPC; ++e) dt = fmaf(xs[e], cr[i][e], dt);
@@ -124,9 +130,11 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
       for (int o = LPR / 2; o > 0; o >>= 1) {
         s += __shfl_xor(s, o, 64);
         if (dot) dt += __shfl_xor(dt, o, 64);
+        if (wide) s64 += __shfl_xor(s64, o, 64);
       }
       if (c == 0 && row < n) {
         xn_out[row] = s;
+        if (wide) xn64[row] = s64;
         mxb = __float_as_uint(s) > mxb ? __float_as_uint(s) : mxb;
         if (dot) {
           cost_out[row] = fmaxf(fmaf(-2.f, dt, s + c0n), 0.f);
@@ -622,10 +630,11 @@ inline unsigned grid_for(long long n, long long per) {
 
 // X: bf16 [n, ldx elements] (Dp = 16..512) or e4m3fn [n, ldx bytes] (Dp = 64..1024). c0/cost/near may
 // be null together (norms only); xn_max (f32 bits, zero-initialised) and erange (int[2], {INT_MAX, -1}
-// initialised) may be null.
+// initialised) may be null; xn64 (f64 [n], may be null) receives the norms summed in f64 (the per-centre
+// Σ|x|² of the training cost: the f32 norms lose ~2^-24·|x|², percents of the cost far from the origin).
 CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, float* xn,
                                 const float* c0, float c0n, float* cost, int* near, unsigned* xn_max, int* erange,
-                                void* stream) {
+                                double* xn64, void* stream) {
   if (n < 0 || ((c0 == nullptr) != (cost == nullptr)) || ((cost == nullptr) != (near == nullptr)))
     return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
@@ -638,7 +647,7 @@ CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int D
   const long long ldb = xfp8 ? ldx : 2 * ldx;
 #define CML_RP(NCH, CPL, F)                                                                                   \
   hipLaunchKernelGGL((row_pass_kernel<NCH, CPL, F, U>), dim3(grid_for(n, 4LL * (64 / ((NCH) / (CPL))) * U)), \
-                     dim3(kThreads), 0, st, x, n, ldb, xn, c0, c0n, cost, near, xn_max, erange)
+                     dim3(kThreads), 0, st, x, n, ldb, xn, c0, c0n, cost, near, xn_max, erange, xn64)
   switch ((int)(rowb / 16) * (xfp8 ? -1 : 1)) {
     case 2: CML_RP(2, 2, false); break;        // bf16 Dp = 16
     case 4: CML_RP(4, 4, false); break;        // 32

@@ -65,7 +65,9 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
                                                                        float* __restrict__ cand_xn,
                                                                        const int* __restrict__ skip,
                                                                        long long cap, const float* __restrict__ cum) {
-  if (skip != nullptr && *skip != 0) return;  // bounds invalid this step (full pass instead)
+  // skip = the step's flags {force, done}: bounds invalid this step (full pass instead), or the fit has
+  // converged and the step is a frozen no-op (kmeans_prune_gate_kernel)
+  if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) return;
   extern __shared__ __align__(16) unsigned char smem[];
   const float c2 = *c2p;
   float* sd = reinterpret_cast<float*>(smem);  // [k] drift
@@ -179,13 +181,45 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   }
 }
 
-// Pruned-step mode: full pass (1) when the bounds are invalid (*force) or more than cap rows are
-// candidates, else the candidate pass (0); mode[1] keeps the candidate count. One thread.
-__global__ void kmeans_prune_gate_kernel(const int* __restrict__ count, long long cap, const int* __restrict__ force,
+// Pruned-step mode: full pass (1) when the bounds are invalid (flags[0], force) or more than cap rows
+// are candidates, else the candidate pass (0); mode[1] keeps the candidate count. flags[1] (done) set by
+// kmeans_converge_latch_kernel once every centre moved <= tol: the step is frozen — candidate pass over
+// 0 rows, so no label changes, the sums and therefore the centres stay bit for bit — which lets the host
+// enqueue steps ahead and read the convergence flag lagged (no per-step host sync). One thread.
+__global__ void kmeans_prune_gate_kernel(int* __restrict__ count, long long cap, const int* __restrict__ flags,
                                          int* __restrict__ mode) {
-  const int full = (*force != 0 || (long long)*count > cap) ? 1 : 0;
+  if (flags[1] != 0) {
+    mode[0] = 0;
+    mode[1] = 0;
+    *count = 0;
+    return;
+  }
+  const int full = (flags[0] != 0 || (long long)*count > cap) ? 1 : 0;
   mode[0] = full;
   mode[1] = full ? 0 : *count;  // re-assigned rows of a candidate pass (stats; count is reset later)
+}
+
+// done |= (every shift2[j] <= lim): Spark's convergence rule (all centres moved at most tol), decided
+// on the device and latched. One workgroup.
+__global__ __launch_bounds__(256) void kmeans_converge_latch_kernel(const double* __restrict__ shift2, int k,
+                                                                     double lim, int* __restrict__ flags) {
+  __shared__ int any_moved;
+  if (threadIdx.x == 0) any_moved = 0;
+  __syncthreads();
+  int moved = 0;
+  for (int j = threadIdx.x; j < k; j += 256) moved |= !(shift2[j] <= lim);  // NaN counts as moved
+  if (moved) any_moved = 1;
+  __syncthreads();
+  if (threadIdx.x == 0 && !any_moved) flags[1] = 1;
+}
+
+// dst <- src (n 32-bit words) unless flags[1] (done) is set: the centres of the last live step's
+// assignment survive the frozen steps (training cost).
+__global__ __launch_bounds__(256) void kmeans_cond_copy_kernel(unsigned* __restrict__ dst,
+                                                               const unsigned* __restrict__ src, long long n,
+                                                               const int* __restrict__ flags) {
+  if (flags[1] != 0) return;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) dst[i] = src[i];
 }
 
 // Centre statistics of the pruned step, part 1 (one workgroup per centre j, over the bf16 centres
@@ -424,8 +458,27 @@ CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const 
   return cml_status();
 }
 
-CML_API int cml_kmeans_prune_gate(const int* count, long long cap, const int* force, int* mode, void* stream) {
-  hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, cap, force, mode);
+// flags: int[2] {force, done} (see kmeans_prune_gate_kernel).
+CML_API int cml_kmeans_prune_gate(int* count, long long cap, const int* flags, int* mode, void* stream) {
+  hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, cap, flags, mode);
+  return cml_status();
+}
+
+CML_API int cml_kmeans_converge_latch(const double* shift2, int k, double lim, int* flags, void* stream) {
+  if (k <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_converge_latch_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, shift2, k, lim, flags);
+  return cml_status();
+}
+
+// n_bytes a multiple of 4, both pointers 4-byte aligned.
+CML_API int cml_kmeans_cond_copy(void* dst, const void* src, long long n_bytes, const int* flags, void* stream) {
+  if (n_bytes % 4 != 0 || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3)) return (int)hipErrorInvalidValue;
+  const long long n = n_bytes / 4;
+  if (n == 0) return 0;
+  long long g = (n + 255) / 256;
+  g = g > 1024 ? 1024 : g;
+  hipLaunchKernelGGL(kmeans_cond_copy_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst,
+                     (const unsigned*)src, n, flags);
   return cml_status();
 }
 

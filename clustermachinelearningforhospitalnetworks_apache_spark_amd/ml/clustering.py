@@ -86,9 +86,9 @@ class KMeans(Estimator):
                           precision=precision, weights=weights, refresh_interval=refresh, device=dev)
         ckdir = conf.get("cml.ml.checkpointDir", None)
         every = int(conf.get("cml.ml.checkpointInterval", 10))
-        n_global = int(comm.sum_scalar(float(eng.n)))
         ckname = ckkey = None
         if ckdir:
+            n_global = int(comm.sum_scalar(float(eng.n)))
             # the key identifies the fit (shape, params and a data fingerprint), and the checkpoint name
             # is derived from it: a restarted process, whose estimator has a new uid, finds it again
             fp = _fingerprint(x, comm)
@@ -123,19 +123,18 @@ class KMeans(Estimator):
             if ckdir and (it % max(every, 1) == 0):
                 ckpt.save(ckdir, ckname, ckkey, it, {"centers": eng.centers.cpu().numpy()}, comm)
 
-        iters = eng.fit(self.getMaxIter(), self.getTol(), start_iter=start, on_iter=on_iter)
+        # without checkpoints a tol > 0 fit reads its convergence flag lagged (models/kmeans.py _fit_lagged)
+        iters = eng.fit(self.getMaxIter(), self.getTol(), start_iter=start, on_iter=on_iter if ckdir else None)
         if ckdir:
             comm.barrier()
             ckpt.clear(ckdir, ckname, comm)
         centers = eng.centers.cpu().numpy()
-        labels, dist = eng.assign()
-        sizes = torch.bincount(labels.long(), minlength=eng.k).to(torch.float64) if eng.n else torch.zeros(
-            eng.k, dtype=torch.float64, device=x.device)
-        comm.allreduce_(sizes)
         model = KMeansModel(centers)
         self._copyValues(model)
-        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(),
-                                            [int(s) for s in sizes.cpu().tolist()]))
+        # trainingCost is the last iteration's cost (Spark computes it while training: here from the f64
+        # sums and norms the engine holds, no pass over X); clusterSizes is lazy as in Spark's
+        # ClusteringSummary — counted on first read from one pruned assign against the final centres
+        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(), eng.cluster_sizes))
         return model
 
 
@@ -258,15 +257,25 @@ class KMeansModel(Model):
 
 
 class KMeansSummary:
+    """Spark's KMeansSummary. ``clusterSizes`` may be given as a zero-argument callable: it is then
+    evaluated on first read (Spark's lazy val) — a collective on a multi-rank session, so every rank
+    reads it (SPMD), as every rank calls ``fit``."""
+
     def __init__(self, model, df, k, num_iter, cost, sizes):
         self._model = model
         self._df = df
         self.k = k
         self.numIter = num_iter
         self.trainingCost = cost
-        self.clusterSizes = sizes
+        self._sizes = sizes
         self.featuresCol = model.getFeaturesCol()
         self.predictionCol = model.getPredictionCol()
+
+    @property
+    def clusterSizes(self) -> List[int]:
+        if callable(self._sizes):
+            self._sizes = list(self._sizes())
+        return self._sizes
 
     @property
     def predictions(self):

@@ -145,11 +145,12 @@ def cached_row_sqnorm(x: torch.Tensor, n: int, dp: int) -> torch.Tensor:
     if ent is not None and ent[0] == x._version and ent[1] == (n, dp):
         return ent[2]
     xn = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
+    xn64 = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
     er = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device=x.device)
     if n:
-        K.row_pass(x, n, dp, xn, erange=er)
+        K.row_pass(x, n, dp, xn, erange=er, xn64=xn64)
     try:
-        x._cml_xnorm = (x._version, (n, dp), xn, er)
+        x._cml_xnorm = (x._version, (n, dp), xn, er, xn64)
     except (AttributeError, RuntimeError):
         pass
     return xn
@@ -284,6 +285,7 @@ class LloydEngine:
         self._cost_fn = None
         self.last_cost = None
         self._shift2 = None
+        self._conv_lim = None  # squared-move limit of a tol > 0 fit's device convergence latch (_fit_lagged)
         self.delta = None  # incremental-sums state (GPU sort regime), see _alloc_gpu
         self._pst = None  # pruned-step state, see _step_prune
         # sum grid of the device sort-regime accumulates (_sum_grid): qscale 0 / unit 1 = plain f64 sums
@@ -318,11 +320,14 @@ class LloydEngine:
         # first pass over X
         ent = getattr(self.x, "_cml_xnorm", None)
         self._erange = None  # bf16 exponent range of X (exactness of the f64 sums), from the row pass
+        self._xnorm64 = None  # ||x||² summed in f64 (training cost), from the same pass
         if ent is not None and ent[0] == self.x._version and ent[1] == (n, dp):
             self._xnorm, self._norms_ready = ent[2], True
             self._erange = ent[3] if len(ent) > 3 else None
+            self._xnorm64 = ent[4] if len(ent) > 4 else None
         else:
             self._xnorm, self._norms_ready = torch.empty(max(n, 1), dtype=torch.float32, device=dev), False
+            self._xnorm64 = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
         self.cost_part = torch.zeros(self.aplan.grid, dtype=torch.float64, device=dev)
         if self.cplan.mode == "priv":
             self.slab = torch.empty(self.cplan.nsl * self.cplan.gx * k * self.cplan.dw, dtype=torch.float32,
@@ -371,15 +376,18 @@ class LloydEngine:
         mxv = self._pst.mx if self._pdev else None
         if mxv is not None:
             mxv.zero_()
+        if self._xnorm64 is None:
+            self._xnorm64 = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
         if n:
             for _, r0, r1, xc in self._x_chunks(whole=True):
                 K.row_pass(xc, r1 - r0, dp, self._xnorm[r0:r1], c0, c0n, None if cost is None else cost[r0:r1],
-                           None if near is None else near[r0:r1], xn_max=mxv, erange=self._erange)
+                           None if near is None else near[r0:r1], xn_max=mxv, erange=self._erange,
+                           xn64=self._xnorm64[r0:r1])
         if mxv is not None and self.comm.is_distributed:
             self.comm.allreduce_(mxv, op="max")
         self._norms_ready = True
         try:
-            self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm, self._erange)
+            self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm, self._erange, self._xnorm64)
         except (AttributeError, RuntimeError):
             pass
 
@@ -542,7 +550,7 @@ class LloydEngine:
             self._graph[1].replay()
         else:
             self._graph.replay()
-        self._cost_fn = self._exact_cost
+        self._cost_fn = self._device_cost if self.cplan.mode != "priv" else self._exact_cost
 
     def _best(self, r0: int, r1: int):
         return None if self.best is None else self.best[r0:r1]
@@ -583,10 +591,13 @@ class LloydEngine:
             handles.append(self.comm.allreduce_async(msg))
         for h in handles:
             h.wait()
-        if self._hs is None:
-            # the exact cost of this assignment is evaluated on first read (_exact_cost) against a copy of
-            # the centres it was made with; streamed rows keep the assign's per-row f32 distances
-            self._cb_cost.copy_(self.cb)
+        # the cost of this assignment is evaluated on first read against a copy of the centres it was made
+        # with: from the exact f64 sums (_device_cost), or — the private-LDS regime sums in f32 — by the
+        # exact cost pass (resident rows) / the assign's per-row distances (streamed rows)
+        self._cb_cost.copy_(self.cb)
+        if self.cplan.mode != "priv":
+            self._cost_fn = self._device_cost
+        elif self._hs is None:
             self._cost_fn = self._exact_cost
         else:
             self.last_cost = self.msgs[:, -1].sum()
@@ -652,7 +663,10 @@ class LloydEngine:
         st.cand_xn = torch.zeros(pad, dtype=torch.float32, device=dev)
         st.count = torch.zeros(1, dtype=torch.int32, device=dev)
         st.pmode = torch.zeros(2, dtype=torch.int32, device=dev)  # [full pass?, re-assigned rows]
-        st.force = torch.ones(1, dtype=torch.int32, device=dev)
+        # step flags [force, done]: force = bounds invalid (a full pass next); done = converged (tol > 0
+        # fits, _fit_lagged): every later step is a frozen no-op until the host reads the flag
+        st.flags = torch.tensor([1, 0], dtype=torch.int32, device=dev)
+        st.force, st.done = st.flags[0:1], st.flags[1:2]
         st.ub = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         st.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         st.drift = torch.zeros(k, dtype=torch.float32, device=dev)
@@ -664,6 +678,7 @@ class LloydEngine:
         st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
         st.mx = torch.zeros(1, dtype=torch.float32, device=dev)  # max ||x||² over all ranks (_ensure_norms)
         st.cb_old = torch.zeros_like(self.cb)
+        st.cb_cost = torch.zeros_like(self.cb)  # centres of the last live step's assignment (training cost)
         # offset-form bounds (kmeans_prune.hip bound_lazy): ub/lb hold ub - cu[label] / lb + cl[label]
         # against these cumulative drifts [cu | cl], so the bounds pass only reads the rows whose label
         # holds; CML_KMEANS_LAZY_BOUNDS=0 keeps the absolute bounds rewritten every step
@@ -694,9 +709,9 @@ class LloydEngine:
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
         K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
-                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.force, zero_count=False,
+                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
                        cum=st.cum) if n else None
-        K.prune_gate(st.count, st.cap_m, st.force, st.pmode)
+        K.prune_gate(st.count, st.cap_m, st.flags, st.pmode)
         K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
                         st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
@@ -708,13 +723,17 @@ class LloydEngine:
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
 
     def _pdev_post(self) -> None:
-        """The device pruned step after its all-reduce: K11 and the centre statistics of the next bounds."""
+        """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
+        in a tol > 0 fit, the device convergence latch (flags[1])."""
         st, k, d = self._pst, self.k, self.d
         st.cb_old.copy_(self.cb)
+        K.cond_copy(st.cb_cost, st.cb_old, st.flags)  # frozen steps keep the last live step's centres
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
                        st.c2, st.count, st.force, cum=st.cum)
-        self._cost_fn = self._exact_cost
+        if self._conv_lim is not None:
+            K.converge_latch(self.shift2, k, self._conv_lim, st.flags)
+        self._cost_fn = self._device_cost
 
     def _seed_from_init(self, sd) -> None:
         """Labels and bounds of every row from the k-means|| init (kmeans_seed_bounds): row x's nearest
@@ -780,11 +799,42 @@ class LloydEngine:
                           qscale=self._qscale, cum=st.cum)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
         self.comm.allreduce_async(msg).wait()
-        st.cb_old.copy_(self.cb)
-        self._update_gpu(self.msgs)
-        K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
-                       st.c2, st.count, st.force, cum=st.cum)
-        self._cost_fn = self._exact_cost
+        self._pdev_post()
+
+    def _norms64(self) -> torch.Tensor:
+        """||x||² of the device rows summed in f64 (from the row pass; one more pass over X only when the
+        f32 norms came from a cache that did not keep them)."""
+        self._ensure_norms()
+        if self._xnorm64 is None:
+            self._xnorm64 = torch.empty(max(self.n, 1), dtype=torch.float64, device=self.device)
+            if self.n:
+                tmp = torch.empty(self.n, dtype=torch.float32, device=self.device)
+                for _, r0, r1, xc in self._x_chunks(whole=True):
+                    K.row_pass(xc, r1 - r0, self.dp, tmp[r0:r1], xn64=self._xnorm64[r0:r1])
+        return self._xnorm64
+
+    def _device_cost(self) -> torch.Tensor:
+        """Cost of the last step's assignment (Spark's per-iteration trainingCost) from what the step
+        already holds: Σ_j (Q_j - 2 c_j·S_j + n_j|c_j|²) with S/n the all-reduced f64 sums of that
+        assignment, c_j the bf16 centres it compared against (the pruned step's cb_old, else the copy
+        _step_gpu keeps) and Q_j = Σ_{i in j} ||x_i||² from the row pass's f64 norms (one deterministic
+        group-sum over the labels, all-reduced) — ~1e-11 relative even far from the origin, where the
+        f32 norms lost percents, and no pass over X. Collective: every rank reads
+        it together. (With the sum grid active — _sum_grid — S holds the gridded values, and the cost
+        is that of the values the centres were computed from.)"""
+        k, d, n, kd = self.k, self.d, self.n, self.k * self.d
+        cb = self._pst.cb_cost if self._pdev else self._cb_cost
+        if n:
+            q = group_reduce(self.labels[:n], self._norms64()[:n], k, "sum").to(torch.float64).contiguous()
+        else:
+            q = torch.zeros(k, dtype=torch.float64, device=self.device)
+        self.comm.allreduce_(q)
+        m = self.msgs
+        s_ = (m[0, :kd] if m.shape[0] == 1 else m[:, :kd].sum(0)).view(k, d) * self._unit
+        cnt = m[0, kd:kd + k] if m.shape[0] == 1 else m[:, kd:kd + k].sum(0)
+        c = cb[:k, :d].to(torch.float64)
+        cost = q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()
+        return cost.clamp(min=0.0)
 
     def _exact_cost(self) -> torch.Tensor:
         """Cost of the last step's assignment (Spark's per-iteration cost) on the device rows: one exact
@@ -1080,6 +1130,8 @@ class LloydEngine:
     def fit(self, max_iter: int, tol: float, start_iter: int = 0, on_iter=None) -> int:
         """Lloyd iterations until every centre moves <= tol or max_iter. ``start_iter`` resumes a
         checkpointed fit; ``on_iter(it)`` runs after each iteration (checkpoint hook)."""
+        if tol > 0 and self._pdev and on_iter is None and os.environ.get("CML_KMEANS_LAGGED_TOL", "1") != "0":
+            return self._fit_lagged(max_iter, tol, start_iter)
         it = start_iter
         while it < max_iter:
             maybe_fail("kmeans.iteration", it)  # crash point (SURVEY.md §5.3 "mid-iteration k")
@@ -1092,7 +1144,84 @@ class LloydEngine:
                 break
         return it
 
+    def _fit_lagged(self, max_iter: int, tol: float, start_iter: int = 0, window: int = 2) -> int:
+        """A tol > 0 fit with no per-step host synchronisation: every step latches Spark's convergence
+        test on the device (kmeans_converge_latch: all centres moved <= tol) and a converged engine's
+        later steps are frozen no-ops (kmeans_prune_gate: no row re-assigned, so sums and centres stay
+        bit for bit). The flag of each step is copied to pinned memory behind its work; the host reads
+        it ``window`` steps late (waiting only for that older step's event, so the GPU always has queued
+        work) and stops at the first converged step — the same iteration count, centres, labels and
+        cost as the synchronous loop, plus at most ``window`` frozen steps of a few small kernels."""
+        st = self._pst
+        self._conv_lim = 2.0 * tol if self.spherical else tol * tol
+        st.done.zero_()
+        total = max(0, max_iter - start_iter)
+        flags = torch.zeros(max(total, 1), dtype=torch.int32, pin_memory=True)
+        events = []
+        stop, checked, it = None, 0, start_iter
+        try:
+            while it < max_iter:
+                maybe_fail("kmeans.iteration", it)
+                with trace("kmeans.step"):
+                    self.step()
+                i = it - start_iter
+                flags[i:i + 1].copy_(st.done, non_blocking=True)
+                ev = torch.cuda.Event()
+                ev.record()
+                events.append(ev)
+                it += 1
+                while checked <= i - window:  # the step `window` back: its flag is (nearly) ready
+                    events[checked].synchronize()
+                    if int(flags[checked]) != 0:
+                        stop = start_iter + checked + 1
+                        break
+                    checked += 1
+                if stop is not None:
+                    break
+            while stop is None and checked < len(events):
+                events[checked].synchronize()
+                if int(flags[checked]) != 0:
+                    stop = start_iter + checked + 1
+                checked += 1
+        finally:
+            self._conv_lim = None
+            st.done.zero_()  # later steps of this engine (more iterations, assigns) run live again
+        return stop if stop is not None else it
+
     # ------------------------------------------------------------------ prediction / cost
+    def final_labels(self) -> torch.Tensor:
+        """Labels of every local row against the current (final) centres — what ``transform`` with the
+        fitted model predicts (Spark's summary.clusterSizes counts these). After device pruned steps this is
+        one pruned assign: the bounds pass against the last update's drifts lists the rows the bounds no
+        longer prove, and K9r re-assigns only those (the full pass when there are too many), on copies of
+        the labels and bounds — the engine's own step state is untouched. Other paths run a full assign."""
+        n, k = self.n, self.k
+        if not (self._pdev and n):
+            return self.assign()[0]
+        st, ap = self._pst, self.aplan
+        lab, ub, lb = self.labels.clone(), st.ub.clone(), st.lb.clone()
+        cand, cand_lab, cand_xn = torch.zeros_like(st.cand), torch.zeros_like(st.cand_lab), torch.zeros_like(st.cand_xn)
+        count = torch.zeros(1, dtype=torch.int32, device=self.device)
+        flags = torch.zeros(2, dtype=torch.int32, device=self.device)
+        pmode = torch.zeros(2, dtype=torch.int32, device=self.device)
+        K.prune_bounds(lab, ub, lb, st.drift, st.dmax, st.thr, st.c2, k, cand, count, xn=self.xnorm, cand_lab=cand_lab,
+                       cand_xn=cand_xn, zero_count=False, cum=st.cum)
+        K.prune_gate(count, st.cap_m, flags, pmode)
+        K.assign_rr_ext(1, self.x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, None, ub, lb, st.mc, st.tau,
+                        gate=pmode, want=1, cum=st.cum)
+        K.assign_rr_ext(2, self.x, st.cap_m, self.dp, self.cb, self.cnorm, ap, cand_xn, lab, None, ub, lb, st.mc,
+                        st.tau, idx=cand, n_dev=count, lab_in=cand_lab, gate=pmode, want=0, cum=st.cum)
+        return lab[:n]
+
+    def cluster_sizes(self) -> List[int]:
+        """Global row count of every cluster under the final centres (a collective)."""
+        if self.n:
+            sizes = torch.bincount(self.final_labels().long(), minlength=self.k).to(torch.float64)
+        else:
+            sizes = torch.zeros(self.k, dtype=torch.float64, device=self.device)
+        self.comm.allreduce_(sizes)
+        return [int(v) for v in sizes.cpu().tolist()]
+
     def assign(self, centers: Optional[torch.Tensor] = None):
         """(labels, squared distance) of every local row against `centers` (default: current)."""
         if centers is not None:

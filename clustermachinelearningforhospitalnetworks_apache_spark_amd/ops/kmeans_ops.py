@@ -58,6 +58,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_converge_latch": (c_int, [c_vp, c_int, ctypes.c_double, c_vp, c_vp]),
+    "cml_kmeans_cond_copy": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
                                        c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
@@ -77,7 +79,7 @@ _native.register_kernel_sigs({
 
 _native.register_kernel_sigs({
     "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
-                                    c_vp, c_vp]),
+                                    c_vp, c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_sum_f32_f64_parts": (c_int, []),
     "cml_kmeans_cost_parts": (c_int, []),
@@ -114,14 +116,18 @@ def _u64(v: int) -> int:
 
 def row_pass(x: torch.Tensor, n: int, dp: int, xn: torch.Tensor, c0: torch.Tensor | None = None, c0n: float = 0.0,
              cost: torch.Tensor | None = None, near: torch.Tensor | None = None,
-             xn_max: torch.Tensor | None = None, erange: torch.Tensor | None = None, stream=None) -> None:
+             xn_max: torch.Tensor | None = None, erange: torch.Tensor | None = None,
+             xn64: torch.Tensor | None = None, stream=None) -> None:
     """One read of X (``kmeans_init.hip``): ``xn`` = ||x||² (bitwise ``row_sqnorm``), optionally the
     first k-means|| cost against the bf16-rounded centre ``c0`` (f32 [dp], norm ``c0n``) with
     ``near`` = 0, the max ||x||² (``xn_max``: f32 [1], zero-initialised, updated by bit-pattern
-    atomicMax) and the range of bf16 exponents (``erange``: int32 [2] = {INT_MAX, -1} initialised)."""
+    atomicMax), the range of bf16 exponents (``erange``: int32 [2] = {INT_MAX, -1} initialised) and the
+    norms summed in f64 (``xn64``: f64 [n], the training cost's per-centre Σ|x|²)."""
+    if xn64 is not None and (xn64.dtype != torch.float64 or not xn64.is_contiguous() or xn64.numel() < n):
+        raise ValueError("row_pass: xn64 must be a contiguous f64 [n] tensor")
     _native.check(_native.kernels().cml_kmeans_row_pass(
         x.data_ptr(), int(n), x.stride(0), int(dp), int(is_fp8(x)), xn.data_ptr(), _ptr(c0), float(c0n), _ptr(cost),
-        _ptr(near), _ptr(xn_max), _ptr(erange), _native.stream_ptr(stream)), "kmeans_row_pass")
+        _ptr(near), _ptr(xn_max), _ptr(erange), _ptr(xn64), _native.stream_ptr(stream)), "kmeans_row_pass")
 
 
 def sum_f64(x: torch.Tensor, n: int, stream=None) -> torch.Tensor:
@@ -613,11 +619,32 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
                   "kmeans_label_hist")
 
 
-def prune_gate(count: torch.Tensor, cap: int, force: torch.Tensor, mode: torch.Tensor, stream=None) -> None:
-    """mode[0] = 1 (full pass) when force[0] or count[0] > cap, else 0 (candidate pass). Device only."""
-    _native.check(_native.kernels().cml_kmeans_prune_gate(count.data_ptr(), int(cap), force.data_ptr(),
+def prune_gate(count: torch.Tensor, cap: int, flags: torch.Tensor, mode: torch.Tensor, stream=None) -> None:
+    """mode[0] = 1 (full pass) when flags[0] (force) or count[0] > cap, else 0 (candidate pass); with
+    flags[1] (done: the fit converged) a frozen step — candidate pass over 0 rows (count zeroed).
+    ``flags``: int32 [2] device tensor. Device only."""
+    if flags.dtype != torch.int32 or flags.numel() < 2:
+        raise ValueError("prune_gate: flags must be int32 [force, done]")
+    _native.check(_native.kernels().cml_kmeans_prune_gate(count.data_ptr(), int(cap), flags.data_ptr(),
                                                           mode.data_ptr(), _native.stream_ptr(stream)),
                   "kmeans_prune_gate")
+
+
+def converge_latch(shift2: torch.Tensor, k: int, lim: float, flags: torch.Tensor, stream=None) -> None:
+    """flags[1] = 1 once every shift2[j] (f64 squared centre moves) is <= lim (latched). Device only."""
+    _native.check(_native.kernels().cml_kmeans_converge_latch(shift2.data_ptr(), int(k), float(lim),
+                                                              flags.data_ptr(), _native.stream_ptr(stream)),
+                  "kmeans_converge_latch")
+
+
+def cond_copy(dst: torch.Tensor, src: torch.Tensor, flags: torch.Tensor, stream=None) -> None:
+    """dst <- src (same size, contiguous) unless flags[1] is set. Device only."""
+    if dst.numel() * dst.element_size() != src.numel() * src.element_size() or not (dst.is_contiguous() and
+                                                                                   src.is_contiguous()):
+        raise ValueError("cond_copy: contiguous tensors of the same size")
+    _native.check(_native.kernels().cml_kmeans_cond_copy(dst.data_ptr(), src.data_ptr(),
+                                                         dst.numel() * dst.element_size(), flags.data_ptr(),
+                                                         _native.stream_ptr(stream)), "kmeans_cond_copy")
 
 
 def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, mx: torch.Tensor, tau: float,
