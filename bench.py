@@ -74,7 +74,8 @@ def kmeans_fit(x, args, comm, seed: int = 42, iters: int = 20, breakdown: bool =
     eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks,
                       incremental=not args.full_accumulate, prune=args.prune)
     eng.track_prune = breakdown
-    init = eng.init_kmeans_parallel(seed=seed) if args.init == "k-means||" else eng.init_random(seed=seed)
+    init = (eng.init_kmeans_parallel(seed=seed, as_device=True) if args.init == "k-means||"
+            else eng.init_random(seed=seed))
     eng.set_centers(init)
     if gpu and breakdown:
         torch.cuda.synchronize()

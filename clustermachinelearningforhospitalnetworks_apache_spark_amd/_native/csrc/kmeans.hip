@@ -1779,16 +1779,16 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
 // the cached norms.
 extern "C" int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, float* xn,
                                    const float* c0, float c0n, float* cost, int* near, unsigned* xn_max,
-                                   int* erange, double* xn64, void* stream);
+                                   int* erange, double* xn64, const float* c0n_dev, void* stream);
 
 CML_API int cml_row_sqnorm_fp8(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
   return cml_kmeans_row_pass(X, n, ldx, Dp, 1, out, nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr,
-                             stream);
+                             nullptr, stream);
 }
 
 CML_API int cml_row_sqnorm_bf16(const void* X, long long n, long long ldx, int Dp, float* out, void* stream) {
   return cml_kmeans_row_pass(X, n, ldx, Dp, 0, out, nullptr, 0.f, nullptr, nullptr, nullptr, nullptr, nullptr,
-                             stream);
+                             nullptr, stream);
 }
 
 // Regime A. rpw rows per wave-instruction, private copies; dw <= cpl*64/rpw.

@@ -55,8 +55,10 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
                                                             const float* __restrict__ c0, float c0n,
                                                             float* __restrict__ cost_out, int* __restrict__ near_out,
                                                             unsigned* __restrict__ xn_max,
-                                                            int* __restrict__ erange, double* __restrict__ xn64) {
+                                                            int* __restrict__ erange, double* __restrict__ xn64,
+                                                            const float* __restrict__ c0n_dev) {
   typedef float f2 __attribute__((ext_vector_type(2)));
+  if (c0n_dev != nullptr) c0n = *c0n_dev;  // ||c0||² left on the device by the centre conversion
   constexpr int LPR = NCH / CPL;
   static_assert(LPR >= 1 && LPR <= 64 && NCH % CPL == 0, "row split");
   const bool wide = xn64 != nullptr;
@@ -268,7 +270,10 @@ __global__ __launch_bounds__(kThreads) void init_sample_kernel(const float* __re
                                                                const long long* __restrict__ ids, long long n,
                                                                unsigned long long key, double scale,
                                                                int* __restrict__ out, int* __restrict__ count,
-                                                               long long cap) {
+                                                               long long cap, const double* __restrict__ scale_dev) {
+  // scale_dev (may be null): {Σ cost over every rank, 2k}: the round's rate 2k / Σcost formed on the
+  // device (no host read of the all-reduced total); Σcost = 0 draws nothing (inf·0 compares false)
+  if (scale_dev != nullptr) scale = scale_dev[1] / scale_dev[0];
   const int lane = threadIdx.x & 63;
   for (long long i0 = (long long)blockIdx.x * blockDim.x; i0 < n; i0 += (long long)gridDim.x * blockDim.x) {
     const long long i = i0 + threadIdx.x;
@@ -468,7 +473,9 @@ __global__ __launch_bounds__(kThreads) void local_pairdist_kernel(const double* 
 // One workgroup per point; centres read transposed (CT[t*k + j]) so a wave's reads are contiguous.
 __global__ __launch_bounds__(kThreads) void local_assign_kernel(const double* __restrict__ P, int m, int d,
                                                                 const double* __restrict__ CT, int k,
-                                                                int* __restrict__ labels, int* __restrict__ moved) {
+                                                                int* __restrict__ labels, int* __restrict__ moved,
+                                                                const int* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;  // converged earlier: a queued iteration is a no-op
   extern __shared__ __align__(16) unsigned char smem[];
   double* prow = reinterpret_cast<double*>(smem);
   __shared__ double bd[kThreads];
@@ -509,7 +516,19 @@ __global__ __launch_bounds__(kThreads) void local_update_kernel(const double* __
                                                                 const double* __restrict__ w,
                                                                 const int* __restrict__ labels, int k,
                                                                 double* __restrict__ C, double* __restrict__ CT,
-                                                                double* __restrict__ cnt, int spherical) {
+                                                                double* __restrict__ cnt, int spherical,
+                                                                int* __restrict__ flags, int slot) {
+  // flags (may be null: unconditional): {stop, moved[2]}. This iteration's assign set moved[slot] if a
+  // label changed; none changed -> converged: latch stop (this and every later queued launch is a no-op,
+  // as the host loop's break was). Block 0 clears the other slot for the next iteration's assign.
+  if (flags != nullptr) {
+    if (flags[0] != 0) return;
+    if (flags[1 + slot] == 0) {
+      if (blockIdx.x == 0 && threadIdx.x == 0) flags[0] = 1;
+      return;
+    }
+    if (blockIdx.x == 0 && threadIdx.x == 0) flags[2 - slot] = 0;
+  }
   extern __shared__ __align__(16) unsigned char smem[];
   int* lab = reinterpret_cast<int*>(smem);                          // [m]
   double* cvals = reinterpret_cast<double*>(smem + (((size_t)m * 4 + 15) & ~(size_t)15));  // [d]
@@ -558,7 +577,8 @@ __global__ __launch_bounds__(kThreads) void local_empty_kernel(const double* __r
                                                                unsigned long long key,
                                                                unsigned long long* __restrict__ ctr,
                                                                double* __restrict__ C, double* __restrict__ CT,
-                                                               int* __restrict__ picks) {
+                                                               int* __restrict__ picks, const int* __restrict__ stop) {
+  if (stop != nullptr && *stop != 0) return;
   __shared__ int nsh;
   const int tid = threadIdx.x;
   if (tid == 0) {
@@ -634,7 +654,7 @@ inline unsigned grid_for(long long n, long long per) {
 // Σ|x|² of the training cost: the f32 norms lose ~2^-24·|x|², percents of the cost far from the origin).
 CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int Dp, int xfp8, float* xn,
                                 const float* c0, float c0n, float* cost, int* near, unsigned* xn_max, int* erange,
-                                double* xn64, void* stream) {
+                                double* xn64, const float* c0n_dev, void* stream) {
   if (n < 0 || ((c0 == nullptr) != (cost == nullptr)) || ((cost == nullptr) != (near == nullptr)))
     return (int)hipErrorInvalidValue;
   if (n == 0) return 0;
@@ -647,7 +667,7 @@ CML_API int cml_kmeans_row_pass(const void* X, long long n, long long ldx, int D
   const long long ldb = xfp8 ? ldx : 2 * ldx;
 #define CML_RP(NCH, CPL, F)                                                                                   \
   hipLaunchKernelGGL((row_pass_kernel<NCH, CPL, F, U>), dim3(grid_for(n, 4LL * (64 / ((NCH) / (CPL))) * U)), \
-                     dim3(kThreads), 0, st, x, n, ldb, xn, c0, c0n, cost, near, xn_max, erange, xn64)
+                     dim3(kThreads), 0, st, x, n, ldb, xn, c0, c0n, cost, near, xn_max, erange, xn64, c0n_dev)
   switch ((int)(rowb / 16) * (xfp8 ? -1 : 1)) {
     case 2: CML_RP(2, 2, false); break;        // bf16 Dp = 16
     case 4: CML_RP(4, 4, false); break;        // 32
@@ -728,10 +748,45 @@ CML_API int cml_kmeans_init_merge(float* cost, int* near, const float* best, con
 
 // count must be zeroed by the caller; at most cap rows are written (count holds the total).
 CML_API int cml_kmeans_init_sample(const float* cost, const long long* ids, long long n, unsigned long long key,
-                                   double scale, int* out, int* count, long long cap, void* stream) {
+                                   double scale, int* out, int* count, long long cap, const double* scale_dev,
+                                   void* stream) {
   if (n <= 0) return 0;
   hipLaunchKernelGGL(init_sample_kernel, dim3(grid_for(n, kThreads * 8LL)), dim3(kThreads), 0, (hipStream_t)stream,
-                     cost, ids, n, key, scale, out, count, cap);
+                     cost, ids, n, key, scale, out, count, cap, scale_dev);
+  return cml_status();
+}
+
+// counts[v] += 1 for every v = vals[i] (0 <= v < m): int32 counts (exact in any order), per-block LDS
+// histograms for m <= 8192 merged with one integer atomic per bin and block, global atomics above.
+__global__ __launch_bounds__(kThreads) void int_hist_kernel(const int* __restrict__ vals, long long n, int m,
+                                                            int* __restrict__ counts) {
+  extern __shared__ int hist[];
+  const bool lds = m <= 8192;
+  if (lds) {
+    for (int i = threadIdx.x; i < m; i += kThreads) hist[i] = 0;
+    __syncthreads();
+  }
+  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
+    const int v = vals[i];
+    if (v >= 0 && v < m) {
+      if (lds) atomicAdd(&hist[v], 1);
+      else atomicAdd(&counts[v], 1);
+    }
+  }
+  if (lds) {
+    __syncthreads();
+    for (int i = threadIdx.x; i < m; i += kThreads)
+      if (hist[i]) atomicAdd(&counts[i], hist[i]);
+  }
+}
+
+// counts: int32 [m], zeroed by the caller.
+CML_API int cml_int_hist(const int* vals, long long n, int m, int* counts, void* stream) {
+  if (n <= 0) return 0;
+  if (m <= 0) return (int)hipErrorInvalidValue;
+  const size_t lds = m <= 8192 ? (size_t)m * 4 : 0;
+  hipLaunchKernelGGL(int_hist_kernel, dim3(grid_for(n, kThreads * 16LL)), dim3(kThreads), lds, (hipStream_t)stream,
+                     vals, n, m, counts);
   return cml_status();
 }
 
@@ -755,27 +810,30 @@ CML_API int cml_local_kpp(const double* P, const double* PT, int m, int d, const
   return cml_status();
 }
 
+// stop / flags (may be null): int[3] {stop, moved[2]} of the host-sync-free loop (local_update_kernel);
+// the assign of iteration i is given moved = flags + 1 + (i & 1) and stop = flags.
 CML_API int cml_local_assign(const double* P, int m, int d, const double* CT, int k, int* labels, int* moved,
-                             void* stream) {
+                             const int* stop, void* stream) {
   if (m <= 0 || (long long)d * 8 > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(local_assign_kernel, dim3(m), dim3(kThreads), (size_t)d * 8, (hipStream_t)stream, P, m, d, CT,
-                     k, labels, moved);
+                     k, labels, moved, stop);
   return cml_status();
 }
 
 CML_API int cml_local_update(const double* P, int m, int d, const double* w, const int* labels, int k, double* C,
-                             double* CT, double* cnt, int spherical, double* /*unused*/, void* stream) {
+                             double* CT, double* cnt, int spherical, int* flags, int slot, void* stream) {
   const size_t lds = (((size_t)m * 4 + 15) & ~(size_t)15) + (size_t)d * 8;
-  if (m <= 0 || lds > 150 * 1024) return (int)hipErrorInvalidValue;
+  if (m <= 0 || lds > 150 * 1024 || slot < 0 || slot > 1) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(local_update_kernel, dim3(k), dim3(kThreads), lds, (hipStream_t)stream, P, m, d, w, labels, k,
-                     C, CT, cnt, spherical);
+                     C, CT, cnt, spherical, flags, slot);
   return cml_status();
 }
 
 // picks: int [2k] scratch.
 CML_API int cml_local_empty(const double* P, int m, int d, const double* cnt, int k, unsigned long long key,
-                            unsigned long long* ctr, double* C, double* CT, int* picks, void* stream) {
+                            unsigned long long* ctr, double* C, double* CT, int* picks, const int* stop,
+                            void* stream) {
   hipLaunchKernelGGL(local_empty_kernel, dim3(1), dim3(kThreads), 0, (hipStream_t)stream, P, m, d, cnt, k, key, ctr,
-                     C, CT, picks);
+                     C, CT, picks, stop);
   return cml_status();
 }

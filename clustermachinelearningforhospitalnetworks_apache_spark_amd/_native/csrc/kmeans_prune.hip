@@ -410,7 +410,9 @@ __global__ __launch_bounds__(256) void kmeans_seed_bounds_kernel(
 // 1024 threads = 1024 / tr of the workgroup's tiles per sweep (tr <= 1024 rows per tile).
 __global__ __launch_bounds__(1024) void kmeans_label_hist_kernel(const int* __restrict__ labels, long long n, int tr,
                                                                  int kp, int* __restrict__ hist,
-                                                                 int* __restrict__ rank) {
+                                                                 int* __restrict__ rank, const int* __restrict__ gate,
+                                                                 int want) {
+  if (gate != nullptr && gate[0] != want) return;  // the pass the gate picked made hist/rank itself
   extern __shared__ int h[];
   for (int i = threadIdx.x; i < kp; i += 1024) h[i] = 0;
   __syncthreads();
@@ -506,10 +508,11 @@ CML_API int cml_kmeans_seed_bounds(const int* nearest, const float* cost, const 
   return cml_status();
 }
 
+// gate (may be null): run only when gate[0] == want (the pruned-step mode flags).
 CML_API int cml_kmeans_label_hist(const int* labels, long long n, int tr, int grid, int kp, int* hist, int* rank,
-                                  void* stream) {
+                                  const int* gate, int want, void* stream) {
   if (tr <= 0 || tr > 1024 || grid <= 0 || kp <= 0 || (size_t)kp * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmeans_label_hist_kernel, dim3(grid), dim3(1024), (size_t)kp * 4, (hipStream_t)stream, labels,
-                     n, tr, kp, hist, rank);
+                     n, tr, kp, hist, rank, gate, want);
   return cml_status();
 }

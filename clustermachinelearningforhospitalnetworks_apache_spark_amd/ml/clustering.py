@@ -111,7 +111,7 @@ class KMeans(Estimator):
                 init = eng.init_random(seed)
         else:
             with trace("kmeans.init"):
-                init = eng.init_kmeans_parallel(seed, self.getInitSteps())
+                init = eng.init_kmeans_parallel(seed, self.getInitSteps(), as_device=True)
             k_eff = getattr(eng, "k_effective", k)
             if k_eff < k:
                 init = init[:k_eff]

@@ -368,7 +368,8 @@ class LloydEngine:
         if self.comm.is_distributed:
             self.comm.allreduce_(st.mx, op="max")
 
-    def _row_pass(self, c0: Optional[torch.Tensor] = None, c0n: float = 0.0, cost=None, near=None) -> None:
+    def _row_pass(self, c0: Optional[torch.Tensor] = None, c0n: float = 0.0, cost=None, near=None,
+                  c0n_dev: Optional[torch.Tensor] = None) -> None:
         """The one pass over X that fills the norms (and max norm, exponent range; with c0 the first
         k-means|| costs), then caches the norms on the feature tensor."""
         n, dp = self.n, self.dp
@@ -382,7 +383,7 @@ class LloydEngine:
             for _, r0, r1, xc in self._x_chunks(whole=True):
                 K.row_pass(xc, r1 - r0, dp, self._xnorm[r0:r1], c0, c0n, None if cost is None else cost[r0:r1],
                            None if near is None else near[r0:r1], xn_max=mxv, erange=self._erange,
-                           xn64=self._xnorm64[r0:r1])
+                           xn64=self._xnorm64[r0:r1], c0n_dev=c0n_dev)
         if mxv is not None and self.comm.is_distributed:
             self.comm.allreduce_(mxv, op="max")
         self._norms_ready = True
@@ -415,7 +416,9 @@ class LloydEngine:
 
     @property
     def global_n(self) -> int:
-        return int(self.comm.sum_scalar(float(self.n)))
+        if getattr(self, "_gn", None) is None:
+            self._gn = int(self.comm.sum_scalar(float(self.n)))
+        return self._gn
 
     def row_ids(self) -> torch.Tensor:
         if self._row_ids is None:
@@ -425,8 +428,13 @@ class LloydEngine:
         return self._row_ids
 
     def set_centers(self, centers) -> None:
+        """New centres (numpy / list, or a device tensor: no host copy) — the k-means|| result of this
+        engine seeds the first step's bounds (_seed_from_init)."""
         self._ensure_norms()
-        c = torch.as_tensor(np.asarray(centers, dtype=np.float64), device=self.device)
+        if torch.is_tensor(centers):
+            c = centers.to(device=self.device, dtype=torch.float64)
+        else:
+            c = torch.as_tensor(np.asarray(centers, dtype=np.float64), device=self.device)
         if c.shape != (self.k, self.d):
             raise ValueError(f"centers shape {tuple(c.shape)} != {(self.k, self.d)}")
         if self.centers.shape == c.shape and self.centers.dtype == c.dtype:
@@ -443,8 +451,9 @@ class LloydEngine:
             self.delta.invalidate()
             # centres straight from this engine's k-means|| init: the first step starts from bounds the
             # init already implies (no full assign pass); anything else takes a full step
-            self._seeded = (seed is not None and seed.out.shape == tuple(c.shape) and
-                            np.array_equal(seed.out, np.asarray(centers, dtype=np.float64)))
+            self._seeded = seed is not None and seed.out.shape == tuple(c.shape) and (
+                centers is seed.out or (seed.out_np is not None and not torch.is_tensor(centers) and
+                                        np.array_equal(seed.out_np, np.asarray(centers, dtype=np.float64))))
             if self._seeded:
                 self._seed_from_init(seed)
             else:
@@ -749,7 +758,7 @@ class LloydEngine:
         pn = (U * U).sum(1)
         cnn = (cbd * cbd).sum(1)
         d2m = (pn[:, None] + cnn[None, :] - 2.0 * (U @ cbd.T)).clamp_(min=0.0)
-        eps = 1e-12 * float(pn.max() + cnn.max())  # f64 rounding of the expansion
+        eps = 1e-12 * (pn.max() + cnn.max())  # f64 rounding of the expansion (a device scalar: no host read)
         top = torch.topk(d2m, min(2, k), dim=1, largest=False)
         a = top.indices[:, 0].to(torch.int32).contiguous()
         d1 = ((top.values[:, 0] + eps).sqrt() * (1.0 + 1e-6)).to(torch.float32).contiguous()
@@ -773,20 +782,19 @@ class LloydEngine:
         st, dl = self._pst, self.delta
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
-        m = 0
         if n:
+            # the gate picks the candidate pass (+ counting-sort ranks of the labels) or, past _PRUNE_CAP
+            # candidates, the full pass (which ranks every row itself) — decided on the device
             K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                            xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, zero_count=True, cum=st.cum)
-            m = int(st.count.item())
-        if m > st.cap_m:
-            st.force.fill_(1)
-            self._step_prune_dev()
-            return
-        st.pmode.copy_(torch.tensor([0, m], dtype=torch.int32))
-        if n:
+            K.prune_gate(st.count, st.cap_m, st.flags, st.pmode)
+            K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                            st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1,
+                            cum=st.cum)
             K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, None, st.ub, st.lb,
-                            st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab, cum=st.cum)
-            K.label_hist(lab, n, ap, self.hist, self.rank)
+                            st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab, gate=st.pmode,
+                            want=0, cum=st.cum)
+            K.label_hist(lab, n, ap, self.hist, self.rank, gate=st.pmode, want=0)
         self.cost_part.zero_()
         dl.invalidate()
         dl.gate(0)
@@ -1294,7 +1302,7 @@ class LloydEngine:
         lab, best = self._assign_all(cands)
         return best.to(torch.float64), lab.long()
 
-    def init_kmeans_parallel(self, seed: int, steps: int = 2) -> np.ndarray:
+    def init_kmeans_parallel(self, seed: int, steps: int = 2, as_device: bool = False):
         """k-means|| (Bahmani et al.), Spark's default initMode (initSteps rounds sampling each row with
         probability 2k·cost/Σcost), then weighted local k-means++ + Lloyd on the distinct candidates.
 
@@ -1304,8 +1312,16 @@ class LloydEngine:
         (cost, nearest candidate), and the local k-means runs as HIP kernels. The nearest candidate of
         every row is carried across rounds (strict improvement keeps the earlier candidate: argmin's
         first-index rule over the concatenated list), so the candidate weights need no extra pass.
+        The GPU path reads the host only where a size decides the next launches: once per round (the
+        sampled counts of every rank, one fixed-size all-gather) plus the pruned pass's row counts, the
+        distinct-candidate count and the result — the first centre, Σcost and the sampling rate, the
+        candidate weights and the local Lloyd's convergence stay on the device (~11 ms of
+        init at the 8-GPU shard was mostly host round trips).
         The CPU path runs the same algorithm in f64, with the same distinct-candidate order (sorted
-        rows) and the bitwise-identical local k-means (host twin of the kernels)."""
+        rows) and the bitwise-identical local k-means (host twin of the kernels). ``as_device``: return
+        the centres as the f64 device tensor (GPU engines; set_centers takes it without a host copy)."""
+        if self.gpu:
+            return self._init_kmeans_parallel_gpu(seed, steps, as_device)
         k = self.k
         ids = self.row_ids()
         gn = self.global_n
@@ -1320,67 +1336,122 @@ class LloydEngine:
                                                                       device=self.device)
         row = self.comm.allgather(row)[owner] if self.comm.is_distributed else row
         centers = [row.reshape(1, self.d)]
-        if self.gpu:
-            costs, nearest = self._init_first_pass(centers[0])
-        elif self.n:
+        if self.n:
             costs, nearest = self._min_dist_idx(centers[0])
         else:
             costs = torch.zeros(0, dtype=torch.float64, device=self.device)
             nearest = torch.zeros(0, dtype=torch.int64, device=self.device)
         ncand = 1
         for step in range(steps):
-            if not self.n:
-                local = 0.0
-            elif self.gpu and costs.dtype == torch.float32:
-                local = float(K.sum_f64(costs, self.n).item())  # no f64 copy of the costs
-            else:
-                local = float(costs[: self.n].sum(dtype=torch.float64).item())
+            local = float(costs[: self.n].sum(dtype=torch.float64).item()) if self.n else 0.0
             sum_cost = self.comm.sum_scalar(local)
             if sum_cost <= 0:
                 break
-            if self.gpu:
-                chosen = self._init_sample(costs, ids, rng.key(seed, 100 + step), 2.0 * k / sum_cost)
-            else:
-                us = rng.uniform(ids, seed, stream=100 + step)  # the sample kernel's test: u < scale·cost
-                chosen = torch.nonzero(us < (2.0 * k / sum_cost) * costs).flatten()
+            us = rng.uniform(ids, seed, stream=100 + step)  # the sample kernel's test: u < scale·cost
+            chosen = torch.nonzero(us < (2.0 * k / sum_cost) * costs).flatten()
             new = self._rows_f64(chosen) if chosen.numel() else torch.zeros((0, self.d), dtype=torch.float64,
                                                                             device=self.device)
             new = self.comm.allgather_cat(new)
             if new.shape[0] == 0:
                 continue
             centers.append(new)
-            if self.gpu:
-                # once most rows sit near a candidate, only the new candidates close to a row's nearest one
-                # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
-                # round (only the first centre so far) everything after the first K9r chunk
-                first = new.shape[0] if step > 0 else self._first_chunk(new.shape[0])
-                if step == 0:
-                    self._init_candidate_pass(new[:first], costs, nearest, ncand)
-                rest = new[first:] if step == 0 else new
-                if rest.shape[0] and not self._init_candidate_pass_pruned(
-                        torch.cat(centers[:-1] + ([new[:first]] if step == 0 else []), 0), rest, costs, nearest,
-                        ncand + (first if step == 0 else 0)):
-                    self._init_candidate_pass(rest, costs, nearest, ncand + (first if step == 0 else 0))
-            elif self.n:
+            if self.n:
                 d_new, i_new = self._min_dist_idx(new)
                 better = d_new < costs
                 costs = torch.where(better, d_new, costs)
                 nearest = torch.where(better, i_new + ncand, nearest)
             ncand += new.shape[0]
+        return self._init_finish(seed, centers, costs, nearest, as_device=False)
+
+    def _init_kmeans_parallel_gpu(self, seed: int, steps: int, as_device: bool):
+        k, n, d, dev, comm = self.k, self.n, self.d, self.device, self.comm
+        ids = self.row_ids()
+        ids64 = ids if ids.dtype == torch.int64 and ids.is_contiguous() else ids.to(torch.int64).contiguous()
+        # first centre: the global row with the smallest counter uniform — one fixed-size all-gather of
+        # [u_min, local rows, row] per rank, picked on the device (no host read)
+        u = rng.uniform(ids, seed, stream=1)
+        if n:
+            lu, li = torch.min(u, 0)
+            row = self._rows_f64(li.reshape(1)).reshape(-1)
+        else:
+            lu = torch.tensor(2.0, dtype=torch.float64, device=dev)
+            row = torch.zeros(d, dtype=torch.float64, device=dev)
+        hdr = torch.cat([lu.reshape(1).to(torch.float64),
+                         torch.full((1,), float(n), dtype=torch.float64, device=dev), row])
+        g = comm.allgather_fixed(hdr)
+        c0 = g[torch.argmin(g[:, 0]), 2:].reshape(1, d)
+        gn_dev = g[:, 1].sum()
+        centers = [c0]
+        costs, nearest = self._init_first_pass(c0)
+        ncand = 1
+        two_k = torch.tensor([0.0, 2.0 * k], dtype=torch.float64, device=dev)
+        cap = min(max(n, 1), max(4096, 8 * k))
+        out = torch.empty(cap, dtype=torch.int32, device=dev)
+        for step in range(steps):
+            # Σcost over every rank and the rate 2k / Σcost stay on the device (the sample kernel forms it)
+            scale = two_k.clone()
+            if n:
+                scale[0:1].copy_(K.sum_f64(costs, n).reshape(1))
+            comm.allreduce_(scale[0:1])
+            cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+            if n:
+                K.init_sample(costs, ids64, n, rng.key(seed, 100 + step), scale, out, cnt)
+            # the one host read of the round: every rank's sampled count (and, once, the global row count)
+            head = torch.cat([cnt.to(torch.float64), gn_dev.reshape(1)])
+            hv = comm.allgather_fixed(head).cpu()
+            counts = [int(v) for v in hv[:, 0].tolist()]
+            if step == 0:
+                self._gn = int(hv[0, 1].item())
+                if self._gn == 0:
+                    raise ValueError("KMeans on an empty dataset")
+            m = counts[comm.rank]
+            if m > cap:  # rare: more than the expected ~2k·(share of the cost) rows; sample again with room
+                out = torch.empty(m, dtype=torch.int32, device=dev)
+                cnt.zero_()
+                K.init_sample(costs, ids64, n, rng.key(seed, 100 + step), scale, out, cnt)
+                cap = m
+            chosen = torch.sort(out[:m]).values.long()
+            new = self._rows_f64(chosen) if m else torch.zeros((0, d), dtype=torch.float64, device=dev)
+            new = comm.allgather_sized(new, counts)
+            if new.shape[0] == 0:
+                continue
+            centers.append(new)
+            # once most rows sit near a candidate, only the new candidates close to a row's nearest one
+            # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
+            # round (only the first centre so far) everything after the first K9r chunk
+            first = new.shape[0] if step > 0 else self._first_chunk(new.shape[0])
+            if step == 0:
+                self._init_candidate_pass(new[:first], costs, nearest, ncand)
+            rest = new[first:] if step == 0 else new
+            if rest.shape[0] and not self._init_candidate_pass_pruned(
+                    torch.cat(centers[:-1] + ([new[:first]] if step == 0 else []), 0), rest, costs, nearest,
+                    ncand + (first if step == 0 else 0)):
+                self._init_candidate_pass(rest, costs, nearest, ncand + (first if step == 0 else 0))
+            ncand += new.shape[0]
+        return self._init_finish(seed, centers, costs, nearest, as_device=as_device)
+
+    def _init_finish(self, seed: int, centers: list, costs: torch.Tensor, nearest: torch.Tensor, as_device: bool):
+        """Distinct candidates, their weights (rows per candidate, all-reduced) and the local k-means."""
+        k = self.k
         cand = torch.cat(centers, 0)
         # distinct candidates in sorted-row order (np.unique's order; identical on every device)
         uniq, inverse = torch.unique(cand, dim=0, return_inverse=True)
         if uniq.shape[0] <= k:
-            out = uniq.cpu().numpy()
+            out = uniq
         else:
             if self.n and self.w is not None:
                 # summed row weights per candidate (deterministic f64 sums, as the Lloyd sums)
                 w = K.sums_reference(self.w[:, None], inverse.reshape(-1)[nearest[: self.n].long()],
                                      uniq.shape[0])[0][:, 0].contiguous()
             elif self.n:
-                # rows per candidate (a histogram of the int32 nearest ids), folded onto the distinct
-                # candidates: integer counts, so the f64 sums are exact in any order
-                per = torch.bincount(nearest[: self.n], minlength=cand.shape[0]).to(torch.float64)
+                # rows per candidate (an int32 histogram of the nearest ids: integer counts, exact in any
+                # order), folded onto the distinct candidates
+                if self.gpu:
+                    per_i = torch.zeros(cand.shape[0], dtype=torch.int32, device=self.device)
+                    K.int_hist(nearest, self.n, cand.shape[0], per_i)
+                    per = per_i.to(torch.float64)
+                else:
+                    per = torch.bincount(nearest[: self.n], minlength=cand.shape[0]).to(torch.float64)
                 w = torch.zeros(uniq.shape[0], dtype=torch.float64, device=self.device)
                 w.index_add_(0, inverse.reshape(-1), per)
             else:
@@ -1391,48 +1462,38 @@ class LloydEngine:
                 # every rank ran the same local k-means on the same candidates and weights; rank 0's
                 # result is taken verbatim (one source of truth for the centres every rank starts from)
                 out = self.comm.broadcast_(out.contiguous(), 0)
-            out = out.cpu().numpy()
-        if out.shape[0] < k:
+        nk = int(out.shape[0])
+        if nk < k:
             # Spark may return fewer centres when there are < k distinct points; pad by repetition so the
             # device buffers keep their shape, and record the real count.
-            self.k_effective = out.shape[0]
-            out = np.concatenate([out, np.repeat(out[-1:], k - out.shape[0], 0)], 0)
+            self.k_effective = nk
+            out = torch.cat([out, out[-1:].expand(k - nk, -1)], 0)
         else:
             self.k_effective = k
+        out = out.to(torch.float64).contiguous()
         if self._pdev and self.n and self.k_effective == k and os.environ.get("CML_KMEANS_SEED_BOUNDS", "1") != "0":
             # what the first Lloyd step needs to start from bounds instead of a full pass (set_centers)
-            self._seed = types.SimpleNamespace(nearest=nearest, costs=costs, inverse=inverse, uniq=uniq,
-                                               out=np.array(out, dtype=np.float64, copy=True))
-        return out
+            self._seed = types.SimpleNamespace(nearest=nearest, costs=costs, inverse=inverse, uniq=uniq, out=out,
+                                               out_np=None)
+        if as_device and self.gpu:
+            return out
+        res = out.cpu().numpy()
+        if getattr(self, "_seed", None) is not None and self._seed.out is out:
+            self._seed.out_np = res
+        return res
 
     def _init_first_pass(self, c0: torch.Tensor):
         """(cost f32, nearest i32) of every local row against the first centre, from the row pass that
-        also fills the norms (one read of X; a second read only if the norms were cached already)."""
+        also fills the norms (one read of X; a second read only if the norms were cached already). The
+        centre's bf16 norm reaches the kernel on the device."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
         cb0 = torch.zeros((32, dp), dtype=torch.bfloat16, device=dev)
         cn0 = torch.zeros(32, dtype=torch.float32, device=dev)
         K.update_centers(None, 1, d, c0.reshape(1, d).to(torch.float64).contiguous().clone(), cb0, dp, 32, cn0, None)
         costs = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         nearest = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
-        self._row_pass(cb0[0].to(torch.float32).contiguous(), float(cn0[0].item()), costs, nearest)
+        self._row_pass(cb0[0].to(torch.float32).contiguous(), 0.0, costs, nearest, c0n_dev=cn0[0:1])
         return costs, nearest
-
-    def _init_sample(self, costs: torch.Tensor, ids: torch.Tensor, key: int, scale: float) -> torch.Tensor:
-        """Sorted local rows chosen by one k-means|| round (K12 sample kernel)."""
-        n = self.n
-        if n == 0:
-            return torch.zeros(0, dtype=torch.int64, device=self.device)
-        ids = ids if ids.dtype == torch.int64 and ids.is_contiguous() else ids.to(torch.int64).contiguous()
-        cap = min(n, max(4096, 8 * self.k))
-        for _ in range(2):
-            out = torch.empty(cap, dtype=torch.int32, device=self.device)
-            cnt = torch.zeros(1, dtype=torch.int32, device=self.device)
-            K.init_sample(costs, ids, n, key, scale, out, cnt)
-            m = int(cnt.item())
-            if m <= cap:
-                return torch.sort(out[:m]).values.long()
-            cap = m  # rare: more than the expected ~2k·(share of the cost) rows; run again with room
-        raise RuntimeError("k-means|| sample did not fit its buffer")
 
     def _init_candidate_pass(self, new: torch.Tensor, costs: torch.Tensor, nearest: torch.Tensor,
                              off: int) -> None:
@@ -1486,7 +1547,7 @@ class LloydEngine:
         Y = new.to(device=dev, dtype=torch.float64)
         pn, yn = (P * P).sum(1), (Y * Y).sum(1)
         d2 = pn[:, None] + yn[None, :] - 2.0 * (P @ Y.T)
-        eps = 1e-12 * float(pn.max() + yn.max())
+        eps = 1e-12 * (pn.max() + yn.max())  # device scalar (no host read)
         vals, order = torch.sort((d2 - eps).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6), dim=1)
         tab_v = vals.to(torch.float32).contiguous()
         tab_j = order.to(torch.int32).contiguous()

@@ -62,7 +62,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_cond_copy": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
                                        c_vp, c_vp, c_vp, c_vp]),
-    "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp]),
+    "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_centre_stats": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
@@ -79,19 +79,21 @@ _native.register_kernel_sigs({
 
 _native.register_kernel_sigs({
     "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
-                                    c_vp, c_vp, c_vp]),
+                                    c_vp, c_vp, c_vp, c_vp]),
+    "cml_int_hist": (c_int, [c_vp, c_ll, c_int, c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_sum_f32_f64_parts": (c_int, []),
     "cml_kmeans_cost_parts": (c_int, []),
     "cml_kmeans_cost_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_sum_f32_f64": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
-                                       c_vp]),
+                                       c_vp, c_vp]),
     "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
                               c_vp]),
-    "cml_local_assign": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
-    "cml_local_update": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
-    "cml_local_empty": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_local_assign": (c_int, [c_vp, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_local_update": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_vp, c_vp, c_int, c_vp, c_int, c_vp]),
+    "cml_local_empty": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                c_vp]),
 })
 _native.register_kernel_sigs({
     "cml_kmeans_exact_assign": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
@@ -117,17 +119,19 @@ def _u64(v: int) -> int:
 def row_pass(x: torch.Tensor, n: int, dp: int, xn: torch.Tensor, c0: torch.Tensor | None = None, c0n: float = 0.0,
              cost: torch.Tensor | None = None, near: torch.Tensor | None = None,
              xn_max: torch.Tensor | None = None, erange: torch.Tensor | None = None,
-             xn64: torch.Tensor | None = None, stream=None) -> None:
+             xn64: torch.Tensor | None = None, c0n_dev: torch.Tensor | None = None, stream=None) -> None:
     """One read of X (``kmeans_init.hip``): ``xn`` = ||x||² (bitwise ``row_sqnorm``), optionally the
     first k-means|| cost against the bf16-rounded centre ``c0`` (f32 [dp], norm ``c0n``) with
     ``near`` = 0, the max ||x||² (``xn_max``: f32 [1], zero-initialised, updated by bit-pattern
     atomicMax), the range of bf16 exponents (``erange``: int32 [2] = {INT_MAX, -1} initialised) and the
-    norms summed in f64 (``xn64``: f64 [n], the training cost's per-centre Σ|x|²)."""
+    norms summed in f64 (``xn64``: f64 [n], the training cost's per-centre Σ|x|²). ``c0n_dev`` (f32 [1]
+    device scalar) replaces ``c0n`` with no host read."""
     if xn64 is not None and (xn64.dtype != torch.float64 or not xn64.is_contiguous() or xn64.numel() < n):
         raise ValueError("row_pass: xn64 must be a contiguous f64 [n] tensor")
     _native.check(_native.kernels().cml_kmeans_row_pass(
         x.data_ptr(), int(n), x.stride(0), int(dp), int(is_fp8(x)), xn.data_ptr(), _ptr(c0), float(c0n), _ptr(cost),
-        _ptr(near), _ptr(xn_max), _ptr(erange), _ptr(xn64), _native.stream_ptr(stream)), "kmeans_row_pass")
+        _ptr(near), _ptr(xn_max), _ptr(erange), _ptr(xn64), _ptr(c0n_dev), _native.stream_ptr(stream)),
+        "kmeans_row_pass")
 
 
 def sum_f64(x: torch.Tensor, n: int, stream=None) -> torch.Tensor:
@@ -169,20 +173,33 @@ def init_merge(cost: torch.Tensor, near: torch.Tensor, best: torch.Tensor, lab: 
                                                           _native.stream_ptr(stream)), "kmeans_init_merge")
 
 
-def init_sample(cost: torch.Tensor, ids: torch.Tensor, n: int, key: int, scale: float, out: torch.Tensor,
+def init_sample(cost: torch.Tensor, ids: torch.Tensor, n: int, key: int, scale, out: torch.Tensor,
                 count: torch.Tensor, stream=None) -> None:
     """Rows with counter-uniform(ids[i]) < scale·cost[i] appended (unordered) to ``out`` (at most
-    len(out)); ``count`` (zeroed by the caller) receives their number."""
+    len(out)); ``count`` (zeroed by the caller) receives their number. ``scale``: a float, or an f64 [2]
+    device tensor {Σcost, 2k} whose quotient 2k / Σcost the kernel forms (no host read)."""
+    dev_scale = torch.is_tensor(scale)
+    if dev_scale and (scale.dtype != torch.float64 or scale.numel() < 2 or not scale.is_contiguous()):
+        raise ValueError("init_sample: device scale is an f64 [2] tensor {sum, 2k}")
     _native.check(_native.kernels().cml_kmeans_init_sample(
-        cost.data_ptr(), ids.data_ptr(), int(n), _u64(key), float(scale), out.data_ptr(), count.data_ptr(),
-        int(out.shape[0]), _native.stream_ptr(stream)), "kmeans_init_sample")
+        cost.data_ptr(), ids.data_ptr(), int(n), _u64(key), 0.0 if dev_scale else float(scale), out.data_ptr(),
+        count.data_ptr(), int(out.shape[0]), scale.data_ptr() if dev_scale else 0, _native.stream_ptr(stream)),
+        "kmeans_init_sample")
+
+
+def int_hist(vals: torch.Tensor, n: int, m: int, counts: torch.Tensor, stream=None) -> None:
+    """counts[v] += #{i < n: vals[i] = v} for int32 values in [0, m) (int32 counts, exact; device only)."""
+    if vals.dtype != torch.int32 or counts.dtype != torch.int32 or counts.numel() < m or not vals.is_contiguous():
+        raise ValueError("int_hist: int32 values and counts [m]")
+    _native.check(_native.kernels().cml_int_hist(vals.data_ptr(), int(n), int(m), counts.data_ptr(),
+                                                 _native.stream_ptr(stream)), "int_hist")
 
 
 def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int, max_iter: int = 30,
                  spherical: bool = False) -> torch.Tensor:
     """Weighted k-means++ seeding + weighted Lloyd on a small candidate set (Spark
-    LocalKMeans.kMeansPlusPlus), f64 [k, d]. GPU tensors run the ``kmeans_init.hip`` kernels (one
-    host read per Lloyd iteration, for the moved flag); CPU tensors the host twin
+    LocalKMeans.kMeansPlusPlus), f64 [k, d]. GPU tensors run the ``kmeans_init.hip`` kernels (no host
+    read: convergence is latched on the device); CPU tensors the host twin
     (``host/kmeans_local.cpp``), which performs the same rounded operations in the same order: both
     return the same bits. Draws: counter uniforms under (seed, 200) for the picks and (seed, 201) for
     empty-cluster reseeds."""
@@ -202,7 +219,6 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         CT = torch.empty((d, k), dtype=torch.float64, device=dev)
         d2 = torch.empty(m, dtype=torch.float64, device=dev)
         lab = torch.full((m,), -1, dtype=torch.int32, device=dev)
-        moved = torch.zeros(1, dtype=torch.int32, device=dev)
         cnt = torch.zeros(k, dtype=torch.float64, device=dev)
         ctr = torch.zeros(1, dtype=torch.int64, device=dev)
         picks = torch.zeros(2 * k, dtype=torch.int32, device=dev)
@@ -213,17 +229,21 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         _native.check(lib.cml_local_kpp(pts.data_ptr(), PT.data_ptr(), m, d, w.data_ptr(), int(k), _u64(key_pp),
                                         C.data_ptr(), CT.data_ptr(), d2.data_ptr(), _ptr(D), st), "local_kpp")
         del D
-        for _ in range(max_iter):
-            moved.zero_()
+        # Lloyd without host reads: flags = {stop, moved[2]}; the update kernel latches stop once an
+        # iteration's assign moved no label (the host loop's break), after which every queued launch
+        # returns at once — max_iter iterations are enqueued back to back, the same bits as the host
+        # twin's loop (a few no-op launches instead of one host round trip per iteration)
+        flags = torch.zeros(3, dtype=torch.int32, device=dev)
+        fp = flags.data_ptr()
+        for it in range(max_iter):
+            slot = it & 1
             _native.check(lib.cml_local_assign(pts.data_ptr(), m, d, CT.data_ptr(), int(k), lab.data_ptr(),
-                                               moved.data_ptr(), st), "local_assign")
-            if int(moved.item()) == 0:
-                break
+                                               fp + 4 * (1 + slot), fp, st), "local_assign")
             _native.check(lib.cml_local_update(pts.data_ptr(), m, d, w.data_ptr(), lab.data_ptr(), int(k),
-                                               C.data_ptr(), CT.data_ptr(), cnt.data_ptr(), int(bool(spherical)), 0,
-                                               st), "local_update")
+                                               C.data_ptr(), CT.data_ptr(), cnt.data_ptr(), int(bool(spherical)), fp,
+                                               slot, st), "local_update")
             _native.check(lib.cml_local_empty(pts.data_ptr(), m, d, cnt.data_ptr(), int(k), _u64(key_e),
-                                              ctr.data_ptr(), C.data_ptr(), CT.data_ptr(), picks.data_ptr(), st),
+                                              ctr.data_ptr(), C.data_ptr(), CT.data_ptr(), picks.data_ptr(), fp, st),
                           "local_empty")
         return C
     P = pts.cpu().contiguous()
@@ -608,14 +628,16 @@ def seed_bounds(nearest: torch.Tensor, cost: torch.Tensor, xn: torch.Tensor, qma
 
 
 def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Tensor, rank: torch.Tensor,
-               stream=None) -> None:
+               stream=None, gate: torch.Tensor | None = None, want: int = 0) -> None:
     """Counting-sort ranks of the current labels in the K9r workgroup geometry (what a full K9r pass
-    leaves in hist/rank for the sort-regime accumulate). Device only."""
+    leaves in hist/rank for the sort-regime accumulate). ``gate``/``want``: run only when gate[0] ==
+    want (device flag). Device only."""
     if labels.dtype != torch.int32 or hist.numel() < plan.grid * plan.kp or rank.numel() < n:
         raise ValueError("label_hist: operand shapes")
     _native.check(_native.kernels().cml_kmeans_label_hist(labels.data_ptr(), int(n), int(plan.round_rows),
                                                           int(plan.grid), int(plan.kp), hist.data_ptr(),
-                                                          rank.data_ptr(), _native.stream_ptr(stream)),
+                                                          rank.data_ptr(), _ptr(gate), int(want),
+                                                          _native.stream_ptr(stream)),
                   "kmeans_label_hist")
 
 

@@ -149,6 +149,27 @@ class Communicator:
         dist.all_gather(outs, pad, group=self.group)
         return [o[:s] for o, s in zip(outs, sizes)]
 
+    def allgather_fixed(self, t: torch.Tensor) -> torch.Tensor:
+        """[world, *t.shape]: every rank's same-shape tensor, in rank order, with no size exchange and no
+        host read (one all_gather_into_tensor on the device stream)."""
+        if not self.is_distributed:
+            return t.reshape((1,) + tuple(t.shape))
+        src = t.contiguous()
+        out = torch.empty((self.world_size,) + tuple(src.shape), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(self._coerce(out), src, group=self.group)
+        return out
+
+    def allgather_sized(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
+        """Concatenation in rank order of every rank's ``t`` whose row counts ``sizes`` every rank already
+        knows (one padded all_gather, no size exchange)."""
+        if not self.is_distributed:
+            return t
+        m = max(max(sizes), 1)
+        pad = torch.zeros((m,) + tuple(t.shape[1:]), dtype=t.dtype, device=t.device)
+        pad[: t.shape[0]] = t
+        g = self.allgather_fixed(pad)
+        return torch.cat([g[r, : sizes[r]] for r in range(self.world_size)], 0)
+
     def allgather_cat(self, t: torch.Tensor) -> torch.Tensor:
         parts = self.allgather(t)
         return parts[0] if len(parts) == 1 else torch.cat(parts, 0)

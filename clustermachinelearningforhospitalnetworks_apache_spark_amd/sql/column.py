@@ -220,7 +220,9 @@ class Lit(Expr):
             vals = np.empty(n, dtype=object)
             vals[:] = self.value
             valid = None if self.value is not None else np.zeros(n, dtype=bool)
-            return ColumnData(vals, valid, dt)
+            cd = ColumnData(vals, valid, dt)
+            cd.scalar = (self.value,)  # a broadcast literal: consumers may use the one value
+            return cd
         v = ts_to_micros(self.value) if isinstance(dt, T.TimestampType) else self.value
         t = torch.full((n,), v, dtype=dt.torch_dtype, device=frame._device)
         return ColumnData(t, None, dt)
@@ -292,6 +294,14 @@ def _parse_ts_column(cd: ColumnData, frame) -> ColumnData:
     such as the reference's BETWEEN bounds, ref.py:126-127, is one parse, not one per row)."""
     dev = frame._device
     n = len(cd)
+    lit = getattr(cd, "scalar", None)
+    if lit is not None and isinstance(lit[0], str):  # a string literal (BETWEEN bounds): one parse, no row scan
+        try:
+            us = ts_to_micros(lit[0])
+        except (TypeError, ValueError):
+            return ColumnData(torch.zeros(n, dtype=torch.int64, device=dev),
+                              torch.zeros(n, dtype=torch.bool, device=dev), T.TimestampType())
+        return ColumnData(torch.full((n,), us, dtype=torch.int64, device=dev), None, T.TimestampType())
     valid = cd.valid_mask().copy()
     if n and valid.all() and all(v is cd.values[0] for v in (cd.values[0], cd.values[n // 2], cd.values[-1])) \
             and isinstance(cd.values[0], str):
