@@ -72,7 +72,7 @@ def kmeans_fit(x, args, comm, seed: int = 42, iters: int = 20, breakdown: bool =
     iterations. Returns (engine, init seconds, per-iteration seconds or None)."""
     gpu = x.is_cuda
     eng = LloydEngine(x, args.dim, args.k, comm, row_chunks=args.chunks,
-                      incremental=not args.full_accumulate, prune=args.prune)
+                      incremental=not args.full_accumulate, prune=args.prune, precision=args.precision)
     eng.track_prune = breakdown
     init = (eng.init_kmeans_parallel(seed=seed, as_device=True) if args.init == "k-means||"
             else eng.init_random(seed=seed))
@@ -125,6 +125,11 @@ def main():
                     help="blobs = the headline data (separated blobs); overlap = blob centres 8x closer; "
                          "uniform = no cluster structure")
     ap.add_argument("--no-overlap", action="store_true", help="skip the extra overlap-data fit")
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "f32", "f64"],
+                    help="feature dtype of the frame (f32/f64: the reference's Double/Integer columns, fitted at "
+                         "source precision by default)")
+    ap.add_argument("--precision", default=None, choices=["auto", "bf16", "exact", "screen"],
+                    help="cml.ml.kmeans.precision of the session (default: auto)")
     ap.add_argument("--init", default="k-means||", choices=["k-means||", "random"])
     ap.add_argument("--chunks", type=int, default=None, help="row chunks per rank (comm/compute overlap)")
     ap.add_argument("--prune", default=None, choices=["on", "off"],
@@ -168,6 +173,9 @@ def main():
         args.rows, args.dim, args.k = min(args.rows, 200_000), min(args.dim, 32), min(args.k, 16)
     spark = (SparkSession.builder.appName("bench-kmeans").master("mi355x" if gpu else "local[1]")
              .config("cml.ml.features.dtype", "bf16" if gpu else "float64").getOrCreate())
+    if args.precision:
+        spark.conf.set("cml.ml.kmeans.precision", args.precision)
+    fdt = {"bf16": torch.bfloat16, "f32": torch.float32, "f64": torch.float64}[args.dtype] if gpu else torch.float64
     comm = spark._comm
     rank, W = comm.rank, comm.world_size
     dev = comm.device
@@ -175,8 +183,7 @@ def main():
     per = args.rows // W
     n_local = per + (1 if rank < args.rows - per * W else 0)
     t0 = time.perf_counter()
-    x = make_blobs(n_local, args.dim, args.k, seed=1000 + rank, device=dev,
-                   dtype=torch.bfloat16 if gpu else torch.float64, spread=_DATA[args.data])
+    x = make_blobs(n_local, args.dim, args.k, seed=1000 + rank, device=dev, dtype=fdt, spread=_DATA[args.data])
     if gpu:
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
@@ -203,7 +210,8 @@ def main():
     acc["assign"] = "pruned (exact bounds)" if eng.prune else "full (every row x every centre)"
     if eng.prune:
         acc["last_step_prune_rank0"] = eng.prune_stats()
-    if gpu:
+    acc["precision"] = eng.precision
+    if gpu and eng.gpu:
         acc.update(_step_rates(eng, comm))
     del eng
     _drop_norm_cache(x)
@@ -220,7 +228,7 @@ def main():
         del eng
         _drop_norm_cache(x)
 
-    if gpu and args.data == "blobs" and not args.no_overlap:
+    if gpu and args.data == "blobs" and args.dtype == "bf16" and not args.no_overlap:
         # the same public-API fit on overlapping blobs (centres 8x closer), where the exact bounds prune
         # little: the robustness of the headline. Same shape, separate data.
         del df
@@ -240,9 +248,10 @@ def main():
 
     total_rows = args.rows
     value = total_rows * args.steps / elapsed
-    headline = (args.rows, args.dim, args.k, args.data) == (100_000_000, 256, 256, "blobs")
+    headline = (args.rows, args.dim, args.k, args.data, args.dtype) == (100_000_000, 256, 256, "blobs", "bf16")
     metric = METRIC if headline else (f"KMeans fit samples/sec (whole node), {args.rows / 1e6:g}M×{args.dim} "
-                                      f"k={args.k}" + ("" if args.data == "blobs" else f", {args.data} data"))
+                                      f"k={args.k}" + ("" if args.data == "blobs" else f", {args.data} data") +
+                                      ("" if args.dtype == "bf16" else f", {args.dtype} rows"))
     if rank == 0:
         out = {
             "metric": metric,
@@ -255,7 +264,7 @@ def main():
             "higher_is_better": True,
             "scaling": "strong",
             "vs_baseline": (value / BASELINE_VALUE) if BASELINE_VALUE else None,
-            "dtype": "bf16" if gpu else "fp64",
+            "dtype": (args.dtype if args.dtype != "f32" else "fp32") if gpu else "fp64",
             "data": f"synthetic ({args.data}: generated on device; centres from k-means|| init inside the timed fit)",
             "config": {
                 "model": f"KMeans k={args.k}, {args.rows}x{args.dim}",
@@ -431,7 +440,7 @@ def bench_logreg(args):
             "value": value, "unit": "rows/s", "n_gpus": W if gpu else 0, "steps": iters, "warmup": args.warmup,
             "ms_per_step": 1000.0 * elapsed / max(iters, 1), "ms_per_gradient_pass": 1000.0 * elapsed / max(passes, 1),
             "gradient_passes": passes, "higher_is_better": True, "scaling": "strong", "vs_baseline": None,
-            "dtype": "bf16" if gpu else "fp64", "data": "synthetic (Gaussian features, logistic labels)",
+            "dtype": (args.dtype if args.dtype != "f32" else "fp32") if gpu else "fp64", "data": "synthetic (Gaussian features, logistic labels)",
             "config": {"model": f"LogisticRegression d={d}", "global_batch": args.rows, "seq_len": None,
                        "parallelism": f"dp{W}"},
             "extra": {"datagen_s": round(gen_s, 3), "scaler_s": round(scaler_s, 3), "final_loss": hist[-1] if hist

@@ -19,15 +19,22 @@ namespace {
 constexpr int kThreads = 256;
 constexpr int kChunk = 1024;  // sorted positions per segmented-sum chunk
 
+// idx / n_dev (both null, or both set): assign only the rows idx[0 .. *n_dev) — the rows the bf16
+// screen could not certify (precision "screen"); labels / best land at the real rows.
 template <typename T, int DREG>
 __global__ __launch_bounds__(kThreads) void exact_assign_kernel(const T* __restrict__ X, long long n, long long ldx,
                                                                 int d, const double* __restrict__ C, int k, int kt,
                                                                 int* __restrict__ labels, double* __restrict__ best,
-                                                                int* __restrict__ changed) {
+                                                                int* __restrict__ changed,
+                                                                const int* __restrict__ idx,
+                                                                const int* __restrict__ n_dev) {
   extern __shared__ __align__(16) unsigned char smem[];
   double* ct = reinterpret_cast<double*>(smem);  // [kt][d]
-  const long long r = (long long)blockIdx.x * kThreads + threadIdx.x;
-  const bool live = r < n;
+  const long long t0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+  const long long cnt = n_dev != nullptr ? (long long)*n_dev : n;
+  if ((long long)blockIdx.x * kThreads >= cnt) return;  // a whole block past the list (block-uniform)
+  const bool live = t0 < cnt && t0 < n;
+  const long long r = live ? (idx != nullptr ? (long long)idx[t0] : t0) : 0;
   double xr[DREG > 0 ? DREG : 1];
   if constexpr (DREG > 0) {
 #pragma unroll
@@ -69,6 +76,82 @@ __global__ __launch_bounds__(kThreads) void exact_assign_kernel(const T* __restr
     if (changed != nullptr && labels[r] != bi) atomicAdd(changed, 1);
     labels[r] = bi;
     best[r] = bd;
+  }
+}
+
+// best[r] = the f64 fold Σ_t (x_t - c_lab,t)² of exact_assign_kernel for row r against its label's
+// centre only (the same operations in the same order, so the same bits as the full assignment's
+// minimum when the label is the argmin): the distances of rows the bf16 screen certified.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void exact_dist_kernel(const T* __restrict__ X, long long n, long long ldx,
+                                                              int d, const double* __restrict__ C,
+                                                              const int* __restrict__ labels, long long lab_off,
+                                                              double* __restrict__ best) {
+  const long long r = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if (r >= n) return;
+  const double* cj = C + (long long)(labels[r] - lab_off) * d;
+  double acc = 0.0;
+  for (int t = 0; t < d; ++t) {
+    const double e = (double)X[r * ldx + t] - cj[t];
+    acc = __fma_rn(e, e, acc);
+  }
+  best[r] = acc;
+}
+
+// Source rows -> the bf16 copy the MFMA screen reads (RNE, zero-padded to ldo) and err[r] >= ||x_r -
+// bf16(x_r)|| (the f64 norm of the rounding, rounded up to f32): the certificate's per-row slack. One
+// wave per row.
+template <typename T>
+__global__ __launch_bounds__(kThreads) void to_bf16_err_kernel(const T* __restrict__ X, long long n, long long ldx,
+                                                               int d, u16* __restrict__ out, long long ldo,
+                                                               float* __restrict__ err) {
+  const int lane = threadIdx.x & 63;
+  const long long w0 = ((long long)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * kThreads) >> 6;
+  for (long long r = w0; r < n; r += nw) {
+    double e2 = 0.0;
+    for (int t = lane; t < ldo; t += 64) {
+      u16 b = 0;
+      if (t < d) {
+        const double v = (double)X[r * ldx + t];
+        b = f32_to_bf16((float)v);  // f64 -> f32 -> bf16: a double rounding, covered by the exact error below
+        const double e = v - (double)bf16_to_f32(b);
+        e2 = __fma_rn(e, e, e2);
+      }
+      out[r * ldo + t] = b;
+    }
+    e2 = wave_sum_f64(e2);
+    if (lane == 0) err[r] = (float)(sqrt(e2) * (1.0 + 1e-6)) + 1e-30f;
+  }
+}
+
+// Rows whose bf16-screen label is not certified (kmeans_screen_cert) are appended to lst (count
+// zeroed by the caller): certified when lb - ub > 2·(err_r + ecmax), ub / lb the K9r top-2 bounds
+// of the bf16 distances (their f32 rounding already inside) and ecmax >= max_j ||c_j - bf16(c_j)||:
+// then every other centre is farther than the label's in exact arithmetic too, so the f64 argmin
+// is the same label (no tie).
+__global__ __launch_bounds__(kThreads) void screen_cert_kernel(const float* __restrict__ ub,
+                                                               const float* __restrict__ lb,
+                                                               const float* __restrict__ err,
+                                                               const double* __restrict__ ecmax, long long n,
+                                                               int* __restrict__ lst, int* __restrict__ count) {
+  const int lane = threadIdx.x & 63;
+  const double ec = *ecmax;
+  for (long long i0 = (long long)blockIdx.x * kThreads; i0 < n; i0 += (long long)gridDim.x * kThreads) {
+    const long long i = i0 + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+      const double gap = (double)lb[i] - (double)ub[i];
+      bad = !(gap > 2.0 * ((double)err[i] + ec) * (1.0 + 1e-9) + 1e-300);
+    }
+    const unsigned long long bal = __ballot(bad);
+    if (bal) {
+      const int leader = __builtin_ctzll(bal);
+      int base = 0;
+      if (lane == leader) base = atomicAdd(count, (int)__popcll(bal));
+      base = __shfl(base, leader, 64);
+      if (bad) lst[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int)i;
+    }
   }
 }
 
@@ -145,17 +228,19 @@ __global__ __launch_bounds__(kThreads) void exact_seg_fix_kernel(const int* __re
 
 // X: f64 (xf64 = 1) or f32 rows [n, ldx elements]; C: f64 [k, d]; labels (int32, read for the change
 // count when `changed` is given) and best (f64) [n].
+// idx / n_dev: see exact_assign_kernel (n is then the capacity of idx, the grid covers it).
 CML_API int cml_kmeans_exact_assign(const void* X, int xf64, long long n, long long ldx, int d, const double* C,
-                                    int k, int* labels, double* best, int* changed, void* stream) {
+                                    int k, int* labels, double* best, int* changed, const int* idx, const int* n_dev,
+                                    void* stream) {
   if (n <= 0) return 0;
-  if (d <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+  if (d <= 0 || k <= 0 || ((idx == nullptr) != (n_dev == nullptr))) return (int)hipErrorInvalidValue;
   const int kt = max(1, min(k, 8192 / d));  // centres per LDS tile (<= 64 KiB)
   const size_t lds = (size_t)kt * d * sizeof(double);
   const dim3 g((unsigned)((n + kThreads - 1) / kThreads));
   hipStream_t st = (hipStream_t)stream;
 #define CML_EA(T, R)                                                                                        \
   hipLaunchKernelGGL((exact_assign_kernel<T, R>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, k, kt, \
-                     labels, best, changed)
+                     labels, best, changed, idx, n_dev)
   if (xf64) {
     if (d <= 4) CML_EA(double, 4);
     else if (d <= 16) CML_EA(double, 16);
@@ -166,6 +251,50 @@ CML_API int cml_kmeans_exact_assign(const void* X, int xf64, long long n, long l
     else CML_EA(float, 0);
   }
 #undef CML_EA
+  return cml_status();
+}
+
+// labels[r] - lab_off indexes C (f64 [*, d]).
+CML_API int cml_kmeans_exact_dist(const void* X, int xf64, long long n, long long ldx, int d, const double* C,
+                                  const int* labels, long long lab_off, double* best, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0) return (int)hipErrorInvalidValue;
+  const dim3 g((unsigned)((n + kThreads - 1) / kThreads));
+  hipStream_t st = (hipStream_t)stream;
+  if (xf64)
+    hipLaunchKernelGGL((exact_dist_kernel<double>), g, dim3(kThreads), 0, st, (const double*)X, n, ldx, d, C, labels,
+                       lab_off, best);
+  else
+    hipLaunchKernelGGL((exact_dist_kernel<float>), g, dim3(kThreads), 0, st, (const float*)X, n, ldx, d, C, labels,
+                       lab_off, best);
+  return cml_status();
+}
+
+// out: bf16 [n, ldo] (ldo >= d, padding zeroed), err: f32 [n].
+CML_API int cml_kmeans_to_bf16_err(const void* X, int xf64, long long n, long long ldx, int d, void* out,
+                                   long long ldo, float* err, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0 || ldo < d) return (int)hipErrorInvalidValue;
+  long long g = (n + 3) / 4;
+  g = g > 8192 ? 8192 : g;
+  hipStream_t st = (hipStream_t)stream;
+  if (xf64)
+    hipLaunchKernelGGL((to_bf16_err_kernel<double>), dim3((unsigned)g), dim3(kThreads), 0, st, (const double*)X, n,
+                       ldx, d, (u16*)out, ldo, err);
+  else
+    hipLaunchKernelGGL((to_bf16_err_kernel<float>), dim3((unsigned)g), dim3(kThreads), 0, st, (const float*)X, n,
+                       ldx, d, (u16*)out, ldo, err);
+  return cml_status();
+}
+
+// lst: int [n] (n entries at most), count: int [1] zeroed by the caller; ecmax: f64 device scalar.
+CML_API int cml_kmeans_screen_cert(const float* ub, const float* lb, const float* err, const double* ecmax,
+                                   long long n, int* lst, int* count, void* stream) {
+  if (n <= 0) return 0;
+  long long g = (n + kThreads * 4 - 1) / (kThreads * 4);
+  g = g > 4096 ? 4096 : (g < 1 ? 1 : g);
+  hipLaunchKernelGGL(screen_cert_kernel, dim3((unsigned)g), dim3(kThreads), 0, (hipStream_t)stream, ub, lb, err,
+                     ecmax, n, lst, count);
   return cml_status();
 }
 

@@ -198,18 +198,29 @@ class LloydEngine:
         # exact f64 sums of those rows); "exact" = the f64 reference algorithm on the rows as given
         # (kmeans_exact.hip on the GPU); "auto" = exact for f32/f64 device rows — the reference's f64
         # feature vectors (ref.py:134-136) are not silently rounded to 8 mantissa bits — and the MFMA
-        # path for bf16 / fp8 rows.
+        # path for bf16 / fp8 rows; "screen" = the exact algorithm's results bit for bit, with the
+        # assignments screened on MFMA (_screen_labels: a bf16 K9r pass with top-2 bounds, a certificate
+        # covering the bf16 rounding of rows and centres, an f64 re-assignment of the uncertified rows) —
+        # what "auto" picks for wide f32/f64 device rows where K9r applies (CML_KMEANS_SCREEN=0: exact).
         precision = (precision or os.environ.get("CML_KMEANS_PRECISION") or "auto").lower()
-        if precision not in ("auto", "bf16", "exact"):
-            raise ValueError(f"KMeans precision must be 'auto', 'bf16' or 'exact', got {precision!r}")
+        if precision not in ("auto", "bf16", "exact", "screen"):
+            raise ValueError(f"KMeans precision must be 'auto', 'bf16', 'exact' or 'screen', got {precision!r}")
+        src_prec = x.is_cuda and x.dtype in (torch.float32, torch.float64)
+        screen_ok = (src_prec and not streamed and weights is None and not spherical and
+                     self.screen_applies(d, k))
         if precision == "auto":
             precision = "exact" if (not x.is_cuda or x.dtype in (torch.float32, torch.float64)) else "bf16"
+            if precision == "exact" and screen_ok and os.environ.get("CML_KMEANS_SCREEN", "1") != "0":
+                precision = "screen"
         if streamed:
             precision = "bf16"
-        if precision == "exact" and x.is_cuda and x.dtype not in (torch.float32, torch.float64):
-            raise ValueError(f"precision 'exact' needs f32/f64 rows, got {x.dtype}")
+        if precision in ("exact", "screen") and x.is_cuda and x.dtype not in (torch.float32, torch.float64):
+            raise ValueError(f"precision {precision!r} needs f32/f64 rows, got {x.dtype}")
+        if precision == "screen" and not screen_ok:
+            precision = "exact"  # (weights, cosine, or no K9r plan at this width: the plain exact kernels)
         self.precision = precision
-        exact_dev = x.is_cuda and precision == "exact"
+        self._screen = precision == "screen"
+        exact_dev = x.is_cuda and precision in ("exact", "screen")
         if exact_dev:
             prune = False  # the reference algorithm (the torch bounds form would need host syncs anyway)
         if prune is None:  # default on GPU rows: exact pruned steps (CML_KMEANS_PRUNE=0 turns them off)
@@ -261,6 +272,11 @@ class LloydEngine:
         elif self.gpu:
             self.x = to_device_matrix(x, d)
             self.dp = self.x.shape[1]
+        elif self._screen:
+            # source rows kept as given (f32 / f64): the exact kernels read them, the screen its bf16 copy
+            self.x = x[:, :d] if x[:, :d].is_contiguous() else x[:, :d].contiguous()
+            self.dp = d
+            self._scr = None
         else:
             self.x = x[:, :d].to(torch.float64)
             self.dp = d
@@ -624,7 +640,133 @@ class LloydEngine:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
         self._shift2 = self.shift2
 
+    # ------------------------------------------------------------------ MFMA-screened exact assignment
+    @staticmethod
+    def screen_applies(d: int, k: int) -> bool:
+        """A K9r plan (every centre in one launch) exists for the bf16 copy of d-wide rows and k centres."""
+        dp = padded_dim(d)
+        if dp not in (128, 256, 512):
+            return False
+        p = K.plan_assign(1, dp, k)
+        return p.rr_ct > 0 and p.kc == p.kp
+
+    def _screen_state(self):
+        """The screen's buffers: the bf16 copy of the rows with each row's rounding error (cached on the
+        source tensor while it is unmodified), its f32 norms, bf16 centres, bounds, candidate list."""
+        if self._scr is not None:
+            return self._scr
+        n, d, dev = self.n, self.d, self.device
+        dp = padded_dim(d)
+        ent = getattr(self.x, "_cml_screen", None)
+        if ent is not None and ent[0] == self.x._version and ent[1] == (n, d):
+            xb, ex = ent[2], ent[3]
+        else:
+            xb, ex = K.to_bf16_err(self.x, d, dp)
+            try:
+                self.x._cml_screen = (self.x._version, (n, d), xb, ex)
+            except (AttributeError, RuntimeError):
+                pass
+        st = types.SimpleNamespace(xb=xb, ex=ex, dp=dp, tau=self.prune_tau(dp))
+        st.xn = cached_row_sqnorm(xb, n, dp) if n else torch.zeros(1, dtype=torch.float32, device=dev)
+        st.rr_max = 0
+        for c in (320, 256, 192, 128, 64):
+            p = K.plan_assign(1, dp, c)
+            if p.rr_ct > 0 and p.kc == p.kp:
+                st.rr_max = c
+                break
+        kp = round_up(max(st.rr_max, self.k), 32)
+        st.cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
+        st.cn = torch.zeros(kp, dtype=torch.float32, device=dev)
+        st.ub = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        st.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
+        st.lst = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        st.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        st.rechecked = []  # uncertified rows per screened pass, read only when track_prune is set
+        self._scr = st
+        return st
+
+    def _screen_labels(self, C: torch.Tensor, lab: torch.Tensor, best: Optional[torch.Tensor] = None) -> None:
+        """Exact f64 argmin labels (lowest index on ties) of every local row against the f64 centres C
+        (at most one K9r launch of them), screened on MFMA: K9r mode 1 on the bf16 copy gives each row's
+        bf16 label with bounds ub >= its distance and lb <= every other distance (f32 rounding inside);
+        the exact distances differ from the bf16 ones by at most ||x - bf16(x)|| + ||c - bf16(c)||, so a row
+        with lb - ub > 2·(err_x + max err_c) has that label exactly; the others are re-assigned in f64
+        (exact_assign over the listed rows). ``best`` (f64 [n], optional) receives the exact squared distance
+        to the label (exact_dist: the exact kernel's fold, the same bits)."""
+        st = self._screen_state()
+        n, d, kc = self.n, self.d, int(C.shape[0])
+        if n == 0:
+            return
+        C = C.to(device=self.device, dtype=torch.float64).contiguous()
+        kp = round_up(kc, 32)
+        st.cb[:kp].zero_()
+        st.cn[:kp].zero_()
+        K.update_centers(None, kc, d, C.clone(), st.cb[:kp], st.dp, kp, st.cn[:kp], None)
+        mc = st.cn[:kc].max().reshape(1)
+        ecmax = ((C - st.cb[:kc, :d].to(torch.float64)) ** 2).sum(1).max().sqrt().reshape(1) * (1.0 + 1e-9)
+        plan = K.plan_assign(n, st.dp, kc)
+        K.assign_rr_ext(1, st.xb, n, st.dp, st.cb[:kp], st.cn[:kp], plan, st.xn, lab, None, st.ub, st.lb, mc, st.tau)
+        st.cnt.zero_()
+        K.screen_cert(st.ub, st.lb, st.ex, ecmax, n, st.lst, st.cnt)
+        if best is not None:
+            K.exact_dist(self.x, C, lab, best)
+        K.exact_assign(self.x, C, labels=lab, idx=st.lst, n_dev=st.cnt,
+                       best=best if best is not None else self._scr_best())
+        if self.track_prune:
+            st.rechecked.append(int(st.cnt.item()))
+
+    def _scr_best(self) -> torch.Tensor:
+        if getattr(self, "_scr_scratch", None) is None:
+            self._scr_scratch = torch.empty(max(self.n, 1), dtype=torch.float64, device=self.device)
+        return self._scr_scratch
+
+    def _screen_min_dist(self, cands: torch.Tensor):
+        """_min_dist_idx of the screen: (exact f64 squared distance to the nearest candidate, its index) of
+        every local row, candidates in K9r-sized chunks merged in order with strict < (the first index on
+        ties, as one exact assignment over the whole list)."""
+        st = self._screen_state()
+        n, dev = self.n, self.device
+        cands = cands.to(device=dev, dtype=torch.float64)
+        best = torch.full((max(n, 1),), math.inf, dtype=torch.float64, device=dev)
+        lab = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
+        lab_c = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        best_c = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+        step = max(1, st.rr_max)
+        for c0 in range(0, int(cands.shape[0]), step):
+            C = cands[c0:c0 + step]
+            self._screen_labels(C, lab_c, best_c)
+            better = best_c[:n] < best[:n]
+            best[:n] = torch.where(better, best_c[:n], best[:n])
+            lab[:n] = torch.where(better, lab_c[:n].long() + c0, lab[:n])
+        return best[:n], lab[:n]
+
+    def _step_screen(self):
+        """One exact Lloyd iteration with the MFMA-screened assignment (the exact path's labels, sums and
+        centres bit for bit); the cost of the assignment is evaluated on first read (exact_dist)."""
+        n, k = self.n, self.k
+        if getattr(self, "_lab32", None) is None:
+            self._lab32 = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
+        lab = self._lab32
+        self._screen_labels(self.centers, lab)
+        sums, counts = K.sums_reference(self.x, lab[:n], k)
+        msg = torch.cat([sums.reshape(-1), counts, torch.zeros(1, dtype=torch.float64, device=self.device)])
+        self.comm.allreduce_(msg)
+        c_used, lab_used = self.centers.clone(), lab[:n].clone()
+        self._update_cpu(msg)
+        self.labels = lab[:n].long()
+
+        def cost():
+            b = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+            if n:
+                K.exact_dist(self.x, c_used, lab_used, b)
+            tot = b[:n].sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=self.device)
+            self.comm.allreduce_(tot)
+            return tot[0]
+        self._cost_fn = cost
+
     def _step_cpu(self):
+        if self._screen:
+            return self._step_screen()
         labels, best = K.assign_reference(self.x, self.centers)
         if self.w is not None:
             aug, _ = K.sums_reference(self._wx, labels, self.k)
@@ -1295,6 +1437,8 @@ class LloydEngine:
 
     def _min_dist_idx(self, cands: torch.Tensor):
         """(squared distance to the nearest of `cands` as f64, its index) of every local row."""
+        if self._screen:
+            return self._screen_min_dist(cands)
         if not self.gpu:
             lab, best = K.assign_reference(self.x, cands)
             return best, lab

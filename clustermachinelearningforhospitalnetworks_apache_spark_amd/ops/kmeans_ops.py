@@ -96,7 +96,11 @@ _native.register_kernel_sigs({
                                 c_vp]),
 })
 _native.register_kernel_sigs({
-    "cml_kmeans_exact_assign": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_exact_assign": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp]),
+    "cml_kmeans_exact_dist": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_ll, c_vp, c_vp]),
+    "cml_kmeans_to_bf16_err": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_ll, c_vp, c_vp]),
+    "cml_kmeans_screen_cert": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_exact_chunks": (c_ll, [c_ll]),
     "cml_kmeans_exact_segsum": (c_int, [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
 })
@@ -783,9 +787,12 @@ def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor
 # ----------------------------------------------------------------------------------------------
 
 def exact_assign(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor | None = None,
-                 changed: torch.Tensor | None = None, stream=None):
+                 changed: torch.Tensor | None = None, stream=None, idx: torch.Tensor | None = None,
+                 n_dev: torch.Tensor | None = None, best: torch.Tensor | None = None):
     """(labels int32, squared distance f64) of device f32/f64 rows against f64 centres in f64
-    (``kmeans_exact.hip``): the source-precision assignment (ties: lowest centre index)."""
+    (``kmeans_exact.hip``): the source-precision assignment (ties: lowest centre index). With ``idx`` /
+    ``n_dev`` (int32 row list, device count) only the listed rows are assigned, into ``labels`` /
+    ``best`` at their real positions."""
     n, d = int(x.shape[0]), int(centers.shape[1])
     if x.dtype not in (torch.float32, torch.float64):
         x = x.to(torch.float64)
@@ -793,11 +800,47 @@ def exact_assign(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor | 
         x = x.contiguous()
     c = centers.to(device=x.device, dtype=torch.float64).contiguous()
     lab = labels if labels is not None else torch.zeros(max(n, 1), dtype=torch.int32, device=x.device)
-    best = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
+    if best is None:
+        best = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
     _native.check(_native.kernels().cml_kmeans_exact_assign(
         x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), int(c.shape[0]),
-        lab.data_ptr(), best.data_ptr(), _ptr(changed), _native.stream_ptr(stream)), "kmeans_exact_assign")
+        lab.data_ptr(), best.data_ptr(), _ptr(changed), _ptr(idx), _ptr(n_dev), _native.stream_ptr(stream)),
+        "kmeans_exact_assign")
     return lab[:n], best[:n]
+
+
+def exact_dist(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor, best: torch.Tensor, lab_off: int = 0,
+               stream=None) -> None:
+    """best[r] = f64 Σ_t (x_t - c_{labels[r] - lab_off, t})² with exact_assign's fold (same bits)."""
+    n, d = int(x.shape[0]), int(centers.shape[1])
+    c = centers.to(device=x.device, dtype=torch.float64).contiguous()
+    if labels.dtype != torch.int32 or best.dtype != torch.float64:
+        raise ValueError("exact_dist: int32 labels, f64 best")
+    _native.check(_native.kernels().cml_kmeans_exact_dist(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), labels.data_ptr(),
+        int(lab_off), best.data_ptr(), _native.stream_ptr(stream)), "kmeans_exact_dist")
+
+
+def to_bf16_err(x: torch.Tensor, d: int, ldo: int, stream=None):
+    """(bf16 [n, ldo] zero-padded copy, f32 [n] upper bounds of ||x_r - bf16(x_r)||) of device f32/f64 rows."""
+    n = int(x.shape[0])
+    out = torch.empty((max(n, 1), ldo), dtype=torch.bfloat16, device=x.device)
+    err = torch.empty(max(n, 1), dtype=torch.float32, device=x.device)
+    _native.check(_native.kernels().cml_kmeans_to_bf16_err(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(d), out.data_ptr(), int(ldo), err.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_to_bf16_err")
+    return out[:n] if n else out[:0], err
+
+
+def screen_cert(ub: torch.Tensor, lb: torch.Tensor, err: torch.Tensor, ecmax: torch.Tensor, n: int,
+                lst: torch.Tensor, count: torch.Tensor, stream=None) -> None:
+    """Append to ``lst`` the rows whose bf16-screen label is not certified (lb - ub <= 2·(err + ecmax));
+    ``count`` (int32 [1], zeroed by the caller) receives their number."""
+    if ecmax.dtype != torch.float64 or lst.dtype != torch.int32 or lst.numel() < n:
+        raise ValueError("screen_cert: f64 ecmax, int32 list of n entries")
+    _native.check(_native.kernels().cml_kmeans_screen_cert(
+        ub.data_ptr(), lb.data_ptr(), err.data_ptr(), ecmax.data_ptr(), int(n), lst.data_ptr(), count.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_screen_cert")
 
 
 def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = None, stream=None):
