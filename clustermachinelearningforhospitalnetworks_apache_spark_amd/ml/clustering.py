@@ -233,8 +233,14 @@ class KMeansModel(Model):
         return assign_reference(x, c)
 
     def _transform(self, df):
-        lab, _ = self._assign(df)
-        return _replace_col(df, self.getPredictionCol(), ColumnData(lab.to(torch.int32), None, T.IntegerType()))
+        """The prediction column is lazy (sql/column.py LazyColumnData): assigned on first read, never
+        when nothing downstream reads it (a Pipeline stage whose output the next stage ignores)."""
+        from ..sql.column import LazyColumnData
+
+        def thunk():
+            lab, _ = self._assign(df)
+            return lab.to(torch.int32), None
+        return _replace_col(df, self.getPredictionCol(), LazyColumnData(thunk, df._nrows, T.IntegerType()))
 
     def computeCost(self, df) -> float:
         _, dist = self._assign(df)

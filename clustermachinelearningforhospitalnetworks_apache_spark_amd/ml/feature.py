@@ -31,6 +31,9 @@ def features_dtype(session) -> torch.dtype:
             "bfloat16": torch.bfloat16, "bf16": torch.bfloat16}[str(name).lower()]
 
 
+_NAN_MSG = "VectorAssembler: encountered NaN values with handleInvalid='error'"
+
+
 class VectorAssembler(Transformer):
     _params = {
         "inputCols": (NO_DEFAULT, "input column names", "liststr"),
@@ -58,15 +61,14 @@ class VectorAssembler(Transformer):
             # one dense vector input already in the target dtype: the assembled matrix IS the input
             # (no 2x HBM footprint for 100+ GB shards); only the invalid-value check reads it
             x = cds[0].values
+            out = ColumnData(x, None, T.VectorUDT())
             if hi == "error" and df._nrows and x.is_floating_point():
-                if x.is_cuda:
-                    from ..ops import frame_ops
-                    bad_any = frame_ops.has_nan(x)
-                else:
-                    bad_any = bool(torch.isnan(x).any().item())
-                if bad_any:
-                    raise ValueError("VectorAssembler: encountered NaN values with handleInvalid='error'")
-            return self._named(df, _replace_col(df, self.getOutputCol(), ColumnData(x, None, T.VectorUDT())))
+                # Spark raises handleInvalid="error" when the assembled rows are consumed (its transform
+                # is lazy); the check is deferred to the first consumer (DataFrame._feature_matrix), and
+                # a consumer whose own pass over the rows already exposes a NaN takes it over for free
+                # (StandardScaler.fit: the moments) — no extra read of a 100+ GB matrix here
+                out.nan_pending = _NAN_MSG
+            return self._named(df, _replace_col(df, self.getOutputCol(), out))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags
             from ..ops import frame_ops
@@ -141,7 +143,9 @@ class StandardScaler(Estimator):
             self._defaultParamMap["outputCol"] = self.uid + "__output"
 
     def _fit(self, df):
-        x = df._feature_matrix(self.getInputCol())
+        col = self.getInputCol()
+        pending = df._pending_nan_check(col)
+        x = df._feature_matrix(col, defer_nan_check=True)
         d = x.shape[1]
         n, s1, s2, shift = glm_ops.moments(x, d)
         comm = df._comm
@@ -156,6 +160,12 @@ class StandardScaler(Estimator):
         t2 = s2 + 2 * delta * s1 + n * delta * delta
         msg = torch.cat([torch.tensor([float(n)], dtype=torch.float64, device=x.device), t1, t2])
         comm.allreduce_(msg)
+        if pending is not None:
+            # the moments carry any NaN of the rows (every rank sees the all-reduced sums): only then the
+            # exact check runs (a NaN sum can also come from +inf and -inf in one column)
+            if bool(torch.isnan(msg).any().item()):
+                df._run_nan_check(col)
+            df._clear_nan_check(col)
         N = msg[0].item()
         T1, T2 = msg[1:1 + d], msg[1 + d:]
         mean = common_t + T1 / max(N, 1)

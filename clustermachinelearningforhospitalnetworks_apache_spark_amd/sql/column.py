@@ -54,7 +54,8 @@ class ColumnData:
                               None if self.codes is None else self.codes[ii])
         ti = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=self.values.device)
         ti = ti.to(self.values.device)
-        return ColumnData(self.values[ti], None if self.valid is None else self.valid[ti], self.dtype)
+        return self._keep_checks(ColumnData(self.values[ti], None if self.valid is None else self.valid[ti],
+                                            self.dtype))
 
     def mask(self, m) -> "ColumnData":
         if self.is_host:
@@ -63,7 +64,65 @@ class ColumnData:
                               None if self.codes is None else self.codes[mm])
         mm = m if isinstance(m, torch.Tensor) else torch.as_tensor(m, device=self.values.device)
         mm = mm.to(self.values.device)
-        return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype)
+        return self._keep_checks(ColumnData(self.values[mm], None if self.valid is None else self.valid[mm],
+                                            self.dtype))
+
+    def _keep_checks(self, out: "ColumnData") -> "ColumnData":
+        """A row subset inherits a deferred NaN check (VectorAssembler handleInvalid="error")."""
+        pend = getattr(self, "nan_pending", None)
+        if pend:
+            out.nan_pending = pend
+        return out
+
+
+class LazyColumnData(ColumnData):
+    """A device column computed on first access of its values (Spark evaluates ``transform`` lazily): a
+    Pipeline stage's prediction column that no later stage reads — KMeansModel's cluster ids before a
+    LogisticRegression — is never computed. ``thunk()`` returns (values tensor, valid or None); the row
+    count is known up front, so schema work, row counts and column projections never trigger it."""
+
+    def __init__(self, thunk, n: int, dtype: T.DataType):
+        self._thunk = thunk
+        self._n = int(n)
+        self.dtype = dtype
+        self.codes = None
+        self._values = None
+        self._valid = None
+
+    def _force(self):
+        if self._thunk is not None:
+            v, ok = self._thunk()
+            self._values, self._valid, self._thunk = v, ok, None
+
+    @property
+    def values(self):
+        self._force()
+        return self._values
+
+    @values.setter
+    def values(self, v):
+        self._thunk, self._values = None, v
+
+    @property
+    def valid(self):
+        self._force()
+        return self._valid
+
+    @valid.setter
+    def valid(self, v):
+        self._force()
+        self._valid = v
+
+    @property
+    def is_host(self) -> bool:
+        return False
+
+    @property
+    def computed(self) -> bool:
+        return self._thunk is None
+
+    def __len__(self):
+        return self._n
 
 
 class DictColumnData(ColumnData):

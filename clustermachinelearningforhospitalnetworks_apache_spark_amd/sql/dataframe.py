@@ -644,12 +644,44 @@ class DataFrame(DataFrameMoreMixin):
         return func(self, *args, **kwargs)
 
     # ------------------------------------------------------------------------------------------ device helpers
-    def _feature_matrix(self, col: str) -> torch.Tensor:
-        """The [n, d] tensor of a vector column (row-major, device-resident)."""
+    def _feature_matrix(self, col: str, defer_nan_check: bool = False) -> torch.Tensor:
+        """The [n, d] tensor of a vector column (row-major, device-resident). A NaN check a producer
+        deferred to its consumers (VectorAssembler handleInvalid="error") runs here, once, unless the
+        caller takes it over (``defer_nan_check``: it calls _run_nan_check / _clear_nan_check)."""
         cd = self._cols[col]
         if not isinstance(cd.dtype, T.VectorUDT):
             raise TypeError(f"column {col!r} is {cd.dtype.simpleString()}, expected vector")
+        if not defer_nan_check and getattr(cd, "nan_pending", None):
+            self._run_nan_check(col)
+            cd.nan_pending = None
         return cd.values
+
+    def _pending_nan_check(self, col: str):
+        return getattr(self._cols[col], "nan_pending", None)
+
+    def _run_nan_check(self, col: str) -> None:
+        """Raise the deferred handleInvalid error when a row of the column holds a NaN on any rank."""
+        cd = self._cols[col]
+        msg = getattr(cd, "nan_pending", None)
+        if not msg:
+            return
+        x = cd.values
+        if not x.numel():
+            bad = False
+        elif x.is_cuda:
+            from ..ops import frame_ops
+            bad = bool(frame_ops.has_nan(x))
+        else:
+            bad = bool(torch.isnan(x).any().item())
+        if self._comm.is_distributed:
+            bad = self._comm.max_scalar(1.0 if bad else 0.0) > 0
+        if bad:
+            raise ValueError(msg)
+
+    def _clear_nan_check(self, col: str) -> None:
+        cd = self._cols[col]
+        if getattr(cd, "nan_pending", None):
+            cd.nan_pending = None
 
     def _numeric(self, col: str, dtype=torch.float64) -> torch.Tensor:
         cd = self._cols[col]

@@ -1,0 +1,43 @@
+"""VectorAssembler(handleInvalid="error") on one dense vector column aliases it and defers the NaN check
+to the consumer (Spark's transform is lazy and raises when rows are consumed): StandardScaler.fit takes
+it over from its moments (no extra read), other estimators run it in _feature_matrix, row subsets
+(randomSplit) inherit it, and a clean column never raises."""
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.clustering import KMeans
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import StandardScaler, VectorAssembler
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+
+
+def _frame(nan_row=None):
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    g = torch.Generator().manual_seed(0)
+    x = torch.randn(2000, 6, generator=g, dtype=torch.float64)
+    if nan_row is not None:
+        x[nan_row, 2] = float("nan")
+    spark.conf.set("cml.ml.features.dtype", "float64")
+    return spark.createDataFrameFromTensors({"raw": x})
+
+
+def test_clean_column_passes_and_aliases():
+    df = _frame()
+    out = VectorAssembler(inputCols=["raw"], outputCol="f").transform(df)
+    assert out._feature_matrix("f").data_ptr() == df._feature_matrix("raw").data_ptr()
+    StandardScaler(inputCol="f", outputCol="s").fit(out)
+    KMeans(k=3, seed=1, maxIter=3).fit(out.withColumnRenamed("f", "features"))
+
+
+@pytest.mark.parametrize("consumer", ["scaler", "kmeans", "split"])
+def test_nan_raises_at_the_consumer(consumer):
+    df = _frame(nan_row=1234)
+    out = VectorAssembler(inputCols=["raw"], outputCol="features").transform(df)  # no raise yet
+    with pytest.raises(ValueError, match="handleInvalid='error'"):
+        if consumer == "scaler":
+            StandardScaler(inputCol="features", outputCol="s").fit(out)
+        elif consumer == "kmeans":
+            KMeans(k=3, seed=1, maxIter=3).fit(out)
+        else:
+            a, b = out.randomSplit([0.5, 0.5], seed=3)
+            part = a if bool(torch.isnan(a._cols["features"].values).any()) else b
+            KMeans(k=3, seed=1, maxIter=3).fit(part)
