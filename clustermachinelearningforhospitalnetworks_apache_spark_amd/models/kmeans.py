@@ -1433,7 +1433,7 @@ class LloydEngine:
             return self.x[idx.long().cpu(), : self.d].to(torch.float64).to(self.device)
         if self.gpu:
             return self.x[idx.long(), : self.d].to(torch.float64)
-        return self.x[idx.long()]
+        return self.x[idx.long()].to(torch.float64)  # (the screen keeps f32 source rows)
 
     def _min_dist_idx(self, cands: torch.Tensor):
         """(squared distance to the nearest of `cands` as f64, its index) of every local row."""

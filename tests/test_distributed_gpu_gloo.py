@@ -155,3 +155,58 @@ def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch, use_gra
     np.testing.assert_array_equal(np.asarray(res["init"]), np.asarray(ref["init"]))
     np.testing.assert_array_equal(np.asarray(res["centers"]), np.asarray(ref["centers"]))
     assert abs(res["cost"] - ref["cost"]) <= 1e-9 * abs(ref["cost"])
+
+
+# ---- four ranks, uneven shards: one rank with no rows, one with fewer rows than one K9r round (64),
+# and one whose candidate cap is tiny (its pruned steps and its seeded first step fall back to the full
+# pass while the others run candidate passes: the collectives must line up all the same)
+
+_SPLITS4 = [0, 0, 37, 120_000, N2]  # rank r holds rows [_SPLITS4[r], _SPLITS4[r + 1])
+
+
+def _rank_main4(rank, world, port, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1"})
+    import torch
+    import torch.distributed as dist
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
+    if rank == 2:
+        LloydEngine._PRUNE_CAP = 1e-4  # this rank's steps take the full-pass branch
+    x = _data2()
+    res = _fit2(x[_SPLITS4[rank]:_SPLITS4[rank + 1]], comm, use_graph=False)
+    res["rows"] = _SPLITS4[rank + 1] - _SPLITS4[rank]
+    with open(f"{out_path}.{rank}", "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_four_uneven_ranks_with_an_empty_one_match_single_rank(tmp_path, monkeypatch):
+    """the default device path (pruned k-means|| init, seeded step, pruned steps) on
+    four gloo ranks sharing the GPU — an empty rank, a 37-row rank, a rank forced onto the _PRUNE_CAP
+    fallback — gives the single-rank fit bit for bit."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
+    monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
+    out = str(tmp_path / "w4")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main4, args=(r, 4, port, out)) for r in range(4)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [json.load(open(f"{out}.{r}")) for r in range(4)]
+    ref = _fit2(_data2(), local_comm(), use_graph=False)
+    for r in range(4):
+        assert res[r]["rows"] == _SPLITS4[r + 1] - _SPLITS4[r]
+        np.testing.assert_array_equal(np.asarray(res[r]["init"]), np.asarray(ref["init"]))
+        np.testing.assert_array_equal(np.asarray(res[r]["centers"]), np.asarray(ref["centers"]))
+        assert abs(res[r]["cost"] - ref["cost"]) <= 1e-9 * abs(ref["cost"])
+    # the capped rank took the full-pass branch, the big rank pruned
+    assert any(full for full, _ in res[2]["hist"]), res[2]["hist"]
+    assert any(not full for full, _ in res[3]["hist"][1:]), res[3]["hist"]
