@@ -79,6 +79,74 @@ __global__ __launch_bounds__(kThreads) void exact_assign_kernel(const T* __restr
   }
 }
 
+// Wide rows (d > 16): the same per-centre fold (t ascending, fma from 0.0, strict < over centres in
+// index order — the same bits as exact_assign_kernel and the host twin), register-blocked over KA
+// centres: a row is read once per KA centres of the LDS tile instead of once per centre (the DREG = 0
+// form re-read the row from L2 for every centre: the screen's f64 re-check ran at a fraction of the
+// memory rate on 128+-wide rows).
+template <typename T, int KA, int DC>
+__global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(const T* __restrict__ X, long long n,
+                                                                     long long ldx, int d,
+                                                                     const double* __restrict__ C, int k, int kt,
+                                                                     int* __restrict__ labels,
+                                                                     double* __restrict__ best,
+                                                                     int* __restrict__ changed,
+                                                                     const int* __restrict__ idx,
+                                                                     const int* __restrict__ n_dev) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* ct = reinterpret_cast<double*>(smem);  // [kt][d]
+  const long long t0 = (long long)blockIdx.x * kThreads + threadIdx.x;
+  const long long cnt = n_dev != nullptr ? (long long)*n_dev : n;
+  if ((long long)blockIdx.x * kThreads >= cnt) return;
+  const bool live = t0 < cnt && t0 < n;
+  const long long r = live ? (idx != nullptr ? (long long)idx[t0] : t0) : 0;
+  const T* xrow = X + r * ldx;
+  double bd = __builtin_huge_val();
+  int bi = 0;
+  for (int c0 = 0; c0 < k; c0 += kt) {
+    const int kc = min(kt, k - c0);
+    __syncthreads();
+    for (int e = threadIdx.x; e < kc * d; e += kThreads) ct[e] = C[(long long)c0 * d + e];
+    __syncthreads();
+    if (!live) continue;
+    for (int j0 = 0; j0 < kc; j0 += KA) {
+      double acc[KA];
+#pragma unroll
+      for (int a = 0; a < KA; ++a) acc[a] = 0.0;
+      for (int tb = 0; tb < d; tb += DC) {
+        double xv[DC];
+#pragma unroll
+        for (int u = 0; u < DC; ++u) xv[u] = tb + u < d ? (double)xrow[tb + u] : 0.0;
+#pragma unroll
+        for (int a = 0; a < KA; ++a) {
+          if (j0 + a < kc) {
+            const double* cj = ct + (long long)(j0 + a) * d + tb;
+#pragma unroll
+            for (int u = 0; u < DC; ++u) {
+              if (tb + u < d) {
+                const double e = xv[u] - cj[u];
+                acc[a] = __fma_rn(e, e, acc[a]);
+              }
+            }
+          }
+        }
+      }
+#pragma unroll
+      for (int a = 0; a < KA; ++a) {
+        if (j0 + a < kc && acc[a] < bd) {  // centres ascending: strict < keeps the lowest index
+          bd = acc[a];
+          bi = c0 + j0 + a;
+        }
+      }
+    }
+  }
+  if (live) {
+    if (changed != nullptr && labels[r] != bi) atomicAdd(changed, 1);
+    labels[r] = bi;
+    best[r] = bd;
+  }
+}
+
 // best[r] = the f64 fold Σ_t (x_t - c_lab,t)² of exact_assign_kernel for row r against its label's
 // centre only (the same operations in the same order, so the same bits as the full assignment's
 // minimum when the label is the argmin): the distances of rows the bf16 screen certified.
@@ -177,17 +245,31 @@ __global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restri
   const int ca = c;
   double acc = 0.0;
   long long next = seg[c + 1];
-  for (long long p = p0; p < p1; ++p) {
-    while (p >= next) {  // cluster c ended: first one -> slot A, a middle one is complete
-      if (col < d) {
-        if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
-        else S[(long long)c * d + col] = acc;
-      }
-      acc = 0.0;
-      ++c;
-      next = seg[c + 1];
+  // PF positions' rows are loaded before any of them is added (the adds keep their order: same bits):
+  // the fold's latency chain no longer serialises the gathers
+  constexpr int PF = 8;
+  for (long long pb = p0; pb < p1; pb += PF) {
+    double v[PF];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const long long p = pb + u;
+      v[u] = (p < p1 && col < d) ? (double)X[(long long)perm[p] * ldx + col] : 0.0;
     }
-    if (col < d) acc += (double)X[(long long)perm[p] * ldx + col];
+#pragma unroll
+    for (int u = 0; u < PF; ++u) {
+      const long long p = pb + u;
+      if (p >= p1) break;
+      while (p >= next) {  // cluster c ended: first one -> slot A, a middle one is complete
+        if (col < d) {
+          if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
+          else S[(long long)c * d + col] = acc;
+        }
+        acc = 0.0;
+        ++c;
+        next = seg[c + 1];
+      }
+      if (col < d) acc += v[u];
+    }
   }
   if (col < d) {
     if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
@@ -241,16 +323,20 @@ CML_API int cml_kmeans_exact_assign(const void* X, int xf64, long long n, long l
 #define CML_EA(T, R)                                                                                        \
   hipLaunchKernelGGL((exact_assign_kernel<T, R>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, k, kt, \
                      labels, best, changed, idx, n_dev)
+#define CML_EW(T)                                                                                          \
+  hipLaunchKernelGGL((exact_assign_wide_kernel<T, 16, 8>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, \
+                     k, kt, labels, best, changed, idx, n_dev)
   if (xf64) {
     if (d <= 4) CML_EA(double, 4);
     else if (d <= 16) CML_EA(double, 16);
-    else CML_EA(double, 0);
+    else CML_EW(double);
   } else {
     if (d <= 4) CML_EA(float, 4);
     else if (d <= 16) CML_EA(float, 16);
-    else CML_EA(float, 0);
+    else CML_EW(float);
   }
 #undef CML_EA
+#undef CML_EW
   return cml_status();
 }
 

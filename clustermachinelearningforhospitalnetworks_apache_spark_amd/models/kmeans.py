@@ -753,7 +753,7 @@ class LloydEngine:
         self.comm.allreduce_(msg)
         c_used, lab_used = self.centers.clone(), lab[:n].clone()
         self._update_cpu(msg)
-        self.labels = lab[:n].long()
+        self.labels = lab[:n]
 
         def cost():
             b = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)

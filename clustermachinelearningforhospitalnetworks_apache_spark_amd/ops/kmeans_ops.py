@@ -850,12 +850,16 @@ def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = No
     d = int(x.shape[1]) if d is None else d
     if x.dtype not in (torch.float32, torch.float64):
         x = x.to(torch.float64)
-    lab = labels[:n].long()
-    counts = torch.bincount(lab, minlength=k)[:k] if n else torch.zeros(k, dtype=torch.int64, device=x.device)
+    lab = labels[:n]
+    lab = lab if lab.dtype == torch.int32 and lab.is_contiguous() else lab.to(torch.int32).contiguous()
+    counts = torch.zeros(k, dtype=torch.int32, device=x.device)
+    if n:
+        int_hist(lab, n, k, counts)  # exact int32 counts, no host read (bincount syncs)
     seg = torch.zeros(k + 1, dtype=torch.int32, device=x.device)
-    seg[1:] = torch.cumsum(counts, 0).to(torch.int32)
+    seg[1:] = torch.cumsum(counts, 0, dtype=torch.int32)
+    # stable sort of the int32 labels (the row order within a cluster is the fold order)
     perm = torch.sort(lab, stable=True).indices.to(torch.int32) if n else torch.zeros(1, dtype=torch.int32,
-                                                                                         device=x.device)
+                                                                                        device=x.device)
     lib = _native.kernels()
     nch = max(1, int(lib.cml_kmeans_exact_chunks(n)))
     slots = torch.empty(2 * nch * d, dtype=torch.float64, device=x.device)

@@ -155,9 +155,10 @@ class Communicator:
         if not self.is_distributed:
             return t.reshape((1,) + tuple(t.shape))
         src = t.contiguous()
-        out = torch.empty((self.world_size,) + tuple(src.shape), dtype=src.dtype, device=src.device)
-        dist.all_gather_into_tensor(self._coerce(out), src, group=self.group)
-        return out
+        # a flat [world · numel] output: the layout every backend accepts (gloo rejects a stacked one)
+        out = torch.empty(self.world_size * src.numel(), dtype=src.dtype, device=src.device)
+        dist.all_gather_into_tensor(self._coerce(out), src.reshape(-1), group=self.group)
+        return out.view((self.world_size,) + tuple(src.shape))
 
     def allgather_sized(self, t: torch.Tensor, sizes: List[int]) -> torch.Tensor:
         """Concatenation in rank order of every rank's ``t`` whose row counts ``sizes`` every rank already
