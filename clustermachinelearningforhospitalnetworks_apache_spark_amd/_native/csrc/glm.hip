@@ -794,9 +794,12 @@ inline int pow2ceil(int v) {
   while (p < v) p <<= 1;
   return p;
 }
+int g_fp8_nch = 0;  // ablation: chunks per lane of the fp8 (16 values / chunk) streaming layout, 0 = auto
+
 inline bool stream_layout(int d, int cpt, int& lpr, int& nch) {
   const int ch = (d + cpt - 1) / cpt;
-  const int want = 16 / cpt > 0 ? 16 / cpt : 1;
+  int want = 16 / cpt > 0 ? 16 / cpt : 1;
+  if (cpt == 16 && g_fp8_nch > 0) want = g_fp8_nch;
   nch = ch < want ? pow2ceil(ch) : want;
   lpr = pow2ceil((ch + nch - 1) / nch);
   if (lpr > 64) {
@@ -874,6 +877,11 @@ int resident_blocks(K kernel, size_t lds = 0) {
     nb = 1;
   }
   return nb;
+}
+
+CML_API int cml_glm_set_fp8_nch(int v) {
+  g_fp8_nch = v;
+  return 0;
 }
 
 CML_API int cml_glm_set_logreg_unroll(int u) {

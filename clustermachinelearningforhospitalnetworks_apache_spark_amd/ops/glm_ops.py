@@ -18,6 +18,7 @@ from ..utils.device import num_cus
 _native.register_kernel_sigs({
     "cml_glm_grid": (c_int, [c_ll, c_int, c_int, c_int, c_int]),
     "cml_glm_set_logreg_unroll": (c_int, [c_int]),
+    "cml_glm_set_fp8_nch": (c_int, [c_int]),
     "cml_col_moments": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_scale_apply": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_vp]),
     "cml_logreg_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
@@ -317,3 +318,8 @@ def set_logreg_unroll(u: int) -> None:
     """Force K13's rows-in-flight per wave (1 or 2; 0 = automatic) — for ablations."""
     _native.kernels().cml_glm_set_logreg_unroll(int(u))
     _UNROLL[0] = int(u)
+
+
+def set_fp8_nch(v: int) -> None:
+    """Ablation: 16-byte chunks per lane of the fp8 streaming layout (0 = auto)."""
+    _native.kernels().cml_glm_set_fp8_nch(int(v))

@@ -133,6 +133,13 @@ class SparkSession:
         if kind == "gpu" and not self._comm.device.type == "cuda":
             log.warning("master=%s requested GPUs but none is visible; running on CPU", opts.get("spark.master"))
         self._device = self._comm.device
+        self._warmup_s = 0.0
+        if self._device.type == "cuda" and str(opts.get("cml.session.warmup", "true")).lower() not in ("0", "false"):
+            from ..utils.warmup import warm_device
+            try:
+                self._warmup_s = warm_device(self._device, int(float(opts.get("cml.session.poolBytes", 1 << 30))))
+            except Exception as e:  # a warm-up is an optimisation: never fail a session on it
+                log.warning("device warm-up skipped: %s", e)
         self._stopped = False
         self.catalog = Catalog(self)
         from .functions import UDFRegistration

@@ -1,0 +1,52 @@
+"""Device warm-up at GPU session start (session conf ``cml.session.warmup``, default on; ``cml.session.poolBytes``).
+
+The first call of every path pays one-time costs that have nothing to do with its data: the caching
+allocator's first hipMalloc of each size class, the first launch of each kernel of the in-tree library
+and of torch's, library handles. The reference workflow's per-batch retrain (``ref.py:91-106``: na.drop,
+VectorAssembler, LinearRegression per micro-batch) ran 95 ms of na.drop and 20 ms of fit cold against
+5 ms and 0.5 ms warm on 4M rows (profiles/r4/per_batch_retrain_4M_rows.log) — a streaming job pays that
+on its first batch. The session therefore (1) reserves one allocator segment (freed at once, so the
+caching allocator keeps it and splits later requests from it) and (2) runs the frame / GLM / evaluator
+kernels a micro-batch runs once on a few rows, so a session's first batch runs at its warm rate. A
+Spark executor warms its JVM the same way before the first task.
+"""
+from __future__ import annotations
+
+import time
+
+import torch
+
+
+def warm_device(device: torch.device, pool_bytes: int = 1 << 30) -> float:
+    """Warm ``device``; returns the seconds it took (0 on a CPU device)."""
+    if device.type != "cuda":
+        return 0.0
+    t0 = time.perf_counter()
+    if pool_bytes > 0:
+        blk = torch.empty(int(pool_bytes), dtype=torch.uint8, device=device)
+        del blk
+    from ..ops import frame_ops, glm_ops
+    n, d = 4096, 4
+    g = torch.Generator(device=device).manual_seed(0)
+    x = torch.randn(n, d, generator=g, device=device, dtype=torch.float64)
+    xi = (x[:, 0] * 100).to(torch.int32)
+    valid = x[:, 1] > -3.0
+    y = x @ torch.ones(d, dtype=torch.float64, device=device)
+    # na.drop / filter: validity + NaN masks, compaction, row gathers
+    good = valid.to(torch.int32) + (~torch.isnan(x[:, 2])).to(torch.int32)
+    keep = good == 2
+    bool(keep.all())
+    idx = frame_ops.compact(keep)
+    for t in (x[:, 0], xi, valid, x):
+        t[idx]
+    # VectorAssembler (K2) and the GLM / evaluator kernels of a per-batch fit
+    m, bad = frame_ops.assemble([(x[:, j], None) for j in range(d)] + [(xi, valid)], out_dtype=torch.float64)
+    bool(bad.any())
+    glm_ops.gram(m, d + 1, y, None)
+    glm_ops.moments(m, d + 1)
+    glm_ops.linear_predict(m, d + 1, torch.zeros(d + 2, dtype=torch.float64, device=device), "identity")
+    frame_ops.reg_metric_sums(y, y * 0.5)
+    torch.sort(xi, stable=True)
+    torch.unique(xi)
+    torch.cuda.synchronize(device)
+    return time.perf_counter() - t0
