@@ -214,12 +214,18 @@ __global__ __launch_bounds__(256) void kmeans_converge_latch_kernel(const double
 }
 
 // dst <- src (n 32-bit words) unless flags[1] (done) is set: the centres of the last live step's
-// assignment survive the frozen steps (training cost).
+// assignment survive the frozen steps (training cost); dst_always (may be null) <- src every step (the
+// pruned step's cb_old: one launch for both copies).
 __global__ __launch_bounds__(256) void kmeans_cond_copy_kernel(unsigned* __restrict__ dst,
                                                                const unsigned* __restrict__ src, long long n,
-                                                               const int* __restrict__ flags) {
-  if (flags[1] != 0) return;
-  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) dst[i] = src[i];
+                                                               const int* __restrict__ flags,
+                                                               unsigned* __restrict__ dst_always) {
+  const bool live = flags[1] == 0;
+  for (long long i = (long long)blockIdx.x * 256 + threadIdx.x; i < n; i += (long long)gridDim.x * 256) {
+    const unsigned v = src[i];
+    if (dst_always != nullptr) dst_always[i] = v;
+    if (live) dst[i] = v;
+  }
 }
 
 // Centre statistics of the pruned step, part 1 (one workgroup per centre j, over the bf16 centres
@@ -473,14 +479,16 @@ CML_API int cml_kmeans_converge_latch(const double* shift2, int k, double lim, i
 }
 
 // n_bytes a multiple of 4, both pointers 4-byte aligned.
-CML_API int cml_kmeans_cond_copy(void* dst, const void* src, long long n_bytes, const int* flags, void* stream) {
-  if (n_bytes % 4 != 0 || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3)) return (int)hipErrorInvalidValue;
+CML_API int cml_kmeans_cond_copy(void* dst, const void* src, long long n_bytes, const int* flags, void* dst_always,
+                                  void* stream) {
+  if (n_bytes % 4 != 0 || ((uintptr_t)dst & 3) || ((uintptr_t)src & 3) || ((uintptr_t)dst_always & 3))
+    return (int)hipErrorInvalidValue;
   const long long n = n_bytes / 4;
   if (n == 0) return 0;
   long long g = (n + 255) / 256;
   g = g > 1024 ? 1024 : g;
   hipLaunchKernelGGL(kmeans_cond_copy_kernel, dim3((unsigned)g), dim3(256), 0, (hipStream_t)stream, (unsigned*)dst,
-                     (const unsigned*)src, n, flags);
+                     (const unsigned*)src, n, flags, (unsigned*)dst_always);
   return cml_status();
 }
 

@@ -805,7 +805,8 @@ class LloydEngine:
         n, k, d, dev, ap = self.n, self.k, self.d, self.device, self.aplan
         tr = ap.round_rows
         st = types.SimpleNamespace(history=[])
-        st.cap_m = max(tr, int(math.ceil(self._PRUNE_CAP * n)))
+        cap = float(os.environ.get("CML_KMEANS_PRUNE_CAP", self._PRUNE_CAP))  # A/B knob (bench --prune-cap)
+        st.cap_m = max(tr, int(math.ceil(cap * n)))
         st.tau = self.prune_tau(self.dp)
         per_wg = -(-(-(-st.cap_m // tr)) // ap.grid) * tr
         pad = round_up(st.cap_m, tr) + tr
@@ -877,8 +878,8 @@ class LloydEngine:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
         in a tol > 0 fit, the device convergence latch (flags[1])."""
         st, k, d = self._pst, self.k, self.d
-        st.cb_old.copy_(self.cb)
-        K.cond_copy(st.cb_cost, st.cb_old, st.flags)  # frozen steps keep the last live step's centres
+        # cb_old <- cb, and cb_cost <- cb unless converged (frozen steps keep the last live step's centres)
+        K.cond_copy(st.cb_cost, self.cb, st.flags, dst_always=st.cb_old)
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
                        st.c2, st.count, st.force, cum=st.cum)

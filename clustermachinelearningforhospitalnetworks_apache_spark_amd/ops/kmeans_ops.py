@@ -59,7 +59,7 @@ _native.register_kernel_sigs({
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_converge_latch": (c_int, [c_vp, c_int, ctypes.c_double, c_vp, c_vp]),
-    "cml_kmeans_cond_copy": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp]),
+    "cml_kmeans_cond_copy": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
                                        c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
@@ -663,14 +663,19 @@ def converge_latch(shift2: torch.Tensor, k: int, lim: float, flags: torch.Tensor
                   "kmeans_converge_latch")
 
 
-def cond_copy(dst: torch.Tensor, src: torch.Tensor, flags: torch.Tensor, stream=None) -> None:
-    """dst <- src (same size, contiguous) unless flags[1] is set. Device only."""
-    if dst.numel() * dst.element_size() != src.numel() * src.element_size() or not (dst.is_contiguous() and
-                                                                                   src.is_contiguous()):
-        raise ValueError("cond_copy: contiguous tensors of the same size")
-    _native.check(_native.kernels().cml_kmeans_cond_copy(dst.data_ptr(), src.data_ptr(),
-                                                         dst.numel() * dst.element_size(), flags.data_ptr(),
-                                                         _native.stream_ptr(stream)), "kmeans_cond_copy")
+def cond_copy(dst: torch.Tensor, src: torch.Tensor, flags: torch.Tensor, stream=None,
+              dst_always: torch.Tensor | None = None) -> None:
+    """dst <- src (same size, contiguous) unless flags[1] is set; ``dst_always`` <- src in the same launch.
+    Device only."""
+    nb = src.numel() * src.element_size()
+    for t in (dst, dst_always):
+        if t is not None and (t.numel() * t.element_size() != nb or not t.is_contiguous()):
+            raise ValueError("cond_copy: contiguous tensors of the same size")
+    if not src.is_contiguous():
+        raise ValueError("cond_copy: contiguous source")
+    _native.check(_native.kernels().cml_kmeans_cond_copy(dst.data_ptr(), src.data_ptr(), nb, flags.data_ptr(),
+                                                         _ptr(dst_always), _native.stream_ptr(stream)),
+                  "kmeans_cond_copy")
 
 
 def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, mx: torch.Tensor, tau: float,
