@@ -223,6 +223,11 @@ def main():
                             "iteration_ms": [round(1000.0 * t, 3) for t in per_it]}
         if eng.prune:
             acc["breakdown"]["prune_history_rank0"] = eng.prune_history()
+        if getattr(eng, "_scr", None) is not None:  # precision "screen": screened rows re-checked in f64,
+            # then per certified step (rows the bounds no longer proved, rows re-assigned exactly, moves)
+            acc["breakdown"]["screen_rechecked_rank0"] = list(eng._scr.rechecked)
+            cert = getattr(eng._scr, "cert", None)
+            acc["breakdown"]["certified_steps_rank0"] = list(cert.history) if cert is not None else None
         # pruned k-means|| rounds: (rows, rows with a few relevant candidates, rows sent to the K9r pass)
         acc["breakdown"]["init_pruned_rounds_rank0"] = getattr(eng, "_init_prune_history", None)
         del eng

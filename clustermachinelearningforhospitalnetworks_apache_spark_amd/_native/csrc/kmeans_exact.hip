@@ -13,6 +13,7 @@
 //                  labels): fixed 1024-position chunks summed sequentially, chunk partials of the
 //                  clusters crossing a chunk edge combined in chunk order — deterministic, no atomics.
 #include "common.h"
+#include "exact_util.h"
 
 namespace {
 
@@ -80,70 +81,105 @@ __global__ __launch_bounds__(kThreads) void exact_assign_kernel(const T* __restr
 }
 
 // Wide rows (d > 16): the same per-centre fold (t ascending, fma from 0.0, strict < over centres in
-// index order — the same bits as exact_assign_kernel and the host twin), register-blocked over KA
-// centres: a row is read once per KA centres of the LDS tile instead of once per centre (the DREG = 0
-// form re-read the row from L2 for every centre: the screen's f64 re-check ran at a fraction of the
-// memory rate on 128+-wide rows).
-template <typename T, int KA, int DC>
-__global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(const T* __restrict__ X, long long n,
-                                                                     long long ldx, int d,
-                                                                     const double* __restrict__ C, int k, int kt,
-                                                                     int* __restrict__ labels,
-                                                                     double* __restrict__ best,
-                                                                     int* __restrict__ changed,
-                                                                     const int* __restrict__ idx,
-                                                                     const int* __restrict__ n_dev) {
+// index order — the same bits as exact_assign_kernel and the host twin). Dimensions outer, KG centre
+// accumulators live in registers: each row is read once per KG centres and every LDS centre value
+// (a wave-uniform broadcast) feeds 64 rows' f64 fma — VALU-bound at the f64 rate. The LDS tile is
+// zero-padded to a DC multiple of dimensions and a KG multiple of centres (a zero term adds +0.0 to a
+// non-negative fold: the same bits). Rows: grid-stride over n or over idx[0 .. *n_dev).
+// Optional outputs: ub / lb = f32 bounds (outward-rounded) of the real distance to the label and to
+// every other centre (the fold's top-2); mv_* = (row, old label, new label) of the rows whose label
+// changed, appended (mv_count) — the certified pruned step's moves (kmeans_cert.hip).
+template <typename T, int KG, int DC>
+__global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
+    const T* __restrict__ X, long long n, long long ldx, int d, const double* __restrict__ C, int k, int kt,
+    int* __restrict__ labels, double* __restrict__ best, int* __restrict__ changed, const int* __restrict__ idx,
+    const int* __restrict__ n_dev, float* __restrict__ ub, float* __restrict__ lb, int* __restrict__ mv_row,
+    int* __restrict__ mv_old, int* __restrict__ mv_new, int* __restrict__ mv_count) {
   extern __shared__ __align__(16) unsigned char smem[];
-  double* ct = reinterpret_cast<double*>(smem);  // [kt][d]
-  const long long t0 = (long long)blockIdx.x * kThreads + threadIdx.x;
-  const long long cnt = n_dev != nullptr ? (long long)*n_dev : n;
-  if ((long long)blockIdx.x * kThreads >= cnt) return;
-  const bool live = t0 < cnt && t0 < n;
-  const long long r = live ? (idx != nullptr ? (long long)idx[t0] : t0) : 0;
-  const T* xrow = X + r * ldx;
-  double bd = __builtin_huge_val();
-  int bi = 0;
-  for (int c0 = 0; c0 < k; c0 += kt) {
-    const int kc = min(kt, k - c0);
+  __shared__ int s_w[kThreads / 64 + 1];
+  double* ct = reinterpret_cast<double*>(smem);  // [round_up(kt, KG)][dpad]
+  const int dpad = (d + DC - 1) / DC * DC;
+  const int ktp = (kt + KG - 1) / KG * KG;
+  long long cnt = n_dev != nullptr ? (long long)*n_dev : n;
+  cnt = cnt < n ? cnt : n;
+  const bool single = k <= kt;
+  auto load_tile = [&](int c0, int kc) {
+    for (int e = threadIdx.x; e < ktp * dpad; e += kThreads) {
+      const int j = e / dpad, t = e - j * dpad;
+      ct[e] = (j < kc && t < d) ? C[(long long)(c0 + j) * d + t] : 0.0;
+    }
+  };
+  if (single) {
+    load_tile(0, k);
     __syncthreads();
-    for (int e = threadIdx.x; e < kc * d; e += kThreads) ct[e] = C[(long long)c0 * d + e];
-    __syncthreads();
-    if (!live) continue;
-    for (int j0 = 0; j0 < kc; j0 += KA) {
-      double acc[KA];
+  }
+  for (long long base = (long long)blockIdx.x * kThreads; base < cnt; base += (long long)gridDim.x * kThreads) {
+    const long long t0 = base + threadIdx.x;
+    const bool live = t0 < cnt;
+    const long long r = live ? (idx != nullptr ? (long long)idx[t0] : t0) : 0;
+    const T* xrow = X + r * ldx;
+    double bd = __builtin_huge_val(), sd = __builtin_huge_val();
+    int bi = 0;
+    for (int c0 = 0; c0 < k; c0 += kt) {
+      const int kc = min(kt, k - c0);
+      if (!single) {
+        __syncthreads();
+        load_tile(c0, kc);
+        __syncthreads();
+      }
+      if (!live) continue;
+      for (int j0 = 0; j0 < kc; j0 += KG) {
+        double acc[KG];
 #pragma unroll
-      for (int a = 0; a < KA; ++a) acc[a] = 0.0;
-      for (int tb = 0; tb < d; tb += DC) {
-        double xv[DC];
+        for (int a = 0; a < KG; ++a) acc[a] = 0.0;
+        for (int tb = 0; tb < dpad; tb += DC) {
+          double xv[DC];
 #pragma unroll
-        for (int u = 0; u < DC; ++u) xv[u] = tb + u < d ? (double)xrow[tb + u] : 0.0;
+          for (int u = 0; u < DC; ++u) xv[u] = tb + u < d ? (double)xrow[tb + u] : 0.0;
 #pragma unroll
-        for (int a = 0; a < KA; ++a) {
-          if (j0 + a < kc) {
-            const double* cj = ct + (long long)(j0 + a) * d + tb;
+          for (int a = 0; a < KG; ++a) {
+            const double* cj = ct + (long long)(j0 + a) * dpad + tb;
 #pragma unroll
             for (int u = 0; u < DC; ++u) {
-              if (tb + u < d) {
-                const double e = xv[u] - cj[u];
-                acc[a] = __fma_rn(e, e, acc[a]);
-              }
+              const double e = xv[u] - cj[u];
+              acc[a] = __fma_rn(e, e, acc[a]);
+            }
+          }
+        }
+#pragma unroll
+        for (int a = 0; a < KG; ++a) {
+          if (j0 + a < kc) {  // centres ascending: strict < keeps the lowest index
+            const double v = acc[a];
+            if (v < bd) {
+              sd = bd;
+              bd = v;
+              bi = c0 + j0 + a;
+            } else if (v < sd) {
+              sd = v;
             }
           }
         }
       }
-#pragma unroll
-      for (int a = 0; a < KA; ++a) {
-        if (j0 + a < kc && acc[a] < bd) {  // centres ascending: strict < keeps the lowest index
-          bd = acc[a];
-          bi = c0 + j0 + a;
-        }
+    }
+    int old = 0;
+    if (live) {
+      old = labels[r];
+      if (changed != nullptr && old != bi) atomicAdd(changed, 1);
+      labels[r] = bi;
+      if (best != nullptr) best[r] = bd;
+      if (ub != nullptr) {
+        ub[r] = f32_up(sqrt(bd) * (1.0 + kFoldMargin));
+        lb[r] = k > 1 ? f32_dn(sqrt(sd) * (1.0 - kFoldMargin)) : __builtin_huge_valf();
       }
     }
-  }
-  if (live) {
-    if (changed != nullptr && labels[r] != bi) atomicAdd(changed, 1);
-    labels[r] = bi;
-    best[r] = bd;
+    if (mv_count != nullptr) {  // block-uniform
+      const int pos = block_append<kThreads>(live && old != bi, mv_count, s_w);
+      if (pos >= 0) {
+        mv_row[pos] = (int)r;
+        mv_old[pos] = old;
+        mv_new[pos] = bi;
+      }
+    }
   }
 }
 
@@ -198,55 +234,90 @@ __global__ __launch_bounds__(kThreads) void to_bf16_err_kernel(const T* __restri
 // of the bf16 distances (their f32 rounding already inside) and ecmax >= max_j ||c_j - bf16(c_j)||:
 // then every other centre is farther than the label's in exact arithmetic too, so the f64 argmin
 // is the same label (no tie).
+// One reservation per block and 1024-row tile (the list order is free: exact_assign writes every listed
+// row at its own position): a per-wave atomic on the single counter serialised ~n/64 atomics in L2 when
+// many rows were uncertified (1.6 ms per 10M-row pass; now ~n/1024 of them).
+constexpr int kCertQ = 4;  // rows per thread per tile
 __global__ __launch_bounds__(kThreads) void screen_cert_kernel(const float* __restrict__ ub,
                                                                const float* __restrict__ lb,
                                                                const float* __restrict__ err,
                                                                const double* __restrict__ ecmax, long long n,
-                                                               int* __restrict__ lst, int* __restrict__ count) {
-  const int lane = threadIdx.x & 63;
+                                                               int* __restrict__ lst, int* __restrict__ count,
+                                                               float* __restrict__ u_out, float* __restrict__ l_out) {
+  __shared__ int wtot[kThreads / 64][kCertQ];
+  __shared__ int base_s;
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const double ec = *ecmax;
-  for (long long i0 = (long long)blockIdx.x * kThreads; i0 < n; i0 += (long long)gridDim.x * kThreads) {
-    const long long i = i0 + threadIdx.x;
-    bool bad = false;
-    if (i < n) {
-      const double gap = (double)lb[i] - (double)ub[i];
-      bad = !(gap > 2.0 * ((double)err[i] + ec) * (1.0 + 1e-9) + 1e-300);
+  constexpr long long kTile = (long long)kThreads * kCertQ;
+  for (long long i0 = (long long)blockIdx.x * kTile; i0 < n; i0 += (long long)gridDim.x * kTile) {
+    unsigned long long bal[kCertQ];
+#pragma unroll
+    for (int q = 0; q < kCertQ; ++q) {
+      const long long i = i0 + (long long)q * kThreads + threadIdx.x;
+      bool bad = false;
+      if (i < n) {
+        const double ubi = (double)ub[i], lbi = (double)lb[i], e = (double)err[i] + ec;
+        bad = !(lbi - ubi > 2.0 * e * (1.0 + 1e-9) + 1e-300);
+        if (u_out != nullptr) {  // real-distance bounds of the screened label (overwritten for listed rows)
+          u_out[i] = f32_up((ubi + e) * (1.0 + kFoldMargin));
+          l_out[i] = f32_dn((lbi - e) * (1.0 - kFoldMargin));
+        }
+      }
+      bal[q] = __ballot(bad);
+      if (lane == 0) wtot[w][q] = (int)__popcll(bal[q]);
     }
-    const unsigned long long bal = __ballot(bad);
-    if (bal) {
-      const int leader = __builtin_ctzll(bal);
-      int base = 0;
-      if (lane == leader) base = atomicAdd(count, (int)__popcll(bal));
-      base = __shfl(base, leader, 64);
-      if (bad) lst[base + __popcll(bal & ((1ull << lane) - 1ull))] = (int)i;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+      int tot = 0;
+      for (int q = 0; q < kCertQ; ++q)
+        for (int v = 0; v < kThreads / 64; ++v) tot += wtot[v][q];
+      base_s = tot ? atomicAdd(count, tot) : 0;
     }
+    __syncthreads();
+    int off = base_s;  // this wave's entries of tile q follow every earlier (q, wave) in (q, wave) order
+#pragma unroll
+    for (int q = 0; q < kCertQ; ++q) {
+      for (int v = 0; v < kThreads / 64; ++v) off += (v < w) ? wtot[v][q] : 0;
+      if ((bal[q] >> lane) & 1ull)
+        lst[off + __popcll(bal[q] & ((1ull << lane) - 1ull))] = (int)(i0 + (long long)q * kThreads + threadIdx.x);
+      for (int v = w; v < kThreads / 64; ++v) off += wtot[v][q];
+    }
+    __syncthreads();  // wtot / base_s reused by the next tile
   }
 }
 
 // seg[c] = first sorted position of cluster c (seg[k] = n); perm[p] = row at sorted position p.
-// Chunk ch covers positions [ch*kChunk, ...): clusters strictly inside it are stored complete into S;
-// the cluster open at its start goes to slot 2ch, the one open at its end (if another) to 2ch+1.
+// Chunk ch covers positions [ch*kChunk, ...): clusters strictly inside it are stored complete into
+// S / S_lo (normalised double-double); the cluster open at its start goes to slot 2ch, the one open at
+// its end (if another) to slot 2ch+1 (hi in slots, lo in slots + 2·nch·d).
 template <typename T>
 __global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restrict__ X, long long ldx, int d,
                                                                const int* __restrict__ perm,
                                                                const int* __restrict__ seg, int k, long long n,
-                                                               double* __restrict__ S, double* __restrict__ slots,
-                                                               int* __restrict__ slot_c) {
+                                                               double* __restrict__ S, double* __restrict__ S_lo,
+                                                               double* __restrict__ slots, int* __restrict__ slot_c) {
   const long long ch = blockIdx.x;
+  const long long nch = gridDim.x;
+  double* slots_lo = slots + 2 * nch * (long long)d;
   const int col = blockIdx.y * 64 + threadIdx.x;
   const long long p0 = ch * kChunk, p1 = min(n, p0 + kChunk);
-  int lo = 0, hi = k;  // seg[lo] <= p0 < seg[hi]
-  while (hi - lo > 1) {
-    const int mid = (lo + hi) >> 1;
-    if (seg[mid] <= p0) lo = mid; else hi = mid;
+  int lo_ = 0, hi_ = k;  // seg[lo_] <= p0 < seg[hi_]
+  while (hi_ - lo_ > 1) {
+    const int mid = (lo_ + hi_) >> 1;
+    if (seg[mid] <= p0) lo_ = mid; else hi_ = mid;
   }
-  int c = lo;
+  int c = lo_;
   while (seg[c + 1] <= p0) ++c;  // skip empty clusters
   const int ca = c;
-  double acc = 0.0;
+  double ah = 0.0, al = 0.0;
   long long next = seg[c + 1];
-  // PF positions' rows are loaded before any of them is added (the adds keep their order: same bits):
-  // the fold's latency chain no longer serialises the gathers
+  auto store = [&](double* dh, double* dl) {
+    dd_norm(ah, al);
+    *dh = ah;
+    *dl = al;
+  };
+  // PF positions' rows are loaded before any of them is added: the adds' latency chain no longer
+  // serialises the gathers
   constexpr int PF = 8;
   for (long long pb = p0; pb < p1; pb += PF) {
     double v[PF];
@@ -261,19 +332,20 @@ __global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restri
       if (p >= p1) break;
       while (p >= next) {  // cluster c ended: first one -> slot A, a middle one is complete
         if (col < d) {
-          if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
-          else S[(long long)c * d + col] = acc;
+          if (c == ca) store(slots + (2 * ch) * (long long)d + col, slots_lo + (2 * ch) * (long long)d + col);
+          else store(S + (long long)c * d + col, S_lo + (long long)c * d + col);
         }
-        acc = 0.0;
+        ah = 0.0;
+        al = 0.0;
         ++c;
         next = seg[c + 1];
       }
-      if (col < d) acc += v[u];
+      if (col < d) dd_add(ah, al, v[u]);
     }
   }
   if (col < d) {
-    if (c == ca) slots[(2 * ch) * (long long)d + col] = acc;
-    else slots[(2 * ch + 1) * (long long)d + col] = acc;
+    const long long sl = c == ca ? 2 * ch : 2 * ch + 1;
+    store(slots + sl * (long long)d + col, slots_lo + sl * (long long)d + col);
   }
   if (blockIdx.y == 0 && threadIdx.x == 0) {
     slot_c[2 * ch] = ca;
@@ -281,15 +353,20 @@ __global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restri
   }
 }
 
-// S[c] for the clusters that touch a chunk edge: the slot partials in chunk order (A before B).
+// S[c] for the clusters that touch a chunk edge: the slot partials (double-double) in chunk order.
 __global__ __launch_bounds__(kThreads) void exact_seg_fix_kernel(const int* __restrict__ seg, int k, int d,
-                                                                 double* __restrict__ S,
+                                                                 long long nch, double* __restrict__ S,
+                                                                 double* __restrict__ S_lo,
                                                                  const double* __restrict__ slots,
                                                                  const int* __restrict__ slot_c) {
   const int c = blockIdx.x;
   const long long s0 = seg[c], s1 = seg[c + 1];
+  const double* slots_lo = slots + 2 * nch * (long long)d;
   if (s1 <= s0) {
-    for (int t = threadIdx.x; t < d; t += kThreads) S[(long long)c * d + t] = 0.0;
+    for (int t = threadIdx.x; t < d; t += kThreads) {
+      S[(long long)c * d + t] = 0.0;
+      S_lo[(long long)c * d + t] = 0.0;
+    }
     return;
   }
   const long long ch0 = s0 / kChunk, ch1 = (s1 - 1) / kChunk;
@@ -297,16 +374,63 @@ __global__ __launch_bounds__(kThreads) void exact_seg_fix_kernel(const int* __re
   for (long long ch = ch0; ch <= ch1; ++ch) edge |= slot_c[2 * ch] == c || slot_c[2 * ch + 1] == c;
   if (!edge) return;  // complete inside one chunk: stored by the partial kernel
   for (int t = threadIdx.x; t < d; t += kThreads) {
-    double s = 0.0;
+    double h = 0.0, l = 0.0;
     for (long long ch = ch0; ch <= ch1; ++ch) {
-      if (slot_c[2 * ch] == c) s += slots[(2 * ch) * (long long)d + t];
-      if (slot_c[2 * ch + 1] == c) s += slots[(2 * ch + 1) * (long long)d + t];
+      for (int q = 0; q < 2; ++q) {
+        if (slot_c[2 * ch + q] == c) {
+          dd_add(h, l, slots[(2 * ch + q) * (long long)d + t]);
+          l += slots_lo[(2 * ch + q) * (long long)d + t];
+        }
+      }
     }
-    S[(long long)c * d + t] = s;
+    dd_norm(h, l);
+    S[(long long)c * d + t] = h;
+    S_lo[(long long)c * d + t] = l;
   }
 }
 
 }  // namespace
+
+// X: f64 (xf64 = 1) or f32 rows [n, ldx elements]; C: f64 [k, d]; labels (int32, read for the change
+// count when `changed` is given) and best (f64) [n].
+// idx / n_dev: see exact_assign_kernel (n is then the capacity of idx, the grid covers it).
+template <typename T, int KG>
+static void launch_wide(const T* X, long long n, long long ldx, int d, const double* C, int k, int* labels,
+                        double* best, int* changed, const int* idx, const int* n_dev, float* ub, float* lb,
+                        int* mv_row, int* mv_old, int* mv_new, int* mv_count, hipStream_t st) {
+  constexpr int DC = 8;
+  const int dpad = (d + DC - 1) / DC * DC;
+  int kt = (8192 / dpad) / KG * KG;  // centres per LDS tile (<= 64 KiB)
+  kt = kt < KG ? KG : kt;
+  const int ktp = kt;
+  const size_t lds = (size_t)ktp * dpad * sizeof(double);
+  if (lds > 65536)
+    (void)hipFuncSetAttribute((const void*)exact_assign_wide_kernel<T, KG, DC>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+  long long blocks = (n + kThreads - 1) / kThreads;
+  if (idx != nullptr) blocks = blocks < 4096 ? blocks : 4096;  // grid-stride over the listed rows
+  hipLaunchKernelGGL((exact_assign_wide_kernel<T, KG, DC>), dim3((unsigned)blocks), dim3(kThreads), lds, st, X, n,
+                     ldx, d, C, k, kt, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new, mv_count);
+}
+
+template <typename T>
+static void launch_wide_any(const T* X, long long n, long long ldx, int d, const double* C, int k, int* labels,
+                            double* best, int* changed, const int* idx, const int* n_dev, float* ub, float* lb,
+                            int* mv_row, int* mv_old, int* mv_new, int* mv_count, hipStream_t st) {
+  const int dpad = (d + 7) / 8 * 8;
+  if (dpad <= 256 && k > 16)
+    launch_wide<T, 32>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                       mv_count, st);
+  else if (dpad <= 512)
+    launch_wide<T, 16>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                       mv_count, st);
+  else if (dpad <= 1024)
+    launch_wide<T, 8>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                      mv_count, st);
+  else
+    launch_wide<T, 1>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                      mv_count, st);
+}
 
 // X: f64 (xf64 = 1) or f32 rows [n, ldx elements]; C: f64 [k, d]; labels (int32, read for the change
 // count when `changed` is given) and best (f64) [n].
@@ -323,20 +447,37 @@ CML_API int cml_kmeans_exact_assign(const void* X, int xf64, long long n, long l
 #define CML_EA(T, R)                                                                                        \
   hipLaunchKernelGGL((exact_assign_kernel<T, R>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, k, kt, \
                      labels, best, changed, idx, n_dev)
-#define CML_EW(T)                                                                                          \
-  hipLaunchKernelGGL((exact_assign_wide_kernel<T, 16, 8>), g, dim3(kThreads), lds, st, (const T*)X, n, ldx, d, C, \
-                     k, kt, labels, best, changed, idx, n_dev)
   if (xf64) {
     if (d <= 4) CML_EA(double, 4);
     else if (d <= 16) CML_EA(double, 16);
-    else CML_EW(double);
+    else launch_wide_any<double>((const double*)X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, nullptr,
+                                 nullptr, nullptr, nullptr, nullptr, nullptr, st);
   } else {
     if (d <= 4) CML_EA(float, 4);
     else if (d <= 16) CML_EA(float, 16);
-    else CML_EW(float);
+    else launch_wide_any<float>((const float*)X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, nullptr,
+                                nullptr, nullptr, nullptr, nullptr, nullptr, st);
   }
 #undef CML_EA
-#undef CML_EW
+  return cml_status();
+}
+
+// The certified step's full re-assignment (any d): the wide fold (same bits as exact_assign) over
+// idx[0 .. *n_dev) writing labels, optional best, the f32 top-2 bounds ub / lb and the move list.
+CML_API int cml_kmeans_exact_top2(const void* X, int xf64, long long n, long long ldx, int d, const double* C, int k,
+                                  int* labels, double* best, const int* idx, const int* n_dev, float* ub, float* lb,
+                                  int* mv_row, int* mv_old, int* mv_new, int* mv_count, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0 || k <= 0 || ub == nullptr || lb == nullptr || ((idx == nullptr) != (n_dev == nullptr)) ||
+      ((mv_count == nullptr) != (mv_row == nullptr)))
+    return (int)hipErrorInvalidValue;
+  hipStream_t st = (hipStream_t)stream;
+  if (xf64)
+    launch_wide_any<double>((const double*)X, n, ldx, d, C, k, labels, best, nullptr, idx, n_dev, ub, lb, mv_row,
+                            mv_old, mv_new, mv_count, st);
+  else
+    launch_wide_any<float>((const float*)X, n, ldx, d, C, k, labels, best, nullptr, idx, n_dev, ub, lb, mv_row,
+                           mv_old, mv_new, mv_count, st);
   return cml_status();
 }
 
@@ -374,32 +515,38 @@ CML_API int cml_kmeans_to_bf16_err(const void* X, int xf64, long long n, long lo
 }
 
 // lst: int [n] (n entries at most), count: int [1] zeroed by the caller; ecmax: f64 device scalar.
+// u_out / l_out (nullable, may alias ub / lb): f32 bounds of the real distance to the screened label
+// and to every other centre, ub + err + ecmax and lb - err - ecmax rounded outward.
 CML_API int cml_kmeans_screen_cert(const float* ub, const float* lb, const float* err, const double* ecmax,
-                                   long long n, int* lst, int* count, void* stream) {
+                                   long long n, int* lst, int* count, float* u_out, float* l_out, void* stream) {
   if (n <= 0) return 0;
-  long long g = (n + kThreads * 4 - 1) / (kThreads * 4);
-  g = g > 4096 ? 4096 : (g < 1 ? 1 : g);
+  long long g = (n + kThreads * kCertQ - 1) / (kThreads * kCertQ);
+  g = g > 2048 ? 2048 : (g < 1 ? 1 : g);
   hipLaunchKernelGGL(screen_cert_kernel, dim3((unsigned)g), dim3(kThreads), 0, (hipStream_t)stream, ub, lb, err,
-                     ecmax, n, lst, count);
+                     ecmax, n, lst, count, u_out, l_out);
   return cml_status();
 }
 
-// Slot scratch: slots f64 [2 * nchunks * d], slot_c int [2 * nchunks], nchunks = ceil(n / 1024).
+// Slot scratch: slots f64 [4 * nchunks * d] (hi then lo), slot_c int [2 * nchunks], nchunks = ceil(n / 1024).
 CML_API long long cml_kmeans_exact_chunks(long long n) { return (n + kChunk - 1) / kChunk; }
 
+// S = the correctly rounded per-cluster sums (double-double accumulation), S_lo = the remainders
+// (S + S_lo = the exact sum; the rank fold of a multi-rank fit adds them).
 CML_API int cml_kmeans_exact_segsum(const void* X, int xf64, long long ldx, int d, const int* perm, const int* seg,
-                                    int k, long long n, double* S, double* slots, int* slot_c, void* stream) {
-  if (d <= 0 || k <= 0) return (int)hipErrorInvalidValue;
+                                    int k, long long n, double* S, double* S_lo, double* slots, int* slot_c,
+                                    void* stream) {
+  if (d <= 0 || k <= 0 || S_lo == nullptr) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
+  const long long nch = n > 0 ? (n + kChunk - 1) / kChunk : 0;
   if (n > 0) {
-    const dim3 g((unsigned)((n + kChunk - 1) / kChunk), (unsigned)((d + 63) / 64));
+    const dim3 g((unsigned)nch, (unsigned)((d + 63) / 64));
     if (xf64)
       hipLaunchKernelGGL((exact_seg_partial_kernel<double>), g, dim3(64), 0, st, (const double*)X, ldx, d, perm, seg,
-                         k, n, S, slots, slot_c);
+                         k, n, S, S_lo, slots, slot_c);
     else
       hipLaunchKernelGGL((exact_seg_partial_kernel<float>), g, dim3(64), 0, st, (const float*)X, ldx, d, perm, seg,
-                         k, n, S, slots, slot_c);
+                         k, n, S, S_lo, slots, slot_c);
   }
-  hipLaunchKernelGGL(exact_seg_fix_kernel, dim3(k), dim3(kThreads), 0, st, seg, k, d, S, slots, slot_c);
+  hipLaunchKernelGGL(exact_seg_fix_kernel, dim3(k), dim3(kThreads), 0, st, seg, k, d, nch, S, S_lo, slots, slot_c);
   return cml_status();
 }

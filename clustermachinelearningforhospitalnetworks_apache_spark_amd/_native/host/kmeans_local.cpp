@@ -205,38 +205,42 @@ CML_HOST_API int cml_exact_assign_host(const double* X, long long n, long long l
   return 0;
 }
 
-// exact_sums: per-cluster sums in the device kernel's order — rows of cluster c in ascending row
-// order occupy sorted positions [seg[c], seg[c+1]); the positions are cut into 1024-position chunks,
-// each chunk's run of the cluster is folded from 0, and the runs are added in chunk order.
+// exact_sums: the correctly rounded per-cluster sums (S) and their remainders (S_lo, nullable) by
+// double-double accumulation — the device kernel's result (csrc/kmeans_exact.hip): hi + lo holds the
+// running sum exactly while the values' exponents span less than ~2^80, so the order of the additions
+// (row order here, sorted chunks there) does not change the rounded total.
+static inline void dd_add_h(double& hi, double& lo, double v) {
+  const double s = hi + v;
+  const double bb = s - hi;
+  lo += (hi - (s - bb)) + (v - bb);
+  hi = s;
+}
+static inline void dd_norm_h(double& hi, double& lo) {
+  const double s = hi + lo;
+  const double bb = s - hi;
+  lo = (hi - (s - bb)) + (lo - bb);
+  hi = s;
+}
+
 CML_HOST_API int cml_exact_sums_host(const double* X, long long n, long long ldx, int d, const long long* labels,
-                                     int k, double* S, double* counts) {
+                                     int k, double* S, double* counts, double* S_lo) {
   if (n < 0 || d <= 0 || k <= 0) return -1;
-  constexpr long long kChunk = 1024;
-  std::vector<long long> cnt(k, 0), seg(k + 1, 0);
+  std::vector<double> lo((size_t)k * d, 0.0);
+  std::vector<long long> cnt(k, 0);
+  for (long long i = 0; i < (long long)k * d; ++i) S[i] = 0.0;
   for (long long r = 0; r < n; ++r) {
-    if (labels[r] < 0 || labels[r] >= k) return -2;
-    ++cnt[labels[r]];
+    const long long c = labels[r];
+    if (c < 0 || c >= k) return -2;
+    ++cnt[c];
+    const double* x = X + r * ldx;
+    double* s = S + c * d;
+    double* l = lo.data() + c * d;
+    for (int t = 0; t < d; ++t) dd_add_h(s[t], l[t], x[t]);
   }
-  for (int c = 0; c < k; ++c) seg[c + 1] = seg[c] + cnt[c];
-  std::vector<std::vector<long long>> rows(k);
-  for (int c = 0; c < k; ++c) rows[c].reserve(cnt[c]);
-  for (long long r = 0; r < n; ++r) rows[labels[r]].push_back(r);
-  std::vector<double> part(d);
-  for (int c = 0; c < k; ++c) {
-    double* s = S + (long long)c * d;
-    for (int t = 0; t < d; ++t) s[t] = 0.0;
-    counts[c] = (double)cnt[c];
-    long long i = 0;
-    while (i < cnt[c]) {
-      const long long ch = (seg[c] + i) / kChunk;
-      const long long end = std::min(cnt[c], (ch + 1) * kChunk - seg[c]);
-      for (int t = 0; t < d; ++t) part[t] = 0.0;
-      for (; i < end; ++i) {
-        const double* x = X + rows[c][i] * ldx;
-        for (int t = 0; t < d; ++t) part[t] = part[t] + x[t];
-      }
-      for (int t = 0; t < d; ++t) s[t] = s[t] + part[t];
-    }
+  for (long long i = 0; i < (long long)k * d; ++i) {
+    dd_norm_h(S[i], lo[i]);
+    if (S_lo != nullptr) S_lo[i] = lo[i];
   }
+  for (int c = 0; c < k; ++c) counts[c] = (double)cnt[c];
   return 0;
 }

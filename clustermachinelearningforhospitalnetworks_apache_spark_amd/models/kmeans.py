@@ -459,6 +459,8 @@ class LloydEngine:
             self.centers = c.contiguous().clone()
         if self.gpu:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+        if getattr(self, "_scr", None) is not None and getattr(self._scr, "cert", None) is not None:
+            self._scr.cert.valid = False  # the certified step restarts from a screened full assignment
         seed, self._seed = getattr(self, "_seed", None), None
         if self._pdev:  # bounds and incremental sums were relative to the old centres: a full step next
             st = self._pst
@@ -691,8 +693,10 @@ class LloydEngine:
         bf16 label with bounds ub >= its distance and lb <= every other distance (f32 rounding inside);
         the exact distances differ from the bf16 ones by at most ||x - bf16(x)|| + ||c - bf16(c)||, so a row
         with lb - ub > 2·(err_x + max err_c) has that label exactly; the others are re-assigned in f64
-        (exact_assign over the listed rows). ``best`` (f64 [n], optional) receives the exact squared distance
-        to the label (exact_dist: the exact kernel's fold, the same bits)."""
+        (exact_top2 over the listed rows: exact_assign's fold, same bits). Afterwards st.ub / st.lb hold
+        f32 bounds of every row's real distance to its label / to every other centre (the certified
+        step's starting bounds). ``best`` (f64 [n], optional) receives the exact squared distance to the
+        label (exact_dist: the exact kernel's fold, the same bits)."""
         st = self._screen_state()
         n, d, kc = self.n, self.d, int(C.shape[0])
         if n == 0:
@@ -707,11 +711,10 @@ class LloydEngine:
         plan = K.plan_assign(n, st.dp, kc)
         K.assign_rr_ext(1, st.xb, n, st.dp, st.cb[:kp], st.cn[:kp], plan, st.xn, lab, None, st.ub, st.lb, mc, st.tau)
         st.cnt.zero_()
-        K.screen_cert(st.ub, st.lb, st.ex, ecmax, n, st.lst, st.cnt)
+        K.screen_cert(st.ub, st.lb, st.ex, ecmax, n, st.lst, st.cnt, u_out=st.ub, l_out=st.lb)
         if best is not None:
             K.exact_dist(self.x, C, lab, best)
-        K.exact_assign(self.x, C, labels=lab, idx=st.lst, n_dev=st.cnt,
-                       best=best if best is not None else self._scr_best())
+        K.exact_top2(self.x, C, lab, st.ub, st.lb, idx=st.lst, n_dev=st.cnt, best=best)
         if self.track_prune:
             st.rechecked.append(int(st.cnt.item()))
 
@@ -740,26 +743,90 @@ class LloydEngine:
             lab[:n] = torch.where(better, lab_c[:n].long() + c0, lab[:n])
         return best[:n], lab[:n]
 
+    def _cert_state(self):
+        """Buffers of the certified pruned step (kmeans_cert.hip): labels, row lists, moves, the move
+        sort, and the double-double cluster sums of the current labels (S_hi + S_lo, int32 counts)."""
+        st = self._screen_state()
+        c = getattr(st, "cert", None)
+        if c is not None:
+            return c
+        n, k, d, dev = self.n, self.k, self.d, self.device
+        m = max(n, 1)
+        i32 = dict(dtype=torch.int32, device=dev)
+        c = types.SimpleNamespace(valid=False, history=[])
+        c.lab = torch.zeros(m, **i32)
+        c.ctr = torch.zeros(4 + 2 * k, **i32)  # [list A, list B, moves, -, move histogram (2k)]
+        c.la, c.lbl = torch.empty(m, **i32), torch.empty(m, **i32)
+        c.mvr, c.mvo, c.mvn = torch.empty(m, **i32), torch.empty(m, **i32), torch.empty(m, **i32)
+        c.seg, c.cursor, c.perm = torch.empty(2 * k + 1, **i32), torch.empty(2 * k, **i32), torch.empty(2 * m, **i32)
+        c.s = torch.empty(k, dtype=torch.float32, device=dev)
+        c.drift = torch.empty(k, dtype=torch.float32, device=dev)
+        c.dtop = torch.zeros(4, dtype=torch.float32, device=dev)
+        ns = K.cert_slices(k)
+        c.P_hi = torch.empty(ns * k * d, dtype=torch.float64, device=dev)
+        c.P_lo = torch.empty(ns * k * d, dtype=torch.float64, device=dev)
+        c.S_hi = c.S_lo = c.cnt = c.C_cur = None
+        st.cert = c
+        return c
+
+    def _exact_global(self, S: torch.Tensor, S_lo: torch.Tensor, counts: Optional[torch.Tensor],
+                      cost: torch.Tensor):
+        """(sums, counts, cost) over every rank: each rank's double-double sums folded in rank order — the
+        one-rank bits for any partitioning of the rows (an f64 all-reduce would round per rank)."""
+        if not self.comm.is_distributed:
+            return S, counts, cost
+        m, k = S.numel(), self.k
+        parts = [S.reshape(-1), S_lo.reshape(-1)]
+        if counts is not None:
+            parts.append(counts.to(torch.float64))
+        parts.append(cost.reshape(1).to(torch.float64))
+        g = self.comm.allgather_fixed(torch.cat(parts))
+        S = K.dd_fold(g[:, :m], g[:, m:2 * m]).reshape(S.shape)
+        counts = g[:, 2 * m:2 * m + k].sum(0) if counts is not None else None
+        return S, counts, g[:, -1].sum()
+
     def _step_screen(self):
-        """One exact Lloyd iteration with the MFMA-screened assignment (the exact path's labels, sums and
-        centres bit for bit); the cost of the assignment is evaluated on first read (exact_dist)."""
-        n, k = self.n, self.k
-        if getattr(self, "_lab32", None) is None:
-            self._lab32 = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
-        lab = self._lab32
-        self._screen_labels(self.centers, lab)
-        sums, counts = K.sums_reference(self.x, lab[:n], k)
-        msg = torch.cat([sums.reshape(-1), counts, torch.zeros(1, dtype=torch.float64, device=self.device)])
-        self.comm.allreduce_(msg)
-        c_used, lab_used = self.centers.clone(), lab[:n].clone()
+        """One exact Lloyd iteration on the source rows (the exact path's labels, sums and centres bit for
+        bit). The first assigns every row through the MFMA screen (_screen_labels) and sums from scratch
+        (double-double, exact_sums); later ones are certified pruned steps (kmeans_cert.hip): Hamerly
+        bounds on the real distances, moved by the centre drifts, prove most labels unchanged; the rest
+        are tightened, re-assigned by the exact fold when still unproven, and the label moves update the
+        double-double sums incrementally (exactly the from-scratch sums). The cost of the assignment is
+        evaluated on first read (exact_dist)."""
+        n, k, d = self.n, self.k, self.d
+        c = self._cert_state()
+        st = self._scr
+        f64 = dict(dtype=torch.float64, device=self.device)
+        if not c.valid:
+            if n:
+                self._screen_labels(self.centers, c.lab)
+                c.S_hi, c.cnt, c.S_lo = K.exact_sums(self.x, c.lab[:n], k, with_lo=True, counts_int=True)
+            else:
+                c.S_hi, c.S_lo = torch.zeros((k, d), **f64), torch.zeros((k, d), **f64)
+                c.cnt = torch.zeros(k, dtype=torch.int32, device=self.device)
+            c.valid = True
+        elif n:
+            K.cert_stats(self.centers, c.C_cur, c.s, c.drift, c.dtop, zero=c.ctr)
+            K.cert_bounds(c.lab, st.ub, st.lb, c.drift, c.dtop, c.s, n, c.la, c.ctr[0:1])
+            K.cert_tighten(self.x, self.centers, c.lab, st.ub, st.lb, c.s, c.la, c.ctr[0:1], c.lbl, c.ctr[1:2])
+            K.exact_top2(self.x, self.centers, c.lab, st.ub, st.lb, idx=c.lbl, n_dev=c.ctr[1:2],
+                         moves=(c.mvr, c.mvo, c.mvn, c.ctr[2:3]))
+            K.cert_moves(self.x, k, c.mvr, c.mvo, c.mvn, c.ctr[2:3], c.ctr[4:], c.seg, c.cursor, c.perm, c.P_hi,
+                         c.P_lo, c.S_hi, c.S_lo, c.cnt)
+            if self.track_prune:
+                c.history.append(tuple(int(v) for v in c.ctr[:3].tolist()))
+        c.C_cur = self.centers.clone()  # the centres of this assignment (set_centers writes in place)
+        S, counts, _ = self._exact_global(c.S_hi, c.S_lo, c.cnt.to(torch.float64), torch.zeros(1, **f64))
+        msg = torch.cat([S.reshape(-1), counts, torch.zeros(1, **f64)])
+        c_used, lab_used = c.C_cur, c.lab[:n].clone()
         self._update_cpu(msg)
-        self.labels = lab[:n]
+        self.labels = c.lab[:n]
 
         def cost():
-            b = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+            b = torch.empty(max(n, 1), **f64)
             if n:
                 K.exact_dist(self.x, c_used, lab_used, b)
-            tot = b[:n].sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=self.device)
+            tot = b[:n].sum().reshape(1) if n else torch.zeros(1, **f64)
             self.comm.allreduce_(tot)
             return tot[0]
         self._cost_fn = cost
@@ -768,14 +835,14 @@ class LloydEngine:
         if self._screen:
             return self._step_screen()
         labels, best = K.assign_reference(self.x, self.centers)
-        if self.w is not None:
-            aug, _ = K.sums_reference(self._wx, labels, self.k)
-            sums, counts, cost = aug[:, : self.d], aug[:, self.d], (best * self.w).sum()
+        if self.w is not None:  # weighted rows: [w·x | w] summed in double-double, the weight column too
+            aug, _, aug_lo = K.sums_reference(self._wx, labels, self.k, with_lo=True)
+            aug, _, cost = self._exact_global(aug, aug_lo, None, (best * self.w).sum())
+            sums, counts = aug[:, : self.d], aug[:, self.d]
         else:
-            sums, counts = K.sums_reference(self.x, labels, self.k)
-            cost = best.sum()
+            sums, counts, sums_lo = K.sums_reference(self.x, labels, self.k, with_lo=True)
+            sums, counts, cost = self._exact_global(sums, sums_lo, counts, best.sum())
         msg = torch.cat([sums.reshape(-1), counts, cost.reshape(1)])
-        self.comm.allreduce_(msg)
         self._update_cpu(msg)
         self.labels = labels
 

@@ -100,15 +100,25 @@ _native.register_kernel_sigs({
                                         c_vp]),
     "cml_kmeans_exact_dist": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_to_bf16_err": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_ll, c_vp, c_vp]),
-    "cml_kmeans_screen_cert": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_screen_cert": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_exact_chunks": (c_ll, [c_ll]),
-    "cml_kmeans_exact_segsum": (c_int, [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_exact_segsum": (c_int, [c_vp, c_int, c_ll, c_int, c_vp, c_vp, c_int, c_ll, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp]),
+    "cml_kmeans_exact_top2": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                        c_vp, c_vp, c_vp]),
+    "cml_kmeans_cert_slices": (c_int, [c_int]),
+    "cml_kmeans_cert_moves": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                      c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 })
 _native.register_host_sigs({
     "cml_local_kmeans_host": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, ctypes.c_uint64, c_int,
                                       c_int, c_vp]),
     "cml_exact_assign_host": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_int]),
-    "cml_exact_sums_host": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp]),
+    "cml_exact_sums_host": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp]),
 })
 
 
@@ -838,19 +848,25 @@ def to_bf16_err(x: torch.Tensor, d: int, ldo: int, stream=None):
 
 
 def screen_cert(ub: torch.Tensor, lb: torch.Tensor, err: torch.Tensor, ecmax: torch.Tensor, n: int,
-                lst: torch.Tensor, count: torch.Tensor, stream=None) -> None:
+                lst: torch.Tensor, count: torch.Tensor, stream=None, u_out: torch.Tensor | None = None,
+                l_out: torch.Tensor | None = None) -> None:
     """Append to ``lst`` the rows whose bf16-screen label is not certified (lb - ub <= 2·(err + ecmax));
-    ``count`` (int32 [1], zeroed by the caller) receives their number."""
+    ``count`` (int32 [1], zeroed by the caller) receives their number. ``u_out`` / ``l_out`` (f32, may
+    be ``ub`` / ``lb``): bounds of the real distance to the label / every other centre (ub + err + ecmax,
+    lb - err - ecmax, rounded outward)."""
     if ecmax.dtype != torch.float64 or lst.dtype != torch.int32 or lst.numel() < n:
         raise ValueError("screen_cert: f64 ecmax, int32 list of n entries")
     _native.check(_native.kernels().cml_kmeans_screen_cert(
         ub.data_ptr(), lb.data_ptr(), err.data_ptr(), ecmax.data_ptr(), int(n), lst.data_ptr(), count.data_ptr(),
-        _native.stream_ptr(stream)), "kmeans_screen_cert")
+        _ptr(u_out), _ptr(l_out), _native.stream_ptr(stream)), "kmeans_screen_cert")
 
 
-def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = None, stream=None):
-    """Deterministic per-cluster f64 sums [k, d] and counts [k] of device f32/f64 rows: a stable sort
-    of the labels, then fixed-chunk sequential sums combined in chunk order (no atomics)."""
+def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = None, stream=None,
+               with_lo: bool = False, counts_int: bool = False):
+    """Per-cluster sums [k, d] and counts [k] of device f32/f64 rows, correctly rounded: double-double
+    accumulation over a stable label sort (fixed chunks, no atomics), so the result is the rounded exact
+    sum — the host twin's bits whatever the order. ``with_lo`` also returns the remainders S_lo (S +
+    S_lo = the exact sum; the rank fold adds them); ``counts_int`` returns int32 counts."""
     n = int(labels.shape[0])
     d = int(x.shape[1]) if d is None else d
     if x.dtype not in (torch.float32, torch.float64):
@@ -862,19 +878,95 @@ def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = No
         int_hist(lab, n, k, counts)  # exact int32 counts, no host read (bincount syncs)
     seg = torch.zeros(k + 1, dtype=torch.int32, device=x.device)
     seg[1:] = torch.cumsum(counts, 0, dtype=torch.int32)
-    # stable sort of the int32 labels (the row order within a cluster is the fold order)
+    # stable sort of the int32 labels (fixed chunks of the sorted order)
     perm = torch.sort(lab, stable=True).indices.to(torch.int32) if n else torch.zeros(1, dtype=torch.int32,
                                                                                         device=x.device)
     lib = _native.kernels()
     nch = max(1, int(lib.cml_kmeans_exact_chunks(n)))
-    slots = torch.empty(2 * nch * d, dtype=torch.float64, device=x.device)
+    slots = torch.empty(4 * nch * d, dtype=torch.float64, device=x.device)
     slot_c = torch.full((2 * nch,), -1, dtype=torch.int32, device=x.device)
     S = torch.zeros((k, d), dtype=torch.float64, device=x.device)
+    S_lo = torch.zeros((k, d), dtype=torch.float64, device=x.device)
     _native.check(lib.cml_kmeans_exact_segsum(x.data_ptr(), int(x.dtype == torch.float64), x.stride(0), d,
                                               perm.data_ptr(), seg.data_ptr(), int(k), n, S.data_ptr(),
-                                              slots.data_ptr(), slot_c.data_ptr(), _native.stream_ptr(stream)),
-                  "kmeans_exact_segsum")
-    return S, counts.to(torch.float64)
+                                              S_lo.data_ptr(), slots.data_ptr(), slot_c.data_ptr(),
+                                              _native.stream_ptr(stream)), "kmeans_exact_segsum")
+    cnt = counts if counts_int else counts.to(torch.float64)
+    return (S, cnt, S_lo) if with_lo else (S, cnt)
+
+
+def exact_top2(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor, ub: torch.Tensor, lb: torch.Tensor,
+               idx: torch.Tensor | None = None, n_dev: torch.Tensor | None = None, best: torch.Tensor | None = None,
+               moves: tuple | None = None, stream=None) -> None:
+    """The exact fold assignment (exact_assign's bits) of every row, or of idx[0 .. n_dev), writing
+    ``labels``, optional ``best`` and the f32 bounds ``ub`` / ``lb`` of the real distance to the label /
+    to every other centre; ``moves`` = (rows, old, new, count) int32 lists receiving the label changes."""
+    n, d = int(x.shape[0]), int(centers.shape[1])
+    if n == 0:
+        return
+    c = centers.to(device=x.device, dtype=torch.float64).contiguous()
+    if labels.dtype != torch.int32 or ub.dtype != torch.float32 or lb.dtype != torch.float32:
+        raise ValueError("exact_top2: int32 labels, f32 bounds")
+    if idx is not None and (idx.numel() < n or n_dev is None):
+        raise ValueError("exact_top2: idx needs n entries and a device count")
+    mr, mo, mn, mc = moves if moves is not None else (None, None, None, None)
+    _native.check(_native.kernels().cml_kmeans_exact_top2(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), int(c.shape[0]),
+        labels.data_ptr(), _ptr(best), _ptr(idx), _ptr(n_dev), ub.data_ptr(), lb.data_ptr(), _ptr(mr), _ptr(mo),
+        _ptr(mn), _ptr(mc), _native.stream_ptr(stream)), "kmeans_exact_top2")
+
+
+def cert_stats(C: torch.Tensor, Cold: torch.Tensor, s: torch.Tensor, drift: torch.Tensor, dtop: torch.Tensor,
+               zero: torch.Tensor | None = None, stream=None) -> None:
+    """Half-separations ``s`` of the centres C, drifts ``drift`` = ||C - Cold|| and their top two
+    (kmeans_cert.hip); zeroes the int32 ``zero`` buffer (the step's counters)."""
+    k, d = int(C.shape[0]), int(C.shape[1])
+    _native.check(_native.kernels().cml_kmeans_cert_stats(
+        C.data_ptr(), Cold.data_ptr(), k, d, s.data_ptr(), drift.data_ptr(), dtop.data_ptr(), _ptr(zero),
+        int(zero.numel()) if zero is not None else 0, _native.stream_ptr(stream)), "kmeans_cert_stats")
+
+
+def cert_bounds(lab, u, l, drift, dtop, s, n: int, lst, count, stream=None) -> None:
+    _native.check(_native.kernels().cml_kmeans_cert_bounds(
+        lab.data_ptr(), u.data_ptr(), l.data_ptr(), drift.data_ptr(), dtop.data_ptr(), s.data_ptr(), int(n),
+        lst.data_ptr(), count.data_ptr(), _native.stream_ptr(stream)), "kmeans_cert_bounds")
+
+
+def cert_tighten(x: torch.Tensor, C: torch.Tensor, lab, u, l, s, la, na, lbst, nbst, stream=None) -> None:
+    n = int(x.shape[0])
+    _native.check(_native.kernels().cml_kmeans_cert_tighten(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(C.shape[1]), C.data_ptr(), lab.data_ptr(),
+        u.data_ptr(), l.data_ptr(), s.data_ptr(), la.data_ptr(), na.data_ptr(), lbst.data_ptr(), nbst.data_ptr(),
+        _native.stream_ptr(stream)), "kmeans_cert_tighten")
+
+
+def cert_slices(k: int) -> int:
+    return int(_native.kernels().cml_kmeans_cert_slices(int(k)))
+
+
+def cert_moves(x: torch.Tensor, k: int, mv_row, mv_old, mv_new, m_dev, hist, seg, cursor, perm, P_hi, P_lo,
+               S_hi, S_lo, cnt, stream=None) -> None:
+    """Apply the label moves to the double-double cluster sums S_hi / S_lo and the int32 counts."""
+    n, d = int(x.shape[0]), int(S_hi.shape[1])
+    _native.check(_native.kernels().cml_kmeans_cert_moves(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, int(k), mv_row.data_ptr(), mv_old.data_ptr(),
+        mv_new.data_ptr(), m_dev.data_ptr(), hist.data_ptr(), seg.data_ptr(), cursor.data_ptr(), perm.data_ptr(),
+        P_hi.data_ptr(), P_lo.data_ptr(), S_hi.data_ptr(), S_lo.data_ptr(), cnt.data_ptr(), 0, 0, 0,
+        _native.stream_ptr(stream)), "kmeans_cert_moves")
+
+
+def dd_fold(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
+    """Rounded sum over the leading (rank) axis of double-double values [W, ...], in rank order (TwoSum
+    per step, exact while the values' exponents span < ~2^80): the same bits as one rank's sums."""
+    h, l = hi[0].clone(), lo[0].clone()
+    for w in range(1, int(hi.shape[0])):
+        v = hi[w]
+        s = h + v
+        bb = s - h
+        l = l + ((h - (s - bb)) + (v - bb))
+        l = l + lo[w]
+        h = s
+    return h + l
 
 
 def assign_reference(x: torch.Tensor, centers: torch.Tensor, chunk: int = 1 << 16):
@@ -916,21 +1008,23 @@ def _assign_reference_blas(x: torch.Tensor, centers: torch.Tensor, chunk: int = 
     return labels, best
 
 
-def sums_reference(x: torch.Tensor, labels: torch.Tensor, k: int):
+def sums_reference(x: torch.Tensor, labels: torch.Tensor, k: int, with_lo: bool = False):
+    """Correctly rounded per-cluster sums and counts (f64); ``with_lo`` adds the double-double remainders."""
     if x.is_cuda:
-        return exact_sums(x, labels, k)
+        return exact_sums(x, labels, k, with_lo=with_lo)
     x = x.to(torch.float64)
     if x.stride(-1) != 1:
         x = x.contiguous()
     n, d = int(x.shape[0]), int(x.shape[1])
     lab = labels.to(torch.int64).contiguous()
     S = torch.empty((k, d), dtype=torch.float64)
+    S_lo = torch.empty((k, d), dtype=torch.float64)
     cnt = torch.empty(k, dtype=torch.float64)
     r = _native.host().cml_exact_sums_host(x.data_ptr(), n, x.stride(0), d, lab.data_ptr(), int(k), S.data_ptr(),
-                                           cnt.data_ptr())
+                                           cnt.data_ptr(), S_lo.data_ptr() if with_lo else 0)
     if r != 0:
         raise ValueError("sums_reference: labels outside [0, k)")
-    return S, cnt
+    return (S, cnt, S_lo) if with_lo else (S, cnt)
 
 
 def _sums_reference_torch(x: torch.Tensor, labels: torch.Tensor, k: int):

@@ -15,7 +15,7 @@ import json,sys; d=json.loads(sys.stdin.read()); e=d['extra']
 print('cfg2 f32 screen fit ms', e['fit_s']*1000, e['precision'], 'init', e['breakdown']['init_ms'], e['breakdown']['iteration_ms'][:5])"
 timeout -k 10 300 rocprofv3 --kernel-trace -d $O/scr -o scr -- python3 bench.py --rows 10000000 --dim 128 --k 64 --dtype f32 --warmup 1 --steps 20 --no-overlap > $O/scr.log 2>&1 || { tail -5 $O/scr.log; exit 1; }
 python3 scripts/rocpd_stats.py $O/scr/scr_results.db --marker to_bf16_err --index 1 --top 25
-timeout -k 10 200 python3 scripts/mb_glm_fp8.py > $O/mb_glm_fp8.log 2>&1 || { tail -5 $O/mb_glm_fp8.log; exit 1; }
+PYTHONPATH=$GRAFT_REPO_ROOT timeout -k 10 200 python3 scripts/mb_glm_fp8.py > $O/mb_glm_fp8.log 2>&1 || { tail -5 $O/mb_glm_fp8.log; exit 1; }
 cat $O/mb_glm_fp8.log | grep -v amdgpu
 timeout -k 10 300 python3 scripts/mb_dropna.py > $O/mb_dropna.log 2>&1 || { tail -5 $O/mb_dropna.log; exit 1; }
 head -10 $O/mb_dropna.log | grep -v amdgpu

@@ -79,3 +79,79 @@ def test_screen_kernels():
     sel = idx.long()
     assert torch.equal(l2[sel], lab[sel]) and torch.equal(b3[sel], best[sel])
     assert int((l2 >= 0).sum()) == 3
+
+
+@pytest.mark.parametrize("n,d,k,dt", [(300_001, 7, 9, torch.float64), (50_000, 130, 33, torch.float32)])
+def test_device_sums_double_double_equal_host_twin(n, d, k, dt):
+    g = torch.Generator().manual_seed(d)
+    x = (torch.randn(n, d, generator=g, dtype=torch.float64) * torch.logspace(-4, 8, n, dtype=torch.float64)[:, None])
+    x = x.to(dt)
+    lab = torch.randint(0, k, (n,), generator=g)
+    Sh, ch, Lh = K.sums_reference(x, lab, k, with_lo=True)
+    Sd, cd, Ld = K.exact_sums(x.cuda(), lab.cuda(), k, with_lo=True)
+    assert torch.equal(Sd.cpu(), Sh) and torch.equal(cd.cpu(), ch)
+    # the remainders agree as values of the exact sum (hi + lo), normalised both ways
+    assert torch.equal(Ld.cpu(), Lh)
+
+
+@pytest.mark.parametrize("n,d,k,dt", [(70_001, 128, 64, torch.float32), (20_000, 300, 17, torch.float64),
+                                      (9_999, 24, 200, torch.float32)])
+def test_exact_top2_bits_and_bounds(n, d, k, dt):
+    g = torch.Generator(device="cuda").manual_seed(n)
+    x = (torch.randn(n, d, device="cuda", generator=g, dtype=torch.float64) * 3).to(dt)
+    C = torch.randn(k, d, device="cuda", generator=g, dtype=torch.float64) * 3
+    lab, best = K.exact_assign(x, C)
+    l2 = torch.full((n,), -1, dtype=torch.int32, device="cuda")
+    b2 = torch.empty(n, dtype=torch.float64, device="cuda")
+    ub = torch.empty(n, dtype=torch.float32, device="cuda")
+    lb = torch.empty(n, dtype=torch.float32, device="cuda")
+    K.exact_top2(x, C, l2, ub, lb, best=b2)
+    assert torch.equal(l2, lab[:n]) and torch.equal(b2, best[:n])
+    D = ((x.double()[:, None, :] - C[None]) ** 2).sum(-1).sqrt()
+    own = D.gather(1, lab[:n].long()[:, None])[:, 0]
+    other = D.scatter(1, lab[:n].long()[:, None], float("inf")).min(1).values
+    assert bool((ub.double() >= own).all()) and bool((lb.double() <= other).all())
+    assert bool((ub.double() <= own * (1 + 1e-6) + 1e-30).all())
+    # listed rows with moves: only listed rows change; moves report (row, old, new)
+    l3 = torch.zeros(n, dtype=torch.int32, device="cuda")
+    idx = torch.arange(0, n, 3, dtype=torch.int32, device="cuda")
+    idx_full = torch.zeros(n, dtype=torch.int32, device="cuda")
+    idx_full[: idx.numel()] = idx
+    cnt = torch.tensor([idx.numel()], dtype=torch.int32, device="cuda")
+    mv = [torch.zeros(n, dtype=torch.int32, device="cuda") for _ in range(3)] + [torch.zeros(1, dtype=torch.int32,
+                                                                                             device="cuda")]
+    K.exact_top2(x, C, l3, ub, lb, idx=idx_full, n_dev=cnt, moves=tuple(mv))
+    sel = idx.long()
+    assert torch.equal(l3[sel], lab[sel])
+    rest = torch.ones(n, dtype=torch.bool, device="cuda")
+    rest[sel] = False
+    assert int(l3[rest].abs().sum()) == 0
+    m = int(mv[3].item())
+    moved = sel[lab[sel] != 0]
+    assert m == moved.numel()
+    rows = mv[0][:m].long().sort().values
+    assert torch.equal(rows, moved.sort().values)
+    assert bool((mv[1][:m] == 0).all()) and torch.equal(mv[2][:m], lab[mv[0][:m].long()])
+
+
+@pytest.mark.parametrize("n,d,k,scale", [(400_000, 128, 64, 4.0), (150_001, 96, 20, 0.5)])
+def test_certified_steps_prune_and_equal_exact(monkeypatch, n, d, k, scale):
+    """The certified pruned steps (kmeans_cert.hip) list few rows once the centres settle, and the fit
+    equals the exact path bit for bit (labels, centres, cost) — incremental double-double sums included."""
+    x = _blobs(n, d, k, seed=7, scale=scale, dtype=torch.float32, offset=-20.0).cuda()
+    res = {}
+    for prec in ("exact", "screen"):
+        eng = LloydEngine(x, d, k, precision=prec)
+        eng.track_prune = True
+        eng.set_centers(eng.init_kmeans_parallel(seed=1))
+        it = eng.fit(12, 0.0)
+        res[prec] = (it, eng.centers.cpu().numpy(), eng.labels[:n].long().cpu(), eng.training_cost())
+        if prec == "screen":
+            hist = eng._scr.cert.history
+            assert len(hist) == 11
+            a, b, m = hist[-1]
+            assert b <= a <= n
+            if scale > 1:
+                assert a < n // 5 and b < n // 20, hist
+    (t0, c0, l0, f0), (t1, c1, l1, f1) = res["exact"], res["screen"]
+    assert t0 == t1 and np.array_equal(c0, c1) and torch.equal(l0, l1) and f0 == f1
