@@ -798,7 +798,9 @@ int g_fp8_nch = 0;  // ablation: chunks per lane of the fp8 (16 values / chunk) 
 
 inline bool stream_layout(int d, int cpt, int& lpr, int& nch) {
   const int ch = (d + cpt - 1) / cpt;
-  int want = 16 / cpt > 0 ? 16 / cpt : 1;
+  // two 16-B chunks per lane for bf16 and fp8 alike: fp8 x 512 at one chunk per lane kept too few bytes in
+  // flight (K13 4.14 -> 5.09 TB/s, K24 5.12 -> 5.80 TB/s at two; four spill: profiles/r4/glm_fp8_layout.log)
+  int want = cpt >= 16 ? 2 : (16 / cpt > 0 ? 16 / cpt : 1);
   if (cpt == 16 && g_fp8_nch > 0) want = g_fp8_nch;
   nch = ch < want ? pow2ceil(ch) : want;
   lpr = pow2ceil((ch + nch - 1) / nch);

@@ -730,6 +730,12 @@ class LloydEngine:
         st = self._screen_state()
         n, dev = self.n, self.device
         cands = cands.to(device=dev, dtype=torch.float64)
+        if int(cands.shape[0]) == 1:  # one candidate: every label is 0, the distance one exact fold
+            lab1 = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+            b1 = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+            if n:
+                K.exact_dist(self.x, cands.contiguous(), lab1, b1)
+            return b1[:n], lab1[:n].long()
         best = torch.full((max(n, 1),), math.inf, dtype=torch.float64, device=dev)
         lab = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)
         lab_c = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
@@ -1414,6 +1420,20 @@ class LloydEngine:
         longer prove, and K9r re-assigns only those (the full pass when there are too many), on copies of
         the labels and bounds — the engine's own step state is untouched. Other paths run a full assign."""
         n, k = self.n, self.k
+        c = getattr(self._scr, "cert", None) if getattr(self, "_scr", None) is not None else None
+        if self._screen and n and c is not None and c.valid:
+            # certified pruned assign on copies: the bounds moved by the last update's drifts prove most
+            # labels; the rest are tightened and re-assigned by the exact fold (same labels as a full pass)
+            st = self._scr
+            lab, u, l = c.lab.clone(), st.ub.clone(), st.lb.clone()
+            ctr = torch.zeros(4 + 2 * k, dtype=torch.int32, device=self.device)
+            la, lbl = torch.empty_like(c.la), torch.empty_like(c.lbl)
+            s_, drift, dtop = torch.empty_like(c.s), torch.empty_like(c.drift), torch.zeros_like(c.dtop)
+            K.cert_stats(self.centers, c.C_cur, s_, drift, dtop, zero=ctr)
+            K.cert_bounds(lab, u, l, drift, dtop, s_, n, la, ctr[0:1])
+            K.cert_tighten(self.x, self.centers, lab, u, l, s_, la, ctr[0:1], lbl, ctr[1:2])
+            K.exact_top2(self.x, self.centers, lab, u, l, idx=lbl, n_dev=ctr[1:2])
+            return lab[:n]
         if not (self._pdev and n):
             return self.assign()[0]
         st, ap = self._pst, self.aplan
@@ -1748,7 +1768,8 @@ class LloydEngine:
         counts its relevant candidates (kmeans init_classify); rows with none are done, rows with at
         most _INIT_LMAX get those distances from a per-row kernel, the rest run the K9r candidate pass
         over their positions (mode 2). Same nearest candidates as the full pass up to the rounding of
-        near-ties. Returns False (nothing changed) when too many rows need the K9r pass to gain."""
+        near-ties. No host read: the list sizes stay on the device (the launches are sized by capacity).
+        Returns False (nothing changed) when the pruned pass does not apply (host rows, pruning off)."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
         if not self._pdev or os.environ.get("CML_KMEANS_INIT_PRUNE", "1") == "0" or not self._rr_max_chunk():
             return False
@@ -1769,35 +1790,36 @@ class LloydEngine:
         list_a = torch.empty((n, 4), dtype=torch.int32, device=dev)  # (row, nearest, reach, cost) entries
         list_b = torch.zeros(n + tr, dtype=torch.int32, device=dev)  # padded: whole tiles of valid rows
         cnt = torch.zeros(2, dtype=torch.int32, device=dev)
-        K.init_classify(costs, nearest, self.xnorm, pn32, tab_v, tau, n, self._INIT_LMAX, list_a, cnt[0:1], list_b,
-                        cnt[1:2])
-        ca, cb = (int(v) for v in cnt.tolist())
-        if cb > 0.6 * n:
-            return False
+        # per-row path limit: each listed candidate costs the row a read of its dp-wide bf16 copy from L2
+        # (1 KiB at dp = 512), so wide rows hand longer lists to the MFMA pass sooner
+        lmax = int(os.environ.get("CML_KMEANS_INIT_LMAX", self._INIT_LMAX if dp <= 256 else 4))
+        lmax = max(0, min(self._INIT_LMAX, lmax))
+        K.init_classify(costs, nearest, self.xnorm, pn32, tab_v, tau, n, lmax, list_a, cnt[0:1], list_b, cnt[1:2])
+        # no host read of the list sizes: the per-row kernel and the K9r candidate pass take them from the
+        # device and size their grids by the capacity (dead tiles exit at once)
         yb = torch.zeros((m, dp), dtype=torch.bfloat16, device=dev)
         yb[:, :d] = Y.to(torch.bfloat16)
-        if ca:
-            K.init_near_list(self.x, dp, costs, nearest, self.xnorm, pn32, tab_v, tab_j, yb, off, tau, list_a,
-                             cnt[0:1], ca)
-        if cb:
-            st = self._pst
-            pad = -(-cb // tr) * tr + tr
-            cxn = torch.zeros(pad, dtype=torch.float32, device=dev)
-            cxn[:cb] = self.xnorm[list_b[:cb].long()]
-            lab_in = torch.full((pad,), -1, dtype=torch.int32, device=dev)
-            c0 = 0
-            for size in self._candidate_chunks(m):
-                kp = round_up(size, 32)
-                cbk = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
-                cnk = torch.zeros(kp, dtype=torch.float32, device=dev)
-                K.update_centers(None, size, d, Y[c0:c0 + size].contiguous().clone(), cbk, dp, kp, cnk, None)
-                plan = K.plan_assign(cb, dp, size, dev.index or 0, fp8=K.is_fp8(self.x))
-                mc = cnk[:size].max().reshape(1)
-                K.assign_rr_ext(2, self.x, cb, dp, cbk, cnk, plan, cxn, self.labels, None, st.ub, st.lb, mc,
-                                self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, merge_cost=costs,
-                                merge_near=nearest, merge_off=off + c0)
-                c0 += size
+        K.init_near_list(self.x, dp, costs, nearest, self.xnorm, pn32, tab_v, tab_j, yb, off, tau, list_a,
+                         cnt[0:1], n)
+        st = self._pst
+        pad = list_b.shape[0]
+        cxn = torch.zeros(pad, dtype=torch.float32, device=dev)
+        torch.index_select(self.xnorm[:n], 0, list_b[:n], out=cxn[:n])  # entries past the count: row 0's, unread
+        lab_in = torch.full((pad,), -1, dtype=torch.int32, device=dev)
+        c0 = 0
+        for size in self._candidate_chunks(m):
+            kp = round_up(size, 32)
+            cbk = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
+            cnk = torch.zeros(kp, dtype=torch.float32, device=dev)
+            K.update_centers(None, size, d, Y[c0:c0 + size].contiguous().clone(), cbk, dp, kp, cnk, None)
+            plan = K.plan_assign(n, dp, size, dev.index or 0, fp8=K.is_fp8(self.x))
+            mc = cnk[:size].max().reshape(1)
+            K.assign_rr_ext(2, self.x, n, dp, cbk, cnk, plan, cxn, self.labels, None, st.ub, st.lb, mc,
+                            self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, merge_cost=costs,
+                            merge_near=nearest, merge_off=off + c0)
+            c0 += size
         if self.track_prune:
+            ca, cb = (int(v) for v in cnt.tolist())
             self._init_prune_history = getattr(self, "_init_prune_history", []) + [(n, ca, cb)]
         return True
 

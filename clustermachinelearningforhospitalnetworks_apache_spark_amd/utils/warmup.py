@@ -39,6 +39,16 @@ def warm_device(device: torch.device, pool_bytes: int = 1 << 30) -> float:
     idx = frame_ops.compact(keep)
     for t in (x[:, 0], xi, valid, x):
         t[idx]
+    # every column dtype a frame holds (numbers, dictionary string codes, masks): its null test, the
+    # int32 tally, and the row gather of the compaction
+    for dt in (torch.float32, torch.float64, torch.int8, torch.int16, torch.int32, torch.int64, torch.uint8,
+               torch.bool, torch.bfloat16):
+        t = x[:, 3].to(dt)
+        if t.is_floating_point():
+            (~torch.isnan(t)).to(torch.int32)
+        (t != 0).to(torch.int32)
+        t[idx]
+        t[keep]
     # VectorAssembler (K2) and the GLM / evaluator kernels of a per-batch fit
     m, bad = frame_ops.assemble([(x[:, j], None) for j in range(d)] + [(xi, valid)], out_dtype=torch.float64)
     bool(bad.any())

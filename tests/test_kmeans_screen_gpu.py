@@ -155,3 +155,18 @@ def test_certified_steps_prune_and_equal_exact(monkeypatch, n, d, k, scale):
                 assert a < n // 5 and b < n // 20, hist
     (t0, c0, l0, f0), (t1, c1, l1, f1) = res["exact"], res["screen"]
     assert t0 == t1 and np.array_equal(c0, c1) and torch.equal(l0, l1) and f0 == f1
+
+
+def test_screen_final_labels_pruned_equal_full_assign():
+    n, d, k = 200_000, 128, 48
+    x = _blobs(n, d, k, seed=3, scale=2.0, dtype=torch.float32).cuda()
+    eng = LloydEngine(x, d, k, precision="screen")
+    eng.set_centers(eng.init_kmeans_parallel(seed=2))
+    eng.fit(5, 0.0)
+    lab_state = eng.labels.clone()
+    fast = eng.final_labels()
+    full, _ = K.exact_assign(x, eng.centers)
+    assert torch.equal(fast.long(), full[:n].long())
+    assert torch.equal(eng.labels, lab_state)
+    assert eng.cluster_sizes() == torch.bincount(full[:n].long(), minlength=k).tolist()
+    eng.step()  # the state is untouched: the next step goes on from it
