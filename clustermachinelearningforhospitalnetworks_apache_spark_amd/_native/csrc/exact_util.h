@@ -59,3 +59,29 @@ __device__ __forceinline__ int block_append(bool flag, int* count, int* s_w) {
   __syncthreads();  // s_w is reused by the next call
   return pos;
 }
+
+// LDS-buffered list append for kernels whose rows append sparsely: entries gather in an LDS buffer
+// (LDS atomics; the order inside a block is free) and reach the global list in one reservation per
+// flush. Call list_flush(..., false) after each block-uniform step (it flushes when fewer than NT slots
+// are left) and list_flush(..., true) at the end.
+constexpr int kBuf = 2048;
+struct ListBuf {
+  int* buf;
+  int* n;
+  int* base;
+};
+
+template <int NT>
+__device__ __forceinline__ void list_flush(ListBuf lb, int* lst, int* count, bool force) {
+  __syncthreads();
+  const int m = *lb.n;
+  if (m > 0 && (force || m > kBuf - NT)) {
+    if (threadIdx.x == 0) *lb.base = atomicAdd(count, m);
+    __syncthreads();
+    const int b = *lb.base;
+    for (int i = threadIdx.x; i < m; i += NT) lst[b + i] = lb.buf[i];
+    __syncthreads();
+    if (threadIdx.x == 0) *lb.n = 0;
+  }
+  __syncthreads();
+}

@@ -24,29 +24,6 @@
 namespace {
 
 constexpr int kT = 256;
-constexpr int kBuf = 2048;  // LDS list buffer of the list producers (flushed with one global atomic)
-
-// LDS-buffered list append: entries gather in LDS (LDS atomics) and reach the global list in one
-// reservation per flush. Call flush_if(false) after each block-uniform step and flush_if(true) at the end.
-struct ListBuf {
-  int* buf;
-  int* n;
-  int* base;
-};
-
-__device__ __forceinline__ void list_flush(ListBuf lb, int* lst, int* count, bool force) {
-  __syncthreads();
-  const int m = *lb.n;
-  if (m > 0 && (force || m > kBuf - kT)) {
-    if (threadIdx.x == 0) *lb.base = atomicAdd(count, m);
-    __syncthreads();
-    const int b = *lb.base;
-    for (int i = threadIdx.x; i < m; i += kT) lst[b + i] = lb.buf[i];
-    __syncthreads();
-    if (threadIdx.x == 0) *lb.n = 0;
-  }
-  __syncthreads();
-}
 
 // grid k + 1: block j < k -> s[j] = half the distance from centre j to the nearest other centre (f32,
 // rounded down; +inf for k = 1); block k -> drift[j] = ||C_j - Cold_j|| (rounded up) for every j and
@@ -150,9 +127,9 @@ __global__ __launch_bounds__(kT) void cert_bounds_kernel(const int* __restrict__
       l[r] = ll;
       if (!(uu < fmaxf(ll, s[a]))) buf[atomicAdd(&nb, 1)] = (int)r;
     }
-    list_flush(lb, lst, count, false);
+    list_flush<kT>(lb, lst, count, false);
   }
-  list_flush(lb, lst, count, true);
+  list_flush<kT>(lb, lst, count, true);
 }
 
 // Listed rows (A): u <- the real distance to the label (16 lanes per row, any summation order: a bound
@@ -196,9 +173,9 @@ __global__ __launch_bounds__(kT) void cert_tighten_kernel(const T* __restrict__ 
       u[r] = uu;
       if (!(uu < fmaxf(l[r], s[a]))) buf[atomicAdd(&nb, 1)] = (int)r;
     }
-    list_flush(lbf, lbst, nbst, false);
+    list_flush<kT>(lbf, lbst, nbst, false);
   }
-  list_flush(lbf, lbst, nbst, true);
+  list_flush<kT>(lbf, lbst, nbst, true);
 }
 
 // Move histogram: bin j = rows moving into cluster j, bin k + j = rows leaving it.

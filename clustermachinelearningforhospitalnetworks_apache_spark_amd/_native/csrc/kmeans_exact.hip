@@ -229,6 +229,80 @@ __global__ __launch_bounds__(kThreads) void to_bf16_err_kernel(const T* __restri
   }
 }
 
+// Split screen (d <= 170): row r -> [hi | lo | hi] in three ds-wide segments of a zero-padded bf16 row
+// (hi = bf16(x), lo = bf16(x - hi)), so that against centres laid out [c_hi | c_hi | c_lo] the MFMA dot is
+// hi·c_hi + lo·c_hi + hi·c_lo: x·c to ~2^-16 instead of ~2^-8 (the plain screen left ~24 % of k-means‖
+// rows inside the bf16 error band on same-blob candidates). Per row: ea = ||lo||, eb = ||x - hi - lo||,
+// en = ||x|| (f32, rounded up) and xn = ||x||² (f32, the K9r row norm).
+template <typename T>
+__global__ __launch_bounds__(kThreads) void to_bf16_split_kernel(const T* __restrict__ X, long long n, long long ldx,
+                                                                 int d, int ds, u16* __restrict__ out, long long ldo,
+                                                                 float* __restrict__ ea, float* __restrict__ eb,
+                                                                 float* __restrict__ en, float* __restrict__ xn) {
+  const int lane = threadIdx.x & 63;
+  const long long w0 = ((long long)blockIdx.x * kThreads + threadIdx.x) >> 6;
+  const long long nw = ((long long)gridDim.x * kThreads) >> 6;
+  for (long long r = w0; r < n; r += nw) {
+    double a2 = 0.0, b2 = 0.0, n2 = 0.0;
+    for (int t = lane; t < ldo; t += 64) out[r * ldo + t] = 0;
+    for (int t = lane; t < d; t += 64) {
+      const double v = (double)X[r * ldx + t];
+      const u16 h = f32_to_bf16((float)v);
+      const double r1 = v - (double)bf16_to_f32(h);
+      const u16 l = f32_to_bf16((float)r1);
+      const double rx = r1 - (double)bf16_to_f32(l);
+      const double lv = (double)bf16_to_f32(l);
+      a2 = __fma_rn(lv, lv, a2);
+      b2 = __fma_rn(rx, rx, b2);
+      n2 = __fma_rn(v, v, n2);
+      out[r * ldo + t] = h;
+      out[r * ldo + ds + t] = l;
+      out[r * ldo + 2 * ds + t] = h;
+    }
+    a2 = wave_sum_f64(a2);
+    b2 = wave_sum_f64(b2);
+    n2 = wave_sum_f64(n2);
+    if (lane == 0) {
+      ea[r] = f32_up(sqrt(a2) * (1.0 + 1e-6));
+      eb[r] = f32_up(sqrt(b2) * (1.0 + 1e-6) + 1e-300);
+      en[r] = f32_up(sqrt(n2) * (1.0 + 1e-6));
+      xn[r] = (float)n2;
+    }
+  }
+}
+
+// Split-screen certificate: with cst = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} the squared
+// distances of the split model differ from the real ones by at most E = 2(ea·cst0 + eb·cst1 +
+// 1.01·en·cst2) per row; the label is certified when sqrt(lb² - E) > sqrt(ub² + E), and u_out / l_out
+// get those bounds (rounded outward).
+__global__ __launch_bounds__(kThreads) void screen_cert_split_kernel(
+    const float* __restrict__ ub, const float* __restrict__ lb, const float* __restrict__ ea,
+    const float* __restrict__ eb, const float* __restrict__ en, const double* __restrict__ cst, long long n,
+    int* __restrict__ lst, int* __restrict__ count, float* __restrict__ u_out, float* __restrict__ l_out) {
+  __shared__ int buf[kBuf];
+  __shared__ int nb, base;
+  if (threadIdx.x == 0) nb = 0;
+  ListBuf lbf{buf, &nb, &base};
+  const double c0 = cst[0], c1 = cst[1], c2 = cst[2];
+  for (long long i0 = (long long)blockIdx.x * kThreads; i0 < n; i0 += (long long)gridDim.x * kThreads) {
+    __syncthreads();
+    const long long i = i0 + threadIdx.x;
+    bool bad = false;
+    if (i < n) {
+      const double e = 2.0 * ((double)ea[i] * c0 + (double)eb[i] * c1 + 1.01 * (double)en[i] * c2) * (1.0 + 1e-6);
+      const double ubi = (double)ub[i], lbi = (double)lb[i];
+      const float uu = f32_up(sqrt(ubi * ubi + e) * (1.0 + kFoldMargin));
+      const float ll = f32_dn(sqrt(fmax(lbi * lbi - e, 0.0)) * (1.0 - kFoldMargin));
+      bad = !(uu < ll);
+      u_out[i] = uu;
+      l_out[i] = ll;
+      if (bad) buf[atomicAdd(&nb, 1)] = (int)i;
+    }
+    list_flush<kThreads>(lbf, lst, count, false);
+  }
+  list_flush<kThreads>(lbf, lst, count, true);
+}
+
 // Rows whose bf16-screen label is not certified (kmeans_screen_cert) are appended to lst (count
 // zeroed by the caller): certified when lb - ub > 2·(err_r + ecmax), ub / lb the K9r top-2 bounds
 // of the bf16 distances (their f32 rounding already inside) and ecmax >= max_j ||c_j - bf16(c_j)||:
@@ -548,5 +622,34 @@ CML_API int cml_kmeans_exact_segsum(const void* X, int xf64, long long ldx, int 
                          k, n, S, S_lo, slots, slot_c);
   }
   hipLaunchKernelGGL(exact_seg_fix_kernel, dim3(k), dim3(kThreads), 0, st, seg, k, d, nch, S, S_lo, slots, slot_c);
+  return cml_status();
+}
+
+// out: bf16 [n, ldo] with ldo >= 3·ds, ds >= d; ea / eb / en / xn: f32 [n].
+CML_API int cml_kmeans_to_bf16_split(const void* X, int xf64, long long n, long long ldx, int d, int ds, void* out,
+                                     long long ldo, float* ea, float* eb, float* en, float* xn, void* stream) {
+  if (n <= 0) return 0;
+  if (d <= 0 || ds < d || ldo < 3LL * ds) return (int)hipErrorInvalidValue;
+  long long g = (n + 3) / 4;
+  g = g > 8192 ? 8192 : g;
+  hipStream_t st = (hipStream_t)stream;
+  if (xf64)
+    hipLaunchKernelGGL((to_bf16_split_kernel<double>), dim3((unsigned)g), dim3(kThreads), 0, st, (const double*)X, n,
+                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn);
+  else
+    hipLaunchKernelGGL((to_bf16_split_kernel<float>), dim3((unsigned)g), dim3(kThreads), 0, st, (const float*)X, n,
+                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn);
+  return cml_status();
+}
+
+// cst: f64 [3] device; lst int [n], count int [1] zeroed by the caller; u_out / l_out f32 [n] (may be ub / lb).
+CML_API int cml_kmeans_screen_cert_split(const float* ub, const float* lb, const float* ea, const float* eb,
+                                         const float* en, const double* cst, long long n, int* lst, int* count,
+                                         float* u_out, float* l_out, void* stream) {
+  if (n <= 0) return 0;
+  long long g = (n + kThreads - 1) / kThreads;
+  g = g > 2048 ? 2048 : g;
+  hipLaunchKernelGGL(screen_cert_split_kernel, dim3((unsigned)g), dim3(kThreads), 0, (hipStream_t)stream, ub, lb, ea,
+                     eb, en, cst, n, lst, count, u_out, l_out);
   return cml_status();
 }

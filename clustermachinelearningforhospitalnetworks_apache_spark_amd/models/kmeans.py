@@ -658,18 +658,32 @@ class LloydEngine:
         if self._scr is not None:
             return self._scr
         n, d, dev = self.n, self.d, self.device
-        dp = padded_dim(d)
+        # split screen when three segments of the row fit one K9r row (d <= 170): x·c to ~2^-16, so the
+        # certificate leaves only real near-ties for the f64 re-check (CML_KMEANS_SCREEN_SPLIT=0: plain)
+        ds = round_up(d, 8)
+        split = (3 * ds <= 512 and os.environ.get("CML_KMEANS_SCREEN_SPLIT", "1") != "0"
+                 and K.plan_assign(1, 512, self.k).rr_ct > 0)
+        dp = 512 if split else padded_dim(d)
+        key = ("split", ds) if split else ("plain", dp)
         ent = getattr(self.x, "_cml_screen", None)
-        if ent is not None and ent[0] == self.x._version and ent[1] == (n, d):
-            xb, ex = ent[2], ent[3]
+        if ent is not None and ent[0] == self.x._version and ent[1] == (n, d) and ent[2] == key:
+            parts = ent[3]
         else:
-            xb, ex = K.to_bf16_err(self.x, d, dp)
+            parts = K.to_bf16_split(self.x, d, ds, dp) if split else K.to_bf16_err(self.x, d, dp)
             try:
-                self.x._cml_screen = (self.x._version, (n, d), xb, ex)
+                self.x._cml_screen = (self.x._version, (n, d), key, parts)
             except (AttributeError, RuntimeError):
                 pass
-        st = types.SimpleNamespace(xb=xb, ex=ex, dp=dp, tau=self.prune_tau(dp))
-        st.xn = cached_row_sqnorm(xb, n, dp) if n else torch.zeros(1, dtype=torch.float32, device=dev)
+        if split:
+            xb, ea, eb, en, xn = parts
+            # the augmented products sum to at most |x|² + |c|² (twice the plain row's): twice the slack
+            st = types.SimpleNamespace(xb=xb, ea=ea, eb=eb, en=en, ex=None, dp=dp, ds=ds, split=True,
+                                       tau=2.0 * self.prune_tau(dp))
+            st.xn = xn
+        else:
+            xb, ex = parts
+            st = types.SimpleNamespace(xb=xb, ex=ex, dp=dp, split=False, tau=self.prune_tau(dp))
+            st.xn = cached_row_sqnorm(xb, n, dp) if n else torch.zeros(1, dtype=torch.float32, device=dev)
         st.rr_max = 0
         for c in (320, 256, 192, 128, 64):
             p = K.plan_assign(1, dp, c)
@@ -705,13 +719,19 @@ class LloydEngine:
         kp = round_up(kc, 32)
         st.cb[:kp].zero_()
         st.cn[:kp].zero_()
-        K.update_centers(None, kc, d, C.clone(), st.cb[:kp], st.dp, kp, st.cn[:kp], None)
+        if st.split:
+            cst = K.split_centres(C, st.ds, st.cb, st.cn)
+        else:
+            K.update_centers(None, kc, d, C.clone(), st.cb[:kp], st.dp, kp, st.cn[:kp], None)
+            ecmax = ((C - st.cb[:kc, :d].to(torch.float64)) ** 2).sum(1).max().sqrt().reshape(1) * (1.0 + 1e-9)
         mc = st.cn[:kc].max().reshape(1)
-        ecmax = ((C - st.cb[:kc, :d].to(torch.float64)) ** 2).sum(1).max().sqrt().reshape(1) * (1.0 + 1e-9)
         plan = K.plan_assign(n, st.dp, kc)
         K.assign_rr_ext(1, st.xb, n, st.dp, st.cb[:kp], st.cn[:kp], plan, st.xn, lab, None, st.ub, st.lb, mc, st.tau)
         st.cnt.zero_()
-        K.screen_cert(st.ub, st.lb, st.ex, ecmax, n, st.lst, st.cnt, u_out=st.ub, l_out=st.lb)
+        if st.split:
+            K.screen_cert_split(st.ub, st.lb, st.ea, st.eb, st.en, cst, n, st.lst, st.cnt, st.ub, st.lb)
+        else:
+            K.screen_cert(st.ub, st.lb, st.ex, ecmax, n, st.lst, st.cnt, u_out=st.ub, l_out=st.lb)
         if best is not None:
             K.exact_dist(self.x, C, lab, best)
         K.exact_top2(self.x, C, lab, st.ub, st.lb, idx=st.lst, n_dev=st.cnt, best=best)

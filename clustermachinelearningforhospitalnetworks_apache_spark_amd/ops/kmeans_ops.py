@@ -106,6 +106,9 @@ _native.register_kernel_sigs({
                                         c_vp]),
     "cml_kmeans_exact_top2": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_to_bf16_split": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp,
+                                         c_vp]),
+    "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -859,6 +862,42 @@ def screen_cert(ub: torch.Tensor, lb: torch.Tensor, err: torch.Tensor, ecmax: to
     _native.check(_native.kernels().cml_kmeans_screen_cert(
         ub.data_ptr(), lb.data_ptr(), err.data_ptr(), ecmax.data_ptr(), int(n), lst.data_ptr(), count.data_ptr(),
         _ptr(u_out), _ptr(l_out), _native.stream_ptr(stream)), "kmeans_screen_cert")
+
+
+def to_bf16_split(x: torch.Tensor, d: int, ds: int, ldo: int, stream=None):
+    """Split-screen copy of device f32/f64 rows: bf16 [n, ldo] = [hi | lo | hi] in ds-wide segments, and
+    f32 [n] ||lo||, ||x - hi - lo||, ||x|| (rounded up) and ||x||² (the K9r row norm)."""
+    n = int(x.shape[0])
+    out = torch.empty((max(n, 1), ldo), dtype=torch.bfloat16, device=x.device)
+    ea, eb, en, xn = (torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(4))
+    _native.check(_native.kernels().cml_kmeans_to_bf16_split(
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(d), int(ds), out.data_ptr(), int(ldo),
+        ea.data_ptr(), eb.data_ptr(), en.data_ptr(), xn.data_ptr(), _native.stream_ptr(stream)), "kmeans_to_bf16_split")
+    return (out[:n] if n else out[:0]), ea, eb, en, xn
+
+
+def split_centres(C: torch.Tensor, ds: int, cb: torch.Tensor, cn: torch.Tensor) -> torch.Tensor:
+    """Centres (f64 [k, d]) in the split screen's layout: cb[:k] = [c_hi | c_hi | c_lo] (bf16), cn[:k] =
+    ||c||² (f32); returns f64 [3] = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} (device)."""
+    k, d = int(C.shape[0]), int(C.shape[1])
+    ch = C.to(torch.bfloat16)
+    r = C - ch.to(torch.float64)
+    cl = r.to(torch.bfloat16)
+    rc = r - cl.to(torch.float64)
+    cb[:k].zero_()
+    cb[:k, :d] = ch
+    cb[:k, ds:ds + d] = ch
+    cb[:k, 2 * ds:2 * ds + d] = cl
+    cn[:k] = (C * C).sum(1).to(torch.float32)
+    return torch.stack([cl.to(torch.float64).norm(dim=1).max(), C.norm(dim=1).max(), rc.norm(dim=1).max()]) * (1 + 1e-9)
+
+
+def screen_cert_split(ub, lb, ea, eb, en, cst, n: int, lst, count, u_out, l_out, stream=None) -> None:
+    """The split screen's certificate (kmeans_exact.hip screen_cert_split_kernel)."""
+    _native.check(_native.kernels().cml_kmeans_screen_cert_split(
+        ub.data_ptr(), lb.data_ptr(), ea.data_ptr(), eb.data_ptr(), en.data_ptr(), cst.data_ptr(), int(n),
+        lst.data_ptr(), count.data_ptr(), u_out.data_ptr(), l_out.data_ptr(), _native.stream_ptr(stream)),
+        "kmeans_screen_cert_split")
 
 
 def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = None, stream=None,

@@ -170,3 +170,37 @@ def test_screen_final_labels_pruned_equal_full_assign():
     assert torch.equal(eng.labels, lab_state)
     assert eng.cluster_sizes() == torch.bincount(full[:n].long(), minlength=k).tolist()
     eng.step()  # the state is untouched: the next step goes on from it
+
+
+def test_split_screen_layout_bounds_and_fewer_rechecks(monkeypatch):
+    """The split screen ([hi | lo | hi] rows against [c_hi | c_hi | c_lo] centres, d <= 170): exact labels,
+    bounds that hold for the real distances, and far fewer rows in the f64 re-check than the plain bf16
+    screen on data whose same-blob centres are near-equidistant."""
+    n, d, k = 150_000, 128, 64
+    x = _blobs(n, d, 16, seed=11, scale=4.0, dtype=torch.float32).cuda()  # 4 centres per blob below
+    xb, ea, eb, en, xn = K.to_bf16_split(x, d, 128, 512)
+    hi = x.to(torch.bfloat16)
+    lo = (x.double() - hi.double()).to(torch.bfloat16)
+    assert torch.equal(xb[:, :d], hi) and torch.equal(xb[:, 128:256], lo) and torch.equal(xb[:, 256:384], hi)
+    assert bool((xb[:, 384:] == 0).all())
+    assert bool((ea.double()[:n] >= lo.double().norm(dim=1)).all())
+    assert bool((eb.double()[:n] >= (x.double() - hi.double() - lo.double()).norm(dim=1)).all())
+    g = torch.Generator().manual_seed(1)
+    C = x[torch.randperm(n, generator=g)[:k].cuda()].double()
+    ref_lab, _ = K.exact_assign(x, C)
+    D = torch.cdist(x.double(), C)
+    own = D.gather(1, ref_lab[:n].long()[:, None])[:, 0]
+    other = D.scatter(1, ref_lab[:n].long()[:, None], float("inf")).min(1).values
+    counts = {}
+    for split in ("1", "0"):
+        monkeypatch.setenv("CML_KMEANS_SCREEN_SPLIT", split)
+        eng = LloydEngine(x, d, k, precision="screen")
+        eng.track_prune = True
+        lab = torch.zeros(n, dtype=torch.int32, device="cuda")
+        eng._screen_labels(C, lab)
+        assert eng._scr.split == (split == "1")
+        assert torch.equal(lab, ref_lab[:n])
+        st = eng._scr
+        assert bool((st.ub[:n].double() >= own * (1 - 1e-7)).all()) and bool((st.lb[:n].double() <= other * (1 + 1e-7)).all())
+        counts[split] = st.rechecked[-1]
+    assert counts["1"] * 5 < counts["0"], counts
