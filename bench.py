@@ -288,8 +288,10 @@ def main():
 
 
 def _step_rates(eng, comm) -> dict:
-    """Steady-state step time of a fitted engine (5 more pruned steps) and a forced full step (bounds
-    invalid: K9r over every row with top-2 bounds + the full counting-sort f64 accumulate)."""
+    """Steady-state step time of a fitted engine (5 more pruned steps), a forced full-assign step (bounds
+    invalid: K9r over every row with top-2 bounds; the sums move by the changed rows as in every step
+    whose labels barely move — what a fit on data the bounds cannot prune runs each iteration), and a
+    forced from-scratch step (also the full counting-sort f64 accumulate: a fit's first step)."""
     out = {}
     comm.barrier()
     torch.cuda.synchronize()
@@ -305,11 +307,20 @@ def _step_rates(eng, comm) -> dict:
         ts = time.perf_counter()
         for _ in range(3):
             eng._pst.force.fill_(1)
-            eng.delta.invalidate()
             eng.step()
         torch.cuda.synchronize()
         comm.barrier()
         out["full_step_ms"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
+        comm.barrier()
+        torch.cuda.synchronize()
+        ts = time.perf_counter()
+        for _ in range(3):
+            eng._pst.force.fill_(1)
+            eng.delta.invalidate()
+            eng.step()
+        torch.cuda.synchronize()
+        comm.barrier()
+        out["full_step_from_scratch_ms"] = 1000.0 * comm.max_scalar(time.perf_counter() - ts) / 3
     if eng.delta is not None and not eng.prune:
         out["last_step_changed_rows_rank0"] = eng.delta.changed_rows()
         comm.barrier()

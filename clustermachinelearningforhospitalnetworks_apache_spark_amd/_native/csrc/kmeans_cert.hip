@@ -132,6 +132,30 @@ __global__ __launch_bounds__(kT) void cert_bounds_kernel(const int* __restrict__
   list_flush<kT>(lb, lst, count, true);
 }
 
+// list_flush that also writes, beside each listed row, its K9r norm and current label (compacted inputs
+// of the K9r candidate pass over list B), when xn is given.
+__device__ __forceinline__ void list_flush_ext(ListBuf lb, int* lst, int* count, bool force, const float* xn,
+                                               float* bxn, const int* lab, int* blab) {
+  __syncthreads();
+  const int m = *lb.n;
+  if (m > 0 && (force || m > kBuf - kT)) {
+    if (threadIdx.x == 0) *lb.base = atomicAdd(count, m);
+    __syncthreads();
+    const int b = *lb.base;
+    for (int i = threadIdx.x; i < m; i += kT) {
+      const int r = lb.buf[i];
+      lst[b + i] = r;
+      if (xn != nullptr) {
+        bxn[b + i] = xn[r];
+        blab[b + i] = lab[r];
+      }
+    }
+    __syncthreads();
+    if (threadIdx.x == 0) *lb.n = 0;
+  }
+  __syncthreads();
+}
+
 // Listed rows (A): u <- the real distance to the label (16 lanes per row, any summation order: a bound
 // with the fold margin); rows still unproven go to list B.
 template <typename T>
@@ -140,7 +164,8 @@ __global__ __launch_bounds__(kT) void cert_tighten_kernel(const T* __restrict__ 
                                                           float* __restrict__ u, const float* __restrict__ l,
                                                           const float* __restrict__ s, const int* __restrict__ la,
                                                           const int* __restrict__ na, int* __restrict__ lbst,
-                                                          int* __restrict__ nbst) {
+                                                          int* __restrict__ nbst, const float* __restrict__ xn,
+                                                          float* __restrict__ bxn, int* __restrict__ blab) {
   __shared__ int buf[kBuf];
   __shared__ int nb, base;
   if (threadIdx.x == 0) nb = 0;
@@ -159,9 +184,19 @@ __global__ __launch_bounds__(kT) void cert_tighten_kernel(const T* __restrict__ 
       a = lab[r];
       const T* x = X + r * ldx;
       const double* c = C + (long long)a * d;
-      for (int t = q; t < d; t += 16) {
-        const double e = (double)x[t] - c[t];
-        acc = __fma_rn(e, e, acc);
+      for (int t0 = q; t0 < d; t0 += 16 * 8) {  // 8 loads in flight per lane before the fmas
+        double xv[8], cv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int t = t0 + 16 * u;
+          xv[u] = t < d ? (double)x[t] : 0.0;
+          cv[u] = t < d ? c[t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const double e = xv[u] - cv[u];
+          acc = __fma_rn(e, e, acc);
+        }
       }
     }
     acc += __shfl_xor(acc, 8, 16);
@@ -173,9 +208,112 @@ __global__ __launch_bounds__(kT) void cert_tighten_kernel(const T* __restrict__ 
       u[r] = uu;
       if (!(uu < fmaxf(l[r], s[a]))) buf[atomicAdd(&nb, 1)] = (int)r;
     }
-    list_flush<kT>(lbf, lbst, nbst, false);
+    list_flush_ext(lbf, lbst, nbst, false, xn, bxn, lab, blab);
   }
-  list_flush<kT>(lbf, lbst, nbst, true);
+  list_flush_ext(lbf, lbst, nbst, true, xn, bxn, lab, blab);
+}
+
+// One block: centres C (f64 [k, d]) -> the split screen's layout cb [kp, ldc] = [c_hi | c_hi | c_lo] in
+// ds-wide segments (bf16; padding rows zero), cn = ||c||² (f32; padding rows +inf: they never win) and
+// cst = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} (rounded up) — the certificate's constants.
+__global__ __launch_bounds__(1024) void split_centres_kernel(const double* __restrict__ C, int k, int kp, int d,
+                                                             int ds, u16* __restrict__ cb, long long ldc,
+                                                             float* __restrict__ cn, double* __restrict__ cst,
+                                                             float* __restrict__ mc) {
+  __shared__ double red[4][16];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  double m0 = 0.0, m1 = 0.0, m2 = 0.0, m3 = 0.0;
+  for (int j = w; j < kp; j += 16) {
+    double a2 = 0.0, c2 = 0.0, r2 = 0.0;
+    for (int t = lane; t < ldc; t += 64) {
+      u16 hb = 0, lb = 0;
+      if (j < k && t < d) {
+        const double v = C[(long long)j * d + t];
+        hb = f32_to_bf16((float)v);
+        const double r1 = v - (double)bf16_to_f32(hb);
+        lb = f32_to_bf16((float)r1);
+        const double lv = (double)bf16_to_f32(lb);
+        const double rc = r1 - lv;
+        a2 = __fma_rn(lv, lv, a2);
+        c2 = __fma_rn(v, v, c2);
+        r2 = __fma_rn(rc, rc, r2);
+      }
+      if (t < ds) {
+        cb[(long long)j * ldc + t] = hb;
+        cb[(long long)j * ldc + ds + t] = hb;
+        cb[(long long)j * ldc + 2 * ds + t] = lb;
+      } else if (t >= 3 * ds) {
+        cb[(long long)j * ldc + t] = 0;
+      }
+    }
+    a2 = wave_sum_f64(a2);
+    c2 = wave_sum_f64(c2);
+    r2 = wave_sum_f64(r2);
+    if (lane == 0) cn[j] = j < k ? (float)c2 : __builtin_huge_valf();
+    if (j < k) m3 = fmax(m3, (double)(float)c2);
+    m0 = fmax(m0, sqrt(a2));
+    m1 = fmax(m1, sqrt(c2));
+    m2 = fmax(m2, sqrt(r2));
+  }
+  if (lane == 0) {
+    red[0][w] = m0;
+    red[1][w] = m1;
+    red[2][w] = m2;
+    red[3][w] = m3;
+  }
+  __syncthreads();
+  if (threadIdx.x < 4) {
+    double m = 0.0;
+    for (int v = 0; v < 16; ++v) m = fmax(m, red[threadIdx.x][v]);
+    if (threadIdx.x < 3) cst[threadIdx.x] = m * (1.0 + 1e-9);
+    else if (mc != nullptr) mc[0] = (float)m;  // the largest centre norm (K9r's slack term)
+  }
+}
+
+// List B after the split-screen K9r candidate pass (labels / bf16-model bounds at the real rows): certified
+// rows keep the screened label with real-distance bounds (and append a move when it changed); the others
+// get their old label back and go to list C for the exact fold (exact_top2, which appends their moves).
+__global__ __launch_bounds__(kT) void cert_list_kernel(const int* __restrict__ lst, const int* __restrict__ cnt_dev,
+                                                       const int* __restrict__ blab, int* __restrict__ lab,
+                                                       float* __restrict__ u, float* __restrict__ l,
+                                                       const float* __restrict__ ea, const float* __restrict__ eb,
+                                                       const float* __restrict__ en, const double* __restrict__ cst,
+                                                       int* __restrict__ lc, int* __restrict__ nc,
+                                                       int* __restrict__ mv_row, int* __restrict__ mv_old,
+                                                       int* __restrict__ mv_new, int* __restrict__ mv_count) {
+  __shared__ int s_w[kT / 64 + 1];
+  const long long cnt = *cnt_dev;
+  const double c0 = cst[0], c1 = cst[1], c2 = cst[2];
+  for (long long i0 = (long long)blockIdx.x * kT; i0 < cnt; i0 += (long long)gridDim.x * kT) {
+    const long long i = i0 + threadIdx.x;
+    bool bad = false, moved = false;
+    int r = 0, old = 0, now = 0;
+    if (i < cnt) {
+      r = lst[i];
+      old = blab[i];
+      now = lab[r];
+      const double e = 2.0 * ((double)ea[r] * c0 + (double)eb[r] * c1 + 1.01 * (double)en[r] * c2) * (1.0 + 1e-6);
+      const double ub = (double)u[r], lbv = (double)l[r];
+      const float uu = f32_up(sqrt(ub * ub + e) * (1.0 + kFoldMargin));
+      const float ll = f32_dn(sqrt(fmax(lbv * lbv - e, 0.0)) * (1.0 - kFoldMargin));
+      bad = !(uu < ll);
+      if (bad) {
+        lab[r] = old;  // exact_top2 reads the old label to log the move
+      } else {
+        u[r] = uu;
+        l[r] = ll;
+        moved = now != old;
+      }
+    }
+    const int pc = block_append<kT>(bad, nc, s_w);
+    if (pc >= 0) lc[pc] = r;
+    const int pm = block_append<kT>(moved, mv_count, s_w);
+    if (pm >= 0) {
+      mv_row[pm] = r;
+      mv_old[pm] = old;
+      mv_new[pm] = now;
+    }
+  }
 }
 
 // Move histogram: bin j = rows moving into cluster j, bin k + j = rows leaving it.
@@ -257,9 +395,30 @@ __global__ __launch_bounds__(kT) void cert_delta_kernel(const T* __restrict__ X,
   for (int t0 = 0; t0 < d; t0 += 64) {
     const int t = t0 + col;
     double h = 0.0, lo = 0.0;
-    if (t < d) {
-      for (long long p = pa + lane; p < pb; p += 4) dd_add(h, lo, (double)X[(long long)perm[p] * ldx + t]);
-      for (long long p = qa + lane; p < qb; p += 4) dd_add(h, lo, -(double)X[(long long)perm[p] * ldx + t]);
+    if (t < d) {  // 8 rows' loads in flight per lane before their adds (the order of exact adds is free)
+      constexpr int B = 8;
+      for (long long p0 = pa + lane; p0 < pb; p0 += 4 * B) {
+        double v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const long long p = p0 + 4 * u;
+          v[u] = p < pb ? (double)X[(long long)perm[p] * ldx + t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          if (p0 + 4 * u < pb) dd_add(h, lo, v[u]);
+      }
+      for (long long p0 = qa + lane; p0 < qb; p0 += 4 * B) {
+        double v[B];
+#pragma unroll
+        for (int u = 0; u < B; ++u) {
+          const long long p = p0 + 4 * u;
+          v[u] = p < qb ? -(double)X[(long long)perm[p] * ldx + t] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < B; ++u)
+          if (p0 + 4 * u < qb) dd_add(h, lo, v[u]);
+      }
     }
     sh_h[threadIdx.x] = h;
     sh_l[threadIdx.x] = lo;
@@ -344,9 +503,12 @@ CML_API int cml_kmeans_cert_bounds(const int* lab, float* u, float* l, const flo
 }
 
 // la / na: list A and its device count; lbst / nbst: list B (capacity n) and its count.
+// xn / bxn / blab (all nullable together): the K9r row norms, and the compacted norm and current label of
+// every list-B row (beside lbst) for the split-screen candidate pass.
 CML_API int cml_kmeans_cert_tighten(const void* X, int xf64, long long n, long long ldx, int d, const double* C,
                                     const int* lab, float* u, const float* l, const float* s, const int* la,
-                                    const int* na, int* lbst, int* nbst, void* stream) {
+                                    const int* na, int* lbst, int* nbst, const float* xn, float* bxn, int* blab,
+                                    void* stream) {
   if (n <= 0) return 0;
   if (d <= 0) return (int)hipErrorInvalidValue;
   long long g = (n + 15) / 16;
@@ -354,15 +516,15 @@ CML_API int cml_kmeans_cert_tighten(const void* X, int xf64, long long n, long l
   hipStream_t st = (hipStream_t)stream;
   if (xf64)
     hipLaunchKernelGGL((cert_tighten_kernel<double>), dim3((unsigned)g), dim3(kT), 0, st, (const double*)X, ldx, d, C,
-                       lab, u, l, s, la, na, lbst, nbst);
+                       lab, u, l, s, la, na, lbst, nbst, xn, bxn, blab);
   else
     hipLaunchKernelGGL((cert_tighten_kernel<float>), dim3((unsigned)g), dim3(kT), 0, st, (const float*)X, ldx, d, C,
-                       lab, u, l, s, la, na, lbst, nbst);
+                       lab, u, l, s, la, na, lbst, nbst, xn, bxn, blab);
   return cml_status();
 }
 
 // Number of row slices of cert_delta (the partial buffers hold ns * k * d doubles each).
-CML_API int cml_kmeans_cert_slices(int k) { return k >= 256 ? 2 : (k >= 64 ? 4 : 8); }
+CML_API int cml_kmeans_cert_slices(int k) { return k >= 256 ? 4 : (k >= 64 ? 8 : 16); }
 
 // The moves (mv_row / mv_old / mv_new, m_dev entries; capacity n) applied to the double-double sums
 // S_hi / S_lo [k, d] and the int counts; hist int [2k] zeroed by cert_stats; seg int [2k + 1],
@@ -397,5 +559,27 @@ CML_API int cml_kmeans_cert_moves(const void* X, int xf64, long long n, long lon
   }
   hipLaunchKernelGGL(cert_apply_kernel, dim3(k), dim3(kT), 0, st, P_hi, P_lo, n > 0 ? ns : 0, k, d, seg, S_hi, S_lo,
                      cnt, C_cur, C_next, shift2);
+  return cml_status();
+}
+
+// cb bf16 [kp, ldc] (ldc >= 3·ds), cn f32 [kp], cst f64 [3].
+CML_API int cml_kmeans_split_centres(const double* C, int k, int kp, int d, int ds, void* cb, long long ldc,
+                                     float* cn, double* cst, float* mc, void* stream) {
+  if (k <= 0 || kp < k || d <= 0 || ds < d || ldc < 3LL * ds) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(split_centres_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, C, k, kp, d, ds, (u16*)cb, ldc,
+                     cn, cst, mc);
+  return cml_status();
+}
+
+// lst / cnt_dev: list B (after the split K9r candidate pass), blab its old labels; lc / nc: list C.
+CML_API int cml_kmeans_cert_list(const int* lst, const int* cnt_dev, long long cap, const int* blab, int* lab, float* u,
+                                 float* l, const float* ea, const float* eb, const float* en, const double* cst,
+                                 int* lc, int* nc, int* mv_row, int* mv_old, int* mv_new, int* mv_count,
+                                 void* stream) {
+  if (cap <= 0) return 0;
+  long long g = (cap + kT - 1) / kT;
+  g = g > 512 ? 512 : g;
+  hipLaunchKernelGGL(cert_list_kernel, dim3((unsigned)g), dim3(kT), 0, (hipStream_t)stream, lst, cnt_dev, blab, lab, u,
+                     l, ea, eb, en, cst, lc, nc, mv_row, mv_old, mv_new, mv_count);
   return cml_status();
 }

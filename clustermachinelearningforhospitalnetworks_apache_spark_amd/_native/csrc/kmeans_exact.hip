@@ -185,21 +185,73 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
 
 // best[r] = the f64 fold Σ_t (x_t - c_lab,t)² of exact_assign_kernel for row r against its label's
 // centre only (the same operations in the same order, so the same bits as the full assignment's
-// minimum when the label is the argmin): the distances of rows the bf16 screen certified.
+// minimum when the label is the argmin): the distances of rows the bf16 screen certified, the lazy cost.
+// One thread per row folds from LDS: the block's 256 rows are staged 16 dimensions at a time through a
+// transposed LDS tile with coalesced 64-B row segments (a thread-per-row walk of the rows straight from
+// HBM read 64 rows x 4 B per load: 0.7 TB/s), and so are the labels' centre columns when the centres fit.
+constexpr int kDistCh = 16;
 template <typename T>
 __global__ __launch_bounds__(kThreads) void exact_dist_kernel(const T* __restrict__ X, long long n, long long ldx,
-                                                              int d, const double* __restrict__ C,
+                                                              int d, const double* __restrict__ C, int kc,
                                                               const int* __restrict__ labels, long long lab_off,
-                                                              double* __restrict__ best) {
-  const long long r = (long long)blockIdx.x * kThreads + threadIdx.x;
-  if (r >= n) return;
-  const double* cj = C + (long long)(labels[r] - lab_off) * d;
+                                                              double* __restrict__ best, bool vec) {
+  __shared__ T xs[kDistCh * (kThreads + 1)];
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* cs = reinterpret_cast<double*>(smem);  // [kc][kDistCh] when kc > 0
+  const long long r0 = (long long)blockIdx.x * kThreads;
+  const long long r = r0 + threadIdx.x;
+  const bool live = r < n;
+  const long long j = live ? (long long)labels[r] - lab_off : 0;
+  const double* cj = C + j * d;
   double acc = 0.0;
-  for (int t = 0; t < d; ++t) {
-    const double e = (double)X[r * ldx + t] - cj[t];
-    acc = __fma_rn(e, e, acc);
+  for (int t0 = 0; t0 < d; t0 += kDistCh) {
+    const int dc = min(kDistCh, d - t0);
+    __syncthreads();
+    if (vec && dc == kDistCh) {  // 16-B loads: 4 (f32) / 2 (f64) dimensions of a row per load
+      constexpr int V = 16 / sizeof(T);
+      for (int e = threadIdx.x; e < kThreads * (kDistCh / V); e += kThreads) {
+        const int rr = e / (kDistCh / V), tv = (e - rr * (kDistCh / V)) * V;
+        const long long row = r0 + rr;
+        T v[V];
+        if (row < n) {
+          const uint4 q = *reinterpret_cast<const uint4*>(X + row * ldx + t0 + tv);
+          __builtin_memcpy(v, &q, 16);
+        } else {
+#pragma unroll
+          for (int u = 0; u < V; ++u) v[u] = (T)0;
+        }
+#pragma unroll
+        for (int u = 0; u < V; ++u) xs[(tv + u) * (kThreads + 1) + rr] = v[u];
+      }
+    } else {
+      for (int e = threadIdx.x; e < kThreads * kDistCh; e += kThreads) {
+        const int rr = e / kDistCh, tt = e - rr * kDistCh;
+        const long long row = r0 + rr;
+        xs[tt * (kThreads + 1) + rr] = (row < n && tt < dc) ? X[row * ldx + t0 + tt] : (T)0;
+      }
+    }
+    if (kc > 0)
+      for (int e = threadIdx.x; e < kc * kDistCh; e += kThreads) {
+        const int jj = e / kDistCh, tt = e - jj * kDistCh;
+        cs[e] = tt < dc ? C[(long long)jj * d + t0 + tt] : 0.0;
+      }
+    __syncthreads();
+    if (live) {
+      if (kc > 0) {
+        const double* cc = cs + j * kDistCh;
+        for (int tt = 0; tt < dc; ++tt) {
+          const double e = (double)xs[tt * (kThreads + 1) + threadIdx.x] - cc[tt];
+          acc = __fma_rn(e, e, acc);
+        }
+      } else {
+        for (int tt = 0; tt < dc; ++tt) {
+          const double e = (double)xs[tt * (kThreads + 1) + threadIdx.x] - cj[t0 + tt];
+          acc = __fma_rn(e, e, acc);
+        }
+      }
+    }
   }
-  best[r] = acc;
+  if (live) best[r] = acc;
 }
 
 // Source rows -> the bf16 copy the MFMA screen reads (RNE, zero-padded to ldo) and err[r] >= ||x_r -
@@ -239,30 +291,52 @@ __global__ __launch_bounds__(kThreads) void to_bf16_split_kernel(const T* __rest
                                                                  int d, int ds, u16* __restrict__ out, long long ldo,
                                                                  float* __restrict__ ea, float* __restrict__ eb,
                                                                  float* __restrict__ en, float* __restrict__ xn) {
-  const int lane = threadIdx.x & 63;
-  const long long w0 = ((long long)blockIdx.x * kThreads + threadIdx.x) >> 6;
-  const long long nw = ((long long)gridDim.x * kThreads) >> 6;
-  for (long long r = w0; r < n; r += nw) {
+  // 16 lanes per row (4 rows per wave); a lane owns 8-dimension groups: one 16-B store per segment
+  // (ds and ldo multiples of 8, checked at launch), the three norms reduced over the 16 lanes
+  const int lane = threadIdx.x & 63, q = lane & 15;
+  const long long g0 = ((long long)blockIdx.x * kThreads + threadIdx.x) >> 4;
+  const long long ng = ((long long)gridDim.x * kThreads) >> 4;
+  const long long rounds = (n + ng - 1) / ng;  // every lane runs the same number of rounds (shuffles)
+  for (long long it = 0; it < rounds; ++it) {
+    const long long r = g0 + it * ng;
+    const bool live = r < n;
     double a2 = 0.0, b2 = 0.0, n2 = 0.0;
-    for (int t = lane; t < ldo; t += 64) out[r * ldo + t] = 0;
-    for (int t = lane; t < d; t += 64) {
-      const double v = (double)X[r * ldx + t];
-      const u16 h = f32_to_bf16((float)v);
-      const double r1 = v - (double)bf16_to_f32(h);
-      const u16 l = f32_to_bf16((float)r1);
-      const double rx = r1 - (double)bf16_to_f32(l);
-      const double lv = (double)bf16_to_f32(l);
-      a2 = __fma_rn(lv, lv, a2);
-      b2 = __fma_rn(rx, rx, b2);
-      n2 = __fma_rn(v, v, n2);
-      out[r * ldo + t] = h;
-      out[r * ldo + ds + t] = l;
-      out[r * ldo + 2 * ds + t] = h;
+    if (live) {
+      uint4* o = reinterpret_cast<uint4*>(out + r * ldo);
+      for (int t0 = 8 * q; t0 < ds; t0 += 128) {
+        unsigned wh[4] = {0u, 0u, 0u, 0u}, wl[4] = {0u, 0u, 0u, 0u};
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+          const int t = t0 + u;
+          if (t < d) {
+            const double v = (double)X[r * ldx + t];
+            const u16 hb = f32_to_bf16((float)v);
+            const double r1 = v - (double)bf16_to_f32(hb);
+            const u16 lb = f32_to_bf16((float)r1);
+            const double lv = (double)bf16_to_f32(lb);
+            const double rx = r1 - lv;
+            a2 = __fma_rn(lv, lv, a2);
+            b2 = __fma_rn(rx, rx, b2);
+            n2 = __fma_rn(v, v, n2);
+            wh[u >> 1] |= (unsigned)hb << (16 * (u & 1));
+            wl[u >> 1] |= (unsigned)lb << (16 * (u & 1));
+          }
+        }
+        const uint4 h4 = {wh[0], wh[1], wh[2], wh[3]}, l4 = {wl[0], wl[1], wl[2], wl[3]};
+        o[t0 / 8] = h4;
+        o[(ds + t0) / 8] = l4;
+        o[(2 * ds + t0) / 8] = h4;
+      }
+      const uint4 z = {0u, 0u, 0u, 0u};
+      for (long long t0 = 3LL * ds + 8 * q; t0 < ldo; t0 += 128) o[t0 / 8] = z;
     }
-    a2 = wave_sum_f64(a2);
-    b2 = wave_sum_f64(b2);
-    n2 = wave_sum_f64(n2);
-    if (lane == 0) {
+#pragma unroll
+    for (int m = 8; m > 0; m >>= 1) {
+      a2 += __shfl_xor(a2, m, 16);
+      b2 += __shfl_xor(b2, m, 16);
+      n2 += __shfl_xor(n2, m, 16);
+    }
+    if (live && q == 0) {
       ea[r] = f32_up(sqrt(a2) * (1.0 + 1e-6));
       eb[r] = f32_up(sqrt(b2) * (1.0 + 1e-6) + 1e-300);
       en[r] = f32_up(sqrt(n2) * (1.0 + 1e-6));
@@ -555,19 +629,23 @@ CML_API int cml_kmeans_exact_top2(const void* X, int xf64, long long n, long lon
   return cml_status();
 }
 
-// labels[r] - lab_off indexes C (f64 [*, d]).
-CML_API int cml_kmeans_exact_dist(const void* X, int xf64, long long n, long long ldx, int d, const double* C,
+// labels[r] - lab_off indexes C (f64 [kc, d]; kc = 0: unknown, the centres are read from global memory).
+CML_API int cml_kmeans_exact_dist(const void* X, int xf64, long long n, long long ldx, int d, const double* C, int kc,
                                   const int* labels, long long lab_off, double* best, void* stream) {
   if (n <= 0) return 0;
   if (d <= 0) return (int)hipErrorInvalidValue;
   const dim3 g((unsigned)((n + kThreads - 1) / kThreads));
   hipStream_t st = (hipStream_t)stream;
+  if ((size_t)kc * kDistCh * sizeof(double) > 32768) kc = 0;
+  const size_t lds = (size_t)kc * kDistCh * sizeof(double);
+  const size_t esz = xf64 ? 8 : 4;
+  const bool vec = ((uintptr_t)X % 16 == 0) && ((ldx * esz) % 16 == 0);
   if (xf64)
-    hipLaunchKernelGGL((exact_dist_kernel<double>), g, dim3(kThreads), 0, st, (const double*)X, n, ldx, d, C, labels,
-                       lab_off, best);
+    hipLaunchKernelGGL((exact_dist_kernel<double>), g, dim3(kThreads), lds, st, (const double*)X, n, ldx, d, C, kc,
+                       labels, lab_off, best, vec);
   else
-    hipLaunchKernelGGL((exact_dist_kernel<float>), g, dim3(kThreads), 0, st, (const float*)X, n, ldx, d, C, labels,
-                       lab_off, best);
+    hipLaunchKernelGGL((exact_dist_kernel<float>), g, dim3(kThreads), lds, st, (const float*)X, n, ldx, d, C, kc,
+                       labels, lab_off, best, vec);
   return cml_status();
 }
 
@@ -629,8 +707,8 @@ CML_API int cml_kmeans_exact_segsum(const void* X, int xf64, long long ldx, int 
 CML_API int cml_kmeans_to_bf16_split(const void* X, int xf64, long long n, long long ldx, int d, int ds, void* out,
                                      long long ldo, float* ea, float* eb, float* en, float* xn, void* stream) {
   if (n <= 0) return 0;
-  if (d <= 0 || ds < d || ldo < 3LL * ds) return (int)hipErrorInvalidValue;
-  long long g = (n + 3) / 4;
+  if (d <= 0 || ds < d || ldo < 3LL * ds || (ds % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
+  long long g = (n + 15) / 16;
   g = g > 8192 ? 8192 : g;
   hipStream_t st = (hipStream_t)stream;
   if (xf64)

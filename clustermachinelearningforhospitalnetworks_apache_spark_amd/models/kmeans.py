@@ -461,6 +461,7 @@ class LloydEngine:
             K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
         if getattr(self, "_scr", None) is not None and getattr(self._scr, "cert", None) is not None:
             self._scr.cert.valid = False  # the certified step restarts from a screened full assignment
+        self._shift_pair = None
         seed, self._seed = getattr(self, "_seed", None), None
         if self._pdev:  # bounds and incremental sums were relative to the old centres: a full step next
             st = self._pst
@@ -676,9 +677,10 @@ class LloydEngine:
                 pass
         if split:
             xb, ea, eb, en, xn = parts
-            # the augmented products sum to at most |x|² + |c|² (twice the plain row's): twice the slack
+            # the K9r slack of 3·ds non-zero products (the zero tail adds no rounding); the lo·hi products
+            # are 2^-8 of the hi·hi ones, so their magnitudes sum to at most 1.02x the plain row's
             st = types.SimpleNamespace(xb=xb, ea=ea, eb=eb, en=en, ex=None, dp=dp, ds=ds, split=True,
-                                       tau=2.0 * self.prune_tau(dp))
+                                       tau=1.02 * self.prune_tau(3 * ds))
             st.xn = xn
         else:
             xb, ex = parts
@@ -720,7 +722,7 @@ class LloydEngine:
         st.cb[:kp].zero_()
         st.cn[:kp].zero_()
         if st.split:
-            cst = K.split_centres(C, st.ds, st.cb, st.cn)
+            cst = K.split_centres(C, st.ds, st.cb[:kp], st.cn[:kp])
         else:
             K.update_centers(None, kc, d, C.clone(), st.cb[:kp], st.dp, kp, st.cn[:kp], None)
             ecmax = ((C - st.cb[:kc, :d].to(torch.float64)) ** 2).sum(1).max().sqrt().reshape(1) * (1.0 + 1e-9)
@@ -792,6 +794,20 @@ class LloydEngine:
         c.P_hi = torch.empty(ns * k * d, dtype=torch.float64, device=dev)
         c.P_lo = torch.empty(ns * k * d, dtype=torch.float64, device=dev)
         c.S_hi = c.S_lo = c.cnt = c.C_cur = None
+        if st.split and n:
+            # list B goes through the split-screen K9r candidate pass first: whole K9r tiles of valid rows
+            c.plan = K.plan_assign(n, st.dp, k)
+            pad = n + c.plan.round_rows
+            c.lbl = torch.zeros(pad, **i32)
+            c.bxn = torch.zeros(pad, dtype=torch.float32, device=dev)
+            c.blab = torch.zeros(pad, **i32)
+            c.lc = torch.empty(m, **i32)
+            c.cst = torch.zeros(3, dtype=torch.float64, device=dev)
+            c.mc = torch.zeros(1, dtype=torch.float32, device=dev)
+            c.kp = round_up(k, 32)
+        # one-rank centre updates land in two alternating buffers (the update kernel writes the next
+        # centres beside the current ones; no per-step host work)
+        c.cbuf = [torch.empty((k, d), dtype=torch.float64, device=dev) for _ in range(2)]
         st.cert = c
         return c
 
@@ -834,28 +850,56 @@ class LloydEngine:
         elif n:
             K.cert_stats(self.centers, c.C_cur, c.s, c.drift, c.dtop, zero=c.ctr)
             K.cert_bounds(c.lab, st.ub, st.lb, c.drift, c.dtop, c.s, n, c.la, c.ctr[0:1])
-            K.cert_tighten(self.x, self.centers, c.lab, st.ub, st.lb, c.s, c.la, c.ctr[0:1], c.lbl, c.ctr[1:2])
-            K.exact_top2(self.x, self.centers, c.lab, st.ub, st.lb, idx=c.lbl, n_dev=c.ctr[1:2],
-                         moves=(c.mvr, c.mvo, c.mvn, c.ctr[2:3]))
+            moves = (c.mvr, c.mvo, c.mvn, c.ctr[2:3])
+            if st.split:
+                # list B: the split-screen K9r candidate pass, its certificate, the exact fold for the rest
+                K.cert_tighten(self.x, self.centers, c.lab, st.ub, st.lb, c.s, c.la, c.ctr[0:1], c.lbl, c.ctr[1:2],
+                               xn=st.xn, bxn=c.bxn, blab=c.blab)
+                K.split_centres_dev(self.centers, st.ds, st.cb[:c.kp], st.cn[:c.kp], c.cst, mc=c.mc)
+                K.assign_rr_ext(2, st.xb, n, st.dp, st.cb[:c.kp], st.cn[:c.kp], c.plan, c.bxn, c.lab, None, st.ub,
+                                st.lb, c.mc, st.tau, idx=c.lbl, n_dev=c.ctr[1:2], lab_in=c.blab)
+                K.cert_list(c.lbl, c.ctr[1:2], n, c.blab, c.lab, st.ub, st.lb, st.ea, st.eb, st.en, c.cst, c.lc,
+                            c.ctr[3:4], moves)
+                K.exact_top2(self.x, self.centers, c.lab, st.ub, st.lb, idx=c.lc, n_dev=c.ctr[3:4], moves=moves)
+            else:
+                K.cert_tighten(self.x, self.centers, c.lab, st.ub, st.lb, c.s, c.la, c.ctr[0:1], c.lbl, c.ctr[1:2])
+                K.exact_top2(self.x, self.centers, c.lab, st.ub, st.lb, idx=c.lbl, n_dev=c.ctr[1:2], moves=moves)
+            fast = not self.comm.is_distributed  # one rank: the update kernel writes the next centres
+            nxt = None
+            if fast:
+                nxt = c.cbuf[1] if self.centers.data_ptr() == c.cbuf[0].data_ptr() else c.cbuf[0]
             K.cert_moves(self.x, k, c.mvr, c.mvo, c.mvn, c.ctr[2:3], c.ctr[4:], c.seg, c.cursor, c.perm, c.P_hi,
-                         c.P_lo, c.S_hi, c.S_lo, c.cnt)
-            if self.track_prune:
-                c.history.append(tuple(int(v) for v in c.ctr[:3].tolist()))
+                         c.P_lo, c.S_hi, c.S_lo, c.cnt, C_cur=self.centers if fast else None, C_next=nxt)
+            if self.track_prune:  # (list A, list B, moves, list C: exact re-assignments after the screen)
+                c.history.append(tuple(int(v) for v in c.ctr[:4].tolist()))
+            if fast:
+                # the exact path's update bits (S / count in IEEE f64, empty clusters keep their centre);
+                # the shift and the cost are evaluated on demand against these two buffers, which the
+                # next step's update (the other buffer) leaves intact
+                c.C_cur, c_used, lab_used = self.centers, self.centers, c.lab[:n]
+                self._shift2, self._shift_pair = None, (nxt, self.centers)
+                self.centers = nxt
+                self.labels = c.lab[:n]
+                self._cost_fn = lambda: self._screen_cost(c_used, lab_used)
+                return
         c.C_cur = self.centers.clone()  # the centres of this assignment (set_centers writes in place)
         S, counts, _ = self._exact_global(c.S_hi, c.S_lo, c.cnt.to(torch.float64), torch.zeros(1, **f64))
         msg = torch.cat([S.reshape(-1), counts, torch.zeros(1, **f64)])
         c_used, lab_used = c.C_cur, c.lab[:n].clone()
+        self._shift_pair = None
         self._update_cpu(msg)
         self.labels = c.lab[:n]
+        self._cost_fn = lambda: self._screen_cost(c_used, lab_used)
 
-        def cost():
-            b = torch.empty(max(n, 1), **f64)
-            if n:
-                K.exact_dist(self.x, c_used, lab_used, b)
-            tot = b[:n].sum().reshape(1) if n else torch.zeros(1, **f64)
-            self.comm.allreduce_(tot)
-            return tot[0]
-        self._cost_fn = cost
+    def _screen_cost(self, C: torch.Tensor, lab: torch.Tensor) -> torch.Tensor:
+        """Cost of an exact assignment: Σ of every row's f64 fold against its label's centre, over ranks."""
+        n = self.n
+        b = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
+        if n:
+            K.exact_dist(self.x, C, lab, b)
+        tot = b[:n].sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=self.device)
+        self.comm.allreduce_(tot)
+        return tot[0]
 
     def _step_cpu(self):
         if self._screen:
@@ -1366,6 +1410,9 @@ class LloydEngine:
 
     def converged(self, tol: float) -> bool:
         """Spark's rule: converged iff every centre moved at most tol (euclidean)."""
+        if self._shift2 is None and getattr(self, "_shift_pair", None) is not None:
+            new, old = self._shift_pair  # the screen's one-rank update: the exact path's expression, on demand
+            self._shift2 = ((new - old) ** 2).sum(1)
         if self._shift2 is None:
             return False
         lim = 2.0 * tol if self.spherical else tol * tol  # cosine: 1 - cos = ||a - b||² / 2 on unit vectors

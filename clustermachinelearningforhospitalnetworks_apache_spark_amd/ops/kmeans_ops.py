@@ -98,7 +98,7 @@ _native.register_kernel_sigs({
 _native.register_kernel_sigs({
     "cml_kmeans_exact_assign": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_vp,
                                         c_vp]),
-    "cml_kmeans_exact_dist": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_ll, c_vp, c_vp]),
+    "cml_kmeans_exact_dist": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_int, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_to_bf16_err": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_ll, c_vp, c_vp]),
     "cml_kmeans_screen_cert": (c_int, [c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_exact_chunks": (c_ll, [c_ll]),
@@ -112,7 +112,10 @@ _native.register_kernel_sigs({
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
-                                        c_vp, c_vp, c_vp]),
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_split_centres": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_cert_list": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
+                                     c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_slices": (c_int, [c_int]),
     "cml_kmeans_cert_moves": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -835,8 +838,8 @@ def exact_dist(x: torch.Tensor, centers: torch.Tensor, labels: torch.Tensor, bes
     if labels.dtype != torch.int32 or best.dtype != torch.float64:
         raise ValueError("exact_dist: int32 labels, f64 best")
     _native.check(_native.kernels().cml_kmeans_exact_dist(
-        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), labels.data_ptr(),
-        int(lab_off), best.data_ptr(), _native.stream_ptr(stream)), "kmeans_exact_dist")
+        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, c.data_ptr(), int(c.shape[0]),
+        labels.data_ptr(), int(lab_off), best.data_ptr(), _native.stream_ptr(stream)), "kmeans_exact_dist")
 
 
 def to_bf16_err(x: torch.Tensor, d: int, ldo: int, stream=None):
@@ -878,16 +881,17 @@ def to_bf16_split(x: torch.Tensor, d: int, ds: int, ldo: int, stream=None):
 
 def split_centres(C: torch.Tensor, ds: int, cb: torch.Tensor, cn: torch.Tensor) -> torch.Tensor:
     """Centres (f64 [k, d]) in the split screen's layout: cb[:k] = [c_hi | c_hi | c_lo] (bf16), cn[:k] =
-    ||c||² (f32); returns f64 [3] = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} (device)."""
+    ||c||² (f32), the padding rows zero with an infinite norm; returns f64 [3] = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} (device)."""
     k, d = int(C.shape[0]), int(C.shape[1])
     ch = C.to(torch.bfloat16)
     r = C - ch.to(torch.float64)
     cl = r.to(torch.bfloat16)
     rc = r - cl.to(torch.float64)
-    cb[:k].zero_()
+    cb.zero_()
     cb[:k, :d] = ch
     cb[:k, ds:ds + d] = ch
     cb[:k, 2 * ds:2 * ds + d] = cl
+    cn.fill_(float("inf"))  # padding centres never win (K11's convention)
     cn[:k] = (C * C).sum(1).to(torch.float32)
     return torch.stack([cl.to(torch.float64).norm(dim=1).max(), C.norm(dim=1).max(), rc.norm(dim=1).max()]) * (1 + 1e-9)
 
@@ -971,12 +975,36 @@ def cert_bounds(lab, u, l, drift, dtop, s, n: int, lst, count, stream=None) -> N
         lst.data_ptr(), count.data_ptr(), _native.stream_ptr(stream)), "kmeans_cert_bounds")
 
 
-def cert_tighten(x: torch.Tensor, C: torch.Tensor, lab, u, l, s, la, na, lbst, nbst, stream=None) -> None:
+def cert_tighten(x: torch.Tensor, C: torch.Tensor, lab, u, l, s, la, na, lbst, nbst, stream=None,
+                 xn: torch.Tensor | None = None, bxn: torch.Tensor | None = None,
+                 blab: torch.Tensor | None = None) -> None:
+    """List A -> tightened upper bounds; still unproven rows to list B (with ``xn``: their K9r norms and
+    current labels compacted into ``bxn`` / ``blab`` beside it)."""
     n = int(x.shape[0])
     _native.check(_native.kernels().cml_kmeans_cert_tighten(
         x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(C.shape[1]), C.data_ptr(), lab.data_ptr(),
         u.data_ptr(), l.data_ptr(), s.data_ptr(), la.data_ptr(), na.data_ptr(), lbst.data_ptr(), nbst.data_ptr(),
-        _native.stream_ptr(stream)), "kmeans_cert_tighten")
+        _ptr(xn), _ptr(bxn), _ptr(blab), _native.stream_ptr(stream)), "kmeans_cert_tighten")
+
+
+def split_centres_dev(C: torch.Tensor, ds: int, cb: torch.Tensor, cn: torch.Tensor, cst: torch.Tensor,
+                      mc: torch.Tensor | None = None, stream=None) -> None:
+    """split_centres in one kernel launch (cb [kp, ldc] bf16, cn [kp] f32, cst f64 [3]; mc f32 [1] = the
+    largest centre norm)."""
+    k, d = int(C.shape[0]), int(C.shape[1])
+    _native.check(_native.kernels().cml_kmeans_split_centres(
+        C.data_ptr(), k, int(cb.shape[0]), d, int(ds), cb.data_ptr(), cb.stride(0), cn.data_ptr(), cst.data_ptr(),
+        _ptr(mc), _native.stream_ptr(stream)), "kmeans_split_centres")
+
+
+def cert_list(lst, cnt, cap: int, blab, lab, u, l, ea, eb, en, cst, lc, nc, moves, stream=None) -> None:
+    """List B after the split K9r candidate pass: certified rows keep their screened labels (moves logged),
+    the rest go to list C with their old labels restored."""
+    mr, mo, mn, mc = moves
+    _native.check(_native.kernels().cml_kmeans_cert_list(
+        lst.data_ptr(), cnt.data_ptr(), int(cap), blab.data_ptr(), lab.data_ptr(), u.data_ptr(), l.data_ptr(),
+        ea.data_ptr(), eb.data_ptr(), en.data_ptr(), cst.data_ptr(), lc.data_ptr(), nc.data_ptr(), mr.data_ptr(),
+        mo.data_ptr(), mn.data_ptr(), mc.data_ptr(), _native.stream_ptr(stream)), "kmeans_cert_list")
 
 
 def cert_slices(k: int) -> int:
@@ -984,14 +1012,16 @@ def cert_slices(k: int) -> int:
 
 
 def cert_moves(x: torch.Tensor, k: int, mv_row, mv_old, mv_new, m_dev, hist, seg, cursor, perm, P_hi, P_lo,
-               S_hi, S_lo, cnt, stream=None) -> None:
-    """Apply the label moves to the double-double cluster sums S_hi / S_lo and the int32 counts."""
+               S_hi, S_lo, cnt, stream=None, C_cur: torch.Tensor | None = None,
+               C_next: torch.Tensor | None = None) -> None:
+    """Apply the label moves to the double-double cluster sums S_hi / S_lo and the int32 counts; with
+    ``C_next`` (one rank) also the centre update C_next = S_hi / count (an empty cluster keeps C_cur)."""
     n, d = int(x.shape[0]), int(S_hi.shape[1])
     _native.check(_native.kernels().cml_kmeans_cert_moves(
         x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), d, int(k), mv_row.data_ptr(), mv_old.data_ptr(),
         mv_new.data_ptr(), m_dev.data_ptr(), hist.data_ptr(), seg.data_ptr(), cursor.data_ptr(), perm.data_ptr(),
-        P_hi.data_ptr(), P_lo.data_ptr(), S_hi.data_ptr(), S_lo.data_ptr(), cnt.data_ptr(), 0, 0, 0,
-        _native.stream_ptr(stream)), "kmeans_cert_moves")
+        P_hi.data_ptr(), P_lo.data_ptr(), S_hi.data_ptr(), S_lo.data_ptr(), cnt.data_ptr(), _ptr(C_cur),
+        _ptr(C_next), 0, _native.stream_ptr(stream)), "kmeans_cert_moves")
 
 
 def dd_fold(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
