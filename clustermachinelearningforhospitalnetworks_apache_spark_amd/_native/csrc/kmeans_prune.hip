@@ -187,13 +187,16 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
 // 0 rows, so no label changes, the sums and therefore the centres stay bit for bit — which lets the host
 // enqueue steps ahead and read the convergence flag lagged (no per-step host sync). One thread.
 __global__ void kmeans_prune_gate_kernel(int* __restrict__ count, long long cap, const int* __restrict__ flags,
-                                         int* __restrict__ mode) {
+                                         int* __restrict__ mode, int* __restrict__ backoff, int nback) {
   if (flags[1] != 0) {
     mode[0] = 0;
     mode[1] = 0;
     *count = 0;
     return;
   }
+  // bounds that stopped pruning (more than cap candidates) stay off for the next nback steps: those go
+  // straight to the full pass, which skips the bounds pass and its compaction (kmeans_centre_stats2)
+  if (backoff != nullptr && flags[0] == 0 && (long long)*count > cap) *backoff = nback;
   const int full = (flags[0] != 0 || (long long)*count > cap) ? 1 : 0;
   mode[0] = full;
   mode[1] = full ? 0 : *count;  // re-assigned rows of a candidate pass (stats; count is reset later)
@@ -296,7 +299,8 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
                                                                    int have_drift, float* __restrict__ thr,
                                                                    float* __restrict__ dmax, float* __restrict__ mc,
                                                                    float* __restrict__ c2, int* __restrict__ count,
-                                                                   int* __restrict__ force, float* __restrict__ cum) {
+                                                                   int* __restrict__ force, float* __restrict__ cum,
+                                                                   int* __restrict__ backoff) {
   __shared__ double smax[256];
   __shared__ float sdm[3];
   __shared__ float d1[256], d2[256];
@@ -341,7 +345,10 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
     sdm[1] = tb < 0.f ? 0.f : tb;
     sdm[2] = (float)ti;
     *count = 0;
-    *force = 0;
+    // a backed-off pruned step forces the next one full (its bounds pass is skipped)
+    const int bo = backoff != nullptr ? *backoff : 0;
+    *force = bo > 0 ? 1 : 0;
+    if (bo > 0) *backoff = bo - 1;
   }
   __syncthreads();
   const double sl = (double)tau * ((double)*mx + smax[0]);
@@ -467,8 +474,11 @@ CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const 
 }
 
 // flags: int[2] {force, done} (see kmeans_prune_gate_kernel).
-CML_API int cml_kmeans_prune_gate(int* count, long long cap, const int* flags, int* mode, void* stream) {
-  hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, cap, flags, mode);
+// backoff (nullable, int [1]): see kmeans_prune_gate_kernel.
+CML_API int cml_kmeans_prune_gate(int* count, long long cap, const int* flags, int* mode, int* backoff, int nback,
+                                  void* stream) {
+  hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, cap, flags, mode,
+                     backoff, nback);
   return cml_status();
 }
 
@@ -497,13 +507,14 @@ CML_API int cml_kmeans_cond_copy(void* dst, const void* src, long long n_bytes, 
 // (f32 [k]), dmax (f32 [3]), mc / c2 (f32 scalars); count and force are reset to 0.
 CML_API int cml_kmeans_centre_stats(const void* cb, const void* cb_old, long long ldc, int k, int d, const float* mx,
                                     float tau, double* cn, double* half, float* drift, float* thr, float* dmax,
-                                    float* mc, float* c2, int* count, int* force, float* cum, void* stream) {
+                                    float* mc, float* c2, int* count, int* force, float* cum, int* backoff,
+                                    void* stream) {
   if (k <= 0 || d <= 0 || d > 8192) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   hipLaunchKernelGGL(kmeans_centre_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(double), st,
                      (const u16*)cb, (const u16*)cb_old, ldc, k, d, cn, drift, half);
   hipLaunchKernelGGL(kmeans_centre_stats2_kernel, dim3(1), dim3(256), 0, st, cn, half, drift, k, mx, tau,
-                     cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force, cum);
+                     cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force, cum, backoff);
   return cml_status();
 }
 

@@ -467,6 +467,7 @@ class LloydEngine:
             st = self._pst
             K.centre_stats(self.cb, None, self.k, self.d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax,
                            st.mc, st.c2, st.count, st.force)
+            st.backoff.zero_()
             self.delta.invalidate()
             # centres straight from this engine's k-means|| init: the first step starts from bounds the
             # init already implies (no full assign pass); anything else takes a full step
@@ -956,6 +957,10 @@ class LloydEngine:
         # fits, _fit_lagged): every later step is a frozen no-op until the host reads the flag
         st.flags = torch.tensor([1, 0], dtype=torch.int32, device=dev)
         st.force, st.done = st.flags[0:1], st.flags[1:2]
+        # steps left that skip the bounds after one went over the cap (data the bounds do not prune);
+        # CML_KMEANS_PRUNE_BACKOFF=0 retries the bounds every step
+        st.backoff = torch.zeros(1, dtype=torch.int32, device=dev)
+        st.nback = int(os.environ.get("CML_KMEANS_PRUNE_BACKOFF", "2"))
         st.ub = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         st.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         st.drift = torch.zeros(k, dtype=torch.float32, device=dev)
@@ -1000,7 +1005,8 @@ class LloydEngine:
         K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                        xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
                        cum=st.cum) if n else None
-        K.prune_gate(st.count, st.cap_m, st.flags, st.pmode)
+        K.prune_gate(st.count, st.cap_m, st.flags, st.pmode, backoff=st.backoff if st.nback > 0 else None,
+                     nback=st.nback)
         K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
                         st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
@@ -1019,7 +1025,7 @@ class LloydEngine:
         K.cond_copy(st.cb_cost, self.cb, st.flags, dst_always=st.cb_old)
         self._update_gpu(self.msgs)
         K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
-                       st.c2, st.count, st.force, cum=st.cum)
+                       st.c2, st.count, st.force, cum=st.cum, backoff=st.backoff if st.nback > 0 else None)
         if self._conv_lim is not None:
             K.converge_latch(self.shift2, k, self._conv_lim, st.flags)
         self._cost_fn = self._device_cost
@@ -1838,7 +1844,13 @@ class LloydEngine:
         near-ties. No host read: the list sizes stay on the device (the launches are sized by capacity).
         Returns False (nothing changed) when the pruned pass does not apply (host rows, pruning off)."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
-        if not self._pdev or os.environ.get("CML_KMEANS_INIT_PRUNE", "1") == "0" or not self._rr_max_chunk():
+        # default on up to Dp = 256; at Dp = 512 the per-row path reads 1 KiB of candidate per listed
+        # candidate and the gathered K9r pass loses to the streaming one: the config-5 pipeline's init
+        # (125M x 512 fp8, k = 128) ran 120 ms pruned vs 97.5 ms full (profiles/r4/pipeline_init_ab.log)
+        mode = os.environ.get("CML_KMEANS_INIT_PRUNE", "auto")
+        if mode == "0" or (mode == "auto" and dp > 256):
+            return False
+        if not self._pdev or not self._rr_max_chunk():
             return False
         if n == 0:
             return True

@@ -57,14 +57,14 @@ _native.register_kernel_sigs({
     "cml_kmeans_prune_lower": (c_int, [c_vp, c_int, c_vp, c_vp, ctypes.c_float, ctypes.c_float, c_ll, c_vp, c_vp]),
     "cml_kmeans_prune_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp,
                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp]),
-    "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_prune_gate": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_converge_latch": (c_int, [c_vp, c_int, ctypes.c_double, c_vp, c_vp]),
     "cml_kmeans_cond_copy": (c_int, [c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_seed_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_ll,
                                        c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_label_hist": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_centre_stats": (c_int, [c_vp, c_vp, c_ll, c_int, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
-                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+                                        c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
@@ -661,15 +661,17 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
                   "kmeans_label_hist")
 
 
-def prune_gate(count: torch.Tensor, cap: int, flags: torch.Tensor, mode: torch.Tensor, stream=None) -> None:
+def prune_gate(count: torch.Tensor, cap: int, flags: torch.Tensor, mode: torch.Tensor, stream=None,
+               backoff: torch.Tensor | None = None, nback: int = 2) -> None:
     """mode[0] = 1 (full pass) when flags[0] (force) or count[0] > cap, else 0 (candidate pass); with
     flags[1] (done: the fit converged) a frozen step — candidate pass over 0 rows (count zeroed).
-    ``flags``: int32 [2] device tensor. Device only."""
+    ``backoff`` (int32 [1]): a step over the cap sets it to ``nback`` and centre_stats then forces that
+    many steps full (no bounds pass). ``flags``: int32 [2] device tensor. Device only."""
     if flags.dtype != torch.int32 or flags.numel() < 2:
         raise ValueError("prune_gate: flags must be int32 [force, done]")
     _native.check(_native.kernels().cml_kmeans_prune_gate(count.data_ptr(), int(cap), flags.data_ptr(),
-                                                          mode.data_ptr(), _native.stream_ptr(stream)),
-                  "kmeans_prune_gate")
+                                                          mode.data_ptr(), _ptr(backoff), int(nback),
+                                                          _native.stream_ptr(stream)), "kmeans_prune_gate")
 
 
 def converge_latch(shift2: torch.Tensor, k: int, lim: float, flags: torch.Tensor, stream=None) -> None:
@@ -697,14 +699,15 @@ def cond_copy(dst: torch.Tensor, src: torch.Tensor, flags: torch.Tensor, stream=
 def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, mx: torch.Tensor, tau: float,
                  cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor, thr: torch.Tensor, dmax: torch.Tensor,
                  mc: torch.Tensor, c2: torch.Tensor, count: torch.Tensor, force: torch.Tensor, stream=None,
-                 cum: torch.Tensor | None = None) -> None:
+                 cum: torch.Tensor | None = None, backoff: torch.Tensor | None = None) -> None:
     """Centre statistics of the device pruned step (``kmeans_prune.hip``) over the bf16 centres: norms,
     drifts against ``cb_old`` (None: no drift), half nearest-centre distances -> thr, dmax, mc, c2;
     resets ``count`` and ``force``. No host synchronisation."""
     _native.check(_native.kernels().cml_kmeans_centre_stats(
         cb.data_ptr(), _ptr(cb_old), cb.stride(0), int(k), int(d), mx.data_ptr(), float(tau), cn.data_ptr(),
         half.data_ptr(), drift.data_ptr(), thr.data_ptr(), dmax.data_ptr(), mc.data_ptr(), c2.data_ptr(),
-        count.data_ptr(), force.data_ptr(), _ptr(cum), _native.stream_ptr(stream)), "kmeans_centre_stats")
+        count.data_ptr(), force.data_ptr(), _ptr(cum), _ptr(backoff), _native.stream_ptr(stream)),
+        "kmeans_centre_stats")
 
 
 def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor,

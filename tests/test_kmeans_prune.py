@@ -408,3 +408,25 @@ def test_training_cost_exact_on_offset_data_gpu(fp8, prune):
     c1 = float(K.cost_pass(xm, n, eng.dp, eng.labels, eng.cb).item())
     ref1 = float(((xf - eng.cb[:k, :d].double()[lab]) ** 2).sum())
     assert abs(c1 - ref1) <= 1e-9 * ref1
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("scale", [0.5, 3.0])
+def test_prune_backoff_same_fit(monkeypatch, scale):
+    """After a pruned step goes over the candidate cap, the next steps skip the bounds pass and run full
+    (CML_KMEANS_PRUNE_BACKOFF): the fit is bit for bit the one that retries the bounds every step."""
+    n, d, k = 150_000, 128, 64
+    x = _blobs(n, d, k, seed=5, scale=scale, device="cuda", dtype=torch.bfloat16)
+    res = {}
+    for nb in ("0", "2"):
+        monkeypatch.setenv("CML_KMEANS_PRUNE_BACKOFF", nb)
+        eng = LloydEngine(x, d, k)
+        assert eng._pdev
+        eng.track_prune = True
+        eng.set_centers(eng.init_kmeans_parallel(seed=4))
+        eng.fit(12, 0.0)
+        res[nb] = (eng.centers.cpu().numpy(), eng.labels[:n].clone(), eng.training_cost(), eng.prune_history())
+    (c0, l0, t0, h0), (c1, l1, t1, h1) = res["0"], res["2"]
+    assert np.array_equal(c0, c1) and torch.equal(l0, l1) and t0 == t1
+    if scale < 1.0:  # overlapping blobs: the backed-off steps are all full
+        assert sum(1 for f, _ in h1 if f) >= sum(1 for f, _ in h0 if f)
