@@ -898,7 +898,7 @@ class LloydEngine:
         b = torch.empty(max(n, 1), dtype=torch.float64, device=self.device)
         if n:
             K.exact_dist(self.x, C, lab, b)
-        tot = b[:n].sum().reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=self.device)
+        tot = K.sum_exact(b[:n]).reshape(1) if n else torch.zeros(1, dtype=torch.float64, device=self.device)
         self.comm.allreduce_(tot)
         return tot[0]
 
@@ -906,13 +906,14 @@ class LloydEngine:
         if self._screen:
             return self._step_screen()
         labels, best = K.assign_reference(self.x, self.centers)
+        # the cost: a correctly rounded sum too (host and device sessions report the same bits)
         if self.w is not None:  # weighted rows: [w·x | w] summed in double-double, the weight column too
             aug, _, aug_lo = K.sums_reference(self._wx, labels, self.k, with_lo=True)
-            aug, _, cost = self._exact_global(aug, aug_lo, None, (best * self.w).sum())
+            aug, _, cost = self._exact_global(aug, aug_lo, None, K.sum_exact(best * self.w))
             sums, counts = aug[:, : self.d], aug[:, self.d]
         else:
             sums, counts, sums_lo = K.sums_reference(self.x, labels, self.k, with_lo=True)
-            sums, counts, cost = self._exact_global(sums, sums_lo, counts, best.sum())
+            sums, counts, cost = self._exact_global(sums, sums_lo, counts, K.sum_exact(best))
         msg = torch.cat([sums.reshape(-1), counts, cost.reshape(1)])
         self._update_cpu(msg)
         self.labels = labels

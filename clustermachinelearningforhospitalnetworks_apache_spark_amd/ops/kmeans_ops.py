@@ -920,13 +920,18 @@ def exact_sums(x: torch.Tensor, labels: torch.Tensor, k: int, d: int | None = No
     lab = labels[:n]
     lab = lab if lab.dtype == torch.int32 and lab.is_contiguous() else lab.to(torch.int32).contiguous()
     counts = torch.zeros(k, dtype=torch.int32, device=x.device)
-    if n:
-        int_hist(lab, n, k, counts)  # exact int32 counts, no host read (bincount syncs)
     seg = torch.zeros(k + 1, dtype=torch.int32, device=x.device)
-    seg[1:] = torch.cumsum(counts, 0, dtype=torch.int32)
-    # stable sort of the int32 labels (fixed chunks of the sorted order)
-    perm = torch.sort(lab, stable=True).indices.to(torch.int32) if n else torch.zeros(1, dtype=torch.int32,
-                                                                                        device=x.device)
+    if k == 1:  # one cluster (sum_exact): the rows in order, no histogram or sort
+        counts.fill_(n)
+        seg[1] = n
+        perm = torch.arange(max(n, 1), dtype=torch.int32, device=x.device)
+    else:
+        if n:
+            int_hist(lab, n, k, counts)  # exact int32 counts, no host read (bincount syncs)
+        seg[1:] = torch.cumsum(counts, 0, dtype=torch.int32)
+        # stable sort of the int32 labels (fixed chunks of the sorted order)
+        perm = torch.sort(lab, stable=True).indices.to(torch.int32) if n else torch.zeros(1, dtype=torch.int32,
+                                                                                            device=x.device)
     lib = _native.kernels()
     nch = max(1, int(lib.cml_kmeans_exact_chunks(n)))
     slots = torch.empty(4 * nch * d, dtype=torch.float64, device=x.device)
@@ -1025,6 +1030,18 @@ def cert_moves(x: torch.Tensor, k: int, mv_row, mv_old, mv_new, m_dev, hist, seg
         mv_new.data_ptr(), m_dev.data_ptr(), hist.data_ptr(), seg.data_ptr(), cursor.data_ptr(), perm.data_ptr(),
         P_hi.data_ptr(), P_lo.data_ptr(), S_hi.data_ptr(), S_lo.data_ptr(), cnt.data_ptr(), _ptr(C_cur),
         _ptr(C_next), 0, _native.stream_ptr(stream)), "kmeans_cert_moves")
+
+
+def sum_exact(v: torch.Tensor) -> torch.Tensor:
+    """Correctly rounded sum of an f64 vector (double-double accumulation; a 0-d tensor on v's device): the
+    same bits on the host and the device, whatever the order — the exact path's trainingCost."""
+    v = v.reshape(-1).to(torch.float64)
+    n = int(v.shape[0])
+    if n == 0:
+        return torch.zeros((), dtype=torch.float64, device=v.device)
+    lab = torch.zeros(n, dtype=torch.int32 if v.is_cuda else torch.int64, device=v.device)
+    S, _ = sums_reference(v.reshape(n, 1), lab, 1)
+    return S.reshape(())
 
 
 def dd_fold(hi: torch.Tensor, lo: torch.Tensor) -> torch.Tensor:
