@@ -22,7 +22,7 @@ import numpy as np
 import torch
 
 from . import types as T
-from .column import (AggExpr, Alias, ColRef, Column, ColumnData, Expr, Lit, SortOrder, _expr, _to_host,
+from .column import (AggExpr, Alias, ColRef, Column, ColumnData, DictColumnData, Expr, Lit, SortOrder, _expr, _to_host,
                      micros_to_datetime, ts_to_micros)
 from .dataframe_more import DataFrameMoreMixin
 
@@ -214,9 +214,22 @@ class DataFrame(DataFrameMoreMixin):
 
     # ------------------------------------------------------------------------------------------ row selection
     def _take_rows(self, idx: torch.Tensor) -> "DataFrame":
+        from ..utils.trace import trace
         idx = idx.to(self._device)
-        cols = {k: v.take(idx) for k, v in self._cols.items()}
-        return self._new(self._schema, cols, int(idx.numel()), self._row_ids[idx])
+        cols = {}
+        host_idx = None
+        with trace("frame.take_rows"):
+            for k, v in self._cols.items():
+                if v.is_host or isinstance(v, DictColumnData):
+                    if host_idx is None:  # one device->host copy of the index for every host column
+                        with trace("frame.take_rows.index_to_host"):
+                            host_idx = idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)
+                    with trace("frame.take_rows.host_column"):
+                        cols[k] = v.take(host_idx)
+                else:
+                    cols[k] = v.take(idx)
+            rid = self._row_ids[idx]
+        return self._new(self._schema, cols, int(idx.numel()), rid)
 
     def _mask_index(self, mask: torch.Tensor) -> torch.Tensor:
         """Ascending row indices of a bool mask (GPU: the K3 compaction kernel)."""
@@ -306,11 +319,19 @@ class DataFrame(DataFrameMoreMixin):
             return self._dropna(names, how, thresh)
 
     def _dropna(self, names, how, thresh) -> "DataFrame":
+        from ..utils.trace import trace
         good = torch.zeros((self._nrows,), dtype=torch.int32, device=self._device)
-        for n in names:
-            cd = self._cols[n]
-            m = _non_null_mask(cd)
-            good += m.to(self._device).to(torch.int32)
+        with trace("dropna.masks"):
+            always = 0  # columns that cannot hold a null: no per-row work (no host mask, no copy)
+            for n in names:
+                cd = self._cols[n]
+                if _never_null(cd):
+                    always += 1
+                    continue
+                m = _non_null_mask(cd)
+                good += m.to(self._device).to(torch.int32)
+            if always:
+                good += always
         if thresh is not None:
             keep = good >= thresh
         elif how == "all":
@@ -716,6 +737,19 @@ class DataFrameNaFunctions:
 
 
 # ---------------------------------------------------------------------------------------------- helpers
+
+def _never_null(cd: ColumnData) -> bool:
+    """No validity mask and no value that reads as null: dictionary strings (nulls are masked rows),
+    device integer/bool columns (floats can hold NaN, which na.drop treats as null)."""
+    if cd.valid is not None:
+        return False
+    if isinstance(cd, DictColumnData):
+        nn = getattr(cd, "_never_null", None)
+        if nn is None:  # code -1 is a null string: one min over the codes, cached on the column
+            nn = cd._never_null = bool(len(cd) == 0 or int(cd.codes.min()) >= 0)
+        return nn
+    return (not cd.is_host) and not cd.values.is_floating_point() and not cd.values.is_complex()
+
 
 def _non_null_mask(cd: ColumnData) -> torch.Tensor:
     if cd.is_host and cd.codes is not None:

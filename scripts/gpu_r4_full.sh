@@ -5,7 +5,7 @@ export TMPDIR=/tmp
 export PYTHONPATH=$GRAFT_REPO_ROOT
 O=gpurun_out/${1:-r4full}
 mkdir -p $O
-timeout -k 10 1000 python -u -m pytest tests -m gpu -q -x --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
+timeout -k 10 1000 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider > $O/pytest_gpu.log 2>&1
 rc=$?
 tail -3 $O/pytest_gpu.log
 grep -E "FAILED|Error" $O/pytest_gpu.log | head -20

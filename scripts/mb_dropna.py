@@ -59,3 +59,7 @@ for rep in range(3):
     w = timed("sql BETWEEN window", lambda: df.filter(
         "event_time BETWEEN '2025-03-31 22:00:00' AND '2025-03-31 23:00:00'"))
     print("rows", df.count(), "clean", clean.count(), "window", w.count(), flush=True)
+
+if os.environ.get("CML_TRACE") == "1":
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import TRACER
+    print(TRACER.report(), flush=True)
