@@ -144,6 +144,12 @@ class SparkSession:
         self.catalog = Catalog(self)
         from .functions import UDFRegistration
         self.udf = UDFRegistration()
+        if self._warmup_s > 0.0:  # the device warm-up ran: the frame path's kernels too
+            from ..utils.warmup import warm_frames
+            try:
+                self._warmup_s += warm_frames(self)
+            except Exception as e:
+                log.warning("frame warm-up skipped: %s", e)
         self._streams = None
         self._start_time = time.time()
         self.sparkContext = _Context(self)
