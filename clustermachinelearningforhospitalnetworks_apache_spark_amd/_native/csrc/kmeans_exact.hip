@@ -537,6 +537,46 @@ __global__ __launch_bounds__(kThreads) void exact_seg_fix_kernel(const int* __re
   }
 }
 
+// Correctly rounded sum of an f64 vector in two launches: every block folds a contiguous range in
+// double-double (threads strided, then the block's partials in thread order), one block folds the block
+// partials in block order (the result is exact whenever the inputs' exponents span < ~2^80, and always
+// deterministic). The exact paths' trainingCost (kmeans_ops.sum_exact).
+constexpr int kSumBlocks = 1024;
+__global__ __launch_bounds__(kThreads) void sum_dd_partial_kernel(const double* __restrict__ v, long long n,
+                                                                  double* __restrict__ part) {
+  __shared__ double sh[kThreads], sl[kThreads];
+  const long long per = (n + gridDim.x - 1) / gridDim.x;
+  const long long a = (long long)blockIdx.x * per, b = min(n, a + per);
+  double h = 0.0, l = 0.0;
+  for (long long i = a + threadIdx.x; i < b; i += kThreads) dd_add(h, l, v[i]);
+  sh[threadIdx.x] = h;
+  sl[threadIdx.x] = l;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    double H = 0.0, L = 0.0;
+    for (int t = 0; t < kThreads; ++t) {
+      dd_add(H, L, sh[t]);
+      L += sl[t];
+    }
+    dd_norm(H, L);
+    part[2 * blockIdx.x] = H;
+    part[2 * blockIdx.x + 1] = L;
+  }
+}
+
+__global__ __launch_bounds__(64) void sum_dd_final_kernel(const double* __restrict__ part, int nb,
+                                                          double* __restrict__ out) {
+  if (threadIdx.x == 0) {
+    double H = 0.0, L = 0.0;
+    for (int i = 0; i < nb; ++i) {
+      dd_add(H, L, part[2 * i]);
+      L += part[2 * i + 1];
+    }
+    dd_norm(H, L);
+    out[0] = H;
+  }
+}
+
 }  // namespace
 
 // X: f64 (xf64 = 1) or f32 rows [n, ldx elements]; C: f64 [k, d]; labels (int32, read for the change
@@ -550,6 +590,8 @@ static void launch_wide(const T* X, long long n, long long ldx, int d, const dou
   const int dpad = (d + DC - 1) / DC * DC;
   int kt = (8192 / dpad) / KG * KG;  // centres per LDS tile (<= 64 KiB)
   kt = kt < KG ? KG : kt;
+  const int kneed = (k + KG - 1) / KG * KG;  // no tile larger than the centres need
+  kt = kt < kneed ? kt : kneed;
   const int ktp = kt;
   const size_t lds = (size_t)ktp * dpad * sizeof(double);
   if (lds > 65536)
@@ -566,7 +608,13 @@ static void launch_wide_any(const T* X, long long n, long long ldx, int d, const
                             double* best, int* changed, const int* idx, const int* n_dev, float* ub, float* lb,
                             int* mv_row, int* mv_old, int* mv_new, int* mv_count, hipStream_t st) {
   const int dpad = (d + 7) / 8 * 8;
-  if (dpad <= 256 && k > 16)
+  if (k <= 4 && dpad <= 2048)  // few centres: no zero-padded accumulators
+    launch_wide<T, 4>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                      mv_count, st);
+  else if (k <= 8 && dpad <= 1024)
+    launch_wide<T, 8>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
+                      mv_count, st);
+  else if (dpad <= 256 && k > 16)
     launch_wide<T, 32>(X, n, ldx, d, C, k, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new,
                        mv_count, st);
   else if (dpad <= 512)
@@ -729,5 +777,15 @@ CML_API int cml_kmeans_screen_cert_split(const float* ub, const float* lb, const
   g = g > 2048 ? 2048 : g;
   hipLaunchKernelGGL(screen_cert_split_kernel, dim3((unsigned)g), dim3(kThreads), 0, (hipStream_t)stream, ub, lb, ea,
                      eb, en, cst, n, lst, count, u_out, l_out);
+  return cml_status();
+}
+
+// out: f64 [1]; part: f64 scratch [2 * kSumBlocks].
+CML_API int cml_kmeans_sum_dd(const double* v, long long n, double* out, double* part, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  long long nb = (n + kThreads * 16 - 1) / (kThreads * 16);
+  nb = nb < 1 ? 1 : (nb > kSumBlocks ? kSumBlocks : nb);
+  hipLaunchKernelGGL(sum_dd_partial_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, v, n, part);
+  hipLaunchKernelGGL(sum_dd_final_kernel, dim3(1), dim3(64), 0, st, part, (int)nb, out);
   return cml_status();
 }

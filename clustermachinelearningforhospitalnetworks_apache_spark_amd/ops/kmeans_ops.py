@@ -109,6 +109,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_to_bf16_split": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp,
                                          c_vp]),
     "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -1035,11 +1036,17 @@ def cert_moves(x: torch.Tensor, k: int, mv_row, mv_old, mv_new, m_dev, hist, seg
 def sum_exact(v: torch.Tensor) -> torch.Tensor:
     """Correctly rounded sum of an f64 vector (double-double accumulation; a 0-d tensor on v's device): the
     same bits on the host and the device, whatever the order — the exact path's trainingCost."""
-    v = v.reshape(-1).to(torch.float64)
+    v = v.reshape(-1).to(torch.float64).contiguous()
     n = int(v.shape[0])
     if n == 0:
         return torch.zeros((), dtype=torch.float64, device=v.device)
-    lab = torch.zeros(n, dtype=torch.int32 if v.is_cuda else torch.int64, device=v.device)
+    if v.is_cuda:  # two launches (block partials in double-double, folded in block order)
+        out = torch.empty(1, dtype=torch.float64, device=v.device)
+        part = torch.empty(2 * 1024, dtype=torch.float64, device=v.device)
+        _native.check(_native.kernels().cml_kmeans_sum_dd(v.data_ptr(), n, out.data_ptr(), part.data_ptr(),
+                                                          _native.stream_ptr(None)), "kmeans_sum_dd")
+        return out.reshape(())
+    lab = torch.zeros(n, dtype=torch.int64, device=v.device)
     S, _ = sums_reference(v.reshape(n, 1), lab, 1)
     return S.reshape(())
 

@@ -206,3 +206,13 @@ def test_split_screen_layout_bounds_and_fewer_rechecks(monkeypatch, k):
         assert bool((st.ub[:n].double() >= own * (1 - 1e-7)).all()) and bool((st.lb[:n].double() <= other * (1 + 1e-7)).all())
         counts[split] = st.rechecked[-1]
     assert counts["1"] < n // 50 and (counts["1"] * 5 <= counts["0"] or counts["1"] <= 100), counts
+
+
+@pytest.mark.parametrize("n", [1, 1000, 3_000_001])
+def test_sum_exact_device_correctly_rounded(n):
+    import math
+    g = torch.Generator().manual_seed(n)
+    v = torch.randn(n, generator=g, dtype=torch.float64) * torch.logspace(-3, 6, n, dtype=torch.float64)
+    dev = K.sum_exact(v.cuda())
+    host = K.sum_exact(v)
+    assert float(dev) == float(host) == math.fsum(v.tolist())
