@@ -113,11 +113,17 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
     load_tile(0, k);
     __syncthreads();
   }
+  // the block's 256 rows are staged DC dimensions at a time through a transposed LDS tile (coalesced
+  // 32-B row segments; a thread-per-row walk of the rows read 64 scattered segments per load and ran a
+  // few-centre pass at 0.4 TB/s), each thread folding its own row from it — the same fold order
+  __shared__ T xs[DC * (kThreads + 1)];
+  __shared__ long long rows_s[kThreads];
   for (long long base = (long long)blockIdx.x * kThreads; base < cnt; base += (long long)gridDim.x * kThreads) {
     const long long t0 = base + threadIdx.x;
     const bool live = t0 < cnt;
     const long long r = live ? (idx != nullptr ? (long long)idx[t0] : t0) : 0;
-    const T* xrow = X + r * ldx;
+    __syncthreads();  // rows_s / xs of the previous base are no longer read
+    rows_s[threadIdx.x] = live ? r : -1;
     double bd = __builtin_huge_val(), sd = __builtin_huge_val();
     int bi = 0;
     for (int c0 = 0; c0 < k; c0 += kt) {
@@ -127,15 +133,21 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
         load_tile(c0, kc);
         __syncthreads();
       }
-      if (!live) continue;
       for (int j0 = 0; j0 < kc; j0 += KG) {
         double acc[KG];
 #pragma unroll
         for (int a = 0; a < KG; ++a) acc[a] = 0.0;
         for (int tb = 0; tb < dpad; tb += DC) {
+          __syncthreads();
+          for (int e = threadIdx.x; e < kThreads * DC; e += kThreads) {
+            const int rr = e / DC, tt = e - rr * DC;
+            const long long row = rows_s[rr];
+            xs[tt * (kThreads + 1) + rr] = (row >= 0 && tb + tt < d) ? X[row * ldx + tb + tt] : (T)0;
+          }
+          __syncthreads();
           double xv[DC];
 #pragma unroll
-          for (int u = 0; u < DC; ++u) xv[u] = tb + u < d ? (double)xrow[tb + u] : 0.0;
+          for (int u = 0; u < DC; ++u) xv[u] = (double)xs[u * (kThreads + 1) + threadIdx.x];
 #pragma unroll
           for (int a = 0; a < KG; ++a) {
             const double* cj = ct + (long long)(j0 + a) * dpad + tb;
@@ -146,16 +158,18 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
             }
           }
         }
+        if (live) {
 #pragma unroll
-        for (int a = 0; a < KG; ++a) {
-          if (j0 + a < kc) {  // centres ascending: strict < keeps the lowest index
-            const double v = acc[a];
-            if (v < bd) {
-              sd = bd;
-              bd = v;
-              bi = c0 + j0 + a;
-            } else if (v < sd) {
-              sd = v;
+          for (int a = 0; a < KG; ++a) {
+            if (j0 + a < kc) {  // centres ascending: strict < keeps the lowest index
+              const double v = acc[a];
+              if (v < bd) {
+                sd = bd;
+                bd = v;
+                bi = c0 + j0 + a;
+              } else if (v < sd) {
+                sd = v;
+              }
             }
           }
         }
@@ -594,7 +608,9 @@ static void launch_wide(const T* X, long long n, long long ldx, int d, const dou
   kt = kt < kneed ? kt : kneed;
   const int ktp = kt;
   const size_t lds = (size_t)ktp * dpad * sizeof(double);
-  if (lds > 65536)
+  // static LDS (the staged rows, their ids, the append scratch) counts against the same budget
+  const size_t stat = (size_t)DC * (kThreads + 1) * sizeof(T) + kThreads * sizeof(long long) + 64;
+  if (lds + stat > 65536)
     (void)hipFuncSetAttribute((const void*)exact_assign_wide_kernel<T, KG, DC>,
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   long long blocks = (n + kThreads - 1) / kThreads;

@@ -366,3 +366,35 @@ def test_rr_fp8_assign_matches_k9(n, d, k):
     assert torch.equal(lab[clear], out[0][0][clear])
     _check_dist(best, ref_d, band)
     _check_dist(out[0][1], ref_d, band)
+
+
+@pytest.mark.parametrize("n,d,k", [(250_003, 256, 200), (120_000, 128, 64), (70_001, 512, 96)])
+def test_rr_and_k9_trajectories_bitwise_on_separated_exact_data(n, d, k):
+    """No near-ties anywhere: small-integer rows (exact in bf16) in blobs 40 units apart, so every row's
+    nearest centre wins by a margin far above any f32 rounding. The K9r fit (incremental sums) and the K9
+    fit then give the same labels after every step and bit-identical centres — a tile-edge or tail bug in
+    either kernel at any step fails this exactly, not within a label-agreement tolerance."""
+    rs = np.random.RandomState(n)
+    cen = rs.randint(0, 3, (k, d)) * 40 + rs.randint(0, 4, (k, d))
+    x = torch.as_tensor(cen[rs.randint(0, k, n)] + rs.randint(-2, 3, (n, d)), dtype=torch.float32,
+                        device="cuda").to(torch.bfloat16)
+    init = cen.astype(np.float64)  # one centre per blob: no centre splits a blob, so no row is near a tie
+    traj = {}
+    for v in (0, 8):
+        K.set_assign_variant(v)
+        K.set_rr_default(False)
+        try:
+            eng = LloydEngine(x, d, k)
+            assert (eng.aplan.rr_ct > 0) == (v == 8)
+            eng.set_centers(init)
+            steps = []
+            for _ in range(8):
+                eng.step()
+                steps.append((eng.labels[:n].clone(), eng.centers.cpu().clone()))
+            traj[v] = steps
+        finally:
+            K.set_assign_variant(0)
+            K.set_rr_default(True)
+    for (l0, c0), (l8, c8) in zip(traj[0], traj[8]):
+        assert torch.equal(l0.long(), l8.long())
+        assert torch.equal(c0, c8)
