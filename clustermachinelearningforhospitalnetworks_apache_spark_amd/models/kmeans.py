@@ -1858,13 +1858,17 @@ class LloydEngine:
         m = int(new.shape[0])
         P = prev.to(device=dev, dtype=torch.float64)
         Y = new.to(device=dev, dtype=torch.float64)
-        pn, yn = (P * P).sum(1), (Y * Y).sum(1)
-        d2 = pn[:, None] + yn[None, :] - 2.0 * (P @ Y.T)
-        eps = 1e-12 * (pn.max() + yn.max())  # device scalar (no host read)
-        vals, order = torch.sort((d2 - eps).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6), dim=1)
-        tab_v = vals.to(torch.float32).contiguous()
-        tab_j = order.to(torch.int32).contiguous()
-        pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
+        tab = K.init_table(P, Y)  # one launch: direct-difference distances, sorted in LDS
+        if tab is not None:
+            tab_v, tab_j, pn32 = tab
+        else:
+            pn, yn = (P * P).sum(1), (Y * Y).sum(1)
+            d2 = pn[:, None] + yn[None, :] - 2.0 * (P @ Y.T)
+            eps = 1e-12 * (pn.max() + yn.max())  # device scalar (no host read)
+            vals, order = torch.sort((d2 - eps).clamp_(min=0.0).sqrt_().mul_(1.0 - 1e-6), dim=1)
+            tab_v = vals.to(torch.float32).contiguous()
+            tab_j = order.to(torch.int32).contiguous()
+            pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
         tau = 2.0 * self._tau
         tr = self.aplan.round_rows
         list_a = torch.empty((n, 4), dtype=torch.int32, device=dev)  # (row, nearest, reach, cost) entries

@@ -110,6 +110,7 @@ _native.register_kernel_sigs({
                                          c_vp]),
     "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_kmeans_init_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -757,6 +758,25 @@ def init_classify(cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor, pn: 
         cost.data_ptr(), near.data_ptr(), xn.data_ptr(), pn.data_ptr(), tab_v.data_ptr(), m, float(tau), int(n),
         int(lmax), list_a.data_ptr(), cnt_a.data_ptr(), list_b.data_ptr(), cnt_b.data_ptr(),
         _native.stream_ptr(stream)), "kmeans_init_classify")
+
+
+def init_table(P: torch.Tensor, Y: torch.Tensor, stream=None):
+    """The pruned k-means|| pass's table in one launch (kmeans_init_table.hip): (f32 [mp, m] distances from
+    every existing candidate to the new ones, rounded down and sorted ascending; int32 [mp, m] their
+    indices; f32 [mp] squared norms rounded up). None when m exceeds the kernel's 1024."""
+    mp, d = int(P.shape[0]), int(P.shape[1])
+    m = int(Y.shape[0])
+    if m > 1024 or not P.is_cuda:
+        return None
+    P = P.to(torch.float64).contiguous()
+    Y = Y.to(torch.float64).contiguous()
+    tab_v = torch.empty((mp, m), dtype=torch.float32, device=P.device)
+    tab_j = torch.empty((mp, m), dtype=torch.int32, device=P.device)
+    pn32 = torch.empty(mp, dtype=torch.float32, device=P.device)
+    _native.check(_native.kernels().cml_kmeans_init_table(P.data_ptr(), mp, Y.data_ptr(), m, d, tab_v.data_ptr(),
+                                                          tab_j.data_ptr(), pn32.data_ptr(),
+                                                          _native.stream_ptr(stream)), "kmeans_init_table")
+    return tab_v, tab_j, pn32
 
 
 def init_near_list(x: torch.Tensor, dp: int, cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor,

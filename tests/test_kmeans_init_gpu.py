@@ -206,3 +206,20 @@ def test_sum_f64_matches_torch(n):
     want = float(x[:n].double().sum())
     assert got == pytest.approx(want, rel=1e-12, abs=1e-12)
     assert float(K.sum_f64(x, n)) == got  # deterministic
+
+
+@pytest.mark.parametrize("mp,m,d", [(1, 1, 3), (257, 513, 256), (640, 1024, 128), (5, 37, 512)])
+def test_init_table_kernel(mp, m, d):
+    """The pruned pass's table in one launch: each row sorted ascending, each entry a lower bound of the
+    real distance within 2e-6 of it, the indices a permutation, the norms rounded up."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+    g = torch.Generator(device="cuda").manual_seed(mp + m)
+    P = torch.randn(mp, d, generator=g, device="cuda", dtype=torch.float64) * 5
+    Y = torch.randn(m, d, generator=g, device="cuda", dtype=torch.float64) * 5
+    tab_v, tab_j, pn32 = K.init_table(P, Y)
+    D = torch.cdist(P, Y)
+    assert bool((tab_v[:, 1:] >= tab_v[:, :-1]).all())
+    assert torch.equal(tab_j.sort(dim=1).values, torch.arange(m, device="cuda", dtype=torch.int32).expand(mp, m))
+    dj = D.gather(1, tab_j.long())
+    assert bool((tab_v.double() <= dj).all()) and bool((tab_v.double() >= dj * (1 - 2e-6) - 1e-30).all())
+    assert bool((pn32.double() >= (P * P).sum(1)).all())
