@@ -766,7 +766,13 @@ class LloydEngine:
         step = max(1, st.rr_max)
         for c0 in range(0, int(cands.shape[0]), step):
             C = cands[c0:c0 + step]
-            self._screen_labels(C, lab_c, best_c)
+            if int(C.shape[0]) <= 8:
+                # a short leftover chunk (e.g. 2 of a round's 130 candidates): the exact fold over every
+                # row reads X once and yields the distances too — cheaper than a screened pass over the
+                # wide split copy plus exact_dist
+                K.exact_top2(self.x, C, lab_c, st.ub, st.lb, best=best_c)
+            else:
+                self._screen_labels(C, lab_c, best_c)
             better = best_c[:n] < best[:n]
             best[:n] = torch.where(better, best_c[:n], best[:n])
             lab[:n] = torch.where(better, lab_c[:n].long() + c0, lab[:n])
