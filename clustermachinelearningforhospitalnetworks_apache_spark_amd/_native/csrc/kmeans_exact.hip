@@ -218,6 +218,52 @@ __global__ __launch_bounds__(kThreads) void exact_dist_kernel(const T* __restric
   const long long j = live ? (long long)labels[r] - lab_off : 0;
   const double* cj = C + j * d;
   double acc = 0.0;
+  if (vec && d % kDistCh == 0) {
+    // every chunk full: 16-B loads with the next chunk's loads in flight (registers) while the block folds
+    // the current one from LDS
+    constexpr int V = 16 / sizeof(T);
+    constexpr int Q = kDistCh / V;  // 16-B loads per thread per chunk
+    uint4 q[Q];
+    auto issue = [&](int t0) {
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        const int e = threadIdx.x + i * kThreads;
+        const int rr = e / Q, tv = (e - rr * Q) * V;
+        const long long row = r0 + rr;
+        q[i] = row < n ? *reinterpret_cast<const uint4*>(X + row * ldx + t0 + tv) : uint4{0u, 0u, 0u, 0u};
+      }
+    };
+    issue(0);
+    for (int t0 = 0; t0 < d; t0 += kDistCh) {
+      __syncthreads();
+#pragma unroll
+      for (int i = 0; i < Q; ++i) {
+        const int e = threadIdx.x + i * kThreads;
+        const int rr = e / Q, tv = (e - rr * Q) * V;
+        T v[V];
+        __builtin_memcpy(v, &q[i], 16);
+#pragma unroll
+        for (int u = 0; u < V; ++u) xs[(tv + u) * (kThreads + 1) + rr] = v[u];
+      }
+      if (kc > 0)
+        for (int e = threadIdx.x; e < kc * kDistCh; e += kThreads) {
+          const int jj = e / kDistCh, tt = e - jj * kDistCh;
+          cs[e] = C[(long long)jj * d + t0 + tt];
+        }
+      if (t0 + kDistCh < d) issue(t0 + kDistCh);
+      __syncthreads();
+      if (live) {
+        const double* cc = kc > 0 ? cs + j * kDistCh : cj + t0;
+#pragma unroll
+        for (int tt = 0; tt < kDistCh; ++tt) {
+          const double e = (double)xs[tt * (kThreads + 1) + threadIdx.x] - cc[tt];
+          acc = __fma_rn(e, e, acc);
+        }
+      }
+    }
+    if (live) best[r] = acc;
+    return;
+  }
   for (int t0 = 0; t0 < d; t0 += kDistCh) {
     const int dc = min(kDistCh, d - t0);
     __syncthreads();

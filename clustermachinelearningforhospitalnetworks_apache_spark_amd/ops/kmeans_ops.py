@@ -257,7 +257,15 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         # twin's loop (a few no-op launches instead of one host round trip per iteration)
         flags = torch.zeros(3, dtype=torch.int32, device=dev)
         fp = flags.data_ptr()
+        # the stop flag is read back every 8 iterations (one small copy): converged local fits (a few
+        # iterations) then launch 8 instead of max_iter x 3 no-op kernels (k-means|| finish on the shard)
+        stop_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         for it in range(max_iter):
+            if it and it % 8 == 0:
+                stop_h.copy_(flags[0:1], non_blocking=True)
+                torch.cuda.current_stream(dev).synchronize()
+                if int(stop_h[0]):
+                    break
             slot = it & 1
             _native.check(lib.cml_local_assign(pts.data_ptr(), m, d, CT.data_ptr(), int(k), lab.data_ptr(),
                                                fp + 4 * (1 + slot), fp, st), "local_assign")
