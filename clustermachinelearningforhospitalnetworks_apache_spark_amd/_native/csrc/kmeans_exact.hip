@@ -350,7 +350,8 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void to_bf16_split_kernel(const T* __restrict__ X, long long n, long long ldx,
                                                                  int d, int ds, u16* __restrict__ out, long long ldo,
                                                                  float* __restrict__ ea, float* __restrict__ eb,
-                                                                 float* __restrict__ en, float* __restrict__ xn) {
+                                                                 float* __restrict__ en, float* __restrict__ xn,
+                                                                 bool vec) {
   // 16 lanes per row (4 rows per wave); a lane owns 8-dimension groups: one 16-B store per segment
   // (ds and ldo multiples of 8, checked at launch), the three norms reduced over the 16 lanes
   const int lane = threadIdx.x & 63, q = lane & 15;
@@ -365,11 +366,22 @@ __global__ __launch_bounds__(kThreads) void to_bf16_split_kernel(const T* __rest
       uint4* o = reinterpret_cast<uint4*>(out + r * ldo);
       for (int t0 = 8 * q; t0 < ds; t0 += 128) {
         unsigned wh[4] = {0u, 0u, 0u, 0u}, wl[4] = {0u, 0u, 0u, 0u};
+        T xv8[8];
+        if (vec && t0 + 8 <= d) {  // 16-B loads of the lane's 8 values
+#pragma unroll
+          for (int h = 0; h < (int)(8 * sizeof(T) / 16); ++h) {
+            const uint4 q4 = *reinterpret_cast<const uint4*>(X + r * ldx + t0 + h * (16 / (int)sizeof(T)));
+            __builtin_memcpy(&xv8[h * (16 / sizeof(T))], &q4, 16);
+          }
+        } else {
+#pragma unroll
+          for (int u = 0; u < 8; ++u) xv8[u] = t0 + u < d ? X[r * ldx + t0 + u] : (T)0;
+        }
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
           const int t = t0 + u;
           if (t < d) {
-            const double v = (double)X[r * ldx + t];
+            const double v = (double)xv8[u];
             const u16 hb = f32_to_bf16((float)v);
             const double r1 = v - (double)bf16_to_f32(hb);
             const u16 lb = f32_to_bf16((float)r1);
@@ -821,12 +833,13 @@ CML_API int cml_kmeans_to_bf16_split(const void* X, int xf64, long long n, long 
   long long g = (n + 15) / 16;
   g = g > 8192 ? 8192 : g;
   hipStream_t st = (hipStream_t)stream;
+  const bool vec = ((uintptr_t)X % 16 == 0) && ((ldx * (xf64 ? 8 : 4)) % 16 == 0);
   if (xf64)
     hipLaunchKernelGGL((to_bf16_split_kernel<double>), dim3((unsigned)g), dim3(kThreads), 0, st, (const double*)X, n,
-                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn);
+                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn, vec);
   else
     hipLaunchKernelGGL((to_bf16_split_kernel<float>), dim3((unsigned)g), dim3(kThreads), 0, st, (const float*)X, n,
-                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn);
+                       ldx, d, ds, (u16*)out, ldo, ea, eb, en, xn, vec);
   return cml_status();
 }
 
