@@ -94,7 +94,7 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
     const T* __restrict__ X, long long n, long long ldx, int d, const double* __restrict__ C, int k, int kt,
     int* __restrict__ labels, double* __restrict__ best, int* __restrict__ changed, const int* __restrict__ idx,
     const int* __restrict__ n_dev, float* __restrict__ ub, float* __restrict__ lb, int* __restrict__ mv_row,
-    int* __restrict__ mv_old, int* __restrict__ mv_new, int* __restrict__ mv_count) {
+    int* __restrict__ mv_old, int* __restrict__ mv_new, int* __restrict__ mv_count, bool vec) {
   extern __shared__ __align__(16) unsigned char smem[];
   __shared__ int s_w[kThreads / 64 + 1];
   double* ct = reinterpret_cast<double*>(smem);  // [round_up(kt, KG)][dpad]
@@ -139,10 +139,28 @@ __global__ __launch_bounds__(kThreads) void exact_assign_wide_kernel(
         for (int a = 0; a < KG; ++a) acc[a] = 0.0;
         for (int tb = 0; tb < dpad; tb += DC) {
           __syncthreads();
-          for (int e = threadIdx.x; e < kThreads * DC; e += kThreads) {
-            const int rr = e / DC, tt = e - rr * DC;
-            const long long row = rows_s[rr];
-            xs[tt * (kThreads + 1) + rr] = (row >= 0 && tb + tt < d) ? X[row * ldx + tb + tt] : (T)0;
+          if (vec && tb + DC <= d) {  // 16-B loads (4 f32 / 2 f64 dimensions of a row each)
+            constexpr int V = 16 / sizeof(T);
+            for (int e = threadIdx.x; e < kThreads * (DC / V); e += kThreads) {
+              const int rr = e / (DC / V), tv = (e - rr * (DC / V)) * V;
+              const long long row = rows_s[rr];
+              T v[V];
+              if (row >= 0) {
+                const uint4 q4 = *reinterpret_cast<const uint4*>(X + row * ldx + tb + tv);
+                __builtin_memcpy(v, &q4, 16);
+              } else {
+#pragma unroll
+                for (int u = 0; u < V; ++u) v[u] = (T)0;
+              }
+#pragma unroll
+              for (int u = 0; u < V; ++u) xs[(tv + u) * (kThreads + 1) + rr] = v[u];
+            }
+          } else {
+            for (int e = threadIdx.x; e < kThreads * DC; e += kThreads) {
+              const int rr = e / DC, tt = e - rr * DC;
+              const long long row = rows_s[rr];
+              xs[tt * (kThreads + 1) + rr] = (row >= 0 && tb + tt < d) ? X[row * ldx + tb + tt] : (T)0;
+            }
           }
           __syncthreads();
           double xv[DC];
@@ -673,8 +691,10 @@ static void launch_wide(const T* X, long long n, long long ldx, int d, const dou
                               hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   long long blocks = (n + kThreads - 1) / kThreads;
   if (idx != nullptr) blocks = blocks < 4096 ? blocks : 4096;  // grid-stride over the listed rows
+  const bool vec = ((uintptr_t)X % 16 == 0) && ((ldx * (long long)sizeof(T)) % 16 == 0);
   hipLaunchKernelGGL((exact_assign_wide_kernel<T, KG, DC>), dim3((unsigned)blocks), dim3(kThreads), lds, st, X, n,
-                     ldx, d, C, k, kt, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new, mv_count);
+                     ldx, d, C, k, kt, labels, best, changed, idx, n_dev, ub, lb, mv_row, mv_old, mv_new, mv_count,
+                     vec);
 }
 
 template <typename T>

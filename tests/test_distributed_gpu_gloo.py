@@ -210,3 +210,65 @@ def test_four_uneven_ranks_with_an_empty_one_match_single_rank(tmp_path, monkeyp
     # the capped rank took the full-pass branch, the big rank pruned
     assert any(full for full, _ in res[2]["hist"]), res[2]["hist"]
     assert any(not full for full, _ in res[3]["hist"][1:]), res[3]["hist"]
+
+
+# ---- precision "screen" (f32 rows, the certified exact path) over three gloo ranks, one of them empty:
+# each rank's double-double sums fold in rank order, so the fit is the one-rank fit bit for bit — for data
+# that is not on any grid (plain f32 rows)
+
+_SPLITS_S = [0, 41_000, 41_000, 90_000]
+NS, DS, KS = 90_000, 128, 24
+
+
+def _data_s():
+    rs = np.random.RandomState(19)
+    cen = rs.randn(KS, DS) * 3 + 50.0
+    return (cen[rs.randint(0, KS, NS)] + rs.randn(NS, DS)).astype(np.float32)
+
+
+def _fit_s(x_local, comm):
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    eng = LloydEngine(torch.as_tensor(x_local, device="cuda"), DS, KS, comm, precision="screen")
+    init = eng.init_kmeans_parallel(seed=8)
+    eng.set_centers(init)
+    it = eng.fit(10, 0.0)
+    return {"init": np.asarray(init).tolist(), "centers": eng.centers.cpu().numpy().tolist(), "it": it,
+            "cost": eng.training_cost(), "sizes": eng.cluster_sizes()}
+
+
+def _rank_main_s(rank, world, port, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port)})
+    import torch
+    import torch.distributed as dist
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
+    x = _data_s()
+    res = _fit_s(x[_SPLITS_S[rank]:_SPLITS_S[rank + 1]], comm)
+    with open(f"{out_path}.{rank}", "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_screen_three_ranks_with_an_empty_one_match_single_rank(tmp_path):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
+    out = str(tmp_path / "s3")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main_s, args=(r, 3, port, out)) for r in range(3)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(300)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [json.load(open(f"{out}.{r}")) for r in range(3)]
+    ref = _fit_s(_data_s(), local_comm())
+    for r in range(3):
+        np.testing.assert_array_equal(np.asarray(res[r]["init"]), np.asarray(ref["init"]))
+        np.testing.assert_array_equal(np.asarray(res[r]["centers"]), np.asarray(ref["centers"]))
+        assert res[r]["it"] == ref["it"] and res[r]["sizes"] == ref["sizes"]
+        assert abs(res[r]["cost"] - ref["cost"]) <= 1e-12 * abs(ref["cost"])
