@@ -529,7 +529,7 @@ __global__ __launch_bounds__(kThreads) void screen_cert_kernel(const float* __re
 // S / S_lo (normalised double-double); the cluster open at its start goes to slot 2ch, the one open at
 // its end (if another) to slot 2ch+1 (hi in slots, lo in slots + 2·nch·d).
 template <typename T>
-__global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restrict__ X, long long ldx, int d,
+__global__ __launch_bounds__(256) void exact_seg_partial_kernel(const T* __restrict__ X, long long ldx, int d,
                                                                const int* __restrict__ perm,
                                                                const int* __restrict__ seg, int k, long long n,
                                                                double* __restrict__ S, double* __restrict__ S_lo,
@@ -537,7 +537,7 @@ __global__ __launch_bounds__(64) void exact_seg_partial_kernel(const T* __restri
   const long long ch = blockIdx.x;
   const long long nch = gridDim.x;
   double* slots_lo = slots + 2 * nch * (long long)d;
-  const int col = blockIdx.y * 64 + threadIdx.x;
+  const int col = blockIdx.y * blockDim.x + threadIdx.x;  // one block spans up to 256 columns: whole-row reads
   const long long p0 = ch * kChunk, p1 = min(n, p0 + kChunk);
   int lo_ = 0, hi_ = k;  // seg[lo_] <= p0 < seg[hi_]
   while (hi_ - lo_ > 1) {
@@ -833,12 +833,15 @@ CML_API int cml_kmeans_exact_segsum(const void* X, int xf64, long long ldx, int 
   hipStream_t st = (hipStream_t)stream;
   const long long nch = n > 0 ? (n + kChunk - 1) / kChunk : 0;
   if (n > 0) {
-    const dim3 g((unsigned)nch, (unsigned)((d + 63) / 64));
+    // threads per block = columns per block: a row's columns in one block (rounded to a wave), so each
+    // gathered row is one contiguous read instead of 64-column pieces
+    const int bt = d <= 64 ? 64 : (d <= 128 ? 128 : 256);
+    const dim3 g((unsigned)nch, (unsigned)((d + bt - 1) / bt));
     if (xf64)
-      hipLaunchKernelGGL((exact_seg_partial_kernel<double>), g, dim3(64), 0, st, (const double*)X, ldx, d, perm, seg,
+      hipLaunchKernelGGL((exact_seg_partial_kernel<double>), g, dim3(bt), 0, st, (const double*)X, ldx, d, perm, seg,
                          k, n, S, S_lo, slots, slot_c);
     else
-      hipLaunchKernelGGL((exact_seg_partial_kernel<float>), g, dim3(64), 0, st, (const float*)X, ldx, d, perm, seg,
+      hipLaunchKernelGGL((exact_seg_partial_kernel<float>), g, dim3(bt), 0, st, (const float*)X, ldx, d, perm, seg,
                          k, n, S, S_lo, slots, slot_c);
   }
   hipLaunchKernelGGL(exact_seg_fix_kernel, dim3(k), dim3(kThreads), 0, st, seg, k, d, nch, S, S_lo, slots, slot_c);
