@@ -1758,9 +1758,10 @@ class LloydEngine:
             elif self.n:
                 # rows per candidate (an int32 histogram of the nearest ids: integer counts, exact in any
                 # order), folded onto the distinct candidates
-                if self.gpu:
+                if self.gpu or nearest.is_cuda:  # device rows (bf16 path or the screen): no bincount sync
                     per_i = torch.zeros(cand.shape[0], dtype=torch.int32, device=self.device)
-                    K.int_hist(nearest, self.n, cand.shape[0], per_i)
+                    near32 = nearest if nearest.dtype == torch.int32 else nearest[: self.n].to(torch.int32)
+                    K.int_hist(near32.contiguous(), self.n, cand.shape[0], per_i)
                     per = per_i.to(torch.float64)
                 else:
                     per = torch.bincount(nearest[: self.n], minlength=cand.shape[0]).to(torch.float64)
