@@ -435,87 +435,6 @@ __global__ __launch_bounds__(kThreads) void to_bf16_split_kernel(const T* __rest
   }
 }
 
-// The split copy and the exact fold distance of every row to ONE centre c0 in one read of X (the first
-// k-means‖ pass of the screen: costs to the first centre): rows staged 8 dimensions at a time through a
-// transposed LDS tile (coalesced loads), one thread per row — the fold runs t ascending as in
-// exact_dist_kernel (same bits), the split segments and norms as in to_bf16_split_kernel (same values).
-template <typename T>
-__global__ __launch_bounds__(kThreads) void to_bf16_split_dist_kernel(
-    const T* __restrict__ X, long long n, long long ldx, int d, int ds, u16* __restrict__ out, long long ldo,
-    float* __restrict__ ea, float* __restrict__ eb, float* __restrict__ en, float* __restrict__ xn,
-    const double* __restrict__ c0, double* __restrict__ best, bool vec) {
-  constexpr int DC = 8;
-  __shared__ T xs[DC * (kThreads + 1)];
-  __shared__ double cs[DC];
-  const long long r0 = (long long)blockIdx.x * kThreads;
-  const long long r = r0 + threadIdx.x;
-  const bool live = r < n;
-  double acc = 0.0, a2 = 0.0, b2 = 0.0, n2 = 0.0;
-  uint4* o = reinterpret_cast<uint4*>(out + (live ? r : 0) * ldo);
-  for (int t0 = 0; t0 < ds; t0 += DC) {
-    __syncthreads();
-    if (vec && t0 + DC <= d) {
-      constexpr int V = 16 / sizeof(T);
-      for (int e = threadIdx.x; e < kThreads * (DC / V); e += kThreads) {
-        const int rr = e / (DC / V), tv = (e - rr * (DC / V)) * V;
-        const long long row = r0 + rr;
-        T v[V];
-        if (row < n) {
-          const uint4 q4 = *reinterpret_cast<const uint4*>(X + row * ldx + t0 + tv);
-          __builtin_memcpy(v, &q4, 16);
-        } else {
-#pragma unroll
-          for (int u = 0; u < V; ++u) v[u] = (T)0;
-        }
-#pragma unroll
-        for (int u = 0; u < V; ++u) xs[(tv + u) * (kThreads + 1) + rr] = v[u];
-      }
-    } else {
-      for (int e = threadIdx.x; e < kThreads * DC; e += kThreads) {
-        const int rr = e / DC, tt = e - rr * DC;
-        const long long row = r0 + rr;
-        xs[tt * (kThreads + 1) + rr] = (row < n && t0 + tt < d) ? X[row * ldx + t0 + tt] : (T)0;
-      }
-    }
-    if (threadIdx.x < DC) cs[threadIdx.x] = t0 + (int)threadIdx.x < d ? c0[t0 + threadIdx.x] : 0.0;
-    __syncthreads();
-    if (live) {
-      unsigned wh[4] = {0u, 0u, 0u, 0u}, wl[4] = {0u, 0u, 0u, 0u};
-#pragma unroll
-      for (int u = 0; u < DC; ++u) {
-        if (t0 + u < d) {
-          const double v = (double)xs[u * (kThreads + 1) + threadIdx.x];
-          const double e = v - cs[u];
-          acc = __fma_rn(e, e, acc);
-          const u16 hb = f32_to_bf16((float)v);
-          const double r1 = v - (double)bf16_to_f32(hb);
-          const u16 lb = f32_to_bf16((float)r1);
-          const double lv = (double)bf16_to_f32(lb);
-          const double rx = r1 - lv;
-          a2 = __fma_rn(lv, lv, a2);
-          b2 = __fma_rn(rx, rx, b2);
-          n2 = __fma_rn(v, v, n2);
-          wh[u >> 1] |= (unsigned)hb << (16 * (u & 1));
-          wl[u >> 1] |= (unsigned)lb << (16 * (u & 1));
-        }
-      }
-      const uint4 h4 = {wh[0], wh[1], wh[2], wh[3]}, l4 = {wl[0], wl[1], wl[2], wl[3]};
-      o[t0 / 8] = h4;
-      o[(ds + t0) / 8] = l4;
-      o[(2 * ds + t0) / 8] = h4;
-    }
-  }
-  if (live) {
-    const uint4 z = {0u, 0u, 0u, 0u};
-    for (long long t0 = 3LL * ds; t0 < ldo; t0 += 8) o[t0 / 8] = z;
-    best[r] = acc;
-    ea[r] = f32_up(sqrt(a2) * (1.0 + 1e-6));
-    eb[r] = f32_up(sqrt(b2) * (1.0 + 1e-6) + 1e-300);
-    en[r] = f32_up(sqrt(n2) * (1.0 + 1e-6));
-    xn[r] = (float)n2;
-  }
-}
-
 // Split-screen certificate: with cst = {max ||c_lo||, max ||c||, max ||c - c_hi - c_lo||} the squared
 // distances of the split model differ from the real ones by at most E = 2(ea·cst0 + eb·cst1 +
 // 1.01·en·cst2) per row; the label is certified when sqrt(lb² - E) > sqrt(ub² + E), and u_out / l_out
@@ -966,23 +885,5 @@ CML_API int cml_kmeans_sum_dd(const double* v, long long n, double* out, double*
   nb = nb < 1 ? 1 : (nb > kSumBlocks ? kSumBlocks : nb);
   hipLaunchKernelGGL(sum_dd_partial_kernel, dim3((unsigned)nb), dim3(kThreads), 0, st, v, n, part);
   hipLaunchKernelGGL(sum_dd_final_kernel, dim3(1), dim3(64), 0, st, part, (int)nb, out);
-  return cml_status();
-}
-
-// to_bf16_split plus best[r] = the exact fold distance of row r to c0 (f64 [d]).
-CML_API int cml_kmeans_to_bf16_split_dist(const void* X, int xf64, long long n, long long ldx, int d, int ds,
-                                          void* out, long long ldo, float* ea, float* eb, float* en, float* xn,
-                                          const double* c0, double* best, void* stream) {
-  if (n <= 0) return 0;
-  if (d <= 0 || ds < d || ldo < 3LL * ds || (ds % 8) || (ldo % 8)) return (int)hipErrorInvalidValue;
-  const dim3 g((unsigned)((n + kThreads - 1) / kThreads));
-  hipStream_t st = (hipStream_t)stream;
-  const bool vec = ((uintptr_t)X % 16 == 0) && ((ldx * (xf64 ? 8 : 4)) % 16 == 0);
-  if (xf64)
-    hipLaunchKernelGGL((to_bf16_split_dist_kernel<double>), g, dim3(kThreads), 0, st, (const double*)X, n, ldx, d, ds,
-                       (u16*)out, ldo, ea, eb, en, xn, c0, best, vec);
-  else
-    hipLaunchKernelGGL((to_bf16_split_dist_kernel<float>), g, dim3(kThreads), 0, st, (const float*)X, n, ldx, d, ds,
-                       (u16*)out, ldo, ea, eb, en, xn, c0, best, vec);
   return cml_status();
 }

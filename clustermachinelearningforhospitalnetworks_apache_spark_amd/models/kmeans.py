@@ -654,13 +654,10 @@ class LloydEngine:
         p = K.plan_assign(1, dp, k)
         return p.rr_ct > 0 and p.kc == p.kp
 
-    def _screen_state(self, c0: Optional[torch.Tensor] = None):
+    def _screen_state(self):
         """The screen's buffers: the bf16 copy of the rows with each row's rounding error (cached on the
-        source tensor while it is unmodified), its f32 norms, bf16 centres, bounds, candidate list. With
-        ``c0`` (one f64 centre) a split copy built here also yields every row's exact fold distance to it
-        in the same read of X (``st.best0``; k-means‖'s first costs)."""
+        source tensor while it is unmodified), its f32 norms, bf16 centres, bounds, candidate list."""
         if self._scr is not None:
-            self._scr.best0 = None
             return self._scr
         n, d, dev = self.n, self.d, self.device
         # split screen when three segments of the row fit one K9r row (d <= 170): x·c to ~2^-16, so the
@@ -671,14 +668,10 @@ class LloydEngine:
         dp = 512 if split else padded_dim(d)
         key = ("split", ds) if split else ("plain", dp)
         ent = getattr(self.x, "_cml_screen", None)
-        best0 = None
         if ent is not None and ent[0] == self.x._version and ent[1] == (n, d) and ent[2] == key:
             parts = ent[3]
         else:
-            if split and c0 is not None and n:
-                parts, best0 = K.to_bf16_split_dist(self.x, d, ds, dp, c0)
-            else:
-                parts = K.to_bf16_split(self.x, d, ds, dp) if split else K.to_bf16_err(self.x, d, dp)
+            parts = K.to_bf16_split(self.x, d, ds, dp) if split else K.to_bf16_err(self.x, d, dp)
             try:
                 self.x._cml_screen = (self.x._version, (n, d), key, parts)
             except (AttributeError, RuntimeError):
@@ -708,7 +701,6 @@ class LloydEngine:
         st.lst = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
         st.cnt = torch.zeros(1, dtype=torch.int32, device=dev)
         st.rechecked = []  # uncertified rows per screened pass, read only when track_prune is set
-        st.best0 = best0
         self._scr = st
         return st
 
@@ -758,18 +750,14 @@ class LloydEngine:
         """_min_dist_idx of the screen: (exact f64 squared distance to the nearest candidate, its index) of
         every local row, candidates in K9r-sized chunks merged in order with strict < (the first index on
         ties, as one exact assignment over the whole list)."""
+        st = self._screen_state()
         n, dev = self.n, self.device
         cands = cands.to(device=dev, dtype=torch.float64)
-        one = int(cands.shape[0]) == 1
-        st = self._screen_state(c0=cands[0] if one else None)
-        if one:  # one candidate: every label is 0, the distance one exact fold
+        if int(cands.shape[0]) == 1:  # one candidate: every label is 0, the distance one exact fold
             lab1 = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
-            if st.best0 is not None:  # computed with the split copy, in its read of X
-                b1, st.best0 = st.best0, None
-            else:
-                b1 = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
-                if n:
-                    K.exact_dist(self.x, cands.contiguous(), lab1, b1)
+            b1 = torch.empty(max(n, 1), dtype=torch.float64, device=dev)
+            if n:
+                K.exact_dist(self.x, cands.contiguous(), lab1, b1)
             return b1[:n], lab1[:n].long()
         best = torch.full((max(n, 1),), math.inf, dtype=torch.float64, device=dev)
         lab = torch.zeros(max(n, 1), dtype=torch.int64, device=dev)

@@ -108,8 +108,6 @@ _native.register_kernel_sigs({
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_to_bf16_split": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp,
                                          c_vp]),
-    "cml_kmeans_to_bf16_split_dist": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_ll, c_vp, c_vp, c_vp,
-                                              c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
@@ -911,21 +909,6 @@ def to_bf16_split(x: torch.Tensor, d: int, ds: int, ldo: int, stream=None):
         x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(d), int(ds), out.data_ptr(), int(ldo),
         ea.data_ptr(), eb.data_ptr(), en.data_ptr(), xn.data_ptr(), _native.stream_ptr(stream)), "kmeans_to_bf16_split")
     return (out[:n] if n else out[:0]), ea, eb, en, xn
-
-
-def to_bf16_split_dist(x: torch.Tensor, d: int, ds: int, ldo: int, c0: torch.Tensor, stream=None):
-    """to_bf16_split and the exact fold distance (exact_dist's bits) of every row to the one centre c0, in
-    one read of X: ((split copy, ||lo||, ||rx||, ||x||, ||x||²), best f64 [n])."""
-    n = int(x.shape[0])
-    out = torch.empty((max(n, 1), ldo), dtype=torch.bfloat16, device=x.device)
-    ea, eb, en, xn = (torch.empty(max(n, 1), dtype=torch.float32, device=x.device) for _ in range(4))
-    best = torch.empty(max(n, 1), dtype=torch.float64, device=x.device)
-    c = c0.reshape(-1).to(device=x.device, dtype=torch.float64).contiguous()
-    _native.check(_native.kernels().cml_kmeans_to_bf16_split_dist(
-        x.data_ptr(), int(x.dtype == torch.float64), n, x.stride(0), int(d), int(ds), out.data_ptr(), int(ldo),
-        ea.data_ptr(), eb.data_ptr(), en.data_ptr(), xn.data_ptr(), c.data_ptr(), best.data_ptr(),
-        _native.stream_ptr(stream)), "kmeans_to_bf16_split_dist")
-    return ((out[:n] if n else out[:0]), ea, eb, en, xn), best
 
 
 def split_centres(C: torch.Tensor, ds: int, cb: torch.Tensor, cn: torch.Tensor) -> torch.Tensor:

@@ -216,21 +216,3 @@ def test_sum_exact_device_correctly_rounded(n):
     dev = K.sum_exact(v.cuda())
     host = K.sum_exact(v)
     assert float(dev) == float(host) == math.fsum(v.tolist())
-
-
-@pytest.mark.parametrize("n,d,dt", [(100_003, 128, torch.float32), (5_000, 130, torch.float64), (777, 7, torch.float32)])
-def test_split_dist_fused_equals_separate(n, d, dt):
-    g = torch.Generator(device="cuda").manual_seed(n)
-    x = (torch.randn(n, d, generator=g, device="cuda", dtype=torch.float64) * 7 + 3).to(dt)
-    ds = (d + 7) // 8 * 8
-    ldo = 512 if 3 * ds <= 512 else 3 * ds
-    c0 = torch.randn(d, generator=g, device="cuda", dtype=torch.float64)
-    (xb, ea, eb, en, xn), best = K.to_bf16_split_dist(x, d, ds, ldo, c0)
-    xb2, ea2, eb2, en2, xn2 = K.to_bf16_split(x, d, ds, ldo)
-    assert torch.equal(xb, xb2)  # the same split copy; the norms agree up to their summation order
-    for a, b in ((ea, ea2), (eb, eb2), (en, en2), (xn, xn2)):
-        torch.testing.assert_close(a[:n], b[:n], rtol=1e-6, atol=1e-30)
-    lab = torch.zeros(n, dtype=torch.int32, device="cuda")
-    b2 = torch.empty(n, dtype=torch.float64, device="cuda")
-    K.exact_dist(x, c0.reshape(1, d), lab, b2)
-    assert torch.equal(best[:n], b2)
