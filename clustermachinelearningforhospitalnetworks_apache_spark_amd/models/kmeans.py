@@ -720,14 +720,18 @@ class LloydEngine:
             return
         C = C.to(device=self.device, dtype=torch.float64).contiguous()
         kp = round_up(kc, 32)
-        st.cb[:kp].zero_()
-        st.cn[:kp].zero_()
-        if st.split:
-            cst = K.split_centres(C, st.ds, st.cb[:kp], st.cn[:kp])
+        if st.split:  # one launch: the layout, the norms, the certificate's constants and max |c|²
+            if getattr(st, "cst", None) is None:
+                st.cst = torch.zeros(3, dtype=torch.float64, device=self.device)
+                st.mc = torch.zeros(1, dtype=torch.float32, device=self.device)
+            K.split_centres_dev(C, st.ds, st.cb[:kp], st.cn[:kp], st.cst, mc=st.mc)
+            cst, mc = st.cst, st.mc
         else:
+            st.cb[:kp].zero_()
+            st.cn[:kp].zero_()
             K.update_centers(None, kc, d, C.clone(), st.cb[:kp], st.dp, kp, st.cn[:kp], None)
             ecmax = ((C - st.cb[:kc, :d].to(torch.float64)) ** 2).sum(1).max().sqrt().reshape(1) * (1.0 + 1e-9)
-        mc = st.cn[:kc].max().reshape(1)
+            mc = st.cn[:kc].max().reshape(1)
         plan = K.plan_assign(n, st.dp, kc)
         K.assign_rr_ext(1, st.xb, n, st.dp, st.cb[:kp], st.cn[:kp], plan, st.xn, lab, None, st.ub, st.lb, mc, st.tau)
         st.cnt.zero_()
