@@ -13,8 +13,9 @@
 //                  feature chunk per workgroup), 64-bit fixed point (order-independent,
 //                  exact), flushed once with integer global adds.
 // K20 tree_route   node_of[t][row] <- left/right child after the level's splits
-// K21 tree_predict per-row traversal of every tree (arrays in LDS), forest mean
-//                  (regression) or summed normalised class distributions (classification)
+// K21 tree_predict per-row traversal of every tree, forest mean (regression) or summed
+//                  normalised class distributions (classification)
+// K21b forest_vote class distribution + thresholded argmax of a classifier transform
 #include "common.h"
 
 namespace {
@@ -288,7 +289,7 @@ __global__ void tree_predict_kernel(const double* __restrict__ X, long long n, l
                                     const int* __restrict__ root, const int* __restrict__ feat,
                                     const double* __restrict__ thr, const int* __restrict__ left,
                                     const int* __restrict__ right, const double* __restrict__ leaf, int S,
-                                    double* __restrict__ out /*[n][S]*/) {
+                                    double div, double* __restrict__ out /*[n][S]*/) {
   for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
     double acc[16];
     for (int s = 0; s < S; ++s) acc[s] = 0.0;
@@ -297,7 +298,34 @@ __global__ void tree_predict_kernel(const double* __restrict__ X, long long n, l
       while (feat[k] >= 0) k = X[r * ld + feat[k]] <= thr[k] ? left[k] : right[k];
       for (int s = 0; s < S; ++s) acc[s] += leaf[(long long)k * S + s];
     }
-    for (int s = 0; s < S; ++s) out[r * S + s] = acc[s];
+    // the forest mean as a true division (correctly rounded, like the host's tensor division)
+    for (int s = 0; s < S; ++s) out[r * S + s] = div == 1.0 ? acc[s] : acc[s] / div;
+  }
+}
+
+// K21b forest vote: per row, the class distribution raw/sum(raw) (uniform 1/S when the sum is not
+// positive) and the prediction argmax(prob / thresholds) (first maximum). Replaces five tensor ops of
+// the transform (row sum, clamp, divide, select, argmax), each a separate launch and, on a session's
+// first tree transform, a separate first-use code-object load.
+__global__ void forest_vote_kernel(const double* __restrict__ raw, long long n, int S,
+                                   const double* __restrict__ thr /* [S] or null */, double* __restrict__ prob,
+                                   double* __restrict__ pred) {
+  for (long long r = (long long)blockIdx.x * blockDim.x + threadIdx.x; r < n; r += (long long)gridDim.x * blockDim.x) {
+    const double* v = raw + r * S;
+    double sum = 0.0;
+    for (int s = 0; s < S; ++s) sum += v[s];
+    int best = 0;
+    double bv = 0.0;
+    for (int s = 0; s < S; ++s) {
+      const double p = sum > 0.0 ? v[s] / sum : 1.0 / (double)S;
+      prob[r * S + s] = p;
+      const double q = thr ? p / fmax(thr[s], 1e-300) : p;
+      if (s == 0 || q > bv) {
+        bv = q;
+        best = s;
+      }
+    }
+    pred[r] = (double)best;
   }
 }
 
@@ -411,9 +439,18 @@ CML_API int cml_tree_route(const void* bins, long long n, int d, int T, int node
 
 CML_API int cml_tree_predict(const double* X, long long n, long long ld, int T, const int* root, const int* feat,
                              const double* thr, const int* left, const int* right, const double* leaf, int S,
-                             double* out, void* stream) {
+                             double div, double* out, void* stream) {
   if (S > 16) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(tree_predict_kernel, dim3(blocks_for(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, X, n, ld,
-                     T, root, feat, thr, left, right, leaf, S, out);
+                     T, root, feat, thr, left, right, leaf, S, div, out);
+  return cml_status();
+}
+
+CML_API int cml_forest_vote(const double* raw, long long n, int S, const double* thr, double* prob, double* pred,
+                            void* stream) {
+  if (S < 1 || S > 16) return (int)hipErrorInvalidValue;
+  if (n <= 0) return 0;
+  hipLaunchKernelGGL(forest_vote_kernel, dim3(blocks_for(n, 256, 8192)), dim3(256), 0, (hipStream_t)stream, raw, n, S,
+                     thr, prob, pred);
   return cml_status();
 }

@@ -201,14 +201,8 @@ class TreeModelMixin:
         kind = "gini"
         raw = TR.predict_forest(self._trees, x, kind, self._num_classes, average=False,
                                 normalize_leaves=self._forest)
-        s = raw.sum(1, keepdim=True)
-        prob = torch.where(s > 0, raw / s.clamp(min=1e-300), torch.full_like(raw, 1.0 / raw.shape[1]))
         thr = self.getOrDefault("thresholds") if self.isDefined("thresholds") else None
-        if thr:
-            t = torch.as_tensor(np.asarray(thr, dtype=np.float64), device=prob.device)
-            pred = torch.argmax(prob / t.clamp(min=1e-300), 1).to(torch.float64)
-        else:
-            pred = torch.argmax(prob, 1).to(torch.float64)
+        prob, pred = TR.forest_vote(raw, thr)
         out = df
         if self.getRawPredictionCol():
             out = _replace_col(out, self.getRawPredictionCol(), ColumnData(raw, None, T.VectorUDT()))

@@ -40,7 +40,9 @@ _native.register_kernel_sigs({
     "cml_tree_best_split": (c_int, [c_vp, c_int, c_int, c_int, c_int, c_vp, c_int, c_vp, c_vp, c_dbl, c_dbl,
                                     c_dbl, c_vp, c_vp]),
     "cml_tree_route": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
-    "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp, c_vp]),
+    "cml_tree_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_dbl, c_vp,
+                                 c_vp]),
+    "cml_forest_vote": (c_int, [c_vp, c_ll, c_int, c_vp, c_vp, c_vp, c_vp]),
 })
 
 
@@ -616,39 +618,68 @@ def predict_forest(trees: List[Node], x: torch.Tensor, kind: str, num_classes: i
     dev = x.device
     n = x.shape[0]
     xx = x.to(torch.float64).contiguous()
-    out = torch.zeros((n, S), dtype=torch.float64, device=dev)
-    if n == 0:
-        return out
     if x.is_cuda and S <= 16:
+        # K21 writes every element and takes the forest mean itself: no tensor op of its own on the device
+        out = torch.empty((n, S), dtype=torch.float64, device=dev)
+        if n == 0:
+            return out
         to = lambda a, dt: torch.as_tensor(np.asarray(a), dtype=dt, device=dev).contiguous()  # noqa: E731
         r, f, th, l, rr, lv = (to(roots, torch.int32), to(feats, torch.int32), to(thrs, torch.float64),
                                to(lefts, torch.int32), to(rights, torch.int32),
                                to(np.asarray(leaves, dtype=np.float64).reshape(-1), torch.float64))
+        div = float(len(trees)) if average and len(trees) > 1 else 1.0
         st = _native.kernels().cml_tree_predict(xx.data_ptr(), n, xx.stride(0), len(trees), r.data_ptr(),
                                                 f.data_ptr(), th.data_ptr(), l.data_ptr(), rr.data_ptr(),
-                                                lv.data_ptr(), S, out.data_ptr(), _native.stream_ptr())
+                                                lv.data_ptr(), S, div, out.data_ptr(), _native.stream_ptr())
         _native.check(st, "tree_predict")
-    else:
-        f = torch.as_tensor(feats, dtype=torch.long, device=dev)
-        th = torch.as_tensor(thrs, dtype=torch.float64, device=dev)
-        l = torch.as_tensor(lefts, dtype=torch.long, device=dev)
-        rr = torch.as_tensor(rights, dtype=torch.long, device=dev)
-        lv = torch.as_tensor(np.asarray(leaves, dtype=np.float64), device=dev)
-        for root in roots:
-            k = torch.full((n,), root, dtype=torch.long, device=dev)
-            for _ in range(64):
-                ff = f[k]
-                inner = ff >= 0
-                if not bool(inner.any()):
-                    break
-                v = xx.gather(1, ff.clamp(min=0).reshape(-1, 1)).reshape(-1)
-                nxt = torch.where(v <= th[k], l[k], rr[k])
-                k = torch.where(inner, nxt, k)
-            out += lv[k]
+        return out
+    out = torch.zeros((n, S), dtype=torch.float64, device=dev)
+    if n == 0:
+        return out
+    f = torch.as_tensor(feats, dtype=torch.long, device=dev)
+    th = torch.as_tensor(thrs, dtype=torch.float64, device=dev)
+    l = torch.as_tensor(lefts, dtype=torch.long, device=dev)
+    rr = torch.as_tensor(rights, dtype=torch.long, device=dev)
+    lv = torch.as_tensor(np.asarray(leaves, dtype=np.float64), device=dev)
+    for root in roots:
+        k = torch.full((n,), root, dtype=torch.long, device=dev)
+        for _ in range(64):
+            ff = f[k]
+            inner = ff >= 0
+            if not bool(inner.any()):
+                break
+            v = xx.gather(1, ff.clamp(min=0).reshape(-1, 1)).reshape(-1)
+            nxt = torch.where(v <= th[k], l[k], rr[k])
+            k = torch.where(inner, nxt, k)
+        out += lv[k]
     if average and len(trees) > 1:
         # true division on every device (a python-scalar divisor becomes a reciprocal multiply on the GPU)
         out /= torch.full((1,), float(len(trees)), dtype=torch.float64, device=dev)
     return out
+
+
+def forest_vote(raw: torch.Tensor, thresholds: Optional[Sequence[float]] = None):
+    """(probability [n, S], prediction [n] f64) of a classifier's summed leaf distributions: raw / row sum
+    (uniform when the sum is not positive), prediction = first argmax of probability / thresholds. One
+    K21b launch on the device (Spark ProbabilisticClassificationModel.transform)."""
+    n, S = raw.shape
+    if raw.is_cuda and S <= 16:
+        rr = raw.to(torch.float64).contiguous()
+        prob = torch.empty_like(rr)
+        pred = torch.empty(n, dtype=torch.float64, device=raw.device)
+        t = None
+        if thresholds:
+            t = torch.as_tensor(np.asarray(thresholds, dtype=np.float64), device=raw.device)
+        st = _native.kernels().cml_forest_vote(rr.data_ptr(), n, S, 0 if t is None else t.data_ptr(),
+                                               prob.data_ptr(), pred.data_ptr(), _native.stream_ptr())
+        _native.check(st, "forest_vote")
+        return prob, pred
+    s = raw.sum(1, keepdim=True)
+    prob = torch.where(s > 0, raw / s.clamp(min=1e-300), torch.full_like(raw, 1.0 / S))
+    if thresholds:
+        t = torch.as_tensor(np.asarray(thresholds, dtype=np.float64), device=prob.device)
+        return prob, torch.argmax(prob / t.clamp(min=1e-300), 1).to(torch.float64)
+    return prob, torch.argmax(prob, 1).to(torch.float64)
 
 
 # ---------------------------------------------------------------------------------------------- boosting

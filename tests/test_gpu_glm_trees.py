@@ -146,3 +146,19 @@ def test_partial_colsum_matches_torch(nb, m):
     got = glm_ops.partial_colsum(part)
     torch.testing.assert_close(got.cpu(), part.cpu().sum(0), rtol=1e-12, atol=1e-12)
     assert torch.equal(got, glm_ops.partial_colsum(part))  # fixed order: bitwise repeatable
+
+
+@pytest.mark.parametrize("S", [2, 3, 7])
+@pytest.mark.parametrize("thr", [None, "set"])
+def test_forest_vote_kernel_matches_torch(S, thr):
+    """K21b (class distribution + thresholded first argmax) against the host rule it replaces, including
+    rows whose leaf counts sum to zero (uniform distribution) and exact ties (first maximum)."""
+    g = torch.Generator().manual_seed(S)
+    n = 5000
+    raw = torch.randint(0, 4, (n, S), generator=g).to(torch.float64)
+    raw[::97] = 0.0
+    t = list(np.linspace(0.3, 0.9, S)) if thr else None
+    pc, yc = TR.forest_vote(raw, t)
+    pg, yg = TR.forest_vote(raw.cuda(), t)
+    assert torch.equal(pg.cpu(), pc)
+    assert torch.equal(yg.cpu(), yc)
