@@ -134,7 +134,7 @@ class SparkSession:
             log.warning("master=%s requested GPUs but none is visible; running on CPU", opts.get("spark.master"))
         self._device = self._comm.device
         self._warmup_s = 0.0
-        if self._device.type == "cuda" and str(opts.get("cml.session.warmup", "true")).lower() not in ("0", "false"):
+        if self._device.type == "cuda" and str(opts.get("cml.session.warmup", os.environ.get("CML_SESSION_WARMUP", "true"))).lower() not in ("0", "false"):
             from ..utils.warmup import warm_device
             try:
                 self._warmup_s = warm_device(self._device, int(float(opts.get("cml.session.poolBytes", 1 << 30))))

@@ -14,6 +14,7 @@ from __future__ import annotations
 
 import time
 
+import numpy as np
 import torch
 
 
@@ -27,8 +28,9 @@ def warm_device(device: torch.device, pool_bytes: int = 1 << 30) -> float:
         del blk
     from ..ops import frame_ops, glm_ops
     n, d = 4096, 4
-    g = torch.Generator(device=device).manual_seed(0)
-    x = torch.randn(n, d, generator=g, device=device, dtype=torch.float64)
+    # host-generated data: a device randn would load torch's distribution kernels (~160 ms on first use)
+    # for a warm-up whose jobs draw their random numbers from the in-tree counter-based generator
+    x = torch.from_numpy(np.random.default_rng(0).standard_normal((n, d))).to(device)
     xi = (x[:, 0] * 100).to(torch.int32)
     valid = x[:, 1] > -3.0
     y = x @ torch.ones(d, dtype=torch.float64, device=device)
@@ -69,8 +71,6 @@ def warm_frames(session) -> float:
     launches (each loads its code object) then happen here and not inside a stream's first batch
     (na.drop ran 12-23 ms cold vs 2-5 ms warm on 4M rows: profiles/r4/dropna_cold_trace.log).
     Tracing is paused so warm-up ranges never show in a job's report."""
-    import numpy as np
-
     from ..sql import types as T
     from ..sql.column import ColumnData, DictColumnData
     from ..sql.dataframe import DataFrame
