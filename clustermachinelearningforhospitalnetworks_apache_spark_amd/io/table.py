@@ -111,9 +111,35 @@ def commit(root: str, add: List[str], remove: List[str], schema: T.StructType, o
     raise RuntimeError("could not commit to table log")
 
 
-def new_data_file(root: str, rank: int) -> str:
+def new_data_file(root: str, rank: int, part: Optional[int] = None) -> str:
     os.makedirs(root, exist_ok=True)
-    return os.path.join(root, f"part-{int(time.time() * 1000)}-r{rank}-{uuid.uuid4().hex[:12]}.parquet")
+    tail = "" if part is None else f"-c{part:03d}"
+    return os.path.join(root, f"part-{int(time.time() * 1000)}-r{rank}-{uuid.uuid4().hex[:12]}{tail}.parquet")
+
+
+def _part_rows() -> int:
+    return max(1, int(os.environ.get("CML_TABLE_PART_ROWS", 1 << 20)))
+
+
+def _write_parts(table, root: str, rank: int) -> List[str]:
+    """Write one rank's Arrow table as consecutive row slices of ~CML_TABLE_PART_ROWS rows (default
+    1 Mi), one Parquet file each, written by parallel threads (Arrow's writer releases the GIL) — a
+    Spark task writes one part file per partition the same way. The paths come back in row order, the
+    order the commit lists them and a snapshot reads them back."""
+    import pyarrow.parquet as pq
+    n = table.num_rows
+    # the split depends on the row count only (row ids, hence seeded row sampling, follow the files)
+    parts = max(1, min(-(-n // _part_rows()), 8))
+    if parts == 1:
+        path = new_data_file(root, rank)
+        pq.write_table(table, path)
+        return [path]
+    step = -(-n // parts)
+    paths = [new_data_file(root, rank, i) for i in range(parts)]
+    from concurrent.futures import ThreadPoolExecutor
+    with ThreadPoolExecutor(min(parts, os.cpu_count() or 1), thread_name_prefix="cml-part-write") as ex:
+        list(ex.map(lambda i: pq.write_table(table.slice(i * step, step), paths[i]), range(parts)))
+    return paths
 
 
 def write_frame(df, root: str, mode: str, operation: str = "WRITE", txn: Optional[dict] = None) -> Optional[int]:
@@ -125,11 +151,8 @@ def write_frame(df, root: str, mode: str, operation: str = "WRITE", txn: Optiona
         raise FileExistsError(f"table at {root} already exists (mode=error)")
     if mode == "ignore" and exists(root):
         return None
-    path = new_data_file(root, comm.rank) if df._nrows > 0 else None
-    if path:
-        pq.write_table(frame_to_arrow(df), path)
-    paths = comm.allgather_object(path)
-    added = [p for p in paths if p]
+    mine = _write_parts(frame_to_arrow(df), root, comm.rank) if df._nrows > 0 else []
+    added = [p for ps in comm.allgather_object(mine) for p in ps]
     version = None
     if comm.is_root:
         removed = snapshot(root)[0] if mode == "overwrite" else []
@@ -146,18 +169,17 @@ class PendingWrite:
     def __init__(self, df, root: str, mode: str, operation: str, txn: Optional[dict]):
         import threading
 
-        import pyarrow.parquet as pq
         from .arrow import frame_to_arrow
         self.df, self.root, self.mode, self.operation, self.txn = df, root, mode, operation, txn
-        self.path = new_data_file(root, df._comm.rank) if df._nrows > 0 else None
+        self.paths: List[str] = []
         self.error: Optional[BaseException] = None
         self.thread = None
-        if self.path:
+        if df._nrows > 0:
             table = frame_to_arrow(df)  # device -> host on the calling thread
 
             def run():
                 try:
-                    pq.write_table(table, self.path)
+                    self.paths = _write_parts(table, root, df._comm.rank)
                 except BaseException as e:  # noqa: BLE001 — re-raised in finish()
                     self.error = e
             self.thread = threading.Thread(target=run, name="cml-table-write", daemon=True)
@@ -170,8 +192,7 @@ class PendingWrite:
         failed = comm.allgather_object(self.error is not None)
         if any(failed):
             raise self.error if self.error is not None else RuntimeError("table write failed on another rank")
-        paths = comm.allgather_object(self.path)
-        added = [p for p in paths if p]
+        added = [p for ps in comm.allgather_object(self.paths) for p in ps]
         version = None
         if comm.is_root:
             removed = snapshot(self.root)[0] if self.mode == "overwrite" else []

@@ -159,3 +159,22 @@ def test_stream_background_thread_process_all_available(spark, tmp_path):
     assert spark.table("mem").count() == 100
     q.stop()
     assert not q.isActive
+
+
+def test_table_write_in_parallel_parts_keeps_row_order(spark, tmp_path, monkeypatch):
+    """A commit of more rows than CML_TABLE_PART_ROWS writes consecutive row slices as separate part
+    files (parallel writer threads); the commit lists them in row order, so the table reads back in the
+    frame's order, from the synchronous and the streaming (background) writer alike."""
+    monkeypatch.setenv("CML_TABLE_PART_ROWS", "7")
+    pdf = hospital_frame(40)
+    df = spark.createDataFrame(pdf)
+    df.write.saveAsTable("tp")
+    root = spark.catalog._table_path("tp")
+    files, _, commits = tbl.snapshot(root)
+    assert len(commits[0]["add"]) == 6 and all(f.endswith(f"-c{i:03d}.parquet") for i, f in enumerate(files))
+    back = spark.table("tp").toPandas()
+    assert back.length_of_stay.tolist() == pdf.length_of_stay.tolist()
+    pend = tbl.write_frame_async(df, root, "append", "STREAMING UPDATE", {"appId": "q", "version": 0})
+    assert pend.finish() == 1
+    back = spark.table("tp").toPandas()
+    assert back.length_of_stay.tolist() == pdf.length_of_stay.tolist() * 2
