@@ -196,6 +196,8 @@ def read_parquet_files(session, paths: Sequence[str], schema: Optional[T.StructT
     import pyarrow as pa
     import pyarrow.parquet as pq
     from ..sql.builder import shard_range
+    from .csv import cap_arrow_threads
+    cap_arrow_threads()
     comm = session._comm
     W, rank = comm.world_size, comm.rank
     paths = list(paths)

@@ -116,6 +116,26 @@ def host_threads() -> int:
     return max(1, min(16, n))
 
 
+_ARROW_CAPPED = False
+
+
+def cap_arrow_threads() -> None:
+    """Size Arrow's CPU and IO thread pools to this process's CPU share (``host_threads``) once. Arrow
+    sizes them from the machine's CPU count; on a GPU box that is many times the process's share, and
+    a Parquet write that spreads its compression over all of them exhausts the cgroup's CPU quota
+    and stalls every thread of the process, the GPU-feeding one included."""
+    global _ARROW_CAPPED
+    if _ARROW_CAPPED:
+        return
+    import pyarrow as pa
+    n = host_threads()
+    if pa.cpu_count() > n:
+        pa.set_cpu_count(n)
+    if pa.io_thread_count() > n:
+        pa.set_io_thread_count(n)
+    _ARROW_CAPPED = True
+
+
 def _dict_run(lib, buf, trip, valid_u8, n, quote, nthreads):
     h = lib.cml_dict_build(buf, trip.ctypes.data, valid_u8.ctypes.data, n, quote.encode(), nthreads)
     try:

@@ -127,6 +127,8 @@ def _write_parts(table, root: str, rank: int) -> List[str]:
     Spark task writes one part file per partition the same way. The paths come back in row order, the
     order the commit lists them and a snapshot reads them back."""
     import pyarrow.parquet as pq
+    from .csv import cap_arrow_threads
+    cap_arrow_threads()
     n = table.num_rows
     # the split depends on the row count only (row ids, hence seeded row sampling, follow the files)
     parts = max(1, min(-(-n // _part_rows()), 8))
