@@ -9,7 +9,7 @@ import hospital_resource_prediction as h
 h.synth_uploads('/tmp/wfsrc/hospitals/incoming', n_files=4, rows=1000000)
 " || exit 1
 for i in 1 2 3 4; do
-  w=$(( i % 2 ))
+  w=$(( i == 4 ? 0 : 1 ))
   rm -rf /tmp/wf$i; mkdir -p /tmp/wf$i; cp -r /tmp/wfsrc/hospitals /tmp/wf$i/
   t0=$(date +%s.%N)
   CML_SESSION_WARMUP=$w timeout -k 10 300 python examples/hospital_resource_prediction.py --master mi355x --out /tmp/wf$i --trace > $OUT/wf_$i.log 2>&1 || { tail -20 $OUT/wf_$i.log; exit 1; }
