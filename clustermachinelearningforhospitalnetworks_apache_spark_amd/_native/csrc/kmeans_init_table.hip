@@ -81,7 +81,75 @@ __global__ __launch_bounds__(kTabThreads) void init_table_kernel(const double* _
   }
 }
 
+// Distinct candidate rows in ascending lexicographic order (models/kmeans.py _init_finish; torch.unique(dim=0)
+// with return_inverse replaced: that sorts with a row comparator and runs ~10 small kernels around a host
+// read of the count). m is a few thousand at most, so pairwise row comparisons — nearly all decided by the
+// first column — are cheap: one block per row.
+//   pass 1: dup[i] = some j < i has the same values (==: -0 equals 0, like the comparator's order)
+//   pass 2: rank[i] = #{j : !dup[j], row j <lex row i} — equal rows get the same rank, the distinct rows
+//           a permutation of 0..u-1 — so inverse = rank, uniq[rank[i]] = row i for !dup[i], u = max rank + 1
+__device__ __forceinline__ int lex_cmp(const double* __restrict__ a, const double* __restrict__ b, int d) {
+  for (int t = 0; t < d; ++t) {
+    if (a[t] < b[t]) return -1;
+    if (a[t] > b[t]) return 1;
+  }
+  return 0;
+}
+
+__device__ __forceinline__ int block_sum(int v, int* red) {
+  red[threadIdx.x] = v;
+  __syncthreads();
+  for (int s = kTabThreads / 2; s > 0; s >>= 1) {
+    if (threadIdx.x < s) red[threadIdx.x] += red[threadIdx.x + s];
+    __syncthreads();
+  }
+  const int r = red[0];
+  __syncthreads();
+  return r;
+}
+
+__global__ __launch_bounds__(kTabThreads) void rows_dup_kernel(const double* __restrict__ P, int m, int d,
+                                                               int* __restrict__ dup) {
+  __shared__ int red[kTabThreads];
+  const int i = blockIdx.x;
+  const double* p = P + (long long)i * d;
+  int hit = 0;
+  for (int j = threadIdx.x; j < i && !hit; j += kTabThreads) hit = lex_cmp(P + (long long)j * d, p, d) == 0;
+  const int any = block_sum(hit, red);
+  if (threadIdx.x == 0) dup[i] = any > 0;
+}
+
+__global__ __launch_bounds__(kTabThreads) void rows_rank_kernel(const double* __restrict__ P, int m, int d,
+                                                                const int* __restrict__ dup, long long* __restrict__ inv,
+                                                                double* __restrict__ uniq, int* __restrict__ count) {
+  __shared__ int red[kTabThreads];
+  const int i = blockIdx.x;
+  const double* p = P + (long long)i * d;
+  int less = 0;
+  for (int j = threadIdx.x; j < m; j += kTabThreads)
+    if (!dup[j] && lex_cmp(P + (long long)j * d, p, d) < 0) ++less;
+  const int r = block_sum(less, red);
+  if (threadIdx.x == 0) {
+    inv[i] = r;
+    if (!dup[i]) atomicMax(count, r + 1);
+  }
+  if (!dup[i])
+    for (int t = threadIdx.x; t < d; t += kTabThreads) uniq[(long long)r * d + t] = p[t];
+}
+
 }  // namespace
+
+// P f64 [m, d] (contiguous); dup int32 [m] workspace; inv int64 [m]; uniq f64 [m, d] (first *count rows
+// written); count int32 [1], zeroed by the caller.
+CML_API int cml_kmeans_unique_rows(const double* P, int m, int d, int* dup, long long* inv, double* uniq, int* count,
+                                   void* stream) {
+  if (m <= 0) return 0;
+  if (d <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(rows_dup_kernel, dim3((unsigned)m), dim3(kTabThreads), 0, (hipStream_t)stream, P, m, d, dup);
+  hipLaunchKernelGGL(rows_rank_kernel, dim3((unsigned)m), dim3(kTabThreads), 0, (hipStream_t)stream, P, m, d, dup, inv,
+                     uniq, count);
+  return cml_status();
+}
 
 // P f64 [mp, d], Y f64 [m, d] (m <= 1024); tab_v f32 / tab_j int32 [mp, m]; pn32 f32 [mp].
 CML_API int cml_kmeans_init_table(const double* P, int mp, const double* Y, int m, int d, float* tab_v, int* tab_j,

@@ -1751,7 +1751,7 @@ class LloydEngine:
         k = self.k
         cand = torch.cat(centers, 0)
         # distinct candidates in sorted-row order (np.unique's order; identical on every device)
-        uniq, inverse = torch.unique(cand, dim=0, return_inverse=True)
+        uniq, inverse = K.unique_rows(cand) if cand.is_cuda else torch.unique(cand, dim=0, return_inverse=True)
         if uniq.shape[0] <= k:
             out = uniq
         else:

@@ -111,6 +111,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_unique_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_tighten": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
@@ -766,6 +767,24 @@ def init_classify(cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor, pn: 
         cost.data_ptr(), near.data_ptr(), xn.data_ptr(), pn.data_ptr(), tab_v.data_ptr(), m, float(tau), int(n),
         int(lmax), list_a.data_ptr(), cnt_a.data_ptr(), list_b.data_ptr(), cnt_b.data_ptr(),
         _native.stream_ptr(stream)), "kmeans_init_classify")
+
+
+def unique_rows(P: torch.Tensor):
+    """``torch.unique(P, dim=0, return_inverse=True)`` for a device f64 [m, d] matrix in two launches
+    (kmeans_init_table.hip: pairwise row comparisons, one block per row) and one host read of the distinct
+    count. Same sorted order and inverse as torch's; host tensors fall back to torch."""
+    if not P.is_cuda or P.dim() != 2 or P.shape[0] == 0:
+        return torch.unique(P, dim=0, return_inverse=True)
+    P = P.to(torch.float64).contiguous()
+    m, d = int(P.shape[0]), int(P.shape[1])
+    dup = torch.empty(m, dtype=torch.int32, device=P.device)
+    inv = torch.empty(m, dtype=torch.int64, device=P.device)
+    uniq = torch.empty((m, d), dtype=torch.float64, device=P.device)
+    count = torch.zeros(1, dtype=torch.int32, device=P.device)
+    _native.check(_native.kernels().cml_kmeans_unique_rows(P.data_ptr(), m, d, dup.data_ptr(), inv.data_ptr(),
+                                                           uniq.data_ptr(), count.data_ptr(), _native.stream_ptr()),
+                  "kmeans_unique_rows")
+    return uniq[: int(count.item())], inv
 
 
 def init_table(P: torch.Tensor, Y: torch.Tensor, stream=None):

@@ -223,3 +223,20 @@ def test_init_table_kernel(mp, m, d):
     dj = D.gather(1, tab_j.long())
     assert bool((tab_v.double() <= dj).all()) and bool((tab_v.double() >= dj * (1 - 2e-6) - 1e-30).all())
     assert bool((pn32.double() >= (P * P).sum(1)).all())
+
+
+@pytest.mark.parametrize("m,d", [(1, 3), (37, 1), (600, 256), (2049, 40)])
+def test_unique_rows_kernel_matches_torch_unique(m, d):
+    """The distinct-candidate kernels against torch.unique(dim=0, return_inverse=True) on the host: the same
+    lexicographically sorted distinct rows and the same inverse, with exact duplicates, rows equal in their
+    first columns only, and integer-valued ties."""
+    g = torch.Generator().manual_seed(m + d)
+    P = torch.randint(-3, 4, (m, d), generator=g).to(torch.float64)
+    if m > 10:
+        P[1::7] = P[0]                     # exact duplicates of one row
+        P[2::5, : d // 2] = P[3, : d // 2]  # shared prefixes
+        P[m // 2:] += torch.rand(m - m // 2, d, generator=g, dtype=torch.float64)
+    want_u, want_i = torch.unique(P, dim=0, return_inverse=True)
+    got_u, got_i = K.unique_rows(P.cuda())
+    assert torch.equal(got_u.cpu(), want_u)
+    assert torch.equal(got_i.cpu(), want_i)
