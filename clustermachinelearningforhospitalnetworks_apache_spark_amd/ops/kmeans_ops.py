@@ -772,8 +772,9 @@ def init_classify(cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor, pn: 
 def unique_rows(P: torch.Tensor):
     """``torch.unique(P, dim=0, return_inverse=True)`` for a device f64 [m, d] matrix in two launches
     (kmeans_init_table.hip: pairwise row comparisons, one block per row) and one host read of the distinct
-    count. Same sorted order and inverse as torch's; host tensors fall back to torch."""
-    if not P.is_cuda or P.dim() != 2 or P.shape[0] == 0:
+    count. Same sorted order and inverse as torch's; host tensors, and more than 8192 rows (the pairwise
+    passes are O(m²)), fall back to torch."""
+    if not P.is_cuda or P.dim() != 2 or P.shape[0] == 0 or P.shape[0] > 8192:
         return torch.unique(P, dim=0, return_inverse=True)
     P = P.to(torch.float64).contiguous()
     m, d = int(P.shape[0]), int(P.shape[1])
