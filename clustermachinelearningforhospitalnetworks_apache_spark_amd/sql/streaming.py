@@ -635,9 +635,16 @@ class StreamingQuery:
             from ..io import table as tbl
             root = self._session.catalog._table_path(self._table)
             if tbl.committed_txn(root, self.id) < bid:
-                # the Parquet write runs in the background while foreachBatch trains on the batch
-                pending = tbl.write_frame_async(df, root, "overwrite" if complete else "append",
-                                                operation="STREAMING UPDATE", txn={"appId": self.id, "version": bid})
+                mode = "overwrite" if complete else "append"
+                txn = {"appId": self.id, "version": bid}
+                # The sink write runs before foreachBatch (parallel part files). CML_SINK_ASYNC=1 overlaps it
+                # with foreachBatch instead: the same batch time on the reference workflow, but the writer
+                # threads then slowed the user's function 1-5x run to run (profiles/r4/workflow/)
+                if os.environ.get("CML_SINK_ASYNC", "0") == "1":
+                    pending = tbl.write_frame_async(df, root, mode, operation="STREAMING UPDATE", txn=txn)
+                else:
+                    with trace("stream.sink_write"):
+                        tbl.write_frame(df, root, mode, "STREAMING UPDATE", txn)
         elif self._path is not None or (w._format not in (None, "console", "memory", "delta", "noop")):
             if self._path is None:
                 raise ValueError("file sink needs a path")
