@@ -132,9 +132,11 @@ class KMeans(Estimator):
         model = KMeansModel(centers)
         self._copyValues(model)
         # trainingCost is the last iteration's cost (Spark computes it while training: here from the f64
-        # sums and norms the engine holds, no pass over X); clusterSizes is lazy as in Spark's
-        # ClusteringSummary — counted on first read from one pruned assign against the final centres
-        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(), eng.cluster_sizes))
+        # sums and norms the engine holds, no pass over X); clusterSizes: one pruned assign against the
+        # final centres, its counts and their all-reduce are enqueued here on every rank (no host read),
+        # so reading the summary later is no collective and the engine is released when fit returns
+        sizes = eng.cluster_sizes_async()
+        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(), sizes))
         return model
 
 
@@ -264,8 +266,8 @@ class KMeansModel(Model):
 
 class KMeansSummary:
     """Spark's KMeansSummary. ``clusterSizes`` may be given as a zero-argument callable: it is then
-    evaluated on first read (Spark's lazy val) — a collective on a multi-rank session, so every rank
-    reads it (SPMD), as every rank calls ``fit``."""
+    evaluated on first read (Spark's lazy val). KMeans.fit passes the reader of counts whose all-reduce
+    every rank already enqueued, so any subset of ranks may read it."""
 
     def __init__(self, model, df, k, num_iter, cost, sizes):
         self._model = model

@@ -17,7 +17,7 @@ import torch
 
 from ..ops import glm_ops
 from ..sql import types as T
-from ..sql.column import ColumnData
+from ..sql.column import ColumnData, NanCheckedColumnData
 from .base import Estimator, Model, Transformer
 from .linalg import DenseVector
 from .param import NO_DEFAULT
@@ -60,14 +60,15 @@ class VectorAssembler(Transformer):
                 and cds[0].values.dtype == dtype and cds[0].values.is_contiguous() and hi != "skip"):
             # one dense vector input already in the target dtype: the assembled matrix IS the input
             # (no 2x HBM footprint for 100+ GB shards); only the invalid-value check reads it
-            x = cds[0].values
+            # (an input whose own deferred check is pending hands it on under "error"; "keep" reads it)
+            x = cds[0]._vals() if hi == "error" else cds[0].values
             out = ColumnData(x, None, T.VectorUDT())
             if hi == "error" and df._nrows and x.is_floating_point():
                 # Spark raises handleInvalid="error" when the assembled rows are consumed (its transform
                 # is lazy); the check is deferred to the first consumer (DataFrame._feature_matrix), and
                 # a consumer whose own pass over the rows already exposes a NaN takes it over for free
                 # (StandardScaler.fit: the moments) — no extra read of a 100+ GB matrix here
-                out.nan_pending = _NAN_MSG
+                out = NanCheckedColumnData(x, None, T.VectorUDT(), getattr(cds[0], "nan_pending", None) or _NAN_MSG)
             return self._named(df, _replace_col(df, self.getOutputCol(), out))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags

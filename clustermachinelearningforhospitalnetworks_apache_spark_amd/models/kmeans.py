@@ -1438,7 +1438,10 @@ class LloydEngine:
     def fit(self, max_iter: int, tol: float, start_iter: int = 0, on_iter=None) -> int:
         """Lloyd iterations until every centre moves <= tol or max_iter. ``start_iter`` resumes a
         checkpointed fit; ``on_iter(it)`` runs after each iteration (checkpoint hook)."""
-        if tol > 0 and self._pdev and on_iter is None and os.environ.get("CML_KMEANS_LAGGED_TOL", "1") != "0":
+        # (a refresh interval re-accumulates from counting-sort ranks that a frozen step does not rebuild:
+        # such fits take the synchronous loop — ADVICE r4)
+        if (tol > 0 and self._pdev and on_iter is None and not self.refresh_interval
+                and os.environ.get("CML_KMEANS_LAGGED_TOL", "1") != "0"):
             return self._fit_lagged(max_iter, tol, start_iter)
         it = start_iter
         while it < max_iter:
@@ -1537,12 +1540,29 @@ class LloydEngine:
 
     def cluster_sizes(self) -> List[int]:
         """Global row count of every cluster under the final centres (a collective)."""
-        if self.n:
-            sizes = torch.bincount(self.final_labels().long(), minlength=self.k).to(torch.float64)
+        return self.cluster_sizes_async()()
+
+    def cluster_sizes_async(self):
+        """Enqueue the final-centre counts of every cluster and their all-reduce (no host read) and return
+        a zero-argument reader of the result. Every rank calls this together (at the end of ``fit``);
+        the reader itself is no collective — one rank alone may read it — and it holds only the k-long
+        count buffer, not the engine (a lazy collective deadlocked ``if rank == 0: print(
+        summary.clusterSizes)`` and kept every per-row buffer of the fit alive)."""
+        k, n = self.k, self.n
+        if n and self.device.type == "cuda":
+            lab = self.final_labels()
+            cnt = torch.zeros(k, dtype=torch.int32, device=self.device)
+            K.int_hist(lab.to(torch.int32).contiguous(), n, k, cnt)  # integer counts: no bincount host sync
+            sizes = cnt.to(torch.int64)
+        elif n:
+            sizes = torch.bincount(self.final_labels().long(), minlength=k).to(torch.int64)
         else:
-            sizes = torch.zeros(self.k, dtype=torch.float64, device=self.device)
-        self.comm.allreduce_(sizes)
-        return [int(v) for v in sizes.cpu().tolist()]
+            sizes = torch.zeros(k, dtype=torch.int64, device=self.device)
+        h = self.comm.allreduce_async(sizes)
+
+        def read() -> List[int]:
+            return [int(v) for v in h.wait().cpu().tolist()]
+        return read
 
     def assign(self, centers: Optional[torch.Tensor] = None):
         """(labels, squared distance) of every local row against `centers` (default: current)."""
@@ -1680,6 +1700,10 @@ class LloydEngine:
         return self._init_finish(seed, centers, costs, nearest, as_device=False)
 
     def _init_kmeans_parallel_gpu(self, seed: int, steps: int, as_device: bool):
+        with trace("kinit.gpu"):
+            return self._init_kmeans_parallel_gpu_body(seed, steps, as_device)
+
+    def _init_kmeans_parallel_gpu_body(self, seed: int, steps: int, as_device: bool):
         k, n, d, dev, comm = self.k, self.n, self.d, self.device, self.comm
         ids = self.row_ids()
         ids64 = ids if ids.dtype == torch.int64 and ids.is_contiguous() else ids.to(torch.int64).contiguous()
@@ -1704,6 +1728,8 @@ class LloydEngine:
         cap = min(max(n, 1), max(4096, 8 * k))
         out = torch.empty(cap, dtype=torch.int32, device=dev)
         for step in range(steps):
+            tr = trace(f"kinit.round{step}")
+            tr.__enter__()
             # Σcost over every rank and the rate 2k / Σcost stay on the device (the sample kernel forms it)
             scale = two_k.clone()
             if n:
@@ -1730,6 +1756,7 @@ class LloydEngine:
             new = self._rows_f64(chosen) if m else torch.zeros((0, d), dtype=torch.float64, device=dev)
             new = comm.allgather_sized(new, counts)
             if new.shape[0] == 0:
+                tr.__exit__(None, None, None)
                 continue
             centers.append(new)
             # once most rows sit near a candidate, only the new candidates close to a row's nearest one
@@ -1744,7 +1771,9 @@ class LloydEngine:
                     ncand + (first if step == 0 else 0)):
                 self._init_candidate_pass(rest, costs, nearest, ncand + (first if step == 0 else 0))
             ncand += new.shape[0]
-        return self._init_finish(seed, centers, costs, nearest, as_device=as_device)
+            tr.__exit__(None, None, None)
+        with trace("kinit.finish"):
+            return self._init_finish(seed, centers, costs, nearest, as_device=as_device)
 
     def _init_finish(self, seed: int, centers: list, costs: torch.Tensor, nearest: torch.Tensor, as_device: bool):
         """Distinct candidates, their weights (rows per candidate, all-reduced) and the local k-means."""

@@ -46,33 +46,83 @@ class ColumnData:
             return np.ones(n, dtype=bool)
         return torch.ones(n, dtype=torch.bool, device=self.values.device)
 
+    def _vals(self):
+        """The values without running a deferred check (NanCheckedColumnData overrides this)."""
+        return self.values
+
     def take(self, idx) -> "ColumnData":
         """Row subset by index tensor (device) / array."""
         if self.is_host:
             ii = idx.cpu().numpy() if isinstance(idx, torch.Tensor) else np.asarray(idx)
             return ColumnData(self.values[ii], None if self.valid is None else self.valid[ii], self.dtype,
                               None if self.codes is None else self.codes[ii])
-        ti = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=self.values.device)
-        ti = ti.to(self.values.device)
-        return self._keep_checks(ColumnData(self.values[ti], None if self.valid is None else self.valid[ti],
-                                            self.dtype))
+        v = self._vals()
+        ti = idx if isinstance(idx, torch.Tensor) else torch.as_tensor(idx, device=v.device)
+        ti = ti.to(v.device)
+        return self._keep_checks(ColumnData(v[ti], None if self.valid is None else self.valid[ti], self.dtype))
 
     def mask(self, m) -> "ColumnData":
         if self.is_host:
             mm = m.cpu().numpy() if isinstance(m, torch.Tensor) else np.asarray(m, dtype=bool)
             return ColumnData(self.values[mm], None if self.valid is None else self.valid[mm], self.dtype,
                               None if self.codes is None else self.codes[mm])
-        mm = m if isinstance(m, torch.Tensor) else torch.as_tensor(m, device=self.values.device)
-        mm = mm.to(self.values.device)
-        return self._keep_checks(ColumnData(self.values[mm], None if self.valid is None else self.valid[mm],
-                                            self.dtype))
+        v = self._vals()
+        mm = m if isinstance(m, torch.Tensor) else torch.as_tensor(m, device=v.device)
+        mm = mm.to(v.device)
+        return self._keep_checks(ColumnData(v[mm], None if self.valid is None else self.valid[mm], self.dtype))
 
     def _keep_checks(self, out: "ColumnData") -> "ColumnData":
         """A row subset inherits a deferred NaN check (VectorAssembler handleInvalid="error")."""
         pend = getattr(self, "nan_pending", None)
         if pend:
-            out.nan_pending = pend
+            return NanCheckedColumnData(out.values, out.valid, out.dtype, pend)
         return out
+
+
+class NanCheckedColumnData(ColumnData):
+    """A vector column whose handleInvalid="error" NaN check is deferred to its first reader (Spark's
+    VectorAssembler raises when the assembled rows are consumed). ``values`` runs the check
+    on this rank's rows before handing them out — any consumer (Binarizer, a second VectorAssembler,
+    collect / show / write) raises on a NaN row. ``DataFrame._feature_matrix`` runs the rank-agreed form
+    first (fits are collectives), and a consumer whose own pass exposes NaNs (StandardScaler's moments)
+    takes the check over through ``_vals()`` and clears it."""
+
+    def __init__(self, values, valid, dtype, msg: str):
+        self._raw = values
+        self.valid = valid
+        self.dtype = dtype
+        self.codes = None
+        self.nan_pending = msg
+
+    def _vals(self):
+        return self._raw
+
+    @property
+    def is_host(self) -> bool:
+        return False
+
+    def __len__(self):
+        return int(self._raw.shape[0])
+
+    @property
+    def values(self):
+        if self.nan_pending:
+            x = self._raw
+            bad = False
+            if x.numel():
+                if x.is_cuda:
+                    from ..ops import frame_ops
+                    bad = bool(frame_ops.has_nan(x))
+                else:
+                    bad = bool(torch.isnan(x).any().item())
+            if bad:
+                raise ValueError(self.nan_pending)
+            self.nan_pending = None
+        return self._raw
+
+    @values.setter
+    def values(self, v):
+        self._raw = v
 
 
 class LazyColumnData(ColumnData):

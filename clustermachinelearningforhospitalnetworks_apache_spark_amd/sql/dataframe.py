@@ -675,7 +675,7 @@ class DataFrame(DataFrameMoreMixin):
         if not defer_nan_check and getattr(cd, "nan_pending", None):
             self._run_nan_check(col)
             cd.nan_pending = None
-        return cd.values
+        return cd._vals()
 
     def _pending_nan_check(self, col: str):
         return getattr(self._cols[col], "nan_pending", None)
@@ -686,7 +686,7 @@ class DataFrame(DataFrameMoreMixin):
         msg = getattr(cd, "nan_pending", None)
         if not msg:
             return
-        x = cd.values
+        x = cd._vals()
         if not x.numel():
             bad = False
         elif x.is_cuda:

@@ -28,7 +28,7 @@ def test_clean_column_passes_and_aliases():
     KMeans(k=3, seed=1, maxIter=3).fit(out.withColumnRenamed("f", "features"))
 
 
-@pytest.mark.parametrize("consumer", ["scaler", "kmeans", "split"])
+@pytest.mark.parametrize("consumer", ["scaler", "kmeans", "split", "binarizer", "collect", "assembler", "topandas"])
 def test_nan_raises_at_the_consumer(consumer):
     df = _frame(nan_row=1234)
     out = VectorAssembler(inputCols=["raw"], outputCol="features").transform(df)  # no raise yet
@@ -37,7 +37,16 @@ def test_nan_raises_at_the_consumer(consumer):
             StandardScaler(inputCol="features", outputCol="s").fit(out)
         elif consumer == "kmeans":
             KMeans(k=3, seed=1, maxIter=3).fit(out)
+        elif consumer == "binarizer":  # readers of the vector values, not only fits, raise
+            from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import Binarizer
+            Binarizer(threshold=0.0, inputCol="features", outputCol="b").transform(out).collect()
+        elif consumer == "collect":
+            out.select("features").collect()
+        elif consumer == "assembler":
+            VectorAssembler(inputCols=["features"], outputCol="g", handleInvalid="keep").transform(out).collect()
+        elif consumer == "topandas":
+            out.toPandas()
         else:
             a, b = out.randomSplit([0.5, 0.5], seed=3)
-            part = a if bool(torch.isnan(a._cols["features"].values).any()) else b
+            part = a if bool(torch.isnan(a._cols["features"]._vals()).any()) else b
             KMeans(k=3, seed=1, maxIter=3).fit(part)
