@@ -127,7 +127,7 @@ def _write_parts(table, root: str, rank: int) -> List[str]:
     Spark task writes one part file per partition the same way. The paths come back in row order, the
     order the commit lists them and a snapshot reads them back."""
     import pyarrow.parquet as pq
-    from .csv import cap_arrow_threads
+    from .csv import cap_arrow_threads, host_threads
     cap_arrow_threads()
     n = table.num_rows
     # the split depends on the row count only (row ids, hence seeded row sampling, follow the files)
@@ -139,7 +139,7 @@ def _write_parts(table, root: str, rank: int) -> List[str]:
     step = -(-n // parts)
     paths = [new_data_file(root, rank, i) for i in range(parts)]
     from concurrent.futures import ThreadPoolExecutor
-    with ThreadPoolExecutor(min(parts, os.cpu_count() or 1), thread_name_prefix="cml-part-write") as ex:
+    with ThreadPoolExecutor(min(parts, host_threads()), thread_name_prefix="cml-part-write") as ex:
         list(ex.map(lambda i: pq.write_table(table.slice(i * step, step), paths[i]), range(parts)))
     return paths
 

@@ -15,6 +15,7 @@ occupancy of 387 becomes 388).
 """
 from __future__ import annotations
 
+import os
 from typing import List, Optional
 
 import numpy as np
@@ -208,9 +209,11 @@ class KMeansModel(Model):
             return int((1.0 - self._centers @ v / nv).argmin())
         return int(((self._centers - v) ** 2).sum(1).argmin())
 
-    def _assign(self, df):
+    def _assign(self, df, want_dist: bool = True):
         """(labels, distance) per local row: squared euclidean, or 1 - cos for distanceMeasure="cosine"
-        (unit rows against the unit centres: ||x - c||² / 2)."""
+        (unit rows against the unit centres: ||x - c||² / 2). f32/f64 device rows (the reference's Double
+        features) are assigned on the MFMA screen with the exact path's labels and distances
+        (LloydEngine.screen_assign); ``want_dist=False`` skips the distances where only labels are read."""
         x = df._feature_matrix(self.getFeaturesCol())
         if not x.is_cuda and df._device.type == "cuda" and not self._cosine():
             # out-of-core column: the streamed MFMA assign (models/kmeans.py _assign_all)
@@ -228,6 +231,12 @@ class KMeansModel(Model):
             dist = dist.to(torch.float64)
             return lab.long(), (dist / 2.0 if cos else dist)
         from ..ops.kmeans_ops import assign_reference
+        if (x.is_cuda and not cos and x.dtype in (torch.float32, torch.float64) and prec in ("auto", "screen")
+                and os.environ.get("CML_KMEANS_SCREEN", "1") != "0"
+                and LloydEngine.screen_applies(int(x.shape[1]), len(self._centers))):
+            from ..parallel.comm import local_comm
+            eng = LloydEngine(x, int(x.shape[1]), len(self._centers), local_comm(), precision="screen")
+            return eng.screen_assign(c, want_dist=want_dist)
         if cos:
             from ..models.kmeans import unit_rows
             lab, dist = assign_reference(unit_rows(x), c)
@@ -240,7 +249,7 @@ class KMeansModel(Model):
         from ..sql.column import LazyColumnData
 
         def thunk():
-            lab, _ = self._assign(df)
+            lab, _ = self._assign(df, want_dist=False)
             return lab.to(torch.int32), None
         return _replace_col(df, self.getPredictionCol(), LazyColumnData(thunk, df._nrows, T.IntegerType()))
 

@@ -130,14 +130,30 @@ class LinearRegression(Estimator):
                          maxBlockSizeInMB=maxBlockSizeInMB)
         self._defaultParamMap.pop("weightCol", None)
 
+    # Spark's WeightedLeastSquares.MAX_NUM_FEATURES: solver "auto" takes the normal equations up to this width
+    _NORMAL_MAX_FEATURES = 4096
+
     def _fit(self, df):
-        if self.getLoss() != "squaredError":
-            raise NotImplementedError("only loss='squaredError' is supported")
+        loss = self.getLoss()
+        if loss not in ("squaredError", "huber"):
+            raise ValueError(f"loss must be 'squaredError' or 'huber', got {loss!r}")
+        solver = self.getSolver()
+        if solver not in ("auto", "normal", "l-bfgs"):
+            raise ValueError(f"solver must be 'auto', 'normal' or 'l-bfgs', got {solver!r}")
         x = df._feature_matrix(self.getFeaturesCol())
         d = x.shape[1]
         y = df._column_data(self.getLabelCol()).values.to(torch.float64)
         w = df._column_data(self.getOrDefault("weightCol")).values.to(torch.float64) \
             if self.isSet("weightCol") else None
+        if loss == "huber":
+            if solver == "normal":
+                raise ValueError("LinearRegression with huber loss only supports the l-bfgs solver")
+            if self.getElasticNetParam() > 0 and self.getRegParam() > 0:
+                raise ValueError("LinearRegression with huber loss only supports L2 regularization")
+        # Spark LinearRegression.train: the normal equations for "normal", and for "auto" with squared
+        # loss up to 4096 features; L-BFGS / OWL-QN passes over the rows otherwise (no D² Gram)
+        if loss == "huber" or solver == "l-bfgs" or (solver == "auto" and d > self._NORMAL_MAX_FEATURES):
+            return self._fit_iterative(df, x, d, y, w, loss)
         G = glm_ops.gram(x, d, y, w)
         df._comm.allreduce_(G)
         Gn = G.cpu().numpy()
@@ -149,6 +165,115 @@ class LinearRegression(Estimator):
         model = LinearRegressionModel(coef, intercept)
         self._copyValues(model)
         model._attach_summary(LinearRegressionTrainingSummary(model, df, Gn, d, self.getRegParam() == 0.0))
+        return model
+
+
+    def _fit_iterative(self, df, x, d, y, w, loss):
+        """Spark's "l-bfgs" path (LinearRegression.train with LeastSquaresAggregator / HuberAggregator):
+        L-BFGS (OWL-QN with an L1 part) over the features scaled by their std; every objective evaluation is
+        one K13 pass of the local rows ('squared' loss: margins, residuals and Xᵀr with the rows read once)
+        all-reduced over the ranks. Squared error also scales the label by its std (the optimum is the
+        normal equations' one); huber keeps the raw label and optimises the scale σ too (through log σ,
+        which keeps it positive as Spark's L-BFGS-B bound does)."""
+        from ..models.optim import lbfgs
+        comm = df._comm
+        n = int(x.shape[0])
+        fi = self.getFitIntercept()
+        reg, alpha = self.getRegParam(), self.getElasticNetParam()
+        # weighted first and second moments of the features and the label, all-reduced (Spark's summarizer)
+        ww = w if w is not None else None
+        mom = torch.zeros(2 * d + 4, dtype=torch.float64, device=x.device)
+        step = max(1, (1 << 24) // max(d, 1))
+        for r0 in range(0, n, step):
+            xf = x[r0:r0 + step, :d].to(torch.float64)
+            yc = y[r0:r0 + step]
+            wc = ww[r0:r0 + step] if ww is not None else torch.ones_like(yc)
+            mom[:d] += wc @ xf
+            mom[d:2 * d] += wc @ (xf * xf)
+            mom[2 * d] += (wc * yc).sum()
+            mom[2 * d + 1] += (wc * yc * yc).sum()
+            mom[2 * d + 2] += wc.sum()
+            mom[2 * d + 3] += (wc * wc).sum()
+        comm.allreduce_(mom)
+        m = mom.cpu().numpy()
+        W, W2 = m[2 * d + 2], m[2 * d + 3]
+        if W <= 0:
+            raise ValueError("LinearRegression: empty training set")
+        mx, my = m[:d] / W, m[2 * d] / W
+        denom = W - W2 / W if W - W2 / W > 0 else W  # unbiased weighted variance (Spark's summarizer)
+        sx = np.sqrt(np.maximum(m[d:2 * d] - W * mx * mx, 0.0) / denom)
+        rawsy = math.sqrt(max(m[2 * d + 1] - W * my * my, 0.0) / denom)
+        if loss == "squaredError" and rawsy == 0.0 and (fi or my == 0.0):
+            # constant label: Spark returns zero coefficients and the label mean (or zero) as intercept
+            model = LinearRegressionModel(np.zeros(d), my if fi else 0.0)
+            self._copyValues(model)
+            model._attach_summary(LinearRegressionTrainingSummary(model, df, None, d, False, [0.0], 0))
+            return model
+        sy = rawsy if rawsy > 0 else abs(my)
+        inv = np.where(sx > 0, 1.0 / np.where(sx > 0, sx, 1.0), 0.0)  # constant features get no weight
+        l2, l1 = reg * (1.0 - alpha), reg * alpha
+        std_pen = self.getStandardization()
+        pen2 = np.full(d, l2) if std_pen else l2 * inv * inv
+        pen1 = (np.full(d, l1) if std_pen else l1 * inv) if l1 > 0 else None
+        huber = loss == "huber"
+        eps = self.getEpsilon()
+        dev = x.device
+        ylab = y if huber else y / sy
+        evals = [0]
+
+        def fg(p):
+            evals[0] += 1
+            beta = p[:d]
+            b = p[d] if fi else 0.0
+            coef = torch.as_tensor(np.r_[beta * inv, b], dtype=torch.float64, device=dev)
+            if not huber:
+                o = glm_ops.loss_grad(x, d, ylab, coef, ww, loss="squared")
+                comm.allreduce_(o)
+                o = o.cpu().numpy()
+                f = o[d + 1] / W + 0.5 * float(np.sum(pen2 * beta * beta))
+                g = np.zeros_like(p)
+                g[:d] = o[:d] * inv / W + pen2 * beta
+                if fi:
+                    g[d] = o[d] / W
+                return f, g
+            sig = math.exp(p[-1])
+            mrg = glm_ops.linear_predict(x, d, coef) if n else torch.zeros(0, dtype=torch.float64, device=dev)
+            r = y - mrg
+            wr = ww if ww is not None else torch.ones_like(r)
+            inb = r.abs() <= eps * sig
+            lrow = torch.where(inb, 0.5 * (sig + r * r / sig), 0.5 * (sig + 2.0 * eps * r.abs() - sig * eps * eps))
+            gm = torch.where(inb, -r / sig, -eps * torch.where(r >= 0, 1.0, -1.0).to(r.dtype))
+            gs = torch.where(inb, 0.5 * (1.0 - (r / sig) ** 2), torch.full_like(r, 0.5 * (1.0 - eps * eps)))
+            # Xᵀ(w·∂ℓ/∂m) through the 'squared' K13 (zero coefficients, label -(w·∂ℓ/∂m): residual = w·∂ℓ/∂m)
+            o = glm_ops.loss_grad(x, d, -(wr * gm), torch.zeros(d + 1, dtype=torch.float64, device=dev),
+                                  None, loss="squared")
+            sc = torch.stack([(wr * lrow).sum(), (wr * gs).sum()])
+            msg = torch.cat([o[:d + 1], sc])
+            comm.allreduce_(msg)
+            o = msg.cpu().numpy()
+            f = o[d + 1] / W + 0.5 * float(np.sum(pen2 * beta * beta))
+            g = np.zeros_like(p)
+            g[:d] = o[:d] * inv / W + pen2 * beta
+            if fi:
+                g[d] = o[d] / W
+            g[-1] = o[d + 2] / W * sig
+            return f, g
+
+        nv = d + 1 + (1 if huber else 0)
+        p0 = np.zeros(nv)
+        if fi and not huber:
+            p0[d] = my / sy
+        l1v = None
+        if pen1 is not None:
+            l1v = np.zeros(nv)
+            l1v[:d] = pen1
+        p, hist, iters = lbfgs(fg, p0, max(self.getMaxIter(), 0), self.getTol(), l1=l1v)
+        scale_y = 1.0 if huber else sy
+        coef = p[:d] * inv * scale_y
+        intercept = (p[d] * scale_y) if fi else 0.0
+        model = LinearRegressionModel(coef, intercept, math.exp(p[-1]) if huber else 1.0)
+        self._copyValues(model)
+        model._attach_summary(LinearRegressionTrainingSummary(model, df, None, d, False, hist, iters))
         return model
 
 
@@ -270,15 +395,18 @@ class LinearRegressionSummary:
 
 
 class LinearRegressionTrainingSummary(LinearRegressionSummary):
-    def __init__(self, model, df, G: np.ndarray, d: int, exact: bool):
+    def __init__(self, model, df, G: Optional[np.ndarray], d: int, exact: bool, history=None, iterations: int = 1):
         super().__init__(model, df)
         self._G = G
         self._d = d
         self._exact = exact
-        self.objectiveHistory = [0.0]
-        self.totalIterations = 1
+        self.objectiveHistory = list(history) if history is not None else [0.0]
+        self.totalIterations = int(iterations)
 
     def _cov(self):
+        if self._G is None:
+            raise RuntimeError("No Std. Error of coefficients available for this LinearRegressionModel "
+                               "(the l-bfgs solver keeps no normal equations)")
         if not self._exact:
             raise RuntimeError("coefficient statistics need regParam=0 (normal equation solver)")
         G, d = self._G, self._d

@@ -119,7 +119,9 @@ def main(argv=None):
         if data.count() < 10:
             return
         model = LinearRegression(featuresCol="features", labelCol="length_of_stay").fit(data)
+        predictions = model.transform(data)  # ref.py:99
         model.write().overwrite().save(os.path.join(args.out, "models", f"linear_regression_model_batch_{batch_id}"))
+        predictions.show()  # ref.py:106 (every rank takes part; rank 0 prints)
         per_batch_rmse.append((batch_id, model.summary.rootMeanSquaredError))
 
     query_stream = (streaming_df.writeStream.foreachBatch(train_model_on_batch).format("delta")

@@ -35,3 +35,17 @@ def test_host_sums_are_correctly_rounded(n, d, k, dt):
     b, _, bl = K.sums_reference(x[h:], lab[h:], k, with_lo=True)
     f = K.dd_fold(torch.stack([a, b]), torch.stack([al, bl]))
     assert torch.equal(f, S)
+
+
+def test_dd_sums_exact_span_guard():
+    """The f64 exponent-span guard of the auto screen: ordinary data passes, 1e-9 beside 1e9
+    (span ~60 binades) does not; all-zero rows pass; the result is cached on the tensor."""
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import dd_sums_exact
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
+    x = torch.randn(5000, 6, dtype=torch.float64)
+    assert dd_sums_exact(x, 6, local_comm())
+    x[1, 1], x[2, 2] = 1e-9, 1e9
+    assert not dd_sums_exact(x, 6, local_comm())
+    assert x._cml_f64span[1] == 6
+    assert dd_sums_exact(torch.zeros(10, 3, dtype=torch.float64), 3, local_comm())
