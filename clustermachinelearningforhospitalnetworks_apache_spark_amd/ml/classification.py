@@ -89,14 +89,27 @@ class LogisticRegression(Estimator):
         mean = msg[1:1 + d] / max(N, 1)
         var = torch.clamp((msg[1 + d:] - N * mean * mean) / max(N - 1, 1), min=0.0)
         std = torch.sqrt(var).cpu().numpy()
+        # L-BFGS state checkpoints (cml.ml.checkpointDir): x, f, g and the s/y history every
+        # cml.ml.checkpointInterval iterations; a restarted fit resumes and ends bit for bit where the
+        # uninterrupted one does
+        from ..utils.checkpoint import FitCheckpoint
+        sgd = self.getSolver() == "sgd" and not multinomial
+        ck = None
+        if not sgd:
+            key = (f"{'multinomial' if multinomial else 'binomial'}|d={d}|C={num_classes}|reg={self.getRegParam()}|"
+                   f"en={self.getElasticNetParam()}|fi={self.getFitIntercept()}|std={self.getStandardization()}|"
+                   f"tol={self.getTol()}")
+            ck = FitCheckpoint(df, "logreg", key, (x, y, w))
         if multinomial:
-            coef, icpt, hist, iters = self._fit_multinomial(x, y, w, d, num_classes, std, comm)
-        elif self.getSolver() == "sgd":
+            coef, icpt, hist, iters = self._fit_multinomial(x, y, w, d, num_classes, std, comm, ck)
+        elif sgd:
             coef, icpt, hist, iters = self._fit_sgd(x, y, w, d, std, comm)
             coef, icpt = coef[None, :], np.array([icpt])
         else:
-            coef, icpt, hist, iters = self._fit_binomial(x, y, w, d, std, comm)
+            coef, icpt, hist, iters = self._fit_binomial(x, y, w, d, std, comm, ck)
             coef, icpt = coef[None, :], np.array([icpt])
+        if ck is not None:
+            ck.clear()
         model = LogisticRegressionModel(coef, icpt, num_classes, multinomial)
         self._copyValues(model)
         model._attach_summary(LogisticRegressionTrainingSummary(model, df, hist, iters))
@@ -106,7 +119,22 @@ class LogisticRegression(Estimator):
         lam, a = self.getRegParam(), self.getElasticNetParam()
         return lam * (1.0 - a), lam * a
 
-    def _fit_binomial(self, x, y, w, d, std, comm):
+    def _lbfgs(self, fg, p0, l1v, ck):
+        """models/optim.lbfgs with the fit's checkpoint (resume + periodic saves) and crash point."""
+        from ..models.optim import lbfgs_state_arrays, lbfgs_state_from_arrays
+        state = None
+        if ck is not None:
+            got = ck.load()
+            if got is not None:
+                state = lbfgs_state_from_arrays(got[1])
+
+        def on_iter(it, st):
+            if ck is not None and ck.due(it):
+                ck.save(it, lbfgs_state_arrays(st))
+        return lbfgs(fg, p0, self.getMaxIter(), self.getTol(), l1=l1v, state=state, on_iter=on_iter,
+                     fault="logreg.iteration")
+
+    def _fit_binomial(self, x, y, w, d, std, comm, ck=None):
         l2, l1 = self._reg()
         sd = np.where(std > 0, std, 1.0)
         active = std > 0
@@ -144,7 +172,7 @@ class LogisticRegression(Estimator):
         l1v = None
         if l1 > 0:
             l1v = np.r_[np.full(d, l1) if standardize else l1 / sd, 0.0]
-        p, hist, iters = lbfgs(fg, p0, self.getMaxIter(), self.getTol(), l1=l1v)
+        p, hist, iters = self._lbfgs(fg, p0, l1v, ck)
         coef = np.where(active, p[:d] / sd, 0.0)
         return coef, float(p[d]) if fi else 0.0, hist, iters
 
@@ -165,7 +193,7 @@ class LogisticRegression(Estimator):
         c = opt.coef.cpu().numpy()
         return c[:d], float(c[d]), hist, opt.steps
 
-    def _fit_multinomial(self, x, y, w, d, C, std, comm):
+    def _fit_multinomial(self, x, y, w, d, C, std, comm, ck=None):
         l2, l1 = self._reg()
         if l1 > 0:
             raise NotImplementedError("multinomial elastic-net (L1) is not supported")
@@ -209,7 +237,7 @@ class LogisticRegression(Estimator):
             return f, G.reshape(-1)
 
         p0 = np.zeros(C * (d + 1))
-        p, hist, iters = lbfgs(fg, p0, self.getMaxIter(), self.getTol())
+        p, hist, iters = self._lbfgs(fg, p0, None, ck)
         P = p.reshape(C, d + 1)
         coef = np.where(active[None, :], P[:, :d] / sd[None, :], 0.0)
         icpt = P[:, d].copy() if fi else np.zeros(C)

@@ -170,16 +170,8 @@ def _weights(df, col: str, device) -> torch.Tensor:
 
 
 def _fingerprint(x: torch.Tensor, comm) -> str:
-    """Global (Σx, Σx²) of the feature matrix in float64: two fits with the same shape and
-    params but different data never share a checkpoint."""
-    s = torch.zeros(2, dtype=torch.float64, device=x.device)
-    step = max(1, (1 << 24) // max(int(x.shape[1]), 1))  # row chunks of 16M elements: bounded f64 temporaries
-    for r0 in range(0, int(x.shape[0]), step):
-        xf = x[r0:r0 + step].to(torch.float64)
-        s[0] += xf.sum()
-        s[1] += (xf * xf).sum()
-    comm.allreduce_(s)
-    return f"{float(s[0]):.17g},{float(s[1]):.17g}"
+    """Global (Σx, Σx²) of the feature matrix in float64 (utils/checkpoint.py data_fingerprint)."""
+    return ckpt.data_fingerprint(x, comm)
 
 
 class KMeansModel(Model):
@@ -217,7 +209,6 @@ class KMeansModel(Model):
         x = df._feature_matrix(self.getFeaturesCol())
         if not x.is_cuda and df._device.type == "cuda" and not self._cosine():
             # out-of-core column: the streamed MFMA assign (models/kmeans.py _assign_all)
-            from ..models.kmeans import LloydEngine
             eng = LloydEngine(x, x.shape[1], len(self._centers), df._comm, device=df._device)
             lab, dist = eng.assign(torch.as_tensor(self._centers))
             return lab.long(), dist.to(torch.float64)

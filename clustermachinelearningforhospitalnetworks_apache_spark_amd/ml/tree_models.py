@@ -91,7 +91,19 @@ class TreeEstimatorMixin:
             p.bootstrap = self.getBootstrap()
             p.feature_subset = self.getFeatureSubsetStrategy()
         eng = TR.ForestEngine(x, y, p, comm, row_ids=df._row_ids, weights=w)
-        trees = eng.fit()
+        # level checkpoints (cml.ml.checkpointDir): the K19 results of the completed levels
+        from ..utils.checkpoint import FitCheckpoint
+        ck = FitCheckpoint(df, "forest", f"{type(self).__name__}|{sorted(p.__dict__.items())}", (x, y, w))
+        replay = None
+        got = ck.load()
+        if got is not None:
+            replay = [got[1][f"l{i}"] for i in range(int(got[1]["levels"][0]))]
+
+        def on_level(levels, done):
+            if ck.due(levels):
+                ck.save(levels, {"levels": np.array([levels]), **{f"l{i}": r for i, r in enumerate(done)}})
+        trees = eng.fit(replay=replay, on_level=on_level if ck.enabled else None)
+        ck.clear()
         return trees, x.shape[1], num_classes
 
 
@@ -117,9 +129,13 @@ class GBTEstimatorMixin(TreeEstimatorMixin):
                           min_weight_fraction=self.getMinWeightFractionPerNode(),
                           min_info_gain=self.getMinInfoGain(), subsampling_rate=self.getSubsamplingRate(),
                           feature_subset=self.getFeatureSubsetStrategy(), seed=int(self.getSeed()))
+        from ..utils.checkpoint import FitCheckpoint
+        ck = FitCheckpoint(df, "gbt", f"{type(self).__name__}|{loss}|step={self.getStepSize()}|"
+                                      f"vtol={self.getValidationTol()}|{sorted(p.__dict__.items())}", (x, y, w, valid))
         trees, tw = TR.fit_gbt(x, y, p, self.getMaxIter(), self.getStepSize(), loss, df._comm,
                                row_ids=df._row_ids, weights=w, valid=valid,
-                               validation_tol=self.getValidationTol())
+                               validation_tol=self.getValidationTol(), ckpt=ck if ck.enabled else None)
+        ck.clear()
         return trees, tw, x.shape[1]
 
 

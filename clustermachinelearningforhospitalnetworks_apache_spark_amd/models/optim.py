@@ -13,22 +13,41 @@ import numpy as np
 
 
 def lbfgs(fg: Callable[[np.ndarray], Tuple[float, np.ndarray]], x0: np.ndarray, max_iter: int = 100,
-          tol: float = 1e-6, m: int = 10, l1: Optional[np.ndarray] = None) -> Tuple[np.ndarray, List[float], int]:
+          tol: float = 1e-6, m: int = 10, l1: Optional[np.ndarray] = None, state: Optional[dict] = None,
+          on_iter: Optional[Callable[[int, dict], None]] = None,
+          fault: Optional[str] = None) -> Tuple[np.ndarray, List[float], int]:
     """Minimise f with L-BFGS (OWL-QN when an L1 weight vector ``l1`` is given).
 
     Convergence (Breeze-style): relative improvement of f below ``tol`` over an
     iteration, or gradient norm below ``tol * max(1, |x|)``.
     Returns (x, objective history, iterations).
+
+    Checkpointing: ``on_iter(it, state)`` runs after every completed iteration with the
+    whole optimizer state (``lbfgs_state``: x, f, g, the s/y history, the objective history); passing such
+    a state back as ``state`` resumes at the next iteration and retraces the uninterrupted run bit for bit
+    (the state is everything an iteration reads). ``fault`` names a crash point (utils/fault.py) armed per
+    iteration.
     """
-    x = np.asarray(x0, dtype=np.float64).copy()
-    f, g = fg(x)
-    if l1 is not None:
-        f += float(np.sum(l1 * np.abs(x)))
-    hist = [f]
-    S: List[np.ndarray] = []
-    Y: List[np.ndarray] = []
-    it = 0
-    for it in range(1, max_iter + 1):
+    if state is not None:
+        x, f, g = state["x"].copy(), float(state["f"]), state["g"].copy()
+        S = [s.copy() for s in state["S"]]
+        Y = [y.copy() for y in state["Y"]]
+        hist = [float(v) for v in state["hist"]]
+        start = int(state["it"]) + 1
+    else:
+        x = np.asarray(x0, dtype=np.float64).copy()
+        f, g = fg(x)
+        if l1 is not None:
+            f += float(np.sum(l1 * np.abs(x)))
+        hist = [f]
+        S, Y = [], []
+        start = 1
+    it = start - 1
+    if fault is not None:
+        from ..utils.fault import maybe_fail
+    for it in range(start, max_iter + 1):
+        if fault is not None:
+            maybe_fail(fault, it)
         pg = _pseudo_grad(x, g, l1) if l1 is not None else g
         if np.linalg.norm(pg) <= tol * max(1.0, np.linalg.norm(x)):
             it -= 1
@@ -56,7 +75,23 @@ def lbfgs(fg: Callable[[np.ndarray], Tuple[float, np.ndarray]], x0: np.ndarray, 
         hist.append(f)
         if improvement < tol:
             break
+        if on_iter is not None:
+            on_iter(it, {"x": x, "f": f, "g": g, "S": S, "Y": Y, "hist": hist, "it": it})
     return x, hist, it
+
+
+def lbfgs_state_arrays(st: dict) -> dict:
+    """An L-BFGS state as named numpy arrays (utils/checkpoint.py stores one .npy per array)."""
+    n = int(st["x"].shape[0])
+    return {"x": st["x"], "f": np.array([st["f"]]), "g": st["g"], "hist": np.asarray(st["hist"], dtype=np.float64),
+            "it": np.array([st["it"]], dtype=np.int64),
+            "S": np.asarray(st["S"], dtype=np.float64).reshape(-1, n),
+            "Y": np.asarray(st["Y"], dtype=np.float64).reshape(-1, n)}
+
+
+def lbfgs_state_from_arrays(a: dict) -> dict:
+    return {"x": a["x"], "f": float(a["f"][0]), "g": a["g"], "hist": list(a["hist"]), "it": int(a["it"][0]),
+            "S": list(a["S"]), "Y": list(a["Y"])}
 
 
 def _two_loop(g, S, Y):

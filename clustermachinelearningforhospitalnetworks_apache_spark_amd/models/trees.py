@@ -346,10 +346,19 @@ class ForestEngine:
             node_of[t] = torch.where(act, new, nd)
 
     # -------------------------------------------------------------- fit
-    def fit(self, splits: Optional[List[np.ndarray]] = None, bins: Optional[torch.Tensor] = None) -> List[Node]:
+    def fit(self, splits: Optional[List[np.ndarray]] = None, bins: Optional[torch.Tensor] = None,
+            replay: Optional[List[np.ndarray]] = None, on_level=None) -> List[Node]:
         """Grow ``num_trees`` trees level-wise.  ``splits``/``bins`` let a caller that fits many
-        trees on the same rows (gradient boosting) find candidates and bin the rows once."""
+        trees on the same rows (gradient boosting) find candidates and bin the rows once.
+
+        Checkpoints: a level's whole outcome is its K19 result ``res`` (identical on every
+        rank: it comes from the all-reduced histogram), so ``on_level(levels_done, [res_0, ...])`` after
+        each level is the forest's state, and ``replay`` (those arrays) resumes a fit — completed levels
+        rebuild their nodes and re-route the rows from the saved results (no histogram pass), the feature
+        subset draws are replayed, and the fit continues bit for bit as the uninterrupted one."""
         p = self.p
+        replay = list(replay) if replay is not None else []
+        done: List[np.ndarray] = []
         T = p.num_trees
         if splits is None:
             splits = self.find_splits()
@@ -384,8 +393,8 @@ class ForestEngine:
             nodes = max(len(l) for l in level_nodes)
             if nodes == 0 or depth == p.max_depth:
                 break  # nodes at maxDepth are leaves; their stats came with the parent's split
-            hist = self.histogram(bins, node_of, wt, nodes)
-            self.comm.allreduce_(hist)
+            from ..utils.fault import maybe_fail
+            maybe_fail("forest.level", depth)  # crash point
             # per-node feature subsets (RF), drawn for every node of the level in order, identically on
             # every rank (same seed, same draws)
             masks = np.ones((T, nodes, self.d), dtype=np.uint8)
@@ -394,7 +403,13 @@ class ForestEngine:
                 for t in range(T):
                     for j in range(len(level_nodes[t])):
                         masks[t, j, rs.choice(self.d, k_sub, replace=False)] = 1
-            res = self.best_splits(hist, masks, nodes)  # [T, nodes, 3 + 3S] (K19)
+            if depth < len(replay):
+                res = np.asarray(replay[depth], dtype=np.float64)
+            else:
+                hist = self.histogram(bins, node_of, wt, nodes)
+                self.comm.allreduce_(hist)
+                res = self.best_splits(hist, masks, nodes)  # [T, nodes, 3 + 3S] (K19)
+            done.append(res)
             S = self.S
             split_feat = np.full((T, nodes), -1, dtype=np.int32)
             split_bin = np.zeros((T, nodes), dtype=np.int32)
@@ -430,6 +445,8 @@ class ForestEngine:
             if depth < p.max_depth and any(next_level):
                 self.route(bins, node_of, split_feat.reshape(-1), split_bin.reshape(-1), left_id.reshape(-1),
                            right_id.reshape(-1), nodes)
+            if on_level is not None and depth >= len(replay):
+                on_level(depth + 1, done)
             level_nodes = next_level
             if not any(level_nodes):
                 break
@@ -713,7 +730,7 @@ def predict_tree(tree: Node, x: torch.Tensor) -> torch.Tensor:
 def fit_gbt(x: torch.Tensor, y: torch.Tensor, params: TreeParams, max_iter: int, step_size: float, loss: str,
             comm: Optional[Communicator] = None, row_ids: Optional[torch.Tensor] = None,
             weights: Optional[torch.Tensor] = None, valid: Optional[torch.Tensor] = None,
-            validation_tol: float = 0.01):
+            validation_tol: float = 0.01, ckpt=None):
     """Gradient-boosted regression trees (Spark ``GradientBoostedTrees.boost``): tree 0 is fit on the
     labels with weight 1, tree m on the pseudo-residuals of the running margin with weight
     ``step_size``.  Candidate splits and the bin codes (K16/K17) are built once and reused by
@@ -721,6 +738,9 @@ def fit_gbt(x: torch.Tensor, y: torch.Tensor, params: TreeParams, max_iter: int,
     per level; the margin is updated in place by K21.  Labels for ``logistic`` must already be
     in {-1, +1}.  ``valid`` (bool per row) holds rows out of training and stops early once the
     validation loss improves by less than ``validation_tol * max(loss, 0.01)`` (Spark's rule).
+    ``ckpt`` (utils/checkpoint.FitCheckpoint): the K19 results of every completed tree are saved every
+    ``checkpointInterval`` trees; a resumed fit replays those trees (nodes, margin and validation updates
+    exactly as they happened) and boosts on — the uninterrupted fit bit for bit.
     Returns (trees, tree_weights)."""
     comm = comm or local_comm()
     if loss not in GBT_LOSSES:
@@ -744,12 +764,33 @@ def fit_gbt(x: torch.Tensor, y: torch.Tensor, params: TreeParams, max_iter: int,
     f = torch.zeros_like(eng.y)
     fv = torch.zeros_like(yv) if yv is not None else None
     best_err, best_m = float("inf"), 0
+    from ..utils.fault import maybe_fail
+    saved: List[List[np.ndarray]] = []  # K19 results per level of every completed tree
+    if ckpt is not None:
+        got = ckpt.load()
+        if got is not None:
+            arrs = got[1]
+            for mm in range(int(arrs["trees"][0])):
+                saved.append([arrs[f"t{mm}_l{lv}"] for lv in range(int(arrs["levels"][mm]))])
+    resumed = len(saved)
     for m in range(max_iter):
+        if m >= resumed:
+            maybe_fail("forest.tree", m)  # crash point
         w = 1.0 if m == 0 else step_size
         if m > 0:
             eng.y = gbt_residual(loss, f, y).contiguous()
         eng.p.seed = params.seed + m
-        t = eng.fit(splits, bins)[0]
+        levels: List[np.ndarray] = []
+        t = eng.fit(splits, bins, replay=saved[m] if m < resumed else None,
+                    on_level=lambda _, done: levels.__setitem__(slice(None), list(done)))[0]
+        if m >= resumed:
+            saved.append(list(levels))
+            if ckpt is not None and ckpt.due(m + 1):
+                arrays = {"trees": np.array([m + 1]), "levels": np.array([len(v) for v in saved])}
+                for mm, lv in enumerate(saved):
+                    for li, r in enumerate(lv):
+                        arrays[f"t{mm}_l{li}"] = r
+                ckpt.save(m + 1, arrays)
         trees.append(t)
         tw.append(w)
         f += w * predict_tree(t, eng.x)

@@ -151,3 +151,57 @@ def clear(directory: str, name: str, comm=None) -> None:
     if comm is not None and not comm.is_root:
         return
     shutil.rmtree(os.path.join(directory, name), ignore_errors=True)
+
+
+def data_fingerprint(x, comm) -> str:
+    """Global (Σx, Σx²) of a device/host tensor in float64 (a collective): two fits with the same shape and
+    params but different data never share a checkpoint."""
+    import torch
+    x2 = x.reshape(x.shape[0], -1) if x.dim() != 2 else x
+    s = torch.zeros(2, dtype=torch.float64, device=x.device)
+    step = max(1, (1 << 24) // max(int(x2.shape[1]), 1))  # row chunks of 16M elements: bounded f64 temporaries
+    for r0 in range(0, int(x2.shape[0]), step):
+        xf = x2[r0:r0 + step].to(torch.float64)
+        s[0] += xf.sum()
+        s[1] += (xf * xf).sum()
+    comm.allreduce_(s)
+    return f"{float(s[0]):.17g},{float(s[1]):.17g}"
+
+
+class FitCheckpoint:
+    """Iteration checkpoints of one estimator fit, enabled by the session conf
+    ``cml.ml.checkpointDir`` (every ``cml.ml.checkpointInterval`` iterations, default 10). The key is the
+    estimator kind, its objective-defining params, the global row count and a fingerprint of every input
+    tensor, so a restarted process (new estimator uid) finds the checkpoint of the same fit and a different
+    fit never does. Every rank constructs it (the fingerprint is a collective); rank 0 writes, and
+    ``load`` broadcasts rank 0's decision (every rank resumes from the same point or none does)."""
+
+    def __init__(self, df, prefix: str, key: str, tensors=()):
+        conf = df._session.conf
+        self.dir = conf.get("cml.ml.checkpointDir", None)
+        self.every = max(1, int(conf.get("cml.ml.checkpointInterval", 10)))
+        self.comm = df._comm
+        self.enabled = bool(self.dir)
+        self.key = self.name = None
+        if self.enabled:
+            n = int(self.comm.sum_scalar(float(df._nrows)))
+            fp = "|".join(data_fingerprint(t, self.comm) for t in tensors if t is not None)
+            self.key = f"{prefix}|n={n}|{key}|data={fp}"
+            self.name = name_for(prefix, self.key)
+
+    def load(self) -> Optional[Tuple[int, Dict[str, np.ndarray]]]:
+        if not self.enabled:
+            return None
+        return load_shared(self.dir, self.name, self.key, self.comm)
+
+    def due(self, iteration: int) -> bool:
+        return self.enabled and iteration % self.every == 0
+
+    def save(self, iteration: int, arrays: Dict[str, np.ndarray]) -> None:
+        if self.enabled:
+            save(self.dir, self.name, self.key, iteration, arrays, self.comm)
+
+    def clear(self) -> None:
+        if self.enabled:
+            self.comm.barrier()
+            clear(self.dir, self.name, self.comm)

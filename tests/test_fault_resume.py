@@ -230,3 +230,79 @@ def test_stream_restart_restores_watermark(spark, tmp_path):
     assert wm > 0
     q = start()  # nothing new to read: the restarted query still reports the committed watermark
     assert q._watermark_ms == wm
+
+
+def _labelled(spark, n=2500, d=5, seed=1, classes=2):
+    import pandas as pd
+    rs = np.random.RandomState(seed)
+    X = rs.randn(n, d) * (1 + np.arange(d))
+    if classes == 2:
+        y = (X @ rs.randn(d) + rs.randn(n) > 0).astype(float)
+    else:
+        y = np.argmax(X[:, :classes] + rs.randn(n, classes), 1).astype(float)
+    pdf = pd.DataFrame(X, columns=[f"f{i}" for i in range(d)])
+    pdf["label"] = y
+    pdf["y"] = X @ np.arange(1, d + 1) + rs.randn(n)
+    df = spark.createDataFrame(pdf)
+    return VectorAssembler(inputCols=[f"f{i}" for i in range(d)], outputCol="features").transform(df)
+
+
+def _kill_and_resume(spark, tmp_path, monkeypatch, make, fault, prefix, read):
+    """Fit uninterrupted; fit with checkpoints and a crash at ``fault``; refit (new estimator): equal."""
+    df = make[0]
+    want = read(make[1]().fit(df))
+    spark.conf.set("cml.ml.checkpointDir", str(tmp_path / "ck"))
+    spark.conf.set("cml.ml.checkpointInterval", "2")
+    monkeypatch.setenv("CML_FAULT", fault)
+    with pytest.raises(InjectedFault):
+        make[1]().fit(df)
+    saved = os.listdir(tmp_path / "ck")
+    assert len(saved) == 1 and saved[0].startswith(prefix), saved
+    assert any(v.startswith("v-") for v in os.listdir(tmp_path / "ck" / saved[0]))
+    monkeypatch.delenv("CML_FAULT")
+    got = read(make[1]().fit(df))
+    assert os.listdir(tmp_path / "ck") == []
+    return want, got
+
+
+@pytest.mark.parametrize("classes,reg,en", [(2, 0.0, 0.0), (2, 0.05, 0.5), (3, 0.01, 0.0)])
+def test_logreg_resumes_from_lbfgs_checkpoint(spark, tmp_path, monkeypatch, classes, reg, en):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegression
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models import optim
+    df = _labelled(spark, classes=classes)
+    starts = []
+    orig = optim.lbfgs
+
+    def spy(*a, **kw):
+        starts.append(None if kw.get("state") is None else kw["state"]["it"])
+        return orig(*a, **kw)
+
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml import classification as C
+    monkeypatch.setattr(C, "lbfgs", spy)
+    mk = lambda: LogisticRegression(maxIter=40, tol=1e-12, regParam=reg, elasticNetParam=en)  # noqa: E731
+    read = lambda m: (m.coefficientMatrix.toArray(), m.interceptVector.toArray(), m.summary.objectiveHistory)  # noqa: E731
+    want, got = _kill_and_resume(spark, tmp_path, monkeypatch, (df, mk), "logreg.iteration=7", "logreg-", read)
+    assert starts[-1] == 6  # resumed from the checkpoint of iteration 6
+    np.testing.assert_array_equal(got[0], want[0])
+    np.testing.assert_array_equal(got[1], want[1])
+    assert got[2] == want[2]
+
+
+def test_forest_resumes_from_level_checkpoint(spark, tmp_path, monkeypatch):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import RandomForestRegressor
+    df = _labelled(spark)
+    mk = lambda: RandomForestRegressor(labelCol="y", numTrees=6, maxDepth=5, seed=4)  # noqa: E731
+    read = lambda m: (m.featureImportances.toArray(), [t.toDebugString.split("\n", 1)[1] for t in m.trees])  # noqa: E731
+    want, got = _kill_and_resume(spark, tmp_path, monkeypatch, (df, mk), "forest.level=3", "forest-", read)
+    np.testing.assert_array_equal(got[0], want[0])
+    assert got[1] == want[1]
+
+
+def test_gbt_resumes_from_tree_checkpoint(spark, tmp_path, monkeypatch):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.regression import GBTRegressor
+    df = _labelled(spark)
+    mk = lambda: GBTRegressor(labelCol="y", maxIter=9, maxDepth=3, seed=2)  # noqa: E731
+    read = lambda m: (m.featureImportances.toArray(), [t.toDebugString.split("\n", 1)[1] for t in m.trees], m.treeWeights)  # noqa: E731
+    want, got = _kill_and_resume(spark, tmp_path, monkeypatch, (df, mk), "forest.tree=5", "gbt-", read)
+    np.testing.assert_array_equal(got[0], want[0])
+    assert got[1] == want[1] and list(got[2]) == list(want[2])
