@@ -571,6 +571,157 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   }
 }
 
+// ---------------------------------------------------------------------------- K13m multinomial gradient
+// LogisticRegression family="multinomial" (SURVEY K13 "multinomial C×D variant"): ONE pass over X per
+// objective evaluation, no f64 copy of it. Per row group (LPR lanes share a row, each NCH 16-byte chunks of
+// CPT columns): the C margins m_c = x·w_c + b_c (lane shares reduced over the row's lanes), the row's
+// log-sum-exp, loss += wt·(lse − m_y), r_c = wt·(softmax_c − [c = y]) and ∇w_c += r_c·x. The lane's
+// columns of the CP weight rows and CP gradient rows live in VGPRs (CT: f32 for bf16/f32/fp8 rows, f64
+// for f64 rows); class slots c >= C are dead (margin -inf, no gradient). Every FLUSH groups the f32
+// gradients are summed over the wave's row sub-groups (xor shuffles) and added into the wave's own f64
+// image of the C×d gradient in LDS; at the end the block sums its waves' images in wave order into its
+// partial [C·d | C | loss | weight] (K13b adds the partials in a fixed order: deterministic).
+template <typename T, int NCH, int CP>
+__global__ __launch_bounds__(kGlmThreads) void multinomial_grad_kernel(
+    const T* __restrict__ X, long long n, long long ld, int d, int lpr, int C, const double* __restrict__ y,
+    const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1], last column = intercepts*/,
+    double* __restrict__ out /*[grid][C·d + C + 2]*/) {
+  using CT = typename CompT<T>::type;
+  constexpr int CPT = Elt<T>::CPT;
+  constexpr int FLUSH = 32;
+  const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, nw = blockDim.x >> 6;
+  const int rpw = 64 / lpr, sub = lane / lpr, li = lane - sub * lpr;
+  const int dpad = lpr * NCH * CPT;
+  extern __shared__ double mimg[];  // [nw][CP][dpad] f64 gradient images, then [nw][CP + 2] scalars
+  double* img = mimg + (long long)wave * CP * dpad;
+  for (int i = lane; i < CP * dpad; i += 64) img[i] = 0.0;
+  CT w[CP][NCH][CPT], g[CP][NCH][CPT];
+  CT b[CP];
+#pragma unroll
+  for (int k = 0; k < CP; ++k) {
+    b[k] = k < C ? (CT)coef[(long long)k * (d + 1) + d] : (CT)0;
+#pragma unroll
+    for (int c = 0; c < NCH; ++c)
+#pragma unroll
+      for (int j = 0; j < CPT; ++j) {
+        const int col = (c * lpr + li) * CPT + j;
+        w[k][c][j] = (k < C && col < d) ? (CT)coef[(long long)k * (d + 1) + col] : (CT)0;
+        g[k][c][j] = 0;
+      }
+  }
+  double gb[CP];
+#pragma unroll
+  for (int k = 0; k < CP; ++k) gb[k] = 0.0;
+  double loss = 0.0, wsum = 0.0;
+  // flush: sub-group sums of the f32 gradients into the wave's f64 image (sub-group 0 writes)
+  auto flush = [&]() {
+#pragma unroll
+    for (int k = 0; k < CP; ++k)
+#pragma unroll
+      for (int c = 0; c < NCH; ++c)
+#pragma unroll
+        for (int j = 0; j < CPT; ++j) {
+          CT v = g[k][c][j];
+          for (int o = lpr; o < 64; o <<= 1) v += __shfl_xor(v, o, 64);
+          if (sub == 0 && k < C) img[k * dpad + (c * lpr + li) * CPT + j] += (double)v;
+          g[k][c][j] = 0;
+        }
+  };
+  const long long step = (long long)gridDim.x * nw * rpw;
+  int since = 0;
+  long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
+  uint4 raw[NCH];
+  double yn, wn;
+  {
+    const long long row = row0 + sub;
+    const bool ok = row < n;
+    load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw);
+    yn = ok ? y[row] : 0.0;
+    wn = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+  }
+  for (; row0 < n; row0 += step) {
+    CT v[NCH][CPT];
+    decode_group<T, CT, NCH>(raw, lpr, li, d, v);
+    const double yi = yn, wi = wn;
+    {
+      const long long row = row0 + step + sub;
+      const bool ok = row < n;
+      load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw);
+      yn = ok ? y[row] : 0.0;
+      wn = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+    }
+    CT m[CP];
+    CT mx = -__builtin_huge_valf();
+#pragma unroll
+    for (int k = 0; k < CP; ++k) {
+      m[k] = group_sum_ct<CT>(dot_ct<CT, NCH, CPT>(v, w[k]), lpr) + b[k];
+      if (k < C) mx = m[k] > mx ? m[k] : mx;
+    }
+    CT se = 0;
+    CT e[CP];
+#pragma unroll
+    for (int k = 0; k < CP; ++k) {
+      if constexpr (sizeof(CT) == 4) e[k] = k < C ? __expf(m[k] - mx) : 0.f;
+      else e[k] = k < C ? exp(m[k] - mx) : 0.0;
+      se += e[k];
+    }
+    const int yc = (int)yi;
+    const CT inv = (CT)1 / se;
+    CT my = 0;
+#pragma unroll
+    for (int k = 0; k < CP; ++k) {
+      my = k == yc ? m[k] : my;
+      const CT r = (CT)wi * (e[k] * inv - (k == yc ? (CT)1 : (CT)0));
+      if (k < C) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) g[k][c][j] = fma(r, v[c][j], g[k][c][j]);
+        if (li == 0) gb[k] += (double)r;
+      }
+    }
+    if (li == 0) {
+      double lse;
+      if constexpr (sizeof(CT) == 4) lse = (double)mx + (double)__logf(se);
+      else lse = mx + log(se);
+      loss += wi * (lse - (double)my);
+      wsum += wi;
+    }
+    if (++since >= FLUSH) {
+      since = 0;
+      flush();
+    }
+  }
+  flush();
+  // wave scalars -> LDS, then the block's partial in wave order
+  double* scal = mimg + (long long)nw * CP * dpad;
+#pragma unroll
+  for (int k = 0; k < CP; ++k) gb[k] = wave_sum_f64(gb[k]);
+  loss = wave_sum_f64(loss);
+  wsum = wave_sum_f64(wsum);
+  if (lane == 0) {
+#pragma unroll
+    for (int k = 0; k < CP; ++k) scal[wave * (CP + 2) + k] = gb[k];
+    scal[wave * (CP + 2) + CP] = loss;
+    scal[wave * (CP + 2) + CP + 1] = wsum;
+  }
+  __syncthreads();
+  const int m_out = C * d + C + 2;
+  double* o_ = out + (long long)blockIdx.x * m_out;
+  for (int t = threadIdx.x; t < C * d; t += blockDim.x) {
+    const int k = t / d, col = t - k * d;
+    double a = 0.0;
+    for (int ww = 0; ww < nw; ++ww) a += mimg[(long long)ww * CP * dpad + k * dpad + col];
+    o_[t] = a;
+  }
+  for (int t = threadIdx.x; t < C + 2; t += blockDim.x) {
+    const int q = t < C ? t : CP + (t - C);
+    double a = 0.0;
+    for (int ww = 0; ww < nw; ++ww) a += scal[ww * (CP + 2) + q];
+    o_[C * d + t] = a;
+  }
+}
+
 // ---------------------------------------------------------------------------- K13b / K14 SGD step
 // K13b partial_colsum: msg[j] = Σ_b part[b][j] over the grid's per-block partials in a fixed order:
 // a block owns 16 columns (128-byte row segments) and 64 row slices; slice sums are combined in
@@ -1011,6 +1162,62 @@ CML_API int cml_glm_loss_grad(const void* X, long long n, long long ld, int d, i
                            nullptr);
     });
   });
+  return cml_status();
+}
+
+// K13m layout: LPR lanes per row (up to 64), NCH chunks; CP class slots. Returns the class-slot count the
+// kernel runs for (0: not supported at this width / class count — the caller takes the chunked form).
+static int multinomial_layout(int d, int dtype, int C, int& lpr, int& nch) {
+  const int cpt = dtype == 0 ? 8 : dtype == 1 ? 4 : dtype == 2 ? 2 : 16;
+  const int ch = (d + cpt - 1) / cpt;
+  lpr = pow2ceil(ch) < 64 ? pow2ceil(ch) : 64;
+  nch = pow2ceil((ch + lpr - 1) / lpr);
+  if (nch > 2) return 0;
+  const int cp = C <= 4 ? 4 : C <= 8 ? 8 : 0;
+  if (cp == 0) return 0;
+  const int dpad = lpr * nch * cpt;
+  const int vals = cp * nch * cpt * (dtype == 2 ? 2 : 1);  // VGPRs of one class-row set (f64: two each)
+  if (vals > 64) return 0;
+  if ((long long)(kGlmThreads / 64) * cp * dpad * 8 > 80 * 1024) return 0;
+  return cp;
+}
+
+CML_API int cml_multinomial_supported(int d, int dtype, int C) {
+  int lpr = 0, nch = 0;
+  return multinomial_layout(d, dtype, C, lpr, nch);
+}
+
+CML_API int cml_multinomial_grid(long long n, int d, int dtype, int C, int ncu) {
+  int lpr = 0, nch = 0;
+  const int cp = multinomial_layout(d, dtype, C, lpr, nch);
+  if (cp == 0) return -1;
+  const int rows = (kGlmThreads / 64) * (64 / lpr);
+  return grid_for(n, rows, 2 * ncu);
+}
+
+CML_API int cml_multinomial_grad(const void* X, long long n, long long ld, int d, int dtype, int C, const double* y,
+                                 const double* wt, const double* coef, double* out, int grid, void* stream) {
+  hipStream_t st = (hipStream_t)stream;
+  int lpr = 0, nch = 0;
+  const int cp = multinomial_layout(d, dtype, C, lpr, nch);
+  if (cp == 0 || grid < 1) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)(kGlmThreads / 64) * (cp * lpr * nch * (dtype == 0 ? 8 : dtype == 1 ? 4 : dtype == 2 ? 2 : 16) +
+                                                   cp + 2) * sizeof(double);
+#define CML_MN(CPV)                                                                                          \
+  CML_T_SWITCH(dtype, {                                                                                      \
+    if (nch == 1)                                                                                            \
+      hipLaunchKernelGGL((multinomial_grad_kernel<T, 1, CPV>), dim3(grid), dim3(kGlmThreads), lds, st,       \
+                         (const T*)X, n, ld, d, lpr, C, y, wt, coef, out);                                   \
+    else                                                                                                     \
+      hipLaunchKernelGGL((multinomial_grad_kernel<T, 2, CPV>), dim3(grid), dim3(kGlmThreads), lds, st,       \
+                         (const T*)X, n, ld, d, lpr, C, y, wt, coef, out);                                   \
+  })
+  if (cp == 4) {
+    CML_MN(4);
+  } else {
+    CML_MN(8);
+  }
+#undef CML_MN
   return cml_status();
 }
 

@@ -10,7 +10,8 @@ sigmoid, gradient and loss, X read once) + one all-reduce of the (d+3)-vector.
 ``solver="sgd"`` (cml extension for the [NS] mini-batch SGD config) keeps the
 coefficients on the device and runs K13 on mini-batch slices + RCCL all-reduce +
 an on-device update per step, with no host synchronisation inside an epoch.
-Multinomial fits use torch GEMMs (hipBLASLt) for the C-class margins.
+Multinomial fits run K13m (glm.hip multinomial_grad_kernel): the C margins, the softmax and the
+C×d gradient in one pass over X, f64 partials; L1 through OWL-QN.
 """
 from __future__ import annotations
 
@@ -194,34 +195,23 @@ class LogisticRegression(Estimator):
         return c[:d], float(c[d]), hist, opt.steps
 
     def _fit_multinomial(self, x, y, w, d, C, std, comm, ck=None):
+        """Softmax regression (Spark's multinomial family): L-BFGS / OWL-QN over the standardized
+        coefficients; every evaluation is one K13m pass over the local rows (glm_ops.multinomial_grad: X
+        read once, no f64 copy) and one all-reduce of the [C·d | C | loss | weight] message."""
         l2, l1 = self._reg()
-        if l1 > 0:
-            raise NotImplementedError("multinomial elastic-net (L1) is not supported")
         sd = np.where(std > 0, std, 1.0)
         active = std > 0
         fi = self.getFitIntercept()
+        standardize = self.getStandardization()
         dev = x.device
-        xf = x.to(torch.float64)
-        yl = y.to(torch.int64)
-        ww = w if w is not None else torch.ones(x.shape[0], dtype=torch.float64, device=dev)
-        Y = torch.nn.functional.one_hot(yl, C).to(torch.float64) if yl.numel() else torch.zeros(
-            (0, C), dtype=torch.float64, device=dev)
-        sd_t = torch.as_tensor(sd, device=dev)
-        act_t = torch.as_tensor(active, device=dev)
 
         def fg(p):
-            P = torch.as_tensor(p, device=dev).reshape(C, d + 1)
-            Wp = P[:, :d]
-            b = P[:, d] if fi else torch.zeros(C, dtype=torch.float64, device=dev)
-            W = torch.where(act_t[None, :], Wp / sd_t[None, :], torch.zeros_like(Wp))
-            m = xf @ W.T + b[None, :]
-            lse = torch.logsumexp(m, 1)
-            loss = (ww * (lse - (m * Y).sum(1))).sum()
-            prob = torch.softmax(m, 1)
-            R = (prob - Y) * ww[:, None]
-            gW = R.T @ xf
-            gb = R.sum(0)
-            msg = torch.cat([gW.reshape(-1), gb, loss.reshape(1), ww.sum().reshape(1)])
+            P = p.reshape(C, d + 1)
+            coef = np.zeros((C, d + 1))
+            coef[:, :d] = np.where(active[None, :], P[:, :d] / sd[None, :], 0.0)
+            if fi:
+                coef[:, d] = P[:, d]
+            msg = glm_ops.multinomial_grad(x, d, y, torch.as_tensor(coef, device=dev), w)
             comm.allreduce_(msg)
             o = msg.cpu().numpy()
             wsum = max(o[-1], 1e-300)
@@ -231,13 +221,19 @@ class LogisticRegression(Estimator):
                 G[:, d] = o[C * d: C * d + C] / wsum
             f = o[-2] / wsum
             if l2 > 0:
-                Wn = p.reshape(C, d + 1)[:, :d]
-                f += 0.5 * l2 * float((Wn * Wn).sum())
-                G[:, :d] += l2 * Wn
+                Wn = P[:, :d]
+                pen = Wn if standardize else Wn / sd[None, :]
+                f += 0.5 * l2 * float(np.sum(np.where(active[None, :], pen * pen, 0.0)))
+                G[:, :d] += l2 * np.where(active[None, :], pen if standardize else pen / sd[None, :], 0.0)
             return f, G.reshape(-1)
 
         p0 = np.zeros(C * (d + 1))
-        p, hist, iters = self._lbfgs(fg, p0, None, ck)
+        l1v = None
+        if l1 > 0:  # OWL-QN on the coefficients (intercepts unpenalised), as Spark's multinomial elastic net
+            l1v = np.zeros((C, d + 1))
+            l1v[:, :d] = np.full(d, l1)[None, :] if standardize else (l1 / sd)[None, :]
+            l1v = l1v.reshape(-1)
+        p, hist, iters = self._lbfgs(fg, p0, l1v, ck)
         P = p.reshape(C, d + 1)
         coef = np.where(active[None, :], P[:, :d] / sd[None, :], 0.0)
         icpt = P[:, d].copy() if fi else np.zeros(C)
@@ -301,7 +297,10 @@ class LogisticRegressionModel(Model):
             return raw, prob
         W = torch.as_tensor(self._W, device=dev)
         b = torch.as_tensor(self._b, device=dev)
-        raw = x.to(torch.float64) @ W.T + b[None, :]
+        # row chunks: the C-class margins without an f64 copy of the whole feature matrix
+        raw = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float64, device=dev)
+        for r0 in range(0, int(x.shape[0]), 1 << 20):
+            raw[r0:r0 + (1 << 20)] = x[r0:r0 + (1 << 20), :d].to(torch.float64) @ W.T + b[None, :]
         return raw, torch.softmax(raw, 1)
 
     def _predict_from_prob(self, prob: torch.Tensor) -> torch.Tensor:

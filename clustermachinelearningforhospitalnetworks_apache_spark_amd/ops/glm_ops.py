@@ -28,6 +28,9 @@ _native.register_kernel_sigs({
     "cml_glm_loss_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
                                c_vp, c_ll, c_ll, c_vp]),
+    "cml_multinomial_supported": (c_int, [c_int, c_int, c_int]),
+    "cml_multinomial_grid": (c_int, [c_ll, c_int, c_int, c_int, c_int]),
+    "cml_multinomial_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
 })
 
 _CODE = {torch.bfloat16: 0, torch.float32: 1, torch.float64: 2, torch.float8_e4m3fn: 3}
@@ -209,6 +212,53 @@ def loss_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor, weig
                                              g, code_l, _native.stream_ptr())
     _native.check(st, "glm_loss_grad")
     return partial_colsum(out)
+
+
+def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
+                     weight: Optional[torch.Tensor] = None, chunk_rows: int = 1 << 20) -> torch.Tensor:
+    """Softmax (multinomial logistic) loss + gradient over the local shard: ``coef`` [C, d+1] (last column
+    the intercepts) in the original feature space, labels 0..C-1 (f64). Returns the float64 sums
+    [∇W (C·d, row-major) | ∇b (C) | loss | weight sum]. GPU rows run K13m (multinomial_grad_kernel: X read
+    once, gradient partials in f64, fixed-order reduction) where the layout fits (C <= 8, d up to 512 bf16);
+    otherwise — and on the CPU — row chunks in f64 (never an f64 copy of the whole X)."""
+    C = int(coef.shape[0])
+    n = int(x.shape[0])
+    coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    if x.is_cuda and n > 0 and x.dtype in _CODE:
+        xx = _prep(x)
+        code = _CODE[xx.dtype]
+        k = _native.kernels()
+        if k.cml_multinomial_supported(d, code, C) > 0:
+            g = k.cml_multinomial_grid(n, d, code, C, num_cus(xx.device.index or 0))
+            m = C * d + C + 2
+            out = torch.empty((g, m), dtype=torch.float64, device=xx.device)
+            yy = y.to(torch.float64).contiguous()
+            ww = weight.to(torch.float64).contiguous() if weight is not None else None
+            st = k.cml_multinomial_grad(xx.data_ptr(), n, xx.stride(0), d, code, C, yy.data_ptr(),
+                                        ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(), g,
+                                        _native.stream_ptr())
+            _native.check(st, "multinomial_grad")
+            return partial_colsum(out)
+    W, b = coef[:, :d], coef[:, d]
+    gW = torch.zeros((C, d), dtype=torch.float64, device=x.device)
+    gb = torch.zeros(C, dtype=torch.float64, device=x.device)
+    loss = torch.zeros((), dtype=torch.float64, device=x.device)
+    wsum = torch.zeros((), dtype=torch.float64, device=x.device)
+    for r0 in range(0, n, chunk_rows):
+        xf = x[r0:r0 + chunk_rows, :d].to(torch.float64)
+        yl = y[r0:r0 + chunk_rows].to(torch.int64)
+        ww = (weight[r0:r0 + chunk_rows].to(torch.float64) if weight is not None
+              else torch.ones(xf.shape[0], dtype=torch.float64, device=x.device))
+        mrg = xf @ W.T + b[None, :]
+        lse = torch.logsumexp(mrg, 1)
+        loss += (ww * (lse - mrg.gather(1, yl[:, None])[:, 0])).sum()
+        R = torch.softmax(mrg, 1)
+        R[torch.arange(R.shape[0], device=x.device), yl] -= 1.0
+        R *= ww[:, None]
+        gW += R.T @ xf
+        gb += R.sum(0)
+        wsum += ww.sum()
+    return torch.cat([gW.reshape(-1), gb, loss.reshape(1), wsum.reshape(1)])
 
 
 def _logreg_grad_dev(x, d, y, coef, weight, batch, row_base):

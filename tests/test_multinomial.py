@@ -1,0 +1,83 @@
+"""Multinomial LogisticRegression (VERDICT r4 missing 3): K13m computes the C margins, softmax, loss and the
+C×d gradient in one pass (no f64 copy of X); the fit matches sklearn's unpenalised multinomial model and
+its L1 form runs OWL-QN. GPU: the kernel equals the f64 chunked oracle on bf16/f32/f64/fp8 rows."""
+import numpy as np
+import pandas as pd
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegression
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.feature import VectorAssembler
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import glm_ops
+
+
+def _data(n=3000, d=6, C=4, seed=0):
+    rs = np.random.RandomState(seed)
+    X = rs.randn(n, d) * (1 + 0.3 * np.arange(d))
+    W = rs.randn(C, d)
+    y = np.array([rs.choice(C, p=np.exp(r - r.max()) / np.exp(r - r.max()).sum()) for r in X @ W.T])
+    return X, y.astype(float)
+
+
+def _frame(X, y):
+    from helpers import session
+    spark = session()
+    pdf = pd.DataFrame(X, columns=[f"f{i}" for i in range(X.shape[1])])
+    pdf["label"] = y
+    return VectorAssembler(inputCols=list(pdf.columns[:-1]), outputCol="features").transform(spark.createDataFrame(pdf))
+
+
+def test_multinomial_matches_sklearn():
+    from sklearn.linear_model import LogisticRegression as SK
+    X, y = _data()
+    m = LogisticRegression(family="multinomial", maxIter=500, tol=1e-12).fit(_frame(X, y))
+    sk = SK(penalty=None, tol=1e-12, max_iter=10000).fit(X, y)
+    W = m.coefficientMatrix.toArray()
+    skW = sk.coef_ - sk.coef_.mean(0, keepdims=True)
+    np.testing.assert_allclose(W, skW, rtol=1e-5, atol=1e-5)
+    np.testing.assert_allclose(m.interceptVector.toArray(), sk.intercept_ - sk.intercept_.mean(), rtol=1e-5, atol=1e-5)
+
+
+def test_multinomial_l1_runs_owlqn():
+    X, y = _data(seed=2)
+    X[:, 4:] = np.random.RandomState(5).randn(X.shape[0], 2) * 0.01  # near-useless features
+    m = LogisticRegression(family="multinomial", regParam=0.05, elasticNetParam=1.0, maxIter=300,
+                           tol=1e-10).fit(_frame(X, y))
+    W = m.coefficientMatrix.toArray()
+    assert np.count_nonzero(W == 0.0) >= 4  # L1 zeroes coefficients exactly
+    dense = LogisticRegression(family="multinomial", regParam=0.05, maxIter=300, tol=1e-10).fit(_frame(X, y))
+    assert np.count_nonzero(dense.coefficientMatrix.toArray() == 0.0) == 0
+
+
+def test_chunked_oracle_matches_closed_form():
+    X, y = _data(n=500, d=5, C=3)
+    coef = torch.randn(3, 6, dtype=torch.float64)
+    x = torch.as_tensor(X)
+    out = glm_ops.multinomial_grad(x, 5, torch.as_tensor(y), coef, chunk_rows=77)
+    mrg = x @ coef[:, :5].T + coef[:, 5]
+    P = torch.softmax(mrg, 1)
+    Y = torch.nn.functional.one_hot(torch.as_tensor(y).long(), 3).double()
+    np.testing.assert_allclose(out[:15].reshape(3, 5).numpy(), ((P - Y).T @ x).numpy(), rtol=1e-12, atol=1e-12)
+    loss = (torch.logsumexp(mrg, 1) - (mrg * Y).sum(1)).sum()
+    assert abs(float(out[-2]) - float(loss)) < 1e-9 and float(out[-1]) == 500.0
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,d,C", [(torch.bfloat16, 256, 8), (torch.bfloat16, 37, 3), (torch.float32, 128, 5),
+                                    (torch.float64, 64, 4), (torch.float8_e4m3fn, 256, 4), (torch.float32, 4, 2)])
+def test_kernel_matches_f64_oracle(dt, d, C):
+    g = torch.Generator(device="cuda").manual_seed(d + C)
+    n = 200_003
+    x = (torch.randn(n, d, generator=g, device="cuda") * 2).to(dt)
+    y = torch.randint(0, C, (n,), generator=g, device="cuda").double()
+    w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    coef = torch.randn(C, d + 1, generator=g, device="cuda", dtype=torch.float64) * 0.2
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
+    assert _native.kernels().cml_multinomial_supported(d, glm_ops._CODE[dt], C) > 0
+    got = glm_ops.multinomial_grad(x, d, y, coef, w)
+    ref = glm_ops.multinomial_grad(x.float().cpu().to(torch.float64) if dt != torch.float64 else x.cpu(), d,
+                                   y.cpu(), coef.cpu(), w.cpu())
+    tol = 1e-9 if dt == torch.float64 else 2e-5
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=tol, atol=tol * float(ref.abs().max()))
+    again = glm_ops.multinomial_grad(x, d, y, coef, w)
+    assert torch.equal(got, again)  # fixed-order partials: bitwise repeatable
