@@ -75,8 +75,13 @@ def build_kernels(force: bool = False, verbose: bool = False) -> Path:
     hipcc = _hipcc()
 
     def compile_one(src: Path) -> Path:
+        # per-object stamp (the source, every header, the flags): an edit to one .hip recompiles that file only
         out = OBJ / (src.stem + ".o")
+        od = _digest([src] + hdrs, " ".join(flags))
+        if _stamp_ok(out, od):
+            return out
         _run([hipcc, *flags, "-I", str(CSRC), "-c", str(src), "-o", str(out)])
+        _write_stamp(out, od)
         if verbose:
             print(f"[cml build] {src.name} -> {out.name}")
         return out

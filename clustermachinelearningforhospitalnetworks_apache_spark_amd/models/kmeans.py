@@ -399,9 +399,11 @@ class LloydEngine:
             self.slots = K.seg_slots(self.cplan, d, dev)
         self.msg_len = k * d + k + 1
         # incremental sums: sort regime with the centres in one LDS chunk (labels are final after one launch)
+        # (the device pruned step allocates its own, larger change lists in _pdev_alloc)
         self.delta = (K.DeltaState(max(maxn, 1), k, d, dp, self.row_chunks, self.msg_len, dev, self.aplan.grid,
                                    fp8=fp8)
-                      if self._incremental and self.cplan.mode == "sort" and self.aplan.kc == self.aplan.kp else None)
+                      if self._incremental and self.cplan.mode == "sort" and self.aplan.kc == self.aplan.kp
+                      and not (self.prune and pdev_ok) else None)
         self.msgs = torch.zeros((self.row_chunks, self.msg_len), dtype=torch.float64, device=dev)
         self.cb = torch.zeros((self.kp, dp), dtype=torch.bfloat16, device=dev)
         self._cb_cost = torch.zeros_like(self.cb)  # centres of the last full/torch-pruned step's assignment
@@ -430,7 +432,7 @@ class LloydEngine:
         """The one pass over X that fills the norms (and max norm, exponent range; with c0 the first
         k-means|| costs), then caches the norms on the feature tensor."""
         n, dp = self.n, self.dp
-        self._erange = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device=self.device)
+        self._erange = self._const([2 ** 31 - 1, -1], torch.int32)
         mxv = self._pst.mx if self._pdev else None
         if mxv is not None:
             mxv.zero_()
@@ -443,11 +445,27 @@ class LloydEngine:
                            xn64=self._xnorm64[r0:r1], c0n_dev=c0n_dev)
         if mxv is not None and self.comm.is_distributed:
             self.comm.allreduce_(mxv, op="max")
+        self._prefetch_erange()
         self._norms_ready = True
         try:
             self.x._cml_xnorm = (self.x._version, (n, dp), self._xnorm, self._erange, self._xnorm64)
         except (AttributeError, RuntimeError):
             pass
+
+    def _prefetch_erange(self) -> None:
+        """Enqueue the rank-agreed exponent range of X (_sum_grid) right behind the row pass and copy it to
+        pinned memory: the first Lloyd step then reads it without waiting for the whole init (a blocking read
+        there drained the queue between the init and step 1)."""
+        if not self.gpu or self._erange is None or K.is_fp8(self.x) or self.cplan.mode != "sort":
+            return
+        er = self._erange.to(torch.int64)
+        if self.comm.is_distributed:
+            self.comm.allreduce_(er[0:1], op="min")
+            self.comm.allreduce_(er[1:2], op="max")
+        self._er_host = torch.empty(2, dtype=torch.int64, pin_memory=True)
+        self._er_host.copy_(er, non_blocking=True)
+        self._er_event = torch.cuda.Event()
+        self._er_event.record()
 
     def _x_chunks(self, whole: bool = False):
         """(chunk, r0, r1, device rows) over the row chunks: slices of the resident matrix (one slice of
@@ -576,12 +594,18 @@ class LloydEngine:
                 for _, r0, r1, xc in self._x_chunks(whole=True):
                     K.row_pass(xc, r1 - r0, self.dp, tmp[r0:r1], erange=er)
             self._erange = er
-        lo = self._erange[0:1].to(torch.int64).clone()
-        hi = self._erange[1:2].to(torch.int64).clone()
-        if self.comm.is_distributed:
-            self.comm.allreduce_(lo, op="min")
-            self.comm.allreduce_(hi, op="max")
-        lo, hi, gn = int(lo.item()), int(hi.item()), self.global_n
+        if getattr(self, "_er_event", None) is not None:  # prefetched behind the row pass (_prefetch_erange)
+            self._er_event.synchronize()
+            lo, hi = int(self._er_host[0]), int(self._er_host[1])
+            self._er_event = None
+        else:
+            lo_t = self._erange[0:1].to(torch.int64).clone()
+            hi_t = self._erange[1:2].to(torch.int64).clone()
+            if self.comm.is_distributed:
+                self.comm.allreduce_(lo_t, op="min")
+                self.comm.allreduce_(hi_t, op="max")
+            lo, hi = int(lo_t.item()), int(hi_t.item())
+        gn = self.global_n
         if hi < 0 or gn == 0:  # every value is zero
             return
         lg = math.ceil(math.log2(gn + 1))
@@ -1027,7 +1051,7 @@ class LloydEngine:
         st.pmode = torch.zeros(2, dtype=torch.int32, device=dev)  # [full pass?, re-assigned rows]
         # step flags [force, done]: force = bounds invalid (a full pass next); done = converged (tol > 0
         # fits, _fit_lagged): every later step is a frozen no-op until the host reads the flag
-        st.flags = torch.tensor([1, 0], dtype=torch.int32, device=dev)
+        st.flags = self._const([1, 0], torch.int32)
         st.force, st.done = st.flags[0:1], st.flags[1:2]
         # steps left that skip the bounds after one went over the cap (data the bounds do not prune);
         # CML_KMEANS_PRUNE_BACKOFF=0 retries the bounds every step
@@ -1111,20 +1135,10 @@ class LloydEngine:
         st, n, k, d = self._pst, self.n, self.k, self.d
         if n == 0:
             return
-        cbd = self.cb[:k, :d].to(torch.float64)
         U = sd.uniq.to(device=self.device, dtype=torch.float64)
-        pn = (U * U).sum(1)
-        cnn = (cbd * cbd).sum(1)
-        d2m = (pn[:, None] + cnn[None, :] - 2.0 * (U @ cbd.T)).clamp_(min=0.0)
-        eps = 1e-12 * (pn.max() + cnn.max())  # f64 rounding of the expansion (a device scalar: no host read)
-        top = torch.topk(d2m, min(2, k), dim=1, largest=False)
-        a = top.indices[:, 0].to(torch.int32).contiguous()
-        d1 = ((top.values[:, 0] + eps).sqrt() * (1.0 + 1e-6)).to(torch.float32).contiguous()
-        if k > 1:
-            d2 = ((top.values[:, 1] - eps).clamp(min=0.0).sqrt() * (1.0 - 1e-6)).to(torch.float32).contiguous()
-        else:
-            d2 = torch.full_like(d1, math.inf)
-        pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
+        # one launch: per distinct candidate its nearest / second-nearest bf16 centre by direct differences
+        # (rounded outward) and its norm rounded up (kmeans_init_fast.hip; was an f64 GEMM + top-k + ~25 ops)
+        a, d1, d2, pn32 = K.seed_table(U, self.cb, k)
         qmap = sd.inverse.reshape(-1).to(torch.int32).contiguous()
         if st.cum is not None:
             st.cum.zero_()  # every row's bounds are written here: offsets against zero drift
@@ -1775,19 +1789,28 @@ class LloydEngine:
             lu, li = torch.min(u, 0)
             row = self._rows_f64(li.reshape(1)).reshape(-1)
         else:
-            lu = torch.tensor(2.0, dtype=torch.float64, device=dev)
+            lu = torch.full((), 2.0, dtype=torch.float64, device=dev)
             row = torch.zeros(d, dtype=torch.float64, device=dev)
         hdr = torch.cat([lu.reshape(1).to(torch.float64),
                          torch.full((1,), float(n), dtype=torch.float64, device=dev), row])
         g = comm.allgather_fixed(hdr)
-        c0 = g[torch.argmin(g[:, 0]), 2:].reshape(1, d)
         gn_dev = g[:, 1].sum()
-        centers = [c0]
+        # every candidate of every round lands in one f64 buffer, in Spark's order (first centre, then each
+        # round's rows by rank and row id): the rounds and the finish read views of it, no concatenations
+        cap = min(max(n, 1), max(4096, 8 * k))
+        cands = torch.empty((1 + steps * 2 * cap if comm.is_distributed else 1 + steps * cap, d), dtype=torch.float64,
+                            device=dev) if steps <= 4 else None
+        if cands is None or cands.shape[0] > 65536:  # (many init steps: grow on demand instead)
+            cands = torch.empty((1 + 4 * k + 1024, d), dtype=torch.float64, device=dev)
+        cands[0].copy_(g[torch.argmin(g[:, 0]), 2:])
+        c0 = cands[0:1]
         costs, nearest = self._init_first_pass(c0)
         ncand = 1
-        two_k = torch.tensor([0.0, 2.0 * k], dtype=torch.float64, device=dev)
-        cap = min(max(n, 1), max(4096, 8 * k))
+        two_k = self._const([0.0, 2.0 * k], torch.float64)
         out = torch.empty(cap, dtype=torch.int32, device=dev)
+        send = torch.empty((cap, d), dtype=torch.float64, device=dev) if comm.is_distributed else None
+        cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+        head = torch.empty(2, dtype=torch.float64, device=dev)
         for step in range(steps):
             tr = trace(f"kinit.round{step}")
             tr.__enter__()
@@ -1796,11 +1819,18 @@ class LloydEngine:
             if n:
                 scale[0:1].copy_(K.sum_f64(costs, n).reshape(1))
             comm.allreduce_(scale[0:1])
-            cnt = torch.zeros(1, dtype=torch.int32, device=dev)
+            cnt.zero_()
+            if cands.shape[0] < ncand + (cap if send is None else 0):
+                cands = self._grow_cands(cands, ncand, ncand + cap)
+            gathered = False
             if n:
                 K.init_sample(costs, ids64, n, rng.key(seed, 100 + step), scale, out, cnt)
+                # the sampled rows in row order, widened to f64, before the host read (device count)
+                if self._hs is None:  # (host rows of an out-of-core engine: the gather below)
+                    gathered = K.gather_rank_rows(self.x, out, cnt, cap, d, cands[ncand:] if send is None else send)
             # the one host read of the round: every rank's sampled count (and, once, the global row count)
-            head = torch.cat([cnt.to(torch.float64), gn_dev.reshape(1)])
+            head[0:1].copy_(cnt)
+            head[1:2].copy_(gn_dev.reshape(1))
             hv = comm.allgather_fixed(head).cpu()
             counts = [int(v) for v in hv[:, 0].tolist()]
             if step == 0:
@@ -1812,34 +1842,66 @@ class LloydEngine:
                 out = torch.empty(m, dtype=torch.int32, device=dev)
                 cnt.zero_()
                 K.init_sample(costs, ids64, n, rng.key(seed, 100 + step), scale, out, cnt)
-                cap = m
-            chosen = torch.sort(out[:m]).values.long()
-            new = self._rows_f64(chosen) if m else torch.zeros((0, d), dtype=torch.float64, device=dev)
-            new = comm.allgather_sized(new, counts)
-            if new.shape[0] == 0:
+                cap, gathered = m, False
+            mt = sum(counts)
+            if cands.shape[0] < ncand + mt:
+                cands = self._grow_cands(cands, ncand, ncand + mt)
+            dst = send if send is not None else cands[ncand:]
+            if m and not gathered:
+                chosen = torch.sort(out[:m]).values.long()
+                if send is not None and send.shape[0] < m:
+                    send = dst = torch.empty((m, d), dtype=torch.float64, device=dev)
+                dst[:m].copy_(self._rows_f64(chosen))
+            if send is not None:
+                pad = max(max(counts), 1)
+                gath = comm.allgather_fixed(send[:pad].contiguous())
+                at = ncand
+                for r in range(comm.world_size):
+                    if counts[r]:
+                        cands[at:at + counts[r]].copy_(gath[r, :counts[r]])
+                    at += counts[r]
+            if mt == 0:
                 tr.__exit__(None, None, None)
                 continue
-            centers.append(new)
+            new = cands[ncand:ncand + mt]
+            # bf16 copies and norms of every new candidate in one K11 launch; each K9r chunk is a view of them
+            # (rows past mt: zero centres with +inf norms, which no row takes)
+            dp = self.dp
+            kp_all = round_up(mt, 64)
+            cbn = torch.empty((kp_all, dp), dtype=torch.bfloat16, device=dev)
+            cnn = torch.empty(kp_all, dtype=torch.float32, device=dev)
+            K.update_centers(None, mt, d, new, cbn, dp, kp_all, cnn, None)
             # once most rows sit near a candidate, only the new candidates close to a row's nearest one
             # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
             # round (only the first centre so far) everything after the first K9r chunk
-            first = new.shape[0] if step > 0 else self._first_chunk(new.shape[0])
-            if step == 0:
-                self._init_candidate_pass(new[:first], costs, nearest, ncand)
-            rest = new[first:] if step == 0 else new
-            if rest.shape[0] and not self._init_candidate_pass_pruned(
-                    torch.cat(centers[:-1] + ([new[:first]] if step == 0 else []), 0), rest, costs, nearest,
-                    ncand + (first if step == 0 else 0)):
-                self._init_candidate_pass(rest, costs, nearest, ncand + (first if step == 0 else 0))
-            ncand += new.shape[0]
+            first = self._first_chunk(mt) if step == 0 else 0
+            if first:
+                self._init_candidate_pass(first, cbn, cnn, 0, costs, nearest, ncand)
+            if mt > first and not self._init_candidate_pass_pruned(
+                    cands[:ncand + first], new[first:], cbn, cnn, first, costs, nearest, ncand + first):
+                self._init_candidate_pass(mt - first, cbn, cnn, first, costs, nearest, ncand + first)
+            ncand += mt
             tr.__exit__(None, None, None)
         with trace("kinit.finish"):
-            return self._init_finish(seed, centers, costs, nearest, as_device=as_device)
+            return self._init_finish(seed, cands[:ncand], costs, nearest, as_device=as_device)
+
+    @staticmethod
+    def _grow_cands(cands: torch.Tensor, used: int, need: int) -> torch.Tensor:
+        out = torch.empty((max(need, 2 * cands.shape[0]), cands.shape[1]), dtype=cands.dtype, device=cands.device)
+        out[:used].copy_(cands[:used])
+        return out
+
+    def _const(self, values, dtype) -> torch.Tensor:
+        """A small device tensor of host values without a blocking copy (pinned staging, non_blocking): a
+        torch.tensor(..., device=cuda) is a pageable copy that waits for every queued kernel, which in the
+        fit's hot path stalled the host behind the row pass (profiles/r5/shard/)."""
+        h = torch.tensor(values, dtype=dtype, pin_memory=self.device.type == "cuda")
+        return h.to(self.device, non_blocking=True)
 
     def _init_finish(self, seed: int, centers: list, costs: torch.Tensor, nearest: torch.Tensor, as_device: bool):
         """Distinct candidates, their weights (rows per candidate, all-reduced) and the local k-means."""
         k = self.k
-        cand = torch.cat(centers, 0)
+        cand = centers if torch.is_tensor(centers) else torch.cat(centers, 0)
         # distinct candidates in sorted-row order (np.unique's order; identical on every device)
         uniq, inverse = K.unique_rows(cand) if cand.is_cuda else torch.unique(cand, dim=0, return_inverse=True)
         if uniq.shape[0] <= k:
@@ -1894,49 +1956,70 @@ class LloydEngine:
         also fills the norms (one read of X; a second read only if the norms were cached already). The
         centre's bf16 norm reaches the kernel on the device."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
-        cb0 = torch.zeros((32, dp), dtype=torch.bfloat16, device=dev)
-        cn0 = torch.zeros(32, dtype=torch.float32, device=dev)
-        K.update_centers(None, 1, d, c0.reshape(1, d).to(torch.float64).contiguous().clone(), cb0, dp, 32, cn0, None)
-        costs = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
-        nearest = torch.zeros(max(n, 1), dtype=torch.int32, device=dev)
+        # K11 writes every row of the 32-row block (zero rows, +inf norms past the first) and rewrites the
+        # f64 centre with its own value: no clears, no copy of c0
+        cb0 = torch.empty((32, dp), dtype=torch.bfloat16, device=dev)
+        cn0 = torch.empty(32, dtype=torch.float32, device=dev)
+        c0 = c0.reshape(1, d)
+        if c0.dtype != torch.float64 or not c0.is_contiguous():
+            c0 = c0.to(torch.float64).contiguous()
+        K.update_centers(None, 1, d, c0, cb0, dp, 32, cn0, None)
+        alloc = torch.empty if n else torch.zeros  # (the row pass writes every row's cost and nearest)
+        costs = alloc(max(n, 1), dtype=torch.float32, device=dev)
+        nearest = alloc(max(n, 1), dtype=torch.int32, device=dev)
         self._row_pass(cb0[0].to(torch.float32).contiguous(), 0.0, costs, nearest, c0n_dev=cn0[0:1])
         return costs, nearest
 
-    def _init_candidate_pass(self, new: torch.Tensor, costs: torch.Tensor, nearest: torch.Tensor,
-                             off: int) -> None:
-        """Merge the distances to the new candidates (K9r, at most 256 centres per launch) into
-        (cost, nearest)."""
-        n, d, dp, dev = self.n, self.d, self.dp, self.device
+    def _init_scratch(self):
+        """Per-engine scratch of the k-means|| candidate passes (allocated once; the K9r passes write every
+        entry they read back, so nothing is cleared per round)."""
+        sc = getattr(self, "_iscr", None)
+        if sc is None:
+            n, dev = self.n, self.device
+            tr = self.aplan.round_rows
+            sc = types.SimpleNamespace()
+            sc.lab = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+            sc.best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
+            sc.list_a = torch.empty((max(n, 1), 4), dtype=torch.int32, device=dev)
+            # list B is read in whole K9r tiles: entries past the count must be valid row ids (zeros once)
+            sc.list_b = torch.zeros(n + tr, dtype=torch.int32, device=dev)
+            sc.cxn = torch.zeros(n + tr, dtype=torch.float32, device=dev)
+            sc.lab_in = torch.full((n + tr,), -1, dtype=torch.int32, device=dev)
+            sc.cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+            self._iscr = sc
+        return sc
+
+    def _init_candidate_pass(self, m: int, cbn: torch.Tensor, cnn: torch.Tensor, c_off: int, costs: torch.Tensor,
+                             nearest: torch.Tensor, off: int) -> None:
+        """Merge the distances to the candidates cbn[c_off : c_off + m] (bf16 copies, norms cnn; K9r, at
+        most 320 centres per launch) into (cost, nearest); candidate i is global index off + i."""
+        n, dp, dev = self.n, self.dp, self.device
         if n == 0:
             return
-        lab = torch.zeros(n, dtype=torch.int32, device=dev)
-        best = torch.empty(n, dtype=torch.float32, device=dev)
+        sc = self._init_scratch()
+        lab, best = sc.lab[:n], sc.best[:n]
         xn = self.xnorm
         parts, c0 = [], 0
-        for size in self._candidate_chunks(new.shape[0]):
-            ch = new[c0:c0 + size].to(torch.float64).contiguous()
-            kc = ch.shape[0]
-            kp = round_up(kc, 32)
-            cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
-            cn = torch.zeros(kp, dtype=torch.float32, device=dev)
-            K.update_centers(None, kc, d, ch.clone(), cb, dp, kp, cn, None)
-            parts.append((c0, kc, cb, cn))
+        for size in self._candidate_chunks(m):
+            kp = round_up(size, 32)
+            parts.append((c0, size, cbn[c_off + c0:c_off + c0 + kp], cnn[c_off + c0:c_off + c0 + kp]))
             c0 += size
         # rows outer (one read of X per pass, streamed out of core), candidate chunks inner: the merges
         # of a row run in candidate order either way
         for _, r0, r1, xc in self._x_chunks(whole=True):
-            m = r1 - r0
-            if m == 0:
+            mm = r1 - r0
+            if mm == 0:
                 continue
             for c0, kc, cb, cn in parts:
-                plan = K.plan_assign(m, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
-                K.assign_bf16(xc, m, dp, cb, cn, plan, lab[r0:r1], best[r0:r1], None, xnorm=xn[r0:r1])
-                K.init_merge(costs[r0:r1], nearest[r0:r1], best[r0:r1], lab[r0:r1], off + c0, m)
+                plan = K.plan_assign(mm, dp, kc, dev.index or 0, fp8=K.is_fp8(self.x))
+                K.assign_bf16(xc, mm, dp, cb, cn, plan, lab[r0:r1], best[r0:r1], None, xnorm=xn[r0:r1])
+                K.init_merge(costs[r0:r1], nearest[r0:r1], best[r0:r1], lab[r0:r1], off + c0, mm)
 
     _INIT_LMAX = 8  # relevant new candidates a row may have to take the per-row path (else the K9r pass)
 
-    def _init_candidate_pass_pruned(self, prev: torch.Tensor, new: torch.Tensor, costs: torch.Tensor,
-                                    nearest: torch.Tensor, off: int) -> bool:
+    def _init_candidate_pass_pruned(self, prev: torch.Tensor, new: torch.Tensor, cbn: torch.Tensor,
+                                    cnn: torch.Tensor, c_off: int, costs: torch.Tensor, nearest: torch.Tensor,
+                                    off: int) -> bool:
         """A k-means|| candidate pass that skips what the triangle inequality rules out: a row at distance
         r from its nearest candidate p can only move to a new candidate y with |p - y| < 2r. With the
         distances from every existing candidate to the new ones sorted (a small f64 table), each row
@@ -1944,7 +2027,9 @@ class LloydEngine:
         most _INIT_LMAX get those distances from a per-row kernel, the rest run the K9r candidate pass
         over their positions (mode 2). Same nearest candidates as the full pass up to the rounding of
         near-ties. No host read: the list sizes stay on the device (the launches are sized by capacity).
-        Returns False (nothing changed) when the pruned pass does not apply (host rows, pruning off)."""
+        ``new`` (f64) are the candidates whose bf16 copies / norms are cbn / cnn[c_off:]; candidate i is
+        global index off + i. Returns False (nothing changed) when the pruned pass does not apply (host rows,
+        pruning off)."""
         n, d, dp, dev = self.n, self.d, self.dp, self.device
         # default on up to Dp = 256; at Dp = 512 the per-row path reads 1 KiB of candidate per listed
         # candidate and the gathered K9r pass loses to the streaming one: the config-5 pipeline's init
@@ -1957,12 +2042,12 @@ class LloydEngine:
         if n == 0:
             return True
         m = int(new.shape[0])
-        P = prev.to(device=dev, dtype=torch.float64)
-        Y = new.to(device=dev, dtype=torch.float64)
-        tab = K.init_table(P, Y)  # one launch: direct-difference distances, sorted in LDS
+        tab = K.init_table(prev, new)  # one launch: direct-difference distances, sorted in LDS
         if tab is not None:
             tab_v, tab_j, pn32 = tab
         else:
+            P = prev.to(device=dev, dtype=torch.float64)
+            Y = new.to(device=dev, dtype=torch.float64)
             pn, yn = (P * P).sum(1), (Y * Y).sum(1)
             d2 = pn[:, None] + yn[None, :] - 2.0 * (P @ Y.T)
             eps = 1e-12 * (pn.max() + yn.max())  # device scalar (no host read)
@@ -1971,36 +2056,30 @@ class LloydEngine:
             tab_j = order.to(torch.int32).contiguous()
             pn32 = (pn * (1.0 + 1e-6)).to(torch.float32).contiguous()
         tau = 2.0 * self._tau
-        tr = self.aplan.round_rows
-        list_a = torch.empty((n, 4), dtype=torch.int32, device=dev)  # (row, nearest, reach, cost) entries
-        list_b = torch.zeros(n + tr, dtype=torch.int32, device=dev)  # padded: whole tiles of valid rows
-        cnt = torch.zeros(2, dtype=torch.int32, device=dev)
+        sc = self._init_scratch()
+        list_a, list_b, cnt = sc.list_a, sc.list_b, sc.cnt
+        cnt.zero_()
         # per-row path limit: each listed candidate costs the row a read of its dp-wide bf16 copy from L2
         # (1 KiB at dp = 512), so wide rows hand longer lists to the MFMA pass sooner
         lmax = int(os.environ.get("CML_KMEANS_INIT_LMAX", self._INIT_LMAX if dp <= 256 else 4))
         lmax = max(0, min(self._INIT_LMAX, lmax))
         K.init_classify(costs, nearest, self.xnorm, pn32, tab_v, tau, n, lmax, list_a, cnt[0:1], list_b, cnt[1:2])
         # no host read of the list sizes: the per-row kernel and the K9r candidate pass take them from the
-        # device and size their grids by the capacity (dead tiles exit at once)
-        yb = torch.zeros((m, dp), dtype=torch.bfloat16, device=dev)
-        yb[:, :d] = Y.to(torch.bfloat16)
-        K.init_near_list(self.x, dp, costs, nearest, self.xnorm, pn32, tab_v, tab_j, yb, off, tau, list_a,
-                         cnt[0:1], n)
+        # device and size their grids by the capacity (dead tiles exit at once); the new candidates' bf16
+        # rows are the K11 copies the K9r chunks use
+        K.init_near_list(self.x, dp, costs, nearest, self.xnorm, pn32, tab_v, tab_j, cbn[c_off:c_off + m], off, tau,
+                         list_a, cnt[0:1], n)
         st = self._pst
-        pad = list_b.shape[0]
-        cxn = torch.zeros(pad, dtype=torch.float32, device=dev)
+        cxn = sc.cxn
         torch.index_select(self.xnorm[:n], 0, list_b[:n], out=cxn[:n])  # entries past the count: row 0's, unread
-        lab_in = torch.full((pad,), -1, dtype=torch.int32, device=dev)
         c0 = 0
         for size in self._candidate_chunks(m):
             kp = round_up(size, 32)
-            cbk = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
-            cnk = torch.zeros(kp, dtype=torch.float32, device=dev)
-            K.update_centers(None, size, d, Y[c0:c0 + size].contiguous().clone(), cbk, dp, kp, cnk, None)
+            cbk, cnk = cbn[c_off + c0:c_off + c0 + kp], cnn[c_off + c0:c_off + c0 + kp]
             plan = K.plan_assign(n, dp, size, dev.index or 0, fp8=K.is_fp8(self.x))
             mc = cnk[:size].max().reshape(1)
             K.assign_rr_ext(2, self.x, n, dp, cbk, cnk, plan, cxn, self.labels, None, st.ub, st.lb, mc,
-                            self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=lab_in, merge_cost=costs,
+                            self._tau, idx=list_b, n_dev=cnt[1:2], lab_in=sc.lab_in, merge_cost=costs,
                             merge_near=nearest, merge_off=off + c0)
             c0 += size
         if self.track_prune:

@@ -111,6 +111,10 @@ _native.register_kernel_sigs({
     "cml_kmeans_screen_cert_split": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_pair_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_gather_rank_rows": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp]),
+    "cml_kmeans_gather_rank_max": (c_int, []),
+    "cml_kmeans_seed_table": (c_int, [c_vp, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_unique_rows": (c_int, [c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_cert_stats": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_cert_bounds": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
@@ -801,10 +805,48 @@ def init_table(P: torch.Tensor, Y: torch.Tensor, stream=None):
     tab_v = torch.empty((mp, m), dtype=torch.float32, device=P.device)
     tab_j = torch.empty((mp, m), dtype=torch.int32, device=P.device)
     pn32 = torch.empty(mp, dtype=torch.float32, device=P.device)
-    _native.check(_native.kernels().cml_kmeans_init_table(P.data_ptr(), mp, Y.data_ptr(), m, d, tab_v.data_ptr(),
-                                                          tab_j.data_ptr(), pn32.data_ptr(),
-                                                          _native.stream_ptr(stream)), "kmeans_init_table")
+    lib = _native.kernels()
+    # the coalesced two-rows-per-workgroup form (kmeans_init_fast.hip) where its LDS fits, else the first one
+    fn = lib.cml_kmeans_pair_table if d <= 3072 else lib.cml_kmeans_init_table
+    _native.check(fn(P.data_ptr(), mp, Y.data_ptr(), m, d, tab_v.data_ptr(), tab_j.data_ptr(), pn32.data_ptr(),
+                     _native.stream_ptr(stream)), "kmeans_init_table")
     return tab_v, tab_j, pn32
+
+
+def gather_rank_rows(x: torch.Tensor, ids: torch.Tensor, cnt: torch.Tensor, cap: int, d: int, dest: torch.Tensor,
+                     pad_rows: int = 0, stream=None) -> bool:
+    """dest[rank(i)] = f64(x[ids[i], :d]) for the first min(cnt, cap) sampled ids (distinct; rank = position
+    in ascending id order): a k-means|| round's candidate rows in row order, widened, without a sort pass
+    or a host read of the count (kmeans_init_fast.hip). Rows [count, pad_rows) are zeroed. False (nothing
+    launched) when cap exceeds the kernel's LDS list; the caller then sorts and gathers itself."""
+    lib = _native.kernels()
+    if cap > int(lib.cml_kmeans_gather_rank_max()) or dest.dtype != torch.float64 or dest.stride(1) != 1 \
+            or dest.stride(0) != d or ids.dtype != torch.int32:
+        return False
+    ldx = x.stride(0) * x.element_size()
+    grid = max(1, min(1024, -(-max(cap, pad_rows, 1) // 4)))
+    _native.check(lib.cml_kmeans_gather_rank_rows(x.data_ptr(), int(ldx), int(is_fp8(x)), int(d), ids.data_ptr(),
+                                                  cnt.data_ptr(), int(cap), dest.data_ptr(), int(pad_rows), grid,
+                                                  _native.stream_ptr(stream)), "kmeans_gather_rank_rows")
+    return True
+
+
+def seed_table(U: torch.Tensor, cb: torch.Tensor, k: int, stream=None):
+    """(a int32, d1 f32, d2 f32, pn f32) per distinct init candidate (rows of U, f64): its nearest centre of
+    the bf16 centres ``cb`` (ties: lowest index), the distances to it and to the second nearest by direct
+    differences in f64 rounded up / down, and ||U_i||² rounded up — the first Lloyd step's seed tables
+    (kmeans_init_fast.hip seed_table_kernel)."""
+    m, d = int(U.shape[0]), int(U.shape[1])
+    U = U.to(torch.float64).contiguous()
+    dev = U.device
+    a = torch.empty(max(m, 1), dtype=torch.int32, device=dev)
+    d1 = torch.empty(max(m, 1), dtype=torch.float32, device=dev)
+    d2 = torch.empty(max(m, 1), dtype=torch.float32, device=dev)
+    pn = torch.empty(max(m, 1), dtype=torch.float32, device=dev)
+    _native.check(_native.kernels().cml_kmeans_seed_table(U.data_ptr(), m, d, cb.data_ptr(), cb.stride(0), int(k),
+                                                          a.data_ptr(), d1.data_ptr(), d2.data_ptr(), pn.data_ptr(),
+                                                          _native.stream_ptr(stream)), "kmeans_seed_table")
+    return a, d1, d2, pn
 
 
 def init_near_list(x: torch.Tensor, dp: int, cost: torch.Tensor, near: torch.Tensor, xn: torch.Tensor,

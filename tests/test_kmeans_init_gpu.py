@@ -240,3 +240,53 @@ def test_unique_rows_kernel_matches_torch_unique(m, d):
     got_u, got_i = K.unique_rows(P.cuda())
     assert torch.equal(got_u.cpu(), want_u)
     assert torch.equal(got_i.cpu(), want_i)
+
+
+@pytest.mark.parametrize("n,d,m,fp8", [(10_000, 256, 513, False), (5_000, 100, 1, False), (3_000, 512, 700, True),
+                                       (2_000, 64, 0, False)])
+def test_gather_rank_rows_kernel(n, d, m, fp8):
+    """A round's sampled rows in row order, widened to f64 from the device count (no sort, no host read),
+    equal to sort + gather; rows past the count are zeroed up to pad_rows."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import padded_dim_fp8
+    g = torch.Generator(device="cuda").manual_seed(n + m)
+    xs = torch.randn(n, d, generator=g, device="cuda") * 3
+    if fp8:
+        x = torch.zeros((n, padded_dim_fp8(d)), dtype=torch.uint8, device="cuda")
+        x[:, :d] = xs.to(torch.float8_e4m3fn).view(torch.uint8)
+        x = x.view(torch.float8_e4m3fn)
+        ref = x[:, :d].float().double()
+    else:
+        x = torch.zeros((n, d + 8), dtype=torch.bfloat16, device="cuda")
+        x[:, :d] = xs.to(torch.bfloat16)
+        ref = x[:, :d].double()
+    cap = 1024
+    ids = torch.randperm(n, generator=g, device="cuda")[:cap].to(torch.int32)
+    cnt = torch.tensor([m], dtype=torch.int32, device="cuda")
+    pad = m + 5
+    dest = torch.full((max(cap, pad), d), 7.0, dtype=torch.float64, device="cuda")
+    assert K.gather_rank_rows(x, ids, cnt, cap, d, dest, pad_rows=pad)
+    want = ref[torch.sort(ids[:m]).values.long()]
+    assert torch.equal(dest[:m], want)
+    assert bool((dest[m:pad] == 0).all())
+
+
+@pytest.mark.parametrize("m,d,k", [(600, 256, 256), (7, 33, 1), (1000, 128, 64)])
+def test_seed_table_kernel(m, d, k):
+    """Per distinct candidate: the nearest bf16 centre and outward-rounded distances to it and to the
+    second nearest (valid bounds of the f64 distances), the norm rounded up."""
+    g = torch.Generator(device="cuda").manual_seed(m * k)
+    C = (torch.randn(k, d, generator=g, device="cuda", dtype=torch.float64) * 4)
+    cb = torch.zeros((round(k / 32 + 0.5) * 32 + 32, d + 16), dtype=torch.bfloat16, device="cuda")
+    cb[:k, :d] = C.to(torch.bfloat16)
+    U = C[torch.randint(0, k, (m,), generator=g, device="cuda")].to(torch.bfloat16).double() + \
+        torch.randn(m, d, generator=g, device="cuda", dtype=torch.float64) * 0.5
+    a, d1, d2, pn = K.seed_table(U, cb, k)
+    D = torch.cdist(U, cb[:k, :d].double())
+    top = torch.sort(D, dim=1).values
+    assert bool((D.gather(1, a[:m].long()[:, None])[:, 0] == top[:, 0]).all())
+    assert bool((d1[:m].double() >= top[:, 0]).all()) and bool((d1[:m].double() <= top[:, 0] * (1 + 1e-5) + 1e-30).all())
+    if k > 1:
+        assert bool((d2[:m].double() <= top[:, 1]).all()) and bool((d2[:m].double() >= top[:, 1] * (1 - 1e-5)).all())
+    else:
+        assert bool(torch.isinf(d2[:m]).all())
+    assert bool((pn[:m].double() >= (U * U).sum(1)).all())
