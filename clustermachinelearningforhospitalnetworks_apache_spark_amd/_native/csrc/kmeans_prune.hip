@@ -51,6 +51,34 @@ __device__ __forceinline__ bool bound_step(int a, float& u, float& w, const floa
   return u <= st[a] || u <= lt;
 }
 
+// The pruned step's gate (kmeans_prune_gate_kernel's body): one thread.
+__device__ __forceinline__ void prune_gate_body(int* __restrict__ count, long long cap, const int* __restrict__ flags,
+                                                int* __restrict__ mode, int* __restrict__ backoff, int nback) {
+  if (flags[1] != 0) {
+    mode[0] = 0;
+    mode[1] = 0;
+    *count = 0;
+    return;
+  }
+  // the count is only ever changed by device-scope atomics: read it the same way (no stale cached copy)
+  const int c = __hip_atomic_load(count, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  if (backoff != nullptr && flags[0] == 0 && (long long)c > cap) *backoff = nback;
+  const int full = (flags[0] != 0 || (long long)c > cap) ? 1 : 0;
+  mode[0] = full;
+  mode[1] = full ? 0 : c;
+}
+
+// Gate folded into the bounds pass (one launch less per step): with gmode != null the workgroup that
+// finishes last (device-scope counter gdone) runs the gate on the final count; a skipped pass (force /
+// done) runs it in workgroup 0 at once.
+struct GateArgs {
+  int* mode;
+  long long cap;
+  int* backoff;
+  int nback;
+  int* done;
+};
+
 __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
                                                                        float* __restrict__ ub,
                                                                        float* __restrict__ lb,
@@ -64,10 +92,15 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
                                                                        int* __restrict__ cand_lab,
                                                                        float* __restrict__ cand_xn,
                                                                        const int* __restrict__ skip,
-                                                                       long long cap, const float* __restrict__ cum) {
+                                                                       long long cap, const float* __restrict__ cum,
+                                                                       GateArgs gate) {
   // skip = the step's flags {force, done}: bounds invalid this step (full pass instead), or the fit has
   // converged and the step is a frozen no-op (kmeans_prune_gate_kernel)
-  if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) return;
+  if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) {
+    if (gate.mode != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+    return;
+  }
   extern __shared__ __align__(16) unsigned char smem[];
   const float c2 = *c2p;
   float* sd = reinterpret_cast<float*>(smem);  // [k] drift
@@ -178,6 +211,14 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
       cand_xn[off] = xn[row];
     }
     ++off;
+  }
+  if (gate.mode != nullptr) {
+    // no fence: the gate reads only the count, which every block changed by an atomic whose result it
+    // waited for (base above) before this completion atomic — device-scope atomics in issue order
+    if (threadIdx.x == 0 && atomicAdd(gate.done, 1) == (int)gridDim.x - 1) {
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+      __hip_atomic_store(gate.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
   }
 }
 
@@ -438,6 +479,189 @@ __global__ __launch_bounds__(1024) void kmeans_label_hist_kernel(const int* __re
   for (int i2 = threadIdx.x; i2 < kp; i2 += 1024) hist[(long long)blockIdx.x * kp + i2] = h[i2];
 }
 
+// ---------------------------------------------------------------------------------------------
+// Fused tail of the device pruned step (fewer launches per Lloyd step: each launch costs ~4-5 us on the
+// shard of an 8-GPU run, where a whole step is ~0.3 ms).
+//
+// kmeans_update_pdev_kernel: K11 (kmeans_update_kernel: new centre = Σx·unit / count, empty clusters keep
+// theirs, bf16 copy, ||cb||²) plus what the pruned step needs from the old and new bf16 centres in the same
+// pass — cb_old <- old cb (always), cb_cost <- old cb unless the fit is frozen (flags[1]; the centres of the
+// last live assignment, for the training cost), cn64 = ||cb_new||² in f64 and drift = |cb_new - cb_old|
+// rounded up. Replaces cond_copy + K11 + the norm/drift half of centre_stats.
+__global__ void kmeans_update_pdev_kernel(const double* __restrict__ bufs, int nbuf, long long bstride, int k, int D,
+                                          double* __restrict__ cent, u16* __restrict__ cb, long long ldc, int Dp,
+                                          float* __restrict__ cnorm, double* __restrict__ shift2, double unit,
+                                          u16* __restrict__ cb_old, u16* __restrict__ cb_cost,
+                                          const int* __restrict__ flags, double* __restrict__ cn64,
+                                          float* __restrict__ drift) {
+  __shared__ double rn[16], rs[16], rd[16];
+  const int c = blockIdx.x, tid = threadIdx.x;
+  const int lane = tid & 63, wave = tid >> 6, nw = blockDim.x >> 6;
+  const bool live = flags[1] == 0;
+  if (c >= k) {
+    for (int d = tid; d < Dp; d += blockDim.x) {
+      const u16 o = cb[(long long)c * ldc + d];
+      cb_old[(long long)c * ldc + d] = o;
+      if (live) cb_cost[(long long)c * ldc + d] = o;
+      cb[(long long)c * ldc + d] = 0;
+    }
+    if (tid == 0) cnorm[c] = __builtin_huge_valf();
+    return;
+  }
+  double cnt = 0.0;
+  for (int b = 0; b < nbuf; ++b) cnt += bufs[b * bstride + (long long)k * D + c];
+  double nrm = 0.0, sh = 0.0, dr = 0.0;
+  for (int d = tid; d < Dp; d += blockDim.x) {
+    const u16 o = cb[(long long)c * ldc + d];
+    cb_old[(long long)c * ldc + d] = o;
+    if (live) cb_cost[(long long)c * ldc + d] = o;
+    if (d < D) {
+      const double old = cent[(long long)c * D + d];
+      double nv = old;
+      if (cnt > 0.0) {
+        double s = 0.0;
+        for (int b = 0; b < nbuf; ++b) s += bufs[b * bstride + (long long)c * D + d];
+        nv = (s * unit) / cnt;
+      }
+      sh += (nv - old) * (nv - old);
+      cent[(long long)c * D + d] = nv;
+      const u16 q = f32_to_bf16((float)nv);
+      cb[(long long)c * ldc + d] = q;
+      const double f = (double)bf16_to_f32(q);
+      nrm += f * f;
+      const double e = f - (double)bf16_to_f32(o);
+      dr += e * e;
+    } else {
+      cb[(long long)c * ldc + d] = 0;
+    }
+  }
+  nrm = wave_sum_f64(nrm);
+  sh = wave_sum_f64(sh);
+  dr = wave_sum_f64(dr);
+  if (lane == 0) { rn[wave] = nrm; rs[wave] = sh; rd[wave] = dr; }
+  __syncthreads();
+  if (tid == 0) {
+    double a = 0.0, b = 0.0, e = 0.0;
+    for (int w = 0; w < nw; ++w) { a += rn[w]; b += rs[w]; e += rd[w]; }
+    cnorm[c] = (float)a;
+    if (shift2 != nullptr) shift2[c] = b;
+    cn64[c] = a;
+    drift[c] = (float)(sqrt(e) * (1.0 + 1e-6));
+  }
+}
+
+// Centre statistics of the pruned step in one launch: one workgroup per centre j computes half_j (half the
+// distance from c_j to its nearest other centre, as kmeans_centre_stats_kernel); the workgroup that
+// finishes last (device-scope counter) runs the single-workgroup part (kmeans_centre_stats2_kernel's work:
+// mc, c2, thr, dmax, the cumulative drifts, the count / force / backoff resets) and re-arms the counter.
+__device__ void centre_stats2_body(const double* __restrict__ cn, const double* __restrict__ half,
+                                   const float* __restrict__ drift, int k, const float* __restrict__ mx, float tau,
+                                   int have_drift, float* __restrict__ thr, float* __restrict__ dmax,
+                                   float* __restrict__ mc, float* __restrict__ c2, int* __restrict__ count,
+                                   int* __restrict__ force, float* __restrict__ cum, int* __restrict__ backoff) {
+  __shared__ double smax[256];
+  __shared__ float sdm[3];
+  __shared__ float d1[256], d2[256];
+  __shared__ int i1[256];
+  const int tid = threadIdx.x;
+  double m = 0.0;
+  float a = -1.f, b = -1.f;
+  int ia = 0;
+  for (int j = tid; j < k; j += 256) {
+    m = cn[j] > m ? cn[j] : m;
+    if (have_drift) {
+      const float v = drift[j];
+      if (v > a) { b = a; a = v; ia = j; }
+      else if (v > b) { b = v; }
+    }
+  }
+  smax[tid] = m;
+  d1[tid] = a;
+  d2[tid] = b;
+  i1[tid] = ia;
+  __syncthreads();
+  if (tid == 0) {
+    double mm = 0.0;
+    float ta = -1.f, tb = -1.f;
+    int ti = 0;
+    for (int t = 0; t < 256; ++t) {
+      mm = smax[t] > mm ? smax[t] : mm;
+      if (d1[t] > ta) { tb = ta > d2[t] ? ta : d2[t]; ta = d1[t]; ti = i1[t]; }
+      else { const float c = d1[t]; tb = c > tb ? c : tb; }
+    }
+    smax[0] = mm;
+    *mc = (float)mm;
+    *c2 = (float)(2.0 * (double)tau * ((double)*mx + mm));
+    if (have_drift) {
+      dmax[0] = ta < 0.f ? 0.f : ta;
+      dmax[1] = tb < 0.f ? 0.f : tb;
+      dmax[2] = (float)ti;
+    }
+    sdm[0] = ta < 0.f ? 0.f : ta;
+    sdm[1] = tb < 0.f ? 0.f : tb;
+    sdm[2] = (float)ti;
+    *count = 0;
+    const int bo = backoff != nullptr ? *backoff : 0;
+    *force = bo > 0 ? 1 : 0;
+    if (bo > 0) *backoff = bo - 1;
+  }
+  __syncthreads();
+  const double sl = (double)tau * ((double)*mx + smax[0]);
+  for (int j = tid; j < k; j += 256) {
+    float t;
+    if (k == 1) t = __builtin_huge_valf();
+    else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
+    else t = -__builtin_huge_valf();
+    thr[j] = t;
+    if (have_drift && cum != nullptr) {
+      cum[j] = (cum[j] + drift[j]) * (1.0f + 2.4e-7f);
+      cum[k + j] = (cum[k + j] + (j == (int)sdm[2] ? sdm[1] : sdm[0])) * (1.0f + 2.4e-7f);
+    }
+  }
+}
+
+__global__ __launch_bounds__(256) void kmeans_centre_half_stats_kernel(
+    const u16* __restrict__ cb, long long ldc, int k, int d, const double* __restrict__ cn,
+    double* __restrict__ half, const float* __restrict__ drift, const float* __restrict__ mx, float tau,
+    float* __restrict__ thr, float* __restrict__ dmax, float* __restrict__ mc, float* __restrict__ c2,
+    int* __restrict__ count, int* __restrict__ force, float* __restrict__ cum, int* __restrict__ backoff,
+    int* __restrict__ done_ctr) {
+  extern __shared__ __align__(16) unsigned char smem[];
+  double* cj = reinterpret_cast<double*>(smem);  // [d]
+  __shared__ double red[256];
+  __shared__ int last;
+  const int j = blockIdx.x, tid = threadIdx.x;
+  for (int t = tid; t < d; t += 256) cj[t] = (double)bf16_to_f32(cb[(long long)j * ldc + t]);
+  __syncthreads();
+  double best = __builtin_huge_val();
+  for (int i = tid; i < k; i += 256) {
+    if (i == j) continue;
+    double s = 0.0;
+    for (int t = 0; t < d; ++t) {
+      const double e = (double)bf16_to_f32(cb[(long long)i * ldc + t]) - cj[t];
+      s += e * e;
+    }
+    best = s < best ? s : best;
+  }
+  red[tid] = best;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if (tid < o) red[tid] = red[tid + o] < red[tid] ? red[tid + o] : red[tid];
+    __syncthreads();
+  }
+  if (tid == 0) {
+    half[j] = 0.5 * sqrt(red[0]);
+    __threadfence();  // half[j] visible device-wide before this block counts itself done
+    last = atomicAdd(done_ctr, 1) == k - 1;
+  }
+  __syncthreads();
+  if (!last) return;
+  __threadfence();  // acquire side: every other block's half[] is visible
+  centre_stats2_body(cn, half, drift, k, mx, tau, 1, thr, dmax, mc, c2, count, force, cum, backoff);
+  // re-armed for the next step (stream order: nothing else reads it now)
+  if (tid == 0) __hip_atomic_store(done_ctr, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
 }  // namespace
 
 CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, const float* xn, float mc, float tau,
@@ -454,22 +678,45 @@ CML_API int cml_kmeans_prune_lower(const float* dist, int k, const int* lab, con
 // appended to cand (at most cap entries are written), their number added to *count (zeroed by the
 // caller). dmax = {largest drift,
 // second largest, index of the largest}. lab / ub / lb 16-byte aligned, k <= 8192.
+CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
+                                          const float* thr, const float* c2, int k, long long n, int* cand, int* count,
+                                          const float* xn, int* cand_lab, float* cand_xn, const int* skip,
+                                          long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
+                                          int nback, int* done, void* stream);
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
                                     const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                     const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                     long long cap, const float* cum, void* stream) {
+  return cml_kmeans_prune_bounds_gated(lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn,
+                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, stream);
+}
+
+// The bounds pass with the step gate folded in (mode / gate_cap / backoff / nback as kmeans_prune_gate; done:
+// int32 [1] zero before the first launch, left zero). With n == 0 the gate still runs (one workgroup).
+CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
+                                          const float* thr, const float* c2, int k, long long n, int* cand, int* count,
+                                          const float* xn, int* cand_lab, float* cand_xn, const int* skip,
+                                          long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
+                                          int nback, int* done, void* stream) {
+  if (mode != nullptr && (skip == nullptr || done == nullptr)) return (int)hipErrorInvalidValue;
   if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
     return (int)hipErrorInvalidValue;
   if (cum != nullptr && k > 4096) return (int)hipErrorInvalidValue;  // 4k floats of LDS
   if (k <= 0 || k > 8192 || n < 0 || n >= (1LL << 31) || ((uintptr_t)lab & 15) || ((uintptr_t)ub & 15) ||
       ((uintptr_t)lb & 15))
     return (int)hipErrorInvalidValue;
-  if (n == 0) return 0;
+  if (n == 0) {
+    if (mode == nullptr) return 0;
+    hipLaunchKernelGGL(kmeans_prune_gate_kernel, dim3(1), dim3(1), 0, (hipStream_t)stream, count, gate_cap, skip, mode,
+                       backoff, nback);
+    return cml_status();
+  }
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
+  const GateArgs g{mode, gate_cap, backoff, nback, done};
   hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
                      (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
-                     dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum);
+                     dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum, g);
   return cml_status();
 }
 
@@ -533,5 +780,30 @@ CML_API int cml_kmeans_label_hist(const int* labels, long long n, int tr, int gr
   if (tr <= 0 || tr > 1024 || grid <= 0 || kp <= 0 || (size_t)kp * 4 > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(kmeans_label_hist_kernel, dim3(grid), dim3(1024), (size_t)kp * 4, (hipStream_t)stream, labels,
                      n, tr, kp, hist, rank, gate, want);
+  return cml_status();
+}
+
+// Fused pruned-step tail (see kmeans_update_pdev_kernel / kmeans_centre_half_stats_kernel). bufs: the
+// all-reduced [k·D sums | k counts | cost] rows (nbuf of them); cb / cb_old / cb_cost bf16 [Kp, ldc];
+// flags int32 [2]; cn64 f64 [k]; drift f32 [k].
+CML_API int cml_kmeans_update_pdev(const double* bufs, int nbuf, long long bstride, int k, int D, double* cent,
+                                   void* cb, long long ldc, int Dp, int Kp, float* cnorm, double* shift2, double unit,
+                                   void* cb_old, void* cb_cost, const int* flags, double* cn64, float* drift,
+                                   void* stream) {
+  if (bufs == nullptr || nbuf < 1 || k <= 0 || Kp < k) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_update_pdev_kernel, dim3(Kp), dim3(256), 0, (hipStream_t)stream, bufs, nbuf, bstride, k,
+                     D, cent, (u16*)cb, ldc, Dp, cnorm, shift2, unit, (u16*)cb_old, (u16*)cb_cost, flags, cn64, drift);
+  return cml_status();
+}
+
+// done_ctr: int32 [1], zero before the first launch (each launch leaves it zero).
+CML_API int cml_kmeans_centre_half_stats(const void* cb, long long ldc, int k, int d, const double* cn, double* half,
+                                         const float* drift, const float* mx, float tau, float* thr, float* dmax,
+                                         float* mc, float* c2, int* count, int* force, float* cum, int* backoff,
+                                         int* done_ctr, void* stream) {
+  if (k <= 0 || d <= 0 || d > 8192) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_centre_half_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(double),
+                     (hipStream_t)stream, (const u16*)cb, ldc, k, d, cn, half, drift, mx, tau, thr, dmax, mc, c2,
+                     count, force, cum, backoff, done_ctr);
   return cml_status();
 }

@@ -1074,6 +1074,10 @@ class LloydEngine:
         # holds; CML_KMEANS_LAZY_BOUNDS=0 keeps the absolute bounds rewritten every step
         st.cum = (torch.zeros(2 * k, dtype=torch.float32, device=dev)
                   if os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096 else None)
+        # completion counters of the fused launches (gate in the bounds pass, stats in the half pass); each
+        # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
+        st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
@@ -1098,11 +1102,16 @@ class LloydEngine:
         st, dl = self._pst, self.delta
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
-        K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
-                       xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
-                       cum=st.cum) if n else None
-        K.prune_gate(st.count, st.cap_m, st.flags, st.pmode, backoff=st.backoff if st.nback > 0 else None,
-                     nback=st.nback)
+        if st.fused:  # bounds pass + gate in one launch
+            K.prune_bounds_gated(lab[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
+                                 self.xnorm, st.cand_lab, st.cand_xn, st.flags, st.cum, st.pmode, st.cap_m,
+                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1])
+        else:
+            K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
+                           xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
+                           cum=st.cum) if n else None
+            K.prune_gate(st.count, st.cap_m, st.flags, st.pmode, backoff=st.backoff if st.nback > 0 else None,
+                         nback=st.nback)
         K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
                         st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
@@ -1117,11 +1126,20 @@ class LloydEngine:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
         in a tol > 0 fit, the device convergence latch (flags[1])."""
         st, k, d = self._pst, self.k, self.d
-        # cb_old <- cb, and cb_cost <- cb unless converged (frozen steps keep the last live step's centres)
-        K.cond_copy(st.cb_cost, self.cb, st.flags, dst_always=st.cb_old)
-        self._update_gpu(self.msgs)
-        K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax, st.mc,
-                       st.c2, st.count, st.force, cum=st.cum, backoff=st.backoff if st.nback > 0 else None)
+        if st.fused and not self.spherical:
+            # K11 + cb_old / cb_cost copies + norms + drifts in one launch, then the centre statistics in one
+            K.update_pdev(self.msgs, k, d, self.centers, self.cb, self.dp, self.kp, self.cnorm, self.shift2,
+                          self._unit, st.cb_old, st.cb_cost, st.flags, st.cn, st.drift)
+            self._shift2 = self.shift2
+            K.centre_half_stats(self.cb, k, d, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc,
+                                st.c2, st.count, st.force, st.cum, st.backoff if st.nback > 0 else None,
+                                st.ctr[1:2])
+        else:
+            # cb_old <- cb, and cb_cost <- cb unless converged (frozen steps keep the last live step's centres)
+            K.cond_copy(st.cb_cost, self.cb, st.flags, dst_always=st.cb_old)
+            self._update_gpu(self.msgs)
+            K.centre_stats(self.cb, st.cb_old, k, d, st.mx, st.tau, st.cn, st.half, st.drift, st.thr, st.dmax,
+                           st.mc, st.c2, st.count, st.force, cum=st.cum, backoff=st.backoff if st.nback > 0 else None)
         if self._conv_lim is not None:
             K.converge_latch(self.shift2, k, self._conv_lim, st.flags)
         self._cost_fn = self._device_cost
@@ -1166,10 +1184,14 @@ class LloydEngine:
             K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, None, st.ub, st.lb,
                             st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab, gate=st.pmode,
                             want=0, cum=st.cum)
-            K.label_hist(lab, n, ap, self.hist, self.rank, gate=st.pmode, want=0)
+            if not self._overlap_split(n):
+                K.label_hist(lab, n, ap, self.hist, self.rank, gate=st.pmode, want=0)
         self.cost_part.zero_()
         dl.invalidate()
         dl.gate(0)
+        split = self._overlap_split(n)
+        if split:
+            return self._seeded_accumulate_overlapped(split, msg)
         # the seeded upper bounds (r + d1) are loose; the accumulate streams every row anyway and leaves
         # the exact one, |x - c_label| rounded up, so the next step's bounds prove as many rows as after a
         # full pass (the seeded lower bounds stay: d2 - r is far below what they are compared with)
@@ -1179,6 +1201,48 @@ class LloydEngine:
                           qscale=self._qscale, cum=st.cum)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
         self.comm.allreduce_async(msg).wait()
+        self._pdev_post()
+
+    def _overlap_split(self, n: int):
+        """Row ranges of the overlapped full accumulate of the seeded step: two chunks
+        whose sums are all-reduced separately, chunk 0's collective running on the process group's stream
+        while chunk 1 accumulates. Multi-rank engines with at least CML_KMEANS_OVERLAP_ROWS local rows
+        (default 4M: the accumulate then takes ~0.5 ms, well above the extra launches); None otherwise."""
+        if not self.comm.is_distributed:
+            return None
+        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))
+        if lim <= 0 or n < max(lim, 2):
+            return None
+        mid = min(n - 1, max(1, round_up(n // 2, 1024)))
+        return ((0, mid), (mid, n))
+
+    def _seeded_accumulate_overlapped(self, split, msg: torch.Tensor) -> None:
+        """The seeded step's full accumulate in two row chunks, each counting-sorted in its own K9r
+        geometry (label_hist) and summed into its own message; chunk 0's all-reduce is enqueued before
+        chunk 1's accumulate, so it overlaps it. The chunk sums are exact (grid sums: _sum_grid), so their
+        sum is the one-chunk message bit for bit; the incremental-sums state gets the local total."""
+        st, dl, ap = self._pst, self.delta, self.aplan
+        k, d, dp, x, lab = self.k, self.d, self.dp, self.x, self.labels
+        if getattr(self, "_msgs2", None) is None:
+            self._msgs2 = torch.empty((2, self.msg_len), dtype=torch.float64, device=self.device)
+            self._hist2 = torch.empty_like(self.hist)
+        handles = []
+        for c, (r0, r1) in enumerate(split):
+            nc = r1 - r0
+            hist_c = self.hist if c == 0 else self._hist2
+            K.label_hist(lab[r0:r1], nc, ap, hist_c, self.rank[r0:r1])
+            K.accumulate_sort(x[r0:r1], nc, dp, d, lab[r0:r1], self.rank[r0:r1], hist_c, ap, k, self.cost_part,
+                              self.off, self.seg, self.perm, self.cplan, self._msgs2[c], self.slots,
+                              ub_centres=self.cb if self._seed_ub else None,
+                              ub=st.ub[r0:r1] if self._seed_ub else None, qscale=self._qscale, cum=st.cum)
+            if c == 0:
+                dl.acc[0].copy_(self._msgs2[0])  # local sums (before the in-place all-reduce)
+            else:
+                dl.acc[0].add_(self._msgs2[1])
+            handles.append(self.comm.allreduce_async(self._msgs2[c]))
+        for h in handles:
+            h.wait()
+        torch.add(self._msgs2[0], self._msgs2[1], out=msg)
         self._pdev_post()
 
     def _norms64(self) -> torch.Tensor:
@@ -1854,7 +1918,11 @@ class LloydEngine:
                 dst[:m].copy_(self._rows_f64(chosen))
             if send is not None:
                 pad = max(max(counts), 1)
-                gath = comm.allgather_fixed(send[:pad].contiguous())
+                if send.shape[0] < pad:  # (a small shard's buffer is sized by its own rows: every rank sends pad)
+                    grown = torch.zeros((pad, d), dtype=torch.float64, device=dev)
+                    grown[:m].copy_(send[:m])
+                    send = grown
+                gath = comm.allgather_fixed(send[:pad])
                 at = ncand
                 for r in range(comm.world_size):
                     if counts[r]:

@@ -15,7 +15,7 @@ from dataclasses import dataclass
 import torch
 
 from .. import _native
-from .._native import c_int, c_ll, c_vp
+from .._native import c_dbl, c_int, c_ll, c_vp
 from ..utils.device import LDS_BUDGET, num_cus, round_up
 
 _native.register_kernel_sigs({
@@ -112,6 +112,13 @@ _native.register_kernel_sigs({
     "cml_kmeans_sum_dd": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_pair_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_prune_bounds_gated": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp, c_vp,
+                                              c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
+                                              c_vp]),
+    "cml_kmeans_update_pdev": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
+                                       c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_centre_half_stats": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp,
+                                             c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_gather_rank_rows": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_int, c_int, c_vp]),
     "cml_kmeans_gather_rank_max": (c_int, []),
     "cml_kmeans_seed_table": (c_int, [c_vp, c_int, c_int, c_vp, c_ll, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
@@ -674,6 +681,44 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
                                                           rank.data_ptr(), _ptr(gate), int(want),
                                                           _native.stream_ptr(stream)),
                   "kmeans_label_hist")
+
+
+def prune_bounds_gated(labels, ub, lb, drift, dmax, thr, c2, k: int, cand, count, xn, cand_lab, cand_xn, flags,
+                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None) -> None:
+    """K9p with the step gate folded in (kmeans_prune.hip): the bounds pass (skipped when flags[0] / flags[1]
+    are set) and, in the workgroup that finishes last, kmeans_prune_gate's decision into ``mode``; ``done``
+    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics."""
+    n = int(labels.shape[0])
+    _native.check(_native.kernels().cml_kmeans_prune_bounds_gated(
+        labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
+        c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
+        flags.data_ptr(), int(cand.shape[0]), _ptr(cum), mode.data_ptr(), int(gate_cap), _ptr(backoff), int(nback),
+        done.data_ptr(), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
+
+
+def update_pdev(msgs: torch.Tensor, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int, kp: int,
+                cnorm: torch.Tensor, shift2: torch.Tensor, unit: float, cb_old: torch.Tensor, cb_cost: torch.Tensor,
+                flags: torch.Tensor, cn64: torch.Tensor, drift: torch.Tensor, stream=None) -> None:
+    """K11 of the device pruned step with its bookkeeping in the same launch (kmeans_prune.hip
+    kmeans_update_pdev_kernel): cb_old <- old cb, cb_cost <- old cb unless frozen (flags[1]), the new centres,
+    their bf16 copy and norms (f32 cnorm, f64 cn64), the shift and the bf16 drift rounded up."""
+    _native.check(_native.kernels().cml_kmeans_update_pdev(
+        msgs.data_ptr(), msgs.shape[0], msgs.stride(0), int(k), int(d), cent.data_ptr(), cb.data_ptr(), cb.stride(0),
+        int(dp), int(kp), cnorm.data_ptr(), shift2.data_ptr(), float(unit), cb_old.data_ptr(), cb_cost.data_ptr(),
+        flags.data_ptr(), cn64.data_ptr(), drift.data_ptr(), _native.stream_ptr(stream)), "kmeans_update_pdev")
+
+
+def centre_half_stats(cb: torch.Tensor, k: int, d: int, cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor,
+                      mx: torch.Tensor, tau: float, thr, dmax, mc, c2, count, force, cum, backoff, done,
+                      stream=None) -> None:
+    """The pruned step's centre statistics in one launch (kmeans_centre_half_stats_kernel): half nearest-centre
+    distances, then — in the workgroup that finishes last — thr, dmax, mc, c2, the cumulative drifts and the
+    count / force / backoff resets (norms and drifts come from update_pdev). ``done``: int32 [1], zero."""
+    _native.check(_native.kernels().cml_kmeans_centre_half_stats(
+        cb.data_ptr(), cb.stride(0), int(k), int(d), cn.data_ptr(), half.data_ptr(), drift.data_ptr(), mx.data_ptr(),
+        float(tau), thr.data_ptr(), dmax.data_ptr(), mc.data_ptr(), c2.data_ptr(), count.data_ptr(),
+        force.data_ptr(), _ptr(cum), _ptr(backoff), done.data_ptr(), _native.stream_ptr(stream)),
+        "kmeans_centre_half_stats")
 
 
 def prune_gate(count: torch.Tensor, cap: int, flags: torch.Tensor, mode: torch.Tensor, stream=None,

@@ -133,13 +133,16 @@ def _rank_main2(rank, world, port, out_path, use_graph=True):
     dist.destroy_process_group()
 
 
-@pytest.mark.parametrize("use_graph", [False, True])
-def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch, use_graph):
+@pytest.mark.parametrize("use_graph,overlap", [(False, False), (True, False), (False, True)])
+def test_two_ranks_default_path_match_single_rank(tmp_path, monkeypatch, use_graph, overlap):
     """Two ranks on the default GPU path (pruned init, seeded step, eager pruned steps around the
     all-reduce — or split graphs) give the single-rank fit bit for bit: init centres, final centres and
-    cost (1/8-grid data: every f64 sum is exact)."""
+    cost (1/8-grid data: every f64 sum is exact). ``overlap``: the seeded step's full accumulate in two
+    chunks whose all-reduces overlap the next chunk (forced on at this size) — the same bits."""
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
     monkeypatch.setenv("CML_KMEANS_PRUNE", "1")
+    if overlap:
+        monkeypatch.setenv("CML_KMEANS_OVERLAP_ROWS", "1")
     out = str(tmp_path / "w2d.json")
     ctx = mp.get_context("spawn")
     port = _free_port()
