@@ -11,10 +11,10 @@
 //                     by direct differences in f64, rounded outward, and ||p||² rounded up: the tables the
 //                     first Lloyd step's seeded bounds read (kmeans_seed_bounds_kernel). Replaces an f64
 //                     GEMM, a top-k and ~25 elementwise ops.
-//   pair_table        init_table's sorted candidate-distance rows with coalesced loads: two existing
-//                     candidates per workgroup, each wave streams whole new-candidate rows (64 lanes x 4
-//                     columns) and reduces with shuffles — the per-thread row walks of the first version
-//                     read 2-KB strided columns (300 us for 513 x 512 candidates at D = 256).
+//   pair_table        init_table's sorted candidate-distance rows with coalesced loads: the new candidates
+//                     transposed, four existing candidates per workgroup, a thread per new candidate — the
+//                     first version's per-thread row walks read 2-KB strided columns (300 us for 513 x 512
+//                     candidates at D = 256).
 #include "common.h"
 
 namespace {
@@ -129,60 +129,72 @@ __global__ __launch_bounds__(kGThreads) void seed_table_kernel(const double* __r
   }
 }
 
-// init_table with coalesced row reads (see the file comment): PB existing candidates per workgroup.
+// init_table with coalesced reads (see the file comment): the new candidates come TRANSPOSED (YT [d][m]),
+// thread t owns candidates t, t+256, ... (up to 4), every step c reads one contiguous run YT[c][*] across
+// the block and the kPB existing candidates' values from LDS; each (p, y) distance is one serial f64 fold.
 constexpr int kTabMax = 1024;
-constexpr int kPB = 2;
+constexpr int kPB = 4;
+constexpr int kJPT = kTabMax / kGThreads;
 __global__ __launch_bounds__(kGThreads) void pair_table_kernel(const double* __restrict__ P, int mp,
-                                                               const double* __restrict__ Y, int m, int d,
+                                                               const double* __restrict__ YT, int m, int d,
                                                                float* __restrict__ tab_v, int* __restrict__ tab_j,
                                                                float* __restrict__ pn32) {
   extern __shared__ double sp[];  // [kPB][d]
   __shared__ float key[kPB][kTabMax];
   __shared__ int id[kPB][kTabMax];
-  const int i0 = blockIdx.x * kPB, lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
+  const int i0 = blockIdx.x * kPB, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int np = min(kPB, mp - i0);
-  for (int e = threadIdx.x; e < kPB * d; e += kGThreads) {
+  for (int e = tid; e < kPB * d; e += kGThreads) {
     const int r = e / d, t = e - r * d;
     sp[e] = r < np ? P[(long long)(i0 + r) * d + t] : 0.0;
   }
-  int mm = 1;
-  while (mm < m) mm <<= 1;
   __syncthreads();
-  for (int j = wave; j < mm; j += kGThreads / 64) {
-    double acc[kPB];
+  double acc[kPB][kJPT];
 #pragma unroll
-    for (int r = 0; r < kPB; ++r) acc[r] = 0.0;
-    if (j < m) {
-      const double* y = Y + (long long)j * d;
-      for (int t = lane; t < d; t += 64) {
-        const double yv = y[t];
+  for (int r = 0; r < kPB; ++r)
 #pragma unroll
-        for (int r = 0; r < kPB; ++r) {
-          const double e = sp[r * d + t] - yv;
-          acc[r] = __fma_rn(e, e, acc[r]);
-        }
-      }
+    for (int q = 0; q < kJPT; ++q) acc[r][q] = 0.0;
+#pragma unroll 4
+  for (int c = 0; c < d; ++c) {
+    double y[kJPT];
+#pragma unroll
+    for (int q = 0; q < kJPT; ++q) {
+      const int j = tid + q * kGThreads;
+      y[q] = j < m ? YT[(long long)c * m + j] : 0.0;
     }
 #pragma unroll
     for (int r = 0; r < kPB; ++r) {
-      const double a = wave_sum_f64(acc[r]);
-      if (lane == 0) {
-        float kv = __builtin_huge_valf();
-        if (j < m) {
-          const double rr = sqrt(a) * (1.0 - 1e-6);
-          kv = (float)rr;
-          if ((double)kv > rr) kv = nextafterf(kv, 0.0f);
-        }
-        key[r][j] = kv;
-        id[r][j] = j;
+      const double pv = sp[r * d + c];
+#pragma unroll
+      for (int q = 0; q < kJPT; ++q) {
+        const double e = pv - y[q];
+        acc[r][q] = __fma_rn(e, e, acc[r][q]);
       }
+    }
+  }
+  int mm = 1;
+  while (mm < m) mm <<= 1;
+#pragma unroll
+  for (int q = 0; q < kJPT; ++q) {
+    const int j = tid + q * kGThreads;
+    if (j >= mm) continue;
+#pragma unroll
+    for (int r = 0; r < kPB; ++r) {
+      float kv = __builtin_huge_valf();
+      if (j < m) {
+        const double rr = sqrt(acc[r][q]) * (1.0 - 1e-6);
+        kv = (float)rr;
+        if ((double)kv > rr) kv = nextafterf(kv, 0.0f);
+      }
+      key[r][j] = kv;
+      id[r][j] = j;
     }
   }
   __syncthreads();
   // bitonic sort of each row's (key, id) ascending, ties by id
   for (int size = 2; size <= mm; size <<= 1) {
     for (int stride = size >> 1; stride > 0; stride >>= 1) {
-      for (int e = threadIdx.x; e < kPB * mm; e += kGThreads) {
+      for (int e = tid; e < kPB * mm; e += kGThreads) {
         const int r = e / mm, t = e - r * mm;
         const int o = t ^ stride;
         if (o > t) {
@@ -202,7 +214,7 @@ __global__ __launch_bounds__(kGThreads) void pair_table_kernel(const double* __r
     }
   }
   for (int r = 0; r < np; ++r) {
-    for (int j = threadIdx.x; j < m; j += kGThreads) {
+    for (int j = tid; j < m; j += kGThreads) {
       tab_v[(long long)(i0 + r) * m + j] = key[r][j];
       tab_j[(long long)(i0 + r) * m + j] = id[r][j];
     }
@@ -243,12 +255,13 @@ CML_API int cml_kmeans_seed_table(const double* U, int m, int d, const void* cb,
   return cml_status();
 }
 
-// P f64 [mp, d], Y f64 [m, d] (m <= 1024); tab_v f32 / tab_j int32 [mp, m]; pn32 f32 [mp].
-CML_API int cml_kmeans_pair_table(const double* P, int mp, const double* Y, int m, int d, float* tab_v, int* tab_j,
+// P f64 [mp, d], YT f64 [d, m] (the new candidates transposed, m <= 1024); tab_v f32 / tab_j int32 [mp, m];
+// pn32 f32 [mp].
+CML_API int cml_kmeans_pair_table(const double* P, int mp, const double* YT, int m, int d, float* tab_v, int* tab_j,
                                   float* pn32, void* stream) {
   if (mp <= 0 || m <= 0) return 0;
-  if (d <= 0 || m > kTabMax || (size_t)kPB * d * 8 > 48 * 1024) return (int)hipErrorInvalidValue;
+  if (d <= 0 || m > kTabMax || (size_t)kPB * d * 8 > 64 * 1024) return (int)hipErrorInvalidValue;
   hipLaunchKernelGGL(pair_table_kernel, dim3((unsigned)((mp + kPB - 1) / kPB)), dim3(kGThreads),
-                     (size_t)kPB * d * 8, (hipStream_t)stream, P, mp, Y, m, d, tab_v, tab_j, pn32);
+                     (size_t)kPB * d * 8, (hipStream_t)stream, P, mp, YT, m, d, tab_v, tab_j, pn32);
   return cml_status();
 }

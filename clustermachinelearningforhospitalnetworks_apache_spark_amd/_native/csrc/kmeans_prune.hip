@@ -627,20 +627,32 @@ __global__ __launch_bounds__(256) void kmeans_centre_half_stats_kernel(
     int* __restrict__ count, int* __restrict__ force, float* __restrict__ cum, int* __restrict__ backoff,
     int* __restrict__ done_ctr) {
   extern __shared__ __align__(16) unsigned char smem[];
-  double* cj = reinterpret_cast<double*>(smem);  // [d]
-  __shared__ double red[256];
+  float* cj = reinterpret_cast<float*>(smem);  // [d] (d a multiple of 8: the padded bf16 rows)
+  __shared__ float red[256];
   __shared__ int last;
   const int j = blockIdx.x, tid = threadIdx.x;
-  for (int t = tid; t < d; t += 256) cj[t] = (double)bf16_to_f32(cb[(long long)j * ldc + t]);
+  for (int t = tid; t < d; t += 256) cj[t] = bf16_to_f32(cb[(long long)j * ldc + t]);
   __syncthreads();
-  double best = __builtin_huge_val();
+  // f32 direct differences (each difference of two bf16 values is exact in f32), 16-byte row reads; the
+  // sum of d rounded squares is within d·2^-24 of the real one, so the result is scaled down by 1 - 4e-5
+  // (d <= 2048) — half_j stays below half the real distance, as the pruning threshold needs
+  float best = __builtin_huge_valf();
   for (int i = tid; i < k; i += 256) {
     if (i == j) continue;
-    double s = 0.0;
-    for (int t = 0; t < d; ++t) {
-      const double e = (double)bf16_to_f32(cb[(long long)i * ldc + t]) - cj[t];
-      s += e * e;
+    const uint4* row = reinterpret_cast<const uint4*>(cb + (long long)i * ldc);
+    float s0 = 0.f, s1 = 0.f;
+    for (int t8 = 0; t8 < (d >> 3); ++t8) {
+      const uint4 w = row[t8];
+      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const float e0 = __uint_as_float(ws[q] << 16) - cj[8 * t8 + 2 * q];
+        const float e1 = __uint_as_float(ws[q] & 0xffff0000u) - cj[8 * t8 + 2 * q + 1];
+        s0 = fmaf(e0, e0, s0);
+        s1 = fmaf(e1, e1, s1);
+      }
     }
+    const float s = s0 + s1;
     best = s < best ? s : best;
   }
   red[tid] = best;
@@ -650,7 +662,7 @@ __global__ __launch_bounds__(256) void kmeans_centre_half_stats_kernel(
     __syncthreads();
   }
   if (tid == 0) {
-    half[j] = 0.5 * sqrt(red[0]);
+    half[j] = 0.5 * sqrt((double)red[0] * (1.0 - 4e-5));
     __threadfence();  // half[j] visible device-wide before this block counts itself done
     last = atomicAdd(done_ctr, 1) == k - 1;
   }
@@ -801,8 +813,8 @@ CML_API int cml_kmeans_centre_half_stats(const void* cb, long long ldc, int k, i
                                          const float* drift, const float* mx, float tau, float* thr, float* dmax,
                                          float* mc, float* c2, int* count, int* force, float* cum, int* backoff,
                                          int* done_ctr, void* stream) {
-  if (k <= 0 || d <= 0 || d > 8192) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeans_centre_half_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(double),
+  if (k <= 0 || d <= 0 || d > 2048 || (d & 7) || (ldc & 7) || ((uintptr_t)cb & 15)) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_centre_half_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(float),
                      (hipStream_t)stream, (const u16*)cb, ldc, k, d, cn, half, drift, mx, tau, thr, dmax, mc, c2,
                      count, force, cum, backoff, done_ctr);
   return cml_status();

@@ -1126,12 +1126,12 @@ class LloydEngine:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
         in a tol > 0 fit, the device convergence latch (flags[1])."""
         st, k, d = self._pst, self.k, self.d
-        if st.fused and not self.spherical:
+        if st.fused and not self.spherical and self.dp <= 2048:
             # K11 + cb_old / cb_cost copies + norms + drifts in one launch, then the centre statistics in one
             K.update_pdev(self.msgs, k, d, self.centers, self.cb, self.dp, self.kp, self.cnorm, self.shift2,
                           self._unit, st.cb_old, st.cb_cost, st.flags, st.cn, st.drift)
             self._shift2 = self.shift2
-            K.centre_half_stats(self.cb, k, d, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc,
+            K.centre_half_stats(self.cb, k, self.dp, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc,
                                 st.c2, st.count, st.force, st.cum, st.backoff if st.nback > 0 else None,
                                 st.ctr[1:2])
         else:

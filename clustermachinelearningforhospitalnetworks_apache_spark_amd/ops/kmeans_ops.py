@@ -852,9 +852,15 @@ def init_table(P: torch.Tensor, Y: torch.Tensor, stream=None):
     pn32 = torch.empty(mp, dtype=torch.float32, device=P.device)
     lib = _native.kernels()
     # the coalesced two-rows-per-workgroup form (kmeans_init_fast.hip) where its LDS fits, else the first one
-    fn = lib.cml_kmeans_pair_table if d <= 3072 else lib.cml_kmeans_init_table
-    _native.check(fn(P.data_ptr(), mp, Y.data_ptr(), m, d, tab_v.data_ptr(), tab_j.data_ptr(), pn32.data_ptr(),
-                     _native.stream_ptr(stream)), "kmeans_init_table")
+    if d <= 2048:  # the transposed, coalesced form (kmeans_init_fast.hip) where its LDS fits
+        YT = Y.t().contiguous()
+        _native.check(lib.cml_kmeans_pair_table(P.data_ptr(), mp, YT.data_ptr(), m, d, tab_v.data_ptr(),
+                                                tab_j.data_ptr(), pn32.data_ptr(), _native.stream_ptr(stream)),
+                      "kmeans_pair_table")
+    else:
+        _native.check(lib.cml_kmeans_init_table(P.data_ptr(), mp, Y.data_ptr(), m, d, tab_v.data_ptr(),
+                                                tab_j.data_ptr(), pn32.data_ptr(), _native.stream_ptr(stream)),
+                      "kmeans_init_table")
     return tab_v, tab_j, pn32
 
 
