@@ -53,7 +53,10 @@ __device__ __forceinline__ bool bound_step(int a, float& u, float& w, const floa
 
 // The pruned step's gate (kmeans_prune_gate_kernel's body): one thread.
 __device__ __forceinline__ void prune_gate_body(int* __restrict__ count, long long cap, const int* __restrict__ flags,
-                                                int* __restrict__ mode, int* __restrict__ backoff, int nback) {
+                                                int* __restrict__ mode, int* __restrict__ backoff, int nback,
+                                                int* __restrict__ zero = nullptr) {
+  // zero: a counter the step's later launches count into (the fp8 screen's uncertified rows), re-armed here
+  if (zero != nullptr) __hip_atomic_store(zero, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   if (flags[1] != 0) {
     mode[0] = 0;
     mode[1] = 0;
@@ -77,6 +80,7 @@ struct GateArgs {
   int* backoff;
   int nback;
   int* done;
+  int* zero = nullptr;  // re-armed by the gate (prune_gate_body)
 };
 
 __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
@@ -98,7 +102,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   // converged and the step is a frozen no-op (kmeans_prune_gate_kernel)
   if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) {
     if (gate.mode != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.zero);
     return;
   }
   extern __shared__ __align__(16) unsigned char smem[];
@@ -216,7 +220,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
     // no fence: the gate reads only the count, which every block changed by an atomic whose result it
     // waited for (base above) before this completion atomic — device-scope atomics in issue order
     if (threadIdx.x == 0 && atomicAdd(gate.done, 1) == (int)gridDim.x - 1) {
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.zero);
       __hip_atomic_store(gate.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -346,11 +350,13 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
   __shared__ float sdm[3];
   __shared__ float d1[256], d2[256];
   __shared__ int i1[256];
+  // the first 256 threads of the workgroup do the work (callers run 256 or more threads; all reach the barriers)
   const int tid = threadIdx.x;
+  const bool act = tid < 256;
   double m = 0.0;
   float a = -1.f, b = -1.f;
   int ia = 0;
-  for (int j = tid; j < k; j += 256) {
+  for (int j = tid; act && j < k; j += 256) {
     m = cn[j] > m ? cn[j] : m;
     if (have_drift) {
       const float v = drift[j];
@@ -358,10 +364,12 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
       else if (v > b) { b = v; }
     }
   }
-  smax[tid] = m;
-  d1[tid] = a;
-  d2[tid] = b;
-  i1[tid] = ia;
+  if (act) {
+    smax[tid] = m;
+    d1[tid] = a;
+    d2[tid] = b;
+    i1[tid] = ia;
+  }
   __syncthreads();
   if (tid == 0) {
     double mm = 0.0;
@@ -393,7 +401,7 @@ __global__ __launch_bounds__(256) void kmeans_centre_stats2_kernel(const double*
   }
   __syncthreads();
   const double sl = (double)tau * ((double)*mx + smax[0]);
-  for (int j = tid; j < k; j += 256) {
+  for (int j = tid; act && j < k; j += 256) {
     float t;
     if (k == 1) t = __builtin_huge_valf();
     else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
@@ -563,11 +571,13 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, const double* 
   __shared__ float sdm[3];
   __shared__ float d1[256], d2[256];
   __shared__ int i1[256];
+  // the first 256 threads of the workgroup do the work (callers run 256 or more threads; all reach the barriers)
   const int tid = threadIdx.x;
+  const bool act = tid < 256;
   double m = 0.0;
   float a = -1.f, b = -1.f;
   int ia = 0;
-  for (int j = tid; j < k; j += 256) {
+  for (int j = tid; act && j < k; j += 256) {
     m = cn[j] > m ? cn[j] : m;
     if (have_drift) {
       const float v = drift[j];
@@ -575,10 +585,12 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, const double* 
       else if (v > b) { b = v; }
     }
   }
-  smax[tid] = m;
-  d1[tid] = a;
-  d2[tid] = b;
-  i1[tid] = ia;
+  if (act) {
+    smax[tid] = m;
+    d1[tid] = a;
+    d2[tid] = b;
+    i1[tid] = ia;
+  }
   __syncthreads();
   if (tid == 0) {
     double mm = 0.0;
@@ -607,7 +619,7 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, const double* 
   }
   __syncthreads();
   const double sl = (double)tau * ((double)*mx + smax[0]);
-  for (int j = tid; j < k; j += 256) {
+  for (int j = tid; act && j < k; j += 256) {
     float t;
     if (k == 1) t = __builtin_huge_valf();
     else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
@@ -620,7 +632,9 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, const double* 
   }
 }
 
-__global__ __launch_bounds__(256) void kmeans_centre_half_stats_kernel(
+constexpr int kHalfThreads = 1024;
+
+__global__ __launch_bounds__(kHalfThreads) void kmeans_centre_half_stats_kernel(
     const u16* __restrict__ cb, long long ldc, int k, int d, const double* __restrict__ cn,
     double* __restrict__ half, const float* __restrict__ drift, const float* __restrict__ mx, float tau,
     float* __restrict__ thr, float* __restrict__ dmax, float* __restrict__ mc, float* __restrict__ c2,
@@ -628,38 +642,66 @@ __global__ __launch_bounds__(256) void kmeans_centre_half_stats_kernel(
     int* __restrict__ done_ctr) {
   extern __shared__ __align__(16) unsigned char smem[];
   float* cj = reinterpret_cast<float*>(smem);  // [d] (d a multiple of 8: the padded bf16 rows)
-  __shared__ float red[256];
+  __shared__ float red[kHalfThreads / 64];
   __shared__ int last;
-  const int j = blockIdx.x, tid = threadIdx.x;
-  for (int t = tid; t < d; t += 256) cj[t] = bf16_to_f32(cb[(long long)j * ldc + t]);
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  for (int t = tid; t < d; t += kHalfThreads) cj[t] = bf16_to_f32(cb[(long long)j * ldc + t]);
   __syncthreads();
-  // f32 direct differences (each difference of two bf16 values is exact in f32), 16-byte row reads; the
-  // sum of d rounded squares is within d·2^-24 of the real one, so the result is scaled down by 1 - 4e-5
-  // (d <= 2048) — half_j stays below half the real distance, as the pruning threshold needs
+  // f32 direct differences (each difference of two bf16 values is exact in f32); the sum of d rounded
+  // squares is within d·2^-24 of the real one, so the result is scaled down by 1 - 4e-5 (d <= 2048) —
+  // half_j stays below half the real distance, as the pruning threshold needs.
+  // L lanes (a power of two) share a row, each reading 16-B chunks c ≡ sub (mod L): coalesced row reads,
+  // 64/L rows per wave instruction, two row groups in flight per lane, then an xor-shuffle sum.
+  const int nch = d >> 3;
+  int L = 1;
+  while (2 * L <= nch && 2 * L <= 64) L *= 2;
+  const int rp = 64 / L, sub = lane & (L - 1), rw = lane / L;
+  const int step = (kHalfThreads / 64) * rp;  // rows per block pass
   float best = __builtin_huge_valf();
-  for (int i = tid; i < k; i += 256) {
-    if (i == j) continue;
-    const uint4* row = reinterpret_cast<const uint4*>(cb + (long long)i * ldc);
-    float s0 = 0.f, s1 = 0.f;
-    for (int t8 = 0; t8 < (d >> 3); ++t8) {
-      const uint4 w = row[t8];
-      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+  for (int i0 = wave * rp + rw; i0 < k; i0 += 2 * step) {
+    float s[2];
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const float e0 = __uint_as_float(ws[q] << 16) - cj[8 * t8 + 2 * q];
-        const float e1 = __uint_as_float(ws[q] & 0xffff0000u) - cj[8 * t8 + 2 * q + 1];
-        s0 = fmaf(e0, e0, s0);
-        s1 = fmaf(e1, e1, s1);
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      float s0 = 0.f, s1 = 0.f;
+      if (i < k) {
+        const uint4* row = reinterpret_cast<const uint4*>(cb + (long long)i * ldc);
+        for (int c = sub; c < nch; c += L) {
+          const uint4 w = row[c];
+          const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+          for (int q = 0; q < 4; ++q) {
+            const float e0 = __uint_as_float(ws[q] << 16) - cj[8 * c + 2 * q];
+            const float e1 = __uint_as_float(ws[q] & 0xffff0000u) - cj[8 * c + 2 * q + 1];
+            s0 = fmaf(e0, e0, s0);
+            s1 = fmaf(e1, e1, s1);
+          }
+        }
+      }
+      s[u] = s0 + s1;
+    }
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      if (o < L) {
+        s[0] += __shfl_xor(s[0], o, 64);
+        s[1] += __shfl_xor(s[1], o, 64);
       }
     }
-    const float s = s0 + s1;
-    best = s < best ? s : best;
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const int i = i0 + u * step;
+      if (i < k && i != j) best = s[u] < best ? s[u] : best;
+    }
   }
-  red[tid] = best;
+#pragma unroll
+  for (int o = 1; o < 64; o <<= 1) {
+    const float v = __shfl_xor(best, o, 64);
+    best = v < best ? v : best;
+  }
+  if (lane == 0) red[wave] = best;
   __syncthreads();
-  for (int o = 128; o > 0; o >>= 1) {
-    if (tid < o) red[tid] = red[tid + o] < red[tid] ? red[tid + o] : red[tid];
-    __syncthreads();
+  if (tid == 0) {
+    for (int w = 1; w < kHalfThreads / 64; ++w) red[0] = red[w] < red[0] ? red[w] : red[0];
   }
   if (tid == 0) {
     half[j] = 0.5 * sqrt((double)red[0] * (1.0 - 4e-5));
@@ -694,13 +736,13 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, void* stream);
+                                          int nback, int* done, int* zero, void* stream);
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
                                     const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                     const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                     long long cap, const float* cum, void* stream) {
   return cml_kmeans_prune_bounds_gated(lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn,
-                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, stream);
+                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, nullptr, stream);
 }
 
 // The bounds pass with the step gate folded in (mode / gate_cap / backoff / nback as kmeans_prune_gate; done:
@@ -709,7 +751,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, void* stream) {
+                                          int nback, int* done, int* zero, void* stream) {
   if (mode != nullptr && (skip == nullptr || done == nullptr)) return (int)hipErrorInvalidValue;
   if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
     return (int)hipErrorInvalidValue;
@@ -725,7 +767,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
   }
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
-  const GateArgs g{mode, gate_cap, backoff, nback, done};
+  const GateArgs g{mode, gate_cap, backoff, nback, done, zero};
   hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
                      (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
                      dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum, g);
@@ -814,7 +856,7 @@ CML_API int cml_kmeans_centre_half_stats(const void* cb, long long ldc, int k, i
                                          float* mc, float* c2, int* count, int* force, float* cum, int* backoff,
                                          int* done_ctr, void* stream) {
   if (k <= 0 || d <= 0 || d > 2048 || (d & 7) || (ldc & 7) || ((uintptr_t)cb & 15)) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeans_centre_half_stats_kernel, dim3(k), dim3(256), (size_t)d * sizeof(float),
+  hipLaunchKernelGGL(kmeans_centre_half_stats_kernel, dim3(k), dim3(kHalfThreads), (size_t)d * sizeof(float),
                      (hipStream_t)stream, (const u16*)cb, ldc, k, d, cn, half, drift, mx, tau, thr, dmax, mc, c2,
                      count, force, cum, backoff, done_ctr);
   return cml_status();

@@ -79,6 +79,23 @@ struct Ext {
   float* mcost = nullptr;
   int* mnear = nullptr;
   int moff = 0;
+  // MODE 3 (fp8 screen, kmeans_mx.hip): hi/lo e4m3 centre operands in lane order, their E8M0 scales, |~c|²
+  // and |~c - cb| per centre (mx_stat)
+  const unsigned char* mx_c = nullptr;
+  const int* mx_s = nullptr;
+  const float* cn_t = nullptr;
+  const float* mx_stat = nullptr;
+  // MODE 3: the rows the screen cannot certify -> (row, old label, |x|²) at positions counted by *u_cnt
+  // (entries past u_cap are not written: the caller's fallback runs the full bf16 pass then)
+  int* u_idx = nullptr;
+  int* u_lab = nullptr;
+  float* u_xn = nullptr;
+  int* u_cnt = nullptr;
+  long long u_cap = 0;
+  // second gate: with gate2 != null the launch runs only when (*gate2 <= g2cap) == (g2le != 0)
+  const int* gate2 = nullptr;
+  long long g2cap = 0;
+  int g2le = 0;
 };
 
 __host__ __device__ constexpr int cn_slots(int kp) { return ((kp + 3) & ~3) > 256 ? ((kp + 3) & ~3) : 256; }
@@ -414,6 +431,138 @@ __device__ __forceinline__ void compute_m32(const u16* __restrict__ C, long long
   barrier();  // B(nt)
 }
 
+// MODE 3 compute waves (fp8 rows, the screen pass): the e4m3 X bytes go straight into
+// v_mfma_scale_f32_16x16x128_f8f6f4 as the B operand (no widening), against the hi/lo e4m3 split of the
+// centres (kmeans_mx.hip) in VGPRs: per 128-k block two MX MFMAs (hi, lo) per centre tile, each at twice the
+// bf16 rate, so the MFMA time of the bf16 pass with none of its conversion work. Lane (r, g) of block b
+// reads the 16-B units 2b and 2b + 1 of the K9r fp8 order (chunks 8b + g and 8b + 4 + g of row r), the
+// 32 bytes of its MX lane; the centre operands follow the same order. Accumulators start at |~c|² + |x|².
+// Keys and the exchange are those of the 16x16 bf16 path (TOP-2).
+typedef int mx_v8i __attribute__((ext_vector_type(8)));
+
+template <int DP, int CT>
+__device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt, int wave, int lane,
+                                           unsigned char* smem, int dbg) {
+  using G = Geo<DP, true, 3, false>;
+  constexpr int NB = DP / 128;          // MX k-blocks per row
+  constexpr int UPS = 2 * NB;           // 16-B read units per 16-row sub-tile
+  constexpr int NU = G::NSUB * UPS;
+  constexpr int TAGB = 2 + (CT > 1) + (CT > 2) + (CT > 4);
+  constexpr int TAGM = (1 << TAGB) - 1;
+  constexpr int PF = 4;                 // units read ahead (two blocks)
+  constexpr int RING = PF + 2;          // a block's first unit stays live while its second lands
+  static_assert(DP % 128 == 0, "MX blocks");
+  unsigned char* trail = smem + G::NS * G::SLOT;
+  int* red = reinterpret_cast<int*>(trail + G::NTR * G::TRB);
+  const int r = lane & 15, g = lane >> 4;
+  const int cw0 = wave * CT * 16;
+  mx_v8i chi[CT][NB], clo[CT][NB];
+  int csc[CT][NB];
+  f32x4 c4[CT];
+#pragma unroll
+  for (int ct = 0; ct < CT; ++ct) {
+    const int c = cw0 + ct * 16 + r;
+#pragma unroll
+    for (int b = 0; b < NB; ++b) {
+      uint4 q[4] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u),
+                    make_uint4(0u, 0u, 0u, 0u)};
+      int sc = 127 | (127 << 8);
+      if (c < kc) {
+        const uint4* src = reinterpret_cast<const uint4*>(ext.mx_c + ((long long)(c * NB + b) * 4 + g) * 64);
+#pragma unroll
+        for (int i = 0; i < 4; ++i) q[i] = src[i];
+        sc = ext.mx_s[(c * NB + b) * 4 + g];
+      }
+      chi[ct][b] = mx_v8i{(int)q[0].x, (int)q[0].y, (int)q[0].z, (int)q[0].w,
+                          (int)q[1].x, (int)q[1].y, (int)q[1].z, (int)q[1].w};
+      clo[ct][b] = mx_v8i{(int)q[2].x, (int)q[2].y, (int)q[2].z, (int)q[2].w,
+                          (int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
+      csc[ct][b] = sc;
+    }
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      const int c2 = cw0 + ct * 16 + 4 * g + i;
+      c4[ct][i] = c2 < kc ? ext.cn_t[c2] : __builtin_huge_valf();
+    }
+  }
+  __builtin_amdgcn_s_setprio(1);
+  int boff[4];
+#pragma unroll
+  for (int b = 0; b < 4; ++b) boff[b] = r * G::ROWB + (((4 * b + g) ^ r) << 4);
+  barrier();  // B(-1): first tile landed
+  for (long long j = 0; j < nt; ++j) {
+    if (dbg & 2) {
+      wait_lgkm0();
+      barrier();
+      continue;
+    }
+    const unsigned char* xs = smem + (int)(j % G::NS) * G::SLOT;
+    const float* tn = reinterpret_cast<const float*>(trail + (int)(j % G::NTR) * G::TRB);
+    int* kred = red + (int)(j & 1) * G::TR * G::STRIDE;
+    float xnv[G::NSUB];
+#pragma unroll
+    for (int t = 0; t < G::NSUB; ++t) xnv[t] = tn[16 * t + r];
+    auto xaddr = [&](int u) {  // unit v of sub-tile t: chunk 4v + g of row 16t + r
+      const int t = u / UPS, v = u % UPS;
+      return xs + 16 * t * G::ROWB + 256 * (v >> 2) + boff[v & 3];
+    };
+    uint4 xr[RING];
+#pragma unroll
+    for (int u = 0; u < PF && u < NU; ++u) xr[u] = *reinterpret_cast<const uint4*>(xaddr(u));
+    f32x4 acc[2][CT];
+    int key[2] = {0x7fffffff, 0x7fffffff};
+    int key2[2] = {0x7fffffff, 0x7fffffff};
+#pragma unroll
+    for (int u = 0; u < NU; ++u) {
+      const int t = u / UPS, v = u % UPS, cur = t & 1, prv = cur ^ 1;
+      if (u + PF < NU) xr[(u + PF) % RING] = *reinterpret_cast<const uint4*>(xaddr(u + PF));
+      if (v & 1) {
+        const int s = v >> 1;  // MX block
+        const uint4 a0 = xr[(u - 1) % RING], a1 = xr[u % RING];
+        const mx_v8i xb = mx_v8i{(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
+        if (s == 0) {
+          key[cur] = 0x7fffffff;
+          key2[cur] = 0x7fffffff;
+        }
+#pragma unroll
+        for (int ct = 0; ct < CT; ++ct) {
+          f32x4 a = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(chi[ct][s], xb, s == 0 ? (c4[ct] + xnv[t]) : acc[cur][ct],
+                                                                    0, 0, 0, csc[ct][s], 0, 127);
+          acc[cur][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(clo[ct][s], xb, a, 0, 0, 1, csc[ct][s], 0, 127);
+        }
+        if (t > 0) {  // keys of the previous sub-tile, spread over this one's blocks
+#pragma unroll
+          for (int e = (s * CT * 4) / NB; e < ((s + 1) * CT * 4) / NB; ++e) {
+            const int ct = e >> 2, i = e & 3;
+            const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
+            key2[prv] = med3(key[prv], kv, key2[prv]);
+            key[prv] = kv < key[prv] ? kv : key[prv];
+          }
+          if (s == NB - 1) {
+            kred[(16 * (t - 1) + r) * G::STRIDE + wave * 4 + g] = key[prv];
+            kred[(16 * (t - 1) + r) * G::STRIDE + 16 + wave * 4 + g] = key2[prv];
+          }
+        }
+      }
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    {
+      constexpr int t = G::NSUB - 1, cur = t & 1;
+#pragma unroll
+      for (int e = 0; e < CT * 4; ++e) {
+        const int ct = e >> 2, i = e & 3;
+        const int kv = (__float_as_int(acc[cur][ct][i]) & ~TAGM) | (ct << 2 | i);
+        key2[cur] = med3(key[cur], kv, key2[cur]);
+        key[cur] = kv < key[cur] ? kv : key[cur];
+      }
+      kred[(16 * t + r) * G::STRIDE + wave * 4 + g] = key[cur];
+      kred[(16 * t + r) * G::STRIDE + 16 + wave * 4 + g] = key2[cur];
+    }
+    wait_lgkm0();
+    barrier();  // B(j)
+  }
+}
+
 // F8: X rows are OCP e4m3fn bytes (SURVEY config 5). They travel through the ring as bytes (half the
 // HBM and LDS traffic) and every compute wave widens its fragments with v_cvt_scalef32_pk_bf16_fp8
 // (exact: e4m3 values are a subset of bf16); one 16-B read then covers TWO k-steps, step 2v+h of lane
@@ -434,6 +583,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   constexpr int TAGM = (1 << TAGB) - 1;
   constexpr bool TOP2 = MODE >= 1;
   if (ext.gate != nullptr && *ext.gate != ext.want) return;  // uniform: before any barrier
+  if (ext.gate2 != nullptr && (((long long)*ext.gate2 <= ext.g2cap) != (ext.g2le != 0))) return;
   if constexpr (MODE == 2) n = *ext.n_dev;
   const int* lab_src = MODE == 2 ? ext.lab_in : labels;  // trailer source of the previous labels
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -454,7 +604,9 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   auto tile_of = [&](long long j) { return (long long)blockIdx.x + j * gridDim.x; };
 
   if (wave < kCompute) {
-   if constexpr (M32) {
+   if constexpr (MODE == 3) {
+    compute_mx<DP, CT>(ext, kc, nt, wave, lane, smem, dbg);
+   } else if constexpr (M32) {
     for (int i = tid; i < cn_slots(kp); i += kCompute * 64) cnl[i] = i < kc ? cnorm[i] : __builtin_huge_valf();
     compute_m32<DP, CT, F8, MODE>(C, ldc, kc, nt, wave, lane, smem, cnl, dbg);
    } else {
@@ -617,11 +769,24 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     constexpr int RPF = G::TR / 2;  // rows per finalize wave
     if (fw == 0) {
       for (int i = lane; i < kp; i += 64) hist[i] = 0;
-      if (lane == 0) misc[0] = 0;
+      // append: this workgroup's change list continues the one an earlier launch of the step left
+      if (lane == 0) misc[0] = dout.append != 0 && dout.wg_count != nullptr ? dout.wg_count[blockIdx.x] : 0;
     }
     double cost = 0.0;
     float mcv = 0.f;
     if constexpr (TOP2) mcv = *ext.mc;
+    float mx_e = 0.f, mx_n = 0.f;  // MODE 3: max|~c - cb|, max|~c|² over the centres
+    if constexpr (MODE == 3) {
+      for (int i = lane; i < kc; i += 64) {
+        mx_e = fmaxf(mx_e, ext.mx_stat[i]);
+        mx_n = fmaxf(mx_n, ext.cn_t[i]);
+      }
+#pragma unroll
+      for (int o = 1; o < 64; o <<= 1) {
+        mx_e = fmaxf(mx_e, __shfl_xor(mx_e, o, 64));
+        mx_n = fmaxf(mx_n, __shfl_xor(mx_n, o, 64));
+      }
+    }
     // LPR_F lanes per row, each taking 16 / LPR_F of the 16 (wave, lane-group) keys; keys are loaded
     // in one batch and reduced branch-free on a 64-bit (value, centre index) composite
     constexpr int LPR_F = 64 / RPF;
@@ -683,7 +848,25 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       const int bi = (int)(best & 0xffffffffu);
       const float dist = fmaxf(__int_as_float((int)((unsigned)(best >> 32) ^ 0x80000000u)), 0.f);
       const bool mine = part == 0 && pos < n;
-      const bool ch = mine && old != bi;
+      // MODE 3 certificate: dist / sd are the MX pass's f32 distances to ~c (error <= 4·tau·(|x|² + max|~c|²)
+      // with the key truncation: the MX MFMA's own sums measured within 2^-17 of Σ|terms|, 2^-15 tested), |~c_j - cb_j| <= e moves a distance by at most e, and the bf16 pass's own
+      // values are within tau·(|x|² + max|cb|²) of the exact ones: when the bf16 bounds U (label) and L (every
+      // other centre) are apart by more than both slacks, the bf16 pass picks this label too. Otherwise the
+      // row goes to the re-check list.
+      bool cert = true;
+      float ubv = 0.f, lbv = 0.f;
+      float xnr = 0.f;
+      if constexpr (MODE == 3) {
+        xnr = reinterpret_cast<const float*>(te)[R];
+        const float sl_t = 4.f * ext.tau * (xnr + mx_n);
+        const float sl_b = ext.tau * (xnr + mcv);
+        const float sd = __int_as_float((int)(sec ^ 0x80000000u));
+        ubv = (sqrtf(dist + sl_t) * (1.0f + 1e-6f) + mx_e) * (1.0f + 1e-6f);
+        lbv = (sqrtf(fmaxf(sd - sl_t, 0.f)) * (1.0f - 1e-6f) - mx_e) * (1.0f - 1e-6f);
+        cert = lbv > 0.f && (lbv * lbv) * (1.0f - 1e-6f) - sl_b > (ubv * ubv) * (1.0f + 1e-6f) + sl_b;
+        lbv = fmaxf(lbv, 0.f);
+      }
+      const bool ch = mine && cert && old != bi;
       if (dout.rows != nullptr) {
         const unsigned long long bal = __ballot(ch);
         if (bal != 0ull) {
@@ -699,8 +882,24 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
           }
         }
       }
+      if constexpr (MODE == 3) {
+        const bool unc = mine && !cert;
+        const unsigned long long bu = __ballot(unc);
+        if (bu != 0ull) {
+          const int leader = __builtin_ctzll(bu);
+          int base = 0;
+          if (lane == leader) base = atomicAdd(ext.u_cnt, (int)__popcll(bu));
+          base = __shfl(base, leader, 64);
+          const long long at = (long long)base + (long long)__popcll(bu & ((1ull << lane) - 1ull));
+          if (unc && at < ext.u_cap) {
+            ext.u_idx[at] = (int)row;
+            ext.u_lab[at] = old;
+            ext.u_xn[at] = xnr;
+          }
+        }
+      }
       if (ch) labels[row] = bi;
-      if (mine) {
+      if (mine && cert) {
         cost += (double)dist;
         if (best_out != nullptr) best_out[row] = dist;
         if constexpr (MODE == 2) {
@@ -711,11 +910,14 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         }
         if (ranking) rank_out[row] = atomicAdd(hist + bi, 1);
         if constexpr (TOP2) {
-          const float xn = reinterpret_cast<const float*>(te)[R];
-          const float slack = ext.tau * (xn + mcv);
-          const float sd = __int_as_float((int)(sec ^ 0x80000000u));
-          float u = sqrtf(dist + slack) * (1.0f + 1e-6f);
-          float w = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
+          float u = ubv, w = lbv;
+          if constexpr (MODE != 3) {
+            const float xn = reinterpret_cast<const float*>(te)[R];
+            const float slack = ext.tau * (xn + mcv);
+            const float sd = __int_as_float((int)(sec ^ 0x80000000u));
+            u = sqrtf(dist + slack) * (1.0f + 1e-6f);
+            w = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
+          }
           if (ext.cu != nullptr) {
             const float cu = ext.cu[bi], cl = ext.cl[bi];
             u = (u - cu) + 1e-6f * (u + cu);
@@ -803,7 +1005,7 @@ inline long long lds_for_mode(int Dp, int kp, bool f8) {
 }
 
 inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
-  const bool m32 = use_m32(Dp, plan_ct(Dp, kp, f8), f8);
+  const bool m32 = mode != 3 && use_m32(Dp, plan_ct(Dp, kp, f8), f8);
   switch (mode * 2 + (m32 ? 1 : 0)) {
     case 0: return lds_for_mode<0, false>(Dp, kp, f8);
     case 1: return lds_for_mode<0, true>(Dp, kp, f8);
@@ -811,6 +1013,7 @@ inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
     case 3: return lds_for_mode<1, true>(Dp, kp, f8);
     case 4: return lds_for_mode<2, false>(Dp, kp, f8);
     case 5: return lds_for_mode<2, true>(Dp, kp, f8);
+    case 6: return f8 ? lds_for_mode<3, false>(Dp, kp, f8) : 0;
     default: return 0;
   }
 }
@@ -829,6 +1032,20 @@ int launch(const void* X, long long n, long long ldx, const u16* C, long long ld
                      (const unsigned char*)X, n, ldb, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist,
                      rank, dout, ext, dbg);
   return cml_status();
+}
+
+// MODE 3 (fp8 screen): fp8 rows, 16x16 tiles only
+inline int dispatch_mx(int Dp, int ct, const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc,
+                       int kp, const float* cnorm, const float* xnorm, int* labels, float* best, double* cost_part,
+                       DeltaOut dout, Ext ext, int grid, int dbg, hipStream_t st) {
+#define CML_RX(D, T)                                                                                                \
+  if (Dp == D && ct == T)                                                                                           \
+  return launch<D, T, true, 3, false>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, nullptr,   \
+                                      nullptr, dout, ext, grid, dbg, st)
+  CML_RX(256, 1); CML_RX(256, 2); CML_RX(256, 3); CML_RX(256, 4);
+  CML_RX(512, 1); CML_RX(512, 2);
+#undef CML_RX
+  return (int)hipErrorInvalidValue;
 }
 
 template <int MODE>
@@ -867,6 +1084,9 @@ inline int dispatch(int mode, int Dp, int ct, bool f8, const void* X, long long 
                                     hist, rank, dout, ext, grid, dbg, st);
     case 2: return dispatch_mode<2>(Dp, ct, f8, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
                                     hist, rank, dout, ext, grid, dbg, st);
+    case 3: return f8 && hist == nullptr ? dispatch_mx(Dp, ct, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best,
+                                                       cost_part, dout, ext, grid, dbg, st)
+                                         : (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -1076,8 +1076,14 @@ class LloydEngine:
                   if os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096 else None)
         # completion counters of the fused launches (gate in the bounds pass, stats in the half pass); each
         # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
-        st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
+        # [2]: the fp8 screen's uncertified-row counter (re-armed by the gate)
+        st.ctr = torch.zeros(3, dtype=torch.int32, device=dev)
         st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
+        # fp8 rows: the full pass is the MX screen (kmeans_rr.h MODE 3) + a bf16 re-check of the rows it cannot
+        # certify; CML_KMEANS_FP8_SCREEN=0 keeps the widening bf16 pass (A/B)
+        st.screen = (st.fused and K.is_fp8(self.x) and self.dp % 128 == 0 and ap.rr_ct > 0
+                     and os.environ.get("CML_KMEANS_FP8_SCREEN", "1") != "0")
+        st.mx_ops = K.mx_centres_buffers(ap.kp, self.dp, dev) if st.screen else None
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
@@ -1105,22 +1111,49 @@ class LloydEngine:
         if st.fused:  # bounds pass + gate in one launch
             K.prune_bounds_gated(lab[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                                  self.xnorm, st.cand_lab, st.cand_xn, st.flags, st.cum, st.pmode, st.cap_m,
-                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1])
+                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1],
+                                 zero=st.ctr[2:3] if st.screen else None)
         else:
             K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                            xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
                            cum=st.cum) if n else None
             K.prune_gate(st.count, st.cap_m, st.flags, st.pmode, backoff=st.backoff if st.nback > 0 else None,
                          nback=st.nback)
-        K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
-                        st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
+        if st.screen:
+            self._pdev_screen()
+        else:
+            K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                            st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
                         gate=st.pmode, want=0, cum=st.cum)
         dl.gate(0)
+        if st.screen:  # counting-sort ranks of the final labels when the sums are re-accumulated in full
+            K.label_hist(lab, n, ap, self.hist, self.rank, gate=dl.mode[0], want=1)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
+
+    def _pdev_screen(self) -> None:
+        """Full pass of a device pruned step on fp8 rows (all launches gated on the full-pass flag): the MX
+        operands of the bf16 centres (kmeans_mx.hip), the MX screen over every row — labels and bounds of
+        the rows whose top-2 gap it certifies, the others listed (row, old label, norm) in the candidate
+        buffers (free in a full step) — then the bf16 candidate pass over that list, or, when the list
+        outgrew its capacity, the bf16 full pass. Labels, change lists and bounds end as the bf16 full
+        pass leaves them (kmeans_rr.h MODE 3); the ranks come from label_hist when needed."""
+        st, dl, ap = self._pst, self.delta, self.aplan
+        n, k, x, lab = self.n, self.k, self.x, self.labels
+        ucnt = st.ctr[2:3]
+        K.mx_centres(self.cb, k, ap.kp, self.dp, out=st.mx_ops, gate=st.pmode)
+        K.assign_rr_ext(3, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                        st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum, mx=st.mx_ops,
+                        ulist=(st.cand, st.cand_lab, st.cand_xn, ucnt, st.cap_m))
+        K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
+                        st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=ucnt, lab_in=st.cand_lab, gate=st.pmode,
+                        want=1, cum=st.cum, gate2=(ucnt, st.cap_m, True), append=True)
+        K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                        st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum, gate2=(ucnt, st.cap_m, False),
+                        append=True)
 
     def _pdev_post(self) -> None:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
@@ -1558,7 +1591,10 @@ class LloydEngine:
         if self._pst is None:
             return {}
         full, m = self._pdev_last() if self._pdev else self._pst.last
-        return {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
+        out = {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
+        if self._pdev and getattr(self._pst, "screen", False) and full:
+            out["screen_rechecked"] = int(self._pst.ctr[2].item())  # rows the fp8 screen left to the bf16 pass
+        return out
 
     def prune_history(self) -> list:
         """(full step?, re-assigned rows) of every pruned step of this engine, rank-local."""

@@ -68,7 +68,9 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
-                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
+                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int,
+                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_int,
+                                         c_int, c_vp]),
     "cml_kmeans_init_classify": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, ctypes.c_float, c_ll, c_int, c_vp,
                                          c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_near_list": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
@@ -114,7 +116,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_pair_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_prune_bounds_gated": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
-                                              c_vp]),
+                                              c_vp, c_vp]),
     "cml_kmeans_update_pdev": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                        c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_centre_half_stats": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp,
@@ -133,6 +135,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_cert_slices": (c_int, [c_int]),
     "cml_kmeans_cert_moves": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_mx_probe": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_mx_centres": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
 })
 _native.register_host_sigs({
     "cml_local_kmeans_host": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, ctypes.c_uint64, c_int,
@@ -684,16 +688,17 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
 
 
 def prune_bounds_gated(labels, ub, lb, drift, dmax, thr, c2, k: int, cand, count, xn, cand_lab, cand_xn, flags,
-                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None) -> None:
+                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None, zero=None) -> None:
     """K9p with the step gate folded in (kmeans_prune.hip): the bounds pass (skipped when flags[0] / flags[1]
     are set) and, in the workgroup that finishes last, kmeans_prune_gate's decision into ``mode``; ``done``
-    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics."""
+    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics.
+    ``zero`` (int32 [1], optional): a counter of the step's later launches, set to 0 by the gate."""
     n = int(labels.shape[0])
     _native.check(_native.kernels().cml_kmeans_prune_bounds_gated(
         labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
         c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
         flags.data_ptr(), int(cand.shape[0]), _ptr(cum), mode.data_ptr(), int(gate_cap), _ptr(backoff), int(nback),
-        done.data_ptr(), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
+        done.data_ptr(), _ptr(zero), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
 
 
 def update_pdev(msgs: torch.Tensor, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int, kp: int,
@@ -770,6 +775,40 @@ def centre_stats(cb: torch.Tensor, cb_old: torch.Tensor | None, k: int, d: int, 
         "kmeans_centre_stats")
 
 
+def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tensor) -> torch.Tensor:
+    """One v_mfma_scale_f32_16x16x128_f8f6f4 (kmeans_mx.hip, a layout/precision probe for tests):
+    out[i, j] = sum_k a[i, k]·b[j, k] with the E8M0 scale of lane l (row l % 16, k block l // 16) from
+    ``sa``/``sb`` (int32 [64]). a, b: uint8 e4m3fn bytes [16, 128]."""
+    if a.shape != (16, 128) or b.shape != (16, 128) or sa.numel() != 64 or sb.numel() != 64:
+        raise ValueError("mx_probe: a, b [16, 128] e4m3 bytes, sa, sb [64] int32")
+    out = torch.empty((16, 16), dtype=torch.float32, device=a.device)
+    _native.check(_native.kernels().cml_mx_probe(a.contiguous().data_ptr(), b.contiguous().data_ptr(),
+                                                 sa.to(torch.int32).contiguous().data_ptr(),
+                                                 sb.to(torch.int32).contiguous().data_ptr(), out.data_ptr(),
+                                                 _native.stream_ptr(None)), "mx_probe")
+    return out
+
+
+def mx_centres_buffers(kp: int, dp: int, device) -> tuple:
+    """The four output tensors of mx_centres."""
+    return (torch.zeros((kp, dp // 128, 4, 64), dtype=torch.uint8, device=device),
+            torch.zeros((kp, dp // 128, 4), dtype=torch.int32, device=device),
+            torch.zeros(kp, dtype=torch.float32, device=device), torch.zeros(kp, dtype=torch.float32, device=device))
+
+
+def mx_centres(cb: torch.Tensor, kc: int, kp: int, dp: int, out=None, stream=None, gate=None):
+    """MX operands of the screen pass (kmeans_mx.hip): hi/lo e4m3 bytes of -2·cb in the K9r fp8 lane order
+    [kp, dp/128, 4, 64], their E8M0 scales [kp, dp/128, 4] (hi | lo << 8), |~c|² [kp] and |~c - cb| [kp]
+    (rounded up). ``out``: the same four tensors, reused; ``gate``: run only when gate[0] == 1."""
+    if out is None:
+        out = mx_centres_buffers(kp, dp, cb.device)
+    mc, ms, cn, stat = out
+    _native.check(_native.kernels().cml_kmeans_mx_centres(cb.data_ptr(), cb.stride(0), int(kc), int(kp), int(dp),
+                                                          mc.data_ptr(), ms.data_ptr(), cn.data_ptr(), stat.data_ptr(),
+                                                          _ptr(gate), _native.stream_ptr(stream)), "kmeans_mx_centres")
+    return out
+
+
 def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor,
                   plan: AssignPlan, xnorm: torch.Tensor, labels: torch.Tensor, cost_part: torch.Tensor | None,
                   ub: torch.Tensor, lb: torch.Tensor, mc: torch.Tensor, tau: float,
@@ -779,14 +818,19 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
                   gate: torch.Tensor | None = None, want: int = 0, stream=None,
                   best: torch.Tensor | None = None, cum: torch.Tensor | None = None,
                   merge_cost: torch.Tensor | None = None, merge_near: torch.Tensor | None = None,
-                  merge_off: int = 0) -> None:
+                  merge_off: int = 0, mx=None, ulist=None, gate2=None, append: bool = False) -> None:
     """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
     the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
     ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
     rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag;
     ``best`` (f32, real rows) receives the squared distance to the new label; ``merge_cost``/``merge_near``
     (mode 2, f32/int32 per real row) take the k-means|| merge: strictly nearer rows get (distance, label +
-    ``merge_off``)."""
+    ``merge_off``).
+
+    ``mode`` 3 (fp8 rows): the MX screen (kmeans_rr.h compute_mx) over every row with the centre operands
+    ``mx`` = mx_centres(...) — certified rows get labels and bounds as mode 1, the others go to ``ulist`` =
+    (rows, old labels, norms, int32 counter, capacity) for a bf16 re-check. ``gate2`` = (int32 [1], cap, le):
+    the launch also needs (gate2 <= cap) == le. ``append``: the change lists continue an earlier launch's."""
     if plan.rr_ct <= 0 or plan.kc != plan.kp:
         raise ValueError("the pruned-step assign needs the K9r plan (Dp in {128, 256, 512}, k <= 256)")
     _native.check(_native.kernels().cml_kmeans_assign_rr_ext(
@@ -798,7 +842,10 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
         delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
         lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _ptr(cum),
         int(cum.shape[0] // 2) if cum is not None else 0, _ptr(merge_cost), _ptr(merge_near), int(merge_off),
-        _native.stream_ptr(stream)),
+        *(_ptr(t) for t in (mx if mx is not None else (None,) * 4)),
+        *(_ptr(t) for t in (ulist[:4] if ulist is not None else (None,) * 4)), int(ulist[4]) if ulist else 0,
+        _ptr(gate2[0] if gate2 else None), int(gate2[1]) if gate2 else 0, int(bool(gate2[2])) if gate2 else 0,
+        int(append), _native.stream_ptr(stream)),
         f"kmeans_assign_rr_ext(mode={mode})")
 
 
