@@ -240,7 +240,6 @@ struct DeltaOut {
   int* overflow;
   int pcap;
   int* lds_count;  // set in the kernel
-  int append = 0;  // K9r: continue the per-workgroup lists of an earlier launch of the step (same grid)
 };
 
 template <int DP, int RT, int RINGMAX, bool SHARED, bool PACK4>
@@ -1679,6 +1678,12 @@ CML_API int cml_kmeans_set_rr_m32(int on) {
   rr::g_m32 = on ? 1 : 0;
   return 0;
 }
+// MX arithmetic of the fp8 K9r passes (kmeans_rr.h compute_mx): on by default; returns the previous setting.
+CML_API int cml_kmeans_set_fp8_mx(int on) {
+  const int prev = rr::g_mx;
+  if (on >= 0) rr::g_mx = on ? 1 : 0;
+  return prev;
+}
 CML_API int cml_kmeans_set_rr_default(int on) {
   g_rr_default = on ? 1 : 0;
   return 0;
@@ -1756,15 +1761,8 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
                                      int rr_ct, const int* idx, const int* n_dev, const int* lab_in, float* ub,
                                      float* lb, const float* mc, float tau, const int* gate, int want, float* best,
                                      const float* cum, int k_cum, float* mcost, int* mnear, int moff,
-                                     const void* mx_c, const int* mx_s, const float* cn_t, const float* mx_stat,
-                                     int* u_idx, int* u_lab, float* u_xn, int* u_cnt, long long u_cap,
-                                     const int* gate2, long long g2cap, int g2le, int append, void* stream) {
-  if (mode < 1 || mode > 3 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
-  if (mode == 3 && (!xfp8 || Dp % 128 != 0 || mx_c == nullptr || mx_s == nullptr || cn_t == nullptr ||
-                    mx_stat == nullptr || u_idx == nullptr || u_lab == nullptr || u_xn == nullptr ||
-                    u_cnt == nullptr || hist != nullptr))
-    return (int)hipErrorInvalidValue;
-  if (append && chg_rows == nullptr) return (int)hipErrorInvalidValue;
+                                     void* stream) {
+  if (mode < 1 || mode > 2 || kc != kp || kc % 16 != 0 || ldc % 8 != 0) return (int)hipErrorInvalidValue;
   if ((mcost == nullptr) != (mnear == nullptr) || (mcost != nullptr && mode != 2)) return (int)hipErrorInvalidValue;
   if (xfp8 ? (ldx % 16 != 0) : (ldx % 8 != 0)) return (int)hipErrorInvalidValue;
   if (rr_ct <= 0 || rr::plan_ct(Dp, kc, xfp8 != 0) != rr_ct) return (int)hipErrorInvalidValue;
@@ -1776,10 +1774,9 @@ CML_API int cml_kmeans_assign_rr_ext(int mode, const void* X, long long n, long 
     return (int)hipErrorInvalidValue;
   const long long lds = rr::lds_for(Dp, kp, xfp8 != 0, mode);
   if (lds <= 0 || lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr, append};
-  const rr::Ext ext{idx,   n_dev, lab_in, ub,   lb,   mc,     tau,  gate,  want,    cum,
-                    cum != nullptr ? cum + k_cum : nullptr, mcost, mnear, moff, (const unsigned char*)mx_c, mx_s,
-                    cn_t,  mx_stat, u_idx, u_lab, u_xn, u_cnt, u_cap, gate2, g2cap, g2le};
+  const DeltaOut dout{chg_rows, chg_old, chg_wg_count, chg_overflow, chg_pcap, nullptr};
+  const rr::Ext ext{idx,  n_dev, lab_in, ub,    lb,    mc,   tau, gate, want, cum, cum != nullptr ? cum + k_cum : nullptr,
+                    mcost, mnear, moff};
   return rr::dispatch(mode, Dp, rr_ct, xfp8 != 0, X, n, ldx, (const u16*)C, ldc, kc, kp, cnorm, xnorm, labels,
                       best, cost_part, hist, rank, dout, ext, grid, g_rr_dbg, (hipStream_t)stream);
 }

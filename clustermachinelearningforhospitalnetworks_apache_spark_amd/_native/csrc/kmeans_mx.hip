@@ -1,25 +1,10 @@
-// MX-scaled fp8 operands of the K9r screen pass (kmeans_rr.h MODE 3, SURVEY config 5: fp8 rows).
+// MX-scaled fp8 MFMA support for the fp8 KMeans passes (kmeans_rr.h compute_mx, SURVEY config 5).
 //
-// v_mfma_scale_f32_16x16x128_f8f6f4 runs e4m3 x e4m3 products at twice the bf16 MFMA rate, with one
-// E8M0 scale per 32-element block of each operand row. The fp8 K9r pass widened every X fragment to bf16
-// in every compute wave (v_cvt_scalef32_pk_bf16_fp8, 8 per 16 bytes) and was bound by that vector work;
-// the screen pass feeds the e4m3 bytes straight to the MX MFMA instead and represents each bf16 centre
-// value -2·c as hi + lo, two e4m3 values under their own block scales:
-//
-//   hi = e4m3(v · 2^s),  lo = e4m3((v - hi·2^-s) · 2^t),  ~c = -(hi·2^-s + lo·2^-t) / 2
-//
-// Two MX MFMAs per 128 k (hi, lo) cost what the four bf16 MFMAs of that k range cost, with no
-// conversion. ~c equals the bf16 centre except where a value sits far below its block's largest (e4m3
-// subnormals drop its low bits); this pass also returns e_j = |~c_j - cb_j| (rounded up) and |~c_j|²,
-// and the screen certifies a row's label only when its top-2 gap exceeds what e and the
-// f32 rounding of both passes can move (kmeans_rr.h, MODE 3). Rows it cannot certify are re-assigned by
-// the bf16 pass, so labels and sums are those of the bf16 path.
-//
-// Lane layout (the K9r fp8 k order): lane (r, g) of MX block b holds the 16-B chunks 8b + g and 8b + 4 + g
-// of row r — the two 16-B units the compute wave reads for that block. The instruction's k order is the
-// same (bytes 0-15 of lane group g are k 16g + j, bytes 16-31 are k 64 + 16g + j), and its scale block q
-// (scale from lane group q) is k [32q, 32q + 32): chunks 8b + 2q, 8b + 2q + 1 — measured on MI355X
-// (scripts/r5/mx_probe_diag3.py; tests/test_kmeans_mx_gpu.py pins it).
+// v_mfma_scale_f32_16x16x128_f8f6f4 runs e4m3 x e4m3 products at twice the bf16 MFMA rate, with one E8M0
+// scale per 32-element block of each operand row. The fp8 K9r pass feeds the e4m3 rows to it directly and
+// splits each bf16 centre value into two e4m3 terms under their own block scales (hi + lo); this file keeps
+// the centres of the fp8 engines on the grid where that split is exact (kmeans_mx_snap_kernel) and holds a
+// one-instruction probe that pins the operand / scale layout (tests/test_kmeans_mx_gpu.py).
 #include "common.h"
 
 typedef int v8i __attribute__((ext_vector_type(8)));
@@ -52,7 +37,7 @@ CML_API int cml_mx_probe(const void* A, const void* B, const int* sa, const int*
 }
 
 // Scale exponent s with m·2^s in [128, 256) (every block value then fits e4m3's 448), clamped to the
-// E8M0 range of the scale 2^-s.
+// E8M0 range of the scale 2^-s (kmeans_rr.h mx_shift: the same rule).
 __device__ __forceinline__ int block_shift(float m) {
   if (!(m > 0.f)) return 0;
   int e;
@@ -62,79 +47,66 @@ __device__ __forceinline__ int block_shift(float m) {
   return s;
 }
 
-// A wave per centre (4 per workgroup). cb: bf16 [kc, ldc]; Dp % 128 == 0; mx_c: bytes
-// [kp][Dp/128][lane group 4][hi 32 | lo 32]; mx_s: int32 [kp][Dp/128][scale block 4] = hi scale | lo scale
-// << 8 (E8M0); cn_t: f32
-// [kp] |~c|² (+inf past kc); e_c: f32 [kp] |~c - cb| rounded up (0 past kc). gate (nullable): run only
-// when gate[0] == 1 (the pruned step's full-pass flag).
-__global__ __launch_bounds__(256) void kmeans_mx_centres_kernel(const u16* __restrict__ cb, long long ldc, int kc,
-                                                                int kp, int Dp, unsigned char* __restrict__ mx_c,
-                                                                int* __restrict__ mx_s, float* __restrict__ cn_t,
-                                                                float* __restrict__ e_c, const int* __restrict__ gate) {
-  if (gate != nullptr && gate[0] != 1) return;
+// Centres onto the MX grid, in place: every 32-element block of a bf16 centre row becomes hi·2^-s + lo·2^-t
+// (the split the MX assign makes of -2·c, scaled by -1/2: the same blocks, shifts one lower), so that split
+// is exact and the MX pass computes the bf16 pass's products. A value loses bits only when it sits ~2^-14
+// or further below its block's largest; the result is a bf16 value again (at most 8 significant bits).
+// Snapping a snapped row changes nothing. A wave per centre, a lane per block (Dp / 32 <= 64). Also
+// rewrites the derived values of the row: cnorm = |c|² (f32 of the f64 sum), and when given cn64 (f64)
+// and drift = |c - cb_old| rounded up (kmeans_update_pdev_kernel's outputs).
+__global__ __launch_bounds__(256) void kmeans_mx_snap_kernel(u16* __restrict__ cb, long long ldc, int kc, int Dp,
+                                                             float* __restrict__ cnorm, double* __restrict__ cn64,
+                                                             const u16* __restrict__ cb_old,
+                                                             float* __restrict__ drift) {
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6;
-  const int nb = Dp / 128, nblk = nb * 4;  // 32-element blocks per centre
   const int c = blockIdx.x * 4 + wave;
-  if (c >= kp) return;
-  {
-    double err = 0.0, nrm = 0.0;
-    for (int q = lane; q < nblk; q += 64) {
-      const int b = q >> 2, sq = q & 3;  // MX block, scale block: k = 128b + 32sq + j
-      float v[32];
+  if (c >= kc) return;
+  u16* row = cb + (long long)c * ldc;
+  double nrm = 0.0, dr = 0.0;
+  for (int q = lane; q < Dp / 32; q += 64) {
+    float v[32];
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const int k = 128 * b + 32 * sq + j;
-        v[j] = c < kc ? -2.f * bf16_to_f32(cb[(long long)c * ldc + k]) : 0.f;
-      }
-      float m = 0.f;
+    for (int j = 0; j < 32; ++j) v[j] = bf16_to_f32(row[32 * q + j]);
+    float m = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) m = fmaxf(m, fabsf(v[j]));
-      const int s = block_shift(m);
-      unsigned hb[32];
-      float r[32];
-      float mr = 0.f;
+    for (int j = 0; j < 32; ++j) m = fmaxf(m, fabsf(v[j]));
+    const int s = block_shift(m);
+    float hv[32];
+    float mr = 0.f;
 #pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        hb[j] = e4m3_of(ldexpf(v[j], s));
-        r[j] = v[j] - ldexpf(f32_of_e4m3(hb[j]), -s);  // exact: both are short dyadic values
-        mr = fmaxf(mr, fabsf(r[j]));
-      }
-      const int t = block_shift(mr);
-      unsigned wh[8] = {0, 0, 0, 0, 0, 0, 0, 0}, wl[8] = {0, 0, 0, 0, 0, 0, 0, 0};
-#pragma unroll
-      for (int j = 0; j < 32; ++j) {
-        const unsigned lb = e4m3_of(ldexpf(r[j], t));
-        const double ct = (double)ldexpf(f32_of_e4m3(hb[j]), -s) + (double)ldexpf(f32_of_e4m3(lb), -t);
-        const double dlt = ct - (double)v[j];
-        err += dlt * dlt;
-        nrm += ct * ct;
-        wh[j >> 2] |= hb[j] << (8 * (j & 3));
-        wl[j >> 2] |= lb << (8 * (j & 3));
-      }
-      // chunk i = 2sq + u of the block sits in lane group i & 3, half i >> 2 (bytes 16·(i >> 2) of its 32)
-#pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const int i = 2 * sq + u;
-        unsigned char* dst = mx_c + ((long long)(c * nb + b) * 4 + (i & 3)) * 64 + 16 * (i >> 2);
-        *reinterpret_cast<uint4*>(dst) = make_uint4(wh[4 * u], wh[4 * u + 1], wh[4 * u + 2], wh[4 * u + 3]);
-        *reinterpret_cast<uint4*>(dst + 32) = make_uint4(wl[4 * u], wl[4 * u + 1], wl[4 * u + 2], wl[4 * u + 3]);
-      }
-      mx_s[(long long)c * nblk + q] = (127 - s) | ((127 - t) << 8);  // lane group sq provides block sq's scale
+    for (int j = 0; j < 32; ++j) {
+      hv[j] = ldexpf(f32_of_e4m3(e4m3_of(ldexpf(v[j], s))), -s);
+      mr = fmaxf(mr, fabsf(v[j] - hv[j]));
     }
-    err = wave_sum_f64(err);
-    nrm = wave_sum_f64(nrm);
-    // ~c = -(hi + lo) / 2: |~c - cb| = sqrt(err) / 2, |~c|² = nrm / 4 (rounded up: the screen's slack)
-    if (lane == 0) {
-      cn_t[c] = c < kc ? (float)(0.25 * nrm) : __builtin_huge_valf();
-      e_c[c] = c < kc ? (float)(0.5 * sqrt(err) * (1.0 + 1e-6)) + 1e-30f : 0.f;
+    const int t = block_shift(mr);
+#pragma unroll
+    for (int j = 0; j < 32; ++j) {
+      const float lo = ldexpf(f32_of_e4m3(e4m3_of(ldexpf(v[j] - hv[j], t))), -t);
+      const u16 b = f32_to_bf16(hv[j] + lo);  // exact: hi + lo has at most 8 significant bits
+      row[32 * q + j] = b;
+      const double f = (double)bf16_to_f32(b);
+      nrm += f * f;
+      if (cb_old != nullptr) {
+        const double e = f - (double)bf16_to_f32(cb_old[(long long)c * ldc + 32 * q + j]);
+        dr += e * e;
+      }
     }
+  }
+  nrm = wave_sum_f64(nrm);
+  dr = wave_sum_f64(dr);
+  if (lane == 0) {
+    cnorm[c] = (float)nrm;
+    if (cn64 != nullptr) cn64[c] = nrm;
+    if (drift != nullptr) drift[c] = (float)(sqrt(dr) * (1.0 + 1e-6));
   }
 }
 
-CML_API int cml_kmeans_mx_centres(const void* cb, long long ldc, int kc, int kp, int Dp, void* mx_c, int* mx_s,
-                                  float* cn_t, float* e_c, const int* gate, void* stream) {
-  if (Dp <= 0 || Dp % 128 != 0 || Dp / 32 > 64 || kc > kp || kc <= 0) return (int)hipErrorInvalidValue;
-  hipLaunchKernelGGL(kmeans_mx_centres_kernel, dim3((kp + 3) / 4), dim3(256), 0, (hipStream_t)stream, (const u16*)cb,
-                     ldc, kc, kp, Dp, (unsigned char*)mx_c, mx_s, cn_t, e_c, gate);
+CML_API int cml_kmeans_mx_snap(void* cb, long long ldc, int kc, int Dp, float* cnorm, double* cn64,
+                               const void* cb_old, float* drift, void* stream) {
+  if (Dp <= 0 || Dp % 32 != 0 || Dp / 32 > 64 || kc < 0 || ldc < Dp || (drift != nullptr) != (cb_old != nullptr))
+    return (int)hipErrorInvalidValue;
+  if (kc == 0) return 0;
+  hipLaunchKernelGGL(kmeans_mx_snap_kernel, dim3((kc + 3) / 4), dim3(256), 0, (hipStream_t)stream, (u16*)cb, ldc, kc,
+                     Dp, cnorm, cn64, (const u16*)cb_old, drift);
   return cml_status();
 }

@@ -53,10 +53,7 @@ __device__ __forceinline__ bool bound_step(int a, float& u, float& w, const floa
 
 // The pruned step's gate (kmeans_prune_gate_kernel's body): one thread.
 __device__ __forceinline__ void prune_gate_body(int* __restrict__ count, long long cap, const int* __restrict__ flags,
-                                                int* __restrict__ mode, int* __restrict__ backoff, int nback,
-                                                int* __restrict__ zero = nullptr) {
-  // zero: a counter the step's later launches count into (the fp8 screen's uncertified rows), re-armed here
-  if (zero != nullptr) __hip_atomic_store(zero, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+                                                int* __restrict__ mode, int* __restrict__ backoff, int nback) {
   if (flags[1] != 0) {
     mode[0] = 0;
     mode[1] = 0;
@@ -80,7 +77,6 @@ struct GateArgs {
   int* backoff;
   int nback;
   int* done;
-  int* zero = nullptr;  // re-armed by the gate (prune_gate_body)
 };
 
 __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
@@ -102,7 +98,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   // converged and the step is a frozen no-op (kmeans_prune_gate_kernel)
   if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) {
     if (gate.mode != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.zero);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
     return;
   }
   extern __shared__ __align__(16) unsigned char smem[];
@@ -220,7 +216,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
     // no fence: the gate reads only the count, which every block changed by an atomic whose result it
     // waited for (base above) before this completion atomic — device-scope atomics in issue order
     if (threadIdx.x == 0 && atomicAdd(gate.done, 1) == (int)gridDim.x - 1) {
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.zero);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
       __hip_atomic_store(gate.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -736,13 +732,13 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, int* zero, void* stream);
+                                          int nback, int* done, void* stream);
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
                                     const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                     const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                     long long cap, const float* cum, void* stream) {
   return cml_kmeans_prune_bounds_gated(lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn,
-                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, nullptr, stream);
+                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, stream);
 }
 
 // The bounds pass with the step gate folded in (mode / gate_cap / backoff / nback as kmeans_prune_gate; done:
@@ -751,7 +747,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, int* zero, void* stream) {
+                                          int nback, int* done, void* stream) {
   if (mode != nullptr && (skip == nullptr || done == nullptr)) return (int)hipErrorInvalidValue;
   if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
     return (int)hipErrorInvalidValue;
@@ -767,7 +763,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
   }
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
-  const GateArgs g{mode, gate_cap, backoff, nback, done, zero};
+  const GateArgs g{mode, gate_cap, backoff, nback, done};
   hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
                      (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
                      dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum, g);

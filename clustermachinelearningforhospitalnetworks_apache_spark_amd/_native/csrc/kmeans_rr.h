@@ -79,23 +79,6 @@ struct Ext {
   float* mcost = nullptr;
   int* mnear = nullptr;
   int moff = 0;
-  // MODE 3 (fp8 screen, kmeans_mx.hip): hi/lo e4m3 centre operands in lane order, their E8M0 scales, |~c|²
-  // and |~c - cb| per centre (mx_stat)
-  const unsigned char* mx_c = nullptr;
-  const int* mx_s = nullptr;
-  const float* cn_t = nullptr;
-  const float* mx_stat = nullptr;
-  // MODE 3: the rows the screen cannot certify -> (row, old label, |x|²) at positions counted by *u_cnt
-  // (entries past u_cap are not written: the caller's fallback runs the full bf16 pass then)
-  int* u_idx = nullptr;
-  int* u_lab = nullptr;
-  float* u_xn = nullptr;
-  int* u_cnt = nullptr;
-  long long u_cap = 0;
-  // second gate: with gate2 != null the launch runs only when (*gate2 <= g2cap) == (g2le != 0)
-  const int* gate2 = nullptr;
-  long long g2cap = 0;
-  int g2le = 0;
 };
 
 __host__ __device__ constexpr int cn_slots(int kp) { return ((kp + 3) & ~3) > 256 ? ((kp + 3) & ~3) : 256; }
@@ -431,24 +414,89 @@ __device__ __forceinline__ void compute_m32(const u16* __restrict__ C, long long
   barrier();  // B(nt)
 }
 
-// MODE 3 compute waves (fp8 rows, the screen pass): the e4m3 X bytes go straight into
-// v_mfma_scale_f32_16x16x128_f8f6f4 as the B operand (no widening), against the hi/lo e4m3 split of the
-// centres (kmeans_mx.hip) in VGPRs: per 128-k block two MX MFMAs (hi, lo) per centre tile, each at twice the
-// bf16 rate, so the MFMA time of the bf16 pass with none of its conversion work. Lane (r, g) of block b
-// reads the 16-B units 2b and 2b + 1 of the K9r fp8 order (chunks 8b + g and 8b + 4 + g of row r), the
-// 32 bytes of its MX lane; the centre operands follow the same order. Accumulators start at |~c|² + |x|².
-// Keys and the exchange are those of the 16x16 bf16 path (TOP-2).
+// MX compute waves (fp8 rows): the e4m3 X bytes go straight into v_mfma_scale_f32_16x16x128_f8f6f4 as the
+// B operand (no widening), against an exact two-term e4m3 split of the bf16 centres held in VGPRs:
+//
+//   v = -2·c (bf16),  hi = e4m3(v·2^s),  lo = e4m3((v - hi·2^-s)·2^t),  v = hi·2^-s + lo·2^-t
+//
+// with E8M0 block scales 2^-s, 2^-t per 32 k (the block's largest value scaled into [128, 256)). The split is
+// exact for centres on the MX grid, which the fp8 engines keep theirs on (kmeans_mx.hip mx_snap after every
+// centre update: a bf16 value far below its block's largest loses the bits e4m3 subnormals cannot hold), so
+// the products are those of the bf16 pass; per 128 k two MX MFMAs (hi, lo) at twice the bf16 rate — the
+// MFMA time of the bf16 pass with none of its v_cvt_scalef32_pk_bf16_fp8 widening of every X fragment in
+// every compute wave, which bound that pass (19.6 ms at 125M x 512, k = 128).
+// Layout (measured, scripts/r5/mx_probe_diag*.py, pinned by tests/test_kmeans_mx_gpu.py): bytes 0-15 of lane
+// (r, g) are k 16g + j, bytes 16-31 are k 64 + 16g + j, and lane group q supplies the scale of k [32q, 32q+32).
+// Lane (r, g) of block b therefore reads the 16-B units 2b and 2b + 1 of the K9r fp8 order (chunks 8b + g
+// and 8b + 4 + g of row r); its split partner for both halves' scale blocks is lane (r, g ^ 1).
+// Accumulators start at |c|² + |x|²; keys and the exchange are those of the 16x16 bf16 path.
 typedef int mx_v8i __attribute__((ext_vector_type(8)));
 
-template <int DP, int CT>
-__device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt, int wave, int lane,
-                                           unsigned char* smem, int dbg) {
-  using G = Geo<DP, true, 3, false>;
+__device__ __forceinline__ unsigned mx_e4m3(float v) {
+  return (unsigned)__builtin_amdgcn_cvt_pk_fp8_f32(v, 0.f, 0, false) & 0xffu;
+}
+__device__ __forceinline__ float mx_f32(unsigned b) { return __builtin_amdgcn_cvt_f32_fp8((int)b, 0); }
+// s with m·2^s in [128, 256): every value of the block fits e4m3 (max 448); E8M0 range clamp
+__device__ __forceinline__ int mx_shift(float m) {
+  if (!(m > 0.f)) return 0;
+  int e;
+  (void)frexpf(m, &e);
+  const int s = 8 - e;
+  return s < -120 ? -120 : (s > 120 ? 120 : s);
+}
+
+// One half of a lane's MX operand: the 16 bf16 values of one 16-B chunk (4 dwords) as -2·c, split into
+// packed hi / lo e4m3 bytes; the block scales are shared with the partner lane (lane ^ 16, the other half
+// of the 32-element block). Returns the E8M0 pair (hi | lo << 8) of this half's block.
+__device__ __forceinline__ int mx_split_half(const uint4 w0, const uint4 w1, unsigned (&wh)[4], unsigned (&wl)[4]) {
+  const unsigned ws[8] = {w0.x, w0.y, w0.z, w0.w, w1.x, w1.y, w1.z, w1.w};
+  float v[16];
+  float m = 0.f;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) {
+    v[2 * e] = -2.f * __uint_as_float(ws[e] << 16);
+    v[2 * e + 1] = -2.f * __uint_as_float(ws[e] & 0xffff0000u);
+    m = fmaxf(m, fmaxf(fabsf(v[2 * e]), fabsf(v[2 * e + 1])));
+  }
+  const int s = mx_shift(fmaxf(m, __shfl_xor(m, 16, 64)));
+  // two values per v_cvt_pk_fp8_f32 into one half of the dword: the bytes are packed as they are made (the
+  // empty asm keeps each packed dword opaque: otherwise the compiler carried every byte in its own VGPR up
+  // to the MFMA operand and spilled)
+  float mr = 0.f;
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q], s), ldexpf(v[4 * q + 1], s), 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q + 2], s), ldexpf(v[4 * q + 3], s), w, true);
+    asm volatile("" : "+v"(w));
+    wh[q] = (unsigned)w;
+    // the residuals, in place
+    v[4 * q] -= ldexpf(__builtin_amdgcn_cvt_f32_fp8(w, 0), -s);
+    v[4 * q + 1] -= ldexpf(__builtin_amdgcn_cvt_f32_fp8(w, 1), -s);
+    v[4 * q + 2] -= ldexpf(__builtin_amdgcn_cvt_f32_fp8(w, 2), -s);
+    v[4 * q + 3] -= ldexpf(__builtin_amdgcn_cvt_f32_fp8(w, 3), -s);
+    mr = fmaxf(fmaxf(mr, fmaxf(fabsf(v[4 * q]), fabsf(v[4 * q + 1]))), fmaxf(fabsf(v[4 * q + 2]), fabsf(v[4 * q + 3])));
+  }
+  const int t = mx_shift(fmaxf(mr, __shfl_xor(mr, 16, 64)));
+#pragma unroll
+  for (int q = 0; q < 4; ++q) {
+    int w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q], t), ldexpf(v[4 * q + 1], t), 0, false);
+    w = __builtin_amdgcn_cvt_pk_fp8_f32(ldexpf(v[4 * q + 2], t), ldexpf(v[4 * q + 3], t), w, true);
+    asm volatile("" : "+v"(w));
+    wl[q] = (unsigned)w;
+  }
+  return (127 - s) | ((127 - t) << 8);
+}
+
+template <int DP, int CT, int MODE>
+__device__ __forceinline__ void compute_mx(const u16* __restrict__ C, long long ldc, const float* __restrict__ cnorm,
+                                           int kc, long long nt, int wave, int lane, unsigned char* smem, int dbg) {
+  using G = Geo<DP, true, MODE, false>;
   constexpr int NB = DP / 128;          // MX k-blocks per row
   constexpr int UPS = 2 * NB;           // 16-B read units per 16-row sub-tile
   constexpr int NU = G::NSUB * UPS;
   constexpr int TAGB = 2 + (CT > 1) + (CT > 2) + (CT > 4);
   constexpr int TAGM = (1 << TAGB) - 1;
+  constexpr bool TOP2 = MODE >= 1;
   constexpr int PF = 4;                 // units read ahead (two blocks)
   constexpr int RING = PF + 2;          // a block's first unit stays live while its second lands
   static_assert(DP % 128 == 0, "MX blocks");
@@ -464,25 +512,37 @@ __device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt,
     const int c = cw0 + ct * 16 + r;
 #pragma unroll
     for (int b = 0; b < NB; ++b) {
-      uint4 q[4] = {make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u), make_uint4(0u, 0u, 0u, 0u),
-                    make_uint4(0u, 0u, 0u, 0u)};
-      int sc = 127 | (127 << 8);
-      if (c < kc) {
-        const uint4* src = reinterpret_cast<const uint4*>(ext.mx_c + ((long long)(c * NB + b) * 4 + g) * 64);
+      // half h: chunk 8b + 4h + g; half h of lanes g and g ^ 1 form scale block 2h + (g >> 1)
+      unsigned wh[2][4], wl[2][4];
+      int sc2[2];
 #pragma unroll
-        for (int i = 0; i < 4; ++i) q[i] = src[i];
-        sc = ext.mx_s[(c * NB + b) * 4 + g];
+      for (int h = 0; h < 2; ++h) {
+        uint4 w0 = make_uint4(0u, 0u, 0u, 0u), w1 = make_uint4(0u, 0u, 0u, 0u);
+        if (c < kc) {
+          const uint4* src = reinterpret_cast<const uint4*>(C + (long long)c * ldc + 16 * (8 * b + 4 * h + g));
+          w0 = src[0];
+          w1 = src[1];
+        }
+        sc2[h] = mx_split_half(w0, w1, wh[h], wl[h]);
+        __builtin_amdgcn_sched_barrier(0);
       }
-      chi[ct][b] = mx_v8i{(int)q[0].x, (int)q[0].y, (int)q[0].z, (int)q[0].w,
-                          (int)q[1].x, (int)q[1].y, (int)q[1].z, (int)q[1].w};
-      clo[ct][b] = mx_v8i{(int)q[2].x, (int)q[2].y, (int)q[2].z, (int)q[2].w,
-                          (int)q[3].x, (int)q[3].y, (int)q[3].z, (int)q[3].w};
-      csc[ct][b] = sc;
+      chi[ct][b] = mx_v8i{(int)wh[0][0], (int)wh[0][1], (int)wh[0][2], (int)wh[0][3],
+                          (int)wh[1][0], (int)wh[1][1], (int)wh[1][2], (int)wh[1][3]};
+      clo[ct][b] = mx_v8i{(int)wl[0][0], (int)wl[0][1], (int)wl[0][2], (int)wl[0][3],
+                          (int)wl[1][0], (int)wl[1][1], (int)wl[1][2], (int)wl[1][3]};
+      // lane group g supplies the scale of block g = 2h + (g' >> 1): half g >> 1 of lane group 2(g & 1)
+      const int src = r + 16 * (2 * (g & 1));
+      const int s0 = __shfl(sc2[0], src, 64);
+      const int s1 = __shfl(sc2[1], src, 64);
+      csc[ct][b] = (g >> 1) ? s1 : s0;
+      // one block at a time: left free, the scheduler hoisted every block's loads and split temporaries
+      // ahead and spilled (the operands alone take 128 VGPRs at CT = 2, D = 512)
+      __builtin_amdgcn_sched_barrier(0);
     }
 #pragma unroll
     for (int i = 0; i < 4; ++i) {
       const int c2 = cw0 + ct * 16 + 4 * g + i;
-      c4[ct][i] = c2 < kc ? ext.cn_t[c2] : __builtin_huge_valf();
+      c4[ct][i] = c2 < kc ? cnorm[c2] : __builtin_huge_valf();
     }
   }
   __builtin_amdgcn_s_setprio(1);
@@ -522,12 +582,12 @@ __device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt,
         const mx_v8i xb = mx_v8i{(int)a0.x, (int)a0.y, (int)a0.z, (int)a0.w, (int)a1.x, (int)a1.y, (int)a1.z, (int)a1.w};
         if (s == 0) {
           key[cur] = 0x7fffffff;
-          key2[cur] = 0x7fffffff;
+          if constexpr (TOP2) key2[cur] = 0x7fffffff;
         }
 #pragma unroll
         for (int ct = 0; ct < CT; ++ct) {
-          f32x4 a = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(chi[ct][s], xb, s == 0 ? (c4[ct] + xnv[t]) : acc[cur][ct],
-                                                                    0, 0, 0, csc[ct][s], 0, 127);
+          const f32x4 a = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(
+              chi[ct][s], xb, s == 0 ? (c4[ct] + xnv[t]) : acc[cur][ct], 0, 0, 0, csc[ct][s], 0, 127);
           acc[cur][ct] = __builtin_amdgcn_mfma_scale_f32_16x16x128_f8f6f4(clo[ct][s], xb, a, 0, 0, 1, csc[ct][s], 0, 127);
         }
         if (t > 0) {  // keys of the previous sub-tile, spread over this one's blocks
@@ -535,12 +595,12 @@ __device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt,
           for (int e = (s * CT * 4) / NB; e < ((s + 1) * CT * 4) / NB; ++e) {
             const int ct = e >> 2, i = e & 3;
             const int kv = (__float_as_int(acc[prv][ct][i]) & ~TAGM) | (ct << 2 | i);
-            key2[prv] = med3(key[prv], kv, key2[prv]);
+            if constexpr (TOP2) key2[prv] = med3(key[prv], kv, key2[prv]);
             key[prv] = kv < key[prv] ? kv : key[prv];
           }
           if (s == NB - 1) {
             kred[(16 * (t - 1) + r) * G::STRIDE + wave * 4 + g] = key[prv];
-            kred[(16 * (t - 1) + r) * G::STRIDE + 16 + wave * 4 + g] = key2[prv];
+            if constexpr (TOP2) kred[(16 * (t - 1) + r) * G::STRIDE + 16 + wave * 4 + g] = key2[prv];
           }
         }
       }
@@ -552,11 +612,11 @@ __device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt,
       for (int e = 0; e < CT * 4; ++e) {
         const int ct = e >> 2, i = e & 3;
         const int kv = (__float_as_int(acc[cur][ct][i]) & ~TAGM) | (ct << 2 | i);
-        key2[cur] = med3(key[cur], kv, key2[cur]);
+        if constexpr (TOP2) key2[cur] = med3(key[cur], kv, key2[cur]);
         key[cur] = kv < key[cur] ? kv : key[cur];
       }
       kred[(16 * t + r) * G::STRIDE + wave * 4 + g] = key[cur];
-      kred[(16 * t + r) * G::STRIDE + 16 + wave * 4 + g] = key2[cur];
+      if constexpr (TOP2) kred[(16 * t + r) * G::STRIDE + 16 + wave * 4 + g] = key2[cur];
     }
     wait_lgkm0();
     barrier();  // B(j)
@@ -567,7 +627,7 @@ __device__ __forceinline__ void compute_mx(const Ext& ext, int kc, long long nt,
 // HBM and LDS traffic) and every compute wave widens its fragments with v_cvt_scalef32_pk_bf16_fp8
 // (exact: e4m3 values are a subset of bf16); one 16-B read then covers TWO k-steps, step 2v+h of lane
 // (r, g) holding k = 64v + 16g + 8h + j, and the centre fragments follow the same k order.
-template <int DP, int CT, bool F8, int MODE, bool M32>
+template <int DP, int CT, bool F8, int MODE, bool M32, bool MX = false>
 __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     const unsigned char* __restrict__ X, long long n, long long ldx, const u16* __restrict__ C, long long ldc, int kc,
     int kp, const float* __restrict__ cnorm, const float* __restrict__ xnorm, int* __restrict__ labels,
@@ -583,7 +643,6 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   constexpr int TAGM = (1 << TAGB) - 1;
   constexpr bool TOP2 = MODE >= 1;
   if (ext.gate != nullptr && *ext.gate != ext.want) return;  // uniform: before any barrier
-  if (ext.gate2 != nullptr && (((long long)*ext.gate2 <= ext.g2cap) != (ext.g2le != 0))) return;
   if constexpr (MODE == 2) n = *ext.n_dev;
   const int* lab_src = MODE == 2 ? ext.lab_in : labels;  // trailer source of the previous labels
   extern __shared__ __attribute__((aligned(16))) unsigned char smem[];
@@ -604,8 +663,8 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
   auto tile_of = [&](long long j) { return (long long)blockIdx.x + j * gridDim.x; };
 
   if (wave < kCompute) {
-   if constexpr (MODE == 3) {
-    compute_mx<DP, CT>(ext, kc, nt, wave, lane, smem, dbg);
+   if constexpr (MX) {
+    compute_mx<DP, CT, MODE>(C, ldc, cnorm, kc, nt, wave, lane, smem, dbg);
    } else if constexpr (M32) {
     for (int i = tid; i < cn_slots(kp); i += kCompute * 64) cnl[i] = i < kc ? cnorm[i] : __builtin_huge_valf();
     compute_m32<DP, CT, F8, MODE>(C, ldc, kc, nt, wave, lane, smem, cnl, dbg);
@@ -769,24 +828,11 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
     constexpr int RPF = G::TR / 2;  // rows per finalize wave
     if (fw == 0) {
       for (int i = lane; i < kp; i += 64) hist[i] = 0;
-      // append: this workgroup's change list continues the one an earlier launch of the step left
-      if (lane == 0) misc[0] = dout.append != 0 && dout.wg_count != nullptr ? dout.wg_count[blockIdx.x] : 0;
+      if (lane == 0) misc[0] = 0;
     }
     double cost = 0.0;
     float mcv = 0.f;
     if constexpr (TOP2) mcv = *ext.mc;
-    float mx_e = 0.f, mx_n = 0.f;  // MODE 3: max|~c - cb|, max|~c|² over the centres
-    if constexpr (MODE == 3) {
-      for (int i = lane; i < kc; i += 64) {
-        mx_e = fmaxf(mx_e, ext.mx_stat[i]);
-        mx_n = fmaxf(mx_n, ext.cn_t[i]);
-      }
-#pragma unroll
-      for (int o = 1; o < 64; o <<= 1) {
-        mx_e = fmaxf(mx_e, __shfl_xor(mx_e, o, 64));
-        mx_n = fmaxf(mx_n, __shfl_xor(mx_n, o, 64));
-      }
-    }
     // LPR_F lanes per row, each taking 16 / LPR_F of the 16 (wave, lane-group) keys; keys are loaded
     // in one batch and reduced branch-free on a 64-bit (value, centre index) composite
     constexpr int LPR_F = 64 / RPF;
@@ -848,25 +894,7 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
       const int bi = (int)(best & 0xffffffffu);
       const float dist = fmaxf(__int_as_float((int)((unsigned)(best >> 32) ^ 0x80000000u)), 0.f);
       const bool mine = part == 0 && pos < n;
-      // MODE 3 certificate: dist / sd are the MX pass's f32 distances to ~c (error <= 4·tau·(|x|² + max|~c|²)
-      // with the key truncation: the MX MFMA's own sums measured within 2^-17 of Σ|terms|, 2^-15 tested), |~c_j - cb_j| <= e moves a distance by at most e, and the bf16 pass's own
-      // values are within tau·(|x|² + max|cb|²) of the exact ones: when the bf16 bounds U (label) and L (every
-      // other centre) are apart by more than both slacks, the bf16 pass picks this label too. Otherwise the
-      // row goes to the re-check list.
-      bool cert = true;
-      float ubv = 0.f, lbv = 0.f;
-      float xnr = 0.f;
-      if constexpr (MODE == 3) {
-        xnr = reinterpret_cast<const float*>(te)[R];
-        const float sl_t = 4.f * ext.tau * (xnr + mx_n);
-        const float sl_b = ext.tau * (xnr + mcv);
-        const float sd = __int_as_float((int)(sec ^ 0x80000000u));
-        ubv = (sqrtf(dist + sl_t) * (1.0f + 1e-6f) + mx_e) * (1.0f + 1e-6f);
-        lbv = (sqrtf(fmaxf(sd - sl_t, 0.f)) * (1.0f - 1e-6f) - mx_e) * (1.0f - 1e-6f);
-        cert = lbv > 0.f && (lbv * lbv) * (1.0f - 1e-6f) - sl_b > (ubv * ubv) * (1.0f + 1e-6f) + sl_b;
-        lbv = fmaxf(lbv, 0.f);
-      }
-      const bool ch = mine && cert && old != bi;
+      const bool ch = mine && old != bi;
       if (dout.rows != nullptr) {
         const unsigned long long bal = __ballot(ch);
         if (bal != 0ull) {
@@ -882,24 +910,8 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
           }
         }
       }
-      if constexpr (MODE == 3) {
-        const bool unc = mine && !cert;
-        const unsigned long long bu = __ballot(unc);
-        if (bu != 0ull) {
-          const int leader = __builtin_ctzll(bu);
-          int base = 0;
-          if (lane == leader) base = atomicAdd(ext.u_cnt, (int)__popcll(bu));
-          base = __shfl(base, leader, 64);
-          const long long at = (long long)base + (long long)__popcll(bu & ((1ull << lane) - 1ull));
-          if (unc && at < ext.u_cap) {
-            ext.u_idx[at] = (int)row;
-            ext.u_lab[at] = old;
-            ext.u_xn[at] = xnr;
-          }
-        }
-      }
       if (ch) labels[row] = bi;
-      if (mine && cert) {
+      if (mine) {
         cost += (double)dist;
         if (best_out != nullptr) best_out[row] = dist;
         if constexpr (MODE == 2) {
@@ -910,14 +922,11 @@ __global__ __launch_bounds__(kThreads, 1) void kmeans_assign_rr(
         }
         if (ranking) rank_out[row] = atomicAdd(hist + bi, 1);
         if constexpr (TOP2) {
-          float u = ubv, w = lbv;
-          if constexpr (MODE != 3) {
-            const float xn = reinterpret_cast<const float*>(te)[R];
-            const float slack = ext.tau * (xn + mcv);
-            const float sd = __int_as_float((int)(sec ^ 0x80000000u));
-            u = sqrtf(dist + slack) * (1.0f + 1e-6f);
-            w = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
-          }
+          const float xn = reinterpret_cast<const float*>(te)[R];
+          const float slack = ext.tau * (xn + mcv);
+          const float sd = __int_as_float((int)(sec ^ 0x80000000u));
+          float u = sqrtf(dist + slack) * (1.0f + 1e-6f);
+          float w = sqrtf(fmaxf(sd - slack, 0.f)) * (1.0f - 1e-6f);
           if (ext.cu != nullptr) {
             const float cu = ext.cu[bi], cl = ext.cl[bi];
             u = (u - cu) + 1e-6f * (u + cu);
@@ -1005,7 +1014,7 @@ inline long long lds_for_mode(int Dp, int kp, bool f8) {
 }
 
 inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
-  const bool m32 = mode != 3 && use_m32(Dp, plan_ct(Dp, kp, f8), f8);
+  const bool m32 = use_m32(Dp, plan_ct(Dp, kp, f8), f8);
   switch (mode * 2 + (m32 ? 1 : 0)) {
     case 0: return lds_for_mode<0, false>(Dp, kp, f8);
     case 1: return lds_for_mode<0, true>(Dp, kp, f8);
@@ -1013,39 +1022,29 @@ inline long long lds_for(int Dp, int kp, bool f8 = false, int mode = 0) {
     case 3: return lds_for_mode<1, true>(Dp, kp, f8);
     case 4: return lds_for_mode<2, false>(Dp, kp, f8);
     case 5: return lds_for_mode<2, true>(Dp, kp, f8);
-    case 6: return f8 ? lds_for_mode<3, false>(Dp, kp, f8) : 0;
     default: return 0;
   }
 }
 
+// MX arithmetic for fp8 rows (compute_mx), on unless cml_kmeans_set_fp8_mx(0) / CML_KMEANS_FP8_MX=0 (the
+// widening bf16 pass: A/B). The fp8 engines snap their centres to the MX grid while it is on.
+inline int g_mx = 1;
+inline bool use_mx(int Dp, bool f8, bool m32) { return f8 && g_mx && !m32 && Dp % 128 == 0; }
+
 // X: bf16 rows (ldx elements) or, with f8, e4m3fn rows (ldx bytes).
-template <int DP, int CT, bool F8, int MODE, bool M32>
+template <int DP, int CT, bool F8, int MODE, bool M32, bool MX = false>
 int launch(const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc, int kp, const float* cnorm,
            const float* xnorm, int* labels, float* best, double* cost_part, int* hist, int* rank, DeltaOut dout,
            Ext ext, int grid, int dbg, hipStream_t st) {
   const size_t lds = (size_t)lds_bytes<DP, F8, MODE, M32>(kp);
   if (lds > 160 * 1024) return (int)hipErrorInvalidValue;
-  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8, MODE, M32>;
+  const void* fn = (const void*)kmeans_assign_rr<DP, CT, F8, MODE, M32, MX>;
   hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
   const long long ldb = F8 ? ldx : 2 * ldx;
-  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8, MODE, M32>), dim3(grid), dim3(kThreads), lds, st,
+  hipLaunchKernelGGL((kmeans_assign_rr<DP, CT, F8, MODE, M32, MX>), dim3(grid), dim3(kThreads), lds, st,
                      (const unsigned char*)X, n, ldb, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist,
                      rank, dout, ext, dbg);
   return cml_status();
-}
-
-// MODE 3 (fp8 screen): fp8 rows, 16x16 tiles only
-inline int dispatch_mx(int Dp, int ct, const void* X, long long n, long long ldx, const u16* C, long long ldc, int kc,
-                       int kp, const float* cnorm, const float* xnorm, int* labels, float* best, double* cost_part,
-                       DeltaOut dout, Ext ext, int grid, int dbg, hipStream_t st) {
-#define CML_RX(D, T)                                                                                                \
-  if (Dp == D && ct == T)                                                                                           \
-  return launch<D, T, true, 3, false>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, nullptr,   \
-                                      nullptr, dout, ext, grid, dbg, st)
-  CML_RX(256, 1); CML_RX(256, 2); CML_RX(256, 3); CML_RX(256, 4);
-  CML_RX(512, 1); CML_RX(512, 2);
-#undef CML_RX
-  return (int)hipErrorInvalidValue;
 }
 
 template <int MODE>
@@ -1054,6 +1053,16 @@ inline int dispatch_mode(int Dp, int ct, bool f8, const void* X, long long n, lo
                          float* best, double* cost_part, int* hist, int* rank, DeltaOut dout, Ext ext, int grid,
                          int dbg, hipStream_t st) {
   const bool m32 = use_m32(Dp, ct, f8);
+  if (use_mx(Dp, f8, m32)) {
+#define CML_RX(D, T)                                                                                                \
+  if (Dp == D && ct == T)                                                                                           \
+  return launch<D, T, true, MODE, false, true>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,   \
+                                               hist, rank, dout, ext, grid, dbg, st)
+    CML_RX(256, 1); CML_RX(256, 2); CML_RX(256, 3); CML_RX(256, 4);
+    CML_RX(512, 1); CML_RX(512, 2);
+#undef CML_RX
+    return (int)hipErrorInvalidValue;
+  }
 #define CML_RR(D, T, F, M)                                                                                          \
   if (Dp == D && ct == T && f8 == F && m32 == M)                                                                    \
   return launch<D, T, F, MODE, M>(X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part, hist, rank,    \
@@ -1084,9 +1093,6 @@ inline int dispatch(int mode, int Dp, int ct, bool f8, const void* X, long long 
                                     hist, rank, dout, ext, grid, dbg, st);
     case 2: return dispatch_mode<2>(Dp, ct, f8, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best, cost_part,
                                     hist, rank, dout, ext, grid, dbg, st);
-    case 3: return f8 && hist == nullptr ? dispatch_mx(Dp, ct, X, n, ldx, C, ldc, kc, kp, cnorm, xnorm, labels, best,
-                                                       cost_part, dout, ext, grid, dbg, st)
-                                         : (int)hipErrorInvalidValue;
     default: return (int)hipErrorInvalidValue;
   }
 }

@@ -331,7 +331,13 @@ class LloydEngine:
             self._wx = torch.cat([self.x * w[:, None], w[:, None]], 1)  # [w·x | w]: one sums pass
         # error allowance of the assign's squared distances (pruning bounds), scaled with the padded
         # width: the f32 accumulation error grows with D; f64 rows keep the fixed floor
+        # fp8 rows: the K9r passes run MX-scaled fp8 MFMAs against an exact e4m3 split of the centres, which
+        # stay on the MX grid (kmeans_mx.hip mx_snap after every update); the allowance is doubled for the MX
+        # instruction's own sums (measured within 2^-17 of Σ|terms| per 128 products)
+        self._mx = self.gpu and K.mx_applies(self.x)
         self._tau = self.prune_tau(self.dp) if self.gpu else self._PRUNE_TAU
+        if self._mx:
+            self._tau *= 2.0
         if row_chunks is None:
             row_chunks = 2 if (self.comm.is_distributed and self.n >= (1 << 20)) else 1
         self.row_chunks = max(1, min(int(row_chunks), max(1, self.n)))
@@ -517,7 +523,8 @@ class LloydEngine:
         else:
             self.centers = c.contiguous().clone()
         if self.gpu:
-            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None,
+                             snap=self._mx)
         if getattr(self, "_scr", None) is not None and getattr(self._scr, "cert", None) is not None:
             self._scr.cert.valid = False  # the certified step restarts from a screened full assignment
         self._shift_pair = None
@@ -702,11 +709,12 @@ class LloydEngine:
         if self.spherical:
             self._prev_centers.copy_(self.centers)
         K.update_centers(msgs, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm,
-                         self.shift2, unit=self._unit)
+                         self.shift2, unit=self._unit, snap=self._mx)
         if self.spherical:  # unit-length centres (empty clusters keep their old, already unit, centre)
             self.centers.div_(self.centers.norm(dim=1, keepdim=True).clamp_(min=1e-300))
             torch.sum((self.centers - self._prev_centers) ** 2, dim=1, out=self.shift2)
-            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None)
+            K.update_centers(None, self.k, self.d, self.centers, self.cb, self.dp, self.kp, self.cnorm, None,
+                             snap=self._mx)
         self._shift2 = self.shift2
 
     # ------------------------------------------------------------------ MFMA-screened exact assignment
@@ -1041,7 +1049,7 @@ class LloydEngine:
         st = types.SimpleNamespace(history=[])
         cap = float(os.environ.get("CML_KMEANS_PRUNE_CAP", self._PRUNE_CAP))  # A/B knob (bench --prune-cap)
         st.cap_m = max(tr, int(math.ceil(cap * n)))
-        st.tau = self.prune_tau(self.dp)
+        st.tau = self._tau
         per_wg = -(-(-(-st.cap_m // tr)) // ap.grid) * tr
         pad = round_up(st.cap_m, tr) + tr
         st.cand = torch.zeros(pad, dtype=torch.int32, device=dev)
@@ -1076,14 +1084,8 @@ class LloydEngine:
                   if os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096 else None)
         # completion counters of the fused launches (gate in the bounds pass, stats in the half pass); each
         # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
-        # [2]: the fp8 screen's uncertified-row counter (re-armed by the gate)
-        st.ctr = torch.zeros(3, dtype=torch.int32, device=dev)
+        st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
         st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
-        # fp8 rows: the full pass is the MX screen (kmeans_rr.h MODE 3) + a bf16 re-check of the rows it cannot
-        # certify; CML_KMEANS_FP8_SCREEN=0 keeps the widening bf16 pass (A/B)
-        st.screen = (st.fused and K.is_fp8(self.x) and self.dp % 128 == 0 and ap.rr_ct > 0
-                     and os.environ.get("CML_KMEANS_FP8_SCREEN", "1") != "0")
-        st.mx_ops = K.mx_centres_buffers(ap.kp, self.dp, dev) if st.screen else None
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
@@ -1111,49 +1113,22 @@ class LloydEngine:
         if st.fused:  # bounds pass + gate in one launch
             K.prune_bounds_gated(lab[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                                  self.xnorm, st.cand_lab, st.cand_xn, st.flags, st.cum, st.pmode, st.cap_m,
-                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1],
-                                 zero=st.ctr[2:3] if st.screen else None)
+                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1])
         else:
             K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                            xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
                            cum=st.cum) if n else None
             K.prune_gate(st.count, st.cap_m, st.flags, st.pmode, backoff=st.backoff if st.nback > 0 else None,
                          nback=st.nback)
-        if st.screen:
-            self._pdev_screen()
-        else:
-            K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
-                            st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
+        K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
+                        st.mc, st.tau, hist=self.hist, rank=self.rank, delta=dl, gate=st.pmode, want=1, cum=st.cum)
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
                         gate=st.pmode, want=0, cum=st.cum)
         dl.gate(0)
-        if st.screen:  # counting-sort ranks of the final labels when the sums are re-accumulated in full
-            K.label_hist(lab, n, ap, self.hist, self.rank, gate=dl.mode[0], want=1)
         K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                           self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
-
-    def _pdev_screen(self) -> None:
-        """Full pass of a device pruned step on fp8 rows (all launches gated on the full-pass flag): the MX
-        operands of the bf16 centres (kmeans_mx.hip), the MX screen over every row — labels and bounds of
-        the rows whose top-2 gap it certifies, the others listed (row, old label, norm) in the candidate
-        buffers (free in a full step) — then the bf16 candidate pass over that list, or, when the list
-        outgrew its capacity, the bf16 full pass. Labels, change lists and bounds end as the bf16 full
-        pass leaves them (kmeans_rr.h MODE 3); the ranks come from label_hist when needed."""
-        st, dl, ap = self._pst, self.delta, self.aplan
-        n, k, x, lab = self.n, self.k, self.x, self.labels
-        ucnt = st.ctr[2:3]
-        K.mx_centres(self.cb, k, ap.kp, self.dp, out=st.mx_ops, gate=st.pmode)
-        K.assign_rr_ext(3, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
-                        st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum, mx=st.mx_ops,
-                        ulist=(st.cand, st.cand_lab, st.cand_xn, ucnt, st.cap_m))
-        K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
-                        st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=ucnt, lab_in=st.cand_lab, gate=st.pmode,
-                        want=1, cum=st.cum, gate2=(ucnt, st.cap_m, True), append=True)
-        K.assign_rr_ext(1, x, n, self.dp, self.cb, self.cnorm, ap, self.xnorm, lab, self.cost_part, st.ub, st.lb,
-                        st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum, gate2=(ucnt, st.cap_m, False),
-                        append=True)
 
     def _pdev_post(self) -> None:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
@@ -1162,7 +1137,7 @@ class LloydEngine:
         if st.fused and not self.spherical and self.dp <= 2048:
             # K11 + cb_old / cb_cost copies + norms + drifts in one launch, then the centre statistics in one
             K.update_pdev(self.msgs, k, d, self.centers, self.cb, self.dp, self.kp, self.cnorm, self.shift2,
-                          self._unit, st.cb_old, st.cb_cost, st.flags, st.cn, st.drift)
+                          self._unit, st.cb_old, st.cb_cost, st.flags, st.cn, st.drift, snap=self._mx)
             self._shift2 = self.shift2
             K.centre_half_stats(self.cb, k, self.dp, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc,
                                 st.c2, st.count, st.force, st.cum, st.backoff if st.nback > 0 else None,
@@ -1591,10 +1566,7 @@ class LloydEngine:
         if self._pst is None:
             return {}
         full, m = self._pdev_last() if self._pdev else self._pst.last
-        out = {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
-        if self._pdev and getattr(self._pst, "screen", False) and full:
-            out["screen_rechecked"] = int(self._pst.ctr[2].item())  # rows the fp8 screen left to the bf16 pass
-        return out
+        return {"full": bool(full), "reassigned_rows": int(m), "rows": self.n}
 
     def prune_history(self) -> list:
         """(full step?, re-assigned rows) of every pruned step of this engine, rank-local."""
@@ -1974,7 +1946,7 @@ class LloydEngine:
             kp_all = round_up(mt, 64)
             cbn = torch.empty((kp_all, dp), dtype=torch.bfloat16, device=dev)
             cnn = torch.empty(kp_all, dtype=torch.float32, device=dev)
-            K.update_centers(None, mt, d, new, cbn, dp, kp_all, cnn, None)
+            K.update_centers(None, mt, d, new, cbn, dp, kp_all, cnn, None, snap=self._mx)
             # once most rows sit near a candidate, only the new candidates close to a row's nearest one
             # can take it over (_init_candidate_pass_pruned): the second round at once; in the first
             # round (only the first centre so far) everything after the first K9r chunk
@@ -2067,7 +2039,7 @@ class LloydEngine:
         c0 = c0.reshape(1, d)
         if c0.dtype != torch.float64 or not c0.is_contiguous():
             c0 = c0.to(torch.float64).contiguous()
-        K.update_centers(None, 1, d, c0, cb0, dp, 32, cn0, None)
+        K.update_centers(None, 1, d, c0, cb0, dp, 32, cn0, None, snap=self._mx)
         alloc = torch.empty if n else torch.zeros  # (the row pass writes every row's cost and nearest)
         costs = alloc(max(n, 1), dtype=torch.float32, device=dev)
         nearest = alloc(max(n, 1), dtype=torch.int32, device=dev)
@@ -2249,7 +2221,7 @@ def assign_gpu(x: torch.Tensor, dp: int, d: int, centers: torch.Tensor, xnorm: O
     cb = torch.zeros((kp, dp), dtype=torch.bfloat16, device=dev)
     cn = torch.zeros(kp, dtype=torch.float32, device=dev)
     cent = centers.to(device=dev, dtype=torch.float64).contiguous().clone()
-    K.update_centers(None, k, d, cent, cb, dp, kp, cn, None)
+    K.update_centers(None, k, d, cent, cb, dp, kp, cn, None, snap=K.mx_applies(x))
     labels = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     best = torch.empty(max(n, 1), dtype=torch.float32, device=dev)
     if n:

@@ -33,6 +33,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_set_rr_default": (c_int, [c_int]),
     "cml_kmeans_set_rr_debug": (c_int, [c_int]),
     "cml_kmeans_set_rr_m32": (c_int, [c_int]),
+    "cml_kmeans_set_fp8_mx": (c_int, [c_int]),
     "cml_kmeans_assign_tile_rows": (c_int, [c_int]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
@@ -68,9 +69,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_assign_rr_ext": (c_int, [c_int, c_vp, c_ll, c_ll, c_int, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                          c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
                                          c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp, c_int,
-                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int,
-                                         c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_ll, c_int,
-                                         c_int, c_vp]),
+                                         c_vp, c_vp, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_kmeans_init_classify": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_int, ctypes.c_float, c_ll, c_int, c_vp,
                                          c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_near_list": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_vp,
@@ -116,7 +115,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_pair_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_prune_bounds_gated": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
-                                              c_vp, c_vp]),
+                                              c_vp]),
     "cml_kmeans_update_pdev": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                        c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_centre_half_stats": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp,
@@ -136,7 +135,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_cert_moves": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_mx_probe": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
-    "cml_kmeans_mx_centres": (c_int, [c_vp, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_mx_snap": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
 })
 _native.register_host_sigs({
     "cml_local_kmeans_host": (c_int, [c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, ctypes.c_uint64, c_int,
@@ -359,6 +358,8 @@ def _apply_env_knobs(lib) -> None:
     m32 = os.environ.get("CML_KMEANS_RR_M32")
     if m32:
         _native.check(lib.cml_kmeans_set_rr_m32(int(m32)), "set_rr_m32")
+    if os.environ.get("CML_KMEANS_FP8_MX") == "0":
+        lib.cml_kmeans_set_fp8_mx(0)
 
 
 def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = False) -> AssignPlan:
@@ -688,29 +689,31 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
 
 
 def prune_bounds_gated(labels, ub, lb, drift, dmax, thr, c2, k: int, cand, count, xn, cand_lab, cand_xn, flags,
-                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None, zero=None) -> None:
+                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None) -> None:
     """K9p with the step gate folded in (kmeans_prune.hip): the bounds pass (skipped when flags[0] / flags[1]
     are set) and, in the workgroup that finishes last, kmeans_prune_gate's decision into ``mode``; ``done``
-    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics.
-    ``zero`` (int32 [1], optional): a counter of the step's later launches, set to 0 by the gate."""
+    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics."""
     n = int(labels.shape[0])
     _native.check(_native.kernels().cml_kmeans_prune_bounds_gated(
         labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
         c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
         flags.data_ptr(), int(cand.shape[0]), _ptr(cum), mode.data_ptr(), int(gate_cap), _ptr(backoff), int(nback),
-        done.data_ptr(), _ptr(zero), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
+        done.data_ptr(), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
 
 
 def update_pdev(msgs: torch.Tensor, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int, kp: int,
                 cnorm: torch.Tensor, shift2: torch.Tensor, unit: float, cb_old: torch.Tensor, cb_cost: torch.Tensor,
-                flags: torch.Tensor, cn64: torch.Tensor, drift: torch.Tensor, stream=None) -> None:
+                flags: torch.Tensor, cn64: torch.Tensor, drift: torch.Tensor, stream=None, snap: bool = False) -> None:
     """K11 of the device pruned step with its bookkeeping in the same launch (kmeans_prune.hip
     kmeans_update_pdev_kernel): cb_old <- old cb, cb_cost <- old cb unless frozen (flags[1]), the new centres,
-    their bf16 copy and norms (f32 cnorm, f64 cn64), the shift and the bf16 drift rounded up."""
+    their bf16 copy and norms (f32 cnorm, f64 cn64), the shift and the bf16 drift rounded up. ``snap``: the
+    bf16 centres then go onto the MX grid, norms and drifts recomputed (mx_snap)."""
     _native.check(_native.kernels().cml_kmeans_update_pdev(
         msgs.data_ptr(), msgs.shape[0], msgs.stride(0), int(k), int(d), cent.data_ptr(), cb.data_ptr(), cb.stride(0),
         int(dp), int(kp), cnorm.data_ptr(), shift2.data_ptr(), float(unit), cb_old.data_ptr(), cb_cost.data_ptr(),
         flags.data_ptr(), cn64.data_ptr(), drift.data_ptr(), _native.stream_ptr(stream)), "kmeans_update_pdev")
+    if snap:
+        mx_snap(cb, k, dp, cnorm, cn64=cn64, cb_old=cb_old, drift=drift, stream=stream)
 
 
 def centre_half_stats(cb: torch.Tensor, k: int, d: int, cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor,
@@ -789,24 +792,32 @@ def mx_probe(a: torch.Tensor, b: torch.Tensor, sa: torch.Tensor, sb: torch.Tenso
     return out
 
 
-def mx_centres_buffers(kp: int, dp: int, device) -> tuple:
-    """The four output tensors of mx_centres."""
-    return (torch.zeros((kp, dp // 128, 4, 64), dtype=torch.uint8, device=device),
-            torch.zeros((kp, dp // 128, 4), dtype=torch.int32, device=device),
-            torch.zeros(kp, dtype=torch.float32, device=device), torch.zeros(kp, dtype=torch.float32, device=device))
+def mx_snap(cb: torch.Tensor, kc: int, dp: int, cnorm: torch.Tensor, cn64: torch.Tensor | None = None,
+            cb_old: torch.Tensor | None = None, drift: torch.Tensor | None = None, stream=None) -> None:
+    """Centres of an fp8 engine onto the MX grid, in place (kmeans_mx.hip kmeans_mx_snap_kernel): each
+    32-element block of a bf16 row becomes its exact two-term e4m3 split (the MX assign's operand), with
+    cnorm (and cn64, drift against cb_old when given) recomputed from the snapped rows."""
+    _native.check(_native.kernels().cml_kmeans_mx_snap(cb.data_ptr(), cb.stride(0), int(kc), int(dp),
+                                                      cnorm.data_ptr(), _ptr(cn64), _ptr(cb_old), _ptr(drift),
+                                                      _native.stream_ptr(stream)), "kmeans_mx_snap")
 
 
-def mx_centres(cb: torch.Tensor, kc: int, kp: int, dp: int, out=None, stream=None, gate=None):
-    """MX operands of the screen pass (kmeans_mx.hip): hi/lo e4m3 bytes of -2·cb in the K9r fp8 lane order
-    [kp, dp/128, 4, 64], their E8M0 scales [kp, dp/128, 4] (hi | lo << 8), |~c|² [kp] and |~c - cb| [kp]
-    (rounded up). ``out``: the same four tensors, reused; ``gate``: run only when gate[0] == 1."""
-    if out is None:
-        out = mx_centres_buffers(kp, dp, cb.device)
-    mc, ms, cn, stat = out
-    _native.check(_native.kernels().cml_kmeans_mx_centres(cb.data_ptr(), cb.stride(0), int(kc), int(kp), int(dp),
-                                                          mc.data_ptr(), ms.data_ptr(), cn.data_ptr(), stat.data_ptr(),
-                                                          _ptr(gate), _native.stream_ptr(stream)), "kmeans_mx_centres")
-    return out
+def set_fp8_mx(on: bool) -> bool:
+    """MX-scaled fp8 MFMA arithmetic for the fp8 K9r passes (default on; CML_KMEANS_FP8_MX=0: the bf16
+    widening pass). Returns the previous setting. Engines created while it is on keep their centres on the
+    MX grid (mx_snap)."""
+    return bool(_native.kernels().cml_kmeans_set_fp8_mx(int(bool(on))))
+
+
+def fp8_mx_on() -> bool:
+    lib = _native.kernels()
+    _apply_env_knobs(lib)
+    return bool(lib.cml_kmeans_set_fp8_mx(-1))
+
+
+def mx_applies(x: torch.Tensor) -> bool:
+    """Whether the fp8 assign passes on ``x`` run MX arithmetic (fp8 rows on the GPU, toggle on)."""
+    return x.is_cuda and is_fp8(x) and fp8_mx_on()
 
 
 def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor, cnorm: torch.Tensor,
@@ -818,19 +829,14 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
                   gate: torch.Tensor | None = None, want: int = 0, stream=None,
                   best: torch.Tensor | None = None, cum: torch.Tensor | None = None,
                   merge_cost: torch.Tensor | None = None, merge_near: torch.Tensor | None = None,
-                  merge_off: int = 0, mx=None, ulist=None, gate2=None, append: bool = False) -> None:
+                  merge_off: int = 0) -> None:
     """K9r with the pruned-step extensions (``kmeans_rr.h``): ``mode`` 1 assigns every row and writes
     the top-2 bounds ``ub``/``lb``; ``mode`` 2 assigns the candidate positions (rows ``idx``, count
     ``n_dev`` on the device; ``xnorm``/``lab_in`` compacted) — labels and bounds land at the real
     rows. ``delta`` logs label changes; ``gate``/``want`` make the launch conditional on a device flag;
     ``best`` (f32, real rows) receives the squared distance to the new label; ``merge_cost``/``merge_near``
     (mode 2, f32/int32 per real row) take the k-means|| merge: strictly nearer rows get (distance, label +
-    ``merge_off``).
-
-    ``mode`` 3 (fp8 rows): the MX screen (kmeans_rr.h compute_mx) over every row with the centre operands
-    ``mx`` = mx_centres(...) — certified rows get labels and bounds as mode 1, the others go to ``ulist`` =
-    (rows, old labels, norms, int32 counter, capacity) for a bf16 re-check. ``gate2`` = (int32 [1], cap, le):
-    the launch also needs (gate2 <= cap) == le. ``append``: the change lists continue an earlier launch's."""
+    ``merge_off``)."""
     if plan.rr_ct <= 0 or plan.kc != plan.kp:
         raise ValueError("the pruned-step assign needs the K9r plan (Dp in {128, 256, 512}, k <= 256)")
     _native.check(_native.kernels().cml_kmeans_assign_rr_ext(
@@ -842,10 +848,7 @@ def assign_rr_ext(mode: int, x: torch.Tensor, n: int, dp: int, cb: torch.Tensor,
         delta.pcap if delta is not None else 0, plan.rr_ct, _ptr(idx), _ptr(n_dev), _ptr(lab_in), ub.data_ptr(),
         lb.data_ptr(), mc.data_ptr(), float(tau), _ptr(gate), int(want), _ptr(best), _ptr(cum),
         int(cum.shape[0] // 2) if cum is not None else 0, _ptr(merge_cost), _ptr(merge_near), int(merge_off),
-        *(_ptr(t) for t in (mx if mx is not None else (None,) * 4)),
-        *(_ptr(t) for t in (ulist[:4] if ulist is not None else (None,) * 4)), int(ulist[4]) if ulist else 0,
-        _ptr(gate2[0] if gate2 else None), int(gate2[1]) if gate2 else 0, int(bool(gate2[2])) if gate2 else 0,
-        int(append), _native.stream_ptr(stream)),
+        _native.stream_ptr(stream)),
         f"kmeans_assign_rr_ext(mode={mode})")
 
 
@@ -981,9 +984,11 @@ def seg_buffer_ints(k: int) -> int:
 
 
 def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int,
-                   kp: int, cnorm: torch.Tensor, shift2: torch.Tensor | None, stream=None, unit: float = 1.0) -> None:
+                   kp: int, cnorm: torch.Tensor, shift2: torch.Tensor | None, stream=None, unit: float = 1.0,
+                   snap: bool = False) -> None:
     """K11: cent <- Σx·unit/count (empty clusters keep their centre), cb <- bf16(cent), cnorm <- ||cb||²;
-    ``unit`` is the sum grid step (accumulate_sort ``qscale`` = 1/unit), 1 for plain sums."""
+    ``unit`` is the sum grid step (accumulate_sort ``qscale`` = 1/unit), 1 for plain sums. ``snap``: cb
+    then goes onto the MX grid (mx_snap; the fp8 engines)."""
     lib = _native.kernels()
     if msgs is not None:
         nbuf, bstride, mp = msgs.shape[0], msgs.stride(0), msgs.data_ptr()
@@ -993,6 +998,8 @@ def update_centers(msgs: torch.Tensor | None, k: int, d: int, cent: torch.Tensor
                                    cnorm.data_ptr(), shift2.data_ptr() if shift2 is not None else 0, float(unit),
                                    _native.stream_ptr(stream))
     _native.check(status, "kmeans_update")
+    if snap:
+        mx_snap(cb, k, dp, cnorm, stream=stream)
 
 
 # ----------------------------------------------------------------------------------------------
