@@ -1,0 +1,131 @@
+# One driver for every GPU-box job (run from the repo root on the box, e.g. through gpurun):
+#
+#   bash scripts/gpu.sh JOB OUT [args...]      results under gpurun_out/OUT/
+#
+# JOB:
+#   tests [files...]      pytest -m gpu (all of tests/ by default), one process, per-test timeout
+#   final                 whole GPU suite, smoke(), headline bench, config-2 f32 fit, config-5 pipeline (trace)
+#   bench [bench args]    python bench.py ARGS -> bench.json (+ stderr)
+#   pipeline [args]       config-5 pipeline bench with the CML_TRACE stage table
+#   profile [bench args]  rocprofv3 kernel trace of bench.py ARGS: per-kernel table of the timed fit
+#   shard [bench args]    the 8-GPU shard (12.5M rows) on a one-rank RCCL group: fit breakdown, merged
+#                         kernel / blocking-call / roctx timeline, kernel table, host syncs, sync audit
+#   strong                strong-scaling emulation: per-rank shards of the headline (100M / N rows)
+#   workflow              the reference workflow end to end on 4M uploaded rows (examples/)
+#   mb SCRIPT [args]      a microbenchmark script (scripts/mb_*.py ...) -> SCRIPT.log
+#
+# Every GPU step runs under its own `timeout -k 10`; steps are chained so a failure ends the job.
+set -o pipefail
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp PYTHONPATH=$PWD
+JOB=${1:?job}
+O=gpurun_out/${2:-$1}
+shift 2 || shift $#
+mkdir -p "$O"
+
+fit_line() {  # one summary line of a bench.py JSON result
+  tail -1 "$1" | python3 -c "
+import json, sys
+d = json.loads(sys.stdin.read()); e = d.get('extra', {}); b = e.get('breakdown') or {}
+print(d['metric'][:60], '| value', d['value'], '| ms/step', round(d['ms_per_step'], 3),
+      '| fit ms', round(1000 * e.get('fit_s', 0), 2), '| engine', e.get('engine_fit_ms'),
+      '| init', b.get('init_ms'), '| steady', e.get('steady_state_ms_per_step'),
+      '| overlap fit', (e.get('overlap') or {}).get('fit_ms'))"
+}
+
+case "$JOB" in
+tests)
+  T=${*:-tests}
+  timeout -k 10 1100 python -u -m pytest -x -v --timeout 120 --timeout-method thread -p no:cacheprovider -m gpu $T \
+    > "$O/tests.log" 2>&1 || { tail -40 "$O/tests.log"; exit 1; }
+  tail -3 "$O/tests.log"
+  ;;
+final)
+  timeout -k 10 1100 python -u -m pytest tests -m gpu -q --timeout 200 --timeout-method thread -p no:cacheprovider \
+    > "$O/pytest_gpu.log" 2>&1
+  rc=$?
+  tail -2 "$O/pytest_gpu.log"
+  grep -E "FAILED|Error" "$O/pytest_gpu.log" | head -20
+  [ $rc -eq 0 ] || exit $rc
+  timeout -k 10 300 python3 -c "import __graft_entry__ as g; g.smoke(); print('smoke ok')" > "$O/smoke.log" 2>&1 \
+    || { tail -5 "$O/smoke.log"; exit 1; }
+  tail -1 "$O/smoke.log"
+  timeout -k 10 500 python3 bench.py > "$O/bench.json" 2> "$O/bench.err" || { tail -5 "$O/bench.err"; exit 1; }
+  fit_line "$O/bench.json"
+  timeout -k 10 300 python3 bench.py --rows 10000000 --dim 128 --k 64 --dtype f32 --warmup 1 --steps 20 \
+    > "$O/cfg2_f32.json" 2> "$O/cfg2_f32.err" || { tail -5 "$O/cfg2_f32.err"; exit 1; }
+  fit_line "$O/cfg2_f32.json"
+  CML_TRACE=1 timeout -k 10 600 python3 bench.py --workload pipeline --steps 2 --warmup 1 > "$O/pipe.json" \
+    2> "$O/pipe.err" || { tail -20 "$O/pipe.err"; exit 1; }
+  cut -c1-240 "$O/pipe.json"
+  grep -A12 "^range" "$O/pipe.err"
+  ;;
+bench)
+  timeout -k 10 900 python3 bench.py "$@" > "$O/bench.json" 2> "$O/bench.err" || { tail -20 "$O/bench.err"; exit 1; }
+  cut -c1-400 "$O/bench.json"
+  ;;
+pipeline)
+  CML_TRACE=1 timeout -k 10 900 python3 bench.py --workload pipeline --steps 2 --warmup 1 "$@" > "$O/pipe.json" \
+    2> "$O/pipe.err" || { tail -20 "$O/pipe.err"; exit 1; }
+  cut -c1-400 "$O/pipe.json"
+  grep -A16 "^range" "$O/pipe.err"
+  ;;
+profile)
+  timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/pf -o pf -- python3 bench.py "$@" > "$O/run.log" 2>&1 \
+    || { tail -20 "$O/run.log"; exit 1; }
+  tail -1 "$O/run.log" | cut -c1-400
+  python3 scripts/rocpd_stats.py /tmp/pf/pf_results.db --top 50 > "$O/kernel_stats.txt"
+  head -30 "$O/kernel_stats.txt"
+  ;;
+shard)
+  export CML_COMM_SELF=1
+  timeout -k 10 300 python3 bench.py --rows 12500000 --warmup 3 --no-overlap --breakdown "$@" > "$O/shard.json" \
+    2> "$O/shard.err" || { tail -5 "$O/shard.err"; exit 1; }
+  fit_line "$O/shard.json"
+  timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --marker-trace -d /tmp/sh -o sh -- python3 bench.py \
+    --rows 12500000 --warmup 3 --no-overlap "$@" > "$O/sh.log" 2>&1 || { tail -5 "$O/sh.log"; exit 1; }
+  python3 scripts/rocpd_timeline.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 > "$O/timeline.txt"
+  python3 scripts/rocpd_stats.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --top 40 > "$O/stats.txt"
+  python3 scripts/rocpd_syncs.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --show 5 > "$O/syncs.txt"
+  timeout -k 10 300 python3 scripts/sync_audit.py --rows 2000000 > "$O/sync_audit.txt" 2>&1 \
+    || { tail -20 "$O/sync_audit.txt"; exit 1; }
+  head -3 "$O/syncs.txt"
+  tail -1 "$O/timeline.txt"
+  head -1 "$O/sync_audit.txt"
+  ;;
+strong)
+  for n in 50000000 25000000 12500000; do
+    timeout -k 10 240 python3 bench.py --rows $n --chunks 2 --steps 20 --warmup 3 --no-overlap > "$O/c2_$n.json" \
+      2> "$O/c2_$n.err" || { tail -5 "$O/c2_$n.err"; exit 1; }
+    CML_COMM_SELF=1 timeout -k 10 240 python3 bench.py --rows $n --steps 20 --warmup 3 --no-overlap \
+      > "$O/self_$n.json" 2> "$O/self_$n.err" || { tail -5 "$O/self_$n.err"; exit 1; }
+    fit_line "$O/c2_$n.json"
+    fit_line "$O/self_$n.json"
+  done
+  ;;
+workflow)
+  python3 -c "
+import sys; sys.path.insert(0, 'examples')
+import hospital_resource_prediction as h
+h.synth_uploads('/tmp/wfsrc/hospitals/incoming', n_files=4, rows=1000000)
+" || exit 1
+  rm -rf /tmp/wf && mkdir -p /tmp/wf && cp -r /tmp/wfsrc/hospitals /tmp/wf/
+  t0=$(date +%s.%N)
+  timeout -k 10 400 python3 examples/hospital_resource_prediction.py --master mi355x --out /tmp/wf --trace \
+    > "$O/workflow.log" 2>&1 || { tail -20 "$O/workflow.log"; exit 1; }
+  t1=$(date +%s.%N)
+  python3 -c "print('workflow wall s', round($t1 - $t0, 3))"
+  grep -A24 "^range" "$O/workflow.log"
+  ;;
+mb)
+  S=${1:?script}
+  shift
+  timeout -k 10 600 python3 -u "$S" "$@" > "$O/$(basename "$S" .py).log" 2>&1 \
+    || { tail -20 "$O/$(basename "$S" .py).log"; exit 1; }
+  grep -v amdgpu.ids "$O/$(basename "$S" .py).log" | tail -40
+  ;;
+*)
+  echo "unknown job $JOB" >&2
+  exit 2
+  ;;
+esac

@@ -3,7 +3,7 @@ widening pass (K.set_fp8_mx(False)), on config-5 shaped data (32 Gaussian blobs,
 one full assign pass, and device pruned Lloyd steps of a fresh engine each way. Labels of the two arithmetics
 may differ inside the rounding band only (tests/test_kmeans_mx_gpu.py).
 
-    python scripts/r5/mb_fp8_mx.py [--rows N] [--dim D] [--k K] [--steps S]
+    python scripts/mb_fp8_mx.py [--rows N] [--dim D] [--k K] [--steps S]
 """
 import argparse
 import time

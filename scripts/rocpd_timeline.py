@@ -1,44 +1,62 @@
-"""Summaries of a rocprofv3 rocpd database (run_results.db): per-kernel stats and a timeline.
+"""Merged timeline of one window of a rocprofv3 database (``--kernel-trace --runtime-trace
+[--marker-trace]``): kernels (start offset, gap before, duration), blocking HIP runtime calls and roctx
+ranges, in time order, between the i-th and (i+1)-th dispatch of a marker kernel.
 
-usage: python scripts/rocpd_timeline.py DB [--after NAME_SUBSTR] [--limit N] [--stats]
---after: start the timeline at the first kernel whose name contains NAME_SUBSTR (e.g. the first
-row-norm kernel of the timed fit); --stats: per-kernel totals of the (selected) range instead."""
+    python scripts/rocpd_timeline.py DB --marker row_pass_kernel --index 1 [--summary]
+"""
 import argparse
 import re
 import sqlite3
-from collections import defaultdict
+
+BLOCKING = ("hipMemcpyWithStream", "hipMemcpy", "hipStreamSynchronize", "hipDeviceSynchronize",
+            "hipEventSynchronize", "hipMemcpyDtoH", "hipMemset", "hipMemcpyAsync")
 
 
 def short(n):
     n = re.sub(r"\(anonymous namespace\)::", "", n)
     n = re.sub(r"^void ", "", n)
-    return n.split("(")[0][:80]
+    return n.split("(")[0][:70]
 
 
-ap = argparse.ArgumentParser()
-ap.add_argument("db")
-ap.add_argument("--after", default=None)
-ap.add_argument("--skip", type=int, default=0, help="skip this many matches of --after")
-ap.add_argument("--limit", type=int, default=200)
-ap.add_argument("--stats", action="store_true")
-a = ap.parse_args()
-rows = sqlite3.connect(a.db).execute("select name, start, end from kernels order by start").fetchall()
-i0 = 0
-if a.after:
-    hits = [i for i, r in enumerate(rows) if a.after in r[0]]
-    i0 = hits[min(a.skip, len(hits) - 1)] if hits else 0
-sel = rows[i0:i0 + a.limit] if not a.stats else rows[i0:]
-if a.stats:
-    agg = defaultdict(lambda: [0, 0])
-    for name, s, e in sel:
-        agg[short(name)][0] += 1
-        agg[short(name)][1] += e - s
-    tot = sum(v[1] for v in agg.values())
-    for k, (c, t) in sorted(agg.items(), key=lambda kv: -kv[1][1])[:a.limit]:
-        print(f"{k:80s} {c:6d} {t / 1e6:10.3f} ms {100 * t / tot:6.2f}%")
-else:
-    t0 = sel[0][1]
-    prev = t0
-    for name, s, e in sel:
-        print(f"{(s - t0) / 1e6:10.3f} gap {(s - prev) / 1e6:7.3f} dur {(e - s) / 1e6:8.3f}  {short(name)}")
-        prev = e
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("db")
+    ap.add_argument("--marker", default="row_pass_kernel")
+    ap.add_argument("--index", type=int, default=1)
+    ap.add_argument("--end-marker", default=None, help="window ends at the next dispatch of this kernel")
+    a = ap.parse_args()
+    c = sqlite3.connect(a.db)
+    ks = list(c.execute("select name, start, end from kernels order by start"))
+    marks = [s for n, s, e in ks if a.marker in n]
+    lo = marks[a.index]
+    hi = marks[a.index + 1] if a.index + 1 < len(marks) else ks[-1][2] + 1
+    sel = [(n, s, e) for n, s, e in ks if lo <= s < hi]
+    ev = [(s, "K", short(n), e - s) for n, s, e in sel]
+    try:
+        regs = list(c.execute("select name, start, end from regions where start >= ? and start < ?",
+                              (lo - 5_000_000, sel[-1][2])))
+    except sqlite3.Error:
+        regs = []
+    for n, s, e in regs:
+        if n in BLOCKING:
+            ev.append((s, "B", n, e - s))
+        elif n.startswith(("kmeans", "kinit", "fit", "lloyd")):
+            ev.append((s, "R", n, e - s))
+    ev.sort()
+    t0 = lo
+    kend = lo
+    busy = 0
+    for t, kind, name, dur in ev:
+        if kind == "K":
+            gap = max(0, t - kend)
+            print(f"{(t - t0) / 1e6:9.3f} K gap {gap / 1e3:7.1f}us dur {dur / 1e3:8.1f}us  {name}")
+            kend = max(kend, t + dur)
+            busy += dur
+        else:
+            print(f"{(t - t0) / 1e6:9.3f} {kind} {'':17s} dur {dur / 1e3:8.1f}us  [{name}]")
+    span = sel[-1][2] - lo
+    print(f"window {span / 1e6:.3f} ms, {len(sel)} kernels, kernel time {busy / 1e6:.3f} ms")
+
+
+if __name__ == "__main__":
+    main()

@@ -1,7 +1,7 @@
 """Where the KMeans fit synchronises with the device: torch's sync debug mode reports every synchronising
 torch call (blocking copies, .item(), nonzero, ...) of one public-API fit, with the Python stack that made it.
 
-    python scripts/r5/sync_audit.py [--rows N] [--dim D] [--k K]
+    python scripts/sync_audit.py [--rows N] [--dim D] [--k K]
 """
 import argparse
 import collections
