@@ -522,9 +522,15 @@ def bench_kmeans_ooc(args):
         "metric": f"Out-of-core KMeans fit samples/sec, {n / 1e6:g}M x {d} fp8 in pinned host memory, k={k}",
         "value": n * args.steps / elapsed, "unit": "samples/s", "n_gpus": 1 if gpu else 0, "steps": args.steps,
         "warmup": 1, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "fp8 rows (e4m3fn), bf16 MFMA", "data": "synthetic Gaussian blobs",
+        "vs_baseline": None, "dtype": _fp8_dtype("fp8 rows (e4m3fn)"), "data": "synthetic Gaussian blobs",
         "config": {"model": f"KMeans k={k}", "global_batch": n, "seq_len": None, "parallelism": "dp1 (streamed)",
                    "rows": n, "dim": d}, "extra": extra}), flush=True)
+
+
+def _fp8_dtype(what: str) -> str:
+    """dtype field of the fp8 workloads: the MFMA the KMeans passes ran (kmeans_ops.set_fp8_mx)."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+    return f"{what}, " + ("MX-scaled fp8 MFMA in the KMeans assign" if K.fp8_mx_on() else "bf16 MFMA")
 
 
 def bench_pipeline(args):
@@ -599,7 +605,7 @@ def bench_pipeline(args):
                       f"{total / 1e9:g}B x {d}",
             "value": total * args.steps / elapsed, "unit": "rows/s", "n_gpus": W if gpu else 0, "steps": args.steps,
             "warmup": args.warmup, "ms_per_step": 1000.0 * elapsed / args.steps, "higher_is_better": True,
-            "scaling": "weak", "vs_baseline": None, "dtype": "fp8 features (e4m3fn), bf16 MFMA" if gpu else "fp64",
+            "scaling": "weak", "vs_baseline": None, "dtype": _fp8_dtype("fp8 features (e4m3fn)") if gpu else "fp64",
             "data": "synthetic (Gaussian blobs, logistic labels), generated on device",
             "config": {"model": "Pipeline[VectorAssembler, StandardScaler, KMeans k=128 x10, LogReg x10]",
                        "global_batch": total, "seq_len": None, "parallelism": f"dp{W}", "rows_per_gpu": n, "dim": d},

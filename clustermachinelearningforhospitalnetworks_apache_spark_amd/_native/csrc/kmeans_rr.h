@@ -425,7 +425,7 @@ __device__ __forceinline__ void compute_m32(const u16* __restrict__ C, long long
 // the products are those of the bf16 pass; per 128 k two MX MFMAs (hi, lo) at twice the bf16 rate — the
 // MFMA time of the bf16 pass with none of its v_cvt_scalef32_pk_bf16_fp8 widening of every X fragment in
 // every compute wave, which bound that pass (19.6 ms at 125M x 512, k = 128).
-// Layout (measured, scripts/r5/mx_probe_diag*.py, pinned by tests/test_kmeans_mx_gpu.py): bytes 0-15 of lane
+// Layout (measured, scripts/mx_probe_layout.py, pinned by tests/test_kmeans_mx_gpu.py): bytes 0-15 of lane
 // (r, g) are k 16g + j, bytes 16-31 are k 64 + 16g + j, and lane group q supplies the scale of k [32q, 32q+32).
 // Lane (r, g) of block b therefore reads the 16-B units 2b and 2b + 1 of the K9r fp8 order (chunks 8b + g
 // and 8b + 4 + g of row r); its split partner for both halves' scale blocks is lane (r, g ^ 1).

@@ -1089,8 +1089,13 @@ class LloydEngine:
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
+        # lean steps (CML_KMEANS_LEAN_STEP, eager steps only: a captured graph must hold the full path for forced
+        # replays): change lists sized for every row of a workgroup, so an unforced step enqueues only the delta
+        # launches — the full re-accumulation's six gated launches ran (as no-ops) in every steady step before
+        lean = os.environ.get("CML_KMEANS_LEAN_STEP", "1") != "0" and not self.use_graph
+        per_wg_all = -(-(-(-max(n, 1) // tr)) // ap.grid) * tr
         self.delta = K.DeltaState(max(n, 1), k, d, self.dp, 1, self.msg_len, dev, ap.grid, fp8=K.is_fp8(self.x),
-                                  cap=max(st.cap_m, 1024), pcap=max(per_wg, 64))
+                                  cap=max(st.cap_m, 1024), pcap=max(per_wg_all if lean else per_wg, 64), lean=lean)
 
     def _step_prune_dev(self) -> None:
         """One exact Lloyd iteration with no host synchronisation (HIP-graph capturable):
@@ -1125,9 +1130,11 @@ class LloydEngine:
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
                         gate=st.pmode, want=0, cum=st.cum)
-        dl.gate(0)
-        K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
-                          self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
+        lean = dl.lean_step()
+        dl.gate(0, lean=lean)
+        if not lean:  # a forced step: the full re-accumulation may run (lean steps never pick it)
+            K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
+                              self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
 
     def _pdev_post(self) -> None:
@@ -1277,7 +1284,9 @@ class LloydEngine:
         k, d, n, kd = self.k, self.d, self.n, self.k * self.d
         cb = self._pst.cb_cost if self._pdev else self._cb_cost
         if n:
-            q = group_reduce(self.labels[:n], self._norms64()[:n], k, "sum").to(torch.float64).contiguous()
+            # (engine labels are always in [0, k): no range check, no host read)
+            q = group_reduce(self.labels[:n], self._norms64()[:n], k, "sum",
+                             ids_in_range=True).to(torch.float64).contiguous()
         else:
             q = torch.zeros(k, dtype=torch.float64, device=self.device)
         self.comm.allreduce_(q)

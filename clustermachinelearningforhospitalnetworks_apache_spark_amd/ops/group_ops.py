@@ -50,10 +50,12 @@ def _torch_reduce(gid: torch.Tensor, vals: Optional[torch.Tensor], G: int, op: s
 
 
 def group_reduce(gid: torch.Tensor, vals: Optional[torch.Tensor], G: int, op: str,
-                 mask: Optional[torch.Tensor] = None, floating: Optional[bool] = None) -> torch.Tensor:
+                 mask: Optional[torch.Tensor] = None, floating: Optional[bool] = None,
+                 ids_in_range: bool = False) -> torch.Tensor:
     """[G] per-group ``op`` ("sum" / "min" / "max") of ``vals`` (None = the row index) over rows whose
     ``mask`` is set. Accumulates in f64 for floating values (or ``floating=True``), else in i64.
-    Empty groups hold the identity (0, +inf / -inf, int64 max / min)."""
+    Empty groups hold the identity (0, +inf / -inf, int64 max / min). ``ids_in_range``: the caller
+    guarantees 0 <= gid < G (e.g. KMeans labels), so the range check — a host read — is skipped."""
     n = int(gid.shape[0])
     if floating is None:
         floating = vals is not None and vals.is_floating_point()
@@ -61,9 +63,10 @@ def group_reduce(gid: torch.Tensor, vals: Optional[torch.Tensor], G: int, op: st
         return _torch_reduce(gid, vals, G, op, mask, floating, n)
     gid32 = gid if gid.dtype == torch.int32 else gid.to(torch.int32)
     gid32 = gid32.contiguous()
-    lo, hi = torch.aminmax(gid32)
-    if int(lo) < 0 or int(hi) >= G:  # the kernel indexes LDS by gid: never launch out of range
-        raise ValueError(f"group_reduce: group ids outside [0, {G})")
+    if not ids_in_range:
+        lo, hi = torch.aminmax(gid32)
+        if int(lo) < 0 or int(hi) >= G:  # the kernel indexes LDS by gid: never launch out of range
+            raise ValueError(f"group_reduce: group ids outside [0, {G})")
     if vals is None:
         vt, vp = 5, None
     else:

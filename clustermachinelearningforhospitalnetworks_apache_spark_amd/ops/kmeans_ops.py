@@ -567,13 +567,19 @@ class DeltaState:
 
     def __init__(self, n: int, k: int, d: int, dp: int, chunks: int, msg_len: int, device, nblk: int,
                  fp8: bool = False, cap_fraction: float | None = None, cap: int | None = None,
-                 pcap: int | None = None):
+                 pcap: int | None = None, lean: bool = False):
         self.k, self.d, self.nblk = k, d, int(nblk)
         if cap_fraction is None:  # steps with more label changes than this re-accumulate in full
             cap_fraction = float(os.environ.get("CML_KMEANS_DELTA_CAP", 0.25))
         self.cap = max(1024, int(n * cap_fraction)) if cap is None else int(cap)
         # change lists are per assign workgroup: nblk lists of pcap entries (slack for uneven churn)
         self.pcap = max(64, -(-2 * self.cap // self.nblk)) if pcap is None else int(pcap)
+        # lean: the lists hold every row of their workgroup (pcap >= its rows), so the delta path can take any
+        # number of changes and a step whose sums are valid never needs the full re-accumulation — the caller
+        # then enqueues only the delta launches (gate(lean=True)); the full path runs on forced steps only
+        self.lean = bool(lean)
+        self.host_forced = True  # the device force flag is set (creation / invalidate): next gate is not lean
+        self.entries = self.nblk * self.pcap if self.lean else self.cap
         self.rows = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
         self.old = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
         self.wg_count = torch.zeros(self.nblk, dtype=torch.int32, device=device)
@@ -583,28 +589,40 @@ class DeltaState:
         self.dh = torch.zeros(2 * k, dtype=torch.int32, device=device)
         self.dseg = torch.zeros(2 * k + 2, dtype=torch.int32, device=device)
         self.cursor = torch.zeros(2 * k, dtype=torch.int32, device=device)
-        self.dperm = torch.zeros(2 * self.cap, dtype=torch.int32, device=device)
+        self.dperm = torch.zeros(2 * self.entries, dtype=torch.int32, device=device)
         self.dsum = torch.zeros(2 * k * d, dtype=torch.float64, device=device)
         self.acc = torch.zeros((chunks, msg_len), dtype=torch.float64, device=device)
         ncu = num_cus(device.index or 0)
         self.plan = AccumPlan(mode="sort", cpl=(dp // 64 if fp8 else (2 if dp <= 128 else (4 if dp <= 256 else 8))),
-                              seg_grid=max(1, min((2 * self.cap + 255) // 256, ncu * 4)), dw=dp)
+                              seg_grid=max(1, min((2 * self.entries + 255) // 256, ncu * 4)), dw=dp)
         self.slots = seg_slots(self.plan, d, device)
 
     def invalidate(self) -> None:
         """Next step re-accumulates in full (labels or acc no longer describe each other)."""
         self.force.fill_(1)
+        self.host_forced = True
 
-    def gate(self, chunk: int, stream=None) -> None:
+    def lean_step(self) -> bool:
+        """Whether the next step may skip the full-accumulate launches (lean lists, no force pending)."""
+        return self.lean and not self.host_forced
+
+    def gate(self, chunk: int, stream=None, lean: bool = False) -> None:
+        """Full re-accumulation or delta for this step, decided on the device. ``lean``: the step enqueues no
+        full path (lean_step()), so only a forced step may pick it — the change count never does."""
+        if lean and not self.lean_step():
+            raise RuntimeError("lean delta gate on a forced step or without lean change lists")
         _native.check(_native.kernels().cml_kmeans_delta_gate(
-            self.wg_count.data_ptr(), self.nblk, self.cap, self.overflow.data_ptr(), self.force[chunk:].data_ptr(),
-            self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(), _native.stream_ptr(stream)), "kmeans_delta_gate")
+            self.wg_count.data_ptr(), self.nblk, (1 << 30) if lean else self.cap, self.overflow.data_ptr(),
+            self.force[chunk:].data_ptr(), self.mode[chunk].data_ptr(), self.k, self.dh.data_ptr(),
+            _native.stream_ptr(stream)), "kmeans_delta_gate")
+        if chunk == self.force.shape[0] - 1:
+            self.host_forced = False  # the gate consumed the device flag (every chunk's gate ran)
 
     def accumulate(self, x: torch.Tensor, dp: int, labels: torch.Tensor, chunk: int, cost_part: torch.Tensor,
                    ncost: int, msg: torch.Tensor, stream=None, qscale: float = 0.0) -> None:
         _native.check(_native.kernels().cml_kmeans_delta_accum(
             x.data_ptr(), x.stride(0), dp, self.d, labels.data_ptr(), self.rows.data_ptr(), self.old.data_ptr(),
-            self.wg_count.data_ptr(), self.nblk, self.pcap, self.cap, self.mode[chunk].data_ptr(), self.k,
+            self.wg_count.data_ptr(), self.nblk, self.pcap, self.entries, self.mode[chunk].data_ptr(), self.k,
             self.dh.data_ptr(), self.dseg.data_ptr(),
             self.cursor.data_ptr(), self.dperm.data_ptr(), self.plan.cpl, self.plan.seg_grid, self.dsum.data_ptr(),
             self.slots[0].data_ptr(), self.slots[1].data_ptr(), self.acc[chunk].data_ptr(), cost_part.data_ptr(),
