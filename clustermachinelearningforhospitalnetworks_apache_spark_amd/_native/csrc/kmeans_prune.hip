@@ -53,7 +53,8 @@ __device__ __forceinline__ bool bound_step(int a, float& u, float& w, const floa
 
 // The pruned step's gate (kmeans_prune_gate_kernel's body): one thread.
 __device__ __forceinline__ void prune_gate_body(int* __restrict__ count, long long cap, const int* __restrict__ flags,
-                                                int* __restrict__ mode, int* __restrict__ backoff, int nback) {
+                                                int* __restrict__ mode, int* __restrict__ backoff, int nback,
+                                                int* __restrict__ mode_host = nullptr) {
   if (flags[1] != 0) {
     mode[0] = 0;
     mode[1] = 0;
@@ -66,6 +67,9 @@ __device__ __forceinline__ void prune_gate_body(int* __restrict__ count, long lo
   const int full = (flags[0] != 0 || (long long)c > cap) ? 1 : 0;
   mode[0] = full;
   mode[1] = full ? 0 : c;
+  // mode_host: pinned host memory the host reads without a synchronisation (a lagged hint of the regime:
+  // models/kmeans.py _pdev_pre enqueues the full-accumulate launches while full passes are being picked)
+  if (mode_host != nullptr) mode_host[0] = full;
 }
 
 // Gate folded into the bounds pass (one launch less per step): with gmode != null the workgroup that
@@ -77,6 +81,7 @@ struct GateArgs {
   int* backoff;
   int nback;
   int* done;
+  int* mode_host = nullptr;
 };
 
 __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
@@ -98,7 +103,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   // converged and the step is a frozen no-op (kmeans_prune_gate_kernel)
   if (skip != nullptr && (skip[0] != 0 || skip[1] != 0)) {
     if (gate.mode != nullptr && blockIdx.x == 0 && threadIdx.x == 0)
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.mode_host);
     return;
   }
   extern __shared__ __align__(16) unsigned char smem[];
@@ -216,7 +221,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
     // no fence: the gate reads only the count, which every block changed by an atomic whose result it
     // waited for (base above) before this completion atomic — device-scope atomics in issue order
     if (threadIdx.x == 0 && atomicAdd(gate.done, 1) == (int)gridDim.x - 1) {
-      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback);
+      prune_gate_body(count, gate.cap, skip, gate.mode, gate.backoff, gate.nback, gate.mode_host);
       __hip_atomic_store(gate.done, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
   }
@@ -732,13 +737,13 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, void* stream);
+                                          int nback, int* done, int* mode_host, void* stream);
 CML_API int cml_kmeans_prune_bounds(const int* lab, float* ub, float* lb, const float* drift, const float* dmax,
                                     const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                     const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                     long long cap, const float* cum, void* stream) {
   return cml_kmeans_prune_bounds_gated(lab, ub, lb, drift, dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn,
-                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, stream);
+                                       skip, cap, cum, nullptr, 0, nullptr, 0, nullptr, nullptr, stream);
 }
 
 // The bounds pass with the step gate folded in (mode / gate_cap / backoff / nback as kmeans_prune_gate; done:
@@ -747,7 +752,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                                           const float* thr, const float* c2, int k, long long n, int* cand, int* count,
                                           const float* xn, int* cand_lab, float* cand_xn, const int* skip,
                                           long long cap, const float* cum, int* mode, long long gate_cap, int* backoff,
-                                          int nback, int* done, void* stream) {
+                                          int nback, int* done, int* mode_host, void* stream) {
   if (mode != nullptr && (skip == nullptr || done == nullptr)) return (int)hipErrorInvalidValue;
   if ((cand_lab == nullptr) != (cand_xn == nullptr) || (cand_lab != nullptr && xn == nullptr))
     return (int)hipErrorInvalidValue;
@@ -763,7 +768,7 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
   }
   const long long per = (long long)kThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
-  const GateArgs g{mode, gate_cap, backoff, nback, done};
+  const GateArgs g{mode, gate_cap, backoff, nback, done, mode_host};
   hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
                      (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
                      dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum, g);

@@ -1086,6 +1086,10 @@ class LloydEngine:
         # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
         st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
         st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
+        # the gate's full-pass flag, stored by the device into pinned host memory and read by the host with no
+        # synchronisation (a few steps stale): steps enqueue the full-accumulate launches while the device keeps
+        # picking full passes (data the bounds do not prune: many label changes), lean steps otherwise
+        st.pm_host = torch.zeros(1, dtype=torch.int32, pin_memory=True) if self.gpu else None
         self._pst = st
         if self._norms_ready:  # norms cached on the feature tensor by an earlier engine
             self._set_mx()
@@ -1118,7 +1122,7 @@ class LloydEngine:
         if st.fused:  # bounds pass + gate in one launch
             K.prune_bounds_gated(lab[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                                  self.xnorm, st.cand_lab, st.cand_xn, st.flags, st.cum, st.pmode, st.cap_m,
-                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1])
+                                 st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1], mode_host=st.pm_host)
         else:
             K.prune_bounds(lab, st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count,
                            xn=self.xnorm, cand_lab=st.cand_lab, cand_xn=st.cand_xn, skip=st.flags, zero_count=False,
@@ -1130,7 +1134,7 @@ class LloydEngine:
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
                         gate=st.pmode, want=0, cum=st.cum)
-        lean = dl.lean_step()
+        lean = dl.lean_step() and not (st.fused and int(st.pm_host[0]) != 0)
         dl.gate(0, lean=lean)
         if not lean:  # a forced step: the full re-accumulation may run (lean steps never pick it)
             K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,

@@ -115,7 +115,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_pair_table": (c_int, [c_vp, c_int, c_vp, c_int, c_int, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_prune_bounds_gated": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp, c_vp,
                                               c_vp, c_vp, c_vp, c_vp, c_ll, c_vp, c_vp, c_ll, c_vp, c_int, c_vp,
-                                              c_vp]),
+                                              c_vp, c_vp]),
     "cml_kmeans_update_pdev": (c_int, [c_vp, c_int, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_int, c_int, c_vp, c_vp,
                                        c_dbl, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_centre_half_stats": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, ctypes.c_float, c_vp,
@@ -707,16 +707,18 @@ def label_hist(labels: torch.Tensor, n: int, plan: "AssignPlan", hist: torch.Ten
 
 
 def prune_bounds_gated(labels, ub, lb, drift, dmax, thr, c2, k: int, cand, count, xn, cand_lab, cand_xn, flags,
-                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None) -> None:
+                       cum, mode, gate_cap: int, backoff, nback: int, done, stream=None, mode_host=None) -> None:
     """K9p with the step gate folded in (kmeans_prune.hip): the bounds pass (skipped when flags[0] / flags[1]
     are set) and, in the workgroup that finishes last, kmeans_prune_gate's decision into ``mode``; ``done``
-    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics."""
+    (int32 [1], zero) is the completion counter. Device only; count is zeroed by the centre statistics.
+    ``mode_host`` (pinned int32 [1], optional): the gate also stores its full-pass flag there, for the host to
+    read without synchronising (a lagged hint)."""
     n = int(labels.shape[0])
     _native.check(_native.kernels().cml_kmeans_prune_bounds_gated(
         labels.data_ptr(), ub.data_ptr(), lb.data_ptr(), drift.data_ptr(), dmax.data_ptr(), thr.data_ptr(),
         c2.data_ptr(), int(k), n, cand.data_ptr(), count.data_ptr(), _ptr(xn), _ptr(cand_lab), _ptr(cand_xn),
         flags.data_ptr(), int(cand.shape[0]), _ptr(cum), mode.data_ptr(), int(gate_cap), _ptr(backoff), int(nback),
-        done.data_ptr(), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
+        done.data_ptr(), _ptr(mode_host), _native.stream_ptr(stream)), "kmeans_prune_bounds_gated")
 
 
 def update_pdev(msgs: torch.Tensor, k: int, d: int, cent: torch.Tensor, cb: torch.Tensor, dp: int, kp: int,
