@@ -2,11 +2,14 @@
 (CML_KMEANS_OVERLAP_ROWS=1): chunk 0's all-reduce is enqueued before chunk 1's accumulate. Under rocprofv3
 (kernel + memory-copy + marker traces) the per-process databases show the order on the device.
 
-    rocprofv3 --kernel-trace --memory-copy-trace --marker-trace -d DIR -o %pid% -- python scripts/overlap_timeline.py run
-    python scripts/overlap_timeline.py show DIR/*.db
+    python scripts/overlap_timeline.py run                       (both ranks from one process)
+    rocprofv3 --kernel-trace --memory-copy-trace --marker-trace -d DIR0 -o r0 -- \
+        python scripts/overlap_timeline.py rank 0 2 PORT &        (one profiled process per rank)
+    python scripts/overlap_timeline.py show DIR0/*.db
 
-``show`` prints, for every process database, the kernels and copies inside the ``kmeans.seeded`` range in time
-order (the gloo all-reduce of a CUDA tensor appears as its device-to-host copy).
+``show`` prints, for every process database, the kernels and copies between the two probe-kernel dispatches that
+bracket the traced seeded step, in time order (the gloo all-reduce of a CUDA tensor appears as its
+device-to-host copy).
 """
 import os
 import socket
@@ -31,8 +34,11 @@ def _rank(rank, world, port):
     import torch.distributed as dist
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import trace
     torch.cuda.set_device(0)
+    pa = torch.zeros((16, 128), dtype=torch.uint8, device="cuda")
+    ps = torch.full((64,), 127, dtype=torch.int32, device="cuda")
     dist.init_process_group("gloo", rank=rank, world_size=world)
     comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
     g = torch.Generator(device="cuda")
@@ -46,8 +52,12 @@ def _rank(rank, world, port):
         init = eng.init_kmeans_parallel(seed=5, as_device=True)
         eng.set_centers(init)
         torch.cuda.synchronize()
+        if it:  # the traced step, bracketed by two dispatches of a one-wave probe kernel (window markers)
+            K.mx_probe(pa, pa, ps, ps)
         with trace("kmeans.seeded" if it else "warmup.seeded"):
             eng.step()
+            if it:
+                K.mx_probe(pa, pa, ps, ps)
             torch.cuda.synchronize()
         eng.fit(3, 0.0)
         torch.cuda.synchronize()
@@ -70,23 +80,23 @@ def run():
 def show(paths):
     for path in paths:
         c = sqlite3.connect(path)
-        try:
-            rng = list(c.execute("select start, end from regions where name = 'kmeans.seeded'"))
-        except sqlite3.Error:
-            rng = []
-        if not rng:
+        ks = list(c.execute("select name, start, end from kernels order by start"))
+        marks = [(s, e) for n, s, e in ks if "mx_probe_kernel" in n]
+        if len(marks) < 2:
+            print(f"{path}: no probe-kernel window ({len(marks)} markers)")
             continue
-        lo, hi = rng[0]
-        ev = [(s, e, "K", n.split("(")[0][:60]) for n, s, e in
-              c.execute("select name, start, end from kernels where start >= ? and start < ?", (lo, hi))]
+        lo, hi = marks[0][1], marks[1][0]
+        ev = [(s, e, "K", n.split("(")[0][:60]) for n, s, e in ks if lo <= s < hi]
         try:
-            for s, e, kind in c.execute("select start, end, name from memory_copies where start >= ? and start < ?",
-                                        (lo, hi)):
-                ev.append((s, e, "C", str(kind)))
+            cols = [r[1] for r in c.execute("pragma table_info(memory_copies)")]
+            for row in c.execute("select * from memory_copies where start >= ? and start < ?", (lo, hi)):
+                r = dict(zip(cols, row))
+                what = "/".join(str(r[k]) for k in ("name", "src_agent_type", "dst_agent_type", "size") if k in r)
+                ev.append((r["start"], r["end"], "C", what))
         except sqlite3.Error as exc:
-            print(f"(no memory copies table: {exc})")
+            print(f"(memory copies: {exc})")
         ev.sort()
-        print(f"=== {path}: kmeans.seeded {(hi - lo) / 1e6:.3f} ms, {len(ev)} events")
+        print(f"=== {path}: seeded step window {(hi - lo) / 1e6:.3f} ms, {len(ev)} events")
         for s, e, kind, name in ev:
             print(f"{(s - lo) / 1e6:9.3f} ms  {kind}  {(e - s) / 1e3:8.1f} us  {name}")
 
@@ -94,5 +104,7 @@ def show(paths):
 if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "show":
         show(sys.argv[2:])
+    elif len(sys.argv) > 1 and sys.argv[1] == "rank":
+        _rank(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
     else:
         run()
