@@ -10,6 +10,7 @@ raises — there is no silent eager fallback on a GPU box.
 """
 from __future__ import annotations
 
+import contextlib
 import ctypes
 import os
 import threading
@@ -60,8 +61,67 @@ def _declare(lib, sigs):
         fn.argtypes = args
 
 
+class _Recorder:
+    """Stands in for the kernel library while a launch sequence is recorded (see ``recording``): every
+    ``cml_*`` call is converted to ctypes once and kept instead of run, and returns status 0."""
+
+    def __init__(self, lib):
+        self._lib = lib
+        self.calls = []
+
+    def __getattr__(self, name):
+        fn = getattr(self._lib, name)
+        types = fn.argtypes or []
+
+        def rec(*args):
+            conv = tuple(a if isinstance(a, t) else t(a) for a, t in zip(args, types))
+            self.calls.append((fn, conv, name))
+            return 0
+        return rec
+
+
+class Recorded:
+    """A recorded launch sequence: replaying it calls the same C entry points with the same (pre-converted)
+    arguments — no Python wrapper, no tensor attribute reads, no argument conversion. For hot loops whose
+    buffers are fixed (the device pruned Lloyd step: ~10 launches at ~20-30 us of host time each eagerly)."""
+
+    __slots__ = ("calls",)
+
+    def __init__(self, calls):
+        self.calls = tuple(calls)
+
+    def __call__(self) -> None:
+        for fn, conv, name in self.calls:
+            st = fn(*conv)
+            if st != 0:
+                raise NativeError(f"{name} failed with hipError {st}")
+
+
+_recording = threading.local()
+
+
+@contextlib.contextmanager
+def recording():
+    """``with recording() as rec: <wrapper calls>``; then ``Recorded(rec.calls)`` replays them. Only for
+    wrappers whose sole effect is their kernel launches (their return values are not produced)."""
+    rec = _Recorder(_real_kernels())
+    prev = getattr(_recording, "rec", None)
+    _recording.rec = rec
+    try:
+        yield rec
+    finally:
+        _recording.rec = prev
+
+
 def kernels():
     """The gfx950 kernel library (built in-tree on first use if missing)."""
+    rec = getattr(_recording, "rec", None)
+    if rec is not None:
+        return rec
+    return _real_kernels()
+
+
+def _real_kernels():
     global _kernels
     if _kernels is not None:
         return _kernels

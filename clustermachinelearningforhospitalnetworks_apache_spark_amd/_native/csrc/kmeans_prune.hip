@@ -25,7 +25,11 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block
+constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block (16384 for the bounds pass)
+// The bounds pass runs 1024-thread workgroups: each takes one slot of the candidate list with a device-scope
+// atomic on ONE counter (and one completion atomic for the folded gate), and those same-address atomics
+// serialise at the L2 — with 256-thread workgroups (4096 rows each) they bounded the pass at ~2-3 TB/s.
+constexpr int kBoundsThreads = 1024;
 
 // Offset form (cum != null): the stored values are us = ub - cu[a] and ls = lb + cl[a] against the
 // per-centre cumulative drifts cu[j] = Σ drift_j and cl[j] = Σ (largest drift of a centre other than
@@ -84,7 +88,7 @@ struct GateArgs {
   int* mode_host = nullptr;
 };
 
-__global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
+__global__ __launch_bounds__(kBoundsThreads) void kmeans_prune_bounds_kernel(const int* __restrict__ lab,
                                                                        float* __restrict__ ub,
                                                                        float* __restrict__ lb,
                                                                        const float* __restrict__ drift,
@@ -112,10 +116,10 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   float* st = sd + k;                          // [k] threshold
   float* scu = st + k;                         // [k] cumulative drifts (offset form)
   float* scl = scu + k;                        // [k]
-  __shared__ int wsum[kThreads / 64];
+  __shared__ int wsum[kBoundsThreads / 64];
   __shared__ int base;
   const bool lazy = cum != nullptr;
-  for (int i = threadIdx.x; i < k; i += kThreads) {
+  for (int i = threadIdx.x; i < k; i += kBoundsThreads) {
     sd[i] = drift[i];
     st[i] = thr[i];
     if (lazy) {
@@ -128,8 +132,8 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   // of any OTHER centre
   const float dm1 = dmax[0], dm2 = dmax[1];
   const int jm = (int)dmax[2];
-  const long long blk0 = (long long)blockIdx.x * kThreads * kIters * 4;
-  unsigned mask = 0;  // bit it*4+j: row blk0 + (it*kThreads + tid)*4 + j is a candidate
+  const long long blk0 = (long long)blockIdx.x * kBoundsThreads * kIters * 4;
+  unsigned mask = 0;  // bit it*4+j: row blk0 + (it*kBoundsThreads + tid)*4 + j is a candidate
   if (lazy) {
     // read-only: rows whose label holds keep their stored offsets. All kIters groups' loads are issued
     // before any test (48 B in flight per lane; one group at a time ran the pass at 3.3 TB/s)
@@ -137,7 +141,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
     float4 U[kIters], W[kIters];
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
-      const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+      const long long r0 = blk0 + ((long long)it * kBoundsThreads + threadIdx.x) * 4;
       if (r0 + 3 < n) {
         L[it] = *reinterpret_cast<const int4*>(lab + r0);
         U[it] = *reinterpret_cast<const float4*>(ub + r0);
@@ -146,7 +150,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
     }
 #pragma unroll
     for (int it = 0; it < kIters; ++it) {
-      const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+      const long long r0 = blk0 + ((long long)it * kBoundsThreads + threadIdx.x) * 4;
       if (r0 >= n) break;
       if (r0 + 3 < n) {
         const int ls[4] = {L[it].x, L[it].y, L[it].z, L[it].w};
@@ -163,7 +167,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   }
 #pragma unroll
   for (int it = 0; it < kIters && !lazy; ++it) {
-    const long long r0 = blk0 + ((long long)it * kThreads + threadIdx.x) * 4;
+    const long long r0 = blk0 + ((long long)it * kBoundsThreads + threadIdx.x) * 4;
     if (r0 >= n) break;
     if (r0 + 3 < n) {
       const int4 l = *reinterpret_cast<const int4*>(lab + r0);
@@ -199,7 +203,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   __syncthreads();
   if (threadIdx.x == 0) {
     int t = 0;
-    for (int w = 0; w < kThreads / 64; ++w) t += wsum[w];
+    for (int w = 0; w < kBoundsThreads / 64; ++w) t += wsum[w];
     base = t ? atomicAdd(count, t) : 0;
   }
   __syncthreads();
@@ -208,7 +212,7 @@ __global__ __launch_bounds__(kThreads) void kmeans_prune_bounds_kernel(const int
   while (mask) {
     const int b = __ffs(mask) - 1;
     mask &= mask - 1;
-    const int row = (int)(blk0 + ((long long)(b >> 2) * kThreads + threadIdx.x) * 4 + (b & 3));
+    const int row = (int)(blk0 + ((long long)(b >> 2) * kBoundsThreads + threadIdx.x) * 4 + (b & 3));
     if (off >= cap) break;  // list full: *count still gets every candidate (the step then runs in full)
     cand[off] = row;
     if (cand_lab != nullptr) {  // compacted label / norm of the candidate (trailer of the K9r mode-2 pass)
@@ -563,11 +567,15 @@ __global__ void kmeans_update_pdev_kernel(const double* __restrict__ bufs, int n
 // distance from c_j to its nearest other centre, as kmeans_centre_stats_kernel); the workgroup that
 // finishes last (device-scope counter) runs the single-workgroup part (kmeans_centre_stats2_kernel's work:
 // mc, c2, thr, dmax, the cumulative drifts, the count / force / backoff resets) and re-arms the counter.
-__device__ void centre_stats2_body(const double* __restrict__ cn, const double* __restrict__ half,
+// decay: half_j is not recomputed this step but lowered to a bound of the new centres' one — the distance
+// from c_j to any c_i shrinks by at most drift_j + drift_i, so half_j' >= half_j - (drift_j + max_{i!=j}
+// drift_i) / 2 (rounded down). A smaller half only makes the thresholds more conservative.
+__device__ void centre_stats2_body(const double* __restrict__ cn, double* __restrict__ half,
                                    const float* __restrict__ drift, int k, const float* __restrict__ mx, float tau,
                                    int have_drift, float* __restrict__ thr, float* __restrict__ dmax,
                                    float* __restrict__ mc, float* __restrict__ c2, int* __restrict__ count,
-                                   int* __restrict__ force, float* __restrict__ cum, int* __restrict__ backoff) {
+                                   int* __restrict__ force, float* __restrict__ cum, int* __restrict__ backoff,
+                                   int decay = 0) {
   __shared__ double smax[256];
   __shared__ float sdm[3];
   __shared__ float d1[256], d2[256];
@@ -622,8 +630,14 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, const double* 
   const double sl = (double)tau * ((double)*mx + smax[0]);
   for (int j = tid; act && j < k; j += 256) {
     float t;
+    double hj = half[j];
+    if (decay && have_drift) {
+      const double other = j == (int)sdm[2] ? (double)sdm[1] : (double)sdm[0];
+      hj = fmax(0.0, hj - 0.5 * ((double)drift[j] + other)) * (1.0 - 1e-12);
+      half[j] = hj;
+    }
     if (k == 1) t = __builtin_huge_valf();
-    else if (half[j] > 0.0) t = (float)((half[j] - sl / (2.0 * half[j])) * (1.0 - 1e-6));
+    else if (hj > 0.0) t = (float)((hj - sl / (2.0 * hj)) * (1.0 - 1e-6));
     else t = -__builtin_huge_valf();
     thr[j] = t;
     if (have_drift && cum != nullptr) {
@@ -766,10 +780,10 @@ CML_API int cml_kmeans_prune_bounds_gated(const int* lab, float* ub, float* lb, 
                        backoff, nback);
     return cml_status();
   }
-  const long long per = (long long)kThreads * kIters * 4;
+  const long long per = (long long)kBoundsThreads * kIters * 4;
   const unsigned grid = (unsigned)((n + per - 1) / per);
   const GateArgs g{mode, gate_cap, backoff, nback, done, mode_host};
-  hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kThreads),
+  hipLaunchKernelGGL(kmeans_prune_bounds_kernel, dim3(grid), dim3(kBoundsThreads),
                      (size_t)(cum != nullptr ? 4 : 2) * k * sizeof(float), (hipStream_t)stream, lab, ub, lb, drift,
                      dmax, thr, c2, k, n, cand, count, xn, cand_lab, cand_xn, skip, cap, cum, g);
   return cml_status();
@@ -817,6 +831,26 @@ CML_API int cml_kmeans_centre_stats(const void* cb, const void* cb_old, long lon
                      (const u16*)cb, (const u16*)cb_old, ldc, k, d, cn, drift, half);
   hipLaunchKernelGGL(kmeans_centre_stats2_kernel, dim3(1), dim3(256), 0, st, cn, half, drift, k, mx, tau,
                      cb_old != nullptr ? 1 : 0, thr, dmax, mc, c2, count, force, cum, backoff);
+  return cml_status();
+}
+
+// The centre statistics of a pruned step that keeps last step's half distances, lowered by the drifts
+// (centre_stats2_body decay): one workgroup instead of the k-workgroup nearest-centre pass. drift / cn as
+// kmeans_update_pdev_kernel leaves them.
+__global__ __launch_bounds__(256) void kmeans_centre_decay_stats_kernel(
+    const double* __restrict__ cn, double* __restrict__ half, const float* __restrict__ drift, int k,
+    const float* __restrict__ mx, float tau, float* __restrict__ thr, float* __restrict__ dmax, float* __restrict__ mc,
+    float* __restrict__ c2, int* __restrict__ count, int* __restrict__ force, float* __restrict__ cum,
+    int* __restrict__ backoff) {
+  centre_stats2_body(cn, half, drift, k, mx, tau, 1, thr, dmax, mc, c2, count, force, cum, backoff, 1);
+}
+
+CML_API int cml_kmeans_centre_decay_stats(const double* cn, double* half, const float* drift, int k, const float* mx,
+                                          float tau, float* thr, float* dmax, float* mc, float* c2, int* count,
+                                          int* force, float* cum, int* backoff, void* stream) {
+  if (k <= 0) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_centre_decay_stats_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, cn, half, drift, k,
+                     mx, tau, thr, dmax, mc, c2, count, force, cum, backoff);
   return cml_status();
 }
 

@@ -40,6 +40,7 @@ from typing import List, Optional
 import numpy as np
 import torch
 
+from .. import _native
 from ..ops import kmeans_ops as K
 from ..ops.group_ops import group_reduce
 from ..parallel.comm import Communicator, local_comm
@@ -1086,6 +1087,9 @@ class LloydEngine:
         # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
         st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
         st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
+        st.half_every = int(os.environ.get("CML_KMEANS_HALF_EVERY", "4"))
+        # recorded launch sequences of the step variants (_pdev_pre / _pdev_post); None: always the wrappers
+        st.replay = {} if os.environ.get("CML_KMEANS_REPLAY", "1") != "0" else None
         # the gate's full-pass flag, stored by the device into pinned host memory and read by the host with no
         # synchronisation (a few steps stale): steps enqueue the full-accumulate launches while the device keeps
         # picking full passes (data the bounds do not prune: many label changes), lean steps otherwise
@@ -1117,6 +1121,23 @@ class LloydEngine:
     def _pdev_pre(self) -> None:
         """The device pruned step up to its all-reduce (bounds, gate, K9r passes, sums -> msg)."""
         st, dl = self._pst, self.delta
+        lean = dl.lean_step() and not (st.fused and int(st.pm_host[0]) != 0)
+        if self._replay_ok():
+            # the launch sequence of this variant, recorded once (fixed buffers and scalars): replayed without
+            # the Python wrappers — the shard's steps were bound by ~25 us of host time per launch
+            key = ("pre", lean)
+            seq = st.replay.get(key)
+            if seq is None:
+                with _native.recording() as rec:
+                    self._pdev_pre_launches(lean)
+                seq = st.replay[key] = _native.Recorded(rec.calls)
+            seq()
+            dl.host_forced = False  # what the recorded gate does on the host
+            return
+        self._pdev_pre_launches(lean)
+
+    def _pdev_pre_launches(self, lean: bool) -> None:
+        st, dl = self._pst, self.delta
         n, k, d, ap = self.n, self.k, self.d, self.aplan
         x, lab, msg = self.x, self.labels, self.msgs[0]
         if st.fused:  # bounds pass + gate in one launch
@@ -1134,25 +1155,52 @@ class LloydEngine:
         K.assign_rr_ext(2, x, st.cap_m, self.dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub,
                         st.lb, st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab,
                         gate=st.pmode, want=0, cum=st.cum)
-        lean = dl.lean_step() and not (st.fused and int(st.pm_host[0]) != 0)
         dl.gate(0, lean=lean)
         if not lean:  # a forced step: the full re-accumulation may run (lean steps never pick it)
             K.accumulate_sort(x, n, self.dp, d, lab, self.rank, self.hist, ap, k, self.cost_part, self.off, self.seg,
                               self.perm, self.cplan, dl.acc[0], self.slots, gate=dl.mode[0], qscale=self._qscale)
         dl.accumulate(x, self.dp, lab, 0, self.cost_part, ap.grid, msg, qscale=self._qscale)
 
+    def _replay_ok(self) -> bool:
+        """Recorded launch sequences for the device pruned step: eager fused steps (a captured graph already
+        replays its launches), the sum regime settled (the first step's _sum_grid); CML_KMEANS_REPLAY=0: off."""
+        st = self._pst
+        return (st.fused and not self.use_graph and self._grid_done and st.replay is not None
+                and not torch.cuda.is_current_stream_capturing())
+
     def _pdev_post(self) -> None:
         """The device pruned step after its all-reduce: K11, the centre statistics of the next bounds and,
         in a tol > 0 fit, the device convergence latch (flags[1])."""
+        st = self._pst
+        exact = self.use_graph or st.half_every <= 1 or self.iterations % st.half_every == 0
+        if self._replay_ok() and not self.spherical and self.dp <= 2048:
+            key = ("post", exact, self._conv_lim)
+            seq = st.replay.get(key)
+            if seq is None:
+                with _native.recording() as rec:
+                    self._pdev_post_launches(exact)
+                seq = st.replay[key] = _native.Recorded(rec.calls)
+            seq()
+        else:
+            self._pdev_post_launches(exact)
+        self._shift2 = self.shift2
+        self._cost_fn = self._device_cost
+
+    def _pdev_post_launches(self, exact: bool) -> None:
         st, k, d = self._pst, self.k, self.d
         if st.fused and not self.spherical and self.dp <= 2048:
             # K11 + cb_old / cb_cost copies + norms + drifts in one launch, then the centre statistics in one
             K.update_pdev(self.msgs, k, d, self.centers, self.cb, self.dp, self.kp, self.cnorm, self.shift2,
                           self._unit, st.cb_old, st.cb_cost, st.flags, st.cn, st.drift, snap=self._mx)
-            self._shift2 = self.shift2
-            K.centre_half_stats(self.cb, k, self.dp, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc,
-                                st.c2, st.count, st.force, st.cum, st.backoff if st.nback > 0 else None,
-                                st.ctr[1:2])
+            # the nearest-centre half distances are recomputed every st.half_every steps (and in captured graphs);
+            # between, they are lowered by the drifts (a valid, slightly looser bound: one small launch)
+            if exact:
+                K.centre_half_stats(self.cb, k, self.dp, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax,
+                                    st.mc, st.c2, st.count, st.force, st.cum, st.backoff if st.nback > 0 else None,
+                                    st.ctr[1:2])
+            else:
+                K.centre_decay_stats(k, st.cn, st.half, st.drift, st.mx, st.tau, st.thr, st.dmax, st.mc, st.c2,
+                                     st.count, st.force, st.cum, st.backoff if st.nback > 0 else None)
         else:
             # cb_old <- cb, and cb_cost <- cb unless converged (frozen steps keep the last live step's centres)
             K.cond_copy(st.cb_cost, self.cb, st.flags, dst_always=st.cb_old)
@@ -1161,7 +1209,6 @@ class LloydEngine:
                            st.mc, st.c2, st.count, st.force, cum=st.cum, backoff=st.backoff if st.nback > 0 else None)
         if self._conv_lim is not None:
             K.converge_latch(self.shift2, k, self._conv_lim, st.flags)
-        self._cost_fn = self._device_cost
 
     def _seed_from_init(self, sd) -> None:
         """Labels and bounds of every row from the k-means|| init (kmeans_seed_bounds): row x's nearest

@@ -135,6 +135,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_cert_moves": (c_int, [c_vp, c_int, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp,
                                       c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_mx_probe": (c_int, [c_vp, c_vp, c_vp, c_vp, c_vp, c_vp]),
+    "cml_kmeans_centre_decay_stats": (c_int, [c_vp, c_vp, c_vp, c_int, c_vp, ctypes.c_float, c_vp, c_vp, c_vp, c_vp,
+                                              c_vp, c_vp, c_vp, c_vp, c_vp]),
     "cml_kmeans_mx_snap": (c_int, [c_vp, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_vp]),
 })
 _native.register_host_sigs({
@@ -734,6 +736,18 @@ def update_pdev(msgs: torch.Tensor, k: int, d: int, cent: torch.Tensor, cb: torc
         flags.data_ptr(), cn64.data_ptr(), drift.data_ptr(), _native.stream_ptr(stream)), "kmeans_update_pdev")
     if snap:
         mx_snap(cb, k, dp, cnorm, cn64=cn64, cb_old=cb_old, drift=drift, stream=stream)
+
+
+def centre_decay_stats(k: int, cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor, mx: torch.Tensor,
+                       tau: float, thr, dmax, mc, c2, count, force, cum, backoff, stream=None) -> None:
+    """The pruned step's centre statistics without the nearest-centre pass (kmeans_centre_decay_stats_kernel):
+    half_j lowered by the step's drifts (half_j - (drift_j + max_{i!=j} drift_i) / 2, still a lower bound of
+    half the nearest-centre distance), then thr, dmax, mc, c2, the cumulative drifts and the resets of
+    centre_half_stats. One workgroup."""
+    _native.check(_native.kernels().cml_kmeans_centre_decay_stats(
+        cn.data_ptr(), half.data_ptr(), drift.data_ptr(), int(k), mx.data_ptr(), float(tau), thr.data_ptr(),
+        dmax.data_ptr(), mc.data_ptr(), c2.data_ptr(), count.data_ptr(), force.data_ptr(), _ptr(cum), _ptr(backoff),
+        _native.stream_ptr(stream)), "kmeans_centre_decay_stats")
 
 
 def centre_half_stats(cb: torch.Tensor, k: int, d: int, cn: torch.Tensor, half: torch.Tensor, drift: torch.Tensor,
