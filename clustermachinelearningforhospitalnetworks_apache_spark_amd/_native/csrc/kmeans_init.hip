@@ -413,7 +413,7 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
       C[(long long)i * d + t] = v;
       CT[(long long)t * k + i] = v;
     }
-    __syncthreads();
+    if (D == nullptr) __syncthreads();  // (crow feeds only the fold below; with D the two row reads overlap)
     if (D != nullptr && in_lds) {
       const double* dr = D + (long long)pk * m;
       for (int q = tid; q < m; q += kKppThreads) {
@@ -530,26 +530,42 @@ __global__ __launch_bounds__(kThreads) void local_update_kernel(const double* __
     if (blockIdx.x == 0 && threadIdx.x == 0) flags[2 - slot] = 0;
   }
   extern __shared__ __align__(16) unsigned char smem[];
-  int* lab = reinterpret_cast<int*>(smem);                          // [m]
+  int* mem = reinterpret_cast<int*>(smem);                          // [m] members of cluster j, ascending
   double* cvals = reinterpret_cast<double*>(smem + (((size_t)m * 4 + 15) & ~(size_t)15));  // [d]
   __shared__ double inv_sh, nrm_sh;
-  const int j = blockIdx.x, tid = threadIdx.x;
-  for (int q = tid; q < m; q += kThreads) lab[q] = labels[q];
-  __syncthreads();
-  double c = 0.0;
-  for (int q = 0; q < m; ++q)
-    if (lab[q] == j) c = __dadd_rn(c, w[q]);
+  __shared__ int wcnt[kThreads / 64], nmem_sh;
+  const int j = blockIdx.x, tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  // members in ascending point order (ballot compaction, 256 points per round): the folds below then
+  // visit only the cluster's points, in the order the all-points loop did (same bits, ~m/k iterations)
+  int nmem = 0;
+  for (int q0 = 0; q0 < m; q0 += kThreads) {
+    const int q = q0 + tid;
+    const bool in = q < m && labels[q] == j;
+    const unsigned long long b = __ballot(in);
+    if (lane == 0) wcnt[wv] = (int)__popcll(b);
+    __syncthreads();
+    int off = nmem;
+    for (int u = 0; u < wv; ++u) off += wcnt[u];
+    if (in) mem[off + (int)__popcll(b & ((1ull << lane) - 1ull))] = q;
+    for (int u = 0; u < kThreads / 64; ++u) nmem += wcnt[u];
+    __syncthreads();  // wcnt reused by the next round
+  }
   if (tid == 0) {
+    double c = 0.0;
+    for (int u = 0; u < nmem; ++u) c = __dadd_rn(c, w[mem[u]]);
     cnt[j] = c;
     inv_sh = c > 0.0 ? __ddiv_rn(1.0, c) : 0.0;
+    nmem_sh = c > 0.0 ? nmem : 0;
   }
   __syncthreads();
-  if (!(c > 0.0)) return;  // empty: local_empty_kernel reseeds it
+  if (nmem_sh == 0) return;  // empty: local_empty_kernel reseeds it
   const double inv = inv_sh;
   for (int t = tid; t < d; t += kThreads) {
     double s = 0.0;
-    for (int q = 0; q < m; ++q)
-      if (lab[q] == j) s = __fma_rn(w[q], P[(long long)q * d + t], s);
+    for (int u = 0; u < nmem; ++u) {
+      const int q = mem[u];
+      s = __fma_rn(w[q], P[(long long)q * d + t], s);
+    }
     cvals[t] = __dmul_rn(s, inv);
   }
   __syncthreads();
@@ -787,6 +803,53 @@ CML_API int cml_int_hist(const int* vals, long long n, int m, int* counts, void*
   const size_t lds = m <= 8192 ? (size_t)m * 4 : 0;
   hipLaunchKernelGGL(int_hist_kernel, dim3(grid_for(n, kThreads * 16LL)), dim3(kThreads), lds, (hipStream_t)stream,
                      vals, n, m, counts);
+  return cml_status();
+}
+
+// Training cost of an assignment from the sums the step already holds (models/kmeans.py _device_cost):
+// out = max(0, Σ_j q_j - 2 c_j·(S_j·unit) + n_j |c_j|²), S / n summed over the `rows` message rows (msg [rows,
+// ldm]: S at j*d + t, n at k*d + j), c the bf16 centres [k, ldc]. One workgroup, fixed reduction order (the
+// same bits every run); replaces a dozen eager torch reductions at the end of every fit.
+__global__ __launch_bounds__(256) void kmeans_cost_combine_kernel(const double* __restrict__ q,
+                                                                  const double* __restrict__ msg, int rows,
+                                                                  long long ldm, int k, int d, double unit,
+                                                                  const unsigned short* __restrict__ cb, int ldc,
+                                                                  double* __restrict__ out) {
+  __shared__ double part[4];
+  const int lane = threadIdx.x & 63, wv = threadIdx.x >> 6;
+  const long long kd = (long long)k * d;
+  double acc = 0.0;  // wave-uniform after the lane reductions
+  for (int j = wv; j < k; j += 4) {
+    double cs = 0.0, cc = 0.0;
+    for (int t = lane; t < d; t += 64) {
+      double s = 0.0;
+      for (int r = 0; r < rows; ++r) s += msg[(long long)r * ldm + (long long)j * d + t];
+      const double c = (double)__uint_as_float((unsigned)cb[(long long)j * ldc + t] << 16);
+      cs += c * (s * unit);
+      cc += c * c;
+    }
+#pragma unroll
+    for (int o = 32; o >= 1; o >>= 1) {
+      cs += __shfl_xor(cs, o, 64);
+      cc += __shfl_xor(cc, o, 64);
+    }
+    double n = 0.0;
+    for (int r = 0; r < rows; ++r) n += msg[(long long)r * ldm + kd + j];
+    acc += q[j] - 2.0 * cs + n * cc;
+  }
+  if (lane == 0) part[wv] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    const double v = (part[0] + part[1]) + (part[2] + part[3]);
+    out[0] = v > 0.0 ? v : 0.0;
+  }
+}
+
+CML_API int cml_kmeans_cost_combine(const double* q, const double* msg, int rows, long long ldm, int k, int d,
+                                    double unit, const void* cb, int ldc, double* out, void* stream) {
+  if (rows <= 0 || k <= 0 || d <= 0 || ldc < d || ldm < (long long)k * d + k) return (int)hipErrorInvalidValue;
+  hipLaunchKernelGGL(kmeans_cost_combine_kernel, dim3(1), dim3(256), 0, (hipStream_t)stream, q, msg, rows, ldm, k,
+                     d, unit, (const unsigned short*)cb, ldc, out);
   return cml_status();
 }
 

@@ -1053,39 +1053,31 @@ class LloydEngine:
         st.tau = self._tau
         per_wg = -(-(-(-st.cap_m // tr)) // ap.grid) * tr
         pad = round_up(st.cap_m, tr) + tr
-        st.cand = torch.zeros(pad, dtype=torch.int32, device=dev)
-        st.cand_lab = torch.zeros(pad, dtype=torch.int32, device=dev)
-        st.cand_xn = torch.zeros(pad, dtype=torch.float32, device=dev)
-        st.count = torch.zeros(1, dtype=torch.int32, device=dev)
-        st.pmode = torch.zeros(2, dtype=torch.int32, device=dev)  # [full pass?, re-assigned rows]
+        # the candidate lists and the small per-step state: views of one zeroed block (one fill instead of
+        # sixteen). pmode = [full pass?, re-assigned rows]; mx = max ||x||² over all ranks (_ensure_norms)
+        lazy = os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096
+        f32, f64, i32 = torch.float32, torch.float64, torch.int32
+        (st.cand, st.cand_lab, st.cand_xn, st.count, st.pmode, st.backoff, st.drift, st.thr, st.dmax, st.cn, st.half,
+         st.mc, st.c2, st.mx, cum, st.ctr) = K.zeros_block(dev, [
+             (pad, i32), (pad, i32), (pad, f32), (1, i32), (2, i32), (1, i32), (k, f32), (k, f32), (3, f32),
+             (k, f64), (k, f64), (1, f32), (1, f32), (1, f32), (2 * k if lazy else 0, f32), (2, i32)])
         # step flags [force, done]: force = bounds invalid (a full pass next); done = converged (tol > 0
         # fits, _fit_lagged): every later step is a frozen no-op until the host reads the flag
         st.flags = self._const([1, 0], torch.int32)
         st.force, st.done = st.flags[0:1], st.flags[1:2]
         # steps left that skip the bounds after one went over the cap (data the bounds do not prune);
         # CML_KMEANS_PRUNE_BACKOFF=0 retries the bounds every step
-        st.backoff = torch.zeros(1, dtype=torch.int32, device=dev)
         st.nback = int(os.environ.get("CML_KMEANS_PRUNE_BACKOFF", "2"))
         st.ub = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
         st.lb = torch.zeros(max(n, 1), dtype=torch.float32, device=dev)
-        st.drift = torch.zeros(k, dtype=torch.float32, device=dev)
-        st.thr = torch.zeros(k, dtype=torch.float32, device=dev)
-        st.dmax = torch.zeros(3, dtype=torch.float32, device=dev)
-        st.cn = torch.zeros(k, dtype=torch.float64, device=dev)
-        st.half = torch.zeros(k, dtype=torch.float64, device=dev)
-        st.mc = torch.zeros(1, dtype=torch.float32, device=dev)
-        st.c2 = torch.zeros(1, dtype=torch.float32, device=dev)
-        st.mx = torch.zeros(1, dtype=torch.float32, device=dev)  # max ||x||² over all ranks (_ensure_norms)
         st.cb_old = torch.zeros_like(self.cb)
         st.cb_cost = torch.zeros_like(self.cb)  # centres of the last live step's assignment (training cost)
         # offset-form bounds (kmeans_prune.hip bound_lazy): ub/lb hold ub - cu[label] / lb + cl[label]
         # against these cumulative drifts [cu | cl], so the bounds pass only reads the rows whose label
         # holds; CML_KMEANS_LAZY_BOUNDS=0 keeps the absolute bounds rewritten every step
-        st.cum = (torch.zeros(2 * k, dtype=torch.float32, device=dev)
-                  if os.environ.get("CML_KMEANS_LAZY_BOUNDS", "1") != "0" and k <= 4096 else None)
+        st.cum = cum if lazy else None
         # completion counters of the fused launches (gate in the bounds pass, stats in the half pass); each
         # launch leaves its counter at zero. CML_KMEANS_FUSED_TAIL=0: the separate launches (A/B)
-        st.ctr = torch.zeros(2, dtype=torch.int32, device=dev)
         st.fused = os.environ.get("CML_KMEANS_FUSED_TAIL", "1") != "0"
         st.half_every = int(os.environ.get("CML_KMEANS_HALF_EVERY", "4"))
         # recorded launch sequences of the step variants (_pdev_pre / _pdev_post); None: always the wrappers
@@ -1332,7 +1324,7 @@ class LloydEngine:
         f32 norms lost percents, and no pass over X. Collective: every rank reads
         it together. (With the sum grid active — _sum_grid — S holds the gridded values, and the cost
         is that of the values the centres were computed from.)"""
-        k, d, n, kd = self.k, self.d, self.n, self.k * self.d
+        k, d, n = self.k, self.d, self.n
         cb = self._pst.cb_cost if self._pdev else self._cb_cost
         if n:
             # (engine labels are always in [0, k): no range check, no host read)
@@ -1341,12 +1333,7 @@ class LloydEngine:
         else:
             q = torch.zeros(k, dtype=torch.float64, device=self.device)
         self.comm.allreduce_(q)
-        m = self.msgs
-        s_ = (m[0, :kd] if m.shape[0] == 1 else m[:, :kd].sum(0)).view(k, d) * self._unit
-        cnt = m[0, kd:kd + k] if m.shape[0] == 1 else m[:, kd:kd + k].sum(0)
-        c = cb[:k, :d].to(torch.float64)
-        cost = q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()
-        return cost.clamp(min=0.0)
+        return K.cost_combine(q, self.msgs, k, d, self._unit, cb)
 
     def _exact_cost(self) -> torch.Tensor:
         """Cost of the last step's assignment (Spark's per-iteration cost) on the device rows: one exact
@@ -1732,10 +1719,9 @@ class LloydEngine:
             return self.assign()[0]
         st, ap = self._pst, self.aplan
         lab, ub, lb = self.labels.clone(), st.ub.clone(), st.lb.clone()
-        cand, cand_lab, cand_xn = torch.zeros_like(st.cand), torch.zeros_like(st.cand_lab), torch.zeros_like(st.cand_xn)
-        count = torch.zeros(1, dtype=torch.int32, device=self.device)
-        flags = torch.zeros(2, dtype=torch.int32, device=self.device)
-        pmode = torch.zeros(2, dtype=torch.int32, device=self.device)
+        pad, i32 = st.cand.shape[0], torch.int32
+        cand, cand_lab, cand_xn, count, flags, pmode = K.zeros_block(self.device, [
+            (pad, i32), (pad, i32), (pad, torch.float32), (1, i32), (2, i32), (2, i32)])
         K.prune_bounds(lab, ub, lb, st.drift, st.dmax, st.thr, st.c2, k, cand, count, xn=self.xnorm, cand_lab=cand_lab,
                        cand_xn=cand_xn, zero_count=False, cum=st.cum)
         K.prune_gate(count, st.cap_m, flags, pmode)
@@ -2062,7 +2048,9 @@ class LloydEngine:
             else:
                 w = torch.zeros(uniq.shape[0], dtype=torch.float64, device=self.device)
             self.comm.allreduce_(w)
-            out = K.local_kmeans(uniq, w, k, seed, max_iter=30, spherical=self.spherical)
+            # unweighted: the weights are row counts summing to the global row count, which is positive
+            # (the candidates are rows), so local_kmeans skips its clamp and all-zero fallback
+            out = K.local_kmeans(uniq, w, k, seed, max_iter=30, spherical=self.spherical, counts=self.w is None)
             if self.comm.is_distributed:
                 # every rank ran the same local k-means on the same candidates and weights; rank 0's
                 # result is taken verbatim (one source of truth for the centres every rank starts from)

@@ -9,6 +9,7 @@ from __future__ import annotations
 
 import ctypes
 import os
+import threading
 
 from dataclasses import dataclass
 
@@ -82,6 +83,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "cml_int_hist": (c_int, [c_vp, c_ll, c_int, c_vp, c_vp]),
+    "cml_kmeans_cost_combine": (c_int, [c_vp, c_vp, c_int, c_ll, c_int, c_int, c_dbl, c_vp, c_int, c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_sum_f32_f64_parts": (c_int, []),
     "cml_kmeans_cost_parts": (c_int, []),
@@ -234,20 +236,64 @@ def int_hist(vals: torch.Tensor, n: int, m: int, counts: torch.Tensor, stream=No
                                                  _native.stream_ptr(stream)), "int_hist")
 
 
+def zeros_block(device, specs) -> list:
+    """Zeroed device tensors of the given (numel, dtype) specs as views of ONE allocation (one fill
+    instead of one per tensor: each small torch.zeros costs ~10-20 us of host time on the launch path).
+    Every view starts on a 512-byte boundary, the caching allocator's granule, so a view keeps the same
+    slack past its end that a separate allocation had."""
+    offs, o = [], 0
+    for numel, dt in specs:
+        offs.append(o)
+        o += -(-max(int(numel), 1) * torch.empty((), dtype=dt).element_size() // 512) * 512
+    blk = torch.zeros(max(o, 512), dtype=torch.uint8, device=device)
+    es = [torch.empty((), dtype=dt).element_size() for _, dt in specs]
+    return [blk[off: off + int(n) * e].view(dt) for off, (n, dt), e in zip(offs, specs, es)]
+
+
+def cost_combine(q: torch.Tensor, msgs: torch.Tensor, k: int, d: int, unit: float, cb: torch.Tensor,
+                 stream=None) -> torch.Tensor:
+    """Σ_j q_j - 2 c_j·(S_j·unit) + n_j |c_j|², clamped at 0 (f64 device scalar): the training cost of an
+    assignment from its per-cluster sums (msgs [rows, >= k*d + k]: S then n), the f64 per-cluster Σ||x||²
+    ``q`` and the bf16 centres ``cb`` it compared against. Device tensors: one single-workgroup kernel; host
+    tensors: the same formula in torch."""
+    kd = k * d
+    if not q.is_cuda or cb.dtype != torch.bfloat16:  # (host engines; centres of another dtype)
+        s_ = msgs[:, :kd].sum(0).view(k, d) * unit
+        cnt = msgs[:, kd:kd + k].sum(0)
+        c = cb[:k, :d].to(torch.float64)
+        return (q.sum() - 2.0 * (c * s_).sum() + (cnt * (c * c).sum(1)).sum()).clamp(min=0.0)
+    if (q.dtype != torch.float64 or msgs.dtype != torch.float64 or q.numel() < k
+            or msgs.dim() != 2 or msgs.shape[1] < kd + k or msgs.stride(1) != 1 or cb.stride(1) != 1
+            or cb.shape[0] < k or cb.shape[1] < d or not q.is_contiguous()):
+        raise ValueError("cost_combine: f64 q [k], f64 msgs [rows, >= k*d + k], centres [>= k, >= d]")
+    out = torch.empty(1, dtype=torch.float64, device=q.device)
+    _native.check(_native.kernels().cml_kmeans_cost_combine(
+        q.data_ptr(), msgs.data_ptr(), int(msgs.shape[0]), int(msgs.stride(0)), int(k), int(d), float(unit),
+        cb.data_ptr(), int(cb.stride(0)), out.data_ptr(), _native.stream_ptr(stream)), "kmeans_cost_combine")
+    return out[0]
+
+
+_STOP = threading.local()  # per-thread pinned stop-flag word of local_kmeans (allocated once)
+
+
 def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int, max_iter: int = 30,
-                 spherical: bool = False) -> torch.Tensor:
+                 spherical: bool = False, counts: bool = False) -> torch.Tensor:
     """Weighted k-means++ seeding + weighted Lloyd on a small candidate set (Spark
     LocalKMeans.kMeansPlusPlus), f64 [k, d]. GPU tensors run the ``kmeans_init.hip`` kernels (no host
     read: convergence is latched on the device); CPU tensors the host twin
     (``host/kmeans_local.cpp``), which performs the same rounded operations in the same order: both
     return the same bits. Draws: counter uniforms under (seed, 200) for the picks and (seed, 201) for
-    empty-cluster reseeds."""
+    empty-cluster reseeds. ``counts``: the caller guarantees non-negative weights with a positive sum
+    (row counts of a non-empty dataset), so the clamp and the all-zero fallback are skipped."""
     from ..utils import rng
     pts = points.to(torch.float64).contiguous()
     m, d = pts.shape
-    w = weights.to(device=pts.device, dtype=torch.float64).clamp(min=0)
-    # all-zero weights -> uniform, decided on the device (no host read before the seeding kernels)
-    w = torch.where(w.sum() > 0, w, torch.ones_like(w)).contiguous()
+    w = weights.to(device=pts.device, dtype=torch.float64)
+    if not counts:
+        # all-zero weights -> uniform, decided on the device (no host read before the seeding kernels)
+        w = w.clamp(min=0)
+        w = torch.where(w.sum() > 0, w, torch.ones_like(w))
+    w = w.contiguous()
     key_pp, key_e = rng.key(seed, 200), rng.key(seed, 201)
     lds_update = ((m * 4 + 15) & ~15) + d * 8
     if pts.is_cuda and d * 8 <= 64 * 1024 and lds_update <= 150 * 1024:
@@ -258,9 +304,12 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         CT = torch.empty((d, k), dtype=torch.float64, device=dev)
         d2 = torch.empty(m, dtype=torch.float64, device=dev)
         lab = torch.full((m,), -1, dtype=torch.int32, device=dev)
-        cnt = torch.zeros(k, dtype=torch.float64, device=dev)
-        ctr = torch.zeros(1, dtype=torch.int64, device=dev)
-        picks = torch.zeros(2 * k, dtype=torch.int32, device=dev)
+        # cnt (f64 [k]), ctr (i64), flags (i32 [3] + pad) and picks (i32 [2k]): views of one zeroed block
+        zb = torch.zeros(16 * k + 24, dtype=torch.uint8, device=dev)
+        cnt = zb[: 8 * k].view(torch.float64)
+        ctr = zb[8 * k: 8 * k + 8].view(torch.int64)
+        flags = zb[8 * k + 8: 8 * k + 20].view(torch.int32)
+        picks = zb[8 * k + 24:].view(torch.int32)
         PT = pts.t().contiguous()
         # pairwise candidate distances up front (one parallel pass) when they fit 1 GiB: each pick is
         # then a row read instead of m dimension folds on the one seeding workgroup
@@ -272,11 +321,12 @@ def local_kmeans(points: torch.Tensor, weights: torch.Tensor, k: int, seed: int,
         # iteration's assign moved no label (the host loop's break), after which every queued launch
         # returns at once — max_iter iterations are enqueued back to back, the same bits as the host
         # twin's loop (a few no-op launches instead of one host round trip per iteration)
-        flags = torch.zeros(3, dtype=torch.int32, device=dev)
         fp = flags.data_ptr()
         # the stop flag is read back every 8 iterations (one small copy): converged local fits (a few
         # iterations) then launch 8 instead of max_iter x 3 no-op kernels (k-means|| finish on the shard)
-        stop_h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
+        stop_h = getattr(_STOP, "h", None)
+        if stop_h is None:
+            stop_h = _STOP.h = torch.zeros(1, dtype=torch.int32, pin_memory=True)
         for it in range(max_iter):
             if it and it % 8 == 0:
                 stop_h.copy_(flags[0:1], non_blocking=True)
@@ -582,18 +632,13 @@ class DeltaState:
         self.lean = bool(lean)
         self.host_forced = True  # the device force flag is set (creation / invalidate): next gate is not lean
         self.entries = self.nblk * self.pcap if self.lean else self.cap
-        self.rows = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
-        self.old = torch.zeros(self.nblk * self.pcap, dtype=torch.int32, device=device)
-        self.wg_count = torch.zeros(self.nblk, dtype=torch.int32, device=device)
-        self.overflow = torch.zeros(1, dtype=torch.int32, device=device)
-        self.mode = torch.zeros((chunks, 2), dtype=torch.int32, device=device)
+        i32, f64, lists = torch.int32, torch.float64, self.nblk * self.pcap
+        (self.rows, self.old, self.wg_count, self.overflow, mode, self.dh, self.dseg, self.cursor, self.dperm,
+         self.dsum, acc) = zeros_block(device, [(lists, i32), (lists, i32), (self.nblk, i32), (1, i32),
+                                                (2 * chunks, i32), (2 * k, i32), (2 * k + 2, i32), (2 * k, i32),
+                                                (2 * self.entries, i32), (2 * k * d, f64), (chunks * msg_len, f64)])
+        self.mode, self.acc = mode.view(chunks, 2), acc.view(chunks, msg_len)
         self.force = torch.ones(chunks, dtype=torch.int32, device=device)
-        self.dh = torch.zeros(2 * k, dtype=torch.int32, device=device)
-        self.dseg = torch.zeros(2 * k + 2, dtype=torch.int32, device=device)
-        self.cursor = torch.zeros(2 * k, dtype=torch.int32, device=device)
-        self.dperm = torch.zeros(2 * self.entries, dtype=torch.int32, device=device)
-        self.dsum = torch.zeros(2 * k * d, dtype=torch.float64, device=device)
-        self.acc = torch.zeros((chunks, msg_len), dtype=torch.float64, device=device)
         ncu = num_cus(device.index or 0)
         self.plan = AccumPlan(mode="sort", cpl=(dp // 64 if fp8 else (2 if dp <= 128 else (4 if dp <= 256 else 8))),
                               seg_grid=max(1, min((2 * self.entries + 255) // 256, ncu * 4)), dw=dp)

@@ -36,9 +36,18 @@ def splitmix64(x: torch.Tensor) -> torch.Tensor:
     return x ^ _lsr(x, 31)
 
 
+def _splitmix64_int(x: int) -> int:
+    """splitmix64 of one value in Python integers (mod 2^64): the bits of ``splitmix64`` without torch ops
+    (a key is derived on every launch path; the tensor form cost ~8 host ops per key)."""
+    m = (1 << 64) - 1
+    x = (x + 0x9E3779B97F4A7C15) & m
+    x = ((x ^ (x >> 30)) * 0xBF58476D1CE4E5B9) & m
+    x = ((x ^ (x >> 27)) * 0x94D049BB133111EB) & m
+    return _s64(x ^ (x >> 31))
+
+
 def key(seed: int, stream: int = 0) -> int:
-    t = torch.tensor([_s64(seed * 0x100000001B3 + stream * 0xC2B2AE3D27D4EB4F)], dtype=torch.int64)
-    return int(splitmix64(t)[0])
+    return _splitmix64_int(_s64(seed * 0x100000001B3 + stream * 0xC2B2AE3D27D4EB4F) & ((1 << 64) - 1))
 
 
 def uniform(row_ids: torch.Tensor, seed: int, stream: int = 0) -> torch.Tensor:

@@ -398,3 +398,21 @@ def test_rr_and_k9_trajectories_bitwise_on_separated_exact_data(n, d, k):
     for (l0, c0), (l8, c8) in zip(traj[0], traj[8]):
         assert torch.equal(l0.long(), l8.long())
         assert torch.equal(c0, c8)
+
+
+@pytest.mark.parametrize("rows,k,d,pad", [(1, 256, 256, 0), (3, 17, 40, 24), (2, 1, 8, 0)])
+def test_cost_combine_kernel_matches_f64_formula(rows, k, d, pad):
+    """kmeans_cost_combine (the training cost from the step's sums) against the same formula in f64 torch."""
+    g = torch.Generator(device="cpu").manual_seed(k * 7 + d)
+    kd = k * d
+    msgs = torch.randn(rows, kd + k + 1, generator=g, dtype=torch.float64) * 50
+    msgs[:, kd:kd + k] = torch.randint(0, 1000, (rows, k), generator=g).double()
+    cb = (torch.randn(k + 5, d + pad, generator=g) * 3).to(torch.bfloat16)
+    q = torch.rand(k, generator=g, dtype=torch.float64) * 1e6 + 1e5
+    unit = 0.25
+    ref = K.cost_combine(q, msgs, k, d, unit, cb)  # host form
+    got = K.cost_combine(q.cuda(), msgs.cuda(), k, d, unit, cb.cuda())
+    assert got.is_cuda
+    torch.testing.assert_close(got.cpu(), ref, rtol=1e-12, atol=1e-6)
+    again = K.cost_combine(q.cuda(), msgs.cuda(), k, d, unit, cb.cuda())
+    assert float(again) == float(got)  # fixed reduction order
