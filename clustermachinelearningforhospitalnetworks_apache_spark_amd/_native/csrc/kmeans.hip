@@ -924,50 +924,23 @@ __global__ __launch_bounds__(kSegThreads, (CPL <= 4 ? 4 : 1)) void kmeans_segacc
     const float cu = sub.cu[cc];
     return (u - cu) + 1e-6f * (u + cu);
   };
-  // Row ids are loaded ahead of their gathers (one memory round trip per batch instead of two dependent
-  // ones), and rows of at most 8 B per lane (bf16 up to 256 columns, fp8 up to 512) are double-buffered:
-  // the next batch's 16 gathers are issued before this batch is summed, so a wave keeps two batches in
-  // flight (the gathered pass sat at 3.7-4.0 TB/s with one)
-  // (the UB form's squared-distance partials leave no room for a second 8-B batch under the 128-VGPR bound)
-  constexpr bool DB = sizeof(raw_t) <= 8 && !(UB && (F8 || sizeof(raw_t) > 4));
-  auto load_batch = [&](raw_t (&dst)[U], int prr, int cn) {
-#pragma unroll
-    for (int u = 0; u < U; ++u) {
-      const long long row = __builtin_amdgcn_readlane(prr, u);
-      if (u < cn && active) {
-        dst[u] = *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ);
-      } else {
-        dst[u] = raw_t{};
-      }
-    }
-  };
-  auto ids_at = [&](long long q0) { return (lane < U && q0 + lane < p1) ? perm[q0 + lane] : 0; };
-  auto cnt_at = [&](long long q0) { return (int)(q0 >= p1 ? 0 : (p1 - q0 < U ? p1 - q0 : U)); };
-  // DB: pr_cur = ids of batch p (its rows already in wnx), pr_next = ids of batch p + U;
-  // otherwise pr_next = ids of batch p
-  int pr_cur = 0, pr_next = ids_at(p0);
-  raw_t wnx[U];
-  if constexpr (DB) {
-    pr_cur = pr_next;
-    load_batch(wnx, pr_cur, cnt_at(p0));
-    pr_next = ids_at(p0 + U);
-  }
+  // the next batch's row ids are loaded one batch ahead: the row gathers then wait for one memory
+  // round trip per batch instead of two dependent ones (the pass was latency-bound at 3.7 TB/s)
+  int pr_next = (lane < U && p0 + lane < p1) ? perm[p0 + lane] : 0;
   for (long long p = p0; p < p1; p += U) {
-    const int cnt = cnt_at(p);
+    const int cnt = (int)(p1 - p < U ? p1 - p : U);
+    const int pr = pr_next;
+    pr_next = (lane < U && p + U + lane < p1) ? perm[p + U + lane] : 0;
     float mine = 0.f;  // UB: squared distance of the batch's row `lane`
     raw_t w[U];
-    int pr;
-    if constexpr (DB) {
-      pr = pr_cur;
 #pragma unroll
-      for (int u = 0; u < U; ++u) w[u] = wnx[u];
-      load_batch(wnx, pr_next, cnt_at(p + U));  // the next batch's gathers go out before this one is summed
-      pr_cur = pr_next;
-      pr_next = ids_at(p + 2 * U);
-    } else {
-      pr = pr_next;
-      pr_next = ids_at(p + U);
-      load_batch(w, pr, cnt);
+    for (int u = 0; u < U; ++u) {
+      const long long row = __builtin_amdgcn_readlane(pr, u);
+      if (u < cnt && active) {
+        w[u] = *reinterpret_cast<const raw_t*>(xb + (row * ldx + col) * ESZ);
+      } else {
+        w[u] = raw_t{};
+      }
     }
     const long long pe = p + cnt;
     if (next >= pe) {

@@ -58,6 +58,7 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
                                                             int* __restrict__ erange, double* __restrict__ xn64,
                                                             const float* __restrict__ c0n_dev) {
   typedef float f2 __attribute__((ext_vector_type(2)));
+  typedef unsigned short us2 __attribute__((ext_vector_type(2)));
   if (c0n_dev != nullptr) c0n = *c0n_dev;  // ||c0||² left on the device by the centre conversion
   constexpr int LPR = NCH / CPL;
   static_assert(LPR >= 1 && LPR <= 64 && NCH % CPL == 0, "row split");
@@ -69,7 +70,9 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
   const long long w0 = ((long long)blockIdx.x * blockDim.x + threadIdx.x) >> 6;
   const long long nw = ((long long)gridDim.x * blockDim.x) >> 6;
   const bool dot = c0 != nullptr;
-  unsigned umx = 0u, umn = 0xffffu;
+  // exponent range on packed 16-bit halves (v_pk_max_u16 / v_pk_sub_u16 / v_pk_min_u16: four instructions per
+  // pair of values instead of ~eight; the pass is VALU-bound): max |bits|, min (|bits| - 1) mod 2^16
+  us2 pmx = {0, 0}, pmn = {0xffff, 0xffff};
   unsigned mxb = 0;
   // this lane's columns of the first centre, in registers for the whole pass (re-reading them from
   // the cache every row tripled the pass's load traffic)
@@ -112,16 +115,19 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
           for (int q = 0; q < 4; ++q) {
             xs[2 * q] = bf16_to_f32((u16)(w[q] & 0xffffu));
             xs[2 * q + 1] = bf16_to_f32((u16)(w[q] >> 16));
-            const unsigned lo = w[q] & 0x7fffu, hi = (w[q] >> 16) & 0x7fffu;  // rows past n load zeros
-            umx = max(umx, max(lo, hi));
-            umn = min(umn, min((lo + 0xffffu) & 0xffffu, (hi + 0xffffu) & 0xffffu));
+            const us2 m = __builtin_bit_cast(us2, w[q] & 0x7fff7fffu);  // rows past n load zeros
+            pmx = __builtin_elementwise_max(pmx, m);
+            pmn = __builtin_elementwise_min(pmn, m - us2{1, 1});  // wraps: a zero goes to 0xffff
           }
         }
 #pragma unroll
         for (int e = 0; e < VPC; ++e) s = fmaf(xs[e], xs[e], s);
-        if (wide) {  // x² of a bf16 / e4m3 value is exact in f32; the f64 sum is exact up to its own rounding
+        if (wide) {  // x² of a bf16 / e4m3 value is exact in f64: one f64 fma adds it with the sum's own rounding
 #pragma unroll
-          for (int e = 0; e < VPC; ++e) s64 += (double)(xs[e] * xs[e]);
+          for (int e = 0; e < VPC; ++e) {
+            const double xd = (double)xs[e];
+            s64 = fma(xd, xd, s64);
+          }
         }
         if (dot) {
 #pragma unroll
@@ -145,6 +151,7 @@ __global__ __launch_bounds__(kThreads) void row_pass_kernel(const unsigned char*
       }
     }
   }
+  unsigned umx = pmx[0] > pmx[1] ? pmx[0] : pmx[1], umn = pmn[0] < pmn[1] ? pmn[0] : pmn[1];
   // wave reductions, one atomic per wave (integer min/max: the result does not depend on order)
 #pragma unroll
   for (int o = 32; o > 0; o >>= 1) {

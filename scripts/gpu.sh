@@ -12,6 +12,7 @@
 #                         kernel / blocking-call / roctx timeline, kernel table, host syncs, sync audit
 #   strong                strong-scaling emulation: per-rank shards of the headline (100M / N rows)
 #   workflow              the reference workflow end to end on 4M uploaded rows (examples/)
+#   ovtl                  2-rank gloo timeline of the seeded step's overlapped accumulate (rocprofv3 per rank)
 #   mb SCRIPT [args]      a microbenchmark script (scripts/mb_*.py ...) -> SCRIPT.log
 #
 # Every GPU step runs under its own `timeout -k 10`; steps are chained so a failure ends the job.
@@ -116,6 +117,22 @@ h.synth_uploads('/tmp/wfsrc/hospitals/incoming', n_files=4, rows=1000000)
   t1=$(date +%s.%N)
   python3 -c "print('workflow wall s', round($t1 - $t0, 3))"
   grep -A24 "^range" "$O/workflow.log"
+  ;;
+ovtl)
+  # two gloo ranks on the one GPU, one rocprofv3 process each: the seeded step's split accumulate and the
+  # order of chunk 0's all-reduce copies against chunk 1's kernels (scripts/overlap_timeline.py)
+  P=$((29500 + RANDOM % 400))
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ov0 -o r0 -- \
+    python3 scripts/overlap_timeline.py rank 0 2 $P > "$O/r0.log" 2>&1 &
+  P0=$!
+  S1=0
+  timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ov1 -o r1 -- \
+    python3 scripts/overlap_timeline.py rank 1 2 $P > "$O/r1.log" 2>&1 || S1=$?
+  S0=0
+  wait $P0 || S0=$?
+  [ $S0 -eq 0 ] && [ $S1 -eq 0 ] || { tail -20 "$O/r0.log" "$O/r1.log"; exit 1; }
+  python3 scripts/overlap_timeline.py show /tmp/ov0/r0_results.db /tmp/ov1/r1_results.db > "$O/timeline.txt"
+  head -80 "$O/timeline.txt"
   ;;
 mb)
   S=${1:?script}

@@ -1,6 +1,5 @@
-"""K12 row pass on 100M x 256 bf16 rows (norms + first k-means|| costs + max norm + exponent range):
-best of 10 timed launches. CML_ROWPASS_PACKED=1 selects the packed-FMA variant (read once per process)."""
-import os
+"""K12 row pass on 100M x 256 bf16 rows (norms in f32 and f64 + first k-means|| costs + max norm + exponent
+range, as LloydEngine._row_pass runs it): best of 10 timed launches."""
 import torch
 from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
 
@@ -9,6 +8,7 @@ x = torch.empty((n, dp), dtype=torch.bfloat16, device="cuda")
 for s in range(0, n, 1 << 24):
     x[s:s + (1 << 24)] = torch.randn((min(1 << 24, n - s), dp), device="cuda").to(torch.bfloat16)
 xn = torch.empty(n, device="cuda")
+xn64 = torch.empty(n, dtype=torch.float64, device="cuda")
 cost = torch.empty(n, device="cuda")
 near = torch.empty(n, dtype=torch.int32, device="cuda")
 c0 = x[7].float().contiguous()
@@ -19,9 +19,10 @@ for _ in range(10):
     er = torch.tensor([2 ** 31 - 1, -1], dtype=torch.int32, device="cuda")
     a, b = torch.cuda.Event(True), torch.cuda.Event(True)
     a.record()
-    K.row_pass(x, n, dp, xn, c0, c0n, cost, near, xn_max=mx, erange=er)
+    K.row_pass(x, n, dp, xn, c0, c0n, cost, near, xn_max=mx, erange=er, xn64=xn64)
     b.record()
     torch.cuda.synchronize()
     best = min(best, a.elapsed_time(b))
-print(f"packed={os.environ.get('CML_ROWPASS_PACKED', '0')} row_pass {best:.3f} ms {n * dp * 2 / best / 1e9:.2f} TB/s "
-      f"erange={er.tolist()}", flush=True)
+print(f"row_pass {best:.3f} ms {n * dp * 2 / best / 1e9:.2f} TB/s "
+      f"erange={er.tolist()} sum(xn)={float(xn.double().sum())!r} sum(xn64)={float(xn64.sum())!r} "
+      f"sum(cost)={float(cost.double().sum())!r}", flush=True)

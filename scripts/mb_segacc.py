@@ -26,12 +26,13 @@ torch.cuda.synchronize()
 msg = torch.zeros_like(eng.msgs[0])
 ub = torch.empty(n, dtype=torch.float32, device=dev)
 gb = n * d * 2 / 1e9
+print(f"sum grid scale {eng._qscale!r} (0: plain f64 sums)")
 
 
 def run(with_ub: bool):
     K.accumulate_sort(x, n, eng.dp, d, eng.labels, eng.rank, eng.hist, eng.aplan, k, eng.cost_part, eng.off,
                       eng.seg, eng.perm, eng.cplan, msg, eng.slots, ub_centres=eng.cb if with_ub else None,
-                      ub=ub if with_ub else None)
+                      ub=ub if with_ub else None, qscale=eng._qscale)
 
 
 for with_ub in (False, True):

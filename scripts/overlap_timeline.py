@@ -3,8 +3,8 @@
 (kernel + memory-copy + marker traces) the per-process databases show the order on the device.
 
     python scripts/overlap_timeline.py run                       (both ranks from one process)
-    rocprofv3 --kernel-trace --memory-copy-trace --marker-trace -d DIR0 -o r0 -- \
-        python scripts/overlap_timeline.py rank 0 2 PORT &        (one profiled process per rank)
+    rocprofv3 --kernel-trace --memory-copy-trace -d DIR0 -o r0 -- \
+        python3 scripts/overlap_timeline.py rank 0 2 PORT &       (one profiled process per rank; same for rank 1)
     python scripts/overlap_timeline.py show DIR0/*.db
 
 ``show`` prints, for every process database, the kernels and copies between the two probe-kernel dispatches that
@@ -12,6 +12,7 @@ bracket the traced seeded step, in time order (the gloo all-reduce of a CUDA ten
 device-to-host copy).
 """
 import os
+import re
 import socket
 import sqlite3
 import sys
@@ -34,7 +35,7 @@ def _rank(rank, world, port):
     import torch.distributed as dist
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
-    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as KO
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.trace import trace
     torch.cuda.set_device(0)
     pa = torch.zeros((16, 128), dtype=torch.uint8, device="cuda")
@@ -53,11 +54,11 @@ def _rank(rank, world, port):
         eng.set_centers(init)
         torch.cuda.synchronize()
         if it:  # the traced step, bracketed by two dispatches of a one-wave probe kernel (window markers)
-            K.mx_probe(pa, pa, ps, ps)
+            KO.mx_probe(pa, pa, ps, ps)
         with trace("kmeans.seeded" if it else "warmup.seeded"):
             eng.step()
             if it:
-                K.mx_probe(pa, pa, ps, ps)
+                KO.mx_probe(pa, pa, ps, ps)
             torch.cuda.synchronize()
         eng.fit(3, 0.0)
         torch.cuda.synchronize()
@@ -80,25 +81,32 @@ def run():
 def show(paths):
     for path in paths:
         c = sqlite3.connect(path)
-        ks = list(c.execute("select name, start, end from kernels order by start"))
-        marks = [(s, e) for n, s, e in ks if "mx_probe_kernel" in n]
+        kcols = [r[1] for r in c.execute("pragma table_info(kernels)")]
+        sid = next((x for x in ("stream_id", "queue_id") if x in kcols), None)
+        ks = list(c.execute(f"select name, start, end, {sid or 0} from kernels order by start"))
+        marks = [(s, e) for n, s, e, _ in ks if "mx_probe_kernel" in n]
         if len(marks) < 2:
             print(f"{path}: no probe-kernel window ({len(marks)} markers)")
             continue
         lo, hi = marks[0][1], marks[1][0]
-        ev = [(s, e, "K", n.split("(")[0][:60]) for n, s, e in ks if lo <= s < hi]
+        def short(n):
+            n = re.sub(r"\(anonymous namespace\)::", "", n)
+            n = re.sub(r"^void ", "", n)
+            return n.split("(")[0][:70]
+        ev = [(s, e, f"K q{q}", short(n)) for n, s, e, q in ks if lo <= s < hi]
         try:
             cols = [r[1] for r in c.execute("pragma table_info(memory_copies)")]
             for row in c.execute("select * from memory_copies where start >= ? and start < ?", (lo, hi)):
                 r = dict(zip(cols, row))
-                what = "/".join(str(r[k]) for k in ("name", "src_agent_type", "dst_agent_type", "size") if k in r)
-                ev.append((r["start"], r["end"], "C", what))
+                what = "/".join(str(r[k]) for k in ("name", "size") if k in r)
+                q = r.get("stream_id", r.get("queue_id", ""))
+                ev.append((r["start"], r["end"], f"C q{q}", what))
         except sqlite3.Error as exc:
             print(f"(memory copies: {exc})")
         ev.sort()
         print(f"=== {path}: seeded step window {(hi - lo) / 1e6:.3f} ms, {len(ev)} events")
         for s, e, kind, name in ev:
-            print(f"{(s - lo) / 1e6:9.3f} ms  {kind}  {(e - s) / 1e3:8.1f} us  {name}")
+            print(f"{(s - lo) / 1e6:9.3f} ms  {kind:6s} {(e - s) / 1e3:8.1f} us  {name}")
 
 
 if __name__ == "__main__":
