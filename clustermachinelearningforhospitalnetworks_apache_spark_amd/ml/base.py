@@ -13,6 +13,7 @@ from typing import Any, Dict, List, Optional, Union
 import torch
 
 from .param import Params
+from ..utils.device import gc_paused
 from ..utils.trace import trace
 from .util import MLReadable, MLWritable
 
@@ -36,7 +37,7 @@ class Estimator(Params, MLWritable, MLReadable):
         if dataset.isStreaming:
             raise RuntimeError("fit() on a streaming DataFrame: use writeStream.foreachBatch to train per batch")
         inst = self.copy(params) if params else self
-        with trace(f"{type(self).__name__}.fit"):
+        with trace(f"{type(self).__name__}.fit"), gc_paused():
             model = inst._fit(dataset)
         if model is not None and getattr(model, "parent", None) is None:
             model.parent = inst

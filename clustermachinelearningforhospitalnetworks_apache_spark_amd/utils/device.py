@@ -1,7 +1,9 @@
-"""Device helpers: gfx950 properties, padding rules, dtype maps."""
+"""Device helpers: gfx950 properties, padding rules, dtype maps, host-latency guards."""
 from __future__ import annotations
 
+import contextlib
 import functools
+import gc
 import os
 
 import torch
@@ -41,3 +43,19 @@ def is_gpu(t: torch.Tensor) -> bool:
 
 def gpu_available() -> bool:
     return torch.cuda.is_available() and os.environ.get("CML_FORCE_CPU") != "1"
+
+
+@contextlib.contextmanager
+def gc_paused():
+    """Python's cyclic garbage collector off for the duration (Estimator.fit). A fit on a small shard is bound by
+    the host's launch latency; a collection pass that lands between two launches idles the GPU for its whole
+    duration. Reference counting still frees everything a fit allocates; the collector resumes (and catches
+    up) when the fit returns. Nested fits (a Pipeline's stages) see it paused already. CML_GC_PAUSE=0: off."""
+    if os.environ.get("CML_GC_PAUSE", "1") == "0" or not gc.isenabled():
+        yield
+        return
+    gc.disable()
+    try:
+        yield
+    finally:
+        gc.enable()

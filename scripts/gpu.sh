@@ -85,13 +85,14 @@ shard)
   fit_line "$O/shard.json"
   timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --marker-trace -d /tmp/sh -o sh -- python3 bench.py \
     --rows 12500000 --warmup 3 --no-overlap "$@" > "$O/sh.log" 2>&1 || { tail -5 "$O/sh.log"; exit 1; }
-  python3 scripts/rocpd_timeline.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 > "$O/timeline.txt"
+  python3 scripts/rocpd_timeline.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --gap-apis 80 --gap-detail 250 \
+    > "$O/timeline.txt"
   python3 scripts/rocpd_stats.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --top 40 > "$O/stats.txt"
   python3 scripts/rocpd_syncs.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --show 5 > "$O/syncs.txt"
   timeout -k 10 300 python3 scripts/sync_audit.py --rows 2000000 > "$O/sync_audit.txt" 2>&1 \
     || { tail -20 "$O/sync_audit.txt"; exit 1; }
   head -3 "$O/syncs.txt"
-  tail -1 "$O/timeline.txt"
+  grep "^window" "$O/timeline.txt"
   head -1 "$O/sync_audit.txt"
   ;;
 strong)

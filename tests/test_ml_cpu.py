@@ -302,3 +302,19 @@ def test_string_indexer_binarizer_minmax(spark, tmp_path):
     mm = MinMaxScaler(inputCol="v", outputCol="m").fit(v)
     got = [r.m[0] for r in mm.transform(v).collect()]
     np.testing.assert_allclose(got, [(x - 0.1) / 0.8 for x in [0.2, 0.9, 0.6, 0.1]])
+
+
+def test_fit_pauses_cyclic_gc_and_restores_it(monkeypatch):
+    """Estimator.fit runs with Python's cyclic collector paused (host-latency guard) and restores it."""
+    import gc
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.device import gc_paused
+    assert gc.isenabled()
+    with gc_paused():
+        assert not gc.isenabled()
+        with gc_paused():  # nested: stays paused, and the inner exit does not re-enable it
+            assert not gc.isenabled()
+        assert not gc.isenabled()
+    assert gc.isenabled()
+    monkeypatch.setenv("CML_GC_PAUSE", "0")
+    with gc_paused():
+        assert gc.isenabled()
