@@ -163,6 +163,10 @@ class DataFrameReader:
         # precise_float: exact round trip of the writer's shortest-repr doubles (the default parser rounds)
         frames = [pd.read_json(f, lines=True, precise_float=True) for f in files]
         pdf = pd.concat(frames, ignore_index=True) if frames else pd.DataFrame()
+        if self._schema is not None and pdf.shape[1] == 0 and len(pdf):
+            # every record is {} (Spark omits null fields): a placeholder column keeps the row count through
+            # Arrow (a column-less table has no rows); the schema select below drops it
+            pdf["__cml_rows"] = 0
         special = _non_numeric_numbers(pdf, files)
         comm = self._session._comm
         a, b = shard_range(len(pdf), comm.rank, comm.world_size)

@@ -36,3 +36,17 @@ def test_json_nan_strings_without_numbers_stay_strings(tmp_path):
     rows = sorted(df.collect(), key=lambda r: r["b"])
     assert [r["a"] for r in rows] == ["NaN", "Infinity", None]
     assert rows[0]["c"] == 'x "NaN" y'
+
+
+def test_json_all_null_rows_round_trip(tmp_path):
+    """Rows whose every field is null are written as {} (Spark omits null fields) and read back as rows of
+    nulls under the schema — also when EVERY record is {} (no column at all in the files; found by
+    tests/test_properties.py)."""
+    spark = SparkSession.builder.master("local[1]").getOrCreate()
+    schema = T.StructType([T.StructField("h", T.StringType()), T.StructField("a", T.LongType()),
+                           T.StructField("x", T.DoubleType())])
+    for rows in ([(None, None, None)], [(None, None, None), (None, None, None)], [(None, None, None), ("p", 2, 0.5)]):
+        path = str(tmp_path / f"n{len(rows)}{rows[-1][0]}")
+        spark.createDataFrame(rows, schema).write.mode("overwrite").json(path)
+        back = spark.read.schema(schema).json(path)
+        assert [tuple(r) for r in back.collect()] == rows
