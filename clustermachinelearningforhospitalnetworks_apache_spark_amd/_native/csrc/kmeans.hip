@@ -1245,43 +1245,49 @@ __global__ __launch_bounds__(256) void init_merge_list_kernel(float* __restrict_
   }
 }
 
-// msg[c] += Σ over the slices overlapping cluster c, in ascending slice order, of their head
-// (A) / tail (B) partials for c. One workgroup per cluster.
+// Σ over the slices overlapping segment c, in ascending slice order, of their head (A) / tail (B) partials
+// for c, column d (what kmeans_segacc left in the slots for segments that cross a wave slice).
+__device__ __forceinline__ double seg_fix(const int* __restrict__ seg, int k, int D, long long n, long long nwaves,
+                                          const double* __restrict__ slots, const int* __restrict__ slot_c, int c,
+                                          int d) {
+  const long long s0 = seg[c], s1 = seg[c + 1];
+  if (s1 <= s0) return 0.0;
+  const long long chunk = seg_chunk(n < (long long)seg[k] ? n : (long long)seg[k], nwaves);  // as kmeans_segacc
+  const long long w0 = s0 / chunk;
+  long long w1 = (s1 - 1) / chunk;
+  if (w1 >= nwaves) w1 = nwaves - 1;
+  double t = 0.0;
+  long long w = w0;
+  // 8 slices per round, loads issued together (a cluster can span thousands of slices)
+  for (; w + 8 <= w1 + 1; w += 8) {
+    double v[8];
+#pragma unroll
+    for (int q = 0; q < 8; ++q) {
+      const long long ww = w + q;
+      const int ca = slot_c[2 * ww], cb = slot_c[2 * ww + 1];
+      const double a = slots[(2 * ww) * (long long)D + d], b = slots[(2 * ww + 1) * (long long)D + d];
+      v[q] = ca == c ? a : 0.0;
+      v[q] = cb == c ? v[q] + b : v[q];
+    }
+#pragma unroll
+    for (int q = 0; q < 8; ++q) t += v[q];
+  }
+  for (; w <= w1; ++w) {
+    if (slot_c[2 * w] == c) t += slots[(2 * w) * (long long)D + d];
+    if (slot_c[2 * w + 1] == c) t += slots[(2 * w + 1) * (long long)D + d];
+  }
+  return t;
+}
+
+// msg[c] += seg_fix(c) for every column. One workgroup per cluster.
 __global__ __launch_bounds__(256) void kmeans_seg_fixup(const int* __restrict__ seg, int k, int D, long long n,
                                                         long long nwaves, const double* __restrict__ slots,
                                                         const int* __restrict__ slot_c, double* __restrict__ msg,
                                                         const int* __restrict__ gate, int want) {
   if (gate != nullptr && gate[0] != want) return;  // step-mode gate (incremental sums)
   const int c = blockIdx.x;
-  const long long s0 = seg[c], s1 = seg[c + 1];
-  if (s1 <= s0) return;
-  const long long chunk = seg_chunk(n < (long long)seg[k] ? n : (long long)seg[k], nwaves);  // as kmeans_segacc
-  const long long w0 = s0 / chunk;
-  long long w1 = (s1 - 1) / chunk;
-  if (w1 >= nwaves) w1 = nwaves - 1;
-  for (int d = threadIdx.x; d < D; d += blockDim.x) {
-    double t = 0.0;
-    long long w = w0;
-    // 8 slices per round, loads issued together (a cluster can span thousands of slices)
-    for (; w + 8 <= w1 + 1; w += 8) {
-      double v[8];
-#pragma unroll
-      for (int q = 0; q < 8; ++q) {
-        const long long ww = w + q;
-        const int ca = slot_c[2 * ww], cb = slot_c[2 * ww + 1];
-        const double a = slots[(2 * ww) * (long long)D + d], b = slots[(2 * ww + 1) * (long long)D + d];
-        v[q] = ca == c ? a : 0.0;
-        v[q] = cb == c ? v[q] + b : v[q];
-      }
-#pragma unroll
-      for (int q = 0; q < 8; ++q) t += v[q];
-    }
-    for (; w <= w1; ++w) {
-      if (slot_c[2 * w] == c) t += slots[(2 * w) * (long long)D + d];
-      if (slot_c[2 * w + 1] == c) t += slots[(2 * w + 1) * (long long)D + d];
-    }
-    msg[(long long)c * D + d] += t;
-  }
+  if (seg[c + 1] <= seg[c]) return;
+  for (int d = threadIdx.x; d < D; d += blockDim.x) msg[(long long)c * D + d] += seg_fix(seg, k, D, n, nwaves, slots, slot_c, c, d);
 }
 
 // One workgroup per (padded) centre. Writes bf16 centre row (zero padded), ||c||² of the
@@ -1379,14 +1385,22 @@ __global__ __launch_bounds__(256) void kmeans_delta_gate(const int* __restrict__
 }
 
 // One delta workgroup per assign workgroup b: its change list is rows/old[b*pcap, + wg_count[b]).
-// Histogram of the 2m delta entries by key, block-aggregated in LDS.
+// Histogram of the 2m delta entries by key, block-aggregated in LDS. The launch also clears the delta sums
+// (dsum, 2k·D doubles: the segmented pass stores or adds into them) and the per-key scatter counters — the
+// separate zeroing and scan launches of each delta step are gone (kmeans_delta_scatter forms the segment
+// offsets itself).
 __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_hist(const int* __restrict__ rows,
                                                                    const int* __restrict__ old,
                                                                    const int* __restrict__ labels,
                                                                    const int* __restrict__ wg_count, int pcap,
                                                                    const int* __restrict__ mode, int k,
-                                                                   int* __restrict__ dh) {
+                                                                   int* __restrict__ dh, double* __restrict__ dsum,
+                                                                   long long nsum, int* __restrict__ cursor) {
   if (mode[0] != 0) return;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < nsum; i += (long long)gridDim.x * blockDim.x)
+    dsum[i] = 0.0;
+  if (blockIdx.x == 0)
+    for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) cursor[i] = 0;
   extern __shared__ int lh[];
   for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
   __syncthreads();
@@ -1400,53 +1414,58 @@ __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_hist(const int* __
     if (lh[i]) atomicAdd(dh + i, lh[i]);
 }
 
-// seg[j] = first sorted position of key j (seg[2k] = 2m); cursor[j] = seg[j]. One workgroup.
-__global__ __launch_bounds__(256) void kmeans_delta_scan(const int* __restrict__ dh, const int* __restrict__ mode,
-                                                         int k, int* __restrict__ seg, int* __restrict__ cursor) {
-  if (mode[0] != 0) return;
-  __shared__ int part[256];
-  const int nk = 2 * k, per = (nk + 255) / 256, t = threadIdx.x;
-  int s = 0;
-  for (int j = t * per; j < (t + 1) * per && j < nk; ++j) s += dh[j];
-  part[t] = s;
-  __syncthreads();
-  if (t == 0) {
-    int acc = 0;
-    for (int i = 0; i < 256; ++i) {
-      const int v = part[i];
-      part[i] = acc;
-      acc += v;
-    }
-    seg[nk] = acc;
-  }
-  __syncthreads();
-  int acc = part[t];
-  for (int j = t * per; j < (t + 1) * per && j < nk; ++j) {
-    seg[j] = acc;
-    cursor[j] = acc;
-    acc += dh[j];
-  }
-}
-
-// perm[cursor[key]++] = row for both entries of every changed row (block reserves per-key ranges).
+// perm[seg[key] + cursor[key]++] = row for both entries of every changed row (block reserves per-key ranges).
+// Every workgroup forms the segment offsets seg (exclusive prefix of the 2k key counts dh) in LDS itself —
+// one scan per workgroup instead of a one-workgroup scan launch between the histogram and this pass — and
+// workgroup 0 publishes them for the segmented sums and the apply; cursor (zeroed by kmeans_delta_hist)
+// counts each key's reserved entries.
 __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_scatter(const int* __restrict__ rows,
                                                                       const int* __restrict__ old,
                                                                       const int* __restrict__ labels,
                                                                       const int* __restrict__ wg_count, int pcap,
                                                                       const int* __restrict__ mode, int k,
                                                                       int* __restrict__ cursor,
-                                                                      int* __restrict__ perm) {
+                                                                      int* __restrict__ perm,
+                                                                      const int* __restrict__ dh,
+                                                                      int* __restrict__ seg) {
   if (mode[0] != 0) return;
-  extern __shared__ int lh[];  // [2k] counts, then bases
-  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = 0;
-  __syncthreads();
+  extern __shared__ int lh[];  // [2k] counts, then bases; [2k + 1] segment offsets
+  const int nk = 2 * k;
+  int* segl = lh + nk;
+  __shared__ int wtot[kDeltaThreads / 64];
+  {
+    // exclusive scan of dh: thread t owns keys [t·per, (t+1)·per), a wave scan of the thread sums, then
+    // the wave totals (the same integer offsets as a serial scan)
+    const int per = (nk + kDeltaThreads - 1) / kDeltaThreads, t = threadIdx.x, lane = t & 63, wv = t >> 6;
+    int sum = 0;
+    for (int j = t * per; j < (t + 1) * per && j < nk; ++j) sum += dh[j];
+    int incl = sum;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+      const int v = __shfl_up(incl, o, 64);
+      if (lane >= o) incl += v;
+    }
+    if (lane == 63) wtot[wv] = incl;
+    for (int i = t; i < nk; i += kDeltaThreads) lh[i] = 0;
+    __syncthreads();
+    int acc = incl - sum;
+    for (int w = 0; w < wv; ++w) acc += wtot[w];
+    for (int j = t * per; j < (t + 1) * per && j < nk; ++j) {
+      segl[j] = acc;
+      acc += dh[j];
+    }
+    if (t == kDeltaThreads - 1) segl[nk] = acc;
+    __syncthreads();
+    if (blockIdx.x == 0)
+      for (int j = t; j <= nk; j += kDeltaThreads) seg[j] = segl[j];
+  }
   const long long i0 = (long long)blockIdx.x * pcap, i1 = i0 + wg_count[blockIdx.x];
   for (long long i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     atomicAdd(lh + labels[rows[i]], 1);
     atomicAdd(lh + k + old[i], 1);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = lh[i] ? atomicAdd(cursor + i, lh[i]) : 0;
+  for (int i = threadIdx.x; i < 2 * k; i += blockDim.x) lh[i] = lh[i] ? segl[i] + atomicAdd(cursor + i, lh[i]) : 0;
   __syncthreads();
   for (long long i = i0 + threadIdx.x; i < i1; i += blockDim.x) {
     const int row = rows[i];
@@ -1457,16 +1476,26 @@ __global__ __launch_bounds__(kDeltaThreads) void kmeans_delta_scatter(const int*
 
 // acc[c] += S[c] - S[k+c] (sums), counts from the segment sizes, cost from the assign partials;
 // on full steps only the cost. Then msg = acc (the buffer that is all-reduced).
+// With slots (the delta path): the segmented pass left its cross-slice partials there instead of adding them
+// into dsum (no seg_fixup launch): each element adds its two segments' partials here, the same additions.
 __global__ void kmeans_delta_apply(double* __restrict__ acc, const double* __restrict__ dsum,
                                    const int* __restrict__ seg, const int* __restrict__ mode, int k, int D,
-                                   const double* __restrict__ cost_part, int ncost, double* __restrict__ msg) {
+                                   const double* __restrict__ cost_part, int ncost, double* __restrict__ msg,
+                                   const double* __restrict__ slots, const int* __restrict__ slot_c, long long nseg,
+                                   long long nwaves) {
   const long long kd = (long long)k * D;
   const long long idx = (long long)blockIdx.x * blockDim.x + threadIdx.x;
   const bool delta = mode[0] == 0;
   if (idx < kd) {
     double v = acc[idx];
     if (delta) {
-      v += dsum[idx] - dsum[kd + idx];
+      double a = dsum[idx], b = dsum[kd + idx];
+      if (slots != nullptr) {
+        const int c = (int)(idx / D), d = (int)(idx - (long long)c * D);
+        a += seg_fix(seg, 2 * k, D, nseg, nwaves, slots, slot_c, c, d);
+        b += seg_fix(seg, 2 * k, D, nseg, nwaves, slots, slot_c, k + c, d);
+      }
+      v += a - b;
       acc[idx] = v;
     }
     msg[idx] = v;
@@ -1595,7 +1624,7 @@ int launch_priv(const u16* X, long long n, long long ldx, const int* labels, int
 // bound of the filled positions (the kernels clamp to seg[k]).
 int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, const int* perm, const int* seg, int k,
                   int cpl, int seg_grid, double* msg, double* slots, int* slot_c, int xfp8, const int* gate, int want,
-                  hipStream_t st, SegUB sub = SegUB{nullptr, 0, nullptr, 0.0}) {
+                  hipStream_t st, SegUB sub = SegUB{nullptr, 0, nullptr, 0.0}, bool fixup = true) {
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
 #define CML_SEG_L(C, F, U, Q)                                                                                       \
   hipLaunchKernelGGL((kmeans_segacc<C, F, U, Q>), dim3(seg_grid), dim3(kSegThreads), 0, st, X, n, ldx, Dp, D, perm, \
@@ -1620,7 +1649,7 @@ int launch_segsum(const void* X, long long n, long long ldx, int Dp, int D, cons
 #undef CML_SEG
 #undef CML_SEG_L
   const int e = cml_status();
-  if (e) return e;
+  if (e || !fixup) return e;
   hipLaunchKernelGGL(kmeans_seg_fixup, dim3(k), dim3(256), 0, st, seg, k, D, n, waves, slots, slot_c, msg, gate,
                      want);
   return cml_status();
@@ -1897,21 +1926,20 @@ CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, 
   hipStream_t st = (hipStream_t)stream;
   const size_t lh = sizeof(int) * 2 * (size_t)k;
   hipLaunchKernelGGL(kmeans_delta_hist, dim3(nblk), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
-                     chg_wg_count, pcap, mode, k, dh);
-  hipLaunchKernelGGL(kmeans_delta_scan, dim3(1), dim3(256), 0, st, dh, mode, k, dseg, cursor);
-  hipLaunchKernelGGL(kmeans_delta_scatter, dim3(nblk), dim3(kDeltaThreads), lh, st, chg_rows, chg_old, labels,
-                     chg_wg_count, pcap, mode, k, cursor, dperm);
-  hipLaunchKernelGGL(zero_f64_gated, dim3(256), dim3(256), 0, st, dsum, 2LL * k * D, mode, 0);
+                     chg_wg_count, pcap, mode, k, dh, dsum, 2LL * k * D, cursor);
+  hipLaunchKernelGGL(kmeans_delta_scatter, dim3(nblk), dim3(kDeltaThreads), lh + sizeof(int) * (2 * (size_t)k + 1), st,
+                     chg_rows, chg_old, labels, chg_wg_count, pcap, mode, k, cursor, dperm, dh, dseg);
   int e = cml_status();
   if (e) return e;
-  if (cap > 0) {
+  if (cap > 0) {  // (the cross-slice partials are added by the apply below: no fixup launch)
     e = launch_segsum(X, 2LL * cap, ldx, Dp, D, dperm, dseg, 2 * k, cpl, seg_grid, dsum, slots, slot_c, xfp8, mode, 0,
-                      st, SegUB{nullptr, 0, nullptr, qscale});
+                      st, SegUB{nullptr, 0, nullptr, qscale}, false);
     if (e) return e;
   }
   const long long total = (long long)k * D + k + 1;
+  const long long waves = (long long)seg_grid * (kSegThreads / 64);
   hipLaunchKernelGGL(kmeans_delta_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, acc, dsum, dseg,
-                     mode, k, D, cost_part, ncost, msg);
+                     mode, k, D, cost_part, ncost, msg, cap > 0 ? slots : nullptr, slot_c, 2LL * cap, waves);
   return cml_status();
 }
 
