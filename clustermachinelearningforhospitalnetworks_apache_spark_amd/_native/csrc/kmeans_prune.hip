@@ -594,21 +594,39 @@ __device__ void centre_stats2_body(const double* __restrict__ cn, double* __rest
       else if (v > b) { b = v; }
     }
   }
-  if (act) {
-    smax[tid] = m;
-    d1[tid] = a;
-    d2[tid] = b;
-    i1[tid] = ia;
+  // max norm and top-2 drifts (+ index of the largest, lowest index on ties) by wave butterflies, then the four
+  // wave results (a thread-0 loop over 256 partials was most of this single-workgroup launch)
+  auto merge = [](float& pa, float& pb, int& pi, float qa, float qb, int qi) {
+    if (qa > pa || (qa == pa && qi < pi)) {
+      pb = qb > pa ? qb : pa;
+      pa = qa;
+      pi = qi;
+    } else {
+      pb = pb > qa ? pb : qa;
+    }
+  };
+#pragma unroll
+  for (int o = 32; o > 0; o >>= 1) {
+    const double om = __shfl_xor(m, o, 64);
+    const float oa = __shfl_xor(a, o, 64), ob = __shfl_xor(b, o, 64);
+    const int oi = __shfl_xor(ia, o, 64);
+    m = om > m ? om : m;
+    merge(a, b, ia, oa, ob, oi);
+  }
+  if (act && (tid & 63) == 0) {
+    smax[tid >> 6] = m;
+    d1[tid >> 6] = a;
+    d2[tid >> 6] = b;
+    i1[tid >> 6] = ia;
   }
   __syncthreads();
   if (tid == 0) {
-    double mm = 0.0;
-    float ta = -1.f, tb = -1.f;
-    int ti = 0;
-    for (int t = 0; t < 256; ++t) {
+    double mm = smax[0];
+    float ta = d1[0], tb = d2[0];
+    int ti = i1[0];
+    for (int t = 1; t < 4; ++t) {
       mm = smax[t] > mm ? smax[t] : mm;
-      if (d1[t] > ta) { tb = ta > d2[t] ? ta : d2[t]; ta = d1[t]; ti = i1[t]; }
-      else { const float c = d1[t]; tb = c > tb ? c : tb; }
+      merge(ta, tb, ti, d1[t], d2[t], i1[t]);
     }
     smax[0] = mm;
     *mc = (float)mm;
