@@ -83,7 +83,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_row_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, ctypes.c_float, c_vp, c_vp, c_vp,
                                     c_vp, c_vp, c_vp, c_vp]),
     "cml_int_hist": (c_int, [c_vp, c_ll, c_int, c_vp, c_vp]),
-    "cml_kmeans_cost_combine": (c_int, [c_vp, c_vp, c_int, c_ll, c_int, c_int, c_dbl, c_vp, c_int, c_vp, c_vp]),
+    "cml_kmeans_cost_combine": (c_int, [c_vp, c_vp, c_int, c_ll, c_int, c_int, c_dbl, c_vp, c_int, c_vp, c_vp, c_vp]),
     "cml_kmeans_init_merge": (c_int, [c_vp, c_vp, c_vp, c_vp, c_int, c_ll, c_vp]),
     "cml_sum_f32_f64_parts": (c_int, []),
     "cml_kmeans_cost_parts": (c_int, []),
@@ -254,8 +254,8 @@ def cost_combine(q: torch.Tensor, msgs: torch.Tensor, k: int, d: int, unit: floa
                  stream=None) -> torch.Tensor:
     """Σ_j q_j - 2 c_j·(S_j·unit) + n_j |c_j|², clamped at 0 (f64 device scalar): the training cost of an
     assignment from its per-cluster sums (msgs [rows, >= k*d + k]: S then n), the f64 per-cluster Σ||x||²
-    ``q`` and the bf16 centres ``cb`` it compared against. Device tensors: one single-workgroup kernel; host
-    tensors: the same formula in torch."""
+    ``q`` and the bf16 centres ``cb`` it compared against. Device tensors: a per-centre term launch and a
+    fixed-order sum (kmeans_init.hip); host tensors: the same formula in torch."""
     kd = k * d
     if not q.is_cuda or cb.dtype != torch.bfloat16:  # (host engines; centres of another dtype)
         s_ = msgs[:, :kd].sum(0).view(k, d) * unit
@@ -266,11 +266,12 @@ def cost_combine(q: torch.Tensor, msgs: torch.Tensor, k: int, d: int, unit: floa
             or msgs.dim() != 2 or msgs.shape[1] < kd + k or msgs.stride(1) != 1 or cb.stride(1) != 1
             or cb.shape[0] < k or cb.shape[1] < d or not q.is_contiguous()):
         raise ValueError("cost_combine: f64 q [k], f64 msgs [rows, >= k*d + k], centres [>= k, >= d]")
-    out = torch.empty(1, dtype=torch.float64, device=q.device)
+    buf = torch.empty(k + 1, dtype=torch.float64, device=q.device)  # [k] per-centre terms, then the total
     _native.check(_native.kernels().cml_kmeans_cost_combine(
         q.data_ptr(), msgs.data_ptr(), int(msgs.shape[0]), int(msgs.stride(0)), int(k), int(d), float(unit),
-        cb.data_ptr(), int(cb.stride(0)), out.data_ptr(), _native.stream_ptr(stream)), "kmeans_cost_combine")
-    return out[0]
+        cb.data_ptr(), int(cb.stride(0)), buf.data_ptr(), buf[k:].data_ptr(), _native.stream_ptr(stream)),
+        "kmeans_cost_combine")
+    return buf[k]
 
 
 _STOP = threading.local()  # per-thread pinned stop-flag word of local_kmeans (allocated once)
