@@ -602,25 +602,31 @@ __global__ __launch_bounds__(kThreads) void local_empty_kernel(const double* __r
                                                                double* __restrict__ C, double* __restrict__ CT,
                                                                int* __restrict__ picks, const int* __restrict__ stop) {
   if (stop != nullptr && *stop != 0) return;
-  __shared__ int nsh;
-  const int tid = threadIdx.x;
-  if (tid == 0) {
-    unsigned long long cc = *ctr;
-    int ne = 0;
-    for (int j = 0; j < k; ++j) {
-      if (!(cnt[j] > 0.0)) {
-        int q = (int)__dmul_rn(cu(cc++, key), (double)m);
-        q = q < m - 1 ? q : m - 1;
-        picks[2 * ne] = j;
-        picks[2 * ne + 1] = q;
-        ++ne;
-      }
+  // the empty clusters in index order take consecutive counter draws: a ballot scan over 256 clusters at a
+  // time gives each its rank (the same draws as one thread walking the clusters, which took ~20 us)
+  __shared__ int wcnt[kThreads / 64];
+  const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+  const unsigned long long cc0 = *ctr;
+  int ne = 0;  // empties so far (uniform)
+  for (int j0 = 0; j0 < k; j0 += kThreads) {
+    const int j = j0 + tid;
+    const bool empty = j < k && !(cnt[j] > 0.0);
+    const unsigned long long b = __ballot(empty);
+    if (lane == 0) wcnt[wv] = (int)__popcll(b);
+    __syncthreads();
+    int off = ne;
+    for (int w = 0; w < wv; ++w) off += wcnt[w];
+    if (empty) {
+      const int e = off + (int)__popcll(b & ((1ull << lane) - 1ull));
+      int q = (int)__dmul_rn(cu(cc0 + (unsigned long long)e, key), (double)m);
+      q = q < m - 1 ? q : m - 1;
+      picks[2 * e] = j;
+      picks[2 * e + 1] = q;
     }
-    *ctr = cc;
-    nsh = ne;
+    for (int w = 0; w < kThreads / 64; ++w) ne += wcnt[w];
+    __syncthreads();  // wcnt reused; picks visible to the whole workgroup
   }
-  __syncthreads();
-  const int ne = nsh;
+  if (tid == 0) *ctr = cc0 + (unsigned long long)ne;
   for (int e = 0; e < ne; ++e) {
     const int j = picks[2 * e], q = picks[2 * e + 1];
     for (int t = tid; t < d; t += kThreads) {
@@ -789,11 +795,22 @@ __global__ __launch_bounds__(kThreads) void int_hist_kernel(const int* __restric
     for (int i = threadIdx.x; i < m; i += kThreads) hist[i] = 0;
     __syncthreads();
   }
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const int v = vals[i];
-    if (v >= 0 && v < m) {
-      if (lds) atomicAdd(&hist[v], 1);
-      else atomicAdd(&counts[v], 1);
+  // tiles of 16 values per thread: the 16 loads of a tile are issued before its atomics (one memory round
+  // trip per tile; a load-then-atomic loop waited for every value in turn: 69 us for 12.5M labels)
+  constexpr int U = 16;
+  for (long long t0 = (long long)blockIdx.x * kThreads * U; t0 < n; t0 += (long long)gridDim.x * kThreads * U) {
+    int v[U];
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      const long long i = t0 + (long long)u * kThreads + threadIdx.x;
+      v[u] = i < n ? vals[i] : -1;
+    }
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+      if (v[u] >= 0 && v[u] < m) {
+        if (lds) atomicAdd(&hist[v[u]], 1);
+        else atomicAdd(&counts[v[u]], 1);
+      }
     }
   }
   if (lds) {
