@@ -135,8 +135,11 @@ class KMeans(Estimator):
         # trainingCost is the last iteration's cost (Spark computes it while training: here from the f64
         # sums and norms the engine holds, no pass over X); clusterSizes: one pruned assign against the
         # final centres, its counts and their all-reduce are enqueued here on every rank (no host read),
-        # so reading the summary later is no collective and the engine is released when fit returns
-        sizes = eng.cluster_sizes_async()
+        # so reading the summary later is no collective and the engine is released when fit returns. The cost
+        # is enqueued first: the final assignment then updates the engine's own labels and bounds in place
+        # (consume=True: nothing steps this engine again)
+        _ = eng.last_cost
+        sizes = eng.cluster_sizes_async(consume=True)
         model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(), sizes))
         return model
 

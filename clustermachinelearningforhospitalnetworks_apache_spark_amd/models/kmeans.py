@@ -552,6 +552,8 @@ class LloydEngine:
     # ------------------------------------------------------------------ iteration
     def step(self) -> None:
         """One Lloyd iteration over the global dataset (all ranks participate)."""
+        if getattr(self, "_consumed", False):
+            raise RuntimeError("LloydEngine: the fit's final assignment consumed this engine's step state")
         self._ensure_norms()
         self._sum_grid()
         if (self.delta is not None and self.refresh_interval and self.iterations
@@ -1694,7 +1696,7 @@ class LloydEngine:
         return stop if stop is not None else it
 
     # ------------------------------------------------------------------ prediction / cost
-    def final_labels(self) -> torch.Tensor:
+    def final_labels(self, in_place: bool = False) -> torch.Tensor:
         """Labels of every local row against the current (final) centres — what ``transform`` with the
         fitted model predicts (Spark's summary.clusterSizes counts these). After device pruned steps this is
         one pruned assign: the bounds pass against the last update's drifts lists the rows the bounds no
@@ -1718,10 +1720,20 @@ class LloydEngine:
         if not (self._pdev and n):
             return self.assign()[0]
         st, ap = self._pst, self.aplan
-        lab, ub, lb = self.labels.clone(), st.ub.clone(), st.lb.clone()
-        pad, i32 = st.cand.shape[0], torch.int32
-        cand, cand_lab, cand_xn, count, flags, pmode = K.zeros_block(self.device, [
-            (pad, i32), (pad, i32), (pad, torch.float32), (1, i32), (2, i32), (2, i32)])
+        if in_place:
+            # the fit's last use of this engine (cluster_sizes_async(consume=True)): the pass updates the step's
+            # own labels, bounds and candidate lists instead of copies (at 100M rows the three copies moved
+            # 2.4 GB); the engine is marked consumed, so no later step runs on the now mismatched state
+            self._consumed = True
+            lab, ub, lb = self.labels, st.ub, st.lb
+            cand, cand_lab, cand_xn, count = st.cand, st.cand_lab, st.cand_xn, st.count
+            flags, pmode = K.zeros_block(self.device, [(2, torch.int32), (2, torch.int32)])
+            count.zero_()
+        else:
+            lab, ub, lb = self.labels.clone(), st.ub.clone(), st.lb.clone()
+            pad, i32 = st.cand.shape[0], torch.int32
+            cand, cand_lab, cand_xn, count, flags, pmode = K.zeros_block(self.device, [
+                (pad, i32), (pad, i32), (pad, torch.float32), (1, i32), (2, i32), (2, i32)])
         K.prune_bounds(lab, ub, lb, st.drift, st.dmax, st.thr, st.c2, k, cand, count, xn=self.xnorm, cand_lab=cand_lab,
                        cand_xn=cand_xn, zero_count=False, cum=st.cum)
         K.prune_gate(count, st.cap_m, flags, pmode)
@@ -1735,7 +1747,7 @@ class LloydEngine:
         """Global row count of every cluster under the final centres (a collective)."""
         return self.cluster_sizes_async()()
 
-    def cluster_sizes_async(self):
+    def cluster_sizes_async(self, consume: bool = False):
         """Enqueue the final-centre counts of every cluster and their all-reduce (no host read) and return
         a zero-argument reader of the result. Every rank calls this together (at the end of ``fit``);
         the reader itself is no collective — one rank alone may read it — and it holds only the k-long
@@ -1743,7 +1755,7 @@ class LloydEngine:
         summary.clusterSizes)`` and kept every per-row buffer of the fit alive)."""
         k, n = self.k, self.n
         if n and self.device.type == "cuda":
-            lab = self.final_labels()
+            lab = self.final_labels(in_place=consume)
             cnt = torch.zeros(k, dtype=torch.int32, device=self.device)
             K.int_hist(lab.to(torch.int32).contiguous(), n, k, cnt)  # integer counts: no bincount host sync
             sizes = cnt.to(torch.int64)

@@ -60,6 +60,13 @@ def test_cluster_sizes_from_pruned_final_assign(n, d, k):
     want = torch.bincount(full.long(), minlength=k).tolist()
     assert eng.cluster_sizes() == want
     eng.step()  # the engine steps on normally after the read
+    # the fit's own last use consumes the step state in place: same sizes, and the engine refuses to step on
+    cost_before = eng.last_cost
+    want2 = torch.bincount(eng.assign()[0].long(), minlength=k).tolist()
+    assert eng.cluster_sizes_async(consume=True)() == want2
+    assert torch.equal(eng.last_cost, cost_before)
+    with pytest.raises(RuntimeError, match="consumed"):
+        eng.step()
 
 
 def test_estimator_fit_lazy_sizes_and_offset_cost():
