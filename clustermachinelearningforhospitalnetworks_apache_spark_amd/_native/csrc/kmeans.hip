@@ -1257,24 +1257,25 @@ __device__ __forceinline__ double seg_fix(const int* __restrict__ seg, int k, in
   long long w1 = (s1 - 1) / chunk;
   if (w1 >= nwaves) w1 = nwaves - 1;
   double t = 0.0;
-  long long w = w0;
-  // 8 slices per round, loads issued together (a cluster can span thousands of slices)
-  for (; w + 8 <= w1 + 1; w += 8) {
+  // 8 slices per round, loads issued together (a cluster can span thousands of slices); the last round is
+  // predicated rather than walked one slice at a time (a segment typically spans ~8 slices: the walk paid one
+  // memory round trip per slice). The sums are exact (grid integers / bf16 values in f64), so the grouping of
+  // the additions does not change them.
+  for (long long w = w0; w <= w1; w += 8) {
     double v[8];
 #pragma unroll
     for (int q = 0; q < 8; ++q) {
       const long long ww = w + q;
-      const int ca = slot_c[2 * ww], cb = slot_c[2 * ww + 1];
-      const double a = slots[(2 * ww) * (long long)D + d], b = slots[(2 * ww + 1) * (long long)D + d];
-      v[q] = ca == c ? a : 0.0;
-      v[q] = cb == c ? v[q] + b : v[q];
+      v[q] = 0.0;
+      if (ww <= w1) {
+        const int ca = slot_c[2 * ww], cb = slot_c[2 * ww + 1];
+        const double a = slots[(2 * ww) * (long long)D + d], b = slots[(2 * ww + 1) * (long long)D + d];
+        v[q] = ca == c ? a : 0.0;
+        v[q] = cb == c ? v[q] + b : v[q];
+      }
     }
 #pragma unroll
     for (int q = 0; q < 8; ++q) t += v[q];
-  }
-  for (; w <= w1; ++w) {
-    if (slot_c[2 * w] == c) t += slots[(2 * w) * (long long)D + d];
-    if (slot_c[2 * w + 1] == c) t += slots[(2 * w + 1) * (long long)D + d];
   }
   return t;
 }
@@ -1915,6 +1916,13 @@ CML_API int cml_kmeans_delta_gate(const int* chg_wg_count, int nblk, int cap, in
   return cml_status();
 }
 
+int g_delta_fused_fixup = 1;  // cml_kmeans_set_delta_fused_fixup (A/B knob)
+CML_API int cml_kmeans_set_delta_fused_fixup(int on) {
+  const int prev = g_delta_fused_fixup;
+  if (on >= 0) g_delta_fused_fixup = on;
+  return prev;
+}
+
 // dseg: 2k+1 ints, cursor: 2k ints, dperm: 2*cap ints, dsum: 2k*D doubles; slots/slot_c sized for
 // seg_grid (cml_kmeans_seg_slot_*); acc/msg: k*D + k + 1 doubles.
 CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, const int* labels, const int* chg_rows,
@@ -1931,15 +1939,18 @@ CML_API int cml_kmeans_delta_accum(const void* X, long long ldx, int Dp, int D, 
                      chg_rows, chg_old, labels, chg_wg_count, pcap, mode, k, cursor, dperm, dh, dseg);
   int e = cml_status();
   if (e) return e;
-  if (cap > 0) {  // (the cross-slice partials are added by the apply below: no fixup launch)
+  // the cross-slice partials: added by the apply (per element, seg_fix) instead of a fixup launch (one
+  // workgroup per key); CML_DELTA_FUSED_FIXUP=0 keeps the launch (A/B: profiles/r5/README.md)
+  const bool fused = g_delta_fused_fixup != 0;
+  if (cap > 0) {
     e = launch_segsum(X, 2LL * cap, ldx, Dp, D, dperm, dseg, 2 * k, cpl, seg_grid, dsum, slots, slot_c, xfp8, mode, 0,
-                      st, SegUB{nullptr, 0, nullptr, qscale}, false);
+                      st, SegUB{nullptr, 0, nullptr, qscale}, !fused);
     if (e) return e;
   }
   const long long total = (long long)k * D + k + 1;
   const long long waves = (long long)seg_grid * (kSegThreads / 64);
   hipLaunchKernelGGL(kmeans_delta_apply, dim3((unsigned)((total + 255) / 256)), dim3(256), 0, st, acc, dsum, dseg,
-                     mode, k, D, cost_part, ncost, msg, cap > 0 ? slots : nullptr, slot_c, 2LL * cap, waves);
+                     mode, k, D, cost_part, ncost, msg, (cap > 0 && fused) ? slots : nullptr, slot_c, 2LL * cap, waves);
   return cml_status();
 }
 

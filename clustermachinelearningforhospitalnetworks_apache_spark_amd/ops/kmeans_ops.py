@@ -35,6 +35,7 @@ _native.register_kernel_sigs({
     "cml_kmeans_set_rr_debug": (c_int, [c_int]),
     "cml_kmeans_set_rr_m32": (c_int, [c_int]),
     "cml_kmeans_set_fp8_mx": (c_int, [c_int]),
+    "cml_kmeans_set_delta_fused_fixup": (c_int, [c_int]),
     "cml_kmeans_assign_tile_rows": (c_int, [c_int]),
     "cml_row_sqnorm_bf16": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
     "cml_row_sqnorm_fp8": (c_int, [c_vp, c_ll, c_ll, c_int, c_vp, c_vp]),
@@ -413,6 +414,9 @@ def _apply_env_knobs(lib) -> None:
         _native.check(lib.cml_kmeans_set_rr_m32(int(m32)), "set_rr_m32")
     if os.environ.get("CML_KMEANS_FP8_MX") == "0":
         lib.cml_kmeans_set_fp8_mx(0)
+    fx = os.environ.get("CML_DELTA_FUSED_FIXUP")
+    if fx:  # incremental sums: cross-slice partials added by the apply instead of a fixup launch (A/B)
+        lib.cml_kmeans_set_delta_fused_fixup(int(fx))
 
 
 def plan_assign(n: int, dp: int, k: int, device_index: int = 0, fp8: bool = False) -> AssignPlan:
