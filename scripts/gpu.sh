@@ -76,6 +76,8 @@ profile)
     || { tail -20 "$O/run.log"; exit 1; }
   tail -1 "$O/run.log" | cut -c1-400
   python3 scripts/rocpd_stats.py /tmp/pf/pf_results.db --top 50 > "$O/kernel_stats.txt"
+  python3 scripts/rocpd_stats.py /tmp/pf/pf_results.db --marker row_pass_kernel --index 1 --top 40 \
+    > "$O/kernel_stats_timed_fit.txt"
   head -30 "$O/kernel_stats.txt"
   ;;
 shard)
