@@ -275,3 +275,24 @@ def test_screen_three_ranks_with_an_empty_one_match_single_rank(tmp_path):
         np.testing.assert_array_equal(np.asarray(res[r]["centers"]), np.asarray(ref["centers"]))
         assert res[r]["it"] == ref["it"] and res[r]["sizes"] == ref["sizes"]
         assert abs(res[r]["cost"] - ref["cost"]) <= 1e-12 * abs(ref["cost"])
+
+
+def test_bench_two_rank_launch_on_one_gpu():
+    """The driver's N > 1 bench launch (torch.distributed.run, one rank per device) with both ranks on cuda:0 and
+    gloo collectives (RCCL needs a device per rank): the GPU shards, the multi-rank fit and the one-line JSON
+    contract (n_gpus = 2, dp2, whole-job value)."""
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ, CML_COMM_BACKEND="gloo", PYTHONPATH=root)
+    out = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+                          "--master-addr", "127.0.0.1", "--master-port", str(29700 + os.getpid() % 200),
+                          os.path.join(root, "bench.py"), "--gpus", "2", "--steps", "3", "--warmup", "1",
+                          "--rows", "2000000", "--no-overlap"],
+                         capture_output=True, text=True, env=env, timeout=110, cwd=root)
+    assert out.returncode == 0, out.stderr[-3000:]
+    lines = [ln for ln in out.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, out.stdout[-2000:]
+    res = json.loads(lines[0])
+    assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["dtype"] == "bf16"
+    assert res["steps"] == 3 and res["value"] > 0 and res["extra"]["iterations"] == 3
