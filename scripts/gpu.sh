@@ -13,6 +13,7 @@
 #   strong                strong-scaling emulation: per-rank shards of the headline (100M / N rows)
 #   workflow              the reference workflow end to end on 4M uploaded rows (examples/)
 #   ovtl                  2-rank gloo timeline of the seeded step's overlapped accumulate (rocprofv3 per rank)
+#   clock                 K9r clock / MFMA busy share, rows from HBM vs from L2 (one rocprofv3 --pmc pass)
 #   mb SCRIPT [args]      a microbenchmark script (scripts/mb_*.py ...) -> SCRIPT.log
 #
 # Every GPU step runs under its own `timeout -k 10`; steps are chained so a failure ends the job.
@@ -136,6 +137,15 @@ ovtl)
   [ $S0 -eq 0 ] && [ $S1 -eq 0 ] || { tail -20 "$O/r0.log" "$O/r1.log"; exit 1; }
   python3 scripts/overlap_timeline.py show /tmp/ov0/r0_results.db /tmp/ov1/r1_results.db > "$O/timeline.txt"
   head -80 "$O/timeline.txt"
+  ;;
+clock)
+  # K9r clock and MFMA busy share with rows from HBM vs from L2 (one PMC pass, kernel trace only)
+  R=$PWD
+  (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
+    --kernel-trace -d /tmp/ck -o ck --output-format csv -- python3 "$R/scripts/mb_k9r_clock.py") > "$O/run.log" 2>&1 \
+    || { tail -20 "$O/run.log"; exit 1; }
+  python3 scripts/mb_k9r_clock.py show /tmp/ck > "$O/clock.txt"
+  cat "$O/clock.txt"
   ;;
 mb)
   S=${1:?script}
