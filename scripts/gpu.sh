@@ -14,6 +14,7 @@
 #   workflow              the reference workflow end to end on 4M uploaded rows (examples/)
 #   ovtl                  2-rank gloo timeline of the seeded step's overlapped accumulate (rocprofv3 per rank)
 #   clock                 K9r clock / MFMA busy share, rows from HBM vs from L2 (one rocprofv3 --pmc pass)
+#   drivers               every scripts/mb_*.py subcommand once at a small size, prof.py on a fresh trace
 #   mb SCRIPT [args]      a microbenchmark script (scripts/mb_*.py ...) -> SCRIPT.log
 #
 # Every GPU step runs under its own `timeout -k 10`; steps are chained so a failure ends the job.
@@ -76,8 +77,8 @@ profile)
   timeout -k 10 900 rocprofv3 --kernel-trace --stats -d /tmp/pf -o pf -- python3 bench.py "$@" > "$O/run.log" 2>&1 \
     || { tail -20 "$O/run.log"; exit 1; }
   tail -1 "$O/run.log" | cut -c1-400
-  python3 scripts/rocpd_stats.py /tmp/pf/pf_results.db --top 50 > "$O/kernel_stats.txt"
-  python3 scripts/rocpd_stats.py /tmp/pf/pf_results.db --marker row_pass_kernel --index 1 --top 40 \
+  python3 scripts/prof.py stats /tmp/pf/pf_results.db --top 50 > "$O/kernel_stats.txt"
+  python3 scripts/prof.py stats /tmp/pf/pf_results.db --marker row_pass_kernel --index 1 --top 40 \
     > "$O/kernel_stats_timed_fit.txt"
   head -30 "$O/kernel_stats.txt"
   ;;
@@ -88,10 +89,10 @@ shard)
   fit_line "$O/shard.json"
   timeout -k 10 300 rocprofv3 --kernel-trace --runtime-trace --marker-trace -d /tmp/sh -o sh -- python3 bench.py \
     --rows 12500000 --warmup 3 --no-overlap "$@" > "$O/sh.log" 2>&1 || { tail -5 "$O/sh.log"; exit 1; }
-  python3 scripts/rocpd_timeline.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --gap-apis 80 --gap-detail 250 \
+  python3 scripts/prof.py timeline /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --gap-apis 80 --gap-detail 250 \
     > "$O/timeline.txt"
-  python3 scripts/rocpd_stats.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --top 40 > "$O/stats.txt"
-  python3 scripts/rocpd_syncs.py /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --show 5 > "$O/syncs.txt"
+  python3 scripts/prof.py stats /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --top 40 > "$O/stats.txt"
+  python3 scripts/prof.py syncs /tmp/sh/sh_results.db --marker row_pass_kernel --index 1 --show 5 > "$O/syncs.txt"
   timeout -k 10 300 python3 scripts/sync_audit.py --rows 2000000 > "$O/sync_audit.txt" 2>&1 \
     || { tail -20 "$O/sync_audit.txt"; exit 1; }
   head -3 "$O/syncs.txt"
@@ -142,10 +143,49 @@ clock)
   # K9r clock and MFMA busy share with rows from HBM vs from L2 (one PMC pass, kernel trace only)
   R=$PWD
   (cd /tmp && timeout -s KILL 120 rocprofv3 --pmc GRBM_GUI_ACTIVE SQ_BUSY_CYCLES SQ_VALU_MFMA_BUSY_CYCLES \
-    --kernel-trace -d /tmp/ck -o ck --output-format csv -- python3 "$R/scripts/mb_k9r_clock.py") > "$O/run.log" 2>&1 \
+    --kernel-trace -d /tmp/ck -o ck --output-format csv -- python3 "$R/scripts/mb_k9r.py" clock) > "$O/run.log" 2>&1 \
     || { tail -20 "$O/run.log"; exit 1; }
-  python3 scripts/mb_k9r_clock.py show /tmp/ck > "$O/clock.txt"
+  python3 scripts/mb_k9r.py clock-show /tmp/ck > "$O/clock.txt"
   cat "$O/clock.txt"
+  ;;
+drivers)
+  # every microbenchmark / trace-reader subcommand once at a small size (a smoke test of the scripts themselves)
+  R=$PWD
+  M="timeout -k 10 180 python3 -u scripts/mb_k9r.py"
+  $M rr 2000000 256 256 0,8 > $O/rr.log 2>&1 && tail -4 $O/rr.log &&
+  $M dbg 2000000 > $O/dbg.log 2>&1 && tail -3 $O/dbg.log &&
+  $M modes 2000000 > $O/modes.log 2>&1 && tail -3 $O/modes.log &&
+  $M pmc-mode 2000000 256 256 1 > $O/pm.log 2>&1 && tail -1 $O/pm.log &&
+  $M sched 2000000 0,1 > $O/sched.log 2>&1 && tail -3 $O/sched.log &&
+  $M ablate 0 8 > $O/ablate.log 2>&1 && tail -3 $O/ablate.log &&
+  (cd /tmp && timeout -k 10 180 rocprofv3 --kernel-trace -d /tmp/drv -o p -- python3 "$R/scripts/mb_k9r.py" pmc 8 2000000) > $O/prof.log 2>&1 &&
+  python3 scripts/prof.py stats /tmp/drv/p_results.db --top 5 > $O/stats.txt && cat $O/stats.txt &&
+  bash scripts/gpu.sh clock "${O#gpurun_out/}/clock" &&
+  K="timeout -k 10 180 python3 -u scripts/mb_kmeans.py"
+  $K accum --scale 0.02 > $O/accum.log 2>&1 && tail -2 $O/accum.log &&
+  $K segacc --rows 2000000 > $O/segacc.log 2>&1 && tail -2 $O/segacc.log &&
+  $K overlap --rows 2000000 > $O/overlap.log 2>&1 && tail -1 $O/overlap.log &&
+  $K rowpass --rows 4000000 > $O/rowpass.log 2>&1 && tail -1 $O/rowpass.log &&
+  $K prune --rows 2000000 --steps 2 --warmup 1 > $O/prune.log 2>&1 && grep untraced $O/prune.log &&
+  $K bounds --rows 2000000 > $O/bounds.log 2>&1 && tail -2 $O/bounds.log &&
+  $K churn --rows 1000000 --iters 3 > $O/churn.log 2>&1 && tail -1 $O/churn.log &&
+  $K graph --rows 1000000 --steps 3 > $O/graph.log 2>&1 && tail -1 $O/graph.log &&
+  $K cert --rows 500000 --reps 1 > $O/cert.log 2>&1 && tail -1 $O/cert.log &&
+  $K fp8-mx --rows 1000000 --steps 2 > $O/fp8mx.log 2>&1 && tail -1 $O/fp8mx.log &&
+  $K host --rows 500000 --iters 3 --top 5 > $O/host.log 2>&1 && head -1 $O/host.log &&
+  L="timeout -k 10 180 python3 -u scripts/mb_ml.py"
+  $L glm --scale 0.02 > $O/glm.log 2>&1 && tail -1 $O/glm.log &&
+  $L glm-fp8 --rows 1000000 > $O/glmfp8.log 2>&1 && tail -1 $O/glmfp8.log &&
+  $L logreg --scale 0.02 > $O/logreg.log 2>&1 && tail -1 $O/logreg.log &&
+  $L trees --scale 0.02 > $O/trees.log 2>&1 && tail -1 $O/trees.log &&
+  $L tree-transform --rows 100000 > $O/tt.log 2>&1 && tail -1 $O/tt.log &&
+  Q="timeout -k 10 180 python3 -u scripts/mb_sql.py"
+  $Q frame --rows 4000000 --reps 2 > $O/frame.log 2>&1 && tail -2 $O/frame.log | cut -c1-200 &&
+  $Q groupby --rows 1000000 > $O/groupby.log 2>&1 && tail -2 $O/groupby.log | cut -c1-200 &&
+  $Q relational --rows 1000000 --host-rows 20000 > $O/rel.log 2>&1 && tail -1 $O/rel.log | cut -c1-200 &&
+  $Q window --rows 1000000 --host-rows 20000 > $O/win.log 2>&1 && tail -1 $O/win.log &&
+  $Q dropna --rows 100000 --reps 1 --dir /tmp/mbd > $O/dropna.log 2>&1 && tail -1 $O/dropna.log &&
+  echo ALL_OK
   ;;
 mb)
   S=${1:?script}
