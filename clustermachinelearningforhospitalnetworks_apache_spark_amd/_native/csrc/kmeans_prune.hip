@@ -25,11 +25,14 @@
 namespace {
 
 constexpr int kThreads = 256;
-constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block (16384 for the bounds pass)
-// The bounds pass runs 1024-thread workgroups: each takes one slot of the candidate list with a device-scope
+constexpr int kIters = 4;  // 4 x 4 rows per lane: 4096 rows per block (8192 for the bounds pass)
+// The bounds pass runs 512-thread workgroups: each takes one slot of the candidate list with a device-scope
 // atomic on ONE counter (and one completion atomic for the folded gate), and those same-address atomics
 // serialise at the L2 — with 256-thread workgroups (4096 rows each) they bounded the pass at ~2-3 TB/s.
-constexpr int kBoundsThreads = 1024;
+// 1024-thread workgroups went the other way: at 78 VGPRs (6 waves per SIMD) only one fits a CU, so 100M rows
+// ran in three rounds of 256 blocks with a ragged tail; 512 threads fit three per CU (same-box A/B,
+// profiles/r5/ab_bounds_wg: 346 -> 300 us per 100M-row pass, headline fit -0.7 ms, 12.5M-row shard unchanged).
+constexpr int kBoundsThreads = 512;
 
 // Offset form (cum != null): the stored values are us = ub - cu[a] and ls = lb + cl[a] against the
 // per-centre cumulative drifts cu[j] = Σ drift_j and cl[j] = Σ (largest drift of a centre other than
