@@ -1119,9 +1119,11 @@ __global__ __launch_bounds__(256) void init_classify_kernel(const float* __restr
 // classify kernel, so no per-row lookups) and keeps the nearest of its relevant new candidates (a
 // prefix of p's sorted table row, at most LMAX). Lane sl of a group loads entry sl of the table row
 // with the X slice; a ballot gives every group's relevant count; candidate l's index comes from lane
-// g*16 + l by ds_bpermute, and the Y slices of 4 candidates are loaded together — the pass was
+// g*16 + l by ds_bpermute, and the Y slices of 2 candidates are loaded together — the pass was
 // latency-bound on dependent loads (list -> row state -> table -> each candidate), now a row costs
-// three memory round trips for up to 4 relevant candidates.
+// three memory round trips for up to 2 relevant candidates. Batches of 4 held 74 VGPRs (6 waves per SIMD);
+// batches of 2 hold 56 (8 waves), and the extra waves hide more than the extra round trips cost (same-box
+// A/B, profiles/r5/ab_near_list: 10.67 -> 10.14 ms for the headline's two launches).
 // Strict improvement over the current cost moves the row; ties among the new candidates go to the
 // lowest index (K9r's argmin rule). A 16-lane sum is 4 DPP steps (no row broadcasts), and the f32
 // math is on packed pairs, so a (row, candidate) pair costs ~a dozen vector instructions.
@@ -1135,7 +1137,7 @@ __global__ __launch_bounds__(256) void init_near_list_kernel(const void* __restr
   typedef float f2 __attribute__((ext_vector_type(2)));
   constexpr int XB = F8 ? NCOL : 2 * NCOL;  // bytes of this lane's X slice
   constexpr int YQ = (2 * NCOL) / 16;       // uint4s of this lane's Y slice
-  constexpr int CB = 4;                     // candidates loaded together
+  constexpr int CB = 2;                     // candidates loaded together
   static_assert(XB % 16 == 0 && (2 * NCOL) % 16 == 0, "16-B slices");
   static_assert(LMAX <= 16 && LMAX % CB == 0, "one table entry per lane of a 16-lane group");
   const unsigned char* xb = reinterpret_cast<const unsigned char*>(X);
