@@ -13,8 +13,11 @@ incremental f64 sums, RCCL all-reduce of the [k·D sums | k counts | cost] messa
 --warmup runs an untimed warm-up fit of that many iterations first. The same fit driven on the
 LloydEngine directly, the steady-state step and a forced full step are reported in extra (not the
 headline), and with --data blobs (the headline) also a fit on overlapping blobs (extra.overlap), where
-the bounds prune little. The dataset is fixed (100M rows total) and sharded over the N ranks, so
-scaling is *strong*. Data: synthetic Gaussian blobs generated on the GPU, bf16 features (no network).
+the bounds prune little. The dataset is ONE fixed table (100M rows total) sharded over the N ranks in
+row order, so scaling is *strong*: every value is generated from its global row index (utils/synth.py),
+and the fit is partition-invariant, so N = 1, 2, 4, 8 fit the same problem and report the same
+trainingCost bits and cluster sizes (extra.training_cost_hex / cluster_sizes_digest). Data: synthetic
+Gaussian blobs generated on the GPU, bf16 features (no network).
 
 Usage (driver contract):
     python bench.py --gpus 1 --steps 20 --warmup 3
@@ -33,6 +36,7 @@ import torch
 
 from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
 from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils.synth import shard_range
 
 METRIC = "KMeans fit samples/sec (whole node), 100M×256 k=256 at 1/2/4/8 MI355X"
 BASELINE_VALUE = None  # the reference publishes no number
@@ -41,22 +45,48 @@ BASELINE_VALUE = None  # the reference publishes no number
 _DATA = {"blobs": 4.0, "overlap": 0.5, "uniform": None}
 
 
-def make_blobs(n: int, d: int, k_true: int, seed: int, device, dtype=torch.bfloat16, chunk: int = 1 << 22,
-               spread=4.0):
-    """n rows of k_true Gaussian blobs (centres randn·spread, unit noise), or U(-2, 2) rows (spread None)."""
-    g = torch.Generator(device=device)
-    g.manual_seed(1234)  # identical blob centres on every rank
-    centers = torch.randn((k_true, d), generator=g, device=device) * (spread or 0.0)
-    g.manual_seed(seed)
-    x = torch.empty((n, d), dtype=dtype, device=device)
-    for s in range(0, n, chunk):
-        m = min(chunk, n - s)
-        if spread is None:
-            x[s:s + m] = (torch.rand((m, d), generator=g, device=device) * 4.0 - 2.0).to(dtype)
-            continue
-        lab = torch.randint(0, k_true, (m,), generator=g, device=device)
-        x[s:s + m] = (centers[lab] + torch.randn((m, d), generator=g, device=device)).to(dtype)
-    return x
+def make_blobs(n: int, d: int, k_true: int, seed: int, device, dtype=torch.bfloat16, spread=4.0, row0: int = 0):
+    """Rows row0 .. row0 + n - 1 of ONE fixed table of k_true Gaussian blobs (centres N(0, spread²), unit noise;
+    U(-2, 2) rows when spread is None). Every value is a pure function of (seed, global row, column)
+    (utils/synth.py, synth.hip), so rank r of W generating its shard writes exactly those rows of the W = 1
+    table: the 1/2/4/8-GPU runs fit the same 100M rows."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
+    centers = None
+    if spread is not None:  # rows 0 .. k_true - 1 of the centre table: identical on every rank
+        centers = synth.synth_rows(0, k_true, d, seed=1234, stream=1, device=device) * spread
+    gdt = dtype if dtype in (torch.bfloat16, torch.float32) or not torch.device(device).type == "cuda" else torch.float32
+    x = synth.synth_rows(row0, n, d, seed=seed, stream=0, centres=centers,
+                         mode="uniform" if spread is None else "normal", dtype=gdt, device=device)
+    return x if x.dtype == dtype else x.to(dtype)
+
+
+def _col_dot(z: torch.Tensor, w: torch.Tensor) -> torch.Tensor:
+    """z @ w in f64, accumulated column by column (elementwise ops: each row's bits do not depend on how many
+    rows the chunk holds, unlike a GEMV whose reduction tiling follows the shape)."""
+    acc = torch.zeros(z.shape[0], dtype=torch.float64, device=z.device)
+    for j, wj in enumerate(w.to(torch.float64).cpu().tolist()):
+        acc.add_(z[:, j].to(torch.float64), alpha=wj)
+    return acc
+
+
+_T0 = time.time()
+try:  # the phase log counts from the process start (import torch included)
+    import psutil
+    _T0 = psutil.Process().create_time()
+except Exception:  # noqa: BLE001
+    pass
+
+
+def _digest(sizes) -> str:
+    """Short digest of a cluster-size list (the labels histogram; equal across rank counts for one problem)."""
+    import hashlib
+    return hashlib.sha256(",".join(str(int(v)) for v in sizes).encode()).hexdigest()[:16]
+
+
+def _phase(comm, what: str) -> None:
+    """Timestamped phase line on rank 0's stderr (where a run's wall time goes: VERDICT r5 weak 9)."""
+    if comm is None or comm.rank == 0:
+        print(f"[bench +{time.time() - _T0:7.2f}s] {what}", file=sys.stderr, flush=True)
 
 
 def _drop_norm_cache(x: torch.Tensor) -> None:
@@ -180,25 +210,34 @@ def main():
     rank, W = comm.rank, comm.world_size
     dev = comm.device
 
-    per = args.rows // W
-    n_local = per + (1 if rank < args.rows - per * W else 0)
+    # this rank's rows of the ONE fixed table: [r0, r1) of args.rows, generated by global row index, so every N
+    # fits the same problem (strong scaling; the fit is partition-invariant bit for bit: tests/test_bench_invariance)
+    r0, r1 = shard_range(args.rows, rank, W)
+    n_local = r1 - r0
+    _phase(comm, f"session up (rank 0 of {W}); generating rows [{r0}, {r1})")
     t0 = time.perf_counter()
-    x = make_blobs(n_local, args.dim, args.k, seed=1000 + rank, device=dev, dtype=fdt, spread=_DATA[args.data])
+    x = make_blobs(n_local, args.dim, args.k, seed=1000, device=dev, dtype=fdt, spread=_DATA[args.data], row0=r0)
     if gpu:
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
     df = spark.createDataFrameFromTensors({"features": x})
 
     # untimed warm-up fit: code objects, allocator pools, RCCL channels (its results are discarded)
+    _phase(comm, f"data ready ({gen_s:.2f} s); warm-up fit")
     if args.warmup > 0:
         api_fit(df, args, seed=7, iters=args.warmup)
         _drop_norm_cache(x)
 
     # the timed region: one whole public-API fit from scratch, bracketed by barrier + device sync
+    _phase(comm, "timed fit")
     model, elapsed = _timed(comm, gpu, lambda: api_fit(df, args, seed=42, iters=args.steps))
+    _phase(comm, f"timed fit done ({1000 * elapsed:.1f} ms); engine / step measurements")
     summ = model.summary
+    sizes = summ.clusterSizes
     acc = {"api": f"KMeans(k={args.k}, maxIter={args.steps}, tol={args.tol:g}, seed=42).fit(df)",
-           "iterations": summ.numIter, "training_cost": summ.trainingCost}
+           "iterations": summ.numIter, "training_cost": summ.trainingCost,
+           "training_cost_hex": float(summ.trainingCost).hex(), "cluster_sizes_digest": _digest(sizes),
+           "cluster_sizes_minmax": [min(sizes), max(sizes)]}
     del model, summ
     _drop_norm_cache(x)
 
@@ -237,13 +276,15 @@ def main():
         # the same public-API fit on overlapping blobs (centres 8x closer), where the exact bounds prune
         # little: the robustness of the headline. Same shape, separate data.
         del df
-        x2 = make_blobs(n_local, args.dim, args.k, seed=2000 + rank, device=dev, spread=_DATA["overlap"])
+        _phase(comm, "overlap-data fits")
+        x2 = make_blobs(n_local, args.dim, args.k, seed=2000, device=dev, spread=_DATA["overlap"], row0=r0)
         df2 = spark.createDataFrameFromTensors({"features": x2})
         api_fit(df2, args, seed=7, iters=max(1, args.warmup))
         _drop_norm_cache(x2)
         m2, el2 = _timed(comm, gpu, lambda: api_fit(df2, args, seed=42, iters=args.steps))
         ov = {"fit_ms": round(1000.0 * el2, 3), "samples_per_s": args.rows * args.steps / el2,
-              "iterations": m2.summary.numIter}
+              "iterations": m2.summary.numIter, "training_cost_hex": float(m2.summary.trainingCost).hex(),
+              "cluster_sizes_digest": _digest(m2.summary.clusterSizes)}
         del m2
         _drop_norm_cache(x2)
         e2, _, _ = kmeans_fit(x2, args, comm, seed=42, iters=args.steps)
@@ -284,6 +325,7 @@ def main():
                       "device": torch.cuda.get_device_name(dev) if gpu else "cpu", **acc},
         }
         print(json.dumps(out), flush=True)
+    _phase(comm, "done")
     spark.stop()
 
 
@@ -352,24 +394,26 @@ def bench_logreg(args):
     comm = Communicator.from_env(want_gpu=gpu)
     rank, W = comm.rank, comm.world_size
     dev = comm.device
-    per = args.rows // W
-    n = per + (1 if rank < args.rows - per * W else 0)
+    # this rank's rows [r0, r1) of one fixed 100M-row table, generated by global row index (utils/synth.py)
+    r0, r1 = shard_range(args.rows, rank, W)
+    n = r1 - r0
     d = args.dim
     t0 = time.perf_counter()
-    g = torch.Generator(device=dev)
-    g.manual_seed(99)
-    w_true = torch.randn(d, generator=g, device=dev) / d ** 0.5
-    scale = torch.rand(d, generator=g, device=dev) * 3 + 0.5
-    g.manual_seed(2000 + rank)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
+    gp = synth.synth_rows(0, 2, d, seed=99, stream=1, device=dev, mode="uniform")  # global parameters
+    w_true = gp[0] * (0.5 * 3 ** 0.5 / d ** 0.5)  # U(-2, 2)·sqrt(3)/2: unit variance, / sqrt(d)
+    scale = (gp[1] + 2.0) * 0.75 + 0.5  # U(0.5, 3.5)
     dt = torch.bfloat16 if gpu else torch.float64
     x = torch.empty((n, d), dtype=dt, device=dev)
     y = torch.empty(n, dtype=torch.float64, device=dev)
     for s0 in range(0, n, 1 << 22):
         m = min(1 << 22, n - s0)
-        xb = torch.randn((m, d), generator=g, device=dev) * scale
-        x[s0:s0 + m] = xb.to(dt)
-        logit = (xb / scale) @ w_true + 0.3 * torch.randn(m, generator=g, device=dev)
+        z = synth.synth_rows(r0 + s0, m, d, seed=2000, stream=0, device=dev)
+        e = synth.synth_rows(r0 + s0, m, 1, seed=2000, stream=2, device=dev)[:, 0]
+        x[s0:s0 + m] = (z * scale).to(dt)
+        logit = _col_dot(z, w_true) + 0.3 * e.to(torch.float64)
         y[s0:s0 + m] = (logit > 0).to(torch.float64)
+        del z, e
     if gpu:
         torch.cuda.synchronize()
     gen_s = time.perf_counter() - t0
@@ -553,21 +597,21 @@ def bench_pipeline(args):
     rank, W = comm.rank, comm.world_size
     dev = spark._device
     t0 = time.perf_counter()
-    g = torch.Generator(device=dev)
-    g.manual_seed(7)
-    centers = torch.randn((32, d), generator=g, device=dev) * 3
-    spread = torch.rand(d, generator=g, device=dev) * 4 + 0.25
-    offset = torch.randn(d, generator=g, device=dev) * 10
-    w_true = torch.randn(d, generator=g, device=dev) / d ** 0.5
-    g.manual_seed(5000 + rank)
+    # weak scaling: rank r holds global rows [r·n, (r + 1)·n) of one table generated by global row index
+    # (utils/synth.py): the rows of the N-GPU run are the first N·n rows of one fixed dataset
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
+    centers = synth.synth_rows(0, 32, d, seed=7, stream=1, device=dev) * 3
+    gp = synth.synth_rows(0, 3, d, seed=7, stream=2, device=dev)
+    spread = (synth.synth_rows(3, 1, d, seed=7, stream=2, device=dev, mode="uniform")[0] + 2.0) + 0.25  # U(.25, 4.25)
+    offset = gp[0] * 10
+    w_true = gp[1] / d ** 0.5
     raw = torch.empty((n, d), dtype=torch.bfloat16 if gpu else torch.float64, device=dev)
     y = torch.empty(n, dtype=torch.float64, device=dev)
     for s0 in range(0, n, 1 << 22):
         m = min(1 << 22, n - s0)
-        z = centers[torch.randint(0, 32, (m,), generator=g, device=dev)] + torch.randn((m, d), generator=g,
-                                                                                         device=dev)
+        z = synth.synth_rows(rank * n + s0, m, d, seed=5000, stream=0, centres=centers, device=dev)
         raw[s0:s0 + m] = (z * spread + offset).to(raw.dtype)
-        y[s0:s0 + m] = ((z @ w_true) > 0).to(torch.float64)
+        y[s0:s0 + m] = (_col_dot(z, w_true) > 0).to(torch.float64)
         del z
     df = spark.createDataFrameFromTensors({"raw": raw, "label": y})
     del raw, y

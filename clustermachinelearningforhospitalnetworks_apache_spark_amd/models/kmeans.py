@@ -1328,14 +1328,42 @@ class LloydEngine:
         is that of the values the centres were computed from.)"""
         k, d, n = self.k, self.d, self.n
         cb = self._pst.cb_cost if self._pdev else self._cb_cost
-        if n:
-            # (engine labels are always in [0, k): no range check, no host read)
-            q = group_reduce(self.labels[:n], self._norms64()[:n], k, "sum",
-                             ids_in_range=True).to(torch.float64).contiguous()
+        if k <= 4096:
+            # Q_j as integer limbs on the grid of the global max ||x||² (exactsum.hip): they add exactly, so Q —
+            # and the cost — are the same bits for any split of the rows over ranks (the scaling curve fits one
+            # problem at every N; an f64 all-reduce of per-rank sums rounded once per rank)
+            bound = self._xmax_dev()
+            limbs = torch.zeros(2 * k, dtype=torch.int64, device=self.device)
+            if n:
+                lab = self.labels[:n]
+                lab = lab if lab.dtype == torch.int32 and lab.is_contiguous() else lab.to(torch.int32).contiguous()
+                K.fixsum(self._norms64()[:n], n, bound, 1.0, lab=lab, k=k, limbs=limbs)
+            self.comm.allreduce_(limbs)
+            q = K.fixsum_finalize(limbs, k, bound, 1.0)
         else:
-            q = torch.zeros(k, dtype=torch.float64, device=self.device)
-        self.comm.allreduce_(q)
+            if n:
+                # (engine labels are always in [0, k): no range check, no host read)
+                q = group_reduce(self.labels[:n], self._norms64()[:n], k, "sum",
+                                 ids_in_range=True).to(torch.float64).contiguous()
+            else:
+                q = torch.zeros(k, dtype=torch.float64, device=self.device)
+            self.comm.allreduce_(q)
         return K.cost_combine(q, self.msgs, k, d, self._unit, cb)
+
+    def _xmax_dev(self) -> torch.Tensor:
+        """Device f32 max ||x||² over every rank: the grid bound of the partition-invariant sums (K.fixsum).
+        The device pruned step keeps it (st.mx); other engines reduce it once (the norms are fixed)."""
+        self._ensure_norms()
+        if self._pdev:
+            return self._pst.mx
+        mx = getattr(self, "_gxmax", None)
+        if mx is None:
+            mx = (self._xnorm[: self.n].max().reshape(1) if self.n
+                  else torch.zeros(1, dtype=torch.float32, device=self.device))
+            if self.comm.is_distributed:
+                self.comm.allreduce_(mx, op="max")
+            self._gxmax = mx
+        return mx
 
     def _exact_cost(self) -> torch.Tensor:
         """Cost of the last step's assignment (Spark's per-iteration cost) on the device rows: one exact
@@ -1935,6 +1963,7 @@ class LloydEngine:
         cands[0].copy_(g[torch.argmin(g[:, 0]), 2:])
         c0 = cands[0:1]
         costs, nearest = self._init_first_pass(c0)
+        xmax = self._xmax_dev()
         ncand = 1
         two_k = self._const([0.0, 2.0 * k], torch.float64)
         out = torch.empty(cap, dtype=torch.int32, device=dev)
@@ -1945,10 +1974,15 @@ class LloydEngine:
             tr = trace(f"kinit.round{step}")
             tr.__enter__()
             # Σcost over every rank and the rate 2k / Σcost stay on the device (the sample kernel forms it)
+            # (Σcost as integer limbs on the grid of 5·max||x||² — a row's squared distance to a candidate row is at
+            # most 4·max||x||², plus the bf16 / MX rounding of the candidate — so the rate is the same bits for
+            # any split of the rows over ranks: exactsum.hip)
             scale = two_k.clone()
+            limbs = torch.zeros(2, dtype=torch.int64, device=dev)
             if n:
-                scale[0:1].copy_(K.sum_f64(costs, n).reshape(1))
-            comm.allreduce_(scale[0:1])
+                K.fixsum(costs, n, xmax, 5.0, limbs=limbs)
+            comm.allreduce_(limbs)
+            K.fixsum_finalize(limbs, 1, xmax, 5.0, out=scale[0:1])
             cnt.zero_()
             if cands.shape[0] < ncand + (cap if send is None else 0):
                 cands = self._grow_cands(cands, ncand, ncand + cap)

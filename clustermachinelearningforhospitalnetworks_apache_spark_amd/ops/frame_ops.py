@@ -33,6 +33,7 @@ _native.register_kernel_sigs({
     "cml_col_absmax": (c_int, [c_vp, c_int, c_ll, c_int, c_ll, c_int, c_vp, c_vp]),
     "cml_quant_fp8": (c_int, [c_vp, c_int, c_ll, c_int, c_ll, c_vp, c_vp, c_ll, c_vp]),
     "cml_has_nan": (c_int, [c_vp, c_ll, c_int, c_ll, c_int, c_vp, c_vp]),
+    "cml_synth_rows": (c_int, [c_ll, c_ll, c_int, c_ll, c_vp, c_int, c_ull, c_ull, c_int, c_vp, c_int, c_vp, c_vp]),
 })
 
 
@@ -64,6 +65,24 @@ def _u64(k: int) -> int:
 
 def _st(stream) -> int:
     return _native.stream_ptr(stream)
+
+
+# ------------------------------------------------------------------------------ synthetic rows
+def synth_rows(row0: int, n: int, d: int, ld: int, centres: Optional[torch.Tensor], kt: int, key: int, key_lab: int,
+               mode: int, out: torch.Tensor, labels: Optional[torch.Tensor] = None, stream=None) -> None:
+    """out[i, :d] = centres[label(row0 + i)] + noise(row0 + i, j), zeros past d (synth.hip; utils/synth.py)."""
+    _dev(out, "synth_rows")
+    if out.dtype not in (torch.bfloat16, torch.float32) or not out.is_contiguous() or out.shape[0] < n \
+            or out.shape[1] != ld or out.data_ptr() % 16:
+        raise ValueError("synth_rows: a contiguous 16-byte aligned [n, ld] bf16 / f32 output")
+    if centres is not None and (centres.dtype != torch.float32 or not centres.is_contiguous()
+                                or tuple(centres.shape) != (kt, d)):
+        raise ValueError("synth_rows: centres must be contiguous f32 [kt, d]")
+    if labels is not None and (labels.dtype != torch.int32 or labels.numel() < n):
+        raise ValueError("synth_rows: int32 labels [n]")
+    _native.check(_native.kernels().cml_synth_rows(
+        int(row0), int(n), int(d), int(ld), _native.ptr(centres), int(kt), _u64(key), _u64(key_lab), int(mode),
+        out.data_ptr(), 0 if out.dtype == torch.bfloat16 else 1, _native.ptr(labels), _st(stream)), "synth_rows")
 
 
 # ------------------------------------------------------------------------------------ K5 / K22

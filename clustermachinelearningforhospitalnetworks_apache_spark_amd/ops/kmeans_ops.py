@@ -90,6 +90,8 @@ _native.register_kernel_sigs({
     "cml_kmeans_cost_parts": (c_int, []),
     "cml_kmeans_cost_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_sum_f32_f64": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
+    "cml_fixsum": (c_int, [c_vp, c_int, c_vp, c_ll, c_int, c_vp, ctypes.c_float, c_vp, c_vp]),
+    "cml_fixsum_finalize": (c_int, [c_vp, c_int, c_vp, ctypes.c_float, c_vp, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,
                                        c_vp, c_vp]),
     "cml_local_kpp": (c_int, [c_vp, c_vp, c_int, c_int, c_vp, c_int, ctypes.c_uint64, c_vp, c_vp, c_vp, c_vp,
@@ -227,6 +229,38 @@ def init_sample(cost: torch.Tensor, ids: torch.Tensor, n: int, key: int, scale, 
         cost.data_ptr(), ids.data_ptr(), int(n), _u64(key), 0.0 if dev_scale else float(scale), out.data_ptr(),
         count.data_ptr(), int(out.shape[0]), scale.data_ptr() if dev_scale else 0, _native.stream_ptr(stream)),
         "kmeans_init_sample")
+
+
+def fixsum(v: torch.Tensor, n: int, bound: torch.Tensor, mul: float = 1.0, lab: torch.Tensor | None = None,
+           k: int = 1, limbs: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """Partition-invariant sum(s) of values 0 <= v <= bound·mul (exactsum.hip): the int64 limbs [2k] of Σ v (per
+    label with ``lab``) on the grid of the device f32 ``bound`` — every rank must pass the same bound. The limbs
+    add exactly, so they are all-reduced (sum) as is and ``fixsum_finalize`` turns them into f64 sums that are
+    the same bits for any split of the rows over ranks."""
+    if not v.is_cuda or v.dtype not in (torch.float32, torch.float64) or not v.is_contiguous():
+        raise ValueError("fixsum: a contiguous f32 / f64 device vector")
+    if bound.dtype != torch.float32 or not bound.is_cuda:
+        raise ValueError("fixsum: the bound is a device f32 scalar")
+    if lab is not None and (lab.dtype != torch.int32 or not lab.is_contiguous() or lab.numel() < n):
+        raise ValueError("fixsum: int32 labels [n]")
+    if lab is None and k != 1:
+        raise ValueError("fixsum: k > 1 needs labels")
+    if limbs is None:
+        limbs = torch.zeros(2 * k, dtype=torch.int64, device=v.device)
+    _native.check(_native.kernels().cml_fixsum(v.data_ptr(), 1 if v.dtype == torch.float32 else 2, _native.ptr(lab),
+                                               int(n), int(k), bound.data_ptr(), float(mul), limbs.data_ptr(),
+                                               _native.stream_ptr(stream)), "fixsum")
+    return limbs
+
+
+def fixsum_finalize(limbs: torch.Tensor, k: int, bound: torch.Tensor, mul: float = 1.0,
+                    out: torch.Tensor | None = None, stream=None) -> torch.Tensor:
+    """f64 [k] sums from (all-reduced) fixsum limbs, in a fixed order (the same bits on every rank)."""
+    if out is None:
+        out = torch.empty(k, dtype=torch.float64, device=limbs.device)
+    _native.check(_native.kernels().cml_fixsum_finalize(limbs.data_ptr(), int(k), bound.data_ptr(), float(mul),
+                                                        out.data_ptr(), _native.stream_ptr(stream)), "fixsum_finalize")
+    return out
 
 
 def int_hist(vals: torch.Tensor, n: int, m: int, counts: torch.Tensor, stream=None) -> None:
