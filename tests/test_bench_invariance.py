@@ -82,7 +82,7 @@ def test_synth_rows_kernel_matches_host_twin_and_shards():
     ref, lab_h = synth.synth_rows(0, n, d, seed=1, centres=c.cpu(), dtype=torch.float64, with_labels=True)
     assert torch.equal(lab.cpu(), lab_h)
     err = (whole[:, :d].cpu().double() - ref).abs()
-    assert float((err / (ref.abs() + 1e-3)).max()) <= 2.0 ** -8 + 1e-4
+    assert bool((err <= ref.abs() * 2.0 ** -8 + 1e-4).all())
 
 
 @pytest.mark.gpu
