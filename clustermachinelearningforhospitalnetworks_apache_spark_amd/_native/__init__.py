@@ -100,17 +100,107 @@ class Recorded:
 _recording = threading.local()
 
 
+class _TorchOpCounter:
+    """Counts the torch operations (other than views) run while a launch sequence is recorded: their effects
+    (a fill, a temporary's allocation, a host read) happen at record time only and are not replayed, so a
+    recording that saw one must not be cached."""
+
+    def __init__(self):
+        self.ops = []
+        self._mode = None
+
+    def __enter__(self):
+        from torch.utils._python_dispatch import TorchDispatchMode
+        counter = self
+
+        class _Mode(TorchDispatchMode):
+            def __torch_dispatch__(self, func, types, args=(), kwargs=None):
+                if not getattr(func, "is_view", False) and func not in _VIEW_LIKE:
+                    counter.ops.append(str(func))
+                return func(*args, **(kwargs or {}))
+
+        self._mode = _Mode()
+        self._mode.__enter__()
+        return self
+
+    def __exit__(self, *exc):
+        self._mode.__exit__(*exc)
+        return False
+
+
+_VIEW_LIKE = set()
+for _name in ("detach.default", "alias.default", "slice.Tensor", "select.int", "view.default", "as_strided.default"):
+    _pkt, _ov = _name.split(".")
+    _VIEW_LIKE.add(getattr(getattr(torch.ops.aten, _pkt), _ov))
+
+
 @contextlib.contextmanager
 def recording():
     """``with recording() as rec: <wrapper calls>``; then ``Recorded(rec.calls)`` replays them. Only for
-    wrappers whose sole effect is their kernel launches (their return values are not produced)."""
+    wrappers whose sole effect is their kernel launches (their return values are not produced). ``rec.torch_ops``
+    lists the torch operations that ran meanwhile (a recording with any is not replayable)."""
     rec = _Recorder(_real_kernels())
     prev = getattr(_recording, "rec", None)
     _recording.rec = rec
+    cnt = _TorchOpCounter()
     try:
-        yield rec
+        with cnt:
+            yield rec
     finally:
         _recording.rec = prev
+        rec.torch_ops = cnt.ops
+
+
+class ReplayGuard:
+    """When a recorded sequence may be replayed: it froze raw pointers (and the stream) at record time, so it is
+    valid only while every tensor behind its pointer arguments is still the one it was recorded with. The guard
+    finds, for each pointer argument, a tensor attribute of ``roots`` whose storage holds it (engine buffers,
+    step state) and keeps (holder, attribute, index, data_ptr); ``valid()`` re-reads those attributes (a few
+    microseconds) — a re-allocated buffer fails it and the caller records again. ``ok`` is False when the
+    recording cannot be replayed at all: a pointer that belongs to no root tensor (a temporary the wrappers
+    allocated, which would dangle), a torch operation during the recording, or a stream other than ``stream``."""
+
+    __slots__ = ("ok", "why", "watch")
+
+    def __init__(self, rec, roots, stream: int):
+        self.ok, self.why, self.watch = True, "", ()
+        if getattr(rec, "torch_ops", None):
+            self.ok, self.why = False, f"torch ops while recording: {rec.torch_ops[:4]}"
+            return
+        ptrs = set()
+        for _fn, conv, name in rec.calls:
+            for a in conv:
+                if isinstance(a, ctypes.c_void_p) and a.value:
+                    ptrs.add(a.value)
+        ptrs.discard(stream)
+        spans = []
+        for obj in roots:
+            if obj is None:
+                continue
+            for attr, v in vars(obj).items():
+                items = [(None, v)] if torch.is_tensor(v) else (
+                    list(enumerate(v)) if isinstance(v, (list, tuple)) else [])
+                for idx, t in items:
+                    if torch.is_tensor(t) and t.numel():
+                        stg = t.untyped_storage()
+                        spans.append((stg.data_ptr(), stg.data_ptr() + stg.nbytes(), obj, attr, idx, t.data_ptr()))
+        watch = {}
+        for p in ptrs:
+            hit = next((sp for sp in spans if sp[0] <= p < sp[1]), None)
+            if hit is None:
+                self.ok, self.why = False, f"pointer {p:#x} is no root tensor's (a temporary)"
+                return
+            watch[(id(hit[2]), hit[3], hit[4])] = hit[2:]
+        self.watch = tuple(watch.values())
+
+    def valid(self) -> bool:
+        for obj, attr, idx, ptr in self.watch:
+            v = getattr(obj, attr, None)
+            if idx is not None:
+                v = v[idx] if isinstance(v, (list, tuple)) and len(v) > idx else None
+            if not torch.is_tensor(v) or v.data_ptr() != ptr:
+                return False
+        return True
 
 
 def kernels():

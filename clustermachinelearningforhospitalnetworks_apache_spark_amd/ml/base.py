@@ -7,6 +7,7 @@ every micro-batch.
 """
 from __future__ import annotations
 
+import contextlib
 import copy
 from typing import Any, Dict, List, Optional, Union
 
@@ -31,13 +32,18 @@ class Transformer(Params, MLWritable, MLReadable):
 
 
 class Estimator(Params, MLWritable, MLReadable):
+    # leaf estimators pause the cycle collector over their hot loops; meta-estimators (Pipeline, CrossValidator,
+    # TrainValidationSplit, OneVsRest) do not, so it runs between their inner fits and reclaims an inner fit's
+    # engine buffers held in reference cycles before the next fold allocates its own
+    _pause_gc = True
+
     def fit(self, dataset, params: Optional[Union[Dict, List[Dict]]] = None):
         if isinstance(params, (list, tuple)):
             return [self.fit(dataset, p) for p in params]
         if dataset.isStreaming:
             raise RuntimeError("fit() on a streaming DataFrame: use writeStream.foreachBatch to train per batch")
         inst = self.copy(params) if params else self
-        with trace(f"{type(self).__name__}.fit"), gc_paused():
+        with trace(f"{type(self).__name__}.fit"), (gc_paused() if inst._pause_gc else contextlib.nullcontext()):
             model = inst._fit(dataset)
         if model is not None and getattr(model, "parent", None) is None:
             model.parent = inst

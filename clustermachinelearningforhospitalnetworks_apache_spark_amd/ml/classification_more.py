@@ -252,6 +252,7 @@ def _raw_confidence(model, df):
 class OneVsRest(Estimator):
     """Multiclass by k binary fits of ``classifier`` (class c vs the rest); prediction = argmax of the
     k positive-class confidences."""
+    _pause_gc = False  # meta-estimator: the collector runs between the inner fits (ml/base.py)
     _params = _OVR_PARAMS
 
     def __init__(self, **kwargs):

@@ -68,7 +68,8 @@ class VectorAssembler(Transformer):
                 # is lazy); the check is deferred to the first consumer (DataFrame._feature_matrix), and
                 # a consumer whose own pass over the rows already exposes a NaN takes it over for free
                 # (StandardScaler.fit: the moments) — no extra read of a 100+ GB matrix here
-                out = NanCheckedColumnData(x, None, T.VectorUDT(), getattr(cds[0], "nan_pending", None) or _NAN_MSG)
+                out = NanCheckedColumnData(x, None, T.VectorUDT(), getattr(cds[0], "nan_pending", None) or _NAN_MSG,
+                                           df._comm)
             return self._named(df, _replace_col(df, self.getOutputCol(), out))
         if df._device.type == "cuda" and cds and df._nrows:
             # K2: one fused pass gathers the typed columns into the row-major matrix + invalid flags

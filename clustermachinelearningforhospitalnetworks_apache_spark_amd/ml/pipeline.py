@@ -13,6 +13,7 @@ from .base import Estimator, Model, Transformer
 
 
 class Pipeline(Estimator):
+    _pause_gc = False  # meta-estimator: the collector runs between the inner fits (ml/base.py)
     _params = {"stages": ([], "a list of pipeline stages", None)}
 
     def __init__(self, stages: Optional[List] = None):

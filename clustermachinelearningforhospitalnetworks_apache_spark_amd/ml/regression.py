@@ -92,8 +92,10 @@ def solve_wls(G: np.ndarray, d: int, reg: float, alpha: float, fit_intercept: bo
         s = np.where(active, sigx, 1.0)
         Z = Cxx / np.outer(s, s)                    # covariance of standardized features
         zt = cxy / s / sy_                          # covariance with standardized label
-        l2 = reg * (1.0 - alpha)
-        l1 = reg * alpha
+        # Spark's WeightedLeastSquares penalises in the label-standardized space with effectiveRegParam =
+        # regParam / std(label) (pinned against sklearn Ridge / Lasso in tests/test_linreg_solvers.py)
+        l2 = reg / sy_ * (1.0 - alpha)
+        l1 = reg / sy_ * alpha
         # standardization=False penalises the original-scale coefficients: rescale per feature
         pen2 = np.full(d, l2) if standardization else l2 / (s * s)
         pen1 = np.full(d, l1) if standardization else l1 / s
@@ -211,7 +213,10 @@ class LinearRegression(Estimator):
             return model
         sy = rawsy if rawsy > 0 else abs(my)
         inv = np.where(sx > 0, 1.0 / np.where(sx > 0, sx, 1.0), 0.0)  # constant features get no weight
-        l2, l1 = reg * (1.0 - alpha), reg * alpha
+        # Spark LinearRegression (l-bfgs): squared error runs on label / std(label) with effectiveRegParam =
+        # regParam / std(label); huber keeps the raw label and regParam as given
+        eff = reg if loss == "huber" else reg / sy
+        l2, l1 = eff * (1.0 - alpha), eff * alpha
         std_pen = self.getStandardization()
         pen2 = np.full(d, l2) if std_pen else l2 * inv * inv
         pen1 = (np.full(d, l1) if std_pen else l1 * inv) if l1 > 0 else None

@@ -116,6 +116,7 @@ def _save_validator_model(inst, path: str, metrics_key: str, metrics: List[float
 class CrossValidator(Estimator, _ValidatorParams):
     """k-fold cross validation: for each param map, the mean metric over ``numFolds`` (train on
     k-1 folds, evaluate on the held-out one); the best map is refit on the whole dataset."""
+    _pause_gc = False  # meta-estimator: the collector runs between the inner fits (ml/base.py)
 
     _params = {
         "numFolds": (3, "number of folds for cross validation (>= 2)", int),
@@ -195,6 +196,7 @@ class CrossValidatorModel(Model, _ValidatorParams):
 
 class TrainValidationSplit(Estimator, _ValidatorParams):
     """One train/validation split (``trainRatio``) per param map; the best map is refit on all rows."""
+    _pause_gc = False  # meta-estimator: the collector runs between the inner fits (ml/base.py)
 
     _params = {
         "trainRatio": (0.75, "ratio between training set and validation set (>= 0, <= 1)", float),

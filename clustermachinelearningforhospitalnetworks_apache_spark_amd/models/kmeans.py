@@ -1084,6 +1084,7 @@ class LloydEngine:
         st.half_every = int(os.environ.get("CML_KMEANS_HALF_EVERY", "4"))
         # recorded launch sequences of the step variants (_pdev_pre / _pdev_post); None: always the wrappers
         st.replay = {} if os.environ.get("CML_KMEANS_REPLAY", "1") != "0" else None
+        st.replay_refused = None  # why a recording was not replayable (_replay), for tests and diagnostics
         # the gate's full-pass flag, stored by the device into pinned host memory and read by the host with no
         # synchronisation (a few steps stale): steps enqueue the full-accumulate launches while the device keeps
         # picking full passes (data the bounds do not prune: many label changes), lean steps otherwise
@@ -1119,16 +1120,33 @@ class LloydEngine:
         if self._replay_ok():
             # the launch sequence of this variant, recorded once (fixed buffers and scalars): replayed without
             # the Python wrappers — the shard's steps were bound by ~25 us of host time per launch
-            key = ("pre", lean)
-            seq = st.replay.get(key)
-            if seq is None:
-                with _native.recording() as rec:
-                    self._pdev_pre_launches(lean)
-                seq = st.replay[key] = _native.Recorded(rec.calls)
-            seq()
-            dl.host_forced = False  # what the recorded gate does on the host
-            return
+            if self._replay(("pre", lean), lambda: self._pdev_pre_launches(lean)):
+                dl.host_forced = False  # what the recorded gate does on the host
+                return
         self._pdev_pre_launches(lean)
+
+    def _replay(self, key, launches) -> bool:
+        """Replay the recorded launch sequence ``key`` of the current stream, recording it first (or again,
+        after a buffer it reads was re-allocated: _native.ReplayGuard). False — nothing ran, the caller runs
+        the wrappers — when the sequence cannot be recorded safely (temporaries or torch ops inside)."""
+        st = self._pst
+        stream = _native.stream_ptr(None)
+        k = (key, stream)  # the recording froze the stream: one per stream
+        ent = st.replay.get(k)
+        if ent is not None and ent[1].valid():
+            ent[0]()
+            return True
+        if ent is not None and not ent[1].ok:
+            return False
+        with _native.recording() as rec:
+            launches()
+        guard = _native.ReplayGuard(rec, (self, st, self.delta, self.aplan, self.cplan), stream)
+        st.replay[k] = (_native.Recorded(rec.calls), guard)
+        if not guard.ok:
+            st.replay_refused = guard.why
+            return False
+        st.replay[k][0]()
+        return True
 
     def _pdev_pre_launches(self, lean: bool) -> None:
         st, dl = self._pst, self.delta
@@ -1167,15 +1185,8 @@ class LloydEngine:
         in a tol > 0 fit, the device convergence latch (flags[1])."""
         st = self._pst
         exact = self.use_graph or st.half_every <= 1 or self.iterations % st.half_every == 0
-        if self._replay_ok() and not self.spherical and self.dp <= 2048:
-            key = ("post", exact, self._conv_lim)
-            seq = st.replay.get(key)
-            if seq is None:
-                with _native.recording() as rec:
-                    self._pdev_post_launches(exact)
-                seq = st.replay[key] = _native.Recorded(rec.calls)
-            seq()
-        else:
+        if not (self._replay_ok() and not self.spherical and self.dp <= 2048
+                and self._replay(("post", exact, self._conv_lim), lambda: self._pdev_post_launches(exact))):
             self._pdev_post_launches(exact)
         self._shift2 = self.shift2
         self._cost_fn = self._device_cost

@@ -89,6 +89,11 @@ class Communicator:
             owns = True
         c = cls(rank, world, device, dist.get_backend(), dist.group.WORLD, owns)
         c._self_group = self_group
+        if c.backend != "gloo":
+            # the gloo side group of the host-side control messages, created HERE, where every rank passes in the
+            # same order: dist.new_group is itself a collective, so creating it lazily at the first object
+            # collective deadlocked whenever that first use was rank-conditional
+            c._cpu_group = dist.new_group(backend="gloo")
         return c
 
     _self_group = False
@@ -108,6 +113,8 @@ class Communicator:
         if self.backend == "gloo":
             return self.group
         if self._cpu_group is None:
+            # (a communicator built around an existing RCCL group rather than by from_env: every rank must reach
+            # this first object collective together)
             self._cpu_group = dist.new_group(backend="gloo")
         return self._cpu_group
 

@@ -75,7 +75,7 @@ class ColumnData:
         """A row subset inherits a deferred NaN check (VectorAssembler handleInvalid="error")."""
         pend = getattr(self, "nan_pending", None)
         if pend:
-            return NanCheckedColumnData(out.values, out.valid, out.dtype, pend)
+            return NanCheckedColumnData(out.values, out.valid, out.dtype, pend, getattr(self, "_comm", None))
         return out
 
 
@@ -87,12 +87,17 @@ class NanCheckedColumnData(ColumnData):
     first (fits are collectives), and a consumer whose own pass exposes NaNs (StandardScaler's moments)
     takes the check over through ``_vals()`` and clears it."""
 
-    def __init__(self, values, valid, dtype, msg: str):
+    def __init__(self, values, valid, dtype, msg: str, comm=None):
         self._raw = values
         self.valid = valid
         self.dtype = dtype
         self.codes = None
         self.nan_pending = msg
+        # the session communicator: the check's verdict is agreed over every rank (ADVICE r5) — every consumer
+        # of a multi-rank frame (collect, toPandas, show, write, a fit) is itself a collective, so all ranks
+        # reach it together and fail together, instead of NaN-free ranks blocking in the consumer's
+        # collective until its timeout while a NaN rank has raised
+        self._comm = comm
 
     def _vals(self):
         return self._raw
@@ -115,6 +120,9 @@ class NanCheckedColumnData(ColumnData):
                     bad = bool(frame_ops.has_nan(x))
                 else:
                     bad = bool(torch.isnan(x).any().item())
+            comm = self._comm
+            if comm is not None and comm.is_distributed:
+                bad = comm.max_scalar(1.0 if bad else 0.0) > 0
             if bad:
                 raise ValueError(self.nan_pending)
             self.nan_pending = None

@@ -61,3 +61,25 @@ def test_huber_matches_sklearn():
     assert abs(m.scale - sk.scale_) < 1e-3 * sk.scale_
     with pytest.raises(ValueError):
         LinearRegression(loss="huber", solver="normal").fit(df)
+
+
+@pytest.mark.parametrize("solver", ["normal", "l-bfgs"])
+def test_regularized_fit_matches_sklearn(solver):
+    """regularized parity pinned against independent solvers. Spark's objective (regParam λ,
+    elasticNetParam α, standardization on) in the label's units is 1/(2n)·RSS + λα·|β_s|₁ + λ(1-α)/(2σ_y)·|β_s|²
+    over the coefficients β_s of the features scaled by their unbiased std (effectiveRegParam = λ / σ_y in
+    the label-standardized space): sklearn Lasso(alpha=λ) and Ridge(alpha=nλ/σ_y) on the scaled features."""
+    from sklearn.linear_model import Lasso, Ridge
+    df, X, y = _frame(n=3000, d=5, seed=4)
+    n = len(y)
+    sx, sy = X.std(0, ddof=1), y.std(ddof=1)
+    Z = X / sx
+    lam = 0.4
+    ridge = LinearRegression(solver=solver, regParam=lam, maxIter=1000, tol=1e-12).fit(df)
+    sk = Ridge(alpha=n * lam / sy, tol=1e-12).fit(Z, y)
+    np.testing.assert_allclose(ridge.coefficients.toArray(), sk.coef_ / sx, rtol=1e-5, atol=1e-6)
+    assert abs(ridge.intercept - sk.intercept_) < 1e-5 * max(1.0, abs(sk.intercept_))
+    lasso = LinearRegression(solver=solver, regParam=lam, elasticNetParam=1.0, maxIter=1000, tol=1e-12).fit(df)
+    sl = Lasso(alpha=lam, tol=1e-12, max_iter=100000).fit(Z, y)
+    np.testing.assert_allclose(lasso.coefficients.toArray(), sl.coef_ / sx, rtol=1e-4, atol=1e-5)
+    assert abs(lasso.intercept - sl.intercept_) < 1e-4 * max(1.0, abs(sl.intercept_))

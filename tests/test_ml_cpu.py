@@ -78,7 +78,8 @@ def test_ridge_and_lasso(hosp):
     Z = (X - mx) / sx
     t = (y - my) / sy
     n = len(y)
-    beta = np.linalg.solve(Z.T @ Z / n + lam * np.eye(4), Z.T @ t / n)
+    # Spark's effectiveRegParam = regParam / std(label) in the label-standardized space
+    beta = np.linalg.solve(Z.T @ Z / n + lam / sy * np.eye(4), Z.T @ t / n)
     np.testing.assert_allclose(m.coefficients.toArray(), beta * sy / sx, rtol=1e-6)
     l1 = LinearRegression(featuresCol="features", labelCol="length_of_stay", regParam=0.5,
                           elasticNetParam=1.0).fit(fd)
