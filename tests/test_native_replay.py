@@ -93,10 +93,11 @@ def test_replayed_steps_follow_the_stream_and_reallocated_buffers():
     dev = torch.device("cuda", 0)
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    c = torch.randn(48, 64, generator=g, device=dev) * 5
+    c = torch.randn(48, 128, generator=g, device=dev) * 5
     x = (c[torch.randint(0, 48, (300_000,), generator=g, device=dev)]
-         + torch.randn(300_000, 64, generator=g, device=dev)).to(torch.bfloat16)
+         + torch.randn(300_000, 128, generator=g, device=dev)).to(torch.bfloat16)
     ref = _engine_fit(x, 10)
+    assert ref._pdev
     st = ref._pst
     assert st.replay_refused is None, st.replay_refused
     assert st.replay and all(ent[1].ok for ent in st.replay.values())
