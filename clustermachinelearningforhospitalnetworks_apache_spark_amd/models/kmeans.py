@@ -1109,21 +1109,84 @@ class LloydEngine:
         writing new labels and top-2 bounds and logging label changes; the incremental sums move by
         the changed rows (exact f64 sums, as the full path); all-reduce; K11; centre statistics for
         the next step's bounds."""
-        self._pdev_pre()
-        self.comm.allreduce_async(self.msgs[0]).wait()
+        if not self._pdev_pre():
+            self.comm.allreduce_async(self.msgs[0]).wait()
         self._pdev_post()
 
-    def _pdev_pre(self) -> None:
-        """The device pruned step up to its all-reduce (bounds, gate, K9r passes, sums -> msg)."""
+    def _pdev_pre(self) -> bool:
+        """The device pruned step up to its all-reduce (bounds, gate, K9r passes, sums -> msg). True when the
+        step ran split (_pdev_pre_split), which all-reduces its own two messages into msgs[0]."""
         st, dl = self._pst, self.delta
-        lean = dl.lean_step() and not (st.fused and int(st.pm_host[0]) != 0)
+        hint_full = st.fused and int(st.pm_host[0]) != 0
+        if hint_full and dl.lean_step() and not torch.cuda.is_current_stream_capturing():
+            split = self._full_split(self.n)
+            if split is not None:
+                self._pdev_pre_split(split)
+                return True
+        lean = dl.lean_step() and not hint_full
         if self._replay_ok():
             # the launch sequence of this variant, recorded once (fixed buffers and scalars): replayed without
             # the Python wrappers — the shard's steps were bound by ~25 us of host time per launch
             if self._replay(("pre", lean), lambda: self._pdev_pre_launches(lean)):
                 dl.host_forced = False  # what the recorded gate does on the host
-                return
+                return False
         self._pdev_pre_launches(lean)
+        return False
+
+    def _full_split(self, n: int):
+        """Row halves of a full-pass step whose first half's all-reduce overlaps the second half's K9r pass
+        (_pdev_pre_split): multi-rank engines with at least CML_KMEANS_OVERLAP_ROWS local rows
+        (default 4M: a full pass is then >= ~1 ms, far above the extra launches). CML_KMEANS_SPLIT_FULL=1 also
+        splits one-rank engines (tests: the split step must give the one-pass bits); =0 never splits."""
+        force = os.environ.get("CML_KMEANS_SPLIT_FULL")
+        if force == "0" or (not self.comm.is_distributed and force != "1"):
+            return None
+        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))
+        if lim <= 0 or n < max(lim, 2 * self.aplan.round_rows):
+            return None
+        mid = min(n - 1, max(1, round_up(n // 2, 1024)))
+        return mid
+
+    def _pdev_pre_split(self, mid: int) -> None:
+        """A full-pass pruned step in two row chunks, its all-reduce overlapped with the distance GEMM (the north
+        star's "all-reduce overlapped with the next shard's distance GEMM"): the bounds pass and gate over every
+        row; chunk 0 = the K9r mode-1 pass over rows [0, mid) (or, when the gate picked candidates, the candidate
+        pass over every candidate) and its delta sums -> message A, whose all-reduce is enqueued at once; chunk 1
+        = the mode-1 pass over rows [mid, n) and its delta sums -> B = the sums' change since A; msgs[0] = A + B.
+        The sums are exact (_sum_grid), so A + B is the one-message step bit for bit on any rank count. Lean
+        (delta) sums only: taken when the host's lagged hint says the gate is picking full passes."""
+        st, dl, ap = self._pst, self.delta, self.aplan
+        n, k, dp = self.n, self.k, self.dp
+        x, lab, xn = self.x, self.labels, self.xnorm
+        if getattr(self, "_msgs_split", None) is None:
+            self._msgs_split = torch.zeros((3, self.msg_len), dtype=torch.float64, device=self.device)
+        A, B, loc = self._msgs_split[0], self._msgs_split[1], self._msgs_split[2]
+        K.prune_bounds_gated(lab[:n], st.ub, st.lb, st.drift, st.dmax, st.thr, st.c2, k, st.cand, st.count, xn,
+                             st.cand_lab, st.cand_xn, st.flags, st.cum, st.pmode, st.cap_m,
+                             st.backoff if st.nback > 0 else None, st.nback, st.ctr[0:1], mode_host=st.pm_host)
+        K.assign_rr_ext(1, x[:mid], mid, dp, self.cb, self.cnorm, ap, xn[:mid], lab[:mid], self.cost_part, st.ub[:mid],
+                        st.lb[:mid], st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum)
+        K.assign_rr_ext(2, x, st.cap_m, dp, self.cb, self.cnorm, ap, st.cand_xn, lab, self.cost_part, st.ub, st.lb,
+                        st.mc, st.tau, delta=dl, idx=st.cand, n_dev=st.count, lab_in=st.cand_lab, gate=st.pmode,
+                        want=0, cum=st.cum)
+        dl.gate(0, lean=True)
+        dl.accumulate(x, dp, lab, 0, self.cost_part, ap.grid, A, qscale=self._qscale)
+        loc.copy_(A)  # this rank's sums after chunk 0 (A is all-reduced in place)
+        h0 = self.comm.allreduce_async(A)
+        # chunk 1 — its K9r pass runs while A's all-reduce is in flight. (Its change lists start empty: a gated-off
+        # pass, when the gate picked candidates, leaves chunk 0's counts behind.)
+        dl.wg_count.zero_()
+        r = n - mid
+        K.assign_rr_ext(1, x[mid:], r, dp, self.cb, self.cnorm, ap, xn[mid:n], lab[mid:n], self.cost_part,
+                        st.ub[mid:n], st.lb[mid:n], st.mc, st.tau, delta=dl, gate=st.pmode, want=1, cum=st.cum)
+        dl.gate(0, lean=True)
+        dl.accumulate(x[mid:], dp, lab[mid:n], 0, self.cost_part, ap.grid, B, qscale=self._qscale)
+        B.sub_(loc)  # the change of this rank's sums over chunk 1 (exact: grid sums)
+        h1 = self.comm.allreduce_async(B)
+        h0.wait()
+        h1.wait()
+        torch.add(A, B, out=self.msgs[0])
+        st.split_steps = getattr(st, "split_steps", 0) + 1
 
     def _replay(self, key, launches) -> bool:
         """Replay the recorded launch sequence ``key`` of the current stream, recording it first (or again,

@@ -296,3 +296,75 @@ def test_bench_two_rank_launch_on_one_gpu():
     res = json.loads(lines[0])
     assert res["n_gpus"] == 2 and res["config"]["parallelism"] == "dp2" and res["dtype"] == "bf16"
     assert res["steps"] == 3 and res["value"] > 0 and res["extra"]["iterations"] == 3
+
+
+# ---- the split full-pass step: on data the bounds cannot prune, each full-pass step runs in
+# two row chunks and chunk 0's all-reduce is in flight during chunk 1's K9r pass; A + B must be the one-message
+# step bit for bit, on two ranks and against one rank
+
+N3, D3, K3 = 240_000, 128, 64
+
+
+def _data3():
+    rs = np.random.RandomState(23)
+    cen = rs.randn(K3, D3) * 0.5  # overlapping blobs: the bounds prune little, the gate picks full passes
+    x = cen[rs.randint(0, K3, N3)] + rs.randn(N3, D3)
+    return np.round(x * 8) / 8
+
+
+def _fit3(x_local, comm):
+    import torch
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+    eng = LloydEngine(torch.as_tensor(x_local, device="cuda").to(torch.bfloat16), D3, K3, comm, prune=True,
+                      precision="bf16")
+    eng.set_centers(eng.init_kmeans_parallel(seed=2))
+    eng.fit(12, 0.0)
+    torch.cuda.synchronize()
+    return {"centers": eng.centers.cpu().numpy().tolist(), "cost": eng.training_cost(),
+            "split": int(getattr(eng._pst, "split_steps", 0)), "pdev": bool(eng._pdev)}
+
+
+def _rank_main3(rank, world, port, out_path):
+    os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
+                       "MASTER_PORT": str(port), "CML_KMEANS_OVERLAP_ROWS": "1"})
+    import torch
+    import torch.distributed as dist
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator
+    torch.cuda.set_device(0)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
+    x = _data3()
+    lo, hi = rank * N3 // world, (rank + 1) * N3 // world
+    res = _fit3(x[lo:hi], comm)
+    with open(f"{out_path}.{rank}", "w") as fh:
+        json.dump(res, fh)
+    dist.barrier()
+    dist.destroy_process_group()
+
+
+def test_split_full_pass_steps_two_ranks_match_single_rank(tmp_path, monkeypatch):
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import local_comm
+    out = str(tmp_path / "w3")
+    ctx = mp.get_context("spawn")
+    port = _free_port()
+    procs = [ctx.Process(target=_rank_main3, args=(r, 2, port, out)) for r in range(2)]
+    for p in procs:
+        p.start()
+    for p in procs:
+        p.join(240)
+    assert all(p.exitcode == 0 for p in procs), [p.exitcode for p in procs]
+    res = [json.load(open(f"{out}.{r}")) for r in range(2)]
+    monkeypatch.setenv("CML_KMEANS_SPLIT_FULL", "0")
+    ref = _fit3(_data3(), local_comm())
+    assert ref["pdev"] and ref["split"] == 0
+    for r in range(2):
+        assert res[r]["split"] > 0, res[r]["split"]  # the overlapped steps ran
+        np.testing.assert_array_equal(np.asarray(res[r]["centers"]), np.asarray(ref["centers"]))
+        assert res[r]["cost"] == ref["cost"]
+    # and on one rank: the split step (forced) is the one-message step bit for bit
+    monkeypatch.setenv("CML_KMEANS_SPLIT_FULL", "1")
+    monkeypatch.setenv("CML_KMEANS_OVERLAP_ROWS", "1")
+    one = _fit3(_data3(), local_comm())
+    assert one["split"] > 0
+    np.testing.assert_array_equal(np.asarray(one["centers"]), np.asarray(ref["centers"]))
+    assert one["cost"] == ref["cost"]
