@@ -12,7 +12,8 @@
 #                         kernel / blocking-call / roctx timeline, kernel table, host syncs, sync audit
 #   strong                strong-scaling emulation: per-rank shards of the headline (100M / N rows)
 #   workflow              the reference workflow end to end on 4M uploaded rows (examples/)
-#   ovtl                  2-rank gloo timeline of the seeded step's overlapped accumulate (rocprofv3 per rank)
+#   ovtl [seeded|full]    2-rank gloo timeline of the seeded step's overlapped accumulate, or of the split
+#                         full-pass step on overlapping data (rocprofv3 per rank)
 #   clock                 K9r clock / MFMA busy share, rows from HBM vs from L2 (one rocprofv3 --pmc pass)
 #   drivers               every scripts/mb_*.py subcommand once at a small size, prof.py on a fresh trace
 #   mb SCRIPT [args]      a microbenchmark script (scripts/mb_*.py ...) -> SCRIPT.log
@@ -127,12 +128,13 @@ ovtl)
   # two gloo ranks on the one GPU, one rocprofv3 process each: the seeded step's split accumulate and the
   # order of chunk 0's all-reduce copies against chunk 1's kernels (scripts/overlap_timeline.py)
   P=$((29500 + RANDOM % 400))
+  W=${1:-seeded}  # seeded | full
   timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ov0 -o r0 -- \
-    python3 scripts/overlap_timeline.py rank 0 2 $P > "$O/r0.log" 2>&1 &
+    python3 scripts/overlap_timeline.py rank 0 2 $P $W > "$O/r0.log" 2>&1 &
   P0=$!
   S1=0
   timeout -k 10 300 rocprofv3 --kernel-trace --memory-copy-trace -d /tmp/ov1 -o r1 -- \
-    python3 scripts/overlap_timeline.py rank 1 2 $P > "$O/r1.log" 2>&1 || S1=$?
+    python3 scripts/overlap_timeline.py rank 1 2 $P $W > "$O/r1.log" 2>&1 || S1=$?
   S0=0
   wait $P0 || S0=$?
   [ $S0 -eq 0 ] && [ $S1 -eq 0 ] || { tail -20 "$O/r0.log" "$O/r1.log"; exit 1; }

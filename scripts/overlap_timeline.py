@@ -7,6 +7,9 @@
         python3 scripts/overlap_timeline.py rank 0 2 PORT &       (one profiled process per rank; same for rank 1)
     python scripts/overlap_timeline.py show DIR0/*.db
 
+A fifth argument ``full`` traces a pruned step on overlapping blobs instead: the split full-pass step, whose
+chunk 0 all-reduce (the device-to-host copy of gloo) must start before chunk 1's K9r pass ends.
+
 ``show`` prints, for every process database, the kernels and copies between the two probe-kernel dispatches that
 bracket the traced seeded step, in time order (the gloo all-reduce of a CUDA tensor appears as its
 device-to-host copy).
@@ -28,7 +31,7 @@ def _free_port():
     return p
 
 
-def _rank(rank, world, port):
+def _rank(rank, world, port, what="seeded"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
                        "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1", "CML_KMEANS_OVERLAP_ROWS": "1"})
     import torch
@@ -44,7 +47,9 @@ def _rank(rank, world, port):
     comm = Communicator(rank, world, torch.device("cuda", 0), "gloo", dist.group.WORLD)
     g = torch.Generator(device="cuda")
     g.manual_seed(11)
-    cen = torch.randn(K, D, generator=g, device="cuda") * 3
+    # "full": overlapping blobs — the bounds prune little, so the pruned steps run the split full pass (chunk 0's
+    # all-reduce in flight during chunk 1's K9r pass, models/kmeans.py _pdev_pre_split)
+    cen = torch.randn(K, D, generator=g, device="cuda") * (0.5 if what == "full" else 3)
     g.manual_seed(100 + rank)
     lab = torch.randint(0, K, (N // world,), generator=g, device="cuda")
     x = (cen[lab] + torch.randn(N // world, D, generator=g, device="cuda")).to(torch.bfloat16)
@@ -53,13 +58,18 @@ def _rank(rank, world, port):
         init = eng.init_kmeans_parallel(seed=5, as_device=True)
         eng.set_centers(init)
         torch.cuda.synchronize()
+        if what == "full":  # past the seeded step, into the steps whose gate picks full passes
+            eng.fit(4, 0.0)
+            torch.cuda.synchronize()
         if it:  # the traced step, bracketed by two dispatches of a one-wave probe kernel (window markers)
             KO.mx_probe(pa, pa, ps, ps)
-        with trace("kmeans.seeded" if it else "warmup.seeded"):
+        with trace(f"kmeans.{what}" if it else f"warmup.{what}"):
             eng.step()
             if it:
                 KO.mx_probe(pa, pa, ps, ps)
             torch.cuda.synchronize()
+        if what == "full" and it:
+            print(f"rank {rank}: split steps {getattr(eng._pst, 'split_steps', 0)}", flush=True)
         eng.fit(3, 0.0)
         torch.cuda.synchronize()
     dist.barrier()
@@ -113,6 +123,6 @@ if __name__ == "__main__":
     if len(sys.argv) > 1 and sys.argv[1] == "show":
         show(sys.argv[2:])
     elif len(sys.argv) > 1 and sys.argv[1] == "rank":
-        _rank(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]))
+        _rank(int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), sys.argv[5] if len(sys.argv) > 5 else "seeded")
     else:
         run()
