@@ -1135,11 +1135,14 @@ class LloydEngine:
 
     def _full_split(self, n: int):
         """Row halves of a full-pass step whose first half's all-reduce overlaps the second half's K9r pass
-        (_pdev_pre_split): multi-rank engines with at least CML_KMEANS_OVERLAP_ROWS local rows
-        (default 4M: a full pass is then >= ~1 ms, far above the extra launches). CML_KMEANS_SPLIT_FULL=1 also
-        splits one-rank engines (tests: the split step must give the one-pass bits); =0 never splits."""
+        (_pdev_pre_split), or None. Opt-in (CML_KMEANS_SPLIT_FULL=1, on any rank count, with at
+        least CML_KMEANS_OVERLAP_ROWS local rows): the Lloyd message is [k·D | k | 1] whatever the chunk, so the
+        second chunk's all-reduce is as long as the unsplit one and stays exposed — the split hides nothing of a
+        latency-bound 257 KiB all-reduce and pays a second delta-sums pipeline and K9r ramp (measured with a
+        one-rank RCCL group at the 8-GPU shard, 12.5M overlap-data rows: 2.25 vs 2.07 ms per step;
+        profiles/r6/README.md). It is kept, tested bit for bit, for bandwidth-bound messages (very large k·D)."""
         force = os.environ.get("CML_KMEANS_SPLIT_FULL")
-        if force == "0" or (not self.comm.is_distributed and force != "1"):
+        if force != "1":
             return None
         lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))
         if lim <= 0 or n < max(lim, 2 * self.aplan.round_rows):

@@ -33,7 +33,8 @@ def _free_port():
 
 def _rank(rank, world, port, what="seeded"):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1", "CML_KMEANS_OVERLAP_ROWS": "1"})
+                       "MASTER_PORT": str(port), "CML_KMEANS_PRUNE": "1", "CML_KMEANS_OVERLAP_ROWS": "1",
+                       "CML_KMEANS_SPLIT_FULL": "1"})
     import torch
     import torch.distributed as dist
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
@@ -114,7 +115,7 @@ def show(paths):
         except sqlite3.Error as exc:
             print(f"(memory copies: {exc})")
         ev.sort()
-        print(f"=== {path}: seeded step window {(hi - lo) / 1e6:.3f} ms, {len(ev)} events")
+        print(f"=== {path}: traced step window {(hi - lo) / 1e6:.3f} ms, {len(ev)} events")
         for s, e, kind, name in ev:
             print(f"{(s - lo) / 1e6:9.3f} ms  {kind:6s} {(e - s) / 1e3:8.1f} us  {name}")
 

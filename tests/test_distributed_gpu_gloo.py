@@ -326,7 +326,7 @@ def _fit3(x_local, comm):
 
 def _rank_main3(rank, world, port, out_path):
     os.environ.update({"RANK": str(rank), "WORLD_SIZE": str(world), "MASTER_ADDR": "127.0.0.1",
-                       "MASTER_PORT": str(port), "CML_KMEANS_OVERLAP_ROWS": "1"})
+                       "MASTER_PORT": str(port), "CML_KMEANS_OVERLAP_ROWS": "1", "CML_KMEANS_SPLIT_FULL": "1"})
     import torch
     import torch.distributed as dist
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.parallel.comm import Communicator

@@ -80,11 +80,14 @@ def test_init_sample_and_merge_match_torch():
 
 
 @pytest.mark.parametrize("m,d,k,spherical", [(1025, 256, 256, False), (300, 7, 20, False), (50, 3, 49, False),
-                                             (2000, 64, 5, False), (600, 32, 40, True), (12, 5, 12, False)])
+                                             (2000, 64, 5, False), (600, 32, 40, True), (12, 5, 12, False),
+                                             (1500, 48, 300, False), (2048, 16, 512, False), (200, 4, 30, False)])
 def test_local_kmeans_device_equals_host_bitwise(m, d, k, spherical):
     rs = np.random.RandomState(m + k)
     pts = rs.randn(m, d) * 3 + rs.randint(0, 8, (m, 1))
     pts[1] = pts[0]  # duplicate candidate
+    if m == 200:  # five distinct points: the weights of every later pick are all zero (the uniform pick)
+        pts = np.tile(pts[:5], (40, 1))
     w = rs.randint(0, 50, m).astype(np.float64)
     w[:3] = 0.0
     if spherical:
@@ -290,3 +293,22 @@ def test_seed_table_kernel(m, d, k):
     else:
         assert bool(torch.isinf(d2[:m]).all())
     assert bool((pn[:m].double() >= (U * U).sum(1)).all())
+
+
+@pytest.mark.gpu
+def test_local_kpp_wave_form_equals_workgroup_form():
+    """The one-wavefront k-means++ seeding (register-resident parts) and the 1024-thread workgroup form
+    (cml_local_kpp_set_wave A/B knob) perform the same operations in the same order: equal centres."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
+    rs = np.random.RandomState(3)
+    pts = torch.as_tensor(rs.randn(1025, 256) * 2 + rs.randint(0, 9, (1025, 1)), device="cuda")
+    w = torch.as_tensor(rs.randint(1, 40, 1025).astype(np.float64), device="cuda")
+    lib = _native.kernels()
+    prev = lib.cml_local_kpp_set_wave(1)
+    try:
+        a = K.local_kmeans(pts, w, 256, seed=4, max_iter=0, counts=True)
+        lib.cml_local_kpp_set_wave(0)
+        b = K.local_kmeans(pts, w, 256, seed=4, max_iter=0, counts=True)
+    finally:
+        lib.cml_local_kpp_set_wave(prev)
+    assert torch.equal(a, b)
