@@ -449,142 +449,6 @@ __global__ __launch_bounds__(kKppThreads) void local_kpp_kernel(const double* __
   }
 }
 
-// The same seeding in ONE wavefront, for the pairwise table D and m <= 256·8 points (the k-means|| finish:
-// ~2k + 1 candidates): the operations and their order are local_kpp_kernel's (and the host twin's), but
-// lane l owns the parts 4l..4l+3 — L points each, with their running distances and pick weights in its
-// registers — so a pick is the lane folds, one wave scan and a walk of the picking lane's own registers:
-// no barrier and no LDS round trip. The one memory access on a pick's critical path is the chosen point's
-// D row (4L contiguous doubles per lane). The 1024-thread form paid three workgroup barriers and an LDS
-// pass per pick (0.81 ms for k = 256, one workgroup: VERDICT r5 weak 2). The picks go to LDS; the chosen
-// rows are copied to C / CT afterwards by local_copy_picks_kernel (wide).
-template <int L>
-__global__ __launch_bounds__(64) void local_kpp_wave_kernel(const double* __restrict__ D, int m,
-                                                            const double* __restrict__ w, int k,
-                                                            unsigned long long key, int* __restrict__ picks) {
-  const int l = threadIdx.x;
-  const int base = 4 * l * L;  // first point of the lane's parts (parts 4l .. 4l + 3)
-  double wl[4 * L], d2[4 * L], pw[4 * L];
-#pragma unroll
-  for (int e = 0; e < 4 * L; ++e) {
-    const int q = base + e;
-    wl[e] = q < m ? w[q] : 0.0;
-    pw[e] = wl[e];
-    d2[e] = 0.0;
-  }
-  for (int i = 0; i < k; ++i) {
-    double part[4];
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {  // part b = 4l + j: its points folded in order from 0
-      double s = 0.0;
-#pragma unroll
-      for (int t = 0; t < L; ++t)
-        if (base + j * L + t < m) s = __dadd_rn(s, pw[j * L + t]);
-      part[j] = s;
-    }
-    double q4 = part[0];
-#pragma unroll
-    for (int j = 1; j < 4; ++j) q4 = __dadd_rn(q4, part[j]);
-    double S = q4;
-#pragma unroll
-    for (int off = 1; off < 64; off <<= 1) {
-      const double o = __shfl_up(S, off, 64);
-      if (l >= off) S = __dadd_rn(o, S);
-    }
-    const double total = __shfl(S, 63, 64);
-    const double u = cu((unsigned long long)i, key);
-    int pick = -1;
-    if (!(total > 0.0)) {
-      pick = (int)__dmul_rn(u, (double)m);
-      pick = pick < m - 1 ? pick : m - 1;
-    } else {
-      const double r = __dmul_rn(u, total);
-      const unsigned long long over = __ballot(S > r);
-      if (over != 0ull) {
-        const int ls = __builtin_ctzll(over);
-        // every lane walks its own parts as if it were the first lane past r; lane ls's walk is the pick
-        const double prevS = __shfl_up(S, 1, 64);
-        double cum = l > 0 ? prevS : 0.0;
-        int mp = -1, lastb = -1;
-#pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          if (mp < 0) {
-            const double nxt = __dadd_rn(cum, part[j]);
-            if (part[j] > 0.0) lastb = j;
-            if (nxt > r) {
-              double c2 = cum;
-              int lastpos = -1;
-              bool done = false;
-#pragma unroll
-              for (int t = 0; t < L; ++t) {
-                const int q = base + j * L + t;
-                if (!done && q < m) {
-                  const double pv = pw[j * L + t];
-                  if (pv > 0.0) lastpos = q;
-                  c2 = __dadd_rn(c2, pv);
-                  if (c2 > r) {
-                    mp = q;
-                    done = true;
-                  }
-                }
-              }
-              if (mp < 0) mp = lastpos;
-            }
-            cum = nxt;
-          }
-        }
-        if (mp < 0 && lastb >= 0) {  // rounding between the lane prefix and the part walk
-#pragma unroll
-          for (int j = 0; j < 4; ++j)
-            if (j == lastb)
-#pragma unroll
-              for (int t = 0; t < L; ++t) {
-                const int q = base + j * L + t;
-                if (q < m && pw[j * L + t] > 0.0) mp = q;
-              }
-        }
-        pick = __shfl(mp, ls, 64);
-      }
-      if (pick < 0) {  // rounding: the last point of positive weight
-        int lastq = -1;
-#pragma unroll
-        for (int e = 0; e < 4 * L; ++e)
-          if (base + e < m && pw[e] > 0.0) lastq = base + e;
-#pragma unroll
-        for (int o = 32; o > 0; o >>= 1) {
-          const int v = __shfl_xor(lastq, o, 64);
-          lastq = v > lastq ? v : lastq;
-        }
-        pick = lastq;
-      }
-      if (pick < 0) pick = 0;
-    }
-    if (l == 0) picks[i] = pick;
-    const double* __restrict__ dr = D + (long long)pick * m;
-#pragma unroll
-    for (int e = 0; e < 4 * L; ++e) {
-      const int q = base + e;
-      if (q < m) {
-        const double acc = dr[q];
-        const double nd = (i == 0 || acc < d2[e]) ? acc : d2[e];
-        d2[e] = nd;
-        pw[e] = __dmul_rn(wl[e], nd);
-      }
-    }
-  }
-}
-
-// C[i] = CT[:, i] = P[picks[i]] (one workgroup per pick).
-__global__ __launch_bounds__(kThreads) void local_copy_picks_kernel(const double* __restrict__ P, int d,
-                                                                   const int* __restrict__ picks, int k,
-                                                                   double* __restrict__ C, double* __restrict__ CT) {
-  const int i = blockIdx.x, pk = picks[i];
-  for (int t = threadIdx.x; t < d; t += kThreads) {
-    const double v = P[(long long)pk * d + t];
-    C[(long long)i * d + t] = v;
-    CT[(long long)t * k + i] = v;
-  }
-}
-
 // D[i][q] = dist(P_q, P_i) (the fold of the k-means++ update: e = P_q[t] - P_i[t], acc = fma(e, e,
 // acc)) for every candidate pair, 16 x 16 pairs per workgroup with both row blocks staged in LDS
 // in 64-dimension slices; each thread folds its pair over the dimensions in order.
@@ -1025,13 +889,6 @@ CML_API int cml_kmeans_cost_combine(const double* q, const double* msg, int rows
   return cml_status();
 }
 
-int g_kpp_wave = 1;  // cml_local_kpp_set_wave (A/B knob: 0 = the 1024-thread workgroup form)
-CML_API int cml_local_kpp_set_wave(int on) {
-  const int prev = g_kpp_wave;
-  if (on >= 0) g_kpp_wave = on;
-  return prev;
-}
-
 // P: f64 [m, d] candidates, PT: the same transposed [d, m], w: f64 [m]; C: f64 [k, d], CT: f64 [d, k],
 // d2: f64 [m] scratch.
 // D: f64 [m, m] scratch for the pairwise distances, or null (then each pick folds its distances from PT).
@@ -1042,18 +899,6 @@ CML_API int cml_local_kpp(const double* P, const double* PT, int m, int d, const
   if (D != nullptr) {
     const unsigned g = (unsigned)((m + kPairT - 1) / kPairT);
     hipLaunchKernelGGL(local_pairdist_kernel, dim3(g, g), dim3(kThreads), 0, st, P, m, d, D);
-  }
-  if (D != nullptr && m <= 256 * 8 && m >= k && g_kpp_wave) {  // one wavefront, registers (local_kpp_wave_kernel)
-    const int L = (m + 255) / 256;
-    int* picks = reinterpret_cast<int*>(d2);  // (d2 is scratch here: m doubles >= k ints, m > k)
-    switch (L) {
-#define CML_KPPW(LL) case LL: hipLaunchKernelGGL(local_kpp_wave_kernel<LL>, dim3(1), dim3(64), 0, st, D, m, w, k, key, picks); break;
-      CML_KPPW(1) CML_KPPW(2) CML_KPPW(3) CML_KPPW(4) CML_KPPW(5) CML_KPPW(6) CML_KPPW(7) CML_KPPW(8)
-#undef CML_KPPW
-      default: return (int)hipErrorInvalidValue;
-    }
-    hipLaunchKernelGGL(local_copy_picks_kernel, dim3(k), dim3(kThreads), 0, st, P, d, picks, k, C, CT);
-    return cml_status();
   }
   const size_t big = ((size_t)d + 2 * (size_t)m) * 8;
   const bool lds_pw = D != nullptr && big <= 150 * 1024;

@@ -1144,7 +1144,7 @@ class LloydEngine:
         force = os.environ.get("CML_KMEANS_SPLIT_FULL")
         if force != "1":
             return None
-        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))
+        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))  # (the split is opt-in above)
         if lim <= 0 or n < max(lim, 2 * self.aplan.round_rows):
             return None
         mid = min(n - 1, max(1, round_up(n // 2, 1024)))
@@ -1343,11 +1343,14 @@ class LloydEngine:
     def _overlap_split(self, n: int):
         """Row ranges of the overlapped full accumulate of the seeded step: two chunks
         whose sums are all-reduced separately, chunk 0's collective running on the process group's stream
-        while chunk 1 accumulates. Multi-rank engines with at least CML_KMEANS_OVERLAP_ROWS local rows
-        (default 4M: the accumulate then takes ~0.5 ms, well above the extra launches); None otherwise."""
+        while chunk 1 accumulates. Opt-in: multi-rank engines with at least CML_KMEANS_OVERLAP_ROWS local rows
+        (default 0 = off); None otherwise. The second chunk's all-reduce carries the same [k·D | k | 1] message
+        as an unsplit step, so it is exposed just as long — the split hides nothing of a latency-bound
+        collective and pays a second counting sort and accumulate: at the 8-GPU shard (12.5M rows, one-rank
+        RCCL group) the fit took 19.6 ms split against 18.9 ms unsplit (profiles/r6/README.md)."""
         if not self.comm.is_distributed:
             return None
-        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 4_000_000))
+        lim = int(os.environ.get("CML_KMEANS_OVERLAP_ROWS", 0))
         if lim <= 0 or n < max(lim, 2):
             return None
         mid = min(n - 1, max(1, round_up(n // 2, 1024)))

@@ -90,7 +90,6 @@ _native.register_kernel_sigs({
     "cml_kmeans_cost_parts": (c_int, []),
     "cml_kmeans_cost_pass": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_ll, c_vp, c_vp, c_vp]),
     "cml_sum_f32_f64": (c_int, [c_vp, c_ll, c_vp, c_vp, c_vp]),
-    "cml_local_kpp_set_wave": (c_int, [c_int]),
     "cml_fixsum": (c_int, [c_vp, c_int, c_vp, c_ll, c_int, c_vp, ctypes.c_float, c_vp, c_vp]),
     "cml_fixsum_finalize": (c_int, [c_vp, c_int, c_vp, ctypes.c_float, c_vp, c_vp]),
     "cml_kmeans_init_sample": (c_int, [c_vp, c_vp, c_ll, ctypes.c_uint64, ctypes.c_double, c_vp, c_vp, c_ll,

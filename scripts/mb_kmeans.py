@@ -23,9 +23,6 @@ subcommand per experiment. The K9/K9r assign pass on its own is scripts/mb_k9r.p
         checked bit for bit against exact_assign
     python scripts/mb_kmeans.py fp8-mx [--rows 20000000] [--dim 512] [--k 128] [--steps 8]
         fp8 rows: MX-scaled fp8 MFMAs against the bf16 widening pass, one assign pass and pruned steps each way
-    python scripts/mb_kmeans.py kpp [--m 1025] [--dim 256] [--k 256] [--reps 20]
-        the k-means|| finish's weighted k-means++ seeding (local_kpp): the one-wavefront form against the
-        1024-thread workgroup form (cml_local_kpp_set_wave), kernel time from the events, equal results checked
     python scripts/mb_kmeans.py host [--rows 12500000] [--dim 256] [--k 256] [--iters 20] [--top 45]
         cProfile of the timed public-API fit after two warm-ups (scripts/sync_audit.py lists its blocking reads)
 """
@@ -407,32 +404,7 @@ def cmd_host(argv):
         print("\n".join(line for line in s.getvalue().splitlines() if line.strip())[:20000])
 
 
-def cmd_kpp(argv):
-    a = parse("kpp", argv, m=1025, dim=256, k=256, reps=20)
-    from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
-    g = torch.Generator(device="cuda")
-    g.manual_seed(5)
-    pts = (torch.randn(a.m, a.dim, device="cuda", generator=g, dtype=torch.float64) * 2).contiguous()
-    w = torch.randint(1, 50, (a.m,), device="cuda", generator=g).to(torch.float64)
-    lib = _native.kernels()
-    prev = lib.cml_local_kpp_set_wave(-1)
-    res = {}
-    try:
-        for form, on in (("wave", 1), ("workgroup", 0)):
-            lib.cml_local_kpp_set_wave(on)
-            out = []
-            ts = event_list(lambda: out.append(K.local_kmeans(pts, w, a.k, seed=3, max_iter=0, counts=True)),
-                            a.reps)
-            res[form] = out[-1]
-            ts.sort()
-            print(f"local k-means++ {form:9s} m={a.m} d={a.dim} k={a.k}: median {ts[len(ts) // 2]:.3f} ms, "
-                  f"min {ts[0]:.3f} ms (pairwise table + seeding + row copies)")
-    finally:
-        lib.cml_local_kpp_set_wave(prev)
-    print("equal centres:", bool(torch.equal(res["wave"], res["workgroup"])))
-
-
-COMMANDS = {"kpp": cmd_kpp, "accum": cmd_accum, "segacc": cmd_segacc, "overlap": cmd_overlap, "rowpass": cmd_rowpass,
+COMMANDS = {"accum": cmd_accum, "segacc": cmd_segacc, "overlap": cmd_overlap, "rowpass": cmd_rowpass,
             "prune": cmd_prune, "bounds": cmd_bounds, "churn": cmd_churn, "graph": cmd_graph, "cert": cmd_cert,
             "fp8-mx": cmd_fp8_mx, "host": cmd_host}
 

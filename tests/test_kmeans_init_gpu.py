@@ -294,21 +294,3 @@ def test_seed_table_kernel(m, d, k):
         assert bool(torch.isinf(d2[:m]).all())
     assert bool((pn[:m].double() >= (U * U).sum(1)).all())
 
-
-@pytest.mark.gpu
-def test_local_kpp_wave_form_equals_workgroup_form():
-    """The one-wavefront k-means++ seeding (register-resident parts) and the 1024-thread workgroup form
-    (cml_local_kpp_set_wave A/B knob) perform the same operations in the same order: equal centres."""
-    from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
-    rs = np.random.RandomState(3)
-    pts = torch.as_tensor(rs.randn(1025, 256) * 2 + rs.randint(0, 9, (1025, 1)), device="cuda")
-    w = torch.as_tensor(rs.randint(1, 40, 1025).astype(np.float64), device="cuda")
-    lib = _native.kernels()
-    prev = lib.cml_local_kpp_set_wave(1)
-    try:
-        a = K.local_kmeans(pts, w, 256, seed=4, max_iter=0, counts=True)
-        lib.cml_local_kpp_set_wave(0)
-        b = K.local_kmeans(pts, w, 256, seed=4, max_iter=0, counts=True)
-    finally:
-        lib.cml_local_kpp_set_wave(prev)
-    assert torch.equal(a, b)
