@@ -1,0 +1,72 @@
+"""fp8 fit-level parity: on the same e4m3 rows and from the same initial centres, the MX
+fit (MX-scaled fp8 MFMAs against centres kept on the two-term e4m3 grid), the widening fit (the rows widened
+to bf16, bf16 centres) and the exact f64 Lloyd fit (kmeans_exact.hip on the f64 values of the same rows)
+reach the same clustering: the MX and widening assignments differ from the f64 one only on near-ties, so the
+final trainingCost and the centres (f64 means, Spark's clusterCenters) stay within stated bounds of the
+f64 fit. Config-5 width (512) and k = 64, 300K rows.
+
+Bounds (measured on MI355X: tests print them): |cost - cost_f64| / cost_f64 <= 1e-4; labels differing from
+the f64 fit <= 0.5 % of the rows; every centre within 2e-3 of the f64 centre relative to the data's
+RMS norm."""
+import pytest
+import torch
+
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.models.kmeans import LloydEngine
+from clustermachinelearningforhospitalnetworks_apache_spark_amd.ops import kmeans_ops as K
+
+pytestmark = pytest.mark.gpu
+
+N, D, KC, ITERS = 300_000, 512, 64, 12
+
+
+def _rows():
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
+    dev = torch.device("cuda", 0)
+    cen = synth.synth_rows(0, KC, D, seed=31, stream=1, device=dev) * 1.5
+    z = synth.synth_rows(0, N, D, seed=32, centres=cen, device=dev)
+    return z.clamp_(-440.0, 440.0).to(torch.float8_e4m3fn)
+
+
+def _fit(x, init, mx=None, exact=False):
+    prev = K.set_fp8_mx(mx) if mx is not None else None
+    try:
+        if exact:
+            eng = LloydEngine(x.to(torch.float64), D, KC, precision="exact")
+        else:
+            eng = LloydEngine(x, D, KC)
+        eng.set_centers(init)
+        eng.fit(ITERS, 0.0)
+        torch.cuda.synchronize()
+        lab = eng.final_labels().to(torch.int64).clone() if not exact else eng.assign()[0].to(torch.int64)
+        return eng.centers.clone(), eng.training_cost(), lab, eng
+    finally:
+        if prev is not None:
+            K.set_fp8_mx(prev)
+
+
+def measure():
+    x = _rows()
+    eng = LloydEngine(x, D, KC)
+    init = torch.as_tensor(eng.init_kmeans_parallel(seed=5), dtype=torch.float64, device="cuda")
+    del eng
+    c_mx, cost_mx, lab_mx, e_mx = _fit(x, init, mx=True)
+    assert e_mx._mx, "the MX path did not run"
+    c_w, cost_w, lab_w, e_w = _fit(x, init, mx=False)
+    assert not e_w._mx
+    c_f, cost_f, lab_f, _ = _fit(x, init, exact=True)
+    scale = float(x.to(torch.float32).pow(2).sum(1).mean().sqrt())
+    out = {}
+    for name, c, cost, lab in (("mx", c_mx, cost_mx, lab_mx), ("widen", c_w, cost_w, lab_w)):
+        out[name] = {"cost_rel": abs(cost - cost_f) / cost_f,
+                     "label_diff": float((lab != lab_f).double().mean()),
+                     "centre_err": float((c - c_f).norm(dim=1).max()) / scale}
+    return out
+
+
+def test_fp8_fit_parity_against_f64_lloyd():
+    res = measure()
+    print(res)
+    for name, r in res.items():
+        assert r["cost_rel"] <= 1e-4, (name, r)
+        assert r["label_diff"] <= 5e-3, (name, r)
+        assert r["centre_err"] <= 2e-3, (name, r)
