@@ -25,6 +25,10 @@ _native.register_kernel_sigs({
     "cml_linear_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_int, c_vp, c_int, c_vp]),
     "cml_gram": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_partial_colsum": (c_int, [c_vp, c_int, c_int, c_vp, c_vp]),
+    "cml_multinomial_mfma_supported": (c_int, [c_int, c_int, c_int]),
+    "cml_multinomial_mfma_grid": (c_int, [c_ll, c_int]),
+    "cml_multinomial_mfma_dpad": (c_int, [c_int, c_int]),
+    "cml_multinomial_mfma_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_glm_loss_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
                                c_vp, c_ll, c_ll, c_vp]),
@@ -219,8 +223,9 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
     """Softmax (multinomial logistic) loss + gradient over the local shard: ``coef`` [C, d+1] (last column
     the intercepts) in the original feature space, labels 0..C-1 (f64). Returns the float64 sums
     [∇W (C·d, row-major) | ∇b (C) | loss | weight sum]. GPU rows run K13m (multinomial_grad_kernel: X read
-    once, gradient partials in f64, fixed-order reduction) where the layout fits (C <= 8, d up to 512 bf16);
-    otherwise — and on the CPU — row chunks in f64 (never an f64 copy of the whole X)."""
+    once, gradient partials in f64, fixed-order reduction) where the layout fits (C <= 8, d up to 512 bf16),
+    and its MFMA form for 9..64 classes on bf16 rows with d <= 256, d % 8 == 0 (glm_mfma.hip: both products on
+    v_mfma_f32_32x32x2_f32); otherwise — and on the CPU — row chunks in f64 (never an f64 copy of the whole X)."""
     C = int(coef.shape[0])
     n = int(x.shape[0])
     coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
@@ -239,6 +244,10 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
                                         _native.stream_ptr())
             _native.check(st, "multinomial_grad")
             return partial_colsum(out)
+        cp = k.cml_multinomial_mfma_supported(d, code, C)
+        if cp > 0:
+            # 9..64 classes on bf16 rows: both products on MFMA (glm_mfma.hip); padded [cp, dp] gradient slots
+            return _multinomial_mfma(xx, d, y, coef, weight, C, cp, int(k.cml_multinomial_mfma_dpad(d, C)))
     W, b = coef[:, :d], coef[:, d]
     gW = torch.zeros((C, d), dtype=torch.float64, device=x.device)
     gb = torch.zeros(C, dtype=torch.float64, device=x.device)
@@ -259,6 +268,22 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
         gb += R.sum(0)
         wsum += ww.sum()
     return torch.cat([gW.reshape(-1), gb, loss.reshape(1), wsum.reshape(1)])
+
+
+def _multinomial_mfma(xx: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor, weight, C: int, cp: int,
+                      dp: int) -> torch.Tensor:
+    """K13m on MFMA (glm_mfma.hip) -> [∇W (C·d) | ∇b (C) | loss | weight sum], the layout of multinomial_grad."""
+    n = int(xx.shape[0])
+    k = _native.kernels()
+    g = k.cml_multinomial_mfma_grid(n, num_cus(xx.device.index or 0))
+    out = torch.empty((g, cp * dp + C + 2), dtype=torch.float64, device=xx.device)
+    yy = y.to(torch.float64).contiguous()
+    ww = weight.to(torch.float64).contiguous() if weight is not None else None
+    _native.check(k.cml_multinomial_mfma_grad(xx.data_ptr(), n, xx.stride(0), d, C, yy.data_ptr(),
+                                              ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
+                                              g, _native.stream_ptr()), "multinomial_mfma_grad")
+    msg = partial_colsum(out)
+    return torch.cat([msg[: cp * dp].view(cp, dp)[:C, :d].reshape(-1), msg[cp * dp:]])
 
 
 def _logreg_grad_dev(x, d, y, coef, weight, batch, row_base):

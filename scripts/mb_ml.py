@@ -8,6 +8,9 @@
     python scripts/mb_ml.py logreg [--scale S] [--out FILE.json]
         K13 logreg_grad by batch size (16K rows .. the whole shard; small batches replayed from one HIP graph so
         launch cost does not hide the kernel), partial_colsum, and K7 moments
+    python scripts/mb_ml.py multinomial [--rows 100000000] [--dim 256]
+        K13m multinomial loss + gradient passes over bf16 rows for C = 4, 8 (VALU kernel), 16, 32, 64 (MFMA kernel):
+        best-of-3 ms, HBM TB/s of the row bytes, and the MFMA-form FLOP rate
     python scripts/mb_ml.py trees [--scale S]
         ForestEngine fits (20 trees, depth 5, 32 bins) with the phase split, cold and warm; GBT fits (20 iterations)
     python scripts/mb_ml.py tree-transform [--rows 2000000]
@@ -283,7 +286,32 @@ def cmd_tree_transform(argv):
     timed("DecisionTreeClassificationModel.transform", lambda: dtc.transform(cte))
 
 
-COMMANDS = {"glm": cmd_glm, "glm-fp8": cmd_glm_fp8, "logreg": cmd_logreg, "trees": cmd_trees,
+def cmd_multinomial(argv):
+    ap = argparse.ArgumentParser(prog="mb_ml.py multinomial")
+    ap.add_argument("--rows", type=int, default=100_000_000)
+    ap.add_argument("--dim", type=int, default=256)
+    a = ap.parse_args(argv)
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
+    dev = torch.device("cuda", 0)
+    n, d = a.rows, a.dim
+    x = synth.synth_rows(0, n, d, seed=3, dtype=torch.bfloat16, device=dev)
+    lib = __import__("clustermachinelearningforhospitalnetworks_apache_spark_amd._native",
+                     fromlist=["kernels"]).kernels()
+    g = torch.Generator(device=dev)
+    g.manual_seed(1)
+    for C in (4, 8, 16, 32, 64):
+        y = torch.randint(0, C, (n,), generator=g, device=dev).to(torch.float64)
+        coef = torch.randn(C, d + 1, generator=g, device=dev, dtype=torch.float64) * 0.05
+        ms = best_ms(lambda: glm_ops.multinomial_grad(x, d, y, coef), reps=3)
+        form = "valu" if lib.cml_multinomial_supported(d, 0, C) > 0 else (
+            "mfma" if lib.cml_multinomial_mfma_supported(d, 0, C) > 0 else "torch-chunks")
+        flop = 4.0 * n * d * (32 if C <= 32 else 64)  # MFMA form: margins + gradient on the padded class tile
+        print(f"multinomial {n}x{d} bf16 C={C:2d} [{form}]: {ms:8.3f} ms, {n * d * 2 / ms / 1e9:6.2f} TB/s rows"
+              + (f", {flop / ms / 1e9:7.1f} TFLOP/s (f32 MFMA)" if form == "mfma" else ""), flush=True)
+        del y
+
+
+COMMANDS = {"multinomial": cmd_multinomial, "glm": cmd_glm, "glm-fp8": cmd_glm_fp8, "logreg": cmd_logreg, "trees": cmd_trees,
             "tree-transform": cmd_tree_transform}
 
 if __name__ == "__main__":

@@ -64,7 +64,11 @@ def test_chunked_oracle_matches_closed_form():
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("dt,d,C", [(torch.bfloat16, 256, 8), (torch.bfloat16, 37, 3), (torch.float32, 128, 5),
-                                    (torch.float64, 64, 4), (torch.float8_e4m3fn, 256, 4), (torch.float32, 4, 2)])
+                                    (torch.float64, 64, 4), (torch.float8_e4m3fn, 256, 4), (torch.float32, 4, 2),
+                                    # MFMA form (glm_mfma.hip): one class tile, two, and the padded two-launch widths
+                                    (torch.bfloat16, 256, 32), (torch.bfloat16, 128, 16), (torch.bfloat16, 40, 12),
+                                    (torch.bfloat16, 256, 64), (torch.bfloat16, 200, 40), (torch.bfloat16, 136, 33),
+                                    (torch.bfloat16, 64, 9)])
 def test_kernel_matches_f64_oracle(dt, d, C):
     g = torch.Generator(device="cuda").manual_seed(d + C)
     n = 200_003
@@ -73,7 +77,9 @@ def test_kernel_matches_f64_oracle(dt, d, C):
     w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
     coef = torch.randn(C, d + 1, generator=g, device="cuda", dtype=torch.float64) * 0.2
     from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
-    assert _native.kernels().cml_multinomial_supported(d, glm_ops._CODE[dt], C) > 0
+    lib = _native.kernels()
+    code = glm_ops._CODE[dt]
+    assert lib.cml_multinomial_supported(d, code, C) > 0 or lib.cml_multinomial_mfma_supported(d, code, C) > 0
     got = glm_ops.multinomial_grad(x, d, y, coef, w)
     ref = glm_ops.multinomial_grad(x.float().cpu().to(torch.float64) if dt != torch.float64 else x.cpu(), d,
                                    y.cpu(), coef.cpu(), w.cpu())
