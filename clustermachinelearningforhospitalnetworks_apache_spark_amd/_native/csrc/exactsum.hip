@@ -6,12 +6,13 @@
 // These sums accumulate INTEGERS, which add exactly in any order, and round to f64 once, after the
 // int64 all-reduce, in a fixed order:
 //
-//   every value v (>= 0) is put on the grid 2^g, g = e(bound) - 62, where `bound` is an upper bound of
+//   every value v (>= 0) is put on the grid 2^g, g = e(bound) - 46, where `bound` is an upper bound of
 //   every value on EVERY rank (a device scalar the ranks agree on: e.g. the all-reduced max ||x||²), so
-//   q = rint(v / 2^g) < 2^62 — one rounding per value at 2^-62 of the bound, the same on any rank;
-//   q is split into two 31-bit limbs, summed as int64 (per thread in registers for one sum, per label in
-//   LDS with integer atomics, then one global atomic per block and limb); fixsum_finalize recombines the
-//   (all-reduced) limbs in double-double and scales by 2^g.
+//   q = rint(v / 2^g) < 2^46 — one rounding per value at 2^-47 of the bound (far below what an f64 sum of
+//   the values keeps), the same on any rank; q is summed as int64 (per thread in registers for one sum, per
+//   label with ONE integer LDS atomic per value — a block sums at most 2^16 values, so its label sums stay below
+//   2^62), and each block's sums go to the global accumulators as two 31-bit limbs (integer atomics);
+//   fixsum_finalize recombines the (all-reduced) limbs in double-double and scales by 2^g.
 #include "common.h"
 
 namespace {
@@ -32,17 +33,22 @@ __device__ __forceinline__ void dd_add(double& h, double& l, double v) {
   two_sum(s, l, h, l);
 }
 
-// grid exponent: every value v <= bound·mul·(1 + 2^-10) lies below 2^(g + 62)
+constexpr int kQBits = 46;             // q < 2^46
+constexpr long long kBlockValues = 1 << 16;  // at most this many values per block (grid sizing): sums < 2^62
+
+// grid exponent: every value v <= bound·mul·(1 + 2^-10) lies below 2^(g + kQBits)
 __device__ __forceinline__ int fix_grid(float bound, float mul) {
   const double m = (double)bound * (double)mul * (1.0 + 1.0 / 1024.0);
   if (!(m > 0.0)) return 0;
-  return ilogb(m) + 1 - 62;
+  return ilogb(m) + 1 - kQBits;
 }
 
-__device__ __forceinline__ long long fix_q(double v, int g) {
-  if (!(v > 0.0)) return 0;  // (negative and NaN values are outside the contract: counted as 0)
-  long long q = (long long)rint(ldexp(v, -g));
-  return q > (1LL << 62) ? (1LL << 62) : q;
+// q = rint(v·2^-g) by a power-of-two multiply (exact) and one rounding conversion; v <= 0 and NaN -> 0
+__device__ __forceinline__ long long fix_q(double v, double scale) {
+  const double t = v * scale;
+  if (!(t > 0.0)) return 0;
+  const long long q = __double2ll_rn(t);
+  return q > (1LL << kQBits) ? (1LL << kQBits) : q;
 }
 
 __device__ __forceinline__ long long wave_sum_i64(long long v) {
@@ -51,19 +57,34 @@ __device__ __forceinline__ long long wave_sum_i64(long long v) {
   return v;
 }
 
-template <typename T>
+// a block sum s (0 <= s < 2^62) into the two global 31-bit limbs
+__device__ __forceinline__ void add_limbs(long long* lo, long long* hi, long long s) {
+  if (s == 0) return;
+  atomicAdd(reinterpret_cast<unsigned long long*>(lo), (unsigned long long)(s & 0x7fffffffLL));
+  atomicAdd(reinterpret_cast<unsigned long long*>(hi), (unsigned long long)(s >> 31));
+}
+
+template <typename T, bool VEC4>
 __global__ __launch_bounds__(kThreads) void fixsum_kernel(const T* __restrict__ v, long long n,
                                                          const float* __restrict__ bound, float mul,
                                                          long long* __restrict__ limbs) {
-  const int g = fix_grid(bound[0], mul);
-  long long lo = 0, hi = 0;  // per thread: at most ~n / (grid·256) values of < 2^31 each
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const long long q = fix_q((double)v[i], g);
-    lo += q & 0x7fffffffLL;
-    hi += q >> 31;
+  const double scale = ldexp(1.0, -fix_grid(bound[0], mul));
+  long long acc = 0;  // < 2^46 per value, at most 256 values per thread: < 2^54
+  const long long stride = (long long)gridDim.x * kThreads;
+  long long i = (long long)blockIdx.x * kThreads + threadIdx.x;
+  if constexpr (VEC4) {  // 16-byte loads of four f32 values (16-byte aligned vectors)
+    const long long n4 = n / 4;
+    const float4* v4 = reinterpret_cast<const float4*>(v);
+    for (long long j = i; j < n4; j += stride) {
+      const float4 w = v4[j];
+      acc += fix_q((double)w.x, scale) + fix_q((double)w.y, scale) + fix_q((double)w.z, scale) +
+             fix_q((double)w.w, scale);
+    }
+    if (blockIdx.x == 0 && threadIdx.x < (unsigned)(n - 4 * n4)) acc += fix_q((double)v[4 * n4 + threadIdx.x], scale);
+  } else {
+    for (long long j = i; j < n; j += stride) acc += fix_q((double)v[j], scale);
   }
-  lo = wave_sum_i64(lo);
-  hi = wave_sum_i64(hi);
+  long long lo = wave_sum_i64(acc & 0x7fffffffLL), hi = wave_sum_i64(acc >> 31);
   if ((threadIdx.x & 63) == 0) {
     if (lo) atomicAdd(reinterpret_cast<unsigned long long*>(&limbs[0]), (unsigned long long)lo);
     if (hi) atomicAdd(reinterpret_cast<unsigned long long*>(&limbs[1]), (unsigned long long)hi);
@@ -74,20 +95,18 @@ template <typename T>
 __global__ __launch_bounds__(kThreads) void fixsum_label_kernel(const int* __restrict__ lab, const T* __restrict__ v,
                                                                long long n, int k, const float* __restrict__ bound,
                                                                float mul, long long* __restrict__ limbs) {
-  extern __shared__ long long acc[];  // [2k]: lo limbs, then hi limbs
-  for (int i = threadIdx.x; i < 2 * k; i += kThreads) acc[i] = 0;
+  extern __shared__ long long acc[];  // [k] label sums of this block (< 2^62: at most kBlockValues values)
+  for (int i = threadIdx.x; i < k; i += kThreads) acc[i] = 0;
   __syncthreads();
-  const int g = fix_grid(bound[0], mul);
-  for (long long i = (long long)blockIdx.x * kThreads + threadIdx.x; i < n; i += (long long)gridDim.x * kThreads) {
-    const long long q = fix_q((double)v[i], g);
-    if (q == 0) continue;
-    const int j = lab[i];
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc[j]), (unsigned long long)(q & 0x7fffffffLL));
-    atomicAdd(reinterpret_cast<unsigned long long*>(&acc[k + j]), (unsigned long long)(q >> 31));
+  const double scale = ldexp(1.0, -fix_grid(bound[0], mul));
+  const long long per = (n + gridDim.x - 1) / gridDim.x;  // a contiguous range per block
+  const long long b0 = (long long)blockIdx.x * per, b1 = b0 + per < n ? b0 + per : n;
+  for (long long i = b0 + threadIdx.x; i < b1; i += kThreads) {
+    const long long q = fix_q((double)v[i], scale);
+    if (q != 0) atomicAdd(reinterpret_cast<unsigned long long*>(&acc[lab[i]]), (unsigned long long)q);
   }
   __syncthreads();
-  for (int i = threadIdx.x; i < 2 * k; i += kThreads)
-    if (acc[i] != 0) atomicAdd(reinterpret_cast<unsigned long long*>(&limbs[i]), (unsigned long long)acc[i]);
+  for (int i = threadIdx.x; i < k; i += kThreads) add_limbs(&limbs[i], &limbs[k + i], acc[i]);
 }
 
 __global__ __launch_bounds__(kThreads) void fixsum_finalize_kernel(const long long* __restrict__ limbs, int k,
@@ -119,24 +138,38 @@ inline unsigned grid_for(long long n, long long per, unsigned cap) {
 CML_API int cml_fixsum(const void* v, int dtype, const int* lab, long long n, int k, const float* bound, float mul,
                        long long* limbs, void* stream) {
   if (n <= 0) return 0;
-  if (k <= 0 || k > 4096 || (lab == nullptr && k != 1) || (dtype != 1 && dtype != 2))
-    return (int)hipErrorInvalidValue;
+  if (k <= 0 || k > 4096 || (lab == nullptr && k != 1) || (dtype != 1 && dtype != 2)) return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
-  const dim3 grid(grid_for(n, kThreads * 16LL, 2048)), block(kThreads);
   if (lab == nullptr) {
-    if (dtype == 1)
-      hipLaunchKernelGGL(fixsum_kernel<float>, grid, block, 0, st, (const float*)v, n, bound, mul, limbs);
+    // at most 256 values per thread (sums < 2^54), ~8 per thread where the grid allows
+    long long g = (n + kThreads * 8LL - 1) / (kThreads * 8LL);
+    const long long gmin = (n + kThreads * 256LL - 1) / (kThreads * 256LL);
+    g = g > 4096 ? 4096 : g;
+    g = g < gmin ? gmin : g;
+    if (g > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+    if (dtype == 1 && (reinterpret_cast<size_t>(v) & 15) == 0)
+      hipLaunchKernelGGL((fixsum_kernel<float, true>), dim3((unsigned)g), dim3(kThreads), 0, st, (const float*)v, n,
+                         bound, mul, limbs);
+    else if (dtype == 1)
+      hipLaunchKernelGGL((fixsum_kernel<float, false>), dim3((unsigned)g), dim3(kThreads), 0, st, (const float*)v, n,
+                         bound, mul, limbs);
     else
-      hipLaunchKernelGGL(fixsum_kernel<double>, grid, block, 0, st, (const double*)v, n, bound, mul, limbs);
+      hipLaunchKernelGGL((fixsum_kernel<double, false>), dim3((unsigned)g), dim3(kThreads), 0, st, (const double*)v, n,
+                         bound, mul, limbs);
     return cml_status();
   }
-  const size_t lds = (size_t)2 * k * sizeof(long long);
+  // at most kBlockValues values per block (its label sums < 2^62), and ~1024 blocks where there are rows for them
+  long long g = (n + kBlockValues - 1) / kBlockValues;
+  const long long want = (n + 255) / 256 < 1024 ? (n + 255) / 256 : 1024;
+  if (g < want) g = want;
+  if (g > 0x7fffffffLL) return (int)hipErrorInvalidValue;
+  const size_t lds = (size_t)k * sizeof(long long);
   if (dtype == 1)
-    hipLaunchKernelGGL(fixsum_label_kernel<float>, grid, block, lds, st, lab, (const float*)v, n, k, bound, mul,
-                       limbs);
+    hipLaunchKernelGGL(fixsum_label_kernel<float>, dim3((unsigned)g), dim3(kThreads), lds, st, lab, (const float*)v, n, k,
+                       bound, mul, limbs);
   else
-    hipLaunchKernelGGL(fixsum_label_kernel<double>, grid, block, lds, st, lab, (const double*)v, n, k, bound, mul,
-                       limbs);
+    hipLaunchKernelGGL(fixsum_label_kernel<double>, dim3((unsigned)g), dim3(kThreads), lds, st, lab, (const double*)v, n,
+                       k, bound, mul, limbs);
   return cml_status();
 }
 
