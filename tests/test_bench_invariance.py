@@ -101,7 +101,13 @@ def test_fixsum_exact_and_split_invariant():
     parts = torch.zeros(2, dtype=torch.int64, device=dev)
     for a, b in zip(cuts[:-1], cuts[1:]):
         parts += K.fixsum(v[a:b].contiguous(), b - a, bound, 1.0)
-    assert torch.equal(whole, parts)
+    # the limbs are not canonical (where a sum is split into 31-bit limbs depends on the partition), their value
+    # hi·2^31 + lo is — and so is the finalized f64
+    def val(lm, j=0, k=1):
+        lm = lm.cpu().tolist()
+        return lm[k + j] * 2 ** 31 + lm[j]
+    assert val(whole) == val(parts)
+    assert torch.equal(K.fixsum_finalize(whole, 1, bound), K.fixsum_finalize(parts, 1, bound))
     tot = float(K.fixsum_finalize(whole, 1, bound)[0])
     exact = math.fsum(v64.cpu().tolist())
     assert abs(tot - exact) <= 1e-13 * exact
@@ -109,7 +115,8 @@ def test_fixsum_exact_and_split_invariant():
     lp = torch.zeros(74, dtype=torch.int64, device=dev)
     for a, b in zip(cuts[:-1], cuts[1:]):
         lp += K.fixsum(v64[a:b].contiguous(), b - a, bound, 1.0, lab=lab[a:b].contiguous(), k=37)
-    assert torch.equal(lw, lp)
+    assert all(val(lw, j, 37) == val(lp, j, 37) for j in range(37))
+    assert torch.equal(K.fixsum_finalize(lw, 37, bound), K.fixsum_finalize(lp, 37, bound))
     q = K.fixsum_finalize(lw, 37, bound).cpu()
     for j in (0, 17, 36):
         ex = math.fsum(v64[lab == j].cpu().tolist())
