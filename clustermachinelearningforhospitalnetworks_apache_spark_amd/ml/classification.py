@@ -297,6 +297,10 @@ class LogisticRegressionModel(Model):
             return raw, prob
         W = torch.as_tensor(self._W, device=dev)
         b = torch.as_tensor(self._b, device=dev)
+        if x.is_cuda:  # K13t: one pass, f64 MFMAs (bf16 / f32 rows, d <= 256, C <= 64)
+            out = glm_ops.multinomial_predict(x, d, torch.cat([W, b[:, None]], 1))
+            if out is not None:
+                return out
         # row chunks: the C-class margins without an f64 copy of the whole feature matrix
         raw = torch.empty((x.shape[0], W.shape[0]), dtype=torch.float64, device=dev)
         for r0 in range(0, int(x.shape[0]), 1 << 20):

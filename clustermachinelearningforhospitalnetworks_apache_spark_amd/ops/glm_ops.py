@@ -28,6 +28,9 @@ _native.register_kernel_sigs({
     "cml_multinomial_mfma_supported": (c_int, [c_int, c_int, c_int]),
     "cml_multinomial_mfma_grid": (c_int, [c_ll, c_int]),
     "cml_multinomial_mfma_dpad": (c_int, [c_int, c_int]),
+    "cml_multinomial_mfma_set_mode": (c_int, [c_int]),
+    "cml_multinomial_predict_lds": (c_ll, [c_int, c_int, c_int]),
+    "cml_multinomial_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_multinomial_mfma_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
     "cml_glm_loss_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
@@ -219,13 +222,16 @@ def loss_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor, weig
 
 
 def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor,
-                     weight: Optional[torch.Tensor] = None, chunk_rows: int = 1 << 20) -> torch.Tensor:
+                     weight: Optional[torch.Tensor] = None, chunk_rows: int = 1 << 20,
+                     prefer_valu: bool = False) -> torch.Tensor:
     """Softmax (multinomial logistic) loss + gradient over the local shard: ``coef`` [C, d+1] (last column
     the intercepts) in the original feature space, labels 0..C-1 (f64). Returns the float64 sums
-    [∇W (C·d, row-major) | ∇b (C) | loss | weight sum]. GPU rows run K13m (multinomial_grad_kernel: X read
-    once, gradient partials in f64, fixed-order reduction) where the layout fits (C <= 8, d up to 512 bf16),
-    and its MFMA form for 9..64 classes on bf16 rows with d <= 256, d % 8 == 0 (glm_mfma.hip: both products on
-    v_mfma_f32_32x32x2_f32); otherwise — and on the CPU — row chunks in f64 (never an f64 copy of the whole X)."""
+    [∇W (C·d, row-major) | ∇b (C) | loss | weight sum]. GPU rows run K13m's MFMA form for C <= 64 on bf16 rows
+    with d <= 256, d % 8 == 0 (glm_mfma.hip: both products on
+    v_mfma_f32_32x32x16_bf16 with the f32 operand — weights, residuals — split into three bf16 terms, so f32
+    precision; ``set_multinomial_mfma_mode(1)`` selects the v_mfma_f32_32x32x2_f32 form), else the VALU kernel
+    (multinomial_grad_kernel: X read once, gradient partials in f64, fixed-order reduction) where its layout fits
+    (C <= 8, d up to 512; also ``prefer_valu=True``); otherwise — and on the CPU — row chunks in f64 (never an f64 copy of the whole X)."""
     C = int(coef.shape[0])
     n = int(x.shape[0])
     coef = coef.to(device=x.device, dtype=torch.float64).contiguous()
@@ -233,6 +239,11 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
         xx = _prep(x)
         code = _CODE[xx.dtype]
         k = _native.kernels()
+        cp = k.cml_multinomial_mfma_supported(d, code, C)
+        if cp > 0 and not prefer_valu:
+            # bf16 rows, d % 8 == 0, d <= 256: the MFMA form for every C <= 64 (at C = 4 and 8 too: 17.5 ms vs
+            # 32 / 56 ms for the VALU kernel over 100M x 256, profiles/r6/multinomial_100Mx256_bf16.log)
+            return _multinomial_mfma(xx, d, y, coef, weight, C, cp, int(k.cml_multinomial_mfma_dpad(d, C)))
         if k.cml_multinomial_supported(d, code, C) > 0:
             g = k.cml_multinomial_grid(n, d, code, C, num_cus(xx.device.index or 0))
             m = C * d + C + 2
@@ -244,9 +255,7 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
                                         _native.stream_ptr())
             _native.check(st, "multinomial_grad")
             return partial_colsum(out)
-        cp = k.cml_multinomial_mfma_supported(d, code, C)
         if cp > 0:
-            # 9..64 classes on bf16 rows: both products on MFMA (glm_mfma.hip); padded [cp, dp] gradient slots
             return _multinomial_mfma(xx, d, y, coef, weight, C, cp, int(k.cml_multinomial_mfma_dpad(d, C)))
     W, b = coef[:, :d], coef[:, d]
     gW = torch.zeros((C, d), dtype=torch.float64, device=x.device)
@@ -268,6 +277,34 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
         gb += R.sum(0)
         wsum += ww.sum()
     return torch.cat([gW.reshape(-1), gb, loss.reshape(1), wsum.reshape(1)])
+
+
+def multinomial_predict(x: torch.Tensor, d: int, coef: torch.Tensor):
+    """K13t (glm_mfma.hip): the multinomial model's raw margins X·Wᵀ + b and softmax probabilities, f64 [n, C]
+    each, in one pass over bf16 / f32 GPU rows (f64 MFMAs; d <= 256, C <= 64). None where unsupported (the
+    caller's f64 chunk path then runs)."""
+    if not x.is_cuda or x.dtype not in (torch.bfloat16, torch.float32) or x.dim() != 2:
+        return None
+    C = int(coef.shape[0])
+    code = _CODE[x.dtype]
+    k = _native.kernels()
+    if k.cml_multinomial_predict_lds(d, code, C) <= 0:
+        return None
+    xx = _prep(x)
+    n = int(xx.shape[0])
+    cf = coef.to(device=x.device, dtype=torch.float64).contiguous()
+    raw = torch.empty((n, C), dtype=torch.float64, device=x.device)
+    prob = torch.empty((n, C), dtype=torch.float64, device=x.device)
+    _native.check(k.cml_multinomial_predict(xx.data_ptr(), n, xx.stride(0), d, code, C, cf.data_ptr(), raw.data_ptr(),
+                                            prob.data_ptr(), num_cus(x.device.index or 0), _native.stream_ptr()),
+                  "multinomial_predict")
+    return raw, prob
+
+
+def set_multinomial_mfma_mode(mode: int) -> int:
+    """K13m MFMA form: 0 = bf16 three-term products (default), 1 = f32 MFMAs, 2 = bf16 with W split in
+    registers on every use (A/B). Returns the previous mode."""
+    return int(_native.kernels().cml_multinomial_mfma_set_mode(int(mode)))
 
 
 def _multinomial_mfma(xx: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tensor, weight, C: int, cp: int,

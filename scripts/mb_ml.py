@@ -286,6 +286,14 @@ def cmd_tree_transform(argv):
     timed("DecisionTreeClassificationModel.transform", lambda: dtc.transform(cte))
 
 
+def _mode_run(mode, x, d, y, coef, C, cp, dp):
+    prev = glm_ops.set_multinomial_mfma_mode(mode)
+    try:
+        return glm_ops._multinomial_mfma(x, d, y, coef, None, C, cp, dp)
+    finally:
+        glm_ops.set_multinomial_mfma_mode(prev)
+
+
 def cmd_multinomial(argv):
     ap = argparse.ArgumentParser(prog="mb_ml.py multinomial")
     ap.add_argument("--rows", type=int, default=100_000_000)
@@ -302,12 +310,26 @@ def cmd_multinomial(argv):
     for C in (4, 8, 16, 32, 64):
         y = torch.randint(0, C, (n,), generator=g, device=dev).to(torch.float64)
         coef = torch.randn(C, d + 1, generator=g, device=dev, dtype=torch.float64) * 0.05
-        ms = best_ms(lambda: glm_ops.multinomial_grad(x, d, y, coef), reps=3)
-        form = "valu" if lib.cml_multinomial_supported(d, 0, C) > 0 else (
-            "mfma" if lib.cml_multinomial_mfma_supported(d, 0, C) > 0 else "torch-chunks")
         flop = 4.0 * n * d * (32 if C <= 32 else 64)  # MFMA form: margins + gradient on the padded class tile
-        print(f"multinomial {n}x{d} bf16 C={C:2d} [{form}]: {ms:8.3f} ms, {n * d * 2 / ms / 1e9:6.2f} TB/s rows"
-              + (f", {flop / ms / 1e9:7.1f} TFLOP/s (f32 MFMA)" if form == "mfma" else ""), flush=True)
+        runs = []
+        if lib.cml_multinomial_supported(d, 0, C) > 0:
+            runs.append(("valu", lambda: glm_ops.multinomial_grad(x, d, y, coef, prefer_valu=True)))
+        cp = lib.cml_multinomial_mfma_supported(d, 0, C)
+        if cp > 0:  # every MFMA form (mode 0, the first, is the default route)
+            dp = lib.cml_multinomial_mfma_dpad(d, C)
+            for mode, name in ((0, "mfma-bf16x3"), (2, "mfma-bf16x3-regsplit"), (1, "mfma-f32")):
+                runs.append((name, (lambda m: lambda: _mode_run(m, x, d, y, coef, C, cp, dp))(mode)))
+        if not runs:
+            runs.append(("torch-chunks", lambda: glm_ops.multinomial_grad(x, d, y, coef)))
+        if lib.cml_multinomial_predict_lds(d, 0, C) > 0:  # K13t: transform (raw + probability, f64 [n, C] each)
+            ms = best_ms(lambda: glm_ops.multinomial_predict(x, d, coef), reps=3)
+            byts = n * d * 2 + 2 * n * C * 8
+            print(f"multinomial transform {n}x{d} bf16 C={C:2d} [K13t f64 mfma]: {ms:8.3f} ms, "
+                  f"{byts / ms / 1e9:6.2f} TB/s (rows in + raw/prob out)", flush=True)
+        for name, fn in runs:
+            ms = best_ms(fn, reps=3)
+            print(f"multinomial {n}x{d} bf16 C={C:2d} [{name}]: {ms:8.3f} ms, {n * d * 2 / ms / 1e9:6.2f} TB/s rows"
+                  + (f", {flop / ms / 1e9:7.1f} useful TFLOP/s" if name.startswith("mfma") else ""), flush=True)
         del y
 
 

@@ -81,9 +81,67 @@ def test_kernel_matches_f64_oracle(dt, d, C):
     code = glm_ops._CODE[dt]
     assert lib.cml_multinomial_supported(d, code, C) > 0 or lib.cml_multinomial_mfma_supported(d, code, C) > 0
     got = glm_ops.multinomial_grad(x, d, y, coef, w)
+    if C <= 8 and lib.cml_multinomial_supported(d, code, C) > 0:  # the VALU kernel too where MFMA is the default
+        valu = glm_ops.multinomial_grad(x, d, y, coef, w, prefer_valu=True)
+        tolv = 1e-9 if dt == torch.float64 else 2e-5
+        np.testing.assert_allclose(valu.cpu().numpy(), got.cpu().numpy(), rtol=tolv, atol=tolv * float(got.abs().max()))
     ref = glm_ops.multinomial_grad(x.float().cpu().to(torch.float64) if dt != torch.float64 else x.cpu(), d,
                                    y.cpu(), coef.cpu(), w.cpu())
     tol = 1e-9 if dt == torch.float64 else 2e-5
     np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=tol, atol=tol * float(ref.abs().max()))
     again = glm_ops.multinomial_grad(x, d, y, coef, w)
     assert torch.equal(got, again)  # fixed-order partials: bitwise repeatable
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("mode", [0, 1, 2])
+@pytest.mark.parametrize("d,C", [(256, 32), (200, 40), (256, 64), (64, 9)])
+def test_mfma_forms_match_f64_oracle(mode, d, C):
+    """The three K13m MFMA forms (bf16 three-term products with W split once in LDS or in registers, and the
+    f32 MFMAs) each match the f64 oracle to f32 precision."""
+    g = torch.Generator(device="cuda").manual_seed(7 * d + C)
+    n = 100_003
+    x = (torch.randn(n, d, generator=g, device="cuda") * 2).to(torch.bfloat16)
+    y = torch.randint(0, C, (n,), generator=g, device="cuda").double()
+    coef = torch.randn(C, d + 1, generator=g, device="cuda", dtype=torch.float64) * 0.2
+    prev = glm_ops.set_multinomial_mfma_mode(mode)
+    try:
+        got = glm_ops.multinomial_grad(x, d, y, coef)
+    finally:
+        glm_ops.set_multinomial_mfma_mode(prev)
+    ref = glm_ops.multinomial_grad(x.float().cpu().to(torch.float64), d, y.cpu(), coef.cpu())
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=2e-5, atol=2e-5 * float(ref.abs().max()))
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("dt,d,C", [(torch.bfloat16, 256, 32), (torch.float32, 37, 5), (torch.bfloat16, 200, 64),
+                                    (torch.float32, 256, 17), (torch.bfloat16, 8, 3), (torch.bfloat16, 130, 48)])
+def test_predict_kernel_matches_f64(dt, d, C):
+    """K13t (multinomial transform on f64 MFMAs) against the f64 margins / softmax of the same rows."""
+    g = torch.Generator(device="cuda").manual_seed(3 * d + C)
+    n = 50_003
+    x = (torch.randn(n, d, generator=g, device="cuda") * 2).to(dt)
+    coef = torch.randn(C, d + 1, generator=g, device="cuda", dtype=torch.float64) * 0.2
+    out = glm_ops.multinomial_predict(x, d, coef)
+    assert out is not None
+    raw, prob = out
+    ref = x.to(torch.float64) @ coef[:, :d].T + coef[:, d]
+    np.testing.assert_allclose(raw.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(prob.cpu().numpy(), torch.softmax(ref, 1).cpu().numpy(), rtol=1e-11, atol=1e-14)
+
+
+@pytest.mark.gpu
+def test_multinomial_model_transform_uses_kernel():
+    """LogisticRegressionModel (multinomial) transform on GPU rows: the K13t path gives the f64 chunk path's
+    predictions."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.ml.classification import LogisticRegressionModel
+    g = torch.Generator(device="cuda").manual_seed(5)
+    n, d, C = 20_000, 64, 7
+    x = torch.randn(n, d, generator=g, device="cuda").to(torch.bfloat16)
+    W = torch.randn(C, d, generator=g, dtype=torch.float64, device="cuda").cpu().numpy()
+    b = torch.randn(C, generator=g, dtype=torch.float64, device="cuda").cpu().numpy()
+    m = LogisticRegressionModel(W, b, numClasses=C, isMultinomial=True)
+    raw, prob = m._scores(x)
+    ref = x.to(torch.float64) @ torch.as_tensor(W, device="cuda").T + torch.as_tensor(b, device="cuda")
+    np.testing.assert_allclose(raw.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12, atol=1e-12)
+    assert torch.equal(m._predict_from_prob(prob), torch.argmax(torch.softmax(ref, 1), 1).double())
