@@ -82,6 +82,7 @@ profile)
   python3 scripts/prof.py stats /tmp/pf/pf_results.db --marker row_pass_kernel --index 1 --top 40 \
     > "$O/kernel_stats_timed_fit.txt"
   head -30 "$O/kernel_stats.txt"
+  [ -z "$KEEPDB" ] || cp /tmp/pf/pf_results.db "$O/"  # KEEPDB=1: the trace itself, for scripts/prof.py here
   ;;
 shard)
   export CML_COMM_SELF=1
