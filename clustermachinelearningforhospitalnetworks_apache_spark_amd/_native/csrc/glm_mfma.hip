@@ -583,6 +583,225 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
   }
 }
 
+// C <= 16: a 16-class tile on v_mfma_f32_16x16x32_bf16 (16 cycles, half the work of a 32x32x16 MFMA): the
+// 32-class tile above spends half its MFMAs on padded classes there. Same algorithm and bf16 x3 split; the
+// shapes (lane l: A[i = l&15][k = 8(l>>4) + j], B[k = 8(l>>4) + j][col l&15], C/D col = l&15, row = 4(l>>4) + reg):
+//   margins  Mᵀ[16 classes][16 rows] per 16-row half u of the 32-row tile: A = W (presplit planes), B = X rows
+//            (one 16-byte read); a lane holds 4 classes of ONE row: the softmax is 4 registers plus two
+//            exchanges (lanes l ^ 16, l ^ 32)
+//   gradient G[16 classes][16 features] per feature tile t, k = the tile's 32 rows: A = R through the per-wave
+//            [row][class] image (ds_read_b64_tr_b16, 32-byte rows), B = X via transposed reads of the X image
+template <int FT>
+__global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
+    const u16* __restrict__ X, long long n, long long ld, int d, int C, const double* __restrict__ y,
+    const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1]*/, double* __restrict__ out) {
+  constexpr int CP = 16;
+  constexpr int DP = 32 * FT;
+  constexpr int BP = DP + 8;                       // split-W pitch (bf16 elements)
+  constexpr size_t WBYTES = (size_t)3 * CP * BP * 2;
+  constexpr int XIMG = ((DP + 127) / 128) * 8192;  // bytes per wave
+  constexpr int RPLANE = 32 * 16;                  // residual plane: [32 rows][16 classes] bf16
+  constexpr int NCHUNK = DP / 8;
+  constexpr int LCH = 32 * NCHUNK / 64;
+  constexpr int NT = DP / 16;                      // 16-feature gradient tiles
+  extern __shared__ __align__(16) unsigned char smem[];
+  __bf16* wb = reinterpret_cast<__bf16*>(smem);                  // [3][CP][BP] hi, mid, lo
+  float* bias_l = reinterpret_cast<float*>(smem + WBYTES);       // [CP], -inf on padded classes
+  const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, r16 = lane & 15, g4 = lane >> 4;
+  unsigned char* xim = smem + WBYTES + CP * 4 + (size_t)wave * XIMG;
+  __bf16* rim = reinterpret_cast<__bf16*>(smem + WBYTES + CP * 4 + 4 * (size_t)XIMG) + (size_t)wave * 3 * RPLANE;
+  double* part = out + (long long)blockIdx.x * (CP * DP + C + 2);
+  for (int i = tid; i < CP * BP; i += kMnThreads) {
+    const int c = i / BP, k = i - c * BP;
+    const float w = (c < C && k < d) ? (float)coef[(long long)c * (d + 1) + k] : 0.f;
+    const __bf16 hi = (__bf16)w;
+    const float r1 = w - (float)hi;
+    const __bf16 mid = (__bf16)r1;
+    wb[i] = hi;
+    wb[CP * BP + i] = mid;
+    wb[2 * CP * BP + i] = (__bf16)(r1 - (float)mid);
+  }
+  for (int c = tid; c < CP; c += kMnThreads) bias_l[c] = c < C ? (float)coef[(long long)c * (d + 1) + d] : -__builtin_huge_valf();
+  for (int i = tid; i < CP * DP + C + 2; i += kMnThreads) part[i] = 0.0;
+  __syncthreads();
+  f32x4 G[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) G[t] = (f32x4)0.f;
+  float gbr[4] = {0.f, 0.f, 0.f, 0.f};
+  double loss = 0.0, wsum = 0.0;
+
+  const long long ntiles = (n + 31) / 32;
+  const long long ngroups = (ntiles + 3) / 4;
+  uint4 xr[LCH];
+  double ynext[2] = {0.0, 0.0}, wnext[2] = {0.0, 0.0};  // the next tile's labels / weights of rows 16u + r16
+  auto load_tile = [&](long long tile) {
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const long long yrow = tile * 32 + 16 * u + r16;
+      ynext[u] = yrow < n ? y[yrow] : 0.0;
+      wnext[u] = yrow < n ? (wt != nullptr ? wt[yrow] : 1.0) : 0.0;
+    }
+    if (tile * 32 + 32 <= n && d == DP) {
+      const u16* base = X + tile * 32 * ld;
+#pragma unroll
+      for (int i = 0; i < LCH; ++i) {
+        const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
+        xr[i] = *reinterpret_cast<const uint4*>(base + r * ld + ch * 8);
+      }
+      return;
+    }
+#pragma unroll
+    for (int i = 0; i < LCH; ++i) {
+      const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
+      const long long row = tile * 32 + r;
+      if (row < n && ch * 8 < d)
+        xr[i] = *reinterpret_cast<const uint4*>(X + row * ld + ch * 8);
+      else
+        xr[i] = make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  const __bf16* wa = wb + r16 * BP + 8 * g4;        // W[class r16][32s + 8 g4 + j]
+  const int trq = (lane >> 2) & 3, trp = lane & 3;  // transposed reads: lane 4q + p of its 16-lane group
+
+  long long g = blockIdx.x;
+  if (g < ngroups) load_tile(4 * g + wave);
+  for (; g < ngroups; g += gridDim.x) {
+    const long long tile = 4 * g + wave;
+#pragma unroll
+    for (int i = 0; i < LCH; ++i) {
+      const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
+      *reinterpret_cast<uint4*>(xim + ximg_off(r, ch)) = xr[i];
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    const double yv[2] = {ynext[0], ynext[1]}, wv[2] = {wnext[0], wnext[1]};
+    if (g + gridDim.x < ngroups) load_tile(4 * (g + gridDim.x) + wave);
+    // margins Mᵀ[class 4 g4 + reg][row 16u + r16] = bias + W·Xᵀ
+    f32x4 M[2];
+    {
+      const float4 b = *reinterpret_cast<const float4*>(bias_l + 4 * g4);
+      M[0] = f32x4{b.x, b.y, b.z, b.w};
+      M[1] = M[0];
+    }
+    __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+    for (int s = 0; s < DP / 32; ++s) {
+      const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + 32 * s));
+      const bf16x8 am = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + CP * BP + 32 * s));
+      const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + 2 * CP * BP + 32 * s));
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {
+        const bf16x8 xb =
+            __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xim + ximg_off(16 * u + r16, 4 * s + g4)));
+        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb, M[u], 0, 0, 0);
+        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, xb, M[u], 0, 0, 0);
+        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb, M[u], 0, 0, 0);
+      }
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // softmax over the 16 classes of row 16u + r16 (4 registers x lanes r16, r16 + 16, + 32, + 48)
+#pragma unroll
+    for (int u = 0; u < 2; ++u) {
+      const bool ok = tile * 32 + 16 * u + r16 < n;
+      const int yc = (int)yv[u];
+      float mx = fmaxf(fmaxf(M[u][0], M[u][1]), fmaxf(M[u][2], M[u][3]));
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float se = 0.f, my = 0.f, e[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        my += (4 * g4 + r == yc) ? M[u][r] : 0.f;
+        e[r] = __expf(M[u][r] - mx);  // padded classes: margin -inf (bias), e = 0
+        se += e[r];
+      }
+      se += __shfl_xor(se, 16, 64);
+      se += __shfl_xor(se, 32, 64);
+      my += __shfl_xor(my, 16, 64);
+      my += __shfl_xor(my, 32, 64);
+      const float inv = 1.f / se, wf32 = (float)wv[u];
+      float rr[4];
+#pragma unroll
+      for (int r = 0; r < 4; ++r) {
+        rr[r] = wf32 * (e[r] * inv - (4 * g4 + r == yc ? 1.f : 0.f));
+        gbr[r] += rr[r];
+      }
+      if (g4 == 0 && ok) {
+        loss += wv[u] * (((double)mx + (double)__logf(se)) - (double)my);
+        wsum += wv[u];
+      }
+      // residual row 16u + r16, classes 4 g4 .. 4 g4 + 3 -> the three bf16 planes of the [row][class] image
+      __bf16 hi[4], mi[4], lo[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        hi[j] = (__bf16)rr[j];
+        const float r1 = rr[j] - (float)hi[j];
+        mi[j] = (__bf16)r1;
+        lo[j] = (__bf16)(r1 - (float)mi[j]);
+      }
+      const int o = (16 * u + r16) * 16 + 4 * g4;
+      *reinterpret_cast<uint2*>(rim + o) = make_uint2(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]));
+      *reinterpret_cast<uint2*>(rim + RPLANE + o) = make_uint2(pack_bf16(mi[0], mi[1]), pack_bf16(mi[2], mi[3]));
+      *reinterpret_cast<uint2*>(rim + 2 * RPLANE + o) = make_uint2(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]));
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+    // gradient: G[t] += R[class][rows 0..31] · X[rows][features 16t ..]; group g4 of a transposed read takes
+    // rows 8 g4 + 4 rd + q
+    {
+      const int r0 = 8 * g4 + trq;
+      const unsigned char* ra = reinterpret_cast<const unsigned char*>(rim);
+      const int oa0 = 2 * (r0 * 16 + 4 * trp), oa1 = 2 * ((r0 + 4) * 16 + 4 * trp);
+      const bf16x8 ah = tr_frag(ra + oa0, ra + oa1);
+      const bf16x8 am = tr_frag(ra + 2 * RPLANE + oa0, ra + 2 * RPLANE + oa1);
+      const bf16x8 al = tr_frag(ra + 4 * RPLANE + oa0, ra + 4 * RPLANE + oa1);
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        const int ch = 2 * t + (trp >> 1);
+        const bf16x8 bx = tr_frag(xim + ximg_off(r0, ch) + 8 * (trp & 1), xim + ximg_off(r0 + 4, ch) + 8 * (trp & 1));
+        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx, G[t], 0, 0, 0);
+        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx, G[t], 0, 0, 0);
+        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bx, G[t], 0, 0, 0);
+      }
+    }
+    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+    __builtin_amdgcn_wave_barrier();
+  }
+  // bias gradient: each register's class summed over the 16 rows of the lane group
+#pragma unroll
+  for (int r = 0; r < 4; ++r)
+#pragma unroll
+    for (int o = 1; o < 16; o <<= 1) gbr[r] += __shfl_xor(gbr[r], o, 64);
+  loss = wave_sum_f64(loss);
+  wsum = wave_sum_f64(wsum);
+  double* pg = part + (4 * g4) * DP + r16;
+#pragma unroll 1
+  for (int w = 0; w < 4; ++w) {
+    if (wave == w) {
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+#pragma unroll
+        for (int r = 0; r < 4; ++r) pg[r * DP + 16 * t] += (double)G[t][r];
+        __builtin_amdgcn_sched_barrier(0);
+      }
+      if (r16 == 0)
+#pragma unroll
+        for (int r = 0; r < 4; ++r)
+          if (4 * g4 + r < C) part[CP * DP + 4 * g4 + r] += (double)gbr[r];
+      if (lane == 0) {
+        part[CP * DP + C] += loss;
+        part[CP * DP + C + 1] += wsum;
+      }
+    }
+    __syncthreads();
+  }
+}
+
+template <int FT>
+constexpr size_t mnc16_lds() {
+  return (size_t)3 * 16 * (32 * FT + 8) * 2 + 16 * 4 + (size_t)4 * ((32 * FT + 127) / 128) * 8192 +
+         (size_t)4 * 3 * 32 * 16 * 2;
+}
+
 template <int CT, int FT, bool PRESPLIT>
 constexpr size_t mn16_lds() {
   return (PRESPLIT ? (size_t)3 * 32 * CT * (32 * FT + 8) * 2 : (size_t)32 * CT * (32 * FT + 4) * 4) + 32 * CT * 4 +
@@ -599,12 +818,15 @@ size_t mn_lds() {
 
 int g_mn_f32 = 0;      // 1: the f32-MFMA form (A/B and precision reference)
 int g_mn_nosplit = 0;  // 1: split W on the fly also where the three bf16 planes fit in LDS (A/B)
-// mode: 0 = bf16 three-term MFMAs (default), 1 = f32 MFMAs, 2 = bf16 with W split on the fly; -1 = query
+int g_mn_no16 = 0;     // 1: C <= 16 on the 32-class tile too (A/B of multinomial_c16_kernel)
+// mode: 0 = bf16 three-term MFMAs (default; C <= 16 on the 16-class tile), 1 = f32 MFMAs, 2 = bf16 with W split
+// on the fly, 3 = mode 0 on the 32-class tile for every C; -1 = query
 CML_API int cml_multinomial_mfma_set_mode(int mode) {
-  const int prev = g_mn_f32 ? 1 : (g_mn_nosplit ? 2 : 0);
+  const int prev = g_mn_f32 ? 1 : (g_mn_nosplit ? 2 : (g_mn_no16 ? 3 : 0));
   if (mode >= 0) {
     g_mn_f32 = mode == 1;
     g_mn_nosplit = mode == 2;
+    g_mn_no16 = mode == 3;
   }
   return prev;
 }
@@ -613,6 +835,7 @@ CML_API int cml_multinomial_mfma_set_mode(int mode) {
 // Returns the class-slot count CP (32 / 64) or 0.
 CML_API int cml_multinomial_mfma_supported(int d, int dtype, int C) {
   if (dtype != 0 || d < 8 || d % 8 != 0 || d > 256 || C < 2 || C > 64) return 0;
+  if (C <= 16 && !g_mn_f32 && !g_mn_nosplit && !g_mn_no16) return 16;  // multinomial_c16_kernel
   return C <= 32 ? 32 : 64;
 }
 
@@ -629,6 +852,7 @@ CML_API int cml_multinomial_mfma_grid(long long n, int ncu) {
 // Padded width DP the partials use: 32·ceil(d / 32), for C > 32 and d > 128 rounded up to 192 / 256.
 CML_API int cml_multinomial_mfma_dpad(int d, int C) {
   int ft = (d + 31) / 32;
+  if (cml_multinomial_mfma_supported(d, 0, C) == 16) return 32 * ft;
   if (C > 32 && ft > 4) ft = ft <= 6 ? 6 : 8;
   return 32 * ft;
 }
@@ -642,6 +866,20 @@ CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, 
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   int ft = (d + 31) / 32;
+  if (cml_multinomial_mfma_supported(d, 0, C) == 16) {
+#define CML_MNC(FTV)                                                                                           \
+    if (ft == FTV) {                                                                                           \
+      constexpr size_t lds = mnc16_lds<FTV>();                                                                 \
+      hipFuncSetAttribute((const void*)multinomial_c16_kernel<FTV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
+                          (int)lds);                                                                           \
+      hipLaunchKernelGGL((multinomial_c16_kernel<FTV>), dim3(grid), dim3(kMnThreads), lds, st, (const u16*)X, n, \
+                         ld, d, C, y, wt, coef, out);                                                          \
+      return cml_status();                                                                                     \
+    }
+    CML_MNC(1) CML_MNC(2) CML_MNC(3) CML_MNC(4) CML_MNC(5) CML_MNC(6) CML_MNC(7) CML_MNC(8)
+#undef CML_MNC
+    return (int)hipErrorInvalidValue;
+  }
   const int ct = C <= 32 ? 1 : 2;
   if (ct == 2 && ft > 4) ft = ft <= 6 ? 6 : 8;  // padded to two launches of FT / 2 gradient tiles
   const u16* x = (const u16*)X;

@@ -289,6 +289,8 @@ def cmd_tree_transform(argv):
 def _mode_run(mode, x, d, y, coef, C, cp, dp):
     prev = glm_ops.set_multinomial_mfma_mode(mode)
     try:
+        lib = glm_ops._native.kernels()
+        cp, dp = lib.cml_multinomial_mfma_supported(d, 0, C), lib.cml_multinomial_mfma_dpad(d, C)
         return glm_ops._multinomial_mfma(x, d, y, coef, None, C, cp, dp)
     finally:
         glm_ops.set_multinomial_mfma_mode(prev)
@@ -310,14 +312,18 @@ def cmd_multinomial(argv):
     for C in (4, 8, 16, 32, 64):
         y = torch.randint(0, C, (n,), generator=g, device=dev).to(torch.float64)
         coef = torch.randn(C, d + 1, generator=g, device=dev, dtype=torch.float64) * 0.05
-        flop = 4.0 * n * d * (32 if C <= 32 else 64)  # MFMA form: margins + gradient on the padded class tile
+        # MFMA form: margins + gradient on the padded class tile (16, 32 or 64 classes)
+        flop = 4.0 * n * d * (16 if C <= 16 else 32 if C <= 32 else 64)
         runs = []
         if lib.cml_multinomial_supported(d, 0, C) > 0:
             runs.append(("valu", lambda: glm_ops.multinomial_grad(x, d, y, coef, prefer_valu=True)))
         cp = lib.cml_multinomial_mfma_supported(d, 0, C)
         if cp > 0:  # every MFMA form (mode 0, the first, is the default route)
             dp = lib.cml_multinomial_mfma_dpad(d, C)
-            for mode, name in ((0, "mfma-bf16x3"), (2, "mfma-bf16x3-regsplit"), (1, "mfma-f32")):
+            for mode, name in ((0, "mfma-bf16x3"), (3, "mfma-bf16x3-32tile"), (2, "mfma-bf16x3-regsplit"),
+                               (1, "mfma-f32")):
+                if mode == 3 and C > 16:
+                    continue
                 runs.append((name, (lambda m: lambda: _mode_run(m, x, d, y, coef, C, cp, dp))(mode)))
         if not runs:
             runs.append(("torch-chunks", lambda: glm_ops.multinomial_grad(x, d, y, coef)))
