@@ -861,7 +861,7 @@ CML_API int cml_multinomial_mfma_dpad(int d, int C) {
 // (K13b: cml_partial_colsum, then the host keeps [:C, :d] of the gradient); X 16-byte aligned, ld % 8 == 0.
 CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, int d, int C, const double* y,
                                       const double* wt, const double* coef, double* out, int grid, void* stream) {
-  if (cml_multinomial_mfma_supported(d, 0, C) == 0 || grid < 1 || n < 1 || ld % 8 != 0 ||
+  if (cml_multinomial_mfma_supported(d, 0, C) == 0 || grid < 1 || n < 1 || ld % 8 != 0 || ld < d ||
       (reinterpret_cast<size_t>(X) & 15) != 0)
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
@@ -1051,6 +1051,9 @@ CML_API int cml_multinomial_predict(const void* X, long long n, long long ld, in
   const long long lds = cml_multinomial_predict_lds(d, dtype, C);
   if (lds == 0) return (int)hipErrorInvalidValue;
   if (n <= 0) return 0;
+  // the 16-byte row loads: a 16-byte aligned base and a 16-byte multiple pitch (glm_ops._prep), ld >= d
+  const long long esz = dtype == 0 ? 2 : 4;
+  if ((reinterpret_cast<size_t>(X) & 15) != 0 || (ld * esz) % 16 != 0 || ld < d) return (int)hipErrorInvalidValue;
   const int k4 = ((d + 31) / 32) * 8, cb = (C + 15) / 16;
   const long long tiles = (n + 15) / 16;
   const int per_cu = (int)((160 * 1024) / lds) > 0 ? (int)((160 * 1024) / lds) : 1;
