@@ -953,37 +953,39 @@ __global__ __launch_bounds__(kPtThreads) void multinomial_predict_kernel(const T
   const int lane = threadIdx.x & 63, wave = threadIdx.x >> 6, r16 = lane & 15, kq = lane >> 4;
   const long long ntiles = (n + 15) / 16;
   const double* wl = w + r16 * LDW + kq * K4;
-  for (long long tile = (long long)blockIdx.x * 4 + wave; tile < ntiles; tile += (long long)gridDim.x * 4) {
+  // the next tile's row segment is in flight (raw 16-byte loads) while this one is multiplied
+  constexpr int NQ = K4 * (int)sizeof(T) / 16;  // 16-byte loads per lane per tile
+  constexpr int EQ = 16 / (int)sizeof(T);       // values per load
+  uint4 xq[NQ];
+  auto load = [&](long long tile) {
     const long long row = tile * 16 + r16;
-    float xv[K4];
     const T* xr = X + row * ld + kq * K4;
-    // 16-byte loads of 8 values (rows 16-byte aligned with a 16-byte multiple pitch: the caller's _prep)
 #pragma unroll
-    for (int u = 0; u < K4 / 8; ++u) {
-      const int f0 = kq * K4 + 8 * u;
-      if (row < n && f0 < d) {
-        if constexpr (sizeof(T) == 2) {
-          const uint4 q = *reinterpret_cast<const uint4*>(xr + 8 * u);
-          const unsigned wv[4] = {q.x, q.y, q.z, q.w};
+    for (int q = 0; q < NQ; ++q) {
+      // rows 16-byte aligned with a 16-byte multiple pitch (the caller's _prep): a load that starts below d
+      // stays inside the row's pitch
+      const bool ok = row < n && kq * K4 + EQ * q < d;
+      xq[q] = ok ? *reinterpret_cast<const uint4*>(xr + EQ * q) : make_uint4(0u, 0u, 0u, 0u);
+    }
+  };
+  long long tile = (long long)blockIdx.x * 4 + wave;
+  if (tile < ntiles) load(tile);
+  for (; tile < ntiles; tile += (long long)gridDim.x * 4) {
+    float xv[K4];
 #pragma unroll
-          for (int j = 0; j < 4; ++j) {
-            xv[8 * u + 2 * j] = __uint_as_float(wv[j] << 16);
-            xv[8 * u + 2 * j + 1] = __uint_as_float(wv[j] & 0xffff0000u);
-          }
-        } else {
-          const float4 a = *reinterpret_cast<const float4*>(xr + 8 * u);
-          // f32 pitch: a multiple of 4 values, so the second half exists only where f0 + 4 < d
-          const float4 b = f0 + 4 < d ? *reinterpret_cast<const float4*>(xr + 8 * u + 4) : make_float4(0.f, 0.f, 0.f, 0.f);
-          xv[8 * u + 0] = a.x; xv[8 * u + 1] = a.y; xv[8 * u + 2] = a.z; xv[8 * u + 3] = a.w;
-          xv[8 * u + 4] = b.x; xv[8 * u + 5] = b.y; xv[8 * u + 6] = b.z; xv[8 * u + 7] = b.w;
-        }
+    for (int q = 0; q < NQ; ++q) {
+      const unsigned wv[4] = {xq[q].x, xq[q].y, xq[q].z, xq[q].w};
 #pragma unroll
-        for (int j = 0; j < 8; ++j) xv[8 * u + j] = f0 + j < d ? xv[8 * u + j] : 0.f;  // the row's pad columns
-      } else {
-#pragma unroll
-        for (int j = 0; j < 8; ++j) xv[8 * u + j] = 0.f;
+      for (int e = 0; e < EQ; ++e) {
+        float v;
+        if constexpr (sizeof(T) == 2)
+          v = __uint_as_float((e & 1) ? (wv[e >> 1] & 0xffff0000u) : (wv[e >> 1] << 16));
+        else
+          v = __uint_as_float(wv[e]);
+        xv[EQ * q + e] = kq * K4 + EQ * q + e < d ? v : 0.f;  // the row's pad columns
       }
     }
+    if (tile + (long long)gridDim.x * 4 < ntiles) load(tile + (long long)gridDim.x * 4);
     f64x4 D[CB];
 #pragma unroll
     for (int cb = 0; cb < CB; ++cb) D[cb] = (f64x4)0.0;
