@@ -591,16 +591,30 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
 //            exchanges (lanes l ^ 16, l ^ 32)
 //   gradient G[16 classes][16 features] per feature tile t, k = the tile's 32 rows: A = R through the per-wave
 //            [row][class] image (ds_read_b64_tr_b16, 32-byte rows), B = X via transposed reads of the X image
+// byte offset of 16-byte chunk ch of tile row `row` in the X image of multinomial_c16_kernel: the chunk XOR is
+// f(row) = 2·b0 ^ 4·b1 ^ 8·b2 ^ 9·b3 of the row's low bits (found by exhaustive search over linear swizzles:
+// conflict-free for both the 16x16x32 row reads of the margins — 16 rows, two column halves — and the
+// transposed gradient reads; ximg_off's XOR leaves the row reads 2-way)
+__device__ __forceinline__ int ximg16_off(int row, int ch) {
+  const int f = ((row & 7) << 1) ^ (((row >> 3) & 1) * 9);
+  return ((ch >> 4) << 13) + (row << 8) + (((ch & 15) ^ f) << 4);
+}
+// element offset of row r of a residual plane of multinomial_c16_kernel
+__device__ __forceinline__ int rimg16_off(int r) { return r * 16 + (r >> 3) * 64; }
+
 template <int FT>
 __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
     const u16* __restrict__ X, long long n, long long ld, int d, int C, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1]*/, double* __restrict__ out) {
   constexpr int CP = 16;
   constexpr int DP = 32 * FT;
-  constexpr int BP = DP + 8;                       // split-W pitch (bf16 elements)
+  constexpr int BP = DP + 16;  // split-W pitch (bf16 elements): rows 8 dwords apart mod 64, so the row reads
+                               // of a 16-lane group (rows r, column half g4) fall on distinct banks
   constexpr size_t WBYTES = (size_t)3 * CP * BP * 2;
   constexpr int XIMG = ((DP + 127) / 128) * 8192;  // bytes per wave
-  constexpr int RPLANE = 32 * 16;                  // residual plane: [32 rows][16 classes] bf16
+  // residual plane: [32 rows][16 classes] bf16, 32-byte rows, 64 elements (128 B) of padding after every 8 rows:
+  // the two 16-lane groups of a transposed read (rows 8 apart) then take different bank halves
+  constexpr int RPLANE = 4 * (8 * 16 + 64);
   constexpr int NCHUNK = DP / 8;
   constexpr int LCH = 32 * NCHUNK / 64;
   constexpr int NT = DP / 16;                      // 16-feature gradient tiles
@@ -670,7 +684,7 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
 #pragma unroll
     for (int i = 0; i < LCH; ++i) {
       const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
-      *reinterpret_cast<uint4*>(xim + ximg_off(r, ch)) = xr[i];
+      *reinterpret_cast<uint4*>(xim + ximg16_off(r, ch)) = xr[i];
     }
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -692,7 +706,7 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
 #pragma unroll
       for (int u = 0; u < 2; ++u) {
         const bf16x8 xb =
-            __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xim + ximg_off(16 * u + r16, 4 * s + g4)));
+            __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xim + ximg16_off(16 * u + r16, 4 * s + g4)));
         M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb, M[u], 0, 0, 0);
         M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, xb, M[u], 0, 0, 0);
         M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb, M[u], 0, 0, 0);
@@ -738,7 +752,7 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
         mi[j] = (__bf16)r1;
         lo[j] = (__bf16)(r1 - (float)mi[j]);
       }
-      const int o = (16 * u + r16) * 16 + 4 * g4;
+      const int o = rimg16_off(16 * u + r16) + 4 * g4;
       *reinterpret_cast<uint2*>(rim + o) = make_uint2(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]));
       *reinterpret_cast<uint2*>(rim + RPLANE + o) = make_uint2(pack_bf16(mi[0], mi[1]), pack_bf16(mi[2], mi[3]));
       *reinterpret_cast<uint2*>(rim + 2 * RPLANE + o) = make_uint2(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]));
@@ -750,14 +764,14 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
     {
       const int r0 = 8 * g4 + trq;
       const unsigned char* ra = reinterpret_cast<const unsigned char*>(rim);
-      const int oa0 = 2 * (r0 * 16 + 4 * trp), oa1 = 2 * ((r0 + 4) * 16 + 4 * trp);
+      const int oa0 = 2 * (rimg16_off(r0) + 4 * trp), oa1 = 2 * (rimg16_off(r0 + 4) + 4 * trp);
       const bf16x8 ah = tr_frag(ra + oa0, ra + oa1);
       const bf16x8 am = tr_frag(ra + 2 * RPLANE + oa0, ra + 2 * RPLANE + oa1);
       const bf16x8 al = tr_frag(ra + 4 * RPLANE + oa0, ra + 4 * RPLANE + oa1);
 #pragma unroll
       for (int t = 0; t < NT; ++t) {
         const int ch = 2 * t + (trp >> 1);
-        const bf16x8 bx = tr_frag(xim + ximg_off(r0, ch) + 8 * (trp & 1), xim + ximg_off(r0 + 4, ch) + 8 * (trp & 1));
+        const bf16x8 bx = tr_frag(xim + ximg16_off(r0, ch) + 8 * (trp & 1), xim + ximg16_off(r0 + 4, ch) + 8 * (trp & 1));
         G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx, G[t], 0, 0, 0);
         G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx, G[t], 0, 0, 0);
         G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bx, G[t], 0, 0, 0);
@@ -798,8 +812,8 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
 
 template <int FT>
 constexpr size_t mnc16_lds() {
-  return (size_t)3 * 16 * (32 * FT + 8) * 2 + 16 * 4 + (size_t)4 * ((32 * FT + 127) / 128) * 8192 +
-         (size_t)4 * 3 * 32 * 16 * 2;
+  return (size_t)3 * 16 * (32 * FT + 16) * 2 + 16 * 4 + (size_t)4 * ((32 * FT + 127) / 128) * 8192 +
+         (size_t)4 * 3 * (4 * (8 * 16 + 64)) * 2;
 }
 
 template <int CT, int FT, bool PRESPLIT>
