@@ -145,3 +145,24 @@ def test_multinomial_model_transform_uses_kernel():
     ref = x.to(torch.float64) @ torch.as_tensor(W, device="cuda").T + torch.as_tensor(b, device="cuda")
     np.testing.assert_allclose(raw.cpu().numpy(), ref.cpu().numpy(), rtol=1e-12, atol=1e-12)
     assert torch.equal(m._predict_from_prob(prob), torch.argmax(torch.softmax(ref, 1), 1).double())
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("n", [1, 5, 31, 33, 127])
+@pytest.mark.parametrize("C", [3, 12, 24])
+def test_mfma_tiny_shapes_match_f64_oracle(n, C):
+    """Row counts below one 32-row tile, just past it, and a few tiles (every wave but one idle): the MFMA forms'
+    partial-tile masking and zero-row tails, for the 16-class and 32-class tiles; and K13t on the same rows."""
+    d = 64
+    g = torch.Generator(device="cuda").manual_seed(n * 100 + C)
+    x = (torch.randn(n, d, generator=g, device="cuda") * 2).to(torch.bfloat16)
+    y = torch.randint(0, C, (n,), generator=g, device="cuda").double()
+    w = torch.rand(n, generator=g, device="cuda", dtype=torch.float64) + 0.5
+    coef = torch.randn(C, d + 1, generator=g, device="cuda", dtype=torch.float64) * 0.2
+    got = glm_ops.multinomial_grad(x, d, y, coef, w)
+    ref = glm_ops.multinomial_grad(x.float().cpu().to(torch.float64), d, y.cpu(), coef.cpu(), w.cpu())
+    np.testing.assert_allclose(got.cpu().numpy(), ref.numpy(), rtol=2e-5, atol=2e-5 * float(ref.abs().max()))
+    raw, prob = glm_ops.multinomial_predict(x, d, coef)
+    want = x.to(torch.float64) @ coef[:, :d].T + coef[:, d]
+    np.testing.assert_allclose(raw.cpu().numpy(), want.cpu().numpy(), rtol=1e-12, atol=1e-12)
+    np.testing.assert_allclose(prob.cpu().numpy(), torch.softmax(want, 1).cpu().numpy(), rtol=1e-11, atol=1e-14)
