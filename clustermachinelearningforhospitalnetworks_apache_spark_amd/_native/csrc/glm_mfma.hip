@@ -602,18 +602,19 @@ __device__ __forceinline__ int ximg16_off(int row, int ch) {
 // element offset of row r of a residual plane of multinomial_c16_kernel
 __device__ __forceinline__ int rimg16_off(int r) { return r * 16 + (r >> 3) * 64; }
 
-template <int FT>
+template <int FT, int CTN>
 __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
     const u16* __restrict__ X, long long n, long long ld, int d, int C, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1]*/, double* __restrict__ out) {
-  constexpr int CP = 16;
+  constexpr int CP = 16 * CTN;  // CTN class tiles of 16
   constexpr int DP = 32 * FT;
   constexpr int BP = DP + 16;  // split-W pitch (bf16 elements): rows 8 dwords apart mod 64, so the row reads
                                // of a 16-lane group (rows r, column half g4) fall on distinct banks
   constexpr size_t WBYTES = (size_t)3 * CP * BP * 2;
   constexpr int XIMG = ((DP + 127) / 128) * 8192;  // bytes per wave
-  // residual plane: [32 rows][16 classes] bf16, 32-byte rows, 64 elements (128 B) of padding after every 8 rows:
-  // the two 16-lane groups of a transposed read (rows 8 apart) then take different bank halves
+  // residual plane (one class tile at a time): [32 rows][16 classes] bf16, 32-byte rows, 64 elements (128 B) of
+  // padding after every 8 rows: the two 16-lane groups of a transposed read (rows 8 apart) then take different
+  // bank halves
   constexpr int RPLANE = 4 * (8 * 16 + 64);
   constexpr int NCHUNK = DP / 8;
   constexpr int LCH = 32 * NCHUNK / 64;
@@ -638,10 +639,16 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
   for (int c = tid; c < CP; c += kMnThreads) bias_l[c] = c < C ? (float)coef[(long long)c * (d + 1) + d] : -__builtin_huge_valf();
   for (int i = tid; i < CP * DP + C + 2; i += kMnThreads) part[i] = 0.0;
   __syncthreads();
-  f32x4 G[NT];
+  f32x4 G[CTN][NT];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) G[t] = (f32x4)0.f;
-  float gbr[4] = {0.f, 0.f, 0.f, 0.f};
+  for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+    for (int t = 0; t < NT; ++t) G[ct][t] = (f32x4)0.f;
+  float gbr[CTN][4];
+#pragma unroll
+  for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+    for (int r = 0; r < 4; ++r) gbr[ct][r] = 0.f;
   double loss = 0.0, wsum = 0.0;
 
   const long long ntiles = (n + 31) / 32;
@@ -674,7 +681,7 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
         xr[i] = make_uint4(0u, 0u, 0u, 0u);
     }
   };
-  const __bf16* wa = wb + r16 * BP + 8 * g4;        // W[class r16][32s + 8 g4 + j]
+  const __bf16* wa = wb + r16 * BP + 8 * g4;        // W[16 ct + r16][32s + 8 g4 + j] at + 16 ct BP
   const int trq = (lane >> 2) & 3, trp = lane & 3;  // transposed reads: lane 4q + p of its 16-lane group
 
   long long g = blockIdx.x;
@@ -690,79 +697,100 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
     __builtin_amdgcn_wave_barrier();
     const double yv[2] = {ynext[0], ynext[1]}, wv[2] = {wnext[0], wnext[1]};
     if (g + gridDim.x < ngroups) load_tile(4 * (g + gridDim.x) + wave);
-    // margins Mᵀ[class 4 g4 + reg][row 16u + r16] = bias + W·Xᵀ
-    f32x4 M[2];
-    {
-      const float4 b = *reinterpret_cast<const float4*>(bias_l + 4 * g4);
-      M[0] = f32x4{b.x, b.y, b.z, b.w};
-      M[1] = M[0];
+    // margins Mᵀ[class 16 ct + 4 g4 + reg][row 16u + r16] = bias + W·Xᵀ
+    f32x4 M[CTN][2];
+#pragma unroll
+    for (int ct = 0; ct < CTN; ++ct) {
+      const float4 b = *reinterpret_cast<const float4*>(bias_l + 16 * ct + 4 * g4);
+      M[ct][0] = f32x4{b.x, b.y, b.z, b.w};
+      M[ct][1] = M[ct][0];
     }
     __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int s = 0; s < DP / 32; ++s) {
-      const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + 32 * s));
-      const bf16x8 am = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + CP * BP + 32 * s));
-      const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wa + 2 * CP * BP + 32 * s));
+      bf16x8 xb[2];
 #pragma unroll
-      for (int u = 0; u < 2; ++u) {
-        const bf16x8 xb =
-            __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xim + ximg16_off(16 * u + r16, 4 * s + g4)));
-        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb, M[u], 0, 0, 0);
-        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, xb, M[u], 0, 0, 0);
-        M[u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb, M[u], 0, 0, 0);
+      for (int u = 0; u < 2; ++u)
+        xb[u] = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(xim + ximg16_off(16 * u + r16, 4 * s + g4)));
+#pragma unroll
+      for (int ct = 0; ct < CTN; ++ct) {
+        const __bf16* wc = wa + 16 * ct * BP + 32 * s;
+        const bf16x8 ah = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wc));
+        const bf16x8 am = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wc + CP * BP));
+        const bf16x8 al = __builtin_bit_cast(bf16x8, *reinterpret_cast<const uint4*>(wc + 2 * CP * BP));
+#pragma unroll
+        for (int u = 0; u < 2; ++u) {
+          M[ct][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, xb[u], M[ct][u], 0, 0, 0);
+          M[ct][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, xb[u], M[ct][u], 0, 0, 0);
+          M[ct][u] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, xb[u], M[ct][u], 0, 0, 0);
+        }
       }
     }
     __builtin_amdgcn_sched_barrier(0);
-    // softmax over the 16 classes of row 16u + r16 (4 registers x lanes r16, r16 + 16, + 32, + 48)
+    // softmax over the CP classes of row 16u + r16 (4·CTN registers x lanes r16, r16 + 16, + 32, + 48); the
+    // residuals replace the margins in M
 #pragma unroll
     for (int u = 0; u < 2; ++u) {
       const bool ok = tile * 32 + 16 * u + r16 < n;
       const int yc = (int)yv[u];
-      float mx = fmaxf(fmaxf(M[u][0], M[u][1]), fmaxf(M[u][2], M[u][3]));
+      float mx = M[0][u][0];
+#pragma unroll
+      for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) mx = fmaxf(mx, M[ct][u][r]);
       mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
       mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
-      float se = 0.f, my = 0.f, e[4];
+      float se = 0.f, my = 0.f;
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        my += (4 * g4 + r == yc) ? M[u][r] : 0.f;
-        e[r] = __expf(M[u][r] - mx);  // padded classes: margin -inf (bias), e = 0
-        se += e[r];
-      }
+      for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          my += (16 * ct + 4 * g4 + r == yc) ? M[ct][u][r] : 0.f;
+          const float e = __expf(M[ct][u][r] - mx);  // padded classes: margin -inf (bias), e = 0
+          M[ct][u][r] = e;
+          se += e;
+        }
       se += __shfl_xor(se, 16, 64);
       se += __shfl_xor(se, 32, 64);
       my += __shfl_xor(my, 16, 64);
       my += __shfl_xor(my, 32, 64);
       const float inv = 1.f / se, wf32 = (float)wv[u];
-      float rr[4];
 #pragma unroll
-      for (int r = 0; r < 4; ++r) {
-        rr[r] = wf32 * (e[r] * inv - (4 * g4 + r == yc ? 1.f : 0.f));
-        gbr[r] += rr[r];
-      }
+      for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          const float rr = wf32 * (M[ct][u][r] * inv - (16 * ct + 4 * g4 + r == yc ? 1.f : 0.f));
+          M[ct][u][r] = rr;
+          gbr[ct][r] += rr;
+        }
       if (g4 == 0 && ok) {
         loss += wv[u] * (((double)mx + (double)__logf(se)) - (double)my);
         wsum += wv[u];
       }
-      // residual row 16u + r16, classes 4 g4 .. 4 g4 + 3 -> the three bf16 planes of the [row][class] image
-      __bf16 hi[4], mi[4], lo[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        hi[j] = (__bf16)rr[j];
-        const float r1 = rr[j] - (float)hi[j];
-        mi[j] = (__bf16)r1;
-        lo[j] = (__bf16)(r1 - (float)mi[j]);
-      }
-      const int o = rimg16_off(16 * u + r16) + 4 * g4;
-      *reinterpret_cast<uint2*>(rim + o) = make_uint2(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]));
-      *reinterpret_cast<uint2*>(rim + RPLANE + o) = make_uint2(pack_bf16(mi[0], mi[1]), pack_bf16(mi[2], mi[3]));
-      *reinterpret_cast<uint2*>(rim + 2 * RPLANE + o) = make_uint2(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]));
     }
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
-    // gradient: G[t] += R[class][rows 0..31] · X[rows][features 16t ..]; group g4 of a transposed read takes
-    // rows 8 g4 + 4 rd + q
-    {
-      const int r0 = 8 * g4 + trq;
+    // gradient, one class tile at a time through the residual image: G[ct][t] += R[class][rows 0..31] ·
+    // X[rows][features 16t ..]; group g4 of a transposed read takes rows 8 g4 + 4 rd + q
+    const int r0 = 8 * g4 + trq;
+#pragma unroll
+    for (int ct = 0; ct < CTN; ++ct) {
+#pragma unroll
+      for (int u = 0; u < 2; ++u) {  // residual rows 16u + r16, classes 4 g4 .. 4 g4 + 3 -> the three planes
+        __bf16 hi[4], mi[4], lo[4];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          hi[j] = (__bf16)M[ct][u][j];
+          const float r1 = M[ct][u][j] - (float)hi[j];
+          mi[j] = (__bf16)r1;
+          lo[j] = (__bf16)(r1 - (float)mi[j]);
+        }
+        const int o = rimg16_off(16 * u + r16) + 4 * g4;
+        *reinterpret_cast<uint2*>(rim + o) = make_uint2(pack_bf16(hi[0], hi[1]), pack_bf16(hi[2], hi[3]));
+        *reinterpret_cast<uint2*>(rim + RPLANE + o) = make_uint2(pack_bf16(mi[0], mi[1]), pack_bf16(mi[2], mi[3]));
+        *reinterpret_cast<uint2*>(rim + 2 * RPLANE + o) =
+            make_uint2(pack_bf16(lo[0], lo[1]), pack_bf16(lo[2], lo[3]));
+      }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
       const unsigned char* ra = reinterpret_cast<const unsigned char*>(rim);
       const int oa0 = 2 * (rimg16_off(r0) + 4 * trp), oa1 = 2 * (rimg16_off(r0 + 4) + 4 * trp);
       const bf16x8 ah = tr_frag(ra + oa0, ra + oa1);
@@ -772,19 +800,21 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
       for (int t = 0; t < NT; ++t) {
         const int ch = 2 * t + (trp >> 1);
         const bf16x8 bx = tr_frag(xim + ximg16_off(r0, ch) + 8 * (trp & 1), xim + ximg16_off(r0 + 4, ch) + 8 * (trp & 1));
-        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx, G[t], 0, 0, 0);
-        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx, G[t], 0, 0, 0);
-        G[t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bx, G[t], 0, 0, 0);
+        G[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ah, bx, G[ct][t], 0, 0, 0);
+        G[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(am, bx, G[ct][t], 0, 0, 0);
+        G[ct][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(al, bx, G[ct][t], 0, 0, 0);
       }
+      __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_wave_barrier();
     }
-    __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-    __builtin_amdgcn_wave_barrier();
   }
   // bias gradient: each register's class summed over the 16 rows of the lane group
 #pragma unroll
-  for (int r = 0; r < 4; ++r)
+  for (int ct = 0; ct < CTN; ++ct)
 #pragma unroll
-    for (int o = 1; o < 16; o <<= 1) gbr[r] += __shfl_xor(gbr[r], o, 64);
+    for (int r = 0; r < 4; ++r)
+#pragma unroll
+      for (int o = 1; o < 16; o <<= 1) gbr[ct][r] += __shfl_xor(gbr[ct][r], o, 64);
   loss = wave_sum_f64(loss);
   wsum = wave_sum_f64(wsum);
   double* pg = part + (4 * g4) * DP + r16;
@@ -792,15 +822,19 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
   for (int w = 0; w < 4; ++w) {
     if (wave == w) {
 #pragma unroll
-      for (int t = 0; t < NT; ++t) {
+      for (int ct = 0; ct < CTN; ++ct)
 #pragma unroll
-        for (int r = 0; r < 4; ++r) pg[r * DP + 16 * t] += (double)G[t][r];
-        __builtin_amdgcn_sched_barrier(0);
-      }
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+          for (int r = 0; r < 4; ++r) pg[(16 * ct + r) * DP + 16 * t] += (double)G[ct][t][r];
+          __builtin_amdgcn_sched_barrier(0);
+        }
       if (r16 == 0)
 #pragma unroll
-        for (int r = 0; r < 4; ++r)
-          if (4 * g4 + r < C) part[CP * DP + 4 * g4 + r] += (double)gbr[r];
+        for (int ct = 0; ct < CTN; ++ct)
+#pragma unroll
+          for (int r = 0; r < 4; ++r)
+            if (16 * ct + 4 * g4 + r < C) part[CP * DP + 16 * ct + 4 * g4 + r] += (double)gbr[ct][r];
       if (lane == 0) {
         part[CP * DP + C] += loss;
         part[CP * DP + C + 1] += wsum;
@@ -810,9 +844,9 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
   }
 }
 
-template <int FT>
+template <int FT, int CTN>
 constexpr size_t mnc16_lds() {
-  return (size_t)3 * 16 * (32 * FT + 16) * 2 + 16 * 4 + (size_t)4 * ((32 * FT + 127) / 128) * 8192 +
+  return (size_t)3 * 16 * CTN * (32 * FT + 16) * 2 + 16 * CTN * 4 + (size_t)4 * ((32 * FT + 127) / 128) * 8192 +
          (size_t)4 * 3 * (4 * (8 * 16 + 64)) * 2;
 }
 
@@ -834,7 +868,7 @@ int g_mn_f32 = 0;      // 1: the f32-MFMA form (A/B and precision reference)
 int g_mn_nosplit = 0;  // 1: split W on the fly also where the three bf16 planes fit in LDS (A/B)
 int g_mn_no16 = 0;     // 1: C <= 16 on the 32-class tile too (A/B of multinomial_c16_kernel)
 // mode: 0 = bf16 three-term MFMAs (default; C <= 16 on the 16-class tile), 1 = f32 MFMAs, 2 = bf16 with W split
-// on the fly, 3 = mode 0 on the 32-class tile for every C; -1 = query
+// on the fly, 3 = mode 0 on 32-class tiles for every C; -1 = query
 CML_API int cml_multinomial_mfma_set_mode(int mode) {
   const int prev = g_mn_f32 ? 1 : (g_mn_nosplit ? 2 : (g_mn_no16 ? 3 : 0));
   if (mode >= 0) {
@@ -849,7 +883,9 @@ CML_API int cml_multinomial_mfma_set_mode(int mode) {
 // Returns the class-slot count CP (32 / 64) or 0.
 CML_API int cml_multinomial_mfma_supported(int d, int dtype, int C) {
   if (dtype != 0 || d < 8 || d % 8 != 0 || d > 256 || C < 2 || C > 64) return 0;
-  if (C <= 16 && !g_mn_f32 && !g_mn_nosplit && !g_mn_no16) return 16;  // multinomial_c16_kernel
+  // multinomial_c16_kernel for C <= 16. Two 16-class tiles (CTN = 2) for 17..32 classes measured slower than the
+  // 32-class tile: 14.45 vs 13.71 ms at C = 32 over 100M x 256 (profiles/r6/README.md)
+  if (C <= 16 && !g_mn_f32 && !g_mn_nosplit && !g_mn_no16) return 16;
   return C <= 32 ? 32 : 64;
 }
 
@@ -866,7 +902,7 @@ CML_API int cml_multinomial_mfma_grid(long long n, int ncu) {
 // Padded width DP the partials use: 32·ceil(d / 32), for C > 32 and d > 128 rounded up to 192 / 256.
 CML_API int cml_multinomial_mfma_dpad(int d, int C) {
   int ft = (d + 31) / 32;
-  if (cml_multinomial_mfma_supported(d, 0, C) == 16) return 32 * ft;
+  if (C <= 32) return 32 * ft;  // (both tile forms)
   if (C > 32 && ft > 4) ft = ft <= 6 ? 6 : 8;
   return 32 * ft;
 }
@@ -880,17 +916,18 @@ CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, 
     return (int)hipErrorInvalidValue;
   hipStream_t st = (hipStream_t)stream;
   int ft = (d + 31) / 32;
-  if (cml_multinomial_mfma_supported(d, 0, C) == 16) {
-#define CML_MNC(FTV)                                                                                           \
-    if (ft == FTV) {                                                                                           \
-      constexpr size_t lds = mnc16_lds<FTV>();                                                                 \
-      hipFuncSetAttribute((const void*)multinomial_c16_kernel<FTV>, hipFuncAttributeMaxDynamicSharedMemorySize, \
-                          (int)lds);                                                                           \
-      hipLaunchKernelGGL((multinomial_c16_kernel<FTV>), dim3(grid), dim3(kMnThreads), lds, st, (const u16*)X, n, \
-                         ld, d, C, y, wt, coef, out);                                                          \
+  if (cml_multinomial_mfma_supported(d, 0, C) == 16) {  // multinomial_c16_kernel
+    const int ctn = 1;
+#define CML_MNC(FTV, CTNV)                                                                                     \
+    if (ft == FTV && ctn == CTNV) {                                                                            \
+      constexpr size_t lds = mnc16_lds<FTV, CTNV>();                                                           \
+      hipFuncSetAttribute((const void*)multinomial_c16_kernel<FTV, CTNV>,                                      \
+                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                               \
+      hipLaunchKernelGGL((multinomial_c16_kernel<FTV, CTNV>), dim3(grid), dim3(kMnThreads), lds, st,            \
+                         (const u16*)X, n, ld, d, C, y, wt, coef, out);                                        \
       return cml_status();                                                                                     \
     }
-    CML_MNC(1) CML_MNC(2) CML_MNC(3) CML_MNC(4) CML_MNC(5) CML_MNC(6) CML_MNC(7) CML_MNC(8)
+    CML_MNC(1, 1) CML_MNC(2, 1) CML_MNC(3, 1) CML_MNC(4, 1) CML_MNC(5, 1) CML_MNC(6, 1) CML_MNC(7, 1) CML_MNC(8, 1)
 #undef CML_MNC
     return (int)hipErrorInvalidValue;
   }

@@ -302,9 +302,9 @@ def multinomial_predict(x: torch.Tensor, d: int, coef: torch.Tensor):
 
 
 def set_multinomial_mfma_mode(mode: int) -> int:
-    """K13m MFMA form: 0 = bf16 three-term products (default; C <= 16 on 16x16x32 MFMAs), 1 = f32 MFMAs, 2 = bf16
-    with W split in registers on every use, 3 = mode 0 on the 32-class tile for every C (A/B). Returns the
-    previous mode."""
+    """K13m MFMA form: 0 = bf16 three-term products (default; C <= 16 on a 16-class tile of 16x16x32 MFMAs),
+    1 = f32 MFMAs, 2 = bf16 with W split in registers on every use, 3 = mode 0 on 32-class tiles of 32x32x16
+    MFMAs for every C (A/B). Returns the previous mode."""
     return int(_native.kernels().cml_multinomial_mfma_set_mode(int(mode)))
 
 

@@ -313,7 +313,7 @@ def cmd_multinomial(argv):
         y = torch.randint(0, C, (n,), generator=g, device=dev).to(torch.float64)
         coef = torch.randn(C, d + 1, generator=g, device=dev, dtype=torch.float64) * 0.05
         # MFMA form: margins + gradient on the padded class tile (16, 32 or 64 classes)
-        flop = 4.0 * n * d * (16 if C <= 16 else 32 if C <= 32 else 64)
+        flop = 4.0 * n * d * (16 if C <= 16 else 32 if C <= 32 else 64)  # (mode 3: 32 for C <= 16 too)
         runs = []
         if lib.cml_multinomial_supported(d, 0, C) > 0:
             runs.append(("valu", lambda: glm_ops.multinomial_grad(x, d, y, coef, prefer_valu=True)))

@@ -95,7 +95,8 @@ def test_kernel_matches_f64_oracle(dt, d, C):
 
 @pytest.mark.gpu
 @pytest.mark.parametrize("mode", [0, 1, 2, 3])
-@pytest.mark.parametrize("d,C", [(256, 32), (200, 40), (256, 64), (64, 9), (256, 8), (136, 16), (40, 3)])
+@pytest.mark.parametrize("d,C", [(256, 32), (200, 40), (256, 64), (64, 9), (256, 8), (136, 16), (40, 3), (96, 17),
+                                 (248, 27)])
 def test_mfma_forms_match_f64_oracle(mode, d, C):
     """The K13m MFMA forms (bf16 three-term products with W split once in LDS or in registers, on the 16-class
     tile for C <= 16 or the 32-class one, and the f32 MFMAs) each match the f64 oracle to f32 precision."""
