@@ -1,8 +1,16 @@
-// K13m on MFMA: the multinomial logistic loss and C×d gradient for up to 64 classes (gfx950).
+// K13m on MFMA: the multinomial logistic loss and C×d gradient for up to 64 classes (gfx950), and K13t, the
+// multinomial model's transform. Kernels, in file order:
+//   multinomial_mfma_kernel   f32 MFMAs (the first form; cml_multinomial_mfma_set_mode(1): A/B and precision
+//                             reference)
+//   multinomial_bf16_kernel   bf16 MFMAs on each f32 operand split into three bf16 terms, 32-class tiles of
+//                             v_mfma_f32_32x32x16_bf16, the data row on the lane: the default for 17..64 classes
+//   multinomial_c16_kernel    the same on a 16-class tile of v_mfma_f32_16x16x32_bf16: the default for C <= 16
+//   multinomial_predict_kernel  K13t: f64 margins + softmax probabilities on v_mfma_f64_16x16x4_f64
+// Measurements: profiles/r6/README.md §4, §7.
 //
 // The VALU form (glm.hip multinomial_grad_kernel) keeps a lane's columns of every class row in VGPRs, which
 // caps it at 8 classes. Past that the work per row — 2·C·d multiply-adds for the margins, 2·C·d for the
-// gradient — is matrix work: this kernel runs both products on v_mfma_f32_32x32x2_f32 (exact f32 products
+// gradient — is matrix work: the first kernel below runs both products on v_mfma_f32_32x32x2_f32 (exact f32 products
 // of the bf16 rows and f32 weights / residuals, f32 accumulation: the VALU kernel's arithmetic), with X read
 // from HBM once per launch:
 //
