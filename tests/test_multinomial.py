@@ -167,3 +167,27 @@ def test_mfma_tiny_shapes_match_f64_oracle(n, C):
     want = x.to(torch.float64) @ coef[:, :d].T + coef[:, d]
     np.testing.assert_allclose(raw.cpu().numpy(), want.cpu().numpy(), rtol=1e-12, atol=1e-12)
     np.testing.assert_allclose(prob.cpu().numpy(), torch.softmax(want, 1).cpu().numpy(), rtol=1e-11, atol=1e-14)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("C", [6, 12])
+def test_multinomial_fit_on_gpu_rows_matches_cpu_fit(C, monkeypatch):
+    """LogisticRegression(family="multinomial") on a GPU frame of bf16 rows — every gradient pass on the MFMA
+    kernels (the 16-class tile at C = 6, the 32-class tile at C = 12) — reaches the coefficients of the CPU
+    fit on the same (exactly representable) rows, whose gradients are f64 row chunks."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd.sql import SparkSession
+    n, d = 60_000, 32
+    X, y = _data(n=n, d=d, C=C, seed=C)
+    xb = torch.as_tensor(X / 3.0, dtype=torch.float32).to(torch.bfloat16)
+    yy = torch.as_tensor(y, dtype=torch.float64)
+    spark = SparkSession.builder.master("mi355x").getOrCreate()
+    gdf = spark.createDataFrameFromTensors({"features": xb.cuda(), "label": yy.cuda()})
+    lr = LogisticRegression(family="multinomial", regParam=1e-3, maxIter=200, tol=1e-10)
+    calls = []
+    real = glm_ops._multinomial_mfma
+    monkeypatch.setattr(glm_ops, "_multinomial_mfma", lambda *a: calls.append(a[6]) or real(*a))
+    mg = lr.fit(gdf)
+    assert calls and set(calls) == {16 if C <= 16 else 32}  # every gradient pass on the MFMA kernel
+    mc = lr.fit(_frame(xb.double().numpy(), y))
+    np.testing.assert_allclose(mg.coefficientMatrix.toArray(), mc.coefficientMatrix.toArray(), rtol=1e-3, atol=1e-3)
+    np.testing.assert_allclose(mg.interceptVector.toArray(), mc.interceptVector.toArray(), rtol=1e-3, atol=1e-3)
