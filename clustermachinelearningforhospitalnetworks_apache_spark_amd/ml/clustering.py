@@ -129,18 +129,35 @@ class KMeans(Estimator):
         if ckdir:
             comm.barrier()
             ckpt.clear(ckdir, ckname, comm)
-        centers = eng.centers.cpu().numpy()
-        model = KMeansModel(centers)
-        self._copyValues(model)
         # trainingCost is the last iteration's cost (Spark computes it while training: here from the f64
         # sums and norms the engine holds, no pass over X); clusterSizes: one pruned assign against the
         # final centres, its counts and their all-reduce are enqueued here on every rank (no host read),
         # so reading the summary later is no collective and the engine is released when fit returns. The cost
         # is enqueued first: the final assignment then updates the engine's own labels and bounds in place
-        # (consume=True: nothing steps this engine again)
-        _ = eng.last_cost
-        sizes = eng.cluster_sizes_async(consume=True)
-        model._attach_summary(KMeansSummary(model, df, eng.k, iters, eng.training_cost(), sizes))
+        # (consume=True: nothing steps this engine again). On a GPU the centres and the cost go to pinned
+        # host memory BEFORE the final assignment is enqueued, and the host waits for those copies only: the
+        # model and the summary are built while the device runs the final assignment
+        cost = eng.last_cost
+        if eng.device.type == "cuda":
+            c_h = torch.empty(eng.centers.shape, dtype=torch.float64, pin_memory=True)
+            c_h.copy_(eng.centers, non_blocking=True)
+            cost_h = None
+            if cost is not None:
+                cost_h = torch.empty((), dtype=cost.dtype, pin_memory=True)
+                cost_h.copy_(cost, non_blocking=True)
+            ready = torch.cuda.Event()
+            ready.record()
+            sizes = eng.cluster_sizes_async(consume=True)
+            ready.synchronize()
+            centers = c_h.numpy()
+            tc = float("nan") if cost_h is None else float(cost_h) / (2.0 if eng.spherical else 1.0)
+        else:
+            sizes = eng.cluster_sizes_async(consume=True)
+            centers = eng.centers.cpu().numpy()
+            tc = eng.training_cost()
+        model = KMeansModel(centers)
+        self._copyValues(model)
+        model._attach_summary(KMeansSummary(model, df, eng.k, iters, tc, sizes))
         return model
 
 
