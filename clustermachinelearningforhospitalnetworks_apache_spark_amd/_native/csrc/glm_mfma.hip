@@ -287,9 +287,28 @@ __device__ __forceinline__ unsigned pack_bf16(__bf16 a, __bf16 b) {
   return (unsigned)__builtin_bit_cast(u16, a) | ((unsigned)__builtin_bit_cast(u16, b) << 16);
 }
 
-template <int CT, int FT, int FTG, bool PRESPLIT>
+// e4m3 rows (F8): a 16-byte load holds 16 values; they are widened exactly to bf16 (two image chunks) when the tile
+// is staged, so the MFMA passes and the image layout are the bf16 ones and HBM reads half the bytes
+template <bool F8>
+struct XLoad {
+  static constexpr int VPL = F8 ? 16 : 8;  // values per 16-byte load
+  static constexpr int ES = F8 ? 1 : 2;    // bytes per value
+};
+__device__ __forceinline__ void widen_e4m3(const uint4 q, uint4& lo, uint4& hi) {
+  const unsigned w[4] = {q.x, q.y, q.z, q.w};
+  unsigned o[8];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    o[2 * j] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, false));
+    o[2 * j + 1] = __builtin_bit_cast(unsigned, __builtin_amdgcn_cvt_scalef32_pk_bf16_fp8(w[j], 1.0f, true));
+  }
+  lo = make_uint4(o[0], o[1], o[2], o[3]);
+  hi = make_uint4(o[4], o[5], o[6], o[7]);
+}
+
+template <int CT, int FT, int FTG, bool PRESPLIT, bool F8 = false>
 __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
-    const u16* __restrict__ X, long long n, long long ld, int d, int C, const double* __restrict__ y,
+    const void* __restrict__ Xv, long long n, long long ld, int d, int C, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1]*/, double* __restrict__ out, int ft0,
     int scalars) {
   constexpr int CP = 32 * CT;
@@ -299,8 +318,10 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
   constexpr size_t WBYTES = PRESPLIT ? (size_t)3 * CP * BP * 2 : (size_t)CP * WP * 4;
   constexpr int XIMG = ((DP + 127) / 128) * 8192;  // bytes per wave
   constexpr int RPLANE = 32 * 32;                  // elements per residual plane
-  constexpr int NCHUNK = DP / 8;
-  constexpr int LCH = 32 * NCHUNK / 64;
+  constexpr int LCHUNK = DP / XLoad<F8>::VPL;  // 16-byte loads per row
+  constexpr int LCH = 32 * LCHUNK / 64;        // loads per lane per tile
+  const unsigned char* X = reinterpret_cast<const unsigned char*>(Xv);
+  constexpr int ES = XLoad<F8>::ES;
   extern __shared__ __align__(16) unsigned char smem[];
   float* wf = reinterpret_cast<float*>(smem);      // [CP][WP] f32 weights, or
   __bf16* wb = reinterpret_cast<__bf16*>(smem);    // PRESPLIT: [3][CP][BP] hi, mid, lo
@@ -374,20 +395,20 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
     ynext = yrow < n ? y[yrow] : 0.0;
     wnext = yrow < n ? (wt != nullptr ? wt[yrow] : 1.0) : 0.0;
     if (tile * 32 + 32 <= n && d == DP) {  // a whole tile of full rows (all but the last tile): no per-load tests
-      const u16* base = X + tile * 32 * ld;
+      const unsigned char* base = X + tile * 32 * ld * ES;
 #pragma unroll
       for (int i = 0; i < LCH; ++i) {
-        const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
-        xr[i] = *reinterpret_cast<const uint4*>(base + r * ld + ch * 8);
+        const int q = lane + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
+        xr[i] = *reinterpret_cast<const uint4*>(base + (r * ld + ch * XLoad<F8>::VPL) * ES);
       }
       return;
     }
 #pragma unroll
     for (int i = 0; i < LCH; ++i) {
-      const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
+      const int q = lane + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
       const long long row = tile * 32 + r;
-      if (row < n && ch * 8 < d)
-        xr[i] = *reinterpret_cast<const uint4*>(X + row * ld + ch * 8);
+      if (row < n && ch * XLoad<F8>::VPL < d)
+        xr[i] = *reinterpret_cast<const uint4*>(X + (row * ld + ch * XLoad<F8>::VPL) * ES);
       else
         xr[i] = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -405,8 +426,15 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_bf16_kernel(
     const int trg = ln >> 4, trq = (ln >> 2) & 3, trp = ln & 3;
 #pragma unroll
     for (int i = 0; i < LCH; ++i) {
-      const int q = ln + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
-      *reinterpret_cast<uint4*>(xim + ximg_off(r, ch)) = xr[i];
+      const int q = ln + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
+      if constexpr (F8) {
+        uint4 lo, hi;
+        widen_e4m3(xr[i], lo, hi);
+        *reinterpret_cast<uint4*>(xim + ximg_off(r, 2 * ch)) = lo;
+        *reinterpret_cast<uint4*>(xim + ximg_off(r, 2 * ch + 1)) = hi;
+      } else {
+        *reinterpret_cast<uint4*>(xim + ximg_off(r, ch)) = xr[i];
+      }
     }
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -610,9 +638,9 @@ __device__ __forceinline__ int ximg16_off(int row, int ch) {
 // element offset of row r of a residual plane of multinomial_c16_kernel
 __device__ __forceinline__ int rimg16_off(int r) { return r * 16 + (r >> 3) * 64; }
 
-template <int FT, int CTN>
+template <int FT, int CTN, bool F8 = false>
 __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
-    const u16* __restrict__ X, long long n, long long ld, int d, int C, const double* __restrict__ y,
+    const void* __restrict__ Xv, long long n, long long ld, int d, int C, const double* __restrict__ y,
     const double* __restrict__ wt, const double* __restrict__ coef /*[C][d+1]*/, double* __restrict__ out) {
   constexpr int CP = 16 * CTN;  // CTN class tiles of 16
   constexpr int DP = 32 * FT;
@@ -624,8 +652,10 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
   // padding after every 8 rows: the two 16-lane groups of a transposed read (rows 8 apart) then take different
   // bank halves
   constexpr int RPLANE = 4 * (8 * 16 + 64);
-  constexpr int NCHUNK = DP / 8;
-  constexpr int LCH = 32 * NCHUNK / 64;
+  constexpr int LCHUNK = DP / XLoad<F8>::VPL;  // 16-byte loads per row
+  constexpr int LCH = 32 * LCHUNK / 64;        // loads per lane per tile
+  const unsigned char* X = reinterpret_cast<const unsigned char*>(Xv);
+  constexpr int ES = XLoad<F8>::ES;
   constexpr int NT = DP / 16;                      // 16-feature gradient tiles
   extern __shared__ __align__(16) unsigned char smem[];
   __bf16* wb = reinterpret_cast<__bf16*>(smem);                  // [3][CP][BP] hi, mid, lo
@@ -671,20 +701,20 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
       wnext[u] = yrow < n ? (wt != nullptr ? wt[yrow] : 1.0) : 0.0;
     }
     if (tile * 32 + 32 <= n && d == DP) {
-      const u16* base = X + tile * 32 * ld;
+      const unsigned char* base = X + tile * 32 * ld * ES;
 #pragma unroll
       for (int i = 0; i < LCH; ++i) {
-        const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
-        xr[i] = *reinterpret_cast<const uint4*>(base + r * ld + ch * 8);
+        const int q = lane + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
+        xr[i] = *reinterpret_cast<const uint4*>(base + (r * ld + ch * XLoad<F8>::VPL) * ES);
       }
       return;
     }
 #pragma unroll
     for (int i = 0; i < LCH; ++i) {
-      const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
+      const int q = lane + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
       const long long row = tile * 32 + r;
-      if (row < n && ch * 8 < d)
-        xr[i] = *reinterpret_cast<const uint4*>(X + row * ld + ch * 8);
+      if (row < n && ch * XLoad<F8>::VPL < d)
+        xr[i] = *reinterpret_cast<const uint4*>(X + (row * ld + ch * XLoad<F8>::VPL) * ES);
       else
         xr[i] = make_uint4(0u, 0u, 0u, 0u);
     }
@@ -698,8 +728,15 @@ __global__ __launch_bounds__(kMnThreads) void multinomial_c16_kernel(
     const long long tile = 4 * g + wave;
 #pragma unroll
     for (int i = 0; i < LCH; ++i) {
-      const int q = lane + 64 * i, r = q / NCHUNK, ch = q - r * NCHUNK;
-      *reinterpret_cast<uint4*>(xim + ximg16_off(r, ch)) = xr[i];
+      const int q = lane + 64 * i, r = q / LCHUNK, ch = q - r * LCHUNK;
+      if constexpr (F8) {
+        uint4 lo, hi;
+        widen_e4m3(xr[i], lo, hi);
+        *reinterpret_cast<uint4*>(xim + ximg16_off(r, 2 * ch)) = lo;
+        *reinterpret_cast<uint4*>(xim + ximg16_off(r, 2 * ch + 1)) = hi;
+      } else {
+        *reinterpret_cast<uint4*>(xim + ximg16_off(r, ch)) = xr[i];
+      }
     }
     __asm__ volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
     __builtin_amdgcn_wave_barrier();
@@ -890,7 +927,10 @@ CML_API int cml_multinomial_mfma_set_mode(int mode) {
 // Supported: bf16 rows (dtype 0), d % 8 == 0, d <= 256, C <= 64 (the caller keeps the VALU kernel for C <= 8).
 // Returns the class-slot count CP (32 / 64) or 0.
 CML_API int cml_multinomial_mfma_supported(int d, int dtype, int C) {
-  if (dtype != 0 || d < 8 || d % 8 != 0 || d > 256 || C < 2 || C > 64) return 0;
+  // bf16 rows (dtype 0, d % 8 == 0) or e4m3 rows (dtype 3, d % 16 == 0: whole 16-byte loads, widened to bf16 when
+  // staged; not on the f32-MFMA form)
+  if (d < 8 || d > 256 || C < 2 || C > 64) return 0;
+  if (!(dtype == 0 && d % 8 == 0) && !(dtype == 3 && d % 16 == 0 && !g_mn_f32)) return 0;
   // multinomial_c16_kernel for C <= 16. Two 16-class tiles (CTN = 2) for 17..32 classes measured slower than the
   // 32-class tile: 14.45 vs 13.71 ms at C = 32 over 100M x 256 (profiles/r6/README.md)
   if (C <= 16 && !g_mn_f32 && !g_mn_nosplit && !g_mn_no16) return 16;
@@ -917,26 +957,34 @@ CML_API int cml_multinomial_mfma_dpad(int d, int C) {
 
 // out: [grid][CP·DP + C + 2] f64 block partials, CP = cml_multinomial_mfma_supported(...), DP = _dpad(d, C)
 // (K13b: cml_partial_colsum, then the host keeps [:C, :d] of the gradient); X 16-byte aligned, ld % 8 == 0.
-CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, int d, int C, const double* y,
-                                      const double* wt, const double* coef, double* out, int grid, void* stream) {
-  if (cml_multinomial_mfma_supported(d, 0, C) == 0 || grid < 1 || n < 1 || ld % 8 != 0 || ld < d ||
+CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, int d, int dtype, int C,
+                                      const double* y, const double* wt, const double* coef, double* out, int grid,
+                                      void* stream) {
+  const int lq = dtype == 3 ? 16 : 8;  // values per 16-byte load: the row pitch is a whole number of them
+  if (cml_multinomial_mfma_supported(d, dtype, C) == 0 || grid < 1 || n < 1 || ld % lq != 0 || ld < d ||
       (reinterpret_cast<size_t>(X) & 15) != 0)
     return (int)hipErrorInvalidValue;
+  const bool f8 = dtype == 3;
   hipStream_t st = (hipStream_t)stream;
   int ft = (d + 31) / 32;
-  if (cml_multinomial_mfma_supported(d, 0, C) == 16) {  // multinomial_c16_kernel
+  if (cml_multinomial_mfma_supported(d, dtype, C) == 16) {  // multinomial_c16_kernel
     const int ctn = 1;
+#define CML_MNC_L(FTV, CTNV, F8V)                                                                              \
+  {                                                                                                            \
+    constexpr size_t lds = mnc16_lds<FTV, CTNV>();                                                             \
+    hipFuncSetAttribute((const void*)multinomial_c16_kernel<FTV, CTNV, F8V>,                                   \
+                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                                 \
+    hipLaunchKernelGGL((multinomial_c16_kernel<FTV, CTNV, F8V>), dim3(grid), dim3(kMnThreads), lds, st, X, n,   \
+                       ld, d, C, y, wt, coef, out);                                                            \
+    return cml_status();                                                                                       \
+  }
 #define CML_MNC(FTV, CTNV)                                                                                     \
     if (ft == FTV && ctn == CTNV) {                                                                            \
-      constexpr size_t lds = mnc16_lds<FTV, CTNV>();                                                           \
-      hipFuncSetAttribute((const void*)multinomial_c16_kernel<FTV, CTNV>,                                      \
-                          hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                               \
-      hipLaunchKernelGGL((multinomial_c16_kernel<FTV, CTNV>), dim3(grid), dim3(kMnThreads), lds, st,            \
-                         (const u16*)X, n, ld, d, C, y, wt, coef, out);                                        \
-      return cml_status();                                                                                     \
+      if (f8) CML_MNC_L(FTV, CTNV, true) else CML_MNC_L(FTV, CTNV, false)                                      \
     }
     CML_MNC(1, 1) CML_MNC(2, 1) CML_MNC(3, 1) CML_MNC(4, 1) CML_MNC(5, 1) CML_MNC(6, 1) CML_MNC(7, 1) CML_MNC(8, 1)
 #undef CML_MNC
+#undef CML_MNC_L
     return (int)hipErrorInvalidValue;
   }
   const int ct = C <= 32 ? 1 : 2;
@@ -953,7 +1001,14 @@ CML_API int cml_multinomial_mfma_grad(const void* X, long long n, long long ld, 
                            n, ld, d, C, y, wt, coef, out, f0, f0 == 0 ? 1 : 0);                               \
     } else {                                                                                                    \
       constexpr bool PS = mn16_lds<CTV, FTV, true>() <= kLdsMax;                                                \
-      if (PS && !g_mn_nosplit) {                                                                                \
+      if (f8) {  /* e4m3 rows: the default split only */                                                        \
+        const size_t lds = mn16_lds<CTV, FTV, PS>();                                                            \
+        hipFuncSetAttribute((const void*)multinomial_bf16_kernel<CTV, FTV, FTGV, PS, true>,                     \
+                            hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \
+        for (int f0 = 0; f0 < FTV; f0 += FTGV)                                                                  \
+          hipLaunchKernelGGL((multinomial_bf16_kernel<CTV, FTV, FTGV, PS, true>), dim3(grid), dim3(kMnThreads),  \
+                             lds, st, X, n, ld, d, C, y, wt, coef, out, f0, f0 == 0 ? 1 : 0);                 \
+      } else if (PS && !g_mn_nosplit) {                                                                         \
         const size_t lds = mn16_lds<CTV, FTV, PS>();                                                            \
         hipFuncSetAttribute((const void*)multinomial_bf16_kernel<CTV, FTV, FTGV, PS>,                           \
                             hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);                             \

@@ -31,7 +31,8 @@ _native.register_kernel_sigs({
     "cml_multinomial_mfma_set_mode": (c_int, [c_int]),
     "cml_multinomial_predict_lds": (c_ll, [c_int, c_int, c_int]),
     "cml_multinomial_predict": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_int, c_vp]),
-    "cml_multinomial_mfma_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_vp]),
+    "cml_multinomial_mfma_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int,
+                                          c_vp]),
     "cml_glm_loss_grad": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_vp, c_vp, c_int, c_int, c_vp]),
     "cml_sgd_update": (c_int, [c_vp, c_int, c_vp, c_vp, c_vp, c_vp, c_dbl, c_dbl, c_int, c_vp, c_vp, c_vp,
                                c_vp, c_ll, c_ll, c_vp]),
@@ -227,7 +228,8 @@ def multinomial_grad(x: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Tenso
     """Softmax (multinomial logistic) loss + gradient over the local shard: ``coef`` [C, d+1] (last column
     the intercepts) in the original feature space, labels 0..C-1 (f64). Returns the float64 sums
     [∇W (C·d, row-major) | ∇b (C) | loss | weight sum]. GPU rows run K13m's MFMA form for C <= 64 on bf16 rows
-    with d <= 256, d % 8 == 0 (glm_mfma.hip: both products on
+    with d <= 256, d % 8 == 0, and on e4m3 rows with d % 16 == 0 (widened exactly to bf16 as they are staged in
+    LDS) (glm_mfma.hip: both products on
     v_mfma_f32_32x32x16_bf16 with the f32 operand — weights, residuals — split into three bf16 terms, so f32
     precision; ``set_multinomial_mfma_mode(1)`` selects the v_mfma_f32_32x32x2_f32 form), else the VALU kernel
     (multinomial_grad_kernel: X read once, gradient partials in f64, fixed-order reduction) where its layout fits
@@ -317,7 +319,7 @@ def _multinomial_mfma(xx: torch.Tensor, d: int, y: torch.Tensor, coef: torch.Ten
     out = torch.empty((g, cp * dp + C + 2), dtype=torch.float64, device=xx.device)
     yy = y.to(torch.float64).contiguous()
     ww = weight.to(torch.float64).contiguous() if weight is not None else None
-    _native.check(k.cml_multinomial_mfma_grad(xx.data_ptr(), n, xx.stride(0), d, C, yy.data_ptr(),
+    _native.check(k.cml_multinomial_mfma_grad(xx.data_ptr(), n, xx.stride(0), d, _CODE[xx.dtype], C, yy.data_ptr(),
                                               ww.data_ptr() if ww is not None else 0, coef.data_ptr(), out.data_ptr(),
                                               g, _native.stream_ptr()), "multinomial_mfma_grad")
     msg = partial_colsum(out)

@@ -290,7 +290,10 @@ def _mode_run(mode, x, d, y, coef, C, cp, dp):
     prev = glm_ops.set_multinomial_mfma_mode(mode)
     try:
         lib = glm_ops._native.kernels()
-        cp, dp = lib.cml_multinomial_mfma_supported(d, 0, C), lib.cml_multinomial_mfma_dpad(d, C)
+        code = glm_ops._CODE[x.dtype]
+        cp, dp = lib.cml_multinomial_mfma_supported(d, code, C), lib.cml_multinomial_mfma_dpad(d, C)
+        if cp <= 0:
+            return None
         return glm_ops._multinomial_mfma(x, d, y, coef, None, C, cp, dp)
     finally:
         glm_ops.set_multinomial_mfma_mode(prev)
@@ -300,41 +303,47 @@ def cmd_multinomial(argv):
     ap = argparse.ArgumentParser(prog="mb_ml.py multinomial")
     ap.add_argument("--rows", type=int, default=100_000_000)
     ap.add_argument("--dim", type=int, default=256)
+    ap.add_argument("--dtype", default="bf16", choices=["bf16", "fp8"], help="row storage (fp8: OCP e4m3)")
+    ap.add_argument("--classes", default="4,8,16,32,64")
     a = ap.parse_args(argv)
     from clustermachinelearningforhospitalnetworks_apache_spark_amd.utils import synth
     dev = torch.device("cuda", 0)
     n, d = a.rows, a.dim
     x = synth.synth_rows(0, n, d, seed=3, dtype=torch.bfloat16, device=dev)
+    code, esz = 0, 2
+    if a.dtype == "fp8":
+        x = x.to(torch.float8_e4m3fn)
+        code, esz = 3, 1
     lib = __import__("clustermachinelearningforhospitalnetworks_apache_spark_amd._native",
                      fromlist=["kernels"]).kernels()
     g = torch.Generator(device=dev)
     g.manual_seed(1)
-    for C in (4, 8, 16, 32, 64):
+    for C in (int(c) for c in a.classes.split(",")):
         y = torch.randint(0, C, (n,), generator=g, device=dev).to(torch.float64)
         coef = torch.randn(C, d + 1, generator=g, device=dev, dtype=torch.float64) * 0.05
         # MFMA form: margins + gradient on the padded class tile (16, 32 or 64 classes)
         flop = 4.0 * n * d * (16 if C <= 16 else 32 if C <= 32 else 64)  # (mode 3: 32 for C <= 16 too)
         runs = []
-        if lib.cml_multinomial_supported(d, 0, C) > 0:
+        if lib.cml_multinomial_supported(d, code, C) > 0:
             runs.append(("valu", lambda: glm_ops.multinomial_grad(x, d, y, coef, prefer_valu=True)))
-        cp = lib.cml_multinomial_mfma_supported(d, 0, C)
+        cp = lib.cml_multinomial_mfma_supported(d, code, C)
         if cp > 0:  # every MFMA form (mode 0, the first, is the default route)
             dp = lib.cml_multinomial_mfma_dpad(d, C)
             for mode, name in ((0, "mfma-bf16x3"), (3, "mfma-bf16x3-32tile"), (2, "mfma-bf16x3-regsplit"),
                                (1, "mfma-f32")):
-                if mode == 3 and C > 16:
+                if (mode == 3 and C > 16) or (code == 3 and mode in (1, 2)):  # (e4m3 rows: bf16 forms only)
                     continue
                 runs.append((name, (lambda m: lambda: _mode_run(m, x, d, y, coef, C, cp, dp))(mode)))
         if not runs:
             runs.append(("torch-chunks", lambda: glm_ops.multinomial_grad(x, d, y, coef)))
-        if lib.cml_multinomial_predict_lds(d, 0, C) > 0:  # K13t: transform (raw + probability, f64 [n, C] each)
+        if code == 0 and lib.cml_multinomial_predict_lds(d, 0, C) > 0:  # K13t: transform (raw + probability, f64 [n, C] each)
             ms = best_ms(lambda: glm_ops.multinomial_predict(x, d, coef), reps=3)
             byts = n * d * 2 + 2 * n * C * 8
             print(f"multinomial transform {n}x{d} bf16 C={C:2d} [K13t f64 mfma]: {ms:8.3f} ms, "
                   f"{byts / ms / 1e9:6.2f} TB/s (rows in + raw/prob out)", flush=True)
         for name, fn in runs:
             ms = best_ms(fn, reps=3)
-            print(f"multinomial {n}x{d} bf16 C={C:2d} [{name}]: {ms:8.3f} ms, {n * d * 2 / ms / 1e9:6.2f} TB/s rows"
+            print(f"multinomial {n}x{d} {a.dtype} C={C:2d} [{name}]: {ms:8.3f} ms, {n * d * esz / ms / 1e9:6.2f} TB/s rows"
                   + (f", {flop / ms / 1e9:7.1f} useful TFLOP/s" if name.startswith("mfma") else ""), flush=True)
         del y
 

@@ -68,7 +68,11 @@ def test_chunked_oracle_matches_closed_form():
                                     # MFMA form (glm_mfma.hip): one class tile, two, and the padded two-launch widths
                                     (torch.bfloat16, 256, 32), (torch.bfloat16, 128, 16), (torch.bfloat16, 40, 12),
                                     (torch.bfloat16, 256, 64), (torch.bfloat16, 200, 40), (torch.bfloat16, 136, 33),
-                                    (torch.bfloat16, 64, 9)])
+                                    (torch.bfloat16, 64, 9),
+                                    # e4m3 rows on the MFMA forms (widened to bf16 in LDS): 16-class, 32-class,
+                                    # two class tiles
+                                    (torch.float8_e4m3fn, 256, 12), (torch.float8_e4m3fn, 64, 20),
+                                    (torch.float8_e4m3fn, 128, 40), (torch.float8_e4m3fn, 48, 3)])
 def test_kernel_matches_f64_oracle(dt, d, C):
     g = torch.Generator(device="cuda").manual_seed(d + C)
     n = 200_003
