@@ -148,6 +148,21 @@ __device__ inline void load_raw_group(const T* X, long long row, long long ld, i
   }
 }
 
+// Branch-free form for K13: a row past n loads row n - 1 (the caller gives it weight 0) and a chunk starting at
+// or beyond d loads chunk 0 (decode_group zeroes it). Exec-masked loads made the wait-count pass assume the
+// worst at every merge: each use of the previous group's label waited for the next group's rows as well.
+template <typename T, int NCH>
+__device__ inline void load_raw_group_clamped(const T* X, long long row, long long n, long long ld, int lpr, int li,
+                                              int d, uint4 (&raw)[NCH]) {
+  constexpr int CPT = Elt<T>::CPT;
+  const T* xr = X + (row < n ? row : n - 1) * ld;
+#pragma unroll
+  for (int c = 0; c < NCH; ++c) {
+    const int c0 = (c * lpr + li) * CPT;
+    raw[c] = *reinterpret_cast<const uint4*>(xr + (c0 < d ? c0 : 0));
+  }
+}
+
 template <typename T, typename CT, int NCH>
 __device__ inline void decode_group(const uint4 (&raw)[NCH], int lpr, int li, int d, CT (&v)[NCH][Elt<T>::CPT]) {
   constexpr int CPT = Elt<T>::CPT;
@@ -308,12 +323,17 @@ __device__ inline CT dot_ct(const CT (&v)[NCH][CPT], const CT (&w)[NCH][CPT]) {
   }
 }
 
-__device__ inline float sigmoid_ct(float m) { return 1.f / (1.f + __expf(-m)); }
+// f32 row math on the transcendental unit: v_exp_f32, v_log_f32 (base 2) and v_rcp_f32 (1 ulp). The IEEE
+// division and the denormal-safe log expansion were ~16 of the ~130 VALU ops per row group of the fp8 K13
+// pass, which issues VALU on ~65% of SIMD cycles (profiles/r6/lr_pmc/).
+__device__ inline float sigmoid_ct(float m) { return __builtin_amdgcn_rcpf(1.f + __expf(-m)); }
 __device__ inline double sigmoid_ct(double m) {
   const double e = exp(-fabs(m));
   return m >= 0 ? 1.0 / (1.0 + e) : e / (1.0 + e);
 }
-__device__ inline float softplus_ct(float m) { return fmaxf(m, 0.f) + __logf(1.f + __expf(-fabsf(m))); }
+__device__ inline float softplus_ct(float m) {
+  return fmaxf(m, 0.f) + 0.693147180559945f * __builtin_amdgcn_logf(1.f + __expf(-fabsf(m)));  // arg in [1, 2]
+}
 __device__ inline double softplus_ct(double m) { return fmax(m, 0.0) + log1p(exp(-fabs(m))); }
 
 // ---------------------------------------------------------------------------- K8 scale
@@ -441,52 +461,60 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     }
   const CT b = (CT)coef[d];
   double gb = 0.0, loss = 0.0, wsum = 0.0;
+  CT gbc = 0, lossc = 0, wsumc = 0;  // f32 data: per-row scalars in f32, folded into f64 with the gradient
   const long long step = (long long)gridDim.x * nw * rpw;
-  // Software pipeline: the raw 16-byte chunks (and y, wt) of the wave's next U row groups are in
-  // flight while the current one is decoded and reduced — a ring of U undecoded groups costs only
-  // NCH·4 + 4 VGPRs per slot (U = 1: one group ahead, the measured optimum; see logreg_unroll).
+  // Software pipeline: the raw 16-byte chunks, labels and weights of the wave's next U row groups are in
+  // flight while the current one is decoded and reduced. The ring has U + 1 slots and the step loop is
+  // unrolled over all of them, so the slot a step refills is never the one it reads: with U slots (the r4
+  // form) the refill of the slot being read needed a second register set and a copy on the back edge, and
+  // the copy waited for every load in flight, the ring's other groups included. Loads are branch-free
+  // (load_raw_group_clamped, labels of rows past n read row n - 1): exec-masked loads made the wait-count
+  // pass assume the worst at every merge. A slot costs NCH·4 + 4 VGPRs.
+  constexpr int S = U + 1;
   int since = 0;
   long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
-  uint4 raw[U][NCH];
-  double yn[U], wn[U];
+  uint4 raw[S][NCH];
+  double yn[S], wn[S];
+  const double* wsrc = wt != nullptr ? wt : y;  // no weight column: a valid address, wi = 1 where it is read
 #pragma unroll
   for (int q = 0; q < U; ++q) {
     const long long row = row0 + q * step + sub;
-    const bool ok = row < n;
-    load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw[q]);
-    yn[q] = ok ? y[row] : 0.0;
-    wn[q] = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+    const long long crow = row < n ? row : n - 1;
+    load_raw_group_clamped<T, NCH>(X, row, n, ld, lpr, li, d, raw[q]);
+    yn[q] = y[crow];
+    wn[q] = wsrc[crow];
   }
-  for (; row0 < n; row0 += U * step) {
+  for (; row0 < n; row0 += S * step) {
 #pragma unroll
-    for (int q = 0; q < U; ++q) {
+    for (int q = 0; q < S; ++q) {
       if (row0 + q * step >= n) break;  // wave-uniform
+      const int ps = (q + U) % S;  // the slot read one step ago
       CT v[NCH][CPT];
       decode_group<T, CT, NCH>(raw[q], lpr, li, d, v);
-      const double yi = yn[q], wi = wn[q];
       {
-        const long long row = row0 + (q + U) * step + sub;
-        const bool ok = row < n;
-        load_raw_group<T, NCH>(X, row, ld, lpr, li, d, ok, raw[q]);
-        yn[q] = ok ? y[row] : 0.0;
-        wn[q] = ok ? (wt != nullptr ? wt[row] : 1.0) : 0.0;
+        const long long nrow = row0 + (q + U) * step + sub;
+        const long long crow = nrow < n ? nrow : n - 1;
+        load_raw_group_clamped<T, NCH>(X, nrow, n, ld, lpr, li, d, raw[ps]);
+        yn[ps] = y[crow];
+        wn[ps] = wsrc[crow];
       }
+      const double yi = yn[q], wi = row0 + q * step + sub < n ? (wt != nullptr ? wn[q] : 1.0) : 0.0;
       CT m = dot_ct<CT, NCH, CPT>(v, w);
       m = group_sum_ct<CT>(m, lpr) + b;
       CT r;
-      double lrow;
+      CT lrow;
       if constexpr (LS == 0) {  // logistic
         r = (CT)wi * (sigmoid_ct(m) - (CT)yi);
-        lrow = (double)softplus_ct(m) - yi * (double)m;
+        lrow = softplus_ct(m) - (CT)yi * m;
       } else if constexpr (LS == 1) {  // hinge, labels {0, 1}
         const CT ys = yi > 0.5 ? (CT)1 : (CT)-1;
         const CT t = (CT)1 - ys * m;
         r = t > (CT)0 ? -(CT)wi * ys : (CT)0;
-        lrow = t > (CT)0 ? (double)t : 0.0;
+        lrow = t > (CT)0 ? t : (CT)0;
       } else {  // squared
         const CT e = m - (CT)yi;
         r = (CT)wi * e;
-        lrow = 0.5 * (double)e * (double)e;
+        lrow = (CT)0.5 * e * e;
       }
       if constexpr (sizeof(CT) == 4 && CPT % 2 == 0) {
         const f32x2_t r2 = {r, r};
@@ -505,14 +533,18 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
 #pragma unroll
           for (int j = 0; j < CPT; ++j) g[c][j] = fma(r, v[c][j], g[c][j]);
       }
-      if (li == 0) {
-        gb += (double)r;
-        loss += wi * lrow;
-        wsum += wi;
-      }
+      // every lane of the row group adds the row's scalars (no li == 0 select: 6 cndmasks); the totals are
+      // scaled by 1/lpr at the end, which is exact (power of two, and the lpr copies sum exactly first)
+      gbc += r;
+      lossc = fma((CT)wi, lrow, lossc);
+      wsumc += (CT)wi;
       if constexpr (sizeof(CT) == 4) {
         if (++since >= FLUSH) {
           since = 0;
+          gb += (double)gbc;
+          loss += (double)lossc;
+          wsum += (double)wsumc;
+          gbc = lossc = wsumc = 0;
 #pragma unroll
           for (int c = 0; c < NCH; ++c)
 #pragma unroll
@@ -528,6 +560,9 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   for (int c = 0; c < NCH; ++c)
 #pragma unroll
     for (int j = 0; j < CPT; ++j) g64[c][j] += (double)g[c][j];
+  gb += (double)gbc;
+  loss += (double)lossc;
+  wsum += (double)wsumc;
   // reduce across row sub-groups, then across waves
   // per-wave rows of lpr·CPT column sums + 3 scalars, sized at launch (logreg_lds_bytes): a fixed
   // fp8-sized buffer (33 KB) would cap residency at 4 blocks per CU for every dtype
@@ -542,6 +577,12 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
     gb += __shfl_xor(gb, o, 64);
     loss += __shfl_xor(loss, o, 64);
     wsum += __shfl_xor(wsum, o, 64);
+  }
+  {
+    const double il = 1.0 / (double)lpr;
+    gb *= il;
+    loss *= il;
+    wsum *= il;
   }
   double* o_ = out + (long long)blockIdx.x * (d + 3);
 #pragma unroll
@@ -1008,11 +1049,13 @@ int grid_for(long long n, int rows_per_block_iter, int cap) {
 
 int g_logreg_unroll = 0;  // 0 = auto, else forced prefetch depth U (ablation: cml_glm_set_logreg_unroll)
 
-int logreg_unroll(int nch) {
+int logreg_unroll(int nch, int cpt) {
   if (g_logreg_unroll == 1 || g_logreg_unroll == 2 || g_logreg_unroll == 4) return g_logreg_unroll;
-  // one group ahead: deeper rings measured SLOWER at every size (profiles/logreg_prefetch_depth.log:
-  // 50M x 256 bf16 5.65 / 4.20 / 2.85 TB/s at U = 1 / 2 / 4, fp8 x 512 3.96 / 2.68 / 1.90)
-  return 1;
+  // fp8 rows: two groups ahead (50M x 512: 5.08 -> 5.49 TB/s, profiles/r6/k13_ring/); bf16 / f32 rows: one
+  // (U = 2: 6.06 -> 5.91 bf16, 6.01 -> 5.46 f32). The r4 ring of U slots was slower at every U > 1
+  // (profiles/logreg_prefetch_depth.log): its back-edge copy waited for the whole ring.
+  (void)nch;
+  return cpt == 16 ? 2 : 1;
 }
 
 #define CML_U_SWITCH(u, BODY)                                          \
@@ -1057,7 +1100,7 @@ CML_API int cml_glm_grid(long long n, int d, int dtype, int ncu, int kind) {
       CML_NCH_SWITCH(nch, { per_cu = resident_blocks(col_moments_kernel<T, NCH>, moments_lds_bytes(lpr, Elt<T>::CPT)); });
     } else if (kind == 1) {
       CML_NCH_SWITCH(nch, {
-        CML_U_SWITCH(logreg_unroll(nch), { per_cu = resident_blocks(logreg_grad_kernel<T, NCH, U>, logreg_lds_bytes(lpr, Elt<T>::CPT)); });
+        CML_U_SWITCH(logreg_unroll(nch, Elt<T>::CPT), { per_cu = resident_blocks(logreg_grad_kernel<T, NCH, U>, logreg_lds_bytes(lpr, Elt<T>::CPT)); });
       });
     } else {
       CML_NCH_SWITCH(nch, { per_cu = resident_blocks(linear_predict_kernel<T, NCH>); });
@@ -1131,7 +1174,7 @@ CML_API int cml_logreg_grad(const void* X, long long n, long long ld, int d, int
     int nch = 0;
     if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
-      CML_U_SWITCH(logreg_unroll(nch), {
+      CML_U_SWITCH(logreg_unroll(nch, Elt<T>::CPT), {
         hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, U>), dim3(grid), dim3(kGlmThreads),
                            logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld,
                            d, lpr, y, wt, coef, out, row_base);

@@ -216,7 +216,9 @@ def cmd_pmc(a):
 
 def cmd_pmccsv(a):
     disp = collections.defaultdict(dict)
-    for f in sorted(glob.glob(os.path.join(a.dir, "*", "*counter_collection.csv"))):
+    fs = glob.glob(os.path.join(a.dir, "*", "*counter_collection.csv")) + \
+        glob.glob(os.path.join(a.dir, "*counter_collection.csv"))
+    for f in sorted(fs):
         tag = os.path.basename(os.path.dirname(f))
         for r in csv.DictReader(open(f)):
             if a.sub not in r["Kernel_Name"]:
@@ -237,6 +239,8 @@ def cmd_pmccsv(a):
                 out.append(f"clock {cyc / d['ms'] / 1e6:.2f} GHz")
                 if "SQ_VALU_MFMA_BUSY_CYCLES" in d:
                     out.append(f"MFMA busy {d['SQ_VALU_MFMA_BUSY_CYCLES'] / 1024 / cyc * 100:.0f}%")
+                if "SQ_INSTS_VALU" in d:  # a wave64 VALU op holds its 16-lane SIMD 4 cycles (more for f64/trans)
+                    out.append(f"VALU issue >= {4 * d['SQ_INSTS_VALU'] / 1024 / cyc * 100:.0f}% of SIMD cycles")
             if "SQ_WAIT_ANY" in d:
                 tot = d["SQ_WAIT_ANY"] + d["SQ_WAIT_INST_ANY"] + d["SQ_ACTIVE_INST_ANY"]
                 out.append("waves: wait {:.0f}% issue-stall {:.0f}% active {:.0f}%".format(
