@@ -198,7 +198,7 @@ __device__ inline void decode_group(const uint4 (&raw)[NCH], int lpr, int li, in
 // Row-streaming layout with the next row group's raw chunks prefetched (as K13). t = x − shift is
 // formed in CT (exact for bf16/f32/fp8 data: the shift is a data row, so it is representable),
 // Σt and Σt² accumulate in f64. Per-wave column sums go through LDS sized at launch.
-template <typename T, int NCH>
+template <typename T, int NCH, int U = 1>
 __global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __restrict__ X, long long n, long long ld,
                                                                   int d, int lpr, const double* __restrict__ shift,
                                                                   double* __restrict__ out /*[grid][2][d]*/) {
@@ -219,22 +219,32 @@ __global__ __launch_bounds__(kGlmThreads) void col_moments_kernel(const T* __res
     }
   const long long step = (long long)gridDim.x * nw * rpw;
   long long row0 = ((long long)blockIdx.x * nw + wave) * rpw;
-  uint4 raw[NCH];
-  if (row0 < n) load_raw_group<T, NCH>(X, row0 + sub, ld, lpr, li, d, row0 + sub < n, raw);
-  for (; row0 < n; row0 += step) {
-    const bool ok = row0 + sub < n;
-    CT v[NCH][CPT];
-    decode_group<T, CT, NCH>(raw, lpr, li, d, v);
-    load_raw_group<T, NCH>(X, row0 + step + sub, ld, lpr, li, d, row0 + step + sub < n, raw);
-    if (ok) {
+  // the K13 ring: U groups in flight, U + 1 slots, branch-free loads (rows past n re-read row n - 1 and
+  // are skipped below)
+  constexpr int S = U + 1;
+  uint4 raw[S][NCH];
+  if (row0 < n) {
 #pragma unroll
-      for (int c = 0; c < NCH; ++c)
+    for (int q = 0; q < U; ++q) load_raw_group_clamped<T, NCH>(X, row0 + q * step + sub, n, ld, lpr, li, d, raw[q]);
+  }
+  for (; row0 < n; row0 += S * step) {
 #pragma unroll
-        for (int j = 0; j < CPT; ++j) {
-          const double t = (double)(v[c][j] - sh[c][j]);
-          s1[c][j] += t;
-          s2[c][j] = fma(t, t, s2[c][j]);
-        }
+    for (int q = 0; q < S; ++q) {
+      if (row0 + q * step >= n) break;  // wave-uniform
+      const bool ok = row0 + q * step + sub < n;
+      CT v[NCH][CPT];
+      decode_group<T, CT, NCH>(raw[q], lpr, li, d, v);
+      load_raw_group_clamped<T, NCH>(X, row0 + (q + U) * step + sub, n, ld, lpr, li, d, raw[(q + U) % S]);
+      if (ok) {
+#pragma unroll
+        for (int c = 0; c < NCH; ++c)
+#pragma unroll
+          for (int j = 0; j < CPT; ++j) {
+            const double t = (double)(v[c][j] - sh[c][j]);
+            s1[c][j] += t;
+            s2[c][j] = fma(t, t, s2[c][j]);
+          }
+      }
     }
   }
 #pragma unroll
@@ -337,6 +347,7 @@ __device__ inline float softplus_ct(float m) {
 __device__ inline double softplus_ct(double m) { return fmax(m, 0.0) + log1p(exp(-fabs(m))); }
 
 // ---------------------------------------------------------------------------- K8 scale
+// (The K13 branch-free loads measured slower here: bf16 -> e4m3 at 50M x 512 5.32 -> 5.06 TB/s, r6.)
 template <typename TI, typename TO, int NCH>
 __global__ __launch_bounds__(kGlmThreads) void scale_apply_kernel(const TI* __restrict__ X, long long n, long long ldx,
                                                                   int d, int lpr, const double* __restrict__ mean,
@@ -1080,6 +1091,19 @@ CML_API int cml_glm_set_fp8_nch(int v) {
   return 0;
 }
 
+int g_moments_unroll = 0;  // 0 = auto, else forced K7 prefetch depth (1 or 2; ablation)
+int moments_unroll(int cpt) {
+  if (g_moments_unroll == 1 || g_moments_unroll == 2) return g_moments_unroll;
+  // profiles/r6/k13_ring/moments_ring.log (the branch-free ring at 1 / 2 groups in flight): bf16 x 256 6.19 /
+  // 6.15 TB/s, e4m3 x 512 5.34 / 5.40, f32 x 256 6.00 / 6.10; the r5 kernel read 5.56 / 5.0-5.3 / 6.07
+  return (cpt == 16 || cpt == 4) ? 2 : 1;
+}
+
+CML_API int cml_glm_set_moments_unroll(int u) {
+  g_moments_unroll = u;
+  return 0;
+}
+
 CML_API int cml_glm_set_logreg_unroll(int u) {
   g_logreg_unroll = u;
   return 0;
@@ -1097,7 +1121,12 @@ CML_API int cml_glm_grid(long long n, int d, int dtype, int ncu, int kind) {
   int per_cu = 1;
   CML_T_SWITCH(dtype, {
     if (kind == 0) {
-      CML_NCH_SWITCH(nch, { per_cu = resident_blocks(col_moments_kernel<T, NCH>, moments_lds_bytes(lpr, Elt<T>::CPT)); });
+      CML_NCH_SWITCH(nch, {
+        if (moments_unroll(Elt<T>::CPT) == 2)
+          per_cu = resident_blocks(col_moments_kernel<T, NCH, 2>, moments_lds_bytes(lpr, Elt<T>::CPT));
+        else
+          per_cu = resident_blocks(col_moments_kernel<T, NCH, 1>, moments_lds_bytes(lpr, Elt<T>::CPT));
+      });
     } else if (kind == 1) {
       CML_NCH_SWITCH(nch, {
         CML_U_SWITCH(logreg_unroll(nch, Elt<T>::CPT), { per_cu = resident_blocks(logreg_grad_kernel<T, NCH, U>, logreg_lds_bytes(lpr, Elt<T>::CPT)); });
@@ -1119,8 +1148,12 @@ CML_API int cml_col_moments(const void* X, long long n, long long ld, int d, int
     int nch = 0;
     if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
-      hipLaunchKernelGGL((col_moments_kernel<T, NCH>), dim3(grid), dim3(kGlmThreads),
-                         moments_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, shift, out);
+      if (moments_unroll(Elt<T>::CPT) == 2)
+        hipLaunchKernelGGL((col_moments_kernel<T, NCH, 2>), dim3(grid), dim3(kGlmThreads),
+                           moments_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, shift, out);
+      else
+        hipLaunchKernelGGL((col_moments_kernel<T, NCH, 1>), dim3(grid), dim3(kGlmThreads),
+                           moments_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, shift, out);
     });
   });
   return cml_status();

@@ -18,6 +18,7 @@ from ..utils.device import num_cus
 _native.register_kernel_sigs({
     "cml_glm_grid": (c_int, [c_ll, c_int, c_int, c_int, c_int]),
     "cml_glm_set_logreg_unroll": (c_int, [c_int]),
+    "cml_glm_set_moments_unroll": (c_int, [c_int]),
     "cml_glm_set_fp8_nch": (c_int, [c_int]),
     "cml_col_moments": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp]),
     "cml_scale_apply": (c_int, [c_vp, c_ll, c_ll, c_int, c_int, c_vp, c_vp, c_int, c_vp, c_ll, c_int, c_int, c_vp]),
@@ -427,6 +428,11 @@ def gram(x: torch.Tensor, d: int, y: torch.Tensor, weight: Optional[torch.Tensor
     _native.check(st, "gram")
     g = out.sum(0).reshape(m, m)
     return torch.triu(g) + torch.triu(g, 1).T
+
+
+def set_moments_unroll(u: int) -> None:
+    """Ablation knob: K7 (column moments) rows in flight per wave (1, 2; 0 = automatic)."""
+    _native.kernels().cml_glm_set_moments_unroll(int(u))
 
 
 def set_logreg_unroll(u: int) -> None:
