@@ -1217,7 +1217,7 @@ CML_API int cml_logreg_grad(const void* X, long long n, long long ld, int d, int
   return cml_status();
 }
 
-// K13 with the hinge (LS = 1) or squared (LS = 2) loss; one group ahead (U = 1, the K13 optimum).
+// K13 with the hinge (LS = 1) or squared (LS = 2) loss, at the logistic form's ring depth.
 CML_API int cml_glm_loss_grad(const void* X, long long n, long long ld, int d, int dtype, const double* y,
                               const double* wt, const double* coef, double* out, int grid, int loss, void* stream) {
   hipStream_t st = (hipStream_t)stream;
@@ -1228,14 +1228,25 @@ CML_API int cml_glm_loss_grad(const void* X, long long n, long long ld, int d, i
     int nch = 0;
     if (!stream_layout(d, Elt<T>::CPT, lpr, nch)) return (int)hipErrorInvalidValue;
     CML_NCH_SWITCH(nch, {
-      if (loss == 1)
+      // the logistic form's ring depth (two groups ahead on e4m3 rows); the caller's grid was sized for it
+      if (Elt<T>::CPT == 16 && logreg_unroll(nch, Elt<T>::CPT) == 2) {
+        if (loss == 1)
+          hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 2, 1>), dim3(grid), dim3(kGlmThreads),
+                             logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
+                             nullptr);
+        else
+          hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 2, 2>), dim3(grid), dim3(kGlmThreads),
+                             logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
+                             nullptr);
+      } else if (loss == 1) {
         hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 1, 1>), dim3(grid), dim3(kGlmThreads),
                            logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
                            nullptr);
-      else
+      } else {
         hipLaunchKernelGGL((logreg_grad_kernel<T, NCH, 1, 2>), dim3(grid), dim3(kGlmThreads),
                            logreg_lds_bytes(lpr, Elt<T>::CPT), st, (const T*)X, n, ld, d, lpr, y, wt, coef, out,
                            nullptr);
+      }
     });
   });
   return cml_status();
