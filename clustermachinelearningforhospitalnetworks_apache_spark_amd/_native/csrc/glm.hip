@@ -489,6 +489,7 @@ __global__ __launch_bounds__(kGlmThreads) void logreg_grad_kernel(
   const double* wsrc = wt != nullptr ? wt : y;  // no weight column: a valid address, wi = 1 where it is read
 #pragma unroll
   for (int q = 0; q < U; ++q) {
+    if (n <= 0) break;  // an empty shard reads nothing (row n - 1 does not exist); the partials stay zero
     const long long row = row0 + q * step + sub;
     const long long crow = row < n ? row : n - 1;
     load_raw_group_clamped<T, NCH>(X, row, n, ld, lpr, li, d, raw[q]);

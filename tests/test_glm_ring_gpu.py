@@ -78,3 +78,19 @@ def test_moments_ring_depths_match_f64(dt, d, n):
             assert torch.equal(cur, bits)  # one grid, the same per-lane order at either depth
     finally:
         glm_ops.set_moments_unroll(0)
+
+
+@pytest.mark.parametrize("dt,code,d", [(torch.float8_e4m3fn, 3, 512), (torch.bfloat16, 0, 256)])
+def test_logreg_kernel_empty_shard_writes_zero_partials(dt, code, d):
+    """n = 0 straight into the kernel (the wrapper takes the host path): no load of row n - 1, zero partials."""
+    from clustermachinelearningforhospitalnetworks_apache_spark_amd import _native
+
+    x = torch.zeros(1, d, dtype=dt, device="cuda")
+    y = torch.zeros(1, dtype=torch.float64, device="cuda")
+    coef = torch.zeros(d + 1, dtype=torch.float64, device="cuda")
+    out = torch.full((4, d + 3), float("nan"), dtype=torch.float64, device="cuda")
+    st = _native.kernels().cml_logreg_grad(x.data_ptr(), 0, x.stride(0), d, code, y.data_ptr(), 0, coef.data_ptr(),
+                                           out.data_ptr(), 4, 0, _native.stream_ptr())
+    _native.check(st, "logreg_grad")
+    torch.cuda.synchronize()
+    assert torch.equal(out, torch.zeros_like(out))
